@@ -1,0 +1,312 @@
+// pybind11 bindings for the CPU-side native runtime: the ZMTP transport and
+// the pickle codec.  Built as `blendtorch/_native*.so` (no HIP dependency, so
+// it runs in Blender-side producer processes and CPU-only tests as well).
+#include <pybind11/eval.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "../codec/pickle_codec.h"
+#include "../transport/zmtp.h"
+
+namespace py = pybind11;
+using namespace btn;
+using zmtp::Frame;
+using zmtp::Message;
+using zmtp::Socket;
+
+namespace {
+
+py::object g_error_type;
+
+// Lets Ctrl-C interrupt a blocking native wait.
+const Socket::Interrupt& signal_check() {
+  static const Socket::Interrupt f = [] {
+    py::gil_scoped_acquire gil;
+    return PyErr_CheckSignals() != 0;
+  };
+  return f;
+}
+
+[[noreturn]] void raise_zmtp(const zmtp::Error& e) {
+  // may be reached with the GIL released (blocking calls); error_already_set
+  // captures the Python error state while we hold it here.
+  py::gil_scoped_acquire gil;
+  if (e.code == zmtp::E_INTR && PyErr_Occurred()) throw py::error_already_set();
+  py::object err = g_error_type(e.code, e.what());
+  PyErr_SetObject(g_error_type.ptr(), err.ptr());
+  throw py::error_already_set();
+}
+
+template <typename F>
+auto guarded(F&& f) -> decltype(f()) {
+  try {
+    return f();
+  } catch (const zmtp::Error& e) {
+    raise_zmtp(e);
+  }
+}
+
+struct PyFrame {
+  Frame f;
+  bool more = false;
+};
+
+Frame frame_from_py(const py::handle& h) {
+  if (py::isinstance<PyFrame>(h)) return h.cast<PyFrame&>().f;
+  py::buffer b = py::reinterpret_borrow<py::buffer>(h);
+  py::buffer_info info = b.request();
+  size_t n = size_t(info.size * info.itemsize);
+  return Frame::copy_of(info.ptr, n);
+}
+
+py::object value_to_py(const codec::Value& v, const uint8_t* base, const py::object& owner) {
+  using K = codec::Value;
+  if (v.np_scalar) {
+    // numpy scalar (e.g. np.float32): 0-d view, then index -> scalar copy
+    py::array a(py::dtype(v.dtype), std::vector<py::ssize_t>{}, std::vector<py::ssize_t>{},
+                const_cast<uint8_t*>(base + v.off), owner);
+    return a[py::tuple()];
+  }
+  if (v.kind == K::BYTES && v.bytearray)
+    return py::reinterpret_steal<py::object>(
+        PyByteArray_FromStringAndSize(reinterpret_cast<const char*>(base + v.off), py::ssize_t(v.len)));
+  switch (v.kind) {
+    case K::NONE: return py::none();
+    case K::BOOL: return py::bool_(v.b);
+    case K::INT: return py::int_(v.i);
+    case K::FLOAT: return py::float_(v.f);
+    case K::STR: return py::str(v.s);
+    case K::BYTES: return py::bytes(reinterpret_cast<const char*>(base + v.off), v.len);
+    case K::LIST: {
+      py::list l;
+      for (auto& x : v.items) l.append(value_to_py(*x, base, owner));
+      return l;
+    }
+    case K::TUPLE: {
+      py::tuple t(v.items.size());
+      for (size_t i = 0; i < v.items.size(); ++i) t[i] = value_to_py(*v.items[i], base, owner);
+      return t;
+    }
+    case K::SET: {
+      py::set s;
+      for (auto& x : v.items) s.add(value_to_py(*x, base, owner));
+      return s;
+    }
+    case K::DICT: {
+      py::dict d;
+      for (size_t i = 0; i + 1 < v.items.size(); i += 2)
+        d[value_to_py(*v.items[i], base, owner)] = value_to_py(*v.items[i + 1], base, owner);
+      return d;
+    }
+    case K::NDARRAY: {
+      py::dtype dt(v.dtype);
+      std::vector<py::ssize_t> shape(v.shape.begin(), v.shape.end());
+      std::vector<py::ssize_t> strides(shape.size());
+      py::ssize_t st = py::ssize_t(v.itemsize());
+      if (v.fortran) {
+        for (size_t i = 0; i < shape.size(); ++i) {
+          strides[i] = st;
+          st *= shape[i];
+        }
+      } else {
+        for (size_t i = shape.size(); i-- > 0;) {
+          strides[i] = st;
+          st *= shape[i];
+        }
+      }
+      // zero-copy view; `owner` keeps the receive buffer alive
+      return py::array(dt, shape, strides, const_cast<uint8_t*>(base + v.off), owner);
+    }
+    default: throw codec::Unsupported("value kind");
+  }
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_native, m) {
+  m.doc() = "blendtorch native runtime: ZMTP transport + pickle codec";
+
+  // Exception type carrying errno; the Python layer maps it onto zmq.error.*
+  py::object builtins = py::module_::import("builtins");
+  g_error_type = py::reinterpret_borrow<py::object>(PyExc_Exception);
+  {
+    py::dict ns;
+    py::exec(R"(
+class NativeError(Exception):
+    def __init__(self, errno, msg):
+        super().__init__(msg)
+        self.errno = errno
+)", ns);
+    g_error_type = ns["NativeError"];
+    m.attr("NativeError") = g_error_type;
+  }
+
+  py::class_<PyFrame>(m, "Frame", py::buffer_protocol())
+      .def_buffer([](PyFrame& f) {
+        return py::buffer_info(const_cast<uint8_t*>(f.f.data()), 1,
+                               py::format_descriptor<uint8_t>::format(), 1,
+                               {py::ssize_t(f.f.size)}, {py::ssize_t(1)}, false);
+      })
+      .def("__len__", [](PyFrame& f) { return f.f.size; })
+      .def_property_readonly("bytes", [](PyFrame& f) {
+        return py::bytes(reinterpret_cast<const char*>(f.f.data()), f.f.size);
+      })
+      .def_property_readonly("more", [](PyFrame& f) { return f.more; })
+      .def_property_readonly("pinned", [](PyFrame& f) { return f.f.buf && f.f.buf->pinned; });
+
+  py::class_<zmtp::Context, std::shared_ptr<zmtp::Context>>(m, "Context")
+      .def(py::init<>())
+      .def("socket", [](zmtp::Context& c, int t) { return guarded([&] { return c.socket(t); }); })
+      .def("term", [](zmtp::Context& c) {
+        py::gil_scoped_release nogil;
+        c.term();
+      });
+
+  m.def("global_context", []() {
+    // never destroyed: the IO thread must outlive interpreter teardown
+    static std::shared_ptr<zmtp::Context> g(&zmtp::Context::global(), [](zmtp::Context*) {});
+    return g;
+  });
+
+  py::class_<Socket, std::shared_ptr<Socket>>(m, "Socket")
+      .def_property_readonly("type", &Socket::type)
+      .def("setsockopt", [](Socket& s, int opt, int64_t v) { guarded([&] { s.setsockopt(opt, v); }); })
+      .def("setsockopt_bytes",
+           [](Socket& s, int opt, const std::string& v) { guarded([&] { s.setsockopt_bytes(opt, v); }); })
+      .def("getsockopt", [](Socket& s, int opt) { return guarded([&] { return s.getsockopt(opt); }); })
+      .def("getsockopt_string",
+           [](Socket& s, int opt) { return guarded([&] { return s.getsockopt_string(opt); }); })
+      .def("bind", [](Socket& s, const std::string& a) {
+        py::gil_scoped_release nogil;
+        return guarded([&] { return s.bind(a); });
+      })
+      .def("unbind", [](Socket& s, const std::string& a) {
+        py::gil_scoped_release nogil;
+        guarded([&] { s.unbind(a); });
+      })
+      .def("connect", [](Socket& s, const std::string& a) {
+        py::gil_scoped_release nogil;
+        guarded([&] { s.connect(a); });
+      })
+      .def("disconnect", [](Socket& s, const std::string& a) {
+        py::gil_scoped_release nogil;
+        guarded([&] { s.disconnect(a); });
+      })
+      .def("send_multipart",
+           [](Socket& s, const py::sequence& parts, int flags) {
+             Message msg;
+             msg.reserve(parts.size());
+             for (auto h : parts) msg.push_back(frame_from_py(h));
+             py::gil_scoped_release nogil;
+             guarded([&] { s.send(std::move(msg), flags, signal_check()); });
+           },
+           py::arg("parts"), py::arg("flags") = 0)
+      .def("recv_multipart",
+           [](Socket& s, int flags) {
+             Message msg;
+             {
+               py::gil_scoped_release nogil;
+               msg = guarded([&] { return s.recv(flags, signal_check()); });
+             }
+             py::list out;
+             for (size_t i = 0; i < msg.size(); ++i) {
+               PyFrame pf;
+               pf.f = std::move(msg[i]);
+               pf.more = i + 1 < msg.size();
+               out.append(py::cast(std::move(pf)));
+             }
+             return out;
+           },
+           py::arg("flags") = 0)
+      .def("events", &Socket::events)
+      .def("close",
+           [](Socket& s, long linger) {
+             py::gil_scoped_release nogil;
+             s.close(linger);
+           },
+           py::arg("linger") = -2)
+      .def_property_readonly("closed", &Socket::closed)
+      .def("num_peers", &Socket::num_peers)
+      .def("stats", [](Socket& s) {
+        auto st = s.stats();
+        py::dict d;
+        d["msgs_in"] = st.msgs_in;
+        d["msgs_out"] = st.msgs_out;
+        d["bytes_in"] = st.bytes_in;
+        d["bytes_out"] = st.bytes_out;
+        return d;
+      });
+
+  m.def("poll",
+        [](const std::vector<std::pair<std::shared_ptr<Socket>, int>>& items, long timeout_ms) {
+          std::vector<std::pair<Socket*, int>> raw;
+          for (auto& it : items) raw.emplace_back(it.first.get(), it.second);
+          py::gil_scoped_release nogil;
+          return guarded([&] { return Socket::poll(raw, timeout_ms, signal_check()); });
+        });
+
+  m.def("greeting_bytes", [](bool as_server) { return py::bytes(zmtp::greeting_bytes(as_server)); });
+  m.def("ready_command", [](int t, const std::string& id) { return py::bytes(zmtp::ready_command(t, id)); },
+        py::arg("socket_type"), py::arg("identity") = "");
+  m.def("socket_types_compatible", &zmtp::socket_types_compatible);
+
+  // ---- codec ----
+  m.def("pickle_describe", [](py::buffer b) {
+    auto info = b.request();
+    try {
+      auto v = codec::parse(static_cast<const uint8_t*>(info.ptr), size_t(info.size * info.itemsize));
+      return codec::describe(*v);
+    } catch (const codec::Unsupported& e) {
+      throw py::value_error(std::string("unsupported pickle: ") + e.what());
+    }
+  });
+  // Zero-copy loads: ndarray values become views over `obj`'s buffer.
+  // Raises ValueError for constructs outside the fast path (caller falls back
+  // to pickle.loads).
+  m.def("fast_loads", [](py::object obj) {
+    py::buffer b = py::reinterpret_borrow<py::buffer>(obj);
+    auto info = b.request();
+    const uint8_t* base = static_cast<const uint8_t*>(info.ptr);
+    try {
+      auto v = codec::parse(base, size_t(info.size * info.itemsize));
+      return value_to_py(*v, base, obj);
+    } catch (const codec::Unsupported& e) {
+      throw py::value_error(std::string("unsupported pickle: ") + e.what());
+    }
+  });
+  m.def("btr_header", [](py::array_t<int64_t, py::array::c_style | py::array::forcecast> offs) {
+    std::vector<int64_t> o(offs.data(), offs.data() + offs.size());
+    auto h = codec::btr_header(o);
+    return py::bytes(reinterpret_cast<const char*>(h.data()), h.size());
+  });
+  m.def("dumps_array_dict",
+        [](const py::dict& d, int protocol) {
+          // Minimal writer used by tests/producers: str keys; values int, float,
+          // str, bool, None or C-contiguous ndarray.
+          codec::Writer w(protocol);
+          w.begin_dict();
+          for (auto kv : d) {
+            w.key(kv.first.cast<std::string>());
+            py::handle v = kv.second;
+            if (v.is_none()) w.none();
+            else if (py::isinstance<py::bool_>(v)) w.boolean(v.cast<bool>());
+            else if (py::isinstance<py::int_>(v)) w.integer(v.cast<int64_t>());
+            else if (py::isinstance<py::float_>(v)) w.real(v.cast<double>());
+            else if (py::isinstance<py::str>(v)) w.str(v.cast<std::string>());
+            else if (py::isinstance<py::array>(v)) {
+              py::array a = py::reinterpret_borrow<py::array>(v);
+              a = py::array::ensure(a, py::array::c_style);
+              std::string ds = py::str(a.dtype().attr("str"));
+              std::vector<int64_t> shape(a.shape(), a.shape() + a.ndim());
+              w.ndarray(ds.substr(1), shape, a.data());
+            } else {
+              throw py::type_error("dumps_array_dict: unsupported value type");
+            }
+          }
+          w.end_dict();
+          auto& out = w.finish();
+          return py::bytes(reinterpret_cast<const char*>(out.data()), out.size());
+        },
+        py::arg("d"), py::arg("protocol") = 4);
+}
