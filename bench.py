@@ -1,0 +1,196 @@
+#!/usr/bin/env python
+"""Headline benchmark: Cube scene 640x480 RGBA, batch 8, streamed into HBM.
+
+Mirrors the reference harness (benchmarks/benchmark.py:7-47: 4 producer
+instances, batch 8, warm-up batch excluded, sec/image + sec/batch) on the
+MI355X-native path:
+
+  K headless Cube producers per GPU (csrc/sim/cubesim, C++ rasteriser; same
+  launch contract and message dict as examples/datagen/cube.blend.py)
+  --ZMTP PUSH/PULL--> native receive into pinned slots --hipMemcpyAsync-->
+  fused gfx950 decode kernel (RGBA->RGB, gamma 2.2, /255, HWC->CHW, fp32)
+  -> batch tensor resident on the GPU.
+
+One process per GPU (``torch.distributed.run``); each rank owns its own
+producers (shard mode, weak scaling), ranks are synchronised with RCCL
+barriers around the timed region and the slowest rank's time is reported.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--producers P]
+                    [--mode rgba|rgb] [--consumer none|disc]
+
+Rank 0 prints ONE JSON line (see README "Benchmark").
+"""
+import argparse
+import fcntl
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+PKG = ROOT / 'pytorch-blender_amd'
+sys.path.insert(0, str(PKG))
+
+# Best published reference row: 5 Blender instances, no UI refresh,
+# 0.011 s/image -> 90.9 images/s (Readme.md:93).
+BASELINE_IMAGES_PER_SEC = 90.9
+METRIC = 'images/sec (whole node) + sec/batch, 640x480 RGBA Cube scene, batch=8'
+
+
+def ensure_built():
+    """Incremental in-tree build, serialised across ranks with a file lock."""
+    from blendtorch import _build
+    lock = ROOT / 'build' / '.bench.lock'
+    lock.parent.mkdir(parents=True, exist_ok=True)
+    with open(lock, 'w') as fp:
+        fcntl.flock(fp, fcntl.LOCK_EX)
+        try:
+            _build.build_all()
+        finally:
+            fcntl.flock(fp, fcntl.LOCK_UN)
+
+
+def cpu_budget():
+    """CPUs usable by this process: affinity mask, capped by a cgroup quota."""
+    cpus = sorted(os.sched_getaffinity(0))
+    try:
+        quota, period = Path('/sys/fs/cgroup/cpu.max').read_text().split()[:2]
+        if quota != 'max':
+            n = max(1, int(int(quota) / int(period)))
+            cpus = cpus[:n] if n < len(cpus) else cpus
+    except (OSError, ValueError):
+        pass
+    return cpus
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=int(os.environ.get('WORLD_SIZE', '1')))
+    ap.add_argument('--steps', type=int, default=200)
+    ap.add_argument('--warmup', type=int, default=20)
+    ap.add_argument('--batch', type=int, default=8)
+    ap.add_argument('--producers', type=int, default=0, help='producer processes per GPU (0 = auto)')
+    ap.add_argument('--mode', choices=['rgba', 'rgb'], default='rgba')
+    ap.add_argument('--proto', choices=['tcp', 'ipc'], default='tcp')
+    ap.add_argument('--consumer', choices=['none', 'disc'], default='none')
+    ap.add_argument('--io-threads', type=int, default=0)
+    ap.add_argument('--start-port', type=int, default=0)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get('RANK', '0'))
+    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    local_world = int(os.environ.get('LOCAL_WORLD_SIZE', str(world)))
+
+    ensure_built()
+    import torch
+    import torch.distributed as dist
+    from blendtorch import btt
+    from blendtorch.btt.gpu import DeviceLoader
+    from blendtorch.ops import DecodeConfig
+
+    torch.cuda.set_device(local_rank)
+    device = torch.device('cuda', local_rank)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=device)
+
+    # partition this node's CPUs between the local ranks; producers are pinned
+    cpus = cpu_budget()
+    share = max(1, len(cpus) // local_world)
+    mine = cpus[local_rank * share:(local_rank + 1) * share] or cpus
+    nprod = args.producers or max(1, min(12, len(mine) - 3))
+    affinity = [[mine[i % len(mine)]] for i in range(nprod)]
+    start_port = args.start_port or (20000 + (os.getpid() % 200) * 50 if world == 1 else 21000 + rank * 64)
+
+    decode = DecodeConfig.unit(channels='rgb', gamma=2.2)
+    launch = dict(producer='cubesim', num_instances=nprod, named_sockets=['DATA'], start_port=start_port,
+                  proto=args.proto, seed=1000 * rank, cpu_affinity=affinity,
+                  instance_args=[['--mode', args.mode, '--sndhwm', '10']] * nprod)
+    model = opt = None
+    if args.consumer == 'disc':
+        from blendtorch.models import Discriminator
+        model = Discriminator(nc=3, ndf=32, adaptive=True).to(device).to(memory_format=torch.channels_last)
+        if world > 1:
+            model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local_rank])
+        opt = torch.optim.Adam(model.parameters(), lr=2e-4)
+        crit = torch.nn.BCELoss()
+
+    total_batches = args.warmup + args.steps
+    with btt.BlenderLauncher(**launch) as bl:
+        dl = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=args.batch, decode=decode, device=device,
+                          max_items=total_batches * args.batch, prefetch=6,
+                          io_threads=args.io_threads or None, timeoutms=60000)
+        it = iter(dl)
+
+        def step():
+            b = next(it)
+            img = b['image']
+            if model is not None:
+                opt.zero_grad(set_to_none=True)
+                out = model(img.contiguous(memory_format=torch.channels_last))
+                loss = crit(out, torch.ones_like(out))
+                loss.backward()
+                opt.step()
+            return img
+
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            img = step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        shape = tuple(img.shape)
+        try:
+            next(it)
+        except StopIteration:
+            pass
+        stats = dict(dl.stats)
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    tmax = float(t.item())
+    images = args.steps * args.batch * world
+    value = images / tmax
+    if rank == 0:
+        print(json.dumps({
+            'metric': METRIC,
+            'value': round(value, 2),
+            'unit': 'images/s',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': round(tmax / args.steps * 1000, 4),
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': round(value / BASELINE_IMAGES_PER_SEC, 3),
+            'dtype': 'fp32',
+            'data': 'synthetic (headless C++ Cube-scene producers, random rotations)',
+            'config': {
+                'model': 'cube-scene-640x480-' + args.mode + (' + dcgan-disc' if model is not None else ''),
+                'global_batch': args.batch * world,
+                'seq_len': None,
+                'parallelism': f'dp{world}',
+                'producers_per_gpu': nprod,
+                'cpus_per_gpu': len(mine),
+                'decode': 'rgba->rgb, gamma 2.2, /255, HWC->CHW fp32 (gfx950 kernel)',
+                'out_shape': list(shape),
+                'proto': args.proto,
+            },
+            'sec_per_image': round(tmax / images, 7),
+            'sec_per_batch': round(tmax / args.steps, 6),
+            'loader_stats': {k: stats.get(k) for k in ('frames', 'batches', 'bad', 'pool_fallbacks')},
+        }), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

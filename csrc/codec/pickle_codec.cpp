@@ -442,6 +442,13 @@ Writer::Writer(int protocol) : protocol_(protocol) {
   op(uint8_t(protocol));
 }
 
+Writer::Writer(int protocol, std::vector<uint8_t>&& storage) : protocol_(protocol), out_(std::move(storage)) {
+  if (protocol < 3 || protocol > 5) throw Unsupported("writer protocol must be 3..5");
+  out_.clear();
+  op(PROTO);
+  op(uint8_t(protocol));
+}
+
 void Writer::raw(const void* p, size_t n) {
   auto* b = static_cast<const uint8_t*>(p);
   out_.insert(out_.end(), b, b + n);

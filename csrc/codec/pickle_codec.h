@@ -70,6 +70,9 @@ std::string describe(const Value& v);
 class Writer {
  public:
   explicit Writer(int protocol = 4);
+  // Reuse `storage`'s capacity (cleared first) -- producers recycle frame
+  // buffers instead of allocating ~1 MB per message.
+  Writer(int protocol, std::vector<uint8_t>&& storage);
   // Dict building (keys are str).  Values written in call order.
   void begin_dict();
   void key(const std::string& k);

@@ -1,0 +1,81 @@
+// gfx950 (CDNA4) kernels for the blendtorch image path.  Host-callable
+// launchers; every pointer is a device pointer, every launch is async on the
+// given stream.
+//
+// The ops are the array ops the reference performs with numpy on the CPU
+// (SURVEY.md §2.5):
+//   * K-flip   np.flipud to upper-left origin      (btb/offscreen.py:95-96)
+//   * K-gamma  u8(255*(x/255)^(1/g)) on RGB        (btb/offscreen.py:105-112)
+//   * K-unpack RGBA -> RGB channel select          (btb/offscreen.py:57-62)
+//   * K-normalize + HWC->CHW                       (examples/densityopt/densityopt.py:117-119)
+//   * K-collate (stack B items)                    (torch default_collate)
+// fused into ONE pass (`decode`), plus a per-pixel 4x4 colour transform on
+// the matrix cores (`color4x4`) and batched pinhole projection (`project`,
+// btb/camera.py:84-162).
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+#include <cstdint>
+
+namespace btn {
+namespace gpu {
+
+enum OutDType : int { OUT_F32 = 0, OUT_BF16 = 1, OUT_F16 = 2, OUT_U8 = 3 };
+enum Layout : int { NCHW = 0, NHWC = 1 };
+
+// Decode a batch of B u8 HWC images into a float/bf16/f16/u8 tensor.
+//   src         B images; image b starts at src + src_offsets[b] (bytes) when
+//               src_offsets != nullptr, else at src + b*H*W*Cin.
+//   lut         device float[4][256]: value for (output channel c, input u8 v).
+//               Gamma, scale and per-channel mean/std are folded into it on
+//               the host (bit-exact with the fp32 reference by construction).
+//   cmap[c]     input channel feeding output channel c (c < Cout).
+//   flip        nullable device u8[B]; 1 = image stored lower-left (GL order).
+//   flip_all    applies to every image (OR-ed with flip[b]).
+//   flip_bits   per-image flip bitmask for b < 256 (kernel-argument copy, so
+//               the stream loader needs no per-batch flag upload).
+struct DecodeParams {
+  const uint8_t* src = nullptr;
+  const int64_t* src_offsets = nullptr;
+  void* dst = nullptr;
+  const float* lut = nullptr;
+  const uint8_t* flip = nullptr;
+  int B = 0, H = 0, W = 0, Cin = 4, Cout = 3;
+  int cmap[4] = {0, 1, 2, 3};
+  int flip_all = 0;
+  uint64_t flip_bits[4] = {0, 0, 0, 0};   // per-image flip for b < 256
+  int out_dtype = OUT_F32;
+  int layout = NCHW;
+};
+hipError_t decode(const DecodeParams& p, hipStream_t stream);
+
+// Per-pixel affine colour transform on the MFMA units:
+//   out[b, c, y, x] = sum_k M[c][k] * lut[k][in[b, y, x, k]] + bias[c]
+// for RGBA u8 HWC input (Cin = 4), f32 NCHW output with Cout <= 4 channels.
+// `lut` is the same folded per-channel table decode() uses (identity for raw
+// values); M is row-major 4x4 f32, bias f32[4] (device pointers).
+struct Color4x4Params {
+  const uint8_t* src = nullptr;
+  const int64_t* src_offsets = nullptr;
+  float* dst = nullptr;
+  const float* lut = nullptr;
+  const float* M = nullptr;
+  const float* bias = nullptr;
+  const uint8_t* flip = nullptr;
+  int B = 0, H = 0, W = 0, Cout = 4;
+  int flip_all = 0;
+  uint64_t flip_bits[4] = {0, 0, 0, 0};
+};
+hipError_t color4x4(const Color4x4Params& p, hipStream_t stream);
+
+// Batched pinhole projection (btb.Camera.world_to_ndc + ndc_to_pixel):
+//   xyzw = [p, 1];  clip = xyzw . (P*V)^T;  ndc = clip.xyz / clip.w
+//   pixel = ((ndc.xy + 1) / 2) * [W, H], y flipped when upper_left.
+//   depth = -(xyzw . V^T).z  (linear camera-space depth)
+// pts: f32 [N,3]; PV, V: f32 row-major 4x4 (device); out_px f32 [N,2];
+// out_depth nullable f32 [N].
+hipError_t project(const float* pts, int64_t N, const float* PV, const float* V, int W, int H,
+                   int upper_left, float* out_px, float* out_depth, hipStream_t stream);
+
+}  // namespace gpu
+}  // namespace btn

@@ -1,0 +1,309 @@
+// gfx950 kernels for the blendtorch image path (see kernels.h).
+//
+// decode: pure streaming op (~1.2 MB read, 3.7 MB fp32 written per 640x480
+// RGBA image), so it is shaped for HBM, not ALU:
+//   * every lane handles PPT consecutive pixels of ONE row, so the HWC->CHW
+//     de-interleave happens in registers: one 16-byte load per lane for RGBA
+//     (12/24 bytes for RGB) and one 16-byte store per output plane -- the
+//     "transpose" needs no LDS round trip because each output plane is a
+//     contiguous run of the same pixels;
+//   * PPT is picked per output dtype so every plane store is exactly 16 B
+//     (f32: 4 px, bf16/f16: 8 px, u8: 16 px);
+//   * gamma + scale + per-channel mean/std are one 1-KiB-per-channel float
+//     table in LDS (one ds_read per element, no pow/div in the kernel, bit-
+//     exact with the fp32 reference because the host builds the table with
+//     the same fp32 expression);
+//   * the vertical flip (GL lower-left readback) is a source-row remap.
+// color4x4: per-pixel 4x4 affine transform on the matrix cores with
+//   v_mfma_f32_4x4x1_16b_f32 (16 independent 4x4 blocks per wave, exact f32):
+//   block = 4 pixels x 4 output channels, K = input channel, 4 MFMAs per
+//   64 pixels; lane l ends up holding output channel (l & 3) of four
+//   consecutive pixels -> one 16-byte store per lane, plane-contiguous.
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace btn {
+namespace gpu {
+
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  // round-to-nearest-even; table values are finite
+  uint32_t u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return uint16_t(u >> 16);
+}
+
+__device__ __forceinline__ uint16_t f2h(float f) {
+  _Float16 h = (_Float16)f;
+  return *reinterpret_cast<uint16_t*>(&h);
+}
+
+template <int PPT, int CIN>
+struct Pixels {
+  uint8_t v[PPT * CIN];
+};
+
+// Load PPT pixels (PPT*CIN bytes) with the widest aligned accesses.
+template <int PPT, int CIN>
+__device__ __forceinline__ void load_pixels(const uint8_t* p, Pixels<PPT, CIN>& px) {
+  constexpr int NB = PPT * CIN;
+  if constexpr (NB % 16 == 0) {
+#pragma unroll
+    for (int i = 0; i < NB / 16; ++i) *reinterpret_cast<uint4*>(&px.v[16 * i]) = reinterpret_cast<const uint4*>(p)[i];
+  } else if constexpr (NB % 8 == 0) {
+#pragma unroll
+    for (int i = 0; i < NB / 8; ++i) *reinterpret_cast<uint2*>(&px.v[8 * i]) = reinterpret_cast<const uint2*>(p)[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < NB / 4; ++i) *reinterpret_cast<uint32_t*>(&px.v[4 * i]) = reinterpret_cast<const uint32_t*>(p)[i];
+  }
+}
+
+template <int PPT, int CIN, int OUTT, int LAYOUT>
+__global__ __launch_bounds__(kBlock) void decode_vec_kernel(DecodeParams p) {
+  __shared__ float lut[4 * 256];
+  for (int i = threadIdx.x; i < p.Cout * 256; i += kBlock) lut[i] = p.lut[i];
+  __syncthreads();
+
+  const int64_t HW = int64_t(p.H) * p.W;
+  const int64_t groups_per_img = HW / PPT;
+  const int64_t total = groups_per_img * p.B;
+  const int cout = p.Cout;
+  int cm[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) cm[c] = p.cmap[c];
+
+  for (int64_t g = int64_t(blockIdx.x) * kBlock + threadIdx.x; g < total; g += int64_t(gridDim.x) * kBlock) {
+    const int b = int(g / groups_per_img);
+    const int64_t q = (g - int64_t(b) * groups_per_img) * PPT;   // first pixel in image
+    const int y = int(q / p.W);
+    const int x = int(q - int64_t(y) * p.W);
+    const bool flip = p.flip_all || (p.flip && p.flip[b]) || (b < 256 && ((p.flip_bits[b >> 6] >> (b & 63)) & 1));
+    const int sy = flip ? p.H - 1 - y : y;
+    const uint8_t* img = p.src + (p.src_offsets ? p.src_offsets[b] : int64_t(b) * HW * CIN);
+    Pixels<PPT, CIN> px;
+    load_pixels<PPT, CIN>(img + (int64_t(sy) * p.W + x) * CIN, px);
+
+    if constexpr (LAYOUT == NCHW) {
+      for (int c = 0; c < cout; ++c) {
+        const float* l = lut + c * 256;
+        const int ic = cm[c];
+        const int64_t off = (int64_t(b) * cout + c) * HW + q;
+        if constexpr (OUTT == OUT_F32) {
+          float o[PPT];
+#pragma unroll
+          for (int i = 0; i < PPT; ++i) o[i] = l[px.v[i * CIN + ic]];
+          float* d = reinterpret_cast<float*>(p.dst) + off;
+#pragma unroll
+          for (int i = 0; i < PPT / 4; ++i) reinterpret_cast<float4*>(d)[i] = make_float4(o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]);
+        } else if constexpr (OUTT == OUT_BF16 || OUTT == OUT_F16) {
+          uint16_t o[PPT];
+#pragma unroll
+          for (int i = 0; i < PPT; ++i) {
+            float v = l[px.v[i * CIN + ic]];
+            o[i] = OUTT == OUT_BF16 ? f2bf(v) : f2h(v);
+          }
+          uint16_t* d = reinterpret_cast<uint16_t*>(p.dst) + off;
+#pragma unroll
+          for (int i = 0; i < PPT / 8; ++i) reinterpret_cast<uint4*>(d)[i] = *reinterpret_cast<const uint4*>(&o[8 * i]);
+        } else {
+          uint8_t o[PPT];
+#pragma unroll
+          for (int i = 0; i < PPT; ++i) o[i] = uint8_t(l[px.v[i * CIN + ic]]);
+          uint8_t* d = reinterpret_cast<uint8_t*>(p.dst) + off;
+#pragma unroll
+          for (int i = 0; i < PPT / 16; ++i) reinterpret_cast<uint4*>(d)[i] = *reinterpret_cast<const uint4*>(&o[16 * i]);
+        }
+      }
+    } else {
+      // NHWC (channels_last): PPT*cout contiguous elements
+      const int64_t off = (int64_t(b) * HW + q) * cout;
+      if constexpr (OUTT == OUT_F32) {
+        float* d = reinterpret_cast<float*>(p.dst) + off;
+        for (int i = 0; i < PPT; ++i)
+          for (int c = 0; c < cout; ++c) d[i * cout + c] = lut[c * 256 + px.v[i * CIN + cm[c]]];
+      } else if constexpr (OUTT == OUT_BF16 || OUTT == OUT_F16) {
+        uint16_t* d = reinterpret_cast<uint16_t*>(p.dst) + off;
+        for (int i = 0; i < PPT; ++i)
+          for (int c = 0; c < cout; ++c) {
+            float v = lut[c * 256 + px.v[i * CIN + cm[c]]];
+            d[i * cout + c] = OUTT == OUT_BF16 ? f2bf(v) : f2h(v);
+          }
+      } else {
+        uint8_t* d = reinterpret_cast<uint8_t*>(p.dst) + off;
+        for (int i = 0; i < PPT; ++i)
+          for (int c = 0; c < cout; ++c) d[i * cout + c] = uint8_t(lut[c * 256 + px.v[i * CIN + cm[c]]]);
+      }
+    }
+  }
+}
+
+// Generic fallback: one pixel per thread (any W, any alignment).
+template <int OUTT>
+__global__ __launch_bounds__(kBlock) void decode_scalar_kernel(DecodeParams p) {
+  __shared__ float lut[4 * 256];
+  for (int i = threadIdx.x; i < p.Cout * 256; i += kBlock) lut[i] = p.lut[i];
+  __syncthreads();
+  const int64_t HW = int64_t(p.H) * p.W;
+  const int64_t total = HW * p.B;
+  for (int64_t g = int64_t(blockIdx.x) * kBlock + threadIdx.x; g < total; g += int64_t(gridDim.x) * kBlock) {
+    const int b = int(g / HW);
+    const int64_t q = g - int64_t(b) * HW;
+    const int y = int(q / p.W), x = int(q - int64_t(y) * p.W);
+    const bool flip = p.flip_all || (p.flip && p.flip[b]) || (b < 256 && ((p.flip_bits[b >> 6] >> (b & 63)) & 1));
+    const int sy = flip ? p.H - 1 - y : y;
+    const uint8_t* img = p.src + (p.src_offsets ? p.src_offsets[b] : int64_t(b) * HW * p.Cin);
+    const uint8_t* s = img + (int64_t(sy) * p.W + x) * p.Cin;
+    for (int c = 0; c < p.Cout; ++c) {
+      float v = lut[c * 256 + s[p.cmap[c]]];
+      int64_t off = p.layout == NCHW ? (int64_t(b) * p.Cout + c) * HW + q : (int64_t(b) * HW + q) * p.Cout + c;
+      if constexpr (OUTT == OUT_F32) reinterpret_cast<float*>(p.dst)[off] = v;
+      else if constexpr (OUTT == OUT_BF16) reinterpret_cast<uint16_t*>(p.dst)[off] = f2bf(v);
+      else if constexpr (OUTT == OUT_F16) reinterpret_cast<uint16_t*>(p.dst)[off] = f2h(v);
+      else reinterpret_cast<uint8_t*>(p.dst)[off] = uint8_t(v);
+    }
+  }
+}
+
+int grid_for(int64_t work) {
+  // 256 CUs x 8 resident 256-thread blocks; grid-stride beyond that
+  int64_t blocks = (work + kBlock - 1) / kBlock;
+  return int(blocks < 2048 ? (blocks > 0 ? blocks : 1) : 2048);
+}
+
+template <int PPT, int CIN, int OUTT>
+hipError_t launch_vec(const DecodeParams& p, hipStream_t s) {
+  int64_t work = int64_t(p.B) * p.H * p.W / PPT;
+  if (p.layout == NCHW)
+    decode_vec_kernel<PPT, CIN, OUTT, NCHW><<<grid_for(work), kBlock, 0, s>>>(p);
+  else
+    decode_vec_kernel<PPT, CIN, OUTT, NHWC><<<grid_for(work), kBlock, 0, s>>>(p);
+  return hipGetLastError();
+}
+
+template <int OUTT>
+hipError_t launch_out(const DecodeParams& p, hipStream_t s) {
+  constexpr int PPT = OUTT == OUT_F32 ? 4 : (OUTT == OUT_U8 ? 16 : 8);
+  // vector path: a lane's PPT pixels sit in one row and its loads are aligned
+  bool aligned = (p.W % PPT) == 0 && (int64_t(p.H) * p.W * p.Cin) % 16 == 0 && (reinterpret_cast<uintptr_t>(p.dst) % 16) == 0 &&
+                 (reinterpret_cast<uintptr_t>(p.src) % 16) == 0 && p.src_offsets == nullptr;
+  if (aligned && p.Cin == 4) return launch_vec<PPT, 4, OUTT>(p, s);
+  if (aligned && p.Cin == 3) return launch_vec<PPT, 3, OUTT>(p, s);
+  int64_t work = int64_t(p.B) * p.H * p.W;
+  decode_scalar_kernel<OUTT><<<grid_for(work), kBlock, 0, s>>>(p);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t decode(const DecodeParams& p, hipStream_t stream) {
+  if (p.B <= 0 || p.H <= 0 || p.W <= 0) return hipSuccess;
+  if (p.Cout < 1 || p.Cout > 4 || p.Cin < 1 || p.Cin > 4) return hipErrorInvalidValue;
+  for (int c = 0; c < p.Cout; ++c)
+    if (p.cmap[c] < 0 || p.cmap[c] >= p.Cin) return hipErrorInvalidValue;
+  switch (p.out_dtype) {
+    case OUT_F32: return launch_out<OUT_F32>(p, stream);
+    case OUT_BF16: return launch_out<OUT_BF16>(p, stream);
+    case OUT_F16: return launch_out<OUT_F16>(p, stream);
+    case OUT_U8: return launch_out<OUT_U8>(p, stream);
+  }
+  return hipErrorInvalidValue;
+}
+
+// ---------------------------------------------------------------------------
+// color4x4 on MFMA (v_mfma_f32_4x4x1_16b_f32)
+// ---------------------------------------------------------------------------
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Each wave owns 64 consecutive pixels of one row segment per iteration.
+// Operand map of the 16-block 4x4x1 MFMA: block = lane>>2, A[i=lane&3][0],
+// B[0][j=lane&3], D[i=reg][j=lane&3].  We set block = 4 pixels, i = pixel in
+// block, j = output channel, k = input channel (4 MFMAs accumulate k=0..3):
+//   lane l supplies A = in[pixel l][k] and B = M[l&3][k];
+//   lane l receives D[r] = out[pixel 4*(l>>2)+r][channel l&3].
+__global__ __launch_bounds__(kBlock) void color4x4_kernel(Color4x4Params p) {
+  __shared__ float lut[4 * 256];
+  for (int i = threadIdx.x; i < 4 * 256; i += kBlock) lut[i] = p.lut[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int j = lane & 3;
+  float bm[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) bm[k] = p.M[j * 4 + k];
+  const float bj = p.bias[j];
+  const int64_t HW = int64_t(p.H) * p.W;
+  const int64_t segs_per_img = HW / 64;   // host guarantees W % 64 == 0
+  const int64_t total = segs_per_img * p.B;
+  const int64_t stride = int64_t(gridDim.x) * (kBlock / 64);
+  for (int64_t g = int64_t(blockIdx.x) * (kBlock / 64) + wave; g < total; g += stride) {
+    const int b = int(g / segs_per_img);
+    const int64_t q0 = (g - int64_t(b) * segs_per_img) * 64;
+    const int y = int(q0 / p.W), x0 = int(q0 - int64_t(y) * p.W);
+    const bool flip = p.flip_all || (p.flip && p.flip[b]) || (b < 256 && ((p.flip_bits[b >> 6] >> (b & 63)) & 1));
+    const int sy = flip ? p.H - 1 - y : y;
+    const uint8_t* img = p.src + (p.src_offsets ? p.src_offsets[b] : int64_t(b) * HW * 4);
+    const uchar4 v = reinterpret_cast<const uchar4*>(img + (int64_t(sy) * p.W + x0) * 4)[lane];
+    const float a0 = lut[0 * 256 + v.x], a1 = lut[1 * 256 + v.y], a2 = lut[2 * 256 + v.z], a3 = lut[3 * 256 + v.w];
+    f32x4 acc = {bj, bj, bj, bj};
+    acc = __builtin_amdgcn_mfma_f32_4x4x1f32(a0, bm[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_4x4x1f32(a1, bm[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_4x4x1f32(a2, bm[2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_4x4x1f32(a3, bm[3], acc, 0, 0, 0);
+    if (j < p.Cout) {
+      float* d = p.dst + (int64_t(b) * p.Cout + j) * HW + q0 + 4 * (lane >> 2);
+      *reinterpret_cast<float4*>(d) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    }
+  }
+}
+
+__global__ void project_kernel(const float* pts, int64_t N, const float* PV, const float* V, int W, int H,
+                               int upper_left, float* out_px, float* out_depth) {
+  __shared__ float m[32];
+  if (threadIdx.x < 16) m[threadIdx.x] = PV[threadIdx.x];
+  else if (threadIdx.x < 32) m[threadIdx.x] = V[threadIdx.x - 16];
+  __syncthreads();
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < N; i += int64_t(gridDim.x) * blockDim.x) {
+    const float x = pts[3 * i], y = pts[3 * i + 1], z = pts[3 * i + 2];
+    float c[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) c[r] = m[4 * r] * x + m[4 * r + 1] * y + m[4 * r + 2] * z + m[4 * r + 3];
+    const float nx = c[0] / c[3], ny = c[1] / c[3];
+    float px = (nx + 1.f) * 0.5f, py = (ny + 1.f) * 0.5f;
+    if (upper_left) py = 1.f - py;
+    out_px[2 * i] = px * W;
+    out_px[2 * i + 1] = py * H;
+    if (out_depth) out_depth[i] = -(m[16 + 8] * x + m[16 + 9] * y + m[16 + 10] * z + m[16 + 11]);
+  }
+}
+
+}  // namespace
+
+hipError_t color4x4(const Color4x4Params& p, hipStream_t stream) {
+  if (p.B <= 0) return hipSuccess;
+  if (p.W % 64 != 0 || p.Cout < 1 || p.Cout > 4 || (reinterpret_cast<uintptr_t>(p.dst) % 16) != 0)
+    return hipErrorInvalidValue;
+  int64_t waves = int64_t(p.B) * p.H * p.W / 64;
+  int64_t blocks = (waves + 3) / 4;
+  int grid = int(blocks < 4096 ? blocks : 4096);
+  color4x4_kernel<<<grid, kBlock, 0, stream>>>(p);
+  return hipGetLastError();
+}
+
+hipError_t project(const float* pts, int64_t N, const float* PV, const float* V, int W, int H, int upper_left,
+                   float* out_px, float* out_depth, hipStream_t stream) {
+  if (N <= 0) return hipSuccess;
+  int64_t blocks = (N + kBlock - 1) / kBlock;
+  int grid = int(blocks < 1024 ? blocks : 1024);
+  project_kernel<<<grid, kBlock, 0, stream>>>(pts, N, PV, V, W, H, upper_left, out_px, out_depth);
+  return hipGetLastError();
+}
+
+}  // namespace gpu
+}  // namespace btn

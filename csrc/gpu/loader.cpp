@@ -1,0 +1,431 @@
+// StreamLoader implementation (see loader.h).
+#include "loader.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <stdexcept>
+
+namespace btn {
+namespace gpu {
+
+namespace {
+
+void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Remove the image entry from the dict and shift every payload offset that
+// lies behind the cut so the tree indexes the compacted metadata bytes.
+void shift_offsets(codec::Value& v, size_t cut, size_t len) {
+  if (v.kind == codec::Value::BYTES || v.kind == codec::Value::NDARRAY || v.np_scalar) {
+    if (v.off >= cut + len) v.off -= len;
+  }
+  for (auto& c : v.items)
+    if (c) shift_offsets(*c, cut, len);
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    (void)hipGetDevice(&prev);
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    if (prev >= 0 && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// PinnedPool
+// ---------------------------------------------------------------------------
+PinnedPool::PinnedPool(size_t slot_bytes, int nslots) : slot_bytes_(slot_bytes), nslots_(nslots) {
+  check(hipHostMalloc(reinterpret_cast<void**>(&base_), slot_bytes_ * size_t(nslots_), hipHostMallocDefault),
+        "hipHostMalloc(pinned pool)");
+  free_.reserve(size_t(nslots_));
+  for (int i = nslots_ - 1; i >= 0; --i) free_.push_back(i);
+}
+
+PinnedPool::~PinnedPool() {
+  if (base_) (void)hipHostFree(base_);
+}
+
+int PinnedPool::free_slots() {
+  std::lock_guard<std::mutex> lk(mu_);
+  return int(free_.size());
+}
+
+BufPtr PinnedPool::alloc(size_t n) {
+  if (n > slot_bytes_) {
+    fallbacks_++;
+    return nullptr;
+  }
+  int id;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (free_.empty()) {
+      fallbacks_++;
+      return nullptr;
+    }
+    id = free_.back();
+    free_.pop_back();
+  }
+  auto b = std::make_shared<Buffer>();
+  b->data = base_ + size_t(id) * slot_bytes_;
+  b->capacity = slot_bytes_;
+  b->owner = this;
+  b->tag = id;
+  b->pinned = true;
+  b->release = &PinnedPool::release;
+  return b;
+}
+
+void PinnedPool::release(void* owner, Buffer* b) {
+  auto* self = static_cast<PinnedPool*>(owner);
+  std::lock_guard<std::mutex> lk(self->mu_);
+  self->free_.push_back(int(b->tag));
+}
+
+// ---------------------------------------------------------------------------
+// StreamLoader
+// ---------------------------------------------------------------------------
+StreamLoader::StreamLoader(const LoaderConfig& cfg) : cfg_(cfg) {
+  if (cfg_.addresses.empty()) throw std::invalid_argument("StreamLoader: no addresses");
+  if (cfg_.batch_size < 1) throw std::invalid_argument("StreamLoader: batch_size < 1");
+  if (cfg_.lut.size() != 4 * 256) throw std::invalid_argument("StreamLoader: lut must hold 4*256 floats");
+  if (cfg_.cout < 1 || cfg_.cout > 4) throw std::invalid_argument("StreamLoader: cout must be 1..4");
+  if (cfg_.color_matrix && (cfg_.matrix.size() != 16 || cfg_.bias.size() != 4))
+    throw std::invalid_argument("StreamLoader: colour matrix needs 16 + 4 floats");
+  int k = std::max(1, std::min<int>(cfg_.io_threads, int(cfg_.addresses.size())));
+  for (int i = 0; i < k; ++i) {
+    ctxs_.emplace_back(new zmtp::Context());
+    auto s = ctxs_.back()->socket(zmtp::PULL);
+    s->setsockopt(zmtp::RCVHWM, cfg_.rcvhwm);
+    s->setsockopt(zmtp::LINGER, 0);
+    socks_.push_back(s);
+  }
+  for (size_t i = 0; i < cfg_.addresses.size(); ++i) socks_[i % socks_.size()]->connect(cfg_.addresses[i]);
+}
+
+StreamLoader::~StreamLoader() { stop(); }
+
+void StreamLoader::start() {
+  if (worker_.joinable()) return;
+  worker_ = std::thread([this] {
+    try {
+      run();
+    } catch (const std::exception& e) {
+      std::lock_guard<std::mutex> lk(mu_);
+      error_ = e.what();
+    }
+    cv_.notify_all();
+  });
+}
+
+bool StreamLoader::wait_shape(long timeout_ms, int* H, int* W, int* C) {
+  std::unique_lock<std::mutex> lk(mu_);
+  cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return have_shape_ || !error_.empty(); });
+  if (!error_.empty()) throw std::runtime_error(error_);
+  if (!have_shape_) return false;
+  *H = H_;
+  *W = W_;
+  *C = C_;
+  return true;
+}
+
+void StreamLoader::post(void* dst, hipStream_t consumer) {
+  DeviceGuard g(cfg_.device);
+  hipEvent_t ev;
+  check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+  check(hipEventRecord(ev, consumer), "hipEventRecord(post)");
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    posted_.push_back({dst, ev});
+  }
+  cv_.notify_all();
+}
+
+bool StreamLoader::next(ReadyBatch* out, hipStream_t consumer, long timeout_ms) {
+  std::unique_lock<std::mutex> lk(mu_);
+  cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms),
+               [&] { return !ready_.empty() || !error_.empty() || exhausted_; });
+  if (ready_.empty()) {
+    if (!error_.empty()) throw std::runtime_error(error_);
+    if (exhausted_) {
+      out->index = -1;
+      return true;
+    }
+    return false;
+  }
+  *out = std::move(ready_.front());
+  ready_.pop_front();
+  lk.unlock();
+  DeviceGuard g(cfg_.device);
+  check(hipStreamWaitEvent(consumer, out->done, 0), "hipStreamWaitEvent");
+  (void)hipEventDestroy(out->done);
+  out->done = nullptr;
+  return true;
+}
+
+void StreamLoader::stop() {
+  stop_ = true;
+  cv_.notify_all();
+  if (worker_.joinable()) worker_.join();
+  for (auto& s : socks_) s->close(0);
+  socks_.clear();
+  ctxs_.clear();   // joins IO threads; queued frames are released
+  DeviceGuard g(cfg_.device);
+  if (stream_) {
+    (void)hipStreamSynchronize(stream_);   // pending host callbacks drop pinned refs
+    (void)hipStreamDestroy(stream_);
+    stream_ = nullptr;
+  }
+  cur_.clear();
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (auto& p : posted_) (void)hipEventDestroy(p.ready);
+    posted_.clear();
+    for (auto& r : ready_)
+      if (r.done) (void)hipEventDestroy(r.done);
+    ready_.clear();
+  }
+  for (auto* p : staging_) (void)hipFree(p);
+  staging_.clear();
+  if (d_lut_) (void)hipFree(d_lut_);
+  if (d_mat_) (void)hipFree(d_mat_);
+  d_lut_ = d_mat_ = nullptr;
+  pool_.reset();
+}
+
+LoaderStats StreamLoader::stats() {
+  std::lock_guard<std::mutex> lk(mu_);
+  LoaderStats s = stats_;
+  s.pool_fallbacks = pool_ ? pool_->fallbacks() : 0;
+  return s;
+}
+
+void StreamLoader::run() {
+  check(hipSetDevice(cfg_.device), "hipSetDevice");
+  check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+  std::vector<std::pair<zmtp::Socket*, int>> items;
+  for (auto& s : socks_) items.emplace_back(s.get(), zmtp::POLLIN);
+  const auto intr = [this] { return stop_.load(); };
+  const int64_t max_frames = cfg_.max_batches < 0 ? -1 : cfg_.max_batches * cfg_.batch_size;
+  int64_t taken = 0;
+  while (!stop_) {
+    if (max_frames >= 0 && taken >= max_frames) break;
+    std::vector<int> ev;
+    try {
+      ev = zmtp::Socket::poll(items, 100, intr);
+    } catch (const zmtp::Error& e) {
+      if (e.code == zmtp::E_INTR) break;
+      throw;
+    }
+    for (size_t i = 0; i < ev.size() && !stop_; ++i) {
+      if (!(ev[i] & zmtp::POLLIN)) continue;
+      // drain what is queued on this socket (bounded, to stay fair)
+      for (int n = 0; n < 64 && !stop_; ++n) {
+        if (max_frames >= 0 && taken >= max_frames) break;
+        zmtp::Message m;
+        try {
+          m = socks_[i]->recv(zmtp::DONTWAIT);
+        } catch (const zmtp::Error& e) {
+          if (e.code == zmtp::E_AGAIN) break;
+          throw;
+        }
+        if (process(std::move(m))) ++taken;
+      }
+    }
+  }
+  std::lock_guard<std::mutex> lk(mu_);
+  exhausted_ = true;
+}
+
+bool StreamLoader::process(zmtp::Message&& msg) {
+  auto bad = [&](const std::string& why) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stats_.bad++;
+      if (!cfg_.skip_bad && error_.empty()) error_ = "StreamLoader: bad message: " + why;
+    }
+    cv_.notify_all();
+    if (!cfg_.skip_bad) stop_ = true;
+    return false;
+  };
+  if (msg.size() != 1) return bad("expected a single-frame message");
+  Item it;
+  it.frame = std::move(msg[0]);
+  const uint8_t* data = it.frame.data();
+  const size_t n = it.frame.size;
+  codec::VPtr root;
+  try {
+    root = codec::parse(data, n);
+  } catch (const std::exception& e) {
+    return bad(std::string("unparseable pickle (") + e.what() + ")");
+  }
+  if (!root || root->kind != codec::Value::DICT) return bad("payload is not a dict");
+  size_t img_idx = size_t(-1);
+  for (size_t i = 0; i + 1 < root->items.size(); i += 2)
+    if (root->items[i]->kind == codec::Value::STR && root->items[i]->s == cfg_.image_key) img_idx = i;
+  if (img_idx == size_t(-1)) return bad("no '" + cfg_.image_key + "' entry");
+  const codec::Value& img = *root->items[img_idx + 1];
+  if (img.kind != codec::Value::NDARRAY || img.dtype != "|u1" || img.fortran)
+    return bad("image must be a C-contiguous uint8 ndarray");
+  int h, w, c;
+  if (img.shape.size() == 3) {
+    h = int(img.shape[0]), w = int(img.shape[1]), c = int(img.shape[2]);
+  } else if (img.shape.size() == 2) {
+    h = int(img.shape[0]), w = int(img.shape[1]), c = 1;
+  } else {
+    return bad("image must be HxW or HxWxC");
+  }
+  if (c < 1 || c > 4) return bad("image channels must be 1..4");
+  if (const codec::Value* o = root->get("origin"))
+    it.flip = o->kind == codec::Value::STR && o->s == "lower-left";
+
+  if (!have_shape_) {
+    for (int k = 0; k < cfg_.cout; ++k)
+      if (cfg_.cmap[k] >= c) throw std::runtime_error("StreamLoader: channel map exceeds image channels");
+    if (cfg_.color_matrix && c != 4) throw std::runtime_error("StreamLoader: colour matrix needs RGBA input");
+    img_bytes_ = size_t(h) * w * c;
+    size_t slot = cfg_.max_frame_bytes ? cfg_.max_frame_bytes : size_t(double(n) * 1.05) + 4096;
+    slot = (slot + 4095) & ~size_t(4095);
+    int nslots = cfg_.pool_slots;
+    if (nslots <= 0) nslots = int(cfg_.addresses.size()) * (cfg_.rcvhwm + 2) + (cfg_.staging_depth + 4) * cfg_.batch_size;
+    pool_ = std::make_shared<PinnedPool>(slot, nslots);
+    for (auto& s : socks_) s->set_allocator(pool_, 64 * 1024);
+    for (int k = 0; k < std::max(2, cfg_.staging_depth); ++k) {
+      uint8_t* p = nullptr;
+      check(hipMalloc(reinterpret_cast<void**>(&p), img_bytes_ * size_t(cfg_.batch_size)), "hipMalloc(staging)");
+      staging_.push_back(p);
+    }
+    check(hipMalloc(reinterpret_cast<void**>(&d_lut_), 4 * 256 * sizeof(float)), "hipMalloc(lut)");
+    check(hipMemcpy(d_lut_, cfg_.lut.data(), 4 * 256 * sizeof(float), hipMemcpyHostToDevice), "upload lut");
+    if (cfg_.color_matrix) {
+      check(hipMalloc(reinterpret_cast<void**>(&d_mat_), 20 * sizeof(float)), "hipMalloc(matrix)");
+      std::vector<float> mb(cfg_.matrix);
+      mb.insert(mb.end(), cfg_.bias.begin(), cfg_.bias.end());
+      check(hipMemcpy(d_mat_, mb.data(), 20 * sizeof(float), hipMemcpyHostToDevice), "upload matrix");
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      H_ = h, W_ = w, C_ = c;
+      have_shape_ = true;
+    }
+    cv_.notify_all();
+  } else if (h != H_ || w != W_ || c != C_) {
+    return bad("image shape changed within the stream");
+  }
+  it.img_off = img.off;
+
+  // metadata: the frame minus the image payload, tree re-based onto it
+  const size_t cut = img.off, len = img.len;
+  it.meta.bytes.reserve(n - len);
+  it.meta.bytes.insert(it.meta.bytes.end(), data, data + cut);
+  it.meta.bytes.insert(it.meta.bytes.end(), data + cut + len, data + n);
+  root->items.erase(root->items.begin() + long(img_idx), root->items.begin() + long(img_idx) + 2);
+  shift_offsets(*root, cut, len);
+  it.meta.tree = root;
+
+  if (cur_.empty()) batch_t0_ = now_ms();
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stats_.frames++;
+    stats_.bytes += n;
+  }
+  cur_.push_back(std::move(it));
+  if (int(cur_.size()) == cfg_.batch_size) launch();
+  return true;
+}
+
+void StreamLoader::on_copied(void* user) {
+  // runs on a HIP runtime thread once the H2D copies of a batch completed:
+  // dropping the frames returns their pinned slots to the pool
+  delete static_cast<std::vector<zmtp::Frame>*>(user);
+}
+
+void StreamLoader::launch() {
+  Posted p{nullptr, nullptr};
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    while (posted_.empty() && !stop_) cv_.wait_for(lk, std::chrono::milliseconds(100));
+    if (stop_) return;
+    p = posted_.front();
+    posted_.pop_front();
+  }
+  const double t_issue = now_ms();
+  const int B = int(cur_.size());
+  uint8_t* stage = staging_[size_t(batch_index_) % staging_.size()];
+  check(hipStreamWaitEvent(stream_, p.ready, 0), "hipStreamWaitEvent(post)");
+  (void)hipEventDestroy(p.ready);
+  uint64_t flips[4] = {0, 0, 0, 0};
+  for (int i = 0; i < B; ++i) {
+    const Item& it = cur_[size_t(i)];
+    check(hipMemcpyAsync(stage + size_t(i) * img_bytes_, it.frame.data() + it.img_off, img_bytes_,
+                         hipMemcpyHostToDevice, stream_),
+          "hipMemcpyAsync(H2D)");
+    if (it.flip && i < 256) flips[i >> 6] |= uint64_t(1) << (i & 63);
+  }
+  bool any_flip_beyond = false;
+  for (int i = 256; i < B; ++i) any_flip_beyond |= cur_[size_t(i)].flip;
+  if (any_flip_beyond) throw std::runtime_error("StreamLoader: per-image flip supports batch <= 256");
+  hipError_t e;
+  if (cfg_.color_matrix) {
+    Color4x4Params cp;
+    cp.src = stage;
+    cp.dst = static_cast<float*>(p.dst);
+    cp.lut = d_lut_;
+    cp.M = d_mat_;
+    cp.bias = d_mat_ + 16;
+    cp.B = B, cp.H = H_, cp.W = W_, cp.Cout = cfg_.cout;
+    cp.flip_all = cfg_.flip_all;
+    std::memcpy(cp.flip_bits, flips, sizeof(flips));
+    e = color4x4(cp, stream_);
+  } else {
+    DecodeParams dp;
+    dp.src = stage;
+    dp.dst = p.dst;
+    dp.lut = d_lut_;
+    dp.B = B, dp.H = H_, dp.W = W_, dp.Cin = C_, dp.Cout = cfg_.cout;
+    std::memcpy(dp.cmap, cfg_.cmap, sizeof(dp.cmap));
+    dp.flip_all = cfg_.flip_all;
+    std::memcpy(dp.flip_bits, flips, sizeof(flips));
+    dp.out_dtype = cfg_.out_dtype;
+    dp.layout = cfg_.layout;
+    e = decode(dp, stream_);
+  }
+  check(e, "decode kernel launch");
+  auto* held = new std::vector<zmtp::Frame>();
+  held->reserve(size_t(B));
+  ReadyBatch rb;
+  rb.index = batch_index_;
+  rb.items.reserve(size_t(B));
+  for (auto& it : cur_) {
+    held->push_back(std::move(it.frame));
+    rb.items.push_back(std::move(it.meta));
+  }
+  cur_.clear();
+  check(hipLaunchHostFunc(stream_, &StreamLoader::on_copied, held), "hipLaunchHostFunc");
+  check(hipEventCreateWithFlags(&rb.done, hipEventDisableTiming), "hipEventCreate(done)");
+  check(hipEventRecord(rb.done, stream_), "hipEventRecord(done)");
+  rb.recv_ms = t_issue - batch_t0_;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stats_.batches++;
+    stats_.h2d_issue_ms += now_ms() - t_issue;
+    ready_.push_back(std::move(rb));
+  }
+  cv_.notify_all();
+  ++batch_index_;
+}
+
+}  // namespace gpu
+}  // namespace btn

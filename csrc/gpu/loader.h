@@ -1,0 +1,175 @@
+// StreamLoader: producer frames -> pinned host slots -> HBM -> decoded batch.
+//
+// Replaces the reference's receive path (pkg_pytorch/blendtorch/btt/
+// dataset.py:64-117 PULL socket per DataLoader worker + pickle.loads +
+// default_collate + worker->main shared-memory copy) with one native
+// pipeline per GPU rank:
+//
+//   producers --PUSH/ZMTP--> K PULL sockets (K IO threads, fair-queued)
+//     -> frame bodies read by the IO thread straight into hipHostMalloc'd
+//        slots (PinnedPool is the socket allocator; no intermediate copy)
+//     -> worker thread: zero-copy pickle scan locates the image payload,
+//        copies only the small non-image bytes (metadata) out
+//     -> B items assembled into batch j; hipMemcpyAsync of every image into
+//        the device staging ring on a private non-blocking HIP stream
+//     -> fused decode kernel (flip/gamma/unpack/normalize/CHW) writes into
+//        the consumer-posted output buffer; host callback recycles the pinned
+//        slots once the DMA has landed; hipEvent marks the batch ready
+//     -> consumer (Python) takes batch j; its torch stream waits on the event.
+//
+// Backpressure is preserved end to end: when the consumer stops posting
+// output buffers the worker stops receiving, each pipe fills to RCVHWM, the
+// TCP window closes and the producers block at SNDHWM -- exactly the
+// behaviour the reference's PUSH/PULL + HWM gives (btb/publisher.py:21-28).
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../codec/pickle_codec.h"
+#include "../common/buffer.h"
+#include "../transport/zmtp.h"
+#include "kernels.h"
+
+namespace btn {
+namespace gpu {
+
+// Fixed-size pinned host slots handed to the transport as its frame
+// allocator.  A slot returns to the pool when the last reference to its
+// Buffer drops (after the H2D copy that reads it has completed).
+class PinnedPool : public Allocator, public std::enable_shared_from_this<PinnedPool> {
+ public:
+  PinnedPool(size_t slot_bytes, int nslots);
+  ~PinnedPool() override;
+  BufPtr alloc(size_t n) override;   // nullptr (heap fallback) if n too big or pool dry
+  size_t slot_bytes() const { return slot_bytes_; }
+  int nslots() const { return nslots_; }
+  int free_slots();
+  uint64_t fallbacks() const { return fallbacks_.load(); }
+
+ private:
+  static void release(void* owner, Buffer* b);
+  size_t slot_bytes_;
+  int nslots_;
+  uint8_t* base_ = nullptr;
+  std::mutex mu_;
+  std::vector<int> free_;
+  std::atomic<uint64_t> fallbacks_{0};
+};
+
+struct LoaderConfig {
+  std::vector<std::string> addresses;
+  int batch_size = 8;
+  std::string image_key = "image";
+  int rcvhwm = 10;
+  int io_threads = 1;
+  int device = 0;
+  int64_t max_batches = -1;          // -1: stream forever
+  size_t max_frame_bytes = 0;        // 0: infer from first frame (x1.05 + 4 KiB)
+  int pool_slots = 0;                // 0: auto
+  int staging_depth = 3;
+  bool skip_bad = false;             // drop malformed messages instead of failing
+  // decode parameters (src/dst/B/H/W/Cin filled per batch)
+  int cout = 3;
+  int cmap[4] = {0, 1, 2, 3};
+  int flip_all = 0;
+  int out_dtype = OUT_F32;
+  int layout = NCHW;
+  std::vector<float> lut;            // 4*256 floats (host)
+  bool color_matrix = false;         // use the MFMA colour-transform kernel
+  std::vector<float> matrix, bias;   // 16 + 4 floats
+};
+
+// One delivered batch: metadata of each item (non-image bytes of the frame,
+// re-based) and the event that completes its device work.
+struct BatchMeta {
+  std::vector<uint8_t> bytes;        // frame with the image payload cut out
+  codec::VPtr tree;                  // parse tree over `bytes` (image entry removed)
+};
+
+struct ReadyBatch {
+  int64_t index = -1;
+  std::vector<BatchMeta> items;
+  hipEvent_t done = nullptr;
+  double recv_ms = 0;                // wall time spent assembling the batch
+};
+
+struct LoaderStats {
+  uint64_t frames = 0, batches = 0, bytes = 0, bad = 0, pool_fallbacks = 0;
+  double h2d_issue_ms = 0;
+};
+
+class StreamLoader {
+ public:
+  explicit StreamLoader(const LoaderConfig& cfg);
+  ~StreamLoader();
+
+  void start();
+  // Blocks until the first frame fixed H, W, Cin (or timeout -> false).
+  bool wait_shape(long timeout_ms, int* H, int* W, int* C);
+  // Queue an output buffer for the next batch.  An event recorded on
+  // `consumer` now is waited on by the loader stream before it writes, so
+  // the caching allocator's reuse of `dst` is safe.
+  void post(void* dst, hipStream_t consumer);
+  // Next completed batch (in order).  Makes `consumer` wait on its event.
+  // Returns false on timeout; throws std::runtime_error on a loader error
+  // or when the stream is exhausted (max_batches reached -> index == -1).
+  bool next(ReadyBatch* out, hipStream_t consumer, long timeout_ms);
+  void stop();
+  LoaderStats stats();
+
+ private:
+  struct Item {
+    zmtp::Frame frame;
+    size_t img_off = 0;
+    bool flip = false;
+    BatchMeta meta;
+  };
+  struct Posted {
+    void* dst;
+    hipEvent_t ready;
+  };
+  void run();
+  bool process(zmtp::Message&& msg);
+  void launch();
+  static void on_copied(void* user);
+
+  LoaderConfig cfg_;
+  std::vector<std::unique_ptr<zmtp::Context>> ctxs_;
+  std::vector<std::shared_ptr<zmtp::Socket>> socks_;
+  std::shared_ptr<PinnedPool> pool_;
+  std::thread worker_;
+  std::atomic<bool> stop_{false};
+
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool have_shape_ = false;
+  int H_ = 0, W_ = 0, C_ = 0;
+  size_t img_bytes_ = 0;
+  std::deque<Posted> posted_;
+  std::deque<ReadyBatch> ready_;
+  std::string error_;
+  bool exhausted_ = false;
+
+  // worker-thread state
+  hipStream_t stream_ = nullptr;
+  std::vector<uint8_t*> staging_;
+  float* d_lut_ = nullptr;
+  float* d_mat_ = nullptr;   // 16 matrix + 4 bias
+  std::vector<Item> cur_;
+  int64_t batch_index_ = 0;
+  double batch_t0_ = 0;
+  LoaderStats stats_;
+};
+
+}  // namespace gpu
+}  // namespace btn

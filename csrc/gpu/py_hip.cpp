@@ -1,0 +1,189 @@
+// pybind11 bindings of the GPU side: gfx950 kernels (pointer-level, the
+// Python layer passes torch tensors' data_ptr() and stream handles) and the
+// StreamLoader.  Built as `blendtorch/_hip*.so` by hipcc for gfx950; it links
+// the HIP runtime torch already loaded (same soname), so device pointers and
+// streams are shared with torch.
+#include <hip/hip_runtime_api.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <stdexcept>
+
+#include "../python/pyvalue.h"
+#include "kernels.h"
+#include "loader.h"
+
+namespace py = pybind11;
+using namespace btn;
+using namespace btn::gpu;
+
+namespace {
+
+template <typename T>
+T* ptr(uintptr_t p) {
+  return reinterpret_cast<T*>(p);
+}
+
+hipStream_t stream_of(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+void fill_cmap(int* dst, const std::vector<int>& cmap) {
+  for (size_t i = 0; i < 4; ++i) dst[i] = i < cmap.size() ? cmap[i] : int(i);
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_hip, m) {
+  m.doc() = "blendtorch gfx950 kernels + GPU stream loader";
+
+  m.def("runtime_version", [] {
+    int v = 0;
+    hipRuntimeGetVersion(&v);
+    return v;
+  });
+  m.def("device_count", [] {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+  });
+  m.def("device_arch", [](int dev) {
+    hipDeviceProp_t p;
+    check(hipGetDeviceProperties(&p, dev), "hipGetDeviceProperties");
+    return std::string(p.gcnArchName);
+  });
+
+  m.def("decode",
+        [](uintptr_t src, uintptr_t src_offsets, uintptr_t dst, uintptr_t lut, uintptr_t flip, int B, int H, int W,
+           int Cin, int Cout, std::vector<int> cmap, int flip_all, int out_dtype, int layout, uintptr_t stream) {
+          DecodeParams p;
+          p.src = ptr<const uint8_t>(src);
+          p.src_offsets = ptr<const int64_t>(src_offsets);
+          p.dst = ptr<void>(dst);
+          p.lut = ptr<const float>(lut);
+          p.flip = ptr<const uint8_t>(flip);
+          p.B = B, p.H = H, p.W = W, p.Cin = Cin, p.Cout = Cout;
+          fill_cmap(p.cmap, cmap);
+          p.flip_all = flip_all;
+          p.out_dtype = out_dtype;
+          p.layout = layout;
+          check(decode(p, stream_of(stream)), "decode");
+        },
+        py::arg("src"), py::arg("src_offsets"), py::arg("dst"), py::arg("lut"), py::arg("flip"), py::arg("B"),
+        py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("Cout"), py::arg("cmap"), py::arg("flip_all"),
+        py::arg("out_dtype"), py::arg("layout"), py::arg("stream"));
+
+  m.def("color4x4",
+        [](uintptr_t src, uintptr_t dst, uintptr_t lut, uintptr_t M, uintptr_t bias, uintptr_t flip, int B, int H,
+           int W, int Cout, int flip_all, uintptr_t stream) {
+          Color4x4Params p;
+          p.src = ptr<const uint8_t>(src);
+          p.dst = ptr<float>(dst);
+          p.lut = ptr<const float>(lut);
+          p.M = ptr<const float>(M);
+          p.bias = ptr<const float>(bias);
+          p.flip = ptr<const uint8_t>(flip);
+          p.B = B, p.H = H, p.W = W, p.Cout = Cout;
+          p.flip_all = flip_all;
+          check(color4x4(p, stream_of(stream)), "color4x4");
+        },
+        py::arg("src"), py::arg("dst"), py::arg("lut"), py::arg("M"), py::arg("bias"), py::arg("flip"), py::arg("B"),
+        py::arg("H"), py::arg("W"), py::arg("Cout"), py::arg("flip_all"), py::arg("stream"));
+
+  m.def("project",
+        [](uintptr_t pts, int64_t N, uintptr_t PV, uintptr_t V, int W, int H, int upper_left, uintptr_t out_px,
+           uintptr_t out_depth, uintptr_t stream) {
+          check(project(ptr<const float>(pts), N, ptr<const float>(PV), ptr<const float>(V), W, H, upper_left,
+                        ptr<float>(out_px), ptr<float>(out_depth), stream_of(stream)),
+                "project");
+        });
+
+  py::class_<StreamLoader>(m, "StreamLoader")
+      .def(py::init([](std::vector<std::string> addresses, int batch_size, std::string image_key, int rcvhwm,
+                       int io_threads, int device, int64_t max_batches, size_t max_frame_bytes, int pool_slots,
+                       int staging_depth, bool skip_bad, int cout, std::vector<int> cmap, int flip_all,
+                       int out_dtype, int layout, std::vector<float> lut, std::vector<float> matrix,
+                       std::vector<float> bias) {
+             LoaderConfig c;
+             c.addresses = std::move(addresses);
+             c.batch_size = batch_size;
+             c.image_key = std::move(image_key);
+             c.rcvhwm = rcvhwm;
+             c.io_threads = io_threads;
+             c.device = device;
+             c.max_batches = max_batches;
+             c.max_frame_bytes = max_frame_bytes;
+             c.pool_slots = pool_slots;
+             c.staging_depth = staging_depth;
+             c.skip_bad = skip_bad;
+             c.cout = cout;
+             fill_cmap(c.cmap, cmap);
+             c.flip_all = flip_all;
+             c.out_dtype = out_dtype;
+             c.layout = layout;
+             c.lut = std::move(lut);
+             c.color_matrix = !matrix.empty();
+             c.matrix = std::move(matrix);
+             c.bias = std::move(bias);
+             return new StreamLoader(c);
+           }),
+           py::arg("addresses"), py::arg("batch_size"), py::arg("image_key"), py::arg("rcvhwm"),
+           py::arg("io_threads"), py::arg("device"), py::arg("max_batches"), py::arg("max_frame_bytes"),
+           py::arg("pool_slots"), py::arg("staging_depth"), py::arg("skip_bad"), py::arg("cout"), py::arg("cmap"),
+           py::arg("flip_all"), py::arg("out_dtype"), py::arg("layout"), py::arg("lut"), py::arg("matrix"),
+           py::arg("bias"))
+      .def("start", &StreamLoader::start)
+      .def("wait_shape",
+           [](StreamLoader& l, long timeout_ms) -> py::object {
+             int H = 0, W = 0, C = 0;
+             bool ok;
+             {
+               py::gil_scoped_release nogil;
+               ok = l.wait_shape(timeout_ms, &H, &W, &C);
+             }
+             if (!ok) return py::none();
+             return py::make_tuple(H, W, C);
+           })
+      .def("post",
+           [](StreamLoader& l, uintptr_t dst, uintptr_t stream) {
+             py::gil_scoped_release nogil;
+             l.post(ptr<void>(dst), stream_of(stream));
+           })
+      .def("next",
+           [](StreamLoader& l, uintptr_t stream, long timeout_ms) -> py::object {
+             ReadyBatch rb;
+             bool ok;
+             {
+               py::gil_scoped_release nogil;
+               ok = l.next(&rb, stream_of(stream), timeout_ms);
+             }
+             if (!ok) return py::none();                 // timeout
+             if (rb.index < 0) return py::make_tuple(-1, py::list(), 0.0);   // exhausted
+             py::list metas;
+             for (auto& it : rb.items) {
+               py::bytearray owner(reinterpret_cast<const char*>(it.bytes.data()), it.bytes.size());
+               const uint8_t* base = reinterpret_cast<const uint8_t*>(PyByteArray_AsString(owner.ptr()));
+               metas.append(pyconv::value_to_py(*it.tree, base, owner));
+             }
+             return py::make_tuple(rb.index, metas, rb.recv_ms);
+           })
+      .def("stop",
+           [](StreamLoader& l) {
+             py::gil_scoped_release nogil;
+             l.stop();
+           })
+      .def("stats", [](StreamLoader& l) {
+        auto s = l.stats();
+        py::dict d;
+        d["frames"] = s.frames;
+        d["batches"] = s.batches;
+        d["bytes"] = s.bytes;
+        d["bad"] = s.bad;
+        d["pool_fallbacks"] = s.pool_fallbacks;
+        d["h2d_issue_ms"] = s.h2d_issue_ms;
+        return d;
+      });
+}

@@ -1,0 +1,265 @@
+// cubesim -- headless stand-in for a Blender instance running
+// examples/datagen/cube.blend.py (or falling_cubes.blend.py).
+//
+// Launch contract is the one BlenderLauncher hands to Blender scripts
+// (reference: pkg_pytorch/blendtorch/btt/launcher.py:114-122, parsed by
+// pkg_blender/blendtorch/btb/arguments.py:5-47):
+//
+//   cubesim [--] -btid I -btseed S -btsockets DATA=tcp://host:port [script args]
+//
+// Script args:  --scene cube|falling_cubes   --mode rgb|rgba   --origin
+// upper-left|lower-left   --frame-range A B   --frames N (-1 = forever)
+// --sndhwm N   --linger MS   --fps F (0 = unthrottled)   --socket NAME
+// --fault none|exit|stall|garbage --fault-after N   --verbose
+//
+// Every frame it publishes, on a bound PUSH socket with SNDHWM/LINGER/
+// IMMEDIATE as btb.DataPublisher does (reference: btb/publisher.py:21-43),
+// the pickled dict {'btid', 'image' (HxWxC u8), 'xy' (8*nboxes x 2 f8),
+// 'frameid'} -- the same keys cube.blend.py publishes (reference:
+// examples/datagen/cube.blend.py:17-24).  Pixels are rendered straight into
+// the pickle payload, so a frame costs one render and zero extra copies
+// before the kernel socket buffer.
+#include <atomic>
+#include <chrono>
+#include <csignal>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../codec/pickle_codec.h"
+#include "../transport/zmtp.h"
+#include "raster.h"
+
+using namespace btn;
+
+namespace {
+
+std::atomic<bool> g_stop{false};
+void on_signal(int) { g_stop = true; }
+
+struct Args {
+  int btid = 0;
+  long long btseed = 0;
+  std::map<std::string, std::string> sockets;
+  std::string scene = "cube";
+  std::string mode = "rgb";
+  std::string origin = "upper-left";
+  std::string socket = "DATA";
+  int frame_start = 0, frame_end = 100;
+  long long frames = -1;
+  int sndhwm = 10;
+  long linger = 0;
+  double fps = 0;
+  std::string fault = "none";
+  long long fault_after = -1;
+  bool verbose = false;
+};
+
+[[noreturn]] void usage(const char* msg) {
+  std::fprintf(stderr, "cubesim: %s\n", msg);
+  std::exit(2);
+}
+
+Args parse(int argc, char** argv) {
+  Args a;
+  std::vector<std::string> v;
+  int start = 1;
+  for (int i = 1; i < argc; ++i)
+    if (std::strcmp(argv[i], "--") == 0) {
+      start = i + 1;
+      break;
+    }
+  for (int i = start; i < argc; ++i) v.push_back(argv[i]);
+  auto need = [&](size_t i) {
+    if (i + 1 >= v.size()) usage(("missing value for " + v[i]).c_str());
+    return v[i + 1];
+  };
+  for (size_t i = 0; i < v.size(); ++i) {
+    const std::string& k = v[i];
+    if (k == "-btid") a.btid = std::stoi(need(i)), ++i;
+    else if (k == "-btseed") a.btseed = std::stoll(need(i)), ++i;
+    else if (k == "-btsockets") {
+      while (i + 1 < v.size() && v[i + 1].rfind("-", 0) != 0) {
+        ++i;
+        auto eq = v[i].find('=');
+        if (eq == std::string::npos) usage("-btsockets expects NAME=ADDRESS");
+        a.sockets[v[i].substr(0, eq)] = v[i].substr(eq + 1);
+      }
+    } else if (k == "--scene") a.scene = need(i), ++i;
+    else if (k == "--mode") a.mode = need(i), ++i;
+    else if (k == "--origin") a.origin = need(i), ++i;
+    else if (k == "--socket") a.socket = need(i), ++i;
+    else if (k == "--frame-range") {
+      a.frame_start = std::stoi(need(i));
+      a.frame_end = std::stoi(need(i + 1));
+      i += 2;
+    } else if (k == "--frames") a.frames = std::stoll(need(i)), ++i;
+    else if (k == "--sndhwm") a.sndhwm = std::stoi(need(i)), ++i;
+    else if (k == "--linger") a.linger = std::stol(need(i)), ++i;
+    else if (k == "--fps") a.fps = std::stod(need(i)), ++i;
+    else if (k == "--fault") a.fault = need(i), ++i;
+    else if (k == "--fault-after") a.fault_after = std::stoll(need(i)), ++i;
+    else if (k == "--verbose") a.verbose = true;
+    // unknown args are ignored, as Blender scripts ignore the remainder
+  }
+  if (a.mode != "rgb" && a.mode != "rgba") usage("--mode must be rgb or rgba");
+  if (a.origin != "upper-left" && a.origin != "lower-left") usage("bad --origin");
+  return a;
+}
+
+// Recycles frame storage: a sent frame's buffer returns here once the IO
+// thread has written it, so steady state allocates nothing.
+struct FramePool {
+  std::mutex mu;
+  std::vector<std::vector<uint8_t>*> free;
+  std::vector<uint8_t> take() {
+    std::lock_guard<std::mutex> lk(mu);
+    if (free.empty()) return {};
+    std::vector<uint8_t> v(std::move(*free.back()));
+    delete free.back();
+    free.pop_back();
+    return v;
+  }
+  void give(std::vector<uint8_t>* v) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (free.size() < 64) free.push_back(v);
+    else delete v;
+  }
+};
+FramePool g_pool;
+
+zmtp::Frame frame_from_vector(std::vector<uint8_t>&& v) {
+  auto* owned = new std::vector<uint8_t>(std::move(v));
+  auto b = std::make_shared<Buffer>();
+  b->data = owned->data();
+  b->capacity = owned->size();
+  b->owner = owned;
+  b->release = [](void* o, Buffer*) { g_pool.give(static_cast<std::vector<uint8_t>*>(o)); };
+  zmtp::Frame f;
+  f.size = owned->size();
+  f.buf = std::move(b);
+  return f;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Args a = parse(argc, argv);
+  if (!a.sockets.count(a.socket)) usage(("no -btsockets entry named " + a.socket).c_str());
+  std::signal(SIGTERM, on_signal);
+  std::signal(SIGINT, on_signal);
+
+  sim::Scene scene = a.scene == "falling_cubes" ? sim::falling_cubes_scene() : sim::cube_scene();
+  const int W = scene.cam.width, H = scene.cam.height, C = a.mode == "rgba" ? 4 : 3;
+  std::mt19937_64 rng(uint64_t(a.btseed));
+  std::uniform_real_distribution<double> U(0.0, 1.0);
+  const double pi = 3.14159265358979323846;
+  if (a.scene == "falling_cubes") {
+    for (auto& b : scene.boxes)
+      b.albedo = {float(U(rng)), float(U(rng)), float(U(rng))};
+  }
+
+  auto sock = zmtp::Context::global().socket(zmtp::PUSH);
+  sock->setsockopt(zmtp::SNDHWM, a.sndhwm);
+  sock->setsockopt(zmtp::LINGER, a.linger);
+  sock->setsockopt(zmtp::IMMEDIATE, 1);
+  sock->bind(a.sockets[a.socket]);
+
+  const zmtp::Socket::Interrupt intr = [] { return g_stop.load(); };
+  const bool lower_left = a.origin == "lower-left";
+  sim::Renderer renderer(scene, C, lower_left);
+  const auto t_start = std::chrono::steady_clock::now();
+  auto next_due = t_start;
+  long long published = 0;
+  int frame = a.frame_start;
+  double render_ms = 0;
+
+  while (!g_stop && (a.frames < 0 || published < a.frames)) {
+    // pre_animation / pre_frame: randomise the pose(s)
+    if (a.scene == "falling_cubes") {
+      if (frame == a.frame_start)
+        for (auto& b : scene.boxes) {
+          b.center = {-3 + 6 * U(rng), -3 + 6 * U(rng), -1.0 + 3 * U(rng)};
+          b.rot = sim::euler_xyz(-pi + 2 * pi * U(rng), -pi + 2 * pi * U(rng), -pi + 2 * pi * U(rng));
+        }
+    } else {
+      scene.boxes[0].rot = sim::euler_xyz(pi * U(rng), pi * U(rng), pi * U(rng));
+    }
+
+    codec::Writer w(4, g_pool.take());
+    w.begin_dict();
+    w.key("btid");
+    w.integer(a.btid);
+    w.key("image");
+    size_t img_off = w.ndarray("u1", {H, W, C});
+    w.key("xy");
+    std::vector<double> xy;
+    for (auto& b : scene.boxes)
+      for (auto& c : b.corners()) {
+        double px = 0, py = 0;
+        scene.cam.project(c, &px, &py);
+        xy.push_back(px);
+        xy.push_back(py);
+      }
+    w.ndarray("f8", {int64_t(xy.size() / 2), 2}, xy.data());
+    w.key("frameid");
+    w.integer(frame);
+    if (lower_left) {
+      w.key("origin");
+      w.str("lower-left");
+    }
+    w.end_dict();
+    auto& buf = w.finish();
+
+    auto r0 = std::chrono::steady_clock::now();
+    renderer.render(scene, buf.data() + img_off);
+    render_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - r0).count();
+
+    if (a.fault != "none" && a.fault_after >= 0 && published == a.fault_after) {
+      if (a.fault == "exit") std::_Exit(3);
+      if (a.fault == "stall") {
+        while (!g_stop) std::this_thread::sleep_for(std::chrono::milliseconds(50));
+        break;
+      }
+      if (a.fault == "garbage") {
+        zmtp::Message m;
+        m.push_back(zmtp::Frame::copy_of("\x80\x04garbage", 9));
+        try {
+          sock->send(std::move(m), 0, intr);
+        } catch (const zmtp::Error&) {
+          break;
+        }
+        ++published;
+        continue;
+      }
+    }
+
+    zmtp::Message msg;
+    msg.push_back(frame_from_vector(std::move(buf)));
+    try {
+      sock->send(std::move(msg), 0, intr);   // blocks at SNDHWM: backpressure
+    } catch (const zmtp::Error& e) {
+      if (e.code == zmtp::E_INTR) break;
+      std::fprintf(stderr, "cubesim[%d]: send failed: %s\n", a.btid, e.what());
+      break;
+    }
+    ++published;
+    frame = frame >= a.frame_end ? a.frame_start : frame + 1;
+    if (a.fps > 0) {
+      next_due += std::chrono::microseconds(int64_t(1e6 / a.fps));
+      std::this_thread::sleep_until(next_due);
+    }
+  }
+  double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+  if (a.verbose)
+    std::fprintf(stderr, "cubesim[%d]: %lld frames in %.2fs (%.1f fps, render %.3f ms/frame)\n", a.btid,
+                 published, secs, published / std::max(secs, 1e-9), render_ms / std::max<long long>(published, 1));
+  sock->close(g_stop ? 0 : -2);
+  return 0;
+}

@@ -1,0 +1,390 @@
+// Headless CPU renderer (see raster.h).  The static background (ground plane
+// lit by the point light, world colour) is shaded once per Renderer; each
+// frame copies it, stamps the boxes' shadow hulls (2-D point-in-polygon on
+// cached ground hit points) and rasterises the boxes' front faces with
+// per-pixel Lambert shading and a depth buffer.
+#include "raster.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+
+namespace btn {
+namespace sim {
+
+namespace {
+constexpr double kPi = 3.14159265358979323846;
+
+inline Vec3 add(const Vec3& a, const Vec3& b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline Vec3 sub(const Vec3& a, const Vec3& b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline Vec3 scale(const Vec3& a, double s) { return {a.x * s, a.y * s, a.z * s}; }
+inline double dot(const Vec3& a, const Vec3& b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+
+// linear radiance -> display 8 bit (power 1/2.2), 4096-entry table over [0,1]
+struct ToneLut {
+  uint8_t v[4097];
+  ToneLut() {
+    for (int i = 0; i <= 4096; ++i) {
+      double x = i / 4096.0;
+      v[i] = uint8_t(std::min(255.0, std::floor(255.0 * std::pow(x, 1.0 / 2.2) + 0.5)));
+    }
+  }
+  inline uint8_t operator()(double x) const {
+    if (!(x > 0)) return 0;
+    if (x >= 1) return 255;
+    return v[int(x * 4096.0)];
+  }
+};
+const ToneLut& tone() {
+  static ToneLut t;
+  return t;
+}
+
+// Ray/oriented-box overlap for t in (tmin, tmax).
+bool ray_hits_box(const Box& b, const Vec3& o, const Vec3& d, double tmin, double tmax) {
+  Vec3 lo = mul_t(b.rot, sub(o, b.center));
+  Vec3 ld = mul_t(b.rot, d);
+  const double ov[3] = {lo.x, lo.y, lo.z}, dv[3] = {ld.x, ld.y, ld.z};
+  const double hv[3] = {b.half.x, b.half.y, b.half.z};
+  for (int a = 0; a < 3; ++a) {
+    if (std::fabs(dv[a]) < 1e-12) {
+      if (ov[a] < -hv[a] || ov[a] > hv[a]) return false;
+      continue;
+    }
+    double inv = 1.0 / dv[a];
+    double t0 = (-hv[a] - ov[a]) * inv, t1 = (hv[a] - ov[a]) * inv;
+    if (t0 > t1) std::swap(t0, t1);
+    tmin = std::max(tmin, t0);
+    tmax = std::min(tmax, t1);
+    if (tmin > tmax) return false;
+  }
+  return true;
+}
+
+inline double light_scale(const Light& l) { return l.power / (4.0 * kPi * kPi); }
+
+}  // namespace
+
+Mat3 euler_xyz(double rx, double ry, double rz) {
+  double cx = std::cos(rx), sx = std::sin(rx), cy = std::cos(ry), sy = std::sin(ry);
+  double cz = std::cos(rz), sz = std::sin(rz);
+  // R = Rz * Ry * Rx
+  return Mat3{cz * cy, cz * sy * sx - sz * cx, cz * sy * cx + sz * sx,
+              sz * cy, sz * sy * sx + cz * cx, sz * sy * cx - cz * sx,
+              -sy,     cy * sx,                cy * cx};
+}
+
+Vec3 mul(const Mat3& m, const Vec3& v) {
+  return {m[0] * v.x + m[1] * v.y + m[2] * v.z, m[3] * v.x + m[4] * v.y + m[5] * v.z,
+          m[6] * v.x + m[7] * v.y + m[8] * v.z};
+}
+
+Vec3 mul_t(const Mat3& m, const Vec3& v) {
+  return {m[0] * v.x + m[3] * v.y + m[6] * v.z, m[1] * v.x + m[4] * v.y + m[7] * v.z,
+          m[2] * v.x + m[5] * v.y + m[8] * v.z};
+}
+
+double Camera::focal_px() const { return lens_mm / sensor_mm * double(std::max(width, height)); }
+
+bool Camera::project(const Vec3& w, double* px, double* py, double* depth) const {
+  Vec3 c = mul_t(rot, sub(w, loc));
+  if (depth) *depth = -c.z;
+  if (c.z >= -1e-12) return false;
+  double f = focal_px();
+  *px = 0.5 * width + f * c.x / (-c.z);
+  *py = 0.5 * height - f * c.y / (-c.z);
+  return true;
+}
+
+std::array<Vec3, 8> Box::corners() const {
+  // Blender default cube vertex order
+  static const int s[8][3] = {{1, 1, 1}, {1, 1, -1}, {1, -1, 1}, {1, -1, -1},
+                              {-1, 1, 1}, {-1, 1, -1}, {-1, -1, 1}, {-1, -1, -1}};
+  std::array<Vec3, 8> out;
+  for (int i = 0; i < 8; ++i) {
+    Vec3 l{s[i][0] * half.x, s[i][1] * half.y, s[i][2] * half.z};
+    out[i] = add(center, mul(rot, l));
+  }
+  return out;
+}
+
+Scene cube_scene() {
+  Scene s;
+  s.cam.width = 640;
+  s.cam.height = 480;
+  s.cam.loc = {7.358891, -6.925791, 4.958309};
+  s.cam.rot = euler_xyz(1.109319, 0.0, 0.814928);
+  s.light.loc = {4.076245, 1.005454, 5.903862};
+  s.light.power = 1000.0;
+  Box b;
+  b.rot = euler_xyz(0, 0, 0);
+  s.boxes.push_back(b);
+  return s;
+}
+
+Scene falling_cubes_scene() {
+  Scene s = cube_scene();
+  s.cam.loc = {14.5, -15.712, 16.754};
+  // look at the origin: -Z toward target, +Y up
+  Vec3 dir = sub(Vec3{0, 0, 0}, s.cam.loc);
+  double n = std::sqrt(dot(dir, dir));
+  dir = scale(dir, 1.0 / n);
+  double pitch = std::acos(-dir.z);             // rotation about x from looking down
+  double yaw = std::atan2(dir.x, -dir.y);
+  s.cam.rot = euler_xyz(pitch, 0.0, yaw);
+  s.light.loc = {4.0, 1.0, 14.0};
+  s.light.power = 6000.0;
+  s.boxes.assign(7, Box());
+  return s;
+}
+
+namespace {
+
+// 2-D convex hull (monotone chain), counter-clockwise, no repeated end point.
+using P2 = std::array<double, 2>;
+int convex_hull(P2* p, int n, P2* h) {
+  std::sort(p, p + n, [](const P2& a, const P2& b) {
+    return a[0] < b[0] || (a[0] == b[0] && a[1] < b[1]);
+  });
+  auto cross = [](const P2& o, const P2& a, const P2& b) {
+    return (a[0] - o[0]) * (b[1] - o[1]) - (a[1] - o[1]) * (b[0] - o[0]);
+  };
+  int k = 0;
+  for (int i = 0; i < n; ++i) {
+    while (k >= 2 && cross(h[k - 2], h[k - 1], p[i]) <= 0) --k;
+    h[k][0] = p[i][0];
+    h[k][1] = p[i][1];
+    ++k;
+  }
+  for (int i = n - 2, t = k + 1; i >= 0; --i) {
+    while (k >= t && cross(h[k - 2], h[k - 1], p[i]) <= 0) --k;
+    h[k][0] = p[i][0];
+    h[k][1] = p[i][1];
+    ++k;
+  }
+  return k - 1;
+}
+
+}  // namespace
+
+Renderer::Renderer(const Scene& s, int channels, bool lower_left)
+    : W_(s.cam.width), H_(s.cam.height), C_(channels), lower_left_(lower_left) {
+  const Camera& cam = s.cam;
+  const double f = cam.focal_px();
+  const ToneLut& T = tone();
+  const Vec3 o = cam.loc;
+  const Vec3 X{cam.rot[0], cam.rot[3], cam.rot[6]};
+  const Vec3 Y{cam.rot[1], cam.rot[4], cam.rot[7]};
+  const Vec3 Z{cam.rot[2], cam.rot[5], cam.rot[8]};
+  const double ls = light_scale(s.light);
+  const Vec3 L = s.light.loc;
+  background_.assign(size_t(W_) * H_ * C_, 255);
+  plane_xy_.assign(size_t(W_) * H_ * 2, std::numeric_limits<float>::quiet_NaN());
+  for (int c = 0; c < 3; ++c) shadow_rgb_[c] = T(s.plane_albedo[c] * s.ambient);
+  for (int y = 0; y < H_; ++y) {
+    const double cy = -((y + 0.5) - 0.5 * H_) / f;
+    for (int x = 0; x < W_; ++x) {
+      const double cx = ((x + 0.5) - 0.5 * W_) / f;
+      const Vec3 d{cx * X.x + cy * Y.x - Z.x, cx * X.y + cy * Y.y - Z.y, cx * X.z + cy * Y.z - Z.z};
+      const int row = lower_left_ ? (H_ - 1 - y) : y;
+      uint8_t* px = &background_[(size_t(row) * W_ + x) * C_];
+      double t = d.z < 0 ? (s.plane_z - o.z) / d.z : -1.0;
+      if (t > 0) {
+        const double hx = o.x + t * d.x, hy = o.y + t * d.y;
+        if (std::fabs(hx) <= s.plane_half && std::fabs(hy) <= s.plane_half) {
+          const Vec3 l = sub(L, Vec3{hx, hy, s.plane_z});
+          const double d2 = dot(l, l);
+          const double e = std::max(0.0, ls * (l.z / std::sqrt(d2)) / d2);
+          for (int c = 0; c < 3; ++c) px[c] = T(s.plane_albedo[c] * (s.ambient + e));
+          plane_xy_[(size_t(y) * W_ + x) * 2] = float(hx);
+          plane_xy_[(size_t(y) * W_ + x) * 2 + 1] = float(hy);
+          continue;
+        }
+      }
+      for (int c = 0; c < 3; ++c) px[c] = T(s.world[c]);
+    }
+  }
+}
+
+inline void Renderer::put(uint8_t* out, int x, int y, float r, float g, float b) const {
+  const ToneLut& T = tone();
+  const int row = lower_left_ ? (H_ - 1 - y) : y;
+  uint8_t* p = out + (size_t(row) * W_ + x) * C_;
+  p[0] = T(r);
+  p[1] = T(g);
+  p[2] = T(b);
+}
+
+void Renderer::render(const Scene& s, uint8_t* out) {
+  const Camera& cam = s.cam;
+  const int W = W_, H = H_;
+  const double f = cam.focal_px();
+  const Vec3 o = cam.loc;
+  const Vec3 X{cam.rot[0], cam.rot[3], cam.rot[6]};
+  const Vec3 Y{cam.rot[1], cam.rot[4], cam.rot[7]};
+  const Vec3 Z{cam.rot[2], cam.rot[5], cam.rot[8]};
+  const double ls = light_scale(s.light);
+  const Vec3 L = s.light.loc;
+  const double amb = s.ambient;
+
+  std::memcpy(out, background_.data(), background_.size());
+
+  // ---- shadows: light-space projection of each box onto the plane ----
+  for (const Box& b : s.boxes) {
+    auto cs = b.corners();
+    P2 pts[8], hull[17];
+    bool above = true;
+    for (int i = 0; i < 8; ++i) {
+      if (cs[i].z >= L.z - 1e-9) above = false;
+      double t = (s.plane_z - L.z) / (cs[i].z - L.z);
+      pts[i][0] = L.x + t * (cs[i].x - L.x);
+      pts[i][1] = L.y + t * (cs[i].y - L.y);
+    }
+    if (!above) continue;   // light inside/below the box: no ground shadow
+    const int nh = convex_hull(pts, 8, hull);
+    if (nh < 3) continue;
+    int x0 = W, y0 = H, x1 = -1, y1 = -1;
+    bool full = false;
+    for (int i = 0; i < nh; ++i) {
+      double px, py;
+      if (!cam.project(Vec3{hull[i][0], hull[i][1], s.plane_z}, &px, &py)) {
+        full = true;
+        break;
+      }
+      x0 = std::min(x0, int(std::floor(px)) - 1);
+      y0 = std::min(y0, int(std::floor(py)) - 1);
+      x1 = std::max(x1, int(std::ceil(px)) + 1);
+      y1 = std::max(y1, int(std::ceil(py)) + 1);
+    }
+    if (full) {
+      x0 = 0, y0 = 0, x1 = W - 1, y1 = H - 1;
+    }
+    x0 = std::max(x0, 0), y0 = std::max(y0, 0), x1 = std::min(x1, W - 1), y1 = std::min(y1, H - 1);
+    // edge equations a*x + b*y + c >= 0 inside (CCW hull)
+    float ea[17], eb[17], ec[17];
+    for (int i = 0; i < nh; ++i) {
+      const P2& p0 = hull[i];
+      const P2& p1 = hull[(i + 1) % nh];
+      ea[i] = float(-(p1[1] - p0[1]));
+      eb[i] = float(p1[0] - p0[0]);
+      ec[i] = float(-(ea[i] * p0[0] + eb[i] * p0[1]));
+    }
+    for (int y = y0; y <= y1; ++y) {
+      const float* pxy = &plane_xy_[(size_t(y) * W) * 2];
+      const int row = lower_left_ ? (H - 1 - y) : y;
+      uint8_t* orow = out + size_t(row) * W * C_;
+      for (int x = x0; x <= x1; ++x) {
+        const float hx = pxy[2 * x], hy = pxy[2 * x + 1];
+        if (hx != hx) continue;
+        bool in = true;
+        for (int i = 0; i < nh; ++i) in &= ea[i] * hx + eb[i] * hy + ec[i] >= 0.f;
+        if (in) {
+          uint8_t* p = orow + size_t(x) * C_;
+          p[0] = shadow_rgb_[0];
+          p[1] = shadow_rgb_[1];
+          p[2] = shadow_rgb_[2];
+        }
+      }
+    }
+  }
+
+  // ---- boxes: front faces, per-pixel Lambert, depth tested ----
+  const bool need_depth = s.boxes.size() > 1;
+  if (need_depth) depth_.assign(size_t(W) * H, std::numeric_limits<float>::infinity());
+  for (size_t bi = 0; bi < s.boxes.size(); ++bi) {
+    const Box& b = s.boxes[bi];
+    const double hv[3] = {b.half.x, b.half.y, b.half.z};
+    for (int axis = 0; axis < 3; ++axis) {
+      for (int sign = -1; sign <= 1; sign += 2) {
+        Vec3 nl{0, 0, 0};
+        (axis == 0 ? nl.x : axis == 1 ? nl.y : nl.z) = sign;
+        const Vec3 n = mul(b.rot, nl);
+        const Vec3 fc = add(b.center, scale(n, hv[axis]));
+        if (dot(n, sub(o, fc)) <= 0) continue;   // back face
+        const int j = (axis + 1) % 3, k = (axis + 2) % 3;
+        Vec3 ej{0, 0, 0}, ek{0, 0, 0};
+        (j == 0 ? ej.x : j == 1 ? ej.y : ej.z) = hv[j];
+        (k == 0 ? ek.x : k == 1 ? ek.y : ek.z) = hv[k];
+        const Vec3 wj = mul(b.rot, ej), wk = mul(b.rot, ek);
+        const Vec3 q[4] = {add(fc, add(wj, wk)), add(fc, sub(wk, wj)), sub(fc, add(wj, wk)),
+                           add(fc, sub(wj, wk))};
+        double px[4], py[4];
+        bool vis = true;
+        for (int i = 0; i < 4; ++i) vis &= cam.project(q[i], &px[i], &py[i]);
+        if (!vis) continue;
+        double area = 0;
+        for (int i = 0; i < 4; ++i) {
+          int i1 = (i + 1) & 3;
+          area += px[i] * py[i1] - px[i1] * py[i];
+        }
+        if (std::fabs(area) < 1e-9) continue;
+        const float sg = area > 0 ? 1.f : -1.f;
+        // edge functions, sign-normalised so inside is >= 0
+        float ea[4], eb[4], ec[4];
+        for (int i = 0; i < 4; ++i) {
+          int i1 = (i + 1) & 3;
+          ea[i] = sg * float(-(py[i1] - py[i]));
+          eb[i] = sg * float(px[i1] - px[i]);
+          ec[i] = -(ea[i] * float(px[i]) + eb[i] * float(py[i]));
+        }
+        int x0 = std::max(0, int(std::floor(*std::min_element(px, px + 4))));
+        int x1 = std::min(W - 1, int(std::ceil(*std::max_element(px, px + 4))));
+        int y0 = std::max(0, int(std::floor(*std::min_element(py, py + 4))));
+        int y1 = std::min(H - 1, int(std::ceil(*std::max_element(py, py + 4))));
+        // per pixel: P = o + t d, t = nd0 / (n.d); light vector l = L - P
+        const float nd0 = float(dot(n, sub(fc, o)));
+        const float nX = float(dot(n, X)), nY = float(dot(n, Y)), nZ = float(dot(n, Z));
+        const float a0 = b.albedo[0], a1 = b.albedo[1], a2 = b.albedo[2];
+        const float lsf = float(ls), ambf = float(amb);
+        const Vec3 Lo = sub(L, o);
+        const float nLo = float(dot(n, Lo));
+        for (int y = y0; y <= y1; ++y) {
+          const float pyc = y + 0.5f;
+          const float cy = -(pyc - 0.5f * H) / float(f);
+          for (int x = x0; x <= x1; ++x) {
+            const float pxc = x + 0.5f;
+            if (ea[0] * pxc + eb[0] * pyc + ec[0] < 0.f || ea[1] * pxc + eb[1] * pyc + ec[1] < 0.f ||
+                ea[2] * pxc + eb[2] * pyc + ec[2] < 0.f || ea[3] * pxc + eb[3] * pyc + ec[3] < 0.f)
+              continue;
+            const float cx = (pxc - 0.5f * W) / float(f);
+            const float dn = cx * nX + cy * nY - nZ;
+            if (dn >= 0.f) continue;
+            const float t = nd0 / dn;
+            if (need_depth) {
+              float& zb = depth_[size_t(y) * W + x];
+              if (t >= zb) continue;
+              zb = t;
+            }
+            const float dx = float(cx * X.x + cy * Y.x - Z.x), dy = float(cx * X.y + cy * Y.y - Z.y),
+                        dz = float(cx * X.z + cy * Y.z - Z.z);
+            const float lx = float(Lo.x) - t * dx, ly = float(Lo.y) - t * dy, lz = float(Lo.z) - t * dz;
+            const float d2 = lx * lx + ly * ly + lz * lz;
+            const float nl_ = nLo - t * dn;   // n . (L - P)
+            float e = nl_ > 0.f ? lsf * nl_ / (d2 * std::sqrt(d2)) : 0.f;
+            if (e > 0.f && s.boxes.size() > 1) {
+              const Vec3 P{o.x + t * dx, o.y + t * dy, o.z + t * dz};
+              const Vec3 l{lx, ly, lz};
+              for (size_t oi = 0; oi < s.boxes.size(); ++oi) {
+                if (oi != bi && ray_hits_box(s.boxes[oi], P, l, 1e-6, 1.0)) {
+                  e = 0.f;
+                  break;
+                }
+              }
+            }
+            const float kk = ambf + e;
+            put(out, x, y, a0 * kk, a1 * kk, a2 * kk);
+          }
+        }
+      }
+    }
+  }
+}
+
+void render(const Scene& s, uint8_t* out, int channels, bool lower_left) {
+  Renderer r(s, channels, lower_left);
+  r.render(s, out);
+}
+
+}  // namespace sim
+}  // namespace btn

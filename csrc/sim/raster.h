@@ -1,0 +1,109 @@
+// Headless CPU renderer for the blendtorch stand-in producers.
+//
+// Blender/Eevee is not available in this stack, so the producers that feed
+// the benchmark and the tests render their scenes here instead.  The scene
+// model covers what the reference's example scenes contain
+// (reference: examples/datagen/cube.blend, falling_cubes.blend -- camera,
+// point light, ground plane, one or more boxes):
+//   * a pinhole camera with Blender's conventions (looks down its local -Z,
+//     +Y up, sensor_fit AUTO, focal length in pixels = lens/sensor * max(W,H));
+//   * a point light with inverse-square falloff plus ambient term;
+//   * an infinite-ish ground plane (square of half-size `plane_half`) that
+//     receives box shadows (shadow rays against each oriented box);
+//   * convex boxes drawn by rasterising their front faces with per-pixel
+//     Lambert shading.
+// Projection helpers follow btb.Camera (reference: pkg_blender/blendtorch/btb/
+// camera.py:84-162): NDC in [-1,1], pixel = (ndc+1)/2 * [W,H] with the y axis
+// flipped for the upper-left origin -- no half-pixel offset.
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <vector>
+
+namespace btn {
+namespace sim {
+
+struct Vec3 {
+  double x = 0, y = 0, z = 0;
+};
+
+using Mat3 = std::array<double, 9>;   // row major
+
+Mat3 euler_xyz(double rx, double ry, double rz);   // Blender 'XYZ' euler: Rz*Ry*Rx
+Vec3 mul(const Mat3& m, const Vec3& v);
+Vec3 mul_t(const Mat3& m, const Vec3& v);          // m^T v
+
+struct Camera {
+  int width = 640, height = 480;
+  double lens_mm = 50.0, sensor_mm = 36.0;
+  double clip_start = 0.1, clip_end = 100.0;
+  Vec3 loc;
+  Mat3 rot;      // camera-to-world rotation
+  double focal_px() const;
+  // world -> pixel (upper-left origin); returns false if behind the camera.
+  bool project(const Vec3& w, double* px, double* py, double* depth = nullptr) const;
+};
+
+struct Box {
+  Vec3 center;
+  Vec3 half{1, 1, 1};
+  Mat3 rot;                                   // local-to-world
+  std::array<float, 3> albedo{0.8f, 0.8f, 0.8f};
+  // The 8 corners in Blender's default-cube vertex order.
+  std::array<Vec3, 8> corners() const;
+};
+
+struct Light {
+  Vec3 loc;
+  double power = 1000.0;   // W-ish; scaled so the default scene is well exposed
+};
+
+struct Scene {
+  Camera cam;
+  Light light;
+  double ambient = 0.08;
+  double plane_z = -2.0;
+  double plane_half = 10.0;
+  std::array<float, 3> plane_albedo{0.8f, 0.8f, 0.8f};
+  std::array<float, 3> world{0.051f, 0.051f, 0.051f};
+  std::vector<Box> boxes;
+};
+
+// The default-cube scene of examples/datagen/cube.blend (640x480, camera at
+// (7.359,-6.926,4.958) with Blender's default rotation, light at
+// (4.076,1.005,5.904), ground plane at z=-2).
+Scene cube_scene();
+// examples/datagen/falling_cubes.blend stand-in: 7 boxes, raised camera.
+Scene falling_cubes_scene();
+
+// Frame renderer.  Camera, light and ground plane are static for the life of
+// a Renderer, so their shading (the whole background) is computed once and
+// cached together with each pixel's ground-plane hit point; a frame then costs
+// one background copy, a 2-D point-in-polygon pass over the image-space bounds
+// of the boxes' shadow hulls, and the boxes' front faces.
+// Output: H*W*channels bytes, row-major HWC uint8, channels 3 or 4 (alpha =
+// 255); `lower_left` stores row 0 = bottom image row (OpenGL readback order).
+class Renderer {
+ public:
+  Renderer(const Scene& s, int channels, bool lower_left);
+  void render(const Scene& s, uint8_t* out);
+  int width() const { return W_; }
+  int height() const { return H_; }
+  int channels() const { return C_; }
+
+ private:
+  void put(uint8_t* out, int x, int y, float r, float g, float b) const;
+  int W_, H_, C_;
+  bool lower_left_;
+  std::vector<uint8_t> background_;     // final HWC bytes, boxes absent
+  std::vector<float> plane_xy_;         // per pixel ground hit (x,y); NaN = no hit
+  uint8_t shadow_rgb_[3];
+  std::vector<float> depth_;
+};
+
+// One-shot convenience wrapper (builds a Renderer per call).
+void render(const Scene& s, uint8_t* out, int channels, bool lower_left);
+
+}  // namespace sim
+}  // namespace btn

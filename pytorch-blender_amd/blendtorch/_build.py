@@ -103,7 +103,7 @@ def build_native(verbose=False, jobs=8):
     py_obj = objs[len(srcs)]
     target = PKG / f'_native{_ext_suffix()}'
     if _newer(target, core + [py_obj]):
-        _run([cxx, '-shared', '-pthread', *core, py_obj, '-o', target], verbose)
+        _run([cxx, '-shared', '-pthread', '-Wl,-Bsymbolic', *core, py_obj, '-o', target], verbose)
     BIN.mkdir(exist_ok=True)
     raster = [o for s, o in zip(sim_srcs, objs[len(srcs) + 1:]) if s.name == 'raster.cpp']
     for s, o in zip(sim_srcs, objs[len(srcs) + 1:]):
@@ -126,7 +126,7 @@ def build_hip(verbose=False, jobs=8):
     if not hipcc.exists():
         raise RuntimeError('hipcc not found; cannot build the HIP extension')
     tl = _torch_lib()
-    gpu_srcs = sorted((CSRC / 'gpu').glob('*.hip'))
+    gpu_srcs = sorted((CSRC / 'gpu').glob('*.hip')) + sorted((CSRC / 'gpu').glob('*.cpp'))
     if not gpu_srcs:
         return None
     hflags = ['-std=c++17', '-O3', '-fPIC', f'--offload-arch={HIP_ARCH}', '-Wall',
@@ -141,7 +141,7 @@ def build_hip(verbose=False, jobs=8):
         objs = [f.result() for f in futs]
     target = PKG / f'_hip{_ext_suffix()}'
     if _newer(target, objs):
-        link = [hipcc, '-shared', '-fPIC', f'--offload-arch={HIP_ARCH}', *objs, '-o', target]
+        link = [hipcc, '-shared', '-fPIC', f'--offload-arch={HIP_ARCH}', '-Wl,-Bsymbolic', *objs, '-o', target]
         if tl is not None:
             # resolve libamdhip64 to the runtime torch already loaded
             link += [f'-L{tl}', f'-Wl,-rpath,{tl}']

@@ -1,0 +1,181 @@
+"""Device-resident streaming: producer frames -> decoded batches in HBM.
+
+:class:`DeviceLoader` is the MI355X-native counterpart of
+``DataLoader(RemoteIterableDataset(...), batch_size=B, num_workers=W)``
+(reference: pkg_pytorch/blendtorch/btt/dataset.py:14-117 and
+benchmarks/benchmark.py:24-41).  Instead of W forked worker processes that
+unpickle each frame, run numpy transforms, ``default_collate`` the batch and
+ship it through shared memory, one native pipeline per GPU rank
+(``csrc/gpu/loader.cpp``) lands frames in pinned host slots, DMAs them to the
+device on a side HIP stream and runs the fused gfx950 decode kernel into a
+tensor the consumer's stream waits on.  Nothing round-trips to the host.
+
+Semantics kept from the reference:
+
+* PULL sockets connect to every address; fair-queued fan-in with RCVHWM
+  backpressure; each message goes to exactly one consumer.
+* ``max_items`` bounds the stream (``stream_length``); silence longer than
+  ``timeoutms`` raises (``dataset.py:98-99``).
+* Every non-image key of the producer dict is collated like
+  ``default_collate`` would (ints -> int64 tensor, ndarrays stacked, ...).
+"""
+from __future__ import annotations
+
+import logging
+import time
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+from torch.utils.data import default_collate
+
+from .. import ops
+from ..ops import DecodeConfig
+from .constants import DEFAULT_TIMEOUTMS
+
+logger = logging.getLogger('blendtorch')
+
+__all__ = ['DeviceLoader', 'DecodeConfig']
+
+
+class DeviceLoader:
+    """Iterate decoded batches of producer frames resident on a GPU.
+
+    Params
+    ------
+    addresses: list of str
+        Producer PUSH addresses (``launch_info.addresses['DATA']``).
+    batch_size: int
+        Items per batch (B).
+    decode: DecodeConfig
+        What the decode kernel does (channels, gamma, normalisation, dtype,
+        layout, flip, optional colour matrix).
+    device: torch.device / int / str
+        Target GPU (default: current device).
+    max_items: int, optional
+        Total items to deliver; the stream ends after ``max_items // B``
+        batches.  None streams forever.
+    timeoutms: int
+        Max wait for the next batch before ``TimeoutError``.
+    prefetch: int
+        Output batches the native pipeline may run ahead of the consumer.
+    io_threads: int, optional
+        Receive IO threads (default: one per 4 addresses, at least 1).
+    image_key: str
+        Dict key holding the u8 HxWxC image.
+    skip_bad: bool
+        Drop malformed messages instead of failing the stream.
+    meta_to_device: bool
+        Move collated metadata tensors to the device as well.
+    """
+
+    def __init__(self, addresses: Sequence[str], batch_size: int = 8, decode: DecodeConfig = DecodeConfig(),
+                 device=None, max_items: Optional[int] = None, timeoutms: int = DEFAULT_TIMEOUTMS,
+                 rcvhwm: int = 10, prefetch: int = 4, io_threads: Optional[int] = None, image_key: str = 'image',
+                 skip_bad: bool = False, meta_to_device: bool = False, staging_depth: int = 3):
+        if isinstance(addresses, str):
+            addresses = [addresses]
+        self.addresses = list(addresses)
+        self.batch_size = int(batch_size)
+        self.decode = decode
+        if device is None:
+            device = torch.device('cuda', torch.cuda.current_device())
+        self.device = torch.device(device) if not isinstance(device, int) else torch.device('cuda', device)
+        if self.device.index is None:
+            self.device = torch.device('cuda', torch.cuda.current_device())
+        self.max_items = max_items
+        self.timeoutms = timeoutms
+        self.rcvhwm = rcvhwm
+        self.prefetch = max(1, int(prefetch))
+        self.io_threads = io_threads or max(1, min(8, (len(self.addresses) + 3) // 4))
+        self.image_key = image_key
+        self.skip_bad = skip_bad
+        self.meta_to_device = meta_to_device
+        self.staging_depth = staging_depth
+        self._loader = None
+        self.shape = None          # (H, W, C) of incoming frames
+        self.stats = {}
+
+    def __len__(self):
+        if self.max_items is None:
+            raise TypeError('infinite stream has no length')
+        return self.max_items // self.batch_size
+
+    def stream_length(self, max_items):
+        self.max_items = max_items
+        return self
+
+    # -- native pipeline -----------------------------------------------------
+    def _make(self):
+        ext = ops.hip_ext()
+        cfg = self.decode
+        lut = ops.build_lut(cfg).reshape(-1).tolist()
+        matrix = [] if cfg.color_matrix is None else np.asarray(cfg.color_matrix, np.float32).reshape(-1).tolist()
+        bias = [] if cfg.color_matrix is None else list(cfg.color_bias or (0.0, 0.0, 0.0, 0.0))
+        max_batches = -1 if self.max_items is None else self.max_items // self.batch_size
+        return ext.StreamLoader(
+            self.addresses, self.batch_size, self.image_key, self.rcvhwm, self.io_threads, self.device.index,
+            max_batches, 0, 0, self.staging_depth, self.skip_bad, cfg.cout, list(cfg.cmap) + [0] * (4 - len(cfg.cmap)),
+            int(cfg.flip), ops.OUT_DTYPES[cfg.dtype], ops.LAYOUTS[cfg.layout], lut, matrix, bias)
+
+    def _post(self, loader, stream):
+        out = torch.empty(self.decode.out_shape(self.batch_size, *self.shape[:2]), dtype=self.decode.torch_dtype(),
+                          device=self.device)
+        loader.post(out.data_ptr(), stream.cuda_stream)
+        return out
+
+    def _collate_meta(self, metas):
+        if not metas or not metas[0]:
+            return {}
+        keys = metas[0].keys()
+        out = {}
+        for k in keys:
+            vals = [m.get(k) for m in metas]
+            try:
+                v = default_collate(vals)
+            except (TypeError, RuntimeError):
+                v = vals
+            if self.meta_to_device and isinstance(v, torch.Tensor):
+                v = v.to(self.device, non_blocking=True)
+            out[k] = v
+        return out
+
+    def __iter__(self):
+        loader = self._make()
+        loader.start()
+        try:
+            with torch.cuda.device(self.device):
+                stream = torch.cuda.current_stream(self.device)
+                shape = None
+                t0 = time.time()
+                while shape is None:
+                    shape = loader.wait_shape(200)
+                    if shape is None and (time.time() - t0) * 1000 > self.timeoutms:
+                        raise TimeoutError('No response within timeout interval.')
+                self.shape = tuple(shape)
+                n_batches = None if self.max_items is None else self.max_items // self.batch_size
+                pending = [self._post(loader, stream) for _ in range(self.prefetch if n_batches is None
+                                                                        else min(self.prefetch, n_batches))]
+                posted = len(pending)
+                delivered = 0
+                while n_batches is None or delivered < n_batches:
+                    t0 = time.time()
+                    r = None
+                    while r is None:
+                        r = loader.next(stream.cuda_stream, 200)
+                        if r is None and (time.time() - t0) * 1000 > self.timeoutms:
+                            raise TimeoutError('No response within timeout interval.')
+                    idx, metas, _ = r
+                    if idx < 0:
+                        break
+                    out = pending.pop(0)
+                    if n_batches is None or posted < n_batches:
+                        pending.append(self._post(loader, stream))
+                        posted += 1
+                    batch = {self.image_key: out}
+                    batch.update(self._collate_meta(metas))
+                    delivered += 1
+                    yield batch
+        finally:
+            self.stats = loader.stats()
+            loader.stop()

@@ -1,0 +1,348 @@
+"""Hand-written gfx950 kernels for the image path, with fp32 PyTorch references.
+
+The reference does all of this with numpy on the CPU, per item, inside
+DataLoader workers:
+
+* vertical flip to the upper-left origin   -- ``btb/offscreen.py:95-96``
+* gamma "linear->sRGB" ``u8(255*(x/255)**(1/g))``, alpha untouched
+                                           -- ``btb/offscreen.py:105-112``,
+                                              ``examples/datagen/generate.py:10-14``
+* RGBA -> RGB channel select               -- ``btb/offscreen.py:57-62``
+* normalize ``(x-127.5)/127.5`` + HWC->CHW -- ``examples/densityopt/densityopt.py:117-119``
+* batch collate                            -- torch ``default_collate``
+
+Here they are one fused HIP kernel over a whole batch (:func:`decode`), plus
+a per-pixel 4x4 colour transform on the MFMA units (:func:`color4x4`) and
+batched pinhole projection (:func:`project`, ``btb/camera.py:84-162``).
+
+Every kernel has a plain-PyTorch fp32 reference (``reference_*``) used by the
+numerics tests.  On a machine with a GPU the HIP extension MUST load:
+:func:`hip_ext` raises instead of silently falling back.
+"""
+from __future__ import annotations
+
+import dataclasses
+import importlib
+from typing import Optional, Sequence
+
+import numpy as np
+
+__all__ = [
+    'DecodeConfig', 'hip_ext', 'hip_available', 'gamma_lut', 'build_lut', 'decode', 'color4x4', 'project',
+    'reference_decode', 'reference_color4x4', 'reference_project', 'reference_gamma',
+]
+
+OUT_DTYPES = {'float32': 0, 'bfloat16': 1, 'float16': 2, 'uint8': 3}
+LAYOUTS = {'nchw': 0, 'nhwc': 1}
+
+_hip = None
+_hip_error = None
+
+
+def hip_ext():
+    """Return the loaded ``blendtorch._hip`` extension (gfx950 kernels).
+
+    Importing torch first makes the extension bind to the HIP runtime torch
+    already loaded (same ``libamdhip64.so.7`` soname).
+    """
+    global _hip, _hip_error
+    if _hip is not None:
+        return _hip
+    import torch  # noqa: F401  (load torch's HIP runtime first)
+    try:
+        _hip = importlib.import_module('blendtorch._hip')
+    except ImportError as e:  # pragma: no cover - depends on build state
+        _hip_error = e
+        raise ImportError(
+            'blendtorch HIP extension is not built; run `python -m blendtorch._build` '
+            f'(hipcc --offload-arch=gfx950): {e}') from e
+    return _hip
+
+
+def hip_available():
+    """True when a GPU is visible AND the HIP extension loads."""
+    import torch
+    if not torch.cuda.is_available():
+        return False
+    hip_ext()
+    return True
+
+
+# ---------------------------------------------------------------------------
+# LUT construction (host, numpy float32 -- bit-exact with the references)
+# ---------------------------------------------------------------------------
+def gamma_lut(gamma: Optional[float]) -> np.ndarray:
+    """uint8[256] table of the reference's gamma correction.
+
+    Same float32 expression as ``OffScreenRenderer._color_correct``
+    (``btb/offscreen.py:105-112``): ``np.uint8(255.0 * (x/255)**(1/g))``,
+    i.e. truncation, pure power law (not piecewise sRGB).
+    """
+    x = np.arange(256, dtype=np.float32)
+    if not gamma:
+        return x.astype(np.uint8)
+    rgb = x / 255
+    return np.uint8(255.0 * rgb ** (1 / gamma))
+
+
+@dataclasses.dataclass(frozen=True)
+class DecodeConfig:
+    """What the fused decode kernel does to each u8 HWC image.
+
+    channels: 'rgb' | 'rgba' | 'bgr' | 'gray' or an explicit input-channel map
+        (output channel c reads input channel ``channels[c]``).
+    gamma: gamma applied to the colour channels (alpha passes through), as the
+        reference's ``_color_correct``; None = off.
+    scale, mean, std: ``out = (g(x) * scale - mean[c]) / std[c]`` in fp32.
+    dtype: 'float32' | 'bfloat16' | 'float16' | 'uint8' (uint8 only without
+        normalisation).
+    layout: 'nchw' (default, the densityopt item_transform) or 'nhwc'.
+    flip: force a vertical flip of every image (GL lower-left -> upper-left).
+        Producers that send lower-left frames with ``origin='lower-left'`` are
+        flipped per image automatically by the stream loader.
+    color_matrix / color_bias: optional 4x4 affine colour transform applied
+        after gamma (RGBA input, fp32 NCHW output; runs on the MFMA units).
+    """
+    channels: object = 'rgb'
+    gamma: Optional[float] = None
+    scale: float = 1.0
+    mean: Optional[Sequence[float]] = None
+    std: Optional[Sequence[float]] = None
+    dtype: str = 'float32'
+    layout: str = 'nchw'
+    flip: bool = False
+    color_matrix: Optional[Sequence[Sequence[float]]] = None
+    color_bias: Optional[Sequence[float]] = None
+
+    def __post_init__(self):
+        # normalise sequences to tuples: configs are hashable cache keys
+        if not isinstance(self.channels, str):
+            object.__setattr__(self, 'channels', tuple(int(c) for c in self.channels))
+        for f in ('mean', 'std', 'color_bias'):
+            v = getattr(self, f)
+            if v is not None:
+                object.__setattr__(self, f, tuple(float(x) for x in v))
+        if self.color_matrix is not None:
+            object.__setattr__(self, 'color_matrix', tuple(tuple(float(x) for x in r) for r in self.color_matrix))
+        if self.dtype not in OUT_DTYPES:
+            raise ValueError(f'dtype must be one of {list(OUT_DTYPES)}')
+        if self.layout not in LAYOUTS:
+            raise ValueError(f'layout must be one of {list(LAYOUTS)}')
+        if self.dtype == 'uint8' and (self.mean is not None or self.std is not None or self.scale != 1.0):
+            raise ValueError('uint8 output cannot be normalised')
+        if self.color_matrix is not None:
+            m = np.asarray(self.color_matrix, dtype=np.float32)
+            if m.shape != (4, 4):
+                raise ValueError('color_matrix must be 4x4')
+            if self.dtype != 'float32' or self.layout != 'nchw':
+                raise ValueError('color_matrix produces float32 NCHW output')
+
+    # -- presets -----------------------------------------------------------
+    @classmethod
+    def densityopt(cls, **kw):
+        """``(x - 127.5) / 127.5`` + HWC->CHW (``densityopt.py:117-119``)."""
+        return cls(mean=(127.5,) * 4, std=(127.5,) * 4, **kw)
+
+    @classmethod
+    def unit(cls, **kw):
+        """x / 255 in [0, 1]."""
+        return cls(scale=1.0 / 255.0, **kw)
+
+    @property
+    def cmap(self):
+        if isinstance(self.channels, str):
+            return {'rgb': [0, 1, 2], 'rgba': [0, 1, 2, 3], 'bgr': [2, 1, 0], 'bgra': [2, 1, 0, 3],
+                    'gray': [0], 'r': [0]}[self.channels]
+        return list(self.channels)
+
+    @property
+    def cout(self):
+        return 4 if self.color_matrix is not None else len(self.cmap)
+
+    def out_shape(self, B, H, W):
+        c = self.cout
+        return (B, c, H, W) if self.layout == 'nchw' else (B, H, W, c)
+
+    def torch_dtype(self):
+        import torch
+        return getattr(torch, self.dtype)
+
+
+def build_lut(cfg: DecodeConfig) -> np.ndarray:
+    """float32[4, 256]: value of output channel c for input byte v.
+
+    Gamma applies to output channels fed by input channels 0..2 (colour), not
+    to alpha (input channel 3), as in the reference.  For a colour matrix the
+    table is indexed by INPUT channel (the MFMA kernel mixes channels after).
+    """
+    g = gamma_lut(cfg.gamma).astype(np.float32)
+    ident = np.arange(256, dtype=np.float32)
+    lut = np.zeros((4, 256), dtype=np.float32)
+    if cfg.color_matrix is not None:
+        for k in range(4):
+            lut[k] = g if k < 3 else ident
+        return lut
+    mean = np.asarray(cfg.mean if cfg.mean is not None else [0.0] * 4, dtype=np.float32)
+    std = np.asarray(cfg.std if cfg.std is not None else [1.0] * 4, dtype=np.float32)
+    scale = np.float32(cfg.scale)
+    for c, ic in enumerate(cfg.cmap):
+        x = g if ic < 3 else ident
+        if cfg.mean is None and cfg.std is None and cfg.scale == 1.0:
+            lut[c] = x
+        else:
+            lut[c] = (x * scale - mean[c]) / std[c]
+    return lut
+
+
+# ---------------------------------------------------------------------------
+# references (plain PyTorch fp32)
+# ---------------------------------------------------------------------------
+def reference_gamma(images, gamma):
+    """Torch port of the reference formula on a u8 tensor (alpha untouched)."""
+    import torch
+    rgb = images[..., :3].to(torch.float32) / 255
+    rgb = (255.0 * rgb ** (1 / gamma)).to(torch.uint8)
+    if images.shape[-1] == 4:
+        return torch.cat([rgb, images[..., 3:4]], dim=-1)
+    return rgb
+
+
+def reference_decode(images, cfg: DecodeConfig, flip=None):
+    """fp32 PyTorch reference of :func:`decode` (images: u8 [B,H,W,C])."""
+    import torch
+    x = images
+    if x.dim() == 3:
+        x = x.unsqueeze(-1)
+    if cfg.flip:
+        x = torch.flip(x, dims=[1])
+    if flip is not None:
+        f = torch.as_tensor(flip, dtype=torch.bool, device=x.device)
+        x = torch.where(f.view(-1, 1, 1, 1), torch.flip(x, dims=[1]), x)
+    chans = []
+    for c, ic in enumerate(cfg.cmap):
+        v = x[..., ic]
+        if cfg.gamma and ic < 3:
+            v = (255.0 * (v.to(torch.float32) / 255) ** (1 / cfg.gamma)).to(torch.uint8)
+        v = v.to(torch.float32)
+        if not (cfg.mean is None and cfg.std is None and cfg.scale == 1.0):
+            mean = (cfg.mean or [0.0] * 4)[c]
+            std = (cfg.std or [1.0] * 4)[c]
+            v = (v * torch.tensor(cfg.scale, dtype=torch.float32) - torch.tensor(mean, dtype=torch.float32)) \
+                / torch.tensor(std, dtype=torch.float32)
+        chans.append(v)
+    out = torch.stack(chans, dim=1 if cfg.layout == 'nchw' else -1)
+    return out.to(cfg.torch_dtype())
+
+
+def reference_color4x4(images, M, bias, gamma=None, flip=False):
+    import torch
+    x = images
+    if flip:
+        x = torch.flip(x, dims=[1])
+    if gamma:
+        x = reference_gamma(x, gamma)
+    x = x.to(torch.float32)
+    M = torch.as_tensor(M, dtype=torch.float32, device=x.device)
+    b = torch.as_tensor(bias, dtype=torch.float32, device=x.device)
+    out = torch.einsum('bhwk,ck->bchw', x, M) + b.view(1, -1, 1, 1)
+    return out
+
+
+def reference_project(points, PV, V, W, H, upper_left=True):
+    """btb.Camera.world_to_ndc + ndc_to_pixel (``camera.py:84-136``) in torch."""
+    import torch
+    p = torch.as_tensor(points, dtype=torch.float64)
+    xyzw = torch.cat([p, torch.ones_like(p[:, :1])], dim=1)
+    clip = xyzw @ torch.as_tensor(PV, dtype=torch.float64).T
+    ndc = clip[:, :3] / clip[:, 3:4]
+    xy = (ndc[:, :2] + 1) * 0.5
+    if upper_left:
+        xy[:, 1] = 1.0 - xy[:, 1]
+    px = xy * torch.tensor([[W, H]], dtype=torch.float64)
+    depth = -(xyzw @ torch.as_tensor(V, dtype=torch.float64).T)[:, 2]
+    return px, depth
+
+
+# ---------------------------------------------------------------------------
+# HIP launchers
+# ---------------------------------------------------------------------------
+_lut_cache = {}
+
+
+def device_lut(cfg: DecodeConfig, device):
+    import torch
+    key = (cfg, str(device))
+    t = _lut_cache.get(key)
+    if t is None:
+        t = torch.from_numpy(build_lut(cfg)).to(device)
+        _lut_cache[key] = t
+    return t
+
+
+def _stream(device):
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def decode(images, cfg: DecodeConfig = DecodeConfig(), flip=None, out=None):
+    """Fused decode of a u8 [B,H,W,C] device tensor with the gfx950 kernel."""
+    import torch
+    ext = hip_ext()
+    if images.dtype != torch.uint8 or not images.is_cuda:
+        raise TypeError('decode expects a uint8 CUDA/HIP tensor')
+    x = images.contiguous()
+    if x.dim() == 3:
+        x = x.unsqueeze(-1)
+    B, H, W, C = x.shape
+    if max(cfg.cmap) >= C:
+        raise ValueError(f'channel map {cfg.cmap} needs more than {C} input channels')
+    if cfg.color_matrix is not None:
+        return color4x4(x, cfg.color_matrix, cfg.color_bias or [0.0] * 4, gamma=cfg.gamma, flip=cfg.flip)
+    if out is None:
+        out = torch.empty(cfg.out_shape(B, H, W), dtype=cfg.torch_dtype(), device=x.device)
+    lut = device_lut(cfg, x.device)
+    fl = 0
+    if flip is not None:
+        fl_t = torch.as_tensor(flip, dtype=torch.uint8, device=x.device).contiguous()
+        if fl_t.numel() != B:
+            raise ValueError('flip needs one flag per image')
+        fl = fl_t.data_ptr()
+    ext.decode(x.data_ptr(), 0, out.data_ptr(), lut.data_ptr(), fl, B, H, W, C, cfg.cout, cfg.cmap,
+               int(cfg.flip), OUT_DTYPES[cfg.dtype], LAYOUTS[cfg.layout], _stream(x.device))
+    return out
+
+
+def color4x4(images, M, bias=(0.0, 0.0, 0.0, 0.0), gamma=None, flip=False, cout=4):
+    """out[b,c] = M[c,:] . g(in[b,:,y,x]) + bias[c] on the MFMA units (fp32)."""
+    import torch
+    ext = hip_ext()
+    x = images.contiguous()
+    B, H, W, C = x.shape
+    if C != 4:
+        raise ValueError('color4x4 needs RGBA input')
+    if W % 64:
+        raise ValueError('color4x4 needs W % 64 == 0')
+    cfg = DecodeConfig(channels='rgba', gamma=gamma, color_matrix=tuple(map(tuple, np.asarray(M, np.float32))))
+    lut = device_lut(cfg, x.device)
+    Mt = torch.as_tensor(np.asarray(M, np.float32), device=x.device).contiguous()
+    bt = torch.as_tensor(np.asarray(bias, np.float32), device=x.device).contiguous()
+    out = torch.empty((B, cout, H, W), dtype=torch.float32, device=x.device)
+    ext.color4x4(x.data_ptr(), out.data_ptr(), lut.data_ptr(), Mt.data_ptr(), bt.data_ptr(), 0, B, H, W, cout,
+                 int(flip), _stream(x.device))
+    return out
+
+
+def project(points, PV, V, W, H, upper_left=True):
+    """Batched world->pixel projection on the GPU (fp32)."""
+    import torch
+    ext = hip_ext()
+    p = points.to(torch.float32).contiguous()
+    dev = p.device
+    PVt = torch.as_tensor(np.asarray(PV, np.float32), device=dev).contiguous()
+    Vt = torch.as_tensor(np.asarray(V, np.float32), device=dev).contiguous()
+    N = p.shape[0]
+    px = torch.empty((N, 2), dtype=torch.float32, device=dev)
+    depth = torch.empty((N,), dtype=torch.float32, device=dev)
+    ext.project(p.data_ptr(), N, PVt.data_ptr(), Vt.data_ptr(), W, H, int(upper_left), px.data_ptr(),
+                depth.data_ptr(), _stream(dev))
+    return px, depth

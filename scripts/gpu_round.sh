@@ -1,0 +1,22 @@
+#!/bin/bash
+# One gpurun session: GPU tests, smoke, bench, profile.  Stops at the first
+# GPU fault / abort / timeout (exit codes other than 0 = ok, 1 = test failure).
+set -u
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
+echo "== host: nproc=$(nproc) affinity=$(python -c 'import os;print(len(os.sched_getaffinity(0)))') cpu.max=$(cat /sys/fs/cgroup/cpu.max 2>/dev/null)" | tee gpurun_out/host.txt
+timeout -k 10 240 python -c "import sys; sys.path.insert(0,'.'); import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { echo build failed; tail -20 gpurun_out/build.log; exit 2; }
+for step in "$@"; do
+  case "$step" in
+    tests) timeout -k 10 400 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -5 gpurun_out/pytest_gpu.log;;
+    smoke) timeout -k 10 200 python -c "import sys; sys.path.insert(0,'.'); import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?; tail -3 gpurun_out/smoke.log;;
+    bench) timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1; rc=$?; tail -3 gpurun_out/bench.log;;
+    bench:*) a="${step#bench:}"; timeout -k 10 300 python bench.py ${a//,/ } >> gpurun_out/bench_sweep.log 2>&1; rc=$?; tail -1 gpurun_out/bench_sweep.log;;
+    prof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 100 --warmup 10 > gpurun_out/prof.log 2>&1; rc=$?; tail -3 gpurun_out/prof.log;;
+    *) echo "unknown step $step"; rc=2;;
+  esac
+  echo "== step $step rc=$rc"
+  ok $rc || exit $rc
+done

@@ -1,0 +1,103 @@
+"""Numerics of the gfx950 kernels against plain-PyTorch fp32 references."""
+import numpy as np
+import pytest
+import torch
+
+from blendtorch import ops
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def dev():
+    assert torch.cuda.is_available(), 'GPU tests need a HIP device'
+    ops.hip_ext()  # must load: no silent fallback
+    return torch.device('cuda', 0)
+
+
+def _imgs(B, H, W, C, dev, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randint(0, 256, (B, H, W, C), dtype=torch.uint8, generator=g).to(dev)
+
+
+@pytest.mark.parametrize('C,channels', [(4, 'rgb'), (4, 'rgba'), (3, 'rgb'), (3, 'bgr'), (4, 'bgra')])
+@pytest.mark.parametrize('dtype', ['float32', 'bfloat16', 'float16'])
+@pytest.mark.parametrize('layout', ['nchw', 'nhwc'])
+def test_decode_matches_reference(dev, C, channels, dtype, layout):
+    x = _imgs(3, 48, 64, C, dev)
+    cfg = ops.DecodeConfig.densityopt(channels=channels, gamma=2.2, dtype=dtype, layout=layout)
+    out = ops.decode(x, cfg)
+    ref = ops.reference_decode(x.cpu(), cfg)
+    torch.cuda.synchronize()
+    assert out.shape == ref.shape and out.dtype == ref.dtype
+    assert torch.equal(out.cpu(), ref), (out.cpu().float() - ref.float()).abs().max()
+
+
+@pytest.mark.parametrize('W', [640, 30, 17])
+def test_decode_unit_flip_shapes(dev, W):
+    x = _imgs(2, 7, W, 4, dev, seed=1)
+    cfg = ops.DecodeConfig.unit(channels='rgb', gamma=2.2, flip=True)
+    out = ops.decode(x, cfg)
+    ref = ops.reference_decode(x.cpu(), cfg)
+    assert torch.equal(out.cpu(), ref)
+
+
+def test_decode_per_image_flip_and_u8(dev):
+    x = _imgs(4, 16, 32, 4, dev, seed=2)
+    cfg = ops.DecodeConfig(channels='rgba', gamma=2.2, dtype='uint8')
+    flip = [1, 0, 0, 1]
+    out = ops.decode(x, cfg, flip=flip)
+    ref = ops.reference_decode(x.cpu(), cfg, flip=flip)
+    assert torch.equal(out.cpu(), ref)
+    # gamma LUT bit-exact with the numpy formula of btb/offscreen.py:105-112
+    np_ref = np.uint8(255.0 * (x.cpu().numpy()[..., :3].astype(np.float32) / 255) ** (1 / 2.2))
+    xf = x.cpu().numpy()
+    xf[[0, 3]] = xf[[0, 3], ::-1]
+    np_ref = np.uint8(255.0 * (xf[..., :3].astype(np.float32) / 255) ** (1 / 2.2))
+    assert np.array_equal(out.cpu().numpy()[:, :3].transpose(0, 2, 3, 1), np_ref)
+
+
+def test_decode_large_batch_vector_path(dev):
+    x = _imgs(8, 480, 640, 4, dev, seed=3)
+    cfg = ops.DecodeConfig.unit(channels='rgb', gamma=2.2)
+    out = ops.decode(x, cfg)
+    ref = ops.reference_decode(x, cfg)  # on-device torch reference
+    assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize('gamma', [None, 2.2])
+def test_color4x4_mfma(dev, gamma):
+    x = _imgs(2, 8, 128, 4, dev, seed=4)
+    rng = np.random.default_rng(0)
+    M = rng.normal(size=(4, 4)).astype(np.float32)
+    b = rng.normal(size=4).astype(np.float32)
+    out = ops.color4x4(x, M, b, gamma=gamma)
+    ref = ops.reference_color4x4(x.cpu(), M, b, gamma=gamma)
+    torch.testing.assert_close(out.cpu(), ref, rtol=1e-5, atol=1e-3)
+
+
+def test_color4x4_identity_layout_probe(dev):
+    """Asymmetric check of the MFMA operand map: a permutation matrix must
+    route input channel k to output channel perm[k] exactly."""
+    x = _imgs(1, 2, 64, 4, dev, seed=5)
+    perm = [2, 0, 3, 1]
+    M = np.zeros((4, 4), np.float32)
+    for k, c in enumerate(perm):
+        M[c, k] = 1.0
+    out = ops.color4x4(x, M, [0, 0, 0, 0])
+    xs = x.cpu().float()
+    for k, c in enumerate(perm):
+        assert torch.equal(out[0, c].cpu(), xs[0, :, :, k]), (k, c)
+
+
+def test_project_matches_reference(dev):
+    rng = np.random.default_rng(1)
+    pts = rng.normal(size=(1000, 3)).astype(np.float32)
+    V = np.eye(4, dtype=np.float32)
+    V[2, 3] = -7.0
+    f = 50 / 36 * 2
+    P = np.array([[f, 0, 0, 0], [0, f * 640 / 480, 0, 0], [0, 0, -1.2, -2.2], [0, 0, -1, 0]], np.float32)
+    px, d = ops.project(torch.from_numpy(pts).to(dev), P @ V, V, 640, 480)
+    rpx, rd = ops.reference_project(pts, (P @ V).astype(np.float64), V.astype(np.float64), 640, 480)
+    torch.testing.assert_close(px.cpu().double(), rpx, rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(d.cpu().double(), rd, rtol=1e-5, atol=1e-4)
