@@ -67,8 +67,8 @@ def cpu_budget():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=int(os.environ.get('WORLD_SIZE', '1')))
-    ap.add_argument('--steps', type=int, default=200)
-    ap.add_argument('--warmup', type=int, default=20)
+    ap.add_argument('--steps', type=int, default=1000)
+    ap.add_argument('--warmup', type=int, default=50)
     ap.add_argument('--batch', type=int, default=8)
     ap.add_argument('--producers', type=int, default=0, help='producer processes per GPU (0 = auto)')
     ap.add_argument('--mode', choices=['rgba', 'rgb'], default='rgba')

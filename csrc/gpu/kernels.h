@@ -51,7 +51,8 @@ hipError_t decode(const DecodeParams& p, hipStream_t stream);
 
 // Per-pixel affine colour transform on the MFMA units:
 //   out[b, c, y, x] = sum_k M[c][k] * lut[k][in[b, y, x, k]] + bias[c]
-// for RGBA u8 HWC input (Cin = 4), f32 NCHW output with Cout <= 4 channels.
+// for RGBA u8 HWC input (Cin = 4), f32 NCHW output with Cout <= 4 channels;
+// H*W % 256 == 0 and W % 4 == 0 (one wave = 256 consecutive pixels).
 // `lut` is the same folded per-channel table decode() uses (identity for raw
 // values); M is row-major 4x4 f32, bias f32[4] (device pointers).
 struct Color4x4Params {

@@ -16,9 +16,9 @@
 //   * the vertical flip (GL lower-left readback) is a source-row remap.
 // color4x4: per-pixel 4x4 affine transform on the matrix cores with
 //   v_mfma_f32_4x4x1_16b_f32 (16 independent 4x4 blocks per wave, exact f32):
-//   block = 4 pixels x 4 output channels, K = input channel, 4 MFMAs per
-//   64 pixels; lane l ends up holding output channel (l & 3) of four
-//   consecutive pixels -> one 16-byte store per lane, plane-contiguous.
+//   block = 4 pixels x 4 output channels, K = input channel, 16 MFMAs per
+//   256 pixels; lane l ends up holding output channel (l & 3) of sixteen
+//   consecutive pixels -> four 16-byte stores per lane, plane-contiguous.
 #include <hip/hip_runtime.h>
 
 #include "kernels.h"
@@ -60,6 +60,44 @@ __device__ __forceinline__ void load_pixels(const uint8_t* p, Pixels<PPT, CIN>& 
   } else {
 #pragma unroll
     for (int i = 0; i < NB / 4; ++i) *reinterpret_cast<uint32_t*>(&px.v[4 * i]) = reinterpret_cast<const uint32_t*>(p)[i];
+  }
+}
+
+template <int PPT, int CIN, int OUTT, int COUT>
+__device__ __forceinline__ void store_nhwc(const DecodeParams& p, const float* lut, const int* cm,
+                                           const Pixels<PPT, CIN>& px, int b, int64_t q, int64_t HW) {
+  constexpr int N = PPT * COUT;
+  const int64_t off = (int64_t(b) * HW + q) * COUT;
+  if constexpr (OUTT == OUT_F32) {
+    float o[N];
+#pragma unroll
+    for (int i = 0; i < PPT; ++i)
+#pragma unroll
+      for (int c = 0; c < COUT; ++c) o[i * COUT + c] = lut[c * 256 + px.v[i * CIN + cm[c]]];
+    float4* d = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.dst) + off);
+#pragma unroll
+    for (int i = 0; i < N / 4; ++i) d[i] = make_float4(o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]);
+  } else if constexpr (OUTT == OUT_BF16 || OUTT == OUT_F16) {
+    uint16_t o[N];
+#pragma unroll
+    for (int i = 0; i < PPT; ++i)
+#pragma unroll
+      for (int c = 0; c < COUT; ++c) {
+        float v = lut[c * 256 + px.v[i * CIN + cm[c]]];
+        o[i * COUT + c] = OUTT == OUT_BF16 ? f2bf(v) : f2h(v);
+      }
+    uint4* d = reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(p.dst) + off);
+#pragma unroll
+    for (int i = 0; i < N / 8; ++i) d[i] = *reinterpret_cast<const uint4*>(&o[8 * i]);
+  } else {
+    uint8_t o[N];
+#pragma unroll
+    for (int i = 0; i < PPT; ++i)
+#pragma unroll
+      for (int c = 0; c < COUT; ++c) o[i * COUT + c] = uint8_t(lut[c * 256 + px.v[i * CIN + cm[c]]]);
+    uint4* d = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(p.dst) + off);
+#pragma unroll
+    for (int i = 0; i < N / 16; ++i) d[i] = *reinterpret_cast<const uint4*>(&o[16 * i]);
   }
 }
 
@@ -120,23 +158,13 @@ __global__ __launch_bounds__(kBlock) void decode_vec_kernel(DecodeParams p) {
         }
       }
     } else {
-      // NHWC (channels_last): PPT*cout contiguous elements
-      const int64_t off = (int64_t(b) * HW + q) * cout;
-      if constexpr (OUTT == OUT_F32) {
-        float* d = reinterpret_cast<float*>(p.dst) + off;
-        for (int i = 0; i < PPT; ++i)
-          for (int c = 0; c < cout; ++c) d[i * cout + c] = lut[c * 256 + px.v[i * CIN + cm[c]]];
-      } else if constexpr (OUTT == OUT_BF16 || OUTT == OUT_F16) {
-        uint16_t* d = reinterpret_cast<uint16_t*>(p.dst) + off;
-        for (int i = 0; i < PPT; ++i)
-          for (int c = 0; c < cout; ++c) {
-            float v = lut[c * 256 + px.v[i * CIN + cm[c]]];
-            d[i * cout + c] = OUTT == OUT_BF16 ? f2bf(v) : f2h(v);
-          }
-      } else {
-        uint8_t* d = reinterpret_cast<uint8_t*>(p.dst) + off;
-        for (int i = 0; i < PPT; ++i)
-          for (int c = 0; c < cout; ++c) d[i * cout + c] = uint8_t(lut[c * 256 + px.v[i * CIN + cm[c]]]);
+      // NHWC (channels_last): PPT*COUT contiguous elements, assembled in
+      // registers and written as 16-byte stores (PPT*sizeof(T) == 16).
+      switch (cout) {
+        case 1: store_nhwc<PPT, CIN, OUTT, 1>(p, lut, cm, px, b, q, HW); break;
+        case 2: store_nhwc<PPT, CIN, OUTT, 2>(p, lut, cm, px, b, q, HW); break;
+        case 3: store_nhwc<PPT, CIN, OUTT, 3>(p, lut, cm, px, b, q, HW); break;
+        default: store_nhwc<PPT, CIN, OUTT, 4>(p, lut, cm, px, b, q, HW); break;
       }
     }
   }
@@ -221,12 +249,16 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// Each wave owns 64 consecutive pixels of one row segment per iteration.
-// Operand map of the 16-block 4x4x1 MFMA: block = lane>>2, A[i=lane&3][0],
-// B[0][j=lane&3], D[i=reg][j=lane&3].  We set block = 4 pixels, i = pixel in
-// block, j = output channel, k = input channel (4 MFMAs accumulate k=0..3):
-//   lane l supplies A = in[pixel l][k] and B = M[l&3][k];
-//   lane l receives D[r] = out[pixel 4*(l>>2)+r][channel l&3].
+// Each wave owns 256 consecutive pixels of one image per iteration.
+// Operand map of the 16-block 4x4x1 MFMA (lane l = 4*blk + i):
+//   A[row i][0] of block blk, B[0][col i] of block blk, D[reg r][col i].
+// Row i of block blk at sub-step s (0..3) is pixel 64*i + 4*blk + s, so each
+// lane's A operands over the four sub-steps are 4 consecutive pixels -> ONE
+// 16-byte load.  K (input channel) accumulates over 4 MFMAs, B = M[i][k].
+// Lane (blk, i) receives in reg r the output channel i of pixel
+// 64*r + 4*blk + s; over s that is 4 consecutive pixels -> one float4 per
+// reg, and for a fixed reg the 16 lanes of one channel cover 64 contiguous
+// pixels: every store instruction writes four 256-byte plane runs.
 __global__ __launch_bounds__(kBlock) void color4x4_kernel(Color4x4Params p) {
   __shared__ float lut[4 * 256];
   for (int i = threadIdx.x; i < 4 * 256; i += kBlock) lut[i] = p.lut[i];
@@ -239,26 +271,40 @@ __global__ __launch_bounds__(kBlock) void color4x4_kernel(Color4x4Params p) {
   for (int k = 0; k < 4; ++k) bm[k] = p.M[j * 4 + k];
   const float bj = p.bias[j];
   const int64_t HW = int64_t(p.H) * p.W;
-  const int64_t segs_per_img = HW / 64;   // host guarantees W % 64 == 0
+  const int64_t segs_per_img = HW / 256;   // host guarantees HW % 256 == 0
   const int64_t total = segs_per_img * p.B;
   const int64_t stride = int64_t(gridDim.x) * (kBlock / 64);
   for (int64_t g = int64_t(blockIdx.x) * (kBlock / 64) + wave; g < total; g += stride) {
     const int b = int(g / segs_per_img);
-    const int64_t q0 = (g - int64_t(b) * segs_per_img) * 64;
-    const int y = int(q0 / p.W), x0 = int(q0 - int64_t(y) * p.W);
+    const int64_t q0 = (g - int64_t(b) * segs_per_img) * 256;
+    // lane's 4 pixels share a row (W % 4 == 0); the segment may span rows
+    const int blk = lane >> 2;
+    const int64_t pl = q0 + 64 * j + 4 * blk;
+    const int y = int(pl / p.W), x = int(pl - int64_t(y) * p.W);
     const bool flip = p.flip_all || (p.flip && p.flip[b]) || (b < 256 && ((p.flip_bits[b >> 6] >> (b & 63)) & 1));
     const int sy = flip ? p.H - 1 - y : y;
     const uint8_t* img = p.src + (p.src_offsets ? p.src_offsets[b] : int64_t(b) * HW * 4);
-    const uchar4 v = reinterpret_cast<const uchar4*>(img + (int64_t(sy) * p.W + x0) * 4)[lane];
-    const float a0 = lut[0 * 256 + v.x], a1 = lut[1 * 256 + v.y], a2 = lut[2 * 256 + v.z], a3 = lut[3 * 256 + v.w];
-    f32x4 acc = {bj, bj, bj, bj};
-    acc = __builtin_amdgcn_mfma_f32_4x4x1f32(a0, bm[0], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_4x4x1f32(a1, bm[1], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_4x4x1f32(a2, bm[2], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_4x4x1f32(a3, bm[3], acc, 0, 0, 0);
+    const uint4 v4 = *reinterpret_cast<const uint4*>(img + (int64_t(sy) * p.W + x) * 4);
+    const uint32_t w[4] = {v4.x, v4.y, v4.z, v4.w};
+    f32x4 acc[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const uint32_t px = w[s];
+      const float a0 = lut[0 * 256 + (px & 0xff)], a1 = lut[1 * 256 + ((px >> 8) & 0xff)];
+      const float a2 = lut[2 * 256 + ((px >> 16) & 0xff)], a3 = lut[3 * 256 + (px >> 24)];
+      f32x4 c = {bj, bj, bj, bj};
+      c = __builtin_amdgcn_mfma_f32_4x4x1f32(a0, bm[0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_4x4x1f32(a1, bm[1], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_4x4x1f32(a2, bm[2], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_4x4x1f32(a3, bm[3], c, 0, 0, 0);
+      acc[s] = c;
+    }
     if (j < p.Cout) {
-      float* d = p.dst + (int64_t(b) * p.Cout + j) * HW + q0 + 4 * (lane >> 2);
-      *reinterpret_cast<float4*>(d) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      // pixel 64*r + 4*blk + s  <-  acc[s][r]
+      float* d = p.dst + (int64_t(b) * p.Cout + j) * HW + q0 + 4 * blk;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        *reinterpret_cast<float4*>(d + 64 * r) = make_float4(acc[0][r], acc[1][r], acc[2][r], acc[3][r]);
     }
   }
 }
@@ -287,9 +333,10 @@ __global__ void project_kernel(const float* pts, int64_t N, const float* PV, con
 
 hipError_t color4x4(const Color4x4Params& p, hipStream_t stream) {
   if (p.B <= 0) return hipSuccess;
-  if (p.W % 64 != 0 || p.Cout < 1 || p.Cout > 4 || (reinterpret_cast<uintptr_t>(p.dst) % 16) != 0)
+  if ((int64_t(p.H) * p.W) % 256 != 0 || p.W % 4 != 0 || p.Cout < 1 || p.Cout > 4 || (reinterpret_cast<uintptr_t>(p.dst) % 16) != 0 ||
+      (reinterpret_cast<uintptr_t>(p.src) % 16) != 0)
     return hipErrorInvalidValue;
-  int64_t waves = int64_t(p.B) * p.H * p.W / 64;
+  int64_t waves = int64_t(p.B) * p.H * p.W / 256;
   int64_t blocks = (waves + 3) / 4;
   int grid = int(blocks < 4096 ? blocks : 4096);
   color4x4_kernel<<<grid, kBlock, 0, stream>>>(p);

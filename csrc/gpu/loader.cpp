@@ -294,7 +294,8 @@ bool StreamLoader::process(zmtp::Message&& msg) {
   if (!have_shape_) {
     for (int k = 0; k < cfg_.cout; ++k)
       if (cfg_.cmap[k] >= c) throw std::runtime_error("StreamLoader: channel map exceeds image channels");
-    if (cfg_.color_matrix && c != 4) throw std::runtime_error("StreamLoader: colour matrix needs RGBA input");
+    if (cfg_.color_matrix && (c != 4 || (int64_t(h) * w) % 256 != 0 || w % 4 != 0))
+      throw std::runtime_error("StreamLoader: colour matrix needs RGBA input with H*W % 256 == 0, W % 4 == 0");
     img_bytes_ = size_t(h) * w * c;
     size_t slot = cfg_.max_frame_bytes ? cfg_.max_frame_bytes : size_t(double(n) * 1.05) + 4096;
     slot = (slot + 4095) & ~size_t(4095);

@@ -320,8 +320,8 @@ def color4x4(images, M, bias=(0.0, 0.0, 0.0, 0.0), gamma=None, flip=False, cout=
     B, H, W, C = x.shape
     if C != 4:
         raise ValueError('color4x4 needs RGBA input')
-    if W % 64:
-        raise ValueError('color4x4 needs W % 64 == 0')
+    if (H * W) % 256 or W % 4:
+        raise ValueError('color4x4 needs H*W % 256 == 0 and W % 4 == 0')
     cfg = DecodeConfig(channels='rgba', gamma=gamma, color_matrix=tuple(map(tuple, np.asarray(M, np.float32))))
     lut = device_lut(cfg, x.device)
     Mt = torch.as_tensor(np.asarray(M, np.float32), device=x.device).contiguous()

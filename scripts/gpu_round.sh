@@ -5,6 +5,8 @@ set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+cleanup() { find gpurun_out -type f -size +8M -print -delete; du -sh gpurun_out; }
+trap cleanup EXIT
 ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
 echo "== host: nproc=$(nproc) affinity=$(python -c 'import os;print(len(os.sched_getaffinity(0)))') cpu.max=$(cat /sys/fs/cgroup/cpu.max 2>/dev/null)" | tee gpurun_out/host.txt
 timeout -k 10 240 python -c "import sys; sys.path.insert(0,'.'); import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { echo build failed; tail -20 gpurun_out/build.log; exit 2; }
@@ -14,7 +16,16 @@ for step in "$@"; do
     smoke) timeout -k 10 200 python -c "import sys; sys.path.insert(0,'.'); import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?; tail -3 gpurun_out/smoke.log;;
     bench) timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1; rc=$?; tail -3 gpurun_out/bench.log;;
     bench:*) a="${step#bench:}"; timeout -k 10 300 python bench.py ${a//,/ } >> gpurun_out/bench_sweep.log 2>&1; rc=$?; tail -1 gpurun_out/bench_sweep.log;;
-    prof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 100 --warmup 10 > gpurun_out/prof.log 2>&1; rc=$?; tail -3 gpurun_out/prof.log;;
+    prof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/rp_prof -o run --output-format csv -- python bench.py --steps 300 --warmup 20 > gpurun_out/prof.log 2>&1; rc=$?; tail -2 gpurun_out/prof.log
+          mkdir -p gpurun_out/prof && find /tmp/rp_prof -name '*stats.csv' -exec cp {} gpurun_out/prof/ \;;;
+    kbench) timeout -k 10 200 python scripts/kernel_bench.py --json gpurun_out/kernel_bench.json > gpurun_out/kernel_bench.log 2>&1; rc=$?; cat gpurun_out/kernel_bench.log;;
+    kprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/rp_kprof -o run --output-format csv -- python scripts/kernel_bench.py --iters 50 > gpurun_out/kprof.log 2>&1; rc=$?
+          mkdir -p gpurun_out/kprof && find /tmp/rp_kprof -name '*stats.csv' -exec cp {} gpurun_out/kprof/ \;;;
+    kpmc) timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAVES --kernel-trace -d /tmp/rp_kpmc1 -o run --output-format csv -- python scripts/kernel_pmc.py > gpurun_out/kpmc1.log 2>&1; rc=$?
+          mkdir -p gpurun_out/kpmc && find /tmp/rp_kpmc1 -name '*counter_collection.csv' -exec cp {} gpurun_out/kpmc/pass1_counters.csv \;
+          ok $rc || { echo "kpmc pass1 rc=$rc"; exit $rc; }
+          timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE --kernel-trace -d /tmp/rp_kpmc2 -o run --output-format csv -- python scripts/kernel_pmc.py > gpurun_out/kpmc2.log 2>&1; rc=$?
+          find /tmp/rp_kpmc2 -name '*counter_collection.csv' -exec cp {} gpurun_out/kpmc/pass2_counters.csv \;;;
     *) echo "unknown step $step"; rc=2;;
   esac
   echo "== step $step rc=$rc"

@@ -67,7 +67,7 @@ def test_decode_large_batch_vector_path(dev):
 
 @pytest.mark.parametrize('gamma', [None, 2.2])
 def test_color4x4_mfma(dev, gamma):
-    x = _imgs(2, 8, 128, 4, dev, seed=4)
+    x = _imgs(2, 16, 96, 4, dev, seed=4)
     rng = np.random.default_rng(0)
     M = rng.normal(size=(4, 4)).astype(np.float32)
     b = rng.normal(size=4).astype(np.float32)
@@ -79,7 +79,7 @@ def test_color4x4_mfma(dev, gamma):
 def test_color4x4_identity_layout_probe(dev):
     """Asymmetric check of the MFMA operand map: a permutation matrix must
     route input channel k to output channel perm[k] exactly."""
-    x = _imgs(1, 2, 64, 4, dev, seed=5)
+    x = _imgs(1, 4, 64, 4, dev, seed=5)
     perm = [2, 0, 3, 1]
     M = np.zeros((4, 4), np.float32)
     for k, c in enumerate(perm):
@@ -88,6 +88,15 @@ def test_color4x4_identity_layout_probe(dev):
     xs = x.cpu().float()
     for k, c in enumerate(perm):
         assert torch.equal(out[0, c].cpu(), xs[0, :, :, k]), (k, c)
+
+
+@pytest.mark.parametrize('flip', [False, True])
+def test_color4x4_full_frame(dev, flip):
+    x = _imgs(3, 480, 640, 4, dev, seed=6)
+    M = np.random.default_rng(2).uniform(-1, 1, size=(4, 4)).astype(np.float32)
+    out = ops.color4x4(x, M, [0.5, -0.5, 0, 1], gamma=2.2, flip=flip)
+    ref = ops.reference_color4x4(x, M, [0.5, -0.5, 0, 1], gamma=2.2, flip=flip)
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-3)
 
 
 def test_project_matches_reference(dev):
