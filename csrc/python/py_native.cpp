@@ -7,6 +7,7 @@
 #include <pybind11/stl.h>
 
 #include "../codec/pickle_codec.h"
+#include "../sim/raster.h"
 #include "../transport/zmtp.h"
 #include "pyvalue.h"
 
@@ -249,4 +250,44 @@ class NativeError(Exception):
           return py::bytes(reinterpret_cast<const char*>(out.data()), out.size());
         },
         py::arg("d"), py::arg("protocol") = 4);
+
+  // ---- headless renderer (used by the bpy shim's GPUOffScreen) ----
+  m.def("render_boxes",
+        [](int width, int height, int channels, bool lower_left, std::vector<double> cam_loc,
+           std::vector<double> cam_rot, double lens, double sensor, std::vector<double> light_loc,
+           double light_power, double plane_z, double plane_half, const py::list& boxes) {
+          if (cam_loc.size() != 3 || cam_rot.size() != 9 || light_loc.size() != 3)
+            throw py::value_error("render_boxes: bad camera/light vectors");
+          if (channels != 3 && channels != 4) throw py::value_error("render_boxes: channels must be 3 or 4");
+          sim::Scene sc;
+          sc.cam.width = width;
+          sc.cam.height = height;
+          sc.cam.lens_mm = lens;
+          sc.cam.sensor_mm = sensor;
+          sc.cam.loc = {cam_loc[0], cam_loc[1], cam_loc[2]};
+          for (int i = 0; i < 9; ++i) sc.cam.rot[i] = cam_rot[i];
+          sc.light.loc = {light_loc[0], light_loc[1], light_loc[2]};
+          sc.light.power = light_power;
+          sc.plane_z = plane_z;
+          sc.plane_half = plane_half;
+          for (auto h : boxes) {
+            auto t = h.cast<py::tuple>();
+            auto c = t[0].cast<std::vector<double>>();
+            auto hf = t[1].cast<std::vector<double>>();
+            auto r = t[2].cast<std::vector<double>>();
+            auto a = t[3].cast<std::vector<double>>();
+            sim::Box b;
+            b.center = {c[0], c[1], c[2]};
+            b.half = {hf[0], hf[1], hf[2]};
+            for (int i = 0; i < 9; ++i) b.rot[i] = r[i];
+            b.albedo = {float(a[0]), float(a[1]), float(a[2])};
+            sc.boxes.push_back(b);
+          }
+          py::array_t<uint8_t> out({height, width, channels});
+          {
+            py::gil_scoped_release nogil;
+            sim::render(sc, out.mutable_data(), channels, lower_left);
+          }
+          return out;
+        });
 }

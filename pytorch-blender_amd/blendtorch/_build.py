@@ -34,6 +34,7 @@ CXXFLAGS = ['-std=c++17', '-O3', '-fPIC', '-Wall', '-Wno-unused-parameter', '-pt
 
 TRANSPORT = ['transport/zmtp.cpp']
 CODEC = ['codec/pickle_codec.cpp']
+RASTER = ['sim/raster.cpp']
 
 
 def _ext_suffix():
@@ -90,12 +91,12 @@ def _obj_path(src: Path, tag: str):
 def build_native(verbose=False, jobs=8):
     """Build `_native` Python module and the C++ simulator executables."""
     cxx = os.environ.get('CXX', 'g++')
-    srcs = [CSRC / s for s in TRANSPORT + CODEC]
+    srcs = [CSRC / s for s in TRANSPORT + CODEC + RASTER]
     py_src = CSRC / 'python' / 'py_native.cpp'
     flags = CXXFLAGS + _py_includes()
     with ThreadPoolExecutor(jobs) as ex:
         futs = [ex.submit(_compile, cxx, s, _obj_path(s, 'cpu'), flags, verbose) for s in srcs + [py_src]]
-        sim_srcs = [CSRC / 'sim' / 'cubesim.cpp', CSRC / 'sim' / 'cartpolesim.cpp', CSRC / 'sim' / 'raster.cpp']
+        sim_srcs = [CSRC / 'sim' / n for n in ('cubesim.cpp', 'cartpolesim.cpp', 'supershapesim.cpp')]
         sim_srcs = [s for s in sim_srcs if s.exists()]
         futs += [ex.submit(_compile, cxx, s, _obj_path(s, 'cpu'), CXXFLAGS, verbose) for s in sim_srcs]
         objs = [f.result() for f in futs]
@@ -105,12 +106,9 @@ def build_native(verbose=False, jobs=8):
     if _newer(target, core + [py_obj]):
         _run([cxx, '-shared', '-pthread', '-Wl,-Bsymbolic', *core, py_obj, '-o', target], verbose)
     BIN.mkdir(exist_ok=True)
-    raster = [o for s, o in zip(sim_srcs, objs[len(srcs) + 1:]) if s.name == 'raster.cpp']
     for s, o in zip(sim_srcs, objs[len(srcs) + 1:]):
-        if s.name == 'raster.cpp':
-            continue
         exe = BIN / s.stem
-        deps = core + [o] + raster
+        deps = core + [o]
         if _newer(exe, deps):
             _run([cxx, '-pthread', '-O3', *deps, '-o', exe], verbose)
     return target

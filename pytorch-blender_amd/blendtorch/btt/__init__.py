@@ -3,19 +3,23 @@
 Public names match the reference: BlenderLauncher, LaunchInfo,
 RemoteIterableDataset, FileDataset, discover_blender, FileRecorder,
 FileReader, DuplexChannel, env.  MI355X additions: DeviceLoader and
-DecodeConfig (``btt.gpu``), the device-resident streaming path.
+DecodeConfig (``btt.gpu``, device-resident streaming; imported lazily so
+the CPU API works without the HIP extension).
 """
 from .launcher import BlenderLauncher
 from .launch_info import LaunchInfo
+from .dataset import RemoteIterableDataset, FileDataset, SingleFileDataset
 from .finder import discover_blender
+from .file import FileRecorder, FileReader
+from .duplex import DuplexChannel
 from .utils import get_primary_ip
 from .constants import DEFAULT_TIMEOUTMS
+from . import env
 
 __version__ = '0.2.0'
 
 
 def __getattr__(name):
-    # heavy / optional pieces import lazily (torch, HIP extension)
     if name in ('DeviceLoader', 'DecodeConfig'):
         from . import gpu
         return getattr(gpu, name)

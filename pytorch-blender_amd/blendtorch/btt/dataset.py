@@ -1,0 +1,131 @@
+"""Datasets over live producer streams and over recordings.
+
+Reference: pkg_pytorch/blendtorch/btt/dataset.py:14-153.
+
+* :class:`RemoteIterableDataset` -- ``IterableDataset``; every DataLoader
+  worker lazily opens its own PULL socket (RCVHWM = ``queue_size``) connected
+  to all producer addresses and yields ``max_items // num_workers`` items.
+  Silence longer than ``timeoutms`` fails with
+  ``AssertionError('No response within timeout interval.')``.  With a
+  ``record_path_prefix`` each worker records raw frames to
+  ``{prefix}_{worker:02d}.btr``.
+* :class:`SingleFileDataset` / :class:`FileDataset` -- map-style replay of
+  one / all recordings matching a prefix (shuffle-capable).
+
+Frames are decoded with the native zero-copy unpickler (image arrays are
+views over the received buffer); for device-resident batches see
+:class:`blendtorch.btt.gpu.DeviceLoader`.
+"""
+import pickle
+from contextlib import ExitStack
+from glob import glob
+
+import torch.utils.data as tud
+
+from ..transport import zmq
+from .constants import DEFAULT_TIMEOUTMS
+from .file import FileReader, FileRecorder
+
+
+def _identity_item_transform(x):
+    return x
+
+
+class RemoteIterableDataset(tud.IterableDataset):
+    """Items streamed from remote producers (``btb.DataPublisher``).
+
+    Params: addresses, queue_size=10, timeoutms=10000, max_items=100000,
+    item_transform=None, record_path_prefix=None (as the reference).
+    Override :meth:`_item` or pass ``item_transform`` to post-process items.
+    """
+
+    def __init__(self, addresses, queue_size=10, timeoutms=DEFAULT_TIMEOUTMS, max_items=100000,
+                 item_transform=None, record_path_prefix=None):
+        self.addresses = addresses
+        self.queue_size = queue_size
+        self.timeoutms = timeoutms
+        self.max_items = max_items
+        self.record_path_prefix = record_path_prefix
+        self.item_transform = item_transform or _identity_item_transform
+
+    def enable_recording(self, fname):
+        """Record raw frames to ``{fname}_{worker:02d}.btr`` (set before iterating)."""
+        self.record_path_prefix = fname
+
+    def stream_length(self, max_items):
+        """Set the artificial length of the stream."""
+        self.max_items = max_items
+
+    def __iter__(self):
+        return self._stream()
+
+    def _stream(self):
+        ctx = zmq.Context()
+        socket = None
+        try:
+            socket = ctx.socket(zmq.PULL)
+            socket.setsockopt(zmq.RCVHWM, self.queue_size)
+            poller = zmq.Poller()
+            poller.register(socket, zmq.POLLIN)
+            for addr in self.addresses:
+                socket.connect(addr)
+
+            wi = tud.get_worker_info()
+            worker_id, num_workers = (wi.id, wi.num_workers) if wi is not None else (0, 1)
+
+            with ExitStack() as es:
+                rec = None
+                if self.record_path_prefix is not None:
+                    rec = es.enter_context(FileRecorder(
+                        FileRecorder.filename(self.record_path_prefix, worker_id), self.max_items))
+                for _ in range(self.max_items // num_workers):
+                    ready = dict(poller.poll(self.timeoutms))
+                    assert socket in ready, 'No response within timeout interval.'
+                    if rec is not None:
+                        data = socket.recv()
+                        rec.save(data, is_pickled=True)
+                        obj = pickle.loads(data)
+                    else:
+                        obj = socket.recv_pyobj()
+                    yield self._item(obj)
+                    del obj
+        finally:
+            if socket is not None:
+                socket.close()
+
+    def _item(self, item):
+        """Transform one received item (default: ``item_transform``)."""
+        return self.item_transform(item)
+
+
+class SingleFileDataset(tud.Dataset):
+    """Replay of one ``.btr`` recording."""
+
+    def __init__(self, path, item_transform=None):
+        self.reader = FileReader(path)
+        self.item_transform = item_transform or _identity_item_transform
+
+    def __len__(self):
+        return len(self.reader)
+
+    def __getitem__(self, idx):
+        return self._item(self.reader[idx])
+
+    def _item(self, item):
+        return self.item_transform(item)
+
+
+class FileDataset(tud.ConcatDataset):
+    """Replay of every recording ``{record_path_prefix}_*.btr`` (sorted)."""
+
+    def __init__(self, record_path_prefix, item_transform=None):
+        fnames = sorted(glob(f'{record_path_prefix}_*.btr'))
+        assert len(fnames) > 0, f'Found no recording files with prefix {record_path_prefix}'
+        super().__init__([SingleFileDataset(f) for f in fnames])
+        self.item_transform = item_transform or _identity_item_transform
+
+    def __getitem__(self, idx):
+        return self._item(super().__getitem__(idx))
+
+    def _item(self, item):
+        return self.item_transform(item)

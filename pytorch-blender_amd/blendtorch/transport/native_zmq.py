@@ -9,7 +9,8 @@ against them) need: ``Context``, ``Socket`` (``setsockopt``, ``bind``,
 Wire format is ZMTP/3.0, so these sockets interoperate with libzmq peers.
 
 Differences from pyzmq worth knowing:
-* all Contexts share one native IO thread;
+* all Contexts of a process share one native IO thread (a forked child gets
+  its own; sockets inherited across fork are parked, never used);
 * ``recv_pyobj`` decodes simple dict/ndarray messages with the native
   zero-copy codec (ndarray values are writable views on the received frame);
   anything else falls back to :func:`pickle.loads`.  Set
@@ -334,19 +335,56 @@ def loads(frame):
     return pickle.loads(memoryview(frame))
 
 
+# --- fork safety -------------------------------------------------------------
+# The native engine runs an IO thread per context; threads do not survive
+# fork().  DataLoader workers fork, so every process lazily gets its own
+# native context, and sockets inherited from the parent are parked (never
+# closed or destroyed in the child: their context's IO thread does not exist
+# there, and the parent still owns the connections).
+_proc_ctx = None
+_proc_pid = None
+_inherited = []
+
+
+def _process_context():
+    global _proc_ctx, _proc_pid
+    pid = os.getpid()
+    if _proc_pid != pid:
+        _proc_ctx = _native.global_context() if _proc_pid is None and pid == _MAIN_PID else _native.Context()
+        _proc_pid = pid
+    return _proc_ctx
+
+
+def _after_fork_in_child():
+    global _live_sockets, _proc_pid
+    with _live_lock:
+        _inherited.extend(_live_sockets)
+        _live_sockets = weakref.WeakSet()
+    _proc_pid = -1
+
+
+_MAIN_PID = os.getpid()
+if hasattr(os, 'register_at_fork'):
+    os.register_at_fork(after_in_child=_after_fork_in_child)
+
+
 class Context:
     _instance = None
 
     def __init__(self, io_threads=1, **kwargs):
-        self._native = _native.global_context()
+        self._native = _process_context()
         self._sockets = weakref.WeakSet()
         self.closed = False
 
     @classmethod
     def instance(cls, io_threads=1):
-        if cls._instance is None:
+        if cls._instance is None or cls._instance._pid != os.getpid():
             cls._instance = cls(io_threads)
         return cls._instance
+
+    @property
+    def _pid(self):
+        return _proc_pid
 
     def socket(self, socket_type, **kwargs):
         if self.closed:

@@ -1,0 +1,71 @@
+"""RemoteIterableDataset through DataLoader workers (reference: tests/test_dataset.py)."""
+import numpy as np
+import pytest
+import torch.utils.data as tud
+
+from blendtorch import btt
+from helpers import BLENDDIR, HEADLESS_BLENDER
+
+BATCH = 4
+INSTANCES = 1
+WORKERS = 4
+NUM_ITEMS = 16
+
+
+@pytest.mark.background
+def test_dataset(free_port):
+    args = dict(scene='', script=BLENDDIR / 'dataset.blend.py', num_instances=INSTANCES, named_sockets=['DATA'],
+                background=True, start_port=free_port, blend_path=HEADLESS_BLENDER)
+    with btt.BlenderLauncher(**args) as bl:
+        ds = btt.RemoteIterableDataset(bl.launch_info.addresses['DATA'])
+        ds.stream_length(NUM_ITEMS)
+        dl = tud.DataLoader(ds, batch_size=BATCH, num_workers=WORKERS, shuffle=False)
+        count = 0
+        for item in dl:
+            assert item['img'].shape == (BATCH, 64, 64)
+            assert item['frameid'].shape == (BATCH,)
+            count += 1
+        assert count == NUM_ITEMS // BATCH
+
+
+@pytest.mark.background
+def test_dataset_recording_and_replay(free_port, tmp_path):
+    args = dict(producer='cubesim', num_instances=2, named_sockets=['DATA'], start_port=free_port, seed=5,
+                instance_args=[['--mode', 'rgb']] * 2)
+    with btt.BlenderLauncher(**args) as bl:
+        ds = btt.RemoteIterableDataset(bl.launch_info.addresses['DATA'], max_items=16,
+                                       record_path_prefix=tmp_path / 'rec')
+        dl = tud.DataLoader(ds, batch_size=4, num_workers=2)
+        live = [b for b in dl]
+    assert len(live) == 4
+    assert sorted(p.name for p in tmp_path.glob('rec_*.btr')) == ['rec_00.btr', 'rec_01.btr']
+    replay = btt.FileDataset(tmp_path / 'rec')
+    assert len(replay) == 16
+    item = replay[3]
+    assert item['image'].shape == (480, 640, 3) and item['xy'].shape == (8, 2)
+    live_frames = sorted((int(b), int(f)) for batch in live for b, f in zip(batch['btid'], batch['frameid']))
+    rep_frames = sorted((replay[i]['btid'], replay[i]['frameid']) for i in range(16))
+    assert live_frames == rep_frames
+
+
+@pytest.mark.background
+def test_dataset_timeout_raises(free_port):
+    ds = btt.RemoteIterableDataset([f'tcp://127.0.0.1:{free_port}'], max_items=1, timeoutms=300)
+    with pytest.raises(AssertionError, match='No response'):
+        next(iter(ds))
+
+
+@pytest.mark.background
+def test_item_transform_and_subclass(free_port):
+    class MyDS(btt.RemoteIterableDataset):
+        def _item(self, item):
+            return item['frameid'] * 10
+
+    args = dict(producer='cubesim', num_instances=1, named_sockets=['DATA'], start_port=free_port,
+                instance_args=[['--frame-range', '0', '3']])
+    with btt.BlenderLauncher(**args) as bl:
+        a = list(btt.RemoteIterableDataset(bl.launch_info.addresses['DATA'], max_items=4,
+                                           item_transform=lambda d: d['frameid']))
+        b = list(MyDS(bl.launch_info.addresses['DATA'], max_items=4))
+    assert all(0 <= x <= 3 for x in a)
+    assert all(x % 10 == 0 for x in b)
