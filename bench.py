@@ -76,6 +76,9 @@ def main():
     ap.add_argument('--consumer', choices=['none', 'disc'], default='none')
     ap.add_argument('--io-threads', type=int, default=0)
     ap.add_argument('--start-port', type=int, default=0)
+    ap.add_argument('--dist', choices=['shard', 'scatter'], default='shard',
+                    help='shard: every rank owns its producers; scatter: rank 0 receives world*B per step '
+                         'and scatters B-image shards over RCCL')
     args = ap.parse_args()
 
     rank = int(os.environ.get('RANK', '0'))
@@ -100,6 +103,10 @@ def main():
     share = max(1, len(cpus) // local_world)
     mine = cpus[local_rank * share:(local_rank + 1) * share] or cpus
     nprod = args.producers or max(1, min(12, len(mine) - 3))
+    if args.dist == 'scatter':
+        # the root hosts every producer, pinned across the whole node
+        mine = cpus
+        nprod = nprod * world if rank == 0 else 0
     affinity = [[mine[i % len(mine)]] for i in range(nprod)]
     start_port = args.start_port or (20000 + (os.getpid() % 200) * 50 if world == 1 else 21000 + rank * 64)
 
@@ -117,11 +124,20 @@ def main():
         crit = torch.nn.BCELoss()
 
     total_batches = args.warmup + args.steps
-    with btt.BlenderLauncher(**launch) as bl:
-        dl = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=args.batch, decode=decode, device=device,
-                          max_items=total_batches * args.batch, prefetch=6,
-                          io_threads=args.io_threads or None, timeoutms=60000)
-        it = iter(dl)
+    from contextlib import ExitStack
+    from blendtorch.parallel import ScatterLoader
+    with ExitStack() as es:
+        dl = None
+        if nprod > 0:
+            bl = es.enter_context(btt.BlenderLauncher(**launch))
+            per_step = args.batch * (world if args.dist == 'scatter' else 1)
+            dl = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=per_step, decode=decode, device=device,
+                              max_items=total_batches * per_step, prefetch=6,
+                              io_threads=args.io_threads or None, timeoutms=60000)
+        if args.dist == 'scatter':
+            it = iter(ScatterLoader(dl, args.batch, (3, 480, 640), torch.float32, device, total_batches))
+        else:
+            it = iter(dl)
 
         def step():
             b = next(it)
@@ -151,7 +167,7 @@ def main():
             next(it)
         except StopIteration:
             pass
-        stats = dict(dl.stats)
+        stats = dict(dl.stats) if dl is not None else {}
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
@@ -177,8 +193,8 @@ def main():
                 'model': 'cube-scene-640x480-' + args.mode + (' + dcgan-disc' if model is not None else ''),
                 'global_batch': args.batch * world,
                 'seq_len': None,
-                'parallelism': f'dp{world}',
-                'producers_per_gpu': nprod,
+                'parallelism': f'dp{world}' + ('-scatter' if args.dist == 'scatter' else ''),
+                'producers_per_gpu': nprod // (world if args.dist == 'scatter' else 1),
                 'cpus_per_gpu': len(mine),
                 'decode': 'rgba->rgb, gamma 2.2, /255, HWC->CHW fp32 (gfx950 kernel)',
                 'out_shape': list(shape),

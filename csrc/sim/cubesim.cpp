@@ -10,7 +10,7 @@
 // Script args:  --scene cube|falling_cubes   --mode rgb|rgba   --origin
 // upper-left|lower-left   --frame-range A B   --frames N (-1 = forever)
 // --sndhwm N   --linger MS   --fps F (0 = unthrottled)   --socket NAME
-// --fault none|exit|stall|garbage --fault-after N   --verbose
+// --fault none|exit|stall|garbage --fault-after N   --rotation RX RY RZ   --verbose
 //
 // Every frame it publishes, on a bound PUSH socket with SNDHWM/LINGER/
 // IMMEDIATE as btb.DataPublisher does (reference: btb/publisher.py:21-43),
@@ -59,6 +59,8 @@ struct Args {
   std::string fault = "none";
   long long fault_after = -1;
   bool verbose = false;
+  bool fixed_rotation = false;
+  double rot[3] = {0, 0, 0};
 };
 
 [[noreturn]] void usage(const char* msg) {
@@ -106,6 +108,12 @@ Args parse(int argc, char** argv) {
     else if (k == "--fault") a.fault = need(i), ++i;
     else if (k == "--fault-after") a.fault_after = std::stoll(need(i)), ++i;
     else if (k == "--verbose") a.verbose = true;
+    else if (k == "--rotation") {
+      if (i + 3 >= v.size()) usage("--rotation needs rx ry rz");
+      for (int r = 0; r < 3; ++r) a.rot[r] = std::stod(v[i + 1 + r]);
+      a.fixed_rotation = true;
+      i += 3;
+    }
     // unknown args are ignored, as Blender scripts ignore the remainder
   }
   if (a.mode != "rgb" && a.mode != "rgba") usage("--mode must be rgb or rgba");
@@ -188,6 +196,8 @@ int main(int argc, char** argv) {
           b.center = {-3 + 6 * U(rng), -3 + 6 * U(rng), -1.0 + 3 * U(rng)};
           b.rot = sim::euler_xyz(-pi + 2 * pi * U(rng), -pi + 2 * pi * U(rng), -pi + 2 * pi * U(rng));
         }
+    } else if (a.fixed_rotation) {
+      scene.boxes[0].rot = sim::euler_xyz(a.rot[0], a.rot[1], a.rot[2]);
     } else {
       scene.boxes[0].rot = sim::euler_xyz(pi * U(rng), pi * U(rng), pi * U(rng));
     }

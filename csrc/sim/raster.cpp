@@ -131,7 +131,7 @@ Scene falling_cubes_scene() {
   double n = std::sqrt(dot(dir, dir));
   dir = scale(dir, 1.0 / n);
   double pitch = std::acos(-dir.z);             // rotation about x from looking down
-  double yaw = std::atan2(dir.x, -dir.y);
+  double yaw = std::atan2(-dir.x, dir.y);   // Rz maps +Y to (-sin, cos)
   s.cam.rot = euler_xyz(pitch, 0.0, yaw);
   s.light.loc = {4.0, 1.0, 14.0};
   s.light.power = 6000.0;
@@ -384,6 +384,72 @@ void Renderer::render(const Scene& s, uint8_t* out) {
 void render(const Scene& s, uint8_t* out, int channels, bool lower_left) {
   Renderer r(s, channels, lower_left);
   r.render(s, out);
+}
+
+void render_mesh(const Camera& cam, const std::vector<float>& verts, const std::vector<int>& tris,
+                 const MeshStyle& style, uint8_t* out, int channels, bool lower_left) {
+  const int W = cam.width, H = cam.height;
+  const ToneLut& T = tone();
+  const size_t nv = verts.size() / 3;
+  // project every vertex once
+  std::vector<float> sx(nv), sy(nv), sz(nv);
+  std::vector<uint8_t> ok(nv);
+  for (size_t i = 0; i < nv; ++i) {
+    double px, py, d;
+    ok[i] = cam.project(Vec3{verts[3 * i], verts[3 * i + 1], verts[3 * i + 2]}, &px, &py, &d);
+    sx[i] = float(px), sy[i] = float(py), sz[i] = float(d);
+  }
+  std::vector<float> depth(size_t(W) * H, std::numeric_limits<float>::infinity());
+  std::vector<float> shade(size_t(W) * H, -1.f);
+  Vec3 L = style.light_dir;
+  const double ln = std::sqrt(dot(L, L));
+  L = scale(L, -1.0 / ln);   // towards the light
+  for (size_t t = 0; t + 2 < tris.size(); t += 3) {
+    const int a = tris[t], b = tris[t + 1], c = tris[t + 2];
+    if (!ok[a] || !ok[b] || !ok[c]) continue;
+    // face normal (world) for shading, two-sided
+    const Vec3 A{verts[3 * a], verts[3 * a + 1], verts[3 * a + 2]};
+    const Vec3 B{verts[3 * b], verts[3 * b + 1], verts[3 * b + 2]};
+    const Vec3 C{verts[3 * c], verts[3 * c + 1], verts[3 * c + 2]};
+    const Vec3 e1 = sub(B, A), e2 = sub(C, A);
+    Vec3 n{e1.y * e2.z - e1.z * e2.y, e1.z * e2.x - e1.x * e2.z, e1.x * e2.y - e1.y * e2.x};
+    const double nn = std::sqrt(dot(n, n));
+    if (nn < 1e-18) continue;
+    n = scale(n, 1.0 / nn);
+    const float lam = float(std::fabs(dot(n, L)));
+    const float area = (sx[b] - sx[a]) * (sy[c] - sy[a]) - (sx[c] - sx[a]) * (sy[b] - sy[a]);
+    if (std::fabs(area) < 1e-12f) continue;
+    const int x0 = std::max(0, int(std::floor(std::min({sx[a], sx[b], sx[c]}))));
+    const int x1 = std::min(W - 1, int(std::ceil(std::max({sx[a], sx[b], sx[c]}))));
+    const int y0 = std::max(0, int(std::floor(std::min({sy[a], sy[b], sy[c]}))));
+    const int y1 = std::min(H - 1, int(std::ceil(std::max({sy[a], sy[b], sy[c]}))));
+    const float inv = 1.f / area;
+    for (int y = y0; y <= y1; ++y) {
+      const float py = y + 0.5f;
+      for (int x = x0; x <= x1; ++x) {
+        const float px = x + 0.5f;
+        const float w0 = ((sx[b] - px) * (sy[c] - py) - (sx[c] - px) * (sy[b] - py)) * inv;
+        const float w1 = ((sx[c] - px) * (sy[a] - py) - (sx[a] - px) * (sy[c] - py)) * inv;
+        const float w2 = 1.f - w0 - w1;
+        if (w0 < 0.f || w1 < 0.f || w2 < 0.f) continue;
+        const float z = w0 * sz[a] + w1 * sz[b] + w2 * sz[c];
+        float& zb = depth[size_t(y) * W + x];
+        if (z >= zb) continue;
+        zb = z;
+        shade[size_t(y) * W + x] = lam;
+      }
+    }
+  }
+  for (int y = 0; y < H; ++y) {
+    const int row = lower_left ? (H - 1 - y) : y;
+    for (int x = 0; x < W; ++x) {
+      uint8_t* p = out + (size_t(row) * W + x) * channels;
+      const float s = shade[size_t(y) * W + x];
+      for (int k = 0; k < 3; ++k)
+        p[k] = s < 0.f ? T(style.background[k]) : T(style.albedo[k] * (float(style.ambient) + (1.f - float(style.ambient)) * s));
+      if (channels == 4) p[3] = 255;
+    }
+  }
 }
 
 }  // namespace sim

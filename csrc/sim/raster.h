@@ -102,6 +102,20 @@ class Renderer {
   std::vector<float> depth_;
 };
 
+// Triangle-mesh rendering (z-buffered, two-sided Lambert from a directional
+// light + ambient) over a uniform background -- used for parametric shapes
+// (the densityopt supershapes).  verts: N x 3 world coordinates; tris:
+// M x 3 vertex indices.  Output HWC u8 (linear values tone-mapped like the
+// box renderer), row 0 = top unless lower_left.
+struct MeshStyle {
+  std::array<float, 3> albedo{0.8f, 0.8f, 0.8f};
+  std::array<float, 3> background{0.05f, 0.05f, 0.05f};
+  Vec3 light_dir{-0.4, -0.6, -0.7};   // direction the light travels
+  double ambient = 0.15;
+};
+void render_mesh(const Camera& cam, const std::vector<float>& verts, const std::vector<int>& tris,
+                 const MeshStyle& style, uint8_t* out, int channels, bool lower_left);
+
 // One-shot convenience wrapper (builds a Renderer per call).
 void render(const Scene& s, uint8_t* out, int channels, bool lower_left);
 

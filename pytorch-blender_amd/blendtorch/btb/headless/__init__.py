@@ -106,6 +106,31 @@ class Object:
     def __repr__(self):
         return f'<headless Object {self.name!r} ({self.type})>'
 
+    # Blender accepts any 3-sequence for these; keep them as mathutils types
+    @property
+    def location(self):
+        return self._location
+
+    @location.setter
+    def location(self, v):
+        self._location = v if isinstance(v, Vector) else Vector(v)
+
+    @property
+    def rotation_euler(self):
+        return self._rotation
+
+    @rotation_euler.setter
+    def rotation_euler(self, v):
+        self._rotation = v if isinstance(v, Euler) else Euler(v)
+
+    @property
+    def scale(self):
+        return self._scale
+
+    @scale.setter
+    def scale(self, v):
+        self._scale = v if isinstance(v, Vector) else Vector(v)
+
     @property
     def matrix_world(self):
         m = np.eye(4)

@@ -218,7 +218,7 @@ class VectorRemoteEnv:
     def _stage(self, obs):
         import torch
         arr = np.asarray(obs, dtype=np.float32)
-        if self.device is None:
+        if self.device is None or torch.device(self.device).type == 'cpu':
             return torch.from_numpy(arr)
         if self._pinned is None or tuple(self._pinned.shape) != arr.shape:
             self._pinned = torch.empty(arr.shape, dtype=torch.float32).pin_memory()

@@ -48,40 +48,45 @@ class Discriminator(nn.Module):
 
 
 class ProbModel(nn.Module):
-    """Factorised LogNormal over simulation parameters (densityopt.py:30-93).
+    """Independent LogNormal distributions over the supershape frequencies
+    (m1, m2) (densityopt.py:30-93).
 
-    ``sample(n)`` draws parameters; ``log_prob(samples)`` gives per-sample
-    log-densities used by the REINFORCE estimator
+    ``m1m2_mean`` is the LogNormal ``loc`` (mean of log m) and
+    ``m1m2_log_std`` the log of its scale, both optimised with the
+    score-function (REINFORCE) gradient
     ``grad E[f(x)] = E[(f(x) - b) grad log p(x)]``.
     """
 
-    def __init__(self, mu0, std0):
+    def __init__(self, m1m2_mean, m1m2_std):
         super().__init__()
-        mu0 = torch.as_tensor(mu0, dtype=torch.float32)
-        std0 = torch.as_tensor(std0, dtype=torch.float32)
-        self.log_mu = nn.Parameter(torch.log(mu0))
-        self.log_std = nn.Parameter(torch.log(std0))
+        self.m1m2_mean = nn.Parameter(torch.as_tensor(m1m2_mean).float(), requires_grad=True)
+        self.m1m2_log_std = nn.Parameter(torch.log(torch.as_tensor(m1m2_std).float()), requires_grad=True)
 
     @property
-    def m(self):
-        return torch.exp(self.log_mu)
-
-    @property
-    def s(self):
-        return torch.exp(self.log_std)
-
-    def dist(self):
-        return D.LogNormal(self.log_mu, torch.exp(self.log_std))
+    def dists(self):
+        # built on the fly so autograd sees fresh graphs every step
+        return (D.LogNormal(self.m1m2_mean[0], torch.exp(self.m1m2_log_std[0])),
+                D.LogNormal(self.m1m2_mean[1], torch.exp(self.m1m2_log_std[1])))
 
     def sample(self, n):
-        with torch.no_grad():
-            return self.dist().sample((n,))
+        m1, m2 = self.dists
+        return {'m1': m1.sample((n,)), 'm2': m2.sample((n,))}
 
     def log_prob(self, samples):
-        return self.dist().log_prob(samples).sum(-1)
+        m1, m2 = self.dists
+        return m1.log_prob(samples['m1']) + m2.log_prob(samples['m2'])
 
     def readable_params(self):
-        return self.dist().mean.detach()
+        return torch.cat([self.m1m2_mean.detach(), torch.exp(self.m1m2_log_std).detach()])
+
+    @staticmethod
+    def to_supershape(samples):
+        """(N, 2, 6) supershape params: rows (m, a=1, b=1, n1=n2=n3=3), m from the samples."""
+        n = samples['m1'].shape[0]
+        params = samples['m1'].new_tensor([[0, 1, 1, 3, 3, 3], [0, 1, 1, 3, 3, 3]]).float().view(1, 2, 6).repeat(n, 1, 1)
+        params[:, 0, 0] = samples['m1'].detach()
+        params[:, 1, 0] = samples['m2'].detach()
+        return params
 
 
 class CartpolePolicy(nn.Module):

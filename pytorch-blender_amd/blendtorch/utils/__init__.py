@@ -1,1 +1,117 @@
-"""(filled in below)"""
+"""Observability and configuration helpers.
+
+The reference's only instrumentation is wall-clock timing in
+benchmarks/benchmark.py:33-47 and the ``'blendtorch'`` logger (SURVEY.md
+§5.1, §5.5).  Added here:
+
+* :class:`Meter` -- rate/latency counters (items/s, ms per stage) that can be
+  dumped as a dict or logged;
+* :func:`trace_range` -- a roctx range (visible in ``rocprofv3
+  --marker-trace`` timelines) around host-side stages, no-op without a GPU;
+* :class:`StreamConfig` -- one place for the GPU streaming knobs whose
+  defaults reproduce the reference's behaviour (HWM 10, 10 s timeout, batch
+  of dicts).
+"""
+from __future__ import annotations
+
+import contextlib
+import dataclasses
+import logging
+import time
+from typing import Dict, Optional
+
+logger = logging.getLogger('blendtorch')
+
+__all__ = ['Meter', 'trace_range', 'StreamConfig', 'get_logger']
+
+
+def get_logger():
+    return logger
+
+
+class Meter:
+    """Accumulates counts and durations per named stage.
+
+    >>> m = Meter()
+    >>> with m.time('recv'):
+    ...     pass
+    >>> m.count('frames', 8)
+    >>> sorted(m.summary())  # doctest: +ELLIPSIS
+    ['elapsed_s', 'frames', 'frames_per_s', 'recv_ms', 'recv_ms_avg']
+    """
+
+    def __init__(self):
+        self.t0 = time.perf_counter()
+        self.counts: Dict[str, float] = {}
+        self.ms: Dict[str, float] = {}
+        self.calls: Dict[str, int] = {}
+
+    def count(self, name, n=1):
+        self.counts[name] = self.counts.get(name, 0) + n
+
+    @contextlib.contextmanager
+    def time(self, name):
+        t = time.perf_counter()
+        try:
+            yield
+        finally:
+            self.ms[name] = self.ms.get(name, 0.0) + (time.perf_counter() - t) * 1e3
+            self.calls[name] = self.calls.get(name, 0) + 1
+
+    def summary(self) -> Dict[str, float]:
+        el = max(time.perf_counter() - self.t0, 1e-9)
+        out = {'elapsed_s': el}
+        for k, v in self.counts.items():
+            out[k] = v
+            out[f'{k}_per_s'] = v / el
+        for k, v in self.ms.items():
+            out[f'{k}_ms'] = v
+            out[f'{k}_ms_avg'] = v / max(1, self.calls[k])
+        return out
+
+    def log(self, level=logging.INFO):
+        logger.log(level, ' '.join(f'{k}={v:.4g}' for k, v in self.summary().items()))
+
+
+@contextlib.contextmanager
+def trace_range(name: str):
+    """roctx range around a host-side stage (ROCm maps torch's nvtx API to
+    roctx); silently a no-op when unavailable."""
+    pushed = False
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.nvtx.range_push(name)
+            pushed = True
+    except Exception:
+        pushed = False
+    try:
+        yield
+    finally:
+        if pushed:
+            import torch
+            torch.cuda.nvtx.range_pop()
+
+
+@dataclasses.dataclass
+class StreamConfig:
+    """Knobs of the device streaming path (defaults = reference behaviour).
+
+    batch_size: items per batch; rcvhwm: receive queue per producer (the
+    reference's ``queue_size``); timeoutms: max silence before failing;
+    prefetch: decoded batches the native pipeline may run ahead;
+    io_threads: receive IO threads (None: one per 4 producers);
+    mode: 'shard' (each rank owns producers) or 'scatter' (root receives and
+    scatters over RCCL).
+    """
+    batch_size: int = 8
+    rcvhwm: int = 10
+    timeoutms: int = 10000
+    prefetch: int = 4
+    io_threads: Optional[int] = None
+    staging_depth: int = 3
+    mode: str = 'shard'
+
+    def __post_init__(self):
+        if self.mode not in ('shard', 'scatter'):
+            raise ValueError("mode must be 'shard' or 'scatter'")

@@ -1,0 +1,82 @@
+"""Blender-side units under the headless emulation: arguments, Signal,
+OffScreenRenderer (gamma/flip vs the GPU decode LUT), AnimationController
+details (rewind, physics range, manual loop)."""
+import numpy as np
+import pytest
+
+from blendtorch import btb, ops
+from blendtorch.btb import headless
+
+
+def test_parse_blendtorch_args():
+    argv = ['blender', '--python', 'x.py', '--', '-btid', '2', '-btseed', '7', '-btsockets', 'DATA=tcp://a:1',
+            'GYM=tcp://b:2', '--x', '3']
+    args, rem = btb.parse_blendtorch_args(argv)
+    assert args.btid == 2 and args.btseed == 7
+    assert args.btsockets == {'DATA': 'tcp://a:1', 'GYM': 'tcp://b:2'}
+    assert rem == ['--x', '3']
+    with pytest.raises(ValueError):
+        btb.parse_blendtorch_args(['blender', '-btid', '1'])
+
+
+def test_signal_add_remove_invoke():
+    got = []
+    s = btb.Signal()
+    h = s.add(lambda a, b: got.append(a * b), b=3)
+    s.add(lambda a: got.append(-a))
+    s.invoke(4)
+    assert got == [12, -4]
+    s.remove(h)
+    s.invoke(1)
+    assert got == [12, -4, -1]
+
+
+def test_offscreen_render_modes_and_gamma():
+    headless.install('cube.blend')
+    cam = btb.Camera()
+    assert cam.shape == (480, 640)
+    off = btb.OffScreenRenderer(camera=cam, mode='rgba', origin='lower-left')
+    raw = off.render().copy()
+    assert raw.shape == (480, 640, 4) and (raw[..., 3] == 255).all()
+    ul = btb.OffScreenRenderer(camera=cam, mode='rgb').render()
+    assert np.array_equal(ul, raw[::-1, :, :3])
+    g = btb.OffScreenRenderer(camera=cam, mode='rgba', gamma_coeff=2.2).render()
+    lut = ops.gamma_lut(2.2)
+    assert np.array_equal(g[..., :3], lut[raw[::-1, :, :3]])     # bit-exact with the GPU LUT
+    assert np.array_equal(g[..., 3], raw[::-1, :, 3])            # alpha untouched
+    # the cube is visible near the image centre
+    assert ul[200:280, 280:360].std() > 5
+
+
+def test_animation_rewind_and_physics_range():
+    bpy = headless.install('falling_cubes.blend')
+    anim = btb.AnimationController()
+    frames = []
+    anim.pre_frame.add(lambda: frames.append(anim.frameid))
+    state = {'rewound': False}
+
+    def post():
+        if anim.frameid == 3 and not state['rewound']:
+            state['rewound'] = True
+            anim.rewind()
+    anim.post_frame.add(post)
+    anim.play(frame_range=(1, 4), num_episodes=1, use_animation=False)
+    assert bpy.context.scene.rigidbody_world.point_cache.frame_end == 4
+    assert frames[:3] == [1, 2, 3] and frames[3] == 1 and frames[-1] == 4
+
+
+def test_utils_coordinates():
+    bpy = headless.install('cube.blend')
+    cube = bpy.data.objects['Cube']
+    cube.location = (1, 2, 3)
+    w = btb.utils.world_coordinates(cube)
+    assert np.allclose(w - btb.utils.object_coordinates(cube), [1, 2, 3])
+    bb = btb.utils.bbox_world_coordinates(cube)
+    assert bb.shape == (8, 3) and np.allclose(bb.min(0), [0, 1, 2])
+    x = np.random.rand(5, 3)
+    assert np.allclose(btb.utils.dehom(btb.utils.hom(x, 2.0)), x / 2.0)
+    p = btb.utils.random_spherical_loc(radius_range=(2, 2))
+    assert abs(np.linalg.norm(p) - 2) < 1e-9
+    cam = btb.Camera()
+    vis = btb.utils.compute_object_visibility(cube, cam, N=10)
+    assert 0.0 <= vis <= 1.0

@@ -1,0 +1,74 @@
+"""RCCL/xGMI distribution helpers, exercised with gloo on CPU (world_size 2)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from blendtorch import parallel
+
+
+def test_shard_addresses_disjoint_cover():
+    addrs = [f'tcp://h:{p}' for p in range(10)]
+    shards = [parallel.shard_addresses(addrs, r, 4) for r in range(4)]
+    flat = sorted(a for s in shards for a in s)
+    assert flat == sorted(addrs)
+    assert all(len(s) in (2, 3) for s in shards)
+    assert parallel.shard_addresses(addrs[:2], 3, 4) == [addrs[1]]
+
+
+def test_partition_cpus():
+    cpus = list(range(16))
+    parts = [parallel.partition_cpus(cpus, r, 4) for r in range(4)]
+    assert parts[0] == [0, 1, 2, 3] and parts[3] == [12, 13, 14, 15]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        r, w, dev = parallel.init_distributed(backend='gloo')
+        B = 3
+        full = torch.arange(world * B * 2, dtype=torch.float32).view(world * B, 2) if r == 0 else None
+        shard = parallel.scatter_batch(full, (B, 2), torch.float32, torch.device('cpu'))
+        ok_scatter = torch.equal(shard, torch.arange(r * B * 2, (r + 1) * B * 2, dtype=torch.float32).view(B, 2))
+        t = torch.full((4,), float(r))
+        parallel.broadcast_tensor(t, src=1)
+        ok_bcast = torch.equal(t, torch.full((4,), 1.0))
+        stats = parallel.all_gather_stats({'fps': 10.0 * (r + 1), 'n': r})
+        ok_stats = [s['fps'] for s in stats] == [10.0 * (i + 1) for i in range(world)]
+
+        def source():
+            for step in range(2):
+                yield {'image': torch.full((world * B, 2), float(step)) + torch.arange(world * B).view(-1, 1),
+                       'btid': torch.arange(world * B)}
+        sl = parallel.ScatterLoader(source() if r == 0 else None, B, (2,), torch.float32, torch.device('cpu'), 2)
+        got = [(b['image'][:, 0].tolist(), b['btid'].tolist()) for b in sl]
+        ok_loader = got[1][1] == list(range(r * B, (r + 1) * B)) and got[1][0][0] == 1.0 + r * B
+        q.put((r, ok_scatter, ok_bcast, ok_stats, ok_loader))
+        torch.distributed.destroy_process_group()
+    except Exception as e:  # surface failures to the parent
+        q.put((rank, repr(e)))
+
+
+def test_collectives_gloo_world2():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert r[1:] == (True, True, True, True), r
