@@ -26,6 +26,9 @@ for step in "$@"; do
           ok $rc || { echo "kpmc pass1 rc=$rc"; exit $rc; }
           timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE --kernel-trace -d /tmp/rp_kpmc2 -o run --output-format csv -- python scripts/kernel_pmc.py > gpurun_out/kpmc2.log 2>&1; rc=$?
           find /tmp/rp_kpmc2 -name '*counter_collection.csv' -exec cp {} gpurun_out/kpmc/pass2_counters.csv \;;;
+    rl) timeout -k 10 200 python benchmarks/bench_rl.py --envs 8 --steps 5000 > gpurun_out/bench_rl.log 2>&1; rc=$?; tail -1 gpurun_out/bench_rl.log
+        timeout -k 10 200 python benchmarks/bench_rl.py --envs 1 --steps 5000 >> gpurun_out/bench_rl.log 2>&1; rc=$?; tail -1 gpurun_out/bench_rl.log;;
+    dopt) timeout -k 10 300 python examples/densityopt/densityopt.py --num-epochs 70 --json gpurun_out/densityopt.json > gpurun_out/densityopt.log 2>&1; rc=$?; tail -2 gpurun_out/densityopt.log;;
     *) echo "unknown step $step"; rc=2;;
   esac
   echo "== step $step rc=$rc"

@@ -69,3 +69,46 @@ def test_device_loader_bad_message_raises(dev, free_port):
         with pytest.raises(RuntimeError, match='bad message'):
             for _ in dl:
                 pass
+
+
+def test_device_loader_supershape_duplex(dev, free_port):
+    """densityopt path: parameters out over the duplex, 64x64 renders back into
+    HBM normalised as the reference's item_transform ((x-127.5)/127.5, CHW)."""
+    with btt.BlenderLauncher(producer='supershapesim', num_instances=2, named_sockets=['DATA', 'CTRL'],
+                             start_port=free_port) as bl:
+        remotes = [btt.DuplexChannel(a) for a in bl.launch_info.addresses['CTRL']]
+        dl = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=16, device=dev, max_items=16,
+                          decode=ops.DecodeConfig.densityopt(channels='rgb'))
+        params = np.tile(np.array([[5, 1, 1, 3, 3, 3]], np.float32), (16, 2, 1))
+        for r, p, i in zip(remotes, np.array_split(params, 2), np.array_split(np.arange(16), 2)):
+            r.send(shape_params=p, shape_ids=i)
+        b = next(iter(dl))
+        assert b['image'].shape == (16, 3, 64, 64)
+        assert sorted(b['shape_id'].tolist()) == list(range(16))
+        assert float(b['image'].min()) >= -1 and float(b['image'].max()) <= 1
+
+
+def test_vector_env_stages_obs_on_device(dev, free_port):
+    from blendtorch.btt.env import VectorRemoteEnv
+    from blendtorch.models import CartpolePolicy
+    with btt.BlenderLauncher(producer='cartpolesim', num_instances=4, named_sockets=['GYM'],
+                             start_port=free_port) as bl:
+        venv = VectorRemoteEnv(bl.launch_info.addresses['GYM'], device=dev)
+        pol = CartpolePolicy().to(dev)
+        obs, _ = venv.reset()
+        assert obs.device == dev and obs.shape == (4, 3)
+        for _ in range(10):
+            obs, rew, done, _ = venv.step(pol(obs))
+        assert obs.device == dev
+        venv.close()
+
+
+def test_scatter_loader_single_rank(dev, free_port):
+    from blendtorch.parallel import ScatterLoader
+    with btt.BlenderLauncher(producer='cubesim', num_instances=1, named_sockets=['DATA'], start_port=free_port,
+                             instance_args=[['--mode', 'rgba']]) as bl:
+        dl = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=4, max_items=8, device=dev,
+                          decode=ops.DecodeConfig.unit())
+        sl = ScatterLoader(dl, 4, (3, 480, 640), torch.float32, dev, 2)
+        out = [b for b in sl]
+        assert len(out) == 2 and out[0]['image'].shape == (4, 3, 480, 640) and out[1]['btid'].shape == (4,)
