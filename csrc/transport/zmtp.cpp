@@ -222,7 +222,7 @@ struct Pipe : std::enable_shared_from_this<Pipe> {
   bool outbound = false;   // created by connect()
   Endpoint ep;
   SockAddr addr;
-  State state = IDLE;
+  std::atomic<State> state{IDLE};   // written by the IO thread, read by senders
   bool attached = false;   // member of Socket::pipes_ (mu_)
   bool gone = false;       // permanently finished (mu_)
   uint64_t id = 0;
@@ -331,7 +331,7 @@ void Context::term() {
   epfd_ = evfd_ = -1;
 }
 
-bool Context::on_io_thread() const { return std::this_thread::get_id() == thread_id_; }
+bool Context::on_io_thread() const { return std::this_thread::get_id() == thread_id_.load(std::memory_order_acquire); }
 
 void Context::wake() {
   uint64_t one = 1;
@@ -362,7 +362,7 @@ void Context::post_sync(std::function<void()> fn) {
 }
 
 void Context::loop() {
-  thread_id_ = std::this_thread::get_id();
+  thread_id_.store(std::this_thread::get_id(), std::memory_order_release);
   std::vector<epoll_event> evs(256);
   while (running_) {
     int timeout = 1000;

@@ -262,7 +262,7 @@ class Context {
   int epfd_ = -1;
   int evfd_ = -1;
   std::thread thread_;
-  std::thread::id thread_id_;
+  std::atomic<std::thread::id> thread_id_{};
   std::atomic<bool> running_{false};
 
   std::mutex cmd_mu_;
