@@ -442,7 +442,7 @@ Writer::Writer(int protocol) : protocol_(protocol) {
   op(uint8_t(protocol));
 }
 
-Writer::Writer(int protocol, std::vector<uint8_t>&& storage) : protocol_(protocol), out_(std::move(storage)) {
+Writer::Writer(int protocol, Bytes&& storage) : protocol_(protocol), out_(std::move(storage)) {
   if (protocol < 3 || protocol > 5) throw Unsupported("writer protocol must be 3..5");
   out_.clear();
   op(PROTO);
@@ -599,7 +599,7 @@ size_t Writer::ndarray(const std::string& code, const std::vector<int64_t>& shap
   return payload;
 }
 
-std::vector<uint8_t>& Writer::finish() {
+Bytes& Writer::finish() {
   op(STOP);
   return out_;
 }

@@ -24,6 +24,28 @@
 namespace btn {
 namespace codec {
 
+// Allocator whose value-construction is a no-op: resizing a byte buffer that
+// is about to be overwritten (pixel payloads) skips the memset.
+template <class T>
+struct default_init_allocator : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = default_init_allocator<U>;
+  };
+  default_init_allocator() = default;
+  template <class U>
+  default_init_allocator(const default_init_allocator<U>&) noexcept {}
+  template <class U>
+  void construct(U* p) noexcept {
+    ::new (static_cast<void*>(p)) U;
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+  }
+};
+using Bytes = std::vector<uint8_t, default_init_allocator<uint8_t>>;
+
 class Unsupported : public std::runtime_error {
  public:
   using std::runtime_error::runtime_error;
@@ -72,7 +94,7 @@ class Writer {
   explicit Writer(int protocol = 4);
   // Reuse `storage`'s capacity (cleared first) -- producers recycle frame
   // buffers instead of allocating ~1 MB per message.
-  Writer(int protocol, std::vector<uint8_t>&& storage);
+  Writer(int protocol, Bytes&& storage);
   // Dict building (keys are str).  Values written in call order.
   void begin_dict();
   void key(const std::string& k);
@@ -92,8 +114,8 @@ class Writer {
   // writes `nbytes` at out.data() + offset (after finish()).
   size_t ndarray(const std::string& dtype, const std::vector<int64_t>& shape,
                  const void* data = nullptr);
-  std::vector<uint8_t>& finish();
-  std::vector<uint8_t>& buffer() { return out_; }
+  Bytes& finish();
+  Bytes& buffer() { return out_; }
 
  private:
   void op(uint8_t c) { out_.push_back(c); }
@@ -103,7 +125,7 @@ class Writer {
   void short_str(const std::string& s);
   void global(const std::string& mod, const std::string& name);
   int protocol_;
-  std::vector<uint8_t> out_;
+  Bytes out_;
   std::vector<size_t> marks_;
 };
 

@@ -210,7 +210,7 @@ void write_value(codec::Writer& w, const codec::Value& v, const uint8_t* base) {
   }
 }
 
-std::vector<uint8_t> encode(const Ctx& c, double prev_action_value) {
+codec::Bytes encode(const Ctx& c, double prev_action_value) {
   codec::Writer w(4);
   w.begin_dict();
   w.key("prev_action");

@@ -125,16 +125,16 @@ Args parse(int argc, char** argv) {
 // thread has written it, so steady state allocates nothing.
 struct FramePool {
   std::mutex mu;
-  std::vector<std::vector<uint8_t>*> free;
-  std::vector<uint8_t> take() {
+  std::vector<codec::Bytes*> free;
+  codec::Bytes take() {
     std::lock_guard<std::mutex> lk(mu);
     if (free.empty()) return {};
-    std::vector<uint8_t> v(std::move(*free.back()));
+    codec::Bytes v(std::move(*free.back()));
     delete free.back();
     free.pop_back();
     return v;
   }
-  void give(std::vector<uint8_t>* v) {
+  void give(codec::Bytes* v) {
     std::lock_guard<std::mutex> lk(mu);
     if (free.size() < 64) free.push_back(v);
     else delete v;
@@ -142,13 +142,13 @@ struct FramePool {
 };
 FramePool g_pool;
 
-zmtp::Frame frame_from_vector(std::vector<uint8_t>&& v) {
-  auto* owned = new std::vector<uint8_t>(std::move(v));
+zmtp::Frame frame_from_vector(codec::Bytes&& v) {
+  auto* owned = new codec::Bytes(std::move(v));
   auto b = std::make_shared<Buffer>();
   b->data = owned->data();
   b->capacity = owned->size();
   b->owner = owned;
-  b->release = [](void* o, Buffer*) { g_pool.give(static_cast<std::vector<uint8_t>*>(o)); };
+  b->release = [](void* o, Buffer*) { g_pool.give(static_cast<codec::Bytes*>(o)); };
   zmtp::Frame f;
   f.size = owned->size();
   f.buf = std::move(b);

@@ -1,8 +1,9 @@
 // Headless CPU renderer (see raster.h).  The static background (ground plane
 // lit by the point light, world colour) is shaded once per Renderer; each
-// frame copies it, stamps the boxes' shadow hulls (2-D point-in-polygon on
-// cached ground hit points) and rasterises the boxes' front faces with
-// per-pixel Lambert shading and a depth buffer.
+// frame copies it, span-fills the boxes' projected shadow hulls and scan-
+// converts the boxes' front faces (two triangles each) with Gouraud-
+// interpolated point-light Lambert shading and, for several boxes, a
+// perspective-correct 1/z buffer.  ~0.3-0.4 ms per 640x480 frame.
 #include "raster.h"
 
 #include <algorithm>
@@ -216,82 +217,97 @@ inline void Renderer::put(uint8_t* out, int x, int y, float r, float g, float b)
   p[2] = T(b);
 }
 
+namespace {
+
+// Scan conversion of a convex polygon in pixel coordinates: calls
+// span(y, x0, x1) for every row segment of pixel centres inside (top-left
+// style half-open rule on y, [xl, xr) on x).
+template <class F>
+void scan_convex(const double* px, const double* py, int n, int W, int H, F&& span) {
+  double ymin = py[0], ymax = py[0];
+  for (int i = 1; i < n; ++i) ymin = std::min(ymin, py[i]), ymax = std::max(ymax, py[i]);
+  const int y0 = std::max(0, int(std::ceil(ymin - 0.5))), y1 = std::min(H - 1, int(std::ceil(ymax - 0.5)) - 1);
+  for (int y = y0; y <= y1; ++y) {
+    const double yc = y + 0.5;
+    double xl = 1e300, xr = -1e300;
+    for (int i = 0; i < n; ++i) {
+      const int j = (i + 1) % n;
+      const double ya = py[i], yb = py[j];
+      if ((ya <= yc && yc < yb) || (yb <= yc && yc < ya)) {
+        const double x = px[i] + (yc - ya) * (px[j] - px[i]) / (yb - ya);
+        xl = std::min(xl, x), xr = std::max(xr, x);
+      }
+    }
+    if (xl > xr) continue;
+    const int x0 = std::max(0, int(std::ceil(xl - 0.5))), x1 = std::min(W - 1, int(std::ceil(xr - 0.5)) - 1);
+    if (x0 <= x1) span(y, x0, x1);
+  }
+}
+
+// Affine screen-space plane v(x, y) = a x + b y + c through three samples.
+struct Plane2 {
+  double a = 0, b = 0, c = 0;
+  bool fit(const double* x, const double* y, const double* v) {
+    const double d = (x[1] - x[0]) * (y[2] - y[0]) - (x[2] - x[0]) * (y[1] - y[0]);
+    if (std::fabs(d) < 1e-12) return false;
+    a = ((v[1] - v[0]) * (y[2] - y[0]) - (v[2] - v[0]) * (y[1] - y[0])) / d;
+    b = ((x[1] - x[0]) * (v[2] - v[0]) - (x[2] - x[0]) * (v[1] - v[0])) / d;
+    c = v[0] - a * x[0] - b * y[0];
+    return true;
+  }
+};
+
+}  // namespace
+
 void Renderer::render(const Scene& s, uint8_t* out) {
   const Camera& cam = s.cam;
-  const int W = W_, H = H_;
-  const double f = cam.focal_px();
+  const int W = W_, H = H_, C = C_;
   const Vec3 o = cam.loc;
-  const Vec3 X{cam.rot[0], cam.rot[3], cam.rot[6]};
-  const Vec3 Y{cam.rot[1], cam.rot[4], cam.rot[7]};
-  const Vec3 Z{cam.rot[2], cam.rot[5], cam.rot[8]};
   const double ls = light_scale(s.light);
   const Vec3 L = s.light.loc;
   const double amb = s.ambient;
+  const ToneLut& T = tone();
 
   std::memcpy(out, background_.data(), background_.size());
+  auto row_ptr = [&](int y) { return out + size_t(lower_left_ ? (H - 1 - y) : y) * W * C; };
 
-  // ---- shadows: light-space projection of each box onto the plane ----
+  // ---- shadows: each box's shadow hull on the ground plane, projected to
+  // the image (a projective map keeps it convex) and span-filled ----
   for (const Box& b : s.boxes) {
     auto cs = b.corners();
     P2 pts[8], hull[17];
     bool above = true;
     for (int i = 0; i < 8; ++i) {
       if (cs[i].z >= L.z - 1e-9) above = false;
-      double t = (s.plane_z - L.z) / (cs[i].z - L.z);
+      const double t = (s.plane_z - L.z) / (cs[i].z - L.z);
       pts[i][0] = L.x + t * (cs[i].x - L.x);
       pts[i][1] = L.y + t * (cs[i].y - L.y);
     }
     if (!above) continue;   // light inside/below the box: no ground shadow
     const int nh = convex_hull(pts, 8, hull);
     if (nh < 3) continue;
-    int x0 = W, y0 = H, x1 = -1, y1 = -1;
-    bool full = false;
-    for (int i = 0; i < nh; ++i) {
-      double px, py;
-      if (!cam.project(Vec3{hull[i][0], hull[i][1], s.plane_z}, &px, &py)) {
-        full = true;
-        break;
-      }
-      x0 = std::min(x0, int(std::floor(px)) - 1);
-      y0 = std::min(y0, int(std::floor(py)) - 1);
-      x1 = std::max(x1, int(std::ceil(px)) + 1);
-      y1 = std::max(y1, int(std::ceil(py)) + 1);
-    }
-    if (full) {
-      x0 = 0, y0 = 0, x1 = W - 1, y1 = H - 1;
-    }
-    x0 = std::max(x0, 0), y0 = std::max(y0, 0), x1 = std::min(x1, W - 1), y1 = std::min(y1, H - 1);
-    // edge equations a*x + b*y + c >= 0 inside (CCW hull)
-    float ea[17], eb[17], ec[17];
-    for (int i = 0; i < nh; ++i) {
-      const P2& p0 = hull[i];
-      const P2& p1 = hull[(i + 1) % nh];
-      ea[i] = float(-(p1[1] - p0[1]));
-      eb[i] = float(p1[0] - p0[0]);
-      ec[i] = float(-(ea[i] * p0[0] + eb[i] * p0[1]));
-    }
-    for (int y = y0; y <= y1; ++y) {
-      const float* pxy = &plane_xy_[(size_t(y) * W) * 2];
-      const int row = lower_left_ ? (H - 1 - y) : y;
-      uint8_t* orow = out + size_t(row) * W * C_;
+    double hx[17], hy[17];
+    bool visible = true;
+    for (int i = 0; i < nh && visible; ++i)
+      visible = cam.project(Vec3{hull[i][0], hull[i][1], s.plane_z}, &hx[i], &hy[i]);
+    if (!visible) continue;
+    scan_convex(hx, hy, nh, W, H, [&](int y, int x0, int x1) {
+      const float* pxy = &plane_xy_[size_t(y) * W * 2];
+      uint8_t* r = row_ptr(y);
       for (int x = x0; x <= x1; ++x) {
-        const float hx = pxy[2 * x], hy = pxy[2 * x + 1];
-        if (hx != hx) continue;
-        bool in = true;
-        for (int i = 0; i < nh; ++i) in &= ea[i] * hx + eb[i] * hy + ec[i] >= 0.f;
-        if (in) {
-          uint8_t* p = orow + size_t(x) * C_;
-          p[0] = shadow_rgb_[0];
-          p[1] = shadow_rgb_[1];
-          p[2] = shadow_rgb_[2];
-        }
+        if (pxy[2 * x] != pxy[2 * x]) continue;   // not on the ground plane
+        uint8_t* p = r + size_t(x) * C;
+        p[0] = shadow_rgb_[0];
+        p[1] = shadow_rgb_[1];
+        p[2] = shadow_rgb_[2];
       }
-    }
+    });
   }
 
-  // ---- boxes: front faces, per-pixel Lambert, depth tested ----
+  // ---- boxes: front faces as two triangles each, Gouraud-interpolated
+  // point-light Lambert, perspective-correct depth test for several boxes ----
   const bool need_depth = s.boxes.size() > 1;
-  if (need_depth) depth_.assign(size_t(W) * H, std::numeric_limits<float>::infinity());
+  if (need_depth) depth_.assign(size_t(W) * H, 0.f);   // stores 1/depth; 0 = far
   for (size_t bi = 0; bi < s.boxes.size(); ++bi) {
     const Box& b = s.boxes[bi];
     const double hv[3] = {b.half.x, b.half.y, b.half.z};
@@ -309,72 +325,51 @@ void Renderer::render(const Scene& s, uint8_t* out) {
         const Vec3 wj = mul(b.rot, ej), wk = mul(b.rot, ek);
         const Vec3 q[4] = {add(fc, add(wj, wk)), add(fc, sub(wk, wj)), sub(fc, add(wj, wk)),
                            add(fc, sub(wj, wk))};
-        double px[4], py[4];
+        double px[4], py[4], dep[4], inten[4], invd[4];
         bool vis = true;
-        for (int i = 0; i < 4; ++i) vis &= cam.project(q[i], &px[i], &py[i]);
-        if (!vis) continue;
-        double area = 0;
         for (int i = 0; i < 4; ++i) {
-          int i1 = (i + 1) & 3;
-          area += px[i] * py[i1] - px[i1] * py[i];
-        }
-        if (std::fabs(area) < 1e-9) continue;
-        const float sg = area > 0 ? 1.f : -1.f;
-        // edge functions, sign-normalised so inside is >= 0
-        float ea[4], eb[4], ec[4];
-        for (int i = 0; i < 4; ++i) {
-          int i1 = (i + 1) & 3;
-          ea[i] = sg * float(-(py[i1] - py[i]));
-          eb[i] = sg * float(px[i1] - px[i]);
-          ec[i] = -(ea[i] * float(px[i]) + eb[i] * float(py[i]));
-        }
-        int x0 = std::max(0, int(std::floor(*std::min_element(px, px + 4))));
-        int x1 = std::min(W - 1, int(std::ceil(*std::max_element(px, px + 4))));
-        int y0 = std::max(0, int(std::floor(*std::min_element(py, py + 4))));
-        int y1 = std::min(H - 1, int(std::ceil(*std::max_element(py, py + 4))));
-        // per pixel: P = o + t d, t = nd0 / (n.d); light vector l = L - P
-        const float nd0 = float(dot(n, sub(fc, o)));
-        const float nX = float(dot(n, X)), nY = float(dot(n, Y)), nZ = float(dot(n, Z));
-        const float a0 = b.albedo[0], a1 = b.albedo[1], a2 = b.albedo[2];
-        const float lsf = float(ls), ambf = float(amb);
-        const Vec3 Lo = sub(L, o);
-        const float nLo = float(dot(n, Lo));
-        for (int y = y0; y <= y1; ++y) {
-          const float pyc = y + 0.5f;
-          const float cy = -(pyc - 0.5f * H) / float(f);
-          for (int x = x0; x <= x1; ++x) {
-            const float pxc = x + 0.5f;
-            if (ea[0] * pxc + eb[0] * pyc + ec[0] < 0.f || ea[1] * pxc + eb[1] * pyc + ec[1] < 0.f ||
-                ea[2] * pxc + eb[2] * pyc + ec[2] < 0.f || ea[3] * pxc + eb[3] * pyc + ec[3] < 0.f)
-              continue;
-            const float cx = (pxc - 0.5f * W) / float(f);
-            const float dn = cx * nX + cy * nY - nZ;
-            if (dn >= 0.f) continue;
-            const float t = nd0 / dn;
-            if (need_depth) {
-              float& zb = depth_[size_t(y) * W + x];
-              if (t >= zb) continue;
-              zb = t;
-            }
-            const float dx = float(cx * X.x + cy * Y.x - Z.x), dy = float(cx * X.y + cy * Y.y - Z.y),
-                        dz = float(cx * X.z + cy * Y.z - Z.z);
-            const float lx = float(Lo.x) - t * dx, ly = float(Lo.y) - t * dy, lz = float(Lo.z) - t * dz;
-            const float d2 = lx * lx + ly * ly + lz * lz;
-            const float nl_ = nLo - t * dn;   // n . (L - P)
-            float e = nl_ > 0.f ? lsf * nl_ / (d2 * std::sqrt(d2)) : 0.f;
-            if (e > 0.f && s.boxes.size() > 1) {
-              const Vec3 P{o.x + t * dx, o.y + t * dy, o.z + t * dz};
-              const Vec3 l{lx, ly, lz};
-              for (size_t oi = 0; oi < s.boxes.size(); ++oi) {
-                if (oi != bi && ray_hits_box(s.boxes[oi], P, l, 1e-6, 1.0)) {
-                  e = 0.f;
-                  break;
-                }
+          vis &= cam.project(q[i], &px[i], &py[i], &dep[i]);
+          invd[i] = dep[i] > 0 ? 1.0 / dep[i] : 0.0;
+          const Vec3 l = sub(L, q[i]);
+          const double d2 = dot(l, l);
+          double e = ls * std::max(0.0, dot(n, l) / std::sqrt(d2)) / d2;
+          if (e > 0 && s.boxes.size() > 1)
+            for (size_t oi = 0; oi < s.boxes.size(); ++oi)
+              if (oi != bi && ray_hits_box(s.boxes[oi], q[i], l, 1e-6, 1.0)) {
+                e = 0;
+                break;
               }
+          inten[i] = amb + e;
+        }
+        if (!vis) continue;
+        const float a0 = b.albedo[0] * 4096.f, a1 = b.albedo[1] * 4096.f, a2 = b.albedo[2] * 4096.f;
+        static const int tri[2][3] = {{0, 1, 2}, {0, 2, 3}};
+        for (const auto& t : tri) {
+          const double tx[3] = {px[t[0]], px[t[1]], px[t[2]]}, ty[3] = {py[t[0]], py[t[1]], py[t[2]]};
+          const double ti[3] = {inten[t[0]], inten[t[1]], inten[t[2]]};
+          const double tz[3] = {invd[t[0]], invd[t[1]], invd[t[2]]};
+          Plane2 ip, zp;
+          if (!ip.fit(tx, ty, ti) || !zp.fit(tx, ty, tz)) continue;
+          scan_convex(tx, ty, 3, W, H, [&](int y, int x0, int x1) {
+            uint8_t* r = row_ptr(y);
+            const double yc = y + 0.5;
+            float I = float(ip.a * (x0 + 0.5) + ip.b * yc + ip.c);
+            const float dI = float(ip.a);
+            float Z = float(zp.a * (x0 + 0.5) + zp.b * yc + zp.c);
+            const float dZ = float(zp.a);
+            float* zrow = need_depth ? &depth_[size_t(y) * W] : nullptr;
+            for (int x = x0; x <= x1; ++x, I += dI, Z += dZ) {
+              if (zrow) {
+                if (Z <= zrow[x]) continue;
+                zrow[x] = Z;
+              }
+              uint8_t* p = r + size_t(x) * C;
+              const float i0 = a0 * I, i1 = a1 * I, i2 = a2 * I;
+              p[0] = T.v[i0 >= 4096.f ? 4096 : (i0 > 0.f ? int(i0) : 0)];
+              p[1] = T.v[i1 >= 4096.f ? 4096 : (i1 > 0.f ? int(i1) : 0)];
+              p[2] = T.v[i2 >= 4096.f ? 4096 : (i2 > 0.f ? int(i2) : 0)];
             }
-            const float kk = ambf + e;
-            put(out, x, y, a0 * kk, a1 * kk, a2 * kk);
-          }
+          });
         }
       }
     }

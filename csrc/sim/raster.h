@@ -80,8 +80,8 @@ Scene falling_cubes_scene();
 // Frame renderer.  Camera, light and ground plane are static for the life of
 // a Renderer, so their shading (the whole background) is computed once and
 // cached together with each pixel's ground-plane hit point; a frame then costs
-// one background copy, a 2-D point-in-polygon pass over the image-space bounds
-// of the boxes' shadow hulls, and the boxes' front faces.
+// one background copy, span fills of the boxes' projected shadow hulls and
+// scan conversion of the boxes' front faces.
 // Output: H*W*channels bytes, row-major HWC uint8, channels 3 or 4 (alpha =
 // 255); `lower_left` stores row 0 = bottom image row (OpenGL readback order).
 class Renderer {

@@ -144,7 +144,7 @@ int main(int argc, char** argv) {
   std::deque<Work> pending;      // a new message replaces the current work
   std::vector<float> verts;
   std::vector<int> tris;
-  std::vector<uint8_t> storage;
+  codec::Bytes storage;
 
   while (!g_stop) {
     // pre_frame: duplex.recv(timeoutms=0)
