@@ -52,27 +52,44 @@ def ensure_built():
 
 
 def cpu_budget():
-    """CPUs usable by this process: affinity mask, capped by a cgroup quota."""
+    """(cpus, pin): CPUs usable by this process and whether pinning producers
+    to them isolates anything.  With a cgroup CPU quota far below the
+    affinity mask (a shared host), the quota is the budget and pinning would
+    only pile producers onto cores other tenants also use."""
     cpus = sorted(os.sched_getaffinity(0))
+    pin = True
     try:
         quota, period = Path('/sys/fs/cgroup/cpu.max').read_text().split()[:2]
         if quota != 'max':
             n = max(1, int(int(quota) / int(period)))
-            cpus = cpus[:n] if n < len(cpus) else cpus
+            if n < len(cpus):
+                pin = n * 2 > len(cpus)
+                cpus = cpus[:n]
     except (OSError, ValueError):
         pass
-    return cpus
+    return cpus, pin
+
+
+def cgroup_cpu_stat():
+    """cgroup v2 cpu.stat counters (usage/throttling) -- producer-bound runs
+    are CPU-quota sensitive, so report them next to the throughput."""
+    try:
+        kv = dict(line.split() for line in Path('/sys/fs/cgroup/cpu.stat').read_text().splitlines())
+        return {k: int(v) for k, v in kv.items()}
+    except (OSError, ValueError):
+        return {}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=int(os.environ.get('WORLD_SIZE', '1')))
-    ap.add_argument('--steps', type=int, default=1000)
+    ap.add_argument('--steps', type=int, default=2000)
     ap.add_argument('--warmup', type=int, default=50)
     ap.add_argument('--batch', type=int, default=8)
     ap.add_argument('--producers', type=int, default=0, help='producer processes per GPU (0 = auto)')
     ap.add_argument('--mode', choices=['rgba', 'rgb'], default='rgba')
-    ap.add_argument('--proto', choices=['tcp', 'ipc'], default='tcp')
+    ap.add_argument('--proto', choices=['tcp', 'ipc'], default='ipc',
+                    help='ipc (Unix-domain ZMTP, same-host producers; default) or tcp')
     ap.add_argument('--consumer', choices=['none', 'disc'], default='none')
     ap.add_argument('--io-threads', type=int, default=0)
     ap.add_argument('--start-port', type=int, default=0)
@@ -99,7 +116,7 @@ def main():
         dist.init_process_group('nccl', device_id=device)
 
     # partition this node's CPUs between the local ranks; producers are pinned
-    cpus = cpu_budget()
+    cpus, pin = cpu_budget()
     share = max(1, len(cpus) // local_world)
     mine = cpus[local_rank * share:(local_rank + 1) * share] or cpus
     nprod = args.producers or max(1, min(12, len(mine) - 3))
@@ -107,7 +124,7 @@ def main():
         # the root hosts every producer, pinned across the whole node
         mine = cpus
         nprod = nprod * world if rank == 0 else 0
-    affinity = [[mine[i % len(mine)]] for i in range(nprod)]
+    affinity = [[mine[i % len(mine)]] for i in range(nprod)] if pin else None
     start_port = args.start_port or (20000 + (os.getpid() % 200) * 50 if world == 1 else 21000 + rank * 64)
 
     decode = DecodeConfig.unit(channels='rgb', gamma=2.2)
@@ -155,6 +172,8 @@ def main():
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
+        cg0 = cgroup_cpu_stat()
+        ru0 = os.times()
         t0 = time.perf_counter()
         for _ in range(args.steps):
             img = step()
@@ -162,6 +181,12 @@ def main():
         if world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t0
+        ru1 = os.times()
+        cg1 = cgroup_cpu_stat()
+        cpu = {'consumer_cpu_s': round((ru1.user - ru0.user) + (ru1.system - ru0.system), 3)}
+        for k in ('usage_usec', 'throttled_usec', 'nr_throttled'):
+            if k in cg0 and k in cg1:
+                cpu['cgroup_' + k] = cg1[k] - cg0[k]
         shape = tuple(img.shape)
         try:
             next(it)
@@ -199,10 +224,12 @@ def main():
                 'decode': 'rgba->rgb, gamma 2.2, /255, HWC->CHW fp32 (gfx950 kernel)',
                 'out_shape': list(shape),
                 'proto': args.proto,
+                'pinned_producers': pin,
             },
             'sec_per_image': round(tmax / images, 7),
             'sec_per_batch': round(tmax / args.steps, 6),
             'loader_stats': {k: stats.get(k) for k in ('frames', 'batches', 'bad', 'pool_fallbacks')},
+            'cpu': cpu,
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()

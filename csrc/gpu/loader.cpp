@@ -70,7 +70,9 @@ BufPtr PinnedPool::alloc(size_t n) {
   }
   int id;
   {
-    std::lock_guard<std::mutex> lk(mu_);
+    std::unique_lock<std::mutex> lk(mu_);
+    if (free_.empty() && wait_ms_ > 0)
+      cv_.wait_for(lk, std::chrono::milliseconds(wait_ms_), [&] { return !free_.empty(); });
     if (free_.empty()) {
       fallbacks_++;
       return nullptr;
@@ -90,8 +92,11 @@ BufPtr PinnedPool::alloc(size_t n) {
 
 void PinnedPool::release(void* owner, Buffer* b) {
   auto* self = static_cast<PinnedPool*>(owner);
-  std::lock_guard<std::mutex> lk(self->mu_);
-  self->free_.push_back(int(b->tag));
+  {
+    std::lock_guard<std::mutex> lk(self->mu_);
+    self->free_.push_back(int(b->tag));
+  }
+  self->cv_.notify_one();
 }
 
 // ---------------------------------------------------------------------------
@@ -184,7 +189,8 @@ void StreamLoader::stop() {
   ctxs_.clear();   // joins IO threads; queued frames are released
   DeviceGuard g(cfg_.device);
   if (stream_) {
-    (void)hipStreamSynchronize(stream_);   // pending host callbacks drop pinned refs
+    (void)hipStreamSynchronize(stream_);
+    reap(true);                            // drop pinned refs of finished copies
     (void)hipStreamDestroy(stream_);
     stream_ = nullptr;
   }
@@ -221,6 +227,7 @@ void StreamLoader::run() {
   const int64_t max_frames = cfg_.max_batches < 0 ? -1 : cfg_.max_batches * cfg_.batch_size;
   int64_t taken = 0;
   while (!stop_) {
+    reap();
     if (max_frames >= 0 && taken >= max_frames) break;
     std::vector<int> ev;
     try {
@@ -300,7 +307,14 @@ bool StreamLoader::process(zmtp::Message&& msg) {
     size_t slot = cfg_.max_frame_bytes ? cfg_.max_frame_bytes : size_t(double(n) * 1.05) + 4096;
     slot = (slot + 4095) & ~size_t(4095);
     int nslots = cfg_.pool_slots;
-    if (nslots <= 0) nslots = int(cfg_.addresses.size()) * (cfg_.rcvhwm + 2) + (cfg_.staging_depth + 4) * cfg_.batch_size;
+    if (nslots <= 0) {
+      // every pipe may hold RCVHWM queued + 1 partial frame; the worker holds
+      // the batch being assembled plus the batches whose copies are in flight
+      nslots = int(cfg_.addresses.size()) * (cfg_.rcvhwm + 2) + (cfg_.staging_depth + 12) * cfg_.batch_size;
+      nslots = std::max(64, nslots + nslots / 2);
+      const size_t cap = size_t(4) << 30;   // <= 4 GiB pinned
+      if (size_t(nslots) * slot > cap) nslots = int(std::max<size_t>(16, cap / slot));
+    }
     pool_ = std::make_shared<PinnedPool>(slot, nslots);
     for (auto& s : socks_) s->set_allocator(pool_, 64 * 1024);
     for (int k = 0; k < std::max(2, cfg_.staging_depth); ++k) {
@@ -347,17 +361,29 @@ bool StreamLoader::process(zmtp::Message&& msg) {
   return true;
 }
 
-void StreamLoader::on_copied(void* user) {
-  // runs on a HIP runtime thread once the H2D copies of a batch completed:
-  // dropping the frames returns their pinned slots to the pool
-  delete static_cast<std::vector<zmtp::Frame>*>(user);
+void StreamLoader::reap(bool wait_all) {
+  // drop the frames of batches whose H2D copies completed: their pinned
+  // slots return to the pool (and unblock an IO thread waiting for one)
+  while (!inflight_.empty()) {
+    Inflight& f = inflight_.front();
+    hipError_t q = wait_all ? hipEventSynchronize(f.copied) : hipEventQuery(f.copied);
+    if (q == hipErrorNotReady) break;
+    (void)hipEventDestroy(f.copied);
+    inflight_.pop_front();
+  }
 }
 
 void StreamLoader::launch() {
   Posted p{nullptr, nullptr};
   {
     std::unique_lock<std::mutex> lk(mu_);
-    while (posted_.empty() && !stop_) cv_.wait_for(lk, std::chrono::milliseconds(100));
+    while (posted_.empty() && !stop_) {
+      lk.unlock();
+      reap();
+      lk.lock();
+      if (!posted_.empty() || stop_) break;
+      cv_.wait_for(lk, std::chrono::milliseconds(2));
+    }
     if (stop_) return;
     p = posted_.front();
     posted_.pop_front();
@@ -375,6 +401,9 @@ void StreamLoader::launch() {
           "hipMemcpyAsync(H2D)");
     if (it.flip && i < 256) flips[i >> 6] |= uint64_t(1) << (i & 63);
   }
+  hipEvent_t copied;
+  check(hipEventCreateWithFlags(&copied, hipEventDisableTiming), "hipEventCreate(copied)");
+  check(hipEventRecord(copied, stream_), "hipEventRecord(copied)");
   bool any_flip_beyond = false;
   for (int i = 256; i < B; ++i) any_flip_beyond |= cur_[size_t(i)].flip;
   if (any_flip_beyond) throw std::runtime_error("StreamLoader: per-image flip supports batch <= 256");
@@ -404,17 +433,18 @@ void StreamLoader::launch() {
     e = decode(dp, stream_);
   }
   check(e, "decode kernel launch");
-  auto* held = new std::vector<zmtp::Frame>();
-  held->reserve(size_t(B));
+  Inflight fl;
+  fl.frames.reserve(size_t(B));
   ReadyBatch rb;
   rb.index = batch_index_;
   rb.items.reserve(size_t(B));
   for (auto& it : cur_) {
-    held->push_back(std::move(it.frame));
+    fl.frames.push_back(std::move(it.frame));
     rb.items.push_back(std::move(it.meta));
   }
   cur_.clear();
-  check(hipLaunchHostFunc(stream_, &StreamLoader::on_copied, held), "hipLaunchHostFunc");
+  fl.copied = copied;
+  inflight_.push_back(std::move(fl));
   check(hipEventCreateWithFlags(&rb.done, hipEventDisableTiming), "hipEventCreate(done)");
   check(hipEventRecord(rb.done, stream_), "hipEventRecord(done)");
   rb.recv_ms = t_issue - batch_t0_;

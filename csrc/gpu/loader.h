@@ -13,8 +13,9 @@
 //     -> B items assembled into batch j; hipMemcpyAsync of every image into
 //        the device staging ring on a private non-blocking HIP stream
 //     -> fused decode kernel (flip/gamma/unpack/normalize/CHW) writes into
-//        the consumer-posted output buffer; host callback recycles the pinned
-//        slots once the DMA has landed; hipEvent marks the batch ready
+//        the consumer-posted output buffer; an event after the copies lets
+//        the worker recycle the pinned slots once the DMA has landed (no host
+//        callback in the stream); hipEvent marks the batch ready
 //     -> consumer (Python) takes batch j; its torch stream waits on the event.
 //
 // Backpressure is preserved end to end: when the consumer stops posting
@@ -50,7 +51,10 @@ class PinnedPool : public Allocator, public std::enable_shared_from_this<PinnedP
  public:
   PinnedPool(size_t slot_bytes, int nslots);
   ~PinnedPool() override;
-  BufPtr alloc(size_t n) override;   // nullptr (heap fallback) if n too big or pool dry
+  // Blocks up to `wait_ms` for a free slot (backpressure on the IO thread),
+  // then returns nullptr (heap fallback) if the pool is still dry.
+  BufPtr alloc(size_t n) override;
+  void set_wait_ms(int ms) { wait_ms_ = ms; }
   size_t slot_bytes() const { return slot_bytes_; }
   int nslots() const { return nslots_; }
   int free_slots();
@@ -62,8 +66,10 @@ class PinnedPool : public Allocator, public std::enable_shared_from_this<PinnedP
   int nslots_;
   uint8_t* base_ = nullptr;
   std::mutex mu_;
+  std::condition_variable cv_;
   std::vector<int> free_;
   std::atomic<uint64_t> fallbacks_{0};
+  int wait_ms_ = 50;
 };
 
 struct LoaderConfig {
@@ -141,7 +147,7 @@ class StreamLoader {
   void run();
   bool process(zmtp::Message&& msg);
   void launch();
-  static void on_copied(void* user);
+  void reap(bool wait_all = false);   // release pinned slots of completed H2D copies
 
   LoaderConfig cfg_;
   std::vector<std::unique_ptr<zmtp::Context>> ctxs_;
@@ -166,6 +172,11 @@ class StreamLoader {
   float* d_lut_ = nullptr;
   float* d_mat_ = nullptr;   // 16 matrix + 4 bias
   std::vector<Item> cur_;
+  struct Inflight {
+    hipEvent_t copied;
+    std::vector<zmtp::Frame> frames;
+  };
+  std::deque<Inflight> inflight_;   // H2D copies not yet known complete
   int64_t batch_index_ = 0;
   double batch_t0_ = 0;
   LoaderStats stats_;
