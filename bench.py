@@ -92,6 +92,8 @@ def main():
                     help='ipc (Unix-domain ZMTP, same-host producers; default) or tcp')
     ap.add_argument('--consumer', choices=['none', 'disc'], default='none')
     ap.add_argument('--io-threads', type=int, default=0)
+    ap.add_argument('--shm', type=int, default=0,
+                    help='>0: producers render into an N-slot shared-memory ring (same host) and send descriptors')
     ap.add_argument('--start-port', type=int, default=0)
     ap.add_argument('--dist', choices=['shard', 'scatter'], default='shard',
                     help='shard: every rank owns its producers; scatter: rank 0 receives world*B per step '
@@ -130,7 +132,8 @@ def main():
     decode = DecodeConfig.unit(channels='rgb', gamma=2.2)
     launch = dict(producer='cubesim', num_instances=nprod, named_sockets=['DATA'], start_port=start_port,
                   proto=args.proto, seed=1000 * rank, cpu_affinity=affinity,
-                  instance_args=[['--mode', args.mode, '--sndhwm', '10']] * nprod)
+                  instance_args=[['--mode', args.mode, '--sndhwm', '10'] + (['--shm', str(args.shm)] if args.shm else [])]
+                  * nprod)
     model = opt = None
     if args.consumer == 'disc':
         from blendtorch.models import Discriminator
@@ -225,6 +228,7 @@ def main():
                 'out_shape': list(shape),
                 'proto': args.proto,
                 'pinned_producers': pin,
+                'shm_slots': args.shm,
             },
             'sec_per_image': round(tmax / images, 7),
             'sec_per_batch': round(tmax / args.steps, 6),

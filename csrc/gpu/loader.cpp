@@ -194,7 +194,11 @@ void StreamLoader::stop() {
     (void)hipStreamDestroy(stream_);
     stream_ = nullptr;
   }
+  for (auto& it : cur_)
+    if (it.seg) it.seg->release(it.slot, it.gen);
   cur_.clear();
+  for (auto& kv : segments_) (void)hipHostUnregister(kv.second->base());
+  segments_.clear();
   {
     std::lock_guard<std::mutex> lk(mu_);
     for (auto& p : posted_) (void)hipEventDestroy(p.ready);
@@ -279,20 +283,46 @@ bool StreamLoader::process(zmtp::Message&& msg) {
     return bad(std::string("unparseable pickle (") + e.what() + ")");
   }
   if (!root || root->kind != codec::Value::DICT) return bad("payload is not a dict");
-  size_t img_idx = size_t(-1);
-  for (size_t i = 0; i + 1 < root->items.size(); i += 2)
-    if (root->items[i]->kind == codec::Value::STR && root->items[i]->s == cfg_.image_key) img_idx = i;
-  if (img_idx == size_t(-1)) return bad("no '" + cfg_.image_key + "' entry");
-  const codec::Value& img = *root->items[img_idx + 1];
-  if (img.kind != codec::Value::NDARRAY || img.dtype != "|u1" || img.fortran)
-    return bad("image must be a C-contiguous uint8 ndarray");
+  size_t img_idx = size_t(-1), shm_idx = size_t(-1);
+  for (size_t i = 0; i + 1 < root->items.size(); i += 2) {
+    if (root->items[i]->kind != codec::Value::STR) continue;
+    if (root->items[i]->s == cfg_.image_key) img_idx = i;
+    else if (root->items[i]->s == "_btshm") shm_idx = i;
+  }
   int h, w, c;
-  if (img.shape.size() == 3) {
-    h = int(img.shape[0]), w = int(img.shape[1]), c = int(img.shape[2]);
-  } else if (img.shape.size() == 2) {
-    h = int(img.shape[0]), w = int(img.shape[1]), c = 1;
+  size_t cut = 0, len = 0;
+  if (shm_idx != size_t(-1)) {
+    // descriptor (segment, slot, byte offset, H, W, C, key): image in shared memory
+    const codec::Value& d = *root->items[shm_idx + 1];
+    if (d.kind != codec::Value::TUPLE || d.items.size() < 8 || d.items[0]->kind != codec::Value::STR)
+      return bad("malformed _btshm descriptor");
+    try {
+      it.seg = segment(d.items[0]->s);
+    } catch (const std::exception& e) {
+      return bad(e.what());
+    }
+    it.slot = uint32_t(d.items[1]->i);
+    it.gen = uint32_t(d.items[7]->i);
+    const int64_t off = d.items[2]->i;
+    h = int(d.items[3]->i), w = int(d.items[4]->i), c = int(d.items[5]->i);
+    if (it.slot >= it.seg->nslots() || off < 0 || size_t(off) + size_t(h) * w * c > it.seg->size())
+      return bad("_btshm descriptor out of range");
+    it.src = it.seg->base() + off;
+    root->items.erase(root->items.begin() + long(shm_idx), root->items.begin() + long(shm_idx) + 2);
   } else {
-    return bad("image must be HxW or HxWxC");
+    if (img_idx == size_t(-1)) return bad("no '" + cfg_.image_key + "' entry");
+    const codec::Value& img = *root->items[img_idx + 1];
+    if (img.kind != codec::Value::NDARRAY || img.dtype != "|u1" || img.fortran)
+      return bad("image must be a C-contiguous uint8 ndarray");
+    if (img.shape.size() == 3) {
+      h = int(img.shape[0]), w = int(img.shape[1]), c = int(img.shape[2]);
+    } else if (img.shape.size() == 2) {
+      h = int(img.shape[0]), w = int(img.shape[1]), c = 1;
+    } else {
+      return bad("image must be HxW or HxWxC");
+    }
+    it.src = data + img.off;
+    cut = img.off, len = img.len;
   }
   if (c < 1 || c > 4) return bad("image channels must be 1..4");
   if (const codec::Value* o = root->get("origin"))
@@ -337,17 +367,21 @@ bool StreamLoader::process(zmtp::Message&& msg) {
     }
     cv_.notify_all();
   } else if (h != H_ || w != W_ || c != C_) {
+    if (it.seg) it.seg->release(it.slot, it.gen);
     return bad("image shape changed within the stream");
   }
-  it.img_off = img.off;
-
   // metadata: the frame minus the image payload, tree re-based onto it
-  const size_t cut = img.off, len = img.len;
   it.meta.bytes.reserve(n - len);
   it.meta.bytes.insert(it.meta.bytes.end(), data, data + cut);
   it.meta.bytes.insert(it.meta.bytes.end(), data + cut + len, data + n);
-  root->items.erase(root->items.begin() + long(img_idx), root->items.begin() + long(img_idx) + 2);
-  shift_offsets(*root, cut, len);
+  if (len) {
+    for (size_t i = 0; i + 1 < root->items.size(); i += 2)
+      if (root->items[i]->kind == codec::Value::STR && root->items[i]->s == cfg_.image_key) {
+        root->items.erase(root->items.begin() + long(i), root->items.begin() + long(i) + 2);
+        break;
+      }
+    shift_offsets(*root, cut, len);
+  }
   it.meta.tree = root;
 
   if (cur_.empty()) batch_t0_ = now_ms();
@@ -355,10 +389,22 @@ bool StreamLoader::process(zmtp::Message&& msg) {
     std::lock_guard<std::mutex> lk(mu_);
     stats_.frames++;
     stats_.bytes += n;
+    if (it.seg) stats_.shm_frames++;
   }
   cur_.push_back(std::move(it));
   if (int(cur_.size()) == cfg_.batch_size) launch();
   return true;
+}
+
+shm::Segment* StreamLoader::segment(const std::string& name) {
+  auto it = segments_.find(name);
+  if (it != segments_.end()) return it->second.get();
+  std::unique_ptr<shm::Segment> seg(shm::Segment::open(name));
+  // pin the producer's ring so the DMA engine reads the slots in place
+  check(hipHostRegister(seg->base(), seg->size(), hipHostRegisterDefault), "hipHostRegister(shm)");
+  auto* raw = seg.get();
+  segments_[name] = std::move(seg);
+  return raw;
 }
 
 void StreamLoader::reap(bool wait_all) {
@@ -369,6 +415,13 @@ void StreamLoader::reap(bool wait_all) {
     hipError_t q = wait_all ? hipEventSynchronize(f.copied) : hipEventQuery(f.copied);
     if (q == hipErrorNotReady) break;
     (void)hipEventDestroy(f.copied);
+    for (auto& s : f.slots) {
+      if (!s.seg->valid(s.slot, s.gen)) {   // reclaimed by the producer under the DMA
+        std::lock_guard<std::mutex> lk(mu_);
+        stats_.shm_torn++;
+      }
+      s.seg->release(s.slot, s.gen);
+    }
     inflight_.pop_front();
   }
 }
@@ -396,7 +449,7 @@ void StreamLoader::launch() {
   uint64_t flips[4] = {0, 0, 0, 0};
   for (int i = 0; i < B; ++i) {
     const Item& it = cur_[size_t(i)];
-    check(hipMemcpyAsync(stage + size_t(i) * img_bytes_, it.frame.data() + it.img_off, img_bytes_,
+    check(hipMemcpyAsync(stage + size_t(i) * img_bytes_, it.src, img_bytes_,
                          hipMemcpyHostToDevice, stream_),
           "hipMemcpyAsync(H2D)");
     if (it.flip && i < 256) flips[i >> 6] |= uint64_t(1) << (i & 63);
@@ -440,6 +493,7 @@ void StreamLoader::launch() {
   rb.items.reserve(size_t(B));
   for (auto& it : cur_) {
     fl.frames.push_back(std::move(it.frame));
+    if (it.seg) fl.slots.push_back({it.seg, it.slot, it.gen});
     rb.items.push_back(std::move(it.meta));
   }
   cur_.clear();

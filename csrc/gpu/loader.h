@@ -30,6 +30,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -38,6 +39,7 @@
 
 #include "../codec/pickle_codec.h"
 #include "../common/buffer.h"
+#include "../transport/shmring.h"
 #include "../transport/zmtp.h"
 #include "kernels.h"
 
@@ -111,6 +113,7 @@ struct ReadyBatch {
 
 struct LoaderStats {
   uint64_t frames = 0, batches = 0, bytes = 0, bad = 0, pool_fallbacks = 0;
+  uint64_t shm_frames = 0, shm_torn = 0;   // via shared memory / slot reclaimed during the copy
   double h2d_issue_ms = 0;
 };
 
@@ -136,7 +139,9 @@ class StreamLoader {
  private:
   struct Item {
     zmtp::Frame frame;
-    size_t img_off = 0;
+    const uint8_t* src = nullptr;      // image bytes: in the frame or in a shm slot
+    shm::Segment* seg = nullptr;       // shared-memory slot to hand back, if any
+    uint32_t slot = 0, gen = 0;
     bool flip = false;
     BatchMeta meta;
   };
@@ -175,7 +180,14 @@ class StreamLoader {
   struct Inflight {
     hipEvent_t copied;
     std::vector<zmtp::Frame> frames;
+    struct Slot {
+      shm::Segment* seg;
+      uint32_t slot, gen;
+    };
+    std::vector<Slot> slots;
   };
+  shm::Segment* segment(const std::string& name);
+  std::map<std::string, std::unique_ptr<shm::Segment>> segments_;   // mapped + hipHostRegister'ed
   std::deque<Inflight> inflight_;   // H2D copies not yet known complete
   int64_t batch_index_ = 0;
   double batch_t0_ = 0;

@@ -184,6 +184,8 @@ PYBIND11_MODULE(_hip, m) {
         d["bad"] = s.bad;
         d["pool_fallbacks"] = s.pool_fallbacks;
         d["h2d_issue_ms"] = s.h2d_issue_ms;
+        d["shm_frames"] = s.shm_frames;
+        d["shm_torn"] = s.shm_torn;
         return d;
       });
 }

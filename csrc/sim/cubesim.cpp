@@ -11,6 +11,7 @@
 // upper-left|lower-left   --frame-range A B   --frames N (-1 = forever)
 // --sndhwm N   --linger MS   --fps F (0 = unthrottled)   --socket NAME
 // --fault none|exit|stall|garbage --fault-after N   --rotation RX RY RZ   --verbose
+// --shm N (render into an N-slot shared-memory ring, send descriptors only)
 //
 // Every frame it publishes, on a bound PUSH socket with SNDHWM/LINGER/
 // IMMEDIATE as btb.DataPublisher does (reference: btb/publisher.py:21-43),
@@ -25,6 +26,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <unistd.h>
 #include <map>
 #include <mutex>
 #include <random>
@@ -33,6 +36,7 @@
 #include <vector>
 
 #include "../codec/pickle_codec.h"
+#include "../transport/shmring.h"
 #include "../transport/zmtp.h"
 #include "raster.h"
 
@@ -59,6 +63,7 @@ struct Args {
   std::string fault = "none";
   long long fault_after = -1;
   bool verbose = false;
+  int shm_slots = 0;        // >0: images go through a shared-memory ring
   bool fixed_rotation = false;
   double rot[3] = {0, 0, 0};
 };
@@ -108,6 +113,7 @@ Args parse(int argc, char** argv) {
     else if (k == "--fault") a.fault = need(i), ++i;
     else if (k == "--fault-after") a.fault_after = std::stoll(need(i)), ++i;
     else if (k == "--verbose") a.verbose = true;
+    else if (k == "--shm") a.shm_slots = std::stoi(need(i)), ++i;
     else if (k == "--rotation") {
       if (i + 3 >= v.size()) usage("--rotation needs rx ry rz");
       for (int r = 0; r < 3; ++r) a.rot[r] = std::stod(v[i + 1 + r]);
@@ -182,6 +188,11 @@ int main(int argc, char** argv) {
   const zmtp::Socket::Interrupt intr = [] { return g_stop.load(); };
   const bool lower_left = a.origin == "lower-left";
   sim::Renderer renderer(scene, C, lower_left);
+  std::unique_ptr<shm::Segment> seg;
+  if (a.shm_slots > 0) {
+    const std::string name = "blendtorch-" + std::to_string(::getpid()) + "-" + std::to_string(a.btid);
+    seg.reset(shm::Segment::create(name, uint32_t(a.shm_slots), size_t(W) * H * C));
+  }
   const auto t_start = std::chrono::steady_clock::now();
   auto next_due = t_start;
   long long published = 0;
@@ -202,12 +213,21 @@ int main(int argc, char** argv) {
       scene.boxes[0].rot = sim::euler_xyz(pi * U(rng), pi * U(rng), pi * U(rng));
     }
 
+    int slot = -1;
+    if (seg) {
+      slot = seg->acquire(-1, &g_stop);   // blocks while every slot is with a consumer
+      if (slot < 0) break;
+    }
+    uint32_t gen = 0;
     codec::Writer w(4, g_pool.take());
     w.begin_dict();
     w.key("btid");
     w.integer(a.btid);
-    w.key("image");
-    size_t img_off = w.ndarray("u1", {H, W, C});
+    size_t img_off = 0;
+    if (!seg) {
+      w.key("image");
+      img_off = w.ndarray("u1", {H, W, C});
+    }
     w.key("xy");
     std::vector<double> xy;
     for (auto& b : scene.boxes)
@@ -224,11 +244,28 @@ int main(int argc, char** argv) {
       w.key("origin");
       w.str("lower-left");
     }
+    if (seg) {
+      // descriptor: (segment, slot, byte offset, H, W, C, image key, generation)
+      gen = ((seg->state(uint32_t(slot)) >> 2) + 1) & 0x3fffffffu;   // publish() will bump to this
+      w.key("_btshm");
+      w.begin_tuple();
+      w.str(seg->name());
+      w.integer(slot);
+      w.integer(int64_t(seg->slot_offset(uint32_t(slot))));
+      w.integer(H);
+      w.integer(W);
+      w.integer(C);
+      w.str("image");
+      w.integer(gen);
+      w.end_tuple();
+    }
     w.end_dict();
     auto& buf = w.finish();
+    uint8_t* pixels = seg ? seg->slot(uint32_t(slot)) : buf.data() + img_off;
 
     auto r0 = std::chrono::steady_clock::now();
-    renderer.render(scene, buf.data() + img_off);
+    renderer.render(scene, pixels);
+    if (seg) seg->publish(uint32_t(slot));   // == gen
     render_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - r0).count();
 
     if (a.fault != "none" && a.fault_after >= 0 && published == a.fault_after) {
@@ -245,6 +282,7 @@ int main(int argc, char** argv) {
         } catch (const zmtp::Error&) {
           break;
         }
+        if (seg) seg->release(uint32_t(slot), seg->publish(uint32_t(slot)));
         ++published;
         continue;
       }

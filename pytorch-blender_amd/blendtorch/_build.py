@@ -32,7 +32,7 @@ ROCM = Path(os.environ.get('ROCM_PATH', '/opt/rocm'))
 
 CXXFLAGS = ['-std=c++17', '-O3', '-fPIC', '-Wall', '-Wno-unused-parameter', '-pthread']
 
-TRANSPORT = ['transport/zmtp.cpp']
+TRANSPORT = ['transport/zmtp.cpp', 'transport/shmring.cpp']
 CODEC = ['codec/pickle_codec.cpp']
 RASTER = ['sim/raster.cpp']
 
@@ -110,7 +110,7 @@ def build_native(verbose=False, jobs=8):
         exe = BIN / s.stem
         deps = core + [o]
         if _newer(exe, deps):
-            _run([cxx, '-pthread', '-O3', *deps, '-o', exe], verbose)
+            _run([cxx, '-pthread', '-O3', *deps, '-o', exe, '-lrt'], verbose)
     return target
 
 

@@ -6,13 +6,22 @@ while no consumer is connected or all consumer queues are full, and no
 message is ever dropped.  Every message is the dict
 ``{'btid': btid, **kwargs}``, pickled.
 """
-from ..transport import zmq
+import os
+
+import numpy as np
+
+from ..transport import shm, zmq
 
 
 class DataPublisher:
-    """Publish rendered images and auxiliary data to ``btt`` datasets."""
+    """Publish rendered images and auxiliary data to ``btt`` datasets.
 
-    def __init__(self, bind_address, btid=None, send_hwm=10, lingerms=0):
+    ``shm_slots > 0`` (same-host consumers only): u8 ndarrays under
+    ``shm_key`` travel through an N-slot shared-memory ring and the message
+    carries a small descriptor instead of the pixels.
+    """
+
+    def __init__(self, bind_address, btid=None, send_hwm=10, lingerms=0, shm_slots=0, shm_key='image'):
         self.ctx = zmq.Context()
         self.sock = self.ctx.socket(zmq.PUSH)
         self.sock.setsockopt(zmq.SNDHWM, send_hwm)
@@ -20,10 +29,23 @@ class DataPublisher:
         self.sock.setsockopt(zmq.IMMEDIATE, 1)
         self.sock.bind(bind_address)
         self.btid = btid
+        self.shm_slots = shm_slots
+        self.shm_key = shm_key
+        self._ring = None
 
     def publish(self, **kwargs):
         """Send ``{'btid': btid, **kwargs}`` (values must be picklable)."""
+        img = kwargs.get(self.shm_key) if self.shm_slots else None
+        if isinstance(img, np.ndarray) and img.dtype == np.uint8:
+            if self._ring is None:
+                self._ring = shm.ShmRing(f'blendtorch-{os.getpid()}-{self.btid}', self.shm_slots, img.nbytes)
+            slot, off, h, w, c, gen = self._ring.put(img)
+            kwargs = {k: v for k, v in kwargs.items() if k != self.shm_key}
+            kwargs[shm.KEY] = (self._ring.name, slot, off, h, w, c, self.shm_key, gen)
         self.sock.send_pyobj({'btid': self.btid, **kwargs})
 
     def close(self):
         self.sock.close()
+        if self._ring is not None:
+            self._ring.close()
+            self._ring = None

@@ -12,7 +12,9 @@ Reference: pkg_pytorch/blendtorch/btt/dataset.py:14-153.
 * :class:`SingleFileDataset` / :class:`FileDataset` -- map-style replay of
   one / all recordings matching a prefix (shuffle-capable).
 
-Frames are decoded with the native zero-copy unpickler (image arrays are
+Same-host producers may send images through shared memory (descriptor key
+``_btshm``); they are materialised transparently.  Frames are decoded with
+the native zero-copy unpickler (image arrays are
 views over the received buffer); for device-resident batches see
 :class:`blendtorch.btt.gpu.DeviceLoader`.
 """
@@ -22,7 +24,7 @@ from glob import glob
 
 import torch.utils.data as tud
 
-from ..transport import zmq
+from ..transport import shm, zmq
 from .constants import DEFAULT_TIMEOUTMS
 from .file import FileReader, FileRecorder
 
@@ -83,14 +85,26 @@ class RemoteIterableDataset(tud.IterableDataset):
                     assert socket in ready, 'No response within timeout interval.'
                     if rec is not None:
                         data = socket.recv()
-                        rec.save(data, is_pickled=True)
                         obj = pickle.loads(data)
+                        if shm.KEY in obj:   # record the materialised frame
+                            obj = shm.resolve(obj)
+                            rec.save(obj, is_pickled=False)
+                        else:
+                            rec.save(data, is_pickled=True)
                     else:
-                        obj = socket.recv_pyobj()
+                        obj = shm.resolve(socket.recv_pyobj())
                     yield self._item(obj)
                     del obj
         finally:
             if socket is not None:
+                # hand back shared-memory slots of frames still queued here
+                try:
+                    while socket.poll(0):
+                        obj = socket.recv_pyobj()
+                        if isinstance(obj, dict) and shm.KEY in obj:
+                            shm.release(obj[shm.KEY])
+                except Exception:
+                    pass
                 socket.close()
 
     def _item(self, item):

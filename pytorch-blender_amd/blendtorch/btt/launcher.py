@@ -245,6 +245,9 @@ class BlenderLauncher:
                     pass
                 p.wait()
         assert all(c is not None for c in self._poll()), 'Not all Blender instances closed.'
+        from ..transport.shm import cleanup_pid
+        for p in procs:   # shared-memory rings of killed producers
+            cleanup_pid(p.pid)
         self.launch_info = None
         logger.info('Blender instances closed')
 

@@ -1,0 +1,193 @@
+"""Python side of the same-host shared-memory frame slots (csrc/transport/shmring.h).
+
+Producers on the consumer's host may place image payloads in a POSIX
+shared-memory ring and send only a descriptor ``'_btshm': (segment, slot,
+byte_offset, H, W, C, key)`` in the message dict.  The GPU loader DMAs the
+slot in place; CPU consumers call :func:`resolve`, which copies the image into
+the dict under ``key`` and hands the slot back.  :class:`ShmRing` is the
+producer side for Python publishers (``btb.DataPublisher(shm_slots=N)``).
+
+Segment layout (shared with C++): header {u64 magic, u32 version, u32 nslots,
+u64 slot_bytes, u64 data_offset}, u32 word per slot (generation << 2 |
+state; states 0 free, 1 writing, 2 published), slots at data_offset (4 KiB
+aligned).  Descriptors carry the generation: a consumer copies, checks that
+the word still reads (gen, published) -- i.e. the producer did not reclaim the
+slot under it -- and hands the slot back.
+"""
+from __future__ import annotations
+
+import mmap
+import os
+import struct
+import time
+
+import numpy as np
+
+MAGIC = 0x6d68735f7462746e
+_HDR = struct.Struct('<QIIQQ')
+FREE, WRITING, PUBLISHED = 0, 1, 2
+KEY = '_btshm'
+
+_views = {}
+_views_pid = None
+
+
+def _path(name):
+    return '/dev/shm/' + name.lstrip('/')
+
+
+class _Segment:
+    def __init__(self, name, fd, mm, owner):
+        self.name = name
+        self.fd = fd
+        self.mm = mm
+        self.owner = owner
+        magic, version, nslots, slot_bytes, data_offset = _HDR.unpack_from(mm, 0)
+        if magic != MAGIC and not owner:
+            raise ValueError(f'{name} is not a blendtorch shm segment')
+        self.nslots, self.slot_bytes, self.data_offset = nslots, slot_bytes, data_offset
+        self.states = np.frombuffer(mm, dtype=np.uint32, count=nslots, offset=_HDR.size)
+
+    def slot_array(self, i, shape, dtype=np.uint8):
+        off = self.data_offset + i * self.slot_bytes
+        return np.frombuffer(self.mm, dtype=dtype, count=int(np.prod(shape)), offset=off).reshape(shape)
+
+    def close(self):
+        self.states = None
+        try:
+            self.mm.close()
+        except BufferError:  # numpy views still alive; the mapping dies with them
+            pass
+        os.close(self.fd)
+        if self.owner:
+            try:
+                os.unlink(_path(self.name))
+            except FileNotFoundError:
+                pass
+
+
+def _open(name):
+    global _views, _views_pid
+    if _views_pid != os.getpid():   # fresh cache after fork
+        _views, _views_pid = {}, os.getpid()
+    seg = _views.get(name)
+    if seg is None:
+        fd = os.open(_path(name), os.O_RDWR)
+        size = os.fstat(fd).st_size
+        seg = _Segment(name, fd, mmap.mmap(fd, size, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE), False)
+        _views[name] = seg
+    return seg
+
+
+class TornFrame(RuntimeError):
+    """The producer reclaimed the slot while it was being read."""
+
+
+def _word(gen, state):
+    return ((int(gen) & 0x3fffffff) << 2) | state
+
+
+def release(desc):
+    """Hand a descriptor's slot back without reading it (dropped messages)."""
+    name, slot, off, h, w, c, key, gen = desc
+    seg = _open(name)
+    if int(seg.states[slot]) == _word(gen, PUBLISHED):
+        seg.states[slot] = _word(gen, FREE)
+
+
+def resolve(obj):
+    """Materialise a shared-memory image into ``obj`` (in place) and free its slot."""
+    if not isinstance(obj, dict) or KEY not in obj:
+        return obj
+    desc = obj.pop(KEY)
+    name, slot, off, h, w, c, key, gen = desc
+    seg = _open(name)
+    published = _word(gen, PUBLISHED)
+    if int(seg.states[slot]) != published:
+        raise TornFrame(f'shm slot {name}:{slot} was reclaimed before it was read')
+    n = h * w * c
+    img = np.frombuffer(seg.mm, dtype=np.uint8, count=n, offset=off).reshape((h, w, c) if c > 1 else (h, w)).copy()
+    if int(seg.states[slot]) != published:
+        raise TornFrame(f'shm slot {name}:{slot} was reclaimed while it was read')
+    seg.states[slot] = _word(gen, FREE)
+    obj[key] = img
+    return obj
+
+
+class ShmRing:
+    """Producer-side ring (single writer).  ``acquire`` blocks while every slot
+    is still with a consumer -- the same backpressure as a full SNDHWM."""
+
+    def __init__(self, name, nslots, slot_bytes):
+        slot_bytes = (slot_bytes + 4095) // 4096 * 4096
+        data_offset = (_HDR.size + 4 * nslots + 4095) // 4096 * 4096
+        size = data_offset + nslots * slot_bytes
+        fd = os.open(_path(name), os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
+        os.ftruncate(fd, size)
+        mm = mmap.mmap(fd, size, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+        _HDR.pack_into(mm, 0, 0, 1, nslots, slot_bytes, data_offset)
+        self.seg = _Segment(name, fd, mm, True)
+        self.seg.states[:] = FREE
+        _HDR.pack_into(mm, 0, MAGIC, 1, nslots, slot_bytes, data_offset)
+        self._next = 0
+        self._published_at = {}
+        self.reclaimed = 0
+
+    @property
+    def name(self):
+        return self.seg.name
+
+    def acquire(self, timeout_s=None, lease_s=2.0):
+        t0 = time.time()
+        n = self.seg.nslots
+        while True:
+            for k in range(n):
+                i = (self._next + k) % n
+                w = int(self.seg.states[i])
+                if w & 3 == FREE:
+                    self.seg.states[i] = (w & ~3) | WRITING
+                    self._next = (i + 1) % n
+                    return i
+            waited = time.time() - t0
+            if timeout_s is not None and waited > timeout_s:
+                raise TimeoutError('no free shared-memory slot')
+            if lease_s is not None and waited > lease_s:
+                pub = [i for i in range(n) if int(self.seg.states[i]) & 3 == PUBLISHED]
+                if pub:   # reclaim the oldest published slot (its message was dropped)
+                    i = min(pub, key=lambda j: self._published_at.get(j, 0.0))
+                    self.seg.states[i] = (int(self.seg.states[i]) & ~3) | WRITING
+                    self.reclaimed += 1
+                    return i
+            time.sleep(0.0002)
+
+    def put(self, image):
+        """Copy ``image`` (u8 HxW[xC]) into a free slot; returns the descriptor
+        fields (slot, byte offset, H, W, C, generation)."""
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        if img.nbytes > self.seg.slot_bytes:
+            raise ValueError('image larger than the ring slot')
+        i = self.acquire()
+        h, w = img.shape[:2]
+        c = img.shape[2] if img.ndim == 3 else 1
+        self.seg.slot_array(i, img.shape)[...] = img
+        gen = ((int(self.seg.states[i]) >> 2) + 1) & 0x3fffffff
+        self._published_at[i] = time.time()
+        self.seg.states[i] = _word(gen, PUBLISHED)
+        return i, self.seg.data_offset + i * self.seg.slot_bytes, h, w, c, gen
+
+    def close(self):
+        self.seg.close()
+
+
+def cleanup_pid(pid):
+    """Remove segments a (dead) producer process left behind."""
+    prefix = f'blendtorch-{pid}-'
+    try:
+        for f in os.listdir('/dev/shm'):
+            if f.startswith(prefix):
+                try:
+                    os.unlink('/dev/shm/' + f)
+                except OSError:
+                    pass
+    except OSError:
+        pass

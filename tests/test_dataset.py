@@ -69,3 +69,36 @@ def test_item_transform_and_subclass(free_port):
         b = list(MyDS(bl.launch_info.addresses['DATA'], max_items=4))
     assert all(0 <= x <= 3 for x in a)
     assert all(x % 10 == 0 for x in b)
+
+
+@pytest.mark.background
+def test_dataset_shared_memory_producers(free_port):
+    """cubesim --shm: descriptors are resolved into images by the CPU dataset;
+    slots are handed back (more items than slots flow through)."""
+    args = dict(producer='cubesim', num_instances=2, named_sockets=['DATA'], start_port=free_port, proto='ipc',
+                instance_args=[['--mode', 'rgb', '--shm', '4', '--rotation', '0.1', '0.2', '0.3']] * 2)
+    with btt.BlenderLauncher(**args) as bl:
+        ds = btt.RemoteIterableDataset(bl.launch_info.addresses['DATA'], max_items=40)
+        items = list(tud.DataLoader(ds, batch_size=4, num_workers=2))
+    assert len(items) == 10
+    assert items[0]['image'].shape == (4, 480, 640, 3)
+    # fixed rotation: every frame identical
+    assert (items[0]['image'][0] == items[-1]['image'][-1]).all()
+
+
+def test_python_publisher_shared_memory(free_port):
+    from blendtorch.btb.publisher import DataPublisher
+    from blendtorch.transport import shm, zmq
+    pub = DataPublisher(f'tcp://127.0.0.1:{free_port}', btid=0, shm_slots=3)
+    ctx = zmq.Context()
+    pull = ctx.socket(zmq.PULL)
+    pull.connect(f'tcp://127.0.0.1:{free_port}')
+    for i in range(10):
+        img = np.full((8, 6, 3), i, np.uint8)
+        pub.publish(image=img, frameid=i)
+        msg = pull.recv_pyobj()
+        assert shm.KEY in msg and 'image' not in msg
+        msg = shm.resolve(msg)
+        assert (msg['image'] == i).all() and msg['frameid'] == i
+    pub.close()
+    pull.close()

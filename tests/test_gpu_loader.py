@@ -113,3 +113,24 @@ def test_scatter_loader_single_rank(dev, free_port):
         sl = ScatterLoader(dl, 4, (3, 480, 640), torch.float32, dev, 2)
         out = [b for b in sl]
         assert len(out) == 2 and out[0]['image'].shape == (4, 3, 480, 640) and out[1]['btid'].shape == (4,)
+
+
+@pytest.mark.parametrize('origin', ['upper-left', 'lower-left'])
+def test_device_loader_shared_memory_producer(dev, free_port, origin):
+    """Images through the shared-memory ring (descriptor messages) decode to
+    exactly what the inline-payload path gives for the same rendered frame."""
+    cfg = ops.DecodeConfig.densityopt(channels='rgb', gamma=2.2)
+    base = ['--mode', 'rgba', '--rotation', '0.4', '0.9', '1.7', '--origin', origin]
+    out = {}
+    for k, extra in (('inline', []), ('shm', ['--shm', '12'])):
+        with btt.BlenderLauncher(producer='cubesim', num_instances=2, named_sockets=['DATA'],
+                                 start_port=free_port + (10 if extra else 0), proto='ipc',
+                                 instance_args=[base + extra] * 2) as bl:
+            dl = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=8, max_items=96, decode=cfg, device=dev)
+            batches = list(dl)
+            assert dl.stats['frames'] == 96 and dl.stats['bad'] == 0
+            out[k] = batches[-1]['image']
+            assert 'xy' in batches[0] and batches[0]['xy'].shape == (8, 8, 2)
+    torch.testing.assert_close(out['shm'], out['inline'], rtol=0, atol=0)
+    import os
+    assert not [f for f in os.listdir('/dev/shm') if f.startswith('blendtorch-')]
