@@ -235,7 +235,9 @@ void StreamLoader::run() {
     if (max_frames >= 0 && taken >= max_frames) break;
     std::vector<int> ev;
     try {
-      ev = zmtp::Socket::poll(items, 100, intr);
+      // with copies in flight, wake up often enough to recycle their slots
+      // promptly (producers / IO threads may be waiting for them)
+      ev = zmtp::Socket::poll(items, inflight_.empty() ? 100 : 1, intr);
     } catch (const zmtp::Error& e) {
       if (e.code == zmtp::E_INTR) break;
       throw;

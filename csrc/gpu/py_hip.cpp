@@ -8,7 +8,10 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <chrono>
+#include <cstring>
 #include <stdexcept>
+#include <sys/mman.h>
 
 #include "../python/pyvalue.h"
 #include "kernels.h"
@@ -100,6 +103,47 @@ PYBIND11_MODULE(_hip, m) {
                         ptr<float>(out_px), ptr<float>(out_depth), stream_of(stream)),
                 "project");
         });
+
+  // Diagnostics: H2D bandwidth of one `nbytes` copy repeated `iters` times
+  // from host memory of the given kind ("hostmalloc", "register", "pageable").
+  m.def("bench_h2d", [](const std::string& kind, size_t nbytes, int iters, int chunks) {
+    py::gil_scoped_release nogil;
+    void* host = nullptr;
+    bool reg = false;
+    if (kind == "hostmalloc") {
+      check(hipHostMalloc(&host, nbytes * chunks, hipHostMallocDefault), "hipHostMalloc");
+    } else {
+      host = mmap(nullptr, nbytes * chunks, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
+      std::memset(host, 1, nbytes * chunks);
+      if (kind == "register") {
+        check(hipHostRegister(host, nbytes * chunks, hipHostRegisterDefault), "hipHostRegister");
+        reg = true;
+      }
+    }
+    void* dev = nullptr;
+    check(hipMalloc(&dev, nbytes * chunks), "hipMalloc");
+    hipStream_t s;
+    check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "stream");
+    auto run = [&] {
+      for (int c = 0; c < chunks; ++c)
+        check(hipMemcpyAsync(static_cast<char*>(dev) + c * nbytes, static_cast<char*>(host) + c * nbytes, nbytes,
+                             hipMemcpyHostToDevice, s), "memcpy");
+    };
+    run();
+    check(hipStreamSynchronize(s), "sync");
+    auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < iters; ++i) run();
+    check(hipStreamSynchronize(s), "sync");
+    double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    (void)hipStreamDestroy(s);
+    (void)hipFree(dev);
+    if (kind == "hostmalloc") (void)hipHostFree(host);
+    else {
+      if (reg) (void)hipHostUnregister(host);
+      munmap(host, nbytes * chunks);
+    }
+    return double(nbytes) * chunks * iters / sec / 1e9;   // GB/s
+  });
 
   py::class_<StreamLoader>(m, "StreamLoader")
       .def(py::init([](std::vector<std::string> addresses, int batch_size, std::string image_key, int rcvhwm,

@@ -29,6 +29,13 @@ for step in "$@"; do
     rl) timeout -k 10 200 python benchmarks/bench_rl.py --envs 8 --steps 5000 > gpurun_out/bench_rl.log 2>&1; rc=$?; tail -1 gpurun_out/bench_rl.log
         timeout -k 10 200 python benchmarks/bench_rl.py --envs 1 --steps 5000 >> gpurun_out/bench_rl.log 2>&1; rc=$?; tail -1 gpurun_out/bench_rl.log;;
     dopt) timeout -k 10 300 python examples/densityopt/densityopt.py --num-epochs 70 --json gpurun_out/densityopt.json > gpurun_out/densityopt.log 2>&1; rc=$?; tail -2 gpurun_out/densityopt.log;;
+    h2d) timeout -k 10 120 python -c "
+import sys; sys.path.insert(0,'pytorch-blender_amd')
+import torch; from blendtorch import ops; e=ops.hip_ext()
+for k in ('hostmalloc','register','pageable'):
+    for chunks in (1,8):
+        print(k, 'chunks', chunks, round(e.bench_h2d(k, 1228800, 200, chunks),2), 'GB/s', flush=True)
+" > gpurun_out/h2d.log 2>&1; rc=$?; cat gpurun_out/h2d.log;;
     *) echo "unknown step $step"; rc=2;;
   esac
   echo "== step $step rc=$rc"
