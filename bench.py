@@ -92,8 +92,9 @@ def main():
                     help='ipc (Unix-domain ZMTP, same-host producers; default) or tcp')
     ap.add_argument('--consumer', choices=['none', 'disc'], default='none')
     ap.add_argument('--io-threads', type=int, default=0)
-    ap.add_argument('--shm', type=int, default=0,
-                    help='>0: producers render into an N-slot shared-memory ring (same host) and send descriptors')
+    ap.add_argument('--shm', type=int, default=48,
+                    help='>0 (default 48): producers render into an N-slot shared-memory ring (same host) and '
+                         'send descriptors; 0: images inline in the ZMTP messages')
     ap.add_argument('--start-port', type=int, default=0)
     ap.add_argument('--dist', choices=['shard', 'scatter'], default='shard',
                     help='shard: every rank owns its producers; scatter: rank 0 receives world*B per step '

@@ -191,7 +191,12 @@ int main(int argc, char** argv) {
   std::unique_ptr<shm::Segment> seg;
   if (a.shm_slots > 0) {
     const std::string name = "blendtorch-" + std::to_string(::getpid()) + "-" + std::to_string(a.btid);
-    seg.reset(shm::Segment::create(name, uint32_t(a.shm_slots), size_t(W) * H * C));
+    try {
+      seg.reset(shm::Segment::create(name, uint32_t(a.shm_slots), size_t(W) * H * C));
+    } catch (const std::exception& e) {
+      // e.g. a small /dev/shm: fall back to inline payloads
+      std::fprintf(stderr, "cubesim[%d]: shared memory disabled (%s)\n", a.btid, e.what());
+    }
   }
   const auto t_start = std::chrono::steady_clock::now();
   auto next_due = t_start;

@@ -31,10 +31,12 @@ Segment* Segment::create(const std::string& name, uint32_t nslots, size_t slot_b
   slot_bytes = round_up(slot_bytes, 4096);
   const size_t data_off = round_up(sizeof(Header) + sizeof(uint32_t) * nslots, 4096);
   const size_t size = data_off + slot_bytes * nslots;
-  if (::ftruncate(fd, off_t(size)) != 0) {
+  // reserve the pages now: a too-small /dev/shm fails here with ENOSPC
+  // instead of SIGBUS on first touch later
+  if (::ftruncate(fd, off_t(size)) != 0 || ::posix_fallocate(fd, 0, off_t(size)) != 0) {
     ::close(fd);
     ::shm_unlink(path.c_str());
-    throw std::runtime_error("shm: ftruncate failed (is /dev/shm large enough?)");
+    throw std::runtime_error("shm: cannot reserve " + std::to_string(size >> 20) + " MiB in /dev/shm");
   }
   void* p = ::mmap(nullptr, size, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
   if (p == MAP_FAILED) {
