@@ -145,6 +145,38 @@ PYBIND11_MODULE(_hip, m) {
     return double(nbytes) * chunks * iters / sec / 1e9;   // GB/s
   });
 
+  // Kernel-only timing (no Python launch overhead): `iters` back-to-back
+  // decode launches between two HIP events; returns microseconds per launch.
+  m.def("bench_decode",
+        [](uintptr_t src, uintptr_t dst, uintptr_t lut, int B, int H, int W, int Cin, int Cout, std::vector<int> cmap,
+           int out_dtype, int layout, int iters) {
+          py::gil_scoped_release nogil;
+          DecodeParams p;
+          p.src = ptr<const uint8_t>(src);
+          p.dst = ptr<void>(dst);
+          p.lut = ptr<const float>(lut);
+          p.B = B, p.H = H, p.W = W, p.Cin = Cin, p.Cout = Cout;
+          fill_cmap(p.cmap, cmap);
+          p.out_dtype = out_dtype;
+          p.layout = layout;
+          hipStream_t s;
+          check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "stream");
+          hipEvent_t a, b;
+          check(hipEventCreate(&a), "event");
+          check(hipEventCreate(&b), "event");
+          for (int i = 0; i < 10; ++i) check(decode(p, s), "decode");
+          check(hipEventRecord(a, s), "record");
+          for (int i = 0; i < iters; ++i) check(decode(p, s), "decode");
+          check(hipEventRecord(b, s), "record");
+          check(hipEventSynchronize(b), "sync");
+          float ms = 0;
+          check(hipEventElapsedTime(&ms, a, b), "elapsed");
+          (void)hipEventDestroy(a);
+          (void)hipEventDestroy(b);
+          (void)hipStreamDestroy(s);
+          return double(ms) * 1000.0 / iters;
+        });
+
   py::class_<StreamLoader>(m, "StreamLoader")
       .def(py::init([](std::vector<std::string> addresses, int batch_size, std::string image_key, int rcvhwm,
                        int io_threads, int device, int64_t max_batches, size_t max_frame_bytes, int pool_slots,

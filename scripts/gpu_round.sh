@@ -29,6 +29,9 @@ for step in "$@"; do
     rl) timeout -k 10 200 python benchmarks/bench_rl.py --envs 8 --steps 5000 > gpurun_out/bench_rl.log 2>&1; rc=$?; tail -1 gpurun_out/bench_rl.log
         timeout -k 10 200 python benchmarks/bench_rl.py --envs 1 --steps 5000 >> gpurun_out/bench_rl.log 2>&1; rc=$?; tail -1 gpurun_out/bench_rl.log;;
     dopt) timeout -k 10 300 python examples/densityopt/densityopt.py --num-epochs 70 --json gpurun_out/densityopt.json > gpurun_out/densityopt.log 2>&1; rc=$?; tail -2 gpurun_out/densityopt.log;;
+    ksweep) for mg in ${KSWEEP_GRIDS:-1024 2048 4096 16384}; do for pm in ${KSWEEP_PPT:-1 2 4}; do
+            BT_DECODE_MAXGRID=$mg BT_DECODE_PPT_MULT=$pm timeout -k 10 120 python scripts/kernel_bench.py --only decode --tag "grid=$mg ppt_mult=$pm" >> gpurun_out/ksweep.log 2>&1 || { rc=$?; break 2; }
+          done; done; rc=${rc:-0}; grep -o "grid=.*speedup" gpurun_out/ksweep.log | sed "s/'torch_eager_us.*//" ;;
     h2d) timeout -k 10 120 python -c "
 import sys; sys.path.insert(0,'pytorch-blender_amd')
 import torch; from blendtorch import ops; e=ops.hip_ext()

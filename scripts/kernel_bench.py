@@ -34,6 +34,7 @@ def timeit(fn, iters=200, warmup=20):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--batch', type=int, default=8)
+    ap.add_argument('--tag', default='')
     ap.add_argument('--iters', type=int, default=200)
     ap.add_argument('--json', default=None)
     ap.add_argument('--only', default=None)
@@ -50,18 +51,23 @@ def main():
         'decode_rgba_u8_gamma': (x4, ops.DecodeConfig(channels='rgba', gamma=2.2, dtype='uint8'), 4, 4),
         'decode_rgba_rgb_f32_nhwc': (x4, ops.DecodeConfig.unit(channels='rgb', layout='nhwc'), 4, 12),
     }
+    ext = ops.hip_ext()
     for name, (x, cfg, inb, outb) in cases.items():
         if a.only and a.only not in name:
             continue
-        us = timeit(lambda: ops.decode(x, cfg), a.iters)
+        out = ops.decode(x, cfg)
+        lut = ops.device_lut(cfg, dev)
+        # kernel-only time (C++ launch loop between HIP events)
+        us = ext.bench_decode(x.data_ptr(), out.data_ptr(), lut.data_ptr(), B, H, W, x.shape[-1], cfg.cout,
+                              list(cfg.cmap), ops.OUT_DTYPES[cfg.dtype], ops.LAYOUTS[cfg.layout], a.iters)
         ref_us = timeit(lambda: ops.reference_decode(x, cfg), max(10, a.iters // 10), 3)
         nbytes = B * H * W * (inb + outb)
         res[name] = {'us': round(us, 2), 'GBps': round(nbytes / us / 1e3, 1), 'torch_eager_us': round(ref_us, 1),
                      'speedup_vs_eager': round(ref_us / us, 1)}
-        print(name, res[name], flush=True)
+        print(a.tag, name, res[name], flush=True)
     if not a.only or 'color' in a.only:
         M = np.random.default_rng(0).normal(size=(4, 4)).astype(np.float32)
-        us = timeit(lambda: ops.color4x4(x4, M, [0, 0, 0, 0], gamma=2.2), a.iters)
+        us = timeit(lambda: ops.color4x4(x4, M, [0, 0, 0, 0], gamma=2.2), a.iters)   # includes Python launch
         ref_us = timeit(lambda: ops.reference_color4x4(x4, M, [0, 0, 0, 0], gamma=2.2), 20, 3)
         nbytes = B * H * W * (4 + 16)
         res['color4x4_mfma_rgba_f32'] = {'us': round(us, 2), 'GBps': round(nbytes / us / 1e3, 1),
