@@ -33,12 +33,13 @@ def main():
     ap.add_argument('--device', default='cuda' if torch.cuda.is_available() else 'cpu')
     ap.add_argument('--start-port', type=int, default=24000)
     ap.add_argument('--render-every', type=int, default=0)
+    ap.add_argument('--python-client', action='store_true', help='use the pure-Python REQ clients')
     a = ap.parse_args()
     dev = torch.device(a.device)
     args = dict(producer='cartpolesim', num_instances=a.envs, named_sockets=['GYM'], start_port=a.start_port,
                 seed=7, instance_args=[['--render-every', str(a.render_every)]] * a.envs)
     with btt.BlenderLauncher(**args) as bl:
-        venv = VectorRemoteEnv(bl.launch_info.addresses['GYM'], device=dev)
+        venv = VectorRemoteEnv(bl.launch_info.addresses['GYM'], device=dev, native=not a.python_client)
         policy = CartpolePolicy().to(dev)
         obs, _ = venv.reset()
         episodes = 0
@@ -48,13 +49,11 @@ def main():
             act = policy(obs)
             obs, rew, done, infos = venv.step(act)
             if bool(done.any()):
-                # reset only the finished envs
-                for i in torch.nonzero(done).flatten().tolist():
-                    venv.envs[i]._send(cmd='reset')
-                    r = venv.envs[i]._recv()
-                    episodes += 1
-                    o = torch.tensor(r['obs'], dtype=torch.float32, device=obs.device)
-                    obs[i] = o
+                # reset only the finished envs (one concurrent round)
+                idx = torch.nonzero(done).flatten().tolist()
+                o, _ = venv.reset(which=idx)
+                obs[idx] = o.to(obs.device)
+                episodes += len(idx)
             return obs
 
         for _ in range(a.warmup):
@@ -71,6 +70,7 @@ def main():
     print(json.dumps({'metric': 'cartpole env steps/s (aggregate)', 'value': round(a.envs * a.steps / dt, 1),
                       'unit': 'steps/s', 'envs': a.envs, 'steps': a.steps, 'per_env_hz': round(a.steps / dt, 1),
                       'ms_per_step': round(dt / a.steps * 1e3, 4), 'device': str(dev), 'episodes': episodes,
+                      'client': 'python' if a.python_client else 'native',
                       'baseline': '2000 Hz (1 env, reference Readme.md:95)'}))
 
 

@@ -290,4 +290,132 @@ class NativeError(Exception):
           }
           return out;
         });
+
+  // ---- batched remote-env client (VectorRemoteEnv fast path) ----
+  // N REQ sockets (RELAXED + CORRELATE, like btt.env.RemoteEnv); step()
+  // fans the requests out before gathering any reply, all with the GIL
+  // released, and decodes numeric obs/reward/done/time straight into arrays.
+  struct VecReq {
+    std::vector<std::shared_ptr<Socket>> socks;
+    std::vector<int64_t> times;
+    std::vector<bool> has_time;
+    std::vector<std::vector<uint8_t>> last;   // raw last replies (for info dicts)
+  };
+  py::class_<VecReq, std::shared_ptr<VecReq>>(m, "VecReq")
+      .def(py::init([](const std::vector<std::string>& addresses, long timeoutms) {
+             auto v = std::make_shared<VecReq>();
+             for (auto& a : addresses) {
+               auto s = zmtp::Context::global().socket(zmtp::REQ);
+               s->setsockopt(zmtp::LINGER, 0);
+               s->setsockopt(zmtp::SNDTIMEO, timeoutms * 10);
+               s->setsockopt(zmtp::RCVTIMEO, timeoutms);
+               s->setsockopt(zmtp::REQ_RELAXED, 1);
+               s->setsockopt(zmtp::REQ_CORRELATE, 1);
+               s->connect(a);
+               v->socks.push_back(s);
+             }
+             v->times.assign(addresses.size(), 0);
+             v->has_time.assign(addresses.size(), false);
+             v->last.resize(addresses.size());
+             return v;
+           }),
+           py::arg("addresses"), py::arg("timeoutms") = 10000)
+      .def("__len__", [](VecReq& v) { return v.socks.size(); })
+      .def("exchange",
+           [](VecReq& v, const std::vector<int>& which, const std::string& cmd,
+              py::array_t<double, py::array::c_style | py::array::forcecast> actions, int obs_dim) {
+             const size_t n = which.size();
+             if (cmd == "step" && size_t(actions.size()) < n) throw py::value_error("one action per env");
+             std::vector<double> act(actions.data(), actions.data() + actions.size());
+             py::array_t<double> obs(std::vector<py::ssize_t>{py::ssize_t(n), py::ssize_t(obs_dim)});
+             py::array_t<double> rew(std::vector<py::ssize_t>{py::ssize_t(n)});
+             py::array_t<bool> done(std::vector<py::ssize_t>{py::ssize_t(n)});
+             double* po = obs.mutable_data();
+             double* pr = rew.mutable_data();
+             bool* pd = done.mutable_data();
+             std::string err;
+             {
+               py::gil_scoped_release nogil;
+               try {
+                 for (size_t k = 0; k < n; ++k) {
+                   const int i = which[k];
+                   codec::Writer w(4);
+                   w.begin_dict();
+                   w.key("cmd");
+                   w.str(cmd);
+                   if (cmd == "step") {
+                     w.key("action");
+                     w.real(act[k]);
+                   }
+                   w.key("time");
+                   if (v.has_time[size_t(i)]) w.integer(v.times[size_t(i)]);
+                   else w.none();
+                   w.end_dict();
+                   auto& b = w.finish();
+                   Message m;
+                   m.push_back(Frame::copy_of(b.data(), b.size()));
+                   v.socks[size_t(i)]->send(std::move(m));
+                 }
+                 for (size_t k = 0; k < n; ++k) {
+                   const int i = which[k];
+                   Message r = v.socks[size_t(i)]->recv();
+                   auto& raw = v.last[size_t(i)];
+                   raw.assign(r[0].data(), r[0].data() + r[0].size);
+                   auto root = codec::parse(raw.data(), raw.size());
+                   auto num = [&](const codec::Value* x, double dflt) {
+                     if (!x) return dflt;
+                     if (x->kind == codec::Value::FLOAT) return x->f;
+                     if (x->kind == codec::Value::INT) return double(x->i);
+                     if (x->kind == codec::Value::BOOL) return x->b ? 1.0 : 0.0;
+                     return dflt;
+                   };
+                   const codec::Value* o = root->get("obs");
+                   for (int d = 0; d < obs_dim; ++d) {
+                     double val = 0;
+                     if (o && (o->kind == codec::Value::TUPLE || o->kind == codec::Value::LIST) &&
+                         size_t(d) < o->items.size())
+                       val = num(o->items[size_t(d)].get(), 0.0);
+                     else if (o && o->kind == codec::Value::NDARRAY && d < o->numel()) {
+                       if (o->dtype == "<f8") std::memcpy(&val, raw.data() + o->off + 8 * size_t(d), 8);
+                       else if (o->dtype == "<f4") {
+                         float f;
+                         std::memcpy(&f, raw.data() + o->off + 4 * size_t(d), 4);
+                         val = f;
+                       }
+                     } else if (o && d == 0)
+                       val = num(o, 0.0);
+                     po[k * size_t(obs_dim) + size_t(d)] = val;
+                   }
+                   pr[k] = num(root->get("reward"), 0.0);
+                   const codec::Value* dn = root->get("done");
+                   pd[k] = dn && ((dn->kind == codec::Value::BOOL && dn->b) || (dn->kind == codec::Value::INT && dn->i));
+                   const codec::Value* t = root->get("time");
+                   if (t && t->kind == codec::Value::INT) {
+                     v.times[size_t(i)] = t->i;
+                     v.has_time[size_t(i)] = true;
+                   }
+                 }
+               } catch (const zmtp::Error& e) {
+                 err = e.code == zmtp::E_AGAIN ? "Failed to receive from remote environment" : e.what();
+               } catch (const std::exception& e) {
+                 err = e.what();
+               }
+             }
+             if (!err.empty()) throw py::value_error(err);
+             return py::make_tuple(obs, rew, done);
+           },
+           py::arg("which"), py::arg("cmd"), py::arg("actions"), py::arg("obs_dim"))
+      .def("last_reply", [](VecReq& v, int i) {
+        // full reply dict of env i (info, rgb_array, ...), decoded lazily
+        auto& raw = v.last[size_t(i)];
+        py::bytearray owner(reinterpret_cast<const char*>(raw.data()), raw.size());
+        const uint8_t* base = reinterpret_cast<const uint8_t*>(PyByteArray_AsString(owner.ptr()));
+        auto root = codec::parse(base, raw.size());
+        return value_to_py(*root, base, owner);
+      })
+      .def("close", [](VecReq& v) {
+        py::gil_scoped_release nogil;
+        for (auto& s : v.socks) s->close(0);
+        v.socks.clear();
+      });
 }

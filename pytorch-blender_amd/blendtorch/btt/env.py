@@ -202,18 +202,32 @@ class VectorRemoteEnv:
 
     ``step(actions)`` sends all N requests before waiting for any reply, so
     the remote simulations advance in parallel and one round trip costs
-    ~max(latency) instead of sum(latency).  Observations (numeric tuples /
-    arrays) are packed into a pinned host buffer and copied to ``device``
-    with one non-blocking transfer; rewards/dones come back as tensors too.
+    ~max(latency) instead of sum(latency).  The native client (C++, GIL
+    released, numeric obs/reward/done decoded straight into arrays) is used
+    for scalar actions and numeric observations of dimension ``obs_dim``;
+    otherwise a Python fallback over :class:`RemoteEnv` is used.  Observations
+    are packed into a pinned host buffer and copied to ``device`` with one
+    non-blocking transfer.  ``infos(i)`` returns env i's full last reply.
     """
 
-    def __init__(self, addresses, device=None, timeoutms=DEFAULT_TIMEOUTMS):
-        self.envs = [RemoteEnv(a, timeoutms=timeoutms) for a in addresses]
+    def __init__(self, addresses, device=None, timeoutms=DEFAULT_TIMEOUTMS, obs_dim=None, native=True):
+        self.addresses = list(addresses)
         self.device = device
+        self.obs_dim = obs_dim
         self._pinned = None
+        self._native = None
+        self.envs = None
+        if native:
+            try:
+                from .. import _native
+                self._native = _native.VecReq(self.addresses, timeoutms)
+            except (ImportError, AttributeError):
+                self._native = None
+        if self._native is None:
+            self.envs = [RemoteEnv(a, timeoutms=timeoutms) for a in self.addresses]
 
     def __len__(self):
-        return len(self.envs)
+        return len(self.addresses)
 
     def _stage(self, obs):
         import torch
@@ -225,25 +239,60 @@ class VectorRemoteEnv:
         self._pinned.numpy()[...] = arr
         return self._pinned.to(self.device, non_blocking=True)
 
-    def reset(self):
-        for e in self.envs:
-            e._send(cmd='reset')
-        replies = [e._recv() for e in self.envs]
-        obs = [r.pop('obs') for r in replies]
-        return self._stage(obs), replies
+    def _exchange(self, which, cmd, actions):
+        if self.obs_dim is None:   # discover the observation size once
+            self._native.exchange(which[:1], cmd, np.asarray(actions[:1], np.float64), 0)
+            r = self._native.last_reply(which[0])
+            self.obs_dim = int(np.size(r.get('obs')))
+            if len(which) == 1:
+                o, rew, done = self._native.exchange([], cmd, np.zeros(0), self.obs_dim)
+                obs = np.asarray(r['obs'], np.float64).reshape(1, -1)
+                return obs, np.array([float(r.get('reward', 0.0))]), np.array([bool(r.get('done', False))])
+            o, rew, done = self._native.exchange(which[1:], cmd, np.asarray(actions[1:], np.float64), self.obs_dim)
+            first = np.asarray(r['obs'], np.float64).reshape(1, -1)
+            return (np.concatenate([first, o]), np.concatenate([[float(r.get('reward', 0.0))], rew]),
+                    np.concatenate([[bool(r.get('done', False))], done]))
+        return self._native.exchange(which, cmd, np.asarray(actions, np.float64), self.obs_dim)
+
+    def reset(self, which=None):
+        """Reset all (or the listed) envs; returns (obs, replies-or-None)."""
+        which = list(range(len(self))) if which is None else list(which)
+        if self._native is not None:
+            obs, _, _ = self._exchange(which, 'reset', np.zeros(len(which)))
+            return self._stage(obs), None
+        for i in which:
+            self.envs[i]._send(cmd='reset')
+        replies = [self.envs[i]._recv() for i in which]
+        return self._stage([r.pop('obs') for r in replies]), replies
 
     def step(self, actions):
+        """Step every env with its action; returns (obs, reward, done, replies-or-None)."""
         import torch
         if isinstance(actions, torch.Tensor):
             actions = actions.detach().cpu().numpy()
+        actions = np.asarray(actions, dtype=np.float64).reshape(len(self), -1)[:, 0]
+        if self._native is not None:
+            obs, rew, done = self._exchange(list(range(len(self))), 'step', actions)
+            return self._stage(obs), torch.from_numpy(np.asarray(rew)), torch.from_numpy(np.asarray(done)), None
         for e, a in zip(self.envs, actions):
-            e._send(cmd='step', action=a.item() if hasattr(a, 'item') else a)
+            e._send(cmd='step', action=float(a))
         replies = [e._recv() for e in self.envs]
         obs = [r.pop('obs') for r in replies]
         rew = torch.tensor([float(r.pop('reward')) for r in replies])
         done = torch.tensor([bool(r.pop('done')) for r in replies])
         return self._stage(obs), rew, done, replies
 
+    def infos(self, i):
+        """Full last reply of env i (native path) as a dict."""
+        if self._native is not None:
+            return self._native.last_reply(i)
+        raise NotImplementedError('replies are returned by step() on the Python path')
+
     def close(self):
-        for e in self.envs:
-            e.close()
+        if self._native is not None:
+            self._native.close()
+            self._native = None
+        if self.envs:
+            for e in self.envs:
+                e.close()
+            self.envs = None
