@@ -1,6 +1,8 @@
 // StreamLoader implementation (see loader.h).
 #include "loader.h"
 
+#include "../common/trace.h"
+
 #include <algorithm>
 #include <chrono>
 #include <cstring>
@@ -263,6 +265,7 @@ void StreamLoader::run() {
 }
 
 bool StreamLoader::process(zmtp::Message&& msg) {
+  trace::Range tr("btn.loader.process");
   auto bad = [&](const std::string& why) {
     {
       std::lock_guard<std::mutex> lk(mu_);
@@ -429,6 +432,7 @@ void StreamLoader::reap(bool wait_all) {
 }
 
 void StreamLoader::launch() {
+  trace::Range tr("btn.loader.launch");
   Posted p{nullptr, nullptr};
   {
     std::unique_lock<std::mutex> lk(mu_);

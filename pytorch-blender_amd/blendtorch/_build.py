@@ -139,7 +139,7 @@ def build_hip(verbose=False, jobs=8):
         objs = [f.result() for f in futs]
     target = PKG / f'_hip{_ext_suffix()}'
     if _newer(target, objs):
-        link = [hipcc, '-shared', '-fPIC', f'--offload-arch={HIP_ARCH}', '-Wl,-Bsymbolic', *objs, '-o', target]
+        link = [hipcc, '-shared', '-fPIC', f'--offload-arch={HIP_ARCH}', '-Wl,-Bsymbolic', *objs, '-o', target, '-ldl']
         if tl is not None:
             # resolve libamdhip64 to the runtime torch already loaded
             link += [f'-L{tl}', f'-Wl,-rpath,{tl}']

@@ -31,6 +31,7 @@ from torch.utils.data import default_collate
 
 from .. import ops
 from ..ops import DecodeConfig
+from ..utils import trace_range
 from .constants import DEFAULT_TIMEOUTMS
 
 logger = logging.getLogger('blendtorch')
@@ -162,7 +163,8 @@ class DeviceLoader:
                     t0 = time.time()
                     r = None
                     while r is None:
-                        r = loader.next(stream.cuda_stream, 200)
+                        with trace_range('btt.DeviceLoader.next'):
+                            r = loader.next(stream.cuda_stream, 200)
                         if r is None and (time.time() - t0) * 1000 > self.timeoutms:
                             raise TimeoutError('No response within timeout interval.')
                     idx, metas, _ = r

@@ -32,6 +32,10 @@ for step in "$@"; do
     ksweep) for mg in ${KSWEEP_GRIDS:-1024 2048 4096 16384}; do for pm in ${KSWEEP_PPT:-1 2 4}; do
             BT_DECODE_MAXGRID=$mg BT_DECODE_PPT_MULT=$pm timeout -k 10 120 python scripts/kernel_bench.py --only decode --tag "grid=$mg ppt_mult=$pm" >> gpurun_out/ksweep.log 2>&1 || { rc=$?; break 2; }
           done; done; rc=${rc:-0}; grep -o "grid=.*speedup" gpurun_out/ksweep.log | sed "s/'torch_eager_us.*//" ;;
+    trace) BLENDTORCH_ROCTX=1 timeout -k 10 300 rocprofv3 --marker-trace --kernel-trace --stats -d /tmp/rp_trace -o run --output-format csv -- python bench.py --steps 300 --warmup 20 > gpurun_out/trace.log 2>&1; rc=$?; tail -2 gpurun_out/trace.log
+          mkdir -p gpurun_out/trace && find /tmp/rp_trace -name '*stats.csv' -exec cp {} gpurun_out/trace/ \;;;
+    dist1) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29555 bench.py --gpus 1 --steps 500 --warmup 20 > gpurun_out/dist1.log 2>&1; rc=$?; grep '^{' gpurun_out/dist1.log;
+           timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29556 bench.py --gpus 1 --steps 300 --warmup 20 --consumer disc >> gpurun_out/dist1.log 2>&1; rc=$?; grep '^{' gpurun_out/dist1.log | tail -1;;
     h2d) timeout -k 10 120 python -c "
 import sys; sys.path.insert(0,'pytorch-blender_amd')
 import torch; from blendtorch import ops; e=ops.hip_ext()
