@@ -18,8 +18,9 @@ CLANG = '/opt/rocm/lib/llvm/bin/clang++'
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize('san,port', [('thread', 39200), ('address', 39300)])
-def test_transport_stress_sanitized(tmp_path, san, port):
+@pytest.mark.parametrize('san', ['thread', 'address'])
+def test_transport_stress_sanitized(tmp_path, san, free_port):
+    port = free_port  # 20 probed-free ports; the stress binds 6 of them
     cxx = CLANG if (san == 'thread' and os.path.exists(CLANG)) else 'g++'
     exe = tmp_path / f'stress_{san}'
     cmd = [cxx, '-std=c++17', '-O1', '-g', f'-fsanitize={san}', '-pthread', *[str(ROOT / s) for s in SRCS],
