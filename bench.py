@@ -95,6 +95,8 @@ def main():
     ap.add_argument('--shm', type=int, default=48,
                     help='>0 (default 48): producers render into an N-slot shared-memory ring (same host) and '
                          'send descriptors; 0: images inline in the ZMTP messages')
+    ap.add_argument('--h2d', choices=['auto', 'copy'], default='auto',
+                    help='auto: decode kernel reads pinned host frames directly (zero-copy); copy: DMA first')
     ap.add_argument('--start-port', type=int, default=0)
     ap.add_argument('--dist', choices=['shard', 'scatter'], default='shard',
                     help='shard: every rank owns its producers; scatter: rank 0 receives world*B per step '
@@ -154,7 +156,7 @@ def main():
             per_step = args.batch * (world if args.dist == 'scatter' else 1)
             dl = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=per_step, decode=decode, device=device,
                               max_items=total_batches * per_step, prefetch=6,
-                              io_threads=args.io_threads or None, timeoutms=60000)
+                              io_threads=args.io_threads or None, timeoutms=60000, h2d=args.h2d)
         if args.dist == 'scatter':
             it = iter(ScatterLoader(dl, args.batch, (3, 480, 640), torch.float32, device, total_batches))
         else:
@@ -230,10 +232,12 @@ def main():
                 'proto': args.proto,
                 'pinned_producers': pin,
                 'shm_slots': args.shm,
+                'h2d': args.h2d,
             },
             'sec_per_image': round(tmax / images, 7),
             'sec_per_batch': round(tmax / args.steps, 6),
-            'loader_stats': {k: stats.get(k) for k in ('frames', 'batches', 'bad', 'pool_fallbacks')},
+            'loader_stats': {k: stats.get(k) for k in ('frames', 'batches', 'bad', 'pool_fallbacks', 'direct_batches',
+                                                       'shm_frames', 'shm_torn')},
             'cpu': cpu,
         }), flush=True)
     if world > 1:

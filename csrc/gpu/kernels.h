@@ -34,9 +34,18 @@ enum Layout : int { NCHW = 0, NHWC = 1 };
 //   flip_all    applies to every image (OR-ed with flip[b]).
 //   flip_bits   per-image flip bitmask for b < 256 (kernel-argument copy, so
 //               the stream loader needs no per-batch flag upload).
+//   srcs[b]     when nsrcs == B: per-image source pointers (kernel-argument
+//               copy).  They may point at pinned / registered HOST memory: the
+//               kernel then streams the frames over PCIe itself (zero-copy
+//               fused read, no staging copy and no DMA-engine round).
+//   max_grid    0: default grid cap; >0 overrides it (launch-shape sweeps).
+constexpr int kMaxSrcs = 64;
 struct DecodeParams {
   const uint8_t* src = nullptr;
   const int64_t* src_offsets = nullptr;
+  const uint8_t* srcs[kMaxSrcs] = {};
+  int nsrcs = 0;
+  int max_grid = 0;
   void* dst = nullptr;
   const float* lut = nullptr;
   const uint8_t* flip = nullptr;
@@ -58,6 +67,8 @@ hipError_t decode(const DecodeParams& p, hipStream_t stream);
 struct Color4x4Params {
   const uint8_t* src = nullptr;
   const int64_t* src_offsets = nullptr;
+  const uint8_t* srcs[kMaxSrcs] = {};   // as DecodeParams::srcs
+  int nsrcs = 0;
   float* dst = nullptr;
   const float* lut = nullptr;
   const float* M = nullptr;

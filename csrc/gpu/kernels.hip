@@ -63,17 +63,41 @@ __device__ __forceinline__ void load_pixels(const uint8_t* p, Pixels<PPT, CIN>& 
   }
 }
 
+// Table lookup of input channel IC for the lane's PPT pixels.  The channel
+// map is a runtime value, but it is uniform across the wave: `lookup`
+// branches on it once (scalar branch) into a fully static body, so every
+// byte of `px` is addressed with a compile-time index and `px` stays in
+// VGPRs (a dynamically indexed byte array would be spilled to scratch).
+template <int PPT, int CIN, int IC>
+__device__ __forceinline__ void lookup_static(const Pixels<PPT, CIN>& px, const float* l, float (&o)[PPT]) {
+#pragma unroll
+  for (int i = 0; i < PPT; ++i) o[i] = l[px.v[i * CIN + IC]];
+}
+
+template <int PPT, int CIN>
+__device__ __forceinline__ void lookup(const Pixels<PPT, CIN>& px, int ic, const float* l, float (&o)[PPT]) {
+  switch (ic) {
+    case 0: lookup_static<PPT, CIN, 0>(px, l, o); break;
+    case 1: if constexpr (CIN > 1) lookup_static<PPT, CIN, 1>(px, l, o); break;
+    case 2: if constexpr (CIN > 2) lookup_static<PPT, CIN, 2>(px, l, o); break;
+    default: if constexpr (CIN > 3) lookup_static<PPT, CIN, 3>(px, l, o); break;
+  }
+}
+
 template <int PPT, int CIN, int OUTT, int COUT>
 __device__ __forceinline__ void store_nhwc(const DecodeParams& p, const float* lut, const int* cm,
                                            const Pixels<PPT, CIN>& px, int b, int64_t q, int64_t HW) {
   constexpr int N = PPT * COUT;
   const int64_t off = (int64_t(b) * HW + q) * COUT;
+  float v[COUT][PPT];
+#pragma unroll
+  for (int c = 0; c < COUT; ++c) lookup<PPT, CIN>(px, cm[c], lut + c * 256, v[c]);
   if constexpr (OUTT == OUT_F32) {
     float o[N];
 #pragma unroll
     for (int i = 0; i < PPT; ++i)
 #pragma unroll
-      for (int c = 0; c < COUT; ++c) o[i * COUT + c] = lut[c * 256 + px.v[i * CIN + cm[c]]];
+      for (int c = 0; c < COUT; ++c) o[i * COUT + c] = v[c][i];
     float4* d = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.dst) + off);
 #pragma unroll
     for (int i = 0; i < N / 4; ++i) d[i] = make_float4(o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]);
@@ -82,10 +106,7 @@ __device__ __forceinline__ void store_nhwc(const DecodeParams& p, const float* l
 #pragma unroll
     for (int i = 0; i < PPT; ++i)
 #pragma unroll
-      for (int c = 0; c < COUT; ++c) {
-        float v = lut[c * 256 + px.v[i * CIN + cm[c]]];
-        o[i * COUT + c] = OUTT == OUT_BF16 ? f2bf(v) : f2h(v);
-      }
+      for (int c = 0; c < COUT; ++c) o[i * COUT + c] = OUTT == OUT_BF16 ? f2bf(v[c][i]) : f2h(v[c][i]);
     uint4* d = reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(p.dst) + off);
 #pragma unroll
     for (int i = 0; i < N / 8; ++i) d[i] = *reinterpret_cast<const uint4*>(&o[8 * i]);
@@ -94,7 +115,7 @@ __device__ __forceinline__ void store_nhwc(const DecodeParams& p, const float* l
 #pragma unroll
     for (int i = 0; i < PPT; ++i)
 #pragma unroll
-      for (int c = 0; c < COUT; ++c) o[i * COUT + c] = uint8_t(lut[c * 256 + px.v[i * CIN + cm[c]]]);
+      for (int c = 0; c < COUT; ++c) o[i * COUT + c] = uint8_t(v[c][i]);
     uint4* d = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(p.dst) + off);
 #pragma unroll
     for (int i = 0; i < N / 16; ++i) d[i] = *reinterpret_cast<const uint4*>(&o[16 * i]);
@@ -122,36 +143,32 @@ __global__ __launch_bounds__(kBlock) void decode_vec_kernel(DecodeParams p) {
     const int x = int(q - int64_t(y) * p.W);
     const bool flip = p.flip_all || (p.flip && p.flip[b]) || (b < 256 && ((p.flip_bits[b >> 6] >> (b & 63)) & 1));
     const int sy = flip ? p.H - 1 - y : y;
-    const uint8_t* img = p.src + (p.src_offsets ? p.src_offsets[b] : int64_t(b) * HW * CIN);
+    const uint8_t* img = p.nsrcs ? p.srcs[b] : p.src + (p.src_offsets ? p.src_offsets[b] : int64_t(b) * HW * CIN);
     Pixels<PPT, CIN> px;
     load_pixels<PPT, CIN>(img + (int64_t(sy) * p.W + x) * CIN, px);
 
     if constexpr (LAYOUT == NCHW) {
-      for (int c = 0; c < cout; ++c) {
-        const float* l = lut + c * 256;
-        const int ic = cm[c];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (c >= cout) break;
+        float v[PPT];
+        lookup<PPT, CIN>(px, cm[c], lut + c * 256, v);
         const int64_t off = (int64_t(b) * cout + c) * HW + q;
         if constexpr (OUTT == OUT_F32) {
-          float o[PPT];
-#pragma unroll
-          for (int i = 0; i < PPT; ++i) o[i] = l[px.v[i * CIN + ic]];
           float* d = reinterpret_cast<float*>(p.dst) + off;
 #pragma unroll
-          for (int i = 0; i < PPT / 4; ++i) reinterpret_cast<float4*>(d)[i] = make_float4(o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]);
+          for (int i = 0; i < PPT / 4; ++i) reinterpret_cast<float4*>(d)[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
         } else if constexpr (OUTT == OUT_BF16 || OUTT == OUT_F16) {
           uint16_t o[PPT];
 #pragma unroll
-          for (int i = 0; i < PPT; ++i) {
-            float v = l[px.v[i * CIN + ic]];
-            o[i] = OUTT == OUT_BF16 ? f2bf(v) : f2h(v);
-          }
+          for (int i = 0; i < PPT; ++i) o[i] = OUTT == OUT_BF16 ? f2bf(v[i]) : f2h(v[i]);
           uint16_t* d = reinterpret_cast<uint16_t*>(p.dst) + off;
 #pragma unroll
           for (int i = 0; i < PPT / 8; ++i) reinterpret_cast<uint4*>(d)[i] = *reinterpret_cast<const uint4*>(&o[8 * i]);
         } else {
           uint8_t o[PPT];
 #pragma unroll
-          for (int i = 0; i < PPT; ++i) o[i] = uint8_t(l[px.v[i * CIN + ic]]);
+          for (int i = 0; i < PPT; ++i) o[i] = uint8_t(v[i]);
           uint8_t* d = reinterpret_cast<uint8_t*>(p.dst) + off;
 #pragma unroll
           for (int i = 0; i < PPT / 16; ++i) reinterpret_cast<uint4*>(d)[i] = *reinterpret_cast<const uint4*>(&o[16 * i]);
@@ -184,7 +201,7 @@ __global__ __launch_bounds__(kBlock) void decode_scalar_kernel(DecodeParams p) {
     const int y = int(q / p.W), x = int(q - int64_t(y) * p.W);
     const bool flip = p.flip_all || (p.flip && p.flip[b]) || (b < 256 && ((p.flip_bits[b >> 6] >> (b & 63)) & 1));
     const int sy = flip ? p.H - 1 - y : y;
-    const uint8_t* img = p.src + (p.src_offsets ? p.src_offsets[b] : int64_t(b) * HW * p.Cin);
+    const uint8_t* img = p.nsrcs ? p.srcs[b] : p.src + (p.src_offsets ? p.src_offsets[b] : int64_t(b) * HW * p.Cin);
     const uint8_t* s = img + (int64_t(sy) * p.W + x) * p.Cin;
     for (int c = 0; c < p.Cout; ++c) {
       float v = lut[c * 256 + s[p.cmap[c]]];
@@ -197,19 +214,27 @@ __global__ __launch_bounds__(kBlock) void decode_scalar_kernel(DecodeParams p) {
   }
 }
 
-int grid_for(int64_t work) {
+int grid_for(int64_t work, int cap = 0) {
   // 256 CUs x 8 resident 256-thread blocks; grid-stride beyond that
+  if (cap <= 0) cap = 2048;
   int64_t blocks = (work + kBlock - 1) / kBlock;
-  return int(blocks < 2048 ? (blocks > 0 ? blocks : 1) : 2048);
+  return int(blocks < cap ? (blocks > 0 ? blocks : 1) : cap);
+}
+
+bool srcs_ok(const uint8_t* const* srcs, int n, int B, uintptr_t align) {
+  if (n != B) return false;
+  for (int b = 0; b < n; ++b)
+    if (!srcs[b] || (reinterpret_cast<uintptr_t>(srcs[b]) % align) != 0) return false;
+  return true;
 }
 
 template <int PPT, int CIN, int OUTT>
 hipError_t launch_vec(const DecodeParams& p, hipStream_t s) {
   int64_t work = int64_t(p.B) * p.H * p.W / PPT;
   if (p.layout == NCHW)
-    decode_vec_kernel<PPT, CIN, OUTT, NCHW><<<grid_for(work), kBlock, 0, s>>>(p);
+    decode_vec_kernel<PPT, CIN, OUTT, NCHW><<<grid_for(work, p.max_grid), kBlock, 0, s>>>(p);
   else
-    decode_vec_kernel<PPT, CIN, OUTT, NHWC><<<grid_for(work), kBlock, 0, s>>>(p);
+    decode_vec_kernel<PPT, CIN, OUTT, NHWC><<<grid_for(work, p.max_grid), kBlock, 0, s>>>(p);
   return hipGetLastError();
 }
 
@@ -217,12 +242,14 @@ template <int OUTT>
 hipError_t launch_out(const DecodeParams& p, hipStream_t s) {
   constexpr int PPT = OUTT == OUT_F32 ? 4 : (OUTT == OUT_U8 ? 16 : 8);
   // vector path: a lane's PPT pixels sit in one row and its loads are aligned
+  const bool src_aligned = p.nsrcs ? srcs_ok(p.srcs, p.nsrcs, p.B, 16)
+                                   : (reinterpret_cast<uintptr_t>(p.src) % 16) == 0 && p.src_offsets == nullptr;
   bool aligned = (p.W % PPT) == 0 && (int64_t(p.H) * p.W * p.Cin) % 16 == 0 && (reinterpret_cast<uintptr_t>(p.dst) % 16) == 0 &&
-                 (reinterpret_cast<uintptr_t>(p.src) % 16) == 0 && p.src_offsets == nullptr;
+                 src_aligned;
   if (aligned && p.Cin == 4) return launch_vec<PPT, 4, OUTT>(p, s);
   if (aligned && p.Cin == 3) return launch_vec<PPT, 3, OUTT>(p, s);
   int64_t work = int64_t(p.B) * p.H * p.W;
-  decode_scalar_kernel<OUTT><<<grid_for(work), kBlock, 0, s>>>(p);
+  decode_scalar_kernel<OUTT><<<grid_for(work, p.max_grid), kBlock, 0, s>>>(p);
   return hipGetLastError();
 }
 
@@ -231,6 +258,7 @@ hipError_t launch_out(const DecodeParams& p, hipStream_t s) {
 hipError_t decode(const DecodeParams& p, hipStream_t stream) {
   if (p.B <= 0 || p.H <= 0 || p.W <= 0) return hipSuccess;
   if (p.Cout < 1 || p.Cout > 4 || p.Cin < 1 || p.Cin > 4) return hipErrorInvalidValue;
+  if (p.nsrcs && (p.nsrcs != p.B || p.nsrcs > kMaxSrcs || !srcs_ok(p.srcs, p.nsrcs, p.B, 1))) return hipErrorInvalidValue;
   for (int c = 0; c < p.Cout; ++c)
     if (p.cmap[c] < 0 || p.cmap[c] >= p.Cin) return hipErrorInvalidValue;
   switch (p.out_dtype) {
@@ -283,7 +311,7 @@ __global__ __launch_bounds__(kBlock) void color4x4_kernel(Color4x4Params p) {
     const int y = int(pl / p.W), x = int(pl - int64_t(y) * p.W);
     const bool flip = p.flip_all || (p.flip && p.flip[b]) || (b < 256 && ((p.flip_bits[b >> 6] >> (b & 63)) & 1));
     const int sy = flip ? p.H - 1 - y : y;
-    const uint8_t* img = p.src + (p.src_offsets ? p.src_offsets[b] : int64_t(b) * HW * 4);
+    const uint8_t* img = p.nsrcs ? p.srcs[b] : p.src + (p.src_offsets ? p.src_offsets[b] : int64_t(b) * HW * 4);
     const uint4 v4 = *reinterpret_cast<const uint4*>(img + (int64_t(sy) * p.W + x) * 4);
     const uint32_t w[4] = {v4.x, v4.y, v4.z, v4.w};
     f32x4 acc[4];
@@ -334,7 +362,7 @@ __global__ void project_kernel(const float* pts, int64_t N, const float* PV, con
 hipError_t color4x4(const Color4x4Params& p, hipStream_t stream) {
   if (p.B <= 0) return hipSuccess;
   if ((int64_t(p.H) * p.W) % 256 != 0 || p.W % 4 != 0 || p.Cout < 1 || p.Cout > 4 || (reinterpret_cast<uintptr_t>(p.dst) % 16) != 0 ||
-      (reinterpret_cast<uintptr_t>(p.src) % 16) != 0)
+      (p.nsrcs ? !srcs_ok(p.srcs, p.nsrcs, p.B, 16) : (reinterpret_cast<uintptr_t>(p.src) % 16) != 0))
     return hipErrorInvalidValue;
   int64_t waves = int64_t(p.B) * p.H * p.W / 256;
   int64_t blocks = (waves + 3) / 4;

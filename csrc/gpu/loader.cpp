@@ -52,6 +52,7 @@ struct DeviceGuard {
 PinnedPool::PinnedPool(size_t slot_bytes, int nslots) : slot_bytes_(slot_bytes), nslots_(nslots) {
   check(hipHostMalloc(reinterpret_cast<void**>(&base_), slot_bytes_ * size_t(nslots_), hipHostMallocDefault),
         "hipHostMalloc(pinned pool)");
+  if (hipHostGetDevicePointer(reinterpret_cast<void**>(&dev_base_), base_, 0) != hipSuccess) dev_base_ = nullptr;
   free_.reserve(size_t(nslots_));
   for (int i = nslots_ - 1; i >= 0; --i) free_.push_back(i);
 }
@@ -199,7 +200,7 @@ void StreamLoader::stop() {
   for (auto& it : cur_)
     if (it.seg) it.seg->release(it.slot, it.gen);
   cur_.clear();
-  for (auto& kv : segments_) (void)hipHostUnregister(kv.second->base());
+  for (auto& kv : segments_) (void)hipHostUnregister(kv.second.seg->base());
   segments_.clear();
   {
     std::lock_guard<std::mutex> lk(mu_);
@@ -301,8 +302,11 @@ bool StreamLoader::process(zmtp::Message&& msg) {
     const codec::Value& d = *root->items[shm_idx + 1];
     if (d.kind != codec::Value::TUPLE || d.items.size() < 8 || d.items[0]->kind != codec::Value::STR)
       return bad("malformed _btshm descriptor");
+    uint8_t* dev_base = nullptr;
     try {
-      it.seg = segment(d.items[0]->s);
+      MappedSegment& ms = segment(d.items[0]->s);
+      it.seg = ms.seg.get();
+      dev_base = ms.dev_base;
     } catch (const std::exception& e) {
       return bad(e.what());
     }
@@ -313,6 +317,7 @@ bool StreamLoader::process(zmtp::Message&& msg) {
     if (it.slot >= it.seg->nslots() || off < 0 || size_t(off) + size_t(h) * w * c > it.seg->size())
       return bad("_btshm descriptor out of range");
     it.src = it.seg->base() + off;
+    if (dev_base) it.dsrc = dev_base + off;
     root->items.erase(root->items.begin() + long(shm_idx), root->items.begin() + long(shm_idx) + 2);
   } else {
     if (img_idx == size_t(-1)) return bad("no '" + cfg_.image_key + "' entry");
@@ -327,6 +332,8 @@ bool StreamLoader::process(zmtp::Message&& msg) {
       return bad("image must be HxW or HxWxC");
     }
     it.src = data + img.off;
+    if (pool_ && it.frame.buf && it.frame.buf->pinned && it.frame.buf->owner == pool_.get())
+      it.dsrc = pool_->device_ptr(it.src);
     cut = img.off, len = img.len;
   }
   if (c < 1 || c > 4) return bad("image channels must be 1..4");
@@ -401,15 +408,17 @@ bool StreamLoader::process(zmtp::Message&& msg) {
   return true;
 }
 
-shm::Segment* StreamLoader::segment(const std::string& name) {
+StreamLoader::MappedSegment& StreamLoader::segment(const std::string& name) {
   auto it = segments_.find(name);
-  if (it != segments_.end()) return it->second.get();
-  std::unique_ptr<shm::Segment> seg(shm::Segment::open(name));
-  // pin the producer's ring so the DMA engine reads the slots in place
-  check(hipHostRegister(seg->base(), seg->size(), hipHostRegisterDefault), "hipHostRegister(shm)");
-  auto* raw = seg.get();
-  segments_[name] = std::move(seg);
-  return raw;
+  if (it != segments_.end()) return it->second;
+  MappedSegment ms;
+  ms.seg.reset(shm::Segment::open(name));
+  // pin + map the producer's ring: the DMA engine (copy path) or the decode
+  // kernel itself (direct path) reads the slots in place
+  check(hipHostRegister(ms.seg->base(), ms.seg->size(), hipHostRegisterMapped), "hipHostRegister(shm)");
+  if (hipHostGetDevicePointer(reinterpret_cast<void**>(&ms.dev_base), ms.seg->base(), 0) != hipSuccess)
+    ms.dev_base = nullptr;
+  return segments_[name] = std::move(ms);
 }
 
 void StreamLoader::reap(bool wait_all) {
@@ -453,16 +462,22 @@ void StreamLoader::launch() {
   check(hipStreamWaitEvent(stream_, p.ready, 0), "hipStreamWaitEvent(post)");
   (void)hipEventDestroy(p.ready);
   uint64_t flips[4] = {0, 0, 0, 0};
+  // direct: the kernel reads every frame from pinned host memory itself
+  bool direct = cfg_.direct && B <= kMaxSrcs;
+  for (int i = 0; i < B && direct; ++i)
+    direct = cur_[size_t(i)].dsrc && (reinterpret_cast<uintptr_t>(cur_[size_t(i)].dsrc) % 16) == 0;
   for (int i = 0; i < B; ++i) {
     const Item& it = cur_[size_t(i)];
-    check(hipMemcpyAsync(stage + size_t(i) * img_bytes_, it.src, img_bytes_,
-                         hipMemcpyHostToDevice, stream_),
-          "hipMemcpyAsync(H2D)");
+    if (!direct)
+      check(hipMemcpyAsync(stage + size_t(i) * img_bytes_, it.src, img_bytes_, hipMemcpyHostToDevice, stream_),
+            "hipMemcpyAsync(H2D)");
     if (it.flip && i < 256) flips[i >> 6] |= uint64_t(1) << (i & 63);
   }
+  // `copied` marks the last device read of the host slots: after the copies,
+  // or (direct) after the kernel that reads them
   hipEvent_t copied;
   check(hipEventCreateWithFlags(&copied, hipEventDisableTiming), "hipEventCreate(copied)");
-  check(hipEventRecord(copied, stream_), "hipEventRecord(copied)");
+  if (!direct) check(hipEventRecord(copied, stream_), "hipEventRecord(copied)");
   bool any_flip_beyond = false;
   for (int i = 256; i < B; ++i) any_flip_beyond |= cur_[size_t(i)].flip;
   if (any_flip_beyond) throw std::runtime_error("StreamLoader: per-image flip supports batch <= 256");
@@ -470,6 +485,10 @@ void StreamLoader::launch() {
   if (cfg_.color_matrix) {
     Color4x4Params cp;
     cp.src = stage;
+    if (direct) {
+      cp.nsrcs = B;
+      for (int i = 0; i < B; ++i) cp.srcs[i] = cur_[size_t(i)].dsrc;
+    }
     cp.dst = static_cast<float*>(p.dst);
     cp.lut = d_lut_;
     cp.M = d_mat_;
@@ -481,6 +500,10 @@ void StreamLoader::launch() {
   } else {
     DecodeParams dp;
     dp.src = stage;
+    if (direct) {
+      dp.nsrcs = B;
+      for (int i = 0; i < B; ++i) dp.srcs[i] = cur_[size_t(i)].dsrc;
+    }
     dp.dst = p.dst;
     dp.lut = d_lut_;
     dp.B = B, dp.H = H_, dp.W = W_, dp.Cin = C_, dp.Cout = cfg_.cout;
@@ -492,6 +515,7 @@ void StreamLoader::launch() {
     e = decode(dp, stream_);
   }
   check(e, "decode kernel launch");
+  if (direct) check(hipEventRecord(copied, stream_), "hipEventRecord(copied)");
   Inflight fl;
   fl.frames.reserve(size_t(B));
   ReadyBatch rb;
@@ -511,6 +535,7 @@ void StreamLoader::launch() {
   {
     std::lock_guard<std::mutex> lk(mu_);
     stats_.batches++;
+    if (direct) stats_.direct_batches++;
     stats_.h2d_issue_ms += now_ms() - t_issue;
     ready_.push_back(std::move(rb));
   }

@@ -61,12 +61,19 @@ class PinnedPool : public Allocator, public std::enable_shared_from_this<PinnedP
   int nslots() const { return nslots_; }
   int free_slots();
   uint64_t fallbacks() const { return fallbacks_.load(); }
+  // Device-visible address of a host byte inside the pool (kernels may read
+  // the slots directly over PCIe), or nullptr if `host` is not in the pool.
+  const uint8_t* device_ptr(const uint8_t* host) const {
+    if (!dev_base_ || host < base_ || host >= base_ + slot_bytes_ * size_t(nslots_)) return nullptr;
+    return dev_base_ + (host - base_);
+  }
 
  private:
   static void release(void* owner, Buffer* b);
   size_t slot_bytes_;
   int nslots_;
   uint8_t* base_ = nullptr;
+  uint8_t* dev_base_ = nullptr;
   std::mutex mu_;
   std::condition_variable cv_;
   std::vector<int> free_;
@@ -86,6 +93,12 @@ struct LoaderConfig {
   int pool_slots = 0;                // 0: auto
   int staging_depth = 3;
   bool skip_bad = false;             // drop malformed messages instead of failing
+  // true: when every frame of a batch sits in device-visible pinned host
+  // memory (pool slot or registered shm ring) with 16-byte alignment, the
+  // decode kernel reads the frames itself over PCIe (zero-copy fused read,
+  // ~45 GB/s vs ~35 GB/s for per-frame DMA copies + decode on MI355X);
+  // false: always DMA into the device staging ring first.
+  bool direct = true;
   // decode parameters (src/dst/B/H/W/Cin filled per batch)
   int cout = 3;
   int cmap[4] = {0, 1, 2, 3};
@@ -114,6 +127,7 @@ struct ReadyBatch {
 struct LoaderStats {
   uint64_t frames = 0, batches = 0, bytes = 0, bad = 0, pool_fallbacks = 0;
   uint64_t shm_frames = 0, shm_torn = 0;   // via shared memory / slot reclaimed during the copy
+  uint64_t direct_batches = 0;             // decoded straight from host memory (no staging copy)
   double h2d_issue_ms = 0;
 };
 
@@ -140,6 +154,7 @@ class StreamLoader {
   struct Item {
     zmtp::Frame frame;
     const uint8_t* src = nullptr;      // image bytes: in the frame or in a shm slot
+    const uint8_t* dsrc = nullptr;     // device-visible alias of `src` (pinned + mapped), or null
     shm::Segment* seg = nullptr;       // shared-memory slot to hand back, if any
     uint32_t slot = 0, gen = 0;
     bool flip = false;
@@ -186,8 +201,12 @@ class StreamLoader {
     };
     std::vector<Slot> slots;
   };
-  shm::Segment* segment(const std::string& name);
-  std::map<std::string, std::unique_ptr<shm::Segment>> segments_;   // mapped + hipHostRegister'ed
+  struct MappedSegment {
+    std::unique_ptr<shm::Segment> seg;
+    uint8_t* dev_base = nullptr;   // device-visible alias of seg->base()
+  };
+  MappedSegment& segment(const std::string& name);
+  std::map<std::string, MappedSegment> segments_;   // mapped + hipHostRegister'ed
   std::deque<Inflight> inflight_;   // H2D copies not yet known complete
   int64_t batch_index_ = 0;
   double batch_t0_ = 0;

@@ -9,6 +9,7 @@
 #include <pybind11/stl.h>
 
 #include <chrono>
+#include <tuple>
 #include <cstring>
 #include <stdexcept>
 #include <sys/mman.h>
@@ -145,6 +146,94 @@ PYBIND11_MODULE(_hip, m) {
     return double(nbytes) * chunks * iters / sec / 1e9;   // GB/s
   });
 
+  // Host-resident frames -> decoded batch, two ways (returns us per batch):
+  //   mode "copy":   B hipMemcpyAsync into a device staging buffer + decode
+  //                  (the DMA-engine path);
+  //   mode "direct": decode reads the B host frames itself over PCIe
+  //                  (zero-copy fused read; srcs[] = host pointers).
+  // `kind` picks the host memory: "hostmalloc" (hipHostMalloc) or
+  // "register" (mmap + hipHostRegister, like the producers' shm ring).
+  // Each iteration rewrites one byte per frame on the host first, and the
+  // result of the last iteration is checked, so a stale GPU-cached read of
+  // host memory would show up as a mismatch (returned as `stale`).
+  m.def("bench_frames_to_device",
+        [](const std::string& mode, const std::string& kind, int B, int H, int W, int Cin, int iters, int max_grid) {
+          py::gil_scoped_release nogil;
+          const size_t img = size_t(H) * W * Cin;
+          const size_t slot = (img + 4095) & ~size_t(4095);
+          uint8_t* host = nullptr;
+          if (kind == "hostmalloc") {
+            check(hipHostMalloc(reinterpret_cast<void**>(&host), slot * B, hipHostMallocDefault), "hipHostMalloc");
+          } else {
+            host = static_cast<uint8_t*>(mmap(nullptr, slot * B, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0));
+            check(hipHostRegister(host, slot * B, hipHostRegisterMapped), "hipHostRegister");
+          }
+          for (size_t i = 0; i < slot * size_t(B); ++i) host[i] = uint8_t(i * 7);
+          uint8_t* dev_host = nullptr;
+          check(hipHostGetDevicePointer(reinterpret_cast<void**>(&dev_host), host, 0), "hipHostGetDevicePointer");
+          uint8_t* stage = nullptr;
+          float *dst = nullptr, *lut = nullptr;
+          check(hipMalloc(reinterpret_cast<void**>(&stage), img * B), "hipMalloc");
+          check(hipMalloc(reinterpret_cast<void**>(&dst), size_t(B) * 3 * H * W * sizeof(float)), "hipMalloc");
+          std::vector<float> hl(4 * 256);
+          for (int i = 0; i < 4 * 256; ++i) hl[size_t(i)] = float(i & 255);
+          check(hipMalloc(reinterpret_cast<void**>(&lut), hl.size() * sizeof(float)), "hipMalloc");
+          check(hipMemcpy(lut, hl.data(), hl.size() * sizeof(float), hipMemcpyHostToDevice), "lut");
+          hipStream_t s;
+          check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "stream");
+          DecodeParams p;
+          p.dst = dst;
+          p.lut = lut;
+          p.B = B, p.H = H, p.W = W, p.Cin = Cin, p.Cout = 3;
+          p.max_grid = max_grid;
+          const bool direct = mode == "direct";
+          if (direct) {
+            p.nsrcs = B;
+            for (int b = 0; b < B; ++b) p.srcs[b] = dev_host + size_t(b) * slot;
+          } else {
+            p.src = stage;
+          }
+          auto run = [&](int it) {
+            for (int b = 0; b < B; ++b) host[size_t(b) * slot] = uint8_t(it);   // fresh content per batch
+            if (!direct)
+              for (int b = 0; b < B; ++b)
+                check(hipMemcpyAsync(stage + size_t(b) * img, host + size_t(b) * slot, img, hipMemcpyHostToDevice, s),
+                      "memcpy");
+            check(decode(p, s), "decode");
+          };
+          for (int i = 0; i < 5; ++i) {
+            run(i);
+            check(hipStreamSynchronize(s), "sync");
+          }
+          auto t0 = std::chrono::steady_clock::now();
+          for (int i = 0; i < iters; ++i) {
+            check(hipStreamSynchronize(s), "sync");   // host rewrites only after the last read
+            run(100 + i);
+          }
+          check(hipStreamSynchronize(s), "sync");
+          double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / iters;
+          // check pixel 0 (channel 0) of every image of the last batch
+          int stale = 0;
+          for (int b = 0; b < B; ++b) {
+            float v = 0;
+            check(hipMemcpy(&v, dst + size_t(b) * 3 * H * W, sizeof(float), hipMemcpyDeviceToHost), "d2h");
+            if (v != float(uint8_t(100 + iters - 1))) ++stale;
+          }
+          (void)hipStreamDestroy(s);
+          (void)hipFree(stage);
+          (void)hipFree(dst);
+          (void)hipFree(lut);
+          if (kind == "hostmalloc") (void)hipHostFree(host);
+          else {
+            (void)hipHostUnregister(host);
+            munmap(host, slot * B);
+          }
+          // us/batch, GB/s of frame bytes, stale (std::tuple: converted after the GIL is re-taken)
+          return std::make_tuple(us, double(img) * B / us / 1e3, stale);
+        },
+        py::arg("mode"), py::arg("kind"), py::arg("B"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("iters"),
+        py::arg("max_grid") = 0);
+
   // Kernel-only timing (no Python launch overhead): `iters` back-to-back
   // decode launches between two HIP events; returns microseconds per launch.
   m.def("bench_decode",
@@ -182,8 +271,9 @@ PYBIND11_MODULE(_hip, m) {
                        int io_threads, int device, int64_t max_batches, size_t max_frame_bytes, int pool_slots,
                        int staging_depth, bool skip_bad, int cout, std::vector<int> cmap, int flip_all,
                        int out_dtype, int layout, std::vector<float> lut, std::vector<float> matrix,
-                       std::vector<float> bias) {
+                       std::vector<float> bias, bool direct) {
              LoaderConfig c;
+             c.direct = direct;
              c.addresses = std::move(addresses);
              c.batch_size = batch_size;
              c.image_key = std::move(image_key);
@@ -210,7 +300,7 @@ PYBIND11_MODULE(_hip, m) {
            py::arg("io_threads"), py::arg("device"), py::arg("max_batches"), py::arg("max_frame_bytes"),
            py::arg("pool_slots"), py::arg("staging_depth"), py::arg("skip_bad"), py::arg("cout"), py::arg("cmap"),
            py::arg("flip_all"), py::arg("out_dtype"), py::arg("layout"), py::arg("lut"), py::arg("matrix"),
-           py::arg("bias"))
+           py::arg("bias"), py::arg("direct") = true)
       .def("start", &StreamLoader::start)
       .def("wait_shape",
            [](StreamLoader& l, long timeout_ms) -> py::object {
@@ -262,6 +352,7 @@ PYBIND11_MODULE(_hip, m) {
         d["h2d_issue_ms"] = s.h2d_issue_ms;
         d["shm_frames"] = s.shm_frames;
         d["shm_torn"] = s.shm_torn;
+        d["direct_batches"] = s.direct_batches;
         return d;
       });
 }

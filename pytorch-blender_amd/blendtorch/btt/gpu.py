@@ -68,12 +68,21 @@ class DeviceLoader:
         Drop malformed messages instead of failing the stream.
     meta_to_device: bool
         Move collated metadata tensors to the device as well.
+    h2d: str
+        ``'auto'`` (default): when a batch's frames all sit in device-visible
+        pinned host memory (the producers' shared-memory ring, or the
+        loader's pinned receive slots) the decode kernel reads them over PCIe
+        itself -- one fused pass, no staging copy; otherwise the frames are
+        DMA'd into a device staging ring first.  ``'copy'``: always DMA.
     """
 
     def __init__(self, addresses: Sequence[str], batch_size: int = 8, decode: DecodeConfig = DecodeConfig(),
                  device=None, max_items: Optional[int] = None, timeoutms: int = DEFAULT_TIMEOUTMS,
                  rcvhwm: int = 10, prefetch: int = 4, io_threads: Optional[int] = None, image_key: str = 'image',
-                 skip_bad: bool = False, meta_to_device: bool = False, staging_depth: int = 3):
+                 skip_bad: bool = False, meta_to_device: bool = False, staging_depth: int = 3, h2d: str = 'auto'):
+        if h2d not in ('auto', 'copy'):
+            raise ValueError("h2d must be 'auto' or 'copy'")
+        self.h2d = h2d
         if isinstance(addresses, str):
             addresses = [addresses]
         self.addresses = list(addresses)
@@ -117,7 +126,8 @@ class DeviceLoader:
         return ext.StreamLoader(
             self.addresses, self.batch_size, self.image_key, self.rcvhwm, self.io_threads, self.device.index,
             max_batches, 0, 0, self.staging_depth, self.skip_bad, cfg.cout, list(cfg.cmap) + [0] * (4 - len(cfg.cmap)),
-            int(cfg.flip), ops.OUT_DTYPES[cfg.dtype], ops.LAYOUTS[cfg.layout], lut, matrix, bias)
+            int(cfg.flip), ops.OUT_DTYPES[cfg.dtype], ops.LAYOUTS[cfg.layout], lut, matrix, bias,
+            self.h2d == 'auto')
 
     def _post(self, loader, stream):
         out = torch.empty(self.decode.out_shape(self.batch_size, *self.shape[:2]), dtype=self.decode.torch_dtype(),

@@ -43,6 +43,18 @@ for k in ('hostmalloc','register','pageable'):
     for chunks in (1,8):
         print(k, 'chunks', chunks, round(e.bench_h2d(k, 1228800, 200, chunks),2), 'GB/s', flush=True)
 " > gpurun_out/h2d.log 2>&1; rc=$?; cat gpurun_out/h2d.log;;
+    f2d) timeout -k 10 180 python -c "
+import sys; sys.path.insert(0,'pytorch-blender_amd')
+import torch; from blendtorch import ops; e=ops.hip_ext()
+import os
+B = int(os.environ.get('F2D_B', '8'))
+for cin in (4, 3):
+  for kind in ('register',):
+    for mode, grids in (('copy', (0,)), ('direct', (0, 128, 256, 512, 1024, 4096))):
+        for g in grids:
+            us, gbs, stale = e.bench_frames_to_device(mode, kind, B, 480, 640, cin, 300, g)
+            print(f'B={B} cin={cin} {kind:10s} {mode:6s} grid={g:5d} {us:8.1f} us/batch {gbs:6.1f} GB/s stale={stale}', flush=True)
+" > gpurun_out/f2d.log 2>&1; rc=$?; cat gpurun_out/f2d.log;;
     *) echo "unknown step $step"; rc=2;;
   esac
   echo "== step $step rc=$rc"

@@ -121,16 +121,38 @@ def test_device_loader_shared_memory_producer(dev, free_port, origin):
     exactly what the inline-payload path gives for the same rendered frame."""
     cfg = ops.DecodeConfig.densityopt(channels='rgb', gamma=2.2)
     base = ['--mode', 'rgba', '--rotation', '0.4', '0.9', '1.7', '--origin', origin]
-    out = {}
-    for k, extra in (('inline', []), ('shm', ['--shm', '12'])):
+    out, stats = {}, {}
+    for i, (k, extra, h2d) in enumerate((('inline', [], 'auto'), ('shm', ['--shm', '12'], 'auto'),
+                                         ('shm-copy', ['--shm', '12'], 'copy'))):
         with btt.BlenderLauncher(producer='cubesim', num_instances=2, named_sockets=['DATA'],
-                                 start_port=free_port + (10 if extra else 0), proto='ipc',
+                                 start_port=free_port + 5 * i, proto='ipc',
                                  instance_args=[base + extra] * 2) as bl:
-            dl = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=8, max_items=96, decode=cfg, device=dev)
+            dl = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=8, max_items=96, decode=cfg, device=dev,
+                              h2d=h2d)
             batches = list(dl)
             assert dl.stats['frames'] == 96 and dl.stats['bad'] == 0
-            out[k] = batches[-1]['image']
+            out[k], stats[k] = batches[-1]['image'], dl.stats
             assert 'xy' in batches[0] and batches[0]['xy'].shape == (8, 8, 2)
     torch.testing.assert_close(out['shm'], out['inline'], rtol=0, atol=0)
+    torch.testing.assert_close(out['shm-copy'], out['inline'], rtol=0, atol=0)
+    # shm frames are registered + mapped: every batch decodes straight from host memory
+    assert stats['shm']['direct_batches'] == 12 and stats['shm-copy']['direct_batches'] == 0
     import os
     assert not [f for f in os.listdir('/dev/shm') if f.startswith('blendtorch-')]
+
+
+def test_device_loader_direct_color4x4(dev, free_port):
+    """The MFMA colour-transform kernel on the direct (zero-copy) path equals
+    the staged-copy path and the fp32 reference."""
+    M = [[0.5, 0.2, 0.1, 0.0], [0.0, 1.0, 0.0, 0.0], [0.1, 0.1, 0.8, 0.0], [0.0, 0.0, 0.0, 1.0]]
+    cfg = ops.DecodeConfig(channels='rgba', color_matrix=M, color_bias=(0.1, 0.0, -0.1, 0.0))
+    res = {}
+    for i, h2d in enumerate(('auto', 'copy')):
+        with btt.BlenderLauncher(producer='cubesim', num_instances=1, named_sockets=['DATA'],
+                                 start_port=free_port + 5 * i, proto='ipc',
+                                 instance_args=[['--mode', 'rgba', '--rotation', '0.1', '0.2', '0.3', '--shm', '8']]) as bl:
+            dl = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=4, max_items=8, decode=cfg, device=dev,
+                              h2d=h2d)
+            res[h2d] = list(dl)[-1]['image']
+            assert dl.stats['direct_batches'] == (2 if h2d == 'auto' else 0)
+    torch.testing.assert_close(res['auto'], res['copy'], rtol=0, atol=0)
