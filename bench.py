@@ -52,22 +52,20 @@ def ensure_built():
 
 
 def cpu_budget():
-    """(cpus, pin): CPUs usable by this process and whether pinning producers
-    to them isolates anything.  With a cgroup CPU quota far below the
-    affinity mask (a shared host), the quota is the budget and pinning would
-    only pile producers onto cores other tenants also use."""
+    """(affinity, budget, pin): CPUs this process may run on, how many of them
+    it may keep busy (cgroup CPU quota), and whether pinning producers to
+    single cores isolates anything.  With a quota far below the affinity mask
+    (a shared host) the quota is the budget and per-core pinning would only
+    pile producers onto cores other tenants also use."""
     cpus = sorted(os.sched_getaffinity(0))
-    pin = True
+    budget = len(cpus)
     try:
         quota, period = Path('/sys/fs/cgroup/cpu.max').read_text().split()[:2]
         if quota != 'max':
-            n = max(1, int(int(quota) / int(period)))
-            if n < len(cpus):
-                pin = n * 2 > len(cpus)
-                cpus = cpus[:n]
+            budget = max(1, min(budget, int(int(quota) / int(period))))
     except (OSError, ValueError):
         pass
-    return cpus, pin
+    return cpus, budget, budget * 2 > len(cpus)
 
 
 def cgroup_cpu_stat():
@@ -120,16 +118,26 @@ def main():
     if world > 1:
         dist.init_process_group('nccl', device_id=device)
 
-    # partition this node's CPUs between the local ranks; producers are pinned
-    cpus, pin = cpu_budget()
-    share = max(1, len(cpus) // local_world)
-    mine = cpus[local_rank * share:(local_rank + 1) * share] or cpus
-    nprod = args.producers or max(1, min(12, len(mine) - 3))
+    # place each rank's producers on CPUs local to its GPU (same NUMA domain as
+    # the GPU's PCIe root: frames are written there and read back by the GPU)
+    from blendtorch.parallel import plan_rank_cpus
+    cpus, budget, pin = cpu_budget()
+    plan = plan_rank_cpus(local_rank, local_world, cpus[:budget] if pin else cpus)
+    share = max(1, budget // local_world)                 # CPUs this rank may keep busy
+    nprod = args.producers or max(1, min(12, share - 3))
     if args.dist == 'scatter':
-        # the root hosts every producer, pinned across the whole node
-        mine = cpus
+        # the root hosts every producer, spread across the whole node
+        plan = {'cpus': cpus[:budget] if pin else cpus, 'numa_local': False, 'domain': cpus}
         nprod = nprod * world if rank == 0 else 0
-    affinity = [[mine[i % len(mine)]] for i in range(nprod)] if pin else None
+    mine = plan['cpus']
+    if pin:
+        affinity = [[mine[i % len(mine)]] for i in range(nprod)]
+    elif plan['numa_local']:
+        affinity = [plan['domain']] * nprod               # soft: any core of the GPU's domain
+    else:
+        affinity = None
+    if plan['numa_local']:
+        os.sched_setaffinity(0, plan['domain'])           # loader threads next to the GPU too
     start_port = args.start_port or (20000 + (os.getpid() % 200) * 50 if world == 1 else 21000 + rank * 64)
 
     decode = DecodeConfig.unit(channels='rgb', gamma=2.2)
@@ -226,7 +234,8 @@ def main():
                 'seq_len': None,
                 'parallelism': f'dp{world}' + ('-scatter' if args.dist == 'scatter' else ''),
                 'producers_per_gpu': nprod // (world if args.dist == 'scatter' else 1),
-                'cpus_per_gpu': len(mine),
+                'cpus_per_gpu': share,
+                'numa_local': plan['numa_local'],
                 'decode': 'rgba->rgb, gamma 2.2, /255, HWC->CHW fp32 (gfx950 kernel)',
                 'out_shape': list(shape),
                 'proto': args.proto,

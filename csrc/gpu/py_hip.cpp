@@ -54,6 +54,11 @@ PYBIND11_MODULE(_hip, m) {
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
     return n;
   });
+  m.def("pci_bus_id", [](int dev) {
+    char buf[64] = {0};
+    check(hipDeviceGetPCIBusId(buf, int(sizeof(buf)), dev), "hipDeviceGetPCIBusId");
+    return std::string(buf);
+  });
   m.def("device_arch", [](int dev) {
     hipDeviceProp_t p;
     check(hipGetDeviceProperties(&p, dev), "hipGetDeviceProperties");

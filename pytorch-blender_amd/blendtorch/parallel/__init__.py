@@ -28,8 +28,10 @@ from typing import Dict, Iterable, List, Optional, Sequence
 import torch
 import torch.distributed as dist
 
-__all__ = ['init_distributed', 'rank_world', 'shard_addresses', 'partition_cpus', 'scatter_batch',
-           'broadcast_tensor', 'all_gather_stats', 'ScatterLoader', 'barrier']
+from .topology import parse_cpulist, plan_rank_cpus  # noqa: E402
+
+__all__ = ['init_distributed', 'rank_world', 'shard_addresses', 'partition_cpus', 'plan_rank_cpus', 'parse_cpulist',
+           'scatter_batch', 'broadcast_tensor', 'all_gather_stats', 'ScatterLoader', 'barrier']
 
 
 def rank_world():

@@ -156,3 +156,14 @@ def test_device_loader_direct_color4x4(dev, free_port):
             res[h2d] = list(dl)[-1]['image']
             assert dl.stats['direct_batches'] == (2 if h2d == 'auto' else 0)
     torch.testing.assert_close(res['auto'], res['copy'], rtol=0, atol=0)
+
+
+def test_gpu_topology_resolves(dev):
+    """hipDeviceGetPCIBusId -> sysfs local_cpulist gives the GPU's NUMA-local CPUs."""
+    import os
+    from blendtorch.parallel import topology
+    bid = topology.gpu_pci_bus_id(0)
+    assert bid and len(bid.split(':')) == 3, bid
+    plan = topology.plan_rank_cpus(0, 1, sorted(os.sched_getaffinity(0)))
+    assert plan['cpus'] and set(plan['cpus']) <= set(os.sched_getaffinity(0))
+    print('gpu0', bid, 'numa_local', plan['numa_local'], 'domain size', len(plan['domain']))

@@ -24,6 +24,45 @@ def test_partition_cpus():
     assert parts[0] == [0, 1, 2, 3] and parts[3] == [12, 13, 14, 15]
 
 
+def test_parse_cpulist():
+    assert parallel.parse_cpulist('0-3,8,10-11\n') == [0, 1, 2, 3, 8, 10, 11]
+    assert parallel.parse_cpulist('') == []
+
+
+def _fake_sysfs(root, layout):
+    for bdf, cpulist in layout.items():
+        (root / bdf).mkdir(parents=True)
+        (root / bdf / 'local_cpulist').write_text(cpulist + '\n')
+    return root
+
+
+def test_plan_rank_cpus_numa_local(tmp_path):
+    # 8 GPUs, 4 per socket; socket 0 = CPUs 0-31, socket 1 = CPUs 32-63
+    bus = [f'0000:{0x10 * (i + 1):02x}:00.0' for i in range(8)]
+    sysfs = _fake_sysfs(tmp_path, {b: ('0-31' if i < 4 else '32-63') for i, b in enumerate(bus)})
+    allowed = list(range(64))
+    plans = [parallel.plan_rank_cpus(r, 8, allowed, bus_ids=bus, sysfs=sysfs) for r in range(8)]
+    assert all(p['numa_local'] for p in plans)
+    assert plans[0]['cpus'] == list(range(0, 8)) and plans[3]['cpus'] == list(range(24, 32))
+    assert plans[4]['cpus'] == list(range(32, 40)) and plans[7]['domain'] == list(range(32, 64))
+    flat = sorted(c for p in plans for c in p['cpus'])
+    assert flat == allowed                          # disjoint, covering
+    # GPU order need not follow socket order: rank 0 on socket 1
+    sysfs2 = _fake_sysfs(tmp_path / 'b', {b: ('32-63' if i % 2 == 0 else '0-31') for i, b in enumerate(bus)})
+    p0 = parallel.plan_rank_cpus(0, 8, allowed, bus_ids=bus, sysfs=sysfs2)
+    assert p0['numa_local'] and set(p0['cpus']) <= set(range(32, 64))
+
+
+def test_plan_rank_cpus_fallback(tmp_path):
+    allowed = list(range(16))
+    p = parallel.plan_rank_cpus(1, 4, allowed, bus_ids=[None] * 4, sysfs=tmp_path)
+    assert not p['numa_local'] and p['cpus'] == [4, 5, 6, 7]
+    # local set disjoint from the allowed CPUs -> fallback
+    sysfs = _fake_sysfs(tmp_path / 'x', {'0000:01:00.0': '100-107'})
+    p = parallel.plan_rank_cpus(0, 1, allowed, bus_ids=['0000:01:00.0'], sysfs=sysfs)
+    assert not p['numa_local'] and p['cpus'] == allowed
+
+
 def _free_port():
     s = socket.socket()
     s.bind(('127.0.0.1', 0))
