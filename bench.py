@@ -95,6 +95,8 @@ def main():
                          'send descriptors; 0: images inline in the ZMTP messages')
     ap.add_argument('--h2d', choices=['auto', 'copy'], default='auto',
                     help='auto: decode kernel reads pinned host frames directly (zero-copy); copy: DMA first')
+    ap.add_argument('--launch-depth', type=int, default=2,
+                    help='direct-path decode launches queued before new batches coalesce into one launch')
     ap.add_argument('--start-port', type=int, default=0)
     ap.add_argument('--dist', choices=['shard', 'scatter'], default='shard',
                     help='shard: every rank owns its producers; scatter: rank 0 receives world*B per step '
@@ -164,7 +166,8 @@ def main():
             per_step = args.batch * (world if args.dist == 'scatter' else 1)
             dl = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=per_step, decode=decode, device=device,
                               max_items=total_batches * per_step, prefetch=6,
-                              io_threads=args.io_threads or None, timeoutms=60000, h2d=args.h2d)
+                              io_threads=args.io_threads or None, timeoutms=60000, h2d=args.h2d,
+                              launch_depth=args.launch_depth)
         if args.dist == 'scatter':
             it = iter(ScatterLoader(dl, args.batch, (3, 480, 640), torch.float32, device, total_batches))
         else:
@@ -242,11 +245,12 @@ def main():
                 'pinned_producers': pin,
                 'shm_slots': args.shm,
                 'h2d': args.h2d,
+                'launch_depth': args.launch_depth,
             },
             'sec_per_image': round(tmax / images, 7),
             'sec_per_batch': round(tmax / args.steps, 6),
             'loader_stats': {k: stats.get(k) for k in ('frames', 'batches', 'bad', 'pool_fallbacks', 'direct_batches',
-                                                       'shm_frames', 'shm_torn')},
+                                                       'launches', 'shm_frames', 'shm_torn')},
             'cpu': cpu,
         }), flush=True)
     if world > 1:

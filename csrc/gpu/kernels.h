@@ -45,6 +45,11 @@ struct DecodeParams {
   const int64_t* src_offsets = nullptr;
   const uint8_t* srcs[kMaxSrcs] = {};
   int nsrcs = 0;
+  // dsts[b] when ndsts == B: per-image output base (image b's Cout*H*W
+  // elements, contiguous in either layout) -- one launch can then decode
+  // images belonging to several consumer batches (launch coalescing).
+  void* dsts[kMaxSrcs] = {};
+  int ndsts = 0;
   int max_grid = 0;
   void* dst = nullptr;
   const float* lut = nullptr;
@@ -69,6 +74,8 @@ struct Color4x4Params {
   const int64_t* src_offsets = nullptr;
   const uint8_t* srcs[kMaxSrcs] = {};   // as DecodeParams::srcs
   int nsrcs = 0;
+  float* dsts[kMaxSrcs] = {};           // as DecodeParams::dsts
+  int ndsts = 0;
   float* dst = nullptr;
   const float* lut = nullptr;
   const float* M = nullptr;

@@ -42,6 +42,13 @@ __device__ __forceinline__ uint16_t f2h(float f) {
   return *reinterpret_cast<uint16_t*>(&h);
 }
 
+// Base of image b's output (elements of type T): per-image pointer when the
+// launch coalesces several batches, else the b-th slab of one dense tensor.
+template <typename T, typename P>
+__device__ __forceinline__ T* image_out(const P& p, int b, int64_t img_elems) {
+  return p.ndsts ? reinterpret_cast<T*>(p.dsts[b]) : reinterpret_cast<T*>(p.dst) + int64_t(b) * img_elems;
+}
+
 template <int PPT, int CIN>
 struct Pixels {
   uint8_t v[PPT * CIN];
@@ -88,7 +95,7 @@ template <int PPT, int CIN, int OUTT, int COUT>
 __device__ __forceinline__ void store_nhwc(const DecodeParams& p, const float* lut, const int* cm,
                                            const Pixels<PPT, CIN>& px, int b, int64_t q, int64_t HW) {
   constexpr int N = PPT * COUT;
-  const int64_t off = (int64_t(b) * HW + q) * COUT;
+  const int64_t off = q * COUT;   // within image b (NHWC)
   float v[COUT][PPT];
 #pragma unroll
   for (int c = 0; c < COUT; ++c) lookup<PPT, CIN>(px, cm[c], lut + c * 256, v[c]);
@@ -98,7 +105,7 @@ __device__ __forceinline__ void store_nhwc(const DecodeParams& p, const float* l
     for (int i = 0; i < PPT; ++i)
 #pragma unroll
       for (int c = 0; c < COUT; ++c) o[i * COUT + c] = v[c][i];
-    float4* d = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.dst) + off);
+    float4* d = reinterpret_cast<float4*>(image_out<float>(p, b, HW * COUT) + off);
 #pragma unroll
     for (int i = 0; i < N / 4; ++i) d[i] = make_float4(o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]);
   } else if constexpr (OUTT == OUT_BF16 || OUTT == OUT_F16) {
@@ -107,7 +114,7 @@ __device__ __forceinline__ void store_nhwc(const DecodeParams& p, const float* l
     for (int i = 0; i < PPT; ++i)
 #pragma unroll
       for (int c = 0; c < COUT; ++c) o[i * COUT + c] = OUTT == OUT_BF16 ? f2bf(v[c][i]) : f2h(v[c][i]);
-    uint4* d = reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(p.dst) + off);
+    uint4* d = reinterpret_cast<uint4*>(image_out<uint16_t>(p, b, HW * COUT) + off);
 #pragma unroll
     for (int i = 0; i < N / 8; ++i) d[i] = *reinterpret_cast<const uint4*>(&o[8 * i]);
   } else {
@@ -116,7 +123,7 @@ __device__ __forceinline__ void store_nhwc(const DecodeParams& p, const float* l
     for (int i = 0; i < PPT; ++i)
 #pragma unroll
       for (int c = 0; c < COUT; ++c) o[i * COUT + c] = uint8_t(v[c][i]);
-    uint4* d = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(p.dst) + off);
+    uint4* d = reinterpret_cast<uint4*>(image_out<uint8_t>(p, b, HW * COUT) + off);
 #pragma unroll
     for (int i = 0; i < N / 16; ++i) d[i] = *reinterpret_cast<const uint4*>(&o[16 * i]);
   }
@@ -153,23 +160,23 @@ __global__ __launch_bounds__(kBlock) void decode_vec_kernel(DecodeParams p) {
         if (c >= cout) break;
         float v[PPT];
         lookup<PPT, CIN>(px, cm[c], lut + c * 256, v);
-        const int64_t off = (int64_t(b) * cout + c) * HW + q;
+        const int64_t off = int64_t(c) * HW + q;   // within image b (NCHW)
         if constexpr (OUTT == OUT_F32) {
-          float* d = reinterpret_cast<float*>(p.dst) + off;
+          float* d = image_out<float>(p, b, HW * cout) + off;
 #pragma unroll
           for (int i = 0; i < PPT / 4; ++i) reinterpret_cast<float4*>(d)[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
         } else if constexpr (OUTT == OUT_BF16 || OUTT == OUT_F16) {
           uint16_t o[PPT];
 #pragma unroll
           for (int i = 0; i < PPT; ++i) o[i] = OUTT == OUT_BF16 ? f2bf(v[i]) : f2h(v[i]);
-          uint16_t* d = reinterpret_cast<uint16_t*>(p.dst) + off;
+          uint16_t* d = image_out<uint16_t>(p, b, HW * cout) + off;
 #pragma unroll
           for (int i = 0; i < PPT / 8; ++i) reinterpret_cast<uint4*>(d)[i] = *reinterpret_cast<const uint4*>(&o[8 * i]);
         } else {
           uint8_t o[PPT];
 #pragma unroll
           for (int i = 0; i < PPT; ++i) o[i] = uint8_t(v[i]);
-          uint8_t* d = reinterpret_cast<uint8_t*>(p.dst) + off;
+          uint8_t* d = image_out<uint8_t>(p, b, HW * cout) + off;
 #pragma unroll
           for (int i = 0; i < PPT / 16; ++i) reinterpret_cast<uint4*>(d)[i] = *reinterpret_cast<const uint4*>(&o[16 * i]);
         }
@@ -205,11 +212,12 @@ __global__ __launch_bounds__(kBlock) void decode_scalar_kernel(DecodeParams p) {
     const uint8_t* s = img + (int64_t(sy) * p.W + x) * p.Cin;
     for (int c = 0; c < p.Cout; ++c) {
       float v = lut[c * 256 + s[p.cmap[c]]];
-      int64_t off = p.layout == NCHW ? (int64_t(b) * p.Cout + c) * HW + q : (int64_t(b) * HW + q) * p.Cout + c;
-      if constexpr (OUTT == OUT_F32) reinterpret_cast<float*>(p.dst)[off] = v;
-      else if constexpr (OUTT == OUT_BF16) reinterpret_cast<uint16_t*>(p.dst)[off] = f2bf(v);
-      else if constexpr (OUTT == OUT_F16) reinterpret_cast<uint16_t*>(p.dst)[off] = f2h(v);
-      else reinterpret_cast<uint8_t*>(p.dst)[off] = uint8_t(v);
+      const int64_t off = p.layout == NCHW ? int64_t(c) * HW + q : q * p.Cout + c;   // within image b
+      const int64_t ie = HW * p.Cout;
+      if constexpr (OUTT == OUT_F32) image_out<float>(p, b, ie)[off] = v;
+      else if constexpr (OUTT == OUT_BF16) image_out<uint16_t>(p, b, ie)[off] = f2bf(v);
+      else if constexpr (OUTT == OUT_F16) image_out<uint16_t>(p, b, ie)[off] = f2h(v);
+      else image_out<uint8_t>(p, b, ie)[off] = uint8_t(v);
     }
   }
 }
@@ -219,6 +227,14 @@ int grid_for(int64_t work, int cap = 0) {
   if (cap <= 0) cap = 2048;
   int64_t blocks = (work + kBlock - 1) / kBlock;
   return int(blocks < cap ? (blocks > 0 ? blocks : 1) : cap);
+}
+
+template <typename T>
+bool dsts_ok(T* const* dsts, int n, int B, uintptr_t align) {
+  if (n != B) return false;
+  for (int b = 0; b < n; ++b)
+    if (!dsts[b] || (reinterpret_cast<uintptr_t>(dsts[b]) % align) != 0) return false;
+  return true;
 }
 
 bool srcs_ok(const uint8_t* const* srcs, int n, int B, uintptr_t align) {
@@ -244,8 +260,8 @@ hipError_t launch_out(const DecodeParams& p, hipStream_t s) {
   // vector path: a lane's PPT pixels sit in one row and its loads are aligned
   const bool src_aligned = p.nsrcs ? srcs_ok(p.srcs, p.nsrcs, p.B, 16)
                                    : (reinterpret_cast<uintptr_t>(p.src) % 16) == 0 && p.src_offsets == nullptr;
-  bool aligned = (p.W % PPT) == 0 && (int64_t(p.H) * p.W * p.Cin) % 16 == 0 && (reinterpret_cast<uintptr_t>(p.dst) % 16) == 0 &&
-                 src_aligned;
+  const bool dst_aligned = p.ndsts ? dsts_ok(p.dsts, p.ndsts, p.B, 16) : (reinterpret_cast<uintptr_t>(p.dst) % 16) == 0;
+  bool aligned = (p.W % PPT) == 0 && (int64_t(p.H) * p.W * p.Cin) % 16 == 0 && dst_aligned && src_aligned;
   if (aligned && p.Cin == 4) return launch_vec<PPT, 4, OUTT>(p, s);
   if (aligned && p.Cin == 3) return launch_vec<PPT, 3, OUTT>(p, s);
   int64_t work = int64_t(p.B) * p.H * p.W;
@@ -259,6 +275,7 @@ hipError_t decode(const DecodeParams& p, hipStream_t stream) {
   if (p.B <= 0 || p.H <= 0 || p.W <= 0) return hipSuccess;
   if (p.Cout < 1 || p.Cout > 4 || p.Cin < 1 || p.Cin > 4) return hipErrorInvalidValue;
   if (p.nsrcs && (p.nsrcs != p.B || p.nsrcs > kMaxSrcs || !srcs_ok(p.srcs, p.nsrcs, p.B, 1))) return hipErrorInvalidValue;
+  if (p.ndsts && (p.ndsts != p.B || p.ndsts > kMaxSrcs || !dsts_ok(p.dsts, p.ndsts, p.B, 1))) return hipErrorInvalidValue;
   for (int c = 0; c < p.Cout; ++c)
     if (p.cmap[c] < 0 || p.cmap[c] >= p.Cin) return hipErrorInvalidValue;
   switch (p.out_dtype) {
@@ -329,7 +346,7 @@ __global__ __launch_bounds__(kBlock) void color4x4_kernel(Color4x4Params p) {
     }
     if (j < p.Cout) {
       // pixel 64*r + 4*blk + s  <-  acc[s][r]
-      float* d = p.dst + (int64_t(b) * p.Cout + j) * HW + q0 + 4 * blk;
+      float* d = image_out<float>(p, b, HW * p.Cout) + int64_t(j) * HW + q0 + 4 * blk;
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         *reinterpret_cast<float4*>(d + 64 * r) = make_float4(acc[0][r], acc[1][r], acc[2][r], acc[3][r]);
@@ -361,7 +378,8 @@ __global__ void project_kernel(const float* pts, int64_t N, const float* PV, con
 
 hipError_t color4x4(const Color4x4Params& p, hipStream_t stream) {
   if (p.B <= 0) return hipSuccess;
-  if ((int64_t(p.H) * p.W) % 256 != 0 || p.W % 4 != 0 || p.Cout < 1 || p.Cout > 4 || (reinterpret_cast<uintptr_t>(p.dst) % 16) != 0 ||
+  if ((int64_t(p.H) * p.W) % 256 != 0 || p.W % 4 != 0 || p.Cout < 1 || p.Cout > 4 ||
+      (p.ndsts ? !dsts_ok(p.dsts, p.ndsts, p.B, 16) : (reinterpret_cast<uintptr_t>(p.dst) % 16) != 0) ||
       (p.nsrcs ? !srcs_ok(p.srcs, p.nsrcs, p.B, 16) : (reinterpret_cast<uintptr_t>(p.src) % 16) != 0))
     return hipErrorInvalidValue;
   int64_t waves = int64_t(p.B) * p.H * p.W / 256;

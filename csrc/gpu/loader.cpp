@@ -200,6 +200,13 @@ void StreamLoader::stop() {
   for (auto& it : cur_)
     if (it.seg) it.seg->release(it.slot, it.gen);
   cur_.clear();
+  for (auto& b : pending_) {
+    for (auto& it : b.items)
+      if (it.seg) it.seg->release(it.slot, it.gen);
+    if (b.ready) (void)hipEventDestroy(b.ready);
+  }
+  pending_.clear();
+  pending_images_ = 0;
   for (auto& kv : segments_) (void)hipHostUnregister(kv.second.seg->base());
   segments_.clear();
   {
@@ -240,11 +247,12 @@ void StreamLoader::run() {
     try {
       // with copies in flight, wake up often enough to recycle their slots
       // promptly (producers / IO threads may be waiting for them)
-      ev = zmtp::Socket::poll(items, inflight_.empty() ? 100 : 1, intr);
+      ev = zmtp::Socket::poll(items, inflight_.empty() && pending_.empty() ? 100 : 1, intr);
     } catch (const zmtp::Error& e) {
       if (e.code == zmtp::E_INTR) break;
       throw;
     }
+    flush_pending(max_frames >= 0 && taken >= max_frames);
     for (size_t i = 0; i < ev.size() && !stop_; ++i) {
       if (!(ev[i] & zmtp::POLLIN)) continue;
       // drain what is queued on this socket (bounded, to stay fair)
@@ -261,6 +269,7 @@ void StreamLoader::run() {
       }
     }
   }
+  if (!stop_) flush_pending(true);   // stream complete: nothing more will join the pending batches
   std::lock_guard<std::mutex> lk(mu_);
   exhausted_ = true;
 }
@@ -440,14 +449,18 @@ void StreamLoader::reap(bool wait_all) {
   }
 }
 
+// One batch of B frames is complete: bind it to the next consumer-posted
+// output buffer and queue it for launch.
 void StreamLoader::launch() {
-  trace::Range tr("btn.loader.launch");
+  trace::Range tr("btn.loader.assemble");
   Posted p{nullptr, nullptr};
   {
     std::unique_lock<std::mutex> lk(mu_);
     while (posted_.empty() && !stop_) {
       lk.unlock();
-      reap();
+      // out of output buffers: the consumer is waiting for batches, so
+      // holding assembled ones back for coalescing would only stall it
+      flush_pending(true);
       lk.lock();
       if (!posted_.empty() || stop_) break;
       cv_.wait_for(lk, std::chrono::milliseconds(2));
@@ -456,57 +469,131 @@ void StreamLoader::launch() {
     p = posted_.front();
     posted_.pop_front();
   }
+  Pending pb;
+  pb.dst = p.dst;
+  pb.ready = p.ready;
+  pb.t0 = batch_t0_;
+  pb.direct = cfg_.direct && int(cur_.size()) <= kMaxSrcs;
+  for (auto& it : cur_)
+    pb.direct = pb.direct && it.dsrc && (reinterpret_cast<uintptr_t>(it.dsrc) % 16) == 0;
+  pb.items = std::move(cur_);
+  cur_.clear();
+  pending_images_ += int(pb.items.size());
+  pending_.push_back(std::move(pb));
+  flush_pending(false);
+}
+
+// Launch coalescing: a direct-path batch launches at once while fewer than
+// kMaxInflight launches are queued on the loader stream; otherwise it waits,
+// and when a launch retires every waiting batch goes out in ONE kernel
+// (per-image source/destination pointers).  When the GPU side is the
+// bottleneck the launches therefore grow -- fewer ramp-up/tail phases per
+// image -- and when the producers are, every batch still launches at once.
+void StreamLoader::flush_pending(bool force) {
+  if (pending_.empty()) return;
+  reap();
+  const bool room = int(inflight_.size()) < cfg_.launch_depth;
+  const bool full = pending_images_ + cfg_.batch_size > kMaxSrcs;
+  const bool copy_waiting = std::any_of(pending_.begin(), pending_.end(), [](const Pending& b) { return !b.direct; });
+  if (!(force || room || full || copy_waiting)) return;
+  // maximal runs of direct batches go out together; copy-path batches one by one
+  std::vector<Pending> group;
+  auto emit = [&] {
+    if (!group.empty()) launch_group(group);
+    group.clear();
+  };
+  while (!pending_.empty()) {
+    Pending b = std::move(pending_.front());
+    pending_.pop_front();
+    if (!b.direct) {
+      emit();
+      group.push_back(std::move(b));
+      emit();
+    } else {
+      group.push_back(std::move(b));
+    }
+  }
+  emit();
+  pending_images_ = 0;
+}
+
+void StreamLoader::launch_group(std::vector<Pending>& group) {
+  trace::Range tr("btn.loader.launch");
   const double t_issue = now_ms();
-  const int B = int(cur_.size());
-  uint8_t* stage = staging_[size_t(batch_index_) % staging_.size()];
-  check(hipStreamWaitEvent(stream_, p.ready, 0), "hipStreamWaitEvent(post)");
-  (void)hipEventDestroy(p.ready);
+  const bool direct = group.front().direct;
+  int total = 0;
+  for (auto& b : group) {
+    check(hipStreamWaitEvent(stream_, b.ready, 0), "hipStreamWaitEvent(post)");
+    (void)hipEventDestroy(b.ready);
+    total += int(b.items.size());
+  }
+  const int B = cfg_.batch_size;
+  const size_t elem = cfg_.color_matrix ? 4 : (cfg_.out_dtype == OUT_F32 ? 4 : (cfg_.out_dtype == OUT_U8 ? 1 : 2));
+  const int cout = cfg_.color_matrix ? 4 : cfg_.cout;
+  const size_t out_img_bytes = size_t(H_) * W_ * cout * elem;
   uint64_t flips[4] = {0, 0, 0, 0};
-  // direct: the kernel reads every frame from pinned host memory itself
-  bool direct = cfg_.direct && B <= kMaxSrcs;
-  for (int i = 0; i < B && direct; ++i)
-    direct = cur_[size_t(i)].dsrc && (reinterpret_cast<uintptr_t>(cur_[size_t(i)].dsrc) % 16) == 0;
-  for (int i = 0; i < B; ++i) {
-    const Item& it = cur_[size_t(i)];
-    if (!direct)
-      check(hipMemcpyAsync(stage + size_t(i) * img_bytes_, it.src, img_bytes_, hipMemcpyHostToDevice, stream_),
+  std::vector<const Item*> all;
+  all.reserve(size_t(total));
+  for (auto& b : group)
+    for (auto& it : b.items) all.push_back(&it);
+  for (int i = 0; i < total; ++i)
+    if (all[size_t(i)]->flip) {
+      if (i >= 256) throw std::runtime_error("StreamLoader: per-image flip supports batch <= 256");
+      flips[i >> 6] |= uint64_t(1) << (i & 63);
+    }
+  uint8_t* stage = nullptr;
+  if (!direct) {   // copy path: exactly one batch per launch
+    stage = staging_[size_t(batch_index_) % staging_.size()];
+    for (int i = 0; i < total; ++i)
+      check(hipMemcpyAsync(stage + size_t(i) * img_bytes_, all[size_t(i)]->src, img_bytes_, hipMemcpyHostToDevice,
+                           stream_),
             "hipMemcpyAsync(H2D)");
-    if (it.flip && i < 256) flips[i >> 6] |= uint64_t(1) << (i & 63);
   }
   // `copied` marks the last device read of the host slots: after the copies,
   // or (direct) after the kernel that reads them
   hipEvent_t copied;
   check(hipEventCreateWithFlags(&copied, hipEventDisableTiming), "hipEventCreate(copied)");
   if (!direct) check(hipEventRecord(copied, stream_), "hipEventRecord(copied)");
-  bool any_flip_beyond = false;
-  for (int i = 256; i < B; ++i) any_flip_beyond |= cur_[size_t(i)].flip;
-  if (any_flip_beyond) throw std::runtime_error("StreamLoader: per-image flip supports batch <= 256");
+  const bool per_image_dst = group.size() > 1;
   hipError_t e;
   if (cfg_.color_matrix) {
     Color4x4Params cp;
     cp.src = stage;
+    cp.dst = static_cast<float*>(group.front().dst);
     if (direct) {
-      cp.nsrcs = B;
-      for (int i = 0; i < B; ++i) cp.srcs[i] = cur_[size_t(i)].dsrc;
+      cp.nsrcs = total;
+      for (int i = 0; i < total; ++i) cp.srcs[i] = all[size_t(i)]->dsrc;
     }
-    cp.dst = static_cast<float*>(p.dst);
+    if (per_image_dst) {
+      cp.ndsts = total;
+      int i = 0;
+      for (auto& b : group)
+        for (size_t k = 0; k < b.items.size(); ++k)
+          cp.dsts[i++] = reinterpret_cast<float*>(static_cast<uint8_t*>(b.dst) + k * out_img_bytes);
+    }
     cp.lut = d_lut_;
     cp.M = d_mat_;
     cp.bias = d_mat_ + 16;
-    cp.B = B, cp.H = H_, cp.W = W_, cp.Cout = cfg_.cout;
+    cp.B = total, cp.H = H_, cp.W = W_, cp.Cout = cfg_.cout;
     cp.flip_all = cfg_.flip_all;
     std::memcpy(cp.flip_bits, flips, sizeof(flips));
     e = color4x4(cp, stream_);
   } else {
     DecodeParams dp;
     dp.src = stage;
+    dp.dst = group.front().dst;
     if (direct) {
-      dp.nsrcs = B;
-      for (int i = 0; i < B; ++i) dp.srcs[i] = cur_[size_t(i)].dsrc;
+      dp.nsrcs = total;
+      for (int i = 0; i < total; ++i) dp.srcs[i] = all[size_t(i)]->dsrc;
     }
-    dp.dst = p.dst;
+    if (per_image_dst) {
+      dp.ndsts = total;
+      int i = 0;
+      for (auto& b : group)
+        for (size_t k = 0; k < b.items.size(); ++k) dp.dsts[i++] = static_cast<uint8_t*>(b.dst) + k * out_img_bytes;
+    }
     dp.lut = d_lut_;
-    dp.B = B, dp.H = H_, dp.W = W_, dp.Cin = C_, dp.Cout = cfg_.cout;
+    dp.B = total, dp.H = H_, dp.W = W_, dp.Cin = C_, dp.Cout = cfg_.cout;
     std::memcpy(dp.cmap, cfg_.cmap, sizeof(dp.cmap));
     dp.flip_all = cfg_.flip_all;
     std::memcpy(dp.flip_bits, flips, sizeof(flips));
@@ -517,30 +604,34 @@ void StreamLoader::launch() {
   check(e, "decode kernel launch");
   if (direct) check(hipEventRecord(copied, stream_), "hipEventRecord(copied)");
   Inflight fl;
-  fl.frames.reserve(size_t(B));
-  ReadyBatch rb;
-  rb.index = batch_index_;
-  rb.items.reserve(size_t(B));
-  for (auto& it : cur_) {
-    fl.frames.push_back(std::move(it.frame));
-    if (it.seg) fl.slots.push_back({it.seg, it.slot, it.gen});
-    rb.items.push_back(std::move(it.meta));
+  fl.frames.reserve(size_t(total));
+  std::vector<ReadyBatch> done;
+  for (auto& b : group) {
+    ReadyBatch rb;
+    rb.index = batch_index_++;
+    rb.items.reserve(b.items.size());
+    for (auto& it : b.items) {
+      fl.frames.push_back(std::move(it.frame));
+      if (it.seg) fl.slots.push_back({it.seg, it.slot, it.gen});
+      rb.items.push_back(std::move(it.meta));
+    }
+    check(hipEventCreateWithFlags(&rb.done, hipEventDisableTiming), "hipEventCreate(done)");
+    check(hipEventRecord(rb.done, stream_), "hipEventRecord(done)");
+    rb.recv_ms = t_issue - b.t0;
+    done.push_back(std::move(rb));
   }
-  cur_.clear();
   fl.copied = copied;
   inflight_.push_back(std::move(fl));
-  check(hipEventCreateWithFlags(&rb.done, hipEventDisableTiming), "hipEventCreate(done)");
-  check(hipEventRecord(rb.done, stream_), "hipEventRecord(done)");
-  rb.recv_ms = t_issue - batch_t0_;
+  (void)B;
   {
     std::lock_guard<std::mutex> lk(mu_);
-    stats_.batches++;
-    if (direct) stats_.direct_batches++;
+    stats_.batches += group.size();
+    stats_.launches++;
+    if (direct) stats_.direct_batches += group.size();
     stats_.h2d_issue_ms += now_ms() - t_issue;
-    ready_.push_back(std::move(rb));
+    for (auto& rb : done) ready_.push_back(std::move(rb));
   }
   cv_.notify_all();
-  ++batch_index_;
 }
 
 }  // namespace gpu

@@ -99,6 +99,9 @@ struct LoaderConfig {
   // ~45 GB/s vs ~35 GB/s for per-frame DMA copies + decode on MI355X);
   // false: always DMA into the device staging ring first.
   bool direct = true;
+  // Direct-path launches queued on the loader stream before new batches wait
+  // and coalesce into one launch (0: always hold until 64 images or stream end).
+  int launch_depth = 2;
   // decode parameters (src/dst/B/H/W/Cin filled per batch)
   int cout = 3;
   int cmap[4] = {0, 1, 2, 3};
@@ -128,6 +131,7 @@ struct LoaderStats {
   uint64_t frames = 0, batches = 0, bytes = 0, bad = 0, pool_fallbacks = 0;
   uint64_t shm_frames = 0, shm_torn = 0;   // via shared memory / slot reclaimed during the copy
   uint64_t direct_batches = 0;             // decoded straight from host memory (no staging copy)
+  uint64_t launches = 0;                   // decode kernel launches (< batches when coalesced)
   double h2d_issue_ms = 0;
 };
 
@@ -166,7 +170,16 @@ class StreamLoader {
   };
   void run();
   bool process(zmtp::Message&& msg);
+  struct Pending {                    // assembled batch waiting for launch
+    std::vector<Item> items;
+    void* dst = nullptr;
+    hipEvent_t ready = nullptr;
+    double t0 = 0;
+    bool direct = false;
+  };
   void launch();
+  void flush_pending(bool force);
+  void launch_group(std::vector<Pending>& group);
   void reap(bool wait_all = false);   // release pinned slots of completed H2D copies
 
   LoaderConfig cfg_;
@@ -192,6 +205,8 @@ class StreamLoader {
   float* d_lut_ = nullptr;
   float* d_mat_ = nullptr;   // 16 matrix + 4 bias
   std::vector<Item> cur_;
+  std::deque<Pending> pending_;
+  int pending_images_ = 0;
   struct Inflight {
     hipEvent_t copied;
     std::vector<zmtp::Frame> frames;

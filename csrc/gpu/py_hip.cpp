@@ -276,9 +276,10 @@ PYBIND11_MODULE(_hip, m) {
                        int io_threads, int device, int64_t max_batches, size_t max_frame_bytes, int pool_slots,
                        int staging_depth, bool skip_bad, int cout, std::vector<int> cmap, int flip_all,
                        int out_dtype, int layout, std::vector<float> lut, std::vector<float> matrix,
-                       std::vector<float> bias, bool direct) {
+                       std::vector<float> bias, bool direct, int launch_depth) {
              LoaderConfig c;
              c.direct = direct;
+             c.launch_depth = launch_depth;
              c.addresses = std::move(addresses);
              c.batch_size = batch_size;
              c.image_key = std::move(image_key);
@@ -305,7 +306,7 @@ PYBIND11_MODULE(_hip, m) {
            py::arg("io_threads"), py::arg("device"), py::arg("max_batches"), py::arg("max_frame_bytes"),
            py::arg("pool_slots"), py::arg("staging_depth"), py::arg("skip_bad"), py::arg("cout"), py::arg("cmap"),
            py::arg("flip_all"), py::arg("out_dtype"), py::arg("layout"), py::arg("lut"), py::arg("matrix"),
-           py::arg("bias"), py::arg("direct") = true)
+           py::arg("bias"), py::arg("direct") = true, py::arg("launch_depth") = 2)
       .def("start", &StreamLoader::start)
       .def("wait_shape",
            [](StreamLoader& l, long timeout_ms) -> py::object {
@@ -358,6 +359,7 @@ PYBIND11_MODULE(_hip, m) {
         d["shm_frames"] = s.shm_frames;
         d["shm_torn"] = s.shm_torn;
         d["direct_batches"] = s.direct_batches;
+        d["launches"] = s.launches;
         return d;
       });
 }

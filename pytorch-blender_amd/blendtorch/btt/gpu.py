@@ -74,15 +74,23 @@ class DeviceLoader:
         loader's pinned receive slots) the decode kernel reads them over PCIe
         itself -- one fused pass, no staging copy; otherwise the frames are
         DMA'd into a device staging ring first.  ``'copy'``: always DMA.
+    launch_depth: int
+        Direct-path decode launches the loader keeps queued on its stream.
+        Batches completing while that many are in flight wait and go out
+        together in one launch (fewer kernel ramp-up/tail phases when the GPU
+        side is the bottleneck).  0: hold batches until 64 images are pending
+        or the stream ends (tests / maximal coalescing).
     """
 
     def __init__(self, addresses: Sequence[str], batch_size: int = 8, decode: DecodeConfig = DecodeConfig(),
                  device=None, max_items: Optional[int] = None, timeoutms: int = DEFAULT_TIMEOUTMS,
                  rcvhwm: int = 10, prefetch: int = 4, io_threads: Optional[int] = None, image_key: str = 'image',
-                 skip_bad: bool = False, meta_to_device: bool = False, staging_depth: int = 3, h2d: str = 'auto'):
+                 skip_bad: bool = False, meta_to_device: bool = False, staging_depth: int = 3, h2d: str = 'auto',
+                 launch_depth: int = 2):
         if h2d not in ('auto', 'copy'):
             raise ValueError("h2d must be 'auto' or 'copy'")
         self.h2d = h2d
+        self.launch_depth = int(launch_depth)
         if isinstance(addresses, str):
             addresses = [addresses]
         self.addresses = list(addresses)
@@ -127,7 +135,7 @@ class DeviceLoader:
             self.addresses, self.batch_size, self.image_key, self.rcvhwm, self.io_threads, self.device.index,
             max_batches, 0, 0, self.staging_depth, self.skip_bad, cfg.cout, list(cfg.cmap) + [0] * (4 - len(cfg.cmap)),
             int(cfg.flip), ops.OUT_DTYPES[cfg.dtype], ops.LAYOUTS[cfg.layout], lut, matrix, bias,
-            self.h2d == 'auto')
+            self.h2d == 'auto', self.launch_depth)
 
     def _post(self, loader, stream):
         out = torch.empty(self.decode.out_shape(self.batch_size, *self.shape[:2]), dtype=self.decode.torch_dtype(),

@@ -167,3 +167,28 @@ def test_gpu_topology_resolves(dev):
     plan = topology.plan_rank_cpus(0, 1, sorted(os.sched_getaffinity(0)))
     assert plan['cpus'] and set(plan['cpus']) <= set(os.sched_getaffinity(0))
     print('gpu0', bid, 'numa_local', plan['numa_local'], 'domain size', len(plan['domain']))
+
+
+@pytest.mark.parametrize('dtype,layout', [('float32', 'nchw'), ('bfloat16', 'nhwc'), ('uint8', 'nchw')])
+def test_device_loader_coalesced_launch(dev, free_port, dtype, layout):
+    """launch_depth=0 holds direct-path batches until 64 images are pending:
+    8 batches of 8 decode in ONE launch through per-image source/destination
+    pointers, bit-exact with the one-copy-per-batch path."""
+    cfg = (ops.DecodeConfig.unit(channels='rgb', gamma=2.2, dtype=dtype, layout=layout) if dtype != 'uint8'
+           else ops.DecodeConfig(channels='rgb', gamma=2.2, dtype=dtype, layout=layout))
+    args = ['--mode', 'rgba', '--rotation', '0.3', '0.5', '0.7', '--shm', '48']   # ring > 32 held frames
+    res = {}
+    for i, (h2d, depth) in enumerate((('auto', 0), ('copy', 2))):
+        with btt.BlenderLauncher(producer='cubesim', num_instances=2, named_sockets=['DATA'],
+                                 start_port=free_port + 5 * i, proto='ipc', instance_args=[args] * 2) as bl:
+            dl = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=8, max_items=64, decode=cfg, device=dev,
+                              h2d=h2d, launch_depth=depth, prefetch=8)
+            res[h2d] = [b['image'].clone() for b in dl]
+            st = dl.stats
+        assert len(res[h2d]) == 8
+        if h2d == 'auto':
+            assert st['direct_batches'] == 8 and st['launches'] == 1, st
+        else:
+            assert st['launches'] == 8 and st['direct_batches'] == 0
+    for a, b in zip(res['auto'], res['copy']):
+        assert torch.equal(a, b)
