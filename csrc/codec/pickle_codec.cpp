@@ -551,7 +551,7 @@ void Writer::end_list() {
   op(APPENDS);
 }
 
-size_t Writer::ndarray(const std::string& code, const std::vector<int64_t>& shape, const void* data) {
+size_t Writer::ndarray(const std::string& code, const std::vector<int64_t>& shape, const void* data, size_t align) {
   size_t item = size_t(std::stoul(code.substr(1)));
   char bo = (item == 1 || code[0] == 'b') ? '|' : '<';
   size_t n = item;
@@ -591,6 +591,16 @@ size_t Writer::ndarray(const std::string& code, const std::vector<int64_t>& shap
   op(TUPLE_);
   op(BUILD);
   op(NEWFALSE);
+  if (align > 1) {
+    const size_t hdr = n < 256 ? 2 : (n <= 0xffffffffu ? 5 : 9);
+    size_t pad = (align - (out_.size() + hdr) % align) % align;
+    if (pad == 1) pad += align;                 // 1 byte is not expressible; 2a + 3b covers the rest
+    if (pad % 2) {
+      op(BININT1), op(0), op(POP);              // 3-byte no-op
+      pad -= 3;
+    }
+    for (; pad; pad -= 2) op(NONE_), op(POP);   // 2-byte no-op
+  }
   bytes(nullptr, n);
   size_t payload = out_.size() - n;
   if (data) std::memcpy(out_.data() + payload, data, n);

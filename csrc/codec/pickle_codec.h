@@ -112,8 +112,13 @@ class Writer {
   // ndarray in C order.  dtype like "u1", "f8", "f4", "i8"; byteorder '|' for
   // single-byte types, '<' otherwise.  Returns the payload offset; the caller
   // writes `nbytes` at out.data() + offset (after finish()).
+  // align > 1: pad with pickle no-ops (NONE+POP, BININT1+POP) so that the
+  // payload starts at a multiple of `align` from the start of the pickle --
+  // a receiver that lands the frame body at an aligned address (the GPU
+  // loader's pinned slots) can then hand the payload to vector loads as is.
+  // The unpickled value is unchanged.
   size_t ndarray(const std::string& dtype, const std::vector<int64_t>& shape,
-                 const void* data = nullptr);
+                 const void* data = nullptr, size_t align = 0);
   Bytes& finish();
   Bytes& buffer() { return out_; }
 

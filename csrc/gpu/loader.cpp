@@ -325,6 +325,13 @@ bool StreamLoader::process(zmtp::Message&& msg) {
     h = int(d.items[3]->i), w = int(d.items[4]->i), c = int(d.items[5]->i);
     if (it.slot >= it.seg->nslots() || off < 0 || size_t(off) + size_t(h) * w * c > it.seg->size())
       return bad("_btshm descriptor out of range");
+    if (!it.seg->valid(it.slot, it.gen)) {
+      // the producer reclaimed the slot (lease expired while this descriptor
+      // sat in a queue): its bytes are another frame's now -- drop it
+      std::lock_guard<std::mutex> lk(mu_);
+      stats_.shm_stale++;
+      return false;
+    }
     it.src = it.seg->base() + off;
     if (dev_base) it.dsrc = dev_base + off;
     root->items.erase(root->items.begin() + long(shm_idx), root->items.begin() + long(shm_idx) + 2);

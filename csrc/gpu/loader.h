@@ -130,6 +130,7 @@ struct ReadyBatch {
 struct LoaderStats {
   uint64_t frames = 0, batches = 0, bytes = 0, bad = 0, pool_fallbacks = 0;
   uint64_t shm_frames = 0, shm_torn = 0;   // via shared memory / slot reclaimed during the copy
+  uint64_t shm_stale = 0;                  // descriptors dropped: slot already reclaimed on arrival
   uint64_t direct_batches = 0;             // decoded straight from host memory (no staging copy)
   uint64_t launches = 0;                   // decode kernel launches (< batches when coalesced)
   double h2d_issue_ms = 0;

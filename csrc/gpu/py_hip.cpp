@@ -358,6 +358,7 @@ PYBIND11_MODULE(_hip, m) {
         d["h2d_issue_ms"] = s.h2d_issue_ms;
         d["shm_frames"] = s.shm_frames;
         d["shm_torn"] = s.shm_torn;
+        d["shm_stale"] = s.shm_stale;
         d["direct_batches"] = s.direct_batches;
         d["launches"] = s.launches;
         return d;

@@ -222,7 +222,7 @@ class NativeError(Exception):
     return py::bytes(reinterpret_cast<const char*>(h.data()), h.size());
   });
   m.def("dumps_array_dict",
-        [](const py::dict& d, int protocol) {
+        [](const py::dict& d, int protocol, size_t align) {
           // Minimal writer used by tests/producers: str keys; values int, float,
           // str, bool, None or C-contiguous ndarray.
           codec::Writer w(protocol);
@@ -240,7 +240,7 @@ class NativeError(Exception):
               a = py::array::ensure(a, py::array::c_style);
               std::string ds = py::str(a.dtype().attr("str"));
               std::vector<int64_t> shape(a.shape(), a.shape() + a.ndim());
-              w.ndarray(ds.substr(1), shape, a.data());
+              w.ndarray(ds.substr(1), shape, a.data(), align);
             } else {
               throw py::type_error("dumps_array_dict: unsupported value type");
             }
@@ -249,7 +249,7 @@ class NativeError(Exception):
           auto& out = w.finish();
           return py::bytes(reinterpret_cast<const char*>(out.data()), out.size());
         },
-        py::arg("d"), py::arg("protocol") = 4);
+        py::arg("d"), py::arg("protocol") = 4, py::arg("align") = 0);
 
   // ---- headless renderer (used by the bpy shim's GPUOffScreen) ----
   m.def("render_boxes",

@@ -226,7 +226,7 @@ codec::Bytes encode(const Ctx& c, double prev_action_value) {
   w.integer(c.time);
   if (c.has_rgb) {
     w.key("rgb_array");
-    w.ndarray("u1", {c.rgb_h, c.rgb_w, 3}, c.rgb.data());
+    w.ndarray("u1", {c.rgb_h, c.rgb_w, 3}, c.rgb.data(), 64);
   }
   if (c.has_obs) {
     w.key("obs");

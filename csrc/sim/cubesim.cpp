@@ -231,7 +231,7 @@ int main(int argc, char** argv) {
     size_t img_off = 0;
     if (!seg) {
       w.key("image");
-      img_off = w.ndarray("u1", {H, W, C});
+      img_off = w.ndarray("u1", {H, W, C}, nullptr, 64);   // 64-byte aligned payload: zero-copy GPU reads
     }
     w.key("xy");
     std::vector<double> xy;

@@ -208,7 +208,7 @@ int main(int argc, char** argv) {
     wr.key("btid");
     wr.integer(btid);
     wr.key("image");
-    const size_t off = wr.ndarray("u1", {size, size, 3});
+    const size_t off = wr.ndarray("u1", {size, size, 3}, nullptr, 64);
     wr.key("shape_id");
     wr.integer(w.ids[k]);
     wr.end_dict();

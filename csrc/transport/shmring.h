@@ -59,7 +59,7 @@ class Segment {
 
   // Producer: claim a FREE slot, waiting up to timeout_ms (-1 forever);
   // returns -1 on timeout or when `stop` becomes true.
-  int acquire(long timeout_ms, const std::atomic<bool>* stop = nullptr, long lease_ms = 2000);
+  int acquire(long timeout_ms, const std::atomic<bool>* stop = nullptr, long lease_ms = 30000);
   uint32_t publish(uint32_t i);        // returns the slot's new generation
   // Consumer: hand a slot back (no-op if it was reclaimed meanwhile).
   void release(uint32_t i, uint32_t gen);

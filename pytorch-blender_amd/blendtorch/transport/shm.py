@@ -137,7 +137,7 @@ class ShmRing:
     def name(self):
         return self.seg.name
 
-    def acquire(self, timeout_s=None, lease_s=2.0):
+    def acquire(self, timeout_s=None, lease_s=30.0):
         t0 = time.time()
         n = self.seg.nslots
         while True:

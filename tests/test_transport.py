@@ -254,3 +254,22 @@ def test_hypothesis_dict_roundtrip():
             return
         assert _eq(pickle.loads(raw), got)
     check()
+
+
+@pytest.mark.parametrize('n', [5, 200, 256, 4099, 921600])
+@pytest.mark.parametrize('align', [16, 64])
+def test_writer_aligned_payload(n, align):
+    """Writer.ndarray(align=...) pads with pickle no-ops so the payload starts
+    at an aligned offset; pickle, numpy and the native scanner read the same
+    value as without padding."""
+    import pickle as _pickle
+    from blendtorch import _native
+    rng = np.random.default_rng(n)
+    for key in ('k', 'key-xyz', 'a' * 37):
+        img = rng.integers(0, 256, size=n, dtype=np.uint8)
+        d = {'btid': 1, key: 2.5, 'image': img, 'xy': np.arange(16.0).reshape(8, 2)}
+        b = _native.dumps_array_dict(d, 4, align)
+        off = b.find(img.tobytes())
+        assert off > 0 and off % align == 0
+        for r in (_pickle.loads(b), _native.fast_loads(b)):
+            assert np.array_equal(r['image'], img) and r[key] == 2.5 and np.array_equal(r['xy'], d['xy'])
