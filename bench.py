@@ -97,6 +97,8 @@ def main():
                     help='auto: decode kernel reads pinned host frames directly (zero-copy); copy: DMA first')
     ap.add_argument('--launch-depth', type=int, default=2,
                     help='direct-path decode launches queued before new batches coalesce into one launch')
+    ap.add_argument('--backend', choices=['nccl', 'gloo'], default='nccl',
+                    help='process-group backend (nccl = RCCL over xGMI; gloo only to rehearse several ranks on one GPU)')
     ap.add_argument('--start-port', type=int, default=0)
     ap.add_argument('--dist', choices=['shard', 'scatter'], default='shard',
                     help='shard: every rank owns its producers; scatter: rank 0 receives world*B per step '
@@ -115,10 +117,14 @@ def main():
     from blendtorch.btt.gpu import DeviceLoader
     from blendtorch.ops import DecodeConfig
 
-    torch.cuda.set_device(local_rank)
-    device = torch.device('cuda', local_rank)
+    gpu = local_rank % max(1, torch.cuda.device_count())    # == local_rank on a full node
+    torch.cuda.set_device(gpu)
+    device = torch.device('cuda', gpu)
     if world > 1:
-        dist.init_process_group('nccl', device_id=device)
+        if args.backend == 'nccl':
+            dist.init_process_group('nccl', device_id=device)
+        else:
+            dist.init_process_group('gloo')
 
     # place each rank's producers on CPUs local to its GPU (same NUMA domain as
     # the GPU's PCIe root: frames are written there and read back by the GPU)
@@ -152,7 +158,7 @@ def main():
         from blendtorch.models import Discriminator
         model = Discriminator(nc=3, ndf=32, adaptive=True).to(device).to(memory_format=torch.channels_last)
         if world > 1:
-            model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local_rank])
+            model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[gpu])
         opt = torch.optim.Adam(model.parameters(), lr=2e-4)
         crit = torch.nn.BCELoss()
 
@@ -211,7 +217,7 @@ def main():
             pass
         stats = dict(dl.stats) if dl is not None else {}
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device if args.backend == 'nccl' else 'cpu')
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     tmax = float(t.item())

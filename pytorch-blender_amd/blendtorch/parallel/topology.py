@@ -48,7 +48,8 @@ def gpu_pci_bus_id(index: int) -> Optional[str]:
     try:
         from .. import ops
         ext = ops.hip_ext()
-        return ext.pci_bus_id(int(index)).lower()
+        n = ext.device_count()
+        return ext.pci_bus_id(int(index) % n).lower() if n > 0 else None
     except Exception:
         return None
 
@@ -86,10 +87,11 @@ def plan_rank_cpus(local_rank: int, local_world: int, allowed: Sequence[int],
     allowed = sorted(set(int(c) for c in allowed))
     if bus_ids is None:
         bus_ids = [gpu_pci_bus_id(r) for r in range(local_world)]
+    allowed_set = set(allowed)
     domains = []
     for bid in bus_ids:
         local = pci_local_cpus(bid, sysfs) if bid else None
-        dom = [c for c in (local or []) if c in set(allowed)]
+        dom = [c for c in (local or []) if c in allowed_set]
         domains.append(tuple(dom) if dom else None)
     if len(domains) != local_world or any(d is None for d in domains):
         return {'cpus': _contiguous(allowed, local_rank, local_world), 'numa_local': False, 'domain': allowed}
