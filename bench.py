@@ -89,6 +89,9 @@ def main():
     ap.add_argument('--proto', choices=['tcp', 'ipc'], default='ipc',
                     help='ipc (Unix-domain ZMTP, same-host producers; default) or tcp')
     ap.add_argument('--consumer', choices=['none', 'disc'], default='none')
+    ap.add_argument('--consumer-dtype', choices=['bf16', 'fp32'], default='bf16',
+                    help='disc consumer: bf16 = decode kernel emits bf16 channels-last frames and the DCGAN step runs '
+                         'under bf16 autocast (MFMA); fp32 = fp32 NCHW frames, fp32 step')
     ap.add_argument('--io-threads', type=int, default=0)
     ap.add_argument('--shm', type=int, default=48,
                     help='>0 (default 48): producers render into an N-slot shared-memory ring (same host) and '
@@ -149,6 +152,10 @@ def main():
     start_port = args.start_port or (20000 + (os.getpid() % 200) * 50 if world == 1 else 21000 + rank * 64)
 
     decode = DecodeConfig.unit(channels='rgb', gamma=2.2)
+    amp = args.consumer == 'disc' and args.consumer_dtype == 'bf16'
+    if amp:
+        # the decode kernel writes what the model's first conv reads: bf16, channels-last
+        decode = DecodeConfig.unit(channels='rgb', gamma=2.2, dtype='bfloat16', layout='nhwc')
     launch = dict(producer='cubesim', num_instances=nprod, named_sockets=['DATA'], start_port=start_port,
                   proto=args.proto, seed=1000 * rank, cpu_affinity=affinity,
                   instance_args=[['--mode', args.mode, '--sndhwm', '10'] + (['--shm', str(args.shm)] if args.shm else [])]
@@ -175,7 +182,8 @@ def main():
                               io_threads=args.io_threads or None, timeoutms=60000, h2d=args.h2d,
                               launch_depth=args.launch_depth)
         if args.dist == 'scatter':
-            it = iter(ScatterLoader(dl, args.batch, (3, 480, 640), torch.float32, device, total_batches))
+            shp, dt = ((480, 640, 3), torch.bfloat16) if amp else ((3, 480, 640), torch.float32)
+            it = iter(ScatterLoader(dl, args.batch, shp, dt, device, total_batches))
         else:
             it = iter(dl)
 
@@ -184,7 +192,13 @@ def main():
             img = b['image']
             if model is not None:
                 opt.zero_grad(set_to_none=True)
-                out = model(img.contiguous(memory_format=torch.channels_last))
+                if amp:
+                    x = img.permute(0, 3, 1, 2)          # NHWC storage -> NCHW view, channels-last strides
+                    with torch.autocast('cuda', dtype=torch.bfloat16):
+                        out = model(x)
+                    out = out.float()
+                else:
+                    out = model(img.contiguous(memory_format=torch.channels_last))
                 loss = crit(out, torch.ones_like(out))
                 loss.backward()
                 opt.step()
@@ -235,7 +249,7 @@ def main():
             'higher_is_better': True,
             'scaling': 'weak',
             'vs_baseline': round(value / BASELINE_IMAGES_PER_SEC, 3),
-            'dtype': 'fp32',
+            'dtype': 'bf16' if amp else 'fp32',
             'data': 'synthetic (headless C++ Cube-scene producers, random rotations)',
             'config': {
                 'model': 'cube-scene-640x480-' + args.mode + (' + dcgan-disc' if model is not None else ''),
@@ -245,7 +259,8 @@ def main():
                 'producers_per_gpu': nprod // (world if args.dist == 'scatter' else 1),
                 'cpus_per_gpu': share,
                 'numa_local': plan['numa_local'],
-                'decode': 'rgba->rgb, gamma 2.2, /255, HWC->CHW fp32 (gfx950 kernel)',
+                'decode': ('rgba->rgb, gamma 2.2, /255, bf16 NHWC (gfx950 kernel)' if amp else
+                           'rgba->rgb, gamma 2.2, /255, HWC->CHW fp32 (gfx950 kernel)'),
                 'out_shape': list(shape),
                 'proto': args.proto,
                 'pinned_producers': pin,

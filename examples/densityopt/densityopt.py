@@ -106,8 +106,11 @@ def run(args):
         update_simulations(remotes, pm.to_supershape(samples))
         t0 = time.time()
         epoch = 0
+        wait_s = 0.0
         while True:
+            tw = time.time()
             sim_batch = next(gen_sim)
+            wait_s += time.time() - tw
             sim_img, sim_shape_id = sim_batch['image'], sim_batch['shape_id']
             # discriminator step
             label = torch.full((BATCH,), TARGET_LABEL, dtype=torch.float32, device=dev)
@@ -148,7 +151,7 @@ def run(args):
         tgt = torch.tensor(np.concatenate((mu_target, std_target))).float()
         diff = (tgt - history[-1]).abs()
         print('Abs.Diff to true params', diff)
-        return {'iterations': epoch, 'seconds': dt, 'iterations_per_s': epoch / dt,
+        return {'iterations': epoch, 'seconds': dt, 'iterations_per_s': epoch / dt, 'sim_wait_s': wait_s,
                 'images_per_s': epoch * BATCH / dt, 'final_params': history[-1].tolist(),
                 'target': tgt.tolist(), 'abs_diff': diff.tolist()}
 
