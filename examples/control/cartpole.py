@@ -14,7 +14,8 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parents[2] / 'pytorch-blender_amd'))
 sys.path.insert(0, str(Path(__file__).resolve().parent))
 
-from cartpole_gym.envs import CartpoleEnv  # noqa: E402
+import cartpole_gym  # noqa: E402,F401  (registers blendtorch-cartpole-v0)
+from blendtorch import btt  # noqa: E402
 
 KAPPA = 30
 
@@ -30,7 +31,7 @@ def main():
     ap.add_argument('--steps', type=int, default=2000)
     ap.add_argument('--real-time', action='store_true')
     a = ap.parse_args()
-    env = CartpoleEnv(real_time=a.real_time)
+    env = btt.env.make('blendtorch-cartpole-v0', real_time=a.real_time)
     obs = env.reset()
     episodes, length, lengths = 0, 0, []
     for _ in range(a.steps):

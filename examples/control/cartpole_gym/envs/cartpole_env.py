@@ -17,15 +17,15 @@ except ImportError:  # spaces are informational only
 
 
 class CartpoleEnv(btt.env.OpenAIRemoteEnv):
-    def __init__(self, render_every=10, real_time=False):
+    def __init__(self, render_every=10, real_time=False, launcher_args=None):
         super().__init__(version='0.0.1')
         here = Path(__file__).parent
         if btt.discover_blender() is not None:
             self.launch(scene=here / 'cartpole.blend', script=here / 'cartpole.blend.py',
-                        real_time=real_time, render_every=render_every)
+                        real_time=real_time, render_every=render_every, launcher_args=launcher_args)
         else:
             self.launch(scene='', script='', producer='cartpolesim', real_time=real_time,
-                        render_every=render_every)
+                        render_every=render_every, launcher_args=launcher_args)
         if spaces is not None:
             self.action_space = spaces.Box(np.float32(-100), np.float32(100), shape=(1,))
             self.observation_space = spaces.Box(np.float32(-10), np.float32(10), shape=(1,))

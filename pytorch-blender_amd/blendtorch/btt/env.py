@@ -48,6 +48,34 @@ except ImportError:  # pragma: no cover - gym is not in this image
 
 GYM_AVAILABLE = _gym is not None
 
+# Environment registry: ``register``/``make`` mirror gym's, so examples can
+# say ``btt.env.make('blendtorch-cartpole-v0')`` with or without gym (the
+# reference relies on ``gym.make``, examples/control/cartpole_gym/__init__.py).
+_REGISTRY = {}
+
+
+def register(id, entry_point, **kwargs):
+    """Register an env id -> ``'module:Class'`` (also with gym when installed)."""
+    _REGISTRY[id] = (entry_point, dict(kwargs))
+    if _gym is not None:
+        try:
+            _gym.envs.registration.register(id=id, entry_point=entry_point, kwargs=dict(kwargs))
+        except Exception:  # already registered with gym
+            pass
+
+
+def make(id, **kwargs):
+    """Instantiate a registered env (gym.make semantics for our own ids)."""
+    if id not in _REGISTRY:
+        if _gym is not None:
+            return _gym.make(id, **kwargs)
+        raise KeyError(f'no environment registered as {id!r}')
+    entry_point, defaults = _REGISTRY[id]
+    import importlib
+    mod, _, attr = entry_point.partition(':')
+    cls = getattr(importlib.import_module(mod), attr)
+    return cls(**{**defaults, **kwargs})
+
 
 def _flags(kwargs):
     """``launch_env`` kwargs -> argparse-style command-line flags."""
@@ -129,16 +157,20 @@ class RemoteEnv:
 
 
 @contextmanager
-def launch_env(scene, script, background=False, producer=None, timeoutms=DEFAULT_TIMEOUTMS, **kwargs):
+def launch_env(scene, script, background=False, producer=None, timeoutms=DEFAULT_TIMEOUTMS, launcher_args=None,
+               **kwargs):
     """Launch one remote env instance and yield a connected :class:`RemoteEnv`.
 
     ``producer`` selects a headless stand-in (e.g. ``'cartpolesim'``) instead
-    of Blender; remaining kwargs become command-line flags of the env script.
+    of Blender; ``launcher_args`` are extra :class:`BlenderLauncher` arguments
+    (``start_port``, ``proto``, ``blend_path``, ...); remaining kwargs become
+    command-line flags of the env script.
     """
     env = None
     try:
         launch = dict(scene=scene, script=script, num_instances=1, named_sockets=['GYM'],
                       instance_args=[_flags(kwargs)], background=background, producer=producer)
+        launch.update(launcher_args or {})
         with BlenderLauncher(**launch) as bl:
             env = RemoteEnv(bl.launch_info.addresses['GYM'][0], timeoutms=timeoutms)
             yield env

@@ -5,7 +5,7 @@ The reply to request k is the ctx after the frame that applied action k;
 import pytest
 
 from blendtorch import btt
-from helpers import BLENDDIR, HEADLESS_BLENDER
+from helpers import BLENDDIR, HEADLESS_BLENDER, ROOT
 
 
 class MyEnv(btt.env.OpenAIRemoteEnv):
@@ -88,3 +88,23 @@ def test_remote_env_timeout_is_valueerror(free_port):
     with pytest.raises(ValueError, match='receive'):
         env.reset()
     env.close()
+
+
+def test_env_registry_make_cartpole(free_port):
+    """``btt.env.make`` resolves a registered id without gym (the reference
+    relies on gym.make for blendtorch-cartpole-v0)."""
+    import sys
+    sys.path.insert(0, str(ROOT / 'examples' / 'control'))
+    import cartpole_gym  # noqa: F401  registers the id
+    from blendtorch import btt
+    env = btt.env.make('blendtorch-cartpole-v0', launcher_args={'start_port': free_port})
+    try:
+        obs = env.reset()
+        assert len(obs) == 3
+        for _ in range(5):
+            obs, reward, done, info = env.step(1.0)
+        assert env.env_time is not None
+    finally:
+        env.close()
+    with pytest.raises(KeyError):
+        btt.env.make('no-such-env-v0')
