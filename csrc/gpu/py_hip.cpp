@@ -271,6 +271,36 @@ PYBIND11_MODULE(_hip, m) {
           return double(ms) * 1000.0 / iters;
         });
 
+  // Kernel-only timing of the MFMA colour transform (see bench_decode).
+  m.def("bench_color4x4",
+        [](uintptr_t src, uintptr_t dst, uintptr_t lut, uintptr_t M, uintptr_t bias, int B, int H, int W, int Cout,
+           int iters) {
+          py::gil_scoped_release nogil;
+          Color4x4Params p;
+          p.src = ptr<const uint8_t>(src);
+          p.dst = ptr<float>(dst);
+          p.lut = ptr<const float>(lut);
+          p.M = ptr<const float>(M);
+          p.bias = ptr<const float>(bias);
+          p.B = B, p.H = H, p.W = W, p.Cout = Cout;
+          hipStream_t s;
+          check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "stream");
+          hipEvent_t a, b;
+          check(hipEventCreate(&a), "event");
+          check(hipEventCreate(&b), "event");
+          for (int i = 0; i < 10; ++i) check(color4x4(p, s), "color4x4");
+          check(hipEventRecord(a, s), "record");
+          for (int i = 0; i < iters; ++i) check(color4x4(p, s), "color4x4");
+          check(hipEventRecord(b, s), "record");
+          check(hipEventSynchronize(b), "sync");
+          float ms = 0;
+          check(hipEventElapsedTime(&ms, a, b), "elapsed");
+          (void)hipEventDestroy(a);
+          (void)hipEventDestroy(b);
+          (void)hipStreamDestroy(s);
+          return double(ms) * 1000.0 / iters;
+        });
+
   py::class_<StreamLoader>(m, "StreamLoader")
       .def(py::init([](std::vector<std::string> addresses, int batch_size, std::string image_key, int rcvhwm,
                        int io_threads, int device, int64_t max_batches, size_t max_frame_bytes, int pool_slots,

@@ -322,10 +322,15 @@ def color4x4(images, M, bias=(0.0, 0.0, 0.0, 0.0), gamma=None, flip=False, cout=
         raise ValueError('color4x4 needs RGBA input')
     if (H * W) % 256 or W % 4:
         raise ValueError('color4x4 needs H*W % 256 == 0 and W % 4 == 0')
-    cfg = DecodeConfig(channels='rgba', gamma=gamma, color_matrix=tuple(map(tuple, np.asarray(M, np.float32))))
-    lut = device_lut(cfg, x.device)
-    Mt = torch.as_tensor(np.asarray(M, np.float32), device=x.device).contiguous()
-    bt = torch.as_tensor(np.asarray(bias, np.float32), device=x.device).contiguous()
+    Mn = np.ascontiguousarray(M, np.float32)
+    bn = np.ascontiguousarray(bias, np.float32)
+    key = ('color4x4', Mn.tobytes(), bn.tobytes(), gamma, str(x.device))
+    cached = _lut_cache.get(key)
+    if cached is None:   # LUT + matrix + bias uploaded once per (M, bias, gamma, device)
+        cfg = DecodeConfig(channels='rgba', gamma=gamma, color_matrix=tuple(map(tuple, Mn)))
+        cached = (device_lut(cfg, x.device), torch.from_numpy(Mn).to(x.device), torch.from_numpy(bn).to(x.device))
+        _lut_cache[key] = cached
+    lut, Mt, bt = cached
     out = torch.empty((B, cout, H, W), dtype=torch.float32, device=x.device)
     ext.color4x4(x.data_ptr(), out.data_ptr(), lut.data_ptr(), Mt.data_ptr(), bt.data_ptr(), 0, B, H, W, cout,
                  int(flip), _stream(x.device))

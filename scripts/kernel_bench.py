@@ -67,10 +67,18 @@ def main():
         print(a.tag, name, res[name], flush=True)
     if not a.only or 'color' in a.only:
         M = np.random.default_rng(0).normal(size=(4, 4)).astype(np.float32)
-        us = timeit(lambda: ops.color4x4(x4, M, [0, 0, 0, 0], gamma=2.2), a.iters)   # includes Python launch
+        cfg = ops.DecodeConfig(channels='rgba', gamma=2.2, color_matrix=M)
+        out = ops.color4x4(x4, M, [0, 0, 0, 0], gamma=2.2)
+        lut = ops.device_lut(cfg, dev)
+        Mt = torch.as_tensor(M, device=dev).contiguous()
+        bt = torch.zeros(4, dtype=torch.float32, device=dev)
+        us = ext.bench_color4x4(x4.data_ptr(), out.data_ptr(), lut.data_ptr(), Mt.data_ptr(), bt.data_ptr(),
+                                B, H, W, 4, a.iters)   # kernel-only (C++ launch loop between HIP events)
+        py_us = timeit(lambda: ops.color4x4(x4, M, [0, 0, 0, 0], gamma=2.2), a.iters)   # incl. Python op overhead
         ref_us = timeit(lambda: ops.reference_color4x4(x4, M, [0, 0, 0, 0], gamma=2.2), 20, 3)
         nbytes = B * H * W * (4 + 16)
         res['color4x4_mfma_rgba_f32'] = {'us': round(us, 2), 'GBps': round(nbytes / us / 1e3, 1),
+                                         'python_op_us': round(py_us, 1),
                                          'torch_eager_us': round(ref_us, 1), 'speedup_vs_eager': round(ref_us / us, 1)}
         print('color4x4_mfma_rgba_f32', res['color4x4_mfma_rgba_f32'], flush=True)
     if a.json:
