@@ -25,7 +25,10 @@ enum Layout : int { NCHW = 0, NHWC = 1 };
 
 // Decode a batch of B u8 HWC images into a float/bf16/f16/u8 tensor.
 //   src         B images; image b starts at src + src_offsets[b] (bytes) when
-//               src_offsets != nullptr, else at src + b*H*W*Cin.
+//               src_offsets != nullptr (device int64[B]: a gather, e.g. random
+//               replay from an HBM-resident frame store), else at src + b*H*W*Cin.
+//   src_offsets_aligned  caller's promise that every src_offsets[b] is a
+//               multiple of 16 (frame-strided stores): keeps the vector path.
 //   lut         device float[4][256]: value for (output channel c, input u8 v).
 //               Gamma, scale and per-channel mean/std are folded into it on
 //               the host (bit-exact with the fp32 reference by construction).
@@ -43,6 +46,7 @@ constexpr int kMaxSrcs = 64;
 struct DecodeParams {
   const uint8_t* src = nullptr;
   const int64_t* src_offsets = nullptr;
+  int src_offsets_aligned = 0;
   const uint8_t* srcs[kMaxSrcs] = {};
   int nsrcs = 0;
   // dsts[b] when ndsts == B: per-image output base (image b's Cout*H*W

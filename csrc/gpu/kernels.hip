@@ -259,7 +259,7 @@ hipError_t launch_out(const DecodeParams& p, hipStream_t s) {
   constexpr int PPT = OUTT == OUT_F32 ? 4 : (OUTT == OUT_U8 ? 16 : 8);
   // vector path: a lane's PPT pixels sit in one row and its loads are aligned
   const bool src_aligned = p.nsrcs ? srcs_ok(p.srcs, p.nsrcs, p.B, 16)
-                                   : (reinterpret_cast<uintptr_t>(p.src) % 16) == 0 && p.src_offsets == nullptr;
+                                   : (reinterpret_cast<uintptr_t>(p.src) % 16) == 0 && (p.src_offsets == nullptr || p.src_offsets_aligned);
   const bool dst_aligned = p.ndsts ? dsts_ok(p.dsts, p.ndsts, p.B, 16) : (reinterpret_cast<uintptr_t>(p.dst) % 16) == 0;
   bool aligned = (p.W % PPT) == 0 && (int64_t(p.H) * p.W * p.Cin) % 16 == 0 && dst_aligned && src_aligned;
   if (aligned && p.Cin == 4) return launch_vec<PPT, 4, OUTT>(p, s);

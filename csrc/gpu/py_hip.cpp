@@ -67,10 +67,12 @@ PYBIND11_MODULE(_hip, m) {
 
   m.def("decode",
         [](uintptr_t src, uintptr_t src_offsets, uintptr_t dst, uintptr_t lut, uintptr_t flip, int B, int H, int W,
-           int Cin, int Cout, std::vector<int> cmap, int flip_all, int out_dtype, int layout, uintptr_t stream) {
+           int Cin, int Cout, std::vector<int> cmap, int flip_all, int out_dtype, int layout, uintptr_t stream,
+           bool src_offsets_aligned) {
           DecodeParams p;
           p.src = ptr<const uint8_t>(src);
           p.src_offsets = ptr<const int64_t>(src_offsets);
+          p.src_offsets_aligned = src_offsets_aligned;
           p.dst = ptr<void>(dst);
           p.lut = ptr<const float>(lut);
           p.flip = ptr<const uint8_t>(flip);
@@ -83,7 +85,7 @@ PYBIND11_MODULE(_hip, m) {
         },
         py::arg("src"), py::arg("src_offsets"), py::arg("dst"), py::arg("lut"), py::arg("flip"), py::arg("B"),
         py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("Cout"), py::arg("cmap"), py::arg("flip_all"),
-        py::arg("out_dtype"), py::arg("layout"), py::arg("stream"));
+        py::arg("out_dtype"), py::arg("layout"), py::arg("stream"), py::arg("src_offsets_aligned") = false);
 
   m.def("color4x4",
         [](uintptr_t src, uintptr_t dst, uintptr_t lut, uintptr_t M, uintptr_t bias, uintptr_t flip, int B, int H,

@@ -3,8 +3,9 @@
 Public names match the reference: BlenderLauncher, LaunchInfo,
 RemoteIterableDataset, FileDataset, discover_blender, FileRecorder,
 FileReader, DuplexChannel, env.  MI355X additions: DeviceLoader and
-DecodeConfig (``btt.gpu``, device-resident streaming; imported lazily so
-the CPU API works without the HIP extension).
+DecodeConfig (``btt.gpu``, device-resident streaming) and DeviceReplayBuffer
+(``btt.replay``, HBM-resident record/replay); imported lazily so the CPU API
+works without the HIP extension.
 """
 from .launcher import BlenderLauncher
 from .launch_info import LaunchInfo
@@ -23,4 +24,7 @@ def __getattr__(name):
     if name in ('DeviceLoader', 'DecodeConfig'):
         from . import gpu
         return getattr(gpu, name)
+    if name == 'DeviceReplayBuffer':
+        from .replay import DeviceReplayBuffer
+        return DeviceReplayBuffer
     raise AttributeError(name)

@@ -28,7 +28,8 @@ from typing import Optional, Sequence
 import numpy as np
 
 __all__ = [
-    'DecodeConfig', 'hip_ext', 'hip_available', 'gamma_lut', 'build_lut', 'decode', 'color4x4', 'project',
+    'DecodeConfig', 'hip_ext', 'hip_available', 'gamma_lut', 'build_lut', 'decode', 'decode_gather', 'color4x4',
+    'project',
     'reference_decode', 'reference_color4x4', 'reference_project', 'reference_gamma',
 ]
 
@@ -147,6 +148,12 @@ class DecodeConfig:
     def unit(cls, **kw):
         """x / 255 in [0, 1]."""
         return cls(scale=1.0 / 255.0, **kw)
+
+    @classmethod
+    def raw(cls, channels='rgba', **kw):
+        """Bytes as they came: u8, channels-last, no gamma (identity table) --
+        e.g. to fill a :class:`~blendtorch.btt.replay.DeviceReplayBuffer`."""
+        return cls(channels=channels, dtype='uint8', layout='nhwc', **kw)
 
     @property
     def cmap(self):
@@ -309,6 +316,33 @@ def decode(images, cfg: DecodeConfig = DecodeConfig(), flip=None, out=None):
         fl = fl_t.data_ptr()
     ext.decode(x.data_ptr(), 0, out.data_ptr(), lut.data_ptr(), fl, B, H, W, C, cfg.cout, cfg.cmap,
                int(cfg.flip), OUT_DTYPES[cfg.dtype], LAYOUTS[cfg.layout], _stream(x.device))
+    return out
+
+
+def decode_gather(store, index, cfg: DecodeConfig = DecodeConfig(), out=None):
+    """Fused gather + decode: ``decode(store[index], cfg)`` without
+    materialising the gathered u8 batch.  ``store`` is a u8 [N,H,W,C] device
+    tensor (e.g. an HBM-resident frame store), ``index`` an int [B] device
+    tensor.  The kernel reads image b at ``store + index[b] * H*W*C``."""
+    import torch
+    ext = hip_ext()
+    if store.dtype != torch.uint8 or not store.is_cuda or not store.is_contiguous() or store.dim() != 4:
+        raise TypeError('decode_gather expects a contiguous uint8 [N,H,W,C] CUDA/HIP tensor')
+    if cfg.color_matrix is not None:
+        raise ValueError('decode_gather: colour matrices are not supported; use color4x4 on store[index]')
+    N, H, W, C = store.shape
+    if max(cfg.cmap) >= C:
+        raise ValueError(f'channel map {cfg.cmap} needs more than {C} input channels')
+    idx = index.to(device=store.device, dtype=torch.int64)
+    B = int(idx.numel())
+    frame = H * W * C
+    offsets = (idx * frame).contiguous()
+    if out is None:
+        out = torch.empty(cfg.out_shape(B, H, W), dtype=cfg.torch_dtype(), device=store.device)
+    lut = device_lut(cfg, store.device)
+    ext.decode(store.data_ptr(), offsets.data_ptr(), out.data_ptr(), lut.data_ptr(), 0, B, H, W, C, cfg.cout,
+               cfg.cmap, int(cfg.flip), OUT_DTYPES[cfg.dtype], LAYOUTS[cfg.layout], _stream(store.device),
+               frame % 16 == 0)
     return out
 
 

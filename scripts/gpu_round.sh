@@ -37,6 +37,7 @@ for step in "$@"; do
     dist1) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29555 bench.py --gpus 1 --steps 500 --warmup 20 > gpurun_out/dist1.log 2>&1; rc=$?; grep '^{' gpurun_out/dist1.log;
            timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29556 bench.py --gpus 1 --steps 300 --warmup 20 --consumer disc >> gpurun_out/dist1.log 2>&1; rc=$?; grep '^{' gpurun_out/dist1.log | tail -1;;
     dist2gloo) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29557 bench.py --gpus 2 --backend gloo --steps 1000 --warmup 20 > gpurun_out/dist2gloo.log 2>&1; rc=$?; grep '^{' gpurun_out/dist2gloo.log;;
+    replay) timeout -k 10 200 python benchmarks/bench_replay.py > gpurun_out/replay.log 2>&1 && timeout -k 10 200 python benchmarks/bench_replay.py --batch 64 --steps 500 >> gpurun_out/replay.log 2>&1 && timeout -k 10 200 python benchmarks/bench_replay.py --graph >> gpurun_out/replay.log 2>&1 && timeout -k 10 200 python benchmarks/bench_replay.py --graph --batch 64 --steps 500 >> gpurun_out/replay.log 2>&1 && timeout -k 10 200 python benchmarks/bench_replay.py --fill producers --frames 2048 --batch 64 --steps 500 >> gpurun_out/replay.log 2>&1; rc=$?; cat gpurun_out/replay.log | grep '^{';;
     h2d) timeout -k 10 120 python -c "
 import sys; sys.path.insert(0,'pytorch-blender_amd')
 import torch; from blendtorch import ops; e=ops.hip_ext()

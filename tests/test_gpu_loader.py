@@ -22,6 +22,10 @@ def test_device_loader_cubesim(dev, free_port):
                              seed=3, instance_args=[['--mode', 'rgba']] * 2) as bl:
         cfg = ops.DecodeConfig.densityopt(channels='rgb', gamma=2.2)
         dl = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=8, max_items=512, decode=cfg, device=dev)
+        # as the reference harness does (benchmarks/benchmark.py:31): let both
+        # producers come up -- 512 frames take ~15 ms, less than a process start
+        import time
+        time.sleep(1.0)
         n = 0
         btids = set()
         for b in dl:

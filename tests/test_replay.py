@@ -1,0 +1,110 @@
+"""DeviceReplayBuffer: .btr recordings / streams -> frame store -> sampled,
+decoded batches.  CPU variants run the fp32 reference ops; the GPU variants
+check the fused gather+decode kernel against them bit for bit."""
+import numpy as np
+import pytest
+import torch
+from torch.utils import data
+
+from blendtorch import btt, ops
+from blendtorch.btt.replay import DeviceReplayBuffer
+
+
+def _record(tmp_path, free_port, n=24):
+    prefix = str(tmp_path / 'rec')
+    with btt.BlenderLauncher(producer='cubesim', num_instances=2, named_sockets=['DATA'], start_port=free_port,
+                             seed=7, instance_args=[['--mode', 'rgba']] * 2) as bl:
+        ds = btt.RemoteIterableDataset(bl.launch_info.addresses['DATA'], max_items=n, record_path_prefix=prefix)
+        items = [x for x in data.DataLoader(ds, batch_size=None, num_workers=0)]
+    assert len(items) == n
+    return prefix, items
+
+
+def test_replay_cpu_from_recordings(tmp_path, free_port):
+    prefix, items = _record(tmp_path, free_port)
+    rb = DeviceReplayBuffer.from_recordings(prefix, device='cpu', chunk=5)
+    assert len(rb) == 24 and rb.frame_shape == (480, 640, 4) and rb.nbytes == 24 * 480 * 640 * 4
+    # insertion order = recording order (one file, one worker)
+    for i in (0, 7, 23):
+        assert np.array_equal(rb.store[i].numpy(), np.asarray(items[i]['image']))
+        assert int(rb.meta['frameid'][i]) == items[i]['frameid'] and int(rb.meta['btid'][i]) == items[i]['btid']
+    cfg = ops.DecodeConfig.densityopt(channels='rgb', gamma=2.2)
+    idx = torch.tensor([3, 3, 11, 0])
+    b = rb.gather(idx, cfg)
+    ref = ops.reference_decode(torch.from_numpy(np.stack([np.asarray(items[i]['image']) for i in idx.tolist()])), cfg)
+    assert torch.equal(b['image'], ref)
+    assert b['frameid'].tolist() == [items[i]['frameid'] for i in idx.tolist()]
+    seen = torch.cat([bb['index'] for bb in rb.batches(8, cfg, shuffle=True, generator=torch.Generator().manual_seed(0))])
+    assert sorted(seen.tolist()) == list(range(24))
+    s = rb.sample(5, cfg, generator=torch.Generator().manual_seed(1))
+    assert s['image'].shape == (5, 3, 480, 640)
+
+
+def test_replay_ring_semantics():
+    rb = DeviceReplayBuffer(4, device='cpu')
+    frames = torch.arange(6, dtype=torch.uint8).view(6, 1, 1, 1).expand(6, 2, 2, 1).contiguous()
+    rb.extend(frames[:3], frameid=np.arange(3))
+    rb.extend(frames[3:], frameid=np.arange(3, 6))
+    assert len(rb) == 4
+    # slots hold frames 4, 5, 2, 3 (oldest overwritten)
+    assert rb.store[:, 0, 0, 0].tolist() == [4, 5, 2, 3] and rb.meta['frameid'].tolist() == [4, 5, 2, 3]
+    with pytest.raises(ValueError):
+        rb.extend(torch.zeros((1, 3, 3, 1), dtype=torch.uint8), frameid=np.zeros(1))
+    with pytest.raises(ValueError):
+        rb.extend(frames[:1])   # metadata keys must match
+
+
+@pytest.mark.gpu
+def test_replay_gpu_gather_decode(tmp_path, free_port):
+    dev = torch.device('cuda', 0)
+    prefix, items = _record(tmp_path, free_port)
+    rb = DeviceReplayBuffer.from_recordings(prefix, device=dev, chunk=8)
+    assert rb.store.is_cuda and len(rb) == 24
+    host = torch.from_numpy(np.stack([np.asarray(it['image']) for it in items]))
+    assert torch.equal(rb.store.cpu(), host)
+    for cfg in (ops.DecodeConfig.densityopt(channels='rgb', gamma=2.2),
+                ops.DecodeConfig.unit(channels='bgr', dtype='bfloat16', layout='nhwc'),
+                ops.DecodeConfig(channels='rgba', gamma=2.2, dtype='uint8')):
+        idx = torch.tensor([5, 0, 23, 5, 17, 2, 9, 11], device=dev)
+        got = rb.gather(idx, cfg)['image']
+        ref = ops.reference_decode(host[idx.cpu()], cfg)
+        assert torch.equal(got.cpu().float(), ref.float()), cfg
+        assert torch.equal(got, ops.decode(rb.store[idx], cfg))
+    n = sum(len(b['index']) for b in rb.batches(8, ops.DecodeConfig.unit(), epochs=2))
+    assert n == 48
+
+
+@pytest.mark.gpu
+def test_replay_gpu_fill_from_device_loader(free_port):
+    from blendtorch.btt.gpu import DeviceLoader
+    dev = torch.device('cuda', 0)
+    with btt.BlenderLauncher(producer='cubesim', num_instances=2, named_sockets=['DATA'], start_port=free_port,
+                             proto='ipc', instance_args=[['--mode', 'rgba', '--shm', '16']] * 2) as bl:
+        dl = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=8, max_items=32, device=dev,
+                          decode=ops.DecodeConfig.raw())
+        rb = DeviceReplayBuffer(64, device=dev).fill_from(dl, 32)
+    assert len(rb) == 32 and rb.frame_shape == (480, 640, 4)
+    assert set(rb.meta) >= {'btid', 'frameid', 'xy'}
+    b = rb.sample(16, ops.DecodeConfig.unit(channels='rgb', gamma=2.2))
+    assert b['image'].shape == (16, 3, 480, 640) and b['xy'].shape == (16, 8, 2)
+
+
+@pytest.mark.gpu
+def test_replay_graphed_sampler():
+    """The HIP-graph-captured sampler returns fresh random batches whose
+    images equal the eager decode of the indices it drew."""
+    dev = torch.device('cuda', 0)
+    rb = DeviceReplayBuffer(64, device=dev)
+    g = torch.Generator(device=dev).manual_seed(3)
+    rb.extend(torch.randint(0, 256, (64, 48, 64, 4), dtype=torch.uint8, device=dev, generator=g),
+              frameid=torch.arange(64, device=dev))
+    cfg = ops.DecodeConfig.unit(channels='rgb', gamma=2.2)
+    sample = rb.graphed_sampler(8, cfg)
+    seen = []
+    for _ in range(5):
+        b = sample()
+        idx = b['index'].clone()
+        seen.append(idx)
+        assert torch.equal(b['image'], ops.decode(rb.store[idx], cfg))
+        assert torch.equal(b['frameid'], idx)
+    assert len({tuple(i.tolist()) for i in seen}) > 1   # new indices every replay
