@@ -534,7 +534,6 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
     (void)hipEventDestroy(b.ready);
     total += int(b.items.size());
   }
-  const int B = cfg_.batch_size;
   const size_t elem = cfg_.color_matrix ? 4 : (cfg_.out_dtype == OUT_F32 ? 4 : (cfg_.out_dtype == OUT_U8 ? 1 : 2));
   const int cout = cfg_.color_matrix ? 4 : cfg_.cout;
   const size_t out_img_bytes = size_t(H_) * W_ * cout * elem;
@@ -629,7 +628,6 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
   }
   fl.copied = copied;
   inflight_.push_back(std::move(fl));
-  (void)B;
   {
     std::lock_guard<std::mutex> lk(mu_);
     stats_.batches += group.size();

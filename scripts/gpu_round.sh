@@ -38,6 +38,11 @@ for step in "$@"; do
            timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29556 bench.py --gpus 1 --steps 300 --warmup 20 --consumer disc >> gpurun_out/dist1.log 2>&1; rc=$?; grep '^{' gpurun_out/dist1.log | tail -1;;
     dist2gloo) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29557 bench.py --gpus 2 --backend gloo --steps 1000 --warmup 20 > gpurun_out/dist2gloo.log 2>&1; rc=$?; grep '^{' gpurun_out/dist2gloo.log;;
     replay) timeout -k 10 200 python benchmarks/bench_replay.py > gpurun_out/replay.log 2>&1 && timeout -k 10 200 python benchmarks/bench_replay.py --batch 64 --steps 500 >> gpurun_out/replay.log 2>&1 && timeout -k 10 200 python benchmarks/bench_replay.py --graph >> gpurun_out/replay.log 2>&1 && timeout -k 10 200 python benchmarks/bench_replay.py --graph --batch 64 --steps 500 >> gpurun_out/replay.log 2>&1 && timeout -k 10 200 python benchmarks/bench_replay.py --fill producers --frames 2048 --batch 64 --steps 500 >> gpurun_out/replay.log 2>&1; rc=$?; cat gpurun_out/replay.log | grep '^{';;
+    dpmc) timeout -k 10 120 rocprofv3 --pmc TCC_EA0_RDREQ_IO_32B_sum TCC_EA0_RDREQ_IO_CREDIT_STALL_sum TCC_EA0_RDREQ_DRAM_32B_sum --kernel-trace -d /tmp/rp_dpmc1 -o run --output-format csv -- python scripts/direct_pmc.py > gpurun_out/dpmc1.log 2>&1; rc=$?
+          mkdir -p gpurun_out/dpmc && find /tmp/rp_dpmc1 -name '*counter_collection.csv' -exec cp {} gpurun_out/dpmc/pass1_counters.csv \;
+          ok $rc || { echo "dpmc pass1 rc=$rc"; exit $rc; }
+          timeout -k 10 120 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --kernel-trace -d /tmp/rp_dpmc2 -o run --output-format csv -- python scripts/direct_pmc.py > gpurun_out/dpmc2.log 2>&1; rc=$?
+          find /tmp/rp_dpmc2 -name '*counter_collection.csv' -exec cp {} gpurun_out/dpmc/pass2_counters.csv \;;;
     h2d) timeout -k 10 120 python -c "
 import sys; sys.path.insert(0,'pytorch-blender_amd')
 import torch; from blendtorch import ops; e=ops.hip_ext()
