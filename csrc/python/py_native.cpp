@@ -7,6 +7,7 @@
 #include <pybind11/stl.h>
 
 #include "../codec/pickle_codec.h"
+#include "../sim/physics.h"
 #include "../sim/raster.h"
 #include "../transport/zmtp.h"
 #include "pyvalue.h"
@@ -252,6 +253,60 @@ class NativeError(Exception):
         py::arg("d"), py::arg("protocol") = 4, py::arg("align") = 0);
 
   // ---- headless renderer (used by the bpy shim's GPUOffScreen) ----
+  // ---- rigid bodies (falling-cubes stand-in physics; also drives the bpy
+  // shim's rigid-body world) ----
+  struct PyRigid {
+    sim::RigidWorld world;
+    std::vector<sim::Box> boxes;
+    explicit PyRigid(double plane_z) : world(plane_z) {}
+  };
+  py::class_<PyRigid>(m, "RigidWorld")
+      .def(py::init<double>(), py::arg("plane_z"))
+      .def("set_bodies",
+           [](PyRigid& w, py::array_t<double, py::array::c_style | py::array::forcecast> centers,
+              py::array_t<double, py::array::c_style | py::array::forcecast> rots,
+              py::array_t<double, py::array::c_style | py::array::forcecast> halves) {
+             const ssize_t n = centers.shape(0);
+             if (centers.ndim() != 2 || centers.shape(1) != 3 || rots.ndim() != 3 || rots.shape(0) != n ||
+                 rots.shape(1) != 3 || rots.shape(2) != 3 || halves.ndim() != 2 || halves.shape(0) != n ||
+                 halves.shape(1) != 3)
+               throw py::value_error("set_bodies: centers (n,3), rots (n,3,3), halves (n,3)");
+             w.boxes.assign(size_t(n), sim::Box());
+             for (ssize_t i = 0; i < n; ++i) {
+               auto& b = w.boxes[size_t(i)];
+               b.center = {centers.at(i, 0), centers.at(i, 1), centers.at(i, 2)};
+               b.half = {halves.at(i, 0), halves.at(i, 1), halves.at(i, 2)};
+               for (int k = 0; k < 9; ++k) b.rot[size_t(k)] = rots.at(i, k / 3, k % 3);
+             }
+             w.world.reset(w.boxes);
+           })
+      .def("step", [](PyRigid& w, double dt) { w.world.step(w.boxes, dt); }, py::arg("dt"))
+      .def("centers",
+           [](PyRigid& w) {
+             py::array_t<double> out({py::ssize_t(w.boxes.size()), py::ssize_t(3)});
+             auto o = out.mutable_unchecked<2>();
+             for (size_t i = 0; i < w.boxes.size(); ++i) {
+               o(i, 0) = w.boxes[i].center.x, o(i, 1) = w.boxes[i].center.y, o(i, 2) = w.boxes[i].center.z;
+             }
+             return out;
+           })
+      .def("rotations",
+           [](PyRigid& w) {
+             py::array_t<double> out({py::ssize_t(w.boxes.size()), py::ssize_t(3), py::ssize_t(3)});
+             auto o = out.mutable_unchecked<3>();
+             for (size_t i = 0; i < w.boxes.size(); ++i)
+               for (int k = 0; k < 9; ++k) o(i, k / 3, k % 3) = w.boxes[i].rot[size_t(k)];
+             return out;
+           })
+      .def("min_corner_z",
+           [](PyRigid& w) {
+             double z = 1e300;
+             for (auto& b : w.boxes)
+               for (auto& c : b.corners()) z = std::min(z, c.z);
+             return z;
+           })
+      .def("kinetic_energy", [](PyRigid& w) { return w.world.kinetic_energy(w.boxes); });
+
   m.def("render_boxes",
         [](int width, int height, int channels, bool lower_left, std::vector<double> cam_loc,
            std::vector<double> cam_rot, double lens, double sensor, std::vector<double> light_loc,

@@ -38,6 +38,7 @@
 #include "../codec/pickle_codec.h"
 #include "../transport/shmring.h"
 #include "../transport/zmtp.h"
+#include "physics.h"
 #include "raster.h"
 
 using namespace btn;
@@ -185,6 +186,7 @@ int main(int argc, char** argv) {
   sock->setsockopt(zmtp::IMMEDIATE, 1);
   sock->bind(a.sockets[a.socket]);
 
+  sim::RigidWorld physics(scene.plane_z);
   const zmtp::Socket::Interrupt intr = [] { return g_stop.load(); };
   const bool lower_left = a.origin == "lower-left";
   sim::Renderer renderer(scene, C, lower_left);
@@ -207,11 +209,18 @@ int main(int argc, char** argv) {
   while (!g_stop && (a.frames < 0 || published < a.frames)) {
     // pre_animation / pre_frame: randomise the pose(s)
     if (a.scene == "falling_cubes") {
-      if (frame == a.frame_start)
+      // pre_animation: re-drop every cube at a random pose, as
+      // falling_cubes.blend.py does (xyz ~ U((-3,-3,6),(3,3,12)), euler ~ U(-pi,pi));
+      // every later frame advances the rigid-body world by one scene frame
+      if (frame == a.frame_start) {
         for (auto& b : scene.boxes) {
-          b.center = {-3 + 6 * U(rng), -3 + 6 * U(rng), -1.0 + 3 * U(rng)};
+          b.center = {-3 + 6 * U(rng), -3 + 6 * U(rng), 6 + 6 * U(rng)};
           b.rot = sim::euler_xyz(-pi + 2 * pi * U(rng), -pi + 2 * pi * U(rng), -pi + 2 * pi * U(rng));
         }
+        physics.reset(scene.boxes);
+      } else {
+        physics.step(scene.boxes, 1.0 / 60.0);
+      }
     } else if (a.fixed_rotation) {
       scene.boxes[0].rot = sim::euler_xyz(a.rot[0], a.rot[1], a.rot[2]);
     } else {

@@ -34,7 +34,7 @@ CXXFLAGS = ['-std=c++17', '-O3', '-fPIC', '-Wall', '-Wno-unused-parameter', '-pt
 
 TRANSPORT = ['transport/zmtp.cpp', 'transport/shmring.cpp']
 CODEC = ['codec/pickle_codec.cpp']
-RASTER = ['sim/raster.cpp']
+RASTER = ['sim/raster.cpp', 'sim/physics.cpp']
 
 
 def _ext_suffix():

@@ -38,7 +38,7 @@ from pathlib import Path
 import numpy as np
 
 from . import mathutils as mu
-from .mathutils import Euler, Matrix, Vector
+from .mathutils import Euler, Matrix, Vector, _euler_from_rot
 
 # ---------------------------------------------------------------------------
 # data model
@@ -102,6 +102,7 @@ class Object:
         self.users = 1
         self.active_material = None
         self.hide_render = False
+        self.rigid_body = None
 
     def __repr__(self):
         return f'<headless Object {self.name!r} ({self.type})>'
@@ -242,10 +243,53 @@ class PointCache:
         self.frame_end = end
 
 
+class RigidBodyObject:
+    """``Object.rigid_body``: an active body with a box collision shape."""
+
+    def __init__(self, type='ACTIVE', collision_shape='BOX', mass=1.0):
+        self.type = type
+        self.collision_shape = collision_shape
+        self.mass = mass
+
+
 class RigidBodyWorld:
+    """Scene rigid-body world.  Objects with a ``rigid_body`` (active, box
+    collision shape) are simulated by the native solver (csrc/sim/physics.cpp):
+    at the cache's first frame the world resets to the objects' current pose
+    (the pose ``pre_animation`` handlers just set), every later frame advances
+    it by one frame and writes the evaluated pose back -- between the
+    frame_change_pre and frame_change_post handlers, as Blender's depsgraph
+    evaluation does."""
+
     def __init__(self):
         self.point_cache = PointCache()
         self.enabled = True
+        self._world = None
+        self._objects = []
+
+    def _bodies(self, scene):
+        return [o for o in scene.objects if getattr(o, 'rigid_body', None) is not None and o.type == 'MESH']
+
+    def evaluate(self, scene):
+        if not self.enabled:
+            return
+        objs = self._bodies(scene)
+        if not objs:
+            return
+        from ... import _native
+        start = self.point_cache.frame_start
+        if self._world is None or scene.frame_current <= start or objs != self._objects:
+            self._world = _native.RigidWorld(float(scene.plane_z if scene.plane_z is not None else 0.0))
+            self._objects = objs
+            centers = np.array([np.asarray(o.location, dtype=np.float64) for o in objs])
+            rots = np.array([np.asarray(o.rotation_euler.to_matrix(), dtype=np.float64) for o in objs])
+            halves = np.array([np.asarray(o.scale, dtype=np.float64) for o in objs])   # unit cube * scale
+            self._world.set_bodies(centers, rots, halves)
+            return
+        self._world.step(1.0 / max(1, scene.render.fps))
+        for o, c, R in zip(objs, self._world.centers(), self._world.rotations()):
+            o.location = Vector(c)
+            o.rotation_euler = _euler_from_rot(np.asarray(R))
 
 
 class Scene:
@@ -267,6 +311,8 @@ class Scene:
         self.frame_current = int(frame)
         for h in list(_state.app.handlers.frame_change_pre):
             h(self, _state.depsgraph)
+        if self.rigidbody_world is not None:
+            self.rigidbody_world.evaluate(self)
         for h in list(_state.app.handlers.frame_change_post):
             h(self, _state.depsgraph)
 
@@ -394,6 +440,7 @@ def make_scene(path=None):
         cubes = []
         for i in range(7):
             c = Object(f'Cube.{i:03d}', Mesh(f'Cube.{i:03d}'), 'MESH', location=(0, 0, 2 * i))
+            c.rigid_body = RigidBodyObject()
             sc.objects[c.name] = c
             cubes.append(c)
         _state.collections['Cubes'] = ObjCollection('Cubes', cubes)
