@@ -151,6 +151,19 @@ def main():
         os.sched_setaffinity(0, plan['domain'])           # loader threads next to the GPU too
     start_port = args.start_port or (20000 + (os.getpid() % 200) * 50 if world == 1 else 21000 + rank * 64)
 
+    # size the producers' shared-memory rings to what /dev/shm can hold for
+    # every local rank (a small /dev/shm would make ring creation fail and the
+    # producers fall back to inline frames)
+    shm_slots = args.shm
+    if shm_slots > 0:
+        try:
+            st = os.statvfs('/dev/shm')
+            free = st.f_bavail * st.f_frsize
+            frame = 480 * 640 * (4 if args.mode == 'rgba' else 3)
+            fit = int(0.6 * free / max(1, frame * max(1, nprod) * local_world))
+            shm_slots = min(shm_slots, fit) if fit >= 8 else 0
+        except OSError:
+            pass
     decode = DecodeConfig.unit(channels='rgb', gamma=2.2)
     amp = args.consumer == 'disc' and args.consumer_dtype == 'bf16'
     if amp:
@@ -158,7 +171,7 @@ def main():
         decode = DecodeConfig.unit(channels='rgb', gamma=2.2, dtype='bfloat16', layout='nhwc')
     launch = dict(producer='cubesim', num_instances=nprod, named_sockets=['DATA'], start_port=start_port,
                   proto=args.proto, seed=1000 * rank, cpu_affinity=affinity,
-                  instance_args=[['--mode', args.mode, '--sndhwm', '10'] + (['--shm', str(args.shm)] if args.shm else [])]
+                  instance_args=[['--mode', args.mode, '--sndhwm', '10'] + (['--shm', str(shm_slots)] if shm_slots else [])]
                   * nprod)
     model = opt = None
     if args.consumer == 'disc':
@@ -264,7 +277,7 @@ def main():
                 'out_shape': list(shape),
                 'proto': args.proto,
                 'pinned_producers': pin,
-                'shm_slots': args.shm,
+                'shm_slots': shm_slots,
                 'h2d': args.h2d,
                 'launch_depth': args.launch_depth,
             },
