@@ -55,6 +55,7 @@ struct DecodeParams {
   void* dsts[kMaxSrcs] = {};
   int ndsts = 0;
   int max_grid = 0;
+  int unroll = 0;   // pixel groups in flight per lane (0: auto, 1 or 2)
   void* dst = nullptr;
   const float* lut = nullptr;
   const uint8_t* flip = nullptr;

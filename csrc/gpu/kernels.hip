@@ -21,6 +21,8 @@
 //   consecutive pixels -> four 16-byte stores per lane, plane-contiguous.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace btn {
@@ -129,7 +131,76 @@ __device__ __forceinline__ void store_nhwc(const DecodeParams& p, const float* l
   }
 }
 
+// Where one lane's group of PPT pixels comes from / goes to.
+struct Group {
+  int b;                 // image
+  int64_t q;             // first pixel (row-major) in the image
+  const uint8_t* src;    // first source byte (flip applied)
+};
+
+template <int PPT, int CIN>
+__device__ __forceinline__ Group locate(const DecodeParams& p, int64_t g, int64_t groups_per_img, int64_t HW) {
+  Group r;
+  r.b = int(g / groups_per_img);
+  r.q = (g - int64_t(r.b) * groups_per_img) * PPT;
+  const int y = int(r.q / p.W);
+  const int x = int(r.q - int64_t(y) * p.W);
+  const int b = r.b;
+  const bool flip = p.flip_all || (p.flip && p.flip[b]) || (b < 256 && ((p.flip_bits[b >> 6] >> (b & 63)) & 1));
+  const int sy = flip ? p.H - 1 - y : y;
+  const uint8_t* img = p.nsrcs ? p.srcs[b] : p.src + (p.src_offsets ? p.src_offsets[b] : int64_t(b) * HW * CIN);
+  r.src = img + (int64_t(sy) * p.W + x) * CIN;
+  return r;
+}
+
 template <int PPT, int CIN, int OUTT, int LAYOUT>
+__device__ __forceinline__ void emit(const DecodeParams& p, const float* lut, const int* cm, int cout, int64_t HW,
+                                     const Group& gr, const Pixels<PPT, CIN>& px) {
+  const int b = gr.b;
+  const int64_t q = gr.q;
+  if constexpr (LAYOUT == NCHW) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (c >= cout) break;
+      float v[PPT];
+      lookup<PPT, CIN>(px, cm[c], lut + c * 256, v);
+      const int64_t off = int64_t(c) * HW + q;   // within image b (NCHW)
+      if constexpr (OUTT == OUT_F32) {
+        float* d = image_out<float>(p, b, HW * cout) + off;
+#pragma unroll
+        for (int i = 0; i < PPT / 4; ++i) reinterpret_cast<float4*>(d)[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+      } else if constexpr (OUTT == OUT_BF16 || OUTT == OUT_F16) {
+        uint16_t o[PPT];
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) o[i] = OUTT == OUT_BF16 ? f2bf(v[i]) : f2h(v[i]);
+        uint16_t* d = image_out<uint16_t>(p, b, HW * cout) + off;
+#pragma unroll
+        for (int i = 0; i < PPT / 8; ++i) reinterpret_cast<uint4*>(d)[i] = *reinterpret_cast<const uint4*>(&o[8 * i]);
+      } else {
+        uint8_t o[PPT];
+#pragma unroll
+        for (int i = 0; i < PPT; ++i) o[i] = uint8_t(v[i]);
+        uint8_t* d = image_out<uint8_t>(p, b, HW * cout) + off;
+#pragma unroll
+        for (int i = 0; i < PPT / 16; ++i) reinterpret_cast<uint4*>(d)[i] = *reinterpret_cast<const uint4*>(&o[16 * i]);
+      }
+    }
+  } else {
+    // NHWC (channels_last): PPT*COUT contiguous elements, assembled in
+    // registers and written as 16-byte stores (PPT*sizeof(T) == 16).
+    switch (cout) {
+      case 1: store_nhwc<PPT, CIN, OUTT, 1>(p, lut, cm, px, b, q, HW); break;
+      case 2: store_nhwc<PPT, CIN, OUTT, 2>(p, lut, cm, px, b, q, HW); break;
+      case 3: store_nhwc<PPT, CIN, OUTT, 3>(p, lut, cm, px, b, q, HW); break;
+      default: store_nhwc<PPT, CIN, OUTT, 4>(p, lut, cm, px, b, q, HW); break;
+    }
+  }
+}
+
+// Grid-stride over pixel groups; U groups per lane per iteration: all U loads
+// are issued before the first table lookup, so each lane keeps U requests in
+// flight (memory-level parallelism once the grid is smaller than the work).
+template <int PPT, int CIN, int OUTT, int LAYOUT, int U>
 __global__ __launch_bounds__(kBlock) void decode_vec_kernel(DecodeParams p) {
   __shared__ float lut[4 * 256];
   for (int i = threadIdx.x; i < p.Cout * 256; i += kBlock) lut[i] = p.lut[i];
@@ -142,54 +213,23 @@ __global__ __launch_bounds__(kBlock) void decode_vec_kernel(DecodeParams p) {
   int cm[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) cm[c] = p.cmap[c];
+  const int64_t stride = int64_t(gridDim.x) * kBlock;
 
-  for (int64_t g = int64_t(blockIdx.x) * kBlock + threadIdx.x; g < total; g += int64_t(gridDim.x) * kBlock) {
-    const int b = int(g / groups_per_img);
-    const int64_t q = (g - int64_t(b) * groups_per_img) * PPT;   // first pixel in image
-    const int y = int(q / p.W);
-    const int x = int(q - int64_t(y) * p.W);
-    const bool flip = p.flip_all || (p.flip && p.flip[b]) || (b < 256 && ((p.flip_bits[b >> 6] >> (b & 63)) & 1));
-    const int sy = flip ? p.H - 1 - y : y;
-    const uint8_t* img = p.nsrcs ? p.srcs[b] : p.src + (p.src_offsets ? p.src_offsets[b] : int64_t(b) * HW * CIN);
-    Pixels<PPT, CIN> px;
-    load_pixels<PPT, CIN>(img + (int64_t(sy) * p.W + x) * CIN, px);
-
-    if constexpr (LAYOUT == NCHW) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        if (c >= cout) break;
-        float v[PPT];
-        lookup<PPT, CIN>(px, cm[c], lut + c * 256, v);
-        const int64_t off = int64_t(c) * HW + q;   // within image b (NCHW)
-        if constexpr (OUTT == OUT_F32) {
-          float* d = image_out<float>(p, b, HW * cout) + off;
-#pragma unroll
-          for (int i = 0; i < PPT / 4; ++i) reinterpret_cast<float4*>(d)[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
-        } else if constexpr (OUTT == OUT_BF16 || OUTT == OUT_F16) {
-          uint16_t o[PPT];
-#pragma unroll
-          for (int i = 0; i < PPT; ++i) o[i] = OUTT == OUT_BF16 ? f2bf(v[i]) : f2h(v[i]);
-          uint16_t* d = image_out<uint16_t>(p, b, HW * cout) + off;
-#pragma unroll
-          for (int i = 0; i < PPT / 8; ++i) reinterpret_cast<uint4*>(d)[i] = *reinterpret_cast<const uint4*>(&o[8 * i]);
-        } else {
-          uint8_t o[PPT];
-#pragma unroll
-          for (int i = 0; i < PPT; ++i) o[i] = uint8_t(v[i]);
-          uint8_t* d = image_out<uint8_t>(p, b, HW * cout) + off;
-#pragma unroll
-          for (int i = 0; i < PPT / 16; ++i) reinterpret_cast<uint4*>(d)[i] = *reinterpret_cast<const uint4*>(&o[16 * i]);
-        }
-      }
+  for (int64_t g0 = int64_t(blockIdx.x) * kBlock + threadIdx.x; g0 < total; g0 += U * stride) {
+    const Group gr0 = locate<PPT, CIN>(p, g0, groups_per_img, HW);
+    Pixels<PPT, CIN> px0;
+    load_pixels<PPT, CIN>(gr0.src, px0);
+    if constexpr (U == 2) {
+      const int64_t g1 = g0 + stride;
+      const bool has1 = g1 < total;
+      // second group's load goes out before the first group's lookups
+      const Group gr1 = locate<PPT, CIN>(p, has1 ? g1 : g0, groups_per_img, HW);
+      Pixels<PPT, CIN> px1;
+      load_pixels<PPT, CIN>(gr1.src, px1);
+      emit<PPT, CIN, OUTT, LAYOUT>(p, lut, cm, cout, HW, gr0, px0);
+      if (has1) emit<PPT, CIN, OUTT, LAYOUT>(p, lut, cm, cout, HW, gr1, px1);
     } else {
-      // NHWC (channels_last): PPT*COUT contiguous elements, assembled in
-      // registers and written as 16-byte stores (PPT*sizeof(T) == 16).
-      switch (cout) {
-        case 1: store_nhwc<PPT, CIN, OUTT, 1>(p, lut, cm, px, b, q, HW); break;
-        case 2: store_nhwc<PPT, CIN, OUTT, 2>(p, lut, cm, px, b, q, HW); break;
-        case 3: store_nhwc<PPT, CIN, OUTT, 3>(p, lut, cm, px, b, q, HW); break;
-        default: store_nhwc<PPT, CIN, OUTT, 4>(p, lut, cm, px, b, q, HW); break;
-      }
+      emit<PPT, CIN, OUTT, LAYOUT>(p, lut, cm, cout, HW, gr0, px0);
     }
   }
 }
@@ -223,9 +263,12 @@ __global__ __launch_bounds__(kBlock) void decode_scalar_kernel(DecodeParams p) {
 }
 
 int grid_for(int64_t work, int cap = 0) {
-  // 256 CUs x 8 resident 256-thread blocks; grid-stride beyond that
-  if (cap <= 0) cap = 2048;
+  // Measured on MI355X (profiles/decode_unroll_sweep.txt): up to ~4k blocks
+  // of work, one resident wave of 2048 blocks (256 CUs x 8) is best; for
+  // large batches a grid of 8192 blocks keeps more stores in flight
+  // (64 x 640x480 RGBA -> f32: 74.7 us at 2048 blocks, 63.3 us at 8192).
   int64_t blocks = (work + kBlock - 1) / kBlock;
+  if (cap <= 0) cap = blocks > 4096 ? 8192 : 2048;
   return int(blocks < cap ? (blocks > 0 ? blocks : 1) : cap);
 }
 
@@ -244,13 +287,29 @@ bool srcs_ok(const uint8_t* const* srcs, int n, int B, uintptr_t align) {
   return true;
 }
 
+template <int PPT, int CIN, int OUTT, int U>
+void launch_vec_u(const DecodeParams& p, int grid, hipStream_t s) {
+  if (p.layout == NCHW)
+    decode_vec_kernel<PPT, CIN, OUTT, NCHW, U><<<grid, kBlock, 0, s>>>(p);
+  else
+    decode_vec_kernel<PPT, CIN, OUTT, NHWC, U><<<grid, kBlock, 0, s>>>(p);
+}
+
 template <int PPT, int CIN, int OUTT>
 hipError_t launch_vec(const DecodeParams& p, hipStream_t s) {
   int64_t work = int64_t(p.B) * p.H * p.W / PPT;
-  if (p.layout == NCHW)
-    decode_vec_kernel<PPT, CIN, OUTT, NCHW><<<grid_for(work, p.max_grid), kBlock, 0, s>>>(p);
+  // launch-shape overrides for sweeps (BT_DECODE_MAXGRID / BT_DECODE_UNROLL)
+  static const int env_grid = std::getenv("BT_DECODE_MAXGRID") ? std::atoi(std::getenv("BT_DECODE_MAXGRID")) : 0;
+  static const int env_unroll = std::getenv("BT_DECODE_UNROLL") ? std::atoi(std::getenv("BT_DECODE_UNROLL")) : 0;
+  const int grid = grid_for(work, p.max_grid > 0 ? p.max_grid : env_grid);
+  // U=2 (two groups' loads in flight per lane) measured no faster than U=1
+  // at 8 or 64 frames once the grid is sized right; kept as an option
+  const int req = p.unroll > 0 ? p.unroll : env_unroll;
+  const int u = req > 0 ? req : 1;
+  if (u >= 2)
+    launch_vec_u<PPT, CIN, OUTT, 2>(p, grid, s);
   else
-    decode_vec_kernel<PPT, CIN, OUTT, NHWC><<<grid_for(work, p.max_grid), kBlock, 0, s>>>(p);
+    launch_vec_u<PPT, CIN, OUTT, 1>(p, grid, s);
   return hipGetLastError();
 }
 

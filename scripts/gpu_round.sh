@@ -43,6 +43,9 @@ for step in "$@"; do
           ok $rc || { echo "dpmc pass1 rc=$rc"; exit $rc; }
           timeout -k 10 120 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --kernel-trace -d /tmp/rp_dpmc2 -o run --output-format csv -- python scripts/direct_pmc.py > gpurun_out/dpmc2.log 2>&1; rc=$?
           find /tmp/rp_dpmc2 -name '*counter_collection.csv' -exec cp {} gpurun_out/dpmc/pass2_counters.csv \;;;
+    usweep) for bsz in 8 64; do for u in 1 2; do for mg in 2048 4096 8192; do
+            BT_DECODE_UNROLL=$u BT_DECODE_MAXGRID=$mg timeout -k 10 120 python scripts/kernel_bench.py --only decode --no-ref --batch $bsz --iters 100 --tag "B=$bsz unroll=$u grid=$mg" >> gpurun_out/usweep.log 2>&1 || { rc=$?; break 3; }
+          done; done; done; rc=${rc:-0}; grep -o "B=.*GBps': [0-9.]*" gpurun_out/usweep.log;;
     h2d) timeout -k 10 120 python -c "
 import sys; sys.path.insert(0,'pytorch-blender_amd')
 import torch; from blendtorch import ops; e=ops.hip_ext()

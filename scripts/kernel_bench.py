@@ -38,6 +38,7 @@ def main():
     ap.add_argument('--iters', type=int, default=200)
     ap.add_argument('--json', default=None)
     ap.add_argument('--only', default=None)
+    ap.add_argument('--no-ref', action='store_true', help='skip the eager-PyTorch reference timings')
     a = ap.parse_args()
     dev = torch.device('cuda', 0)
     B, H, W = a.batch, 480, 640
@@ -60,7 +61,7 @@ def main():
         # kernel-only time (C++ launch loop between HIP events)
         us = ext.bench_decode(x.data_ptr(), out.data_ptr(), lut.data_ptr(), B, H, W, x.shape[-1], cfg.cout,
                               list(cfg.cmap), ops.OUT_DTYPES[cfg.dtype], ops.LAYOUTS[cfg.layout], a.iters)
-        ref_us = timeit(lambda: ops.reference_decode(x, cfg), max(10, a.iters // 10), 3)
+        ref_us = float('nan') if a.no_ref else timeit(lambda: ops.reference_decode(x, cfg), max(10, a.iters // 10), 3)
         nbytes = B * H * W * (inb + outb)
         res[name] = {'us': round(us, 2), 'GBps': round(nbytes / us / 1e3, 1), 'torch_eager_us': round(ref_us, 1),
                      'speedup_vs_eager': round(ref_us / us, 1)}
