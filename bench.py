@@ -86,6 +86,8 @@ def main():
     ap.add_argument('--batch', type=int, default=8)
     ap.add_argument('--producers', type=int, default=0, help='producer processes per GPU (0 = auto)')
     ap.add_argument('--mode', choices=['rgba', 'rgb'], default='rgba')
+    ap.add_argument('--resolution', default='640x480',
+                    help='frame size WxH (the headline config is 640x480; smaller frames probe per-message costs)')
     ap.add_argument('--proto', choices=['tcp', 'ipc'], default='ipc',
                     help='ipc (Unix-domain ZMTP, same-host producers; default) or tcp')
     ap.add_argument('--consumer', choices=['none', 'disc'], default='none')
@@ -151,6 +153,7 @@ def main():
         os.sched_setaffinity(0, plan['domain'])           # loader threads next to the GPU too
     start_port = args.start_port or (20000 + (os.getpid() % 200) * 50 if world == 1 else 21000 + rank * 64)
 
+    res_w, res_h = (int(v) for v in args.resolution.lower().split('x'))
     # size the producers' shared-memory rings to what /dev/shm can hold for
     # every local rank (a small /dev/shm would make ring creation fail and the
     # producers fall back to inline frames)
@@ -159,7 +162,7 @@ def main():
         try:
             st = os.statvfs('/dev/shm')
             free = st.f_bavail * st.f_frsize
-            frame = 480 * 640 * (4 if args.mode == 'rgba' else 3)
+            frame = res_w * res_h * (4 if args.mode == 'rgba' else 3)
             fit = int(0.6 * free / max(1, frame * max(1, nprod) * local_world))
             shm_slots = min(shm_slots, fit) if fit >= 8 else 0
         except OSError:
@@ -171,7 +174,7 @@ def main():
         decode = DecodeConfig.unit(channels='rgb', gamma=2.2, dtype='bfloat16', layout='nhwc')
     launch = dict(producer='cubesim', num_instances=nprod, named_sockets=['DATA'], start_port=start_port,
                   proto=args.proto, seed=1000 * rank, cpu_affinity=affinity,
-                  instance_args=[['--mode', args.mode, '--sndhwm', '10'] + (['--shm', str(shm_slots)] if shm_slots else [])]
+                  instance_args=[['--mode', args.mode, '--sndhwm', '10', '--resolution', f'{res_w}x{res_h}'] + (['--shm', str(shm_slots)] if shm_slots else [])]
                   * nprod)
     model = opt = None
     if args.consumer == 'disc':
@@ -195,7 +198,7 @@ def main():
                               io_threads=args.io_threads or None, timeoutms=60000, h2d=args.h2d,
                               launch_depth=args.launch_depth)
         if args.dist == 'scatter':
-            shp, dt = ((480, 640, 3), torch.bfloat16) if amp else ((3, 480, 640), torch.float32)
+            shp, dt = ((res_h, res_w, 3), torch.bfloat16) if amp else ((3, res_h, res_w), torch.float32)
             it = iter(ScatterLoader(dl, args.batch, shp, dt, device, total_batches))
         else:
             it = iter(dl)
@@ -265,7 +268,7 @@ def main():
             'dtype': 'bf16' if amp else 'fp32',
             'data': 'synthetic (headless C++ Cube-scene producers, random rotations)',
             'config': {
-                'model': 'cube-scene-640x480-' + args.mode + (' + dcgan-disc' if model is not None else ''),
+                'model': f'cube-scene-{res_w}x{res_h}-' + args.mode + (' + dcgan-disc' if model is not None else ''),
                 'global_batch': args.batch * world,
                 'seq_len': None,
                 'parallelism': f'dp{world}' + ('-scatter' if args.dist == 'scatter' else ''),

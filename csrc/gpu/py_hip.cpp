@@ -35,6 +35,80 @@ void check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// Native default_collate of a batch's metadata: for every key of the first
+// item's dict, values of one scalar kind become one numpy array (int ->
+// int64, float -> float64, bool -> bool, numpy scalars keep their dtype),
+// same-shape C-order ndarrays are stacked into one [B, ...] array; anything
+// else (strings, nested containers, ragged arrays, missing keys) comes back
+// as a list of per-item Python values.  torch.from_numpy on the arrays gives
+// what torch.utils.data.default_collate would, without per-item objects.
+py::dict collate_meta(const std::vector<BatchMeta>& items) {
+  using K = codec::Value;
+  py::dict out;
+  if (items.empty() || !items[0].tree || items[0].tree->kind != K::DICT) return out;
+  const size_t B = items.size();
+  const K& first = *items[0].tree;
+  for (size_t k = 0; k + 1 < first.items.size(); k += 2) {
+    if (first.items[k]->kind != K::STR) continue;
+    const std::string& key = first.items[k]->s;
+    std::vector<const K*> vals(B, nullptr);
+    bool all = true;
+    for (size_t i = 0; i < B && all; ++i) {
+      vals[i] = items[i].tree ? items[i].tree->get(key) : nullptr;
+      all = vals[i] != nullptr;
+    }
+    const K* v0 = all ? vals[0] : nullptr;
+    auto same = [&](auto pred) {
+      for (auto* v : vals)
+        if (!pred(*v)) return false;
+      return true;
+    };
+    py::object col;
+    if (v0 && !v0->np_scalar && v0->kind == K::INT &&
+        same([](const K& v) { return v.kind == K::INT && !v.np_scalar; })) {
+      py::array_t<int64_t> a(static_cast<py::ssize_t>(B));
+      for (size_t i = 0; i < B; ++i) a.mutable_at(i) = vals[i]->i;
+      col = a;
+    } else if (v0 && !v0->np_scalar && v0->kind == K::FLOAT &&
+               same([](const K& v) { return v.kind == K::FLOAT && !v.np_scalar; })) {
+      py::array_t<double> a(static_cast<py::ssize_t>(B));
+      for (size_t i = 0; i < B; ++i) a.mutable_at(i) = vals[i]->f;
+      col = a;
+    } else if (v0 && !v0->np_scalar && v0->kind == K::BOOL &&
+               same([](const K& v) { return v.kind == K::BOOL && !v.np_scalar; })) {
+      py::array_t<bool> a(static_cast<py::ssize_t>(B));
+      for (size_t i = 0; i < B; ++i) a.mutable_at(i) = vals[i]->b;
+      col = a;
+    } else if (v0 && (v0->kind == K::NDARRAY || v0->np_scalar) &&
+               same([&](const K& v) {
+                 return (v.kind == K::NDARRAY || v.np_scalar) && v.np_scalar == v0->np_scalar && !v.fortran &&
+                        v.dtype == v0->dtype && v.shape == v0->shape;
+               })) {
+      std::vector<py::ssize_t> shape{py::ssize_t(B)};
+      if (!v0->np_scalar) shape.insert(shape.end(), v0->shape.begin(), v0->shape.end());
+      py::array a{py::dtype(v0->dtype), shape};
+      const size_t nb = v0->np_scalar ? v0->itemsize() : size_t(v0->numel()) * v0->itemsize();
+      auto* dst = static_cast<uint8_t*>(a.mutable_data());
+      for (size_t i = 0; i < B; ++i) std::memcpy(dst + i * nb, items[i].bytes.data() + vals[i]->off, nb);
+      col = a;
+    } else {
+      py::list l;
+      for (size_t i = 0; i < B; ++i) {
+        if (!vals[i]) {
+          l.append(py::none());
+          continue;
+        }
+        py::bytearray owner(reinterpret_cast<const char*>(items[i].bytes.data()), items[i].bytes.size());
+        const uint8_t* base = reinterpret_cast<const uint8_t*>(PyByteArray_AsString(owner.ptr()));
+        l.append(pyconv::value_to_py(*vals[i], base, owner));
+      }
+      col = l;
+    }
+    out[py::str(key)] = col;
+  }
+  return out;
+}
+
 void fill_cmap(int* dst, const std::vector<int>& cmap) {
   for (size_t i = 0; i < 4; ++i) dst[i] = i < cmap.size() ? cmap[i] : int(i);
 }
@@ -373,6 +447,18 @@ PYBIND11_MODULE(_hip, m) {
                metas.append(pyconv::value_to_py(*it.tree, base, owner));
              }
              return py::make_tuple(rb.index, metas, rb.recv_ms);
+           })
+      .def("next_collated",
+           [](StreamLoader& l, uintptr_t stream, long timeout_ms) -> py::object {
+             ReadyBatch rb;
+             bool ok;
+             {
+               py::gil_scoped_release nogil;
+               ok = l.next(&rb, stream_of(stream), timeout_ms);
+             }
+             if (!ok) return py::none();
+             if (rb.index < 0) return py::make_tuple(-1, py::dict(), 0.0);
+             return py::make_tuple(rb.index, collate_meta(rb.items), rb.recv_ms);
            })
       .def("stop",
            [](StreamLoader& l) {

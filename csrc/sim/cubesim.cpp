@@ -67,6 +67,7 @@ struct Args {
   int shm_slots = 0;        // >0: images go through a shared-memory ring
   bool fixed_rotation = false;
   double rot[3] = {0, 0, 0};
+  int width = 0, height = 0;   // 0: the scene's resolution (640x480)
 };
 
 [[noreturn]] void usage(const char* msg) {
@@ -115,6 +116,16 @@ Args parse(int argc, char** argv) {
     else if (k == "--fault-after") a.fault_after = std::stoll(need(i)), ++i;
     else if (k == "--verbose") a.verbose = true;
     else if (k == "--shm") a.shm_slots = std::stoi(need(i)), ++i;
+    else if (k == "--resolution") {
+      // WxH: render size (render.resolution_x/_y); the camera's field of view is kept
+      const std::string r = need(i);
+      const auto x = r.find('x');
+      if (x == std::string::npos) usage("--resolution expects WxH");
+      a.width = std::stoi(r.substr(0, x));
+      a.height = std::stoi(r.substr(x + 1));
+      if (a.width < 1 || a.height < 1) usage("bad --resolution");
+      ++i;
+    }
     else if (k == "--rotation") {
       if (i + 3 >= v.size()) usage("--rotation needs rx ry rz");
       for (int r = 0; r < 3; ++r) a.rot[r] = std::stod(v[i + 1 + r]);
@@ -171,6 +182,7 @@ int main(int argc, char** argv) {
   std::signal(SIGINT, on_signal);
 
   sim::Scene scene = a.scene == "falling_cubes" ? sim::falling_cubes_scene() : sim::cube_scene();
+  if (a.width > 0) scene.cam.width = a.width, scene.cam.height = a.height;
   const int W = scene.cam.width, H = scene.cam.height, C = a.mode == "rgba" ? 4 : 3;
   std::mt19937_64 rng(uint64_t(a.btseed));
   std::uniform_real_distribution<double> U(0.0, 1.0);

@@ -143,17 +143,18 @@ class DeviceLoader:
         loader.post(out.data_ptr(), stream.cuda_stream)
         return out
 
-    def _collate_meta(self, metas):
-        if not metas or not metas[0]:
-            return {}
-        keys = metas[0].keys()
+    def _collate_meta(self, meta):
+        """Natively collated metadata (key -> ndarray, or per-item list for
+        values that do not stack) -> what ``default_collate`` would give."""
         out = {}
-        for k in keys:
-            vals = [m.get(k) for m in metas]
-            try:
-                v = default_collate(vals)
-            except (TypeError, RuntimeError):
-                v = vals
+        for k, v in meta.items():
+            if isinstance(v, np.ndarray):
+                v = torch.from_numpy(v)
+            else:
+                try:
+                    v = default_collate(v)
+                except (TypeError, RuntimeError):
+                    pass
             if self.meta_to_device and isinstance(v, torch.Tensor):
                 v = v.to(self.device, non_blocking=True)
             out[k] = v
@@ -182,7 +183,7 @@ class DeviceLoader:
                     r = None
                     while r is None:
                         with trace_range('btt.DeviceLoader.next'):
-                            r = loader.next(stream.cuda_stream, 200)
+                            r = loader.next_collated(stream.cuda_stream, 200)
                         if r is None and (time.time() - t0) * 1000 > self.timeoutms:
                             raise TimeoutError('No response within timeout interval.')
                     idx, metas, _ = r

@@ -196,3 +196,48 @@ def test_device_loader_coalesced_launch(dev, free_port, dtype, layout):
             assert st['launches'] == 8 and st['direct_batches'] == 0
     for a, b in zip(res['auto'], res['copy']):
         assert torch.equal(a, b)
+
+
+def _same(a, b):
+    if isinstance(b, torch.Tensor):
+        return isinstance(a, torch.Tensor) and a.dtype == b.dtype and torch.equal(a, b)
+    if isinstance(b, dict):
+        return isinstance(a, dict) and a.keys() == b.keys() and all(_same(a[k], b[k]) for k in b)
+    if isinstance(b, (list, tuple)):
+        return isinstance(a, (list, tuple)) and len(a) == len(b) and all(_same(x, y) for x, y in zip(a, b))
+    return a == b
+
+
+def test_device_loader_native_collate_matches_default_collate(dev, free_port):
+    """The loader collates metadata natively; every key must come out exactly
+    as torch's default_collate would give it (ints, floats, bools, numpy
+    scalars, stacked arrays, strings, nested dicts, ragged arrays)."""
+    import threading
+    from torch.utils.data import default_collate
+    from blendtorch.btb.publisher import DataPublisher
+    addr = f'tcp://127.0.0.1:{free_port}'
+    pub = DataPublisher(addr, btid=3, lingerms=5000)
+    sent = []
+
+    def produce():
+        for i in range(8):
+            m = dict(image=np.full((16, 32, 4), i, np.uint8), frameid=i, t=0.5 * i, ok=bool(i % 2),
+                     f32=np.float32(i) / 3, xy=np.arange(6, dtype=np.float64).reshape(3, 2) + i, name=f'n{i}',
+                     info={'a': i, 'b': [i, i + 1]}, ragged=np.zeros(i + 1, np.int16))
+            sent.append(m)
+            pub.publish(**m)
+
+    th = threading.Thread(target=produce)
+    dl = DeviceLoader([addr], batch_size=8, max_items=8, device=dev, decode=ops.DecodeConfig.unit(channels='rgb'))
+    th.start()
+    b = next(iter(dl))
+    th.join()
+    pub.close()
+    ref = {k: [dict(m, btid=3)[k] for m in sent] for k in list(sent[0]) + ['btid'] if k != 'image'}
+    for k, vals in ref.items():
+        got = b[k]
+        if k == 'ragged':
+            assert isinstance(got, list) and all(np.array_equal(g, v) for g, v in zip(got, vals))
+            continue
+        assert _same(got, default_collate(vals)), k
+    assert b['image'].shape == (8, 3, 16, 32)
