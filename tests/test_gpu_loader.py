@@ -241,3 +241,21 @@ def test_device_loader_native_collate_matches_default_collate(dev, free_port):
             continue
         assert _same(got, default_collate(vals)), k
     assert b['image'].shape == (8, 3, 16, 32)
+
+
+def test_train_keypoints_example_learns(dev, free_port, tmp_path):
+    """examples/datagen/train_keypoints.py: bf16 NHWC frames straight from the
+    decode kernel train a CNN on the streamed corner annotations; the loss
+    must drop well below its start (the corners are learnable from pixels)."""
+    import importlib.util
+    import json
+    from helpers import ROOT
+    spec = importlib.util.spec_from_file_location('train_keypoints', ROOT / 'examples' / 'datagen' / 'train_keypoints.py')
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    out = tmp_path / 'kp.json'
+    mod.main(['--steps', '80', '--batch', '16', '--producers', '4', '--start-port', str(free_port),
+              '--json', str(out)])
+    res = json.loads(out.read_text())
+    assert res['loss_last10'] < 0.5 * res['loss_first10'], res
+    assert res['samples_per_s'] if 'samples_per_s' in res else res['value'] > 0
