@@ -105,8 +105,9 @@ def main():
     ap.add_argument('--backend', choices=['nccl', 'gloo'], default='nccl',
                     help='process-group backend (nccl = RCCL over xGMI; gloo only to rehearse several ranks on one GPU)')
     ap.add_argument('--start-port', type=int, default=0)
-    ap.add_argument('--dist', choices=['shard', 'scatter'], default='shard',
-                    help='shard: every rank owns its producers; scatter: rank 0 receives world*B per step '
+    ap.add_argument('--dist', choices=['shard', 'pool', 'scatter'], default='shard',
+                    help='shard: every rank owns its producers; pool: every rank launches producers and connects '
+                         'to all of them (PUSH round-robin across GPUs); scatter: rank 0 receives world*B per step '
                          'and scatters B-image shards over RCCL')
     args = ap.parse_args()
 
@@ -193,7 +194,11 @@ def main():
         if nprod > 0:
             bl = es.enter_context(btt.BlenderLauncher(**launch))
             per_step = args.batch * (world if args.dist == 'scatter' else 1)
-            dl = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=per_step, decode=decode, device=device,
+            addrs = bl.launch_info.addresses['DATA']
+            if args.dist == 'pool':
+                from blendtorch.parallel import pool_addresses
+                addrs = pool_addresses(addrs)
+            dl = DeviceLoader(addrs, batch_size=per_step, decode=decode, device=device,
                               max_items=total_batches * per_step, prefetch=6,
                               io_threads=args.io_threads or None, timeoutms=60000, h2d=args.h2d,
                               launch_depth=args.launch_depth)
@@ -246,6 +251,8 @@ def main():
         except StopIteration:
             pass
         stats = dict(dl.stats) if dl is not None else {}
+        if world > 1 and args.dist == 'pool':
+            dist.barrier()   # other ranks may still be drawing on this rank's producers
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=device if args.backend == 'nccl' else 'cpu')
     if world > 1:
@@ -271,7 +278,7 @@ def main():
                 'model': f'cube-scene-{res_w}x{res_h}-' + args.mode + (' + dcgan-disc' if model is not None else ''),
                 'global_batch': args.batch * world,
                 'seq_len': None,
-                'parallelism': f'dp{world}' + ('-scatter' if args.dist == 'scatter' else ''),
+                'parallelism': f'dp{world}' + ('' if args.dist == 'shard' else '-' + args.dist),
                 'producers_per_gpu': nprod // (world if args.dist == 'scatter' else 1),
                 'cpus_per_gpu': share,
                 'numa_local': plan['numa_local'],

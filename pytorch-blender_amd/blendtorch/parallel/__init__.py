@@ -9,6 +9,9 @@ MI355X node every GPU is a rank (``torch.distributed`` with backend
   disjoint subset of the producers and streams its own frames straight into
   its own HBM -- no GPU-GPU traffic on the hot path, weak scaling by
   construction;
+* **pool mode** (:func:`pool_addresses`): every rank launches its producers
+  but connects to all of them; PUSH round-robin balances frames across the
+  GPUs, which is the reference's fan-out semantics at node scale;
 * **scatter mode** (:class:`ScatterLoader`): a root rank receives
   ``world x B`` frames and hands each rank its B-image shard with one
   grouped send/recv round (``batch_isend_irecv``: the root drives all its
@@ -30,7 +33,8 @@ import torch.distributed as dist
 
 from .topology import parse_cpulist, plan_rank_cpus  # noqa: E402
 
-__all__ = ['init_distributed', 'rank_world', 'shard_addresses', 'partition_cpus', 'plan_rank_cpus', 'parse_cpulist',
+__all__ = ['init_distributed', 'rank_world', 'shard_addresses', 'pool_addresses', 'partition_cpus', 'plan_rank_cpus',
+           'parse_cpulist',
            'scatter_batch', 'broadcast_tensor', 'all_gather_stats', 'ScatterLoader', 'barrier']
 
 
@@ -68,6 +72,24 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 600):
 def barrier():
     if dist.is_available() and dist.is_initialized():
         dist.barrier()
+
+
+def pool_addresses(local_addresses: Sequence[str]) -> List[str]:
+    """Pool mode: every rank's producer addresses, gathered on every rank.
+
+    A loader that connects to the whole pool gets the reference's M producers
+    x W consumers topology across GPUs (examples/datagen/Readme.md:168-177):
+    each producer's PUSH socket round-robins frames over all connected ranks,
+    so a slower rank simply receives fewer frames, and a dead producer only
+    thins the pool.  Same-host shared-memory frames stay zero-copy: any rank
+    can map a producer's ring and hand the slot back.
+    """
+    local = list(local_addresses)
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return local
+    gathered = [None] * dist.get_world_size()
+    dist.all_gather_object(gathered, local)
+    return [a for part in gathered for a in part]
 
 
 def shard_addresses(addresses: Sequence[str], rank: int, world: int) -> List[str]:

@@ -47,6 +47,7 @@ for step in "$@"; do
             BT_DECODE_UNROLL=$u BT_DECODE_MAXGRID=$mg timeout -k 10 120 python scripts/kernel_bench.py --only decode --no-ref --batch $bsz --iters 100 --tag "B=$bsz unroll=$u grid=$mg" >> gpurun_out/usweep.log 2>&1 || { rc=$?; break 3; }
           done; done; done; rc=${rc:-0}; grep -o "B=.*GBps': [0-9.]*" gpurun_out/usweep.log;;
     train) timeout -k 10 300 python examples/datagen/train_keypoints.py --steps 400 --json gpurun_out/train_keypoints.json > gpurun_out/train.log 2>&1; rc=$?; grep '^{' gpurun_out/train.log;;
+    dist2pool) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29558 bench.py --gpus 2 --backend gloo --dist pool --steps 1000 --warmup 20 > gpurun_out/dist2pool.log 2>&1; rc=$?; grep '^{' gpurun_out/dist2pool.log;;
     h2d) timeout -k 10 120 python -c "
 import sys; sys.path.insert(0,'pytorch-blender_amd')
 import torch; from blendtorch import ops; e=ops.hip_ext()

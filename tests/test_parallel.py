@@ -99,6 +99,47 @@ def _worker(rank, world, port, q):
         q.put((rank, repr(e)))
 
 
+def _pool_worker(rank, world, port, prod_port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        from blendtorch import btt
+        parallel.init_distributed(backend='gloo')
+        with btt.BlenderLauncher(producer='cubesim', num_instances=1, named_sockets=['DATA'],
+                                 start_port=prod_port + 10 * rank, seed=rank,
+                                 instance_args=[['--mode', 'rgb', '--resolution', '64x48',
+                                                 '--frame-range', str(1000 * rank), str(1000 * rank + 100)]]) as bl:
+            addrs = parallel.pool_addresses(bl.launch_info.addresses['DATA'])
+            ds = btt.RemoteIterableDataset(addrs, max_items=40, timeoutms=30000)
+            import time
+            time.sleep(1.0)            # both ranks connected before frames flow
+            sources = [int(item['frameid']) // 1000 for item in ds]   # which rank's producer
+            torch.distributed.barrier()   # keep producers alive until both ranks are done
+        q.put((rank, len(addrs), sorted(set(sources)), len(sources)))
+        torch.distributed.destroy_process_group()
+    except Exception as e:  # surface failures to the parent
+        q.put((rank, repr(e)))
+
+
+def test_pool_mode_gloo_world2():
+    """Pool mode: each rank launches one producer (frame ids 0.. on rank 0,
+    1000.. on rank 1) and connects to both; every rank receives frames from
+    both producers (PUSH round-robin across ranks)."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    base = 36000 + (os.getpid() % 500) * 20
+    procs = [ctx.Process(target=_pool_worker, args=(r, 2, port, base, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert len(r) == 4, r
+        assert r[1] == 2 and r[3] == 40 and r[2] == [0, 1], r
+
+
 def test_collectives_gloo_world2():
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
