@@ -35,12 +35,14 @@ def main():
     ap.add_argument('--render-every', type=int, default=0)
     ap.add_argument('--python-client', action='store_true', help='use the pure-Python REQ clients')
     ap.add_argument('--proto', choices=['tcp', 'ipc'], default='tcp', help='tcp (as the reference) or ipc (same host)')
+    ap.add_argument('--io-threads', type=int, default=0, help='native client IO threads (0: one per 4 envs)')
     a = ap.parse_args()
     dev = torch.device(a.device)
     args = dict(producer='cartpolesim', num_instances=a.envs, named_sockets=['GYM'], start_port=a.start_port, proto=a.proto,
                 seed=7, instance_args=[['--render-every', str(a.render_every)]] * a.envs)
     with btt.BlenderLauncher(**args) as bl:
-        venv = VectorRemoteEnv(bl.launch_info.addresses['GYM'], device=dev, native=not a.python_client)
+        venv = VectorRemoteEnv(bl.launch_info.addresses['GYM'], device=dev, native=not a.python_client,
+                               io_threads=a.io_threads)
         policy = CartpolePolicy().to(dev)
         obs, _ = venv.reset()
         episodes = 0
@@ -71,7 +73,7 @@ def main():
     print(json.dumps({'metric': 'cartpole env steps/s (aggregate)', 'value': round(a.envs * a.steps / dt, 1),
                       'unit': 'steps/s', 'envs': a.envs, 'steps': a.steps, 'per_env_hz': round(a.steps / dt, 1),
                       'ms_per_step': round(dt / a.steps * 1e3, 4), 'device': str(dev), 'episodes': episodes,
-                      'client': 'python' if a.python_client else 'native', 'proto': a.proto,
+                      'client': 'python' if a.python_client else 'native', 'proto': a.proto, 'io_threads': a.io_threads,
                       'baseline': '2000 Hz (1 env, reference Readme.md:95)'}))
 
 

@@ -242,7 +242,8 @@ class VectorRemoteEnv:
     non-blocking transfer.  ``infos(i)`` returns env i's full last reply.
     """
 
-    def __init__(self, addresses, device=None, timeoutms=DEFAULT_TIMEOUTMS, obs_dim=None, native=True):
+    def __init__(self, addresses, device=None, timeoutms=DEFAULT_TIMEOUTMS, obs_dim=None, native=True,
+                 io_threads=0):
         self.addresses = list(addresses)
         self.device = device
         self.obs_dim = obs_dim
@@ -252,7 +253,8 @@ class VectorRemoteEnv:
         if native:
             try:
                 from .. import _native
-                self._native = _native.VecReq(self.addresses, timeoutms)
+                # io_threads 0: one native IO thread per 2 envs, at most 4
+                self._native = _native.VecReq(self.addresses, timeoutms, io_threads)
             except (ImportError, AttributeError):
                 self._native = None
         if self._native is None:

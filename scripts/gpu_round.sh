@@ -50,8 +50,8 @@ for step in "$@"; do
     dist2pool) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29558 bench.py --gpus 2 --backend gloo --dist pool --steps 1000 --warmup 20 > gpurun_out/dist2pool.log 2>&1; rc=$?; grep '^{' gpurun_out/dist2pool.log;;
     trainprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/rp_train -o run --output-format csv -- python examples/datagen/train_keypoints.py --steps 60 > gpurun_out/trainprof.log 2>&1; rc=$?; grep '^{' gpurun_out/trainprof.log
           mkdir -p gpurun_out/trainprof && find /tmp/rp_train -name '*kernel_stats.csv' -exec cp {} gpurun_out/trainprof/ \;;;
-    rlsweep) for cfg in "8 tcp" "8 ipc" "32 ipc" "1 ipc"; do set -- $cfg
-            timeout -k 10 200 python benchmarks/bench_rl.py --envs $1 --proto $2 --steps 4000 >> gpurun_out/rlsweep.log 2>&1 || { rc=$?; break; }
+    rlsweep) for cfg in ${RL_CFGS:-"8 tcp 0" "8 ipc 0" "32 ipc 0" "1 ipc 0"}; do set -- $cfg
+            timeout -k 10 200 python benchmarks/bench_rl.py --envs $1 --proto $2 --io-threads $3 --steps 4000 >> gpurun_out/rlsweep.log 2>&1 || { rc=$?; break; }
           done; rc=${rc:-0}; grep '^{' gpurun_out/rlsweep.log;;
     h2d) timeout -k 10 120 python -c "
 import sys; sys.path.insert(0,'pytorch-blender_amd')
