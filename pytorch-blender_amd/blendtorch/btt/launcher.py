@@ -202,6 +202,8 @@ class BlenderLauncher:
         for i, p in enumerate(self.launch_info.processes):
             if p.poll() is not None:
                 logger.warning(f'instance {i} exited with {p.returncode}; respawning')
+                from ..transport.shm import cleanup_pid
+                cleanup_pid(p.pid)   # its shm ring (consumers keep their mappings until they let go)
                 self.launch_info.processes[i] = self._spawn(i)
                 n += 1
         self.respawn_count += n

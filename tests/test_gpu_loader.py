@@ -259,3 +259,21 @@ def test_train_keypoints_example_learns(dev, free_port, tmp_path):
     res = json.loads(out.read_text())
     assert res['loss_last10'] < 0.5 * res['loss_first10'], res
     assert res['samples_per_s'] if 'samples_per_s' in res else res['value'] > 0
+
+
+def test_device_loader_survives_producer_crash_with_respawn(dev, free_port):
+    """A shared-memory producer that crashes mid-stream (fault injection) is
+    respawned by the launcher; the GPU stream keeps going on the survivors
+    and the new instance's ring, and no /dev/shm segment is left behind."""
+    import os
+    # paced producers (300 fps each) so the 800-frame stream outlives the crash and the respawn
+    args = [['--mode', 'rgba', '--shm', '16', '--fps', '300'],
+            ['--mode', 'rgba', '--shm', '16', '--fps', '300', '--fault', 'exit', '--fault-after', '30']]
+    with btt.BlenderLauncher(producer='cubesim', num_instances=2, named_sockets=['DATA'], start_port=free_port,
+                             proto='ipc', respawn=True, instance_args=args) as bl:
+        dl = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=8, max_items=800, device=dev,
+                          decode=ops.DecodeConfig.unit(channels='rgb'), timeoutms=30000)
+        n = sum(1 for _ in dl)
+        assert n == 100 and dl.stats['bad'] == 0
+        assert bl.respawn_count >= 1
+    assert not [f for f in os.listdir('/dev/shm') if f.startswith('blendtorch-')]
