@@ -1,0 +1,2 @@
+"""Command-line applications of blendtorch.btt (``blendtorch-launch``: see
+``launch.py``)."""
