@@ -246,7 +246,13 @@ PYBIND11_MODULE(_hip, m) {
           if (kind == "hostmalloc") {
             check(hipHostMalloc(reinterpret_cast<void**>(&host), slot * B, hipHostMallocDefault), "hipHostMalloc");
           } else {
-            host = static_cast<uint8_t*>(mmap(nullptr, slot * B, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0));
+            // "register": shared mapping (like the producers' shm ring, 4 KiB pages);
+            // "register_thp": private anonymous mapping with MADV_HUGEPAGE (2 MiB pages)
+            const bool thp = kind == "register_thp";
+            host = static_cast<uint8_t*>(mmap(nullptr, slot * B, PROT_READ | PROT_WRITE,
+                                              (thp ? MAP_PRIVATE : MAP_SHARED) | MAP_ANONYMOUS, -1, 0));
+            if (thp) (void)madvise(host, slot * B, MADV_HUGEPAGE);
+            std::memset(host, 0, slot * B);   // fault the pages in (huge where possible)
             check(hipHostRegister(host, slot * B, hipHostRegisterMapped), "hipHostRegister");
           }
           for (size_t i = 0; i < slot * size_t(B); ++i) host[i] = uint8_t(i * 7);

@@ -65,9 +65,9 @@ import sys; sys.path.insert(0,'pytorch-blender_amd')
 import torch; from blendtorch import ops; e=ops.hip_ext()
 import os
 B = int(os.environ.get('F2D_B', '8'))
-for cin in (4, 3):
-  for kind in ('register',):
-    for mode, grids in (('copy', (0,)), ('direct', (0, 128, 256, 512, 1024, 4096))):
+for cin in (4,):
+  for kind in ('register', 'register_thp', 'hostmalloc'):
+    for mode, grids in (('copy', (0,)), ('direct', (0, 4096))):
         for g in grids:
             us, gbs, stale = e.bench_frames_to_device(mode, kind, B, 480, 640, cin, 300, g)
             print(f'B={B} cin={cin} {kind:10s} {mode:6s} grid={g:5d} {us:8.1f} us/batch {gbs:6.1f} GB/s stale={stale}', flush=True)
