@@ -11,6 +11,7 @@
 // upper-left|lower-left   --frame-range A B   --frames N (-1 = forever)
 // --sndhwm N   --linger MS   --fps F (0 = unthrottled)   --socket NAME
 // --fault none|exit|stall|garbage --fault-after N   --rotation RX RY RZ   --verbose
+// --resolution WxH   --stamp (integrity tests: btid/seq in the first 16 image bytes)
 // --shm N (render into an N-slot shared-memory ring, send descriptors only)
 //
 // Every frame it publishes, on a bound PUSH socket with SNDHWM/LINGER/
@@ -68,6 +69,7 @@ struct Args {
   bool fixed_rotation = false;
   double rot[3] = {0, 0, 0};
   int width = 0, height = 0;   // 0: the scene's resolution (640x480)
+  bool stamp = false;          // integrity tests: (btid, seq) written into the first image row
 };
 
 [[noreturn]] void usage(const char* msg) {
@@ -115,6 +117,7 @@ Args parse(int argc, char** argv) {
     else if (k == "--fault") a.fault = need(i), ++i;
     else if (k == "--fault-after") a.fault_after = std::stoll(need(i)), ++i;
     else if (k == "--verbose") a.verbose = true;
+    else if (k == "--stamp") a.stamp = true;
     else if (k == "--shm") a.shm_slots = std::stoi(need(i)), ++i;
     else if (k == "--resolution") {
       // WxH: render size (render.resolution_x/_y); the camera's field of view is kept
@@ -266,6 +269,10 @@ int main(int argc, char** argv) {
     w.ndarray("f8", {int64_t(xy.size() / 2), 2}, xy.data());
     w.key("frameid");
     w.integer(frame);
+    if (a.stamp) {
+      w.key("seq");
+      w.integer(published);
+    }
     if (lower_left) {
       w.key("origin");
       w.str("lower-left");
@@ -291,6 +298,14 @@ int main(int argc, char** argv) {
 
     auto r0 = std::chrono::steady_clock::now();
     renderer.render(scene, pixels);
+    if (a.stamp) {
+      // bytes 0..15 of the stored image (first stored row): 'B','T', btid (u16 LE),
+      // 4 zero bytes, seq (u64 LE) -- lets tests match every decoded image to its metadata
+      uint8_t st[16] = {'B', 'T', uint8_t(a.btid & 0xff), uint8_t((a.btid >> 8) & 0xff), 0, 0, 0, 0};
+      const uint64_t q = uint64_t(published);
+      std::memcpy(st + 8, &q, 8);
+      std::memcpy(pixels, st, sizeof(st));
+    }
     if (seg) seg->publish(uint32_t(slot));   // == gen
     render_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - r0).count();
 
