@@ -20,11 +20,17 @@ struct Roctx {
   Roctx() {
     const char* e = std::getenv("BLENDTORCH_ROCTX");
     if (!e || e[0] != '1') return;
-    void* h = dlopen("libroctx64.so", RTLD_NOW | RTLD_GLOBAL);
-    if (!h) h = dlopen("/opt/rocm/lib/libroctx64.so", RTLD_NOW | RTLD_GLOBAL);
-    if (!h) return;
-    push = reinterpret_cast<int (*)(const char*)>(dlsym(h, "roctxRangePushA"));
-    pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));
+    // prefer the roctx the process already loaded (torch links its own copy,
+    // and that is the one rocprofv3 hooks); else load one
+    push = reinterpret_cast<int (*)(const char*)>(dlsym(RTLD_DEFAULT, "roctxRangePushA"));
+    pop = reinterpret_cast<int (*)()>(dlsym(RTLD_DEFAULT, "roctxRangePop"));
+    if (!push || !pop) {
+      void* h = dlopen("libroctx64.so", RTLD_NOW | RTLD_GLOBAL);
+      if (!h) h = dlopen("/opt/rocm/lib/libroctx64.so", RTLD_NOW | RTLD_GLOBAL);
+      if (!h) return;
+      push = reinterpret_cast<int (*)(const char*)>(dlsym(h, "roctxRangePushA"));
+      pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));
+    }
     on = push && pop;
   }
   static Roctx& get() {
