@@ -186,7 +186,9 @@ def main():
         opt = torch.optim.Adam(model.parameters(), lr=2e-4)
         crit = torch.nn.BCELoss()
 
-    total_batches = args.warmup + args.steps
+    WARM_RESERVE = 2000   # extra warm-up batches allowed while producers come up
+    total_batches = args.warmup + args.steps + (WARM_RESERVE if args.dist != 'scatter' else 0)
+    last = {'btid': None}
     from contextlib import ExitStack
     from blendtorch.parallel import ScatterLoader
     with ExitStack() as es:
@@ -211,6 +213,7 @@ def main():
         def step():
             b = next(it)
             img = b['image']
+            last['btid'] = b.get('btid')
             if model is not None:
                 opt.zero_grad(set_to_none=True)
                 if amp:
@@ -225,8 +228,16 @@ def main():
                 opt.step()
             return img
 
-        for _ in range(args.warmup):
+        # warm-up: at least W batches, and (shard/pool) until every local producer
+        # has delivered a frame, so the timed region starts in steady state on every rank
+        seen = set()
+        n_warm, t_warm = 0, time.time()
+        while n_warm < args.warmup or (args.dist != 'scatter' and len(seen) < nprod and n_warm < WARM_RESERVE
+                                       and time.time() - t_warm < 20):
             step()
+            n_warm += 1
+            if last['btid'] is not None:
+                seen.update(int(x) for x in last['btid'])
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -246,10 +257,13 @@ def main():
             if k in cg0 and k in cg1:
                 cpu['cgroup_' + k] = cg1[k] - cg0[k]
         shape = tuple(img.shape)
-        try:
-            next(it)
-        except StopIteration:
-            pass
+        if args.dist == 'scatter':
+            try:            # run the source to its end so its stats are final
+                next(it)
+            except StopIteration:
+                pass
+        else:
+            it.close()      # stops the native loader and publishes its stats
         stats = dict(dl.stats) if dl is not None else {}
         if world > 1 and args.dist == 'pool':
             dist.barrier()   # other ranks may still be drawing on this rank's producers
