@@ -308,3 +308,56 @@ def test_device_loader_end_to_end_integrity(dev, free_port, launch_depth):
         assert len(seqs) == len(set(seqs))             # no duplicates
         assert sorted(seqs) == seqs                     # per-producer order preserved
     assert st['direct_batches'] > 0
+
+
+_MATRIX = [
+    # (batch, resolution, mode, shm, origin, decode, launch_depth)
+    (1, '640x480', 'rgba', True, 'upper-left', 'densityopt', 2),
+    (3, '64x48', 'rgb', False, 'upper-left', 'unit', 2),
+    (100, '64x48', 'rgba', True, 'upper-left', 'unit', 2),          # > 64 images: staged-copy path
+    (8, '62x46', 'rgba', True, 'upper-left', 'unit', 2),            # W % 4 != 0: scalar kernel on host frames
+    (8, '64x48', 'rgba', True, 'lower-left', 'densityopt', 0),      # per-image flip in coalesced launches
+    (8, '64x48', 'rgba', True, 'upper-left', 'color', 0),           # MFMA colour matrix, coalesced
+    (16, '64x48', 'rgba', False, 'lower-left', 'bf16nhwc', 0),      # inline frames, bf16 NHWC, flip
+]
+
+
+@pytest.mark.parametrize('B,res,mode,use_shm,origin,dec,depth', _MATRIX)
+def test_device_loader_config_matrix(dev, free_port, B, res, mode, use_shm, origin, dec, depth):
+    """Batch sizes, odd widths, inline vs shared-memory frames, flips, dtypes
+    and coalescing, all against the fp32 reference decode of the same frame
+    (fixed pose: every frame renders identically)."""
+    M = [[0.9, 0.1, 0.0, 0.0], [0.0, 1.0, 0.0, 0.0], [0.2, 0.0, 0.8, 0.0], [0.0, 0.0, 0.0, 1.0]]
+    cfg = {'densityopt': ops.DecodeConfig.densityopt(channels='rgb', gamma=2.2),
+           'unit': ops.DecodeConfig.unit(channels='rgb'),
+           'color': ops.DecodeConfig(channels='rgba', gamma=2.2, color_matrix=M, color_bias=(0.0, 0.1, 0.0, 0.0)),
+           'bf16nhwc': ops.DecodeConfig.unit(channels='bgr', gamma=2.2, dtype='bfloat16', layout='nhwc')}[dec]
+    args = ['--mode', mode, '--resolution', res, '--rotation', '0.3', '0.6', '0.9', '--origin', origin]
+    if use_shm:
+        args += ['--shm', '128']
+    # one reference frame through the CPU path
+    with btt.BlenderLauncher(producer='cubesim', num_instances=1, named_sockets=['DATA'], start_port=free_port,
+                             proto='ipc', instance_args=[args]) as bl:
+        from blendtorch.transport import shm
+        s = zmq.Context().socket(zmq.PULL)
+        s.connect(bl.launch_info.addresses['DATA'][0])
+        assert s.poll(20000)
+        frame = np.ascontiguousarray(shm.resolve(s.recv_pyobj())['image'])
+        s.close()
+    flip = origin == 'lower-left'
+    if dec == 'color':
+        ref = ops.reference_color4x4(torch.from_numpy(frame[None]), M, cfg.color_bias, gamma=2.2, flip=flip)[0]
+        tol = 1e-5   # MFMA accumulation order vs the fp32 reference
+    else:
+        ref = ops.reference_decode(torch.from_numpy(frame[None]), cfg, flip=[int(flip)])[0]
+        tol = 0
+    with btt.BlenderLauncher(producer='cubesim', num_instances=2, named_sockets=['DATA'], start_port=free_port + 5,
+                             proto='ipc', instance_args=[args] * 2) as bl:
+        dl = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=B, max_items=4 * B, device=dev, decode=cfg,
+                          launch_depth=depth, prefetch=4)
+        for b in dl:
+            img = b['image'].cpu()
+            assert img.shape[0] == B
+            for k in range(B):
+                torch.testing.assert_close(img[k].float(), ref.float(), rtol=0, atol=tol)
+        assert dl.stats['bad'] == 0
