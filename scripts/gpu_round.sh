@@ -21,11 +21,12 @@ for step in "$@"; do
     kbench) timeout -k 10 200 python scripts/kernel_bench.py --json gpurun_out/kernel_bench.json > gpurun_out/kernel_bench.log 2>&1; rc=$?; cat gpurun_out/kernel_bench.log;;
     kprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/rp_kprof -o run --output-format csv -- python scripts/kernel_bench.py --iters 50 > gpurun_out/kprof.log 2>&1; rc=$?
           mkdir -p gpurun_out/kprof && find /tmp/rp_kprof -name '*stats.csv' -exec cp {} gpurun_out/kprof/ \;;;
-    kpmc) timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAVES --kernel-trace -d /tmp/rp_kpmc1 -o run --output-format csv -- python scripts/kernel_pmc.py > gpurun_out/kpmc1.log 2>&1; rc=$?
-          mkdir -p gpurun_out/kpmc && find /tmp/rp_kpmc1 -name '*counter_collection.csv' -exec cp {} gpurun_out/kpmc/pass1_counters.csv \;
-          ok $rc || { echo "kpmc pass1 rc=$rc"; exit $rc; }
-          timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE --kernel-trace -d /tmp/rp_kpmc2 -o run --output-format csv -- python scripts/kernel_pmc.py > gpurun_out/kpmc2.log 2>&1; rc=$?
-          find /tmp/rp_kpmc2 -name '*counter_collection.csv' -exec cp {} gpurun_out/kpmc/pass2_counters.csv \;;;
+    kpmc) for pass in "SQ_INSTS_MFMA SQ_INSTS_VALU_MFMA_F32 SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVES SQ_INSTS_VALU SQ_BUSY_CYCLES" "FETCH_SIZE" "WRITE_SIZE GRBM_GUI_ACTIVE"; do
+            n=$((${n:-0}+1))
+            timeout -k 10 240 rocprofv3 --pmc $pass --kernel-trace -d /tmp/rp_kpmc$n -o run --output-format csv -- python scripts/kernel_pmc.py > gpurun_out/kpmc$n.log 2>&1; rc=$?
+            mkdir -p gpurun_out/kpmc && find /tmp/rp_kpmc$n -name '*counter_collection.csv' -exec cp {} gpurun_out/kpmc/pass${n}_counters.csv \;
+            ok $rc || { echo "kpmc pass $n rc=$rc"; exit $rc; }
+          done;;
     rl) timeout -k 10 200 python benchmarks/bench_rl.py --envs 8 --steps 5000 > gpurun_out/bench_rl.log 2>&1; rc=$?; tail -1 gpurun_out/bench_rl.log
         timeout -k 10 200 python benchmarks/bench_rl.py --envs 1 --steps 5000 >> gpurun_out/bench_rl.log 2>&1; rc=$?; tail -1 gpurun_out/bench_rl.log;;
     dopt) timeout -k 10 300 python examples/densityopt/densityopt.py --num-epochs 70 --json gpurun_out/densityopt.json > gpurun_out/densityopt.log 2>&1; rc=$?; tail -2 gpurun_out/densityopt.log;;
