@@ -386,9 +386,11 @@ class NativeError(Exception):
       .def("__len__", [](VecReq& v) { return v.socks.size(); })
       .def("exchange",
            [](VecReq& v, const std::vector<int>& which, const std::string& cmd,
-              py::array_t<double, py::array::c_style | py::array::forcecast> actions, int obs_dim) {
+              py::array_t<double, py::array::c_style | py::array::forcecast> actions, int obs_dim, int phase) {
+             // phase 0: send all requests, then gather all replies; 1: send only
+             // (step_async); 2: gather only (step_wait) -- cmd/actions unused
              const size_t n = which.size();
-             if (cmd == "step" && size_t(actions.size()) < n) throw py::value_error("one action per env");
+             if (phase != 2 && cmd == "step" && size_t(actions.size()) < n) throw py::value_error("one action per env");
              std::vector<double> act(actions.data(), actions.data() + actions.size());
              py::array_t<double> obs(std::vector<py::ssize_t>{py::ssize_t(n), py::ssize_t(obs_dim)});
              py::array_t<double> rew(std::vector<py::ssize_t>{py::ssize_t(n)});
@@ -400,7 +402,7 @@ class NativeError(Exception):
              {
                py::gil_scoped_release nogil;
                try {
-                 for (size_t k = 0; k < n; ++k) {
+                 for (size_t k = 0; k < n && phase != 2; ++k) {
                    const int i = which[k];
                    codec::Writer w(4);
                    w.begin_dict();
@@ -419,7 +421,7 @@ class NativeError(Exception):
                    m.push_back(Frame::copy_of(b.data(), b.size()));
                    v.socks[size_t(i)]->send(std::move(m));
                  }
-                 for (size_t k = 0; k < n; ++k) {
+                 for (size_t k = 0; k < n && phase != 1; ++k) {
                    const int i = which[k];
                    Message r = v.socks[size_t(i)]->recv();
                    auto& raw = v.last[size_t(i)];
@@ -467,7 +469,7 @@ class NativeError(Exception):
              if (!err.empty()) throw py::value_error(err);
              return py::make_tuple(obs, rew, done);
            },
-           py::arg("which"), py::arg("cmd"), py::arg("actions"), py::arg("obs_dim"))
+           py::arg("which"), py::arg("cmd"), py::arg("actions"), py::arg("obs_dim"), py::arg("phase") = 0)
       .def("last_reply", [](VecReq& v, int i) {
         // full reply dict of env i (info, rgb_array, ...), decoded lazily
         auto& raw = v.last[size_t(i)];

@@ -316,6 +316,30 @@ class VectorRemoteEnv:
         done = torch.tensor([bool(r.pop('done')) for r in replies])
         return self._stage(obs), rew, done, replies
 
+    def step_async(self, actions):
+        """Send every env its action and return at once (gym VectorEnv
+        style): the remote simulations advance while the caller does other
+        work (e.g. a training step); collect with :meth:`step_wait`."""
+        import torch
+        if self._native is None or self.obs_dim is None:
+            self._async = actions          # Python path / first call: plain step in step_wait
+            return
+        if isinstance(actions, torch.Tensor):
+            actions = actions.detach().cpu().numpy()
+        actions = np.asarray(actions, dtype=np.float64).reshape(len(self), -1)[:, 0]
+        self._native.exchange(list(range(len(self))), 'step', actions, self.obs_dim, 1)
+        self._async = None
+
+    def step_wait(self):
+        """Replies to the last :meth:`step_async`: (obs, reward, done, replies-or-None)."""
+        import torch
+        pending = getattr(self, '_async', None)
+        if pending is not None:
+            self._async = None
+            return self.step(pending)
+        obs, rew, done = self._native.exchange(list(range(len(self))), 'step', np.zeros(0), self.obs_dim, 2)
+        return self._stage(obs), torch.from_numpy(np.asarray(rew)), torch.from_numpy(np.asarray(done)), None
+
     def infos(self, i):
         """Full last reply of env i (native path) as a dict."""
         if self._native is not None:

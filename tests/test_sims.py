@@ -160,3 +160,28 @@ def test_falling_cubes_fall_within_episode(free_port, producer):
     # falling from z in [6, 12]: the cubes move down the image (pixel y grows)
     assert ys[-1] > ys[0] + 5
     assert all(b >= a - 1e-6 for a, b in zip(ys[:25], ys[1:26]))   # monotone while in free fall
+
+
+def test_vector_env_step_async_matches_step(free_port):
+    """step_async/step_wait (gym VectorEnv style) drive the same deterministic
+    trajectories as step(): two identically seeded env sets, one stepped
+    synchronously, one asynchronously."""
+    trajs = []
+    for k, asynchronous in enumerate((False, True)):
+        with btt.BlenderLauncher(producer='cartpolesim', num_instances=3, named_sockets=['GYM'],
+                                 start_port=free_port + 10 * k, seed=11) as bl:
+            venv = VectorRemoteEnv(bl.launch_info.addresses['GYM'])
+            obs, _ = venv.reset()
+            out = [obs.clone()]
+            for t in range(12):
+                act = torch.full((3,), 0.5 * ((t % 3) - 1))
+                if asynchronous:
+                    venv.step_async(act)
+                    obs, rew, done, _ = venv.step_wait()
+                else:
+                    obs, rew, done, _ = venv.step(act)
+                out.append(obs.clone())
+            venv.close()
+        trajs.append(torch.stack(out))
+    assert trajs[0].shape == (13, 3, 3)
+    torch.testing.assert_close(trajs[0], trajs[1])
