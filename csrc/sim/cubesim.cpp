@@ -79,6 +79,8 @@ struct Args {
 
 Args parse(int argc, char** argv) {
   Args a;
+  // BlenderLauncher(shm_slots=N) exports BLENDTORCH_SHM_SLOTS; --shm overrides
+  if (const char* e = std::getenv("BLENDTORCH_SHM_SLOTS")) a.shm_slots = std::atoi(e);
   std::vector<std::string> v;
   int start = 1;
   for (int i = 1; i < argc; ++i)

@@ -18,10 +18,15 @@ class DataPublisher:
 
     ``shm_slots > 0`` (same-host consumers only): u8 ndarrays under
     ``shm_key`` travel through an N-slot shared-memory ring and the message
-    carries a small descriptor instead of the pixels.
+    carries a small descriptor instead of the pixels.  ``None`` (default)
+    takes the value from ``BLENDTORCH_SHM_SLOTS`` (set by
+    ``btt.BlenderLauncher(shm_slots=N)``), else 0: plain pickled frames as
+    in the reference.
     """
 
-    def __init__(self, bind_address, btid=None, send_hwm=10, lingerms=0, shm_slots=0, shm_key='image'):
+    def __init__(self, bind_address, btid=None, send_hwm=10, lingerms=0, shm_slots=None, shm_key='image'):
+        if shm_slots is None:
+            shm_slots = int(os.environ.get('BLENDTORCH_SHM_SLOTS', '0') or 0)
         self.ctx = zmq.Context()
         self.sock = self.ctx.socket(zmq.PUSH)
         self.sock.setsockopt(zmq.SNDHWM, send_hwm)

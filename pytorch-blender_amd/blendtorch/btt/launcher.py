@@ -59,8 +59,13 @@ class BlenderLauncher:
 
     Params mirror the reference (scene, script, num_instances, named_sockets,
     start_port, bind_addr, instance_args, proto, blend_path, seed, background)
-    plus ``producer``, ``cpu_affinity``, ``respawn``, ``env`` and
-    ``stdout``/``stderr`` (passed to Popen).
+    plus ``producer``, ``cpu_affinity``, ``respawn``, ``env``, ``shm_slots``
+    and ``stdout``/``stderr`` (passed to Popen).
+
+    ``shm_slots > 0`` opts every instance into the same-host shared-memory
+    frame ring (``BLENDTORCH_SHM_SLOTS`` in the children's environment: a
+    scene script's ``btb.DataPublisher`` and the native producers pick it
+    up without code changes).  Only for consumers on this host.
 
     Attributes
     ----------
@@ -71,7 +76,7 @@ class BlenderLauncher:
     def __init__(self, scene=None, script=None, num_instances=1, named_sockets=None, start_port=11000,
                  bind_addr='127.0.0.1', instance_args=None, proto='tcp', blend_path=None, seed=None,
                  background=False, producer=None, cpu_affinity=None, respawn=False, env=None, stdout=None,
-                 stderr=None):
+                 stderr=None, shm_slots=0):
         assert num_instances > 0
         self.num_instances = num_instances
         self.start_port = start_port
@@ -90,7 +95,9 @@ class BlenderLauncher:
         if cpu_affinity is not None:
             assert len(cpu_affinity) == num_instances
         self.respawn = respawn
-        self.env = env
+        self.env = dict(env or {})
+        if shm_slots:
+            self.env['BLENDTORCH_SHM_SLOTS'] = int(shm_slots)
         self.stdout = stdout
         self.stderr = stderr
 

@@ -4,7 +4,7 @@ import pytest
 import torch.utils.data as tud
 
 from blendtorch import btt
-from helpers import BLENDDIR, HEADLESS_BLENDER
+from helpers import BLENDDIR, HEADLESS_BLENDER, ROOT
 
 BATCH = 4
 INSTANCES = 1
@@ -102,3 +102,24 @@ def test_python_publisher_shared_memory(free_port):
         assert (msg['image'] == i).all() and msg['frameid'] == i
     pub.close()
     pull.close()
+
+
+def test_launcher_shm_slots_reaches_scene_scripts(free_port):
+    """BlenderLauncher(shm_slots=N) switches an unmodified scene script's
+    DataPublisher to the shared-memory ring (descriptor messages), and the
+    CPU dataset resolves them back into images."""
+    from blendtorch.transport import shm, zmq
+    ex = ROOT / 'examples' / 'datagen'
+    args = dict(scene=ex / 'cube.blend', script=ex / 'cube.blend.py', num_instances=1, named_sockets=['DATA'],
+                start_port=free_port, background=True, blend_path=HEADLESS_BLENDER, shm_slots=8)
+    with btt.BlenderLauncher(**args) as bl:
+        s = zmq.Context().socket(zmq.PULL)
+        s.connect(bl.launch_info.addresses['DATA'][0])
+        assert s.poll(30000)
+        raw = s.recv_pyobj()
+        assert shm.KEY in raw and 'image' not in raw
+        shm.release(raw[shm.KEY])
+        s.close()
+        ds = btt.RemoteIterableDataset(bl.launch_info.addresses['DATA'], max_items=12)
+        items = list(ds)
+    assert len(items) == 12 and items[0]['image'].shape == (480, 640, 3)

@@ -361,3 +361,17 @@ def test_device_loader_config_matrix(dev, free_port, B, res, mode, use_shm, orig
             for k in range(B):
                 torch.testing.assert_close(img[k].float(), ref.float(), rtol=0, atol=tol)
         assert dl.stats['bad'] == 0
+
+
+def test_scene_script_producers_zero_copy(dev, free_port):
+    """Unmodified scene scripts (examples/datagen/cube.blend.py under the bpy
+    emulation) launched with shm_slots take the zero-copy path into HBM."""
+    from helpers import HEADLESS_BLENDER, ROOT
+    ex = ROOT / 'examples' / 'datagen'
+    with btt.BlenderLauncher(scene=ex / 'cube.blend', script=ex / 'cube.blend.py', num_instances=2,
+                             named_sockets=['DATA'], start_port=free_port, background=True,
+                             blend_path=HEADLESS_BLENDER, shm_slots=16) as bl:
+        dl = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=4, max_items=32, device=dev,
+                          decode=ops.DecodeConfig.unit(channels='rgb', gamma=2.2), timeoutms=60000)
+        n = sum(1 for _ in dl)
+    assert n == 8 and dl.stats['shm_frames'] == 32 and dl.stats['direct_batches'] == 8
