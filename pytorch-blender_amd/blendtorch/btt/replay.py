@@ -198,6 +198,34 @@ class DeviceReplayBuffer:
                 view.release()
         return buf
 
+    def save_recordings(self, record_path_prefix: str, files: int = 1, chunk: int = 64):
+        """Write the stored frames (oldest first) as ``.btr`` recordings,
+        ``{prefix}_{i:02d}.btr`` for i < ``files``: one message per frame,
+        ``{image_key: u8 HxWxC, **metadata}``. The files are the format
+        ``FileRecorder`` writes, so ``FileDataset`` (CPU) and
+        :meth:`from_recordings` (GPU) read them back. This is how a stream
+        consumed on the GPU path gets recorded."""
+        from .file import FileRecorder
+        n = self._size
+        start = self._next if n == self.capacity else 0   # ring order: oldest first
+        order = [(start + i) % self.capacity for i in range(n)]
+        per = [order[i::files] for i in range(files)]
+        paths = []
+        for fi, idxs in enumerate(per):
+            path = FileRecorder.filename(record_path_prefix, fi)
+            with FileRecorder(path, max_messages=max(1, len(idxs))) as rec:
+                for s in range(0, len(idxs), chunk):
+                    sel = torch.as_tensor(idxs[s:s + chunk], dtype=torch.int64, device=self.device)
+                    imgs = self.store.index_select(0, sel).cpu().numpy()
+                    meta = {k: v.index_select(0, sel).cpu().numpy() for k, v in self.meta.items()}
+                    for j in range(len(imgs)):
+                        item = {self.image_key: imgs[j]}
+                        for k, v in meta.items():
+                            item[k] = v[j].item() if v[j].ndim == 0 else v[j]
+                        rec.save(item, is_pickled=False)
+            paths.append(path)
+        return paths
+
     # -- sampling --------------------------------------------------------------
     def _decode(self, idx: torch.Tensor, decode: DecodeConfig):
         if self.device.type == 'cuda' and decode.color_matrix is None:

@@ -108,3 +108,20 @@ def test_replay_graphed_sampler():
         assert torch.equal(b['image'], ops.decode(rb.store[idx], cfg))
         assert torch.equal(b['frameid'], idx)
     assert len({tuple(i.tolist()) for i in seen}) > 1   # new indices every replay
+
+
+def test_replay_save_recordings_roundtrip(tmp_path):
+    """Frames in a (ring-wrapped) buffer -> .btr files -> FileDataset and
+    from_recordings give back the same frames and metadata, oldest first."""
+    rb = DeviceReplayBuffer(5, device='cpu')
+    frames = torch.arange(7, dtype=torch.uint8).view(7, 1, 1, 1).expand(7, 4, 6, 3).contiguous()
+    rb.extend(frames, frameid=np.arange(7), xy=np.arange(7 * 4, dtype=np.float64).reshape(7, 2, 2))
+    paths = rb.save_recordings(str(tmp_path / 'hbm'), files=2)
+    assert len(paths) == 2
+    ds = btt.FileDataset(str(tmp_path / 'hbm'))
+    got = sorted((int(it['frameid']), int(it['image'][0, 0, 0]), it['xy'].tolist()) for it in ds)
+    assert [g[0] for g in got] == [2, 3, 4, 5, 6]            # the 5 newest survive the ring
+    assert all(g[0] == g[1] for g in got)
+    assert got[0][2] == np.arange(8, 12, dtype=np.float64).reshape(2, 2).tolist()
+    back = DeviceReplayBuffer.from_recordings(str(tmp_path / 'hbm'), device='cpu', meta_keys=('frameid',))
+    assert len(back) == 5 and sorted(back.meta['frameid'].tolist()) == [2, 3, 4, 5, 6]
