@@ -58,6 +58,18 @@ class RemoteIterableDataset(tud.IterableDataset):
         """Set the artificial length of the stream."""
         self.max_items = max_items
 
+    def device_loader(self, batch_size, device=None, decode=None, **kwargs):
+        """The MI355X path for this stream: a :class:`blendtorch.btt.gpu.DeviceLoader`
+        over the same producers, stream length, timeout and queue size,
+        delivering decoded batches in GPU memory instead of host items
+        (``item_transform`` and recording do not apply; decode with
+        ``decode`` on the GPU, record via ``DeviceReplayBuffer``)."""
+        from .gpu import DeviceLoader
+        from ..ops import DecodeConfig
+        return DeviceLoader(self.addresses, batch_size=batch_size, device=device, max_items=self.max_items,
+                            timeoutms=self.timeoutms, rcvhwm=self.queue_size,
+                            decode=decode if decode is not None else DecodeConfig(), **kwargs)
+
     def __iter__(self):
         return self._stream()
 

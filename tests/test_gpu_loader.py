@@ -375,3 +375,14 @@ def test_scene_script_producers_zero_copy(dev, free_port):
                           decode=ops.DecodeConfig.unit(channels='rgb', gamma=2.2), timeoutms=60000)
         n = sum(1 for _ in dl)
     assert n == 8 and dl.stats['shm_frames'] == 32 and dl.stats['direct_batches'] == 8
+
+
+def test_remote_iterable_dataset_device_loader(dev, free_port):
+    """RemoteIterableDataset.device_loader: the reference-style dataset object
+    hands its stream to the GPU path with the same length/timeout."""
+    with btt.BlenderLauncher(producer='cubesim', num_instances=1, named_sockets=['DATA'], start_port=free_port,
+                             proto='ipc', shm_slots=16) as bl:
+        ds = btt.RemoteIterableDataset(bl.launch_info.addresses['DATA'], max_items=24)
+        dl = ds.device_loader(8, device=dev, decode=ops.DecodeConfig.unit(channels='rgb'))
+        shapes = [tuple(b['image'].shape) for b in dl]
+    assert shapes == [(8, 3, 480, 640)] * 3 and dl.stats['direct_batches'] == 3
