@@ -56,9 +56,11 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 600):
     """
     rank, world, local = rank_world()
     use_gpu = torch.cuda.is_available()
+    # local % count: several ranks may share a GPU when rehearsing with gloo
     device = torch.device('cuda', local % max(1, torch.cuda.device_count())) if use_gpu else torch.device('cpu')
     if use_gpu:
         torch.cuda.set_device(device)
+    backend = backend or os.environ.get('BLENDTORCH_DIST_BACKEND') or None   # e.g. gloo to rehearse ranks on one GPU
     if (world > 1 or backend is not None) and not dist.is_initialized():
         backend = backend or ('nccl' if use_gpu else 'gloo')
         kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))

@@ -54,6 +54,7 @@ for step in "$@"; do
     rlsweep) for cfg in ${RL_CFGS:-"8 tcp 0" "8 ipc 0" "32 ipc 0" "1 ipc 0"}; do set -- $cfg
             timeout -k 10 200 python benchmarks/bench_rl.py --envs $1 --proto $2 --io-threads $3 --steps 4000 >> gpurun_out/rlsweep.log 2>&1 || { rc=$?; break; }
           done; rc=${rc:-0}; grep '^{' gpurun_out/rlsweep.log;;
+    train2) BLENDTORCH_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29559 examples/datagen/train_keypoints.py --steps 150 --batch 16 --producers 4 > gpurun_out/train2.log 2>&1; rc=$?; grep '^{' gpurun_out/train2.log;;
     h2d) timeout -k 10 120 python -c "
 import sys; sys.path.insert(0,'pytorch-blender_amd')
 import torch; from blendtorch import ops; e=ops.hip_ext()
