@@ -179,6 +179,8 @@ def main():
                   * nprod)
     model = opt = None
     if args.consumer == 'disc':
+        if os.environ.get('BT_CUDNN_BENCHMARK', '1') == '1':
+            torch.backends.cudnn.benchmark = True   # MIOpen find: best conv kernels for these fixed shapes
         from blendtorch.models import Discriminator
         model = Discriminator(nc=3, ndf=32, adaptive=True).to(device).to(memory_format=torch.channels_last)
         if world > 1:
