@@ -37,6 +37,15 @@ struct ToneLut {
     return v[int(x * 4096.0)];
   }
 };
+// floor / ceil to int without a libm call (exact for |v| < 2^31; the
+// arguments are clamped to a range far outside any image first)
+inline int ifloor(float v) {
+  v = std::min(std::max(v, -1e9f), 1e9f);
+  const int i = int(v);
+  return i - (v < float(i));
+}
+inline int iceil(float v) { return -ifloor(-v); }
+
 const ToneLut& tone() {
   static ToneLut t;
   return t;
@@ -402,23 +411,20 @@ void render_mesh(const Camera& cam, const std::vector<float>& verts, const std::
   for (size_t t = 0; t + 2 < tris.size(); t += 3) {
     const int a = tris[t], b = tris[t + 1], c = tris[t + 2];
     if (!ok[a] || !ok[b] || !ok[c]) continue;
-    // face normal (world) for shading, two-sided
-    const Vec3 A{verts[3 * a], verts[3 * a + 1], verts[3 * a + 2]};
-    const Vec3 B{verts[3 * b], verts[3 * b + 1], verts[3 * b + 2]};
-    const Vec3 C{verts[3 * c], verts[3 * c + 1], verts[3 * c + 2]};
-    const Vec3 e1 = sub(B, A), e2 = sub(C, A);
-    Vec3 n{e1.y * e2.z - e1.z * e2.y, e1.z * e2.x - e1.x * e2.z, e1.x * e2.y - e1.y * e2.x};
-    const double nn = std::sqrt(dot(n, n));
-    if (nn < 1e-18) continue;
-    n = scale(n, 1.0 / nn);
-    const float lam = float(std::fabs(dot(n, L)));
+    // pixel centres (x + 0.5, y + 0.5) inside the triangle's bounding box; a
+    // dense mesh seen at 64x64 has mostly sub-pixel triangles that cover no
+    // centre at all -- they are rejected before any shading work
+    const float minx = std::min({sx[a], sx[b], sx[c]}), maxx = std::max({sx[a], sx[b], sx[c]});
+    const float miny = std::min({sy[a], sy[b], sy[c]}), maxy = std::max({sy[a], sy[b], sy[c]});
+    const int x0 = std::max(0, iceil(minx - 0.5f));
+    const int x1 = std::min(W - 1, ifloor(maxx - 0.5f));
+    const int y0 = std::max(0, iceil(miny - 0.5f));
+    const int y1 = std::min(H - 1, ifloor(maxy - 0.5f));
+    if (x0 > x1 || y0 > y1) continue;
     const float area = (sx[b] - sx[a]) * (sy[c] - sy[a]) - (sx[c] - sx[a]) * (sy[b] - sy[a]);
     if (std::fabs(area) < 1e-12f) continue;
-    const int x0 = std::max(0, int(std::floor(std::min({sx[a], sx[b], sx[c]}))));
-    const int x1 = std::min(W - 1, int(std::ceil(std::max({sx[a], sx[b], sx[c]}))));
-    const int y0 = std::max(0, int(std::floor(std::min({sy[a], sy[b], sy[c]}))));
-    const int y1 = std::min(H - 1, int(std::ceil(std::max({sy[a], sy[b], sy[c]}))));
     const float inv = 1.f / area;
+    float lam = -1.f;   // face shading, computed on the first covered pixel
     for (int y = y0; y <= y1; ++y) {
       const float py = y + 0.5f;
       for (int x = x0; x <= x1; ++x) {
@@ -430,10 +436,23 @@ void render_mesh(const Camera& cam, const std::vector<float>& verts, const std::
         const float z = w0 * sz[a] + w1 * sz[b] + w2 * sz[c];
         float& zb = depth[size_t(y) * W + x];
         if (z >= zb) continue;
+        if (lam < 0.f) {
+          // face normal (world) for shading, two-sided
+          const Vec3 A{verts[3 * a], verts[3 * a + 1], verts[3 * a + 2]};
+          const Vec3 B{verts[3 * b], verts[3 * b + 1], verts[3 * b + 2]};
+          const Vec3 C{verts[3 * c], verts[3 * c + 1], verts[3 * c + 2]};
+          const Vec3 e1 = sub(B, A), e2 = sub(C, A);
+          Vec3 n{e1.y * e2.z - e1.z * e2.y, e1.z * e2.x - e1.x * e2.z, e1.x * e2.y - e1.y * e2.x};
+          const double nn = std::sqrt(dot(n, n));
+          if (nn < 1e-18) goto next_triangle;   // degenerate in 3-D: never drawn
+          n = scale(n, 1.0 / nn);
+          lam = float(std::fabs(dot(n, L)));
+        }
         zb = z;
         shade[size_t(y) * W + x] = lam;
       }
     }
+  next_triangle:;
   }
   for (int y = 0; y < H; ++y) {
     const int row = lower_left ? (H - 1 - y) : y;

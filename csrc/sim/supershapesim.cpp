@@ -86,6 +86,7 @@ int main(int argc, char** argv) {
     }
   for (int i = start; i < argc; ++i) v.push_back(argv[i]);
   int btid = 0, uv = 100, size = 64;
+  int bench = 0;   // --bench N: render N pseudo-random shapes, print ms/shape + checksum, exit
   bool gamma = true;
   std::map<std::string, std::string> sockets;
   for (size_t i = 0; i < v.size(); ++i) {
@@ -100,13 +101,46 @@ int main(int argc, char** argv) {
     } else if (v[i] == "--no-gamma") gamma = false;
     else if (v[i] == "--uv" && i + 1 < v.size()) uv = std::stoi(v[++i]);
     else if (v[i] == "--size" && i + 1 < v.size()) size = std::stoi(v[++i]);
+    else if (v[i] == "--bench" && i + 1 < v.size()) bench = std::stoi(v[++i]);
   }
-  if (!sockets.count("DATA") || !sockets.count("CTRL")) {
+  if (!bench && (!sockets.count("DATA") || !sockets.count("CTRL"))) {
     std::fprintf(stderr, "supershapesim: needs -btsockets DATA=... CTRL=...\n");
     return 2;
   }
   std::signal(SIGTERM, on_signal);
   std::signal(SIGINT, on_signal);
+  sim::Camera cam;
+  cam.width = cam.height = size;
+  cam.lens_mm = 150.0;
+  cam.loc = {10.0, -10.0, 6.0};
+  {
+    // look at the origin (-Z forward, +Y up)
+    const double dx = -cam.loc.x, dy = -cam.loc.y, dz = -cam.loc.z;
+    const double n = std::sqrt(dx * dx + dy * dy + dz * dz);
+    const double pitch = std::acos(-dz / n), yaw = std::atan2(-dx / n, dy / n);
+    cam.rot = sim::euler_xyz(pitch, 0.0, yaw);
+  }
+  sim::MeshStyle style;
+  if (bench > 0) {
+    std::vector<float> verts;
+    std::vector<int> tris;
+    std::vector<uint8_t> img(size_t(size) * size * 3);
+    uint64_t h = 1469598103934665603ull;
+    uint32_t rs = 12345;
+    auto rnd = [&] { rs = rs * 1664525u + 1013904223u; return float(rs >> 8) / float(1u << 24); };
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int k = 0; k < bench; ++k) {
+      float p[12] = {1 + 9 * rnd(), 1, 1, 1 + 4 * rnd(), 1 + 4 * rnd(), 1 + 4 * rnd(),
+                     1 + 9 * rnd(), 1, 1, 1 + 4 * rnd(), 1 + 4 * rnd(), 1 + 4 * rnd()};
+      supershape_mesh(p, uv, verts, tris);
+      sim::render_mesh(cam, verts, tris, style, img.data(), 3, false);
+      for (uint8_t b : img) h = (h ^ b) * 1099511628211ull;
+    }
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    std::printf("supershapesim bench: %d shapes, %.3f ms/shape, checksum %016llx\n", bench, ms / bench,
+                (unsigned long long)h);
+    return 0;
+  }
 
   auto pub = zmtp::Context::global().socket(zmtp::PUSH);
   pub->setsockopt(zmtp::SNDHWM, 10);
@@ -120,18 +154,6 @@ int main(int argc, char** argv) {
   ctrl->bind(sockets["CTRL"]);
   const zmtp::Socket::Interrupt intr = [] { return g_stop.load(); };
 
-  sim::Camera cam;
-  cam.width = cam.height = size;
-  cam.lens_mm = 150.0;
-  cam.loc = {10.0, -10.0, 6.0};
-  {
-    // look at the origin (-Z forward, +Y up)
-    const double dx = -cam.loc.x, dy = -cam.loc.y, dz = -cam.loc.z;
-    const double n = std::sqrt(dx * dx + dy * dy + dz * dz);
-    const double pitch = std::acos(-dz / n), yaw = std::atan2(-dx / n, dy / n);
-    cam.rot = sim::euler_xyz(pitch, 0.0, yaw);
-  }
-  sim::MeshStyle style;
   std::vector<uint8_t> glut(256);
   for (int i = 0; i < 256; ++i)
     glut[i] = gamma ? uint8_t(255.0f * std::pow(float(i) / 255.0f, float(1.0 / 2.2))) : uint8_t(i);
