@@ -340,6 +340,32 @@ class VectorRemoteEnv:
         obs, rew, done = self._native.exchange(list(range(len(self))), 'step', np.zeros(0), self.obs_dim, 2)
         return self._stage(obs), torch.from_numpy(np.asarray(rew)), torch.from_numpy(np.asarray(done)), None
 
+    def rgb_batch(self, decode=None, key='rgb_array'):
+        """The latest rendered frames of all envs as one decoded GPU batch
+        (pixel-based policies): the u8 ``HxWx3`` arrays of the last replies
+        are packed into one pinned buffer, copied to ``device`` in a single
+        transfer and run through the fused decode kernel (``decode``:
+        :class:`~blendtorch.ops.DecodeConfig`, default /255 CHW fp32).
+        Returns None when the envs did not render on their last step
+        (``--render-every``)."""
+        import torch
+        from .. import ops
+        replies = [self.infos(i) for i in range(len(self))] if self._native is not None else None
+        if replies is None:
+            raise NotImplementedError('rgb_batch needs the native client')
+        frames = [r.get(key) for r in replies]
+        if any(f is None for f in frames):
+            return None
+        arr = np.stack([np.asarray(f, dtype=np.uint8) for f in frames])
+        decode = decode or ops.DecodeConfig.unit(channels='rgb')
+        dev = torch.device(self.device) if self.device is not None else torch.device('cpu')
+        if dev.type != 'cuda':
+            return ops.reference_decode(torch.from_numpy(arr), decode)
+        if getattr(self, '_rgb_pinned', None) is None or tuple(self._rgb_pinned.shape) != arr.shape:
+            self._rgb_pinned = torch.empty(arr.shape, dtype=torch.uint8).pin_memory()
+        self._rgb_pinned.numpy()[...] = arr
+        return ops.decode(self._rgb_pinned.to(dev, non_blocking=True), decode)
+
     def infos(self, i):
         """Full last reply of env i (native path) as a dict."""
         if self._native is not None:

@@ -386,3 +386,18 @@ def test_remote_iterable_dataset_device_loader(dev, free_port):
         dl = ds.device_loader(8, device=dev, decode=ops.DecodeConfig.unit(channels='rgb'))
         shapes = [tuple(b['image'].shape) for b in dl]
     assert shapes == [(8, 3, 480, 640)] * 3 and dl.stats['direct_batches'] == 3
+
+
+def test_vector_env_rgb_batch_gpu(dev, free_port):
+    from blendtorch.btt.env import VectorRemoteEnv
+    with btt.BlenderLauncher(producer='cartpolesim', num_instances=3, named_sockets=['GYM'], start_port=free_port,
+                             instance_args=[['--render-every', '1']] * 3) as bl:
+        venv = VectorRemoteEnv(bl.launch_info.addresses['GYM'], device=dev)
+        venv.reset()
+        venv.step(torch.zeros(3))
+        cfg = ops.DecodeConfig.unit(channels='rgb', dtype='bfloat16')
+        rgb = venv.rgb_batch(cfg)
+        host = np.stack([np.asarray(venv.infos(i)['rgb_array']) for i in range(3)])
+        venv.close()
+    assert rgb.device == dev and rgb.shape == (3, 3, 270, 480)
+    assert torch.equal(rgb.cpu(), ops.reference_decode(torch.from_numpy(host), cfg))

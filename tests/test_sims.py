@@ -185,3 +185,17 @@ def test_vector_env_step_async_matches_step(free_port):
         trajs.append(torch.stack(out))
     assert trajs[0].shape == (13, 3, 3)
     torch.testing.assert_close(trajs[0], trajs[1])
+
+
+def test_vector_env_rgb_batch_cpu(free_port):
+    """Rendered frames of all envs come back as one decoded batch (CPU
+    reference path here; the GPU test runs the decode kernel)."""
+    with btt.BlenderLauncher(producer='cartpolesim', num_instances=2, named_sockets=['GYM'], start_port=free_port,
+                             instance_args=[['--render-every', '1']] * 2) as bl:
+        venv = VectorRemoteEnv(bl.launch_info.addresses['GYM'])
+        venv.reset()
+        venv.step(torch.zeros(2))
+        rgb = venv.rgb_batch()
+        venv.close()
+    assert rgb.shape == (2, 3, 270, 480) and rgb.dtype == torch.float32
+    assert 0.0 <= float(rgb.min()) and float(rgb.max()) <= 1.0 and float(rgb.std()) > 0
