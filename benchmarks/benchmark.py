@@ -50,6 +50,8 @@ def main(argv=None):
     ap.add_argument('--sleep', type=float, default=5.0, help='start-up wait before consuming (reference: 5 s)')
     ap.add_argument('--start-port', type=int, default=11000)
     ap.add_argument('--json', action='store_true', help='print one JSON line instead of the reference text')
+    ap.add_argument('--shm-slots', type=int, default=0,
+                    help='>0: producers use the same-host shared-memory frame ring (BlenderLauncher(shm_slots=N))')
     args = ap.parse_args(argv)
 
     import torch
@@ -66,7 +68,8 @@ def main(argv=None):
         blend_path = None if shutil.which('blender') else str(Path(btb.__file__).parent / 'headless' / 'bin')
         launch_args = dict(scene=EXAMPLES_DIR / f'{args.scene}.blend', script=EXAMPLES_DIR / f'{args.scene}.blend.py',
                            blend_path=blend_path, instance_args=[script_args] * args.instances)
-    launch_args.update(num_instances=args.instances, named_sockets=['DATA'], start_port=args.start_port)
+    launch_args.update(num_instances=args.instances, named_sockets=['DATA'], start_port=args.start_port,
+                       shm_slots=args.shm_slots)
 
     with btt.BlenderLauncher(**launch_args) as bl:
         addrs = bl.launch_info.addresses['DATA']
@@ -100,6 +103,7 @@ def main(argv=None):
     B = args.items // args.batch - 1
     if args.json:
         print(json.dumps({'path': args.path, 'scene': args.scene, 'mode': args.mode, 'instances': args.instances,
+                          'shm_slots': args.shm_slots,
                           'sec_per_image': (t1 - t0) / N, 'sec_per_batch': (t1 - t0) / B,
                           'images_per_sec': N / (t1 - t0), 'shape': list(imgshape)}))
     else:

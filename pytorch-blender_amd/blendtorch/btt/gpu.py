@@ -105,7 +105,10 @@ class DeviceLoader:
         self.timeoutms = timeoutms
         self.rcvhwm = rcvhwm
         self.prefetch = max(1, int(prefetch))
-        self.io_threads = io_threads or max(1, min(8, (len(self.addresses) + 3) // 4))
+        # one receive thread per producer up to 4: a thread copying inline
+        # 1.2 MB frames out of sockets tops out near 7-9k frames/s
+        # (profiles/reference_harness.md), shm descriptors cost it little
+        self.io_threads = io_threads or max(1, min(4, len(self.addresses)))
         self.image_key = image_key
         self.skip_bad = skip_bad
         self.meta_to_device = meta_to_device
