@@ -138,7 +138,9 @@ def main():
     cpus, budget, pin = cpu_budget()
     plan = plan_rank_cpus(local_rank, local_world, cpus[:budget] if pin else cpus)
     share = max(1, budget // local_world)                 # CPUs this rank may keep busy
-    nprod = args.producers or max(1, min(12, share - 3))
+    # one producer renders ~14k frames/s on the MI355X host (profiles/render_sweep.md):
+    # 4 saturate a GPU's PCIe link, 8 leave 2.5x headroom on a shared node
+    nprod = args.producers or max(1, min(8, share - 3))
     if args.dist == 'scatter':
         # the root hosts every producer, spread across the whole node
         plan = {'cpus': cpus[:budget] if pin else cpus, 'numa_local': False, 'domain': cpus}

@@ -13,6 +13,8 @@
 // --fault none|exit|stall|garbage --fault-after N   --rotation RX RY RZ   --verbose
 // --resolution WxH   --stamp (integrity tests: btid/seq in the first 16 image bytes)
 // --shm N (render into an N-slot shared-memory ring, send descriptors only)
+// --bench N (no sockets: render N frames into 8 rotating buffers, full vs
+// incremental (DirtyRect) rendering, and report the byte mismatches -- 0)
 //
 // Every frame it publishes, on a bound PUSH socket with SNDHWM/LINGER/
 // IMMEDIATE as btb.DataPublisher does (reference: btb/publisher.py:21-43),
@@ -70,6 +72,7 @@ struct Args {
   double rot[3] = {0, 0, 0};
   int width = 0, height = 0;   // 0: the scene's resolution (640x480)
   bool stamp = false;          // integrity tests: (btid, seq) written into the first image row
+  long long bench = 0;         // >0: offline render benchmark / incremental-render check
 };
 
 [[noreturn]] void usage(const char* msg) {
@@ -121,6 +124,7 @@ Args parse(int argc, char** argv) {
     else if (k == "--verbose") a.verbose = true;
     else if (k == "--stamp") a.stamp = true;
     else if (k == "--shm") a.shm_slots = std::stoi(need(i)), ++i;
+    else if (k == "--bench") a.bench = std::stoll(need(i)), ++i;
     else if (k == "--resolution") {
       // WxH: render size (render.resolution_x/_y); the camera's field of view is kept
       const std::string r = need(i);
@@ -178,11 +182,50 @@ zmtp::Frame frame_from_vector(codec::Bytes&& v) {
   return f;
 }
 
+// --bench N: the render loop without sockets.  Every frame is rendered twice,
+// once in full into a scratch buffer and once incrementally into the next of
+// 8 rotating buffers (a ring slot's life; the full renders rotate over 8
+// buffers of their own); both timings and the number of
+// differing bytes (must be 0) are printed.
+template <class Pose>
+int bench(const Args& a, sim::Scene& scene, sim::Renderer& r, Pose& pose) {
+  const size_t n = size_t(r.width()) * r.height() * r.channels();
+  constexpr int kSlots = 8;
+  std::vector<std::vector<uint8_t>> slots(kSlots, std::vector<uint8_t>(n));
+  std::vector<sim::DirtyRect> dirty(kSlots);
+  std::vector<std::vector<uint8_t>> fulls(kSlots, std::vector<uint8_t>(n));   // as cold as the slots
+  double t_full = 0, t_inc = 0;
+  long long mismatches = 0;
+  uint64_t h = 1469598103934665603ull;   // FNV-1a over every incremental frame
+  int frame = a.frame_start;
+  for (long long i = 0; i < a.bench; ++i) {
+    pose(frame);
+    frame = frame >= a.frame_end ? a.frame_start : frame + 1;
+    const uint8_t* full = fulls[size_t(i % kSlots)].data();
+    auto t0 = std::chrono::steady_clock::now();
+    r.render(scene, fulls[size_t(i % kSlots)].data());
+    auto t1 = std::chrono::steady_clock::now();
+    uint8_t* out = slots[size_t(i % kSlots)].data();
+    r.render(scene, out, &dirty[size_t(i % kSlots)]);
+    auto t2 = std::chrono::steady_clock::now();
+    t_full += std::chrono::duration<double, std::milli>(t1 - t0).count();
+    t_inc += std::chrono::duration<double, std::milli>(t2 - t1).count();
+    for (size_t k = 0; k < n; ++k) {
+      mismatches += out[k] != full[k];
+      h = (h ^ out[k]) * 1099511628211ull;
+    }
+  }
+  std::printf("{\"frames\": %lld, \"full_ms\": %.4f, \"incremental_ms\": %.4f, \"mismatched_bytes\": %lld, "
+              "\"checksum\": \"%016llx\"}\n",
+              a.bench, t_full / a.bench, t_inc / a.bench, mismatches, (unsigned long long)h);
+  return mismatches == 0 ? 0 : 1;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
   Args a = parse(argc, argv);
-  if (!a.sockets.count(a.socket)) usage(("no -btsockets entry named " + a.socket).c_str());
+  if (a.bench <= 0 && !a.sockets.count(a.socket)) usage(("no -btsockets entry named " + a.socket).c_str());
   std::signal(SIGTERM, on_signal);
   std::signal(SIGINT, on_signal);
 
@@ -197,34 +240,9 @@ int main(int argc, char** argv) {
       b.albedo = {float(U(rng)), float(U(rng)), float(U(rng))};
   }
 
-  auto sock = zmtp::Context::global().socket(zmtp::PUSH);
-  sock->setsockopt(zmtp::SNDHWM, a.sndhwm);
-  sock->setsockopt(zmtp::LINGER, a.linger);
-  sock->setsockopt(zmtp::IMMEDIATE, 1);
-  sock->bind(a.sockets[a.socket]);
-
   sim::RigidWorld physics(scene.plane_z);
-  const zmtp::Socket::Interrupt intr = [] { return g_stop.load(); };
-  const bool lower_left = a.origin == "lower-left";
-  sim::Renderer renderer(scene, C, lower_left);
-  std::unique_ptr<shm::Segment> seg;
-  if (a.shm_slots > 0) {
-    const std::string name = "blendtorch-" + std::to_string(::getpid()) + "-" + std::to_string(a.btid);
-    try {
-      seg.reset(shm::Segment::create(name, uint32_t(a.shm_slots), size_t(W) * H * C));
-    } catch (const std::exception& e) {
-      // e.g. a small /dev/shm: fall back to inline payloads
-      std::fprintf(stderr, "cubesim[%d]: shared memory disabled (%s)\n", a.btid, e.what());
-    }
-  }
-  const auto t_start = std::chrono::steady_clock::now();
-  auto next_due = t_start;
-  long long published = 0;
-  int frame = a.frame_start;
-  double render_ms = 0;
-
-  while (!g_stop && (a.frames < 0 || published < a.frames)) {
-    // pre_animation / pre_frame: randomise the pose(s)
+  // pre_animation / pre_frame: randomise the pose(s)
+  auto pose = [&](int frame) {
     if (a.scene == "falling_cubes") {
       // pre_animation: re-drop every cube at a random pose, as
       // falling_cubes.blend.py does (xyz ~ U((-3,-3,6),(3,3,12)), euler ~ U(-pi,pi));
@@ -243,6 +261,41 @@ int main(int argc, char** argv) {
     } else {
       scene.boxes[0].rot = sim::euler_xyz(pi * U(rng), pi * U(rng), pi * U(rng));
     }
+  };
+  const bool lower_left = a.origin == "lower-left";
+  sim::Renderer renderer(scene, C, lower_left);
+  if (a.bench > 0) return bench(a, scene, renderer, pose);
+
+  auto sock = zmtp::Context::global().socket(zmtp::PUSH);
+  sock->setsockopt(zmtp::SNDHWM, a.sndhwm);
+  sock->setsockopt(zmtp::LINGER, a.linger);
+  sock->setsockopt(zmtp::IMMEDIATE, 1);
+  sock->bind(a.sockets[a.socket]);
+
+  const zmtp::Socket::Interrupt intr = [] { return g_stop.load(); };
+  std::unique_ptr<shm::Segment> seg;
+  if (a.shm_slots > 0) {
+    const std::string name = "blendtorch-" + std::to_string(::getpid()) + "-" + std::to_string(a.btid);
+    try {
+      seg.reset(shm::Segment::create(name, uint32_t(a.shm_slots), size_t(W) * H * C));
+    } catch (const std::exception& e) {
+      // e.g. a small /dev/shm: fall back to inline payloads
+      std::fprintf(stderr, "cubesim[%d]: shared memory disabled (%s)\n", a.btid, e.what());
+    }
+  }
+  // what each ring slot's last frame drew over the background: a slot is
+  // re-rendered by restoring that rectangle only (BLENDTORCH_FULL_RENDER=1: off)
+  const char* full_env = std::getenv("BLENDTORCH_FULL_RENDER");
+  const bool incremental = !(full_env && std::atoi(full_env) != 0);
+  std::vector<sim::DirtyRect> slot_dirty(seg ? size_t(a.shm_slots) : 0);
+  const auto t_start = std::chrono::steady_clock::now();
+  auto next_due = t_start;
+  long long published = 0;
+  int frame = a.frame_start;
+  double render_ms = 0;
+
+  while (!g_stop && (a.frames < 0 || published < a.frames)) {
+    pose(frame);
 
     int slot = -1;
     if (seg) {
@@ -299,7 +352,8 @@ int main(int argc, char** argv) {
     uint8_t* pixels = seg ? seg->slot(uint32_t(slot)) : buf.data() + img_off;
 
     auto r0 = std::chrono::steady_clock::now();
-    renderer.render(scene, pixels);
+    sim::DirtyRect* dirty = seg && incremental ? &slot_dirty[size_t(slot)] : nullptr;
+    renderer.render(scene, pixels, dirty);
     if (a.stamp) {
       // bytes 0..15 of the stored image (first stored row): 'B','T', btid (u16 LE),
       // 4 zero bytes, seq (u64 LE) -- lets tests match every decoded image to its metadata
@@ -307,6 +361,7 @@ int main(int argc, char** argv) {
       const uint64_t q = uint64_t(published);
       std::memcpy(st + 8, &q, 8);
       std::memcpy(pixels, st, sizeof(st));
+      if (dirty) dirty->add(lower_left ? H - 1 : 0, 0, (int(sizeof(st)) + C - 1) / C - 1);
     }
     if (seg) seg->publish(uint32_t(slot));   // == gen
     render_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - r0).count();

@@ -77,6 +77,23 @@ Scene cube_scene();
 // examples/datagen/falling_cubes.blend stand-in: 7 boxes, raised camera.
 Scene falling_cubes_scene();
 
+// Bounding rectangle (image coordinates, row 0 = top, inclusive) of every
+// pixel a frame wrote over the background.  A buffer that is rendered into
+// again and again (a shared-memory ring slot) keeps the rectangle its last
+// frame left; the next render restores the background inside it only,
+// instead of copying the whole background.  `known` false = the buffer's
+// content is unknown (fresh slot): full background copy.
+struct DirtyRect {
+  int x0 = 1 << 30, y0 = 1 << 30, x1 = -1, y1 = -1;
+  bool known = false;
+  bool empty() const { return x1 < x0 || y1 < y0; }
+  void reset() { x0 = y0 = 1 << 30, x1 = y1 = -1; }
+  void add(int y, int a, int b) {
+    y0 = y < y0 ? y : y0, y1 = y > y1 ? y : y1;
+    x0 = a < x0 ? a : x0, x1 = b > x1 ? b : x1;
+  }
+};
+
 // Frame renderer.  Camera, light and ground plane are static for the life of
 // a Renderer, so their shading (the whole background) is computed once and
 // cached together with each pixel's ground-plane hit point; a frame then costs
@@ -87,7 +104,9 @@ Scene falling_cubes_scene();
 class Renderer {
  public:
   Renderer(const Scene& s, int channels, bool lower_left);
-  void render(const Scene& s, uint8_t* out);
+  // dirty: the rectangle `out`'s previous frame left (updated to this
+  // frame's); nullptr = `out` holds anything, copy the whole background
+  void render(const Scene& s, uint8_t* out, DirtyRect* dirty = nullptr);
   int width() const { return W_; }
   int height() const { return H_; }
   int channels() const { return C_; }
@@ -98,8 +117,13 @@ class Renderer {
   bool lower_left_;
   std::vector<uint8_t> background_;     // final HWC bytes, boxes absent
   std::vector<float> plane_xy_;         // per pixel ground hit (x,y); NaN = no hit
+  // per image row: the ground plane covers pixels [plane_x0_, plane_x1_] and
+  // nothing else (plane_dense_ = 1), or the row needs the per-pixel test
+  std::vector<int> plane_x0_, plane_x1_;
+  std::vector<uint8_t> plane_dense_;
   uint8_t shadow_rgb_[3];
-  std::vector<float> depth_;
+  std::vector<float> depth_;             // 1/depth per pixel, zero outside depth_rect_
+  DirtyRect depth_rect_;                // pixels of depth_ the last frame wrote
 };
 
 // Triangle-mesh rendering (z-buffered, two-sided Lambert from a directional

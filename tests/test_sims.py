@@ -199,3 +199,22 @@ def test_vector_env_rgb_batch_cpu(free_port):
         venv.close()
     assert rgb.shape == (2, 3, 270, 480) and rgb.dtype == torch.float32
     assert 0.0 <= float(rgb.min()) and float(rgb.max()) <= 1.0 and float(rgb.std()) > 0
+
+
+@pytest.mark.parametrize('args', [
+    ['--mode', 'rgba'],
+    ['--mode', 'rgb', '--origin', 'lower-left'],
+    ['--scene', 'falling_cubes', '--mode', 'rgba', '--frame-range', '0', '40'],
+    ['--scene', 'falling_cubes', '--mode', 'rgb', '--resolution', '160x120'],
+])
+def test_cubesim_incremental_render_is_exact(args):
+    """Ring-slot frames are rendered incrementally (only the rectangle the
+    slot's previous frame drew is restored from the cached background): every
+    frame must equal a full render byte for byte."""
+    import json
+    import subprocess
+    from pathlib import Path
+    exe = Path(btt.__file__).resolve().parents[1] / 'bin' / 'cubesim'
+    out = subprocess.run([str(exe), '--bench', '120', *args], capture_output=True, text=True, timeout=120)
+    rep = json.loads(out.stdout)
+    assert out.returncode == 0 and rep['mismatched_bytes'] == 0 and rep['frames'] == 120
