@@ -481,16 +481,42 @@ void render_mesh(const Camera& cam, const std::vector<float>& verts, const std::
   const int W = cam.width, H = cam.height;
   const ToneLut& T = tone();
   const size_t nv = verts.size() / 3;
-  // project every vertex once
-  std::vector<float> sx(nv), sy(nv), sz(nv);
-  std::vector<uint8_t> ok(nv);
+  // project every vertex once (Camera::project's arithmetic, focal length
+  // hoisted), and keep the range of pixel-centre columns / rows each vertex
+  // bounds: a triangle's candidate pixels are then integer min/max of its
+  // corners' ranges (rounding is monotone, so this equals rounding the
+  // triangle's float bounding box)
+  // (branch-free loops over flat arrays: the compiler vectorises both)
+  // per-thread scratch, reused across calls (every entry is written below)
+  thread_local std::vector<float> sx, sy, sz;
+  thread_local std::vector<int> cx0, cx1, cy0, cy1;
+  thread_local std::vector<uint8_t> ok;
+  for (auto* v : {&sx, &sy, &sz}) v->resize(nv);
+  for (auto* v : {&cx0, &cx1, &cy0, &cy1}) v->resize(nv);
+  ok.resize(nv);
+  const double f = cam.focal_px(), hw = 0.5 * W, hh = 0.5 * H;
+  const Mat3& R = cam.rot;
+  const double lx = cam.loc.x, ly = cam.loc.y, lz = cam.loc.z;
   for (size_t i = 0; i < nv; ++i) {
-    double px, py, d;
-    ok[i] = cam.project(Vec3{verts[3 * i], verts[3 * i + 1], verts[3 * i + 2]}, &px, &py, &d);
-    sx[i] = float(px), sy[i] = float(py), sz[i] = float(d);
+    const double wx = double(verts[3 * i]) - lx, wy = double(verts[3 * i + 1]) - ly, wz = double(verts[3 * i + 2]) - lz;
+    const double cx = R[0] * wx + R[3] * wy + R[6] * wz;   // mul_t(rot, w - loc)
+    const double cy = R[1] * wx + R[4] * wy + R[7] * wz;
+    const double cz = R[2] * wx + R[5] * wy + R[8] * wz;
+    ok[i] = cz < -1e-12;
+    sz[i] = float(-cz);
+    const double d = ok[i] ? -cz : 1.0;   // behind the camera: any finite value, never used
+    sx[i] = float(hw + f * cx / d), sy[i] = float(hh - f * cy / d);
   }
-  std::vector<float> depth(size_t(W) * H, std::numeric_limits<float>::infinity());
-  std::vector<float> shade(size_t(W) * H, -1.f);
+  for (size_t i = 0; i < nv; ++i) {
+    const float px = std::min(std::max(sx[i] - 0.5f, -1e9f), 1e9f);
+    const float py = std::min(std::max(sy[i] - 0.5f, -1e9f), 1e9f);
+    const int fx = int(px), fy = int(py);   // truncation, then floor / ceil fix-ups
+    cx1[i] = fx - (px < float(fx)), cx0[i] = fx + (px > float(fx));
+    cy1[i] = fy - (py < float(fy)), cy0[i] = fy + (py > float(fy));
+  }
+  thread_local std::vector<float> depth, shade;
+  depth.assign(size_t(W) * H, std::numeric_limits<float>::infinity());
+  shade.assign(size_t(W) * H, -1.f);
   Vec3 L = style.light_dir;
   const double ln = std::sqrt(dot(L, L));
   L = scale(L, -1.0 / ln);   // towards the light
@@ -500,13 +526,12 @@ void render_mesh(const Camera& cam, const std::vector<float>& verts, const std::
     // pixel centres (x + 0.5, y + 0.5) inside the triangle's bounding box; a
     // dense mesh seen at 64x64 has mostly sub-pixel triangles that cover no
     // centre at all -- they are rejected before any shading work
-    const float minx = std::min({sx[a], sx[b], sx[c]}), maxx = std::max({sx[a], sx[b], sx[c]});
-    const float miny = std::min({sy[a], sy[b], sy[c]}), maxy = std::max({sy[a], sy[b], sy[c]});
-    const int x0 = std::max(0, iceil(minx - 0.5f));
-    const int x1 = std::min(W - 1, ifloor(maxx - 0.5f));
-    const int y0 = std::max(0, iceil(miny - 0.5f));
-    const int y1 = std::min(H - 1, ifloor(maxy - 0.5f));
-    if (x0 > x1 || y0 > y1) continue;
+    const int x0 = std::max(0, std::min({cx0[a], cx0[b], cx0[c]}));
+    const int x1 = std::min(W - 1, std::max({cx1[a], cx1[b], cx1[c]}));
+    if (x0 > x1) continue;
+    const int y0 = std::max(0, std::min({cy0[a], cy0[b], cy0[c]}));
+    const int y1 = std::min(H - 1, std::max({cy1[a], cy1[b], cy1[c]}));
+    if (y0 > y1) continue;
     const float area = (sx[b] - sx[a]) * (sy[c] - sy[a]) - (sx[c] - sx[a]) * (sy[b] - sy[a]);
     if (std::fabs(area) < 1e-12f) continue;
     const float inv = 1.f / area;

@@ -128,17 +128,20 @@ int main(int argc, char** argv) {
     uint64_t h = 1469598103934665603ull;
     uint32_t rs = 12345;
     auto rnd = [&] { rs = rs * 1664525u + 1013904223u; return float(rs >> 8) / float(1u << 24); };
+    double mesh_ms = 0;
     const auto t0 = std::chrono::steady_clock::now();
     for (int k = 0; k < bench; ++k) {
       float p[12] = {1 + 9 * rnd(), 1, 1, 1 + 4 * rnd(), 1 + 4 * rnd(), 1 + 4 * rnd(),
                      1 + 9 * rnd(), 1, 1, 1 + 4 * rnd(), 1 + 4 * rnd(), 1 + 4 * rnd()};
+      const auto m0 = std::chrono::steady_clock::now();
       supershape_mesh(p, uv, verts, tris);
+      mesh_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - m0).count();
       sim::render_mesh(cam, verts, tris, style, img.data(), 3, false);
       for (uint8_t b : img) h = (h ^ b) * 1099511628211ull;
     }
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    std::printf("supershapesim bench: %d shapes, %.3f ms/shape, checksum %016llx\n", bench, ms / bench,
-                (unsigned long long)h);
+    std::printf("supershapesim bench: %d shapes, %.3f ms/shape (mesh %.3f), checksum %016llx\n", bench,
+                ms / bench, mesh_ms / bench, (unsigned long long)h);
     return 0;
   }
 
