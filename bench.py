@@ -7,9 +7,11 @@ MI355X-native path:
 
   K headless Cube producers per GPU (csrc/sim/cubesim, C++ rasteriser; same
   launch contract and message dict as examples/datagen/cube.blend.py)
-  --ZMTP PUSH/PULL--> native receive into pinned slots --hipMemcpyAsync-->
-  fused gfx950 decode kernel (RGBA->RGB, gamma 2.2, /255, HWC->CHW, fp32)
-  -> batch tensor resident on the GPU.
+  render into a shared-memory frame ring --ZMTP PUSH/PULL descriptors-->
+  native loader --> fused gfx950 decode kernel reading the pinned ring slots
+  over PCIe itself (zero-copy; RGBA->RGB, gamma 2.2, /255, HWC->CHW, fp32)
+  -> batch tensor resident on the GPU.  (--shm 0: frames inline in the
+  messages, received into pinned slots; --h2d copy: DMA to HBM first.)
 
 One process per GPU (``torch.distributed.run``); each rank owns its own
 producers (shard mode, weak scaling), ranks are synchronised with RCCL
@@ -269,6 +271,7 @@ def main():
         else:
             it.close()      # stops the native loader and publishes its stats
         stats = dict(dl.stats) if dl is not None else {}
+        metrics = dl.metrics() if dl is not None else {}
         if world > 1 and args.dist == 'pool':
             dist.barrier()   # other ranks may still be drawing on this rank's producers
 
@@ -313,6 +316,11 @@ def main():
             'sec_per_batch': round(tmax / args.steps, 6),
             'loader_stats': {k: stats.get(k) for k in ('frames', 'batches', 'bad', 'pool_fallbacks', 'direct_batches',
                                                        'launches', 'shm_frames', 'shm_torn')},
+            # device time per image (H2D + decode, sampled launches) and the
+            # producers' share of the frames (whole run incl. warm-up)
+            'gpu_us_per_image': (round(metrics['gpu_us_per_image'], 3)
+                                 if metrics.get('gpu_us_per_image') is not None else None),
+            'frames_per_producer': metrics.get('frames_per_producer'),
             'cpu': cpu,
         }), flush=True)
     if world > 1:

@@ -417,7 +417,10 @@ bool StreamLoader::process(zmtp::Message&& msg) {
     std::lock_guard<std::mutex> lk(mu_);
     stats_.frames++;
     stats_.bytes += n;
+    stats_.image_bytes += img_bytes_;
     if (it.seg) stats_.shm_frames++;
+    if (const codec::Value* b = root->get("btid"))
+      if (b->kind == codec::Value::INT) stats_.frames_per_btid[b->i]++;
   }
   cur_.push_back(std::move(it));
   if (int(cur_.size()) == cfg_.batch_size) launch();
@@ -445,6 +448,17 @@ void StreamLoader::reap(bool wait_all) {
     hipError_t q = wait_all ? hipEventSynchronize(f.copied) : hipEventQuery(f.copied);
     if (q == hipErrorNotReady) break;
     (void)hipEventDestroy(f.copied);
+    if (f.t0) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, f.t0, f.t1) == hipSuccess) {
+        std::lock_guard<std::mutex> lk(mu_);
+        stats_.timed_launches++;
+        stats_.timed_images += uint64_t(f.images);
+        stats_.timed_gpu_ms += ms;
+      }
+      (void)hipEventDestroy(f.t0);
+      (void)hipEventDestroy(f.t1);
+    }
     for (auto& s : f.slots) {
       if (!s.seg->valid(s.slot, s.gen)) {   // reclaimed by the producer under the DMA
         std::lock_guard<std::mutex> lk(mu_);
@@ -547,6 +561,16 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
       if (i >= 256) throw std::runtime_error("StreamLoader: per-image flip supports batch <= 256");
       flips[i >> 6] |= uint64_t(1) << (i & 63);
     }
+  // sampled GPU timing: events bracket this launch's copies + kernel (the
+  // stream has already passed the consumers' post events here)
+  hipEvent_t t0 = nullptr, t1 = nullptr;
+  if (stats_.launches % kTimedEvery == 0 && hipEventCreate(&t0) == hipSuccess) {
+    if (hipEventCreate(&t1) != hipSuccess || hipEventRecord(t0, stream_) != hipSuccess) {
+      (void)hipEventDestroy(t0);
+      if (t1) (void)hipEventDestroy(t1);
+      t0 = t1 = nullptr;
+    }
+  }
   uint8_t* stage = nullptr;
   if (!direct) {   // copy path: exactly one batch per launch
     stage = staging_[size_t(batch_index_) % staging_.size()];
@@ -609,7 +633,9 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
   }
   check(e, "decode kernel launch");
   if (direct) check(hipEventRecord(copied, stream_), "hipEventRecord(copied)");
+  if (t0) check(hipEventRecord(t1, stream_), "hipEventRecord(t1)");
   Inflight fl;
+  fl.t0 = t0, fl.t1 = t1, fl.images = total;
   fl.frames.reserve(size_t(total));
   std::vector<ReadyBatch> done;
   for (auto& b : group) {

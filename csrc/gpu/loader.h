@@ -133,7 +133,13 @@ struct LoaderStats {
   uint64_t shm_stale = 0;                  // descriptors dropped: slot already reclaimed on arrival
   uint64_t direct_batches = 0;             // decoded straight from host memory (no staging copy)
   uint64_t launches = 0;                   // decode kernel launches (< batches when coalesced)
+  uint64_t image_bytes = 0;                // image bytes that crossed host -> device
   double h2d_issue_ms = 0;
+  // GPU time of every kTimedEvery-th launch (timing events around its H2D
+  // copies + decode kernel): per-image device cost without timing every launch
+  uint64_t timed_launches = 0, timed_images = 0;
+  double timed_gpu_ms = 0;
+  std::map<int64_t, uint64_t> frames_per_btid;   // provenance: frames per producer id
 };
 
 class StreamLoader {
@@ -208,8 +214,11 @@ class StreamLoader {
   std::vector<Item> cur_;
   std::deque<Pending> pending_;
   int pending_images_ = 0;
+  static constexpr int kTimedEvery = 16;
   struct Inflight {
     hipEvent_t copied;
+    hipEvent_t t0 = nullptr, t1 = nullptr;   // sampled launch timing (or null)
+    int images = 0;
     std::vector<zmtp::Frame> frames;
     struct Slot {
       shm::Segment* seg;

@@ -485,6 +485,13 @@ PYBIND11_MODULE(_hip, m) {
         d["shm_stale"] = s.shm_stale;
         d["direct_batches"] = s.direct_batches;
         d["launches"] = s.launches;
+        d["image_bytes"] = s.image_bytes;
+        d["timed_launches"] = s.timed_launches;
+        d["timed_images"] = s.timed_images;
+        d["timed_gpu_ms"] = s.timed_gpu_ms;
+        py::dict per;
+        for (const auto& kv : s.frames_per_btid) per[py::int_(kv.first)] = kv.second;
+        d["frames_per_btid"] = per;
         return d;
       });
 }

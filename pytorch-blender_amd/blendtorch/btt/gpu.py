@@ -61,7 +61,7 @@ class DeviceLoader:
     prefetch: int
         Output batches the native pipeline may run ahead of the consumer.
     io_threads: int, optional
-        Receive IO threads (default: one per 4 addresses, at least 1).
+        Receive IO threads (default: one per address, at most 4).
     image_key: str
         Dict key holding the u8 HxWxC image.
     skip_bad: bool
@@ -80,13 +80,16 @@ class DeviceLoader:
         together in one launch (fewer kernel ramp-up/tail phases when the GPU
         side is the bottleneck).  0: hold batches until 64 images are pending
         or the stream ends (tests / maximal coalescing).
+    log_every: float, optional
+        Log :meth:`metrics` on the ``'blendtorch'`` logger every that many
+        seconds while iterating.
     """
 
     def __init__(self, addresses: Sequence[str], batch_size: int = 8, decode: DecodeConfig = DecodeConfig(),
                  device=None, max_items: Optional[int] = None, timeoutms: int = DEFAULT_TIMEOUTMS,
                  rcvhwm: int = 10, prefetch: int = 4, io_threads: Optional[int] = None, image_key: str = 'image',
                  skip_bad: bool = False, meta_to_device: bool = False, staging_depth: int = 3, h2d: str = 'auto',
-                 launch_depth: int = 2):
+                 launch_depth: int = 2, log_every: Optional[float] = None):
         if h2d not in ('auto', 'copy'):
             raise ValueError("h2d must be 'auto' or 'copy'")
         self.h2d = h2d
@@ -114,8 +117,18 @@ class DeviceLoader:
         self.meta_to_device = meta_to_device
         self.staging_depth = staging_depth
         self._loader = None
+        self._live = None          # native pipeline while iterating
         self.shape = None          # (H, W, C) of incoming frames
         self.stats = {}
+        self.log_every = log_every
+        self._t_start = self._t_end = None
+        self._wait_s = 0.0
+
+    @classmethod
+    def from_config(cls, addresses: Sequence[str], config, decode: DecodeConfig = DecodeConfig(), device=None,
+                    max_items: Optional[int] = None) -> 'DeviceLoader':
+        """Build from a :class:`blendtorch.utils.StreamConfig`."""
+        return cls(addresses, decode=decode, device=device, max_items=max_items, **config.kwargs())
 
     def __len__(self):
         if self.max_items is None:
@@ -163,9 +176,54 @@ class DeviceLoader:
             out[k] = v
         return out
 
+    def metrics(self) -> dict:
+        """Pipeline counters: live while iterating, final afterwards.
+
+        ``frames_per_s`` / ``h2d_gbytes_per_s``: delivered frames and the image
+        bytes they moved host -> device, over the time since the first frame;
+        ``frames_per_producer``: frames per producer ``btid`` (provenance, as
+        the reference's messages carry it); ``gpu_us_per_image``: device time
+        (H2D copies + decode kernel) per image, sampled every 16th launch with
+        timing events; ``images_per_launch``: launch coalescing;
+        ``consumer_wait_s``: time the consumer spent blocked on the next batch.
+        """
+        s = self._live.stats() if self._live is not None else dict(self.stats)
+        if not s or self._t_start is None:
+            return {}
+        elapsed = max(1e-9, (self._t_end or time.perf_counter()) - self._t_start)
+        per = {int(k): int(v) for k, v in s.get('frames_per_btid', {}).items()}
+        timed = s.get('timed_images', 0)
+        return {
+            'elapsed_s': elapsed,
+            'frames': s['frames'],
+            'batches': s['batches'],
+            'frames_per_s': s['frames'] / elapsed,
+            'h2d_gbytes_per_s': s.get('image_bytes', 0) / elapsed / 1e9,
+            'frames_per_producer': per,
+            'producer_frames_per_s': {k: v / elapsed for k, v in per.items()},
+            'gpu_us_per_image': s['timed_gpu_ms'] * 1e3 / timed if timed else None,
+            'launches': s['launches'],
+            'images_per_launch': s['frames'] / s['launches'] if s['launches'] else None,
+            'direct_batches': s['direct_batches'],
+            'consumer_wait_s': self._wait_s,
+            'bad': s['bad'], 'shm_stale': s['shm_stale'], 'shm_torn': s['shm_torn'],
+            'pool_fallbacks': s['pool_fallbacks'],
+        }
+
+    def _log_metrics(self):
+        m = self.metrics()
+        if m:
+            logger.info('DeviceLoader: %.0f frames/s, %.1f GB/s H2D, %s us/image on the GPU, %.2f images/launch, '
+                        'consumer wait %.2fs, producers %s', m['frames_per_s'], m['h2d_gbytes_per_s'],
+                        'n/a' if m['gpu_us_per_image'] is None else '%.1f' % m['gpu_us_per_image'],
+                        m['images_per_launch'] or 0.0, m['consumer_wait_s'], m['frames_per_producer'])
+
     def __iter__(self):
         loader = self._make()
         loader.start()
+        self._live = loader
+        self._t_start = self._t_end = None
+        self._wait_s = 0.0
         try:
             with torch.cuda.device(self.device):
                 stream = torch.cuda.current_stream(self.device)
@@ -176,6 +234,8 @@ class DeviceLoader:
                     if shape is None and (time.time() - t0) * 1000 > self.timeoutms:
                         raise TimeoutError('No response within timeout interval.')
                 self.shape = tuple(shape)
+                self._t_start = time.perf_counter()
+                last_log = self._t_start
                 n_batches = None if self.max_items is None else self.max_items // self.batch_size
                 pending = [self._post(loader, stream) for _ in range(self.prefetch if n_batches is None
                                                                         else min(self.prefetch, n_batches))]
@@ -183,12 +243,17 @@ class DeviceLoader:
                 delivered = 0
                 while n_batches is None or delivered < n_batches:
                     t0 = time.time()
+                    tw = time.perf_counter()
                     r = None
                     while r is None:
                         with trace_range('btt.DeviceLoader.next'):
                             r = loader.next_collated(stream.cuda_stream, 200)
                         if r is None and (time.time() - t0) * 1000 > self.timeoutms:
                             raise TimeoutError('No response within timeout interval.')
+                    self._wait_s += time.perf_counter() - tw
+                    if self.log_every is not None and tw - last_log >= self.log_every:
+                        last_log = tw
+                        self._log_metrics()
                     idx, metas, _ = r
                     if idx < 0:
                         break
@@ -202,4 +267,6 @@ class DeviceLoader:
                     yield batch
         finally:
             self.stats = loader.stats()
+            self._t_end = time.perf_counter()
+            self._live = None
             loader.stop()

@@ -95,14 +95,23 @@ def trace_range(name: str):
 
 @dataclasses.dataclass
 class StreamConfig:
-    """Knobs of the device streaming path (defaults = reference behaviour).
+    """Knobs of the device streaming path in one place (defaults = reference
+    behaviour where the reference has the knob).
+
+    Pass it as ``DeviceLoader.from_config(addresses, cfg, decode=...)``;
+    every field maps onto the :class:`~blendtorch.btt.DeviceLoader` argument
+    of the same name.
 
     batch_size: items per batch; rcvhwm: receive queue per producer (the
-    reference's ``queue_size``); timeoutms: max silence before failing;
-    prefetch: decoded batches the native pipeline may run ahead;
-    io_threads: receive IO threads (None: one per 4 producers);
-    mode: 'shard' (each rank owns producers) or 'scatter' (root receives and
-    scatters over RCCL).
+    reference's ``queue_size``, 10); timeoutms: max silence before failing
+    (10 s, ``btt/constants.py``); prefetch: output batches the native
+    pipeline may run ahead; io_threads: receive IO threads (None: one per
+    producer, at most 4); staging_depth: device staging buffers of the copy
+    path; h2d: 'auto' (zero-copy reads of pinned frames when possible) or
+    'copy'; launch_depth: decode launches queued before batches coalesce;
+    image_key: dict key of the image; skip_bad: drop malformed messages
+    instead of failing; meta_to_device: move collated metadata to the GPU;
+    log_every: seconds between metric log lines (None: off).
     """
     batch_size: int = 8
     rcvhwm: int = 10
@@ -110,8 +119,18 @@ class StreamConfig:
     prefetch: int = 4
     io_threads: Optional[int] = None
     staging_depth: int = 3
-    mode: str = 'shard'
+    h2d: str = 'auto'
+    launch_depth: int = 2
+    image_key: str = 'image'
+    skip_bad: bool = False
+    meta_to_device: bool = False
+    log_every: Optional[float] = None
 
     def __post_init__(self):
-        if self.mode not in ('shard', 'scatter'):
-            raise ValueError("mode must be 'shard' or 'scatter'")
+        if self.h2d not in ('auto', 'copy'):
+            raise ValueError("h2d must be 'auto' or 'copy'")
+        if self.batch_size < 1 or self.prefetch < 1:
+            raise ValueError('batch_size and prefetch must be >= 1')
+
+    def kwargs(self) -> dict:
+        return dataclasses.asdict(self)

@@ -401,3 +401,32 @@ def test_vector_env_rgb_batch_gpu(dev, free_port):
         venv.close()
     assert rgb.device == dev and rgb.shape == (3, 3, 270, 480)
     assert torch.equal(rgb.cpu(), ops.reference_decode(torch.from_numpy(host), cfg))
+
+
+def test_device_loader_metrics(dev, free_port, caplog):
+    """metrics(): live while iterating and final afterwards -- per-producer
+    provenance, H2D bytes, sampled GPU time per image, coalescing, consumer
+    wait; StreamConfig builds the same loader; log_every logs them."""
+    import logging
+    import time
+    from blendtorch.utils import StreamConfig
+    with btt.BlenderLauncher(producer='cubesim', num_instances=2, named_sockets=['DATA'], start_port=free_port,
+                             seed=5, instance_args=[['--mode', 'rgba']] * 2) as bl:
+        cfg = StreamConfig(batch_size=8, log_every=0.0)
+        dl = DeviceLoader.from_config(bl.launch_info.addresses['DATA'], cfg, max_items=1024, device=dev,
+                                      decode=ops.DecodeConfig.unit(channels='rgb'))
+        assert dl.metrics() == {}
+        time.sleep(1.0)
+        live = None
+        with caplog.at_level(logging.INFO, logger='blendtorch'):
+            for i, b in enumerate(dl):
+                if i == 64:
+                    live = dl.metrics()
+        m = dl.metrics()
+    assert live and 0 < live['frames'] <= m['frames']
+    assert m['frames'] == 1024 and m['batches'] == 128 and m['bad'] == 0
+    assert set(m['frames_per_producer']) == {0, 1} and sum(m['frames_per_producer'].values()) == 1024
+    assert m['h2d_gbytes_per_s'] > 0 and m['frames_per_s'] > 0
+    assert m['gpu_us_per_image'] is not None and m['gpu_us_per_image'] > 0
+    assert m['images_per_launch'] >= 8 and m['consumer_wait_s'] >= 0
+    assert any('DeviceLoader:' in r.getMessage() for r in caplog.records)
