@@ -1,4 +1,4 @@
-// StreamLoader: producer frames -> pinned host slots -> HBM -> decoded batch.
+// StreamLoader: producer frames -> decoded batch in HBM.
 //
 // Replaces the reference's receive path (pkg_pytorch/blendtorch/btt/
 // dataset.py:64-117 PULL socket per DataLoader worker + pickle.loads +
@@ -6,16 +6,22 @@
 // pipeline per GPU rank:
 //
 //   producers --PUSH/ZMTP--> K PULL sockets (K IO threads, fair-queued)
-//     -> frame bodies read by the IO thread straight into hipHostMalloc'd
-//        slots (PinnedPool is the socket allocator; no intermediate copy)
+//     -> the image is either in the producer's shared-memory ring (the
+//        message carries a `_btshm` descriptor; the ring is hipHostRegister'ed
+//        and mapped once) or inline, read by the IO thread straight into
+//        hipHostMalloc'd slots (PinnedPool is the socket allocator)
 //     -> worker thread: zero-copy pickle scan locates the image payload,
 //        copies only the small non-image bytes (metadata) out
-//     -> B items assembled into batch j; hipMemcpyAsync of every image into
-//        the device staging ring on a private non-blocking HIP stream
-//     -> fused decode kernel (flip/gamma/unpack/normalize/CHW) writes into
-//        the consumer-posted output buffer; an event after the copies lets
-//        the worker recycle the pinned slots once the DMA has landed (no host
-//        callback in the stream); hipEvent marks the batch ready
+//     -> B items + the next consumer-posted output buffer form a batch;
+//        direct path (default, every frame device-visible and 16-byte
+//        aligned): the fused decode kernel reads the host frames over PCIe
+//        itself, and batches that wait while `launch_depth` launches are
+//        queued go out together in one launch; copy path: hipMemcpyAsync of
+//        every image into a device staging ring first, then the kernel
+//     -> the kernel (flip/gamma/unpack/normalize/CHW|NHWC) writes the
+//        consumer's tensor on a private non-blocking HIP stream; an event
+//        after the last host read lets the worker hand slots back (no host
+//        callback in the stream); a per-batch event marks it ready
 //     -> consumer (Python) takes batch j; its torch stream waits on the event.
 //
 // Backpressure is preserved end to end: when the consumer stops posting

@@ -6,9 +6,10 @@
 benchmarks/benchmark.py:24-41).  Instead of W forked worker processes that
 unpickle each frame, run numpy transforms, ``default_collate`` the batch and
 ship it through shared memory, one native pipeline per GPU rank
-(``csrc/gpu/loader.cpp``) lands frames in pinned host slots, DMAs them to the
-device on a side HIP stream and runs the fused gfx950 decode kernel into a
-tensor the consumer's stream waits on.  Nothing round-trips to the host.
+(``csrc/gpu/loader.cpp``) takes frames from the producers' pinned
+shared-memory ring (or receives them into pinned slots) and runs the fused
+gfx950 decode kernel, which reads them over PCIe itself, into a tensor the
+consumer's stream waits on.  Nothing round-trips through pageable memory.
 
 Semantics kept from the reference:
 
