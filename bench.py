@@ -100,6 +100,9 @@ def main():
     ap.add_argument('--shm', type=int, default=48,
                     help='>0 (default 48): producers render into an N-slot shared-memory ring (same host) and '
                          'send descriptors; 0: images inline in the ZMTP messages')
+    ap.add_argument('--codec', choices=['none', 'tile16'], default='none',
+                    help='shm frames: none = raw HWC; tile16 = key-frame deltas (the background crosses PCIe once, '
+                         'then only the 16x16 tiles that differ from it; csrc/codec/tiledelta.h)')
     ap.add_argument('--h2d', choices=['auto', 'copy'], default='auto',
                     help='auto: decode kernel reads pinned host frames directly (zero-copy); copy: DMA first')
     ap.add_argument('--launch-depth', type=int, default=2,
@@ -179,7 +182,7 @@ def main():
         decode = DecodeConfig.unit(channels='rgb', gamma=2.2, dtype='bfloat16', layout='nhwc')
     launch = dict(producer='cubesim', num_instances=nprod, named_sockets=['DATA'], start_port=start_port,
                   proto=args.proto, seed=1000 * rank, cpu_affinity=affinity,
-                  instance_args=[['--mode', args.mode, '--sndhwm', '10', '--resolution', f'{res_w}x{res_h}'] + (['--shm', str(shm_slots)] if shm_slots else [])]
+                  instance_args=[['--mode', args.mode, '--sndhwm', '10', '--resolution', f'{res_w}x{res_h}'] + (['--shm', str(shm_slots), '--codec', args.codec] if shm_slots else [])]
                   * nprod)
     model = opt = None
     if args.consumer == 'disc':
@@ -311,11 +314,12 @@ def main():
                 'shm_slots': shm_slots,
                 'h2d': args.h2d,
                 'launch_depth': args.launch_depth,
+                'codec': args.codec if shm_slots else 'none',
             },
             'sec_per_image': round(tmax / images, 7),
             'sec_per_batch': round(tmax / args.steps, 6),
             'loader_stats': {k: stats.get(k) for k in ('frames', 'batches', 'bad', 'pool_fallbacks', 'direct_batches',
-                                                       'launches', 'shm_frames', 'shm_torn')},
+                                                       'launches', 'shm_frames', 'shm_torn', 'tiled_frames')},
             # device time per image (H2D + decode, sampled launches) and the
             # producers' share of the frames (whole run incl. warm-up)
             'gpu_us_per_image': (round(metrics['gpu_us_per_image'], 3)

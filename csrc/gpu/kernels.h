@@ -68,6 +68,25 @@ struct DecodeParams {
 };
 hipError_t decode(const DecodeParams& p, hipStream_t stream);
 
+// Key-frame delta frames (csrc/codec/tiledelta.h), decoded in two launches
+// on `stream` with the same table, channel map, dtype and layout as decode():
+//   1. output image b <- fills[b]: its producer's key frame, already decoded
+//      (decode() of the key frame, B = 1, the image's flip) and kept in HBM;
+//   2. the payload tiles of image b (p.srcs[b]: the encoded frame, usually
+//      host memory mapped for the device) are decoded over it.  One wave
+//      slice per 16x16 tile: the tile's position and its pixels are
+//      independent loads, and a tile's bytes are one contiguous run.
+// tile_start[b] .. tile_start[b + 1] are image b's payload tiles (prefix sums
+// over the launch, tile_start[B] = total).  Needs p.nsrcs == B, H % 16 ==
+// W % 16 == 0, Cin 3 or 4, and out_img_bytes % 16 == 0.
+struct TileParams {
+  const void* fills[kMaxSrcs] = {};
+  int tile_start[kMaxSrcs + 1] = {};
+  int64_t out_img_bytes = 0;
+  int64_t payload_off = 0;   // tiledelta::payload_offset(H, W)
+};
+hipError_t decode_tiles(const DecodeParams& p, const TileParams& t, hipStream_t stream);
+
 // Per-pixel affine colour transform on the MFMA units:
 //   out[b, c, y, x] = sum_k M[c][k] * lut[k][in[b, y, x, k]] + bias[c]
 // for RGBA u8 HWC input (Cin = 4), f32 NCHW output with Cout <= 4 channels;

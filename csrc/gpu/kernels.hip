@@ -234,6 +234,56 @@ __global__ __launch_bounds__(kBlock) void decode_vec_kernel(DecodeParams p) {
   }
 }
 
+// Key-frame delta, launch 1: every image starts as its producer's decoded
+// key frame (16-byte copies, HBM to HBM).
+__global__ __launch_bounds__(kBlock) void tile_fill_kernel(DecodeParams p, TileParams t) {
+  const int64_t per = t.out_img_bytes / 16;
+  const int64_t total = per * p.B;
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < total; i += int64_t(gridDim.x) * kBlock) {
+    const int b = int(i / per);
+    const int64_t j = i - int64_t(b) * per;
+    uint8_t* d = p.ndsts ? static_cast<uint8_t*>(p.dsts[b]) : static_cast<uint8_t*>(p.dst) + int64_t(b) * t.out_img_bytes;
+    reinterpret_cast<uint4*>(d)[j] = reinterpret_cast<const uint4*>(t.fills[b])[j];
+  }
+}
+
+// Key-frame delta, launch 2: decode the payload tiles over the filled images.
+// LPT = 256 / PPT lanes per 16x16 tile (64 for f32, 32 bf16/f16, 16 u8); lane
+// `idx` of a tile takes PPT pixels of tile row idx / (16 / PPT).
+template <int PPT, int CIN, int OUTT, int LAYOUT>
+__global__ __launch_bounds__(kBlock) void tile_scatter_kernel(DecodeParams p, TileParams t) {
+  __shared__ float lut[4 * 256];
+  for (int i = threadIdx.x; i < p.Cout * 256; i += kBlock) lut[i] = p.lut[i];
+  __syncthreads();
+  constexpr int T = 16, LPT = T * T / PPT, LPR = T / PPT;
+  const int64_t HW = int64_t(p.H) * p.W;
+  const int ntx = p.W / T;
+  const int64_t total = int64_t(t.tile_start[p.B]) * LPT;
+  const int cout = p.Cout;
+  int cm[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) cm[c] = p.cmap[c];
+  for (int64_t g = int64_t(blockIdx.x) * kBlock + threadIdx.x; g < total; g += int64_t(gridDim.x) * kBlock) {
+    const int gt = int(g / LPT), idx = int(g - int64_t(gt) * LPT);
+    int b = 0;
+    while (b + 1 < p.B && gt >= t.tile_start[b + 1]) ++b;
+    const int k = gt - t.tile_start[b];
+    const uint8_t* enc = p.srcs[b];
+    // independent loads: the tile's position and its pixels
+    const uint32_t pos = reinterpret_cast<const uint32_t*>(enc)[1 + k];
+    Pixels<PPT, CIN> px;
+    load_pixels<PPT, CIN>(enc + t.payload_off + (int64_t(k) * T * T + int64_t(idx) * PPT) * CIN, px);
+    const int r = idx / LPR, col = (idx - r * LPR) * PPT;
+    const int sy = int(pos / ntx) * T + r, x = int(pos % ntx) * T + col;
+    const bool flip = p.flip_all || (p.flip && p.flip[b]) || (b < 256 && ((p.flip_bits[b >> 6] >> (b & 63)) & 1));
+    Group gr;
+    gr.b = b;
+    gr.q = int64_t(flip ? p.H - 1 - sy : sy) * p.W + x;
+    gr.src = nullptr;
+    emit<PPT, CIN, OUTT, LAYOUT>(p, lut, cm, cout, HW, gr, px);
+  }
+}
+
 // Generic fallback: one pixel per thread (any W, any alignment).
 template <int OUTT>
 __global__ __launch_bounds__(kBlock) void decode_scalar_kernel(DecodeParams p) {
@@ -330,6 +380,26 @@ hipError_t launch_out(const DecodeParams& p, hipStream_t s) {
 
 }  // namespace
 
+template <int PPT, int CIN, int OUTT>
+void launch_tiles(const DecodeParams& p, const TileParams& t, int grid, hipStream_t s) {
+  if (p.layout == NCHW)
+    tile_scatter_kernel<PPT, CIN, OUTT, NCHW><<<grid, kBlock, 0, s>>>(p, t);
+  else
+    tile_scatter_kernel<PPT, CIN, OUTT, NHWC><<<grid, kBlock, 0, s>>>(p, t);
+}
+
+template <int OUTT>
+void launch_tiles_out(const DecodeParams& p, const TileParams& t, hipStream_t s) {
+  constexpr int PPT = OUTT == OUT_F32 ? 4 : (OUTT == OUT_U8 ? 16 : 8);
+  const int64_t work = int64_t(t.tile_start[p.B]) * (256 / PPT);
+  if (work <= 0) return;
+  const int grid = grid_for(work, p.max_grid);
+  if (p.Cin == 4)
+    launch_tiles<PPT, 4, OUTT>(p, t, grid, s);
+  else
+    launch_tiles<PPT, 3, OUTT>(p, t, grid, s);
+}
+
 hipError_t decode(const DecodeParams& p, hipStream_t stream) {
   if (p.B <= 0 || p.H <= 0 || p.W <= 0) return hipSuccess;
   if (p.Cout < 1 || p.Cout > 4 || p.Cin < 1 || p.Cin > 4) return hipErrorInvalidValue;
@@ -344,6 +414,35 @@ hipError_t decode(const DecodeParams& p, hipStream_t stream) {
     case OUT_U8: return launch_out<OUT_U8>(p, stream);
   }
   return hipErrorInvalidValue;
+}
+
+hipError_t decode_tiles(const DecodeParams& p, const TileParams& t, hipStream_t stream) {
+  if (p.B <= 0) return hipSuccess;
+  const int ppt = p.out_dtype == OUT_F32 ? 4 : (p.out_dtype == OUT_U8 ? 16 : 8);
+  const size_t elem = p.out_dtype == OUT_F32 ? 4 : (p.out_dtype == OUT_U8 ? 1 : 2);
+  if (p.B > kMaxSrcs || p.nsrcs != p.B || p.H % 16 != 0 || p.W % 16 != 0 || (p.Cin != 3 && p.Cin != 4) ||
+      p.Cout < 1 || p.Cout > 4 || p.W % ppt != 0 || t.payload_off % 16 != 0 || t.out_img_bytes % 16 != 0 ||
+      t.out_img_bytes != int64_t(p.H) * p.W * p.Cout * int64_t(elem) || !srcs_ok(p.srcs, p.nsrcs, p.B, 16) ||
+      (p.ndsts ? !dsts_ok(p.dsts, p.ndsts, p.B, 16) : (reinterpret_cast<uintptr_t>(p.dst) % 16) != 0) ||
+      t.tile_start[0] != 0)
+    return hipErrorInvalidValue;
+  const int64_t ntiles = int64_t(p.H / 16) * (p.W / 16);
+  for (int b = 0; b < p.B; ++b)
+    if (!t.fills[b] || (reinterpret_cast<uintptr_t>(t.fills[b]) % 16) != 0 || t.tile_start[b + 1] < t.tile_start[b] ||
+        t.tile_start[b + 1] - t.tile_start[b] > ntiles)
+      return hipErrorInvalidValue;
+  for (int c = 0; c < p.Cout; ++c)
+    if (p.cmap[c] < 0 || p.cmap[c] >= p.Cin) return hipErrorInvalidValue;
+  const int64_t chunks = t.out_img_bytes / 16 * p.B;
+  tile_fill_kernel<<<grid_for(chunks, 0), kBlock, 0, stream>>>(p, t);
+  switch (p.out_dtype) {
+    case OUT_F32: launch_tiles_out<OUT_F32>(p, t, stream); break;
+    case OUT_BF16: launch_tiles_out<OUT_BF16>(p, t, stream); break;
+    case OUT_F16: launch_tiles_out<OUT_F16>(p, t, stream); break;
+    case OUT_U8: launch_tiles_out<OUT_U8>(p, t, stream); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

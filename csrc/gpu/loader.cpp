@@ -1,6 +1,7 @@
 // StreamLoader implementation (see loader.h).
 #include "loader.h"
 
+#include "../codec/tiledelta.h"
 #include "../common/trace.h"
 
 #include <algorithm>
@@ -209,6 +210,12 @@ void StreamLoader::stop() {
   pending_images_ = 0;
   for (auto& kv : segments_) (void)hipHostUnregister(kv.second.seg->base());
   segments_.clear();
+  for (auto& kv : keys_) {
+    if (kv.second.dev) (void)hipFree(kv.second.dev);
+    for (void* d : kv.second.decoded)
+      if (d) (void)hipFree(d);
+  }
+  keys_.clear();
   {
     std::lock_guard<std::mutex> lk(mu_);
     for (auto& p : posted_) (void)hipEventDestroy(p.ready);
@@ -323,7 +330,8 @@ bool StreamLoader::process(zmtp::Message&& msg) {
     it.gen = uint32_t(d.items[7]->i);
     const int64_t off = d.items[2]->i;
     h = int(d.items[3]->i), w = int(d.items[4]->i), c = int(d.items[5]->i);
-    if (it.slot >= it.seg->nslots() || off < 0 || size_t(off) + size_t(h) * w * c > it.seg->size())
+    const bool has_codec = d.items.size() >= 9 && d.items[8]->kind == codec::Value::TUPLE;
+    if (it.slot >= it.seg->nslots() || off < 0 || (!has_codec && size_t(off) + size_t(h) * w * c > it.seg->size()))
       return bad("_btshm descriptor out of range");
     if (!it.seg->valid(it.slot, it.gen)) {
       // the producer reclaimed the slot (lease expired while this descriptor
@@ -334,6 +342,30 @@ bool StreamLoader::process(zmtp::Message&& msg) {
     }
     it.src = it.seg->base() + off;
     if (dev_base) it.dsrc = dev_base + off;
+    if (d.items.size() >= 9 && d.items[8]->kind == codec::Value::TUPLE) {
+      // 9th element (codec, key segment, key generation): key-frame delta
+      const codec::Value& cd = *d.items[8];
+      if (cd.items.size() < 3 || cd.items[0]->kind != codec::Value::STR || cd.items[0]->s != tiledelta::kName ||
+          cd.items[1]->kind != codec::Value::STR)
+        return bad("unknown _btshm codec");
+      if (!tiledelta::supported(h, w, c)) return bad("tile16 frame size must be a multiple of 16");
+      // the tile count and every position must stay inside this slot and
+      // frame: the scatter kernel trusts them when it reads host memory
+      const size_t slot_end = it.seg->slot_offset(it.slot) + it.seg->slot_bytes();
+      if (size_t(off) < it.seg->slot_offset(it.slot) || size_t(off) + 4 > slot_end)
+        return bad("_btshm tile16 frame out of range");
+      const long ntiles = tiledelta::check(it.src, h, w, c, slot_end - size_t(off));
+      if (ntiles < 0) return bad("malformed tile16 frame");
+      it.ntiles = int(ntiles);
+      try {
+        KeyFrame& kf = key_frame(cd.items[1]->s, size_t(h) * w * c);
+        it.key = &kf;
+        it.key_host = kf.seg->slot(0);
+      } catch (const std::exception& e) {
+        return bad(e.what());
+      }
+      it.tiled = true;
+    }
     root->items.erase(root->items.begin() + long(shm_idx), root->items.begin() + long(shm_idx) + 2);
   } else {
     if (img_idx == size_t(-1)) return bad("no '" + cfg_.image_key + "' entry");
@@ -417,7 +449,12 @@ bool StreamLoader::process(zmtp::Message&& msg) {
     std::lock_guard<std::mutex> lk(mu_);
     stats_.frames++;
     stats_.bytes += n;
-    stats_.image_bytes += img_bytes_;
+    if (it.tiled) {
+      stats_.image_bytes += 4 * (size_t(it.ntiles) + 1) + size_t(it.ntiles) * tiledelta::tile_bytes(c);
+      stats_.tiled_frames++;
+    } else {
+      stats_.image_bytes += img_bytes_;
+    }
     if (it.seg) stats_.shm_frames++;
     if (const codec::Value* b = root->get("btid"))
       if (b->kind == codec::Value::INT) stats_.frames_per_btid[b->i]++;
@@ -425,6 +462,47 @@ bool StreamLoader::process(zmtp::Message&& msg) {
   cur_.push_back(std::move(it));
   if (int(cur_.size()) == cfg_.batch_size) launch();
   return true;
+}
+
+StreamLoader::KeyFrame& StreamLoader::key_frame(const std::string& name, size_t bytes) {
+  auto it = keys_.find(name);
+  if (it != keys_.end()) return it->second;
+  KeyFrame kf;
+  kf.seg.reset(shm::Segment::open(name));
+  if (kf.seg->nslots() < 1 || kf.seg->slot_bytes() < bytes || kf.seg->state(0) % 4 != shm::PUBLISHED)
+    throw std::runtime_error("tile16 key segment " + name + " is not a published key frame");
+  // once per producer: the key frame stays in HBM for the stream's lifetime
+  check(hipMalloc(reinterpret_cast<void**>(&kf.dev), bytes), "hipMalloc(key frame)");
+  check(hipMemcpy(kf.dev, kf.seg->slot(0), bytes, hipMemcpyHostToDevice), "upload key frame");
+  return keys_[name] = std::move(kf);
+}
+
+const void* StreamLoader::decoded_key(KeyFrame& kf, bool flip, size_t out_img_bytes) {
+  void*& d = kf.decoded[flip ? 1 : 0];
+  if (d) return d;
+  // the key frame through this loader's own decode (table, channels, dtype,
+  // layout, flip): every tiled image of this producer starts as a copy of it
+  check(hipMalloc(&d, out_img_bytes), "hipMalloc(decoded key)");
+  DecodeParams dp;
+  dp.src = kf.dev;
+  dp.dst = d;
+  dp.lut = d_lut_;
+  dp.B = 1, dp.H = H_, dp.W = W_, dp.Cin = C_, dp.Cout = cfg_.cout;
+  std::memcpy(dp.cmap, cfg_.cmap, sizeof(dp.cmap));
+  dp.flip_all = cfg_.flip_all || flip;
+  dp.out_dtype = cfg_.out_dtype;
+  dp.layout = cfg_.layout;
+  check(decode(dp, stream_), "decode(key frame)");
+  return d;
+}
+
+void StreamLoader::materialize(Item& it) {
+  if (!it.tiled) return;
+  it.expanded.resize(img_bytes_);
+  tiledelta::expand(it.src, it.key_host, H_, W_, C_, it.expanded.data());
+  it.src = it.expanded.data();
+  it.dsrc = nullptr;
+  it.tiled = false;
 }
 
 StreamLoader::MappedSegment& StreamLoader::segment(const std::string& name) {
@@ -496,7 +574,15 @@ void StreamLoader::launch() {
   pb.t0 = batch_t0_;
   pb.direct = cfg_.direct && int(cur_.size()) <= kMaxSrcs;
   for (auto& it : cur_)
-    pb.direct = pb.direct && it.dsrc && (reinterpret_cast<uintptr_t>(it.dsrc) % 16) == 0;
+    pb.direct = pb.direct && it.dsrc && (reinterpret_cast<uintptr_t>(it.dsrc) % 16) == 0 &&
+                !(it.tiled && cfg_.color_matrix);
+  // a batch of key-frame deltas only decodes as such (fill + tile scatter);
+  // in any other batch (copy path, MFMA colour kernel, mixed producers) they
+  // are rebuilt on the host
+  pb.tiled = pb.direct && std::all_of(cur_.begin(), cur_.end(), [](const Item& it) { return it.tiled; });
+  if (!pb.tiled)
+    for (auto& it : cur_) materialize(it);
+  pb.direct = pb.direct && std::all_of(cur_.begin(), cur_.end(), [](const Item& it) { return it.dsrc != nullptr; });
   pb.items = std::move(cur_);
   cur_.clear();
   pending_images_ += int(pb.items.size());
@@ -531,6 +617,7 @@ void StreamLoader::flush_pending(bool force) {
       group.push_back(std::move(b));
       emit();
     } else {
+      if (!group.empty() && group.front().tiled != b.tiled) emit();   // one kernel family per launch
       group.push_back(std::move(b));
     }
   }
@@ -629,7 +716,19 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
     std::memcpy(dp.flip_bits, flips, sizeof(flips));
     dp.out_dtype = cfg_.out_dtype;
     dp.layout = cfg_.layout;
-    e = decode(dp, stream_);
+    if (group.front().tiled) {
+      TileParams tp;
+      tp.out_img_bytes = int64_t(out_img_bytes);
+      tp.payload_off = int64_t(tiledelta::payload_offset(H_, W_));
+      for (int i = 0; i < total; ++i) {
+        const Item& it = *all[size_t(i)];
+        tp.fills[i] = decoded_key(*it.key, cfg_.flip_all || it.flip, out_img_bytes);
+        tp.tile_start[i + 1] = tp.tile_start[i] + it.ntiles;
+      }
+      e = decode_tiles(dp, tp, stream_);
+    } else {
+      e = decode(dp, stream_);
+    }
   }
   check(e, "decode kernel launch");
   if (direct) check(hipEventRecord(copied, stream_), "hipEventRecord(copied)");
@@ -645,6 +744,7 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
     for (auto& it : b.items) {
       fl.frames.push_back(std::move(it.frame));
       if (it.seg) fl.slots.push_back({it.seg, it.slot, it.gen});
+      if (!it.expanded.empty()) fl.expanded.push_back(std::move(it.expanded));
       rb.items.push_back(std::move(it.meta));
     }
     check(hipEventCreateWithFlags(&rb.done, hipEventDisableTiming), "hipEventCreate(done)");

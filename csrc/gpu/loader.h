@@ -140,6 +140,7 @@ struct LoaderStats {
   uint64_t direct_batches = 0;             // decoded straight from host memory (no staging copy)
   uint64_t launches = 0;                   // decode kernel launches (< batches when coalesced)
   uint64_t image_bytes = 0;                // image bytes that crossed host -> device
+  uint64_t tiled_frames = 0;               // key-frame delta frames (tiledelta.h)
   double h2d_issue_ms = 0;
   // GPU time of every kTimedEvery-th launch (timing events around its H2D
   // copies + decode kernel): per-image device cost without timing every launch
@@ -168,6 +169,7 @@ class StreamLoader {
   LoaderStats stats();
 
  private:
+  struct KeyFrame;
   struct Item {
     zmtp::Frame frame;
     const uint8_t* src = nullptr;      // image bytes: in the frame or in a shm slot
@@ -175,8 +177,16 @@ class StreamLoader {
     shm::Segment* seg = nullptr;       // shared-memory slot to hand back, if any
     uint32_t slot = 0, gen = 0;
     bool flip = false;
+    // key-frame delta (csrc/codec/tiledelta.h): `src`/`dsrc` point at the
+    // encoded frame (ntiles payload tiles); the key frame is at key_host (shm)
+    bool tiled = false;
+    int ntiles = 0;
+    KeyFrame* key = nullptr;
+    const uint8_t* key_host = nullptr;
+    std::vector<uint8_t> expanded;     // copy path: the frame rebuilt on the host
     BatchMeta meta;
   };
+  void materialize(Item& it);
   struct Posted {
     void* dst;
     hipEvent_t ready;
@@ -189,6 +199,7 @@ class StreamLoader {
     hipEvent_t ready = nullptr;
     double t0 = 0;
     bool direct = false;
+    bool tiled = false;               // every image a key-frame delta: fill + tile scatter
   };
   void launch();
   void flush_pending(bool force);
@@ -231,6 +242,7 @@ class StreamLoader {
       uint32_t slot, gen;
     };
     std::vector<Slot> slots;
+    std::vector<std::vector<uint8_t>> expanded;   // pageable copy sources, alive until `copied`
   };
   struct MappedSegment {
     std::unique_ptr<shm::Segment> seg;
@@ -238,6 +250,14 @@ class StreamLoader {
   };
   MappedSegment& segment(const std::string& name);
   std::map<std::string, MappedSegment> segments_;   // mapped + hipHostRegister'ed
+  struct KeyFrame {
+    std::unique_ptr<shm::Segment> seg;
+    uint8_t* dev = nullptr;          // HBM copy, made on first use
+    void* decoded[2] = {nullptr, nullptr};   // decoded for this loader (upper-left, flipped)
+  };
+  KeyFrame& key_frame(const std::string& name, size_t bytes);
+  const void* decoded_key(KeyFrame& kf, bool flip, size_t out_img_bytes);
+  std::map<std::string, KeyFrame> keys_;
   std::deque<Inflight> inflight_;   // H2D copies not yet known complete
   int64_t batch_index_ = 0;
   double batch_t0_ = 0;

@@ -486,6 +486,7 @@ PYBIND11_MODULE(_hip, m) {
         d["direct_batches"] = s.direct_batches;
         d["launches"] = s.launches;
         d["image_bytes"] = s.image_bytes;
+        d["tiled_frames"] = s.tiled_frames;
         d["timed_launches"] = s.timed_launches;
         d["timed_images"] = s.timed_images;
         d["timed_gpu_ms"] = s.timed_gpu_ms;

@@ -13,6 +13,7 @@
 // --fault none|exit|stall|garbage --fault-after N   --rotation RX RY RZ   --verbose
 // --resolution WxH   --stamp (integrity tests: btid/seq in the first 16 image bytes)
 // --shm N (render into an N-slot shared-memory ring, send descriptors only)
+// --codec tile16 (shm frames as key-frame deltas, csrc/codec/tiledelta.h)
 // --bench N (no sockets: render N frames into 8 rotating buffers, full vs
 // incremental (DirtyRect) rendering, and report the byte mismatches -- 0)
 //
@@ -39,6 +40,7 @@
 #include <vector>
 
 #include "../codec/pickle_codec.h"
+#include "../codec/tiledelta.h"
 #include "../transport/shmring.h"
 #include "../transport/zmtp.h"
 #include "physics.h"
@@ -68,6 +70,7 @@ struct Args {
   long long fault_after = -1;
   bool verbose = false;
   int shm_slots = 0;        // >0: images go through a shared-memory ring
+  std::string codec = "none";   // shm frames: none (raw HWC) | tile16 (key-frame delta, tiledelta.h)
   bool fixed_rotation = false;
   double rot[3] = {0, 0, 0};
   int width = 0, height = 0;   // 0: the scene's resolution (640x480)
@@ -84,6 +87,7 @@ Args parse(int argc, char** argv) {
   Args a;
   // BlenderLauncher(shm_slots=N) exports BLENDTORCH_SHM_SLOTS; --shm overrides
   if (const char* e = std::getenv("BLENDTORCH_SHM_SLOTS")) a.shm_slots = std::atoi(e);
+  if (const char* e = std::getenv("BLENDTORCH_SHM_CODEC")) a.codec = e;
   std::vector<std::string> v;
   int start = 1;
   for (int i = 1; i < argc; ++i)
@@ -124,6 +128,7 @@ Args parse(int argc, char** argv) {
     else if (k == "--verbose") a.verbose = true;
     else if (k == "--stamp") a.stamp = true;
     else if (k == "--shm") a.shm_slots = std::stoi(need(i)), ++i;
+    else if (k == "--codec") a.codec = need(i), ++i;
     else if (k == "--bench") a.bench = std::stoll(need(i)), ++i;
     else if (k == "--resolution") {
       // WxH: render size (render.resolution_x/_y); the camera's field of view is kept
@@ -144,6 +149,7 @@ Args parse(int argc, char** argv) {
     // unknown args are ignored, as Blender scripts ignore the remainder
   }
   if (a.mode != "rgb" && a.mode != "rgba") usage("--mode must be rgb or rgba");
+  if (a.codec != "none" && a.codec != btn::tiledelta::kName) usage("--codec must be none or tile16");
   if (a.origin != "upper-left" && a.origin != "lower-left") usage("bad --origin");
   return a;
 }
@@ -273,16 +279,29 @@ int main(int argc, char** argv) {
   sock->bind(a.sockets[a.socket]);
 
   const zmtp::Socket::Interrupt intr = [] { return g_stop.load(); };
-  std::unique_ptr<shm::Segment> seg;
+  std::unique_ptr<shm::Segment> seg, key_seg;
+  // key-frame delta codec: the background goes once into a segment of its
+  // own, every frame into its slot as a tile map + the tiles that differ
+  bool tiled = a.shm_slots > 0 && a.codec == tiledelta::kName && tiledelta::supported(H, W, C);
   if (a.shm_slots > 0) {
     const std::string name = "blendtorch-" + std::to_string(::getpid()) + "-" + std::to_string(a.btid);
     try {
-      seg.reset(shm::Segment::create(name, uint32_t(a.shm_slots), size_t(W) * H * C));
+      const size_t raw = size_t(W) * H * C;
+      seg.reset(shm::Segment::create(name, uint32_t(a.shm_slots), tiled ? std::max(raw, tiledelta::max_bytes(H, W, C)) : raw));
+      if (tiled) {
+        key_seg.reset(shm::Segment::create(name + "-key", 1, raw));
+        const int k = key_seg->acquire(0);
+        std::memcpy(key_seg->slot(uint32_t(k)), renderer.background().data(), raw);
+        key_seg->publish(uint32_t(k));   // stays published: consumers only read it
+      }
     } catch (const std::exception& e) {
       // e.g. a small /dev/shm: fall back to inline payloads
       std::fprintf(stderr, "cubesim[%d]: shared memory disabled (%s)\n", a.btid, e.what());
+      seg.reset(), key_seg.reset(), tiled = false;
     }
   }
+  std::vector<uint8_t> tiled_frame(tiled ? size_t(W) * H * C : 0);   // the full frame, rendered incrementally
+  sim::DirtyRect tiled_dirty;
   // what each ring slot's last frame drew over the background: a slot is
   // re-rendered by restoring that rectangle only (BLENDTORCH_FULL_RENDER=1: off)
   const char* full_env = std::getenv("BLENDTORCH_FULL_RENDER");
@@ -345,6 +364,13 @@ int main(int argc, char** argv) {
       w.integer(C);
       w.str("image");
       w.integer(gen);
+      if (tiled) {   // 9th element: (codec, key segment, key generation)
+        w.begin_tuple();
+        w.str(tiledelta::kName);
+        w.str(key_seg->name());
+        w.integer(int64_t(key_seg->state(0) >> 2));
+        w.end_tuple();
+      }
       w.end_tuple();
     }
     w.end_dict();
@@ -352,7 +378,9 @@ int main(int argc, char** argv) {
     uint8_t* pixels = seg ? seg->slot(uint32_t(slot)) : buf.data() + img_off;
 
     auto r0 = std::chrono::steady_clock::now();
-    sim::DirtyRect* dirty = seg && incremental ? &slot_dirty[size_t(slot)] : nullptr;
+    sim::DirtyRect* dirty = tiled ? &tiled_dirty : (seg && incremental ? &slot_dirty[size_t(slot)] : nullptr);
+    uint8_t* const slot_bytes = pixels;
+    if (tiled) pixels = tiled_frame.data();
     renderer.render(scene, pixels, dirty);
     if (a.stamp) {
       // bytes 0..15 of the stored image (first stored row): 'B','T', btid (u16 LE),
@@ -362,6 +390,17 @@ int main(int argc, char** argv) {
       std::memcpy(st + 8, &q, 8);
       std::memcpy(pixels, st, sizeof(st));
       if (dirty) dirty->add(lower_left ? H - 1 : 0, 0, (int(sizeof(st)) + C - 1) / C - 1);
+    }
+    if (tiled) {
+      // everything outside this frame's dirty rectangle is background
+      if (tiled_dirty.empty())
+        tiledelta::encode(pixels, key_seg->slot(0), H, W, C, 0, -1, 0, -1, slot_bytes);
+      else if (lower_left)   // DirtyRect rows are image rows (0 = top); stored rows are flipped
+        tiledelta::encode(pixels, key_seg->slot(0), H, W, C, H - 1 - tiled_dirty.y1, H - 1 - tiled_dirty.y0,
+                          tiled_dirty.x0, tiled_dirty.x1, slot_bytes);
+      else
+        tiledelta::encode(pixels, key_seg->slot(0), H, W, C, tiled_dirty.y0, tiled_dirty.y1, tiled_dirty.x0,
+                          tiled_dirty.x1, slot_bytes);
     }
     if (seg) seg->publish(uint32_t(slot));   // == gen
     render_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - r0).count();

@@ -110,6 +110,8 @@ class Renderer {
   int width() const { return W_; }
   int height() const { return H_; }
   int channels() const { return C_; }
+  // the stored bytes of a frame without boxes (what a DirtyRect restores)
+  const std::vector<uint8_t>& background() const { return background_; }
 
  private:
   void put(uint8_t* out, int x, int y, float r, float g, float b) const;

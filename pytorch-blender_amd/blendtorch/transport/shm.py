@@ -2,7 +2,9 @@
 
 Producers on the consumer's host may place image payloads in a POSIX
 shared-memory ring and send only a descriptor ``'_btshm': (segment, slot,
-byte_offset, H, W, C, key)`` in the message dict.  The GPU loader DMAs the
+byte_offset, H, W, C, key, generation[, codec])`` in the message dict; a 9th
+element ``('tile16', key_segment, key_generation)`` marks a key-frame delta
+frame (csrc/codec/tiledelta.h), which :func:`resolve` rebuilds.  The GPU loader DMAs the
 slot in place; CPU consumers call :func:`resolve`, which copies the image into
 the dict under ``key`` and hands the slot back.  :class:`ShmRing` is the
 producer side for Python publishers (``btb.DataPublisher(shm_slots=N)``).
@@ -87,9 +89,34 @@ def _word(gen, state):
     return ((int(gen) & 0x3fffffff) << 2) | state
 
 
+TILE = 16   # csrc/codec/tiledelta.h kTile
+
+
+def _expand_tiled(seg, off, h, w, c, codec):
+    """Rebuild a key-frame delta frame (csrc/codec/tiledelta.h): the key frame
+    from the producer's key segment, overwritten by the slot's payload tiles."""
+    kind, key_name = codec[0], codec[1]
+    if kind != 'tile16':
+        raise ValueError(f'unknown shm codec {kind!r}')
+    ty, tx = h // TILE, w // TILE
+    nt = ty * tx
+    n = int(np.frombuffer(seg.mm, dtype=np.uint32, count=1, offset=off)[0])
+    pos = np.frombuffer(seg.mm, dtype=np.uint32, count=n, offset=off + 4).astype(np.int64)
+    pay_off = off + (((nt + 1) * 4 + 255) & ~255)
+    if n > nt or (n and int(pos.max()) >= nt):
+        raise ValueError(f'malformed tile16 frame in {seg.name}')
+    kseg = _open(key_name)
+    img = np.frombuffer(kseg.mm, dtype=np.uint8, count=h * w * c, offset=kseg.data_offset).copy()
+    if n:
+        tiles = np.frombuffer(seg.mm, dtype=np.uint8, count=n * TILE * TILE * c, offset=pay_off)
+        view = img.reshape(ty, TILE, tx, TILE, c)
+        view[pos // tx, :, pos % tx] = tiles.reshape(n, TILE, TILE, c)
+    return img
+
+
 def release(desc):
     """Hand a descriptor's slot back without reading it (dropped messages)."""
-    name, slot, off, h, w, c, key, gen = desc
+    name, slot, off, h, w, c, key, gen = desc[:8]
     seg = _open(name)
     if int(seg.states[slot]) == _word(gen, PUBLISHED):
         seg.states[slot] = _word(gen, FREE)
@@ -100,13 +127,17 @@ def resolve(obj):
     if not isinstance(obj, dict) or KEY not in obj:
         return obj
     desc = obj.pop(KEY)
-    name, slot, off, h, w, c, key, gen = desc
+    name, slot, off, h, w, c, key, gen = desc[:8]
     seg = _open(name)
     published = _word(gen, PUBLISHED)
     if int(seg.states[slot]) != published:
         raise TornFrame(f'shm slot {name}:{slot} was reclaimed before it was read')
-    n = h * w * c
-    img = np.frombuffer(seg.mm, dtype=np.uint8, count=n, offset=off).reshape((h, w, c) if c > 1 else (h, w)).copy()
+    if len(desc) > 8 and desc[8]:
+        img = _expand_tiled(seg, off, h, w, c, desc[8])
+    else:
+        n = h * w * c
+        img = np.frombuffer(seg.mm, dtype=np.uint8, count=n, offset=off).copy()
+    img = img.reshape((h, w, c) if c > 1 else (h, w))
     if int(seg.states[slot]) != published:
         raise TornFrame(f'shm slot {name}:{slot} was reclaimed while it was read')
     seg.states[slot] = _word(gen, FREE)

@@ -123,3 +123,26 @@ def test_launcher_shm_slots_reaches_scene_scripts(free_port):
         ds = btt.RemoteIterableDataset(bl.launch_info.addresses['DATA'], max_items=12)
         items = list(ds)
     assert len(items) == 12 and items[0]['image'].shape == (480, 640, 3)
+
+
+@pytest.mark.background
+@pytest.mark.parametrize('extra', [['--mode', 'rgba'], ['--mode', 'rgb', '--origin', 'lower-left', '--stamp'],
+                                   ['--mode', 'rgba', '--scene', 'falling_cubes']])
+def test_dataset_tile_codec_matches_raw(free_port, extra):
+    """cubesim --codec tile16 (key-frame deltas in the shm ring) gives the CPU
+    dataset exactly the frames the raw shm path gives for the same seed."""
+    from blendtorch.transport import shm
+    frames = {}
+    for i, codec in enumerate(('none', 'tile16')):
+        args = dict(producer='cubesim', num_instances=1, named_sockets=['DATA'], start_port=free_port + 5 * i,
+                    proto='ipc', seed=11, instance_args=[extra + ['--shm', '6', '--codec', codec]])
+        with btt.BlenderLauncher(**args) as bl:
+            ds = btt.RemoteIterableDataset(bl.launch_info.addresses['DATA'], max_items=24)
+            frames[codec] = [(it['frameid'], it['image']) for it in ds]
+    assert len(frames['tile16']) == 24
+    for (fa, a), (fb, b) in zip(frames['none'], frames['tile16']):
+        assert fa == fb and a.shape == b.shape and np.array_equal(a, b)
+    # frames differ from each other (random poses), so tiles were really sent
+    assert not np.array_equal(frames['tile16'][0][1], frames['tile16'][1][1])
+    assert not [f for f in __import__('os').listdir('/dev/shm') if f.startswith('blendtorch-')]
+    del shm

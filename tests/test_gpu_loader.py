@@ -430,3 +430,35 @@ def test_device_loader_metrics(dev, free_port, caplog):
     assert m['gpu_us_per_image'] is not None and m['gpu_us_per_image'] > 0
     assert m['images_per_launch'] >= 8 and m['consumer_wait_s'] >= 0
     assert any('DeviceLoader:' in r.getMessage() for r in caplog.records)
+
+
+@pytest.mark.parametrize('extra,cfg', [
+    (['--mode', 'rgba'], dict(channels='rgb', gamma=2.2, scale=1 / 255)),
+    (['--mode', 'rgb', '--origin', 'lower-left'], dict(channels='rgb', dtype='bfloat16', layout='nhwc', scale=1 / 255)),
+    (['--mode', 'rgba', '--scene', 'falling_cubes'], dict(channels='rgba', dtype='uint8', layout='nhwc')),
+])
+def test_device_loader_tile_codec(dev, free_port, extra, cfg):
+    """Key-frame delta frames (cubesim --codec tile16): the decode kernel
+    resolves every 16x16 tile from the HBM key frame or the host payload and
+    matches the raw shm path bit for bit, on the direct path and on the copy
+    path (host-side rebuild); only the changed tiles cross PCIe."""
+    import os
+    decode = ops.DecodeConfig(**cfg)
+    out, stats = {}, {}
+    runs = (('raw', 'none', 'auto'), ('tile', 'tile16', 'auto'), ('tile-copy', 'tile16', 'copy'))
+    for i, (k, codec, h2d) in enumerate(runs):
+        with btt.BlenderLauncher(producer='cubesim', num_instances=1, named_sockets=['DATA'], seed=7,
+                                 start_port=free_port + 5 * i, proto='ipc',
+                                 instance_args=[extra + ['--shm', '12', '--codec', codec]]) as bl:
+            dl = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=8, max_items=48, decode=decode,
+                              device=dev, h2d=h2d)
+            out[k] = torch.cat([b['image'] for b in dl])
+            stats[k] = dl.stats
+            assert dl.stats['frames'] == 48 and dl.stats['bad'] == 0
+    for k in ('tile', 'tile-copy'):
+        torch.testing.assert_close(out[k], out['raw'], rtol=0, atol=0)
+    assert stats['tile']['tiled_frames'] == 48 and stats['tile']['direct_batches'] == 6
+    assert stats['tile-copy']['direct_batches'] == 0
+    assert stats['tile']['image_bytes'] < stats['raw']['image_bytes'] / 2
+    assert not torch.equal(out['raw'][0], out['raw'][1])   # random poses
+    assert not [f for f in os.listdir('/dev/shm') if f.startswith('blendtorch-')]
