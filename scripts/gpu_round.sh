@@ -18,6 +18,8 @@ for step in "$@"; do
     bench:*) a="${step#bench:}"; timeout -k 10 300 python bench.py ${a//,/ } >> gpurun_out/bench_sweep.log 2>&1; rc=$?; tail -1 gpurun_out/bench_sweep.log;;
     prof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/rp_prof -o run --output-format csv -- python bench.py --steps 300 --warmup 20 > gpurun_out/prof.log 2>&1; rc=$?; tail -2 gpurun_out/prof.log
           mkdir -p gpurun_out/prof && find /tmp/rp_prof -name '*stats.csv' -exec cp {} gpurun_out/prof/ \;;;
+    prof:*) a="${step#prof:}"; tag=$(echo "$a" | tr -c 'a-zA-Z0-9\n' '_'); timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/rp_prof_$tag -o run --output-format csv -- python bench.py --steps 300 --warmup 20 ${a//,/ } > gpurun_out/prof_$tag.log 2>&1; rc=$?; grep '^{' gpurun_out/prof_$tag.log | cut -c1-200
+          mkdir -p gpurun_out/prof_$tag && find /tmp/rp_prof_$tag -name '*stats.csv' -exec cp {} gpurun_out/prof_$tag/ \;;;
     kbench) timeout -k 10 200 python scripts/kernel_bench.py --json gpurun_out/kernel_bench.json > gpurun_out/kernel_bench.log 2>&1; rc=$?; cat gpurun_out/kernel_bench.log;;
     kprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/rp_kprof -o run --output-format csv -- python scripts/kernel_bench.py --iters 50 > gpurun_out/kprof.log 2>&1; rc=$?
           mkdir -p gpurun_out/kprof && find /tmp/rp_kprof -name '*stats.csv' -exec cp {} gpurun_out/kprof/ \;;;
