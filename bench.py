@@ -96,6 +96,9 @@ def main():
     ap.add_argument('--consumer-dtype', choices=['bf16', 'fp32'], default='bf16',
                     help='disc consumer: bf16 = decode kernel emits bf16 channels-last frames and the DCGAN step runs '
                          'under bf16 autocast (MFMA); fp32 = fp32 NCHW frames, fp32 step')
+    ap.add_argument('--graph', choices=['auto', 'on', 'off'], default='auto',
+                    help='disc consumer: capture the whole training step (forward, backward, Adam) in one HIP graph '
+                         'and replay it per batch (auto: on for a single rank; DDP steps stay eager)')
     ap.add_argument('--io-threads', type=int, default=0)
     ap.add_argument('--shm', type=int, default=48,
                     help='>0 (default 48): producers render into an N-slot shared-memory ring (same host) and '
@@ -103,8 +106,11 @@ def main():
     ap.add_argument('--codec', choices=['none', 'tile16'], default='none',
                     help='shm frames: none = raw HWC; tile16 = key-frame deltas (the background crosses PCIe once, '
                          'then only the 16x16 tiles that differ from it; csrc/codec/tiledelta.h)')
-    ap.add_argument('--h2d', choices=['auto', 'copy'], default='auto',
-                    help='auto: decode kernel reads pinned host frames directly (zero-copy); copy: DMA first')
+    ap.add_argument('--h2d', choices=['auto', 'copy'], default=None,
+                    help='auto: decode kernel reads pinned host frames directly (zero-copy); copy: DMA first. '
+                         'Default: auto, but copy for the disc consumer -- its graphed training step runs faster '
+                         'when the copy engines, not CUs waiting on PCIe reads, move the frames '
+                         '(profiles/consumer_step.md)')
     ap.add_argument('--launch-depth', type=int, default=2,
                     help='direct-path decode launches queued before new batches coalesce into one launch')
     ap.add_argument('--backend', choices=['nccl', 'gloo'], default='nccl',
@@ -115,6 +121,8 @@ def main():
                          'to all of them (PUSH round-robin across GPUs); scatter: rank 0 receives world*B per step '
                          'and scatters B-image shards over RCCL')
     args = ap.parse_args()
+    if args.h2d is None:
+        args.h2d = 'copy' if args.consumer == 'disc' else 'auto'
 
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
@@ -192,7 +200,9 @@ def main():
         model = Discriminator(nc=3, ndf=32, adaptive=True).to(device).to(memory_format=torch.channels_last)
         if world > 1:
             model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[gpu])
-        opt = torch.optim.Adam(model.parameters(), lr=2e-4)
+        use_graph = args.graph == 'on' or (args.graph == 'auto' and world == 1)
+        # capturable Adam keeps its step counters on the GPU, so the update can live inside the graph
+        opt = torch.optim.Adam(model.parameters(), lr=2e-4, capturable=use_graph)
         crit = torch.nn.BCELoss()
 
     WARM_RESERVE = 2000   # extra warm-up batches allowed while producers come up
@@ -219,22 +229,61 @@ def main():
         else:
             it = iter(dl)
 
+        def as_input(img):
+            # NHWC bf16 storage -> NCHW view with channels-last strides; fp32 NCHW -> channels-last copy
+            return img.permute(0, 3, 1, 2) if amp else img.contiguous(memory_format=torch.channels_last)
+
+        def train(x):
+            opt.zero_grad(set_to_none=True)
+            if amp:
+                # no autocast weight cache: a captured graph must recast the live weights on every replay
+                with torch.autocast('cuda', dtype=torch.bfloat16, cache_enabled=not use_graph):
+                    out = model(x)
+                out = out.float()
+            else:
+                out = model(x)
+            loss = crit(out, torch.ones_like(out))
+            loss.backward()
+            opt.step()
+            return loss
+
+        # whole-step HIP graph: the batch is copied into a static input buffer
+        # (one 15 MB device copy) and ~100 kernels replay as one launch, which
+        # takes the Python/autograd/MIOpen dispatch cost off the critical path
+        cap = {'graph': None, 'x': None, 'state': 'eager' if model is None or not use_graph else 'pending'}
+
+        def graphed(x):
+            if cap['state'] == 'pending':
+                cap['x'] = torch.empty_like(x)          # same (channels-last) strides as every batch
+                cap['x'].copy_(x)
+                side = torch.cuda.Stream()
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):           # eager warm-up: MIOpen find, allocator, Adam state
+                    for _ in range(3):
+                        train(cap['x'])
+                torch.cuda.current_stream().wait_stream(side)
+                g = torch.cuda.CUDAGraph()
+                try:
+                    opt.zero_grad(set_to_none=True)
+                    with torch.cuda.graph(g):
+                        train(cap['x'])
+                    cap['graph'], cap['state'] = g, 'graph'
+                except RuntimeError as e:              # keep the run alive; the JSON says which mode ran
+                    print(f'[bench] HIP graph capture failed, eager steps: {e}', file=sys.stderr, flush=True)
+                    cap['state'] = 'eager'
+                return
+            if cap['state'] == 'graph':
+                cap['x'].copy_(x)
+                cap['graph'].replay()
+            else:
+                train(x)
+
         def step():
             b = next(it)
             img = b['image']
             last['btid'] = b.get('btid')
             if model is not None:
-                opt.zero_grad(set_to_none=True)
-                if amp:
-                    x = img.permute(0, 3, 1, 2)          # NHWC storage -> NCHW view, channels-last strides
-                    with torch.autocast('cuda', dtype=torch.bfloat16):
-                        out = model(x)
-                    out = out.float()
-                else:
-                    out = model(img.contiguous(memory_format=torch.channels_last))
-                loss = crit(out, torch.ones_like(out))
-                loss.backward()
-                opt.step()
+                graphed(as_input(img))
             return img
 
         # warm-up: at least W batches, and (shard/pool) until every local producer
@@ -315,6 +364,7 @@ def main():
                 'h2d': args.h2d,
                 'launch_depth': args.launch_depth,
                 'codec': args.codec if shm_slots else 'none',
+                'consumer_step': cap['state'] if model is not None else None,
             },
             'sec_per_image': round(tmax / images, 7),
             'sec_per_batch': round(tmax / args.steps, 6),

@@ -120,5 +120,15 @@ hipError_t color4x4(const Color4x4Params& p, hipStream_t stream);
 hipError_t project(const float* pts, int64_t N, const float* PV, const float* V, int W, int H,
                    int upper_left, float* out_px, float* out_depth, hipStream_t stream);
 
+// Adaptive average pooling over channels-last (NHWC) activations, the
+// consumer model's pooling layer (nn.AdaptiveAvgPool2d semantics: output
+// cell (i, j) averages input rows [floor(i*H/OH), ceil((i+1)*H/OH)) and the
+// same for columns).  dtype: OUT_F32 or OUT_BF16 (fp32 accumulation, RNE).
+// forward: x [N,H,W,C] -> y [N,OH,OW,C]; backward: gy [N,OH,OW,C] -> gx [N,H,W,C].
+hipError_t adaptive_avgpool_nhwc(const void* x, void* y, int N, int H, int W, int C, int OH, int OW, int dtype,
+                                 hipStream_t stream);
+hipError_t adaptive_avgpool_nhwc_bwd(const void* gy, void* gx, int N, int H, int W, int C, int OH, int OW,
+                                     int dtype, hipStream_t stream);
+
 }  // namespace gpu
 }  // namespace btn

@@ -556,5 +556,117 @@ hipError_t project(const float* pts, int64_t N, const float* PV, const float* V,
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Adaptive average pooling, NHWC.  The pooled maps are small (the DCGAN
+// consumer pools 8 x 30 x 40 x 256 bf16 down to 4 x 4), so the kernels are
+// shaped for parallelism, not bandwidth: forward = one lane per output
+// element, lanes of a wave walk adjacent channels (every window load is one
+// coalesced 128/256-byte row segment); backward = one lane per input element
+// gathering the (at most a few) output cells whose window covers it -- no
+// atomics, every gradient written once.
+
+template <int DT>
+__device__ __forceinline__ float load_act(const void* p, int64_t i) {
+  if constexpr (DT == OUT_BF16)
+    return __uint_as_float(uint32_t(reinterpret_cast<const uint16_t*>(p)[i]) << 16);
+  else
+    return reinterpret_cast<const float*>(p)[i];
+}
+
+template <int DT>
+__device__ __forceinline__ void store_act(void* p, int64_t i, float v) {
+  if constexpr (DT == OUT_BF16)
+    reinterpret_cast<uint16_t*>(p)[i] = f2bf(v);
+  else
+    reinterpret_cast<float*>(p)[i] = v;
+}
+
+__device__ __forceinline__ int win_start(int i, int in, int out) { return int((int64_t(i) * in) / out); }
+__device__ __forceinline__ int win_end(int i, int in, int out) { return int((int64_t(i + 1) * in + out - 1) / out); }
+
+template <int DT>
+__global__ __launch_bounds__(kBlock) void avgpool_fwd_kernel(const void* __restrict__ x, void* __restrict__ y, int N,
+                                                             int H, int W, int C, int OH, int OW) {
+  const int64_t total = int64_t(N) * OH * OW * C;
+  for (int64_t o = int64_t(blockIdx.x) * kBlock + threadIdx.x; o < total; o += int64_t(gridDim.x) * kBlock) {
+    const int c = int(o % C);
+    int64_t r = o / C;
+    const int j = int(r % OW);
+    r /= OW;
+    const int i = int(r % OH);
+    const int n = int(r / OH);
+    const int h0 = win_start(i, H, OH), h1 = win_end(i, H, OH);
+    const int w0 = win_start(j, W, OW), w1 = win_end(j, W, OW);
+    float acc = 0.f;
+    for (int h = h0; h < h1; ++h) {
+      const int64_t row = ((int64_t(n) * H + h) * W) * C + c;
+#pragma unroll 4
+      for (int w = w0; w < w1; ++w) acc += load_act<DT>(x, row + int64_t(w) * C);
+    }
+    store_act<DT>(y, o, acc / float((h1 - h0) * (w1 - w0)));
+  }
+}
+
+template <int DT>
+__global__ __launch_bounds__(kBlock) void avgpool_bwd_kernel(const void* __restrict__ gy, void* __restrict__ gx, int N,
+                                                             int H, int W, int C, int OH, int OW) {
+  const int64_t total = int64_t(N) * H * W * C;
+  for (int64_t e = int64_t(blockIdx.x) * kBlock + threadIdx.x; e < total; e += int64_t(gridDim.x) * kBlock) {
+    const int c = int(e % C);
+    int64_t r = e / C;
+    const int w = int(r % W);
+    r /= W;
+    const int h = int(r % H);
+    const int n = int(r / H);
+    // output rows whose window covers h: floor(h*OH/H) .. ceil((h+1)*OH/H)-1
+    const int i0 = int((int64_t(h) * OH) / H), i1 = int((int64_t(h + 1) * OH + H - 1) / H);
+    const int j0 = int((int64_t(w) * OW) / W), j1 = int((int64_t(w + 1) * OW + W - 1) / W);
+    float acc = 0.f;
+    for (int i = i0; i < i1 && i < OH; ++i) {
+      const int hs = win_start(i, H, OH), he = win_end(i, H, OH);
+      if (h < hs || h >= he) continue;
+      for (int j = j0; j < j1 && j < OW; ++j) {
+        const int ws = win_start(j, W, OW), we = win_end(j, W, OW);
+        if (w < ws || w >= we) continue;
+        acc += load_act<DT>(gy, ((int64_t(n) * OH + i) * OW + j) * C + c) / float((he - hs) * (we - ws));
+      }
+    }
+    store_act<DT>(gx, e, acc);
+  }
+}
+
+namespace {
+int pool_grid(int64_t total) {
+  const int64_t blocks = (total + kBlock - 1) / kBlock;
+  return int(blocks < 8192 ? (blocks < 1 ? 1 : blocks) : 8192);
+}
+}  // namespace
+
+hipError_t adaptive_avgpool_nhwc(const void* x, void* y, int N, int H, int W, int C, int OH, int OW, int dtype,
+                                 hipStream_t stream) {
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || OH <= 0 || OW <= 0) return hipErrorInvalidValue;
+  const int grid = pool_grid(int64_t(N) * OH * OW * C);
+  if (dtype == OUT_BF16)
+    avgpool_fwd_kernel<OUT_BF16><<<grid, kBlock, 0, stream>>>(x, y, N, H, W, C, OH, OW);
+  else if (dtype == OUT_F32)
+    avgpool_fwd_kernel<OUT_F32><<<grid, kBlock, 0, stream>>>(x, y, N, H, W, C, OH, OW);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t adaptive_avgpool_nhwc_bwd(const void* gy, void* gx, int N, int H, int W, int C, int OH, int OW, int dtype,
+                                     hipStream_t stream) {
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || OH <= 0 || OW <= 0) return hipErrorInvalidValue;
+  const int grid = pool_grid(int64_t(N) * H * W * C);
+  if (dtype == OUT_BF16)
+    avgpool_bwd_kernel<OUT_BF16><<<grid, kBlock, 0, stream>>>(gy, gx, N, H, W, C, OH, OW);
+  else if (dtype == OUT_F32)
+    avgpool_bwd_kernel<OUT_F32><<<grid, kBlock, 0, stream>>>(gy, gx, N, H, W, C, OH, OW);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 }  // namespace gpu
 }  // namespace btn

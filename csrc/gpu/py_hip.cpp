@@ -186,6 +186,18 @@ PYBIND11_MODULE(_hip, m) {
                 "project");
         });
 
+  m.def("adaptive_avgpool_nhwc",
+        [](uintptr_t x, uintptr_t y, int N, int H, int W, int C, int OH, int OW, int dtype, uintptr_t stream) {
+          check(adaptive_avgpool_nhwc(ptr<const void>(x), ptr<void>(y), N, H, W, C, OH, OW, dtype, stream_of(stream)),
+                "adaptive_avgpool_nhwc");
+        });
+  m.def("adaptive_avgpool_nhwc_bwd",
+        [](uintptr_t gy, uintptr_t gx, int N, int H, int W, int C, int OH, int OW, int dtype, uintptr_t stream) {
+          check(adaptive_avgpool_nhwc_bwd(ptr<const void>(gy), ptr<void>(gx), N, H, W, C, OH, OW, dtype,
+                                          stream_of(stream)),
+                "adaptive_avgpool_nhwc_bwd");
+        });
+
   // Diagnostics: H2D bandwidth of one `nbytes` copy repeated `iters` times
   // from host memory of the given kind ("hostmalloc", "register", "pageable").
   m.def("bench_h2d", [](const std::string& kind, size_t nbytes, int iters, int chunks) {

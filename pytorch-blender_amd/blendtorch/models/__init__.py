@@ -38,7 +38,10 @@ class Discriminator(nn.Module):
                        nn.LeakyReLU(0.2, inplace=True)]
             cin = ndf * mult
         if adaptive:
-            layers += [nn.AdaptiveAvgPool2d(4)]
+            # gfx950 NHWC pooling kernels on the GPU (PyTorch's NHWC adaptive pool
+            # took ~100 us of a 1.2 ms training step, profiles/consumer_step.md)
+            from ..ops import AdaptiveAvgPool2d
+            layers += [AdaptiveAvgPool2d(4)]
         layers += [nn.Conv2d(cin, 1, 4, 1, 0, bias=False), nn.Sigmoid()]
         self.features = nn.Sequential(*layers)
         self.apply(_weights_init)

@@ -29,7 +29,7 @@ import numpy as np
 
 __all__ = [
     'DecodeConfig', 'hip_ext', 'hip_available', 'gamma_lut', 'build_lut', 'decode', 'decode_gather', 'color4x4',
-    'project',
+    'project', 'adaptive_avg_pool_nhwc', 'AdaptiveAvgPool2d',
     'reference_decode', 'reference_color4x4', 'reference_project', 'reference_gamma',
 ]
 
@@ -385,3 +385,102 @@ def project(points, PV, V, W, H, upper_left=True):
     ext.project(p.data_ptr(), N, PVt.data_ptr(), Vt.data_ptr(), W, H, int(upper_left), px.data_ptr(),
                 depth.data_ptr(), _stream(dev))
     return px, depth
+
+
+# ---------------------------------------------------------------------------
+# consumer-model op: adaptive average pooling on channels-last activations
+
+_POOL_DTYPES = {'torch.float32': 0, 'torch.bfloat16': 1}
+
+
+def _pool_launch(name, src, dst, N, H, W, C, OH, OW):
+    ext = hip_ext()
+    getattr(ext, name)(src.data_ptr(), dst.data_ptr(), N, H, W, C, OH, OW, _POOL_DTYPES[str(src.dtype)],
+                       _stream(src.device))
+
+
+def _as_nhwc(x):
+    """[N,C,H,W] tensor -> its [N,H,W,C] storage view (copies unless channels-last)."""
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def _pool_function():
+    import torch
+
+    class _AdaptiveAvgPoolNHWC(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, oh, ow):
+            N, C, H, W = x.shape
+            xs = _as_nhwc(x)
+            y = torch.empty((N, oh, ow, C), dtype=x.dtype, device=x.device)
+            _pool_launch('adaptive_avgpool_nhwc', xs, y, N, H, W, C, oh, ow)
+            ctx.shape = (N, C, H, W, oh, ow)
+            return y.permute(0, 3, 1, 2)
+
+        @staticmethod
+        def backward(ctx, gy):
+            N, C, H, W, oh, ow = ctx.shape
+            gys = _as_nhwc(gy)
+            gx = torch.empty((N, H, W, C), dtype=gy.dtype, device=gy.device)
+            _pool_launch('adaptive_avgpool_nhwc_bwd', gys, gx, N, H, W, C, oh, ow)
+            return gx.permute(0, 3, 1, 2), None, None
+
+    return _AdaptiveAvgPoolNHWC
+
+
+_POOL_FN = None
+
+
+def adaptive_avg_pool_nhwc(x, output_size):
+    """``F.adaptive_avg_pool2d`` for GPU activations on the gfx950 kernels
+    (fp32 or bf16; the result and the input gradient are channels-last)."""
+    global _POOL_FN
+    if _POOL_FN is None:
+        _POOL_FN = _pool_function()
+    oh, ow = (output_size, output_size) if isinstance(output_size, int) else output_size
+    if x.dim() != 4 or str(x.dtype) not in _POOL_DTYPES:
+        raise ValueError(f'adaptive_avg_pool_nhwc needs a 4-D float32/bfloat16 tensor, got {x.dtype} {tuple(x.shape)}')
+    return _POOL_FN.apply(x, oh, ow)
+
+
+def reference_adaptive_avg_pool(x, output_size):
+    """fp32 reference (PyTorch)."""
+    import torch.nn.functional as F
+    return F.adaptive_avg_pool2d(x.float(), output_size)
+
+
+_POOL_MODULE = None
+
+
+def _pool_module():
+    import torch.nn as nn
+    import torch.nn.functional as F
+
+    class AdaptiveAvgPool2d(nn.Module):
+        """Drop-in ``nn.AdaptiveAvgPool2d``: GPU fp32/bf16 inputs run the gfx950
+        kernels, anything else (CPU tensors, other dtypes) the PyTorch op."""
+
+        def __init__(self, output_size):
+            super().__init__()
+            self.output_size = output_size
+
+        def forward(self, x):
+            if x.is_cuda and str(x.dtype) in _POOL_DTYPES:
+                return adaptive_avg_pool_nhwc(x, self.output_size)
+            return F.adaptive_avg_pool2d(x, self.output_size)
+
+        def extra_repr(self):
+            return f'output_size={self.output_size}'
+
+    AdaptiveAvgPool2d.__module__ = __name__
+    return AdaptiveAvgPool2d
+
+
+def __getattr__(name):
+    # built on first use so importing ``blendtorch.ops`` does not import torch
+    global _POOL_MODULE
+    if name == 'AdaptiveAvgPool2d':
+        if _POOL_MODULE is None:
+            _POOL_MODULE = _pool_module()
+        return _POOL_MODULE
+    raise AttributeError(f'module {__name__!r} has no attribute {name!r}')

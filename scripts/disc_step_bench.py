@@ -1,0 +1,85 @@
+"""Consumer-step microbenchmark: DCGAN discriminator training step (forward,
+backward, Adam) on a batch of 8 x 3 x 480 x 640 frames, in the layouts and
+dtypes the bench consumer can use.  Input is a random HBM tensor, so the
+number is the model step alone (no streaming).
+
+    python scripts/disc_step_bench.py [--iters 200] [--only bf16-nhwc]
+"""
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1] / 'pytorch-blender_amd'))
+
+import torch  # noqa: E402
+
+from blendtorch.models import Discriminator  # noqa: E402
+
+VARIANTS = {
+    'bf16-nhwc': (torch.bfloat16, torch.channels_last),
+    'bf16-nchw': (torch.bfloat16, torch.contiguous_format),
+    'fp32-nhwc': (torch.float32, torch.channels_last),
+    'fp32-nchw': (torch.float32, torch.contiguous_format),
+}
+
+
+def run(name, iters, batch, graph):
+    dt, fmt = VARIANTS[name]
+    dev = torch.device('cuda', 0)
+    torch.manual_seed(0)
+    model = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=fmt)
+    opt = torch.optim.Adam(model.parameters(), lr=2e-4, capturable=graph)
+    crit = torch.nn.BCELoss()
+    x = torch.rand(batch, 3, 480, 640, device=dev).to(memory_format=fmt)
+    amp = dt == torch.bfloat16
+    if amp:
+        x = x.to(torch.bfloat16)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast('cuda', dtype=torch.bfloat16, enabled=amp, cache_enabled=not graph):
+            out = model(x)
+        loss = crit(out.float(), torch.ones(batch, device=dev))
+        loss.backward()
+        opt.step()
+
+    for _ in range(5):
+        step()
+    torch.cuda.synchronize()
+    fn = step
+    if graph:
+        g = torch.cuda.CUDAGraph()
+        opt.zero_grad(set_to_none=True)
+        with torch.cuda.graph(g):
+            step()
+        fn = g.replay
+        for _ in range(3):
+            fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / iters * 1000
+    return {'variant': name, 'graph': graph, 'ms_per_step': round(ms, 4), 'images_per_s': round(batch / ms * 1000, 1)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--iters', type=int, default=200)
+    ap.add_argument('--batch', type=int, default=8)
+    ap.add_argument('--only', default='')
+    ap.add_argument('--graph', choices=['both', 'on', 'off'], default='both')
+    args = ap.parse_args()
+    torch.backends.cudnn.benchmark = True
+    names = [args.only] if args.only else list(VARIANTS)
+    graphs = {'both': (False, True), 'on': (True,), 'off': (False,)}[args.graph]
+    for n in names:
+        for g in graphs:
+            print(json.dumps(run(n, args.iters, args.batch, g)), flush=True)
+
+
+if __name__ == '__main__':
+    main()

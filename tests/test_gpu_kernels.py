@@ -110,3 +110,38 @@ def test_project_matches_reference(dev):
     rpx, rd = ops.reference_project(pts, (P @ V).astype(np.float64), V.astype(np.float64), 640, 480)
     torch.testing.assert_close(px.cpu().double(), rpx, rtol=1e-4, atol=1e-2)
     torch.testing.assert_close(d.cpu().double(), rd, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize('shape,out', [((8, 256, 30, 40), 4), ((2, 5, 7, 5), (3, 2)), ((1, 3, 3, 2), (5, 4)),
+                                       ((2, 64, 16, 16), 4)])
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('channels_last', [True, False])
+def test_adaptive_avg_pool_nhwc(dev, shape, out, dtype, channels_last):
+    g = torch.Generator().manual_seed(3)
+    x32 = torch.randn(shape, generator=g)
+    fmt = torch.channels_last if channels_last else torch.contiguous_format
+    x = x32.to(dev, dtype).to(memory_format=fmt).requires_grad_(True)
+    y = ops.adaptive_avg_pool_nhwc(x, out)
+    gy32 = torch.randn(y.shape, generator=g)
+    y.backward(gy32.to(dev, dtype))
+    xr = x32.to(dtype).float().requires_grad_(True)          # same (rounded) inputs, fp32 math
+    yr = ops.reference_adaptive_avg_pool(xr, out)
+    yr.backward(gy32.to(dtype).float())
+    torch.cuda.synchronize()
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert y.shape == yr.shape and y.dtype == dtype
+    assert torch.allclose(y.detach().float().cpu(), yr.detach(), atol=tol, rtol=tol)
+    assert torch.allclose(x.grad.float().cpu(), xr.grad, atol=tol, rtol=tol)
+
+
+def test_discriminator_pool_runs_hip_kernel(dev):
+    from blendtorch.models import Discriminator
+    net = Discriminator(adaptive=True).to(dev).to(memory_format=torch.channels_last)
+    pool = [m for m in net.modules() if type(m).__name__ == 'AdaptiveAvgPool2d'][0]
+    assert type(pool) is ops.AdaptiveAvgPool2d
+    x = torch.rand(2, 3, 96, 128, device=dev).to(memory_format=torch.channels_last)
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        out = net(x)
+    out.float().sum().backward()
+    assert out.shape == (2,) and torch.isfinite(out.float()).all()
+    assert all(torch.isfinite(p.grad).all() for p in net.parameters())
