@@ -130,5 +130,27 @@ hipError_t adaptive_avgpool_nhwc(const void* x, void* y, int N, int H, int W, in
 hipError_t adaptive_avgpool_nhwc_bwd(const void* gy, void* gx, int N, int H, int W, int C, int OH, int OW,
                                      int dtype, hipStream_t stream);
 
+// Training-mode BatchNorm2d fused with LeakyReLU over channels-last
+// activations (x: [M = N*H*W, C], dtype OUT_F32 or OUT_BF16; C % 8 == 0 and
+// C / (16 / sizeof(dtype)) must divide 256).  fp32 statistics.
+//   forward:  bn_stats (per-block partial sums) -> bn_finalize (mean, invstd,
+//             running stats) -> bn_apply (y = leaky((x-mean)*invstd*w+b))
+//   backward: bn_bwd_reduce (partial sum(gz), sum(gz*xhat)) -> bn_bwd_finalize
+//             (dw, db) -> bn_bwd_apply (gx)
+// `partial` is scratch of bn_partial_floats(M, C) floats.
+int64_t bn_partial_floats(int64_t M, int C, int dtype);
+hipError_t bn_stats(const void* x, int64_t M, int C, int dtype, float* partial, hipStream_t stream);
+hipError_t bn_finalize(const float* partial, int64_t M, int C, int dtype, float eps, float momentum, float* mean,
+                       float* invstd, float* running_mean, float* running_var, hipStream_t stream);
+hipError_t bn_apply(const void* x, void* y, int64_t M, int C, int dtype, const float* mean, const float* invstd,
+                    const float* w, const float* b, float slope, hipStream_t stream);
+hipError_t bn_bwd_reduce(const void* x, const void* gy, int64_t M, int C, int dtype, const float* mean,
+                         const float* invstd, const float* w, const float* b, float slope, float* partial,
+                         hipStream_t stream);
+hipError_t bn_bwd_finalize(const float* partial, int64_t M, int C, int dtype, float* dw, float* db, hipStream_t stream);
+hipError_t bn_bwd_apply(const void* x, const void* gy, void* gx, int64_t M, int C, int dtype, const float* mean,
+                        const float* invstd, const float* w, const float* b, const float* dw, const float* db,
+                        float slope, hipStream_t stream);
+
 }  // namespace gpu
 }  // namespace btn

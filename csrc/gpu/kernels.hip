@@ -668,5 +668,301 @@ hipError_t adaptive_avgpool_nhwc_bwd(const void* gy, void* gx, int N, int H, int
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Training-mode BatchNorm2d + LeakyReLU, channels-last.  The consumer's
+// BN -> LeakyReLU pairs were 7 MIOpen/PyTorch kernels per layer and step
+// (mean/variance, final, normalise, leaky; and the same backwards), each a
+// full pass over the activation.  Here: forward = one statistics pass + one
+// normalise-and-activate pass; backward = one reduction pass + one gradient
+// pass, with the activation's derivative recomputed from x (z > 0 <=> y > 0
+// for a positive slope), so nothing but x is kept for backward.
+//
+// Reductions: a lane owns V = 16 B of channels of a row (8 bf16 / 4 fp32),
+// the G = C / V lanes of one row read it as one contiguous segment and
+// R = 256 / G rows are in flight per block; per-block partial sums go through
+// LDS to a [blocks, 2C] scratch that one lane per channel folds in fp64.
+
+constexpr int kBnMaxBlocks = 1024;
+
+template <int DT>
+struct BnVec {
+  static constexpr int V = DT == OUT_BF16 ? 8 : 4;
+  static constexpr int ES = DT == OUT_BF16 ? 2 : 4;
+};
+
+template <int DT>
+__device__ __forceinline__ void bn_load(const void* p, int64_t e, float (&v)[BnVec<DT>::V]) {
+  const uint4 raw = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(p) + e * BnVec<DT>::ES);
+  const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+  if constexpr (DT == OUT_BF16) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = __uint_as_float(w[i]);
+  }
+}
+
+template <int DT>
+__device__ __forceinline__ void bn_store(void* p, int64_t e, const float (&v)[BnVec<DT>::V]) {
+  uint4 raw;
+  if constexpr (DT == OUT_BF16) {
+    raw.x = uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16);
+    raw.y = uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16);
+    raw.z = uint32_t(f2bf(v[4])) | (uint32_t(f2bf(v[5])) << 16);
+    raw.w = uint32_t(f2bf(v[6])) | (uint32_t(f2bf(v[7])) << 16);
+  } else {
+    raw = make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3]));
+  }
+  *reinterpret_cast<uint4*>(reinterpret_cast<char*>(p) + e * BnVec<DT>::ES) = raw;
+}
+
+// BWD = false: sums of x and x^2.  BWD = true: sums of gz and gz * xhat.
+template <int DT, bool BWD>
+__global__ __launch_bounds__(kBlock) void bn_reduce_kernel(const void* __restrict__ x, const void* __restrict__ gy,
+                                                           int64_t M, int C, int64_t rows_per_block,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ w, const float* __restrict__ b,
+                                                           float slope, float* __restrict__ partial) {
+  constexpr int V = BnVec<DT>::V;
+  __shared__ float ls[kBlock * V], lq[kBlock * V];
+  const int G = C / V, R = kBlock / G;
+  const int g = int(threadIdx.x) % G, r0 = int(threadIdx.x) / G;
+  const int c0 = g * V;
+  float mu[V], is[V], ww[V], bb[V];
+  if constexpr (BWD) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) mu[i] = mean[c0 + i], is[i] = invstd[c0 + i], ww[i] = w[c0 + i], bb[i] = b[c0 + i];
+  }
+  float s[V], q[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) s[i] = 0.f, q[i] = 0.f;
+  const int64_t row_begin = int64_t(blockIdx.x) * rows_per_block;
+  const int64_t row_end = row_begin + rows_per_block < M ? row_begin + rows_per_block : M;
+  for (int64_t r = row_begin + r0; r < row_end; r += R) {
+    float v[V];
+    bn_load<DT>(x, r * C + c0, v);
+    if constexpr (BWD) {
+      float gv[V];
+      bn_load<DT>(gy, r * C + c0, gv);
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        const float xh = (v[i] - mu[i]) * is[i];
+        const float gz = (xh * ww[i] + bb[i]) > 0.f ? gv[i] : gv[i] * slope;
+        s[i] += gz;
+        q[i] += gz * xh;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < V; ++i) s[i] += v[i], q[i] += v[i] * v[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < V; ++i) ls[r0 * C + c0 + i] = s[i], lq[r0 * C + c0 + i] = q[i];
+  __syncthreads();
+  for (int c = int(threadIdx.x); c < C; c += kBlock) {
+    float a = 0.f, q2 = 0.f;
+    for (int r = 0; r < R; ++r) a += ls[r * C + c], q2 += lq[r * C + c];
+    partial[int64_t(blockIdx.x) * 2 * C + c] = a;
+    partial[int64_t(blockIdx.x) * 2 * C + C + c] = q2;
+  }
+}
+
+// One block per channel folds the per-block partials (fp64, LDS tree); a
+// single lane per channel walking 1024 partials serially cost ~1 ms per step.
+__device__ __forceinline__ void bn_fold(const float* __restrict__ partial, int nblocks, int C, int c, double& s,
+                                        double& q) {
+  __shared__ double ss[kBlock], qq[kBlock];
+  double a = 0.0, b2 = 0.0;
+  for (int b = int(threadIdx.x); b < nblocks; b += kBlock)
+    a += partial[int64_t(b) * 2 * C + c], b2 += partial[int64_t(b) * 2 * C + C + c];
+  ss[threadIdx.x] = a;
+  qq[threadIdx.x] = b2;
+  __syncthreads();
+  for (int k = kBlock / 2; k > 0; k >>= 1) {
+    if (int(threadIdx.x) < k) ss[threadIdx.x] += ss[threadIdx.x + k], qq[threadIdx.x] += qq[threadIdx.x + k];
+    __syncthreads();
+  }
+  s = ss[0];
+  q = qq[0];
+}
+
+__global__ __launch_bounds__(kBlock) void bn_finalize_kernel(const float* __restrict__ partial, int nblocks, int64_t M,
+                                                             int C, float eps, float momentum, float* mean,
+                                                             float* invstd, float* rm, float* rv) {
+  const int c = int(blockIdx.x);
+  double s, q;
+  bn_fold(partial, nblocks, C, c, s, q);
+  if (threadIdx.x != 0) return;
+  const double mu = s / double(M);
+  double var = q / double(M) - mu * mu;
+  var = var < 0.0 ? 0.0 : var;
+  mean[c] = float(mu);
+  invstd[c] = float(1.0 / sqrt(var + double(eps)));
+  if (rm) {
+    rm[c] = float((1.0 - momentum) * rm[c] + momentum * mu);
+    rv[c] = float((1.0 - momentum) * rv[c] + momentum * var * double(M) / double(M > 1 ? M - 1 : 1));
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void bn_bwd_finalize_kernel(const float* __restrict__ partial, int nblocks,
+                                                                 int C, float* dw, float* db) {
+  const int c = int(blockIdx.x);
+  double s, q;
+  bn_fold(partial, nblocks, C, c, s, q);
+  if (threadIdx.x != 0) return;
+  db[c] = float(s);
+  dw[c] = float(q);
+}
+
+// BWD = false: y = leaky(xhat * w + b).  BWD = true: gx = w * invstd * (gz - db/M - xhat * dw/M).
+template <int DT, bool BWD>
+__global__ __launch_bounds__(kBlock) void bn_apply_kernel(const void* __restrict__ x, const void* __restrict__ gy,
+                                                          void* __restrict__ out, int64_t M, int C,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd,
+                                                          const float* __restrict__ w, const float* __restrict__ b,
+                                                          const float* __restrict__ dw, const float* __restrict__ db,
+                                                          float slope) {
+  constexpr int V = BnVec<DT>::V;
+  const int G = C / V;
+  const int64_t total = M * G;
+  const float invM = 1.f / float(M);
+  for (int64_t idx = int64_t(blockIdx.x) * kBlock + threadIdx.x; idx < total; idx += int64_t(gridDim.x) * kBlock) {
+    const int c0 = int(idx % G) * V;
+    const int64_t e = idx * V;
+    float v[V], o[V];
+    bn_load<DT>(x, e, v);
+    if constexpr (BWD) {
+      float gv[V];
+      bn_load<DT>(gy, e, gv);
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        const int c = c0 + i;
+        const float xh = (v[i] - mean[c]) * invstd[c];
+        const float gz = (xh * w[c] + b[c]) > 0.f ? gv[i] : gv[i] * slope;
+        o[i] = w[c] * invstd[c] * (gz - db[c] * invM - xh * dw[c] * invM);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        const int c = c0 + i;
+        const float z = (v[i] - mean[c]) * invstd[c] * w[c] + b[c];
+        o[i] = z > 0.f ? z : z * slope;
+      }
+    }
+    bn_store<DT>(out, e, o);
+  }
+}
+
+namespace {
+bool bn_shape_ok(int64_t M, int C, int dtype) {
+  if (M <= 0 || C <= 0 || (dtype != OUT_F32 && dtype != OUT_BF16)) return false;
+  const int V = dtype == OUT_BF16 ? 8 : 4;
+  return C % V == 0 && kBlock % (C / V) == 0;
+}
+
+void bn_blocks(int64_t M, int C, int dtype, int& nblocks, int64_t& rows_per_block) {
+  const int V = dtype == OUT_BF16 ? 8 : 4;
+  const int R = kBlock / (C / V);
+  const int64_t want = (M + R - 1) / R;
+  nblocks = int(want < kBnMaxBlocks ? want : kBnMaxBlocks);
+  rows_per_block = (M + nblocks - 1) / nblocks;
+}
+
+int bn_grid(int64_t work) {
+  const int64_t blocks = (work + kBlock - 1) / kBlock;
+  return int(blocks < 8192 ? (blocks < 1 ? 1 : blocks) : 8192);
+}
+}  // namespace
+
+int64_t bn_partial_floats(int64_t M, int C, int dtype) {
+  if (!bn_shape_ok(M, C, dtype)) return -1;
+  int nb;
+  int64_t rpb;
+  bn_blocks(M, C, dtype, nb, rpb);
+  return int64_t(nb) * 2 * C;
+}
+
+hipError_t bn_stats(const void* x, int64_t M, int C, int dtype, float* partial, hipStream_t stream) {
+  if (!bn_shape_ok(M, C, dtype)) return hipErrorInvalidValue;
+  int nb;
+  int64_t rpb;
+  bn_blocks(M, C, dtype, nb, rpb);
+  if (dtype == OUT_BF16)
+    bn_reduce_kernel<OUT_BF16, false><<<nb, kBlock, 0, stream>>>(x, nullptr, M, C, rpb, nullptr, nullptr, nullptr,
+                                                                 nullptr, 0.f, partial);
+  else
+    bn_reduce_kernel<OUT_F32, false><<<nb, kBlock, 0, stream>>>(x, nullptr, M, C, rpb, nullptr, nullptr, nullptr,
+                                                                nullptr, 0.f, partial);
+  return hipGetLastError();
+}
+
+hipError_t bn_finalize(const float* partial, int64_t M, int C, int dtype, float eps, float momentum, float* mean,
+                       float* invstd, float* running_mean, float* running_var, hipStream_t stream) {
+  if (!bn_shape_ok(M, C, dtype)) return hipErrorInvalidValue;
+  int nb;
+  int64_t rpb;
+  bn_blocks(M, C, dtype, nb, rpb);
+  bn_finalize_kernel<<<C, kBlock, 0, stream>>>(partial, nb, M, C, eps, momentum, mean, invstd,
+                                                                       running_mean, running_var);
+  return hipGetLastError();
+}
+
+hipError_t bn_apply(const void* x, void* y, int64_t M, int C, int dtype, const float* mean, const float* invstd,
+                    const float* w, const float* b, float slope, hipStream_t stream) {
+  if (!bn_shape_ok(M, C, dtype)) return hipErrorInvalidValue;
+  const int V = dtype == OUT_BF16 ? 8 : 4;
+  const int grid = bn_grid(M * (C / V));
+  if (dtype == OUT_BF16)
+    bn_apply_kernel<OUT_BF16, false><<<grid, kBlock, 0, stream>>>(x, nullptr, y, M, C, mean, invstd, w, b, nullptr,
+                                                                  nullptr, slope);
+  else
+    bn_apply_kernel<OUT_F32, false><<<grid, kBlock, 0, stream>>>(x, nullptr, y, M, C, mean, invstd, w, b, nullptr,
+                                                                 nullptr, slope);
+  return hipGetLastError();
+}
+
+hipError_t bn_bwd_reduce(const void* x, const void* gy, int64_t M, int C, int dtype, const float* mean,
+                         const float* invstd, const float* w, const float* b, float slope, float* partial,
+                         hipStream_t stream) {
+  if (!bn_shape_ok(M, C, dtype)) return hipErrorInvalidValue;
+  int nb;
+  int64_t rpb;
+  bn_blocks(M, C, dtype, nb, rpb);
+  if (dtype == OUT_BF16)
+    bn_reduce_kernel<OUT_BF16, true><<<nb, kBlock, 0, stream>>>(x, gy, M, C, rpb, mean, invstd, w, b, slope, partial);
+  else
+    bn_reduce_kernel<OUT_F32, true><<<nb, kBlock, 0, stream>>>(x, gy, M, C, rpb, mean, invstd, w, b, slope, partial);
+  return hipGetLastError();
+}
+
+hipError_t bn_bwd_finalize(const float* partial, int64_t M, int C, int dtype, float* dw, float* db,
+                           hipStream_t stream) {
+  if (!bn_shape_ok(M, C, dtype)) return hipErrorInvalidValue;
+  int nb;
+  int64_t rpb;
+  bn_blocks(M, C, dtype, nb, rpb);
+  bn_bwd_finalize_kernel<<<C, kBlock, 0, stream>>>(partial, nb, C, dw, db);
+  return hipGetLastError();
+}
+
+hipError_t bn_bwd_apply(const void* x, const void* gy, void* gx, int64_t M, int C, int dtype, const float* mean,
+                        const float* invstd, const float* w, const float* b, const float* dw, const float* db,
+                        float slope, hipStream_t stream) {
+  if (!bn_shape_ok(M, C, dtype)) return hipErrorInvalidValue;
+  const int V = dtype == OUT_BF16 ? 8 : 4;
+  const int grid = bn_grid(M * (C / V));
+  if (dtype == OUT_BF16)
+    bn_apply_kernel<OUT_BF16, true><<<grid, kBlock, 0, stream>>>(x, gy, gx, M, C, mean, invstd, w, b, dw, db, slope);
+  else
+    bn_apply_kernel<OUT_F32, true><<<grid, kBlock, 0, stream>>>(x, gy, gx, M, C, mean, invstd, w, b, dw, db, slope);
+  return hipGetLastError();
+}
+
 }  // namespace gpu
 }  // namespace btn

@@ -198,6 +198,37 @@ PYBIND11_MODULE(_hip, m) {
                 "adaptive_avgpool_nhwc_bwd");
         });
 
+  // fused training BatchNorm2d + LeakyReLU (channels-last); pointers are device addresses
+  m.def("bn_partial_floats", [](int64_t M, int C, int dtype) { return bn_partial_floats(M, C, dtype); });
+  m.def("bn_forward",
+        [](uintptr_t x, uintptr_t y, int64_t M, int C, int dtype, uintptr_t partial, float eps, float momentum,
+           uintptr_t mean, uintptr_t invstd, uintptr_t rm, uintptr_t rv, uintptr_t w, uintptr_t b, float slope,
+           uintptr_t stream) {
+          hipStream_t s = stream_of(stream);
+          check(bn_stats(ptr<const void>(x), M, C, dtype, ptr<float>(partial), s), "bn_stats");
+          check(bn_finalize(ptr<const float>(partial), M, C, dtype, eps, momentum, ptr<float>(mean), ptr<float>(invstd),
+                            ptr<float>(rm), ptr<float>(rv), s),
+                "bn_finalize");
+          check(bn_apply(ptr<const void>(x), ptr<void>(y), M, C, dtype, ptr<const float>(mean),
+                         ptr<const float>(invstd), ptr<const float>(w), ptr<const float>(b), slope, s),
+                "bn_apply");
+        });
+  m.def("bn_backward",
+        [](uintptr_t x, uintptr_t gy, uintptr_t gx, int64_t M, int C, int dtype, uintptr_t partial, uintptr_t mean,
+           uintptr_t invstd, uintptr_t w, uintptr_t b, uintptr_t dw, uintptr_t db, float slope, uintptr_t stream) {
+          hipStream_t s = stream_of(stream);
+          check(bn_bwd_reduce(ptr<const void>(x), ptr<const void>(gy), M, C, dtype, ptr<const float>(mean),
+                              ptr<const float>(invstd), ptr<const float>(w), ptr<const float>(b), slope,
+                              ptr<float>(partial), s),
+                "bn_bwd_reduce");
+          check(bn_bwd_finalize(ptr<const float>(partial), M, C, dtype, ptr<float>(dw), ptr<float>(db), s),
+                "bn_bwd_finalize");
+          check(bn_bwd_apply(ptr<const void>(x), ptr<const void>(gy), ptr<void>(gx), M, C, dtype,
+                             ptr<const float>(mean), ptr<const float>(invstd), ptr<const float>(w),
+                             ptr<const float>(b), ptr<const float>(dw), ptr<const float>(db), slope, s),
+                "bn_bwd_apply");
+        });
+
   // Diagnostics: H2D bandwidth of one `nbytes` copy repeated `iters` times
   // from host memory of the given kind ("hostmalloc", "register", "pageable").
   m.def("bench_h2d", [](const std::string& kind, size_t nbytes, int iters, int chunks) {

@@ -29,19 +29,25 @@ def _weights_init(m):
 class Discriminator(nn.Module):
     """DCGAN discriminator: N x nc x H x W -> N probabilities."""
 
-    def __init__(self, nc=3, ndf=32, adaptive=False):
+    def __init__(self, nc=3, ndf=32, adaptive=False, fused=True):
         super().__init__()
+        from .. import ops
         layers = []
         cin = nc
         for i, mult in enumerate((1, 2, 4, 8)):
-            layers += [nn.Conv2d(cin, ndf * mult, 4, 2, 1, bias=False), nn.BatchNorm2d(ndf * mult),
-                       nn.LeakyReLU(0.2, inplace=True)]
+            if fused:
+                # BN + LeakyReLU as one gfx950 op on GPU training steps (7 MIOpen/PyTorch
+                # kernels -> 3 forward + 3 backward); the Identity keeps the module
+                # indices, so state dicts match the unfused stack
+                norm_act = [ops.BatchNormLeakyReLU2d(ndf * mult, slope=0.2), nn.Identity()]
+            else:
+                norm_act = [nn.BatchNorm2d(ndf * mult), nn.LeakyReLU(0.2, inplace=True)]
+            layers += [nn.Conv2d(cin, ndf * mult, 4, 2, 1, bias=False)] + norm_act
             cin = ndf * mult
         if adaptive:
             # gfx950 NHWC pooling kernels on the GPU (PyTorch's NHWC adaptive pool
             # took ~100 us of a 1.2 ms training step, profiles/consumer_step.md)
-            from ..ops import AdaptiveAvgPool2d
-            layers += [AdaptiveAvgPool2d(4)]
+            layers += [ops.AdaptiveAvgPool2d(4)]
         layers += [nn.Conv2d(cin, 1, 4, 1, 0, bias=False), nn.Sigmoid()]
         self.features = nn.Sequential(*layers)
         self.apply(_weights_init)

@@ -29,7 +29,7 @@ import numpy as np
 
 __all__ = [
     'DecodeConfig', 'hip_ext', 'hip_available', 'gamma_lut', 'build_lut', 'decode', 'decode_gather', 'color4x4',
-    'project', 'adaptive_avg_pool_nhwc', 'AdaptiveAvgPool2d',
+    'project', 'adaptive_avg_pool_nhwc', 'AdaptiveAvgPool2d', 'batch_norm_leaky_relu', 'BatchNormLeakyReLU2d',
     'reference_decode', 'reference_color4x4', 'reference_project', 'reference_gamma',
 ]
 
@@ -400,8 +400,10 @@ def _pool_launch(name, src, dst, N, H, W, C, OH, OW):
 
 
 def _as_nhwc(x):
-    """[N,C,H,W] tensor -> its [N,H,W,C] storage view (copies unless channels-last)."""
-    return x.permute(0, 2, 3, 1).contiguous()
+    """[N,C,H,W] tensor -> its [N,H,W,C] storage view (copies unless channels-last;
+    the kernels' 16-byte vector accesses also need a 16-byte aligned base)."""
+    xs = x.permute(0, 2, 3, 1).contiguous()
+    return xs if xs.data_ptr() % 16 == 0 else xs.clone()
 
 
 def _pool_function():
@@ -476,11 +478,129 @@ def _pool_module():
     return AdaptiveAvgPool2d
 
 
+# ---------------------------------------------------------------------------
+# consumer-model op: training BatchNorm2d fused with LeakyReLU (channels-last)
+
+def _bn_function():
+    import torch
+
+    class _BatchNormLeakyReLU(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, slope):
+            ext = hip_ext()
+            N, C, H, W = x.shape
+            M = N * H * W
+            dt = _POOL_DTYPES[str(x.dtype)]
+            xs = _as_nhwc(x)
+            w = weight.detach().float().contiguous()
+            b = bias.detach().float().contiguous()
+            part = torch.empty(ext.bn_partial_floats(M, C, dt), dtype=torch.float32, device=x.device)
+            mean = torch.empty(C, dtype=torch.float32, device=x.device)
+            invstd = torch.empty_like(mean)
+            y = torch.empty_like(xs)
+            rm = running_mean.data_ptr() if running_mean is not None else 0
+            rv = running_var.data_ptr() if running_var is not None else 0
+            ext.bn_forward(xs.data_ptr(), y.data_ptr(), M, C, dt, part.data_ptr(), float(eps), float(momentum),
+                           mean.data_ptr(), invstd.data_ptr(), rm, rv, w.data_ptr(), b.data_ptr(), float(slope),
+                           _stream(x.device))
+            ctx.save_for_backward(xs, w, b, mean, invstd)
+            ctx.slope = float(slope)
+            return y.permute(0, 3, 1, 2)
+
+        @staticmethod
+        def backward(ctx, gy):
+            ext = hip_ext()
+            xs, w, b, mean, invstd = ctx.saved_tensors
+            N, H, W, C = xs.shape
+            M = N * H * W
+            dt = _POOL_DTYPES[str(xs.dtype)]
+            gys = _as_nhwc(gy.to(xs.dtype))
+            gx = torch.empty_like(xs)
+            dw = torch.empty(C, dtype=torch.float32, device=xs.device)
+            db = torch.empty_like(dw)
+            part = torch.empty(ext.bn_partial_floats(M, C, dt), dtype=torch.float32, device=xs.device)
+            ext.bn_backward(xs.data_ptr(), gys.data_ptr(), gx.data_ptr(), M, C, dt, part.data_ptr(), mean.data_ptr(),
+                            invstd.data_ptr(), w.data_ptr(), b.data_ptr(), dw.data_ptr(), db.data_ptr(), ctx.slope,
+                            _stream(xs.device))
+            return gx.permute(0, 3, 1, 2), dw, db, None, None, None, None, None
+
+    return _BatchNormLeakyReLU
+
+
+_BN_FN = None
+
+
+def bn_supported(x):
+    """True when the fused kernels take ``x`` (GPU fp32/bf16, 16-byte channel
+    groups that tile a 256-lane block)."""
+    if not (x.is_cuda and x.dim() == 4 and str(x.dtype) in _POOL_DTYPES):
+        return False
+    N, C, H, W = x.shape
+    return hip_ext().bn_partial_floats(N * H * W, C, _POOL_DTYPES[str(x.dtype)]) > 0
+
+
+def batch_norm_leaky_relu(x, weight, bias, running_mean=None, running_var=None, eps=1e-5, momentum=0.1,
+                          slope=0.2):
+    """``leaky_relu(batch_norm(x, training=True), slope)`` on the gfx950
+    kernels; updates ``running_mean``/``running_var`` in place like PyTorch
+    (unbiased variance, ``momentum``)."""
+    global _BN_FN
+    if _BN_FN is None:
+        _BN_FN = _bn_function()
+    if not bn_supported(x):
+        raise ValueError(f'batch_norm_leaky_relu: unsupported input {x.dtype} {tuple(x.shape)} on {x.device}')
+    return _BN_FN.apply(x, weight, bias, running_mean, running_var, eps, momentum, slope)
+
+
+def reference_batch_norm_leaky_relu(x, weight, bias, running_mean=None, running_var=None, eps=1e-5, momentum=0.1,
+                                    slope=0.2):
+    """fp32 reference (PyTorch)."""
+    import torch.nn.functional as F
+    y = F.batch_norm(x.float(), running_mean, running_var, weight, bias, training=True, momentum=momentum, eps=eps)
+    return F.leaky_relu(y, slope)
+
+
+_BN_MODULE = None
+
+
+def _bn_module():
+    import torch.nn as nn
+    import torch.nn.functional as F
+
+    class BatchNormLeakyReLU2d(nn.BatchNorm2d):
+        """``nn.BatchNorm2d`` followed by ``LeakyReLU(slope)``; same parameters
+        and buffers as ``nn.BatchNorm2d`` (state dicts interchange).  Training
+        steps on GPU fp32/bf16 inputs run the fused gfx950 kernels; eval mode
+        and other inputs run the PyTorch ops."""
+
+        def __init__(self, num_features, slope=0.2, **kw):
+            super().__init__(num_features, **kw)
+            self.slope = slope
+
+        def forward(self, x):
+            if (self.training and self.affine and self.track_running_stats and self.momentum is not None
+                    and bn_supported(x)):
+                self.num_batches_tracked.add_(1)
+                return batch_norm_leaky_relu(x, self.weight, self.bias, self.running_mean, self.running_var,
+                                             self.eps, self.momentum, self.slope)
+            return F.leaky_relu(super().forward(x), self.slope)
+
+        def extra_repr(self):
+            return super().extra_repr() + f', slope={self.slope}'
+
+    BatchNormLeakyReLU2d.__module__ = __name__
+    return BatchNormLeakyReLU2d
+
+
 def __getattr__(name):
     # built on first use so importing ``blendtorch.ops`` does not import torch
-    global _POOL_MODULE
+    global _POOL_MODULE, _BN_MODULE
     if name == 'AdaptiveAvgPool2d':
         if _POOL_MODULE is None:
             _POOL_MODULE = _pool_module()
         return _POOL_MODULE
+    if name == 'BatchNormLeakyReLU2d':
+        if _BN_MODULE is None:
+            _BN_MODULE = _bn_module()
+        return _BN_MODULE
     raise AttributeError(f'module {__name__!r} has no attribute {name!r}')

@@ -145,3 +145,56 @@ def test_discriminator_pool_runs_hip_kernel(dev):
     out.float().sum().backward()
     assert out.shape == (2,) and torch.isfinite(out.float()).all()
     assert all(torch.isfinite(p.grad).all() for p in net.parameters())
+
+
+@pytest.mark.parametrize('shape', [(8, 32, 60, 80), (4, 256, 15, 20), (3, 64, 7, 9), (2, 128, 1, 1)])
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('channels_last', [True, False])
+def test_batch_norm_leaky_relu(dev, shape, dtype, channels_last):
+    g = torch.Generator().manual_seed(5)
+    C = shape[1]
+    x32 = torch.randn(shape, generator=g) * 1.5 + 0.3
+    w32 = torch.rand(C, generator=g) + 0.5
+    b32 = torch.randn(C, generator=g) * 0.1
+    fmt = torch.channels_last if channels_last else torch.contiguous_format
+    x = x32.to(dev, dtype).to(memory_format=fmt).requires_grad_(True)
+    w = w32.to(dev).requires_grad_(True)
+    b = b32.to(dev).requires_grad_(True)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    y = ops.batch_norm_leaky_relu(x, w, b, rm, rv, 1e-5, 0.1, 0.2)
+    gy32 = torch.randn(y.shape, generator=g)
+    y.backward(gy32.to(dev, dtype))
+
+    xr = x32.to(dtype).float().requires_grad_(True)
+    wr, br = w32.clone().requires_grad_(True), b32.clone().requires_grad_(True)
+    rmr, rvr = torch.zeros(C), torch.ones(C)
+    yr = ops.reference_batch_norm_leaky_relu(xr, wr, br, rmr, rvr, 1e-5, 0.1, 0.2)
+    yr.backward(gy32.to(dtype).float())
+    torch.cuda.synchronize()
+    tol = 2e-4 if dtype == torch.float32 else 3e-2
+    assert y.shape == yr.shape and y.dtype == dtype
+    assert torch.allclose(y.detach().float().cpu(), yr.detach(), atol=tol, rtol=tol)
+    assert torch.allclose(rm.cpu(), rmr, atol=1e-4, rtol=1e-4)
+    assert torch.allclose(rv.cpu(), rvr, atol=1e-4, rtol=1e-4)
+    gtol = 1e-3 if dtype == torch.float32 else 5e-2
+    assert torch.allclose(x.grad.float().cpu(), xr.grad, atol=gtol, rtol=gtol)
+    assert torch.allclose(w.grad.cpu(), wr.grad, atol=gtol * C, rtol=gtol)
+    assert torch.allclose(b.grad.cpu(), br.grad, atol=gtol * C, rtol=gtol)
+
+
+def test_discriminator_fused_matches_unfused(dev):
+    from blendtorch.models import Discriminator
+    torch.manual_seed(0)
+    a = Discriminator(adaptive=True).to(dev).to(memory_format=torch.channels_last)
+    b = Discriminator(adaptive=True, fused=False).to(dev).to(memory_format=torch.channels_last)
+    b.load_state_dict(a.state_dict())
+    x = torch.rand(4, 3, 96, 128, device=dev).to(memory_format=torch.channels_last)
+    ya, yb = a(x), b(x)
+    ya.sum().backward()
+    yb.sum().backward()
+    torch.cuda.synchronize()
+    assert torch.allclose(ya, yb, atol=1e-4, rtol=1e-4)
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        assert torch.allclose(pa.grad, pb.grad, atol=1e-3, rtol=1e-2), n
+    for (n, ba), bb in zip(a.named_buffers(), b.buffers()):
+        assert torch.allclose(ba.float(), bb.float(), atol=1e-4, rtol=1e-4), n
