@@ -67,7 +67,7 @@ def cpu_stream(addresses):
 
 def run(args):
     dev = torch.device(args.device)
-    netD = Discriminator().to(dev)
+    netD = Discriminator(fused=args.fused_bn).to(dev)
     here = Path(__file__).resolve().parent
     launch = dict(num_instances=args.instances, named_sockets=['DATA', 'CTRL'], start_port=args.start_port)
     if args.producer == 'blender':
@@ -165,6 +165,8 @@ def main():
     ap.add_argument('--device', default='cuda' if torch.cuda.is_available() else 'cpu')
     ap.add_argument('--start-port', default=26000, type=int)
     ap.add_argument('--json', default=None)
+    ap.add_argument('--no-fused-bn', dest='fused_bn', action='store_false',
+                    help='discriminator with MIOpen BatchNorm + PyTorch LeakyReLU instead of the fused gfx950 op')
     ap.add_argument('--verbose', action='store_true')
     args = ap.parse_args()
     res = run(args)
