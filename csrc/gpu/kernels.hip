@@ -729,7 +729,11 @@ __global__ __launch_bounds__(kBlock) void bn_reduce_kernel(const void* __restric
                                                            const float* __restrict__ w, const float* __restrict__ b,
                                                            float slope, float* __restrict__ partial) {
   constexpr int V = BnVec<DT>::V;
-  __shared__ float ls[kBlock * V], lq[kBlock * V];
+  // partials laid out [V][kBlock + 1]: lane t's V values land in V different
+  // rows at column t, so the write is bank-conflict free (a [row][C] layout
+  // put the lanes' 8-float runs on the same banks)
+  constexpr int LS = kBlock + 1;
+  __shared__ float ls[V * LS], lq[V * LS];
   const int G = C / V, R = kBlock / G;
   const int g = int(threadIdx.x) % G, r0 = int(threadIdx.x) / G;
   const int c0 = g * V;
@@ -762,11 +766,14 @@ __global__ __launch_bounds__(kBlock) void bn_reduce_kernel(const void* __restric
     }
   }
 #pragma unroll
-  for (int i = 0; i < V; ++i) ls[r0 * C + c0 + i] = s[i], lq[r0 * C + c0 + i] = q[i];
+  for (int i = 0; i < V; ++i) ls[i * LS + threadIdx.x] = s[i], lq[i * LS + threadIdx.x] = q[i];
   __syncthreads();
   for (int c = int(threadIdx.x); c < C; c += kBlock) {
+    // channel c = group c / V, element c % V; its R partials sit in lanes r * G + c / V
+    const float* ps = ls + (c % V) * LS + c / V;
+    const float* pq = lq + (c % V) * LS + c / V;
     float a = 0.f, q2 = 0.f;
-    for (int r = 0; r < R; ++r) a += ls[r * C + c], q2 += lq[r * C + c];
+    for (int r = 0; r < R; ++r) a += ps[r * G], q2 += pq[r * G];
     partial[int64_t(blockIdx.x) * 2 * C + c] = a;
     partial[int64_t(blockIdx.x) * 2 * C + C + c] = q2;
   }

@@ -390,12 +390,21 @@ def project(points, PV, V, W, H, upper_left=True):
 # ---------------------------------------------------------------------------
 # consumer-model op: adaptive average pooling on channels-last activations
 
-_POOL_DTYPES = {'torch.float32': 0, 'torch.bfloat16': 1}
+_DT_CODES = {}
+
+
+def _dt(x):
+    """Kernel dtype code of a tensor (None when unsupported); keyed by the
+    torch dtype object, so the per-call cost is one dict lookup."""
+    if not _DT_CODES:
+        import torch
+        _DT_CODES.update({torch.float32: 0, torch.bfloat16: 1})
+    return _DT_CODES.get(x.dtype)
 
 
 def _pool_launch(name, src, dst, N, H, W, C, OH, OW):
     ext = hip_ext()
-    getattr(ext, name)(src.data_ptr(), dst.data_ptr(), N, H, W, C, OH, OW, _POOL_DTYPES[str(src.dtype)],
+    getattr(ext, name)(src.data_ptr(), dst.data_ptr(), N, H, W, C, OH, OW, _dt(src),
                        _stream(src.device))
 
 
@@ -440,7 +449,7 @@ def adaptive_avg_pool_nhwc(x, output_size):
     if _POOL_FN is None:
         _POOL_FN = _pool_function()
     oh, ow = (output_size, output_size) if isinstance(output_size, int) else output_size
-    if x.dim() != 4 or str(x.dtype) not in _POOL_DTYPES:
+    if x.dim() != 4 or _dt(x) is None:
         raise ValueError(f'adaptive_avg_pool_nhwc needs a 4-D float32/bfloat16 tensor, got {x.dtype} {tuple(x.shape)}')
     return _POOL_FN.apply(x, oh, ow)
 
@@ -467,7 +476,7 @@ def _pool_module():
             self.output_size = output_size
 
         def forward(self, x):
-            if x.is_cuda and str(x.dtype) in _POOL_DTYPES:
+            if x.is_cuda and _dt(x) is not None:
                 return adaptive_avg_pool_nhwc(x, self.output_size)
             return F.adaptive_avg_pool2d(x, self.output_size)
 
@@ -490,7 +499,7 @@ def _bn_function():
             ext = hip_ext()
             N, C, H, W = x.shape
             M = N * H * W
-            dt = _POOL_DTYPES[str(x.dtype)]
+            dt = _dt(x)
             xs = _as_nhwc(x)
             w = weight.detach().float().contiguous()
             b = bias.detach().float().contiguous()
@@ -513,8 +522,8 @@ def _bn_function():
             xs, w, b, mean, invstd = ctx.saved_tensors
             N, H, W, C = xs.shape
             M = N * H * W
-            dt = _POOL_DTYPES[str(xs.dtype)]
-            gys = _as_nhwc(gy.to(xs.dtype))
+            dt = _dt(xs)
+            gys = _as_nhwc(gy if gy.dtype == xs.dtype else gy.to(xs.dtype))
             gx = torch.empty_like(xs)
             dw = torch.empty(C, dtype=torch.float32, device=xs.device)
             db = torch.empty_like(dw)
@@ -528,15 +537,21 @@ def _bn_function():
 
 
 _BN_FN = None
+_BN_SHAPES = {}
 
 
 def bn_supported(x):
     """True when the fused kernels take ``x`` (GPU fp32/bf16, 16-byte channel
     groups that tile a 256-lane block)."""
-    if not (x.is_cuda and x.dim() == 4 and str(x.dtype) in _POOL_DTYPES):
+    dt = _dt(x)
+    if dt is None or not x.is_cuda or x.dim() != 4:
         return False
     N, C, H, W = x.shape
-    return hip_ext().bn_partial_floats(N * H * W, C, _POOL_DTYPES[str(x.dtype)]) > 0
+    key = (C, dt)
+    ok = _BN_SHAPES.get(key)
+    if ok is None:     # the kernels' shape rule depends on C and dtype only
+        ok = _BN_SHAPES[key] = hip_ext().bn_partial_floats(1, C, dt) > 0
+    return ok
 
 
 def batch_norm_leaky_relu(x, weight, bias, running_mean=None, running_var=None, eps=1e-5, momentum=0.1,
@@ -549,6 +564,10 @@ def batch_norm_leaky_relu(x, weight, bias, running_mean=None, running_var=None, 
         _BN_FN = _bn_function()
     if not bn_supported(x):
         raise ValueError(f'batch_norm_leaky_relu: unsupported input {x.dtype} {tuple(x.shape)} on {x.device}')
+    return _BN_FN.apply(x, weight, bias, running_mean, running_var, eps, momentum, slope)
+
+
+def _bn_apply_unchecked(x, weight, bias, running_mean, running_var, eps, momentum, slope):
     return _BN_FN.apply(x, weight, bias, running_mean, running_var, eps, momentum, slope)
 
 
@@ -580,9 +599,12 @@ def _bn_module():
         def forward(self, x):
             if (self.training and self.affine and self.track_running_stats and self.momentum is not None
                     and bn_supported(x)):
+                global _BN_FN
+                if _BN_FN is None:
+                    _BN_FN = _bn_function()
                 self.num_batches_tracked.add_(1)
-                return batch_norm_leaky_relu(x, self.weight, self.bias, self.running_mean, self.running_var,
-                                             self.eps, self.momentum, self.slope)
+                return _bn_apply_unchecked(x, self.weight, self.bias, self.running_mean, self.running_var,
+                                           self.eps, self.momentum, self.slope)
             return F.leaky_relu(super().forward(x), self.slope)
 
         def extra_repr(self):
