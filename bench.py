@@ -201,8 +201,9 @@ def main():
         if world > 1:
             model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[gpu])
         use_graph = args.graph == 'on' or (args.graph == 'auto' and world == 1)
-        # capturable Adam keeps its step counters on the GPU, so the update can live inside the graph
-        opt = torch.optim.Adam(model.parameters(), lr=2e-4, capturable=use_graph)
+        # fused Adam: one multi-tensor kernel for the whole update (0.95 -> 0.84 ms graphed step,
+        # profiles/consumer_step.md); capturable keeps its step counters on the GPU for the graph
+        opt = torch.optim.Adam(model.parameters(), lr=2e-4, capturable=use_graph, fused=True)
         crit = torch.nn.BCELoss()
 
     WARM_RESERVE = 2000   # extra warm-up batches allowed while producers come up

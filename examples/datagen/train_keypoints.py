@@ -76,7 +76,7 @@ def main(argv=None):
     model = KeypointNet().to(dev).to(memory_format=torch.channels_last)
     if world > 1:
         model = nn.parallel.DistributedDataParallel(model, device_ids=[dev.index])
-    opt = torch.optim.AdamW(model.parameters(), lr=a.lr)
+    opt = torch.optim.AdamW(model.parameters(), lr=a.lr, fused=dev.type == 'cuda')   # one multi-tensor kernel
     scale = torch.tensor([W, H], dtype=torch.float32, device=dev)
     port = a.start_port or (25000 + (os.getpid() % 100) * 40 if world == 1 else 25000 + rank * 40)
     with btt.BlenderLauncher(producer='cubesim', num_instances=a.producers, named_sockets=['DATA'], proto='ipc',

@@ -96,7 +96,7 @@ def run(args):
 
         mu = np.asarray(mu_target) + np.random.randn(2) if args.random_start else [1.2, 3.0]
         pm = ProbModel(mu, [0.4, 0.4])
-        optD = optim.Adam(netD.parameters(), lr=5e-5, betas=(0.5, 0.999))
+        optD = optim.Adam(netD.parameters(), lr=5e-5, betas=(0.5, 0.999), fused=dev.type == 'cuda')
         optS = optim.Adam(pm.parameters(), lr=5e-2, betas=(0.7, 0.999))
         crit = nn.BCELoss(reduction='none')
         b = 0.7
