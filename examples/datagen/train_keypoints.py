@@ -22,6 +22,7 @@ Prints one JSON line: samples/s, and the first and last loss (mean squared error
 the corner positions, in units of the image size).
 """
 import argparse
+import functools
 import json
 import os
 import sys
@@ -37,16 +38,23 @@ from blendtorch import btt, ops, parallel  # noqa: E402
 from blendtorch.btt.gpu import DeviceLoader  # noqa: E402
 
 
-def block(cin, cout, stride):
-    return nn.Sequential(nn.Conv2d(cin, cout, 3, stride, 1, bias=False), nn.BatchNorm2d(cout), nn.ReLU(inplace=True))
+def _block_factory(cin, cout, stride, fused=True):
+    if fused:
+        # BN + ReLU (a LeakyReLU of slope 0) as one gfx950 op on GPU training steps:
+        # 8 passes over the activation per step instead of 13 (csrc/gpu/kernels.hip bn_*)
+        norm_act = [ops.BatchNormLeakyReLU2d(cout, slope=0.0), nn.Identity()]
+    else:
+        norm_act = [nn.BatchNorm2d(cout), nn.ReLU(inplace=True)]
+    return nn.Sequential(nn.Conv2d(cin, cout, 3, stride, 1, bias=False), *norm_act)
 
 
 class KeypointNet(nn.Module):
     """Small strided CNN: 3x480x640 -> 8 corners (x, y) in [0, 1]."""
 
-    def __init__(self, width=32, corners=8):
+    def __init__(self, width=32, corners=8, fused=True):
         super().__init__()
         w = width
+        block = functools.partial(_block_factory, fused=fused)
         self.features = nn.Sequential(
             block(3, w, 2), block(w, w, 1),            # 240x320
             block(w, 2 * w, 2), block(2 * w, 2 * w, 1),  # 120x160
@@ -54,7 +62,7 @@ class KeypointNet(nn.Module):
             block(4 * w, 8 * w, 2),                    # 30x40
             block(8 * w, 8 * w, 2),                    # 15x20
         )
-        self.head = nn.Sequential(nn.AdaptiveAvgPool2d((3, 4)), nn.Flatten(), nn.Linear(8 * w * 12, 256),
+        self.head = nn.Sequential(ops.AdaptiveAvgPool2d((3, 4)) if fused else nn.AdaptiveAvgPool2d((3, 4)), nn.Flatten(), nn.Linear(8 * w * 12, 256),
                                   nn.ReLU(inplace=True), nn.Linear(256, 2 * corners))
 
     def forward(self, x):
@@ -69,11 +77,13 @@ def main(argv=None):
     ap.add_argument('--lr', type=float, default=2e-3)
     ap.add_argument('--start-port', type=int, default=0)
     ap.add_argument('--json', default=None)
+    ap.add_argument('--no-fused-bn', dest='fused_bn', action='store_false',
+                    help='MIOpen BatchNorm + ReLU instead of the fused gfx950 op')
     a = ap.parse_args(argv)
 
     rank, world, dev = parallel.init_distributed()
     W, H = 640, 480
-    model = KeypointNet().to(dev).to(memory_format=torch.channels_last)
+    model = KeypointNet(fused=a.fused_bn).to(dev).to(memory_format=torch.channels_last)
     if world > 1:
         model = nn.parallel.DistributedDataParallel(model, device_ids=[dev.index])
     opt = torch.optim.AdamW(model.parameters(), lr=a.lr, fused=dev.type == 'cuda')   # one multi-tensor kernel
