@@ -87,6 +87,7 @@ Args parse(int argc, char** argv) {
   Args a;
   // BlenderLauncher(shm_slots=N) exports BLENDTORCH_SHM_SLOTS; --shm overrides
   if (const char* e = std::getenv("BLENDTORCH_SHM_SLOTS")) a.shm_slots = std::atoi(e);
+  if (const char* e = std::getenv("BLENDTORCH_SHM_CODEC")) a.codec = e;   // BlenderLauncher(shm_codec=...)
   if (const char* e = std::getenv("BLENDTORCH_SHM_CODEC")) a.codec = e;
   std::vector<std::string> v;
   int start = 1;

@@ -6,11 +6,21 @@ while no consumer is connected or all consumer queues are full, and no
 message is ever dropped.  Every message is the dict
 ``{'btid': btid, **kwargs}``, pickled.
 """
+import itertools
 import os
 
 import numpy as np
 
 from ..transport import shm, zmq
+
+
+_SEGMENTS = itertools.count()
+
+
+def _segment_name(btid, kind='ring'):
+    """Unique per process and publisher (consumers cache mappings by name);
+    the ``blendtorch-<pid>-`` prefix is what ``shm.cleanup_pid`` removes."""
+    return f'blendtorch-{os.getpid()}-{btid}-{kind}{next(_SEGMENTS)}'
 
 
 class DataPublisher:
@@ -22,11 +32,26 @@ class DataPublisher:
     takes the value from ``BLENDTORCH_SHM_SLOTS`` (set by
     ``btt.BlenderLauncher(shm_slots=N)``), else 0: plain pickled frames as
     in the reference.
+
+    ``shm_codec='tile16'`` (or ``BLENDTORCH_SHM_CODEC=tile16``) sends ring
+    frames as key-frame deltas: the first published image (or the one given
+    to :meth:`set_key_frame`, e.g. the empty scene) goes once into a key
+    segment, and every frame then carries only the 16x16 tiles that differ
+    from it -- lossless, and with a static camera most of the frame never
+    crosses PCIe again.  Frames whose size is not a multiple of 16 go raw.
     """
 
-    def __init__(self, bind_address, btid=None, send_hwm=10, lingerms=0, shm_slots=None, shm_key='image'):
+    def __init__(self, bind_address, btid=None, send_hwm=10, lingerms=0, shm_slots=None, shm_key='image',
+                 shm_codec=None):
         if shm_slots is None:
             shm_slots = int(os.environ.get('BLENDTORCH_SHM_SLOTS', '0') or 0)
+        if shm_codec is None:
+            shm_codec = os.environ.get('BLENDTORCH_SHM_CODEC', 'none') or 'none'
+        if shm_codec not in ('none', 'tile16'):
+            raise ValueError(f'shm_codec must be none or tile16, not {shm_codec!r}')
+        self.shm_codec = shm_codec
+        self._key = None
+        self._key_ring = None
         self.ctx = zmq.Context()
         self.sock = self.ctx.socket(zmq.PUSH)
         self.sock.setsockopt(zmq.SNDHWM, send_hwm)
@@ -42,15 +67,39 @@ class DataPublisher:
         """Send ``{'btid': btid, **kwargs}`` (values must be picklable)."""
         img = kwargs.get(self.shm_key) if self.shm_slots else None
         if isinstance(img, np.ndarray) and img.dtype == np.uint8:
+            tiled = self.shm_codec == 'tile16' and shm.tile16_supported(img.shape)
             if self._ring is None:
-                self._ring = shm.ShmRing(f'blendtorch-{os.getpid()}-{self.btid}', self.shm_slots, img.nbytes)
-            slot, off, h, w, c, gen = self._ring.put(img)
+                c = img.shape[2] if img.ndim == 3 else 1
+                cap = max(img.nbytes, shm.tile16_max_bytes(img.shape[0], img.shape[1], c)) if tiled else img.nbytes
+                self._ring = shm.ShmRing(_segment_name(self.btid), self.shm_slots, cap)
+            if tiled and (self._key is None or self._key.shape != img.shape):
+                self.set_key_frame(img)
+            if tiled and self._key.shape == img.shape:
+                slot, off, h, w, c, gen, _ = self._ring.put_tile16(img, self._key)
+                extra = (('tile16', self._key_ring.name, self._key_gen),)
+            else:
+                slot, off, h, w, c, gen = self._ring.put(img)
+                extra = ()
             kwargs = {k: v for k, v in kwargs.items() if k != self.shm_key}
-            kwargs[shm.KEY] = (self._ring.name, slot, off, h, w, c, self.shm_key, gen)
+            kwargs[shm.KEY] = (self._ring.name, slot, off, h, w, c, self.shm_key, gen) + extra
         self.sock.send_pyobj({'btid': self.btid, **kwargs})
+
+    def set_key_frame(self, image):
+        """Publish ``image`` (u8 HxW[xC]) as the key frame of the tile16 codec.
+        It is written once into its own segment; a consumer reads it once."""
+        key = np.ascontiguousarray(image, dtype=np.uint8).copy()
+        if self._key_ring is not None:
+            # a new key gets a new segment: consumers cache keys by segment name
+            self._key_ring.close()
+        self._key_ring = shm.ShmRing(_segment_name(self.btid, 'key'), 1, key.nbytes)
+        _, _, _, _, _, self._key_gen = self._key_ring.put(key)
+        self._key = key
 
     def close(self):
         self.sock.close()
         if self._ring is not None:
             self._ring.close()
             self._ring = None
+        if self._key_ring is not None:
+            self._key_ring.close()
+            self._key_ring = None

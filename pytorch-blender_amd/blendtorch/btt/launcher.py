@@ -66,6 +66,8 @@ class BlenderLauncher:
     frame ring (``BLENDTORCH_SHM_SLOTS`` in the children's environment: a
     scene script's ``btb.DataPublisher`` and the native producers pick it
     up without code changes).  Only for consumers on this host.
+    ``shm_codec='tile16'`` (``BLENDTORCH_SHM_CODEC``) additionally sends the
+    ring frames as key-frame deltas (only changed 16x16 tiles).
 
     Attributes
     ----------
@@ -76,7 +78,7 @@ class BlenderLauncher:
     def __init__(self, scene=None, script=None, num_instances=1, named_sockets=None, start_port=11000,
                  bind_addr='127.0.0.1', instance_args=None, proto='tcp', blend_path=None, seed=None,
                  background=False, producer=None, cpu_affinity=None, respawn=False, env=None, stdout=None,
-                 stderr=None, shm_slots=0):
+                 stderr=None, shm_slots=0, shm_codec=None):
         assert num_instances > 0
         self.num_instances = num_instances
         self.start_port = start_port
@@ -98,6 +100,8 @@ class BlenderLauncher:
         self.env = dict(env or {})
         if shm_slots:
             self.env['BLENDTORCH_SHM_SLOTS'] = int(shm_slots)
+        if shm_codec:
+            self.env['BLENDTORCH_SHM_CODEC'] = str(shm_codec)
         self.stdout = stdout
         self.stderr = stderr
 

@@ -49,6 +49,7 @@ class _Segment:
             raise ValueError(f'{name} is not a blendtorch shm segment')
         self.nslots, self.slot_bytes, self.data_offset = nslots, slot_bytes, data_offset
         self.states = np.frombuffer(mm, dtype=np.uint32, count=nslots, offset=_HDR.size)
+        self.ino = os.fstat(fd).st_ino
 
     def slot_array(self, i, shape, dtype=np.uint8):
         off = self.data_offset + i * self.slot_bytes
@@ -73,6 +74,16 @@ def _open(name):
     if _views_pid != os.getpid():   # fresh cache after fork
         _views, _views_pid = {}, os.getpid()
     seg = _views.get(name)
+    if seg is not None:
+        # a producer may have closed the segment and created a new one under
+        # the same name: the cached mapping would show the old, unlinked file
+        try:
+            stale = os.stat(_path(name)).st_ino != seg.ino
+        except FileNotFoundError:
+            stale = True
+        if stale:
+            del _views[name]
+            seg = None
     if seg is None:
         fd = os.open(_path(name), os.O_RDWR)
         size = os.fstat(fd).st_size
@@ -206,8 +217,52 @@ class ShmRing:
         self.seg.states[i] = _word(gen, PUBLISHED)
         return i, self.seg.data_offset + i * self.seg.slot_bytes, h, w, c, gen
 
+    def put_tile16(self, image, key):
+        """Write ``image`` into a free slot as a key-frame delta against ``key``
+        (same shape; csrc/codec/tiledelta.h layout: tile count, tile positions,
+        payload tiles of 16 rows x 16*C bytes).  Needs H and W multiples of 16
+        and slots of :func:`tile16_max_bytes`.  Returns the same fields as
+        :meth:`put` plus the number of payload tiles."""
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        h, w = img.shape[:2]
+        c = img.shape[2] if img.ndim == 3 else 1
+        ty, tx = h // TILE, w // TILE
+        nt = ty * tx
+        f = img.reshape(ty, TILE, tx, TILE, c)
+        changed = (f != key.reshape(ty, TILE, tx, TILE, c)).any(axis=(1, 3, 4))     # [ty, tx]
+        pos = np.flatnonzero(changed).astype(np.uint32)
+        n = len(pos)
+        pay = tile16_payload_offset(h, w)
+        if pay + n * TILE * TILE * c > self.seg.slot_bytes:
+            raise ValueError('tile16 frame larger than the ring slot')
+        i = self.acquire()
+        off = self.seg.data_offset + i * self.seg.slot_bytes
+        hdr = np.frombuffer(self.seg.mm, dtype=np.uint32, count=1 + nt, offset=off)
+        hdr[0] = n
+        hdr[1:1 + n] = pos
+        if n:
+            dst = np.frombuffer(self.seg.mm, dtype=np.uint8, count=n * TILE * TILE * c, offset=off + pay)
+            dst.reshape(n, TILE, TILE, c)[...] = f.transpose(0, 2, 1, 3, 4)[changed]
+        gen = ((int(self.seg.states[i]) >> 2) + 1) & 0x3fffffff
+        self._published_at[i] = time.time()
+        self.seg.states[i] = _word(gen, PUBLISHED)
+        return i, off, h, w, c, gen, n
+
     def close(self):
         self.seg.close()
+
+
+def tile16_supported(shape):
+    return len(shape) in (2, 3) and shape[0] % TILE == 0 and shape[1] % TILE == 0 and shape[0] > 0 and shape[1] > 0
+
+
+def tile16_payload_offset(h, w):
+    """Byte offset of the first payload tile (count + positions, 256-B aligned)."""
+    return (((h // TILE) * (w // TILE) + 1) * 4 + 255) & ~255
+
+
+def tile16_max_bytes(h, w, c):
+    return tile16_payload_offset(h, w) + (h // TILE) * (w // TILE) * TILE * TILE * c
 
 
 def cleanup_pid(pid):

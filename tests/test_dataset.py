@@ -104,20 +104,71 @@ def test_python_publisher_shared_memory(free_port):
     pull.close()
 
 
-def test_launcher_shm_slots_reaches_scene_scripts(free_port):
-    """BlenderLauncher(shm_slots=N) switches an unmodified scene script's
-    DataPublisher to the shared-memory ring (descriptor messages), and the
-    CPU dataset resolves them back into images."""
+def _moving_square_frames(n, h=48, w=64, c=4):
+    bg = (np.arange(h * w * c, dtype=np.uint32) % 251).astype(np.uint8).reshape(h, w, c)
+    frames = []
+    for i in range(n):
+        f = bg.copy()
+        y, x = (3 * i) % (h - 10), (5 * i) % (w - 12)
+        f[y:y + 10, x:x + 12] = 200 + i
+        frames.append(f)
+    return bg, frames
+
+
+def test_python_publisher_tile16_codec(free_port):
+    """DataPublisher(shm_codec='tile16'): key frame once, then only changed
+    16x16 tiles; shm.resolve rebuilds every frame exactly; other sizes go raw."""
+    from blendtorch.btb.publisher import DataPublisher
+    from blendtorch.transport import shm, zmq
+    bg, frames = _moving_square_frames(12)
+    pub = DataPublisher(f'tcp://127.0.0.1:{free_port}', btid=0, shm_slots=4, shm_codec='tile16')
+    pub.set_key_frame(bg)
+    pull = zmq.Context().socket(zmq.PULL)
+    pull.connect(f'tcp://127.0.0.1:{free_port}')
+    try:
+        _check_tile16_stream(pub, pull, frames, free_port)
+    finally:
+        pub.close()
+        pull.close()
+
+
+def _check_tile16_stream(pub, pull, frames, free_port):
+    from blendtorch.btb.publisher import DataPublisher
+    from blendtorch.transport import shm
+    for i, f in enumerate(frames):
+        pub.publish(image=f, frameid=i)
+        msg = pull.recv_pyobj()
+        desc = msg[shm.KEY]
+        assert len(desc) == 9 and desc[8][0] == 'tile16'
+        seg = shm._open(desc[0])
+        ntiles = int(np.frombuffer(seg.mm, dtype=np.uint32, count=1, offset=desc[2])[0])
+        assert 1 <= ntiles <= 4          # a 10x12 square touches at most 2x2 tiles
+        msg = shm.resolve(msg)
+        assert np.array_equal(msg['image'], f) and msg['frameid'] == i
+    pub.publish(image=np.full((10, 6, 3), 7, np.uint8), frameid=99)   # not a multiple of 16: raw
+    msg = pull.recv_pyobj()
+    assert len(msg[shm.KEY]) == 8
+    with pytest.raises(ValueError):
+        DataPublisher(f'tcp://127.0.0.1:{free_port + 1}', shm_slots=2, shm_codec='jpeg')
+
+
+@pytest.mark.parametrize('codec', [None, 'tile16'])
+def test_launcher_shm_slots_reaches_scene_scripts(free_port, codec):
+    """BlenderLauncher(shm_slots=N[, shm_codec='tile16']) switches an
+    unmodified scene script's DataPublisher to the shared-memory ring
+    (descriptor messages, key-frame deltas with the codec), and the CPU
+    dataset resolves them back into images."""
     from blendtorch.transport import shm, zmq
     ex = ROOT / 'examples' / 'datagen'
     args = dict(scene=ex / 'cube.blend', script=ex / 'cube.blend.py', num_instances=1, named_sockets=['DATA'],
-                start_port=free_port, background=True, blend_path=HEADLESS_BLENDER, shm_slots=8)
+                start_port=free_port, background=True, blend_path=HEADLESS_BLENDER, shm_slots=8, shm_codec=codec)
     with btt.BlenderLauncher(**args) as bl:
         s = zmq.Context().socket(zmq.PULL)
         s.connect(bl.launch_info.addresses['DATA'][0])
         assert s.poll(30000)
         raw = s.recv_pyobj()
         assert shm.KEY in raw and 'image' not in raw
+        assert (len(raw[shm.KEY]) == 9 and raw[shm.KEY][8][0] == 'tile16') if codec else len(raw[shm.KEY]) == 8
         shm.release(raw[shm.KEY])
         s.close()
         ds = btt.RemoteIterableDataset(bl.launch_info.addresses['DATA'], max_items=12)

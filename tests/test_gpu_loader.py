@@ -462,3 +462,42 @@ def test_device_loader_tile_codec(dev, free_port, extra, cfg):
     assert stats['tile']['image_bytes'] < stats['raw']['image_bytes'] / 2
     assert not torch.equal(out['raw'][0], out['raw'][1])   # random poses
     assert not [f for f in os.listdir('/dev/shm') if f.startswith('blendtorch-')]
+
+
+def test_device_loader_python_publisher_tile16(dev, free_port):
+    """A Python producer (btb.DataPublisher, shm_codec='tile16') streams
+    key-frame deltas into the GPU loader: decoded batches equal the raw frames
+    through the fp32 reference decode, on the fused fill + tile-scatter path."""
+    import threading
+    from blendtorch.btb.publisher import DataPublisher
+    h, w = 48, 64
+    bg = (np.arange(h * w * 4, dtype=np.uint32) % 251).astype(np.uint8).reshape(h, w, 4)
+    frames = []
+    for i in range(16):
+        f = bg.copy()
+        f[(3 * i) % 38:(3 * i) % 38 + 10, (5 * i) % 52:(5 * i) % 52 + 12] = 200 + i
+        frames.append(f)
+    addr = f'tcp://127.0.0.1:{free_port}'
+    pub = DataPublisher(addr, btid=3, shm_slots=8, shm_codec='tile16')
+    pub.set_key_frame(bg)
+
+    def produce():
+        for i, f in enumerate(frames):
+            pub.publish(image=f, frameid=i)
+
+    t = threading.Thread(target=produce, daemon=True)
+    t.start()
+    cfg = ops.DecodeConfig.unit(channels='rgb', gamma=2.2)
+    got = {}
+    try:
+        dl = DeviceLoader([addr], batch_size=4, max_items=16, decode=cfg, device=dev, timeoutms=20000)
+        for b in dl:
+            for img, fid in zip(b['image'], b['frameid'].tolist()):
+                got[int(fid)] = img
+        t.join(10)
+    finally:
+        pub.close()
+    assert dl.stats['frames'] == 16 and dl.stats['bad'] == 0 and dl.stats['tiled_frames'] == 16
+    ref = ops.reference_decode(torch.from_numpy(np.stack(frames)), cfg)
+    for i in range(16):
+        torch.testing.assert_close(got[i].cpu(), ref[i], rtol=0, atol=0)
