@@ -25,11 +25,11 @@ VARIANTS = {
 }
 
 
-def run(name, iters, batch, graph, fused_adam=False):
+def run(name, iters, batch, graph, fused_adam=False, fused_bn=True):
     dt, fmt = VARIANTS[name]
     dev = torch.device('cuda', 0)
     torch.manual_seed(0)
-    model = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=fmt)
+    model = Discriminator(nc=3, ndf=32, adaptive=True, fused=fused_bn).to(dev).to(memory_format=fmt)
     opt = torch.optim.Adam(model.parameters(), lr=2e-4, capturable=graph, fused=fused_adam or None)
     crit = torch.nn.BCELoss()
     x = torch.rand(batch, 3, 480, 640, device=dev).to(memory_format=fmt)
@@ -63,7 +63,7 @@ def run(name, iters, batch, graph, fused_adam=False):
         fn()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / iters * 1000
-    return {'variant': name, 'graph': graph, 'fused_adam': fused_adam, 'ms_per_step': round(ms, 4), 'images_per_s': round(batch / ms * 1000, 1)}
+    return {'variant': name, 'graph': graph, 'fused_adam': fused_adam, 'fused_bn': fused_bn, 'ms_per_step': round(ms, 4), 'images_per_s': round(batch / ms * 1000, 1)}
 
 
 def main():
@@ -74,13 +74,15 @@ def main():
     ap.add_argument('--graph', choices=['both', 'on', 'off'], default='both')
     ap.add_argument('--no-fused-adam', dest='fused_adam', action='store_false',
                     help='foreach Adam instead of torch.optim.Adam(fused=True) (one multi-tensor kernel)')
+    ap.add_argument('--no-fused-bn', dest='fused_bn', action='store_false',
+                    help='MIOpen BatchNorm + PyTorch LeakyReLU instead of the fused gfx950 op')
     args = ap.parse_args()
     torch.backends.cudnn.benchmark = True
     names = [args.only] if args.only else list(VARIANTS)
     graphs = {'both': (False, True), 'on': (True,), 'off': (False,)}[args.graph]
     for n in names:
         for g in graphs:
-            print(json.dumps(run(n, args.iters, args.batch, g, args.fused_adam)), flush=True)
+            print(json.dumps(run(n, args.iters, args.batch, g, args.fused_adam, args.fused_bn)), flush=True)
 
 
 if __name__ == '__main__':
