@@ -376,6 +376,9 @@ def main():
             'gpu_us_per_image': (round(metrics['gpu_us_per_image'], 3)
                                  if metrics.get('gpu_us_per_image') is not None else None),
             'frames_per_producer': metrics.get('frames_per_producer'),
+            # host time blocked in the loader's next() per batch (whole run incl. warm-up)
+            'consumer_wait_ms_per_batch': (round(metrics['consumer_wait_s'] * 1e3 / max(1, metrics['batches']), 4)
+                                           if metrics.get('consumer_wait_s') is not None else None),
             'cpu': cpu,
         }), flush=True)
     if world > 1:
