@@ -376,6 +376,9 @@ def main():
             'gpu_us_per_image': (round(metrics['gpu_us_per_image'], 3)
                                  if metrics.get('gpu_us_per_image') is not None else None),
             'frames_per_producer': metrics.get('frames_per_producer'),
+            # image bytes moved host -> device per second (tile16 moves only the changed tiles)
+            'h2d_gbytes_per_s': (round(metrics['h2d_gbytes_per_s'], 2)
+                                 if metrics.get('h2d_gbytes_per_s') is not None else None),
             # host time blocked in the loader's next() per batch (whole run incl. warm-up)
             'consumer_wait_ms_per_batch': (round(metrics['consumer_wait_s'] * 1e3 / max(1, metrics['batches']), 4)
                                            if metrics.get('consumer_wait_s') is not None else None),
