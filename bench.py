@@ -18,7 +18,12 @@ producers (shard mode, weak scaling), ranks are synchronised with RCCL
 barriers around the timed region and the slowest rank's time is reported.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--producers P]
-                    [--mode rgba|rgb] [--consumer none|disc]
+                    [--mode rgba|rgb] [--consumer none|disc] [--codec none|tile16]
+                    [--h2d auto|copy] [--graph auto|on|off] [--dist shard|pool|scatter]
+
+--consumer disc adds a DCGAN discriminator training step per batch (bf16,
+fused gfx950 BN+LeakyReLU and pooling kernels, fused Adam, one HIP graph per
+step on a single rank; profiles/consumer_step.md).
 
 Rank 0 prints ONE JSON line (see README "Benchmark").
 """
