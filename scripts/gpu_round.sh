@@ -20,6 +20,14 @@ for step in "$@"; do
           mkdir -p gpurun_out/prof && find /tmp/rp_prof -name '*stats.csv' -exec cp {} gpurun_out/prof/ \;;;
     prof:*) a="${step#prof:}"; tag=$(echo "$a" | tr -c 'a-zA-Z0-9\n' '_'); timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/rp_prof_$tag -o run --output-format csv -- python bench.py --steps 300 --warmup 20 ${a//,/ } > gpurun_out/prof_$tag.log 2>&1; rc=$?; grep '^{' gpurun_out/prof_$tag.log | cut -c1-200
           mkdir -p gpurun_out/prof_$tag && find /tmp/rp_prof_$tag -name '*stats.csv' -exec cp {} gpurun_out/prof_$tag/ \;;;
+    cpmc) for pass in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES" "FETCH_SIZE" "WRITE_SIZE GRBM_GUI_ACTIVE"; do
+            n=$((${n:-0}+1))
+            timeout -s KILL 90 rocprofv3 --pmc $pass --kernel-trace -d /tmp/rp_cpmc$n -o run --output-format csv -- python scripts/consumer_pmc.py > gpurun_out/cpmc$n.log 2>&1; rc=$?
+            mkdir -p gpurun_out/cpmc && find /tmp/rp_cpmc$n -name '*counter_collection.csv' -exec cp {} gpurun_out/cpmc/pass${n}_counters.csv \;
+            rm -f gpurun_out/cpmc$n.log
+            ok $rc || { echo "cpmc pass $n rc=$rc"; exit $rc; }
+          done;;
+    dstep) timeout -k 10 200 python scripts/disc_step_bench.py --only bf16-nhwc > gpurun_out/disc_step.log 2>&1; rc=$?; grep '^{' gpurun_out/disc_step.log;;
     kbench) timeout -k 10 200 python scripts/kernel_bench.py --json gpurun_out/kernel_bench.json > gpurun_out/kernel_bench.log 2>&1; rc=$?; cat gpurun_out/kernel_bench.log;;
     kprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/rp_kprof -o run --output-format csv -- python scripts/kernel_bench.py --iters 50 > gpurun_out/kprof.log 2>&1; rc=$?
           mkdir -p gpurun_out/kprof && find /tmp/rp_kprof -name '*stats.csv' -exec cp {} gpurun_out/kprof/ \;;;
