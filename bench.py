@@ -31,6 +31,7 @@ import argparse
 import fcntl
 import json
 import os
+import signal
 import sys
 import time
 from pathlib import Path
@@ -43,6 +44,12 @@ sys.path.insert(0, str(PKG))
 # 0.011 s/image -> 90.9 images/s (Readme.md:93).
 BASELINE_IMAGES_PER_SEC = 90.9
 METRIC = 'images/sec (whole node) + sec/batch, 640x480 RGBA Cube scene, batch=8'
+# What vs_baseline compares: our producers are C++ stand-ins for Blender, so
+# the ratio is NOT a framework speedup over blendtorch on equal producers.
+PRODUCER = 'cubesim (C++ stand-in for Blender/Eevee, dirty-rect incremental CPU raster)'
+BASELINE_NOTE = ('vs_baseline = value / 90.9 img/s, the reference\'s best row: 5 Blender/Eevee instances '
+                 '(Readme.md:93). The producers differ (C++ stand-in vs Blender), so the ratio reflects the whole '
+                 'pipeline incl. rendering, not the streaming framework alone.')
 
 
 def ensure_built():
@@ -85,9 +92,11 @@ def cgroup_cpu_stat():
         return {}
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=int(os.environ.get('WORLD_SIZE', '1')))
+    ap.add_argument('--gpus', type=int, default=int(os.environ.get('WORLD_SIZE', '1')),
+                    help='GPUs (= ranks).  Without a torchrun environment and N > 1 this process becomes a '
+                         'supervisor that starts N ranks itself (blendtorch/parallel/launch.py)')
     ap.add_argument('--steps', type=int, default=2000)
     ap.add_argument('--warmup', type=int, default=50)
     ap.add_argument('--batch', type=int, default=8)
@@ -125,9 +134,49 @@ def main():
                     help='shard: every rank owns its producers; pool: every rank launches producers and connects '
                          'to all of them (PUSH round-robin across GPUs); scatter: rank 0 receives world*B per step '
                          'and scatters B-image shards over RCCL')
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
     if args.h2d is None:
         args.h2d = 'copy' if args.consumer == 'disc' else 'auto'
+    return args
+
+
+def supervise(args, argv) -> int:
+    """``--gpus N`` without torchrun: start N ranks of this script and relay.
+
+    Runs BEFORE anything touches the GPU in this process (the device count
+    comes from a child interpreter); the ranks inherit stdout, so rank 0's
+    JSON line reaches the caller unchanged.  Never silently runs fewer ranks:
+    with RCCL every rank needs its own GPU; ``--backend gloo`` may rehearse N
+    ranks on fewer GPUs (ranks share devices round-robin)."""
+    import importlib.util   # by path: the blendtorch.parallel package imports torch
+    spec = importlib.util.spec_from_file_location('bt_launch', PKG / 'blendtorch' / 'parallel' / 'launch.py')
+    launch = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(launch)
+    ensure_built()          # once, before the ranks race for the build lock
+    n = args.gpus
+    have = launch.visible_gpu_count()
+    if have < 1 or (args.backend == 'nccl' and have < n):
+        print(f'[bench] --gpus {n} needs {n} visible GPUs for RCCL, found {have} '
+              f'(use --backend gloo to rehearse several ranks on fewer GPUs)', file=sys.stderr, flush=True)
+        return 3
+    codes, rc = launch.spawn_ranks([sys.executable, '-u', str(Path(__file__).resolve())] + list(argv), n)
+    if rc:
+        print(f'[bench] rank exit codes {codes}', file=sys.stderr, flush=True)
+    return rc
+
+
+def _r(v, nd):
+    return None if v is None else round(v, nd)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse_args(argv)
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        return supervise(args, argv)
+    # a supervisor stops ranks with SIGTERM: unwind so the producer processes
+    # this rank launched are torn down by BlenderLauncher.__exit__
+    signal.signal(signal.SIGTERM, lambda *_: sys.exit(143))
 
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
@@ -144,11 +193,19 @@ def main():
     gpu = local_rank % max(1, torch.cuda.device_count())    # == local_rank on a full node
     torch.cuda.set_device(gpu)
     device = torch.device('cuda', gpu)
+    world_seen, allreduce = 1, None
     if world > 1:
         if args.backend == 'nccl':
             dist.init_process_group('nccl', device_id=device)
         else:
             dist.init_process_group('gloo')
+        world_seen = dist.get_world_size()
+        # collective sanity check: sum over ranks of (rank + 1) == w (w + 1) / 2
+        chk = torch.tensor([float(rank + 1)], device=device if args.backend == 'nccl' else 'cpu')
+        dist.all_reduce(chk)
+        allreduce = {'value': float(chk.item()), 'expected': world_seen * (world_seen + 1) / 2}
+        if allreduce['value'] != allreduce['expected']:
+            raise RuntimeError(f'all_reduce sanity check failed: {allreduce}')
 
     # place each rank's producers on CPUs local to its GPU (same NUMA domain as
     # the GPU's PCIe root: frames are written there and read back by the GPU)
@@ -307,6 +364,7 @@ def main():
             dist.barrier()
         cg0 = cgroup_cpu_stat()
         ru0 = os.times()
+        snap0 = dl.snapshot() if dl is not None else {}
         t0 = time.perf_counter()
         for _ in range(args.steps):
             img = step()
@@ -314,6 +372,7 @@ def main():
         if world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t0
+        snap1 = dl.snapshot() if dl is not None else {}
         ru1 = os.times()
         cg1 = cgroup_cpu_stat()
         cpu = {'consumer_cpu_s': round((ru1.user - ru0.user) + (ru1.system - ru0.system), 3)}
@@ -333,12 +392,28 @@ def main():
         if world > 1 and args.dist == 'pool':
             dist.barrier()   # other ranks may still be drawing on this rank's producers
 
+    win = DeviceLoader.window(snap0, snap1)
     t = torch.tensor([elapsed], dtype=torch.float64, device=device if args.backend == 'nccl' else 'cpu')
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     tmax = float(t.item())
     images = args.steps * args.batch * world
     value = images / tmax
+    mine_info = {
+        'rank': rank, 'gpu': gpu, 'pid': os.getpid(),
+        'elapsed_s': round(elapsed, 6),
+        'images_per_s': round(args.steps * args.batch / elapsed, 1),
+        'producers': nprod,
+        'cpus': share,
+        'numa_local': plan['numa_local'],
+        'cpu_domain': [min(plan['domain']), max(plan['domain'])] if plan['domain'] else None,
+        'loader_frames_per_s': round(win['frames_per_s'], 1) if win else None,
+        'h2d_gbytes_per_s': round(win['h2d_gbytes_per_s'], 2) if win else None,
+    }
+    per_rank = [mine_info]
+    if world > 1:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine_info)
     if rank == 0:
         print(json.dumps({
             'metric': METRIC,
@@ -351,6 +426,14 @@ def main():
             'higher_is_better': True,
             'scaling': 'weak',
             'vs_baseline': round(value / BASELINE_IMAGES_PER_SEC, 3),
+            'producer': PRODUCER,
+            'baseline_note': BASELINE_NOTE,
+            'world_size_seen': world_seen,
+            'backend': (args.backend if world > 1 else None),
+            'allreduce_check': allreduce,
+            'rank_time_s': {'min': round(min(r['elapsed_s'] for r in per_rank), 6),
+                            'max': round(max(r['elapsed_s'] for r in per_rank), 6)},
+            'per_rank': per_rank,
             'dtype': 'bf16' if amp else 'fp32',
             'data': 'synthetic (headless C++ Cube-scene producers, random rotations)',
             'config': {
@@ -376,17 +459,19 @@ def main():
             'sec_per_batch': round(tmax / args.steps, 6),
             'loader_stats': {k: stats.get(k) for k in ('frames', 'batches', 'bad', 'pool_fallbacks', 'direct_batches',
                                                        'launches', 'shm_frames', 'shm_torn', 'tiled_frames')},
-            # device time per image (H2D + decode, sampled launches) and the
-            # producers' share of the frames (whole run incl. warm-up)
-            'gpu_us_per_image': (round(metrics['gpu_us_per_image'], 3)
-                                 if metrics.get('gpu_us_per_image') is not None else None),
-            'frames_per_producer': metrics.get('frames_per_producer'),
-            # image bytes moved host -> device per second (tile16 moves only the changed tiles)
-            'h2d_gbytes_per_s': (round(metrics['h2d_gbytes_per_s'], 2)
-                                 if metrics.get('h2d_gbytes_per_s') is not None else None),
-            # host time blocked in the loader's next() per batch (whole run incl. warm-up)
-            'consumer_wait_ms_per_batch': (round(metrics['consumer_wait_s'] * 1e3 / max(1, metrics['batches']), 4)
-                                           if metrics.get('consumer_wait_s') is not None else None),
+            # rank 0's loader over the TIMED WINDOW only (snapshots at t0 / t1):
+            # device time per image (H2D + decode, sampled launches after the cold
+            # start), image bytes host -> device per second (tile16 moves only the
+            # changed tiles), per-producer rates and ring occupancy at both ends
+            'gpu_us_per_image': _r(win.get('gpu_us_per_image'), 3),
+            'h2d_gbytes_per_s': _r(win.get('h2d_gbytes_per_s'), 2),
+            'loader_frames_per_s': _r(win.get('frames_per_s'), 1),
+            'producer_frames_per_s': win.get('producer_frames_per_s'),
+            'ring_t0': win.get('ring_t0'),
+            'ring_t1': win.get('ring_t1'),
+            'consumer_wait_ms_per_batch': _r(win.get('consumer_wait_ms_per_batch'), 4),
+            # whole run incl. start-up (for comparison with the window)
+            'run_frames_per_producer': metrics.get('frames_per_producer'),
             'cpu': cpu,
         }), flush=True)
     if world > 1:
@@ -394,4 +479,4 @@ def main():
 
 
 if __name__ == '__main__':
-    main()
+    sys.exit(main() or 0)

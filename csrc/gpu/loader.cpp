@@ -236,6 +236,12 @@ LoaderStats StreamLoader::stats() {
   std::lock_guard<std::mutex> lk(mu_);
   LoaderStats s = stats_;
   s.pool_fallbacks = pool_ ? pool_->fallbacks() : 0;
+  s.ring_slots = s.ring_published = s.ring_held = 0;
+  for (const shm::Segment* g : seg_list_) {
+    s.ring_slots += g->nslots();
+    s.ring_published += g->count(shm::PUBLISHED);
+    s.ring_held += g->count(shm::HELD);
+  }
   return s;
 }
 
@@ -333,9 +339,10 @@ bool StreamLoader::process(zmtp::Message&& msg) {
     const bool has_codec = d.items.size() >= 9 && d.items[8]->kind == codec::Value::TUPLE;
     if (it.slot >= it.seg->nslots() || off < 0 || (!has_codec && size_t(off) + size_t(h) * w * c > it.seg->size()))
       return bad("_btshm descriptor out of range");
-    if (!it.seg->valid(it.slot, it.gen)) {
+    if (!it.seg->claim(it.slot, it.gen)) {
       // the producer reclaimed the slot (lease expired while this descriptor
-      // sat in a queue): its bytes are another frame's now -- drop it
+      // sat in a queue): its bytes are another frame's now -- drop it.  Once
+      // claimed (HELD) the slot is ours until reap() hands it back.
       std::lock_guard<std::mutex> lk(mu_);
       stats_.shm_stale++;
       return false;
@@ -359,6 +366,7 @@ bool StreamLoader::process(zmtp::Message&& msg) {
       it.ntiles = int(ntiles);
       try {
         KeyFrame& kf = key_frame(cd.items[1]->s, size_t(h) * w * c);
+        kf.refs++;
         it.key = &kf;
         it.key_host = kf.seg->slot(0);
       } catch (const std::exception& e) {
@@ -515,6 +523,10 @@ StreamLoader::MappedSegment& StreamLoader::segment(const std::string& name) {
   check(hipHostRegister(ms.seg->base(), ms.seg->size(), hipHostRegisterMapped), "hipHostRegister(shm)");
   if (hipHostGetDevicePointer(reinterpret_cast<void**>(&ms.dev_base), ms.seg->base(), 0) != hipSuccess)
     ms.dev_base = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    seg_list_.push_back(ms.seg.get());   // ring occupancy in stats()
+  }
   return segments_[name] = std::move(ms);
 }
 
@@ -537,14 +549,47 @@ void StreamLoader::reap(bool wait_all) {
       (void)hipEventDestroy(f.t0);
       (void)hipEventDestroy(f.t1);
     }
+    uint64_t torn = 0;
     for (auto& s : f.slots) {
-      if (!s.seg->valid(s.slot, s.gen)) {   // reclaimed by the producer under the DMA
-        std::lock_guard<std::mutex> lk(mu_);
-        stats_.shm_torn++;
-      }
+      if (!s.seg->valid(s.slot, s.gen)) torn++;   // a HELD slot taken back (dead-consumer lease)
       s.seg->release(s.slot, s.gen);
     }
+    if (torn) {
+      // the batch went out with another frame's pixels under its metadata:
+      // never deliver that silently (skip_bad only counts it)
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        stats_.shm_torn += torn;
+        if (!cfg_.skip_bad && error_.empty())
+          error_ = "StreamLoader: " + std::to_string(torn) +
+                   " shared-memory slot(s) were reclaimed by their producer while a batch read them";
+      }
+      cv_.notify_all();
+      if (!cfg_.skip_bad) stop_ = true;
+    }
+    retired_launch_ = f.launch_no;
     inflight_.pop_front();
+  }
+  evict_keys();
+}
+
+// Key frames a producer replaced (set_key_frame) are never referenced again:
+// free their HBM copies once no queued batch and no in-flight launch uses them.
+void StreamLoader::evict_keys() {
+  for (auto it = keys_.begin(); it != keys_.end();) {
+    KeyFrame& kf = it->second;
+    if (kf.refs == 0 && kf.last_launch <= retired_launch_ && launch_no_ - kf.last_launch > kKeyIdleLaunches) {
+      if (kf.dev) (void)hipFree(kf.dev);
+      for (void* d : kf.decoded)
+        if (d) (void)hipFree(d);
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        stats_.keys_evicted++;
+      }
+      it = keys_.erase(it);
+    } else {
+      ++it;
+    }
   }
 }
 
@@ -651,7 +696,9 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
   // sampled GPU timing: events bracket this launch's copies + kernel (the
   // stream has already passed the consumers' post events here)
   hipEvent_t t0 = nullptr, t1 = nullptr;
-  if (stats_.launches % kTimedEvery == 0 && hipEventCreate(&t0) == hipSuccess) {
+  const int64_t launch_no = ++launch_no_;
+  // skip the cold first launches (allocation, code-object load, page faults)
+  if (launch_no > kTimedSkip && launch_no % kTimedEvery == 0 && hipEventCreate(&t0) == hipSuccess) {
     if (hipEventCreate(&t1) != hipSuccess || hipEventRecord(t0, stream_) != hipSuccess) {
       (void)hipEventDestroy(t0);
       if (t1) (void)hipEventDestroy(t1);
@@ -722,6 +769,8 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
       tp.payload_off = int64_t(tiledelta::payload_offset(H_, W_));
       for (int i = 0; i < total; ++i) {
         const Item& it = *all[size_t(i)];
+        it.key->refs--;
+        it.key->last_launch = launch_no;
         tp.fills[i] = decoded_key(*it.key, cfg_.flip_all || it.flip, out_img_bytes);
         tp.tile_start[i + 1] = tp.tile_start[i] + it.ntiles;
       }
@@ -734,6 +783,7 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
   if (direct) check(hipEventRecord(copied, stream_), "hipEventRecord(copied)");
   if (t0) check(hipEventRecord(t1, stream_), "hipEventRecord(t1)");
   Inflight fl;
+  fl.launch_no = launch_no;
   fl.t0 = t0, fl.t1 = t1, fl.images = total;
   fl.frames.reserve(size_t(total));
   std::vector<ReadyBatch> done;

@@ -5,15 +5,19 @@
 // publish frames whose bytes are a function of (producer, sequence). They
 // hand descriptors (segment, slot, generation, sequence) to C consumer threads
 // through a queue that stands in for the ZMTP socket. Each consumer maps the
-// segments itself (Segment::open, as the GPU loader does), checks the slot is
-// still at the descriptor's generation, verifies every byte, re-checks the
-// generation (torn-read detection), and hands the slot back. A fraction of
-// descriptors is dropped without release (a consumer that went away). The
-// producers must then recover those slots through the lease and keep going.
+// segments itself (Segment::open, as the GPU loader does), claims the slot at
+// the descriptor's generation (PUBLISHED -> HELD; a failed claim is a stale
+// descriptor), verifies every byte, re-checks the generation (torn-read
+// detection), and hands the slot back. A fraction of descriptors is dropped
+// without release (a consumer that went away): the producers must recover
+// those slots through the lease and keep going. Another fraction is held for
+// twice the lease before it is read (a paused consumer): a held slot must
+// never be reclaimed under it.
 //
-// Exit 0 and "verified=N corrupt=0" when every frame that was still valid
-// after its read carried exactly the producer's bytes.
+// Exit 0 and "verified=N corrupt=0 torn=0" when every claimed frame carried
+// exactly the producer's bytes and none was taken back while held.
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -83,7 +87,7 @@ int main(int argc, char** argv) {
       qcv.notify_all();
     });
 
-  std::atomic<int> verified{0}, corrupt{0}, stale{0}, dropped{0};
+  std::atomic<int> verified{0}, corrupt{0}, stale{0}, dropped{0}, torn{0}, paused{0};
   for (int c = 0; c < C; ++c)
     threads.emplace_back([&, c] {
       std::map<int, std::unique_ptr<shm::Segment>> mapped;   // consumer-side mappings
@@ -104,9 +108,13 @@ int main(int argc, char** argv) {
           dropped++;
           continue;
         }
-        if (!m->valid(d.slot, d.gen)) {
+        if (!m->claim(d.slot, d.gen)) {   // reclaimed while queued: drop it
           stale++;
           continue;
+        }
+        if ((rnd >> 16) % 50 == 1) {      // ~2%: consumer pauses past the lease
+          paused++;
+          std::this_thread::sleep_for(std::chrono::milliseconds(2 * lease_ms));
         }
         const uint8_t* s = m->slot(d.slot);
         bool ok = true;
@@ -115,14 +123,15 @@ int main(int argc, char** argv) {
           if (ok) verified++;
           else corrupt++;
         } else {
-          stale++;
+          torn++;
         }
         m->release(d.slot, d.gen);
       }
     });
   for (auto& t : threads) t.join();
-  std::printf("verified=%d corrupt=%d stale=%d dropped=%d reclaimed=%llu\n", verified.load(), corrupt.load(),
-              stale.load(), dropped.load(), (unsigned long long)reclaimed.load());
+  std::printf("verified=%d corrupt=%d torn=%d stale=%d dropped=%d paused=%d reclaimed=%llu\n", verified.load(),
+              corrupt.load(), torn.load(), stale.load(), dropped.load(), paused.load(),
+              (unsigned long long)reclaimed.load());
   segs.clear();   // unlinks
-  return corrupt.load() == 0 && verified.load() > 0 ? 0 : 1;
+  return corrupt.load() == 0 && torn.load() == 0 && verified.load() > 0 ? 0 : 1;
 }

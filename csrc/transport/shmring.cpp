@@ -120,13 +120,20 @@ int Segment::acquire(long timeout_ms, const std::atomic<bool>* stop, long lease_
     const int64_t waited = now_us() - t0;
     if (timeout_ms >= 0 && waited >= timeout_ms * 1000) return -1;
     if (lease_ms > 0 && waited >= lease_ms * 1000) {
-      // reclaim the slot published longest ago (its message was dropped)
+      // reclaim the slot published longest ago (its message was dropped);
+      // held slots only after a much longer stall (their consumer died)
+      const bool take_held = waited >= lease_ms * 1000 * kHeldLeaseFactor;
       uint32_t best = n;
-      for (uint32_t i = 0; i < n; ++i)
-        if ((state(i) & 3u) == PUBLISHED && (best == n || published_at_[i] < published_at_[best])) best = i;
+      for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t st = state(i) & 3u;
+        if ((st == PUBLISHED || (take_held && st == HELD)) &&
+            (best == n || published_at_[i] < published_at_[best]))
+          best = i;
+      }
       if (best < n) {
         uint32_t w = state(best);
-        if ((w & 3u) == PUBLISHED &&
+        const uint32_t st = w & 3u;
+        if ((st == PUBLISHED || (take_held && st == HELD)) &&
             states()[best].compare_exchange_strong(w, (w & ~3u) | WRITING, std::memory_order_acq_rel)) {
           ++reclaimed_;
           next_ = (best + 1) % n;
@@ -148,23 +155,35 @@ uint32_t Segment::publish(uint32_t i) {
   return gen;
 }
 
+bool Segment::claim(uint32_t i, uint32_t gen) {
+  if (i >= hdr_->nslots) return false;
+  uint32_t expect = (gen << 2) | PUBLISHED;
+  return states()[i].compare_exchange_strong(expect, (gen << 2) | HELD, std::memory_order_acq_rel);
+}
+
 void Segment::release(uint32_t i, uint32_t gen) {
   if (i >= hdr_->nslots) return;
-  uint32_t expect = (gen << 2) | PUBLISHED;
+  uint32_t expect = (gen << 2) | HELD;
+  if (states()[i].compare_exchange_strong(expect, gen << 2 | FREE, std::memory_order_acq_rel)) return;
+  expect = (gen << 2) | PUBLISHED;   // never claimed (a dropped descriptor)
   states()[i].compare_exchange_strong(expect, gen << 2 | FREE, std::memory_order_acq_rel);
 }
 
 bool Segment::valid(uint32_t i, uint32_t gen) const {
-  return i < hdr_->nslots && state(i) == ((gen << 2) | PUBLISHED);
+  if (i >= hdr_->nslots) return false;
+  const uint32_t w = state(i);
+  return w == ((gen << 2) | PUBLISHED) || w == ((gen << 2) | HELD);
+}
+
+uint32_t Segment::count(SlotState st) const {
+  uint32_t c = 0;
+  for (uint32_t i = 0; i < hdr_->nslots; ++i) c += (state(i) & 3u) == uint32_t(st);
+  return c;
 }
 
 uint32_t Segment::state(uint32_t i) const { return states()[i].load(std::memory_order_acquire); }
 
-uint32_t Segment::free_count() const {
-  uint32_t c = 0;
-  for (uint32_t i = 0; i < hdr_->nslots; ++i) c += (state(i) & 3u) == FREE;
-  return c;
-}
+uint32_t Segment::free_count() const { return count(FREE); }
 
 }  // namespace shm
 }  // namespace btn

@@ -12,13 +12,18 @@
 //
 // Layout: [Header | word[nslots] (uint32) | pad to 4 KiB | slot 0 | slot 1 ...]
 // Slot word = generation << 2 | state.  States: FREE (0) -> WRITING (1,
-// producer) -> PUBLISHED (2, generation bumped) -> FREE (consumer, after its
-// copy completed, by CAS on the exact published word).  Descriptors carry the
-// generation, so a consumer can tell whether a slot was reclaimed under it.
-// Lease: a message dropped without being consumed (a consumer that closes
-// with frames still queued) would pin its slot forever; when the producer
-// has found no free slot for `lease_ms`, it reclaims the longest-published
-// slot (counted in reclaimed()).
+// producer) -> PUBLISHED (2, generation bumped) -> HELD (3, a consumer took
+// the descriptor: CAS on the exact published word) -> FREE (consumer, after
+// its last read of the slot completed).  Descriptors carry the generation, so
+// a consumer can tell whether a slot was reclaimed before it claimed it.
+// Lease: a message dropped without being consumed (a consumer that died with
+// frames still queued) would pin its slot forever; when the producer has
+// found no free slot for `lease_ms`, it reclaims the longest-PUBLISHED slot
+// (counted in reclaimed()).  A claimed (HELD) slot is never taken back while
+// its consumer may still read it -- a paused consumer (eval pass, checkpoint,
+// breakpoint) only stalls the producer, exactly like a full SNDHWM -- unless
+// the stall lasts kHeldLeaseFactor x lease_ms (a consumer that died holding
+// slots); the consumer then sees valid() fail and reports the batch torn.
 #pragma once
 
 #include <atomic>
@@ -31,7 +36,8 @@ namespace btn {
 namespace shm {
 
 constexpr uint64_t kMagic = 0x6d68735f7462746eull;   // "ntbt_shm"
-enum SlotState : uint32_t { FREE = 0, WRITING = 1, PUBLISHED = 2 };
+enum SlotState : uint32_t { FREE = 0, WRITING = 1, PUBLISHED = 2, HELD = 3 };
+constexpr long kHeldLeaseFactor = 20;
 
 struct Header {
   uint64_t magic;
@@ -61,10 +67,14 @@ class Segment {
   // returns -1 on timeout or when `stop` becomes true.
   int acquire(long timeout_ms, const std::atomic<bool>* stop = nullptr, long lease_ms = 30000);
   uint32_t publish(uint32_t i);        // returns the slot's new generation
-  // Consumer: hand a slot back (no-op if it was reclaimed meanwhile).
+  // Consumer: take the descriptor's slot (PUBLISHED -> HELD).  False when the
+  // producer reclaimed it first: the descriptor is stale and must be dropped.
+  bool claim(uint32_t i, uint32_t gen);
+  // Consumer: hand a slot back, claimed or not (no-op if it was reclaimed meanwhile).
   void release(uint32_t i, uint32_t gen);
-  // Consumer: is the slot still holding generation `gen`?
+  // Consumer: is the slot still holding generation `gen` (published or held)?
   bool valid(uint32_t i, uint32_t gen) const;
+  uint32_t count(SlotState st) const;   // slots currently in state `st`
   uint32_t state(uint32_t i) const;
   uint32_t free_count() const;
   uint64_t reclaimed() const { return reclaimed_; }

@@ -211,6 +211,51 @@ class DeviceLoader:
             'pool_fallbacks': s['pool_fallbacks'],
         }
 
+    def snapshot(self) -> dict:
+        """Raw cumulative pipeline counters at this instant (plus the wall
+        clock and the consumer's accumulated wait).  Two snapshots bracket a
+        timed region; :meth:`window` turns them into rates for that region
+        only -- unlike :meth:`metrics`, which spans the whole run including
+        start-up and warm-up (reference timing: benchmarks/benchmark.py:33-47
+        excludes the first batch the same way)."""
+        s = self._live.stats() if self._live is not None else dict(self.stats)
+        s = dict(s)
+        s['t'] = time.perf_counter()
+        s['consumer_wait_s'] = self._wait_s
+        return s
+
+    @staticmethod
+    def window(s0: dict, s1: dict) -> dict:
+        """Rates between two :meth:`snapshot` results (the timed window)."""
+        if not s0 or not s1 or 'frames' not in s0 or 'frames' not in s1:
+            return {}
+        dt = max(1e-9, s1['t'] - s0['t'])
+        d = {k: s1.get(k, 0) - s0.get(k, 0) for k in ('frames', 'batches', 'launches', 'image_bytes', 'timed_images',
+                                                      'timed_gpu_ms', 'shm_stale', 'shm_torn', 'bad')}
+        p0 = {int(k): int(v) for k, v in s0.get('frames_per_btid', {}).items()}
+        p1 = {int(k): int(v) for k, v in s1.get('frames_per_btid', {}).items()}
+        per = {k: round((v - p0.get(k, 0)) / dt, 1) for k, v in sorted(p1.items())}
+        out = {
+            'window_s': dt,
+            'frames': d['frames'],
+            'frames_per_s': d['frames'] / dt,
+            'h2d_gbytes_per_s': d['image_bytes'] / dt / 1e9,
+            'gpu_us_per_image': d['timed_gpu_ms'] * 1e3 / d['timed_images'] if d['timed_images'] else None,
+            'timed_images': d['timed_images'],
+            'images_per_launch': d['frames'] / d['launches'] if d['launches'] else None,
+            'producer_frames_per_s': per,
+            'consumer_wait_ms_per_batch': ((s1['consumer_wait_s'] - s0['consumer_wait_s']) * 1e3 / d['batches']
+                                           if d['batches'] else None),
+            'shm_stale': d['shm_stale'], 'shm_torn': d['shm_torn'], 'bad': d['bad'],
+        }
+        # producer ring occupancy (frames rendered and not yet handed back) at both ends:
+        # a window that starts on a full ring and ends on an empty one measured a drain
+        for tag, s in (('t0', s0), ('t1', s1)):
+            if 'ring_slots' in s:
+                out[f'ring_{tag}'] = {'published': s.get('ring_published', 0), 'held': s.get('ring_held', 0),
+                                      'slots': s['ring_slots']}
+        return out
+
     def _log_metrics(self):
         m = self.metrics()
         if m:

@@ -12,7 +12,7 @@ echo "== host: nproc=$(nproc) affinity=$(python -c 'import os;print(len(os.sched
 timeout -k 10 240 python -c "import sys; sys.path.insert(0,'.'); import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { echo build failed; tail -20 gpurun_out/build.log; exit 2; }
 for step in "$@"; do
   case "$step" in
-    tests) timeout -k 10 400 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -5 gpurun_out/pytest_gpu.log;;
+    tests) timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -5 gpurun_out/pytest_gpu.log;;
     smoke) timeout -k 10 200 python -c "import sys; sys.path.insert(0,'.'); import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?; tail -3 gpurun_out/smoke.log;;
     bench) timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1; rc=$?; tail -3 gpurun_out/bench.log;;
     bench:*) a="${step#bench:}"; timeout -k 10 300 python bench.py ${a//,/ } >> gpurun_out/bench_sweep.log 2>&1; rc=$?; tail -1 gpurun_out/bench_sweep.log;;
@@ -47,6 +47,9 @@ for step in "$@"; do
           mkdir -p gpurun_out/trace && find /tmp/rp_trace -name '*stats.csv' -exec cp {} gpurun_out/trace/ \;;;
     dist1) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29555 bench.py --gpus 1 --steps 500 --warmup 20 > gpurun_out/dist1.log 2>&1; rc=$?; grep '^{' gpurun_out/dist1.log;
            timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29556 bench.py --gpus 1 --steps 300 --warmup 20 --consumer disc >> gpurun_out/dist1.log 2>&1; rc=$?; grep '^{' gpurun_out/dist1.log | tail -1;;
+    sup2) timeout -k 10 300 python bench.py --gpus 2 --backend gloo --steps 1000 --warmup 20 > gpurun_out/sup2.log 2>&1; rc=$?; grep '^{' gpurun_out/sup2.log | cut -c1-600;;
+    sup2:*) a="${step#sup2:}"; timeout -k 10 300 python bench.py --gpus 2 --backend gloo ${a//,/ } >> gpurun_out/sup2.log 2>&1; rc=$?; grep '^{' gpurun_out/sup2.log | tail -1 | cut -c1-600;;
+    short) timeout -k 10 200 python bench.py --steps 20 --warmup 5 > gpurun_out/short.log 2>&1; rc=$?; grep '^{' gpurun_out/short.log;;
     dist2gloo) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29557 bench.py --gpus 2 --backend gloo --steps 1000 --warmup 20 > gpurun_out/dist2gloo.log 2>&1; rc=$?; grep '^{' gpurun_out/dist2gloo.log;;
     replay) timeout -k 10 200 python benchmarks/bench_replay.py > gpurun_out/replay.log 2>&1 && timeout -k 10 200 python benchmarks/bench_replay.py --batch 64 --steps 500 >> gpurun_out/replay.log 2>&1 && timeout -k 10 200 python benchmarks/bench_replay.py --graph >> gpurun_out/replay.log 2>&1 && timeout -k 10 200 python benchmarks/bench_replay.py --graph --batch 64 --steps 500 >> gpurun_out/replay.log 2>&1 && timeout -k 10 200 python benchmarks/bench_replay.py --fill producers --frames 2048 --batch 64 --steps 500 >> gpurun_out/replay.log 2>&1; rc=$?; cat gpurun_out/replay.log | grep '^{';;
     dpmc) timeout -k 10 120 rocprofv3 --pmc TCC_EA0_RDREQ_IO_32B_sum TCC_EA0_RDREQ_IO_CREDIT_STALL_sum TCC_EA0_RDREQ_DRAM_32B_sum --kernel-trace -d /tmp/rp_dpmc1 -o run --output-format csv -- python scripts/direct_pmc.py > gpurun_out/dpmc1.log 2>&1; rc=$?
