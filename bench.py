@@ -125,11 +125,15 @@ def parse_args(argv=None):
                          'Default: auto, but copy for the disc consumer -- its graphed training step runs faster '
                          'when the copy engines, not CUs waiting on PCIe reads, move the frames '
                          '(profiles/consumer_step.md)')
+    ap.add_argument('--copy-streams', type=int, default=2,
+                    help='copy path: HIP streams a batch\'s frame copies are spread over (several DMA engines)')
     ap.add_argument('--launch-depth', type=int, default=2,
                     help='direct-path decode launches queued before new batches coalesce into one launch')
     ap.add_argument('--backend', choices=['nccl', 'gloo'], default='nccl',
                     help='process-group backend (nccl = RCCL over xGMI; gloo only to rehearse several ranks on one GPU)')
     ap.add_argument('--start-port', type=int, default=0)
+    ap.add_argument('--force-pg', action='store_true',
+                    help='initialise a process group even for one rank (rehearses the collective code paths)')
     ap.add_argument('--dist', choices=['shard', 'pool', 'scatter'], default='shard',
                     help='shard: every rank owns its producers; pool: every rank launches producers and connects '
                          'to all of them (PUSH round-robin across GPUs); scatter: rank 0 receives world*B per step '
@@ -194,7 +198,15 @@ def main(argv=None):
     torch.cuda.set_device(gpu)
     device = torch.device('cuda', gpu)
     world_seen, allreduce = 1, None
-    if world > 1:
+    if world == 1 and args.force_pg:
+        # a 1-rank process group: rehearses the collective path (e.g. RCCL
+        # all-reduce captured in the step graph) on a single GPU
+        from blendtorch.parallel.launch import free_port
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        os.environ.setdefault('MASTER_PORT', str(free_port()))
+        os.environ.setdefault('RANK', '0')
+        os.environ['WORLD_SIZE'] = '1'
+    if world > 1 or args.force_pg:
         if args.backend == 'nccl':
             dist.init_process_group('nccl', device_id=device)
         else:
@@ -216,10 +228,11 @@ def main(argv=None):
     # one producer renders ~14k frames/s on the MI355X host (profiles/render_sweep.md):
     # 4 saturate a GPU's PCIe link, 8 leave 2.5x headroom on a shared node
     nprod = args.producers or max(1, min(8, share - 3))
-    if args.dist == 'scatter':
-        # the root hosts every producer, spread across the whole node
-        plan = {'cpus': cpus[:budget] if pin else cpus, 'numa_local': False, 'domain': cpus}
-        nprod = nprod * world if rank == 0 else 0
+    if args.dist == 'scatter' and not args.producers:
+        # every frame crosses the ROOT's PCIe link (~42k RGBA frames/s, which 4-8
+        # producers saturate): 8 producers in total, launched NUMA-local on
+        # every rank, and the root connects to all of them
+        nprod = max(1, -(-8 // world))
     mine = plan['cpus']
     if pin:
         affinity = [[mine[i % len(mine)]] for i in range(nprod)]
@@ -260,9 +273,12 @@ def main(argv=None):
             torch.backends.cudnn.benchmark = True   # MIOpen find: best conv kernels for these fixed shapes
         from blendtorch.models import Discriminator
         model = Discriminator(nc=3, ndf=32, adaptive=True).to(device).to(memory_format=torch.channels_last)
-        if world > 1:
-            model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[gpu])
-        use_graph = args.graph == 'on' or (args.graph == 'auto' and world == 1)
+        if dist.is_initialized():
+            # data parallel: identical initial weights on every rank; gradients are
+            # averaged inside the (captured) step, see CapturedStep
+            for p_ in model.state_dict().values():
+                dist.broadcast(p_, 0)
+        use_graph = args.graph == 'on' or (args.graph == 'auto' and (world == 1 or args.backend == 'nccl'))
         # fused Adam: one multi-tensor kernel for the whole update (0.95 -> 0.84 ms graphed step,
         # profiles/consumer_step.md); capturable keeps its step counters on the GPU for the graph
         opt = torch.optim.Adam(model.parameters(), lr=2e-4, capturable=use_graph, fused=True)
@@ -279,16 +295,20 @@ def main(argv=None):
             bl = es.enter_context(btt.BlenderLauncher(**launch))
             per_step = args.batch * (world if args.dist == 'scatter' else 1)
             addrs = bl.launch_info.addresses['DATA']
-            if args.dist == 'pool':
+            if args.dist in ('pool', 'scatter'):
                 from blendtorch.parallel import pool_addresses
                 addrs = pool_addresses(addrs)
-            dl = DeviceLoader(addrs, batch_size=per_step, decode=decode, device=device,
-                              max_items=total_batches * per_step, prefetch=6,
-                              io_threads=args.io_threads or None, timeoutms=60000, h2d=args.h2d,
-                              launch_depth=args.launch_depth)
+            if args.dist != 'scatter' or rank == 0:
+                # scatter: the root's loader lands raw u8 frames (alpha dropped when
+                # the decode does not read it) -- the bytes that cross xGMI
+                ldec = decode if args.dist != 'scatter' else DecodeConfig.raw(
+                    channels='rgba' if 3 in decode.cmap else 'rgb')
+                dl = DeviceLoader(addrs, batch_size=per_step, decode=ldec, device=device,
+                                  max_items=total_batches * per_step, prefetch=6,
+                                  io_threads=args.io_threads or None, timeoutms=60000, h2d=args.h2d,
+                                  launch_depth=args.launch_depth, copy_streams=args.copy_streams)
         if args.dist == 'scatter':
-            shp, dt = ((res_h, res_w, 3), torch.bfloat16) if amp else ((3, res_h, res_w), torch.float32)
-            it = iter(ScatterLoader(dl, args.batch, shp, dt, device, total_batches))
+            it = iter(ScatterLoader(dl, args.batch, decode, device, total_batches))
         else:
             it = iter(dl)
 
@@ -296,50 +316,32 @@ def main(argv=None):
             # NHWC bf16 storage -> NCHW view with channels-last strides; fp32 NCHW -> channels-last copy
             return img.permute(0, 3, 1, 2) if amp else img.contiguous(memory_format=torch.channels_last)
 
-        def train(x):
-            opt.zero_grad(set_to_none=True)
+        def loss_fn(m, x):
             if amp:
                 # no autocast weight cache: a captured graph must recast the live weights on every replay
                 with torch.autocast('cuda', dtype=torch.bfloat16, cache_enabled=not use_graph):
-                    out = model(x)
+                    out = m(x)
                 out = out.float()
             else:
-                out = model(x)
-            loss = crit(out, torch.ones_like(out))
-            loss.backward()
-            opt.step()
-            return loss
+                out = m(x)
+            return crit(out, torch.ones_like(out))
 
-        # whole-step HIP graph: the batch is copied into a static input buffer
-        # (one 15 MB device copy) and ~100 kernels replay as one launch, which
-        # takes the Python/autograd/MIOpen dispatch cost off the critical path
-        cap = {'graph': None, 'x': None, 'state': 'eager' if model is None or not use_graph else 'pending'}
+        # whole-step HIP graph (forward, backward, gradient all-reduce over RCCL
+        # when world > 1, fused Adam): the batch is copied into a static input
+        # buffer and ~100 kernels replay as one launch, which takes the Python /
+        # autograd / MIOpen dispatch cost off the critical path
+        # (blendtorch/parallel/step.py; DDP's host-side reducer cannot be captured)
+        stepper = None
+        if model is not None:
+            from blendtorch.parallel.step import CapturedStep
+            stepper = CapturedStep(model, opt, loss_fn, graph=use_graph,
+                                   allreduce='always' if args.force_pg else dist.is_initialized())
 
         def graphed(x):
-            if cap['state'] == 'pending':
-                cap['x'] = torch.empty_like(x)          # same (channels-last) strides as every batch
-                cap['x'].copy_(x)
-                side = torch.cuda.Stream()
-                side.wait_stream(torch.cuda.current_stream())
-                with torch.cuda.stream(side):           # eager warm-up: MIOpen find, allocator, Adam state
-                    for _ in range(3):
-                        train(cap['x'])
-                torch.cuda.current_stream().wait_stream(side)
-                g = torch.cuda.CUDAGraph()
-                try:
-                    opt.zero_grad(set_to_none=True)
-                    with torch.cuda.graph(g):
-                        train(cap['x'])
-                    cap['graph'], cap['state'] = g, 'graph'
-                except RuntimeError as e:              # keep the run alive; the JSON says which mode ran
-                    print(f'[bench] HIP graph capture failed, eager steps: {e}', file=sys.stderr, flush=True)
-                    cap['state'] = 'eager'
-                return
-            if cap['state'] == 'graph':
-                cap['x'].copy_(x)
-                cap['graph'].replay()
-            else:
-                train(x)
+            stepper(x)
+            if stepper.error:
+                print(f'[bench] HIP graph capture failed, eager steps: {stepper.error}', file=sys.stderr, flush=True)
+                stepper.error = None
 
         def step():
             b = next(it)
@@ -389,7 +391,7 @@ def main(argv=None):
             it.close()      # stops the native loader and publishes its stats
         stats = dict(dl.stats) if dl is not None else {}
         metrics = dl.metrics() if dl is not None else {}
-        if world > 1 and args.dist == 'pool':
+        if world > 1 and args.dist in ('pool', 'scatter'):
             dist.barrier()   # other ranks may still be drawing on this rank's producers
 
     win = DeviceLoader.window(snap0, snap1)
@@ -441,7 +443,7 @@ def main(argv=None):
                 'global_batch': args.batch * world,
                 'seq_len': None,
                 'parallelism': f'dp{world}' + ('' if args.dist == 'shard' else '-' + args.dist),
-                'producers_per_gpu': nprod // (world if args.dist == 'scatter' else 1),
+                'producers_per_gpu': nprod,
                 'cpus_per_gpu': share,
                 'numa_local': plan['numa_local'],
                 'decode': ('rgba->rgb, gamma 2.2, /255, bf16 NHWC (gfx950 kernel)' if amp else
@@ -452,8 +454,10 @@ def main(argv=None):
                 'shm_slots': shm_slots,
                 'h2d': args.h2d,
                 'launch_depth': args.launch_depth,
+                'copy_streams': args.copy_streams if args.h2d == 'copy' else None,
                 'codec': args.codec if shm_slots else 'none',
-                'consumer_step': cap['state'] if model is not None else None,
+                'consumer_step': stepper.state if stepper is not None else None,
+                'consumer_collectives_per_step': stepper.collectives if stepper is not None else None,
             },
             'sec_per_image': round(tmax / images, 7),
             'sec_per_batch': round(tmax / args.steps, 6),
@@ -474,7 +478,7 @@ def main(argv=None):
             'run_frames_per_producer': metrics.get('frames_per_producer'),
             'cpu': cpu,
         }), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

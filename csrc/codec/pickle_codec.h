@@ -74,6 +74,13 @@ struct Value {
   char byteorder = '=';           // DTYPE
   bool np_scalar = false;         // INT/FLOAT/BOOL decoded from a numpy scalar
   bool bytearray = false;         // BYTES that were a bytearray (protocol 5)
+  // BYTES / NDARRAY whose payload is not a byte range of the frame (protocol
+  // 2 writes bytes as _codecs.encode(latin-1 text)): the decoded bytes live
+  // here and `off` is relative to them
+  std::shared_ptr<const Bytes> owned;
+
+  // payload start: inside the frame (`base`) or in `owned`
+  const uint8_t* ptr(const uint8_t* base) const { return owned ? owned->data() + off : base + off; }
 
   const Value* get(const std::string& key) const;   // DICT lookup by str key
   int64_t numel() const;

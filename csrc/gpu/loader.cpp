@@ -25,7 +25,7 @@ double now_ms() {
 // Remove the image entry from the dict and shift every payload offset that
 // lies behind the cut so the tree indexes the compacted metadata bytes.
 void shift_offsets(codec::Value& v, size_t cut, size_t len) {
-  if (v.kind == codec::Value::BYTES || v.kind == codec::Value::NDARRAY || v.np_scalar) {
+  if ((v.kind == codec::Value::BYTES || v.kind == codec::Value::NDARRAY || v.np_scalar) && !v.owned) {
     if (v.off >= cut + len) v.off -= len;
   }
   for (auto& c : v.items)
@@ -188,16 +188,27 @@ void StreamLoader::stop() {
   stop_ = true;
   cv_.notify_all();
   if (worker_.joinable()) worker_.join();
+  drain_sockets();
   for (auto& s : socks_) s->close(0);
   socks_.clear();
   ctxs_.clear();   // joins IO threads; queued frames are released
   DeviceGuard g(cfg_.device);
+  for (auto cs : copy_streams_) {
+    (void)hipStreamSynchronize(cs);
+    (void)hipStreamDestroy(cs);
+  }
+  copy_streams_.clear();
+  for (auto ev : copy_done_) (void)hipEventDestroy(ev);
+  copy_done_.clear();
   if (stream_) {
     (void)hipStreamSynchronize(stream_);
     reap(true);                            // drop pinned refs of finished copies
     (void)hipStreamDestroy(stream_);
     stream_ = nullptr;
   }
+  for (auto ev : stage_free_)
+    if (ev) (void)hipEventDestroy(ev);
+  stage_free_.clear();
   for (auto& it : cur_)
     if (it.seg) it.seg->release(it.slot, it.gen);
   cur_.clear();
@@ -218,6 +229,7 @@ void StreamLoader::stop() {
   keys_.clear();
   {
     std::lock_guard<std::mutex> lk(mu_);
+    seg_list_.clear();
     for (auto& p : posted_) (void)hipEventDestroy(p.ready);
     posted_.clear();
     for (auto& r : ready_)
@@ -230,6 +242,40 @@ void StreamLoader::stop() {
   if (d_mat_) (void)hipFree(d_mat_);
   d_lut_ = d_mat_ = nullptr;
   pool_.reset();
+}
+
+// Descriptors still queued in the sockets when the loader stops would pin
+// their producers' ring slots until the lease reclaims them: hand them back
+// (the reference's PULL socket simply drops queued messages on close).
+void StreamLoader::drain_sockets() {
+  for (auto& s : socks_) {
+    for (int n = 0; n < 4096; ++n) {
+      zmtp::Message m;
+      try {
+        m = s->recv(zmtp::DONTWAIT);
+      } catch (const zmtp::Error&) {
+        break;
+      }
+      if (m.size() != 1) continue;
+      try {
+        codec::VPtr root = codec::parse(m[0].data(), m[0].size);
+        if (!root || root->kind != codec::Value::DICT) continue;
+        const codec::Value* d = root->get("_btshm");
+        if (!d || d->kind != codec::Value::TUPLE || d->items.size() < 8 || d->items[0]->kind != codec::Value::STR)
+          continue;
+        const uint32_t slot = uint32_t(d->items[1]->i), gen = uint32_t(d->items[7]->i);
+        auto it = segments_.find(d->items[0]->s);
+        if (it != segments_.end()) {
+          it->second.seg->release(slot, gen);
+        } else {
+          std::unique_ptr<shm::Segment> seg(shm::Segment::open(d->items[0]->s));
+          seg->release(slot, gen);
+        }
+      } catch (const std::exception&) {
+        continue;   // producer gone / not a descriptor: nothing to hand back
+      }
+    }
+  }
 }
 
 LoaderStats StreamLoader::stats() {
@@ -248,6 +294,14 @@ LoaderStats StreamLoader::stats() {
 void StreamLoader::run() {
   check(hipSetDevice(cfg_.device), "hipSetDevice");
   check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+  for (int k = 0; cfg_.copy_streams > 1 && k < std::min(cfg_.copy_streams, 4); ++k) {
+    hipStream_t cs;
+    hipEvent_t ev;
+    check(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "hipStreamCreate(copy)");
+    check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate(copy)");
+    copy_streams_.push_back(cs);
+    copy_done_.push_back(ev);
+  }
   std::vector<std::pair<zmtp::Socket*, int>> items;
   for (auto& s : socks_) items.emplace_back(s.get(), zmtp::POLLIN);
   const auto intr = [this] { return stop_.load(); };
@@ -387,10 +441,17 @@ bool StreamLoader::process(zmtp::Message&& msg) {
     } else {
       return bad("image must be HxW or HxWxC");
     }
-    it.src = data + img.off;
-    if (pool_ && it.frame.buf && it.frame.buf->pinned && it.frame.buf->owner == pool_.get())
-      it.dsrc = pool_->device_ptr(it.src);
-    cut = img.off, len = img.len;
+    if (img.owned) {
+      // protocol-2 frame: the pixels were decoded out of latin-1 text, they
+      // are not a byte range of the frame -- take them by the copy path
+      it.expanded.assign(img.owned->begin() + long(img.off), img.owned->begin() + long(img.off + img.len));
+      it.src = it.expanded.data();
+    } else {
+      it.src = data + img.off;
+      if (pool_ && it.frame.buf && it.frame.buf->pinned && it.frame.buf->owner == pool_.get())
+        it.dsrc = pool_->device_ptr(it.src);
+      cut = img.off, len = img.len;
+    }
   }
   if (c < 1 || c > 4) return bad("image channels must be 1..4");
   if (const codec::Value* o = root->get("origin"))
@@ -511,6 +572,8 @@ void StreamLoader::materialize(Item& it) {
   it.src = it.expanded.data();
   it.dsrc = nullptr;
   it.tiled = false;
+  if (it.key) it.key->refs--;   // rebuilt on the host: the HBM key is not read for it
+  it.key = nullptr;
 }
 
 StreamLoader::MappedSegment& StreamLoader::segment(const std::string& name) {
@@ -706,12 +769,30 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
     }
   }
   uint8_t* stage = nullptr;
+  const size_t stage_idx = size_t(batch_index_) % staging_.size();
   if (!direct) {   // copy path: exactly one batch per launch
-    stage = staging_[size_t(batch_index_) % staging_.size()];
-    for (int i = 0; i < total; ++i)
-      check(hipMemcpyAsync(stage + size_t(i) * img_bytes_, all[size_t(i)]->src, img_bytes_, hipMemcpyHostToDevice,
-                           stream_),
-            "hipMemcpyAsync(H2D)");
+    stage = staging_[stage_idx];
+    if (copy_streams_.empty()) {
+      for (int i = 0; i < total; ++i)
+        check(hipMemcpyAsync(stage + size_t(i) * img_bytes_, all[size_t(i)]->src, img_bytes_, hipMemcpyHostToDevice,
+                             stream_),
+              "hipMemcpyAsync(H2D)");
+    } else {
+      // frames round-robin over the copy streams (separate hardware queues,
+      // so several DMA engines read host memory at once); each copy stream
+      // first waits until the kernel that last read this staging buffer is done
+      const size_t K = copy_streams_.size();
+      hipEvent_t freed = stage_idx < stage_free_.size() ? stage_free_[stage_idx] : nullptr;
+      for (size_t k = 0; k < K && k < size_t(total); ++k) {
+        if (freed) check(hipStreamWaitEvent(copy_streams_[k], freed, 0), "hipStreamWaitEvent(stage)");
+        for (int i = int(k); i < total; i += int(K))
+          check(hipMemcpyAsync(stage + size_t(i) * img_bytes_, all[size_t(i)]->src, img_bytes_,
+                               hipMemcpyHostToDevice, copy_streams_[k]),
+                "hipMemcpyAsync(H2D)");
+        check(hipEventRecord(copy_done_[k], copy_streams_[k]), "hipEventRecord(copy)");
+        check(hipStreamWaitEvent(stream_, copy_done_[k], 0), "hipStreamWaitEvent(copy)");
+      }
+    }
   }
   // `copied` marks the last device read of the host slots: after the copies,
   // or (direct) after the kernel that reads them
@@ -781,6 +862,12 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
   }
   check(e, "decode kernel launch");
   if (direct) check(hipEventRecord(copied, stream_), "hipEventRecord(copied)");
+  if (!direct && !copy_streams_.empty()) {
+    if (stage_free_.size() < staging_.size()) stage_free_.resize(staging_.size(), nullptr);
+    if (!stage_free_[stage_idx])
+      check(hipEventCreateWithFlags(&stage_free_[stage_idx], hipEventDisableTiming), "hipEventCreate(stage)");
+    check(hipEventRecord(stage_free_[stage_idx], stream_), "hipEventRecord(stage)");
+  }
   if (t0) check(hipEventRecord(t1, stream_), "hipEventRecord(t1)");
   Inflight fl;
   fl.launch_no = launch_no;

@@ -105,6 +105,10 @@ struct LoaderConfig {
   // ~45 GB/s vs ~35 GB/s for per-frame DMA copies + decode on MI355X);
   // false: always DMA into the device staging ring first.
   bool direct = true;
+  // Copy path: a batch's frames are spread over this many HIP streams so
+  // several DMA engines pull from host memory concurrently (1: all on the
+  // loader stream).  Bounded by the runtime's hardware queues.
+  int copy_streams = 2;
   // Direct-path launches queued on the loader stream before new batches wait
   // and coalesce into one launch (0: always hold until 64 images or stream end).
   int launch_depth = 2;
@@ -146,6 +150,10 @@ struct LoaderStats {
   // copies + decode kernel): per-image device cost without timing every launch
   uint64_t timed_launches = 0, timed_images = 0;
   double timed_gpu_ms = 0;
+  uint64_t keys_evicted = 0;               // replaced tile16 key frames freed from HBM
+  // producer rings at the time of stats(): slots, frames published and not
+  // yet claimed (waiting in queues), frames claimed by this loader
+  uint64_t ring_slots = 0, ring_published = 0, ring_held = 0;
   std::map<int64_t, uint64_t> frames_per_btid;   // provenance: frames per producer id
 };
 
@@ -205,6 +213,8 @@ class StreamLoader {
   void flush_pending(bool force);
   void launch_group(std::vector<Pending>& group);
   void reap(bool wait_all = false);   // release pinned slots of completed H2D copies
+  void evict_keys();
+  void drain_sockets();               // stop(): hand back ring slots of still-queued descriptors
 
   LoaderConfig cfg_;
   std::vector<std::unique_ptr<zmtp::Context>> ctxs_;
@@ -231,8 +241,16 @@ class StreamLoader {
   std::vector<Item> cur_;
   std::deque<Pending> pending_;
   int pending_images_ = 0;
-  static constexpr int kTimedEvery = 16;
+  static constexpr int kTimedEvery = 4;
+  static constexpr int kTimedSkip = 8;         // cold launches never sampled
+  static constexpr int64_t kKeyIdleLaunches = 64;
+  int64_t launch_no_ = 0, retired_launch_ = 0;
+  std::vector<hipStream_t> copy_streams_;      // copy path fan-out (cfg_.copy_streams > 1)
+  std::vector<hipEvent_t> copy_done_;          // one per copy stream, reused
+  std::vector<hipEvent_t> stage_free_;         // per staging buffer: last kernel reading it
+  std::vector<shm::Segment*> seg_list_;        // mapped rings, for stats() (guarded by mu_)
   struct Inflight {
+    int64_t launch_no = 0;
     hipEvent_t copied;
     hipEvent_t t0 = nullptr, t1 = nullptr;   // sampled launch timing (or null)
     int images = 0;
@@ -254,6 +272,8 @@ class StreamLoader {
     std::unique_ptr<shm::Segment> seg;
     uint8_t* dev = nullptr;          // HBM copy, made on first use
     void* decoded[2] = {nullptr, nullptr};   // decoded for this loader (upper-left, flipped)
+    int refs = 0;                    // items holding it that have not launched yet
+    int64_t last_launch = 0;         // last launch that read it
   };
   KeyFrame& key_frame(const std::string& name, size_t bytes);
   const void* decoded_key(KeyFrame& kf, bool flip, size_t out_img_bytes);

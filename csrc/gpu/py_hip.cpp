@@ -89,7 +89,7 @@ py::dict collate_meta(const std::vector<BatchMeta>& items) {
       py::array a{py::dtype(v0->dtype), shape};
       const size_t nb = v0->np_scalar ? v0->itemsize() : size_t(v0->numel()) * v0->itemsize();
       auto* dst = static_cast<uint8_t*>(a.mutable_data());
-      for (size_t i = 0; i < B; ++i) std::memcpy(dst + i * nb, items[i].bytes.data() + vals[i]->off, nb);
+      for (size_t i = 0; i < B; ++i) std::memcpy(dst + i * nb, vals[i]->ptr(items[i].bytes.data()), nb);
       col = a;
     } else {
       py::list l;
@@ -431,9 +431,10 @@ PYBIND11_MODULE(_hip, m) {
                        int io_threads, int device, int64_t max_batches, size_t max_frame_bytes, int pool_slots,
                        int staging_depth, bool skip_bad, int cout, std::vector<int> cmap, int flip_all,
                        int out_dtype, int layout, std::vector<float> lut, std::vector<float> matrix,
-                       std::vector<float> bias, bool direct, int launch_depth) {
+                       std::vector<float> bias, bool direct, int launch_depth, int copy_streams) {
              LoaderConfig c;
              c.direct = direct;
+             c.copy_streams = copy_streams;
              c.launch_depth = launch_depth;
              c.addresses = std::move(addresses);
              c.batch_size = batch_size;
@@ -461,7 +462,8 @@ PYBIND11_MODULE(_hip, m) {
            py::arg("io_threads"), py::arg("device"), py::arg("max_batches"), py::arg("max_frame_bytes"),
            py::arg("pool_slots"), py::arg("staging_depth"), py::arg("skip_bad"), py::arg("cout"), py::arg("cmap"),
            py::arg("flip_all"), py::arg("out_dtype"), py::arg("layout"), py::arg("lut"), py::arg("matrix"),
-           py::arg("bias"), py::arg("direct") = true, py::arg("launch_depth") = 2)
+           py::arg("bias"), py::arg("direct") = true, py::arg("launch_depth") = 2,
+           py::arg("copy_streams") = 2)
       .def("start", &StreamLoader::start)
       .def("wait_shape",
            [](StreamLoader& l, long timeout_ms) -> py::object {
@@ -533,6 +535,10 @@ PYBIND11_MODULE(_hip, m) {
         d["timed_launches"] = s.timed_launches;
         d["timed_images"] = s.timed_images;
         d["timed_gpu_ms"] = s.timed_gpu_ms;
+        d["keys_evicted"] = s.keys_evicted;
+        d["ring_slots"] = s.ring_slots;
+        d["ring_published"] = s.ring_published;
+        d["ring_held"] = s.ring_held;
         py::dict per;
         for (const auto& kv : s.frames_per_btid) per[py::int_(kv.first)] = kv.second;
         d["frames_per_btid"] = per;

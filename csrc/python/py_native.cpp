@@ -1,6 +1,7 @@
 // pybind11 bindings for the CPU-side native runtime: the ZMTP transport and
 // the pickle codec.  Built as `blendtorch/_native*.so` (no HIP dependency, so
 // it runs in Blender-side producer processes and CPU-only tests as well).
+#include <atomic>
 #include <pybind11/eval.h>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
@@ -192,6 +193,20 @@ class NativeError(Exception):
   m.def("ready_command", [](int t, const std::string& id) { return py::bytes(zmtp::ready_command(t, id)); },
         py::arg("socket_type"), py::arg("identity") = "");
   m.def("socket_types_compatible", &zmtp::socket_types_compatible);
+
+  // ---- shared-memory slot words ----
+  // Atomic compare-and-swap on word `i` of a writable uint32 array mapped
+  // over a ring segment (csrc/transport/shmring.h states): the Python
+  // consumer claims / releases slots with the same atomics as the C++ side.
+  m.def("slot_cas", [](py::array words, size_t i, uint32_t expected, uint32_t desired) {
+    // no conversion: a cast copy would make the CAS act on a temporary
+    if (!words.dtype().is(py::dtype::of<uint32_t>()) || !(words.flags() & py::array::c_style))
+      throw py::type_error("slot_cas needs a C-contiguous uint32 array over the segment");
+    auto info = words.request(true);
+    if (info.ndim != 1 || i >= size_t(info.shape[0])) throw py::index_error("slot index out of range");
+    auto* w = reinterpret_cast<std::atomic<uint32_t>*>(static_cast<uint32_t*>(info.ptr) + i);
+    return w->compare_exchange_strong(expected, desired, std::memory_order_acq_rel);
+  });
 
   // ---- codec ----
   m.def("pickle_describe", [](py::buffer b) {
@@ -441,10 +456,10 @@ class NativeError(Exception):
                          size_t(d) < o->items.size())
                        val = num(o->items[size_t(d)].get(), 0.0);
                      else if (o && o->kind == codec::Value::NDARRAY && d < o->numel()) {
-                       if (o->dtype == "<f8") std::memcpy(&val, raw.data() + o->off + 8 * size_t(d), 8);
+                       if (o->dtype == "<f8") std::memcpy(&val, o->ptr(reinterpret_cast<const uint8_t*>(raw.data())) + 8 * size_t(d), 8);
                        else if (o->dtype == "<f4") {
                          float f;
-                         std::memcpy(&f, raw.data() + o->off + 4 * size_t(d), 4);
+                         std::memcpy(&f, o->ptr(reinterpret_cast<const uint8_t*>(raw.data())) + 4 * size_t(d), 4);
                          val = f;
                        }
                      } else if (o && d == 0)

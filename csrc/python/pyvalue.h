@@ -13,24 +13,31 @@ namespace pyconv {
 
 namespace py = pybind11;
 
+// Keeps a value's decoded (`owned`) payload alive for numpy views over it.
+inline py::object owned_keeper(const codec::Value& v) {
+  auto* keep = new std::shared_ptr<const codec::Bytes>(v.owned);
+  return py::capsule(keep, [](void* p) { delete static_cast<std::shared_ptr<const codec::Bytes>*>(p); });
+}
+
 inline py::object value_to_py(const codec::Value& v, const uint8_t* base, const py::object& owner) {
   using K = codec::Value;
+  const uint8_t* data = v.ptr(base);
   if (v.np_scalar) {
     // numpy scalar (e.g. np.float32): 0-d view, then index -> scalar copy
     py::array a(py::dtype(v.dtype), std::vector<py::ssize_t>{}, std::vector<py::ssize_t>{},
-                const_cast<uint8_t*>(base + v.off), owner);
+                const_cast<uint8_t*>(data), v.owned ? owned_keeper(v) : owner);
     return a[py::tuple()];
   }
   if (v.kind == K::BYTES && v.bytearray)
     return py::reinterpret_steal<py::object>(
-        PyByteArray_FromStringAndSize(reinterpret_cast<const char*>(base + v.off), py::ssize_t(v.len)));
+        PyByteArray_FromStringAndSize(reinterpret_cast<const char*>(data), py::ssize_t(v.len)));
   switch (v.kind) {
     case K::NONE: return py::none();
     case K::BOOL: return py::bool_(v.b);
     case K::INT: return py::int_(v.i);
     case K::FLOAT: return py::float_(v.f);
     case K::STR: return py::str(v.s);
-    case K::BYTES: return py::bytes(reinterpret_cast<const char*>(base + v.off), v.len);
+    case K::BYTES: return py::bytes(reinterpret_cast<const char*>(data), v.len);
     case K::LIST: {
       py::list l;
       for (auto& x : v.items) l.append(value_to_py(*x, base, owner));
@@ -69,7 +76,7 @@ inline py::object value_to_py(const codec::Value& v, const uint8_t* base, const 
         }
       }
       // zero-copy view; `owner` keeps the receive buffer alive
-      return py::array(dt, shape, strides, const_cast<uint8_t*>(base + v.off), owner);
+      return py::array(dt, shape, strides, const_cast<uint8_t*>(data), v.owned ? owned_keeper(v) : owner);
     }
     default: throw codec::Unsupported("value kind");
   }

@@ -12,6 +12,7 @@
 // --sndhwm N   --linger MS   --fps F (0 = unthrottled)   --socket NAME
 // --fault none|exit|stall|garbage --fault-after N   --rotation RX RY RZ   --verbose
 // --resolution WxH   --stamp (integrity tests: btid/seq in the first 16 image bytes)
+// --lease-ms N       shm ring lease (default 30000): unclaimed slots reclaimed after starving N ms
 // --shm N (render into an N-slot shared-memory ring, send descriptors only)
 // --codec tile16 (shm frames as key-frame deltas, csrc/codec/tiledelta.h)
 // --bench N (no sockets: render N frames into 8 rotating buffers, full vs
@@ -75,6 +76,7 @@ struct Args {
   double rot[3] = {0, 0, 0};
   int width = 0, height = 0;   // 0: the scene's resolution (640x480)
   bool stamp = false;          // integrity tests: (btid, seq) written into the first image row
+  long lease_ms = 30000;       // shm ring: reclaim unclaimed slots after starving this long (shmring.h)
   long long bench = 0;         // >0: offline render benchmark / incremental-render check
 };
 
@@ -128,6 +130,7 @@ Args parse(int argc, char** argv) {
     else if (k == "--fault-after") a.fault_after = std::stoll(need(i)), ++i;
     else if (k == "--verbose") a.verbose = true;
     else if (k == "--stamp") a.stamp = true;
+    else if (k == "--lease-ms") a.lease_ms = std::stol(need(i)), ++i;
     else if (k == "--shm") a.shm_slots = std::stoi(need(i)), ++i;
     else if (k == "--codec") a.codec = need(i), ++i;
     else if (k == "--bench") a.bench = std::stoll(need(i)), ++i;
@@ -319,7 +322,7 @@ int main(int argc, char** argv) {
 
     int slot = -1;
     if (seg) {
-      slot = seg->acquire(-1, &g_stop);   // blocks while every slot is with a consumer
+      slot = seg->acquire(-1, &g_stop, a.lease_ms);   // blocks while every slot is with a consumer
       if (slot < 0) break;
     }
     uint32_t gen = 0;

@@ -835,7 +835,13 @@ void Context::io_read(const std::shared_ptr<Pipe>& p) {
           } else {
             sz = h[1];
           }
-          if (h[0] & F_COMMAND) need += sz;   // commands must be whole in rbuf
+          if (h[0] & F_COMMAND) {             // commands must be whole in rbuf
+            if (sz > (64u << 20)) {            // (and a 64-bit size must not wrap `need`)
+              close_pipe(p, true);
+              return;
+            }
+            need += sz;
+          }
         }
       } else {
         need = 1;
@@ -896,6 +902,12 @@ void Context::io_read(const std::shared_ptr<Pipe>& p) {
       }
       if (flags & F_COMMAND) {
         const uint8_t* c = h + hl;
+        // a command is name-length byte + name + body: reject frames too short
+        // for their own name before reading any of it (a peer may send sz 0)
+        if (sz < 1 || size_t(c[0]) > sz - 1) {
+          close_pipe(p, false);
+          return;
+        }
         size_t nl = c[0];
         std::string name(reinterpret_cast<const char*>(c + 1), std::min<size_t>(nl, sz - 1));
         const uint8_t* body = c + 1 + nl;
@@ -945,6 +957,10 @@ void Context::io_read(const std::shared_ptr<Pipe>& p) {
       }
       if (p->state != Pipe::ACTIVE) {
         close_pipe(p, false);
+        return;
+      }
+      if (sz > (uint64_t(2) << 30)) {   // > 2 GiB: a corrupt or hostile length, not a frame
+        close_pipe(p, true);
         return;
       }
       bool more = flags & F_MORE;

@@ -13,7 +13,9 @@ Reference: pkg_pytorch/blendtorch/btt/dataset.py:14-153.
   one / all recordings matching a prefix (shuffle-capable).
 
 Same-host producers may send images through shared memory (descriptor key
-``_btshm``); they are materialised transparently.  Frames are decoded with
+``_btshm``); they are materialised transparently.  A descriptor whose slot
+the producer reclaimed while it sat in a queue (lease) is dropped, never
+delivered with another frame's pixels.  Frames are decoded with
 the native zero-copy unpickler (image arrays are
 views over the received buffer); for device-resident batches see
 :class:`blendtorch.btt.gpu.DeviceLoader`.
@@ -92,7 +94,8 @@ class RemoteIterableDataset(tud.IterableDataset):
                 if self.record_path_prefix is not None:
                     rec = es.enter_context(FileRecorder(
                         FileRecorder.filename(self.record_path_prefix, worker_id), self.max_items))
-                for _ in range(self.max_items // num_workers):
+                n = 0
+                while n < self.max_items // num_workers:
                     ready = dict(poller.poll(self.timeoutms))
                     assert socket in ready, 'No response within timeout interval.'
                     if rec is not None:
@@ -100,11 +103,16 @@ class RemoteIterableDataset(tud.IterableDataset):
                         obj = pickle.loads(data)
                         if shm.KEY in obj:   # record the materialised frame
                             obj = shm.resolve(obj)
+                            if obj is None:  # stale descriptor: slot reclaimed while queued
+                                continue
                             rec.save(obj, is_pickled=False)
                         else:
                             rec.save(data, is_pickled=True)
                     else:
                         obj = shm.resolve(socket.recv_pyobj())
+                        if obj is None:
+                            continue
+                    n += 1
                     yield self._item(obj)
                     del obj
         finally:

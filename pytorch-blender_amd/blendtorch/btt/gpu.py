@@ -81,6 +81,10 @@ class DeviceLoader:
         together in one launch (fewer kernel ramp-up/tail phases when the GPU
         side is the bottleneck).  0: hold batches until 64 images are pending
         or the stream ends (tests / maximal coalescing).
+    copy_streams: int
+        Copy path (``h2d='copy'`` or frames that are not device-visible): the
+        frames of a batch are spread over this many HIP streams so several
+        DMA engines pull from host memory concurrently (1: one stream).
     log_every: float, optional
         Log :meth:`metrics` on the ``'blendtorch'`` logger every that many
         seconds while iterating.
@@ -90,11 +94,12 @@ class DeviceLoader:
                  device=None, max_items: Optional[int] = None, timeoutms: int = DEFAULT_TIMEOUTMS,
                  rcvhwm: int = 10, prefetch: int = 4, io_threads: Optional[int] = None, image_key: str = 'image',
                  skip_bad: bool = False, meta_to_device: bool = False, staging_depth: int = 3, h2d: str = 'auto',
-                 launch_depth: int = 2, log_every: Optional[float] = None):
+                 launch_depth: int = 2, log_every: Optional[float] = None, copy_streams: int = 2):
         if h2d not in ('auto', 'copy'):
             raise ValueError("h2d must be 'auto' or 'copy'")
         self.h2d = h2d
         self.launch_depth = int(launch_depth)
+        self.copy_streams = max(1, min(4, int(copy_streams)))
         if isinstance(addresses, str):
             addresses = [addresses]
         self.addresses = list(addresses)
@@ -152,7 +157,7 @@ class DeviceLoader:
             self.addresses, self.batch_size, self.image_key, self.rcvhwm, self.io_threads, self.device.index,
             max_batches, 0, 0, self.staging_depth, self.skip_bad, cfg.cout, list(cfg.cmap) + [0] * (4 - len(cfg.cmap)),
             int(cfg.flip), ops.OUT_DTYPES[cfg.dtype], ops.LAYOUTS[cfg.layout], lut, matrix, bias,
-            self.h2d == 'auto', self.launch_depth)
+            self.h2d == 'auto', self.launch_depth, self.copy_streams)
 
     def _post(self, loader, stream):
         out = torch.empty(self.decode.out_shape(self.batch_size, *self.shape[:2]), dtype=self.decode.torch_dtype(),

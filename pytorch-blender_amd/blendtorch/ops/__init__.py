@@ -402,8 +402,20 @@ def _dt(x):
     return _DT_CODES.get(x.dtype)
 
 
+# Host-side count of launches of the consumer-model kernels, by kernel name.
+# Tests assert the fused gfx950 path ran on the bench shapes instead of the
+# PyTorch fallback the modules take for unsupported inputs (a captured HIP
+# graph counts once, at capture).
+KERNEL_CALLS = {}
+
+
+def _count(name):
+    KERNEL_CALLS[name] = KERNEL_CALLS.get(name, 0) + 1
+
+
 def _pool_launch(name, src, dst, N, H, W, C, OH, OW):
     ext = hip_ext()
+    _count(name)
     getattr(ext, name)(src.data_ptr(), dst.data_ptr(), N, H, W, C, OH, OW, _dt(src),
                        _stream(src.device))
 
@@ -509,6 +521,7 @@ def _bn_function():
             y = torch.empty_like(xs)
             rm = running_mean.data_ptr() if running_mean is not None else 0
             rv = running_var.data_ptr() if running_var is not None else 0
+            _count('bn_forward')
             ext.bn_forward(xs.data_ptr(), y.data_ptr(), M, C, dt, part.data_ptr(), float(eps), float(momentum),
                            mean.data_ptr(), invstd.data_ptr(), rm, rv, w.data_ptr(), b.data_ptr(), float(slope),
                            _stream(x.device))
@@ -528,6 +541,7 @@ def _bn_function():
             dw = torch.empty(C, dtype=torch.float32, device=xs.device)
             db = torch.empty_like(dw)
             part = torch.empty(ext.bn_partial_floats(M, C, dt), dtype=torch.float32, device=xs.device)
+            _count('bn_backward')
             ext.bn_backward(xs.data_ptr(), gys.data_ptr(), gx.data_ptr(), M, C, dt, part.data_ptr(), mean.data_ptr(),
                             invstd.data_ptr(), w.data_ptr(), b.data_ptr(), dw.data_ptr(), db.data_ptr(), ctx.slope,
                             _stream(xs.device))

@@ -13,10 +13,11 @@ MI355X node every GPU is a rank (``torch.distributed`` with backend
   but connects to all of them; PUSH round-robin balances frames across the
   GPUs, which is the reference's fan-out semantics at node scale;
 * **scatter mode** (:class:`ScatterLoader`): a root rank receives
-  ``world x B`` frames and hands each rank its B-image shard with one
-  grouped send/recv round (``batch_isend_irecv``: the root drives all its
-  xGMI links concurrently -- point-to-point links, so a ring would be the
-  wrong shape here), metadata follows as one small object scatter.
+  ``world x B`` undecoded u8 frames and hands each rank its B-image shard
+  plus packed metadata bytes in one grouped send/recv round
+  (``batch_isend_irecv``: the root drives all its xGMI links concurrently --
+  point-to-point links, so a ring would be the wrong shape here); each rank
+  decodes its own shard.
 
 Plus the small collectives the examples need: :func:`broadcast_tensor`
 (duplex simulation parameters), :func:`all_gather_stats` (per-rank
@@ -35,7 +36,8 @@ from .topology import parse_cpulist, plan_rank_cpus  # noqa: E402
 
 __all__ = ['init_distributed', 'rank_world', 'shard_addresses', 'pool_addresses', 'partition_cpus', 'plan_rank_cpus',
            'parse_cpulist',
-           'scatter_batch', 'broadcast_tensor', 'all_gather_stats', 'ScatterLoader', 'barrier']
+           'scatter_batch', 'broadcast_tensor', 'all_gather_stats', 'ScatterLoader', 'barrier', 'pack_meta',
+           'unpack_meta']
 
 
 def rank_world():
@@ -163,51 +165,184 @@ def all_gather_stats(stats: Dict[str, float], device: Optional[torch.device] = N
     return [dict(zip(keys, o.tolist())) for o in out]
 
 
+_META_DTYPES = {}
+
+
+def _meta_schema(batch, n, image_key):
+    """Split a collated batch's metadata into fixed-size tensor keys (sent as
+    raw bytes in the image round) and everything else (object keys)."""
+    tensors, objects = [], []
+    for k, v in batch.items():
+        if k == image_key:
+            continue
+        if isinstance(v, torch.Tensor) and v.dim() >= 1 and v.shape[0] == n and not v.is_complex():
+            tensors.append((k, str(v.dtype).replace('torch.', ''), tuple(v.shape[1:])))
+        else:
+            objects.append(k)
+    return tensors, objects
+
+
+def pack_meta(batch, schema, n):
+    """Per-item bytes of every tensor key, concatenated: u8 [n, M] (CPU)."""
+    cols = []
+    for k, _, _ in schema:
+        v = batch[k].detach().to('cpu').contiguous()
+        cols.append(v.reshape(n, -1).view(torch.uint8).reshape(n, -1))
+    if not cols:
+        return torch.zeros((n, 0), dtype=torch.uint8)
+    return torch.cat(cols, dim=1).contiguous()
+
+
+def unpack_meta(packed, schema):
+    """Inverse of :func:`pack_meta` (views into ``packed``; any device)."""
+    out, off = {}, 0
+    n = packed.shape[0]
+    for k, dt, shape in schema:
+        dtype = getattr(torch, dt)
+        per = int(torch.tensor([], dtype=dtype).element_size())
+        for d in shape:
+            per *= int(d)
+        col = packed[:, off:off + per].contiguous()
+        out[k] = col.view(dtype).reshape((n,) + tuple(shape))
+        off += per
+    return out
+
+
 class ScatterLoader:
-    """Scatter-mode distribution: the root rank streams ``world*B`` items per
-    step with a :class:`blendtorch.btt.gpu.DeviceLoader` (or any iterable of
-    batch dicts) and every rank receives its ``B``-item shard in HBM.
+    """Scatter-mode distribution (north-star config 3): ONE root rank receives
+    ``world * B`` frames per step and every rank gets its B-frame shard.
+
+    What crosses xGMI is the undecoded u8 pixels (3-4 B/px instead of 12 B/px
+    of fp32 planes) plus every fixed-size metadata tensor (btid, frameid,
+    keypoints ...) packed into one byte row per item -- both in ONE grouped
+    ``batch_isend_irecv`` round: the root posts a send per peer at once, so
+    each point-to-point xGMI link carries its shard concurrently (a ring would
+    serialise them).  Every rank then runs the fused decode kernel on its own
+    shard.  The metadata schema is agreed once (first step); only keys that
+    are not fixed-size tensors (rare) fall back to a per-step object scatter.
 
     Params
     ------
-    source: iterable of dict batches on the root (ignored elsewhere); the
-        image tensor must have leading dim ``world * B``.
+    source: iterable of batch dicts on the root (ignored elsewhere): the image
+        under ``image_key`` is u8 ``[world*B, H, W, C]`` channels-last (a
+        :class:`~blendtorch.btt.gpu.DeviceLoader` with
+        ``DecodeConfig.raw(...)``), metadata collated per item.
     batch_size: per-rank B.
-    shape, dtype: per-item image shape / dtype (identical on all ranks).
+    decode: :class:`~blendtorch.ops.DecodeConfig` applied to each shard (None:
+        deliver the u8 shard).  CUDA shards run the gfx950 kernel, CPU shards
+        (gloo rehearsals) the PyTorch reference -- bit-identical.
+    device: where shards land and are decoded.
     num_batches: steps to deliver (all ranks must agree).
+    comm_device: device of the tensors handed to the process group (default:
+        ``device`` for NCCL/RCCL, CPU for gloo).
+
+    Reference semantics: the fan-out of PUSH/PULL round-robin across consumers
+    (examples/datagen/Readme.md:168-177) and densityopt's partition of work
+    over instances (examples/densityopt/densityopt.py:95-107).
     """
 
-    def __init__(self, source: Optional[Iterable], batch_size: int, shape: Sequence[int], dtype: torch.dtype,
-                 device: torch.device, num_batches: int, image_key: str = 'image', src: int = 0):
+    def __init__(self, source: Optional[Iterable], batch_size: int, decode, device: torch.device,
+                 num_batches: int, image_key: str = 'image', src: int = 0, comm_device=None):
         self.source = source
-        self.batch_size = batch_size
-        self.shape = tuple(shape)
-        self.dtype = dtype
-        self.device = device
-        self.num_batches = num_batches
+        self.batch_size = int(batch_size)
+        self.decode = decode
+        self.device = torch.device(device)
+        self.num_batches = int(num_batches)
         self.image_key = image_key
         self.src = src
+        self.comm_device = comm_device
+        self.stats = {'steps': 0, 'object_scatters': 0, 'bytes_sent': 0}
 
     def __len__(self):
         return self.num_batches
 
+    def _comm_dev(self):
+        if self.comm_device is not None:
+            return torch.device(self.comm_device)
+        if dist.is_available() and dist.is_initialized() and dist.get_backend() != 'nccl':
+            return torch.device('cpu')
+        return self.device
+
+    def _decode(self, shard):
+        if self.decode is None:
+            return shard
+        from .. import ops
+        if shard.is_cuda:
+            return ops.decode(shard, self.decode)
+        return ops.reference_decode(shard, self.decode)
+
     def __iter__(self):
         rank, world, _ = rank_world()
+        multi = world > 1 and dist.is_available() and dist.is_initialized()
         it = iter(self.source) if rank == self.src else None
-        B = self.batch_size
+        B, cdev = self.batch_size, self._comm_dev()
+        header = None          # (H, W, C, tensor schema, object keys), agreed on the first step
         for _ in range(self.num_batches):
-            full, metas = None, None
+            batch = next(it) if rank == self.src else None
+            if header is None:
+                if rank == self.src:
+                    img0 = batch[self.image_key]
+                    if img0.dtype != torch.uint8 or img0.dim() != 4 or img0.shape[0] != world * B:
+                        raise ValueError(f'scatter source must deliver u8 [{world * B},H,W,C] images, got '
+                                         f'{img0.dtype} {tuple(img0.shape)}')
+                    header = (tuple(img0.shape[1:]),) + _meta_schema(batch, world * B, self.image_key)
+                if multi:
+                    box = [header]
+                    dist.broadcast_object_list(box, src=self.src)
+                    header = box[0]
+            shape, schema, objects = header
             if rank == self.src:
-                batch = next(it)
                 full = batch[self.image_key]
-                metas = [{k: (v[r * B:(r + 1) * B] if hasattr(v, '__getitem__') and not isinstance(v, str) else v)
-                          for k, v in batch.items() if k != self.image_key} for r in range(world)]
-            img = scatter_batch(full, (B,) + self.shape, self.dtype, self.device, self.src)
-            meta = {}
-            if world > 1:
-                box = [None]
-                dist.scatter_object_list(box, metas if rank == self.src else None, src=self.src)
-                meta = box[0]
-            elif metas:
-                meta = metas[0]
-            yield {self.image_key: img, **meta}
+                if full.device != cdev:
+                    full = full.to(cdev)
+                meta = pack_meta(batch, schema, world * B).to(cdev, non_blocking=True)
+                img = full[self.src * B:(self.src + 1) * B]
+                mrow = meta[self.src * B:(self.src + 1) * B]
+                if multi:
+                    ops_ = []
+                    for r in range(world):
+                        if r != self.src:
+                            ops_.append(dist.P2POp(dist.isend, full[r * B:(r + 1) * B], r))
+                            ops_.append(dist.P2POp(dist.isend, meta[r * B:(r + 1) * B], r))
+                    for w in dist.batch_isend_irecv(ops_):
+                        w.wait()
+                    self.stats['bytes_sent'] += (world - 1) * B * (full[0].numel() + meta.shape[1])
+            else:
+                row = 0
+                for _, dt, shp in schema:
+                    per = torch.tensor([], dtype=getattr(torch, dt)).element_size()
+                    for d in shp:
+                        per *= int(d)
+                    row += per
+                img = torch.empty((B,) + tuple(shape), dtype=torch.uint8, device=cdev)
+                mrow = torch.empty((B, row), dtype=torch.uint8, device=cdev)
+                for w in dist.batch_isend_irecv([dist.P2POp(dist.irecv, img, self.src),
+                                                 dist.P2POp(dist.irecv, mrow, self.src)]):
+                    w.wait()
+            if img.device != self.device:
+                img = img.to(self.device, non_blocking=True)
+            out = {self.image_key: self._decode(img)}
+            out.update(unpack_meta(mrow, schema))
+            if objects:
+                # keys that are not fixed-size tensors: the slow path, per step
+                self.stats['object_scatters'] += 1
+                parts = None
+                if rank == self.src:
+                    parts = [{k: _slice_obj(batch[k], r * B, (r + 1) * B) for k in objects} for r in range(world)]
+                if multi:
+                    box = [None]
+                    dist.scatter_object_list(box, parts, src=self.src)
+                    out.update(box[0])
+                else:
+                    out.update(parts[0])
+            self.stats['steps'] += 1
+            yield out
+        if it is not None and hasattr(it, 'close'):
+            it.close()      # finish the root's loader so its stats are final
+
+
+def _slice_obj(v, a, b):
+    try:
+        return v[a:b]
+    except TypeError:
+        return v

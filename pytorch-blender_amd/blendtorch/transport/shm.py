@@ -11,10 +11,13 @@ producer side for Python publishers (``btb.DataPublisher(shm_slots=N)``).
 
 Segment layout (shared with C++): header {u64 magic, u32 version, u32 nslots,
 u64 slot_bytes, u64 data_offset}, u32 word per slot (generation << 2 |
-state; states 0 free, 1 writing, 2 published), slots at data_offset (4 KiB
-aligned).  Descriptors carry the generation: a consumer copies, checks that
-the word still reads (gen, published) -- i.e. the producer did not reclaim the
-slot under it -- and hands the slot back.
+state; states 0 free, 1 writing, 2 published, 3 held), slots at data_offset
+(4 KiB aligned).  Descriptors carry the generation: a consumer claims the slot
+(CAS (gen, published) -> (gen, held)), copies, and hands it back (CAS (gen,
+held) -> (gen, free)).  A producer starved for its lease reclaims only
+published (unclaimed) slots, so a paused consumer never has a frame taken
+from under it; a descriptor whose slot was reclaimed while it sat in a queue
+is stale and is dropped (:func:`resolve` returns None).
 """
 from __future__ import annotations
 
@@ -27,8 +30,25 @@ import numpy as np
 
 MAGIC = 0x6d68735f7462746e
 _HDR = struct.Struct('<QIIQQ')
-FREE, WRITING, PUBLISHED = 0, 1, 2
+FREE, WRITING, PUBLISHED, HELD = 0, 1, 2, 3
+HELD_LEASE_FACTOR = 20    # csrc/transport/shmring.h kHeldLeaseFactor
 KEY = '_btshm'
+
+try:   # atomic slot words (CPython build of the native module; absent inside Blender's Python)
+    from .._native import slot_cas as _native_cas
+except ImportError:  # pragma: no cover - exercised only without the native build
+    _native_cas = None
+
+
+def _cas(states, i, expected, desired):
+    """Compare-and-swap slot word ``i`` (atomic when the native module is
+    available; a plain check-then-store otherwise)."""
+    if _native_cas is not None:
+        return _native_cas(states, int(i), int(expected), int(desired))
+    if int(states[i]) != expected:
+        return False
+    states[i] = desired
+    return True
 
 _views = {}
 _views_pid = None
@@ -76,11 +96,13 @@ def _open(name):
     seg = _views.get(name)
     if seg is not None:
         # a producer may have closed the segment and created a new one under
-        # the same name: the cached mapping would show the old, unlinked file
+        # the same name: the cached mapping would show the old, unlinked file.
+        # A file that is merely gone (unlinked, e.g. a retired key frame) is
+        # still readable through the cached mapping.
         try:
             stale = os.stat(_path(name)).st_ino != seg.ino
         except FileNotFoundError:
-            stale = True
+            stale = False
         if stale:
             del _views[name]
             seg = None
@@ -94,6 +116,9 @@ def _open(name):
 
 class TornFrame(RuntimeError):
     """The producer reclaimed the slot while it was being read."""
+
+
+stats = {'stale': 0, 'torn': 0}   # descriptors dropped by resolve() in this process
 
 
 def _word(gen, state):
@@ -128,31 +153,52 @@ def _expand_tiled(seg, off, h, w, c, codec):
 def release(desc):
     """Hand a descriptor's slot back without reading it (dropped messages)."""
     name, slot, off, h, w, c, key, gen = desc[:8]
-    seg = _open(name)
-    if int(seg.states[slot]) == _word(gen, PUBLISHED):
-        seg.states[slot] = _word(gen, FREE)
+    try:
+        seg = _open(name)
+    except FileNotFoundError:
+        return            # producer gone: nothing to hand back
+    if not _cas(seg.states, slot, _word(gen, HELD), _word(gen, FREE)):
+        _cas(seg.states, slot, _word(gen, PUBLISHED), _word(gen, FREE))
 
 
-def resolve(obj):
-    """Materialise a shared-memory image into ``obj`` (in place) and free its slot."""
+def claim(desc):
+    """Take a descriptor's slot (PUBLISHED -> HELD); False if it is stale."""
+    name, slot, off, h, w, c, key, gen = desc[:8]
+    return _cas(_open(name).states, slot, _word(gen, PUBLISHED), _word(gen, HELD))
+
+
+def resolve(obj, strict=False):
+    """Materialise a shared-memory image into ``obj`` (in place) and free its slot.
+
+    Returns ``obj``, or None when the descriptor is stale (its producer
+    reclaimed the slot while the message sat in a queue) or the slot was taken
+    back during the copy -- the caller drops such a message rather than
+    deliver another frame's pixels under its metadata.  ``strict=True``
+    raises :class:`TornFrame` instead."""
     if not isinstance(obj, dict) or KEY not in obj:
         return obj
     desc = obj.pop(KEY)
     name, slot, off, h, w, c, key, gen = desc[:8]
     seg = _open(name)
-    published = _word(gen, PUBLISHED)
-    if int(seg.states[slot]) != published:
-        raise TornFrame(f'shm slot {name}:{slot} was reclaimed before it was read')
-    if len(desc) > 8 and desc[8]:
-        img = _expand_tiled(seg, off, h, w, c, desc[8])
-    else:
-        n = h * w * c
-        img = np.frombuffer(seg.mm, dtype=np.uint8, count=n, offset=off).copy()
-    img = img.reshape((h, w, c) if c > 1 else (h, w))
-    if int(seg.states[slot]) != published:
-        raise TornFrame(f'shm slot {name}:{slot} was reclaimed while it was read')
-    seg.states[slot] = _word(gen, FREE)
-    obj[key] = img
+    if not _cas(seg.states, slot, _word(gen, PUBLISHED), _word(gen, HELD)):
+        stats['stale'] += 1
+        if strict:
+            raise TornFrame(f'shm slot {name}:{slot} was reclaimed before it was read')
+        return None
+    try:
+        if len(desc) > 8 and desc[8]:
+            img = _expand_tiled(seg, off, h, w, c, desc[8])
+        else:
+            n = h * w * c
+            img = np.frombuffer(seg.mm, dtype=np.uint8, count=n, offset=off).copy()
+    finally:
+        ok = _cas(seg.states, slot, _word(gen, HELD), _word(gen, FREE))
+    if not ok:
+        stats['torn'] += 1
+        if strict:
+            raise TornFrame(f'shm slot {name}:{slot} was reclaimed while it was read')
+        return None
+    obj[key] = img.reshape((h, w, c) if c > 1 else (h, w))
     return obj
 
 
@@ -160,12 +206,21 @@ class ShmRing:
     """Producer-side ring (single writer).  ``acquire`` blocks while every slot
     is still with a consumer -- the same backpressure as a full SNDHWM."""
 
-    def __init__(self, name, nslots, slot_bytes):
+    def __init__(self, name, nslots, slot_bytes, lease_s=30.0):
+        self.lease_s = lease_s
         slot_bytes = (slot_bytes + 4095) // 4096 * 4096
         data_offset = (_HDR.size + 4 * nslots + 4095) // 4096 * 4096
         size = data_offset + nslots * slot_bytes
         fd = os.open(_path(name), os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
-        os.ftruncate(fd, size)
+        try:
+            os.ftruncate(fd, size)
+            # reserve the pages now: a too-small /dev/shm fails here (ENOSPC)
+            # instead of SIGBUS on the first slot write (as shmring.cpp does)
+            os.posix_fallocate(fd, 0, size)
+        except OSError:
+            os.close(fd)
+            os.unlink(_path(name))
+            raise
         mm = mmap.mmap(fd, size, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
         _HDR.pack_into(mm, 0, 0, 1, nslots, slot_bytes, data_offset)
         self.seg = _Segment(name, fd, mm, True)
@@ -179,7 +234,12 @@ class ShmRing:
     def name(self):
         return self.seg.name
 
-    def acquire(self, timeout_s=None, lease_s=30.0):
+    def acquire(self, timeout_s=None, lease_s=None):
+        """Claim a free slot for writing.  ``lease_s`` (default: the ring's
+        ``lease_s``, 30 s) bounds how long the producer waits before taking
+        back the oldest slot no consumer has claimed."""
+        if lease_s is None:
+            lease_s = self.lease_s
         t0 = time.time()
         n = self.seg.nslots
         while True:
@@ -194,12 +254,16 @@ class ShmRing:
             if timeout_s is not None and waited > timeout_s:
                 raise TimeoutError('no free shared-memory slot')
             if lease_s is not None and waited > lease_s:
-                pub = [i for i in range(n) if int(self.seg.states[i]) & 3 == PUBLISHED]
-                if pub:   # reclaim the oldest published slot (its message was dropped)
-                    i = min(pub, key=lambda j: self._published_at.get(j, 0.0))
-                    self.seg.states[i] = (int(self.seg.states[i]) & ~3) | WRITING
-                    self.reclaimed += 1
-                    return i
+                # reclaim the oldest unclaimed slot (its message was dropped);
+                # claimed (held) ones only after a far longer stall (dead consumer)
+                ok = (PUBLISHED, HELD) if waited > lease_s * HELD_LEASE_FACTOR else (PUBLISHED,)
+                cand = [i for i in range(n) if int(self.seg.states[i]) & 3 in ok]
+                if cand:
+                    i = min(cand, key=lambda j: self._published_at.get(j, 0.0))
+                    w = int(self.seg.states[i])
+                    if w & 3 in ok and _cas(self.seg.states, i, w, (w & ~3) | WRITING):
+                        self.reclaimed += 1
+                        return i
             time.sleep(0.0002)
 
     def put(self, image):

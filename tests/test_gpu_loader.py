@@ -109,14 +109,28 @@ def test_vector_env_stages_obs_on_device(dev, free_port):
 
 
 def test_scatter_loader_single_rank(dev, free_port):
+    """Scatter mode on one rank: the root loader lands raw u8 frames, the
+    shard is decoded by the gfx950 kernel -- equal to decoding the same
+    frames directly -- and the metadata arrives as typed tensors."""
     from blendtorch.parallel import ScatterLoader
+    cfg = ops.DecodeConfig.unit(channels='rgb', gamma=2.2)
     with btt.BlenderLauncher(producer='cubesim', num_instances=1, named_sockets=['DATA'], start_port=free_port,
                              instance_args=[['--mode', 'rgba']]) as bl:
         dl = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=4, max_items=8, device=dev,
-                          decode=ops.DecodeConfig.unit())
-        sl = ScatterLoader(dl, 4, (3, 480, 640), torch.float32, dev, 2)
+                          decode=ops.DecodeConfig.raw(channels='rgb'))
+        raw = []
+
+        def tap():
+            for b in dl:
+                raw.append(b['image'].clone())
+                yield b
+        sl = ScatterLoader(tap(), 4, cfg, dev, 2)
         out = [b for b in sl]
-        assert len(out) == 2 and out[0]['image'].shape == (4, 3, 480, 640) and out[1]['btid'].shape == (4,)
+    assert len(out) == 2 and out[0]['image'].shape == (4, 3, 480, 640) and out[1]['btid'].shape == (4,)
+    assert out[0]['xy'].shape == (4, 8, 2) and out[0]['xy'].dtype == torch.float64
+    for b, r in zip(out, raw):
+        torch.testing.assert_close(b['image'], ops.decode(r, cfg), rtol=0, atol=0)
+    assert sl.stats['object_scatters'] == 0
 
 
 @pytest.mark.parametrize('origin', ['upper-left', 'lower-left'])

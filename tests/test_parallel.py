@@ -86,13 +86,30 @@ def _worker(rank, world, port, q):
         stats = parallel.all_gather_stats({'fps': 10.0 * (r + 1), 'n': r})
         ok_stats = [s['fps'] for s in stats] == [10.0 * (i + 1) for i in range(world)]
 
+        # scatter mode: u8 frames + packed metadata in one P2P round, decoded per rank
+        from blendtorch import ops
+        cfg = ops.DecodeConfig.unit(channels='rgb', gamma=2.2)
+        H, W = 6, 8
+
+        def frames(step):
+            g = torch.Generator().manual_seed(step)
+            return torch.randint(0, 256, (world * B, H, W, 4), dtype=torch.uint8, generator=g)
+
         def source():
-            for step in range(2):
-                yield {'image': torch.full((world * B, 2), float(step)) + torch.arange(world * B).view(-1, 1),
-                       'btid': torch.arange(world * B)}
-        sl = parallel.ScatterLoader(source() if r == 0 else None, B, (2,), torch.float32, torch.device('cpu'), 2)
-        got = [(b['image'][:, 0].tolist(), b['btid'].tolist()) for b in sl]
-        ok_loader = got[1][1] == list(range(r * B, (r + 1) * B)) and got[1][0][0] == 1.0 + r * B
+            for step in range(3):
+                yield {'image': frames(step), 'btid': torch.arange(world * B) + 100 * step,
+                       'xy': torch.arange(world * B * 16, dtype=torch.float64).view(world * B, 8, 2) + step,
+                       'name': [f's{step}i{i}' for i in range(world * B)]}
+        sl = parallel.ScatterLoader(source() if r == 0 else None, B, cfg, torch.device('cpu'), 3)
+        ok_loader = True
+        for step, b in enumerate(sl):
+            full = frames(step)[r * B:(r + 1) * B]
+            ok_loader &= torch.equal(b['image'], ops.reference_decode(full, cfg))   # bit-exact
+            ok_loader &= b['btid'].tolist() == [100 * step + i for i in range(r * B, (r + 1) * B)]
+            xy = torch.arange(world * B * 16, dtype=torch.float64).view(world * B, 8, 2)[r * B:(r + 1) * B] + step
+            ok_loader &= b['xy'].dtype == torch.float64 and torch.equal(b['xy'], xy)
+            ok_loader &= b['name'] == [f's{step}i{i}' for i in range(r * B, (r + 1) * B)]
+        ok_loader &= sl.stats['steps'] == 3 and sl.stats['object_scatters'] == 3
         q.put((r, ok_scatter, ok_bcast, ok_stats, ok_loader))
         torch.distributed.destroy_process_group()
     except Exception as e:  # surface failures to the parent
@@ -140,6 +157,18 @@ def test_pool_mode_gloo_world2():
         assert r[1] == 2 and r[3] == 40 and r[2] == [0, 1], r
 
 
+def test_pack_meta_roundtrip():
+    b = {'btid': torch.arange(4), 'xy': torch.rand(4, 8, 2, dtype=torch.float64),
+         'f': torch.rand(4).half(), 'flag': torch.tensor([True, False, True, True])}
+    tensors, objects = parallel.__dict__['_meta_schema'](dict(b, image=None), 4, 'image')
+    assert objects == [] and [k for k, _, _ in tensors] == ['btid', 'xy', 'f', 'flag']
+    packed = parallel.pack_meta(b, tensors, 4)
+    assert packed.dtype == torch.uint8 and packed.shape == (4, 8 + 128 + 2 + 1)
+    out = parallel.unpack_meta(packed[2:4], tensors)
+    for k, v in b.items():
+        assert out[k].dtype == v.dtype and torch.equal(out[k], v[2:4]), k
+
+
 def test_collectives_gloo_world2():
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
@@ -152,3 +181,46 @@ def test_collectives_gloo_world2():
         p.join(timeout=60)
     for r in res:
         assert r[1:] == (True, True, True, True), r
+
+
+def _grad_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        from blendtorch.parallel.step import CapturedStep, allreduce_gradients
+        parallel.init_distributed(backend='gloo')
+        torch.manual_seed(0)
+        m = torch.nn.Sequential(torch.nn.Linear(4, 3), torch.nn.ReLU(), torch.nn.Linear(3, 1))
+        for p in m.parameters():
+            p.grad = torch.full_like(p, float(rank + 1))
+        n = allreduce_gradients(m.parameters(), bucket_mb=1e-5)      # tiny buckets: one per tensor
+        ok_avg = n == 4 and all(torch.equal(p.grad, torch.full_like(p, 1.5)) for p in m.parameters())
+        # data-parallel step without DDP: ranks see different data, weights stay identical
+        opt = torch.optim.SGD(m.parameters(), lr=0.1)
+        step = CapturedStep(m, opt, lambda mod, x: mod(x).pow(2).mean(), graph=False)
+        for i in range(3):
+            step(torch.randn(8, 4, generator=torch.Generator().manual_seed(10 * rank + i)))
+        w = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+        allw = [torch.empty_like(w) for _ in range(world)]
+        torch.distributed.all_gather(allw, w)
+        ok_sync = all(torch.equal(allw[0], x) for x in allw) and step.collectives == 1
+        q.put((rank, ok_avg, ok_sync))
+        torch.distributed.destroy_process_group()
+    except Exception as e:  # surface failures to the parent
+        q.put((rank, repr(e)))
+
+
+def test_manual_grad_allreduce_gloo_world2():
+    """allreduce_gradients / CapturedStep (eager here): averaged gradients and
+    weights that stay bit-identical across ranks without DDP."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_grad_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert r[1:] == (True, True), r
