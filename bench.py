@@ -132,6 +132,8 @@ def parse_args(argv=None):
     ap.add_argument('--backend', choices=['nccl', 'gloo'], default='nccl',
                     help='process-group backend (nccl = RCCL over xGMI; gloo only to rehearse several ranks on one GPU)')
     ap.add_argument('--start-port', type=int, default=0)
+    ap.add_argument('--consumer-input', choices=['stream', 'resident'], default='stream',
+                    help='diagnostic: resident = the consumer trains on one fixed batch while the stream keeps running')
     ap.add_argument('--force-pg', action='store_true',
                     help='initialise a process group even for one rank (rehearses the collective code paths)')
     ap.add_argument('--dist', choices=['shard', 'pool', 'scatter'], default='shard',
@@ -343,12 +345,22 @@ def main(argv=None):
                 print(f'[bench] HIP graph capture failed, eager steps: {stepper.error}', file=sys.stderr, flush=True)
                 stepper.error = None
 
+        fixed = {}
+
         def step():
             b = next(it)
             img = b['image']
             last['btid'] = b.get('btid')
             if model is not None:
-                graphed(as_input(img))
+                if args.consumer_input == 'resident':
+                    # diagnostic: keep streaming, but train on one fixed batch (no
+                    # dependency on the loader's events) -- separates contention
+                    # from waiting in the streamed-vs-resident step-time gap
+                    if 'x' not in fixed:
+                        fixed['x'] = as_input(img).clone(memory_format=torch.channels_last)
+                    graphed(fixed['x'])
+                else:
+                    graphed(as_input(img))
             return img
 
         # warm-up: at least W batches, and (shard/pool) until every local producer

@@ -51,6 +51,10 @@ for step in "$@"; do
     sup2:*) a="${step#sup2:}"; timeout -k 10 300 python bench.py --gpus 2 --backend gloo ${a//,/ } >> gpurun_out/sup2.log 2>&1; rc=$?; grep '^{' gpurun_out/sup2.log | tail -1 | cut -c1-600;;
     gtests:*) a="${step#gtests:}"; timeout -k 10 500 python -u -m pytest ${a//,/ } -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu_sel.log 2>&1; rc=$?; grep -E "PASS|FAIL|ERROR|passed|failed" gpurun_out/pytest_gpu_sel.log | tail -30;;
     b:*) a="${step#b:}"; tag=$(echo "$a" | tr -c 'a-zA-Z0-9\n' '_' | cut -c1-60); timeout -k 10 300 python bench.py ${a//,/ } > gpurun_out/b_$tag.log 2>&1; rc=$?; grep '^{' gpurun_out/b_$tag.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$a', '->', d['value'], d['unit'], d['ms_per_step'], 'ms', d.get('h2d_gbytes_per_s'), 'GB/s', d['config'].get('consumer_step'), d.get('world_size_seen'))" || tail -5 gpurun_out/b_$tag.log;;
+    ktrace:*) a="${step#ktrace:}"; tag=$(echo "$a" | tr -c 'a-zA-Z0-9\n' '_' | cut -c1-50); timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d /tmp/rp_kt_$tag -o run --output-format csv -- python bench.py ${a//,/ } > gpurun_out/kt_$tag.log 2>&1; rc=$?; grep '^{' gpurun_out/kt_$tag.log | cut -c1-300
+          python scripts/trace_timeline.py /tmp/rp_kt_$tag --last ${KT_LAST:-20000} > gpurun_out/kt_$tag.txt 2>&1; cat gpurun_out/kt_$tag.txt;;
+    ktstep) timeout -k 10 300 rocprofv3 --kernel-trace -d /tmp/rp_ktstep -o run --output-format csv -- python scripts/disc_step_bench.py --only bf16-nhwc --graph on --iters 300 > gpurun_out/ktstep.log 2>&1; rc=$?; grep '^{' gpurun_out/ktstep.log
+          python scripts/trace_timeline.py /tmp/rp_ktstep --last ${KT_LAST:-20000} > gpurun_out/ktstep.txt 2>&1; cat gpurun_out/ktstep.txt;;
     short) timeout -k 10 200 python bench.py --steps 20 --warmup 5 > gpurun_out/short.log 2>&1; rc=$?; grep '^{' gpurun_out/short.log;;
     dist2gloo) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29557 bench.py --gpus 2 --backend gloo --steps 1000 --warmup 20 > gpurun_out/dist2gloo.log 2>&1; rc=$?; grep '^{' gpurun_out/dist2gloo.log;;
     replay) timeout -k 10 200 python benchmarks/bench_replay.py > gpurun_out/replay.log 2>&1 && timeout -k 10 200 python benchmarks/bench_replay.py --batch 64 --steps 500 >> gpurun_out/replay.log 2>&1 && timeout -k 10 200 python benchmarks/bench_replay.py --graph >> gpurun_out/replay.log 2>&1 && timeout -k 10 200 python benchmarks/bench_replay.py --graph --batch 64 --steps 500 >> gpurun_out/replay.log 2>&1 && timeout -k 10 200 python benchmarks/bench_replay.py --fill producers --frames 2048 --batch 64 --steps 500 >> gpurun_out/replay.log 2>&1; rc=$?; cat gpurun_out/replay.log | grep '^{';;
