@@ -485,6 +485,41 @@ class NativeError(Exception):
              return py::make_tuple(obs, rew, done);
            },
            py::arg("which"), py::arg("cmd"), py::arg("actions"), py::arg("obs_dim"), py::arg("phase") = 0)
+      .def("roundtrip",
+           [](VecReq& v, int i, py::bytes request) {
+             // one pickled request -> the raw reply frame, GIL released
+             // (btt.env.RemoteEnv on the native client: N = 1)
+             if (i < 0 || size_t(i) >= v.socks.size()) throw py::index_error("env index");
+             std::string req = request;
+             std::string err;
+             Message r;
+             {
+               py::gil_scoped_release nogil;
+               try {
+                 Message m;
+                 m.push_back(Frame::copy_of(req.data(), req.size()));
+                 try {
+                   v.socks[size_t(i)]->send(std::move(m));
+                 } catch (const zmtp::Error& e) {
+                   throw std::runtime_error(e.code == zmtp::E_AGAIN ? "Failed to send to remote environment"
+                                                                    : e.what());
+                 }
+                 try {
+                   r = v.socks[size_t(i)]->recv();
+                 } catch (const zmtp::Error& e) {
+                   throw std::runtime_error(e.code == zmtp::E_AGAIN ? "Failed to receive from remote environment"
+                                                                    : e.what());
+                 }
+               } catch (const std::exception& e) {
+                 err = e.what();
+               }
+             }
+             if (!err.empty()) throw py::value_error(err);
+             if (r.size() != 1) throw py::value_error("expected a single-frame reply");
+             v.last[size_t(i)].assign(r[0].data(), r[0].data() + r[0].size);
+             return py::bytes(reinterpret_cast<const char*>(r[0].data()), r[0].size);
+           },
+           py::arg("i"), py::arg("request"))
       .def("last_reply", [](VecReq& v, int i) {
         // full reply dict of env i (info, rgb_array, ...), decoded lazily
         auto& raw = v.last[size_t(i)];

@@ -1,50 +1,60 @@
-"""Blender-side cart-pole env (needs cartpole.blend with Bullet rigid bodies).
-The native stand-in blendtorch/bin/cartpolesim implements the same env."""
+"""Cart-pole environment, Blender side (scene: cartpole.blend with Bullet
+rigid bodies; contract of the reference's
+examples/control/cartpole_gym/envs/cartpole.blend.py).
+
+Action: a force on the cart, applied as a change of the slider motor's target
+velocity over one frame (dv = F / m_total / fps).  Observation: (cart x, pole
+x, pole angle); reward 0; the episode is done once the pole tilts past 0.6
+rad or the cart leaves [-4, 4].  The native stand-in
+``blendtorch/bin/cartpolesim`` implements the same env without Blender.
+"""
 import argparse
 
 import bpy
 import numpy as np
 from blendtorch import btb
 
+MAX_ANGLE, MAX_OFFSET = 0.6, 4.0
+
 
 class CartpoleEnv(btb.env.BaseEnv):
     def __init__(self, agent):
         super().__init__(agent)
-        self.cart = bpy.data.objects['Cart']
-        self.pole = bpy.data.objects['Pole']
-        self.polerot = bpy.data.objects['PoleRotHelp']
-        self.motor = bpy.data.objects['Motor'].rigid_body_constraint
-        self.fps = bpy.context.scene.render.fps   # physics must run at the same rate
-        self.total_mass = self.cart.rigid_body.mass + self.pole.rigid_body.mass
+        objs = bpy.data.objects
+        self.cart, self.pole, self.hinge = objs['Cart'], objs['Pole'], objs['PoleRotHelp']
+        self.motor = objs['Motor'].rigid_body_constraint
+        # velocity change per unit force in one frame (physics runs at the scene fps)
+        self.dv_per_force = 1.0 / ((self.cart.rigid_body.mass + self.pole.rigid_body.mass)
+                                   * bpy.context.scene.render.fps)
 
     def _env_reset(self):
-        self.motor.motor_lin_target_velocity = 0.
-        self.cart.location = (0.0, 0, 1.2)
-        self.polerot.rotation_euler[1] = np.random.uniform(-0.6, 0.6)
+        self.motor.motor_lin_target_velocity = 0.0
+        self.cart.location = (0.0, 0.0, 1.2)
+        self.hinge.rotation_euler[1] = np.random.uniform(-MAX_ANGLE, MAX_ANGLE)
 
     def _env_prepare_step(self, action):
-        # constant acceleration between steps: v(t+1) = v(t) + (f/m) dt
-        self.motor.motor_lin_target_velocity += action / self.total_mass / self.fps
+        self.motor.motor_lin_target_velocity += action * self.dv_per_force
 
     def _env_post_step(self):
-        c = self.cart.matrix_world.translation[0]
-        p = self.pole.matrix_world.translation[0]
-        a = self.pole.matrix_world.to_euler('XYZ')[1]
-        return dict(obs=(c, p, a), reward=0., done=bool(abs(a) > 0.6 or abs(c) > 4.0))
+        cart_x = self.cart.matrix_world.translation[0]
+        pole_x = self.pole.matrix_world.translation[0]
+        angle = self.pole.matrix_world.to_euler('XYZ')[1]
+        return {'obs': (cart_x, pole_x, angle), 'reward': 0.0,
+                'done': bool(abs(angle) > MAX_ANGLE or abs(cart_x) > MAX_OFFSET)}
 
 
-def main():
-    args, remainder = btb.parse_blendtorch_args()
-    parser = argparse.ArgumentParser()
-    parser.add_argument('--render-every', default=None, type=int)
-    parser.add_argument('--real-time', dest='realtime', action='store_true')
-    parser.add_argument('--no-real-time', dest='realtime', action='store_false')
-    envargs = parser.parse_args(remainder)
-    agent = btb.env.RemoteControlledAgent(args.btsockets['GYM'], real_time=envargs.realtime)
-    env = CartpoleEnv(agent)
-    if envargs.render_every:
-        env.attach_default_renderer(every_nth=envargs.render_every)
+def env_options(argv):
+    p = argparse.ArgumentParser()
+    p.add_argument('--render-every', type=int, default=None)
+    p.add_argument('--real-time', dest='realtime', action='store_true')
+    p.add_argument('--no-real-time', dest='realtime', action='store_false')
+    return p.parse_args(argv)
+
+
+if __name__ == '__main__':
+    btargs, rest = btb.parse_blendtorch_args()
+    opts = env_options(rest)
+    env = CartpoleEnv(btb.env.RemoteControlledAgent(btargs.btsockets['GYM'], real_time=opts.realtime))
+    if opts.render_every:
+        env.attach_default_renderer(every_nth=opts.render_every)
     env.run(frame_range=(1, 10000), use_animation=True)
-
-
-main()

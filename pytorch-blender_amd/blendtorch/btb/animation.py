@@ -1,20 +1,28 @@
 """Blender frame loop with fine-grained callbacks.
 
-Reference: pkg_blender/blendtorch/btb/animation.py:9-213.  Six signals:
-``pre_play``, ``pre_animation``, ``pre_frame``, ``post_frame``,
-``post_animation``, ``post_play``.  Two drivers:
+Behavioural contract (reference: pkg_blender/blendtorch/btb/animation.py:9-213):
+six :class:`~blendtorch.btb.signal.Signal` s fire in this order for a range
+``(a, b)`` and E episodes ::
 
-* ``use_animation=True`` -- Blender's own (non-blocking, UI timer driven)
-  playback: ``frame_change_pre`` drives pre-frame work and a POST_PIXEL draw
-  handler of the first 3D view drives post-frame work, which makes offscreen
-  rendering inside ``post_frame`` safe.  POST_PIXEL may fire several times
-  per frame; a pending flag plus the last handled frame id suppresses
-  duplicates (``:56-65``).
-* ``use_animation=False`` -- a blocking ``frame_set`` loop (works with
-  ``--background``), as fast as the scene evaluates.
+    pre_play
+    E x [ pre_animation, (pre_frame, post_frame) for a..b, post_animation ]
+    post_play
 
-``num_episodes=-1`` loops forever; ``rewind()`` restarts the episode; the
-rigid-body cache range follows the animation range when ``use_physics``.
+Two ways of advancing frames:
+
+* ``use_animation=True`` (interactive Blender): Blender's timer-driven
+  playback runs the frames and :meth:`play` returns at once.  Frame changes
+  arrive through ``frame_change_pre``; post-frame work is attached to the
+  first 3D view's POST_PIXEL draw callback (``use_offline_render``), because
+  only inside a draw callback may an offscreen render read the GL context.
+  A view may be drawn several times per frame and other views draw too, so a
+  post-frame event is accepted once per frame and only from that view.
+* ``use_animation=False`` (``--background``): :meth:`play` itself steps
+  ``frame_set`` through the range, as fast as the scene evaluates.
+
+``num_episodes=-1`` plays forever; :meth:`rewind` jumps back to the first
+frame (a new episode starts there); with ``use_physics`` the rigid-body point
+cache is resized to the range so simulations run over all of it.
 """
 import sys
 
@@ -23,131 +31,124 @@ import bpy
 from .signal import Signal
 from .utils import find_first_view3d
 
+_SIGNALS = ('pre_play', 'pre_animation', 'pre_frame', 'post_frame', 'post_animation', 'post_play')
+
+
+class _Run:
+    """State of one :meth:`AnimationController.play` call."""
+
+    __slots__ = ('first', 'last', 'episodes_left', 'timer_driven', 'draw_bound', 'awaiting_post', 'posted_frame',
+                 'view_space', 'draw_handle')
+
+    def __init__(self, first, last, episodes, timer_driven, draw_bound):
+        self.first, self.last = first, last
+        self.episodes_left = episodes
+        self.timer_driven = timer_driven
+        self.draw_bound = draw_bound          # post-frame work runs in a 3D view's draw callback
+        self.awaiting_post = False            # a pre-frame fired and its post-frame has not run yet
+        self.posted_frame = None              # frame whose post-frame already ran
+        self.view_space = None
+        self.draw_handle = None
+
+    def accepts_post(self, frame):
+        """One post-frame event per frame, and (draw-bound) only from our view."""
+        if not self.awaiting_post or self.posted_frame == frame:
+            return False
+        if self.draw_bound and bpy.context.space_data != self.view_space:
+            return False
+        return True
+
 
 class AnimationController:
-    """Drive Blender's animation system and emit per-frame signals."""
+    """Drive Blender's animation system and emit per-frame signals
+    (``pre_play``, ``pre_animation``, ``pre_frame``, ``post_frame``,
+    ``post_animation``, ``post_play``)."""
 
     def __init__(self):
-        self.pre_animation = Signal()
-        self.pre_frame = Signal()
-        self.post_frame = Signal()
-        self.post_animation = Signal()
-        self.pre_play = Signal()
-        self.post_play = Signal()
-        self._plyctx = None
-
-    class _PlayContext:
-        """Book-keeping of one ``play`` call."""
-
-        def __init__(self, frame_range, num_episodes, use_animation, use_offline_render):
-            self.frame_range = frame_range
-            self.num_episodes = num_episodes
-            self.use_animation = use_animation
-            self.use_offline_render = use_offline_render
-            self.episode = 0
-            self.pending_post_frame = False
-            self.last_post_frame = 0
-            self.draw_handler = None
-            self.draw_space = None
-
-        def skip_post_frame(self, current_frame):
-            """True when a post-frame event must be ignored: nothing pending,
-            already handled for this frame, or a redraw of another 3D view."""
-            if not self.pending_post_frame or self.last_post_frame == current_frame:
-                return True
-            return (self.use_animation and self.use_offline_render
-                    and bpy.context.space_data != self.draw_space)
+        for name in _SIGNALS:
+            setattr(self, name, Signal())
+        self._run = None
 
     @property
     def frameid(self):
         """Current frame number of the scene."""
         return bpy.context.scene.frame_current
 
-    def play(self, frame_range=None, num_episodes=-1, use_animation=True, use_offline_render=True,
-             use_physics=True):
-        """Start playing ``frame_range`` (inclusive) ``num_episodes`` times."""
-        assert self._plyctx is None, 'Animation already running'
-        self._plyctx = AnimationController._PlayContext(
-            frame_range=AnimationController.setup_frame_range(frame_range, physics=use_physics),
-            num_episodes=num_episodes if num_episodes >= 0 else sys.maxsize,
-            use_animation=use_animation,
-            use_offline_render=use_offline_render)
-        if use_animation:
-            self._play_animation()
-        else:
-            self._play_manual()
-
     @staticmethod
     def setup_frame_range(frame_range, physics=True):
-        """Apply ``frame_range`` (or the scene's) to the scene and, with
-        ``physics``, to the rigid-body point cache; returns the range."""
+        """Make ``frame_range`` (default: the scene's) the scene's range and,
+        with ``physics``, the rigid-body cache's range.  Returns ``(a, b)``."""
         scene = bpy.context.scene
-        if frame_range is None:
-            frame_range = (scene.frame_start, scene.frame_end)
-        scene.frame_start, scene.frame_end = frame_range[0], frame_range[1]
-        if physics and scene.rigidbody_world:
-            scene.rigidbody_world.point_cache.frame_start = frame_range[0]
-            scene.rigidbody_world.point_cache.frame_end = frame_range[1]
-        return frame_range
+        first, last = frame_range if frame_range is not None else (scene.frame_start, scene.frame_end)
+        scene.frame_start, scene.frame_end = first, last
+        world = scene.rigidbody_world if physics else None
+        if world:
+            cache = world.point_cache
+            cache.frame_start, cache.frame_end = first, last
+        return (first, last)
 
-    def _play_animation(self):
+    def play(self, frame_range=None, num_episodes=-1, use_animation=True, use_offline_render=True,
+             use_physics=True):
+        """Play ``frame_range`` (inclusive) ``num_episodes`` times (-1: forever).
+
+        Blocking unless ``use_animation`` (then Blender's timer drives frames)."""
+        if self._run is not None:
+            raise AssertionError('Animation already running')
+        first, last = self.setup_frame_range(frame_range, physics=use_physics)
+        episodes = sys.maxsize if num_episodes < 0 else num_episodes
+        self._run = run = _Run(first, last, episodes, use_animation, use_animation and use_offline_render)
         self.pre_play.invoke()
-        bpy.app.handlers.frame_change_pre.append(self._on_pre_frame)
-        if self._plyctx.use_offline_render:
-            _, self._plyctx.draw_space, _ = find_first_view3d()
-            self._plyctx.draw_handler = bpy.types.SpaceView3D.draw_handler_add(
-                self._on_post_frame, (), 'WINDOW', 'POST_PIXEL')
+        bpy.app.handlers.frame_change_pre.append(self._frame_begins)
+        if run.draw_bound:
+            _, run.view_space, _ = find_first_view3d()
+            run.draw_handle = bpy.types.SpaceView3D.draw_handler_add(self._frame_ends, (), 'WINDOW', 'POST_PIXEL')
         else:
-            bpy.app.handlers.frame_change_post.append(self._on_post_frame)
-        bpy.context.scene.frame_set(self._plyctx.frame_range[0])
-        bpy.ops.screen.animation_play()   # returns immediately
-
-    def _play_manual(self):
-        self.pre_play.invoke()
-        bpy.app.handlers.frame_change_pre.append(self._on_pre_frame)
-        bpy.app.handlers.frame_change_post.append(self._on_post_frame)
-        ctx = self._plyctx
-        while ctx.episode < ctx.num_episodes:
-            bpy.context.scene.frame_set(ctx.frame_range[0])
-            while self.frameid < ctx.frame_range[1]:
-                bpy.context.scene.frame_set(self.frameid + 1)
-                if self._plyctx is None:   # _cancel ran inside frame_set
-                    return
+            bpy.app.handlers.frame_change_post.append(self._frame_ends)
+        if use_animation:
+            bpy.context.scene.frame_set(first)
+            bpy.ops.screen.animation_play()       # returns immediately; the timer takes over
+            return
+        scene = bpy.context.scene
+        while self._run is run:
+            scene.frame_set(first)
+            while self._run is run and scene.frame_current < last:
+                scene.frame_set(scene.frame_current + 1)
 
     def rewind(self):
         """Jump back to the first frame of the range (starts a new episode)."""
-        if self._plyctx is not None:
-            self._set_frame(self._plyctx.frame_range[0])
+        if self._run is not None:
+            bpy.context.scene.frame_set(self._run.first)
 
-    def _set_frame(self, frame_index):
-        bpy.context.scene.frame_set(frame_index)
-
-    def _on_pre_frame(self, scene, *args):
-        if self.frameid == self._plyctx.frame_range[0]:
+    # -- handlers --------------------------------------------------------------
+    def _frame_begins(self, scene, *unused):
+        run = self._run
+        if self.frameid == run.first:
             self.pre_animation.invoke()
         self.pre_frame.invoke()
-        self._plyctx.pending_post_frame = True
+        run.awaiting_post = True
 
-    def _on_post_frame(self, *args):
-        ctx = self._plyctx
-        if ctx is None or ctx.skip_post_frame(self.frameid):
+    def _frame_ends(self, *unused):
+        run = self._run
+        frame = self.frameid
+        if run is None or not run.accepts_post(frame):
             return
-        ctx.pending_post_frame = False
-        ctx.last_post_frame = self.frameid
+        run.awaiting_post = False
+        run.posted_frame = frame
         self.post_frame.invoke()
-        if self.frameid == ctx.frame_range[1]:
-            self.post_animation.invoke()
-            ctx.episode += 1
-            if ctx.episode == ctx.num_episodes:
-                self._cancel()
+        if frame != run.last:
+            return
+        self.post_animation.invoke()
+        run.episodes_left -= 1
+        if run.episodes_left == 0:
+            self._finish()
 
-    def _cancel(self):
-        bpy.app.handlers.frame_change_pre.remove(self._on_pre_frame)
-        if self._plyctx.draw_handler is not None:
-            bpy.types.SpaceView3D.draw_handler_remove(self._plyctx.draw_handler, 'WINDOW')
-            self._plyctx.draw_handler = None
+    def _finish(self):
+        run = self._run
+        bpy.app.handlers.frame_change_pre.remove(self._frame_begins)
+        if run.draw_handle is not None:
+            bpy.types.SpaceView3D.draw_handler_remove(run.draw_handle, 'WINDOW')
         else:
-            bpy.app.handlers.frame_change_post.remove(self._on_post_frame)
+            bpy.app.handlers.frame_change_post.remove(self._frame_ends)
         bpy.ops.screen.animation_cancel(restore_frame=False)
+        self._run = None
         self.post_play.invoke()
-        self._plyctx = None

@@ -1,14 +1,15 @@
-"""Camera intrinsics/extrinsics and world->pixel projection.
+"""Camera intrinsics/extrinsics and world -> pixel projection.
 
-Reference: pkg_blender/blendtorch/btb/camera.py:8-204.  ``view_matrix`` is
-the inverse of the camera's normalised world matrix, ``proj_matrix`` comes
-from ``calc_matrix_camera`` at the render resolution.  Projection:
+API and numbers follow pkg_blender/blendtorch/btb/camera.py:8-204:
+``view_matrix`` is the inverse of the camera's (scale-free) world matrix,
+``proj_matrix`` Blender's ``calc_matrix_camera`` at the render size, and ::
 
-    ndc   = dehom([p, 1] @ (P V)^T)
-    pixel = ((ndc.xy + 1) / 2) * [W, H]   (y flipped for 'upper-left')
-    depth = -([p, 1] @ V^T).z             (linear camera-space depth)
+    ndc   = dehom([p, 1] (P V)^T)
+    pixel = (ndc.xy + 1) / 2 * [W, H]      (y mirrored for origin 'upper-left')
+    depth = -([p, 1] V^T).z                (linear depth along the view axis)
 
-For many points at once on the GPU see :func:`blendtorch.ops.project`.
+All projections go through :func:`_project`, the same math as the batched
+GPU path (:func:`blendtorch.ops.project` / ``ops.reference_project``).
 """
 import bpy
 import numpy as np
@@ -16,91 +17,116 @@ from mathutils import Vector
 
 from . import utils
 
+_ORIGINS = ('upper-left', 'lower-left')
+
+
+def _as_np(m):
+    return np.array(m, dtype=np.float64)
+
+
+def _project(points, view, proj, want_depth):
+    """Homogeneous projection of N x 3 points: (ndc N x 3, depth N or None)."""
+    p = utils.hom(np.atleast_2d(np.asarray(points, dtype=np.float64)), 1.0)
+    eye = p @ view.T                           # camera space
+    ndc = utils.dehom(eye @ proj.T)
+    return ndc, (-eye[:, 2] if want_depth else None)
+
+
+def _render_shape(render=None):
+    """(H, W) of the render output: resolution scaled by its percentage."""
+    r = render if render is not None else bpy.context.scene.render
+    pct = r.resolution_percentage / 100.0
+    return int(r.resolution_y * pct), int(r.resolution_x * pct)
+
+
+def _view_of(obj):
+    """World -> camera transform of ``obj`` (scene camera if None)."""
+    obj = obj if obj is not None else bpy.context.scene.camera
+    return obj.matrix_world.normalized().inverted()
+
+
+def _proj_of(obj, shape):
+    """Camera -> clip transform of ``obj`` for an image of ``shape`` (H, W)."""
+    obj = obj if obj is not None else bpy.context.scene.camera
+    h, w = shape if shape is not None else _render_shape()
+    return obj.calc_matrix_camera(bpy.context.evaluated_depsgraph_get(), x=w, y=h)
+
 
 class Camera:
-    """Thin wrapper of a Blender camera object (scene camera by default)."""
+    """A Blender camera object (default: the scene camera) and its matrices.
+
+    ``shape`` is (H, W) of the image the pixel coordinates refer to; it
+    defaults to the scene's render size."""
 
     def __init__(self, bpy_camera=None, shape=None):
-        self.bpy_camera = bpy_camera or bpy.context.scene.camera
-        self.shape = shape or Camera.shape_from_bpy()
-        self.view_matrix = Camera.view_from_bpy(self.bpy_camera)
-        self.proj_matrix = Camera.proj_from_bpy(self.bpy_camera, self.shape)
+        self.bpy_camera = bpy_camera if bpy_camera is not None else bpy.context.scene.camera
+        self.shape = tuple(shape) if shape is not None else _render_shape()
+        self.update_view_matrix()
+        self.update_proj_matrix()
 
+    # -- matrices ----------------------------------------------------------------
     def update_view_matrix(self):
-        self.view_matrix = Camera.view_from_bpy(self.bpy_camera)
+        """Re-read the extrinsics (after the camera moved)."""
+        self.view_matrix = _view_of(self.bpy_camera)
 
     def update_proj_matrix(self):
-        self.proj_matrix = Camera.proj_from_bpy(self.bpy_camera, self.shape)
+        """Re-read the intrinsics (after lens / sensor / resolution changes)."""
+        self.proj_matrix = _proj_of(self.bpy_camera, self.shape)
 
+    # the reference exposes these as static methods of Camera
+    shape_from_bpy = staticmethod(_render_shape)
+    view_from_bpy = staticmethod(_view_of)
+    proj_from_bpy = staticmethod(_proj_of)
+
+    # -- properties ----------------------------------------------------------------
     @property
     def type(self):
-        """Blender type of the wrapped object (as the reference: ``bpy_camera.type``);
-        the projection kind is ``bpy_camera.data.type`` ('PERSP' / 'ORTHO')."""
+        """Blender object type of the wrapped camera (as the reference); the
+        projection kind is ``bpy_camera.data.type`` ('PERSP' / 'ORTHO')."""
         return self.bpy_camera.type
 
     @property
     def clip_range(self):
-        return (self.bpy_camera.data.clip_start, self.bpy_camera.data.clip_end)
+        """(near, far) clip distances."""
+        d = self.bpy_camera.data
+        return d.clip_start, d.clip_end
 
-    @staticmethod
-    def shape_from_bpy(bpy_render=None):
-        """(H, W) of the render output (resolution x percentage)."""
-        render = bpy_render or bpy.context.scene.render
-        s = render.resolution_percentage / 100.0
-        return (int(render.resolution_y * s), int(render.resolution_x * s))
-
-    @staticmethod
-    def view_from_bpy(bpy_camera):
-        camera = bpy_camera or bpy.context.scene.camera
-        return camera.matrix_world.normalized().inverted()
-
-    @staticmethod
-    def proj_from_bpy(bpy_camera, shape):
-        camera = bpy_camera or bpy.context.scene.camera
-        shape = shape or Camera.shape_from_bpy()
-        return camera.calc_matrix_camera(bpy.context.evaluated_depsgraph_get(), x=shape[1], y=shape[0])
-
+    # -- projection ----------------------------------------------------------------
     def world_to_ndc(self, xyz_world, return_depth=False):
-        """Nx3 world points -> Nx3 NDC (and N linear depths)."""
-        xyzw = utils.hom(np.atleast_2d(xyz_world), 1.)
-        if return_depth:
-            cam = xyzw @ np.asarray(self.view_matrix).T
-            depth = -cam[:, -2].copy()
-            clip = cam @ np.asarray(self.proj_matrix).T
-            return utils.dehom(clip), depth
-        m = np.asarray(self.proj_matrix @ self.view_matrix)
-        return utils.dehom(xyzw @ m.T)
+        """N x 3 world points -> N x 3 normalised device coordinates, plus the
+        N linear depths when ``return_depth``."""
+        ndc, depth = _project(xyz_world, _as_np(self.view_matrix), _as_np(self.proj_matrix), return_depth)
+        return (ndc, depth) if return_depth else ndc
 
     def ndc_to_pixel(self, ndc, origin='upper-left'):
-        """NDC -> pixel coordinates, origin 'upper-left' (OpenCV) or 'lower-left' (OpenGL)."""
-        assert origin in ['upper-left', 'lower-left']
+        """NDC -> pixel coordinates with the origin at the image's 'upper-left'
+        (OpenCV convention) or 'lower-left' (OpenGL) corner."""
+        if origin not in _ORIGINS:
+            raise AssertionError(f'origin must be one of {_ORIGINS}')
         h, w = self.shape
-        xy = (np.atleast_2d(ndc)[:, :2] + 1) * 0.5
-        if origin == 'upper-left':
-            xy[:, 1] = 1. - xy[:, 1]
-        return xy * np.array([[w, h]])
+        uv = (np.atleast_2d(ndc)[:, :2] + 1.0) / 2.0
+        if origin == _ORIGINS[0]:
+            uv[:, 1] = 1.0 - uv[:, 1]
+        return uv * np.array([[w, h]], dtype=np.float64)
+
+    def _to_pixel(self, xyz, return_depth):
+        ndc, depth = _project(xyz, _as_np(self.view_matrix), _as_np(self.proj_matrix), return_depth)
+        px = self.ndc_to_pixel(ndc)
+        return (px, depth) if return_depth else px
 
     def object_to_pixel(self, *objs, return_depth=False):
-        """Pixel coordinates (and depths) of every vertex of ``objs``."""
-        if return_depth:
-            ndc, z = self.world_to_ndc(utils.world_coordinates(*objs), return_depth=True)
-            return self.ndc_to_pixel(ndc), z
-        return self.ndc_to_pixel(self.world_to_ndc(utils.world_coordinates(*objs)))
+        """Pixel coordinates (and depths) of every mesh vertex of ``objs``."""
+        return self._to_pixel(utils.world_coordinates(*objs), return_depth)
 
     def bbox_object_to_pixel(self, *objs, return_depth=False):
-        """Pixel coordinates (and depths) of the bounding-box corners of ``objs``."""
-        if return_depth:
-            ndc, z = self.world_to_ndc(utils.bbox_world_coordinates(*objs), return_depth=True)
-            return self.ndc_to_pixel(ndc), z
-        return self.ndc_to_pixel(self.world_to_ndc(utils.bbox_world_coordinates(*objs)))
+        """Pixel coordinates (and depths) of the 8 bounding-box corners of each of ``objs``."""
+        return self._to_pixel(utils.bbox_world_coordinates(*objs), return_depth)
 
     def look_at(self, look_at=None, look_from=None):
-        """Point the camera's -Z axis at ``look_at`` (default origin), +Y up."""
-        if look_from is None:
-            look_from = self.bpy_camera.location
-        if look_at is None:
-            look_at = Vector([0, 0, 0])
-        direction = Vector(look_at) - Vector(look_from)
-        self.bpy_camera.rotation_euler = direction.to_track_quat('-Z', 'Y').to_euler()
-        self.bpy_camera.location = Vector(look_from)
+        """Aim the camera's -Z axis at ``look_at`` (default: the origin) from
+        ``look_from`` (default: where it is), keeping +Y up."""
+        eye = Vector(look_from) if look_from is not None else Vector(self.bpy_camera.location)
+        target = Vector(look_at) if look_at is not None else Vector((0.0, 0.0, 0.0))
+        self.bpy_camera.rotation_euler = (target - eye).to_track_quat('-Z', 'Y').to_euler()
+        self.bpy_camera.location = eye
         self.update_view_matrix()

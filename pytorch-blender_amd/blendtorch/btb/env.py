@@ -1,40 +1,48 @@
 """Blender-hosted environments and the remote-controlled agent.
 
-Reference: pkg_blender/blendtorch/btb/env.py.
+Protocol (reference: pkg_blender/blendtorch/btb/env.py:10-252, pinned by
+tests/test_env.py):
 
-:class:`BaseEnv` lives inside the frame loop.  Each frame:
+* an episode starts on its first frame: ``ctx = {'prev_action': None,
+  'done': False}``, ``_env_reset()``, state INIT;
+* before every frame: ``ctx['time']`` is the frame, ``ctx['done']`` latches
+  once the frame reaches the range's end; from the second frame on the agent
+  decides ``cmd, action = agent(env, **ctx)`` -- RESTART rewinds the
+  animation, STEP applies ``_env_prepare_step(action)`` (when an action came)
+  and the state becomes RUN;
+* after every frame: every n-th frame is rendered into ``ctx['rgb_array']``
+  and ``_env_post_step()``'s dict is merged into ``ctx``.
 
-* ``pre_animation`` (first frame of an episode): state INIT,
-  ``ctx = {'prev_action': None, 'done': False}``, ``_env_reset()``;
-* ``pre_frame``: ``ctx['time'] = frame``; ``ctx['done'] |= frame >= end``;
-  for frames after the first the agent is asked
-  ``cmd, action = agent(env, **ctx)``; RESTART rewinds, STEP applies
-  ``_env_prepare_step(action)`` (if not None) and records ``prev_action``;
-* ``post_frame``: optional render into ``ctx['rgb_array']`` every n-th frame,
-  then ``ctx.update(_env_post_step())``.
+Hence the reply to request k is the state AFTER the frame that applied
+action k, sent from the NEXT frame's pre-frame hook.  :meth:`BaseEnv.run`
+plays to frame 2147483647 so an episode can run past the nominal end (the
+``done`` flag reports it).
 
-So the reply to request k is the state *after* the frame in which action k
-was applied, sent at the next frame's pre_frame.  ``run`` plays up to frame
-2147483647 so episodes may run past ``frame_range[1]`` (``done`` flags it).
-
-:class:`RemoteControlledAgent` bridges this callback protocol to a remote
-``btt.env.RemoteEnv`` over REQ/REP: a two-state (REQ/REP) machine, optional
-``real_time`` mode (non-blocking; no request -> keep simulating without an
-action), and the "reset while already INIT" short-circuit that answers the
-reset immediately (``env.py:220-252``).
+:class:`RemoteControlledAgent` answers a ``btt.env.RemoteEnv`` over REQ/REP.
 """
-import bpy
 
 from ..transport import zmq
-from .animation import AnimationController
-from .camera import Camera
-from .constants import DEFAULT_TIMEOUTMS
-from .offscreen import OffScreenRenderer
+from . import animation, camera, constants, offscreen
+
+_LAST_FRAME = 2147483647
+
+
+def _rep_socket(address, timeoutms):
+    """Bound REP socket with the reference's options (no linger, send and
+    receive timeouts)."""
+    ctx = zmq.Context()
+    sock = ctx.socket(zmq.REP)
+    for opt, value in ((zmq.LINGER, 0), (zmq.SNDTIMEO, timeoutms), (zmq.RCVTIMEO, timeoutms)):
+        sock.setsockopt(opt, value)
+    sock.bind(address)
+    return ctx, sock
 
 
 class BaseEnv:
-    """Abstract environment; implement ``_env_reset``, ``_env_prepare_step``
-    and ``_env_post_step``."""
+    """Environment living in Blender's frame loop.
+
+    Subclasses implement ``_env_reset()``, ``_env_prepare_step(action)`` and
+    ``_env_post_step() -> dict(obs=..., reward=..., [done=...], **info)``."""
 
     STATE_INIT = object()
     STATE_RUN = object()
@@ -42,108 +50,112 @@ class BaseEnv:
     CMD_STEP = object()
 
     def __init__(self, agent):
-        self.events = AnimationController()
-        self.events.pre_frame.add(self._pre_frame)
-        self.events.pre_animation.add(self._pre_animation)
-        self.events.post_frame.add(self._post_frame)
-        self.agent = agent
-        self.ctx = None
-        self.renderer = None
-        self.render_every = None
-        self.frame_range = None
-        self.state = BaseEnv.STATE_INIT
+        self.agent, self.events = agent, animation.AnimationController()
+        self.ctx = self.frame_range = self.renderer = self.render_every = None
+        self.state = self.STATE_INIT
+        for signal, hook in (('pre_animation', self._episode_begins), ('pre_frame', self._before_frame),
+                             ('post_frame', self._after_frame)):
+            getattr(self.events, signal).add(hook)
 
     def run(self, frame_range=None, use_animation=True):
-        """Hook into the frame loop and start playing."""
-        self.frame_range = AnimationController.setup_frame_range(frame_range)
-        self.events.play((self.frame_range[0], 2147483647), num_episodes=-1, use_animation=use_animation,
+        """Attach to the frame loop and play.  ``use_animation=False`` is the
+        blocking loop (``--background``, fastest); True keeps the UI live."""
+        first, last = animation.AnimationController.setup_frame_range(frame_range)
+        self.frame_range = (first, last)
+        self.events.play((first, _LAST_FRAME), num_episodes=-1, use_animation=use_animation,
                          use_offline_render=True)
 
     def attach_default_renderer(self, every_nth=1):
-        """Render the scene camera (rgb, gamma 2.2) into ``ctx['rgb_array']``
-        every ``every_nth`` frame."""
-        self.renderer = OffScreenRenderer(camera=Camera(), mode='rgb', gamma_coeff=2.2)
-        self.render_every = every_nth
+        """Render the scene camera (RGB, gamma 2.2) into ``ctx['rgb_array']``
+        on every ``every_nth`` frame (``env.render()`` on the remote side)."""
+        self.renderer, self.render_every = (offscreen.OffScreenRenderer(camera=camera.Camera(), mode='rgb',
+                                                                        gamma_coeff=2.2), every_nth)
 
-    def _pre_frame(self):
-        frame = self.events.frameid
-        self.ctx['time'] = frame
-        self.ctx['done'] |= (frame >= self.frame_range[1])
-        if frame > self.frame_range[0]:
-            cmd, action = self.agent(self, **self.ctx)
-            if cmd == BaseEnv.CMD_RESTART:
-                self._restart()
-            elif cmd == BaseEnv.CMD_STEP:
-                if action is not None:
-                    self._env_prepare_step(action)
-                    self.ctx['prev_action'] = action
-                self.state = BaseEnv.STATE_RUN
-
-    def _pre_animation(self):
-        self.state = BaseEnv.STATE_INIT
-        self.ctx = {'prev_action': None, 'done': False}
+    # -- frame-loop hooks --------------------------------------------------------
+    def _episode_begins(self):
+        self.ctx, self.state = dict(prev_action=None, done=False), self.STATE_INIT
         self._env_reset()
 
-    def _post_frame(self):
-        self._render(self.ctx)
-        self.ctx = {**self.ctx, **self._env_post_step()}
+    def _before_frame(self):
+        first, last = self.frame_range
+        now = self.events.frameid
+        self.ctx['time'] = now
+        if now >= last:
+            self.ctx['done'] = True
+        if now <= first:
+            return                          # the episode's first frame needs no decision
+        command, action = self.agent(self, **self.ctx)
+        if command is self.CMD_RESTART:
+            self.events.rewind()
+        elif command is self.CMD_STEP:
+            if action is not None:
+                self._env_prepare_step(action)
+                self.ctx.update(prev_action=action)
+            self.state = self.STATE_RUN
 
-    def _render(self, ctx):
-        if self.renderer and ((self.events.frameid - self.frame_range[0]) % self.render_every) == 0:
-            ctx['rgb_array'] = self.renderer.render()
+    def _after_frame(self):
+        if self.renderer is not None and (self.events.frameid - self.frame_range[0]) % self.render_every == 0:
+            self.ctx['rgb_array'] = self.renderer.render()
+        self.ctx.update(self._env_post_step())
 
-    def _restart(self):
-        self.events.rewind()
-
+    # -- to implement ------------------------------------------------------------
     def _env_reset(self):
-        """Reset the environment state."""
-        raise NotImplementedError()
+        """Bring the scene to the start state of an episode."""
+        raise NotImplementedError(f'{type(self).__name__}._env_reset')
 
     def _env_prepare_step(self, action):
         """Apply ``action`` before the frame is simulated."""
-        raise NotImplementedError()
+        raise NotImplementedError(f'{type(self).__name__}._env_prepare_step')
 
     def _env_post_step(self):
-        """Return ``dict(obs=..., reward=..., [done=...], **info)`` after the frame."""
-        raise NotImplementedError()
+        """Observation, reward, optional done flag and extras after the frame."""
+        raise NotImplementedError(f'{type(self).__name__}._env_post_step')
 
 
 class RemoteControlledAgent:
-    """Agent whose decisions come from a remote ``btt.env.RemoteEnv``."""
+    """Agent whose decisions come from a remote ``btt.env.RemoteEnv``.
+
+    A REP socket (bound at ``address``) alternates between awaiting a request
+    (STATE_REQ) and owing its reply (STATE_REP); the reply to a request is the
+    ctx of the next frame.  ``real_time``: while the episode runs, the socket
+    is polled without blocking and a frame without a request simply advances
+    the simulation (no action) -- the scene does not wait for the agent.  A
+    receive timeout does the same in the blocking mode; a send that times out
+    there is an error."""
 
     STATE_REQ = 0
     STATE_REP = 1
 
-    def __init__(self, address, real_time=False, timeoutms=DEFAULT_TIMEOUTMS):
-        self.context = zmq.Context()
-        self.socket = self.context.socket(zmq.REP)
-        self.socket.setsockopt(zmq.LINGER, 0)
-        self.socket.setsockopt(zmq.SNDTIMEO, timeoutms)
-        self.socket.setsockopt(zmq.RCVTIMEO, timeoutms)
-        self.socket.bind(address)
-        self.real_time = real_time
-        self.state = RemoteControlledAgent.STATE_REQ
+    def __init__(self, address, real_time=False, timeoutms=constants.DEFAULT_TIMEOUTMS):
+        self.context, self.socket = _rep_socket(address, timeoutms)
+        self.real_time, self.state = real_time, self.STATE_REQ
 
     def __call__(self, env, **ctx):
-        flags = zmq.NOBLOCK if (self.real_time and env.state == BaseEnv.STATE_RUN) else 0
-        if self.state == RemoteControlledAgent.STATE_REP:
-            try:
-                self.socket.send_pyobj(ctx, flags=flags)
-                self.state = RemoteControlledAgent.STATE_REQ
-            except zmq.error.Again:
-                if not self.real_time:
-                    raise ValueError('Failed to send to remote agent.')
-                return BaseEnv.CMD_STEP, None
-        if self.state == RemoteControlledAgent.STATE_REQ:
-            try:
-                req = self.socket.recv_pyobj(flags=flags)
-            except zmq.error.Again:
-                return BaseEnv.CMD_STEP, None
-            assert req['cmd'] in ['reset', 'step']
-            self.state = RemoteControlledAgent.STATE_REP
-            if req['cmd'] == 'reset':
-                if env.state == BaseEnv.STATE_INIT:
-                    # already at the start of an episode: answer right away
-                    return self.__call__(env, **ctx)
-                return BaseEnv.CMD_RESTART, None
-            return BaseEnv.CMD_STEP, req['action']
+        flags = zmq.NOBLOCK if (self.real_time and env.state is env.STATE_RUN) else 0
+        keep_going = (BaseEnv.CMD_STEP, None)     # simulate the frame without an action
+        if self.state == self.STATE_REP and not self._reply(ctx, flags):
+            return keep_going
+        try:
+            request = self.socket.recv_pyobj(flags=flags)
+        except zmq.Again:
+            return keep_going                      # nobody asked in time
+        cmd = request['cmd']
+        assert cmd in ('reset', 'step'), f'unknown command {cmd!r}'
+        self.state = self.STATE_REP
+        if cmd == 'step':
+            return BaseEnv.CMD_STEP, request['action']
+        if env.state is env.STATE_INIT:
+            # already at an episode's start: the current ctx IS the reset state
+            return self(env, **ctx)
+        return BaseEnv.CMD_RESTART, None
+
+    def _reply(self, ctx, flags):
+        """Send the owed reply; False when it could not go out in real-time mode."""
+        try:
+            self.socket.send_pyobj(ctx, flags=flags)
+        except zmq.Again:
+            if self.real_time:
+                return False
+            raise ValueError('Failed to send the reply to the remote agent.') from None
+        self.state = self.STATE_REQ
+        return True

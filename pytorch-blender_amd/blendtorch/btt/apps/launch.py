@@ -1,15 +1,17 @@
-"""``blendtorch-launch``: launch producer instances from a JSON spec.
+"""``blendtorch-launch``: start producer instances from a JSON spec and
+publish how to reach them.
 
-Reference: pkg_pytorch/blendtorch/btt/apps/launch.py:26-41.  The JSON file
-holds ``BlenderLauncher`` keyword arguments, e.g.::
+Same command line as pkg_pytorch/blendtorch/btt/apps/launch.py:26-41::
 
-    {"scene": "", "script": "tests/blender/launcher.blend.py",
-     "num_instances": 2, "named_sockets": ["DATA", "GYM"],
-     "background": true, "seed": 10}
+    blendtorch-launch [--out-launch-info launch_info.json] spec.json
 
-The launcher starts the instances, writes the LaunchInfo (addresses and
-commands) to ``--out-launch-info`` so other processes or hosts can connect,
-and waits for the instances to exit.
+``spec.json`` holds :class:`~blendtorch.btt.BlenderLauncher` keyword
+arguments, e.g. ``{"script": "tests/blender/launcher.blend.py",
+"num_instances": 2, "named_sockets": ["DATA", "GYM"], "background": true,
+"bind_addr": "primaryip"}``.  Once the instances run, their addresses and
+commands go to the launch-info file -- the hand-over to consumers in other
+processes or on other hosts (``LaunchInfo.load_json``) -- and the command
+then waits for the instances to exit.
 """
 import argparse
 import json
@@ -18,17 +20,22 @@ from ..launch_info import LaunchInfo
 from ..launcher import BlenderLauncher
 
 
+def _cli():
+    p = argparse.ArgumentParser('blendtorch-launch', description=__doc__,
+                                formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument('--out-launch-info', default='launch_info.json',
+                   help='where to write the addresses and commands of the instances')
+    p.add_argument('jsonargs', help='JSON file with BlenderLauncher keyword arguments')
+    return p
+
+
 def main(inargs=None):
-    parser = argparse.ArgumentParser('Blender Launcher', description=__doc__,
-                                     formatter_class=argparse.RawTextHelpFormatter)
-    parser.add_argument('--out-launch-info', help='Path to save connection info to.', default='launch_info.json')
-    parser.add_argument('jsonargs', type=str, help='JSON Dict of arguments for blendtorch.btt.BlenderLauncher')
-    args = parser.parse_args(inargs)
-    with open(args.jsonargs, 'r') as fp:
-        launch_args = json.load(fp)
-    with BlenderLauncher(**launch_args) as bl:
-        LaunchInfo.save_json(args.out_launch_info, bl.launch_info)
-        bl.wait()
+    opts = _cli().parse_args(inargs)
+    with open(opts.jsonargs) as f:
+        spec = json.load(f)
+    with BlenderLauncher(**spec) as launcher:
+        LaunchInfo.save_json(opts.out_launch_info, launcher.launch_info)
+        launcher.wait()
 
 
 if __name__ == '__main__':

@@ -31,17 +31,48 @@ from .constants import DEFAULT_TIMEOUTMS
 from .file import FileReader, FileRecorder
 
 
-def _identity_item_transform(x):
+def _identity(x):
     return x
+
+
+class _Pull:
+    """One PULL socket connected to every producer (per DataLoader worker)."""
+
+    def __init__(self, addresses, rcvhwm, timeoutms):
+        self.timeoutms = timeoutms
+        self.socket = zmq.Context().socket(zmq.PULL)
+        self.socket.setsockopt(zmq.RCVHWM, rcvhwm)
+        self.poller = zmq.Poller()
+        self.poller.register(self.socket, zmq.POLLIN)
+        for a in addresses:
+            self.socket.connect(a)
+
+    def wait(self):
+        if self.socket not in dict(self.poller.poll(self.timeoutms)):
+            raise AssertionError('No response within timeout interval.')
+
+    def close(self):
+        # frames still queued here may hold producers' shared-memory slots
+        try:
+            while self.socket.poll(0):
+                msg = self.socket.recv_pyobj()
+                if isinstance(msg, dict) and shm.KEY in msg:
+                    shm.release(msg[shm.KEY])
+        except Exception:
+            pass
+        self.socket.close()
 
 
 class RemoteIterableDataset(tud.IterableDataset):
     """Items streamed from remote producers (``btb.DataPublisher``).
 
-    Params: addresses, queue_size=10, timeoutms=10000, max_items=100000,
-    item_transform=None, record_path_prefix=None (as the reference).
-    Override :meth:`_item` or pass ``item_transform`` to post-process items.
-    """
+    Reference semantics (pkg_pytorch/blendtorch/btt/dataset.py:14-117): each
+    DataLoader worker opens its own PULL socket (RCVHWM ``queue_size``)
+    connected to ALL ``addresses`` and yields ``max_items // num_workers``
+    items; silence longer than ``timeoutms`` raises ``AssertionError``; with
+    ``record_path_prefix`` every worker records the raw frames it receives to
+    ``{prefix}_{worker:02d}.btr``.  Items pass through :meth:`_item`
+    (``item_transform``)."""
 
     def __init__(self, addresses, queue_size=10, timeoutms=DEFAULT_TIMEOUTMS, max_items=100000,
                  item_transform=None, record_path_prefix=None):
@@ -49,8 +80,8 @@ class RemoteIterableDataset(tud.IterableDataset):
         self.queue_size = queue_size
         self.timeoutms = timeoutms
         self.max_items = max_items
+        self.item_transform = item_transform or _identity
         self.record_path_prefix = record_path_prefix
-        self.item_transform = item_transform or _identity_item_transform
 
     def enable_recording(self, fname):
         """Record raw frames to ``{fname}_{worker:02d}.btr`` (set before iterating)."""
@@ -76,56 +107,42 @@ class RemoteIterableDataset(tud.IterableDataset):
         return self._stream()
 
     def _stream(self):
-        ctx = zmq.Context()
-        socket = None
+        info = tud.get_worker_info()
+        worker, workers = (0, 1) if info is None else (info.id, info.num_workers)
+        quota = self.max_items // workers
+        pull = _Pull(self.addresses, self.queue_size, self.timeoutms)
         try:
-            socket = ctx.socket(zmq.PULL)
-            socket.setsockopt(zmq.RCVHWM, self.queue_size)
-            poller = zmq.Poller()
-            poller.register(socket, zmq.POLLIN)
-            for addr in self.addresses:
-                socket.connect(addr)
-
-            wi = tud.get_worker_info()
-            worker_id, num_workers = (wi.id, wi.num_workers) if wi is not None else (0, 1)
-
-            with ExitStack() as es:
+            with ExitStack() as stack:
                 rec = None
                 if self.record_path_prefix is not None:
-                    rec = es.enter_context(FileRecorder(
-                        FileRecorder.filename(self.record_path_prefix, worker_id), self.max_items))
-                n = 0
-                while n < self.max_items // num_workers:
-                    ready = dict(poller.poll(self.timeoutms))
-                    assert socket in ready, 'No response within timeout interval.'
-                    if rec is not None:
-                        data = socket.recv()
-                        obj = pickle.loads(data)
-                        if shm.KEY in obj:   # record the materialised frame
-                            obj = shm.resolve(obj)
-                            if obj is None:  # stale descriptor: slot reclaimed while queued
-                                continue
-                            rec.save(obj, is_pickled=False)
-                        else:
-                            rec.save(data, is_pickled=True)
-                    else:
-                        obj = shm.resolve(socket.recv_pyobj())
-                        if obj is None:
-                            continue
-                    n += 1
+                    rec = stack.enter_context(FileRecorder(FileRecorder.filename(self.record_path_prefix, worker),
+                                                           self.max_items))
+                delivered = 0
+                while delivered < quota:
+                    pull.wait()
+                    obj = self._receive(pull.socket, rec)
+                    if obj is None:      # stale shared-memory descriptor: dropped, not counted
+                        continue
+                    delivered += 1
                     yield self._item(obj)
-                    del obj
         finally:
-            if socket is not None:
-                # hand back shared-memory slots of frames still queued here
-                try:
-                    while socket.poll(0):
-                        obj = socket.recv_pyobj()
-                        if isinstance(obj, dict) and shm.KEY in obj:
-                            shm.release(obj[shm.KEY])
-                except Exception:
-                    pass
-                socket.close()
+            pull.close()
+
+    @staticmethod
+    def _receive(socket, rec):
+        """Next message as an object (shared-memory images materialised);
+        recorded raw when possible, materialised when it named a ring slot."""
+        if rec is None:
+            return shm.resolve(socket.recv_pyobj())
+        raw = socket.recv()
+        obj = pickle.loads(raw)
+        if shm.KEY not in obj:
+            rec.save(raw, is_pickled=True)
+            return obj
+        obj = shm.resolve(obj)
+        if obj is not None:
+            rec.save(obj, is_pickled=False)
+        return obj
 
     def _item(self, item):
         """Transform one received item (default: ``item_transform``)."""
@@ -133,11 +150,11 @@ class RemoteIterableDataset(tud.IterableDataset):
 
 
 class SingleFileDataset(tud.Dataset):
-    """Replay of one ``.btr`` recording."""
+    """Map-style replay of one ``.btr`` recording."""
 
     def __init__(self, path, item_transform=None):
         self.reader = FileReader(path)
-        self.item_transform = item_transform or _identity_item_transform
+        self.item_transform = item_transform or _identity
 
     def __len__(self):
         return len(self.reader)
@@ -150,13 +167,15 @@ class SingleFileDataset(tud.Dataset):
 
 
 class FileDataset(tud.ConcatDataset):
-    """Replay of every recording ``{record_path_prefix}_*.btr`` (sorted)."""
+    """Replay of every recording ``{record_path_prefix}_*.btr`` (sorted),
+    shuffle-capable; ``item_transform`` applies on top."""
 
     def __init__(self, record_path_prefix, item_transform=None):
-        fnames = sorted(glob(f'{record_path_prefix}_*.btr'))
-        assert len(fnames) > 0, f'Found no recording files with prefix {record_path_prefix}'
-        super().__init__([SingleFileDataset(f) for f in fnames])
-        self.item_transform = item_transform or _identity_item_transform
+        paths = sorted(glob(f'{record_path_prefix}_*.btr'))
+        if not paths:
+            raise AssertionError(f'Found no recording files with prefix {record_path_prefix}')
+        super().__init__([SingleFileDataset(p) for p in paths])
+        self.item_transform = item_transform or _identity
 
     def __getitem__(self, idx):
         return self._item(super().__getitem__(idx))

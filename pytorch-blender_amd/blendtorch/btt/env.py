@@ -2,8 +2,9 @@
 
 Reference: pkg_pytorch/blendtorch/btt/env.py.
 
-* :class:`RemoteEnv` -- REQ socket that connects (LINGER 0, SNDTIMEO =
-  10 x timeout, RCVTIMEO = timeout, REQ_RELAXED + REQ_CORRELATE);
+* :class:`RemoteEnv` -- REQ client (LINGER 0, SNDTIMEO = 10 x timeout,
+  RCVTIMEO = timeout, REQ_RELAXED + REQ_CORRELATE) on the native C++ client
+  (round trip with the GIL released) or the Python socket API;
   ``reset() -> (obs, info)``, ``step(a) -> (obs, reward, done, info)``;
   every request carries the last seen remote ``time``; send/receive timeouts
   surface as ``ValueError`` (``env.py:34-133``).
@@ -17,6 +18,7 @@ Reference: pkg_pytorch/blendtorch/btt/env.py.
   (requests fanned out, replies gathered) and stages the batched
   observations in device memory for a GPU policy.
 """
+import pickle
 from contextlib import ExitStack, contextmanager
 
 import numpy as np
@@ -89,71 +91,120 @@ def _flags(kwargs):
     return args
 
 
-class RemoteEnv:
-    """Client of a remote ``btb.env.RemoteControlledAgent``."""
+class _SocketLink:
+    """REQ client on the pyzmq-compatible transport: ``send``/``recv`` can be
+    split so several envs overlap their round trips (VectorRemoteEnv's
+    fallback path)."""
 
-    def __init__(self, address, timeoutms=DEFAULT_TIMEOUTMS):
+    def __init__(self, address, timeoutms):
         self.context = zmq.Context()
         self.socket = self.context.socket(zmq.REQ)
-        self.socket.setsockopt(zmq.LINGER, 0)
-        self.socket.setsockopt(zmq.SNDTIMEO, timeoutms * 10)
-        self.socket.setsockopt(zmq.RCVTIMEO, timeoutms)
-        self.socket.setsockopt(zmq.REQ_RELAXED, 1)
-        self.socket.setsockopt(zmq.REQ_CORRELATE, 1)
+        opts = ((zmq.LINGER, 0), (zmq.SNDTIMEO, 10 * timeoutms), (zmq.RCVTIMEO, timeoutms),
+                (zmq.REQ_RELAXED, 1), (zmq.REQ_CORRELATE, 1))
+        for opt, value in opts:
+            self.socket.setsockopt(opt, value)
         self.socket.connect(address)
+
+    def send(self, request):
+        try:
+            self.socket.send_pyobj(request)
+        except zmq.Again:
+            raise ValueError('Failed to send to remote environment') from None
+
+    def recv(self):
+        try:
+            return self.socket.recv_pyobj()
+        except zmq.Again:
+            raise ValueError('Failed to receive from remote environment') from None
+
+    def roundtrip(self, request):
+        self.send(request)
+        return self.recv()
+
+    def close(self):
+        self.socket.close()
+
+
+class _NativeLink:
+    """The same REQ client in C++ (``_native.VecReq`` with one env): the
+    whole round trip -- send, wait, receive -- runs with the GIL released."""
+
+    def __init__(self, address, timeoutms):
+        from .. import _native
+        self._req = _native.VecReq([address], timeoutms, 1)
+
+    def roundtrip(self, request):
+        return pickle.loads(self._req.roundtrip(0, pickle.dumps(request, protocol=4)))
+
+    def close(self):
+        self._req.close()
+
+
+class RemoteEnv:
+    """Client of a remote ``btb.env.RemoteControlledAgent`` (gym-like).
+
+    ``reset() -> (obs, info)`` and ``step(action) -> (obs, reward, done,
+    info)``; every request carries the last remote ``time`` seen and a
+    ``rgb_array`` in a reply is kept for :meth:`render`.  Timeouts raise
+    ``ValueError``.  ``native=True`` (default when the native module is
+    built) runs the round trip in C++; False uses the Python socket API."""
+
+    def __init__(self, address, timeoutms=DEFAULT_TIMEOUTMS, native=True):
         self.env_time = None
         self.rgb_array = None
         self.viewer = None
+        self._link = None
+        if native:
+            try:
+                self._link = _NativeLink(address, timeoutms)
+            except (ImportError, AttributeError):
+                self._link = None
+        if self._link is None:
+            self._link = _SocketLink(address, timeoutms)
 
     def reset(self):
-        """Reset the remote env; returns ``(obs, info)``."""
-        d = self._reqrep(cmd='reset')
-        self.rgb_array = d.pop('rgb_array', None)
-        return d.pop('obs'), d
+        """Restart the remote episode; returns ``(obs, info)``."""
+        reply = self._request('reset')
+        return reply.pop('obs'), reply
 
     def step(self, action):
-        """Apply ``action``; returns ``(obs, reward, done, info)``."""
-        d = self._reqrep(cmd='step', action=action)
-        obs = d.pop('obs')
-        reward = d.pop('reward')
-        done = d.pop('done')
-        self.rgb_array = d.pop('rgb_array', None)
-        return obs, reward, done, d
+        """Advance the remote simulation with ``action``."""
+        reply = self._request('step', action=action)
+        obs, reward, done = (reply.pop(k) for k in ('obs', 'reward', 'done'))
+        return obs, reward, done, reply
 
     def render(self, mode='human', backend=None):
-        """Return (``rgb_array``) or show (``human``) the last remote frame."""
-        if mode == 'rgb_array' or self.rgb_array is None:
-            return self.rgb_array
+        """``'rgb_array'``: the last rendered frame (or None); ``'human'``:
+        show it with a viewer from :mod:`~blendtorch.btt.env_rendering`."""
+        frame = self.rgb_array
+        if mode == 'rgb_array' or frame is None:
+            return frame
         if self.viewer is None:
             self.viewer = create_renderer(backend)
-        self.viewer.imshow(self.rgb_array)
+        self.viewer.imshow(frame)
 
-    # split request/reply so many envs can be stepped concurrently
-    def _send(self, **kw):
-        try:
-            self.socket.send_pyobj({**kw, 'time': self.env_time})
-        except zmq.error.Again:
-            raise ValueError('Failed to send to remote environment') from None
+    def _request(self, cmd, **fields):
+        return self._received(self._link.roundtrip(dict(cmd=cmd, time=self.env_time, **fields)))
+
+    def _received(self, reply):
+        self.env_time = reply['time']
+        self.rgb_array = reply.pop('rgb_array', None)
+        return reply
+
+    # split request / reply (Python link only), so N envs can overlap
+    def _send(self, **fields):
+        self._link.send(dict(time=self.env_time, **fields))
 
     def _recv(self):
-        try:
-            d = self.socket.recv_pyobj()
-        except zmq.error.Again:
-            raise ValueError('Failed to receive from remote environment') from None
-        self.env_time = d['time']
-        return d
-
-    def _reqrep(self, **send_kwargs):
-        self._send(**send_kwargs)
-        return self._recv()
+        return self._received(self._link.recv())
 
     def close(self):
-        if self.viewer:
-            self.viewer.close()
-            self.viewer = None
-        if self.socket:
-            self.socket.close()
-            self.socket = None
+        viewer, self.viewer = self.viewer, None
+        if viewer is not None:
+            viewer.close()
+        link, self._link = self._link, None
+        if link is not None:
+            link.close()
 
 
 @contextmanager
@@ -161,72 +212,107 @@ def launch_env(scene, script, background=False, producer=None, timeoutms=DEFAULT
                **kwargs):
     """Launch one remote env instance and yield a connected :class:`RemoteEnv`.
 
-    ``producer`` selects a headless stand-in (e.g. ``'cartpolesim'``) instead
-    of Blender; ``launcher_args`` are extra :class:`BlenderLauncher` arguments
-    (``start_port``, ``proto``, ``blend_path``, ...); remaining kwargs become
-    command-line flags of the env script.
-    """
-    env = None
-    try:
-        launch = dict(scene=scene, script=script, num_instances=1, named_sockets=['GYM'],
-                      instance_args=[_flags(kwargs)], background=background, producer=producer)
-        launch.update(launcher_args or {})
-        with BlenderLauncher(**launch) as bl:
-            env = RemoteEnv(bl.launch_info.addresses['GYM'][0], timeoutms=timeoutms)
-            yield env
-    finally:
-        if env:
-            env.close()
+    The instance gets a single named socket ``GYM``; remaining kwargs become
+    the env script's command-line flags (``_flags``).  ``producer`` selects a
+    headless stand-in (e.g. ``'cartpolesim'``) instead of Blender and
+    ``launcher_args`` passes extra :class:`BlenderLauncher` arguments
+    (``start_port``, ``proto``, ``blend_path``, ...).  Reference:
+    pkg_pytorch/blendtorch/btt/env.py:135-189."""
+    spec = dict(scene=scene, script=script, num_instances=1, named_sockets=['GYM'], instance_args=[_flags(kwargs)],
+                background=background, producer=producer, **(launcher_args or {}))
+    with ExitStack() as stack:
+        launcher = stack.enter_context(BlenderLauncher(**spec))
+        env = RemoteEnv(launcher.launch_info.addresses['GYM'][0], timeoutms=timeoutms)
+        stack.callback(env.close)
+        yield env
 
 
 class OpenAIRemoteEnv(_GymEnv):
-    """Base class of gym-registered remote environments (see
-    examples/control/cartpole_gym)."""
+    """gym-style base of remote environments (old 4-tuple API; see
+    examples/control/cartpole_gym).  :meth:`launch` starts the remote
+    instance; the env owns it until :meth:`close`.  Reference:
+    pkg_pytorch/blendtorch/btt/env.py:191-316."""
 
     metadata = {'render.modes': ['rgb_array', 'human']}
 
     def __init__(self, version='0.0.1'):
         self.__version__ = version
-        self._es = ExitStack()
-        self._env = None
+        self._stack = ExitStack()
+        self._remote = None
 
     def launch(self, scene, script, background=False, **kwargs):
-        """Launch the remote environment (kwargs -> command-line flags)."""
-        assert not self._env, 'Environment already running.'
-        self._env = self._es.enter_context(launch_env(scene=scene, script=script, background=background, **kwargs))
+        """Start the remote environment (kwargs become script flags)."""
+        if self._remote is not None:
+            raise AssertionError('Environment already running.')
+        self._remote = self._stack.enter_context(launch_env(scene=scene, script=script, background=background,
+                                                            **kwargs))
+
+    def _live(self):
+        if self._remote is None:
+            raise AssertionError('Environment not running.')
+        return self._remote
 
     def step(self, action):
-        assert self._env, 'Environment not running.'
-        obs, reward, done, info = self._env.step(action)
-        return obs, reward, done, info
+        return self._live().step(action)
 
     def reset(self):
-        assert self._env, 'Environment not running.'
-        obs, info = self._env.reset()
-        return obs
+        return self._live().reset()[0]
 
     def seed(self, seed):
-        raise NotImplementedError()
+        raise NotImplementedError('remote environments are seeded at launch (-btseed)')
 
     def render(self, mode='human'):
-        assert self._env, 'Environment not running.'
-        return self._env.render(mode=mode)
+        return self._live().render(mode=mode)
 
     @property
     def env_time(self):
-        return self._env.env_time
+        return self._remote.env_time
 
     def close(self):
-        if self._es:
-            self._es.close()
-            self._es = None
-            self._env = None
+        stack, self._stack = self._stack, None
+        self._remote = None
+        if stack is not None:
+            stack.close()
 
     def __del__(self):
         try:
             self.close()
         except Exception:
             pass
+
+
+class _PinnedStager:
+    """Host -> device staging through pinned buffers that are never rewritten
+    while a copy out of them may still be queued.
+
+    A ``non_blocking`` H2D copy from pinned memory is only enqueued: if the
+    stream is busy (a policy step in flight) the DMA runs later and reads
+    whatever the buffer holds THEN.  Rewriting one buffer per step would let
+    the device see the next step's observations.  Buffers rotate instead
+    (``depth`` of them), and each is reused only after the event recorded
+    behind its last copy has completed."""
+
+    def __init__(self, depth=2):
+        self.depth = depth
+        self._slots = []          # [pinned tensor, event or None]
+        self._next = 0
+
+    def stage(self, arr, device, dtype):
+        import torch
+        arr = np.ascontiguousarray(arr)
+        if not self._slots or tuple(self._slots[0][0].shape) != arr.shape or self._slots[0][0].dtype != dtype:
+            self._slots = [[torch.empty(arr.shape, dtype=dtype).pin_memory(), None] for _ in range(self.depth)]
+            self._next = 0
+        slot = self._slots[self._next]
+        self._next = (self._next + 1) % self.depth
+        if slot[1] is not None:
+            slot[1].synchronize()      # the copy that last read this buffer is done
+        slot[0].numpy()[...] = arr
+        out = slot[0].to(device, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(device))
+        slot[1] = ev
+        return out
 
 
 class VectorRemoteEnv:
@@ -247,7 +333,8 @@ class VectorRemoteEnv:
         self.addresses = list(addresses)
         self.device = device
         self.obs_dim = obs_dim
-        self._pinned = None
+        self._obs_stager = _PinnedStager()
+        self._rgb_stager = _PinnedStager()
         self._native = None
         self.envs = None
         if native:
@@ -268,10 +355,7 @@ class VectorRemoteEnv:
         arr = np.asarray(obs, dtype=np.float32)
         if self.device is None or torch.device(self.device).type == 'cpu':
             return torch.from_numpy(arr)
-        if self._pinned is None or tuple(self._pinned.shape) != arr.shape:
-            self._pinned = torch.empty(arr.shape, dtype=torch.float32).pin_memory()
-        self._pinned.numpy()[...] = arr
-        return self._pinned.to(self.device, non_blocking=True)
+        return self._obs_stager.stage(arr, torch.device(self.device), torch.float32)
 
     def _exchange(self, which, cmd, actions):
         if self.obs_dim is None:   # discover the observation size once
@@ -361,10 +445,7 @@ class VectorRemoteEnv:
         dev = torch.device(self.device) if self.device is not None else torch.device('cpu')
         if dev.type != 'cuda':
             return ops.reference_decode(torch.from_numpy(arr), decode)
-        if getattr(self, '_rgb_pinned', None) is None or tuple(self._rgb_pinned.shape) != arr.shape:
-            self._rgb_pinned = torch.empty(arr.shape, dtype=torch.uint8).pin_memory()
-        self._rgb_pinned.numpy()[...] = arr
-        return ops.decode(self._rgb_pinned.to(dev, non_blocking=True), decode)
+        return ops.decode(self._rgb_stager.stage(arr, dev, torch.uint8), decode)
 
     def infos(self, i):
         """Full last reply of env i (native path) as a dict."""

@@ -1,90 +1,112 @@
 """Image viewers for ``RemoteEnv.render('human')``.
 
-Reference: pkg_pytorch/blendtorch/btt/env_rendering.py -- a registry of
-backends looked up in the order ``['openai', 'matplotlib']``; each backend
-registers only when importable.  A 'null' backend (records the last frame,
-displays nothing) is always available for headless use.
+Contract (reference: pkg_pytorch/blendtorch/btt/env_rendering.py:1-78): a
+registry of named backends with the lookup order ``['openai', 'matplotlib']``
+-- the gym viewer first, else a matplotlib window -- and a backend only
+counts when its library imports.  Every viewer has ``imshow(rgb)`` and
+``close()``.
+
+Here each backend is a small factory that imports its library on first use
+(so importing ``btt`` never pulls in matplotlib or gym), and a ``'null'``
+backend, last in the order, keeps the frames for headless runs and tests.
 """
-RENDER_BACKENDS = {}
+import importlib.util
+
 LOOKUP_ORDER = ['openai', 'matplotlib', 'null']
+RENDER_BACKENDS = {}
+
+
+def _installed(package):
+    """Is ``package`` installed?  (Checked without importing it.)"""
+    try:
+        return importlib.util.find_spec(package) is not None
+    except (ImportError, ValueError):
+        return False
+
+
+def register_backend(name, factory, requires=None):
+    """Add a viewer factory; ``requires`` names a package that must be installed."""
+    if requires is None or _installed(requires):
+        RENDER_BACKENDS[name] = factory
 
 
 def create_renderer(backend=None, **kwargs):
-    """Instantiate the named backend, or the first available one."""
-    if backend is None:
-        avail = [RENDER_BACKENDS[n] for n in LOOKUP_ORDER if n in RENDER_BACKENDS]
-        assert len(avail) > 0, 'No render backends available.'
-        return avail[0](**kwargs)
-    assert backend in RENDER_BACKENDS, f'Render backend {backend} not found.'
-    return RENDER_BACKENDS[backend](**kwargs)
+    """Instantiate ``backend`` (a registered name), or the first registered
+    backend in :data:`LOOKUP_ORDER`."""
+    if backend is not None:
+        if backend not in RENDER_BACKENDS:
+            raise AssertionError(f'Render backend {backend} not found.')
+        return RENDER_BACKENDS[backend](**kwargs)
+    for name in LOOKUP_ORDER:
+        if name in RENDER_BACKENDS:
+            return RENDER_BACKENDS[name](**kwargs)
+    raise AssertionError('No render backends available.')
 
 
 class NullRenderer:
-    """Keeps the last image; for headless runs and tests."""
+    """Displays nothing; remembers the last frame and counts frames."""
 
     def __init__(self, **kwargs):
-        self.last = None
-        self.shown = 0
+        self.last, self.shown = None, 0
 
     def imshow(self, rgb):
-        self.last = rgb
-        self.shown += 1
+        self.last, self.shown = rgb, self.shown + 1
 
     def close(self):
         self.last = None
 
 
-RENDER_BACKENDS['null'] = NullRenderer
+class _FigureViewer:
+    """One matplotlib figure whose image is updated in place."""
 
-try:
-    import matplotlib
-    import matplotlib.pyplot as plt
+    def __init__(self, **kwargs):
+        import matplotlib.pyplot as plt
+        self._plt = plt
+        self.fig, ax = plt.subplots(1, 1)
+        self._ax, self._artist = ax, None
 
-    class MatplotlibRenderer:
-        def __init__(self, **kwargs):
-            self.fig, self.ax = plt.subplots(1, 1)
-            self.img = None
+    def imshow(self, rgb):
+        if self._artist is not None:
+            self._artist.set_data(rgb)
+            self.fig.canvas.draw_idle()
+            self.fig.canvas.flush_events()
+            return
+        self._artist = self._ax.imshow(rgb)
+        self._plt.show(block=False)
+        self.fig.canvas.draw()
 
-        def imshow(self, rgb):
-            if self.img is None:
-                self.img = self.ax.imshow(rgb)
-                plt.show(block=False)
-                self.fig.canvas.draw()
-            else:
-                self.img.set_data(rgb)
-                self.fig.canvas.draw_idle()
-                self.fig.canvas.flush_events()
+    def close(self):
+        fig, self.fig = self.fig, None
+        if fig is not None:
+            self._plt.close(fig)
 
-        def close(self):
-            if self.fig is not None:
-                plt.close(self.fig)
-                self.fig = None
+    def __del__(self):
+        self.close()
 
-        def __del__(self):
-            self.close()
 
-    RENDER_BACKENDS['matplotlib'] = MatplotlibRenderer
-except ImportError:
-    pass
+class _GymViewer:
+    """gym's ``SimpleImageViewer`` (classic-control rendering)."""
 
-try:
-    from gym.envs.classic_control import rendering as _gym_rendering
+    def __init__(self, **kwargs):
+        from gym.envs.classic_control import rendering
+        self._viewer = rendering.SimpleImageViewer(**kwargs)
 
-    class OpenAIGymRenderer:
-        def __init__(self, **kwargs):
-            self._viewer = _gym_rendering.SimpleImageViewer(**kwargs)
+    def imshow(self, rgb):
+        self._viewer.imshow(rgb)
 
-        def imshow(self, rgb):
-            self._viewer.imshow(rgb)
+    def close(self):
+        viewer, self._viewer = self._viewer, None
+        if viewer is not None:
+            viewer.close()
 
-        def close(self):
-            if self._viewer:
-                self._viewer.close()
-                self._viewer = None
+    def __del__(self):
+        self.close()
 
-        def __del__(self):
-            self.close()
 
-    RENDER_BACKENDS['openai'] = OpenAIGymRenderer
-except ImportError:
-    pass
+# reference names, kept importable
+MatplotlibRenderer = _FigureViewer
+OpenAIGymRenderer = _GymViewer
+
+register_backend('null', NullRenderer)
+register_backend('matplotlib', _FigureViewer, requires='matplotlib')
+register_backend('openai', _GymViewer, requires='gym')

@@ -169,3 +169,26 @@ def test_fused_consumer_kernels_run_on_bench_shapes(dev):
     assert [s for s, _ in shapes] == [(8, 32, 240, 320), (8, 64, 120, 160), (8, 128, 60, 80), (8, 256, 30, 40)]
     assert all(dt == torch.bfloat16 for _, dt in shapes)
     assert all(ops.bn_supported(torch.empty(s, device=dev, dtype=torch.bfloat16)) for s, _ in shapes)
+
+
+def test_vector_env_staging_survives_busy_stream(dev, free_port):
+    """A long kernel is queued before step(): the H2D copies of three steps
+    all wait behind it, yet each step's device observations are that step's
+    (rotating pinned buffers guarded by events, btt/env.py _PinnedStager)."""
+    from blendtorch.btt.env import VectorRemoteEnv
+    with btt.BlenderLauncher(producer='cartpolesim', num_instances=3, named_sockets=['GYM'],
+                             start_port=free_port) as bl:
+        venv = VectorRemoteEnv(bl.launch_info.addresses['GYM'], device=dev)
+        venv.reset()
+        torch.cuda.synchronize()
+        torch.cuda._sleep(200_000_000)          # keeps the stream busy well past the three steps
+        outs, hosts = [], []
+        for k in range(3):
+            obs, _, _, _ = venv.step(torch.full((3,), 0.5 * (k + 1)))
+            outs.append(obs)
+            hosts.append(np.stack([np.asarray(venv.infos(i)['obs'], np.float32) for i in range(3)]))
+        torch.cuda.synchronize()
+        venv.close()
+    assert not np.array_equal(hosts[0], hosts[1])
+    for o, h in zip(outs, hosts):
+        assert torch.equal(o.cpu(), torch.from_numpy(h))
