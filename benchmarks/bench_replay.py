@@ -28,6 +28,9 @@ def main():
     ap.add_argument('--fill', choices=['producers', 'synthetic'], default='synthetic')
     ap.add_argument('--dtype', choices=['float32', 'bfloat16'], default='float32')
     ap.add_argument('--graph', action='store_true', help='replay a HIP-graph-captured sampler')
+    ap.add_argument('--sampler', choices=['fused', 'legacy'], default='fused',
+                    help='fused: ONE launch (Philox draw + gather + decode + metadata); legacy: randint, '
+                         'decode_gather and one index_select per metadata key (the round-1 path)')
     a = ap.parse_args()
 
     import torch
@@ -52,7 +55,16 @@ def main():
     torch.cuda.synchronize()
     fill_s = time.perf_counter() - t0
     cfg = ops.DecodeConfig.unit(channels='rgb', gamma=2.2, dtype=a.dtype)
-    sample = rb.graphed_sampler(a.batch, cfg) if a.graph else (lambda: rb.sample(a.batch, cfg))
+    def legacy():
+        idx = torch.randint(0, len(rb), (a.batch,), device=dev)
+        out = {'image': ops.decode_gather(rb.store, idx, cfg), 'index': idx}
+        out.update({k: v.index_select(0, idx) for k, v in rb.meta.items()})
+        return out
+
+    if a.sampler == 'legacy':
+        sample = legacy
+    else:
+        sample = rb.graphed_sampler(a.batch, cfg) if a.graph else (lambda: rb.sample(a.batch, cfg))
     for _ in range(a.warmup):
         sample()
     torch.cuda.synchronize()
@@ -61,7 +73,11 @@ def main():
         b = sample()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    H, W, C = rb.frame_shape
+    moved = a.batch * H * W * (C + cfg.cout * (4 if a.dtype == 'float32' else 2))   # bytes read + written
     print(json.dumps({'metric': 'replay images/s (HBM store -> gather+decode)', 'value': round(a.steps * a.batch / dt, 1),
+                      'sampler': a.sampler, 'us_per_batch': round(dt / a.steps * 1e6, 2),
+                      'effective_tbps': round(moved * a.steps / dt / 1e12, 3),
                       'unit': 'images/s', 'batch': a.batch, 'frames': a.frames, 'store_gb': round(rb.nbytes / 1e9, 2),
                       'fill': a.fill, 'fill_s': round(fill_s, 2), 'ms_per_batch': round(dt / a.steps * 1e3, 4),
                       'dtype': a.dtype, 'graph': a.graph, 'out_shape': list(b['image'].shape)}), flush=True)

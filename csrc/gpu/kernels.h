@@ -87,6 +87,37 @@ struct TileParams {
 };
 hipError_t decode_tiles(const DecodeParams& p, const TileParams& t, hipStream_t stream);
 
+// Fused replay sample (DeviceReplayBuffer.sample / gather) in ONE launch:
+//   * draw B frame indices in [0, count) on the device with Philox4x32-10
+//     (key = seed, counter = (b, C)).  C is ctr_value (eager callers keep the
+//     count on the host: one launch), or *counter when counter != nullptr --
+//     then a one-lane kernel queued behind the sample advances *counter by B,
+//     so a captured HIP graph draws fresh indices on every replay;
+//     or take the indices from index_in (gather of given frames);
+//   * decode frame idx[b] of the HBM-resident u8 store (p.src, stride
+//     frame_bytes) exactly as decode() does (p.lut, cmap, dtype, layout,
+//     flip_all) into the dense output p.dst;
+//   * copy row idx[b] of every fixed-size metadata column (meta_src[k]:
+//     [capacity, meta_bytes[k]]) to meta_dst[k][b].
+// p.B <= kMaxReplayB.  counter: nullable device u64 (Philox counter);
+// index_out (nullable) receives the int64 indices.
+constexpr int kMaxReplayB = 1024;
+constexpr int kMaxMeta = 8;
+struct ReplayParams {
+  int64_t count = 0;
+  int64_t frame_bytes = 0;
+  uint64_t seed = 0;
+  uint64_t* counter = nullptr;
+  uint64_t ctr_value = 0;
+  const int64_t* index_in = nullptr;
+  int64_t* index_out = nullptr;
+  int nmeta = 0;
+  const uint8_t* meta_src[kMaxMeta] = {};
+  uint8_t* meta_dst[kMaxMeta] = {};
+  int meta_bytes[kMaxMeta] = {};
+};
+hipError_t replay_sample(const DecodeParams& p, const ReplayParams& r, hipStream_t stream);
+
 // Per-pixel affine colour transform on the MFMA units:
 //   out[b, c, y, x] = sum_k M[c][k] * lut[k][in[b, y, x, k]] + bias[c]
 // for RGBA u8 HWC input (Cin = 4), f32 NCHW output with Cout <= 4 channels;

@@ -446,6 +446,188 @@ hipError_t decode_tiles(const DecodeParams& p, const TileParams& t, hipStream_t 
 }
 
 // ---------------------------------------------------------------------------
+// fused replay sample: Philox index draw + gather + decode + metadata gather
+// ---------------------------------------------------------------------------
+namespace {
+
+// Philox4x32-10 (Salmon et al., SC'11), first output word.
+__device__ __forceinline__ uint32_t philox_word(uint64_t seed, uint64_t ctr, uint32_t b) {
+  uint32_t c0 = b, c1 = uint32_t(ctr), c2 = uint32_t(ctr >> 32), c3 = 0;
+  uint32_t k0 = uint32_t(seed), k1 = uint32_t(seed >> 32);
+#pragma unroll
+  for (int round = 0; round < 10; ++round) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    c0 = hi1 ^ c1 ^ k0;
+    c1 = lo1;
+    c2 = hi0 ^ c3 ^ k1;
+    c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c0;
+}
+
+// Block prologue shared by both replay kernels: the table, this launch's B
+// frame indices (drawn or given) in LDS, and the counter hand-over.
+struct ReplayShared {
+  float lut[4 * 256];
+  int64_t idx[kMaxReplayB];
+  uint64_t ctr;
+};
+
+__device__ void replay_prologue(const DecodeParams& p, const ReplayParams& r, ReplayShared& sh) {
+  for (int i = threadIdx.x; i < p.Cout * 256; i += kBlock) sh.lut[i] = p.lut[i];
+  if (threadIdx.x == 0) sh.ctr = r.index_in ? 0 : (r.counter ? r.counter[0] : r.ctr_value);
+  __syncthreads();
+  for (int b = threadIdx.x; b < p.B; b += kBlock) {
+    const int64_t i = r.index_in ? r.index_in[b]
+                                 : int64_t((uint64_t(philox_word(r.seed, sh.ctr, uint32_t(b))) * uint64_t(r.count)) >> 32);
+    sh.idx[b] = i;
+    if (blockIdx.x == 0 && r.index_out) r.index_out[b] = i;
+  }
+  __syncthreads();
+}
+
+// The counter moves on in a one-lane kernel queued right behind the sample:
+// every block of the sample reads it, so no block may advance it in-kernel
+// without a grid-wide handshake -- and a per-block atomic (or fence) on one
+// address serialises thousands of blocks (measured 68 -> 517 us).
+__global__ void replay_advance_kernel(uint64_t* counter, int B) { counter[0] += uint64_t(B); }
+
+// metadata unit m of the launch: 4-byte words of 4-byte-multiple columns,
+// single bytes otherwise
+__device__ __forceinline__ void replay_meta(const ReplayParams& r, const ReplayShared& sh, int B, int64_t m) {
+  for (int k = 0; k < r.nmeta; ++k) {
+    const int nb = r.meta_bytes[k];
+    const int w = (nb % 4 == 0) ? 4 : 1;
+    const int64_t per = nb / w, units = per * B;
+    if (m < units) {
+      const int b = int(m / per);
+      const int64_t j = (m - int64_t(b) * per) * w;
+      const uint8_t* s = r.meta_src[k] + sh.idx[b] * nb + j;
+      uint8_t* d = r.meta_dst[k] + int64_t(b) * nb + j;
+      if (w == 4) *reinterpret_cast<uint32_t*>(d) = *reinterpret_cast<const uint32_t*>(s);
+      else *d = *s;
+      return;
+    }
+    m -= units;
+  }
+}
+
+template <int PPT, int CIN, int OUTT, int LAYOUT>
+__global__ __launch_bounds__(kBlock) void replay_vec_kernel(DecodeParams p, ReplayParams r, int64_t meta_units) {
+  __shared__ ReplayShared sh;
+  replay_prologue(p, r, sh);
+  const int64_t HW = int64_t(p.H) * p.W;
+  const int64_t groups_per_img = HW / PPT;
+  const int64_t groups = groups_per_img * p.B;
+  const int cout = p.Cout;
+  int cm[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) cm[c] = p.cmap[c];
+  const int64_t stride = int64_t(gridDim.x) * kBlock;
+  for (int64_t g = int64_t(blockIdx.x) * kBlock + threadIdx.x; g < groups + meta_units; g += stride) {
+    if (g >= groups) {
+      replay_meta(r, sh, p.B, g - groups);
+      continue;
+    }
+    Group gr;
+    gr.b = int(g / groups_per_img);
+    gr.q = (g - int64_t(gr.b) * groups_per_img) * PPT;
+    const int y = int(gr.q / p.W), x = int(gr.q - int64_t(y) * p.W);
+    const int sy = p.flip_all ? p.H - 1 - y : y;
+    gr.src = p.src + sh.idx[gr.b] * r.frame_bytes + (int64_t(sy) * p.W + x) * CIN;
+    Pixels<PPT, CIN> px;
+    load_pixels<PPT, CIN>(gr.src, px);
+    emit<PPT, CIN, OUTT, LAYOUT>(p, sh.lut, cm, cout, HW, gr, px);
+  }
+}
+
+// any shape / alignment: one pixel per lane
+template <int OUTT>
+__global__ __launch_bounds__(kBlock) void replay_scalar_kernel(DecodeParams p, ReplayParams r, int64_t meta_units) {
+  __shared__ ReplayShared sh;
+  replay_prologue(p, r, sh);
+  const int64_t HW = int64_t(p.H) * p.W;
+  const int64_t total = HW * p.B;
+  const int64_t ie = HW * p.Cout;
+  for (int64_t g = int64_t(blockIdx.x) * kBlock + threadIdx.x; g < total + meta_units; g += int64_t(gridDim.x) * kBlock) {
+    if (g >= total) {
+      replay_meta(r, sh, p.B, g - total);
+      continue;
+    }
+    const int b = int(g / HW);
+    const int64_t q = g - int64_t(b) * HW;
+    const int y = int(q / p.W), x = int(q - int64_t(y) * p.W);
+    const int sy = p.flip_all ? p.H - 1 - y : y;
+    const uint8_t* s = p.src + sh.idx[b] * r.frame_bytes + (int64_t(sy) * p.W + x) * p.Cin;
+    for (int c = 0; c < p.Cout; ++c) {
+      const float v = sh.lut[c * 256 + s[p.cmap[c]]];
+      const int64_t off = p.layout == NCHW ? int64_t(c) * HW + q : q * p.Cout + c;
+      if constexpr (OUTT == OUT_F32) reinterpret_cast<float*>(p.dst)[int64_t(b) * ie + off] = v;
+      else if constexpr (OUTT == OUT_BF16) reinterpret_cast<uint16_t*>(p.dst)[int64_t(b) * ie + off] = f2bf(v);
+      else if constexpr (OUTT == OUT_F16) reinterpret_cast<uint16_t*>(p.dst)[int64_t(b) * ie + off] = f2h(v);
+      else reinterpret_cast<uint8_t*>(p.dst)[int64_t(b) * ie + off] = uint8_t(v);
+    }
+  }
+}
+
+template <int OUTT>
+hipError_t launch_replay(const DecodeParams& p, const ReplayParams& r, int64_t meta_units, hipStream_t s) {
+  constexpr int PPT = OUTT == OUT_F32 ? 4 : (OUTT == OUT_U8 ? 16 : 8);
+  const bool vec = (p.W % PPT) == 0 && r.frame_bytes % 16 == 0 && (p.Cin == 3 || p.Cin == 4) &&
+                   (reinterpret_cast<uintptr_t>(p.src) % 16) == 0 && (reinterpret_cast<uintptr_t>(p.dst) % 16) == 0 &&
+                   (int64_t(p.H) * p.W * p.Cin) % 16 == 0;
+  if (vec) {
+    const int grid = grid_for(int64_t(p.B) * p.H * p.W / PPT + meta_units, p.max_grid);
+#define BT_REPLAY(CIN, LAY) replay_vec_kernel<PPT, CIN, OUTT, LAY><<<grid, kBlock, 0, s>>>(p, r, meta_units)
+    if (p.Cin == 4) {
+      if (p.layout == NCHW) BT_REPLAY(4, NCHW);
+      else BT_REPLAY(4, NHWC);
+    } else {
+      if (p.layout == NCHW) BT_REPLAY(3, NCHW);
+      else BT_REPLAY(3, NHWC);
+    }
+#undef BT_REPLAY
+  } else {
+    replay_scalar_kernel<OUTT><<<grid_for(int64_t(p.B) * p.H * p.W + meta_units, p.max_grid), kBlock, 0, s>>>(
+        p, r, meta_units);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t replay_sample(const DecodeParams& p, const ReplayParams& r, hipStream_t stream) {
+  if (p.B <= 0) return hipSuccess;
+  if (p.B > kMaxReplayB || p.H <= 0 || p.W <= 0 || p.Cin < 1 || p.Cin > 4 || p.Cout < 1 || p.Cout > 4 || !p.src ||
+      !p.dst || !p.lut || r.frame_bytes != int64_t(p.H) * p.W * p.Cin || r.nmeta < 0 || r.nmeta > kMaxMeta)
+    return hipErrorInvalidValue;
+  if (!r.index_in && (r.count < 1 || r.count > (int64_t(1) << 32))) return hipErrorInvalidValue;
+  for (int c = 0; c < p.Cout; ++c)
+    if (p.cmap[c] < 0 || p.cmap[c] >= p.Cin) return hipErrorInvalidValue;
+  int64_t meta_units = 0;
+  for (int k = 0; k < r.nmeta; ++k) {
+    const int nb = r.meta_bytes[k];
+    if (nb <= 0 || !r.meta_src[k] || !r.meta_dst[k]) return hipErrorInvalidValue;
+    if (nb % 4 == 0 && ((reinterpret_cast<uintptr_t>(r.meta_src[k]) | reinterpret_cast<uintptr_t>(r.meta_dst[k])) % 4))
+      return hipErrorInvalidValue;
+    meta_units += int64_t(p.B) * (nb % 4 == 0 ? nb / 4 : nb);
+  }
+  hipError_t e = hipErrorInvalidValue;
+  switch (p.out_dtype) {
+    case OUT_F32: e = launch_replay<OUT_F32>(p, r, meta_units, stream); break;
+    case OUT_BF16: e = launch_replay<OUT_BF16>(p, r, meta_units, stream); break;
+    case OUT_F16: e = launch_replay<OUT_F16>(p, r, meta_units, stream); break;
+    case OUT_U8: e = launch_replay<OUT_U8>(p, r, meta_units, stream); break;
+  }
+  if (e != hipSuccess || r.index_in || !r.counter) return e;
+  replay_advance_kernel<<<1, 1, 0, stream>>>(r.counter, p.B);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // color4x4 on MFMA (v_mfma_f32_4x4x1_16b_f32)
 // ---------------------------------------------------------------------------
 namespace {

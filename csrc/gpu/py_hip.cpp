@@ -161,6 +161,44 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("Cout"), py::arg("cmap"), py::arg("flip_all"),
         py::arg("out_dtype"), py::arg("layout"), py::arg("stream"), py::arg("src_offsets_aligned") = false);
 
+  m.def("replay_sample",
+        [](uintptr_t store, int64_t count, uintptr_t dst, uintptr_t lut, int B, int H, int W, int Cin, int Cout,
+           std::vector<int> cmap, int flip_all, int out_dtype, int layout, uint64_t seed, uintptr_t counter,
+           uint64_t ctr_value, uintptr_t index_in, uintptr_t index_out, std::vector<uintptr_t> meta_src, std::vector<uintptr_t> meta_dst,
+           std::vector<int> meta_bytes, uintptr_t stream) {
+          DecodeParams p;
+          p.src = ptr<const uint8_t>(store);
+          p.dst = ptr<void>(dst);
+          p.lut = ptr<const float>(lut);
+          p.B = B, p.H = H, p.W = W, p.Cin = Cin, p.Cout = Cout;
+          fill_cmap(p.cmap, cmap);
+          p.flip_all = flip_all;
+          p.out_dtype = out_dtype;
+          p.layout = layout;
+          ReplayParams r;
+          r.count = count;
+          r.frame_bytes = int64_t(H) * W * Cin;
+          r.seed = seed;
+          r.counter = ptr<uint64_t>(counter);
+          r.ctr_value = ctr_value;
+          r.index_in = ptr<const int64_t>(index_in);
+          r.index_out = ptr<int64_t>(index_out);
+          if (meta_src.size() != meta_dst.size() || meta_src.size() != meta_bytes.size() ||
+              meta_src.size() > size_t(kMaxMeta))
+            throw std::invalid_argument("replay_sample: metadata columns mismatch or > kMaxMeta");
+          r.nmeta = int(meta_src.size());
+          for (int k = 0; k < r.nmeta; ++k) {
+            r.meta_src[k] = ptr<const uint8_t>(meta_src[size_t(k)]);
+            r.meta_dst[k] = ptr<uint8_t>(meta_dst[size_t(k)]);
+            r.meta_bytes[k] = meta_bytes[size_t(k)];
+          }
+          check(replay_sample(p, r, stream_of(stream)), "replay_sample");
+        },
+        py::arg("store"), py::arg("count"), py::arg("dst"), py::arg("lut"), py::arg("B"), py::arg("H"), py::arg("W"),
+        py::arg("Cin"), py::arg("Cout"), py::arg("cmap"), py::arg("flip_all"), py::arg("out_dtype"), py::arg("layout"),
+        py::arg("seed"), py::arg("counter"), py::arg("ctr_value"), py::arg("index_in"), py::arg("index_out"), py::arg("meta_src"),
+        py::arg("meta_dst"), py::arg("meta_bytes"), py::arg("stream"));
+
   m.def("color4x4",
         [](uintptr_t src, uintptr_t dst, uintptr_t lut, uintptr_t M, uintptr_t bias, uintptr_t flip, int B, int H,
            int W, int Cout, int flip_all, uintptr_t stream) {

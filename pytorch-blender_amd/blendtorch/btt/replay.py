@@ -60,7 +60,7 @@ class DeviceReplayBuffer:
         Message key of the image when filling from recordings / loaders.
     """
 
-    def __init__(self, capacity: int, device=None, image_key: str = 'image'):
+    def __init__(self, capacity: int, device=None, image_key: str = 'image', seed: Optional[int] = None):
         if capacity < 1:
             raise ValueError('capacity must be >= 1')
         self.capacity = int(capacity)
@@ -70,6 +70,11 @@ class DeviceReplayBuffer:
         self.meta: Dict[str, torch.Tensor] = {}
         self._size = 0
         self._next = 0
+        # sampler state of the fused kernel: Philox key and counter (host-side
+        # for eager sampling: one launch per batch; graphed samplers keep a
+        # device counter the captured graph advances itself)
+        self.seed = int(torch.initial_seed() if seed is None else seed) & (2 ** 64 - 1)
+        self._ctr = 0
         if self.device.type == 'cuda':
             ops.hip_ext()   # fail loudly here, not at the first sample()
 
@@ -227,6 +232,9 @@ class DeviceReplayBuffer:
         return paths
 
     # -- sampling --------------------------------------------------------------
+    def _fused(self, decode: DecodeConfig):
+        return self.device.type == 'cuda' and decode.color_matrix is None and self.store.is_contiguous()
+
     def _decode(self, idx: torch.Tensor, decode: DecodeConfig):
         if self.device.type == 'cuda' and decode.color_matrix is None:
             return ops.decode_gather(self.store, idx, decode)
@@ -236,20 +244,36 @@ class DeviceReplayBuffer:
         return ops.reference_decode(imgs, decode)
 
     def gather(self, idx: torch.Tensor, decode: DecodeConfig = DecodeConfig()):
-        """Decoded frames ``idx`` (device int tensor) + their metadata."""
+        """Decoded frames ``idx`` (device int tensor) + their metadata.  On a
+        GPU: one fused launch decodes the frames and gathers every metadata
+        column (``ops.replay_sample`` with given indices)."""
         if self._size == 0:
             raise IndexError('empty replay buffer')
         idx = idx.to(self.device, torch.int64)
+        if self._fused(decode):
+            img, idx, meta = ops.replay_sample(self.store, self._size, int(idx.numel()), decode, index=idx,
+                                               meta=self.meta)
+            return {self.image_key: img, **meta, 'index': idx}
         out = {self.image_key: self._decode(idx, decode)}
         for k, v in self.meta.items():
             out[k] = v.index_select(0, idx)
         out['index'] = idx
         return out
 
-    def sample(self, batch_size: int, decode: DecodeConfig = DecodeConfig(), generator=None):
-        """Uniform random batch (with replacement), indices drawn on the device."""
+    def sample(self, batch_size: int, decode: DecodeConfig = DecodeConfig(), generator=None, _counter=None):
+        """Uniform random batch (with replacement).  On a GPU (no ``generator``)
+        ONE fused launch draws the indices (Philox), decodes the frames and
+        gathers their metadata; with a ``torch.Generator`` the indices come
+        from ``torch.randint`` instead."""
         if self._size == 0:
             raise IndexError('empty replay buffer')
+        if generator is None and self._fused(decode):
+            ctr = _counter
+            if ctr is None:
+                ctr, self._ctr = self._ctr, self._ctr + batch_size
+            img, idx, meta = ops.replay_sample(self.store, self._size, batch_size, decode, seed=self.seed,
+                                               counter=ctr, meta=self.meta)
+            return {self.image_key: img, **meta, 'index': idx}
         idx = torch.randint(0, self._size, (batch_size,), device=self.device, generator=generator)
         return self.gather(idx, decode)
 
@@ -266,15 +290,19 @@ class DeviceReplayBuffer:
         """
         if self.device.type != 'cuda':
             return lambda: self.sample(batch_size, decode)
+        # the captured sample reads its Philox counter from device memory and
+        # advances it there: every replay draws new indices
+        counter = torch.tensor([self._ctr], dtype=torch.int64, device=self.device)
+        self._ctr += 1 << 40          # disjoint from later eager draws
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
             for _ in range(warmup):   # allocations, LUT upload, kernel selection outside the capture
-                self.sample(batch_size, decode)
+                self.sample(batch_size, decode, _counter=counter)
         torch.cuda.current_stream(self.device).wait_stream(side)
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
-            out = self.sample(batch_size, decode)
+            out = self.sample(batch_size, decode, _counter=counter)
 
         def replay():
             graph.replay()

@@ -346,6 +346,83 @@ def decode_gather(store, index, cfg: DecodeConfig = DecodeConfig(), out=None):
     return out
 
 
+def philox_indices(seed: int, counter: int, B: int, count: int) -> np.ndarray:
+    """The frame indices :func:`replay_sample` draws (numpy reference):
+    Philox4x32-10 with key ``seed`` and counter ``(b, counter)`` for image b,
+    first output word scaled to ``[0, count)`` as ``(word * count) >> 32``."""
+    M0, M1, W0, W1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57), 0x9E3779B9, 0xBB67AE85
+    mask = np.uint64(0xFFFFFFFF)
+    c0 = np.arange(B, dtype=np.uint64)
+    c1 = np.full(B, counter & 0xFFFFFFFF, np.uint64)
+    c2 = np.full(B, (counter >> 32) & 0xFFFFFFFF, np.uint64)
+    c3 = np.zeros(B, np.uint64)
+    k0, k1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+    for _ in range(10):
+        p0, p1 = M0 * c0, M1 * c2          # < 2^64: exact in uint64
+        hi0, lo0 = p0 >> np.uint64(32), p0 & mask
+        hi1, lo1 = p1 >> np.uint64(32), p1 & mask
+        c0, c1, c2, c3 = (hi1 ^ c1 ^ np.uint64(k0)), lo1, (hi0 ^ c3 ^ np.uint64(k1)), lo0
+        k0, k1 = (k0 + W0) & 0xFFFFFFFF, (k1 + W1) & 0xFFFFFFFF
+    return ((c0 * np.uint64(count)) >> np.uint64(32)).astype(np.int64)
+
+
+def replay_sample(store, count: int, batch: int, cfg: DecodeConfig = DecodeConfig(), seed: int = 0, counter=None,
+                  index=None, meta=None, out=None):
+    """Fused replay sample on the gfx950 kernel: draw ``batch`` frame indices
+    in ``[0, count)`` on the device (Philox, see :func:`philox_indices`) --
+    or use ``index`` (int64 [batch]) -- decode those frames of ``store`` (u8
+    [N,H,W,C] on the device) with ``cfg``, and gather row ``idx`` of every
+    ``meta`` column (dict name -> device tensor [N, ...]), in ONE launch.
+
+    ``counter``: an int (the Philox counter; the caller advances it by
+    ``batch``), or a device int64 tensor holding it -- then a one-lane kernel
+    behind the sample advances it, so a captured HIP graph draws fresh
+    indices on every replay.  Returns ``(images, index, meta_out)``."""
+    import torch
+    ext = hip_ext()
+    if store.dtype != torch.uint8 or not store.is_cuda or store.dim() != 4 or not store.is_contiguous():
+        raise TypeError('replay_sample expects a contiguous uint8 [N,H,W,C] device tensor')
+    if cfg.color_matrix is not None:
+        raise ValueError('replay_sample does not apply colour matrices (use gather + color4x4)')
+    N, H, W, C = store.shape
+    if max(cfg.cmap) >= C:
+        raise ValueError(f'channel map {cfg.cmap} needs more than {C} input channels')
+    dev = store.device
+    if out is None:
+        out = torch.empty(cfg.out_shape(batch, H, W), dtype=cfg.torch_dtype(), device=dev)
+    idx_out = torch.empty(batch, dtype=torch.int64, device=dev)
+    idx_in, ctr_ptr, ctr_value = 0, 0, 0
+    if index is not None:
+        index = index.to(dev, torch.int64).contiguous()
+        if index.numel() != batch:
+            raise ValueError('index needs one entry per image')
+        idx_in = index.data_ptr()
+    elif isinstance(counter, torch.Tensor):
+        if counter.dtype != torch.int64 or counter.numel() < 1 or counter.device != dev:
+            raise ValueError('a device counter must be an int64 tensor on the store\'s device')
+        ctr_ptr = counter.data_ptr()
+    elif counter is not None:
+        ctr_value = int(counter) & (2 ** 64 - 1)
+    else:
+        raise ValueError('drawing indices needs a counter (int or device tensor)')
+    meta = meta or {}
+    mout, src, dst, nbytes = {}, [], [], []
+    for k, col in meta.items():
+        if col.device != dev or not col.is_contiguous() or col.shape[0] != N:
+            raise ValueError(f'metadata column {k!r} must be a contiguous [{N}, ...] tensor on {dev}')
+        o = torch.empty((batch,) + tuple(col.shape[1:]), dtype=col.dtype, device=dev)
+        mout[k] = o
+        src.append(col.data_ptr())
+        dst.append(o.data_ptr())
+        nbytes.append(col[0].numel() * col.element_size())
+    lut = device_lut(cfg, dev)
+    ext.replay_sample(store.data_ptr(), int(count), out.data_ptr(), lut.data_ptr(), batch, H, W, C, cfg.cout,
+                      cfg.cmap, int(cfg.flip), OUT_DTYPES[cfg.dtype], LAYOUTS[cfg.layout], int(seed) & (2 ** 64 - 1),
+                      ctr_ptr, ctr_value, idx_in, idx_out.data_ptr(), src, dst, nbytes,
+                      _stream(dev))
+    return out, idx_out, mout
+
+
 def color4x4(images, M, bias=(0.0, 0.0, 0.0, 0.0), gamma=None, flip=False, cout=4):
     """out[b,c] = M[c,:] . g(in[b,:,y,x]) + bias[c] on the MFMA units (fp32)."""
     import torch

@@ -55,6 +55,18 @@ for step in "$@"; do
           python scripts/trace_timeline.py /tmp/rp_kt_$tag --last ${KT_LAST:-20000} > gpurun_out/kt_$tag.txt 2>&1; cat gpurun_out/kt_$tag.txt;;
     ktstep) timeout -k 10 300 rocprofv3 --kernel-trace -d /tmp/rp_ktstep -o run --output-format csv -- python scripts/disc_step_bench.py --only bf16-nhwc --graph on --iters 300 > gpurun_out/ktstep.log 2>&1; rc=$?; grep '^{' gpurun_out/ktstep.log
           python scripts/trace_timeline.py /tmp/rp_ktstep --last ${KT_LAST:-20000} > gpurun_out/ktstep.txt 2>&1; cat gpurun_out/ktstep.txt;;
+    replay2) for args in "--batch 8" "--batch 64 --steps 500" "--batch 8 --graph" "--batch 64 --steps 500 --graph" "--batch 8 --sampler legacy" "--batch 64 --steps 500 --sampler legacy" "--batch 64 --steps 500 --dtype bfloat16"; do
+            timeout -k 10 200 python benchmarks/bench_replay.py $args >> gpurun_out/replay2.log 2>&1 || { rc=$?; break; }
+          done; rc=${rc:-0}; grep '^{' gpurun_out/replay2.log | python -c "
+import json,sys
+for l in sys.stdin:
+    d=json.loads(l); print(d['sampler'], 'B', d['batch'], 'graph', d['graph'], d['dtype'], d['us_per_batch'], 'us', d['effective_tbps'], 'TB/s', d['value'], 'img/s')";;
+    rpmc) for pass in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES" "FETCH_SIZE" "WRITE_SIZE GRBM_GUI_ACTIVE"; do
+            n=$((${n:-0}+1))
+            timeout -s KILL 90 rocprofv3 --pmc $pass --kernel-trace -d /tmp/rp_rpmc$n -o run --output-format csv -- python scripts/replay_pmc.py > gpurun_out/rpmc$n.log 2>&1; rc=$?
+            mkdir -p gpurun_out/rpmc && find /tmp/rp_rpmc$n -name '*counter_collection.csv' -exec cp {} gpurun_out/rpmc/pass${n}_counters.csv \;
+            ok $rc || { echo "rpmc pass $n rc=$rc"; exit $rc; }
+          done;;
     short) timeout -k 10 200 python bench.py --steps 20 --warmup 5 > gpurun_out/short.log 2>&1; rc=$?; grep '^{' gpurun_out/short.log;;
     dist2gloo) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29557 bench.py --gpus 2 --backend gloo --steps 1000 --warmup 20 > gpurun_out/dist2gloo.log 2>&1; rc=$?; grep '^{' gpurun_out/dist2gloo.log;;
     replay) timeout -k 10 200 python benchmarks/bench_replay.py > gpurun_out/replay.log 2>&1 && timeout -k 10 200 python benchmarks/bench_replay.py --batch 64 --steps 500 >> gpurun_out/replay.log 2>&1 && timeout -k 10 200 python benchmarks/bench_replay.py --graph >> gpurun_out/replay.log 2>&1 && timeout -k 10 200 python benchmarks/bench_replay.py --graph --batch 64 --steps 500 >> gpurun_out/replay.log 2>&1 && timeout -k 10 200 python benchmarks/bench_replay.py --fill producers --frames 2048 --batch 64 --steps 500 >> gpurun_out/replay.log 2>&1; rc=$?; cat gpurun_out/replay.log | grep '^{';;

@@ -125,3 +125,70 @@ def test_replay_save_recordings_roundtrip(tmp_path):
     assert got[0][2] == np.arange(8, 12, dtype=np.float64).reshape(2, 2).tolist()
     back = DeviceReplayBuffer.from_recordings(str(tmp_path / 'hbm'), device='cpu', meta_keys=('frameid',))
     assert len(back) == 5 and sorted(back.meta['frameid'].tolist()) == [2, 3, 4, 5, 6]
+
+
+def test_philox_reference_properties():
+    """The numpy Philox reference: deterministic, counter-sensitive, in range."""
+    a = ops.philox_indices(7, 0, 64, 1000)
+    assert a.dtype == np.int64 and a.min() >= 0 and a.max() < 1000
+    assert np.array_equal(a, ops.philox_indices(7, 0, 64, 1000))
+    assert not np.array_equal(a, ops.philox_indices(7, 64, 64, 1000))
+    assert not np.array_equal(a, ops.philox_indices(8, 0, 64, 1000))
+    # roughly uniform
+    big = ops.philox_indices(1, 0, 40000, 10)
+    assert np.bincount(big, minlength=10).min() > 3600
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('shape', [(48, 64, 4), (46, 62, 3)])      # vector path / scalar path
+def test_replay_fused_sample_kernel(shape):
+    """ops.replay_sample: ONE launch draws the Philox indices (== the numpy
+    reference), decodes those frames bit-exactly and gathers every metadata
+    column (8-byte, 4-byte-multiple and 1-byte rows); the device counter
+    advances by B per launch."""
+    dev = torch.device('cuda', 0)
+    N = 50
+    g = torch.Generator(device=dev).manual_seed(0)
+    store = torch.randint(0, 256, (N,) + shape, dtype=torch.uint8, device=dev, generator=g)
+    meta = {'frameid': torch.arange(N, device=dev) * 3, 'xy': torch.rand(N, 8, 2, device=dev, dtype=torch.float64),
+            'flag': torch.arange(N, device=dev) % 3 == 0}
+    counter = torch.zeros(2, dtype=torch.int64, device=dev)
+    cfgs = [ops.DecodeConfig.densityopt(channels='rgb', gamma=2.2),
+            ops.DecodeConfig.unit(channels='bgr', dtype='bfloat16', layout='nhwc'),
+            ops.DecodeConfig(channels='rgb', gamma=2.2, dtype='uint8', flip=True)]
+    for step, cfg in enumerate(cfgs):
+        B = 13
+        img, idx, mo = ops.replay_sample(store, N - 3, B, cfg, seed=1234, counter=counter, meta=meta)
+        torch.cuda.synchronize()
+        expect = ops.philox_indices(1234, step * B, B, N - 3)
+        assert idx.cpu().numpy().tolist() == expect.tolist()
+        assert counter[0].item() == (step + 1) * B
+        ref = ops.reference_decode(store.cpu()[torch.from_numpy(expect)], cfg)
+        assert torch.equal(img.cpu(), ref), cfg
+        for k, col in meta.items():
+            assert torch.equal(mo[k], col[idx]), k
+    # a host-side counter value: one launch, nothing advanced on the device
+    img, idx, _ = ops.replay_sample(store, N, 7, cfgs[0], seed=5, counter=123)
+    assert idx.cpu().tolist() == ops.philox_indices(5, 123, 7, N).tolist() and counter[0].item() == 3 * 13
+    # given indices (gather mode) leave the counter alone
+    want = torch.tensor([0, N - 1, 7, 7], device=dev)
+    img, idx, mo = ops.replay_sample(store, N, 4, cfgs[0], index=want, meta=meta)
+    assert torch.equal(idx, want) and counter[0].item() == 3 * 13
+    assert torch.equal(img, ops.decode(store[want].contiguous(), cfgs[0]))
+
+
+@pytest.mark.gpu
+def test_replay_buffer_uses_fused_sampler():
+    dev = torch.device('cuda', 0)
+    rb = DeviceReplayBuffer(32, device=dev, seed=99)
+    g = torch.Generator(device=dev).manual_seed(1)
+    rb.extend(torch.randint(0, 256, (20, 48, 64, 4), dtype=torch.uint8, device=dev, generator=g),
+              frameid=torch.arange(20, device=dev), xy=torch.rand(20, 8, 2, device=dev))
+    cfg = ops.DecodeConfig.unit(channels='rgb', gamma=2.2)
+    b1, b2 = rb.sample(8, cfg), rb.sample(8, cfg)
+    torch.cuda.synchronize()
+    assert b1['index'].tolist() == ops.philox_indices(99, 0, 8, 20).tolist()
+    assert b2['index'].tolist() == ops.philox_indices(99, 8, 8, 20).tolist()
+    for b in (b1, b2):
+        assert torch.equal(b['image'], ops.decode(rb.store[b['index']], cfg))
+        assert torch.equal(b['frameid'], b['index']) and torch.equal(b['xy'], rb.meta['xy'][b['index']])
