@@ -24,3 +24,28 @@ def test_reference_harness_cpu(free_port, scene, producer):
 def test_install_scripts_parse():
     subprocess.run(['bash', '-n', str(ROOT / 'scripts' / 'install_blender.sh')], check=True)
     subprocess.run([sys.executable, '-m', 'py_compile', str(ROOT / 'scripts' / 'install_btb.py')], check=True)
+
+
+def test_sweep_rows_carry_reference_and_producers(monkeypatch, capsys):
+    """benchmarks/sweep.py: one JSON row per (mode, producer count) with the
+    matching reference row (Readme.md:88-93) and the producer caveat."""
+    import importlib.util
+    import json
+    from helpers import ROOT
+    spec = importlib.util.spec_from_file_location('sweep', ROOT / 'benchmarks' / 'sweep.py')
+    sweep = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sweep)
+
+    def fake(mode, n, steps, warmup, extra):
+        return {'producer': 'cubesim (stand-in)', 'config': {'cpus_per_gpu': 16}, 'n_gpus': 1,
+                'value': 1000.0 * n, 'sec_per_image': 1 / (1000.0 * n), 'sec_per_batch': 8 / (1000.0 * n),
+                'steps': steps}
+    monkeypatch.setattr(sweep, 'run_row', fake)
+    sweep.main(['--producers', '1,5,8', '--modes', 'rgb,rgba', '--steps', '3'])
+    rows = [json.loads(l) for l in capsys.readouterr().out.splitlines()]
+    assert [(r['mode'], r['producers']) for r in rows] == [('rgb', 1), ('rgb', 5), ('rgb', 8),
+                                                          ('rgba', 1), ('rgba', 5), ('rgba', 8)]
+    r5 = rows[1]
+    assert r5['reference_row']['sec_per_image'] == 0.011 and r5['reference_row']['note'] == 'no UI refresh'
+    assert r5['ratio_vs_reference_row'] == round(0.011 * 5000, 1)
+    assert rows[2]['reference_row'] is None and rows[0]['cpus'] == 16 and 'stand-in' in rows[0]['producer']
