@@ -132,6 +132,10 @@ def parse_args(argv=None):
     ap.add_argument('--backend', choices=['nccl', 'gloo'], default='nccl',
                     help='process-group backend (nccl = RCCL over xGMI; gloo only to rehearse several ranks on one GPU)')
     ap.add_argument('--start-port', type=int, default=0)
+    ap.add_argument('--step-decode', choices=['on', 'off'], default='on',
+                    help='disc consumer with --h2d copy: on = the loader only DMAs raw frames into the batch '
+                         'tensor and the decode kernel runs inside the captured training step (one queue, no '
+                         'loader kernels competing with the step); off = the loader decodes')
     ap.add_argument('--consumer-input', choices=['stream', 'resident'], default='stream',
                     help='diagnostic: resident = the consumer trains on one fixed batch while the stream keeps running')
     ap.add_argument('--force-pg', action='store_true',
@@ -262,6 +266,9 @@ def main(argv=None):
             pass
     decode = DecodeConfig.unit(channels='rgb', gamma=2.2)
     amp = args.consumer == 'disc' and args.consumer_dtype == 'bf16'
+    # decode inside the consumer's captured step (frames arrive by DMA only)
+    step_decode = (args.consumer == 'disc' and args.h2d == 'copy' and args.dist != 'scatter'
+                   and args.step_decode == 'on')
     if amp:
         # the decode kernel writes what the model's first conv reads: bf16, channels-last
         decode = DecodeConfig.unit(channels='rgb', gamma=2.2, dtype='bfloat16', layout='nhwc')
@@ -305,6 +312,11 @@ def main(argv=None):
                 # the decode does not read it) -- the bytes that cross xGMI
                 ldec = decode if args.dist != 'scatter' else DecodeConfig.raw(
                     channels='rgba' if 3 in decode.cmap else 'rgb')
+                if step_decode:
+                    # the loader only DMAs the frames into the consumer's tensor
+                    # (identity decode = no kernel on the loader's queue); the
+                    # decode runs inside the captured training step
+                    ldec = DecodeConfig.raw(channels=args.mode)
                 dl = DeviceLoader(addrs, batch_size=per_step, decode=ldec, device=device,
                                   max_items=total_batches * per_step, prefetch=6,
                                   io_threads=args.io_threads or None, timeoutms=60000, h2d=args.h2d,
@@ -315,10 +327,16 @@ def main(argv=None):
             it = iter(dl)
 
         def as_input(img):
+            if step_decode:
+                return img                  # raw u8 NHWC frames: decoded in loss_fn
             # NHWC bf16 storage -> NCHW view with channels-last strides; fp32 NCHW -> channels-last copy
             return img.permute(0, 3, 1, 2) if amp else img.contiguous(memory_format=torch.channels_last)
 
         def loss_fn(m, x):
+            if step_decode:
+                from blendtorch import ops
+                x = ops.decode(x, decode)   # gfx950 decode, captured with the step
+                x = x.permute(0, 3, 1, 2) if amp else x.contiguous(memory_format=torch.channels_last)
             if amp:
                 # no autocast weight cache: a captured graph must recast the live weights on every replay
                 with torch.autocast('cuda', dtype=torch.bfloat16, cache_enabled=not use_graph):
@@ -357,7 +375,8 @@ def main(argv=None):
                     # dependency on the loader's events) -- separates contention
                     # from waiting in the streamed-vs-resident step-time gap
                     if 'x' not in fixed:
-                        fixed['x'] = as_input(img).clone(memory_format=torch.channels_last)
+                        x0 = as_input(img)
+                        fixed['x'] = x0.clone() if step_decode else x0.clone(memory_format=torch.channels_last)
                     graphed(fixed['x'])
                 else:
                     graphed(as_input(img))
@@ -469,6 +488,7 @@ def main(argv=None):
                 'copy_streams': args.copy_streams if args.h2d == 'copy' else None,
                 'codec': args.codec if shm_slots else 'none',
                 'consumer_step': stepper.state if stepper is not None else None,
+                'decode_in_step': step_decode,
                 'consumer_collectives_per_step': stepper.collectives if stepper is not None else None,
             },
             'sec_per_image': round(tmax / images, 7),

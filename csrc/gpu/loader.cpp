@@ -463,6 +463,12 @@ bool StreamLoader::process(zmtp::Message&& msg) {
     if (cfg_.color_matrix && (c != 4 || (int64_t(h) * w) % 256 != 0 || w % 4 != 0))
       throw std::runtime_error("StreamLoader: colour matrix needs RGBA input with H*W % 256 == 0, W % 4 == 0");
     img_bytes_ = size_t(h) * w * c;
+    passthrough_ = cfg_.out_dtype == OUT_U8 && cfg_.layout == NHWC && cfg_.cout == c && !cfg_.flip_all &&
+                   !cfg_.color_matrix;
+    for (int k = 0; passthrough_ && k < c; ++k) {
+      passthrough_ = cfg_.cmap[k] == k;
+      for (int v = 0; passthrough_ && v < 256; ++v) passthrough_ = cfg_.lut[size_t(k) * 256 + size_t(v)] == float(v);
+    }
     size_t slot = cfg_.max_frame_bytes ? cfg_.max_frame_bytes : size_t(double(n) * 1.05) + 4096;
     slot = (slot + 4095) & ~size_t(4095);
     int nslots = cfg_.pool_slots;
@@ -770,7 +776,31 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
   }
   uint8_t* stage = nullptr;
   const size_t stage_idx = size_t(batch_index_) % staging_.size();
-  if (!direct) {   // copy path: exactly one batch per launch
+  const bool passthrough = !direct && passthrough_ &&
+                           std::none_of(all.begin(), all.end(), [](const Item* it) { return it->flip; });
+  if (passthrough) {
+    // identity decode: the frames go by DMA straight into the consumer's
+    // tensor (its post event already gates stream_; the copy streams wait on
+    // stream_'s progress through it), and no kernel is launched
+    hipEvent_t gate;
+    check(hipEventCreateWithFlags(&gate, hipEventDisableTiming), "hipEventCreate(gate)");
+    check(hipEventRecord(gate, stream_), "hipEventRecord(gate)");
+    const size_t K = std::max<size_t>(1, copy_streams_.size());
+    int i = 0;
+    for (auto& b : group)
+      for (size_t k = 0; k < b.items.size(); ++k, ++i) {
+        hipStream_t cs = copy_streams_.empty() ? stream_ : copy_streams_[size_t(i) % K];
+        if (cs != stream_ && size_t(i) < K) check(hipStreamWaitEvent(cs, gate, 0), "hipStreamWaitEvent(gate)");
+        check(hipMemcpyAsync(static_cast<uint8_t*>(b.dst) + k * img_bytes_, all[size_t(i)]->src, img_bytes_,
+                             hipMemcpyHostToDevice, cs),
+              "hipMemcpyAsync(H2D passthrough)");
+      }
+    for (size_t k = 0; k < copy_streams_.size() && k < size_t(total); ++k) {
+      check(hipEventRecord(copy_done_[k], copy_streams_[k]), "hipEventRecord(copy)");
+      check(hipStreamWaitEvent(stream_, copy_done_[k], 0), "hipStreamWaitEvent(copy)");
+    }
+    (void)hipEventDestroy(gate);
+  } else if (!direct) {   // copy path: exactly one batch per launch
     stage = staging_[stage_idx];
     if (copy_streams_.empty()) {
       for (int i = 0; i < total; ++i)
@@ -800,8 +830,10 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
   check(hipEventCreateWithFlags(&copied, hipEventDisableTiming), "hipEventCreate(copied)");
   if (!direct) check(hipEventRecord(copied, stream_), "hipEventRecord(copied)");
   const bool per_image_dst = group.size() > 1;
-  hipError_t e;
-  if (cfg_.color_matrix) {
+  hipError_t e = hipSuccess;
+  if (passthrough) {
+    // nothing to launch: the DMA wrote the output
+  } else if (cfg_.color_matrix) {
     Color4x4Params cp;
     cp.src = stage;
     cp.dst = static_cast<float*>(group.front().dst);
@@ -862,7 +894,7 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
   }
   check(e, "decode kernel launch");
   if (direct) check(hipEventRecord(copied, stream_), "hipEventRecord(copied)");
-  if (!direct && !copy_streams_.empty()) {
+  if (!direct && !passthrough && !copy_streams_.empty()) {
     if (stage_free_.size() < staging_.size()) stage_free_.resize(staging_.size(), nullptr);
     if (!stage_free_[stage_idx])
       check(hipEventCreateWithFlags(&stage_free_[stage_idx], hipEventDisableTiming), "hipEventCreate(stage)");
@@ -896,6 +928,7 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
     stats_.batches += group.size();
     stats_.launches++;
     if (direct) stats_.direct_batches += group.size();
+    if (passthrough) stats_.passthrough_batches += group.size();
     stats_.h2d_issue_ms += now_ms() - t_issue;
     for (auto& rb : done) ready_.push_back(std::move(rb));
   }

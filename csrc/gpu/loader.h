@@ -154,6 +154,7 @@ struct LoaderStats {
   // producer rings at the time of stats(): slots, frames published and not
   // yet claimed (waiting in queues), frames claimed by this loader
   uint64_t ring_slots = 0, ring_published = 0, ring_held = 0;
+  uint64_t passthrough_batches = 0;        // copy path, identity decode: DMA only, no kernel
   std::map<int64_t, uint64_t> frames_per_btid;   // provenance: frames per producer id
 };
 
@@ -249,6 +250,10 @@ class StreamLoader {
   std::vector<hipEvent_t> copy_done_;          // one per copy stream, reused
   std::vector<hipEvent_t> stage_free_;         // per staging buffer: last kernel reading it
   std::vector<shm::Segment*> seg_list_;        // mapped rings, for stats() (guarded by mu_)
+  // the configured decode is the identity on the frame bytes (u8, NHWC, all
+  // channels in order, identity table, no flip): copy-path batches are then
+  // DMA'd straight into the consumer's tensor and no kernel runs at all
+  bool passthrough_ = false;
   struct Inflight {
     int64_t launch_no = 0;
     hipEvent_t copied;

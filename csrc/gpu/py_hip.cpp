@@ -574,6 +574,7 @@ PYBIND11_MODULE(_hip, m) {
         d["timed_images"] = s.timed_images;
         d["timed_gpu_ms"] = s.timed_gpu_ms;
         d["keys_evicted"] = s.keys_evicted;
+        d["passthrough_batches"] = s.passthrough_batches;
         d["ring_slots"] = s.ring_slots;
         d["ring_published"] = s.ring_published;
         d["ring_held"] = s.ring_held;

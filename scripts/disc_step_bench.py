@@ -25,7 +25,7 @@ VARIANTS = {
 }
 
 
-def run(name, iters, batch, graph, fused_adam=False, fused_bn=True):
+def run(name, iters, batch, graph, fused_adam=False, fused_bn=True, dma=0):
     dt, fmt = VARIANTS[name]
     dev = torch.device('cuda', 0)
     torch.manual_seed(0)
@@ -48,6 +48,17 @@ def run(name, iters, batch, graph, fused_adam=False, fused_bn=True):
     for _ in range(5):
         step()
     torch.cuda.synchronize()
+    # optional background H2D traffic shaped like the stream loader's copy path:
+    # 8 frames of 640x480 RGBA (9.8 MB) per step from pinned host memory, spread
+    # over `dma` side streams -- isolates what DMA alone does to the step
+    side = [torch.cuda.Stream() for _ in range(dma)]
+    hsrc = [torch.empty(1228800, dtype=torch.uint8).pin_memory() for _ in range(8)] if dma else []
+    ddst = [torch.empty(1228800, dtype=torch.uint8, device=dev) for _ in range(8)] if dma else []
+
+    def traffic():
+        for i in range(8 if dma else 0):
+            with torch.cuda.stream(side[i % dma]):
+                ddst[i].copy_(hsrc[i], non_blocking=True)
     fn = step
     if graph:
         g = torch.cuda.CUDAGraph()
@@ -60,10 +71,12 @@ def run(name, iters, batch, graph, fused_adam=False, fused_bn=True):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(iters):
+        traffic()
         fn()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / iters * 1000
-    return {'variant': name, 'graph': graph, 'fused_adam': fused_adam, 'fused_bn': fused_bn, 'ms_per_step': round(ms, 4), 'images_per_s': round(batch / ms * 1000, 1)}
+    return {'variant': name, 'graph': graph, 'fused_adam': fused_adam, 'fused_bn': fused_bn, 'dma_streams': dma,
+            'ms_per_step': round(ms, 4), 'images_per_s': round(batch / ms * 1000, 1)}
 
 
 def main():
@@ -74,6 +87,7 @@ def main():
     ap.add_argument('--graph', choices=['both', 'on', 'off'], default='both')
     ap.add_argument('--no-fused-adam', dest='fused_adam', action='store_false',
                     help='foreach Adam instead of torch.optim.Adam(fused=True) (one multi-tensor kernel)')
+    ap.add_argument('--dma', type=int, default=0, help='side streams of background H2D traffic (9.8 MB per step)')
     ap.add_argument('--no-fused-bn', dest='fused_bn', action='store_false',
                     help='MIOpen BatchNorm + PyTorch LeakyReLU instead of the fused gfx950 op')
     args = ap.parse_args()
@@ -82,7 +96,7 @@ def main():
     graphs = {'both': (False, True), 'on': (True,), 'off': (False,)}[args.graph]
     for n in names:
         for g in graphs:
-            print(json.dumps(run(n, args.iters, args.batch, g, args.fused_adam, args.fused_bn)), flush=True)
+            print(json.dumps(run(n, args.iters, args.batch, g, args.fused_adam, args.fused_bn, args.dma)), flush=True)
 
 
 if __name__ == '__main__':

@@ -115,6 +115,8 @@ def test_copy_path_stream_fanout_integrity(dev, free_port):
                     assert seq > seen.get(btid, -1)
                     seen[btid] = seq
             assert dl.stats['direct_batches'] == 0 and dl.stats['frames'] == 1600
+            # identity decode on the copy path: DMA straight into the batch tensor, no kernel
+            assert dl.stats['passthrough_batches'] == 200
 
 
 def test_window_metrics_scope(dev, free_port):
