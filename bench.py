@@ -132,6 +132,9 @@ def parse_args(argv=None):
     ap.add_argument('--backend', choices=['nccl', 'gloo'], default='nccl',
                     help='process-group backend (nccl = RCCL over xGMI; gloo only to rehearse several ranks on one GPU)')
     ap.add_argument('--start-port', type=int, default=0)
+    ap.add_argument('--cast', choices=['fused', 'autocast'], default='fused',
+                    help='disc consumer, bf16: fused = all conv weights cast in one gfx950 launch per direction '
+                         '(Discriminator.forward_bf16); autocast = torch.autocast (a cast per layer each way)')
     ap.add_argument('--step-decode', choices=['on', 'off'], default='on',
                     help='disc consumer with --h2d copy: on = the loader only DMAs raw frames into the batch '
                          'tensor and the decode kernel runs inside the captured training step (one queue, no '
@@ -337,7 +340,9 @@ def main(argv=None):
                 from blendtorch import ops
                 x = ops.decode(x, decode)   # gfx950 decode, captured with the step
                 x = x.permute(0, 3, 1, 2) if amp else x.contiguous(memory_format=torch.channels_last)
-            if amp:
+            if amp and args.cast == 'fused':
+                out = m.forward_bf16(x.to(torch.bfloat16)).float()   # one cast launch per direction
+            elif amp:
                 # no autocast weight cache: a captured graph must recast the live weights on every replay
                 with torch.autocast('cuda', dtype=torch.bfloat16, cache_enabled=not use_graph):
                     out = m(x)
@@ -489,6 +494,7 @@ def main(argv=None):
                 'codec': args.codec if shm_slots else 'none',
                 'consumer_step': stepper.state if stepper is not None else None,
                 'decode_in_step': step_decode,
+                'cast': args.cast if amp else None,
                 'consumer_collectives_per_step': stepper.collectives if stepper is not None else None,
             },
             'sec_per_image': round(tmax / images, 7),

@@ -171,8 +171,10 @@ hipError_t adaptive_avgpool_nhwc_bwd(const void* gy, void* gx, int N, int H, int
 // `partial` is scratch of bn_partial_floats(M, C) floats.
 int64_t bn_partial_floats(int64_t M, int C, int dtype);
 hipError_t bn_stats(const void* x, int64_t M, int C, int dtype, float* partial, hipStream_t stream);
+// num_batches_tracked (nullable): the module's int64 counter, incremented on the device.
 hipError_t bn_finalize(const float* partial, int64_t M, int C, int dtype, float eps, float momentum, float* mean,
-                       float* invstd, float* running_mean, float* running_var, hipStream_t stream);
+                       float* invstd, float* running_mean, float* running_var, hipStream_t stream,
+                       int64_t* num_batches_tracked = nullptr);
 hipError_t bn_apply(const void* x, void* y, int64_t M, int C, int dtype, const float* mean, const float* invstd,
                     const float* w, const float* b, float slope, hipStream_t stream);
 hipError_t bn_bwd_reduce(const void* x, const void* gy, int64_t M, int C, int dtype, const float* mean,
@@ -182,6 +184,21 @@ hipError_t bn_bwd_finalize(const float* partial, int64_t M, int C, int dtype, fl
 hipError_t bn_bwd_apply(const void* x, const void* gy, void* gx, int64_t M, int C, int dtype, const float* mean,
                         const float* invstd, const float* w, const float* b, const float* dw, const float* db,
                         float slope, hipStream_t stream);
+
+// Multi-tensor dtype cast in ONE launch (the consumer step's weight casts
+// for bf16 compute and the cast of the bf16 weight gradients back to fp32 --
+// a dozen tiny launches otherwise).  mode CAST_F32_TO_BF16 (RNE) or
+// CAST_BF16_TO_F32; tensor k has numel[k] elements (contiguous).
+constexpr int kMaxCast = 32;
+enum CastMode : int { CAST_F32_TO_BF16 = 0, CAST_BF16_TO_F32 = 1 };
+struct CastParams {
+  const void* src[kMaxCast] = {};
+  void* dst[kMaxCast] = {};
+  int64_t numel[kMaxCast] = {};
+  int n = 0;
+  int mode = CAST_F32_TO_BF16;
+};
+hipError_t multi_cast(const CastParams& p, hipStream_t stream);
 
 }  // namespace gpu
 }  // namespace btn

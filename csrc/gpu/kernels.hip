@@ -982,11 +982,13 @@ __device__ __forceinline__ void bn_fold(const float* __restrict__ partial, int n
 
 __global__ __launch_bounds__(kBlock) void bn_finalize_kernel(const float* __restrict__ partial, int nblocks, int64_t M,
                                                              int C, float eps, float momentum, float* mean,
-                                                             float* invstd, float* rm, float* rv) {
+                                                             float* invstd, float* rm, float* rv,
+                                                             int64_t* tracked) {
   const int c = int(blockIdx.x);
   double s, q;
   bn_fold(partial, nblocks, C, c, s, q);
   if (threadIdx.x != 0) return;
+  if (tracked && c == 0) tracked[0] += 1;   // BatchNorm2d.num_batches_tracked (saves a launch)
   const double mu = s / double(M);
   double var = q / double(M) - mu * mu;
   var = var < 0.0 ? 0.0 : var;
@@ -1092,13 +1094,14 @@ hipError_t bn_stats(const void* x, int64_t M, int C, int dtype, float* partial, 
 }
 
 hipError_t bn_finalize(const float* partial, int64_t M, int C, int dtype, float eps, float momentum, float* mean,
-                       float* invstd, float* running_mean, float* running_var, hipStream_t stream) {
+                       float* invstd, float* running_mean, float* running_var, hipStream_t stream,
+                       int64_t* num_batches_tracked) {
   if (!bn_shape_ok(M, C, dtype)) return hipErrorInvalidValue;
   int nb;
   int64_t rpb;
   bn_blocks(M, C, dtype, nb, rpb);
-  bn_finalize_kernel<<<C, kBlock, 0, stream>>>(partial, nb, M, C, eps, momentum, mean, invstd,
-                                                                       running_mean, running_var);
+  bn_finalize_kernel<<<C, kBlock, 0, stream>>>(partial, nb, M, C, eps, momentum, mean, invstd, running_mean,
+                                                running_var, num_batches_tracked);
   return hipGetLastError();
 }
 
@@ -1150,6 +1153,50 @@ hipError_t bn_bwd_apply(const void* x, const void* gy, void* gx, int64_t M, int 
     bn_apply_kernel<OUT_BF16, true><<<grid, kBlock, 0, stream>>>(x, gy, gx, M, C, mean, invstd, w, b, dw, db, slope);
   else
     bn_apply_kernel<OUT_F32, true><<<grid, kBlock, 0, stream>>>(x, gy, gx, M, C, mean, invstd, w, b, dw, db, slope);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// multi-tensor cast (fp32 <-> bf16)
+// ---------------------------------------------------------------------------
+namespace {
+
+// blockIdx.y = tensor, blockIdx.x strides over its elements, 4 per lane
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void multi_cast_kernel(CastParams p) {
+  const int k = int(blockIdx.y);
+  const int64_t n = p.numel[k];
+  for (int64_t i = (int64_t(blockIdx.x) * kBlock + threadIdx.x) * 4; i < n; i += int64_t(gridDim.x) * kBlock * 4) {
+    if constexpr (MODE == CAST_F32_TO_BF16) {
+      const float* s = static_cast<const float*>(p.src[k]);
+      uint16_t* d = static_cast<uint16_t*>(p.dst[k]);
+      for (int j = 0; j < 4 && i + j < n; ++j) {
+        const float f = s[i + j];
+        d[i + j] = f != f ? uint16_t(0x7FC0) : f2bf(f);   // NaN stays a quiet NaN (as torch)
+      }
+    } else {
+      const uint16_t* s = static_cast<const uint16_t*>(p.src[k]);
+      float* d = static_cast<float*>(p.dst[k]);
+      for (int j = 0; j < 4 && i + j < n; ++j) d[i + j] = __uint_as_float(uint32_t(s[i + j]) << 16);
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t multi_cast(const CastParams& p, hipStream_t stream) {
+  if (p.n <= 0) return hipSuccess;
+  if (p.n > kMaxCast) return hipErrorInvalidValue;
+  int64_t most = 0;
+  for (int k = 0; k < p.n; ++k) {
+    if (p.numel[k] < 0 || (p.numel[k] > 0 && (!p.src[k] || !p.dst[k]))) return hipErrorInvalidValue;
+    most = p.numel[k] > most ? p.numel[k] : most;
+  }
+  const int64_t blocks = (most + 4 * kBlock - 1) / (4 * kBlock);
+  const dim3 grid(unsigned(blocks < 1024 ? (blocks > 0 ? blocks : 1) : 1024), unsigned(p.n));
+  if (p.mode == CAST_F32_TO_BF16) multi_cast_kernel<CAST_F32_TO_BF16><<<grid, kBlock, 0, stream>>>(p);
+  else if (p.mode == CAST_BF16_TO_F32) multi_cast_kernel<CAST_BF16_TO_F32><<<grid, kBlock, 0, stream>>>(p);
+  else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

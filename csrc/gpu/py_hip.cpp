@@ -199,6 +199,22 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("seed"), py::arg("counter"), py::arg("ctr_value"), py::arg("index_in"), py::arg("index_out"), py::arg("meta_src"),
         py::arg("meta_dst"), py::arg("meta_bytes"), py::arg("stream"));
 
+  m.def("multi_cast",
+        [](std::vector<uintptr_t> src, std::vector<uintptr_t> dst, std::vector<int64_t> numel, int mode,
+           uintptr_t stream) {
+          if (src.size() != dst.size() || src.size() != numel.size() || src.size() > size_t(kMaxCast))
+            throw std::invalid_argument("multi_cast: list lengths differ or exceed kMaxCast");
+          CastParams p;
+          p.n = int(src.size());
+          p.mode = mode;
+          for (int k = 0; k < p.n; ++k) {
+            p.src[k] = ptr<const void>(src[size_t(k)]);
+            p.dst[k] = ptr<void>(dst[size_t(k)]);
+            p.numel[k] = numel[size_t(k)];
+          }
+          check(multi_cast(p, stream_of(stream)), "multi_cast");
+        });
+
   m.def("color4x4",
         [](uintptr_t src, uintptr_t dst, uintptr_t lut, uintptr_t M, uintptr_t bias, uintptr_t flip, int B, int H,
            int W, int Cout, int flip_all, uintptr_t stream) {
@@ -241,16 +257,19 @@ PYBIND11_MODULE(_hip, m) {
   m.def("bn_forward",
         [](uintptr_t x, uintptr_t y, int64_t M, int C, int dtype, uintptr_t partial, float eps, float momentum,
            uintptr_t mean, uintptr_t invstd, uintptr_t rm, uintptr_t rv, uintptr_t w, uintptr_t b, float slope,
-           uintptr_t stream) {
+           uintptr_t stream, uintptr_t tracked) {
           hipStream_t s = stream_of(stream);
           check(bn_stats(ptr<const void>(x), M, C, dtype, ptr<float>(partial), s), "bn_stats");
           check(bn_finalize(ptr<const float>(partial), M, C, dtype, eps, momentum, ptr<float>(mean), ptr<float>(invstd),
-                            ptr<float>(rm), ptr<float>(rv), s),
+                            ptr<float>(rm), ptr<float>(rv), s, ptr<int64_t>(tracked)),
                 "bn_finalize");
           check(bn_apply(ptr<const void>(x), ptr<void>(y), M, C, dtype, ptr<const float>(mean),
                          ptr<const float>(invstd), ptr<const float>(w), ptr<const float>(b), slope, s),
                 "bn_apply");
-        });
+        },
+        py::arg("x"), py::arg("y"), py::arg("M"), py::arg("C"), py::arg("dtype"), py::arg("partial"), py::arg("eps"),
+        py::arg("momentum"), py::arg("mean"), py::arg("invstd"), py::arg("rm"), py::arg("rv"), py::arg("w"),
+        py::arg("b"), py::arg("slope"), py::arg("stream"), py::arg("tracked") = 0);
   m.def("bn_backward",
         [](uintptr_t x, uintptr_t gy, uintptr_t gx, int64_t M, int C, int dtype, uintptr_t partial, uintptr_t mean,
            uintptr_t invstd, uintptr_t w, uintptr_t b, uintptr_t dw, uintptr_t db, float slope, uintptr_t stream) {

@@ -55,6 +55,23 @@ class Discriminator(nn.Module):
     def forward(self, x):
         return self.features(x).view(-1, 1).squeeze(1)
 
+    def forward_bf16(self, x):
+        """bf16 forward without autocast: ONE kernel casts every conv weight
+        to bf16 (and one casts their gradients back to fp32 in backward)
+        instead of a cast per layer each way; numerically the same as
+        ``autocast(bfloat16)`` over :meth:`forward` (RNE weight casts, bf16
+        activations).  ``x``: bf16 on the GPU."""
+        import torch.nn.functional as F
+        from .. import ops
+        convs = [m for m in self.features if isinstance(m, nn.Conv2d)]
+        weights = iter(ops.cast_bf16(*[c.weight for c in convs]))
+        for m in self.features:
+            if isinstance(m, nn.Conv2d):
+                x = F.conv2d(x, next(weights), None, m.stride, m.padding, m.dilation, m.groups)
+            else:
+                x = m(x)
+        return x.view(-1, 1).squeeze(1)
+
 
 class ProbModel(nn.Module):
     """Independent LogNormal distributions over the supershape frequencies

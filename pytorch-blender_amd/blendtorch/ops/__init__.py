@@ -577,6 +577,60 @@ def _pool_module():
 
 
 # ---------------------------------------------------------------------------
+# consumer-model op: one-launch fp32 -> bf16 cast of a parameter list
+
+def _cast_function():
+    import torch
+
+    def launch(srcs, outs, mode):
+        ext = hip_ext()
+        _count('multi_cast')
+        ext.multi_cast([t.data_ptr() for t in srcs], [o.data_ptr() for o in outs], [t.numel() for t in srcs], mode,
+                       _stream(srcs[0].device))
+
+    class _CastBF16(torch.autograd.Function):
+        """fp32 tensors -> bf16 copies (forward) and bf16 gradients -> fp32
+        (backward), each direction ONE multi-tensor kernel (autocast casts
+        every weight, and every weight gradient back, separately)."""
+
+        @staticmethod
+        def forward(ctx, *ws):
+            outs = [torch.empty_like(w, dtype=torch.bfloat16) for w in ws]
+            launch(ws, outs, 0)
+            return tuple(outs)
+
+        @staticmethod
+        def backward(ctx, *gs):
+            have = [g for g in gs if g is not None]
+            dense = [g if g.is_non_overlapping_and_dense() else g.contiguous() for g in have]
+            outs = [torch.empty_like(g, dtype=torch.float32) for g in dense]
+            if dense:
+                launch(dense, outs, 1)
+            it = iter(outs)
+            return tuple(next(it) if g is not None else None for g in gs)
+
+    return _CastBF16
+
+
+_CAST_FN = None
+
+
+def cast_bf16(*tensors):
+    """bf16 copies of GPU fp32 ``tensors`` (differentiable) in one gfx950
+    launch per direction -- the consumer step's weight casts without a
+    separate cast kernel per layer.  Tensors must be dense (any strides)."""
+    global _CAST_FN
+    if _CAST_FN is None:
+        _CAST_FN = _cast_function()
+    if len(tensors) > 32:
+        raise ValueError('cast_bf16 takes at most 32 tensors per call')
+    for t in tensors:
+        if not (t.is_cuda and t.dtype.is_floating_point and t.element_size() == 4 and t.is_non_overlapping_and_dense()):
+            raise ValueError('cast_bf16 needs dense fp32 GPU tensors')
+    return _CAST_FN.apply(*tensors)
+
+
+# ---------------------------------------------------------------------------
 # consumer-model op: training BatchNorm2d fused with LeakyReLU (channels-last)
 
 def _bn_function():
@@ -584,7 +638,7 @@ def _bn_function():
 
     class _BatchNormLeakyReLU(torch.autograd.Function):
         @staticmethod
-        def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, slope):
+        def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, slope, tracked=None):
             ext = hip_ext()
             N, C, H, W = x.shape
             M = N * H * W
@@ -601,7 +655,7 @@ def _bn_function():
             _count('bn_forward')
             ext.bn_forward(xs.data_ptr(), y.data_ptr(), M, C, dt, part.data_ptr(), float(eps), float(momentum),
                            mean.data_ptr(), invstd.data_ptr(), rm, rv, w.data_ptr(), b.data_ptr(), float(slope),
-                           _stream(x.device))
+                           _stream(x.device), tracked.data_ptr() if tracked is not None else 0)
             ctx.save_for_backward(xs, w, b, mean, invstd)
             ctx.slope = float(slope)
             return y.permute(0, 3, 1, 2)
@@ -622,7 +676,7 @@ def _bn_function():
             ext.bn_backward(xs.data_ptr(), gys.data_ptr(), gx.data_ptr(), M, C, dt, part.data_ptr(), mean.data_ptr(),
                             invstd.data_ptr(), w.data_ptr(), b.data_ptr(), dw.data_ptr(), db.data_ptr(), ctx.slope,
                             _stream(xs.device))
-            return gx.permute(0, 3, 1, 2), dw, db, None, None, None, None, None
+            return gx.permute(0, 3, 1, 2), dw, db, None, None, None, None, None, None
 
     return _BatchNormLeakyReLU
 
@@ -658,8 +712,8 @@ def batch_norm_leaky_relu(x, weight, bias, running_mean=None, running_var=None, 
     return _BN_FN.apply(x, weight, bias, running_mean, running_var, eps, momentum, slope)
 
 
-def _bn_apply_unchecked(x, weight, bias, running_mean, running_var, eps, momentum, slope):
-    return _BN_FN.apply(x, weight, bias, running_mean, running_var, eps, momentum, slope)
+def _bn_apply_unchecked(x, weight, bias, running_mean, running_var, eps, momentum, slope, tracked=None):
+    return _BN_FN.apply(x, weight, bias, running_mean, running_var, eps, momentum, slope, tracked)
 
 
 def reference_batch_norm_leaky_relu(x, weight, bias, running_mean=None, running_var=None, eps=1e-5, momentum=0.1,
@@ -693,9 +747,9 @@ def _bn_module():
                 global _BN_FN
                 if _BN_FN is None:
                     _BN_FN = _bn_function()
-                self.num_batches_tracked.add_(1)
+                # num_batches_tracked is incremented by the finalize kernel (one launch fewer)
                 return _bn_apply_unchecked(x, self.weight, self.bias, self.running_mean, self.running_var,
-                                           self.eps, self.momentum, self.slope)
+                                           self.eps, self.momentum, self.slope, self.num_batches_tracked)
             return F.leaky_relu(super().forward(x), self.slope)
 
         def extra_repr(self):
