@@ -48,8 +48,11 @@ std::string dtype_str(const std::string& code, char bo) {
   if (code.size() < 2) throw Unsupported("dtype code " + code);
   char kind = code[0];
   std::string size = code.substr(1);
-  if (kind == 'V' || kind == 'O' || kind == 'U' || kind == 'S' || kind == 'M' || kind == 'm')
+  // plain numeric dtypes only: bool, (u)int, float, complex of 1..16 bytes
+  if (kind != 'b' && kind != 'i' && kind != 'u' && kind != 'f' && kind != 'c')
     throw Unsupported("dtype kind " + code);
+  if (size != "1" && size != "2" && size != "4" && size != "8" && size != "16")
+    throw Unsupported("dtype size " + code);
   char order = bo;
   if (size == "1" || kind == 'b') order = '|';
   else if (order == '=' || order == '|') order = '<';   // native little endian host
@@ -435,8 +438,14 @@ int64_t Value::numel() const {
 }
 
 size_t Value::itemsize() const {
-  if (dtype.size() < 3) return 0;
-  return size_t(std::stoul(dtype.substr(2)));
+  // dtype is "<order><kind><digits>" as built by dtype_str (validated there)
+  size_t n = 0;
+  if (dtype.size() < 3 || dtype.size() > 4) return 0;
+  for (size_t i = 2; i < dtype.size(); ++i) {
+    if (dtype[i] < '0' || dtype[i] > '9') return 0;
+    n = n * 10 + size_t(dtype[i] - '0');
+  }
+  return n;
 }
 
 VPtr parse(const uint8_t* data, size_t n) {

@@ -52,3 +52,21 @@ def test_shmring_stress_sanitized(tmp_path, san):
     assert 'corrupt=0' in r.stdout and 'WARNING: ThreadSanitizer' not in r.stderr
     stats = dict(kv.split('=') for kv in r.stdout.split())
     assert int(stats['reclaimed']) > 0 and int(stats['verified']) > 1000
+
+
+@pytest.mark.slow
+def test_wire_fuzz_asan_ubsan(tmp_path, free_port):
+    """Peer-controlled bytes under ASan + UBSan (csrc/tests/fuzz_wire.cpp):
+    20k mutated pickles (wrapping 64-bit lengths, hostile shapes, truncation)
+    never yield a payload range outside the frame, and hostile ZMTP peers
+    (zero-size / overlong commands, 2^62-byte frames, garbage) cannot take the
+    process down or stop a well-behaved peer's delivery."""
+    exe = tmp_path / 'fuzz_wire'
+    cmd = ['g++', '-std=c++17', '-O1', '-g', '-fsanitize=address,undefined', '-fno-sanitize-recover=undefined',
+           '-pthread', str(ROOT / 'csrc/tests/fuzz_wire.cpp'), str(ROOT / 'csrc/transport/zmtp.cpp'),
+           str(ROOT / 'csrc/codec/pickle_codec.cpp'), '-o', str(exe)]
+    subprocess.run(cmd, check=True, capture_output=True, timeout=300)
+    env = dict(os.environ, ASAN_OPTIONS='detect_leaks=0:halt_on_error=1', UBSAN_OPTIONS='halt_on_error=1')
+    r = subprocess.run([str(exe), str(free_port)], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr[-4000:]
+    assert 'bad_ranges=0' in r.stdout and 'delivered=1' in r.stdout
