@@ -370,8 +370,11 @@ def main(argv=None):
 
         fixed = {}
 
+        from blendtorch.utils import trace_range
+
         def step():
-            b = next(it)
+            with trace_range('bench.next'):
+                b = next(it)
             img = b['image']
             last['btid'] = b.get('btid')
             if model is not None:
@@ -384,7 +387,8 @@ def main(argv=None):
                         fixed['x'] = x0.clone() if step_decode else x0.clone(memory_format=torch.channels_last)
                     graphed(fixed['x'])
                 else:
-                    graphed(as_input(img))
+                    with trace_range('bench.train'):
+                        graphed(as_input(img))
             return img
 
         # warm-up: at least W batches, and (shard/pool) until every local producer

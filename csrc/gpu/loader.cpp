@@ -163,6 +163,7 @@ void StreamLoader::post(void* dst, hipStream_t consumer) {
 }
 
 bool StreamLoader::next(ReadyBatch* out, hipStream_t consumer, long timeout_ms) {
+  trace::Range tr("btn.loader.next");
   std::unique_lock<std::mutex> lk(mu_);
   cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms),
                [&] { return !ready_.empty() || !error_.empty() || exhausted_; });
@@ -314,6 +315,7 @@ void StreamLoader::run() {
     try {
       // with copies in flight, wake up often enough to recycle their slots
       // promptly (producers / IO threads may be waiting for them)
+      trace::Range tp("btn.loader.poll");
       ev = zmtp::Socket::poll(items, inflight_.empty() && pending_.empty() ? 100 : 1, intr);
     } catch (const zmtp::Error& e) {
       if (e.code == zmtp::E_INTR) break;

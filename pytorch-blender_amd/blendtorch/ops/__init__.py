@@ -579,6 +579,12 @@ def _pool_module():
 # ---------------------------------------------------------------------------
 # consumer-model op: one-launch fp32 -> bf16 cast of a parameter list
 
+def _dense(t):
+    """Non-overlapping and dense (any dimension order we produce: contiguous or channels-last)."""
+    import torch
+    return t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last))
+
+
 def _cast_function():
     import torch
 
@@ -602,7 +608,7 @@ def _cast_function():
         @staticmethod
         def backward(ctx, *gs):
             have = [g for g in gs if g is not None]
-            dense = [g if g.is_non_overlapping_and_dense() else g.contiguous() for g in have]
+            dense = [g if _dense(g) else g.contiguous() for g in have]
             outs = [torch.empty_like(g, dtype=torch.float32) for g in dense]
             if dense:
                 launch(dense, outs, 1)
@@ -619,13 +625,14 @@ def cast_bf16(*tensors):
     """bf16 copies of GPU fp32 ``tensors`` (differentiable) in one gfx950
     launch per direction -- the consumer step's weight casts without a
     separate cast kernel per layer.  Tensors must be dense (any strides)."""
+    import torch
     global _CAST_FN
     if _CAST_FN is None:
         _CAST_FN = _cast_function()
     if len(tensors) > 32:
         raise ValueError('cast_bf16 takes at most 32 tensors per call')
     for t in tensors:
-        if not (t.is_cuda and t.dtype.is_floating_point and t.element_size() == 4 and t.is_non_overlapping_and_dense()):
+        if not (t.is_cuda and t.dtype == torch.float32 and _dense(t)):
             raise ValueError('cast_bf16 needs dense fp32 GPU tensors')
     return _CAST_FN.apply(*tensors)
 

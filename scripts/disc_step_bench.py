@@ -25,7 +25,7 @@ VARIANTS = {
 }
 
 
-def run(name, iters, batch, graph, fused_adam=False, fused_bn=True, dma=0):
+def run(name, iters, batch, graph, fused_adam=False, fused_bn=True, dma=0, cast='autocast', u8=False):
     dt, fmt = VARIANTS[name]
     dev = torch.device('cuda', 0)
     torch.manual_seed(0)
@@ -36,11 +36,28 @@ def run(name, iters, batch, graph, fused_adam=False, fused_bn=True, dma=0):
     amp = dt == torch.bfloat16
     if amp:
         x = x.to(torch.bfloat16)
+    if u8:
+        # what bench.py --consumer disc trains on: raw RGBA u8 NHWC frames,
+        # decoded (gamma, /255, bf16 NHWC) inside the step
+        from blendtorch import ops
+        raw = torch.randint(0, 256, (batch, 480, 640, 4), dtype=torch.uint8, device=dev)
+        dcfg = ops.DecodeConfig.unit(channels='rgb', gamma=2.2, dtype='bfloat16' if amp else 'float32',
+                                     layout='nhwc')
+
+    def inputs():
+        if not u8:
+            return x
+        y = ops.decode(raw, dcfg).permute(0, 3, 1, 2)
+        return y if amp else y.contiguous(memory_format=torch.channels_last)
 
     def step():
         opt.zero_grad(set_to_none=True)
-        with torch.autocast('cuda', dtype=torch.bfloat16, enabled=amp, cache_enabled=not graph):
-            out = model(x)
+        xi = inputs()
+        if amp and cast == 'fused':
+            out = model.forward_bf16(xi)
+        else:
+            with torch.autocast('cuda', dtype=torch.bfloat16, enabled=amp, cache_enabled=not graph):
+                out = model(xi)
         loss = crit(out.float(), torch.ones(batch, device=dev))
         loss.backward()
         opt.step()
@@ -76,6 +93,7 @@ def run(name, iters, batch, graph, fused_adam=False, fused_bn=True, dma=0):
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / iters * 1000
     return {'variant': name, 'graph': graph, 'fused_adam': fused_adam, 'fused_bn': fused_bn, 'dma_streams': dma,
+            'cast': cast, 'u8_input': u8,
             'ms_per_step': round(ms, 4), 'images_per_s': round(batch / ms * 1000, 1)}
 
 
@@ -88,15 +106,25 @@ def main():
     ap.add_argument('--no-fused-adam', dest='fused_adam', action='store_false',
                     help='foreach Adam instead of torch.optim.Adam(fused=True) (one multi-tensor kernel)')
     ap.add_argument('--dma', type=int, default=0, help='side streams of background H2D traffic (9.8 MB per step)')
+    ap.add_argument('--cpu-load', type=int, default=0, help='busy-looping CPU processes alongside (producer load)')
     ap.add_argument('--no-fused-bn', dest='fused_bn', action='store_false',
                     help='MIOpen BatchNorm + PyTorch LeakyReLU instead of the fused gfx950 op')
+    ap.add_argument('--cast', choices=['autocast', 'fused'], default='autocast',
+                    help='fused = Discriminator.forward_bf16 (one weight-cast launch per direction)')
+    ap.add_argument('--u8', action='store_true', help='train on raw u8 RGBA frames decoded inside the step')
     args = ap.parse_args()
+    import subprocess
+    hogs = [subprocess.Popen([sys.executable, '-c', 'while True: pass']) for _ in range(args.cpu_load)]
     torch.backends.cudnn.benchmark = True
     names = [args.only] if args.only else list(VARIANTS)
     graphs = {'both': (False, True), 'on': (True,), 'off': (False,)}[args.graph]
     for n in names:
         for g in graphs:
-            print(json.dumps(run(n, args.iters, args.batch, g, args.fused_adam, args.fused_bn, args.dma)), flush=True)
+            r = run(n, args.iters, args.batch, g, args.fused_adam, args.fused_bn, args.dma, args.cast, args.u8)
+            r['cpu_load'] = args.cpu_load
+            print(json.dumps(r), flush=True)
+    for h in hogs:
+        h.kill()
 
 
 if __name__ == '__main__':

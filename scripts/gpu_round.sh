@@ -73,6 +73,9 @@ for l in open('gpurun_out/sweep.jsonl'):
     d=json.loads(l); print(d['mode'], d['producers'], d['images_per_s'], d['sec_per_image'], d['ratio_vs_reference_row'], d['h2d_gbytes_per_s'])";;
     rtrace) timeout -k 10 200 rocprofv3 --kernel-trace --stats -d /tmp/rp_rtrace -o run --output-format csv -- python benchmarks/bench_replay.py --batch 8 --frames 1024 --steps 500 > gpurun_out/rtrace.log 2>&1; rc=$?
           mkdir -p gpurun_out/rtrace && find /tmp/rp_rtrace -name '*kernel_stats.csv' -exec cp {} gpurun_out/rtrace/ \; ; head -5 gpurun_out/rtrace/*kernel_stats.csv | cut -c1-220;;
+    mtrace:*) a="${step#mtrace:}"; BLENDTORCH_ROCTX=1 timeout -k 10 300 rocprofv3 --marker-trace --kernel-trace -d /tmp/rp_mt -o run --output-format csv -- python bench.py ${a//,/ } > gpurun_out/mtrace.log 2>&1; rc=$?; grep '^{' gpurun_out/mtrace.log | cut -c1-200
+          python scripts/marker_summary.py /tmp/rp_mt > gpurun_out/mtrace.txt 2>&1; cat gpurun_out/mtrace.txt
+          python scripts/trace_timeline.py /tmp/rp_mt --last 20000 > gpurun_out/mtrace_k.txt 2>&1; head -30 gpurun_out/mtrace_k.txt;;
     short) timeout -k 10 200 python bench.py --steps 20 --warmup 5 > gpurun_out/short.log 2>&1; rc=$?; grep '^{' gpurun_out/short.log;;
     dist2gloo) timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29557 bench.py --gpus 2 --backend gloo --steps 1000 --warmup 20 > gpurun_out/dist2gloo.log 2>&1; rc=$?; grep '^{' gpurun_out/dist2gloo.log;;
     replay) timeout -k 10 200 python benchmarks/bench_replay.py > gpurun_out/replay.log 2>&1 && timeout -k 10 200 python benchmarks/bench_replay.py --batch 64 --steps 500 >> gpurun_out/replay.log 2>&1 && timeout -k 10 200 python benchmarks/bench_replay.py --graph >> gpurun_out/replay.log 2>&1 && timeout -k 10 200 python benchmarks/bench_replay.py --graph --batch 64 --steps 500 >> gpurun_out/replay.log 2>&1 && timeout -k 10 200 python benchmarks/bench_replay.py --fill producers --frames 2048 --batch 64 --steps 500 >> gpurun_out/replay.log 2>&1; rc=$?; cat gpurun_out/replay.log | grep '^{';;

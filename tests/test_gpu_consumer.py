@@ -58,4 +58,4 @@ def test_discriminator_forward_bf16_equals_autocast(dev):
     for ma, mb in zip(a.modules(), b.modules()):
         if isinstance(ma, ops.BatchNormLeakyReLU2d):
             assert int(ma.num_batches_tracked) == int(mb.num_batches_tracked) == 1   # counted on the device
-            torch.testing.assert_close(mb.running_mean, ma.running_mean, rtol=0, atol=0)
+            torch.testing.assert_close(mb.running_mean, ma.running_mean, rtol=1e-4, atol=1e-6)
