@@ -132,6 +132,9 @@ def parse_args(argv=None):
     ap.add_argument('--backend', choices=['nccl', 'gloo'], default='nccl',
                     help='process-group backend (nccl = RCCL over xGMI; gloo only to rehearse several ranks on one GPU)')
     ap.add_argument('--start-port', type=int, default=0)
+    ap.add_argument('--optim', choices=['gfx950', 'torch'], default='gfx950',
+                    help='disc consumer optimizer: gfx950 = ops.FusedAdam (two launches per step); '
+                         'torch = torch.optim.Adam(fused=True, capturable=True)')
     ap.add_argument('--cast', choices=['fused', 'autocast'], default='fused',
                     help='disc consumer, bf16: fused = all conv weights cast in one gfx950 launch per direction '
                          '(Discriminator.forward_bf16); autocast = torch.autocast (a cast per layer each way)')
@@ -293,7 +296,13 @@ def main(argv=None):
         use_graph = args.graph == 'on' or (args.graph == 'auto' and (world == 1 or args.backend == 'nccl'))
         # fused Adam: one multi-tensor kernel for the whole update (0.95 -> 0.84 ms graphed step,
         # profiles/consumer_step.md); capturable keeps its step counters on the GPU for the graph
-        opt = torch.optim.Adam(model.parameters(), lr=2e-4, capturable=use_graph, fused=True)
+        if args.optim == 'gfx950':
+            # ops.FusedAdam: one 1-lane schedule kernel + one update kernel over all
+            # parameters (device step counter: capturable)
+            from blendtorch import ops
+            opt = ops.FusedAdam(model.parameters(), lr=2e-4)
+        else:
+            opt = torch.optim.Adam(model.parameters(), lr=2e-4, capturable=use_graph, fused=True)
         crit = torch.nn.BCELoss()
 
     WARM_RESERVE = 2000   # extra warm-up batches allowed while producers come up
@@ -499,6 +508,7 @@ def main(argv=None):
                 'consumer_step': stepper.state if stepper is not None else None,
                 'decode_in_step': step_decode,
                 'cast': args.cast if amp else None,
+                'optim': args.optim if model is not None else None,
                 'consumer_collectives_per_step': stepper.collectives if stepper is not None else None,
             },
             'sec_per_image': round(tmax / images, 7),

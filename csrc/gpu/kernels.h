@@ -200,5 +200,36 @@ struct CastParams {
 };
 hipError_t multi_cast(const CastParams& p, hipStream_t stream);
 
+// Adam / AdamW over a list of fp32 parameters in ONE launch, graph-capturable:
+// the step counter and the bias corrections live on the device.
+//   adam_schedule (one lane): step += 1; sched = {lr / (1 - b1^step),
+//                             1 / sqrt(1 - b2^step), lr}   (hp = {lr})
+//   adam_update: per element, PyTorch's Adam arithmetic
+//       g = grad (+ wd * p unless decoupled); decoupled: p *= 1 - lr * wd
+//       m = b1 m + (1 - b1) g;  v = b2 v + (1 - b2) g^2
+//       p -= sched[0] * m / (sqrt(v) * sched[1] + eps)
+//     grads fp32 or bf16 (grad_bf16); optional bf16 shadow copy of the new
+//     weights (shadow[k] != nullptr), what a bf16 forward reads next step.
+// The tensors' 4-element groups are laid end to end: tensor k owns groups
+// [gstart[k], gstart[k+1]); each lane updates one group.
+constexpr int kMaxAdam = 32;
+struct AdamParams {
+  float* p[kMaxAdam] = {};
+  const void* g[kMaxAdam] = {};
+  float* m[kMaxAdam] = {};
+  float* v[kMaxAdam] = {};
+  uint16_t* shadow[kMaxAdam] = {};
+  int64_t numel[kMaxAdam] = {};
+  int64_t gstart[kMaxAdam + 1] = {};
+  int n = 0;
+  int grad_bf16 = 0;
+  int decoupled = 0;   // AdamW
+  int maximize = 0;
+  float beta1 = 0.9f, beta2 = 0.999f, eps = 1e-8f, weight_decay = 0.f;
+  const float* sched = nullptr;   // device [3], written by adam_schedule
+};
+hipError_t adam_schedule(float* step, const float* hp, float* sched, float beta1, float beta2, hipStream_t stream);
+hipError_t adam_update(const AdamParams& p, hipStream_t stream);
+
 }  // namespace gpu
 }  // namespace btn

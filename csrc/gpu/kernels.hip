@@ -1200,5 +1200,128 @@ hipError_t multi_cast(const CastParams& p, hipStream_t stream) {
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Adam / AdamW
+// ---------------------------------------------------------------------------
+namespace {
+
+// One lane: the step counter and the bias corrections, so that the update
+// kernel's blocks all read a value no block is writing.
+__global__ void adam_schedule_kernel(float* step, const float* hp, float* sched, float beta1, float beta2) {
+  if (threadIdx.x != 0) return;
+  const float s = step[0] + 1.f;
+  step[0] = s;
+  const float lr = hp[0];
+  const double bc1 = 1.0 - pow(double(beta1), double(s));
+  const double bc2 = 1.0 - pow(double(beta2), double(s));
+  sched[0] = float(double(lr) / bc1);
+  sched[1] = float(1.0 / sqrt(bc2));
+  sched[2] = lr;
+}
+
+template <bool GBF16>
+__global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
+  const int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x;   // 4-element group
+  if (q >= a.gstart[a.n]) return;
+  int k = 0;
+  while (q >= a.gstart[k + 1]) ++k;     // <= kMaxAdam compares, mostly uniform across a wave
+  const int64_t e0 = (q - a.gstart[k]) * 4;
+  const int64_t n = a.numel[k];
+  const float step_size = a.sched[0], inv_bc2 = a.sched[1], lr = a.sched[2];
+  const float b1 = a.beta1, b2 = a.beta2, wd = a.weight_decay;
+  float* P = a.p[k];
+  float* M = a.m[k];
+  float* V = a.v[k];
+  float pv[4], gv[4], mv[4], vv[4];
+  const bool full = e0 + 4 <= n;   // tensors are 16-byte aligned (host-checked), so a full group is one dwordx4
+  if (full) {
+    const float4 p4 = *reinterpret_cast<const float4*>(P + e0);
+    const float4 m4 = *reinterpret_cast<const float4*>(M + e0);
+    const float4 v4 = *reinterpret_cast<const float4*>(V + e0);
+    pv[0] = p4.x, pv[1] = p4.y, pv[2] = p4.z, pv[3] = p4.w;
+    mv[0] = m4.x, mv[1] = m4.y, mv[2] = m4.z, mv[3] = m4.w;
+    vv[0] = v4.x, vv[1] = v4.y, vv[2] = v4.z, vv[3] = v4.w;
+    if constexpr (GBF16) {
+      const uint2 g2 = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(a.g[k]) + e0);
+      gv[0] = __uint_as_float(g2.x << 16), gv[1] = __uint_as_float(g2.x & 0xFFFF0000u);
+      gv[2] = __uint_as_float(g2.y << 16), gv[3] = __uint_as_float(g2.y & 0xFFFF0000u);
+    } else {
+      const float4 g4 = *reinterpret_cast<const float4*>(static_cast<const float*>(a.g[k]) + e0);
+      gv[0] = g4.x, gv[1] = g4.y, gv[2] = g4.z, gv[3] = g4.w;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool in = e0 + j < n;
+      pv[j] = in ? P[e0 + j] : 0.f;
+      mv[j] = in ? M[e0 + j] : 0.f;
+      vv[j] = in ? V[e0 + j] : 0.f;
+      if constexpr (GBF16)
+        gv[j] = in ? __uint_as_float(uint32_t(static_cast<const uint16_t*>(a.g[k])[e0 + j]) << 16) : 0.f;
+      else
+        gv[j] = in ? static_cast<const float*>(a.g[k])[e0 + j] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float g = a.maximize ? -gv[j] : gv[j];
+    if (wd != 0.f) {
+      if (a.decoupled) pv[j] *= 1.f - lr * wd;
+      else g += wd * pv[j];
+    }
+    mv[j] = b1 * mv[j] + (1.f - b1) * g;
+    vv[j] = b2 * vv[j] + (1.f - b2) * g * g;
+    pv[j] -= step_size * mv[j] / (sqrtf(vv[j]) * inv_bc2 + a.eps);
+  }
+  uint16_t* S = a.shadow[k];
+  if (full) {
+    *reinterpret_cast<float4*>(P + e0) = make_float4(pv[0], pv[1], pv[2], pv[3]);
+    *reinterpret_cast<float4*>(M + e0) = make_float4(mv[0], mv[1], mv[2], mv[3]);
+    *reinterpret_cast<float4*>(V + e0) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+    if (S) {
+      uint2 s2;
+      s2.x = uint32_t(f2bf(pv[0])) | (uint32_t(f2bf(pv[1])) << 16);
+      s2.y = uint32_t(f2bf(pv[2])) | (uint32_t(f2bf(pv[3])) << 16);
+      *reinterpret_cast<uint2*>(S + e0) = s2;
+    }
+  } else {
+    for (int j = 0; j < 4 && e0 + j < n; ++j) {
+      P[e0 + j] = pv[j], M[e0 + j] = mv[j], V[e0 + j] = vv[j];
+      if (S) S[e0 + j] = f2bf(pv[j]);
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t adam_schedule(float* step, const float* hp, float* sched, float beta1, float beta2, hipStream_t stream) {
+  if (!step || !hp || !sched) return hipErrorInvalidValue;
+  adam_schedule_kernel<<<1, 64, 0, stream>>>(step, hp, sched, beta1, beta2);
+  return hipGetLastError();
+}
+
+hipError_t adam_update(const AdamParams& p, hipStream_t stream) {
+  if (p.n <= 0) return hipSuccess;
+  if (p.n > kMaxAdam || !p.sched) return hipErrorInvalidValue;
+  if (p.gstart[0] != 0) return hipErrorInvalidValue;
+  for (int k = 0; k < p.n; ++k) {
+    if (p.numel[k] < 0 || p.gstart[k + 1] - p.gstart[k] != (p.numel[k] + 3) / 4) return hipErrorInvalidValue;
+    if (p.numel[k] > 0 && (!p.p[k] || !p.g[k] || !p.m[k] || !p.v[k])) return hipErrorInvalidValue;
+    // full groups are read and written as 16-byte (8-byte for bf16) vectors
+    const uintptr_t mis = reinterpret_cast<uintptr_t>(p.p[k]) | reinterpret_cast<uintptr_t>(p.m[k]) |
+                          reinterpret_cast<uintptr_t>(p.v[k]) |
+                          (reinterpret_cast<uintptr_t>(p.g[k]) << (p.grad_bf16 ? 1 : 0)) |
+                          (reinterpret_cast<uintptr_t>(p.shadow[k]) << 1);
+    if (mis & 15) return hipErrorInvalidValue;
+  }
+  const int64_t groups = p.gstart[p.n];
+  if (groups == 0) return hipSuccess;
+  const int64_t blocks = (groups + kBlock - 1) / kBlock;
+  if (blocks > int64_t(1) << 30) return hipErrorInvalidValue;
+  if (p.grad_bf16) adam_update_kernel<true><<<unsigned(blocks), kBlock, 0, stream>>>(p);
+  else adam_update_kernel<false><<<unsigned(blocks), kBlock, 0, stream>>>(p);
+  return hipGetLastError();
+}
+
 }  // namespace gpu
 }  // namespace btn

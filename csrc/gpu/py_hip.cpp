@@ -215,6 +215,39 @@ PYBIND11_MODULE(_hip, m) {
           check(multi_cast(p, stream_of(stream)), "multi_cast");
         });
 
+  m.def("adam_schedule",
+        [](uintptr_t step, uintptr_t hp, uintptr_t sched, float beta1, float beta2, uintptr_t stream) {
+          check(adam_schedule(ptr<float>(step), ptr<const float>(hp), ptr<float>(sched), beta1, beta2,
+                              stream_of(stream)),
+                "adam_schedule");
+        });
+
+  m.def("adam_update",
+        [](std::vector<uintptr_t> params, std::vector<uintptr_t> grads, std::vector<uintptr_t> exp_avg,
+           std::vector<uintptr_t> exp_avg_sq, std::vector<uintptr_t> shadow, std::vector<int64_t> numel,
+           uintptr_t sched, int grad_bf16, float beta1, float beta2, float eps, float weight_decay, int decoupled,
+           int maximize, uintptr_t stream) {
+          const size_t n = params.size();
+          if (grads.size() != n || exp_avg.size() != n || exp_avg_sq.size() != n || shadow.size() != n ||
+              numel.size() != n || n > size_t(kMaxAdam))
+            throw std::invalid_argument("adam_update: list lengths differ or exceed kMaxAdam");
+          AdamParams a;
+          a.n = int(n);
+          for (size_t k = 0; k < n; ++k) {
+            a.p[k] = ptr<float>(params[k]);
+            a.g[k] = ptr<const void>(grads[k]);
+            a.m[k] = ptr<float>(exp_avg[k]);
+            a.v[k] = ptr<float>(exp_avg_sq[k]);
+            a.shadow[k] = ptr<uint16_t>(shadow[k]);
+            a.numel[k] = numel[k];
+            a.gstart[k + 1] = a.gstart[k] + (numel[k] + 3) / 4;
+          }
+          a.sched = ptr<const float>(sched);
+          a.grad_bf16 = grad_bf16, a.decoupled = decoupled, a.maximize = maximize;
+          a.beta1 = beta1, a.beta2 = beta2, a.eps = eps, a.weight_decay = weight_decay;
+          check(adam_update(a, stream_of(stream)), "adam_update");
+        });
+
   m.def("color4x4",
         [](uintptr_t src, uintptr_t dst, uintptr_t lut, uintptr_t M, uintptr_t bias, uintptr_t flip, int B, int H,
            int W, int Cout, int flip_all, uintptr_t stream) {

@@ -777,4 +777,7 @@ def __getattr__(name):
         if _BN_MODULE is None:
             _BN_MODULE = _bn_module()
         return _BN_MODULE
+    if name == 'FusedAdam':
+        from .adam import FusedAdam
+        return FusedAdam
     raise AttributeError(f'module {__name__!r} has no attribute {name!r}')

@@ -80,13 +80,21 @@ class CapturedStep:
         algorithm search, optimizer state).
     graph: False runs the same step eagerly (fallback / comparison).
 
+    split: capture forward+loss and backward+update as two graphs sharing one
+        memory pool, so a caller can act between them: ``step(x, mid=fn)``
+        runs ``fn()`` after enqueuing the forward (e.g. to gate the next
+        batches' host->device DMA onto the backward's conv kernels instead of
+        the memory-bound forward, see bench.py --dma-phase).
+
     ``state`` is ``'graph'`` after a successful capture, ``'eager'`` otherwise.
     """
 
     def __init__(self, model: torch.nn.Module, optimizer: torch.optim.Optimizer,
                  loss_fn: Callable[[torch.nn.Module, torch.Tensor], torch.Tensor], allreduce: bool = True,
-                 warmup: int = 3, graph: bool = True, group=None, bucket_mb: float = 64.0):
+                 warmup: int = 3, graph: bool = True, group=None, bucket_mb: float = 64.0, split: bool = False):
         self.model, self.opt, self.loss_fn = model, optimizer, loss_fn
+        self.split = split
+        self.graph_bwd: Optional[torch.cuda.CUDAGraph] = None
         self.allreduce, self.warmup, self.group, self.bucket_mb = allreduce, warmup, group, bucket_mb
         self.state = 'pending' if graph else 'eager'
         self.graph: Optional[torch.cuda.CUDAGraph] = None
@@ -95,15 +103,20 @@ class CapturedStep:
         self.collectives = 0
         self.error = None
 
-    def _train(self, x):
+    def _forward(self, x):
         self.opt.zero_grad(set_to_none=True)
-        loss = self.loss_fn(self.model, x)
+        return self.loss_fn(self.model, x)
+
+    def _backward(self, loss):
         loss.backward()
         if self.allreduce:
             self.collectives = allreduce_gradients(self.model.parameters(), self.group, self.bucket_mb,
                                                    force=self.allreduce == 'always')
         self.opt.step()
         return loss.detach()
+
+    def _train(self, x):
+        return self._backward(self._forward(x))
 
     def _capture(self, x):
         self.x = torch.empty_like(x)         # same strides (channels-last stays channels-last)
@@ -117,22 +130,43 @@ class CapturedStep:
         g = torch.cuda.CUDAGraph()
         try:
             self.opt.zero_grad(set_to_none=True)
-            with torch.cuda.graph(g):
-                self.loss = self._train(self.x)
+            if self.split:
+                with torch.cuda.graph(g):
+                    loss = self._forward(self.x)
+                gb = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gb, pool=g.pool()):
+                    self.loss = self._backward(loss)
+                del loss
+                self.graph_bwd = gb
+            else:
+                with torch.cuda.graph(g):
+                    self.loss = self._train(self.x)
             self.graph, self.state = g, 'graph'
         except RuntimeError as e:          # keep the run alive; callers report which mode ran
             self.error = str(e)
             self.state = 'eager'
 
-    def __call__(self, x: torch.Tensor) -> torch.Tensor:
+    def _replay(self, mid):
+        self.graph.replay()
+        if self.graph_bwd is not None:
+            if mid is not None:
+                mid()
+            self.graph_bwd.replay()
+        elif mid is not None:
+            mid()
+
+    def __call__(self, x: torch.Tensor, mid: Optional[Callable[[], None]] = None) -> torch.Tensor:
         if self.state == 'pending':
             self._capture(x)
             if self.state == 'graph':
-                self.graph.replay()
+                self._replay(mid)
                 return self.loss
         if self.state == 'graph':
             if x.data_ptr() != self.x.data_ptr():
                 self.x.copy_(x)
-            self.graph.replay()
+            self._replay(mid)
             return self.loss
-        return self._train(x)
+        loss = self._forward(x)
+        if mid is not None:
+            mid()
+        return self._backward(loss)

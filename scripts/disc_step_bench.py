@@ -25,12 +25,17 @@ VARIANTS = {
 }
 
 
-def run(name, iters, batch, graph, fused_adam=False, fused_bn=True, dma=0, cast='autocast', u8=False):
+def run(name, iters, batch, graph, fused_adam=False, fused_bn=True, dma=0, cast='autocast', u8=False, optim='torch',
+        dma_phase='none', split=False):
     dt, fmt = VARIANTS[name]
     dev = torch.device('cuda', 0)
     torch.manual_seed(0)
     model = Discriminator(nc=3, ndf=32, adaptive=True, fused=fused_bn).to(dev).to(memory_format=fmt)
-    opt = torch.optim.Adam(model.parameters(), lr=2e-4, capturable=graph, fused=fused_adam or None)
+    if optim == 'gfx950':
+        from blendtorch import ops
+        opt = ops.FusedAdam(model.parameters(), lr=2e-4)
+    else:
+        opt = torch.optim.Adam(model.parameters(), lr=2e-4, capturable=graph, fused=fused_adam or None)
     crit = torch.nn.BCELoss()
     x = torch.rand(batch, 3, 480, 640, device=dev).to(memory_format=fmt)
     amp = dt == torch.bfloat16
@@ -72,12 +77,38 @@ def run(name, iters, batch, graph, fused_adam=False, fused_bn=True, dma=0, cast=
     hsrc = [torch.empty(1228800, dtype=torch.uint8).pin_memory() for _ in range(8)] if dma else []
     ddst = [torch.empty(1228800, dtype=torch.uint8, device=dev) for _ in range(8)] if dma else []
 
-    def traffic():
+    def copies():
+        # dma_phase: none = issued unordered (they run whenever the DMA engines
+        # are free); start = gated on the step's start, so they overlap the
+        # forward (what the stream loader's post events do); mid = gated
+        # between the forward and the backward graph
+        ev = None
+        if dma_phase != 'none':
+            ev = torch.cuda.Event()
+            ev.record()
         for i in range(8 if dma else 0):
             with torch.cuda.stream(side[i % dma]):
+                if ev is not None:
+                    torch.cuda.current_stream().wait_event(ev)
                 ddst[i].copy_(hsrc[i], non_blocking=True)
     fn = step
-    if graph:
+    if graph and split:
+        from blendtorch.parallel.step import CapturedStep
+
+        def loss_fn(m, _):
+            xi = inputs()
+            if amp and cast == 'fused':
+                out = m.forward_bf16(xi)
+            else:
+                with torch.autocast('cuda', dtype=torch.bfloat16, enabled=amp, cache_enabled=False):
+                    out = m(xi)
+            return crit(out.float(), torch.ones(batch, device=dev))
+        stepper = CapturedStep(model, opt, loss_fn, allreduce=False, split=True)
+        probe = torch.zeros(1, device=dev)
+        fn = (lambda: stepper(probe, mid=copies)) if dma_phase == 'mid' else (lambda: stepper(probe))
+        for _ in range(3):
+            fn()
+    elif graph:
         g = torch.cuda.CUDAGraph()
         opt.zero_grad(set_to_none=True)
         with torch.cuda.graph(g):
@@ -88,12 +119,13 @@ def run(name, iters, batch, graph, fused_adam=False, fused_bn=True, dma=0, cast=
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(iters):
-        traffic()
+        if dma and dma_phase != 'mid':
+            copies()
         fn()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / iters * 1000
     return {'variant': name, 'graph': graph, 'fused_adam': fused_adam, 'fused_bn': fused_bn, 'dma_streams': dma,
-            'cast': cast, 'u8_input': u8,
+            'cast': cast, 'u8_input': u8, 'optim': optim, 'dma_phase': dma_phase if dma else None, 'split': split,
             'ms_per_step': round(ms, 4), 'images_per_s': round(batch / ms * 1000, 1)}
 
 
@@ -111,6 +143,9 @@ def main():
                     help='MIOpen BatchNorm + PyTorch LeakyReLU instead of the fused gfx950 op')
     ap.add_argument('--cast', choices=['autocast', 'fused'], default='autocast',
                     help='fused = Discriminator.forward_bf16 (one weight-cast launch per direction)')
+    ap.add_argument('--optim', choices=['torch', 'gfx950'], default='torch')
+    ap.add_argument('--dma-phase', choices=['none', 'start', 'mid'], default='none')
+    ap.add_argument('--split', action='store_true', help='forward and backward as two graphs (CapturedStep split)')
     ap.add_argument('--u8', action='store_true', help='train on raw u8 RGBA frames decoded inside the step')
     args = ap.parse_args()
     import subprocess
@@ -120,7 +155,8 @@ def main():
     graphs = {'both': (False, True), 'on': (True,), 'off': (False,)}[args.graph]
     for n in names:
         for g in graphs:
-            r = run(n, args.iters, args.batch, g, args.fused_adam, args.fused_bn, args.dma, args.cast, args.u8)
+            r = run(n, args.iters, args.batch, g, args.fused_adam, args.fused_bn, args.dma, args.cast, args.u8, args.optim,
+                    args.dma_phase, args.split or args.dma_phase == 'mid')
             r['cpu_load'] = args.cpu_load
             print(json.dumps(r), flush=True)
     for h in hogs:

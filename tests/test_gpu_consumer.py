@@ -59,3 +59,33 @@ def test_discriminator_forward_bf16_equals_autocast(dev):
         if isinstance(ma, ops.BatchNormLeakyReLU2d):
             assert int(ma.num_batches_tracked) == int(mb.num_batches_tracked) == 1   # counted on the device
             torch.testing.assert_close(mb.running_mean, ma.running_mean, rtol=1e-4, atol=1e-6)
+
+
+def test_split_graph_step_equals_single_graph(dev):
+    """CapturedStep(split=True): forward and backward+update as two graphs in
+    one pool replay to the same weights as the one-graph step."""
+    from blendtorch.models import Discriminator
+    from blendtorch.parallel.step import CapturedStep
+    torch.manual_seed(0)
+    nets = [Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=torch.channels_last)
+            for _ in range(2)]
+    nets[1].load_state_dict(nets[0].state_dict())
+    crit = torch.nn.BCELoss()
+
+    def loss_fn(m, x):
+        out = m.forward_bf16(x).float()
+        return crit(out, torch.ones_like(out))
+
+    steps = [CapturedStep(n, ops.FusedAdam(n.parameters(), lr=2e-4), loss_fn, allreduce=False, warmup=2,
+                          split=s) for n, s in zip(nets, (False, True))]
+    g = torch.Generator(device=dev).manual_seed(5)
+    xs = [torch.rand(4, 3, 96, 128, device=dev, generator=g).to(torch.bfloat16)
+          .contiguous(memory_format=torch.channels_last) for _ in range(4)]
+    hits = []
+    for x in xs:
+        steps[0](x)
+        steps[1](x, mid=lambda: hits.append(1))
+    torch.cuda.synchronize()
+    assert steps[1].state == 'graph' and steps[1].graph_bwd is not None and len(hits) == len(xs)
+    for pa, pb in zip(nets[0].parameters(), nets[1].parameters()):
+        torch.testing.assert_close(pb, pa, rtol=0, atol=0)

@@ -224,3 +224,28 @@ def test_manual_grad_allreduce_gloo_world2():
         p.join(timeout=60)
     for r in res:
         assert r[1:] == (True, True), r
+
+
+def test_captured_step_split_mid_hook_eager():
+    """split/mid: the hook runs between forward and backward, and the update
+    equals the unsplit step (eager on the CPU; GPU graph replay in
+    tests/test_gpu_consumer.py)."""
+    from blendtorch.parallel.step import CapturedStep
+    order = []
+    torch.manual_seed(0)
+    a = torch.nn.Sequential(torch.nn.Linear(4, 3), torch.nn.ReLU(), torch.nn.Linear(3, 1))
+    b = torch.nn.Sequential(torch.nn.Linear(4, 3), torch.nn.ReLU(), torch.nn.Linear(3, 1))
+    b.load_state_dict(a.state_dict())
+
+    def loss_fn(mod, x):
+        order.append('fwd')
+        return mod(x).pow(2).mean()
+
+    sa = CapturedStep(a, torch.optim.SGD(a.parameters(), lr=0.1), loss_fn, allreduce=False, graph=False, split=True)
+    sb = CapturedStep(b, torch.optim.SGD(b.parameters(), lr=0.1), loss_fn, allreduce=False, graph=False)
+    x = torch.randn(8, 4, generator=torch.Generator().manual_seed(1))
+    sa(x, mid=lambda: order.append('mid'))
+    assert order == ['fwd', 'mid']
+    sb(x)
+    for p, q in zip(a.parameters(), b.parameters()):
+        assert torch.equal(p, q)
