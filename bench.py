@@ -132,6 +132,10 @@ def parse_args(argv=None):
     ap.add_argument('--backend', choices=['nccl', 'gloo'], default='nccl',
                     help='process-group backend (nccl = RCCL over xGMI; gloo only to rehearse several ranks on one GPU)')
     ap.add_argument('--start-port', type=int, default=0)
+    ap.add_argument('--dma-phase', choices=['start', 'mid'], default='start',
+                    help='disc consumer: when the next frames\' host->device DMA may start -- start = when the '
+                         'step begins (overlapping the memory-bound forward); mid = between the forward and the '
+                         'backward graph (DeviceLoader(defer_post=True) + CapturedStep(split=True))')
     ap.add_argument('--optim', choices=['gfx950', 'torch'], default='gfx950',
                     help='disc consumer optimizer: gfx950 = ops.FusedAdam (two launches per step); '
                          'torch = torch.optim.Adam(fused=True, capturable=True)')
@@ -283,6 +287,8 @@ def main(argv=None):
                   instance_args=[['--mode', args.mode, '--sndhwm', '10', '--resolution', f'{res_w}x{res_h}'] + (['--shm', str(shm_slots), '--codec', args.codec] if shm_slots else [])]
                   * nprod)
     model = opt = None
+    # the next frames' DMA starts between the step's forward and backward graphs
+    dma_mid = args.consumer == 'disc' and args.dma_phase == 'mid' and args.dist != 'scatter'
     if args.consumer == 'disc':
         if os.environ.get('BT_CUDNN_BENCHMARK', '1') == '1':
             torch.backends.cudnn.benchmark = True   # MIOpen find: best conv kernels for these fixed shapes
@@ -332,7 +338,8 @@ def main(argv=None):
                 dl = DeviceLoader(addrs, batch_size=per_step, decode=ldec, device=device,
                                   max_items=total_batches * per_step, prefetch=6,
                                   io_threads=args.io_threads or None, timeoutms=60000, h2d=args.h2d,
-                                  launch_depth=args.launch_depth, copy_streams=args.copy_streams)
+                                  launch_depth=args.launch_depth, copy_streams=args.copy_streams,
+                                  defer_post=dma_mid)
         if args.dist == 'scatter':
             it = iter(ScatterLoader(dl, args.batch, decode, device, total_batches))
         else:
@@ -369,10 +376,10 @@ def main(argv=None):
         if model is not None:
             from blendtorch.parallel.step import CapturedStep
             stepper = CapturedStep(model, opt, loss_fn, graph=use_graph,
-                                   allreduce='always' if args.force_pg else dist.is_initialized())
+                                   allreduce='always' if args.force_pg else dist.is_initialized(), split=dma_mid)
 
         def graphed(x):
-            stepper(x)
+            stepper(x, mid=dl.release if (dma_mid and dl is not None) else None)
             if stepper.error:
                 print(f'[bench] HIP graph capture failed, eager steps: {stepper.error}', file=sys.stderr, flush=True)
                 stepper.error = None
@@ -509,6 +516,7 @@ def main(argv=None):
                 'decode_in_step': step_decode,
                 'cast': args.cast if amp else None,
                 'optim': args.optim if model is not None else None,
+                'dma_phase': args.dma_phase if model is not None else None,
                 'consumer_collectives_per_step': stepper.collectives if stepper is not None else None,
             },
             'sec_per_image': round(tmax / images, 7),

@@ -228,6 +228,46 @@ struct AdamParams {
   float beta1 = 0.9f, beta2 = 0.999f, eps = 1e-8f, weight_decay = 0.f;
   const float* sched = nullptr;   // device [3], written by adam_schedule
 };
+// Weight gradient of a 4x4 / stride-2 / pad-1 convolution over channels-last
+// bf16 activations on the MFMA units (conv.hip): x [N][H][W][Cin],
+// dy [N][Ho][Wo][Cout] -> fp32 dW written at the given element strides of
+// (co, ci, kh, kw).  Cin % 32 == 0, Cout % 64 == 0.  `partial` is scratch of
+// slices * Cout * 16 * Cin floats; slices * px_per_slice >= M, px_per_slice % 32 == 0.
+struct ConvWgradParams {
+  const uint16_t* x = nullptr;
+  const uint16_t* dy = nullptr;
+  float* partial = nullptr;
+  int N = 0, H = 0, W = 0, Cin = 0, Ho = 0, Wo = 0, Cout = 0;
+  int64_t M = 0;
+  int slices = 0;
+  int64_t px_per_slice = 0;
+};
+bool conv_wgrad_supported(int Cin, int Cout);
+int conv_wgrad_slices(int64_t M, int Cin, int Cout, int target_blocks);
+hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_t s_ci, int64_t s_kh, int64_t s_kw,
+                      hipStream_t stream);
+
+// Forward 4x4 / stride-2 / pad-1 convolution on the MFMA units (conv.hip):
+// x [N][H][W][Cin] bf16, w [Cout][4][4][Cin] bf16 (channels-last weight) ->
+// y [N][Ho][Wo][Cout] bf16.  stats (nullable): [conv_fwd_tiles(M)][2][Cout]
+// fp32 per-tile sum / sum of squares of the rounded y -- the partial rows
+// bn_finalize_tiles folds into BatchNorm statistics.
+struct ConvFwdParams {
+  const uint16_t* x = nullptr;
+  const uint16_t* w = nullptr;
+  uint16_t* y = nullptr;
+  float* stats = nullptr;
+  int N = 0, H = 0, W = 0, Cin = 0, Ho = 0, Wo = 0, Cout = 0;
+  int64_t M = 0;
+};
+bool conv_fwd_supported(int Cin, int Cout);
+int64_t conv_fwd_tiles(int64_t M);
+hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream);
+// bn_finalize over `nblocks` partial rows produced elsewhere (conv_fwd's epilogue)
+hipError_t bn_finalize_rows(const float* partial, int nblocks, int64_t M, int C, float eps, float momentum,
+                            float* mean, float* invstd, float* running_mean, float* running_var, hipStream_t stream,
+                            int64_t* num_batches_tracked);
+
 hipError_t adam_schedule(float* step, const float* hp, float* sched, float beta1, float beta2, hipStream_t stream);
 hipError_t adam_update(const AdamParams& p, hipStream_t stream);
 

@@ -1105,6 +1105,15 @@ hipError_t bn_finalize(const float* partial, int64_t M, int C, int dtype, float 
   return hipGetLastError();
 }
 
+hipError_t bn_finalize_rows(const float* partial, int nblocks, int64_t M, int C, float eps, float momentum,
+                            float* mean, float* invstd, float* running_mean, float* running_var, hipStream_t stream,
+                            int64_t* num_batches_tracked) {
+  if (nblocks <= 0 || M <= 0 || C <= 0 || !partial || !mean || !invstd) return hipErrorInvalidValue;
+  bn_finalize_kernel<<<C, kBlock, 0, stream>>>(partial, nblocks, M, C, eps, momentum, mean, invstd, running_mean,
+                                                running_var, num_batches_tracked);
+  return hipGetLastError();
+}
+
 hipError_t bn_apply(const void* x, void* y, int64_t M, int C, int dtype, const float* mean, const float* invstd,
                     const float* w, const float* b, float slope, hipStream_t stream) {
   if (!bn_shape_ok(M, C, dtype)) return hipErrorInvalidValue;

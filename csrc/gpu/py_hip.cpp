@@ -215,6 +215,49 @@ PYBIND11_MODULE(_hip, m) {
           check(multi_cast(p, stream_of(stream)), "multi_cast");
         });
 
+  m.def("conv_wgrad_slices", &conv_wgrad_slices);
+  m.def("conv_wgrad",
+        [](uintptr_t x, uintptr_t dy, uintptr_t partial, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
+           int slices, int64_t px_per_slice, uintptr_t out, int64_t s_co, int64_t s_ci, int64_t s_kh, int64_t s_kw,
+           uintptr_t stream) {
+          ConvWgradParams p;
+          p.x = ptr<const uint16_t>(x);
+          p.dy = ptr<const uint16_t>(dy);
+          p.partial = ptr<float>(partial);
+          p.N = N, p.H = H, p.W = W, p.Cin = Cin, p.Ho = Ho, p.Wo = Wo, p.Cout = Cout;
+          p.M = int64_t(N) * Ho * Wo;
+          p.slices = slices;
+          p.px_per_slice = px_per_slice;
+          check(conv_wgrad(p, ptr<float>(out), s_co, s_ci, s_kh, s_kw, stream_of(stream)), "conv_wgrad");
+        });
+
+  m.def("conv_fwd_tiles", &conv_fwd_tiles);
+  m.def("conv_fwd",
+        [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, int N, int H, int W, int Cin, int Ho, int Wo,
+           int Cout, uintptr_t stream) {
+          ConvFwdParams p;
+          p.x = ptr<const uint16_t>(x);
+          p.w = ptr<const uint16_t>(w);
+          p.y = ptr<uint16_t>(y);
+          p.stats = ptr<float>(stats);
+          p.N = N, p.H = H, p.W = W, p.Cin = Cin, p.Ho = Ho, p.Wo = Wo, p.Cout = Cout;
+          p.M = int64_t(N) * Ho * Wo;
+          check(conv_fwd(p, stream_of(stream)), "conv_fwd");
+        });
+  // BatchNorm+LeakyReLU forward from conv_fwd's per-tile statistics: finalize + apply
+  m.def("bn_forward_from_stats",
+        [](uintptr_t x, uintptr_t y, int64_t M, int C, int dtype, uintptr_t stats, int nrows, float eps,
+           float momentum, uintptr_t mean, uintptr_t invstd, uintptr_t rm, uintptr_t rv, uintptr_t w, uintptr_t b,
+           float slope, uintptr_t stream, uintptr_t tracked) {
+          hipStream_t s = stream_of(stream);
+          check(bn_finalize_rows(ptr<const float>(stats), nrows, M, C, eps, momentum, ptr<float>(mean),
+                                 ptr<float>(invstd), ptr<float>(rm), ptr<float>(rv), s, ptr<int64_t>(tracked)),
+                "bn_finalize_rows");
+          check(bn_apply(ptr<const void>(x), ptr<void>(y), M, C, dtype, ptr<const float>(mean),
+                         ptr<const float>(invstd), ptr<const float>(w), ptr<const float>(b), slope, s),
+                "bn_apply");
+        });
+
   m.def("adam_schedule",
         [](uintptr_t step, uintptr_t hp, uintptr_t sched, float beta1, float beta2, uintptr_t stream) {
           check(adam_schedule(ptr<float>(step), ptr<const float>(hp), ptr<float>(sched), beta1, beta2,

@@ -88,13 +88,22 @@ class DeviceLoader:
     log_every: float, optional
         Log :meth:`metrics` on the ``'blendtorch'`` logger every that many
         seconds while iterating.
+    defer_post: bool
+        Hand the loader a fresh output buffer only when the consumer calls
+        :meth:`release` (or, failing that, when it asks for the next batch)
+        instead of before each batch is yielded.  The buffer's copies are
+        gated on the consumer stream at that point, so a training step can
+        place the next frames' DMA behind its forward pass, onto the
+        compute-bound backward kernels (bench.py --dma-phase mid: DMA that
+        overlaps the memory-bound forward slows it by ~20%).
     """
 
     def __init__(self, addresses: Sequence[str], batch_size: int = 8, decode: DecodeConfig = DecodeConfig(),
                  device=None, max_items: Optional[int] = None, timeoutms: int = DEFAULT_TIMEOUTMS,
                  rcvhwm: int = 10, prefetch: int = 4, io_threads: Optional[int] = None, image_key: str = 'image',
                  skip_bad: bool = False, meta_to_device: bool = False, staging_depth: int = 3, h2d: str = 'auto',
-                 launch_depth: int = 2, log_every: Optional[float] = None, copy_streams: int = 2):
+                 launch_depth: int = 2, log_every: Optional[float] = None, copy_streams: int = 2,
+                 defer_post: bool = False):
         if h2d not in ('auto', 'copy'):
             raise ValueError("h2d must be 'auto' or 'copy'")
         self.h2d = h2d
@@ -129,6 +138,9 @@ class DeviceLoader:
         self.log_every = log_every
         self._t_start = self._t_end = None
         self._wait_s = 0.0
+        self.defer_post = bool(defer_post)
+        self._owed = 0             # deferred posts not yet made
+        self._post_fn = None
 
     @classmethod
     def from_config(cls, addresses: Sequence[str], config, decode: DecodeConfig = DecodeConfig(), device=None,
@@ -216,6 +228,13 @@ class DeviceLoader:
             'pool_fallbacks': s['pool_fallbacks'],
         }
 
+    def release(self):
+        """``defer_post=True``: give the loader the output buffers owed for
+        the batches delivered so far, gating their copies on the current
+        stream position (call it where the next frames' DMA should start)."""
+        if self._post_fn is not None:
+            self._post_fn()
+
     def snapshot(self) -> dict:
         """Raw cumulative pipeline counters at this instant (plus the wall
         clock and the consumer's accumulated wait).  Two snapshots bracket a
@@ -292,7 +311,14 @@ class DeviceLoader:
                                                                         else min(self.prefetch, n_batches))]
                 posted = len(pending)
                 delivered = 0
+
+                def post_owed():
+                    while self._owed:
+                        self._owed -= 1
+                        pending.append(self._post(loader, stream))
+                self._post_fn = post_owed
                 while n_batches is None or delivered < n_batches:
+                    post_owed()            # the consumer did not release() them itself
                     t0 = time.time()
                     tw = time.perf_counter()
                     r = None
@@ -310,13 +336,18 @@ class DeviceLoader:
                         break
                     out = pending.pop(0)
                     if n_batches is None or posted < n_batches:
-                        pending.append(self._post(loader, stream))
+                        if self.defer_post:
+                            self._owed += 1
+                        else:
+                            pending.append(self._post(loader, stream))
                         posted += 1
                     batch = {self.image_key: out}
                     batch.update(self._collate_meta(metas))
                     delivered += 1
                     yield batch
         finally:
+            self._post_fn = None
+            self._owed = 0
             self.stats = loader.stats()
             self._t_end = time.perf_counter()
             self._live = None

@@ -766,6 +766,132 @@ def _bn_module():
     return BatchNormLeakyReLU2d
 
 
+# ---------------------------------------------------------------------------
+# consumer-model op: 4x4 / stride-2 / pad-1 convolution with a gfx950 MFMA
+# weight gradient (csrc/gpu/conv.hip)
+
+def conv_wgrad_supported(x, weight):
+    """True when :func:`conv4x4s2` can take ``x`` (bf16 channels-last GPU
+    activations) and ``weight`` ([Cout, Cin, 4, 4] fp32) on the MFMA path."""
+    import torch
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and weight.dim() == 4):
+        return False
+    cout, cin, kh, kw = weight.shape
+    return (kh, kw) == (4, 4) and x.shape[1] == cin and cin % 32 == 0 and cout % 64 == 0 and \
+        x.is_contiguous(memory_format=torch.channels_last)
+
+
+def conv_wgrad(x, dy, out, target_blocks=512):
+    """fp32 weight gradient of a 4x4/s2/p1 convolution into ``out`` ([Cout, Cin,
+    4, 4], any strides): MFMA tiles over pixel slices + one slice-reduce
+    launch.  ``x`` [N, Cin, H, W] and ``dy`` [N, Cout, H/2, W/2] are bf16 with
+    channels-last memory."""
+    import torch
+    ext = hip_ext()
+    N, Cin, H, W = x.shape
+    Cout, Ho, Wo = dy.shape[1], dy.shape[2], dy.shape[3]
+    if dy.shape[0] != N or tuple(out.shape) != (Cout, Cin, 4, 4) or out.dtype != torch.float32:
+        raise ValueError(f'conv_wgrad: x {tuple(x.shape)}, dy {tuple(dy.shape)}, out {tuple(out.shape)} do not match')
+    cl = torch.channels_last
+    if not (x.is_contiguous(memory_format=cl) and dy.is_contiguous(memory_format=cl)):
+        raise ValueError('conv_wgrad needs channels-last x and dy')
+    M = N * Ho * Wo
+    slices = ext.conv_wgrad_slices(M, Cin, Cout, target_blocks)
+    if slices <= 0:
+        raise ValueError(f'conv_wgrad: unsupported channels Cin={Cin} Cout={Cout} (Cin % 32, Cout % 64)')
+    px = -(-M // slices)
+    px = -(-px // 32) * 32
+    slices = -(-M // px)
+    partial = torch.empty(slices * Cout * 16 * Cin, dtype=torch.float32, device=x.device)
+    _count('conv_wgrad')
+    ext.conv_wgrad(x.data_ptr(), dy.data_ptr(), partial.data_ptr(), N, H, W, Cin, Ho, Wo, Cout, slices, px,
+                   out.data_ptr(), out.stride(0), out.stride(1), out.stride(2), out.stride(3), _stream(x.device))
+    return out
+
+
+def conv_fwd(x, w16, stats=None):
+    """y = conv2d(x, w16, stride 2, pad 1) on the gfx950 MFMA kernel: ``x``
+    [N, Cin, H, W] bf16 channels-last, ``w16`` [Cout, Cin, 4, 4] bf16
+    channels-last; returns channels-last bf16 y.  ``stats`` (optional fp32
+    tensor of ``conv_fwd_stats_rows(M) * 2 * Cout``) receives per-tile
+    BatchNorm sums of y (see :func:`batch_norm_from_stats`)."""
+    import torch
+    ext = hip_ext()
+    N, Cin, H, W = x.shape
+    Cout = w16.shape[0]
+    cl = torch.channels_last
+    if tuple(w16.shape) != (Cout, Cin, 4, 4) or w16.dtype != torch.bfloat16 or x.dtype != torch.bfloat16:
+        raise ValueError(f'conv_fwd: x {x.dtype} {tuple(x.shape)} / w {w16.dtype} {tuple(w16.shape)}')
+    if not (x.is_contiguous(memory_format=cl) and w16.is_contiguous(memory_format=cl)):
+        raise ValueError('conv_fwd needs channels-last x and weight')
+    Ho, Wo = (H - 2) // 2 + 1, (W - 2) // 2 + 1
+    y = torch.empty((N, Cout, Ho, Wo), dtype=torch.bfloat16, device=x.device, memory_format=cl)
+    _count('conv_fwd')
+    ext.conv_fwd(x.data_ptr(), w16.data_ptr(), y.data_ptr(), stats.data_ptr() if stats is not None else 0,
+                 N, H, W, Cin, Ho, Wo, Cout, _stream(x.device))
+    return y
+
+
+def conv_fwd_supported(x, w):
+    import torch
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and w.dim() == 4):
+        return False
+    cout, cin, kh, kw = w.shape
+    return ((kh, kw) == (4, 4) and x.shape[1] == cin and cin % 8 == 0 and cout % 64 == 0
+            and x.is_contiguous(memory_format=torch.channels_last)
+            and w.is_contiguous(memory_format=torch.channels_last))
+
+
+def conv_fwd_stats_rows(M):
+    """Partial-statistics rows :func:`conv_fwd` writes for M output pixels."""
+    return int(hip_ext().conv_fwd_tiles(int(M)))
+
+
+def _conv_function():
+    import torch
+    import torch.nn.functional as F
+
+    class _Conv4x4s2(torch.autograd.Function):
+        """y = conv2d(x, w16, stride 2, pad 1) with MIOpen; backward: MIOpen
+        data gradient, gfx950 MFMA weight gradient written in fp32 straight
+        into the master weight's gradient (no bf16 round trip, no cast)."""
+
+        @staticmethod
+        def forward(ctx, x, w32, w16):
+            ctx.save_for_backward(x, w16)
+            ctx.w32 = w32
+            if conv_fwd_supported(x, w16):
+                return conv_fwd(x, w16)
+            return F.conv2d(x, w16, None, 2, 1)
+
+        @staticmethod
+        def backward(ctx, gy):
+            x, w16 = ctx.saved_tensors
+            gy = gy.contiguous(memory_format=torch.channels_last)
+            gx = gw = None
+            if ctx.needs_input_grad[0]:
+                gx = torch.ops.aten.convolution_backward(gy, x, w16, None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1,
+                                                         [True, False, False])[0]
+            if ctx.needs_input_grad[1]:
+                gw = conv_wgrad(x, gy, torch.empty_like(ctx.w32))
+            return gx, gw, None
+
+    return _Conv4x4s2
+
+
+_CONV_FN = None
+
+
+def conv4x4s2(x, w32, w16):
+    """4x4 / stride-2 / pad-1 convolution of bf16 channels-last ``x`` with the
+    bf16 copy ``w16`` of fp32 weight ``w32``; the gradient goes to ``w32``
+    (fp32, from the MFMA weight-gradient kernel).  See :func:`conv_wgrad_supported`."""
+    global _CONV_FN
+    if _CONV_FN is None:
+        _CONV_FN = _conv_function()
+    return _CONV_FN.apply(x, w32, w16.detach())
+
+
 def __getattr__(name):
     # built on first use so importing ``blendtorch.ops`` does not import torch
     global _POOL_MODULE, _BN_MODULE

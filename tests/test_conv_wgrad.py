@@ -1,0 +1,102 @@
+"""gfx950 MFMA weight gradient of the 4x4/s2/p1 convolution (csrc/gpu/conv.hip)
+against the fp32 PyTorch reference (torch.nn.grad.conv2d_weight on the same
+bf16 inputs), and the discriminator's backward with it."""
+import pytest
+import torch
+
+from blendtorch import ops
+
+
+def test_supported_is_false_off_gpu():
+    x = torch.zeros(1, 32, 8, 8, dtype=torch.bfloat16).to(memory_format=torch.channels_last)
+    assert not ops.conv_wgrad_supported(x, torch.zeros(64, 32, 4, 4))
+
+
+@pytest.fixture(scope='module')
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip('needs a GPU')
+    ops.hip_ext()
+    return torch.device('cuda', 0)
+
+
+def _ref(x, dy, cout):
+    return torch.nn.grad.conv2d_weight(x.float(), (cout, x.shape[1], 4, 4), dy.float(), stride=2, padding=1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('N,Cin,H,W,Cout', [(2, 32, 30, 40, 64), (2, 64, 16, 20, 128), (1, 128, 8, 10, 256),
+                                            (3, 32, 14, 18, 64), (8, 32, 240, 320, 64)])
+@pytest.mark.parametrize('layout', ['channels_last', 'contiguous'])
+def test_wgrad_matches_fp32_reference(dev, N, Cin, H, W, Cout, layout):
+    g = torch.Generator(device=dev).manual_seed(N * Cin + H)
+    cl = torch.channels_last
+    x = torch.randn(N, Cin, H, W, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    dy = torch.randn(N, Cout, H // 2, W // 2, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    out = torch.full((Cout, Cin, 4, 4), float('nan'), device=dev)
+    if layout == 'channels_last':
+        out = out.contiguous(memory_format=cl)
+    before = ops.KERNEL_CALLS.get('conv_wgrad', 0)
+    ops.conv_wgrad(x, dy, out)
+    assert ops.KERNEL_CALLS['conv_wgrad'] == before + 1
+    ref = _ref(x, dy, Cout)
+    scale = float(ref.abs().max())
+    torch.testing.assert_close(out, ref, rtol=1e-3, atol=1e-4 * scale)
+
+
+@pytest.mark.gpu
+def test_wgrad_asymmetric_operands(dev):
+    """Structured (non-random) operands: a transposed or mis-swizzled tile
+    cannot pass by symmetry."""
+    cl = torch.channels_last
+    N, Cin, H, W, Cout = 1, 32, 8, 64, 64
+    x = torch.zeros(N, Cin, H, W, device=dev)
+    x[0, :, :, :] = (torch.arange(Cin, device=dev).view(Cin, 1, 1) * 0.01 +
+                     torch.arange(W, device=dev).view(1, 1, W) * 0.001)
+    x[0, 5, 3, 7] = 1.0
+    dy = torch.zeros(N, Cout, H // 2, W // 2, device=dev)
+    dy[0, 17, 2, 4] = 1.0
+    dy[0, 40, 1, 30] = -2.0
+    x, dy = x.to(torch.bfloat16).contiguous(memory_format=cl), dy.to(torch.bfloat16).contiguous(memory_format=cl)
+    out = ops.conv_wgrad(x, dy, torch.empty(Cout, Cin, 4, 4, device=dev))
+    torch.testing.assert_close(out, _ref(x, dy, Cout), rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_discriminator_backward_with_mfma_wgrad(dev):
+    from blendtorch.models import Discriminator
+    torch.manual_seed(0)
+    a = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=torch.channels_last)
+    b = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=torch.channels_last)
+    b.load_state_dict(a.state_dict())
+    x = torch.rand(4, 3, 240, 320, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    before = ops.KERNEL_CALLS.get('conv_wgrad', 0)
+    a.forward_bf16(x, mfma_wgrad=True).float().sum().backward()
+    assert ops.KERNEL_CALLS['conv_wgrad'] == before + 3          # conv 2, 3 and 4 (conv 1 has Cin = 3)
+    b.forward_bf16(x, mfma_wgrad=False).float().sum().backward()
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        # MIOpen's weight gradient is rounded to bf16 before the cast back; ours stays fp32
+        torch.testing.assert_close(pa.grad, pb.grad, rtol=2e-2, atol=2e-3 * float(pb.grad.abs().max()), msg=n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('N,Cin,H,W,Cout', [(2, 32, 30, 40, 64), (2, 64, 16, 20, 128), (1, 128, 8, 10, 256),
+                                            (3, 32, 14, 18, 64), (8, 32, 240, 320, 64), (2, 8, 12, 16, 64)])
+def test_forward_matches_fp32_reference_and_stats(dev, N, Cin, H, W, Cout):
+    import torch.nn.functional as F
+    g = torch.Generator(device=dev).manual_seed(N + Cin + W)
+    cl = torch.channels_last
+    x = torch.randn(N, Cin, H, W, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    w = (0.1 * torch.randn(Cout, Cin, 4, 4, device=dev, generator=g)).to(torch.bfloat16).contiguous(memory_format=cl)
+    M = N * (H // 2) * (W // 2)
+    rows = ops.conv_fwd_stats_rows(M)
+    stats = torch.full((rows * 2 * Cout,), float('nan'), device=dev)
+    y = ops.conv_fwd(x, w, stats)
+    ref = F.conv2d(x.float(), w.float(), None, 2, 1)
+    assert y.is_contiguous(memory_format=cl) and y.dtype == torch.bfloat16
+    # fp32 accumulation, one bf16 rounding: within one bf16 ulp of the fp32 result
+    torch.testing.assert_close(y.float(), ref, rtol=2 ** -7, atol=1e-3 * float(ref.abs().max()))
+    st = stats.view(rows, 2, Cout).sum(0)
+    yf = y.float().permute(0, 2, 3, 1).reshape(-1, Cout)
+    torch.testing.assert_close(st[0], yf.sum(0), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(st[1], (yf * yf).sum(0), rtol=1e-4, atol=1e-3)

@@ -61,31 +61,54 @@ def test_discriminator_forward_bf16_equals_autocast(dev):
             torch.testing.assert_close(mb.running_mean, ma.running_mean, rtol=1e-4, atol=1e-6)
 
 
-def test_split_graph_step_equals_single_graph(dev):
-    """CapturedStep(split=True): forward and backward+update as two graphs in
-    one pool replay to the same weights as the one-graph step."""
-    from blendtorch.models import Discriminator
+def _split_vs_single(dev, make, loss_fn, xs, lr):
     from blendtorch.parallel.step import CapturedStep
     torch.manual_seed(0)
-    nets = [Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=torch.channels_last)
-            for _ in range(2)]
+    nets = [make() for _ in range(2)]
     nets[1].load_state_dict(nets[0].state_dict())
-    crit = torch.nn.BCELoss()
-
-    def loss_fn(m, x):
-        out = m.forward_bf16(x).float()
-        return crit(out, torch.ones_like(out))
-
-    steps = [CapturedStep(n, ops.FusedAdam(n.parameters(), lr=2e-4), loss_fn, allreduce=False, warmup=2,
-                          split=s) for n, s in zip(nets, (False, True))]
-    g = torch.Generator(device=dev).manual_seed(5)
-    xs = [torch.rand(4, 3, 96, 128, device=dev, generator=g).to(torch.bfloat16)
-          .contiguous(memory_format=torch.channels_last) for _ in range(4)]
+    steps = [CapturedStep(n, ops.FusedAdam(n.parameters(), lr=lr), loss_fn, allreduce=False, warmup=2, split=s)
+             for n, s in zip(nets, (False, True))]
     hits = []
     for x in xs:
         steps[0](x)
         steps[1](x, mid=lambda: hits.append(1))
     torch.cuda.synchronize()
     assert steps[1].state == 'graph' and steps[1].graph_bwd is not None and len(hits) == len(xs)
-    for pa, pb in zip(nets[0].parameters(), nets[1].parameters()):
+    return list(zip(nets[0].parameters(), nets[1].parameters()))
+
+
+def test_split_graph_step_equals_single_graph(dev):
+    """CapturedStep(split=True): forward and backward+update as two graphs in
+    one pool replay to the same weights as the one-graph step (an MLP: GEMMs
+    and elementwise kernels sum in a fixed order, so bit-exact)."""
+    def make():
+        return torch.nn.Sequential(torch.nn.Linear(64, 128), torch.nn.GELU(), torch.nn.Linear(128, 8)).to(dev)
+
+    g = torch.Generator(device=dev).manual_seed(5)
+    xs = [torch.randn(32, 64, device=dev, generator=g) for _ in range(5)]
+    for pa, pb in _split_vs_single(dev, make, lambda m, x: m(x).pow(2).mean(), xs, 1e-2):
         torch.testing.assert_close(pb, pa, rtol=0, atol=0)
+
+
+def test_split_graph_discriminator_step(dev):
+    """The bench consumer step split in two graphs trains like the one-graph
+    step.  MIOpen's weight-gradient kernels sum with atomics, so the two runs
+    differ by rounding; early Adam steps move each weight by about +-lr, so
+    the check is that nearly every weight agrees far below lr."""
+    from blendtorch.models import Discriminator
+    lr = 2e-4
+    crit = torch.nn.BCELoss()
+
+    def make():
+        return Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=torch.channels_last)
+
+    def loss_fn(m, x):
+        out = m.forward_bf16(x).float()
+        return crit(out, torch.ones_like(out))
+
+    g = torch.Generator(device=dev).manual_seed(5)
+    xs = [torch.rand(4, 3, 96, 128, device=dev, generator=g).to(torch.bfloat16)
+          .contiguous(memory_format=torch.channels_last) for _ in range(4)]
+    for pa, pb in _split_vs_single(dev, make, loss_fn, xs, lr):
+        d = (pb - pa).abs()
+        assert float(d.mean()) < 0.05 * lr and float((d > 0.5 * lr).float().mean()) < 0.01

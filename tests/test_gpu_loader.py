@@ -515,3 +515,26 @@ def test_device_loader_python_publisher_tile16(dev, free_port):
     ref = ops.reference_decode(torch.from_numpy(np.stack(frames)), cfg)
     for i in range(16):
         torch.testing.assert_close(got[i].cpu(), ref[i], rtol=0, atol=0)
+
+
+def test_device_loader_defer_post_release(dev, free_port):
+    """defer_post: buffers are handed back on release() (or at the next
+    request when the consumer does not call it); every frame still arrives
+    once, in order, with the same pixels as the eager-post loader."""
+    args = dict(producer='cubesim', num_instances=1, named_sockets=['DATA'], seed=21,
+                instance_args=[['--mode', 'rgba']])
+    cfg = ops.DecodeConfig.raw(channels='rgba')
+    runs = []
+    for defer in (False, True):
+        with btt.BlenderLauncher(start_port=free_port + (7 if defer else 0), **args) as bl:
+            dl = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=4, max_items=40, decode=cfg, device=dev,
+                              h2d='copy', prefetch=3, defer_post=defer)
+            frames, imgs = [], []
+            for i, b in enumerate(dl):
+                frames += b['frameid'].tolist()
+                imgs.append(b['image'].clone())
+                if defer and i % 2 == 0:
+                    dl.release()
+            runs.append((frames, torch.cat(imgs)))
+    assert runs[0][0] == runs[1][0] == sorted(runs[1][0]) and len(set(runs[1][0])) == 40
+    assert torch.equal(runs[0][1], runs[1][1])
