@@ -132,6 +132,9 @@ def parse_args(argv=None):
     ap.add_argument('--backend', choices=['nccl', 'gloo'], default='nccl',
                     help='process-group backend (nccl = RCCL over xGMI; gloo only to rehearse several ranks on one GPU)')
     ap.add_argument('--start-port', type=int, default=0)
+    ap.add_argument('--host-sync', choices=['auto', 'on', 'off'], default='auto',
+                    help='loader/consumer ordering by host-side event checks (on) or cross-stream waits (off); '
+                         'auto = on for the DMA copy path (--h2d copy, the disc consumer), off for the direct path')
     ap.add_argument('--dma-phase', choices=['start', 'mid'], default='start',
                     help='disc consumer: when the next frames\' host->device DMA may start -- start = when the '
                          'step begins (overlapping the memory-bound forward); mid = between the forward and the '
@@ -339,7 +342,8 @@ def main(argv=None):
                                   max_items=total_batches * per_step, prefetch=6,
                                   io_threads=args.io_threads or None, timeoutms=60000, h2d=args.h2d,
                                   launch_depth=args.launch_depth, copy_streams=args.copy_streams,
-                                  defer_post=dma_mid)
+                                  defer_post=dma_mid,
+                                  host_sync=None if args.host_sync == 'auto' else args.host_sync == 'on')
         if args.dist == 'scatter':
             it = iter(ScatterLoader(dl, args.batch, decode, device, total_batches))
         else:
@@ -517,6 +521,7 @@ def main(argv=None):
                 'cast': args.cast if amp else None,
                 'optim': args.optim if model is not None else None,
                 'dma_phase': args.dma_phase if model is not None else None,
+                'host_sync': args.host_sync,
                 'consumer_collectives_per_step': stepper.collectives if stepper is not None else None,
             },
             'sec_per_image': round(tmax / images, 7),

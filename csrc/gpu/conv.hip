@@ -147,27 +147,38 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p)
 
   const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(p.x, int64_t(p.N) * p.H * p.W * p.Cin * 2);
   const __amdgpu_buffer_rsrc_t rs_dy = make_rsrc(p.dy, p.M * p.Cout * 2);
-  uint4 rdy, rx0, rx1;
-  auto load = [&](int step) {
-    const int64_t m0 = m_begin + int64_t(step) * BPX;
+  // Stage loads run kDepth stages ahead of the MFMAs in a register ring (one
+  // block per CU: nothing else would hide the ~0.8 us load latency; one stage
+  // in flight ran latency-bound at ~1800 cycles per 32-pixel step).  Stages
+  // past the slice load out of range (zeros, no memory traffic), so the loop
+  // has no tail and the compiler keeps counted vmcnt waits.
+  constexpr int kDepth = 4;
+  struct Stage {
+    uint4 dy, x0, x1;
+  };
+  Stage ring[kDepth];
+  int next_stage = 0;
+  auto load = [&](Stage& r) {
+    const int64_t m0 = m_begin + int64_t(next_stage) * BPX;
     const int64_t md = m0 + dpx;
-    rdy = bload(rs_dy, md < m_end ? uint32_t((md * p.Cout + co0 + dch * 8) * 2) : kOOB);
+    r.dy = bload(rs_dy, md < m_end ? uint32_t((md * p.Cout + co0 + dch * 8) * 2) : kOOB);
     auto xload = [&](const PixelCursor& c, int64_t m) {
       const int ih = 2 * c.oh - 1 + kh, iw = 2 * c.ow - 1 + kw;
       const bool ok = m < m_end && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
       return bload(rs_x, ok ? uint32_t((((int64_t(c.n) * p.H + ih) * p.W + iw) * p.Cin + ci) * 2) : kOOB);
     };
-    rx0 = xload(c0, m0 + xpx0);
-    rx1 = xload(c1, m0 + xpx0 + 16);
+    r.x0 = xload(c0, m0 + xpx0);
+    r.x1 = xload(c1, m0 + xpx0 + 16);
     c0.advance(p.Ho, p.Wo);
     c1.advance(p.Ho, p.Wo);
+    ++next_stage;
   };
-  auto store = [&](int buf) {
+  auto store = [&](const Stage& r, int buf) {
     char* dyi = smem + buf * STAGE;
     char* xi = dyi + DY_TILE;
-    *reinterpret_cast<uint4*>(dyi + dy_off(dpx, dch * 16)) = rdy;
-    *reinterpret_cast<uint4*>(xi + x_off(xpx0, xch * 16)) = rx0;
-    *reinterpret_cast<uint4*>(xi + x_off(xpx0 + 16, xch * 16)) = rx1;
+    *reinterpret_cast<uint4*>(dyi + dy_off(dpx, dch * 16)) = r.dy;
+    *reinterpret_cast<uint4*>(xi + x_off(xpx0, xch * 16)) = r.x0;
+    *reinterpret_cast<uint4*>(xi + x_off(xpx0 + 16, xch * 16)) = r.x1;
   };
 
   f32x4 acc[2][4];
@@ -177,26 +188,31 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p)
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int wco = (wave >> 1) * 32, wkc = (wave & 1) * 64;
-  if (nsteps > 0) {
-    load(0);
-    store(0);
-  }
-  __syncthreads();
-  for (int s = 0; s < nsteps; ++s) {
-    if (s + 1 < nsteps) load(s + 1);   // in flight while this stage's MFMAs run
-    const char* dyi = smem + (s & 1) * STAGE;
-    const char* xi = dyi + DY_TILE;
-    bf16x8 a[2], bm[4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) a[i] = frag<false>(dyi, lane, wco + 16 * i);
+  for (int u = 0; u < kDepth; ++u) load(ring[u]);
+  const int padded = (nsteps + kDepth - 1) / kDepth * kDepth;
+  for (int s0 = 0; s0 < padded; s0 += kDepth) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bm[j] = frag<true>(xi, lane, wkc + 16 * j);
+    for (int u = 0; u < kDepth; ++u) {
+      const int buf = u & 1;   // kDepth is even: (s0 + u) & 1
+      store(ring[u], buf);     // waits for this stage's loads only (counted vmcnt)
+      // LDS-only barrier: the ring's later stages stay in flight across it
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      load(ring[u]);           // stage s + kDepth
+      const char* dyi = smem + buf * STAGE;
+      const char* xi = dyi + DY_TILE;
+      bf16x8 a[2], bm[4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 2; ++i) a[i] = frag<false>(dyi, lane, wco + 16 * i);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bm[j], acc[i][j], 0, 0, 0);
-    if (s + 1 < nsteps) store((s + 1) & 1);
-    __syncthreads();
+      for (int j = 0; j < 4; ++j) bm[j] = frag<true>(xi, lane, wkc + 16 * j);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bm[j], acc[i][j], 0, 0, 0);
+    }
   }
 
   // C/D map of 16x16x32: column = lane & 15 (kc), row = 4 * (lane >> 4) + reg (co)

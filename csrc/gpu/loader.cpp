@@ -178,11 +178,34 @@ bool StreamLoader::next(ReadyBatch* out, hipStream_t consumer, long timeout_ms) 
   *out = std::move(ready_.front());
   ready_.pop_front();
   lk.unlock();
-  DeviceGuard g(cfg_.device);
-  check(hipStreamWaitEvent(consumer, out->done, 0), "hipStreamWaitEvent");
-  (void)hipEventDestroy(out->done);
-  out->done = nullptr;
+  if (out->done) {   // host_sync = false: the consumer stream waits on the device
+    DeviceGuard g(cfg_.device);
+    check(hipStreamWaitEvent(consumer, out->done, 0), "hipStreamWaitEvent");
+    (void)hipEventDestroy(out->done);
+    out->done = nullptr;
+  }
+  out->pending.reset();
   return true;
+}
+
+// host_sync: hand out, in order, the launched batches whose device work the
+// host has seen complete (worker thread).
+void StreamLoader::promote_ready() {
+  bool any = false;
+  while (!unready_.empty() && unready_.front().pending->done()) {
+    std::lock_guard<std::mutex> lk(mu_);
+    ready_.push_back(std::move(unready_.front()));
+    unready_.pop_front();
+    any = true;
+  }
+  if (any) cv_.notify_all();
+}
+
+void StreamLoader::host_wait(hipEvent_t ev) {
+  while (hipEventQuery(ev) == hipErrorNotReady && !stop_) {
+    promote_ready();
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
 }
 
 void StreamLoader::stop() {
@@ -237,6 +260,7 @@ void StreamLoader::stop() {
       if (r.done) (void)hipEventDestroy(r.done);
     ready_.clear();
   }
+  unready_.clear();
   for (auto* p : staging_) (void)hipFree(p);
   staging_.clear();
   if (d_lut_) (void)hipFree(d_lut_);
@@ -309,6 +333,7 @@ void StreamLoader::run() {
   const int64_t max_frames = cfg_.max_batches < 0 ? -1 : cfg_.max_batches * cfg_.batch_size;
   int64_t taken = 0;
   while (!stop_) {
+    promote_ready();
     reap();
     if (max_frames >= 0 && taken >= max_frames) break;
     std::vector<int> ev;
@@ -316,7 +341,10 @@ void StreamLoader::run() {
       // with copies in flight, wake up often enough to recycle their slots
       // promptly (producers / IO threads may be waiting for them)
       trace::Range tp("btn.loader.poll");
-      ev = zmtp::Socket::poll(items, inflight_.empty() && pending_.empty() ? 100 : 1, intr);
+      ev = zmtp::Socket::poll(items, inflight_.empty() && pending_.empty() && unready_.empty() ? 100 : (unready_.empty() ? 1 : 0),
+                              intr);
+      if (!unready_.empty() && std::none_of(ev.begin(), ev.end(), [](int e) { return e != 0; }))
+        std::this_thread::sleep_for(std::chrono::microseconds(10));   // nothing to receive: poll completions
     } catch (const zmtp::Error& e) {
       if (e.code == zmtp::E_INTR) break;
       throw;
@@ -339,6 +367,10 @@ void StreamLoader::run() {
     }
   }
   if (!stop_) flush_pending(true);   // stream complete: nothing more will join the pending batches
+  while (!stop_ && !unready_.empty()) {
+    unready_.front().pending->wait();
+    promote_ready();
+  }
   std::lock_guard<std::mutex> lk(mu_);
   exhausted_ = true;
 }
@@ -606,9 +638,9 @@ void StreamLoader::reap(bool wait_all) {
   // slots return to the pool (and unblock an IO thread waiting for one)
   while (!inflight_.empty()) {
     Inflight& f = inflight_.front();
-    hipError_t q = wait_all ? hipEventSynchronize(f.copied) : hipEventQuery(f.copied);
-    if (q == hipErrorNotReady) break;
-    (void)hipEventDestroy(f.copied);
+    if (wait_all) f.copied->wait();
+    else if (!f.copied->done()) break;
+    f.copied.reset();
     if (f.t0) {
       float ms = 0;
       if (hipEventElapsedTime(&ms, f.t0, f.t1) == hipSuccess) {
@@ -676,8 +708,17 @@ void StreamLoader::launch() {
       // out of output buffers: the consumer is waiting for batches, so
       // holding assembled ones back for coalescing would only stall it
       flush_pending(true);
+      promote_ready();
       lk.lock();
       if (!posted_.empty() || stop_) break;
+      if (!unready_.empty()) {
+        // the consumer is most likely waiting for one of these: keep
+        // promoting at a fine grain instead of sleeping through a post
+        lk.unlock();
+        std::this_thread::sleep_for(std::chrono::microseconds(10));
+        lk.lock();
+        continue;
+      }
       cv_.wait_for(lk, std::chrono::milliseconds(2));
     }
     if (stop_) return;
@@ -747,7 +788,8 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
   const bool direct = group.front().direct;
   int total = 0;
   for (auto& b : group) {
-    check(hipStreamWaitEvent(stream_, b.ready, 0), "hipStreamWaitEvent(post)");
+    if (cfg_.host_sync) host_wait(b.ready);   // the consumer is done with the buffer
+    else check(hipStreamWaitEvent(stream_, b.ready, 0), "hipStreamWaitEvent(post)");
     (void)hipEventDestroy(b.ready);
     total += int(b.items.size());
   }
@@ -780,7 +822,29 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
   const size_t stage_idx = size_t(batch_index_) % staging_.size();
   const bool passthrough = !direct && passthrough_ &&
                            std::none_of(all.begin(), all.end(), [](const Item* it) { return it->flip; });
-  if (passthrough) {
+  auto copied = std::make_shared<EventSet>();
+  auto add_event = [&](hipStream_t st) {
+    hipEvent_t ev;
+    check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate(copied)");
+    check(hipEventRecord(ev, st), "hipEventRecord(copied)");
+    copied->ev.push_back(ev);
+  };
+  if (passthrough && cfg_.host_sync) {
+    // identity decode, host-ordered: the buffer is free (post event seen
+    // complete), so the frames go by DMA straight into the consumer's tensor
+    // over the copy streams with no stream waits at all; one event per
+    // stream marks both the slots' release and the batch's readiness
+    const size_t K = std::max<size_t>(1, copy_streams_.size());
+    int i = 0;
+    for (auto& b : group)
+      for (size_t k = 0; k < b.items.size(); ++k, ++i) {
+        hipStream_t cs = copy_streams_.empty() ? stream_ : copy_streams_[size_t(i) % K];
+        check(hipMemcpyAsync(static_cast<uint8_t*>(b.dst) + k * img_bytes_, all[size_t(i)]->src, img_bytes_,
+                             hipMemcpyHostToDevice, cs),
+              "hipMemcpyAsync(H2D passthrough)");
+      }
+    for (size_t k = 0; k < K && k < size_t(total); ++k) add_event(copy_streams_.empty() ? stream_ : copy_streams_[k]);
+  } else if (passthrough) {
     // identity decode: the frames go by DMA straight into the consumer's
     // tensor (its post event already gates stream_; the copy streams wait on
     // stream_'s progress through it), and no kernel is launched
@@ -828,9 +892,8 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
   }
   // `copied` marks the last device read of the host slots: after the copies,
   // or (direct) after the kernel that reads them
-  hipEvent_t copied;
-  check(hipEventCreateWithFlags(&copied, hipEventDisableTiming), "hipEventCreate(copied)");
-  if (!direct) check(hipEventRecord(copied, stream_), "hipEventRecord(copied)");
+  const bool host_passthrough = passthrough && cfg_.host_sync;
+  if (!direct && !host_passthrough) add_event(stream_);
   const bool per_image_dst = group.size() > 1;
   hipError_t e = hipSuccess;
   if (passthrough) {
@@ -895,12 +958,17 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
     }
   }
   check(e, "decode kernel launch");
-  if (direct) check(hipEventRecord(copied, stream_), "hipEventRecord(copied)");
+  if (direct) add_event(stream_);
   if (!direct && !passthrough && !copy_streams_.empty()) {
     if (stage_free_.size() < staging_.size()) stage_free_.resize(staging_.size(), nullptr);
     if (!stage_free_[stage_idx])
       check(hipEventCreateWithFlags(&stage_free_[stage_idx], hipEventDisableTiming), "hipEventCreate(stage)");
     check(hipEventRecord(stage_free_[stage_idx], stream_), "hipEventRecord(stage)");
+  }
+  if (t0 && host_passthrough) {   // the copies ran on other streams: nothing on stream_ to time
+    (void)hipEventDestroy(t0);
+    (void)hipEventDestroy(t1);
+    t0 = t1 = nullptr;
   }
   if (t0) check(hipEventRecord(t1, stream_), "hipEventRecord(t1)");
   Inflight fl;
@@ -918,8 +986,19 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
       if (!it.expanded.empty()) fl.expanded.push_back(std::move(it.expanded));
       rb.items.push_back(std::move(it.meta));
     }
-    check(hipEventCreateWithFlags(&rb.done, hipEventDisableTiming), "hipEventCreate(done)");
-    check(hipEventRecord(rb.done, stream_), "hipEventRecord(done)");
+    if (host_passthrough) {
+      rb.pending = copied;        // the DMA is all the batch's device work
+    } else if (cfg_.host_sync) {
+      auto fin = std::make_shared<EventSet>();
+      hipEvent_t ev;
+      check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate(done)");
+      check(hipEventRecord(ev, stream_), "hipEventRecord(done)");
+      fin->ev.push_back(ev);
+      rb.pending = fin;
+    } else {
+      check(hipEventCreateWithFlags(&rb.done, hipEventDisableTiming), "hipEventCreate(done)");
+      check(hipEventRecord(rb.done, stream_), "hipEventRecord(done)");
+    }
     rb.recv_ms = t_issue - b.t0;
     done.push_back(std::move(rb));
   }
@@ -932,7 +1011,12 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
     if (direct) stats_.direct_batches += group.size();
     if (passthrough) stats_.passthrough_batches += group.size();
     stats_.h2d_issue_ms += now_ms() - t_issue;
-    for (auto& rb : done) ready_.push_back(std::move(rb));
+    if (!cfg_.host_sync)
+      for (auto& rb : done) ready_.push_back(std::move(rb));
+  }
+  if (cfg_.host_sync) {
+    for (auto& rb : done) unready_.push_back(std::move(rb));
+    promote_ready();
   }
   cv_.notify_all();
 }

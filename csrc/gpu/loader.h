@@ -112,6 +112,15 @@ struct LoaderConfig {
   // Direct-path launches queued on the loader stream before new batches wait
   // and coalesce into one launch (0: always hold until 64 images or stream end).
   int launch_depth = 2;
+  // Order the loader's work against the consumer on the HOST: a posted
+  // buffer is written only once the host has seen its post event complete,
+  // and a batch is handed out only once the host has seen all its device
+  // work (copies / kernel) complete -- no cross-stream hipStreamWaitEvent in
+  // either direction.  Each such wait costs 28-430 us of host time on ROCm
+  // 7 (profiles/r2/hip_api_cost.json), and issuing them per batch from the
+  // loader thread held up the consumer's graph launches (~0.2 ms per step of
+  // the disc consumer).  false: the GPU-side waits of round 1.
+  bool host_sync = true;
   // decode parameters (src/dst/B/H/W/Cin filled per batch)
   int cout = 3;
   int cmap[4] = {0, 1, 2, 3};
@@ -130,10 +139,32 @@ struct BatchMeta {
   codec::VPtr tree;                  // parse tree over `bytes` (image entry removed)
 };
 
+// Events owned jointly by an in-flight launch (slot release) and the batches
+// waiting for completion (host_sync); destroyed with the last owner.
+struct EventSet {
+  std::vector<hipEvent_t> ev;
+  EventSet() = default;
+  EventSet(const EventSet&) = delete;
+  EventSet& operator=(const EventSet&) = delete;
+  ~EventSet() {
+    for (auto e : ev) (void)hipEventDestroy(e);
+  }
+  // all complete? (errors count as complete: the stream reports them later)
+  bool done() const {
+    for (auto e : ev)
+      if (hipEventQuery(e) == hipErrorNotReady) return false;
+    return true;
+  }
+  void wait() const {
+    for (auto e : ev) (void)hipEventSynchronize(e);
+  }
+};
+
 struct ReadyBatch {
   int64_t index = -1;
   std::vector<BatchMeta> items;
-  hipEvent_t done = nullptr;
+  hipEvent_t done = nullptr;         // GPU-side completion (host_sync = false)
+  std::shared_ptr<EventSet> pending; // host-side completion (host_sync): ready once done()
   double recv_ms = 0;                // wall time spent assembling the batch
 };
 
@@ -254,9 +285,12 @@ class StreamLoader {
   // channels in order, identity table, no flip): copy-path batches are then
   // DMA'd straight into the consumer's tensor and no kernel runs at all
   bool passthrough_ = false;
+  void promote_ready();                 // host_sync: completed batches -> ready_
+  void host_wait(hipEvent_t ev);        // host_sync: poll an event, promoting meanwhile
+  std::deque<ReadyBatch> unready_;      // host_sync: launched, device work not yet seen complete
   struct Inflight {
     int64_t launch_no = 0;
-    hipEvent_t copied;
+    std::shared_ptr<EventSet> copied;
     hipEvent_t t0 = nullptr, t1 = nullptr;   // sampled launch timing (or null)
     int images = 0;
     std::vector<zmtp::Frame> frames;

@@ -564,9 +564,10 @@ PYBIND11_MODULE(_hip, m) {
                        int io_threads, int device, int64_t max_batches, size_t max_frame_bytes, int pool_slots,
                        int staging_depth, bool skip_bad, int cout, std::vector<int> cmap, int flip_all,
                        int out_dtype, int layout, std::vector<float> lut, std::vector<float> matrix,
-                       std::vector<float> bias, bool direct, int launch_depth, int copy_streams) {
+                       std::vector<float> bias, bool direct, int launch_depth, int copy_streams, bool host_sync) {
              LoaderConfig c;
              c.direct = direct;
+             c.host_sync = host_sync;
              c.copy_streams = copy_streams;
              c.launch_depth = launch_depth;
              c.addresses = std::move(addresses);
@@ -596,7 +597,7 @@ PYBIND11_MODULE(_hip, m) {
            py::arg("pool_slots"), py::arg("staging_depth"), py::arg("skip_bad"), py::arg("cout"), py::arg("cmap"),
            py::arg("flip_all"), py::arg("out_dtype"), py::arg("layout"), py::arg("lut"), py::arg("matrix"),
            py::arg("bias"), py::arg("direct") = true, py::arg("launch_depth") = 2,
-           py::arg("copy_streams") = 2)
+           py::arg("copy_streams") = 2, py::arg("host_sync") = true)
       .def("start", &StreamLoader::start)
       .def("wait_shape",
            [](StreamLoader& l, long timeout_ms) -> py::object {

@@ -55,17 +55,18 @@ class Discriminator(nn.Module):
     def forward(self, x):
         return self.features(x).view(-1, 1).squeeze(1)
 
-    def forward_bf16(self, x, mfma_wgrad=True):
+    def forward_bf16(self, x, mfma=True):
         """bf16 forward without autocast: ONE kernel casts every conv weight
         to bf16 (and one casts their gradients back to fp32 in backward)
         instead of a cast per layer each way; numerically the same as
         ``autocast(bfloat16)`` over :meth:`forward` (RNE weight casts, bf16
         activations).  ``x``: bf16 on the GPU.
 
-        ``mfma_wgrad``: the 4x4/s2 layers whose channels fit (Cin % 32,
-        Cout % 64: all but the first) take their weight gradient from the
-        gfx950 MFMA kernel (``ops.conv4x4s2``), in fp32, instead of MIOpen's
-        bf16 path (zero-fill + atomic GEMM + cast per layer)."""
+        ``mfma``: the 4x4/s2 layers whose channels fit (Cin % 32, Cout % 64:
+        all but the first) run on the gfx950 MFMA conv kernels
+        (``ops.conv4x4s2``): forward, and the weight gradient in fp32 instead
+        of MIOpen's bf16 path (zero-fill + atomic GEMM + cast per layer).
+        ``mfma=False`` is bit-identical to autocast over :meth:`forward`."""
         import torch.nn.functional as F
         from .. import ops
         convs = [m for m in self.features if isinstance(m, nn.Conv2d)]
@@ -73,7 +74,7 @@ class Discriminator(nn.Module):
         for m in self.features:
             if isinstance(m, nn.Conv2d):
                 w16 = next(weights)
-                if (mfma_wgrad and m.stride == (2, 2) and m.padding == (1, 1) and m.bias is None and m.groups == 1
+                if (mfma and m.stride == (2, 2) and m.padding == (1, 1) and m.bias is None and m.groups == 1
                         and m.dilation == (1, 1) and ops.conv_wgrad_supported(x, m.weight)):
                     x = ops.conv4x4s2(x, m.weight, w16)
                 else:

@@ -82,15 +82,25 @@ def run(name, iters, batch, graph, fused_adam=False, fused_bn=True, dma=0, cast=
         # are free); start = gated on the step's start, so they overlap the
         # forward (what the stream loader's post events do); mid = gated
         # between the forward and the backward graph
+        t0 = time.perf_counter()
         ev = None
         if dma_phase != 'none':
             ev = torch.cuda.Event()
             ev.record()
+            evs.append(ev)
+        if dma_phase == 'start_prev':   # gate on the event of two steps ago (already passed, usually)
+            ev = evs[-3] if len(evs) >= 3 else None
+        if dma_phase == 'record':       # record only: no cross-stream wait
+            ev = None
         for i in range(8 if dma else 0):
             with torch.cuda.stream(side[i % dma]):
                 if ev is not None:
                     torch.cuda.current_stream().wait_event(ev)
                 ddst[i].copy_(hsrc[i], non_blocking=True)
+        del evs[:-4]
+        host_copy_s[0] += time.perf_counter() - t0
+    evs = []
+    host_copy_s = [0.0]
     fn = step
     if graph and split:
         from blendtorch.parallel.step import CapturedStep
@@ -117,6 +127,7 @@ def run(name, iters, batch, graph, fused_adam=False, fused_bn=True, dma=0, cast=
         for _ in range(3):
             fn()
     torch.cuda.synchronize()
+    host_copy_s[0] = 0.0
     t0 = time.perf_counter()
     for _ in range(iters):
         if dma and dma_phase != 'mid':
@@ -124,9 +135,11 @@ def run(name, iters, batch, graph, fused_adam=False, fused_bn=True, dma=0, cast=
         fn()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / iters * 1000
+    copy_ms = host_copy_s[0] / iters * 1000
     return {'variant': name, 'graph': graph, 'fused_adam': fused_adam, 'fused_bn': fused_bn, 'dma_streams': dma,
             'cast': cast, 'u8_input': u8, 'optim': optim, 'dma_phase': dma_phase if dma else None, 'split': split,
-            'ms_per_step': round(ms, 4), 'images_per_s': round(batch / ms * 1000, 1)}
+            'ms_per_step': round(ms, 4), 'images_per_s': round(batch / ms * 1000, 1),
+            'host_ms_issuing_copies': round(copy_ms, 4)}
 
 
 def main():
@@ -144,7 +157,7 @@ def main():
     ap.add_argument('--cast', choices=['autocast', 'fused'], default='autocast',
                     help='fused = Discriminator.forward_bf16 (one weight-cast launch per direction)')
     ap.add_argument('--optim', choices=['torch', 'gfx950'], default='torch')
-    ap.add_argument('--dma-phase', choices=['none', 'start', 'mid'], default='none')
+    ap.add_argument('--dma-phase', choices=['none', 'record', 'start', 'start_prev', 'mid'], default='none')
     ap.add_argument('--split', action='store_true', help='forward and backward as two graphs (CapturedStep split)')
     ap.add_argument('--u8', action='store_true', help='train on raw u8 RGBA frames decoded inside the step')
     args = ap.parse_args()

@@ -2,7 +2,7 @@
 set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_conv_wgrad.py tests/test_adam.py tests/test_gpu_consumer.py tests/test_gpu_loader.py > gpurun_out/r2_tests.log 2>&1; rc=$?
+timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread -s -m gpu tests/test_conv_wgrad.py tests/test_adam.py tests/test_gpu_consumer.py tests/test_gpu_loader.py > gpurun_out/r2_tests.log 2>&1; rc=$?
 tail -25 gpurun_out/r2_tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 200 python scripts/conv_bench.py > gpurun_out/conv_bench.log 2>&1; rc=$?; cat gpurun_out/conv_bench.log | tail -5; [ $rc -eq 0 ] || exit $rc
 bash scripts/dma_phase.sh

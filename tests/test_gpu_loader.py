@@ -538,3 +538,36 @@ def test_device_loader_defer_post_release(dev, free_port):
             runs.append((frames, torch.cat(imgs)))
     assert runs[0][0] == runs[1][0] == sorted(runs[1][0]) and len(set(runs[1][0])) == 40
     assert torch.equal(runs[0][1], runs[1][1])
+
+
+@pytest.mark.parametrize('h2d,decode', [('copy', 'raw'), ('copy', 'unit'), ('auto', 'unit')])
+def test_host_sync_many_small_batches_match_cpu(dev, free_port, h2d, decode):
+    """host_sync (default): the loader orders itself against the consumer with
+    host-side event checks only.  Small frames (which stay cache-resident
+    between reuses of a posted buffer) over many batches must still arrive
+    exactly as the CPU path receives them."""
+    cfg = ops.DecodeConfig.raw(channels='rgba') if decode == 'raw' else ops.DecodeConfig.unit(channels='rgb')
+    n = 240
+    args = dict(producer='cubesim', num_instances=1, named_sockets=['DATA'], seed=5,
+                instance_args=[['--mode', 'rgba', '--resolution', '64x48']])
+    port = free_port + {'raw': 0, 'unit': 10}[decode] + (20 if h2d == 'auto' else 0)
+    with btt.BlenderLauncher(start_port=port, **args) as bl:
+        ctx = zmq.Context()
+        s = ctx.socket(zmq.PULL)
+        s.connect(bl.launch_info.addresses['DATA'][0])
+        cpu = []
+        for _ in range(n):
+            assert s.poll(20000)
+            cpu.append(s.recv_pyobj())
+        s.close()
+    imgs = torch.from_numpy(np.stack([np.ascontiguousarray(m['image']) for m in cpu]))
+    ref = imgs if decode == 'raw' else ops.reference_decode(imgs, cfg)
+    with btt.BlenderLauncher(start_port=port + 5, **args) as bl:
+        dl = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=4, max_items=n, decode=cfg, device=dev,
+                          h2d=h2d, prefetch=2, host_sync=True)
+        got, fids = [], []
+        for b in dl:
+            got.append(b['image'].float().mean().item())   # consume on the device, as a model would
+            fids += b['frameid'].tolist()
+            assert torch.equal(b['image'].cpu(), ref[len(fids) - 4:len(fids)]), f'batch ending at {len(fids)}'
+    assert fids == [m['frameid'] for m in cpu]
