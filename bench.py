@@ -125,8 +125,10 @@ def parse_args(argv=None):
                          'Default: auto, but copy for the disc consumer -- its graphed training step runs faster '
                          'when the copy engines, not CUs waiting on PCIe reads, move the frames '
                          '(profiles/consumer_step.md)')
-    ap.add_argument('--copy-streams', type=int, default=2,
-                    help='copy path: HIP streams a batch\'s frame copies are spread over (several DMA engines)')
+    ap.add_argument('--copy-streams', type=int, default=None,
+                    help='copy path: HIP streams a batch\'s frame copies are spread over (several DMA engines); '
+                         'default 2, or 1 for the disc consumer (it needs ~12 GB/s, and one DMA stream '
+                         'disturbs its step least: 9.72k vs 9.59k img/s, profiles/r2/host_sync.txt)')
     ap.add_argument('--launch-depth', type=int, default=2,
                     help='direct-path decode launches queued before new batches coalesce into one launch')
     ap.add_argument('--backend', choices=['nccl', 'gloo'], default='nccl',
@@ -341,7 +343,8 @@ def main(argv=None):
                 dl = DeviceLoader(addrs, batch_size=per_step, decode=ldec, device=device,
                                   max_items=total_batches * per_step, prefetch=6,
                                   io_threads=args.io_threads or None, timeoutms=60000, h2d=args.h2d,
-                                  launch_depth=args.launch_depth, copy_streams=args.copy_streams,
+                                  launch_depth=args.launch_depth,
+                                  copy_streams=args.copy_streams or (1 if args.consumer == 'disc' else 2),
                                   defer_post=dma_mid,
                                   host_sync=None if args.host_sync == 'auto' else args.host_sync == 'on')
         if args.dist == 'scatter':

@@ -101,12 +101,19 @@ __device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return make_uint4(v[0], v[1], v[2], v[3]);
 }
 
+// frag() with a precomputed lane offset: rows r0 (off) and r0 + 4 (off + row4)
+__device__ __forceinline__ bf16x8 frag_at(const char* img, int off, int row4) {
+  const s16x4 lo = tr_read(img, off);
+  const s16x4 hi = tr_read(img, off + row4);
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
 struct PixelCursor {   // (n, oh, ow) of pixel m, advanced by BPX per k-step
   int n, oh, ow;
-  __device__ void init(int64_t m, int Ho, int Wo) {
-    const int64_t hw = int64_t(Ho) * Wo;
-    n = int(m / hw);
-    const int r = int(m - int64_t(n) * hw);
+  __device__ void init(int m, int Ho, int Wo) {
+    const int hw = Ho * Wo;
+    n = m / hw;
+    const int r = m - n * hw;
     oh = r / Wo;
     ow = r - oh * Wo;
   }
@@ -130,9 +137,11 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p)
   const int w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
   const int slice = w / T, tile = w - slice * T;
   const int co0 = (tile / KT) * BCO, kt = tile - (tile / KT) * KT;
-  const int64_t m_begin = int64_t(slice) * p.px_per_slice;
-  const int64_t m_end = m_begin + p.px_per_slice < p.M ? m_begin + p.px_per_slice : p.M;
-  const int nsteps = m_end > m_begin ? int((m_end - m_begin + BPX - 1) / BPX) : 0;
+  // all index math in 32 bits (the host guarantees every byte offset < 2^31):
+  // 64-bit address arithmetic made this kernel VALU-bound (9.5 VALU per MFMA)
+  const int m_begin = slice * int(p.px_per_slice);
+  const int m_end = m_begin + int(p.px_per_slice) < int(p.M) ? m_begin + int(p.px_per_slice) : int(p.M);
+  const int nsteps = m_end > m_begin ? (m_end - m_begin + BPX - 1) / BPX : 0;
 
   // this thread's staging work: one dY chunk, two X chunks per k-step
   const int dpx = t >> 3, dch = t & 7;                 // dY: pixel, 16-byte chunk
@@ -148,8 +157,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p)
   const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(p.x, int64_t(p.N) * p.H * p.W * p.Cin * 2);
   const __amdgpu_buffer_rsrc_t rs_dy = make_rsrc(p.dy, p.M * p.Cout * 2);
   // Stage loads run kDepth stages ahead of the MFMAs in a register ring (one
-  // block per CU: nothing else would hide the ~0.8 us load latency; one stage
-  // in flight ran latency-bound at ~1800 cycles per 32-pixel step).  Stages
+  // block per CU: nothing else would hide the ~0.8 us load latency).  Stages
   // past the slice load out of range (zeros, no memory traffic), so the loop
   // has no tail and the compiler keeps counted vmcnt waits.
   constexpr int kDepth = 4;
@@ -157,28 +165,34 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p)
     uint4 dy, x0, x1;
   };
   Stage ring[kDepth];
-  int next_stage = 0;
+  int md = m_begin + dpx;                                           // this thread's dY pixel
+  uint32_t dy_byte = uint32_t(md) * uint32_t(p.Cout * 2) + uint32_t((co0 + dch * 8) * 2);
+  const uint32_t dy_step = uint32_t(BPX * p.Cout * 2);
+  int mx = m_begin + xpx0;                                          // X pixels mx, mx + 16
+  const int row_elems = p.W * p.Cin;
+  auto xload = [&](const PixelCursor& c, int m) {
+    const int ih = 2 * c.oh - 1 + kh, iw = 2 * c.ow - 1 + kw;
+    const bool ok = m < m_end && unsigned(ih) < unsigned(p.H) && unsigned(iw) < unsigned(p.W);
+    const int e = (c.n * p.H + ih) * row_elems + iw * p.Cin + ci;
+    return bload(rs_x, ok ? uint32_t(e) * 2u : kOOB);
+  };
   auto load = [&](Stage& r) {
-    const int64_t m0 = m_begin + int64_t(next_stage) * BPX;
-    const int64_t md = m0 + dpx;
-    r.dy = bload(rs_dy, md < m_end ? uint32_t((md * p.Cout + co0 + dch * 8) * 2) : kOOB);
-    auto xload = [&](const PixelCursor& c, int64_t m) {
-      const int ih = 2 * c.oh - 1 + kh, iw = 2 * c.ow - 1 + kw;
-      const bool ok = m < m_end && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
-      return bload(rs_x, ok ? uint32_t((((int64_t(c.n) * p.H + ih) * p.W + iw) * p.Cin + ci) * 2) : kOOB);
-    };
-    r.x0 = xload(c0, m0 + xpx0);
-    r.x1 = xload(c1, m0 + xpx0 + 16);
+    r.dy = bload(rs_dy, md < m_end ? dy_byte : kOOB);
+    r.x0 = xload(c0, mx);
+    r.x1 = xload(c1, mx + 16);
+    md += BPX;
+    dy_byte += dy_step;
+    mx += BPX;
     c0.advance(p.Ho, p.Wo);
     c1.advance(p.Ho, p.Wo);
-    ++next_stage;
   };
+  const int st_dy = dy_off(dpx, dch * 16), st_x0 = DY_TILE + x_off(xpx0, xch * 16),
+            st_x1 = DY_TILE + x_off(xpx0 + 16, xch * 16);
   auto store = [&](const Stage& r, int buf) {
-    char* dyi = smem + buf * STAGE;
-    char* xi = dyi + DY_TILE;
-    *reinterpret_cast<uint4*>(dyi + dy_off(dpx, dch * 16)) = r.dy;
-    *reinterpret_cast<uint4*>(xi + x_off(xpx0, xch * 16)) = r.x0;
-    *reinterpret_cast<uint4*>(xi + x_off(xpx0 + 16, xch * 16)) = r.x1;
+    char* base = smem + buf * STAGE;
+    *reinterpret_cast<uint4*>(base + st_dy) = r.dy;
+    *reinterpret_cast<uint4*>(base + st_x0) = r.x0;
+    *reinterpret_cast<uint4*>(base + st_x1) = r.x1;
   };
 
   f32x4 acc[2][4];
@@ -188,6 +202,15 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p)
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int wco = (wave >> 1) * 32, wkc = (wave & 1) * 64;
+  // per-lane transposed-read offsets (loop invariant): row 8g+q, columns col+4p
+  int ra[2], rb[4];
+  {
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) ra[i] = dy_off(8 * g + q, (wco + 16 * i + 4 * pp) * 2);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) rb[j] = x_off(8 * g + q, (wkc + 16 * j + 4 * pp) * 2);
+  }
 #pragma unroll
   for (int u = 0; u < kDepth; ++u) load(ring[u]);
   const int padded = (nsteps + kDepth - 1) / kDepth * kDepth;
@@ -200,13 +223,12 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       load(ring[u]);           // stage s + kDepth
-      const char* dyi = smem + buf * STAGE;
-      const char* xi = dyi + DY_TILE;
+      const char* base = smem + buf * STAGE;
       bf16x8 a[2], bm[4];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) a[i] = frag<false>(dyi, lane, wco + 16 * i);
+      for (int i = 0; i < 2; ++i) a[i] = frag_at(base, ra[i], 4 * DY_ROW);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bm[j] = frag<true>(xi, lane, wkc + 16 * j);
+      for (int j = 0; j < 4; ++j) bm[j] = frag_at(base + DY_TILE, rb[j], 4 * X_ROW);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -229,21 +251,44 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p)
       }
 }
 
-// sum the S slices; write fp32 dW[co][kh][kw][ci] at the parameter's strides
+// Sum the S slices into fp32 dW[co][kh][kw][ci] at the parameter's strides.
+// blockIdx.y takes a group of kSliceGroup slices and each lane four
+// consecutive elements (one 16-byte load per slice, all of a group's loads
+// independent and in flight together); groups add into the zeroed output
+// with float atomics (S / kSliceGroup adds per element).  One lane per
+// element walking all S slices serially was latency-bound (17 us at S = 64).
+constexpr int kSliceGroup = 8;
+
 __global__ __launch_bounds__(kThreads) void conv_wgrad_reduce_kernel(const float* __restrict__ partial, int S,
                                                                      int Cout, int Cin, float* __restrict__ out,
                                                                      int64_t s_co, int64_t s_ci, int64_t s_kh,
                                                                      int64_t s_kw) {
   const int KC = 16 * Cin;
-  const int64_t total = int64_t(Cout) * KC;
-  for (int64_t e = int64_t(blockIdx.x) * kThreads + threadIdx.x; e < total; e += int64_t(gridDim.x) * kThreads) {
-    float s = 0.f;
-    for (int k = 0; k < S; ++k) s += partial[int64_t(k) * total + e];
-    const int co = int(e / KC), kc = int(e - int64_t(co) * KC);
+  const int total = Cout * KC;
+  const int e0 = (int(blockIdx.x) * kThreads + int(threadIdx.x)) * 4;
+  if (e0 >= total) return;
+  const int k0 = int(blockIdx.y) * kSliceGroup;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int k = 0; k < kSliceGroup; ++k) {
+    if (k0 + k < S) {
+      const float4 v = *reinterpret_cast<const float4*>(partial + int64_t(k0 + k) * total + e0);
+      acc.x += v.x, acc.y += v.y, acc.z += v.z, acc.w += v.w;
+    }
+  }
+  const float vals[4] = {acc.x, acc.y, acc.z, acc.w};
+  const bool single = S <= kSliceGroup;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int e = e0 + j;
+    const int co = e / KC, kc = e - co * KC;
     const int tap = kc / Cin, ci = kc - tap * Cin;
-    out[co * s_co + ci * s_ci + (tap >> 2) * s_kh + (tap & 3) * s_kw] = s;
+    float* dst = out + co * s_co + ci * s_ci + (tap >> 2) * s_kh + (tap & 3) * s_kw;
+    if (single) *dst = vals[j];
+    else atomicAdd(dst, vals[j]);
   }
 }
+
 
 // ---------------------------------------------------------------------------
 // Forward: y[m][co] = sum_kc X_im2col[m][kc] * W[co][kc], with the BatchNorm
@@ -428,10 +473,15 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
   const int64_t blocks = tiles * p.slices;
   if (blocks > (int64_t(1) << 31) - 1) return hipErrorInvalidValue;
   conv_wgrad_kernel<<<unsigned(blocks), kThreads, 0, stream>>>(p);
-  const int64_t total = int64_t(p.Cout) * 16 * p.Cin;
-  const int64_t rb = (total + kThreads - 1) / kThreads;
-  conv_wgrad_reduce_kernel<<<unsigned(rb < 4096 ? rb : 4096), kThreads, 0, stream>>>(
-      p.partial, p.slices, p.Cout, p.Cin, out, s_co, s_ci, s_kh, s_kw);
+  const int64_t total = int64_t(p.Cout) * 16 * p.Cin;   // multiple of 4 * kThreads? not needed: lanes past it return
+  if (p.slices > kSliceGroup) {
+    // groups add atomically: start from zero (out is dense: contiguous or channels-last)
+    const hipError_t e = hipMemsetAsync(out, 0, size_t(total) * sizeof(float), stream);
+    if (e != hipSuccess) return e;
+  }
+  const dim3 rgrid(unsigned((total / 4 + kThreads - 1) / kThreads), unsigned((p.slices + kSliceGroup - 1) / kSliceGroup));
+  conv_wgrad_reduce_kernel<<<rgrid, kThreads, 0, stream>>>(p.partial, p.slices, p.Cout, p.Cin, out, s_co, s_ci,
+                                                           s_kh, s_kw);
   return hipGetLastError();
 }
 

@@ -71,14 +71,25 @@ class Discriminator(nn.Module):
         from .. import ops
         convs = [m for m in self.features if isinstance(m, nn.Conv2d)]
         weights = iter(ops.cast_bf16(*[c.weight for c in convs]))
-        for m in self.features:
+        layers = list(self.features)
+        stats = None
+        for i, m in enumerate(layers):
             if isinstance(m, nn.Conv2d):
                 w16 = next(weights)
                 if (mfma and m.stride == (2, 2) and m.padding == (1, 1) and m.bias is None and m.groups == 1
                         and m.dilation == (1, 1) and ops.conv_wgrad_supported(x, m.weight)):
-                    x = ops.conv4x4s2(x, m.weight, w16)
+                    nxt = layers[i + 1] if i + 1 < len(layers) else None
+                    fuse = (isinstance(nxt, ops.BatchNormLeakyReLU2d) and ops.conv_fwd_supported(x, w16)
+                            and nxt.fused_with_stats(x.new_empty((1, m.out_channels, 1, 1))))
+                    if fuse:   # BN statistics come out of the conv kernel's epilogue
+                        x, stats = ops.conv4x4s2(x, m.weight, w16, with_stats=True)
+                    else:
+                        x = ops.conv4x4s2(x, m.weight, w16)
                 else:
                     x = F.conv2d(x, w16, None, m.stride, m.padding, m.dilation, m.groups)
+            elif stats is not None and isinstance(m, ops.BatchNormLeakyReLU2d):
+                x = m.forward_from_stats(x, stats)
+                stats = None
             else:
                 x = m(x)
         return x.view(-1, 1).squeeze(1)

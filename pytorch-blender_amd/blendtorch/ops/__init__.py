@@ -645,7 +645,8 @@ def _bn_function():
 
     class _BatchNormLeakyReLU(torch.autograd.Function):
         @staticmethod
-        def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, slope, tracked=None):
+        def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, slope, tracked=None,
+                    stats=None):
             ext = hip_ext()
             N, C, H, W = x.shape
             M = N * H * W
@@ -653,16 +654,25 @@ def _bn_function():
             xs = _as_nhwc(x)
             w = weight.detach().float().contiguous()
             b = bias.detach().float().contiguous()
-            part = torch.empty(ext.bn_partial_floats(M, C, dt), dtype=torch.float32, device=x.device)
             mean = torch.empty(C, dtype=torch.float32, device=x.device)
             invstd = torch.empty_like(mean)
             y = torch.empty_like(xs)
             rm = running_mean.data_ptr() if running_mean is not None else 0
             rv = running_var.data_ptr() if running_var is not None else 0
-            _count('bn_forward')
-            ext.bn_forward(xs.data_ptr(), y.data_ptr(), M, C, dt, part.data_ptr(), float(eps), float(momentum),
-                           mean.data_ptr(), invstd.data_ptr(), rm, rv, w.data_ptr(), b.data_ptr(), float(slope),
-                           _stream(x.device), tracked.data_ptr() if tracked is not None else 0)
+            tr = tracked.data_ptr() if tracked is not None else 0
+            if stats is not None:
+                # per-tile sums from the producing conv's epilogue (conv_fwd): no reduction pass over x
+                _count('bn_forward_from_stats')
+                ext.bn_forward_from_stats(xs.data_ptr(), y.data_ptr(), M, C, dt, stats.data_ptr(),
+                                          stats.numel() // (2 * C), float(eps), float(momentum), mean.data_ptr(),
+                                          invstd.data_ptr(), rm, rv, w.data_ptr(), b.data_ptr(), float(slope),
+                                          _stream(x.device), tr)
+            else:
+                part = torch.empty(ext.bn_partial_floats(M, C, dt), dtype=torch.float32, device=x.device)
+                _count('bn_forward')
+                ext.bn_forward(xs.data_ptr(), y.data_ptr(), M, C, dt, part.data_ptr(), float(eps), float(momentum),
+                               mean.data_ptr(), invstd.data_ptr(), rm, rv, w.data_ptr(), b.data_ptr(), float(slope),
+                               _stream(x.device), tr)
             ctx.save_for_backward(xs, w, b, mean, invstd)
             ctx.slope = float(slope)
             return y.permute(0, 3, 1, 2)
@@ -683,7 +693,7 @@ def _bn_function():
             ext.bn_backward(xs.data_ptr(), gys.data_ptr(), gx.data_ptr(), M, C, dt, part.data_ptr(), mean.data_ptr(),
                             invstd.data_ptr(), w.data_ptr(), b.data_ptr(), dw.data_ptr(), db.data_ptr(), ctx.slope,
                             _stream(xs.device))
-            return gx.permute(0, 3, 1, 2), dw, db, None, None, None, None, None, None
+            return gx.permute(0, 3, 1, 2), dw, db, None, None, None, None, None, None, None
 
     return _BatchNormLeakyReLU
 
@@ -719,8 +729,9 @@ def batch_norm_leaky_relu(x, weight, bias, running_mean=None, running_var=None, 
     return _BN_FN.apply(x, weight, bias, running_mean, running_var, eps, momentum, slope)
 
 
-def _bn_apply_unchecked(x, weight, bias, running_mean, running_var, eps, momentum, slope, tracked=None):
-    return _BN_FN.apply(x, weight, bias, running_mean, running_var, eps, momentum, slope, tracked)
+def _bn_apply_unchecked(x, weight, bias, running_mean, running_var, eps, momentum, slope, tracked=None,
+                        stats=None):
+    return _BN_FN.apply(x, weight, bias, running_mean, running_var, eps, momentum, slope, tracked, stats)
 
 
 def reference_batch_norm_leaky_relu(x, weight, bias, running_mean=None, running_var=None, eps=1e-5, momentum=0.1,
@@ -758,6 +769,21 @@ def _bn_module():
                 return _bn_apply_unchecked(x, self.weight, self.bias, self.running_mean, self.running_var,
                                            self.eps, self.momentum, self.slope, self.num_batches_tracked)
             return F.leaky_relu(super().forward(x), self.slope)
+
+        def fused_with_stats(self, x):
+            """True when :meth:`forward_from_stats` applies to ``x``."""
+            return (self.training and self.affine and self.track_running_stats and self.momentum is not None
+                    and bn_supported(x))
+
+        def forward_from_stats(self, x, stats):
+            """Training forward with the batch statistics already summed by
+            the producing kernel (``conv_fwd``'s epilogue rows, see
+            :func:`conv4x4s2`): finalize + apply only."""
+            global _BN_FN
+            if _BN_FN is None:
+                _BN_FN = _bn_function()
+            return _bn_apply_unchecked(x, self.weight, self.bias, self.running_mean, self.running_var, self.eps,
+                                       self.momentum, self.slope, self.num_batches_tracked, stats)
 
         def extra_repr(self):
             return super().extra_repr() + f', slope={self.slope}'
@@ -857,15 +883,22 @@ def _conv_function():
         into the master weight's gradient (no bf16 round trip, no cast)."""
 
         @staticmethod
-        def forward(ctx, x, w32, w16):
+        def forward(ctx, x, w32, w16, with_stats=False):
             ctx.save_for_backward(x, w16)
             ctx.w32 = w32
+            if with_stats:
+                N, _, H, W = x.shape
+                M = N * ((H - 2) // 2 + 1) * ((W - 2) // 2 + 1)
+                stats = torch.empty(conv_fwd_stats_rows(M) * 2 * w16.shape[0], dtype=torch.float32, device=x.device)
+                y = conv_fwd(x, w16, stats)
+                ctx.mark_non_differentiable(stats)
+                return y, stats
             if conv_fwd_supported(x, w16):
                 return conv_fwd(x, w16)
             return F.conv2d(x, w16, None, 2, 1)
 
         @staticmethod
-        def backward(ctx, gy):
+        def backward(ctx, gy, gstats=None):
             x, w16 = ctx.saved_tensors
             gy = gy.contiguous(memory_format=torch.channels_last)
             gx = gw = None
@@ -874,7 +907,7 @@ def _conv_function():
                                                          [True, False, False])[0]
             if ctx.needs_input_grad[1]:
                 gw = conv_wgrad(x, gy, torch.empty_like(ctx.w32))
-            return gx, gw, None
+            return gx, gw, None, None
 
     return _Conv4x4s2
 
@@ -882,14 +915,18 @@ def _conv_function():
 _CONV_FN = None
 
 
-def conv4x4s2(x, w32, w16):
+def conv4x4s2(x, w32, w16, with_stats=False):
     """4x4 / stride-2 / pad-1 convolution of bf16 channels-last ``x`` with the
     bf16 copy ``w16`` of fp32 weight ``w32``; the gradient goes to ``w32``
-    (fp32, from the MFMA weight-gradient kernel).  See :func:`conv_wgrad_supported`."""
+    (fp32, from the MFMA weight-gradient kernel).  See :func:`conv_wgrad_supported`.
+    ``with_stats``: return ``(y, stats)``, the per-tile BatchNorm sums of y
+    from the forward kernel's epilogue (for ``BatchNormLeakyReLU2d.forward_from_stats``)."""
     global _CONV_FN
     if _CONV_FN is None:
         _CONV_FN = _conv_function()
-    return _CONV_FN.apply(x, w32, w16.detach())
+    if with_stats and not conv_fwd_supported(x, w16):
+        raise ValueError('conv4x4s2(with_stats=True) needs the MFMA forward (see conv_fwd_supported)')
+    return _CONV_FN.apply(x, w32, w16.detach(), with_stats)
 
 
 def __getattr__(name):

@@ -75,8 +75,10 @@ def test_discriminator_backward_with_mfma_convs(dev):
         n.load_state_dict(nets[0].state_dict())
     x = torch.rand(4, 3, 240, 320, device=dev).contiguous(memory_format=torch.channels_last)
     before = ops.KERNEL_CALLS.get('conv_wgrad', 0)
+    bn_before = ops.KERNEL_CALLS.get('bn_forward_from_stats', 0)
     nets[0].forward_bf16(x.to(torch.bfloat16), mfma=True).float().sum().backward()
     assert ops.KERNEL_CALLS['conv_wgrad'] == before + 3          # conv 2, 3 and 4 (conv 1 has Cin = 3)
+    assert ops.KERNEL_CALLS['bn_forward_from_stats'] == bn_before + 3   # their BNs take the epilogue sums
     nets[1].forward_bf16(x.to(torch.bfloat16), mfma=False).float().sum().backward()
     nets[2](x).sum().backward()                                   # fp32 reference
     for (n, pa), pb, pr in zip(nets[0].named_parameters(), nets[1].parameters(), nets[2].parameters()):
@@ -88,6 +90,11 @@ def test_discriminator_backward_with_mfma_convs(dev):
         ca, cb = cos(pa.grad), cos(pb.grad)
         print(n, f'cos(mfma, fp32)={ca:.6f} cos(miopen, fp32)={cb:.6f}')
         assert ca > 0.99 and ca >= cb - 2e-3, n
+    for ma, mb in zip(nets[0].modules(), nets[1].modules()):
+        if isinstance(ma, ops.BatchNormLeakyReLU2d):
+            assert int(ma.num_batches_tracked) == int(mb.num_batches_tracked) == 1
+            torch.testing.assert_close(ma.running_mean, mb.running_mean, rtol=2e-2, atol=1e-4)
+            torch.testing.assert_close(ma.running_var, mb.running_var, rtol=2e-2, atol=1e-4)
 
 
 @pytest.mark.gpu
