@@ -292,6 +292,7 @@ def main(argv=None):
                   instance_args=[['--mode', args.mode, '--sndhwm', '10', '--resolution', f'{res_w}x{res_h}'] + (['--shm', str(shm_slots), '--codec', args.codec] if shm_slots else [])]
                   * nprod)
     model = opt = None
+    copy_streams = args.copy_streams or (1 if args.consumer == 'disc' else 2)
     # the next frames' DMA starts between the step's forward and backward graphs
     dma_mid = args.consumer == 'disc' and args.dma_phase == 'mid' and args.dist != 'scatter'
     if args.consumer == 'disc':
@@ -344,7 +345,7 @@ def main(argv=None):
                                   max_items=total_batches * per_step, prefetch=6,
                                   io_threads=args.io_threads or None, timeoutms=60000, h2d=args.h2d,
                                   launch_depth=args.launch_depth,
-                                  copy_streams=args.copy_streams or (1 if args.consumer == 'disc' else 2),
+                                  copy_streams=copy_streams,
                                   defer_post=dma_mid,
                                   host_sync=None if args.host_sync == 'auto' else args.host_sync == 'on')
         if args.dist == 'scatter':
@@ -517,7 +518,7 @@ def main(argv=None):
                 'shm_slots': shm_slots,
                 'h2d': args.h2d,
                 'launch_depth': args.launch_depth,
-                'copy_streams': args.copy_streams if args.h2d == 'copy' else None,
+                'copy_streams': copy_streams if args.h2d == 'copy' else None,
                 'codec': args.codec if shm_slots else 'none',
                 'consumer_step': stepper.state if stepper is not None else None,
                 'decode_in_step': step_decode,
