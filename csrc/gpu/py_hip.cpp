@@ -414,7 +414,8 @@ PYBIND11_MODULE(_hip, m) {
   // result of the last iteration is checked, so a stale GPU-cached read of
   // host memory would show up as a mismatch (returned as `stale`).
   m.def("bench_frames_to_device",
-        [](const std::string& mode, const std::string& kind, int B, int H, int W, int Cin, int iters, int max_grid) {
+        [](const std::string& mode, const std::string& kind, int B, int H, int W, int Cin, int iters, int max_grid,
+           int copy_streams, bool pipelined) {
           py::gil_scoped_release nogil;
           const size_t img = size_t(H) * W * Cin;
           const size_t slot = (img + 4095) & ~size_t(4095);
@@ -444,6 +445,23 @@ PYBIND11_MODULE(_hip, m) {
           check(hipMemcpy(lut, hl.data(), hl.size() * sizeof(float), hipMemcpyHostToDevice), "lut");
           hipStream_t s;
           check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "stream");
+          // copy mode over K streams: frame b on stream b % K (each its own
+          // hardware queue, so several SDMA engines pull concurrently); the
+          // decode stream joins them with one event per stream
+          const int K = copy_streams < 1 ? 1 : (copy_streams > 4 ? 4 : copy_streams);
+          std::vector<hipStream_t> cs(size_t(K), nullptr);
+          std::vector<hipEvent_t> ce(size_t(K), nullptr);
+          for (int k = 1; k < K; ++k) {
+            check(hipStreamCreateWithFlags(&cs[size_t(k)], hipStreamNonBlocking), "stream");
+            check(hipEventCreateWithFlags(&ce[size_t(k)], hipEventDisableTiming), "event");
+          }
+          cs[0] = s;
+          hipEvent_t kdone;
+          check(hipEventCreateWithFlags(&kdone, hipEventDisableTiming), "event");
+          // pipelined: two staging buffers, no host sync between batches (the
+          // copies of batch i+1 overlap the decode of batch i)
+          uint8_t* stage2 = nullptr;
+          if (pipelined) check(hipMalloc(reinterpret_cast<void**>(&stage2), img * B), "hipMalloc");
           DecodeParams p;
           p.dst = dst;
           p.lut = lut;
@@ -456,22 +474,35 @@ PYBIND11_MODULE(_hip, m) {
           } else {
             p.src = stage;
           }
-          auto run = [&](int it) {
-            for (int b = 0; b < B; ++b) host[size_t(b) * slot] = uint8_t(it);   // fresh content per batch
-            if (!direct)
+          auto run = [&](int it, bool rewrite) {
+            if (rewrite)
+              for (int b = 0; b < B; ++b) host[size_t(b) * slot] = uint8_t(it);   // fresh content per batch
+            uint8_t* st = (pipelined && (it & 1)) ? stage2 : stage;
+            if (!direct) {
+              p.src = st;
+              for (int k = 1; k < K; ++k) check(hipStreamWaitEvent(cs[size_t(k)], kdone, 0), "wait");   // staging free
               for (int b = 0; b < B; ++b)
-                check(hipMemcpyAsync(stage + size_t(b) * img, host + size_t(b) * slot, img, hipMemcpyHostToDevice, s),
+                check(hipMemcpyAsync(st + size_t(b) * img, host + size_t(b) * slot, img, hipMemcpyHostToDevice,
+                                     cs[size_t(b % K)]),
                       "memcpy");
+              for (int k = 1; k < K; ++k) {
+                check(hipEventRecord(ce[size_t(k)], cs[size_t(k)]), "record");
+                check(hipStreamWaitEvent(s, ce[size_t(k)], 0), "wait");
+              }
+            }
             check(decode(p, s), "decode");
+            check(hipEventRecord(kdone, s), "record");
           };
           for (int i = 0; i < 5; ++i) {
-            run(i);
+            run(i, true);
             check(hipStreamSynchronize(s), "sync");
           }
           auto t0 = std::chrono::steady_clock::now();
           for (int i = 0; i < iters; ++i) {
-            check(hipStreamSynchronize(s), "sync");   // host rewrites only after the last read
-            run(100 + i);
+            if (!pipelined) check(hipStreamSynchronize(s), "sync");   // host rewrites only after the last read
+            const bool last = i == iters - 1;
+            if (pipelined && last) check(hipStreamSynchronize(s), "sync");
+            run(100 + i, !pipelined || last);
           }
           check(hipStreamSynchronize(s), "sync");
           double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / iters;
@@ -482,6 +513,12 @@ PYBIND11_MODULE(_hip, m) {
             check(hipMemcpy(&v, dst + size_t(b) * 3 * H * W, sizeof(float), hipMemcpyDeviceToHost), "d2h");
             if (v != float(uint8_t(100 + iters - 1))) ++stale;
           }
+          for (int k = 1; k < K; ++k) {
+            (void)hipStreamDestroy(cs[size_t(k)]);
+            (void)hipEventDestroy(ce[size_t(k)]);
+          }
+          (void)hipEventDestroy(kdone);
+          if (stage2) (void)hipFree(stage2);
           (void)hipStreamDestroy(s);
           (void)hipFree(stage);
           (void)hipFree(dst);
@@ -495,7 +532,7 @@ PYBIND11_MODULE(_hip, m) {
           return std::make_tuple(us, double(img) * B / us / 1e3, stale);
         },
         py::arg("mode"), py::arg("kind"), py::arg("B"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("iters"),
-        py::arg("max_grid") = 0);
+        py::arg("max_grid") = 0, py::arg("copy_streams") = 1, py::arg("pipelined") = false);
 
   // Kernel-only timing (no Python launch overhead): `iters` back-to-back
   // decode launches between two HIP events; returns microseconds per launch.

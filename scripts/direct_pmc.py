@@ -12,5 +12,5 @@ from blendtorch import ops  # noqa: E402
 
 e = ops.hip_ext()
 for mode in ('copy', 'direct'):
-    us, gbs, stale = e.bench_frames_to_device(mode, 'register', 8, 480, 640, 4, 10, 0)
+    us, gbs, stale = e.bench_frames_to_device(mode, 'register', 8, 480, 640, 4, 10, 0, 1, False)
     print(mode, round(us, 1), 'us/batch', round(gbs, 1), 'GB/s', 'stale', stale, flush=True)
