@@ -291,18 +291,32 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_reduce_kernel(const float
 
 
 // ---------------------------------------------------------------------------
-// Forward: y[m][co] = sum_kc X_im2col[m][kc] * W[co][kc], with the BatchNorm
-// statistics of y (per-channel sum and sum of squares of the bf16-rounded
-// outputs) reduced in the epilogue into one partial row per pixel tile -- the
-// rows bn_finalize folds, so the separate BN reduction pass over y is gone.
-// Both MFMA operands have K (kc) contiguous in memory here (an im2col row is
-// 4 neighbouring input pixels' channels; a channels-last weight row is
-// [kh][kw][ci]), so tiles are staged as plain 128-byte LDS rows (16-byte
-// chunks XOR-swizzled by row) and read with ds_read_b128.
+// Tap-gather GEMM: the forward convolution AND the data gradient.
+//
+//   out[pixel m][col] = sum over taps t, channels c of
+//                       src[n][r0(m) + dr(t)][c0(m) + dc(t)][c] * w[col][wtap(t)][c]
+//
+// forward (16 taps):   src = x, r0 = 2a - 1, c0 = 2b - 1, (dr, dc) = (kh, kw),
+//                      w = the channels-last weight [Cout][kh][kw][Cin]; out = y.
+// data gradient: dx[n][ih][iw] only receives from the 2 x 2 taps whose
+//   stride-2 phase matches (ih, iw), so it is 4 GEMMs (parity classes
+//   (ph, pw) = blockIdx.y) of 4 taps each over the grid ih = 2a + ph,
+//   iw = 2b + pw: src = dy, r0 = a, c0 = b, dr = ph - t/2, dc = pw - t%2,
+//   kh = 1 - ph + 2(t/2), kw = 1 - pw + 2(t%2), and w = the weight transposed
+//   to [Cin][kh][kw][Cout] (conv_weight_t).
+//
+// Both MFMA operands have K (tap, channel) contiguous in memory: a tap's C
+// channels are one NHWC pixel, a weight row is [kh][kw][c].  Tiles stage as
+// 128-byte LDS rows (16-byte chunks XOR-swizzled by row) read with
+// ds_read_b128.  All index math is 32-bit and per-pixel bases are computed
+// once; padding reads are range-checked buffer loads that return zeros.  The
+// epilogue goes through LDS so every global store is 16 bytes; the forward
+// also sums each output channel (and its square) of the bf16-rounded result
+// into one partial row per pixel tile, which bn_finalize folds.
 
 constexpr int FBM = 128;   // pixels per block
 constexpr int FBN = 64;    // output channels per block
-constexpr int FBK = 64;    // kc per k-step
+constexpr int FBK = 64;    // K per k-step
 constexpr int F_ROW = FBK * 2;                  // 128-byte LDS rows
 constexpr int FA_TILE = FBM * F_ROW;            // 16 KiB
 constexpr int FB_TILE = FBN * F_ROW;            // 8 KiB
@@ -310,64 +324,104 @@ constexpr int F_STAGE = FA_TILE + FB_TILE;
 
 __device__ __forceinline__ int f_off(int r, int chunk) { return r * F_ROW + ((chunk ^ (r & 7)) << 4); }
 
-__global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * F_STAGE + 2 * 2 * FBN * 4];
-  float* red = reinterpret_cast<float*>(smem + 2 * F_STAGE);   // [2 waves in m][2][FBN]
+struct TapGemm {
+  const uint16_t* src = nullptr;
+  const uint16_t* w = nullptr;     // [NOUT][16][C]
+  uint16_t* dst = nullptr;
+  float* stats = nullptr;          // forward only (nullable)
+  int N = 0, SH = 0, SW = 0, C = 0, cshift = 0;   // src [N][SH][SW][C], C = 1 << cshift
+  int GH = 0, GW = 0, M = 0;       // GEMM rows: m = (n * GH + a) * GW + b
+  int NOUT = 0, OH = 0, OW = 0;    // dst [N][OH][OW][NOUT]
+};
+
+// BN = output channels per block (64, or 32 for 32-channel outputs such as
+// the first layer's data gradient); 4 waves as WGM (pixels) x WGN (channels).
+template <bool DGRAD, int BN>
+__global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
+  constexpr int WGM = BN == 64 ? 2 : 4, WGN = 4 / WGM;
+  constexpr int FM = FBM / WGM / 16, FN = BN / WGN / 16;   // 16x16 fragments per wave
+  __shared__ __attribute__((aligned(16))) char smem[2 * F_STAGE + 4 * 2 * 64 * 4];
+  float* red = reinterpret_cast<float*>(smem + 2 * F_STAGE);   // [WGM][2][BN]
   const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
-  const int K = 16 * p.Cin, NT = p.Cout / FBN;
-  const int64_t MT = (p.M + FBM - 1) / FBM;
+  constexpr int NTAPS = DGRAD ? 4 : 16;
+  const int K = NTAPS * p.C, NT = p.NOUT / BN;
+  const int ph = DGRAD ? int(blockIdx.y) >> 1 : 0, pw = DGRAD ? int(blockIdx.y) & 1 : 0;
 
   const int nwg = int(gridDim.x), b = int(blockIdx.x);
   const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
-  const int mt = w / NT, co0 = (w - mt * NT) * FBN;
-  const int64_t m0 = int64_t(mt) * FBM;
+  const int mt = w / NT, n0 = (w - mt * NT) * BN;
+  const int m0 = mt * FBM;
 
-  // staging: A chunks rows ar + 32j (j = 0..3), B chunks rows ar + 32j (j = 0, 1); chunk ac
+  // this thread's 4 GEMM rows (staging A, and the epilogue stores): ar + 32j
   const int ar = t >> 3, ac = t & 7;
-  int pn[4], poh[4], pow_[4];
+  int rb[4], cb[4], base[4], obase[4];
   bool pin[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int64_t m = m0 + ar + 32 * j;
+    const int m = m0 + ar + 32 * j;
     pin[j] = m < p.M;
-    const int64_t mm = pin[j] ? m : 0;
-    const int64_t hw = int64_t(p.Ho) * p.Wo;
-    pn[j] = int(mm / hw);
-    const int r = int(mm - int64_t(pn[j]) * hw);
-    poh[j] = r / p.Wo;
-    pow_[j] = r - poh[j] * p.Wo;
+    const int mm = pin[j] ? m : 0;
+    const int n = mm / (p.GH * p.GW), rem = mm - n * (p.GH * p.GW);
+    const int a = rem / p.GW, bb = rem - a * p.GW;
+    rb[j] = DGRAD ? a : 2 * a - 1;
+    cb[j] = DGRAD ? bb : 2 * bb - 1;
+    base[j] = (n * p.SH + rb[j]) * p.SW + cb[j];
+    obase[j] = DGRAD ? ((n * p.OH + 2 * a + ph) * p.OW + 2 * bb + pw) * p.NOUT : mm * p.NOUT;
   }
-  const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(p.x, int64_t(p.N) * p.H * p.W * p.Cin * 2);
+  const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(p.src, int64_t(p.N) * p.SH * p.SW * p.C * 2);
+  const uint16_t* wrow0 = p.w + (n0 + ar) * (16 * p.C);
+  const uint16_t* wrow1 = p.w + (n0 + (BN == 64 ? ar + 32 : ar)) * (16 * p.C);
   uint4 ra[4], rb0, rb1;
   auto load = [&](int ks) {
     const int kc = ks * FBK + ac * 8;
-    const int kh = kc / (4 * p.Cin), rem = kc - kh * 4 * p.Cin;
-    const int kw = rem / p.Cin, ci = rem - kw * p.Cin;
+    const int tap = kc >> p.cshift, ch = kc & (p.C - 1);
+    int dr, dc, wtap;
+    if (DGRAD) {
+      dr = ph - (tap >> 1);
+      dc = pw - (tap & 1);
+      wtap = (1 - ph + 2 * (tap >> 1)) * 4 + (1 - pw + 2 * (tap & 1));
+    } else {
+      dr = tap >> 2;
+      dc = tap & 3;
+      wtap = tap;
+    }
+    const int toff = dr * p.SW + dc;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int ih = 2 * poh[j] - 1 + kh, iw = 2 * pow_[j] - 1 + kw;
-      const bool ok = pin[j] && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
-      ra[j] = bload(rs_x, ok ? uint32_t((((int64_t(pn[j]) * p.H + ih) * p.W + iw) * p.Cin + ci) * 2) : kOOB);
+      const bool ok = pin[j] && unsigned(rb[j] + dr) < unsigned(p.SH) && unsigned(cb[j] + dc) < unsigned(p.SW);
+      ra[j] = bload(rs_src, ok ? uint32_t((((base[j] + toff) << p.cshift) + ch) * 2) : kOOB);
     }
-    rb0 = *reinterpret_cast<const uint4*>(p.w + int64_t(co0 + ar) * K + kc);
-    rb1 = *reinterpret_cast<const uint4*>(p.w + int64_t(co0 + ar + 32) * K + kc);
+    const int woff = wtap * p.C + ch;
+    rb0 = *reinterpret_cast<const uint4*>(wrow0 + woff);
+    if (BN == 64) rb1 = *reinterpret_cast<const uint4*>(wrow1 + woff);
   };
+  const int st_a = f_off(ar, ac);   // rows ar + 32j keep the swizzle phase: (ar + 32j) & 7 == ar & 7
   auto store = [&](int buf) {
     char* ai = smem + buf * F_STAGE;
-    char* bi = ai + FA_TILE;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) *reinterpret_cast<uint4*>(ai + f_off(ar + 32 * j, ac)) = ra[j];
-    *reinterpret_cast<uint4*>(bi + f_off(ar, ac)) = rb0;
-    *reinterpret_cast<uint4*>(bi + f_off(ar + 32, ac)) = rb1;
+    for (int j = 0; j < 4; ++j) *reinterpret_cast<uint4*>(ai + st_a + j * 32 * F_ROW) = ra[j];
+    *reinterpret_cast<uint4*>(ai + FA_TILE + st_a) = rb0;
+    if (BN == 64) *reinterpret_cast<uint4*>(ai + FA_TILE + st_a + 32 * F_ROW) = rb1;
   };
 
-  f32x4 acc[4][2];
+  f32x4 acc[FM][FN];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int wm = wave >> 1, wn = wave & 1;
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int row0 = wm * (FBM / WGM), col0 = wn * (BN / WGN);
+  // fragment read offsets (loop invariant): row r, chunk 4 kk + lane / 16
+  int fa[FM][2], fb[FN][2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int chunk = 4 * kk + (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) fa[i][kk] = f_off(row0 + 16 * i + (lane & 15), chunk);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) fb[j][kk] = FA_TILE + f_off(col0 + 16 * j + (lane & 15), chunk);
+  }
   const int nsteps = K / FBK;
   load(0);
   store(0);
@@ -375,54 +429,51 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdParams p) {
   for (int s = 0; s < nsteps; ++s) {
     if (s + 1 < nsteps) load(s + 1);
     const char* ai = smem + (s & 1) * F_STAGE;
-    const char* bi = ai + FA_TILE;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const int chunk = 4 * kk + (lane >> 4);
-      bf16x8 a[4], bb[2];
+      bf16x8 a[FM], bb[FN];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = wm * 64 + 16 * i + (lane & 15);
-        a[i] = *reinterpret_cast<const bf16x8*>(ai + f_off(r, chunk));
-      }
+      for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const bf16x8*>(ai + fa[i][kk]);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int r = wn * 32 + 16 * j + (lane & 15);
-        bb[j] = *reinterpret_cast<const bf16x8*>(bi + f_off(r, chunk));
-      }
+      for (int j = 0; j < FN; ++j) bb[j] = *reinterpret_cast<const bf16x8*>(ai + fb[j][kk]);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bb[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bb[j], acc[i][j], 0, 0, 0);
     }
     if (s + 1 < nsteps) store((s + 1) & 1);
     __syncthreads();
   }
 
-  // epilogue: bf16 y (RNE), and BN sums of the rounded values per channel
-  float sum[2] = {0.f, 0.f}, sq[2] = {0.f, 0.f};
+  // epilogue: round to bf16 (RNE) into an LDS tile [FBM][BN] (128-byte row
+  // pitch, same swizzle), sum the rounded values per channel (forward), then
+  // 16-byte stores of whole row chunks
+  uint16_t* tile = reinterpret_cast<uint16_t*>(smem);
+  float sum[FN], sq[FN];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int j = 0; j < FN; ++j) sum[j] = sq[j] = 0.f;
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int64_t m = m0 + wm * 64 + 16 * i + 4 * (lane >> 4) + r;
-        const int co = co0 + wn * 32 + 16 * j + (lane & 15);
-        const float v = acc[i][j][r];
-        uint32_t u = __float_as_uint(v);
-        u += 0x7FFFu + ((u >> 16) & 1u);               // round to nearest even (finite values)
+        const int row = row0 + 16 * i + 4 * (lane >> 4) + r;
+        const int col = col0 + 16 * j + (lane & 15);
+        uint32_t u = __float_as_uint(acc[i][j][r]);
+        u += 0x7FFFu + ((u >> 16) & 1u);
         const uint16_t h = uint16_t(u >> 16);
-        if (m < p.M) {
-          p.y[m * p.Cout + co] = h;
+        tile[(f_off(row, col >> 3) >> 1) + (col & 7)] = h;
+        if (!DGRAD && m0 + row < p.M) {
           const float vr = __uint_as_float(uint32_t(h) << 16);
           sum[j] += vr;
           sq[j] += vr * vr;
         }
       }
-  if (p.stats) {
+  if (!DGRAD && p.stats) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {   // lanes l, l^16, l^32, l^48 hold the same channel
+    for (int j = 0; j < FN; ++j) {   // lanes l, l^16, l^32, l^48 hold the same channel
       sum[j] += __shfl_xor(sum[j], 16);
       sum[j] += __shfl_xor(sum[j], 32);
       sq[j] += __shfl_xor(sq[j], 16);
@@ -430,19 +481,38 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdParams p) {
     }
     if (lane < 16) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        red[(wm * 2 + 0) * FBN + wn * 32 + 16 * j + lane] = sum[j];
-        red[(wm * 2 + 1) * FBN + wn * 32 + 16 * j + lane] = sq[j];
+      for (int j = 0; j < FN; ++j) {
+        red[(wm * 2 + 0) * BN + col0 + 16 * j + lane] = sum[j];
+        red[(wm * 2 + 1) * BN + col0 + 16 * j + lane] = sq[j];
       }
     }
-    __syncthreads();
-    if (t < 2 * FBN) {
-      const int which = t / FBN, c = t - which * FBN;   // 0: sum, 1: sum of squares
-      const float v = red[which * FBN + c] + red[(2 + which) * FBN + c];
-      p.stats[int64_t(mt) * 2 * p.Cout + which * p.Cout + co0 + c] = v;
+  }
+  __syncthreads();
+  if (ac < BN / 8) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!pin[j]) continue;
+      const uint4 v = *reinterpret_cast<const uint4*>(smem + st_a + j * 32 * F_ROW);
+      *reinterpret_cast<uint4*>(p.dst + obase[j] + n0 + ac * 8) = v;
     }
   }
-  (void)MT;
+  if (!DGRAD && p.stats && t < 2 * BN) {
+    const int which = t / BN, c = t - which * BN;   // 0: sum, 1: sum of squares
+    float v = 0.f;
+#pragma unroll
+    for (int g = 0; g < WGM; ++g) v += red[(g * 2 + which) * BN + c];
+    p.stats[mt * 2 * p.NOUT + which * p.NOUT + n0 + c] = v;
+  }
+}
+
+// [Cout][kh][kw][Cin] (channels-last weight, any dtype pair) -> [Cin][kh][kw][Cout]
+__global__ __launch_bounds__(kThreads) void weight_t_kernel(const uint16_t* __restrict__ w, uint16_t* __restrict__ wt,
+                                                            int Cout, int Cin) {
+  const int total = Cout * 16 * Cin;
+  for (int e = int(blockIdx.x) * kThreads + int(threadIdx.x); e < total; e += int(gridDim.x) * kThreads) {
+    const int ci = e % Cin, tap = (e / Cin) % 16, co = e / (16 * Cin);
+    wt[(ci * 16 + tap) * Cout + co] = w[e];
+  }
 }
 
 }  // namespace
@@ -485,7 +555,31 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
   return hipGetLastError();
 }
 
-bool conv_fwd_supported(int Cin, int Cout) { return Cin >= 8 && Cin % 8 == 0 && (16 * Cin) % FBK == 0 && Cout % FBN == 0; }
+namespace {
+int ilog2_exact(int v) {
+  int k = 0;
+  while ((1 << k) < v) ++k;
+  return (1 << k) == v ? k : -1;
+}
+}  // namespace
+
+bool conv_fwd_supported(int Cin, int Cout) {
+  return Cin >= 8 && ilog2_exact(Cin) >= 0 && (16 * Cin) % FBK == 0 && Cout % 32 == 0;
+}
+
+bool conv_dgrad_supported(int Cin, int Cout) {
+  return Cout >= 16 && ilog2_exact(Cout) >= 0 && (4 * Cout) % FBK == 0 && Cin % 32 == 0;
+}
+
+namespace {
+template <bool DGRAD>
+void launch_tap_gemm(const TapGemm& g, unsigned ytiles, hipStream_t stream) {
+  const bool wide = g.NOUT % 64 == 0;
+  const int64_t blocks = conv_fwd_tiles(g.M) * (g.NOUT / (wide ? 64 : 32));
+  if (wide) tap_gemm_kernel<DGRAD, 64><<<dim3(unsigned(blocks), ytiles), kThreads, 0, stream>>>(g);
+  else tap_gemm_kernel<DGRAD, 32><<<dim3(unsigned(blocks), ytiles), kThreads, 0, stream>>>(g);
+}
+}  // namespace
 
 int64_t conv_fwd_tiles(int64_t M) { return (M + FBM - 1) / FBM; }
 
@@ -493,11 +587,41 @@ hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream) {
   if (!conv_fwd_supported(p.Cin, p.Cout) || !p.x || !p.w || !p.y) return hipErrorInvalidValue;
   if (p.Ho != (p.H + 2 - 4) / 2 + 1 || p.Wo != (p.W + 2 - 4) / 2 + 1 || p.M != int64_t(p.N) * p.Ho * p.Wo)
     return hipErrorInvalidValue;
-  if ((reinterpret_cast<uintptr_t>(p.x) | reinterpret_cast<uintptr_t>(p.w)) & 15) return hipErrorInvalidValue;
-  if (int64_t(p.N) * p.H * p.W * p.Cin * 2 >= int64_t(kOOB)) return hipErrorInvalidValue;   // 32-bit buffer offsets
-  const int64_t blocks = conv_fwd_tiles(p.M) * (p.Cout / FBN);
-  if (blocks > (int64_t(1) << 31) - 1) return hipErrorInvalidValue;
-  conv_fwd_kernel<<<unsigned(blocks), kThreads, 0, stream>>>(p);
+  if ((reinterpret_cast<uintptr_t>(p.x) | reinterpret_cast<uintptr_t>(p.w) | reinterpret_cast<uintptr_t>(p.y)) & 15)
+    return hipErrorInvalidValue;
+  if (int64_t(p.N) * p.H * p.W * p.Cin * 2 >= int64_t(kOOB) || p.M * p.Cout >= int64_t(kOOB))
+    return hipErrorInvalidValue;   // 32-bit offsets
+  TapGemm g;
+  g.src = p.x, g.w = p.w, g.dst = p.y, g.stats = p.stats;
+  g.N = p.N, g.SH = p.H, g.SW = p.W, g.C = p.Cin, g.cshift = ilog2_exact(p.Cin);
+  g.GH = p.Ho, g.GW = p.Wo, g.M = int(p.M);
+  g.NOUT = p.Cout, g.OH = p.Ho, g.OW = p.Wo;
+  launch_tap_gemm<false>(g, 1, stream);
+  return hipGetLastError();
+}
+
+hipError_t conv_weight_t(const uint16_t* w, uint16_t* wt, int Cout, int Cin, hipStream_t stream) {
+  if (!w || !wt || Cout <= 0 || Cin <= 0) return hipErrorInvalidValue;
+  const int total = Cout * 16 * Cin;
+  const int blocks = (total + kThreads - 1) / kThreads;
+  weight_t_kernel<<<blocks < 2048 ? blocks : 2048, kThreads, 0, stream>>>(w, wt, Cout, Cin);
+  return hipGetLastError();
+}
+
+hipError_t conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int N, int H, int W, int Cin, int Cout,
+                      hipStream_t stream) {
+  if (!conv_dgrad_supported(Cin, Cout) || !dy || !wt || !dx || H % 2 || W % 2) return hipErrorInvalidValue;
+  if ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(wt) | reinterpret_cast<uintptr_t>(dx)) & 15)
+    return hipErrorInvalidValue;
+  const int Ho = H / 2, Wo = W / 2;
+  if (int64_t(N) * Ho * Wo * Cout * 2 >= int64_t(kOOB) || int64_t(N) * H * W * Cin >= int64_t(kOOB))
+    return hipErrorInvalidValue;
+  TapGemm g;
+  g.src = dy, g.w = wt, g.dst = dx;
+  g.N = N, g.SH = Ho, g.SW = Wo, g.C = Cout, g.cshift = ilog2_exact(Cout);
+  g.GH = Ho, g.GW = Wo, g.M = N * Ho * Wo;   // one parity class: every (a, b)
+  g.NOUT = Cin, g.OH = H, g.OW = W;
+  launch_tap_gemm<true>(g, 4, stream);
   return hipGetLastError();
 }
 

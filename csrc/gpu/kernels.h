@@ -263,6 +263,14 @@ struct ConvFwdParams {
 bool conv_fwd_supported(int Cin, int Cout);
 int64_t conv_fwd_tiles(int64_t M);
 hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream);
+// Data gradient of the same convolution (same tap-gather GEMM kernel, four
+// stride-2 parity classes in one launch): dy [N][H/2][W/2][Cout] bf16,
+// wt = conv_weight_t(w) [Cin][4][4][Cout] bf16 -> dx [N][H][W][Cin] bf16.
+// Cout a power of two >= 16, Cin % 64 == 0, H and W even.
+bool conv_dgrad_supported(int Cin, int Cout);
+hipError_t conv_weight_t(const uint16_t* w, uint16_t* wt, int Cout, int Cin, hipStream_t stream);
+hipError_t conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int N, int H, int W, int Cin, int Cout,
+                      hipStream_t stream);
 // bn_finalize over `nblocks` partial rows produced elsewhere (conv_fwd's epilogue)
 hipError_t bn_finalize_rows(const float* partial, int nblocks, int64_t M, int C, float eps, float momentum,
                             float* mean, float* invstd, float* running_mean, float* running_var, hipStream_t stream,

@@ -232,6 +232,16 @@ PYBIND11_MODULE(_hip, m) {
         });
 
   m.def("conv_fwd_tiles", &conv_fwd_tiles);
+  m.def("conv_dgrad_supported", &conv_dgrad_supported);
+  m.def("conv_weight_t", [](uintptr_t w, uintptr_t wt, int Cout, int Cin, uintptr_t stream) {
+    check(conv_weight_t(ptr<const uint16_t>(w), ptr<uint16_t>(wt), Cout, Cin, stream_of(stream)), "conv_weight_t");
+  });
+  m.def("conv_dgrad", [](uintptr_t dy, uintptr_t wt, uintptr_t dx, int N, int H, int W, int Cin, int Cout,
+                         uintptr_t stream) {
+    check(conv_dgrad(ptr<const uint16_t>(dy), ptr<const uint16_t>(wt), ptr<uint16_t>(dx), N, H, W, Cin, Cout,
+                     stream_of(stream)),
+          "conv_dgrad");
+  });
   m.def("conv_fwd",
         [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, int N, int H, int W, int Cin, int Ho, int Wo,
            int Cout, uintptr_t stream) {

@@ -858,12 +858,40 @@ def conv_fwd(x, w16, stats=None):
     return y
 
 
+def conv_dgrad(dy, w16, in_shape):
+    """Data gradient of :func:`conv_fwd` on the same MFMA kernel (four
+    stride-2 parity classes, 4 taps each): ``dy`` [N, Cout, H/2, W/2] bf16
+    channels-last, ``w16`` [Cout, Cin, 4, 4] bf16 channels-last -> dx
+    [N, Cin, H, W] bf16 channels-last."""
+    import torch
+    ext = hip_ext()
+    N, Cin, H, W = in_shape
+    Cout = w16.shape[0]
+    cl = torch.channels_last
+    if not (dy.is_contiguous(memory_format=cl) and w16.is_contiguous(memory_format=cl)):
+        raise ValueError('conv_dgrad needs channels-last dy and weight')
+    if tuple(dy.shape) != (N, Cout, H // 2, W // 2) or dy.dtype != torch.bfloat16 or w16.dtype != torch.bfloat16:
+        raise ValueError(f'conv_dgrad: dy {dy.dtype} {tuple(dy.shape)} / w {tuple(w16.shape)} vs input {in_shape}')
+    wt = torch.empty(Cin * 16 * Cout, dtype=torch.bfloat16, device=dy.device)
+    ext.conv_weight_t(w16.data_ptr(), wt.data_ptr(), Cout, Cin, _stream(dy.device))
+    dx = torch.empty((N, Cin, H, W), dtype=torch.bfloat16, device=dy.device, memory_format=cl)
+    _count('conv_dgrad')
+    ext.conv_dgrad(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), N, H, W, Cin, Cout, _stream(dy.device))
+    return dx
+
+
+def conv_dgrad_supported(x, w):
+    """True when :func:`conv_dgrad` takes the gradient of ``conv_fwd(x, w)``."""
+    return (conv_fwd_supported(x, w) and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0
+            and bool(hip_ext().conv_dgrad_supported(int(w.shape[1]), int(w.shape[0]))))
+
+
 def conv_fwd_supported(x, w):
     import torch
     if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and w.dim() == 4):
         return False
     cout, cin, kh, kw = w.shape
-    return ((kh, kw) == (4, 4) and x.shape[1] == cin and cin % 8 == 0 and cout % 64 == 0
+    return ((kh, kw) == (4, 4) and x.shape[1] == cin and cin >= 8 and cin & (cin - 1) == 0 and cout % 32 == 0
             and x.is_contiguous(memory_format=torch.channels_last)
             and w.is_contiguous(memory_format=torch.channels_last))
 
@@ -903,8 +931,11 @@ def _conv_function():
             gy = gy.contiguous(memory_format=torch.channels_last)
             gx = gw = None
             if ctx.needs_input_grad[0]:
-                gx = torch.ops.aten.convolution_backward(gy, x, w16, None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1,
-                                                         [True, False, False])[0]
+                if conv_dgrad_supported(x, w16):
+                    gx = conv_dgrad(gy, w16, tuple(x.shape))
+                else:
+                    gx = torch.ops.aten.convolution_backward(gy, x, w16, None, [2, 2], [1, 1], [1, 1], False, [0, 0],
+                                                             1, [True, False, False])[0]
             if ctx.needs_input_grad[1]:
                 gw = conv_wgrad(x, gy, torch.empty_like(ctx.w32))
             return gx, gw, None, None

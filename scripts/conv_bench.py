@@ -56,6 +56,11 @@ def main():
         row['mfma_fwd_stats_us'] = round(timed(lambda: ops.conv_fwd(x, w16, stats), a.iters), 2)
         yref = F.conv2d(x.float(), w16.float(), None, 2, 1)
         row['fwd_rel_err'] = float(f'{float((ops.conv_fwd(x, w16).float() - yref).abs().max() / yref.abs().max()):.2e}')
+        row['miopen_dgrad_us'] = round(timed(lambda: torch.ops.aten.convolution_backward(
+            dy, x, w16, None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False]), a.iters), 2)
+        row['mfma_dgrad_us'] = round(timed(lambda: ops.conv_dgrad(dy, w16, tuple(x.shape)), a.iters), 2)
+        dref = torch.nn.grad.conv2d_input(tuple(x.shape), w16.float(), dy.float(), stride=2, padding=1)
+        row['dgrad_rel_err'] = float(f'{float((ops.conv_dgrad(dy, w16, tuple(x.shape)).float() - dref).abs().max() / dref.abs().max()):.2e}')
         ref = torch.nn.grad.conv2d_weight(x.float(), (cout, cin, 4, 4), dy.float(), stride=2, padding=1)
         for tb in (256, 512, 1024, 2048):
             us = timed(lambda: ops.conv_wgrad(x, dy, out, target_blocks=tb), a.iters)

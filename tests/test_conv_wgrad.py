@@ -99,7 +99,8 @@ def test_discriminator_backward_with_mfma_convs(dev):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('N,Cin,H,W,Cout', [(2, 32, 30, 40, 64), (2, 64, 16, 20, 128), (1, 128, 8, 10, 256),
-                                            (3, 32, 14, 18, 64), (8, 32, 240, 320, 64), (2, 8, 12, 16, 64)])
+                                            (3, 32, 14, 18, 64), (8, 32, 240, 320, 64), (2, 8, 12, 16, 64),
+                                            (2, 16, 20, 24, 32), (1, 64, 6, 10, 96)])
 def test_forward_matches_fp32_reference_and_stats(dev, N, Cin, H, W, Cout):
     import torch.nn.functional as F
     g = torch.Generator(device=dev).manual_seed(N + Cin + W)
@@ -118,3 +119,20 @@ def test_forward_matches_fp32_reference_and_stats(dev, N, Cin, H, W, Cout):
     yf = y.float().permute(0, 2, 3, 1).reshape(-1, Cout)
     torch.testing.assert_close(st[0], yf.sum(0), rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(st[1], (yf * yf).sum(0), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('N,Cin,H,W,Cout', [(2, 64, 30, 40, 64), (2, 64, 16, 20, 128), (1, 128, 8, 10, 256),
+                                            (3, 64, 14, 18, 32), (8, 64, 120, 160, 128), (2, 128, 12, 16, 16),
+                                            (8, 32, 240, 320, 64), (2, 32, 10, 12, 64)])
+def test_dgrad_matches_fp32_reference(dev, N, Cin, H, W, Cout):
+    g = torch.Generator(device=dev).manual_seed(N * 7 + Cin + W)
+    cl = torch.channels_last
+    w = (0.1 * torch.randn(Cout, Cin, 4, 4, device=dev, generator=g)).to(torch.bfloat16).contiguous(memory_format=cl)
+    dy = torch.randn(N, Cout, H // 2, W // 2, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    before = ops.KERNEL_CALLS.get('conv_dgrad', 0)
+    dx = ops.conv_dgrad(dy, w, (N, Cin, H, W))
+    assert ops.KERNEL_CALLS['conv_dgrad'] == before + 1
+    ref = torch.nn.grad.conv2d_input((N, Cin, H, W), w.float(), dy.float(), stride=2, padding=1)
+    assert dx.is_contiguous(memory_format=cl) and dx.dtype == torch.bfloat16
+    torch.testing.assert_close(dx.float(), ref, rtol=2 ** -7, atol=1e-3 * float(ref.abs().max()))
