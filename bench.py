@@ -141,6 +141,9 @@ def parse_args(argv=None):
                     help='disc consumer: when the next frames\' host->device DMA may start -- start = when the '
                          'step begins (overlapping the memory-bound forward); mid = between the forward and the '
                          'backward graph (DeviceLoader(defer_post=True) + CapturedStep(split=True))')
+    ap.add_argument('--head', choices=['fused', 'torch'], default='fused',
+                    help='disc consumer: fused = pool/conv/sigmoid/BCE head as gfx950 kernels (ops.disc_head_bce); '
+                         'torch = the library layers + BCELoss')
     ap.add_argument('--optim', choices=['gfx950', 'torch'], default='gfx950',
                     help='disc consumer optimizer: gfx950 = ops.FusedAdam (two launches per step); '
                          'torch = torch.optim.Adam(fused=True, capturable=True)')
@@ -364,6 +367,9 @@ def main(argv=None):
                 from blendtorch import ops
                 x = ops.decode(x, decode)   # gfx950 decode, captured with the step
                 x = x.permute(0, 3, 1, 2) if amp else x.contiguous(memory_format=torch.channels_last)
+            if amp and args.cast == 'fused' and args.head == 'fused':
+                # pool -> conv -> sigmoid -> BCE in 2 + 2 gfx950 launches (ops.disc_head_bce)
+                return m.bce_loss_bf16(x.to(torch.bfloat16), 1.0)
             if amp and args.cast == 'fused':
                 out = m.forward_bf16(x.to(torch.bfloat16)).float()   # one cast launch per direction
             elif amp:
@@ -525,6 +531,7 @@ def main(argv=None):
                 'cast': args.cast if amp else None,
                 'optim': args.optim if model is not None else None,
                 'dma_phase': args.dma_phase if model is not None else None,
+                'head': args.head if model is not None else None,
                 'host_sync': args.host_sync,
                 'consumer_collectives_per_step': stepper.collectives if stepper is not None else None,
             },

@@ -1,0 +1,155 @@
+// The discriminator's head as three small kernels instead of ~20 library
+// launches: AdaptiveAvgPool2d(OH x OW) -> Conv2d(C, 1, (OH, OW)) -> sigmoid ->
+// binary cross-entropy (mean over the batch), forward and backward.
+//
+// With the pooled map exactly consumed by the last convolution, each image's
+// logit is a dot product of its feature map with the pooling-folded weight:
+//   logit_n = sum_{i,j,c} pooled[n][i][j][c] * w[c][i][j]
+//   dL/dz[n][h][w][c] = dlogit_n * sum_{(i,j) whose window holds (h,w)} w[c][i][j] / |window(i,j)|
+//   dL/dw[c][i][j] = sum_n dlogit_n * pooled[n][i][j][c],  dlogit_n = g * (sigmoid(logit_n) - y_n) / N
+// (PyTorch's BCE backward reduces to the same (p - y) / N once p(1-p) > 1e-12.)
+// Pooling, the dot products and the loss run in fp32 on bf16 features; the
+// weight and its gradient stay fp32 (no cast).  Reference head:
+// examples/densityopt/densityopt.py:139-190 (conv4x4 -> sigmoid, BCELoss).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "kernels.h"
+
+namespace btn {
+namespace gpu {
+namespace {
+
+constexpr int kHeadThreads = 256;
+
+__device__ __forceinline__ int wstart(int i, int in, int out) { return (i * in) / out; }
+__device__ __forceinline__ int wend(int i, int in, int out) { return ((i + 1) * in + out - 1) / out; }
+__device__ __forceinline__ float bf(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
+
+// one block per (pooling cell, image): pooled values of the cell and the
+// cell's share of the image's logit
+__global__ __launch_bounds__(kHeadThreads) void head_fwd_kernel(HeadParams p) {
+  __shared__ float red[kHeadThreads / 64];
+  const int cell = int(blockIdx.x), n = int(blockIdx.y);
+  const int i = cell / p.OW, j = cell - i * p.OW;
+  const int h0 = wstart(i, p.H, p.OH), h1 = wend(i, p.H, p.OH);
+  const int w0 = wstart(j, p.W, p.OW), w1 = wend(j, p.W, p.OW);
+  const float inv = 1.f / float((h1 - h0) * (w1 - w0));
+  float part = 0.f;
+  for (int c = int(threadIdx.x); c < p.C; c += kHeadThreads) {
+    float s = 0.f;
+    for (int h = h0; h < h1; ++h) {
+      const uint16_t* row = p.z + (int64_t(n * p.H + h) * p.W) * p.C + c;
+      for (int w = w0; w < w1; ++w) s += bf(row[int64_t(w) * p.C]);
+    }
+    const float pooled = s * inv;
+    p.pooled[(int64_t(n) * p.OH * p.OW + cell) * p.C + c] = pooled;
+    part += pooled * p.w[c * p.ws_c + i * p.ws_i + j * p.ws_j];
+  }
+  for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = part;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float v = 0.f;
+    for (int k = 0; k < kHeadThreads / 64; ++k) v += red[k];
+    p.partial[n * p.OH * p.OW + cell] = v;
+  }
+}
+
+// one wave: logits, sigmoid, mean BCE, and dlogit/g for the backward
+__global__ __launch_bounds__(64) void head_loss_kernel(HeadParams p) {
+  const int cells = p.OH * p.OW;
+  float total = 0.f;
+  for (int n = int(threadIdx.x); n < p.N; n += 64) {
+    float logit = 0.f;
+    for (int k = 0; k < cells; ++k) logit += p.partial[n * cells + k];
+    const float y = p.target ? p.target[n] : p.target_value;
+    const float pr = 1.f / (1.f + expf(-logit));
+    const float lp = fmaxf(logf(pr), -100.f), lq = fmaxf(logf(1.f - pr), -100.f);
+    total += -(y * lp + (1.f - y) * lq);
+    p.dlogit[n] = (pr - y) / float(p.N);
+    if (p.logit) p.logit[n] = logit;
+  }
+  for (int o = 32; o > 0; o >>= 1) total += __shfl_xor(total, o);
+  if (threadIdx.x == 0) p.loss[0] = total / float(p.N);
+}
+
+// dz: 8 channels of one pixel per lane (one 16-byte store)
+__global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p) {
+  const int groups = p.C / 8;
+  const int64_t total = int64_t(p.N) * p.H * p.W * groups;
+  const float g = p.gscale[0];
+  for (int64_t e = int64_t(blockIdx.x) * kHeadThreads + threadIdx.x; e < total;
+       e += int64_t(gridDim.x) * kHeadThreads) {
+    const int c0 = int(e % groups) * 8;
+    int64_t r = e / groups;
+    const int w = int(r % p.W);
+    r /= p.W;
+    const int h = int(r % p.H);
+    const int n = int(r / p.H);
+    const float d = g * p.dlogit[n];
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int i0 = (h * p.OH) / p.H, i1 = ((h + 1) * p.OH + p.H - 1) / p.H;
+    const int j0 = (w * p.OW) / p.W, j1 = ((w + 1) * p.OW + p.W - 1) / p.W;
+    for (int i = i0; i < i1 && i < p.OH; ++i) {
+      const int hs = wstart(i, p.H, p.OH), he = wend(i, p.H, p.OH);
+      if (h < hs || h >= he) continue;
+      for (int j = j0; j < j1 && j < p.OW; ++j) {
+        const int ws = wstart(j, p.W, p.OW), we = wend(j, p.W, p.OW);
+        if (w < ws || w >= we) continue;
+        const float inv = d / float((he - hs) * (we - ws));
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += inv * p.w[(c0 + k) * p.ws_c + i * p.ws_i + j * p.ws_j];
+      }
+    }
+    uint32_t packed[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint32_t lo = __float_as_uint(acc[2 * k]), hi = __float_as_uint(acc[2 * k + 1]);
+      lo += 0x7FFFu + ((lo >> 16) & 1u);
+      hi += 0x7FFFu + ((hi >> 16) & 1u);
+      packed[k] = (lo >> 16) | (hi & 0xFFFF0000u);
+    }
+    *reinterpret_cast<uint4*>(p.dz + ((int64_t(n * p.H + h) * p.W + w) * p.C + c0)) =
+        make_uint4(packed[0], packed[1], packed[2], packed[3]);
+  }
+}
+
+__global__ __launch_bounds__(kHeadThreads) void head_wgrad_kernel(HeadParams p) {
+  const int cells = p.OH * p.OW;
+  const int total = p.C * cells;
+  const float g = p.gscale[0];
+  for (int e = int(blockIdx.x) * kHeadThreads + int(threadIdx.x); e < total; e += int(gridDim.x) * kHeadThreads) {
+    const int c = e % p.C, cell = e / p.C;
+    float s = 0.f;
+    for (int n = 0; n < p.N; ++n) s += p.dlogit[n] * p.pooled[(int64_t(n) * cells + cell) * p.C + c];
+    const int i = cell / p.OW, j = cell - i * p.OW;
+    p.dw[c * p.ws_c + i * p.ws_i + j * p.ws_j] = g * s;
+  }
+}
+
+}  // namespace
+
+hipError_t head_forward(const HeadParams& p, hipStream_t stream) {
+  if (p.N <= 0 || p.C <= 0 || p.OH <= 0 || p.OW <= 0 || p.H < p.OH || p.W < p.OW || !p.z || !p.w || !p.pooled ||
+      !p.partial || !p.loss || !p.dlogit)
+    return hipErrorInvalidValue;
+  head_fwd_kernel<<<dim3(unsigned(p.OH * p.OW), unsigned(p.N)), kHeadThreads, 0, stream>>>(p);
+  head_loss_kernel<<<1, 64, 0, stream>>>(p);
+  return hipGetLastError();
+}
+
+hipError_t head_backward(const HeadParams& p, hipStream_t stream) {
+  if (p.C % 8 || !p.dz || !p.dw || !p.gscale || !p.dlogit || !p.pooled) return hipErrorInvalidValue;
+  if (reinterpret_cast<uintptr_t>(p.dz) & 15) return hipErrorInvalidValue;
+  const int64_t total = int64_t(p.N) * p.H * p.W * (p.C / 8);
+  const int64_t blocks = (total + kHeadThreads - 1) / kHeadThreads;
+  head_bwd_kernel<<<unsigned(blocks < 4096 ? blocks : 4096), kHeadThreads, 0, stream>>>(p);
+  const int wtotal = p.C * p.OH * p.OW;
+  head_wgrad_kernel<<<(wtotal + kHeadThreads - 1) / kHeadThreads, kHeadThreads, 0, stream>>>(p);
+  return hipGetLastError();
+}
+
+}  // namespace gpu
+}  // namespace btn

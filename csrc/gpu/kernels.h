@@ -276,6 +276,33 @@ hipError_t bn_finalize_rows(const float* partial, int nblocks, int64_t M, int C,
                             float* mean, float* invstd, float* running_mean, float* running_var, hipStream_t stream,
                             int64_t* num_batches_tracked);
 
+// Discriminator head (head.hip): AdaptiveAvgPool2d(OH, OW) -> Conv2d(C, 1,
+// (OH, OW), no bias) -> sigmoid -> mean binary cross-entropy against target
+// (per-image tensor, or target_value when target is null), forward and
+// backward in three launches each way.  z: bf16 [N][H][W][C] (channels-last);
+// w: fp32, element (c, i, j) at c*ws_c + i*ws_i + j*ws_j.  Forward writes
+// pooled [N][OH][OW][C], partial [N][OH*OW], loss [1], dlogit [N] (= (p-y)/N),
+// logit [N] (nullable).  Backward scales by gscale[0] (the loss's incoming
+// gradient, on the device) and writes dz (bf16, like z) and dw (fp32, like w).
+struct HeadParams {
+  const uint16_t* z = nullptr;
+  const float* w = nullptr;
+  int64_t ws_c = 0, ws_i = 0, ws_j = 0;
+  int N = 0, H = 0, W = 0, C = 0, OH = 0, OW = 0;
+  const float* target = nullptr;
+  float target_value = 1.f;
+  float* pooled = nullptr;
+  float* partial = nullptr;
+  float* loss = nullptr;
+  float* dlogit = nullptr;
+  float* logit = nullptr;
+  const float* gscale = nullptr;
+  uint16_t* dz = nullptr;
+  float* dw = nullptr;
+};
+hipError_t head_forward(const HeadParams& p, hipStream_t stream);
+hipError_t head_backward(const HeadParams& p, hipStream_t stream);
+
 hipError_t adam_schedule(float* step, const float* hp, float* sched, float beta1, float beta2, hipStream_t stream);
 hipError_t adam_update(const AdamParams& p, hipStream_t stream);
 

@@ -268,6 +268,39 @@ PYBIND11_MODULE(_hip, m) {
                 "bn_apply");
         });
 
+  m.def("head_forward",
+        [](uintptr_t z, uintptr_t w, int64_t ws_c, int64_t ws_i, int64_t ws_j, int N, int H, int W, int C, int OH,
+           int OW, uintptr_t target, float target_value, uintptr_t pooled, uintptr_t partial, uintptr_t loss,
+           uintptr_t dlogit, uintptr_t logit, uintptr_t stream) {
+          HeadParams p;
+          p.z = ptr<const uint16_t>(z);
+          p.w = ptr<const float>(w);
+          p.ws_c = ws_c, p.ws_i = ws_i, p.ws_j = ws_j;
+          p.N = N, p.H = H, p.W = W, p.C = C, p.OH = OH, p.OW = OW;
+          p.target = ptr<const float>(target);
+          p.target_value = target_value;
+          p.pooled = ptr<float>(pooled);
+          p.partial = ptr<float>(partial);
+          p.loss = ptr<float>(loss);
+          p.dlogit = ptr<float>(dlogit);
+          p.logit = ptr<float>(logit);
+          check(head_forward(p, stream_of(stream)), "head_forward");
+        });
+  m.def("head_backward",
+        [](uintptr_t w, int64_t ws_c, int64_t ws_i, int64_t ws_j, int N, int H, int W, int C, int OH, int OW,
+           uintptr_t pooled, uintptr_t dlogit, uintptr_t gscale, uintptr_t dz, uintptr_t dw, uintptr_t stream) {
+          HeadParams p;
+          p.w = ptr<const float>(w);
+          p.ws_c = ws_c, p.ws_i = ws_i, p.ws_j = ws_j;
+          p.N = N, p.H = H, p.W = W, p.C = C, p.OH = OH, p.OW = OW;
+          p.pooled = ptr<float>(pooled);
+          p.dlogit = ptr<float>(dlogit);
+          p.gscale = ptr<const float>(gscale);
+          p.dz = ptr<uint16_t>(dz);
+          p.dw = ptr<float>(dw);
+          check(head_backward(p, stream_of(stream)), "head_backward");
+        });
+
   m.def("adam_schedule",
         [](uintptr_t step, uintptr_t hp, uintptr_t sched, float beta1, float beta2, uintptr_t stream) {
           check(adam_schedule(ptr<float>(step), ptr<const float>(hp), ptr<float>(sched), beta1, beta2,

@@ -17,6 +17,10 @@ import torch.nn as nn
 import torch.distributions as D
 
 
+def _pair(v):
+    return tuple(v) if isinstance(v, (tuple, list)) else (v, v)
+
+
 def _weights_init(m):
     name = m.__class__.__name__
     if 'Conv' in name:
@@ -67,11 +71,38 @@ class Discriminator(nn.Module):
         (``ops.conv4x4s2``): forward, and the weight gradient in fp32 instead
         of MIOpen's bf16 path (zero-fill + atomic GEMM + cast per layer).
         ``mfma=False`` is bit-identical to autocast over :meth:`forward`."""
+        return self._run_bf16(x, list(self.features), mfma).view(-1, 1).squeeze(1)
+
+    def bce_loss_bf16(self, x, target=1.0, mfma=True):
+        """Mean binary cross-entropy of :meth:`forward_bf16`'s output against
+        ``target`` (scalar or [N]), with the adaptive head (pool -> 4x4 conv ->
+        sigmoid -> BCE) fused into ``ops.disc_head_bce`` (2 launches forward,
+        2 backward, instead of ~20 library kernels; fp32 weight and gradient).
+        Falls back to :meth:`forward_bf16` + ``BCELoss`` off that shape.
+        Returns the loss."""
         import torch.nn.functional as F
         from .. import ops
-        convs = [m for m in self.features if isinstance(m, nn.Conv2d)]
-        weights = iter(ops.cast_bf16(*[c.weight for c in convs]))
         layers = list(self.features)
+        head = layers[-3:]
+        fused = (len(head) == 3 and isinstance(head[0], ops.AdaptiveAvgPool2d) and isinstance(head[1], nn.Conv2d)
+                 and isinstance(head[2], nn.Sigmoid) and head[1].out_channels == 1 and head[1].bias is None
+                 and head[1].stride == (1, 1) and head[1].padding == (0, 0)
+                 and tuple(head[1].kernel_size) == _pair(head[0].output_size))
+        if not fused:
+            out = self.forward_bf16(x, mfma).float()
+            tgt = target if isinstance(target, torch.Tensor) else torch.full_like(out, float(target))
+            return F.binary_cross_entropy(out, tgt)
+        z = self._run_bf16(x, layers[:-3], mfma)
+        if not (z.is_cuda and z.is_contiguous(memory_format=torch.channels_last)):
+            z = z.contiguous(memory_format=torch.channels_last)
+        loss, _ = ops.disc_head_bce(z, head[1].weight, target, _pair(head[0].output_size))
+        return loss
+
+    def _run_bf16(self, x, layers, mfma):
+        import torch.nn.functional as F
+        from .. import ops
+        convs = [m for m in layers if isinstance(m, nn.Conv2d)]
+        weights = iter(ops.cast_bf16(*[c.weight for c in convs]))
         stats = None
         for i, m in enumerate(layers):
             if isinstance(m, nn.Conv2d):
@@ -92,7 +123,7 @@ class Discriminator(nn.Module):
                 stats = None
             else:
                 x = m(x)
-        return x.view(-1, 1).squeeze(1)
+        return x
 
 
 class ProbModel(nn.Module):

@@ -960,6 +960,78 @@ def conv4x4s2(x, w32, w16, with_stats=False):
     return _CONV_FN.apply(x, w32, w16.detach(), with_stats)
 
 
+# ---------------------------------------------------------------------------
+# consumer-model op: the discriminator head (pool -> conv -> sigmoid -> BCE)
+# in 2 + 2 launches (csrc/gpu/head.hip)
+
+def _head_function():
+    import torch
+
+    class _DiscHeadBCE(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, z, w, target, oh, ow):
+            ext = hip_ext()
+            N, C, H, W = z.shape
+            dev = z.device
+            pooled = torch.empty(N * oh * ow * C, dtype=torch.float32, device=dev)
+            partial = torch.empty(N * oh * ow, dtype=torch.float32, device=dev)
+            loss = torch.empty((), dtype=torch.float32, device=dev)
+            dlogit = torch.empty(N, dtype=torch.float32, device=dev)
+            logit = torch.empty(N, dtype=torch.float32, device=dev)
+            tptr, tval = 0, 1.0
+            if isinstance(target, torch.Tensor):
+                target = target.to(device=dev, dtype=torch.float32).contiguous()
+                tptr = target.data_ptr()
+            else:
+                tval = float(target)
+            _count('head_forward')
+            ext.head_forward(z.data_ptr(), w.data_ptr(), w.stride(1), w.stride(2), w.stride(3), N, H, W, C, oh, ow,
+                             tptr, tval, pooled.data_ptr(), partial.data_ptr(), loss.data_ptr(), dlogit.data_ptr(),
+                             logit.data_ptr(), _stream(dev))
+            ctx.save_for_backward(w, pooled, dlogit)
+            ctx.zshape, ctx.pool = (N, C, H, W), (oh, ow)
+            ctx.mark_non_differentiable(logit)
+            return loss, logit
+
+        @staticmethod
+        def backward(ctx, gloss, glogit=None):
+            ext = hip_ext()
+            w, pooled, dlogit = ctx.saved_tensors
+            N, C, H, W = ctx.zshape
+            oh, ow = ctx.pool
+            g = gloss.to(torch.float32).reshape(1).contiguous()
+            dz = torch.empty((N, C, H, W), dtype=torch.bfloat16, device=w.device, memory_format=torch.channels_last)
+            dw = torch.empty_like(w)
+            _count('head_backward')
+            ext.head_backward(w.data_ptr(), w.stride(1), w.stride(2), w.stride(3), N, H, W, C, oh, ow,
+                              pooled.data_ptr(), dlogit.data_ptr(), g.data_ptr(), dz.data_ptr(), dw.data_ptr(),
+                              _stream(w.device))
+            return dz, dw, None, None, None
+
+    return _DiscHeadBCE
+
+
+_HEAD_FN = None
+
+
+def disc_head_bce(z, w, target=1.0, pool=(4, 4)):
+    """``BCELoss()(sigmoid(conv2d(adaptive_avg_pool2d(z, pool), w)).view(-1), target)``
+    for a head conv that consumes the whole pooled map (``w``: fp32
+    [1, C, pool_h, pool_w]); ``z`` bf16 channels-last [N, C, H, W] on the GPU.
+    Returns ``(loss, logits)``; gradients flow to ``z`` (bf16) and ``w``
+    (fp32).  Pool, dot products and loss run in fp32."""
+    import torch
+    global _HEAD_FN
+    if _HEAD_FN is None:
+        _HEAD_FN = _head_function()
+    oh, ow = pool
+    if not (z.is_cuda and z.dtype == torch.bfloat16 and z.is_contiguous(memory_format=torch.channels_last)):
+        raise ValueError('disc_head_bce needs bf16 channels-last GPU features')
+    if tuple(w.shape) != (1, z.shape[1], oh, ow) or w.dtype != torch.float32 or z.shape[1] % 8:
+        raise ValueError(f'disc_head_bce: weight {tuple(w.shape)} {w.dtype} does not fit features {tuple(z.shape)}')
+    return _HEAD_FN.apply(z, w, target, oh, ow)
+
+
 def __getattr__(name):
     # built on first use so importing ``blendtorch.ops`` does not import torch
     global _POOL_MODULE, _BN_MODULE

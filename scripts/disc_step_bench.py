@@ -26,7 +26,7 @@ VARIANTS = {
 
 
 def run(name, iters, batch, graph, fused_adam=False, fused_bn=True, dma=0, cast='autocast', u8=False, optim='torch',
-        dma_phase='none', split=False):
+        dma_phase='none', split=False, head='torch'):
     dt, fmt = VARIANTS[name]
     dev = torch.device('cuda', 0)
     torch.manual_seed(0)
@@ -58,6 +58,10 @@ def run(name, iters, batch, graph, fused_adam=False, fused_bn=True, dma=0, cast=
     def step():
         opt.zero_grad(set_to_none=True)
         xi = inputs()
+        if amp and cast == 'fused' and head == 'fused':
+            model.bce_loss_bf16(xi, 1.0).backward()
+            opt.step()
+            return
         if amp and cast == 'fused':
             out = model.forward_bf16(xi)
         else:
@@ -137,7 +141,7 @@ def run(name, iters, batch, graph, fused_adam=False, fused_bn=True, dma=0, cast=
     ms = (time.perf_counter() - t0) / iters * 1000
     copy_ms = host_copy_s[0] / iters * 1000
     return {'variant': name, 'graph': graph, 'fused_adam': fused_adam, 'fused_bn': fused_bn, 'dma_streams': dma,
-            'cast': cast, 'u8_input': u8, 'optim': optim, 'dma_phase': dma_phase if dma else None, 'split': split,
+            'cast': cast, 'u8_input': u8, 'optim': optim, 'head': head, 'dma_phase': dma_phase if dma else None, 'split': split,
             'ms_per_step': round(ms, 4), 'images_per_s': round(batch / ms * 1000, 1),
             'host_ms_issuing_copies': round(copy_ms, 4)}
 
@@ -157,6 +161,7 @@ def main():
     ap.add_argument('--cast', choices=['autocast', 'fused'], default='autocast',
                     help='fused = Discriminator.forward_bf16 (one weight-cast launch per direction)')
     ap.add_argument('--optim', choices=['torch', 'gfx950'], default='torch')
+    ap.add_argument('--head', choices=['torch', 'fused'], default='torch')
     ap.add_argument('--dma-phase', choices=['none', 'record', 'start', 'start_prev', 'mid'], default='none')
     ap.add_argument('--split', action='store_true', help='forward and backward as two graphs (CapturedStep split)')
     ap.add_argument('--u8', action='store_true', help='train on raw u8 RGBA frames decoded inside the step')
@@ -169,7 +174,7 @@ def main():
     for n in names:
         for g in graphs:
             r = run(n, args.iters, args.batch, g, args.fused_adam, args.fused_bn, args.dma, args.cast, args.u8, args.optim,
-                    args.dma_phase, args.split or args.dma_phase == 'mid')
+                    args.dma_phase, args.split or args.dma_phase == 'mid', args.head)
             r['cpu_load'] = args.cpu_load
             print(json.dumps(r), flush=True)
     for h in hogs:

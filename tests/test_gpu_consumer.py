@@ -112,3 +112,51 @@ def test_split_graph_discriminator_step(dev):
     for pa, pb in _split_vs_single(dev, make, loss_fn, xs, lr):
         d = (pb - pa).detach().abs()
         assert float(d.mean()) < 0.1 * lr and float((d > 0.5 * lr).float().mean()) < 0.02
+
+
+@pytest.mark.parametrize('target', ['ones', 'mixed'])
+@pytest.mark.parametrize('wlayout', ['contiguous', 'channels_last'])
+def test_disc_head_bce_matches_fp32_reference(dev, target, wlayout):
+    import torch.nn.functional as F
+    g = torch.Generator(device=dev).manual_seed(11)
+    z = (0.5 * torch.randn(8, 256, 30, 40, device=dev, generator=g)).to(torch.bfloat16)
+    z = z.contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    w = 0.02 * torch.randn(1, 256, 4, 4, device=dev, generator=g)
+    if wlayout == 'channels_last':
+        w = w.contiguous(memory_format=torch.channels_last)
+    w.requires_grad_(True)
+    y = torch.ones(8, device=dev) if target == 'ones' else torch.tensor([1., 0., 1., 1., 0., 0., 1., 0.], device=dev)
+    before = ops.KERNEL_CALLS.get('head_forward', 0)
+    loss, logits = ops.disc_head_bce(z, w, 1.0 if target == 'ones' else y)
+    loss.backward()
+    assert ops.KERNEL_CALLS['head_forward'] == before + 1
+    zr = z.detach().float().requires_grad_(True)
+    wr = w.detach().clone().requires_grad_(True)
+    out = torch.sigmoid(F.conv2d(F.adaptive_avg_pool2d(zr, 4), wr)).view(-1)
+    ref = F.binary_cross_entropy(out, y)
+    ref.backward()
+    torch.testing.assert_close(loss, ref, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(torch.sigmoid(logits), out.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(w.grad, wr.grad, rtol=1e-4, atol=1e-7)
+    assert z.grad.dtype == torch.bfloat16 and z.grad.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(z.grad.float(), zr.grad, rtol=2 ** -7, atol=1e-3 * float(zr.grad.abs().max()))
+
+
+def test_discriminator_bce_loss_bf16(dev):
+    """The fused-head loss of the whole discriminator equals the unfused
+    bf16 forward + BCELoss, and trains the same parameters."""
+    from blendtorch.models import Discriminator
+    torch.manual_seed(0)
+    a = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=torch.channels_last)
+    b = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=torch.channels_last)
+    b.load_state_dict(a.state_dict())
+    x = torch.rand(4, 3, 120, 160, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    la = a.bce_loss_bf16(x, 1.0)
+    out = b.forward_bf16(x).float()
+    lb = torch.nn.functional.binary_cross_entropy(out, torch.ones_like(out))
+    torch.testing.assert_close(la, lb, rtol=2e-2, atol=1e-4)   # the head pools/dots in fp32, the library in bf16
+    la.backward()
+    lb.backward()
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        ga, gb = pa.grad.flatten().double(), pb.grad.flatten().double()
+        assert float(ga @ gb / (ga.norm() * gb.norm())) > 0.98, n
