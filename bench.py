@@ -287,9 +287,12 @@ def main(argv=None):
     # decode inside the consumer's captured step (frames arrive by DMA only)
     step_decode = (args.consumer == 'disc' and args.h2d == 'copy' and args.dist != 'scatter'
                    and args.step_decode == 'on')
+    # RGBA frames decoded to 4-channel bf16: the first conv's MFMA kernel reads
+    # 8-byte pixels and ignores alpha (weight 0) -- cheaper than a 3-channel layout
+    rgba_in = amp and args.cast == 'fused' and args.mode == 'rgba'
     if amp:
         # the decode kernel writes what the model's first conv reads: bf16, channels-last
-        decode = DecodeConfig.unit(channels='rgb', gamma=2.2, dtype='bfloat16', layout='nhwc')
+        decode = DecodeConfig.unit(channels='rgba' if rgba_in else 'rgb', gamma=2.2, dtype='bfloat16', layout='nhwc')
     launch = dict(producer='cubesim', num_instances=nprod, named_sockets=['DATA'], start_port=start_port,
                   proto=args.proto, seed=1000 * rank, cpu_affinity=affinity,
                   instance_args=[['--mode', args.mode, '--sndhwm', '10', '--resolution', f'{res_w}x{res_h}'] + (['--shm', str(shm_slots), '--codec', args.codec] if shm_slots else [])]

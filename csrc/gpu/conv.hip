@@ -108,6 +108,12 @@ __device__ __forceinline__ bf16x8 frag_at(const char* img, int off, int row4) {
   return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint2 bload8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, int(off), 0, 0);
+  return make_uint2(v[0], v[1]);
+}
+
 struct PixelCursor {   // (n, oh, ow) of pixel m, advanced by BPX per k-step
   int n, oh, ow;
   __device__ void init(int m, int Ho, int Wo) {
@@ -251,6 +257,112 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p)
       }
 }
 
+// ---------------------------------------------------------------------------
+// Weight gradient of the FIRST layer: 4-channel input (RGB frames decoded as
+// RGBA bf16; the alpha channel's gradient is computed and discarded), Cout %
+// 32 == 0.  KC = 16 taps x 4 channels = 64, one 32 x 64 tile per block and
+// pixel slice.  A 16-byte chunk of an im2col row is two horizontally
+// adjacent input pixels (taps kw, kw+1) -- 8-byte aligned only, and at the
+// left / right image border half of it is padding -- so it is two bounds-
+// checked 8-byte buffer loads.  LDS images: dY [32 px][32 co] (64-byte rows),
+// X [32 px][64 kc] (128-byte rows), both read by ds_read_b64_tr_b16.
+constexpr int C4_DY_ROW = 64, C4_X_ROW = 128;
+constexpr int C4_DY_TILE = BPX * C4_DY_ROW, C4_X_TILE = BPX * C4_X_ROW;
+constexpr int C4_STAGE = C4_DY_TILE + C4_X_TILE;
+
+// 64-byte rows: 4 rows per bank row; the row pair 8 apart (same bank window
+// otherwise) flips its 32-byte half
+__device__ __forceinline__ int c4dy_off(int r, int byte) {
+  return r * C4_DY_ROW + ((((byte >> 5) ^ ((r >> 3) & 1)) << 5) | (byte & 31));
+}
+// 128-byte rows: the dY scheme of the main kernel
+__device__ __forceinline__ int c4x_off(int r, int byte) { return dy_off(r, byte); }
+
+__global__ __launch_bounds__(kThreads) void conv_wgrad_c4_kernel(ConvWgradParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * C4_STAGE];
+  const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
+  const int T = p.Cout / 32;
+  const int nwg = int(gridDim.x), b = int(blockIdx.x);
+  const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  const int slice = w / T, co0 = (w - slice * T) * 32;
+  const int m_begin = slice * int(p.px_per_slice);
+  const int m_end = m_begin + int(p.px_per_slice) < int(p.M) ? m_begin + int(p.px_per_slice) : int(p.M);
+  const int nsteps = m_end > m_begin ? (m_end - m_begin + BPX - 1) / BPX : 0;
+
+  const int dpx = (t & 127) >> 2, dch = t & 3;          // dY: threads < 128, 4 chunks per pixel row
+  const bool dy_loader = t < 128;
+  const int xpx = t >> 3, xch = t & 7;                  // X: one 2-pixel chunk per thread
+  const int kh = xch >> 1, kw = (xch & 1) * 2;
+  PixelCursor c;
+  c.init(m_begin + xpx, p.Ho, p.Wo);
+  const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(p.x, int64_t(p.N) * p.H * p.W * 4 * 2);
+  const __amdgpu_buffer_rsrc_t rs_dy = make_rsrc(p.dy, p.M * p.Cout * 2);
+  constexpr int kDepth = 4;
+  struct Stage {
+    uint4 dy;
+    uint2 x0, x1;
+  };
+  Stage ring[kDepth];
+  int md = m_begin + dpx, mx = m_begin + xpx;
+  uint32_t dy_byte = uint32_t(md) * uint32_t(p.Cout * 2) + uint32_t((co0 + dch * 8) * 2);
+  const uint32_t dy_step = uint32_t(BPX * p.Cout * 2);
+  auto load = [&](Stage& r) {
+    r.dy = bload(rs_dy, dy_loader && md < m_end ? dy_byte : kOOB);
+    const int ih = 2 * c.oh - 1 + kh, iw = 2 * c.ow - 1 + kw;
+    const bool row_ok = mx < m_end && unsigned(ih) < unsigned(p.H);
+    const int e = ((c.n * p.H + ih) * p.W + iw) * 4;
+    r.x0 = bload8(rs_x, row_ok && unsigned(iw) < unsigned(p.W) ? uint32_t(e) * 2u : kOOB);
+    r.x1 = bload8(rs_x, row_ok && unsigned(iw + 1) < unsigned(p.W) ? uint32_t(e + 4) * 2u : kOOB);
+    md += BPX;
+    mx += BPX;
+    dy_byte += dy_step;
+    c.advance(p.Ho, p.Wo);
+  };
+  const int st_dy = c4dy_off(dpx, dch * 16), st_x = C4_DY_TILE + c4x_off(xpx, xch * 16);
+  auto store = [&](const Stage& r, int buf) {
+    char* base = smem + buf * C4_STAGE;
+    if (dy_loader) *reinterpret_cast<uint4*>(base + st_dy) = r.dy;
+    *reinterpret_cast<uint4*>(base + st_x) = make_uint4(r.x0.x, r.x0.y, r.x1.x, r.x1.y);
+  };
+  // wave: co fragment wave / 2, kc fragments 2 (wave % 2) + {0, 1}
+  const int fco = (wave >> 1) * 16, fkc = (wave & 1) * 32;
+  int ra, rb[2];
+  {
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+    ra = c4dy_off(8 * g + q, (fco + 4 * pp) * 2);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) rb[j] = C4_DY_TILE + c4x_off(8 * g + q, (fkc + 16 * j + 4 * pp) * 2);
+  }
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int u = 0; u < kDepth; ++u) load(ring[u]);
+  const int padded = (nsteps + kDepth - 1) / kDepth * kDepth;
+  for (int s0 = 0; s0 < padded; s0 += kDepth) {
+#pragma unroll
+    for (int u = 0; u < kDepth; ++u) {
+      const int buf = u & 1;
+      store(ring[u], buf);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      load(ring[u]);
+      const char* base = smem + buf * C4_STAGE;
+      const bf16x8 a = frag_at(base, ra, 4 * C4_DY_ROW);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, frag_at(base, rb[j], 4 * C4_X_ROW), acc[j], 0, 0, 0);
+    }
+  }
+  float* out = p.partial + int64_t(slice) * p.Cout * 64;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = co0 + fco + 4 * (lane >> 4) + r;
+      out[co * 64 + fkc + 16 * j + (lane & 15)] = acc[j][r];
+    }
+}
+
 // Sum the S slices into fp32 dW[co][kh][kw][ci] at the parameter's strides.
 // blockIdx.y takes a group of kSliceGroup slices and each lane four
 // consecutive elements (one 16-byte load per slice, all of a group's loads
@@ -260,7 +372,8 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p)
 constexpr int kSliceGroup = 8;
 
 __global__ __launch_bounds__(kThreads) void conv_wgrad_reduce_kernel(const float* __restrict__ partial, int S,
-                                                                     int Cout, int Cin, float* __restrict__ out,
+                                                                     int Cout, int Cin, int cin_out,
+                                                                     float* __restrict__ out,
                                                                      int64_t s_co, int64_t s_ci, int64_t s_kh,
                                                                      int64_t s_kw) {
   const int KC = 16 * Cin;
@@ -283,6 +396,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_reduce_kernel(const float
     const int e = e0 + j;
     const int co = e / KC, kc = e - co * KC;
     const int tap = kc / Cin, ci = kc - tap * Cin;
+    if (ci >= cin_out) continue;   // padded input channel (4-channel first layer)
     float* dst = out + co * s_co + ci * s_ci + (tap >> 2) * s_kh + (tap & 3) * s_kw;
     if (single) *dst = vals[j];
     else atomicAdd(dst, vals[j]);
@@ -332,11 +446,12 @@ struct TapGemm {
   int N = 0, SH = 0, SW = 0, C = 0, cshift = 0;   // src [N][SH][SW][C], C = 1 << cshift
   int GH = 0, GW = 0, M = 0;       // GEMM rows: m = (n * GH + a) * GW + b
   int NOUT = 0, OH = 0, OW = 0;    // dst [N][OH][OW][NOUT]
+  int wc = 0;                      // C4 mode: weight input channels (3 or 4)
 };
 
 // BN = output channels per block (64, or 32 for 32-channel outputs such as
 // the first layer's data gradient); 4 waves as WGM (pixels) x WGN (channels).
-template <bool DGRAD, int BN>
+template <bool DGRAD, int BN, bool C4 = false>
 __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   constexpr int WGM = BN == 64 ? 2 : 4, WGN = 4 / WGM;
   constexpr int FM = FBM / WGM / 16, FN = BN / WGN / 16;   // 16x16 fragments per wave
@@ -344,7 +459,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   float* red = reinterpret_cast<float*>(smem + 2 * F_STAGE);   // [WGM][2][BN]
   const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
   constexpr int NTAPS = DGRAD ? 4 : 16;
-  const int K = NTAPS * p.C, NT = p.NOUT / BN;
+  const int K = C4 ? FBK : NTAPS * p.C, NT = p.NOUT / BN;
   const int ph = DGRAD ? int(blockIdx.y) >> 1 : 0, pw = DGRAD ? int(blockIdx.y) & 1 : 0;
 
   const int nwg = int(gridDim.x), b = int(blockIdx.x);
@@ -373,7 +488,34 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   const uint16_t* wrow0 = p.w + (n0 + ar) * (16 * p.C);
   const uint16_t* wrow1 = p.w + (n0 + (BN == 64 ? ar + 32 : ar)) * (16 * p.C);
   uint4 ra[4], rb0, rb1;
+  auto load_c4 = [&]() {
+    // first layer, 4-channel input: K = 16 taps x 4 = one k-step; chunk ac is
+    // taps (kh, kw) and (kh, kw + 1) of one row -- two adjacent input pixels,
+    // each checked against the border on its own
+    const int kh = ac >> 1, kw = (ac & 1) * 2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool rok = pin[j] && unsigned(rb[j] + kh) < unsigned(p.SH);
+      const int e = (base[j] + kh * p.SW + kw) * 4;
+      const uint2 lo = bload8(rs_src, rok && unsigned(cb[j] + kw) < unsigned(p.SW) ? uint32_t(e) * 2u : kOOB);
+      const uint2 hi = bload8(rs_src, rok && unsigned(cb[j] + kw + 1) < unsigned(p.SW) ? uint32_t(e + 4) * 2u : kOOB);
+      ra[j] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+    }
+    // weights: 4 input channels, or 3 (an RGB model fed RGBA: channel 3 gets weight 0)
+    const int tap = kh * 4 + kw;
+    if (p.wc == 4) {
+      rb0 = *reinterpret_cast<const uint4*>(p.w + ((n0 + ar) * 16 + tap) * 4);
+    } else {
+      const uint16_t* q = p.w + ((n0 + ar) * 16 + tap) * 3;
+      rb0 = make_uint4(uint32_t(q[0]) | (uint32_t(q[1]) << 16), uint32_t(q[2]),
+                       uint32_t(q[3]) | (uint32_t(q[4]) << 16), uint32_t(q[5]));
+    }
+  };
   auto load = [&](int ks) {
+    if constexpr (C4) {
+      load_c4();
+      return;
+    }
     const int kc = ks * FBK + ac * 8;
     const int tap = kc >> p.cshift, ch = kc & (p.C - 1);
     int dr, dc, wtap;
@@ -517,11 +659,13 @@ __global__ __launch_bounds__(kThreads) void weight_t_kernel(const uint16_t* __re
 
 }  // namespace
 
-bool conv_wgrad_supported(int Cin, int Cout) { return Cin >= 32 && Cin % 32 == 0 && Cout >= 64 && Cout % 64 == 0; }
+bool conv_wgrad_supported(int Cin, int Cout) {
+  return (Cin >= 32 && Cin % 32 == 0 && Cout >= 64 && Cout % 64 == 0) || (Cin == 4 && Cout % 32 == 0 && Cout > 0);
+}
 
 int conv_wgrad_slices(int64_t M, int Cin, int Cout, int target_blocks) {
   if (!conv_wgrad_supported(Cin, Cout) || M <= 0) return 0;
-  const int64_t tiles = int64_t(Cout / BCO) * (16 * Cin / BKC);
+  const int64_t tiles = Cin == 4 ? Cout / 32 : int64_t(Cout / BCO) * (16 * Cin / BKC);
   int64_t s = (target_blocks + tiles - 1) / tiles;
   const int64_t max_s = (M + BPX - 1) / BPX;
   s = s < 1 ? 1 : (s > max_s ? max_s : s);
@@ -530,7 +674,8 @@ int conv_wgrad_slices(int64_t M, int Cin, int Cout, int target_blocks) {
 
 hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_t s_ci, int64_t s_kh, int64_t s_kw,
                       hipStream_t stream) {
-  if (!conv_wgrad_supported(p.Cin, p.Cout) || p.slices <= 0 || !p.x || !p.dy || !p.partial || !out)
+  if (!conv_wgrad_supported(p.Cin, p.Cout) || p.slices <= 0 || !p.x || !p.dy || !p.partial || !out ||
+      p.cin_out < 0 || p.cin_out > p.Cin)
     return hipErrorInvalidValue;
   if (p.Ho != (p.H + 2 - 4) / 2 + 1 || p.Wo != (p.W + 2 - 4) / 2 + 1 || p.M != int64_t(p.N) * p.Ho * p.Wo)
     return hipErrorInvalidValue;   // 4x4 / stride 2 / pad 1 only
@@ -539,19 +684,23 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
   if ((reinterpret_cast<uintptr_t>(p.x) | reinterpret_cast<uintptr_t>(p.dy)) & 15) return hipErrorInvalidValue;
   if (int64_t(p.N) * p.H * p.W * p.Cin * 2 >= int64_t(kOOB) || p.M * p.Cout * 2 >= int64_t(kOOB))
     return hipErrorInvalidValue;   // 32-bit buffer offsets
-  const int64_t tiles = int64_t(p.Cout / BCO) * (16 * p.Cin / BKC);
+  const bool c4 = p.Cin == 4;
+  const int64_t tiles = c4 ? p.Cout / 32 : int64_t(p.Cout / BCO) * (16 * p.Cin / BKC);
   const int64_t blocks = tiles * p.slices;
   if (blocks > (int64_t(1) << 31) - 1) return hipErrorInvalidValue;
-  conv_wgrad_kernel<<<unsigned(blocks), kThreads, 0, stream>>>(p);
-  const int64_t total = int64_t(p.Cout) * 16 * p.Cin;   // multiple of 4 * kThreads? not needed: lanes past it return
+  if (c4) conv_wgrad_c4_kernel<<<unsigned(blocks), kThreads, 0, stream>>>(p);
+  else conv_wgrad_kernel<<<unsigned(blocks), kThreads, 0, stream>>>(p);
+  const int64_t total = int64_t(p.Cout) * 16 * p.Cin;   // partial elements per slice
+  const int cin_out = p.cin_out > 0 ? p.cin_out : p.Cin;
   if (p.slices > kSliceGroup) {
     // groups add atomically: start from zero (out is dense: contiguous or channels-last)
-    const hipError_t e = hipMemsetAsync(out, 0, size_t(total) * sizeof(float), stream);
+    const hipError_t e = hipMemsetAsync(out, 0, size_t(p.Cout) * 16 * size_t(cin_out) * sizeof(float), stream);
     if (e != hipSuccess) return e;
   }
   const dim3 rgrid(unsigned((total / 4 + kThreads - 1) / kThreads), unsigned((p.slices + kSliceGroup - 1) / kSliceGroup));
-  conv_wgrad_reduce_kernel<<<rgrid, kThreads, 0, stream>>>(p.partial, p.slices, p.Cout, p.Cin, out, s_co, s_ci,
-                                                           s_kh, s_kw);
+  conv_wgrad_reduce_kernel<<<rgrid, kThreads, 0, stream>>>(p.partial, p.slices, p.Cout, p.Cin,
+                                                           p.cin_out > 0 ? p.cin_out : p.Cin, out, s_co, s_ci, s_kh,
+                                                           s_kw);
   return hipGetLastError();
 }
 
@@ -564,7 +713,7 @@ int ilog2_exact(int v) {
 }  // namespace
 
 bool conv_fwd_supported(int Cin, int Cout) {
-  return Cin >= 8 && ilog2_exact(Cin) >= 0 && (16 * Cin) % FBK == 0 && Cout % 32 == 0;
+  return (Cin == 4 || (Cin >= 8 && ilog2_exact(Cin) >= 0 && (16 * Cin) % FBK == 0)) && Cout % 32 == 0;
 }
 
 bool conv_dgrad_supported(int Cin, int Cout) {
@@ -576,8 +725,15 @@ template <bool DGRAD>
 void launch_tap_gemm(const TapGemm& g, unsigned ytiles, hipStream_t stream) {
   const bool wide = g.NOUT % 64 == 0;
   const int64_t blocks = conv_fwd_tiles(g.M) * (g.NOUT / (wide ? 64 : 32));
-  if (wide) tap_gemm_kernel<DGRAD, 64><<<dim3(unsigned(blocks), ytiles), kThreads, 0, stream>>>(g);
-  else tap_gemm_kernel<DGRAD, 32><<<dim3(unsigned(blocks), ytiles), kThreads, 0, stream>>>(g);
+  const dim3 grid(unsigned(blocks), ytiles);
+  if (!DGRAD && g.C == 4) {
+    if (wide) tap_gemm_kernel<false, 64, true><<<grid, kThreads, 0, stream>>>(g);
+    else tap_gemm_kernel<false, 32, true><<<grid, kThreads, 0, stream>>>(g);
+  } else if (wide) {
+    tap_gemm_kernel<DGRAD, 64><<<grid, kThreads, 0, stream>>>(g);
+  } else {
+    tap_gemm_kernel<DGRAD, 32><<<grid, kThreads, 0, stream>>>(g);
+  }
 }
 }  // namespace
 
@@ -596,6 +752,8 @@ hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream) {
   g.N = p.N, g.SH = p.H, g.SW = p.W, g.C = p.Cin, g.cshift = ilog2_exact(p.Cin);
   g.GH = p.Ho, g.GW = p.Wo, g.M = int(p.M);
   g.NOUT = p.Cout, g.OH = p.Ho, g.OW = p.Wo;
+  g.wc = p.Cin == 4 ? (p.w_channels > 0 ? p.w_channels : 4) : p.Cin;
+  if (p.Cin == 4 && g.wc != 3 && g.wc != 4) return hipErrorInvalidValue;
   launch_tap_gemm<false>(g, 1, stream);
   return hipGetLastError();
 }

@@ -241,7 +241,9 @@ struct ConvWgradParams {
   int64_t M = 0;
   int slices = 0;
   int64_t px_per_slice = 0;
+  int cin_out = 0;   // dW input channels written (0: Cin); 3 for a 4-channel (RGBA-fed) first layer
 };
+// Cin % 32 == 0 with Cout % 64 == 0, or Cin == 4 (the first layer) with Cout % 32 == 0.
 bool conv_wgrad_supported(int Cin, int Cout);
 int conv_wgrad_slices(int64_t M, int Cin, int Cout, int target_blocks);
 hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_t s_ci, int64_t s_kh, int64_t s_kw,
@@ -259,7 +261,9 @@ struct ConvFwdParams {
   float* stats = nullptr;
   int N = 0, H = 0, W = 0, Cin = 0, Ho = 0, Wo = 0, Cout = 0;
   int64_t M = 0;
+  int w_channels = 0;   // Cin == 4 (first layer): 3 = an RGB weight [Cout][4][4][3], input channel 3 ignored
 };
+// Cin a power of two >= 8, or Cin == 4 (first layer, RGBA-decoded frames); Cout % 32 == 0.
 bool conv_fwd_supported(int Cin, int Cout);
 int64_t conv_fwd_tiles(int64_t M);
 hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream);

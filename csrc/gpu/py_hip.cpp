@@ -219,8 +219,9 @@ PYBIND11_MODULE(_hip, m) {
   m.def("conv_wgrad",
         [](uintptr_t x, uintptr_t dy, uintptr_t partial, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
            int slices, int64_t px_per_slice, uintptr_t out, int64_t s_co, int64_t s_ci, int64_t s_kh, int64_t s_kw,
-           uintptr_t stream) {
+           uintptr_t stream, int cin_out) {
           ConvWgradParams p;
+          p.cin_out = cin_out;
           p.x = ptr<const uint16_t>(x);
           p.dy = ptr<const uint16_t>(dy);
           p.partial = ptr<float>(partial);
@@ -229,7 +230,10 @@ PYBIND11_MODULE(_hip, m) {
           p.slices = slices;
           p.px_per_slice = px_per_slice;
           check(conv_wgrad(p, ptr<float>(out), s_co, s_ci, s_kh, s_kw, stream_of(stream)), "conv_wgrad");
-        });
+        },
+        py::arg("x"), py::arg("dy"), py::arg("partial"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("Cin"),
+        py::arg("Ho"), py::arg("Wo"), py::arg("Cout"), py::arg("slices"), py::arg("px_per_slice"), py::arg("out"),
+        py::arg("s_co"), py::arg("s_ci"), py::arg("s_kh"), py::arg("s_kw"), py::arg("stream"), py::arg("cin_out") = 0);
 
   m.def("conv_fwd_tiles", &conv_fwd_tiles);
   m.def("conv_dgrad_supported", &conv_dgrad_supported);
@@ -244,8 +248,9 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("conv_fwd",
         [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, int N, int H, int W, int Cin, int Ho, int Wo,
-           int Cout, uintptr_t stream) {
+           int Cout, uintptr_t stream, int w_channels) {
           ConvFwdParams p;
+          p.w_channels = w_channels;
           p.x = ptr<const uint16_t>(x);
           p.w = ptr<const uint16_t>(w);
           p.y = ptr<uint16_t>(y);
@@ -253,7 +258,9 @@ PYBIND11_MODULE(_hip, m) {
           p.N = N, p.H = H, p.W = W, p.Cin = Cin, p.Ho = Ho, p.Wo = Wo, p.Cout = Cout;
           p.M = int64_t(N) * Ho * Wo;
           check(conv_fwd(p, stream_of(stream)), "conv_fwd");
-        });
+        },
+        py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"), py::arg("N"), py::arg("H"), py::arg("W"),
+        py::arg("Cin"), py::arg("Ho"), py::arg("Wo"), py::arg("Cout"), py::arg("stream"), py::arg("w_channels") = 0);
   // BatchNorm+LeakyReLU forward from conv_fwd's per-tile statistics: finalize + apply
   m.def("bn_forward_from_stats",
         [](uintptr_t x, uintptr_t y, int64_t M, int C, int dtype, uintptr_t stats, int nrows, float eps,

@@ -60,7 +60,9 @@ class Discriminator(nn.Module):
         return self.features(x).view(-1, 1).squeeze(1)
 
     def forward_bf16(self, x, mfma=True):
-        """bf16 forward without autocast: ONE kernel casts every conv weight
+        """bf16 forward without autocast.  ``x`` may carry a 4th (alpha)
+        channel that the first convolution ignores (RGBA-decoded frames feed
+        its MFMA kernel directly; ``mfma`` only).  ONE kernel casts every conv weight
         to bf16 (and one casts their gradients back to fp32 in backward)
         instead of a cast per layer each way; numerically the same as
         ``autocast(bfloat16)`` over :meth:`forward` (RNE weight casts, bf16

@@ -803,8 +803,10 @@ def conv_wgrad_supported(x, weight):
     if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and weight.dim() == 4):
         return False
     cout, cin, kh, kw = weight.shape
-    return (kh, kw) == (4, 4) and x.shape[1] == cin and cin % 32 == 0 and cout % 64 == 0 and \
-        x.is_contiguous(memory_format=torch.channels_last)
+    xc = x.shape[1]
+    big = xc == cin and cin % 32 == 0 and cout % 64 == 0
+    first = xc == 4 and cin in (3, 4) and cout % 32 == 0     # RGBA-fed first layer
+    return (kh, kw) == (4, 4) and (big or first) and x.is_contiguous(memory_format=torch.channels_last)
 
 
 def conv_wgrad(x, dy, out, target_blocks=512):
@@ -816,7 +818,8 @@ def conv_wgrad(x, dy, out, target_blocks=512):
     ext = hip_ext()
     N, Cin, H, W = x.shape
     Cout, Ho, Wo = dy.shape[1], dy.shape[2], dy.shape[3]
-    if dy.shape[0] != N or tuple(out.shape) != (Cout, Cin, 4, 4) or out.dtype != torch.float32:
+    cin_out = out.shape[1] if (Cin == 4 and out.dim() == 4 and out.shape[1] == 3) else Cin
+    if dy.shape[0] != N or tuple(out.shape) != (Cout, cin_out, 4, 4) or out.dtype != torch.float32:
         raise ValueError(f'conv_wgrad: x {tuple(x.shape)}, dy {tuple(dy.shape)}, out {tuple(out.shape)} do not match')
     cl = torch.channels_last
     if not (x.is_contiguous(memory_format=cl) and dy.is_contiguous(memory_format=cl)):
@@ -831,7 +834,8 @@ def conv_wgrad(x, dy, out, target_blocks=512):
     partial = torch.empty(slices * Cout * 16 * Cin, dtype=torch.float32, device=x.device)
     _count('conv_wgrad')
     ext.conv_wgrad(x.data_ptr(), dy.data_ptr(), partial.data_ptr(), N, H, W, Cin, Ho, Wo, Cout, slices, px,
-                   out.data_ptr(), out.stride(0), out.stride(1), out.stride(2), out.stride(3), _stream(x.device))
+                   out.data_ptr(), out.stride(0), out.stride(1), out.stride(2), out.stride(3), _stream(x.device),
+                   cin_out)
     return out
 
 
@@ -846,7 +850,9 @@ def conv_fwd(x, w16, stats=None):
     N, Cin, H, W = x.shape
     Cout = w16.shape[0]
     cl = torch.channels_last
-    if tuple(w16.shape) != (Cout, Cin, 4, 4) or w16.dtype != torch.bfloat16 or x.dtype != torch.bfloat16:
+    # first layer fed RGBA: a 3-input-channel weight, the 4th input channel ignored
+    wc = 3 if (Cin == 4 and w16.shape[1] == 3) else Cin
+    if tuple(w16.shape) != (Cout, wc, 4, 4) or w16.dtype != torch.bfloat16 or x.dtype != torch.bfloat16:
         raise ValueError(f'conv_fwd: x {x.dtype} {tuple(x.shape)} / w {w16.dtype} {tuple(w16.shape)}')
     if not (x.is_contiguous(memory_format=cl) and w16.is_contiguous(memory_format=cl)):
         raise ValueError('conv_fwd needs channels-last x and weight')
@@ -854,7 +860,7 @@ def conv_fwd(x, w16, stats=None):
     y = torch.empty((N, Cout, Ho, Wo), dtype=torch.bfloat16, device=x.device, memory_format=cl)
     _count('conv_fwd')
     ext.conv_fwd(x.data_ptr(), w16.data_ptr(), y.data_ptr(), stats.data_ptr() if stats is not None else 0,
-                 N, H, W, Cin, Ho, Wo, Cout, _stream(x.device))
+                 N, H, W, Cin, Ho, Wo, Cout, _stream(x.device), wc if Cin == 4 else 0)
     return y
 
 
@@ -891,7 +897,9 @@ def conv_fwd_supported(x, w):
     if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and w.dim() == 4):
         return False
     cout, cin, kh, kw = w.shape
-    return ((kh, kw) == (4, 4) and x.shape[1] == cin and cin >= 8 and cin & (cin - 1) == 0 and cout % 32 == 0
+    xc = x.shape[1]
+    channels_ok = (xc == cin and cin >= 8 and cin & (cin - 1) == 0) or (xc == 4 and cin in (3, 4))
+    return ((kh, kw) == (4, 4) and channels_ok and cout % 32 == 0
             and x.is_contiguous(memory_format=torch.channels_last)
             and w.is_contiguous(memory_format=torch.channels_last))
 
@@ -923,6 +931,8 @@ def _conv_function():
                 return y, stats
             if conv_fwd_supported(x, w16):
                 return conv_fwd(x, w16)
+            if w16.shape[1] != x.shape[1]:
+                raise ValueError('conv4x4s2: an RGB weight on RGBA input needs the MFMA forward')
             return F.conv2d(x, w16, None, 2, 1)
 
         @staticmethod
@@ -934,8 +944,12 @@ def _conv_function():
                 if conv_dgrad_supported(x, w16):
                     gx = conv_dgrad(gy, w16, tuple(x.shape))
                 else:
-                    gx = torch.ops.aten.convolution_backward(gy, x, w16, None, [2, 2], [1, 1], [1, 1], False, [0, 0],
-                                                             1, [True, False, False])[0]
+                    wfull = w16
+                    if w16.shape[1] != x.shape[1]:   # RGBA-fed RGB weight: zero weight on the extra channel
+                        wfull = torch.cat([w16, w16.new_zeros(w16.shape[0], x.shape[1] - w16.shape[1], 4, 4)], 1)
+                        wfull = wfull.contiguous(memory_format=torch.channels_last)
+                    gx = torch.ops.aten.convolution_backward(gy, x, wfull, None, [2, 2], [1, 1], [1, 1], False,
+                                                             [0, 0], 1, [True, False, False])[0]
             if ctx.needs_input_grad[1]:
                 gw = conv_wgrad(x, gy, torch.empty_like(ctx.w32))
             return gx, gw, None, None

@@ -46,8 +46,8 @@ def run(name, iters, batch, graph, fused_adam=False, fused_bn=True, dma=0, cast=
         # decoded (gamma, /255, bf16 NHWC) inside the step
         from blendtorch import ops
         raw = torch.randint(0, 256, (batch, 480, 640, 4), dtype=torch.uint8, device=dev)
-        dcfg = ops.DecodeConfig.unit(channels='rgb', gamma=2.2, dtype='bfloat16' if amp else 'float32',
-                                     layout='nhwc')
+        dcfg = ops.DecodeConfig.unit(channels='rgba' if (amp and cast == 'fused') else 'rgb', gamma=2.2,
+                                     dtype='bfloat16' if amp else 'float32', layout='nhwc')
 
     def inputs():
         if not u8:

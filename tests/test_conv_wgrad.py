@@ -136,3 +136,49 @@ def test_dgrad_matches_fp32_reference(dev, N, Cin, H, W, Cout):
     ref = torch.nn.grad.conv2d_input((N, Cin, H, W), w.float(), dy.float(), stride=2, padding=1)
     assert dx.is_contiguous(memory_format=cl) and dx.dtype == torch.bfloat16
     torch.testing.assert_close(dx.float(), ref, rtol=2 ** -7, atol=1e-3 * float(ref.abs().max()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('N,H,W', [(2, 30, 40), (8, 480, 640), (3, 14, 18)])
+def test_first_layer_rgba_forward_and_wgrad(dev, N, H, W):
+    """RGBA-decoded frames into an RGB first layer: the 4-channel MFMA paths
+    ignore the alpha channel (weight 0) and produce the 3-channel gradient."""
+    import torch.nn.functional as F
+    g = torch.Generator(device=dev).manual_seed(H + W)
+    cl = torch.channels_last
+    x = torch.rand(N, 4, H, W, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    w = (0.1 * torch.randn(32, 3, 4, 4, device=dev, generator=g)).to(torch.bfloat16).contiguous(memory_format=cl)
+    rows = ops.conv_fwd_stats_rows(N * (H // 2) * (W // 2))
+    stats = torch.empty(rows * 2 * 32, device=dev)
+    y = ops.conv_fwd(x, w, stats)
+    ref = F.conv2d(x[:, :3].float(), w.float(), None, 2, 1)
+    torch.testing.assert_close(y.float(), ref, rtol=2 ** -7, atol=1e-3 * float(ref.abs().max()))
+    yf = y.float().permute(0, 2, 3, 1).reshape(-1, 32)
+    torch.testing.assert_close(stats.view(rows, 2, 32).sum(0)[0], yf.sum(0), rtol=1e-4, atol=1e-3)
+    dy = torch.randn(N, 32, H // 2, W // 2, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    for layout in (torch.contiguous_format, cl):
+        out = torch.full((32, 3, 4, 4), float('nan'), device=dev).contiguous(memory_format=layout)
+        ops.conv_wgrad(x, dy, out)
+        wref = torch.nn.grad.conv2d_weight(x[:, :3].float(), (32, 3, 4, 4), dy.float(), stride=2, padding=1)
+        torch.testing.assert_close(out, wref, rtol=1e-3, atol=1e-4 * float(wref.abs().max()))
+
+
+@pytest.mark.gpu
+def test_discriminator_rgba_input_equals_rgb(dev):
+    from blendtorch.models import Discriminator
+    torch.manual_seed(0)
+    a = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=torch.channels_last)
+    b = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=torch.channels_last)
+    b.load_state_dict(a.state_dict())
+    x4 = torch.rand(4, 4, 120, 160, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x3 = x4[:, :3].contiguous(memory_format=torch.channels_last)
+    before = ops.KERNEL_CALLS.get('conv_wgrad', 0)
+    la = a.bce_loss_bf16(x4, 1.0)
+    la.backward()
+    assert ops.KERNEL_CALLS['conv_wgrad'] == before + 4          # all four 4x4/s2 layers on the MFMA path
+    lb = b.bce_loss_bf16(x3, 1.0)
+    lb.backward()
+    torch.testing.assert_close(la, lb, rtol=1e-2, atol=1e-4)
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        ga, gb = pa.grad.flatten().double(), pb.grad.flatten().double()
+        assert float(ga @ gb / (ga.norm() * gb.norm())) > 0.99, n
