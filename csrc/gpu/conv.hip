@@ -30,6 +30,7 @@
 // a cast kernel per layer on it (profiles/r2/disc_mtrace_kernels.txt).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "kernels.h"
@@ -647,6 +648,17 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   }
 }
 
+// several weights at once (blockIdx.y = tensor): the data gradients' operands for every layer in one launch
+__global__ __launch_bounds__(kThreads) void weight_t_multi_kernel(WeightTParams p) {
+  const int k = int(blockIdx.y);
+  const int Cout = p.cout[k], Cin = p.cin[k];
+  const int total = Cout * 16 * Cin;
+  for (int e = int(blockIdx.x) * kThreads + int(threadIdx.x); e < total; e += int(gridDim.x) * kThreads) {
+    const int ci = e % Cin, tap = (e / Cin) % 16, co = e / (16 * Cin);
+    p.dst[k][(ci * 16 + tap) * Cout + co] = p.src[k][e];
+  }
+}
+
 // [Cout][kh][kw][Cin] (channels-last weight, any dtype pair) -> [Cin][kh][kw][Cout]
 __global__ __launch_bounds__(kThreads) void weight_t_kernel(const uint16_t* __restrict__ w, uint16_t* __restrict__ wt,
                                                             int Cout, int Cin) {
@@ -763,6 +775,19 @@ hipError_t conv_weight_t(const uint16_t* w, uint16_t* wt, int Cout, int Cin, hip
   const int total = Cout * 16 * Cin;
   const int blocks = (total + kThreads - 1) / kThreads;
   weight_t_kernel<<<blocks < 2048 ? blocks : 2048, kThreads, 0, stream>>>(w, wt, Cout, Cin);
+  return hipGetLastError();
+}
+
+hipError_t conv_weight_t_multi(const WeightTParams& p, hipStream_t stream) {
+  if (p.n <= 0) return hipSuccess;
+  if (p.n > kMaxWeightT) return hipErrorInvalidValue;
+  int most = 0;
+  for (int k = 0; k < p.n; ++k) {
+    if (!p.src[k] || !p.dst[k] || p.cout[k] <= 0 || p.cin[k] <= 0) return hipErrorInvalidValue;
+    most = std::max(most, p.cout[k] * 16 * p.cin[k]);
+  }
+  const int blocks = (most + kThreads - 1) / kThreads;
+  weight_t_multi_kernel<<<dim3(unsigned(blocks < 1024 ? blocks : 1024), unsigned(p.n)), kThreads, 0, stream>>>(p);
   return hipGetLastError();
 }
 

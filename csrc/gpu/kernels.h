@@ -273,6 +273,15 @@ hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream);
 // Cout a power of two >= 16, Cin % 64 == 0, H and W even.
 bool conv_dgrad_supported(int Cin, int Cout);
 hipError_t conv_weight_t(const uint16_t* w, uint16_t* wt, int Cout, int Cin, hipStream_t stream);
+constexpr int kMaxWeightT = 8;
+struct WeightTParams {   // conv_weight_t for several weights in one launch
+  const uint16_t* src[kMaxWeightT] = {};
+  uint16_t* dst[kMaxWeightT] = {};
+  int cout[kMaxWeightT] = {};
+  int cin[kMaxWeightT] = {};
+  int n = 0;
+};
+hipError_t conv_weight_t_multi(const WeightTParams& p, hipStream_t stream);
 hipError_t conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int N, int H, int W, int Cin, int Cout,
                       hipStream_t stream);
 // bn_finalize over `nblocks` partial rows produced elsewhere (conv_fwd's epilogue)

@@ -240,6 +240,21 @@ PYBIND11_MODULE(_hip, m) {
   m.def("conv_weight_t", [](uintptr_t w, uintptr_t wt, int Cout, int Cin, uintptr_t stream) {
     check(conv_weight_t(ptr<const uint16_t>(w), ptr<uint16_t>(wt), Cout, Cin, stream_of(stream)), "conv_weight_t");
   });
+  m.def("conv_weight_t_multi", [](std::vector<uintptr_t> src, std::vector<uintptr_t> dst, std::vector<int> cout,
+                                  std::vector<int> cin, uintptr_t stream) {
+    const size_t n = src.size();
+    if (dst.size() != n || cout.size() != n || cin.size() != n || n > size_t(kMaxWeightT))
+      throw std::invalid_argument("conv_weight_t_multi: list lengths differ or exceed kMaxWeightT");
+    WeightTParams p;
+    p.n = int(n);
+    for (size_t k = 0; k < n; ++k) {
+      p.src[k] = ptr<const uint16_t>(src[k]);
+      p.dst[k] = ptr<uint16_t>(dst[k]);
+      p.cout[k] = cout[k];
+      p.cin[k] = cin[k];
+    }
+    check(conv_weight_t_multi(p, stream_of(stream)), "conv_weight_t_multi");
+  });
   m.def("conv_dgrad", [](uintptr_t dy, uintptr_t wt, uintptr_t dx, int N, int H, int W, int Cin, int Cout,
                          uintptr_t stream) {
     check(conv_dgrad(ptr<const uint16_t>(dy), ptr<const uint16_t>(wt), ptr<uint16_t>(dx), N, H, W, Cin, Cout,

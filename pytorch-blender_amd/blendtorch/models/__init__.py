@@ -104,20 +104,31 @@ class Discriminator(nn.Module):
         import torch.nn.functional as F
         from .. import ops
         convs = [m for m in layers if isinstance(m, nn.Conv2d)]
-        weights = iter(ops.cast_bf16(*[c.weight for c in convs]))
+        w16s = ops.cast_bf16(*[c.weight for c in convs])
+        weights = iter(w16s)
+        # data-gradient operands of the MFMA layers that need one (not the first:
+        # its input is the batch), transposed in one launch per step
+        wts = {}
+        if mfma and torch.is_grad_enabled() and x.is_cuda:
+            need = [k for k, c in enumerate(convs) if k > 0 and c.in_channels % 32 == 0 and c.stride == (2, 2)
+                    and tuple(c.kernel_size) == (4, 4) and c.out_channels % 32 == 0]
+            if need:
+                wts = dict(zip(need, ops.conv_weights_t([w16s[k] for k in need])))
+        ci = -1
         stats = None
         for i, m in enumerate(layers):
             if isinstance(m, nn.Conv2d):
                 w16 = next(weights)
+                ci += 1
                 if (mfma and m.stride == (2, 2) and m.padding == (1, 1) and m.bias is None and m.groups == 1
                         and m.dilation == (1, 1) and ops.conv_wgrad_supported(x, m.weight)):
                     nxt = layers[i + 1] if i + 1 < len(layers) else None
                     fuse = (isinstance(nxt, ops.BatchNormLeakyReLU2d) and ops.conv_fwd_supported(x, w16)
                             and nxt.fused_with_stats(x.new_empty((1, m.out_channels, 1, 1))))
                     if fuse:   # BN statistics come out of the conv kernel's epilogue
-                        x, stats = ops.conv4x4s2(x, m.weight, w16, with_stats=True)
+                        x, stats = ops.conv4x4s2(x, m.weight, w16, with_stats=True, wt=wts.get(ci))
                     else:
-                        x = ops.conv4x4s2(x, m.weight, w16)
+                        x = ops.conv4x4s2(x, m.weight, w16, wt=wts.get(ci))
                 else:
                     x = F.conv2d(x, w16, None, m.stride, m.padding, m.dilation, m.groups)
             elif stats is not None and isinstance(m, ops.BatchNormLeakyReLU2d):

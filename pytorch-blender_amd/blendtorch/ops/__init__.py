@@ -809,7 +809,7 @@ def conv_wgrad_supported(x, weight):
     return (kh, kw) == (4, 4) and (big or first) and x.is_contiguous(memory_format=torch.channels_last)
 
 
-def conv_wgrad(x, dy, out, target_blocks=512):
+def conv_wgrad(x, dy, out, target_blocks=None):
     """fp32 weight gradient of a 4x4/s2/p1 convolution into ``out`` ([Cout, Cin,
     4, 4], any strides): MFMA tiles over pixel slices + one slice-reduce
     launch.  ``x`` [N, Cin, H, W] and ``dy`` [N, Cout, H/2, W/2] are bf16 with
@@ -825,6 +825,10 @@ def conv_wgrad(x, dy, out, target_blocks=512):
     if not (x.is_contiguous(memory_format=cl) and dy.is_contiguous(memory_format=cl)):
         raise ValueError('conv_wgrad needs channels-last x and dy')
     M = N * Ho * Wo
+    if target_blocks is None:
+        # 2 blocks per CU; the first layer's single tile: fewer, longer slices
+        # (its slice partials are added atomically, 32-way instead of 64-way)
+        target_blocks = 256 if Cin == 4 else 512
     slices = ext.conv_wgrad_slices(M, Cin, Cout, target_blocks)
     if slices <= 0:
         raise ValueError(f'conv_wgrad: unsupported channels Cin={Cin} Cout={Cout} (Cin % 32, Cout % 64)')
@@ -864,7 +868,25 @@ def conv_fwd(x, w16, stats=None):
     return y
 
 
-def conv_dgrad(dy, w16, in_shape):
+def conv_weights_t(weights):
+    """[Cin*16*Cout] bf16 transposes ([ci][kh][kw][co]) of channels-last bf16
+    conv weights, all in one launch: the data-gradient operands of a model's
+    layers, made once per step (``conv_dgrad(..., wt=)``)."""
+    import torch
+    ws = [w.detach() for w in weights]
+    outs = [torch.empty(w.numel(), dtype=torch.bfloat16, device=w.device) for w in ws]
+    if ws:
+        for w in ws:
+            if not (w.dtype == torch.bfloat16 and w.is_contiguous(memory_format=torch.channels_last)):
+                raise ValueError('conv_weights_t needs channels-last bf16 weights')
+        _count('conv_weight_t_multi')
+        hip_ext().conv_weight_t_multi([w.data_ptr() for w in ws], [o.data_ptr() for o in outs],
+                                      [int(w.shape[0]) for w in ws], [int(w.shape[1]) for w in ws],
+                                      _stream(ws[0].device))
+    return outs
+
+
+def conv_dgrad(dy, w16, in_shape, wt=None):
     """Data gradient of :func:`conv_fwd` on the same MFMA kernel (four
     stride-2 parity classes, 4 taps each): ``dy`` [N, Cout, H/2, W/2] bf16
     channels-last, ``w16`` [Cout, Cin, 4, 4] bf16 channels-last -> dx
@@ -878,8 +900,11 @@ def conv_dgrad(dy, w16, in_shape):
         raise ValueError('conv_dgrad needs channels-last dy and weight')
     if tuple(dy.shape) != (N, Cout, H // 2, W // 2) or dy.dtype != torch.bfloat16 or w16.dtype != torch.bfloat16:
         raise ValueError(f'conv_dgrad: dy {dy.dtype} {tuple(dy.shape)} / w {tuple(w16.shape)} vs input {in_shape}')
-    wt = torch.empty(Cin * 16 * Cout, dtype=torch.bfloat16, device=dy.device)
-    ext.conv_weight_t(w16.data_ptr(), wt.data_ptr(), Cout, Cin, _stream(dy.device))
+    if wt is None:
+        wt = torch.empty(Cin * 16 * Cout, dtype=torch.bfloat16, device=dy.device)
+        ext.conv_weight_t(w16.data_ptr(), wt.data_ptr(), Cout, Cin, _stream(dy.device))
+    elif wt.numel() != Cin * 16 * Cout or wt.dtype != torch.bfloat16:
+        raise ValueError('conv_dgrad: wt is not this weight\'s transpose (conv_weights_t)')
     dx = torch.empty((N, Cin, H, W), dtype=torch.bfloat16, device=dy.device, memory_format=cl)
     _count('conv_dgrad')
     ext.conv_dgrad(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), N, H, W, Cin, Cout, _stream(dy.device))
@@ -919,9 +944,10 @@ def _conv_function():
         into the master weight's gradient (no bf16 round trip, no cast)."""
 
         @staticmethod
-        def forward(ctx, x, w32, w16, with_stats=False):
+        def forward(ctx, x, w32, w16, with_stats=False, wt=None):
+            ctx.set_materialize_grads(False)   # no zero-filled gradient for the stats output
             ctx.save_for_backward(x, w16)
-            ctx.w32 = w32
+            ctx.w32, ctx.wt = w32, wt
             if with_stats:
                 N, _, H, W = x.shape
                 M = N * ((H - 2) // 2 + 1) * ((W - 2) // 2 + 1)
@@ -938,11 +964,13 @@ def _conv_function():
         @staticmethod
         def backward(ctx, gy, gstats=None):
             x, w16 = ctx.saved_tensors
+            if gy is None:
+                return None, None, None, None, None
             gy = gy.contiguous(memory_format=torch.channels_last)
             gx = gw = None
             if ctx.needs_input_grad[0]:
                 if conv_dgrad_supported(x, w16):
-                    gx = conv_dgrad(gy, w16, tuple(x.shape))
+                    gx = conv_dgrad(gy, w16, tuple(x.shape), ctx.wt)
                 else:
                     wfull = w16
                     if w16.shape[1] != x.shape[1]:   # RGBA-fed RGB weight: zero weight on the extra channel
@@ -952,7 +980,7 @@ def _conv_function():
                                                              [0, 0], 1, [True, False, False])[0]
             if ctx.needs_input_grad[1]:
                 gw = conv_wgrad(x, gy, torch.empty_like(ctx.w32))
-            return gx, gw, None, None
+            return gx, gw, None, None, None
 
     return _Conv4x4s2
 
@@ -960,7 +988,7 @@ def _conv_function():
 _CONV_FN = None
 
 
-def conv4x4s2(x, w32, w16, with_stats=False):
+def conv4x4s2(x, w32, w16, with_stats=False, wt=None):
     """4x4 / stride-2 / pad-1 convolution of bf16 channels-last ``x`` with the
     bf16 copy ``w16`` of fp32 weight ``w32``; the gradient goes to ``w32``
     (fp32, from the MFMA weight-gradient kernel).  See :func:`conv_wgrad_supported`.
@@ -971,7 +999,7 @@ def conv4x4s2(x, w32, w16, with_stats=False):
         _CONV_FN = _conv_function()
     if with_stats and not conv_fwd_supported(x, w16):
         raise ValueError('conv4x4s2(with_stats=True) needs the MFMA forward (see conv_fwd_supported)')
-    return _CONV_FN.apply(x, w32, w16.detach(), with_stats)
+    return _CONV_FN.apply(x, w32, w16.detach(), with_stats, wt)
 
 
 # ---------------------------------------------------------------------------
@@ -984,6 +1012,7 @@ def _head_function():
     class _DiscHeadBCE(torch.autograd.Function):
         @staticmethod
         def forward(ctx, z, w, target, oh, ow):
+            ctx.set_materialize_grads(False)   # no zero-filled gradient for the logits output
             ext = hip_ext()
             N, C, H, W = z.shape
             dev = z.device
@@ -1009,6 +1038,8 @@ def _head_function():
 
         @staticmethod
         def backward(ctx, gloss, glogit=None):
+            if gloss is None:
+                return None, None, None, None, None
             ext = hip_ext()
             w, pooled, dlogit = ctx.saved_tensors
             N, C, H, W = ctx.zshape
