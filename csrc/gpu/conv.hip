@@ -115,6 +115,17 @@ __device__ __forceinline__ uint2 bload8(__amdgpu_buffer_rsrc_t r, uint32_t off) 
   return make_uint2(v[0], v[1]);
 }
 
+// The slice-reduce adds slice groups atomically into the gradient, which must
+// start at zero: the weight-gradient kernel clears it (every block a share,
+// plain stores) -- the reduce runs after it on the stream, so no separate
+// memset launch is needed.
+__device__ __forceinline__ void zero_output(const ConvWgradParams& p) {
+  if (!p.zero_out) return;
+  const int per = (p.zero_count + int(gridDim.x) - 1) / int(gridDim.x);
+  const int e0 = int(blockIdx.x) * per, e1 = e0 + per < p.zero_count ? e0 + per : p.zero_count;
+  for (int e = e0 + int(threadIdx.x); e < e1; e += int(blockDim.x)) p.zero_out[e] = 0.f;
+}
+
 struct PixelCursor {   // (n, oh, ow) of pixel m, advanced by BPX per k-step
   int n, oh, ow;
   __device__ void init(int m, int Ho, int Wo) {
@@ -245,6 +256,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p)
   }
 
   // C/D map of 16x16x32: column = lane & 15 (kc), row = 4 * (lane >> 4) + reg (co)
+  zero_output(p);
   float* out = p.partial + int64_t(slice) * p.Cout * KC;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -354,6 +366,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4_kernel(ConvWgradParams
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, frag_at(base, rb[j], 4 * C4_X_ROW), acc[j], 0, 0, 0);
     }
   }
+  zero_output(p);
   float* out = p.partial + int64_t(slice) * p.Cout * 64;
 #pragma unroll
   for (int j = 0; j < 2; ++j)
@@ -700,15 +713,15 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
   const int64_t tiles = c4 ? p.Cout / 32 : int64_t(p.Cout / BCO) * (16 * p.Cin / BKC);
   const int64_t blocks = tiles * p.slices;
   if (blocks > (int64_t(1) << 31) - 1) return hipErrorInvalidValue;
-  if (c4) conv_wgrad_c4_kernel<<<unsigned(blocks), kThreads, 0, stream>>>(p);
-  else conv_wgrad_kernel<<<unsigned(blocks), kThreads, 0, stream>>>(p);
+  ConvWgradParams q = p;
+  if (p.slices > kSliceGroup) {   // groups add atomically: the main kernel zeroes out first (dense tensor)
+    q.zero_out = out;
+    q.zero_count = p.Cout * 16 * (p.cin_out > 0 ? p.cin_out : p.Cin);
+  }
+  if (c4) conv_wgrad_c4_kernel<<<unsigned(blocks), kThreads, 0, stream>>>(q);
+  else conv_wgrad_kernel<<<unsigned(blocks), kThreads, 0, stream>>>(q);
   const int64_t total = int64_t(p.Cout) * 16 * p.Cin;   // partial elements per slice
   const int cin_out = p.cin_out > 0 ? p.cin_out : p.Cin;
-  if (p.slices > kSliceGroup) {
-    // groups add atomically: start from zero (out is dense: contiguous or channels-last)
-    const hipError_t e = hipMemsetAsync(out, 0, size_t(p.Cout) * 16 * size_t(cin_out) * sizeof(float), stream);
-    if (e != hipSuccess) return e;
-  }
   const dim3 rgrid(unsigned((total / 4 + kThreads - 1) / kThreads), unsigned((p.slices + kSliceGroup - 1) / kSliceGroup));
   conv_wgrad_reduce_kernel<<<rgrid, kThreads, 0, stream>>>(p.partial, p.slices, p.Cout, p.Cin,
                                                            p.cin_out > 0 ? p.cin_out : p.Cin, out, s_co, s_ci, s_kh,

@@ -242,6 +242,8 @@ struct ConvWgradParams {
   int slices = 0;
   int64_t px_per_slice = 0;
   int cin_out = 0;   // dW input channels written (0: Cin); 3 for a 4-channel (RGBA-fed) first layer
+  float* zero_out = nullptr;   // set by conv_wgrad: the kernel clears the output for the atomic reduce
+  int zero_count = 0;
 };
 // Cin % 32 == 0 with Cout % 64 == 0, or Cin == 4 (the first layer) with Cout % 32 == 0.
 bool conv_wgrad_supported(int Cin, int Cout);

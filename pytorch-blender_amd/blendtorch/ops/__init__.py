@@ -826,9 +826,7 @@ def conv_wgrad(x, dy, out, target_blocks=None):
         raise ValueError('conv_wgrad needs channels-last x and dy')
     M = N * Ho * Wo
     if target_blocks is None:
-        # 2 blocks per CU; the first layer's single tile: fewer, longer slices
-        # (its slice partials are added atomically, 32-way instead of 64-way)
-        target_blocks = 256 if Cin == 4 else 512
+        target_blocks = 512   # 2 blocks per CU (profiles/r2/conv_bench_v2.jsonl)
     slices = ext.conv_wgrad_slices(M, Cin, Cout, target_blocks)
     if slices <= 0:
         raise ValueError(f'conv_wgrad: unsupported channels Cin={Cin} Cout={Cout} (Cin % 32, Cout % 64)')
