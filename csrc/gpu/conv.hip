@@ -144,6 +144,43 @@ struct PixelCursor {   // (n, oh, ow) of pixel m, advanced by BPX per k-step
   }
 };
 
+// One X pixel's im2col source for a thread's fixed (kh, kw, ci), advanced BPX
+// output pixels per k-step: the element offset moves by constant jumps (next
+// column block, next row, next image), so a k-step costs a few adds and
+// selects -- recomputing (n, ih, iw) -> offset with multiplies, and the
+// divergent while loop of PixelCursor, made this kernel VALU-bound.
+struct XCursor {
+  int oh, ow, e;
+  __device__ void init(int m, const ConvWgradParams& p, int kh, int kw, int ci) {
+    const int hw = p.Ho * p.Wo;
+    const int n = m / hw, r = m - n * hw;
+    oh = r / p.Wo;
+    ow = r - oh * p.Wo;
+    e = (n * p.H + 2 * oh - 1 + kh) * (p.W * p.Cin) + (2 * ow - 1 + kw) * p.Cin + ci;
+  }
+  // col = 2 BPX Cin, row = 2 W Cin - 2 Wo Cin, img = (H - 2 Ho) W Cin;
+  // single: Wo >= BPX (block-uniform), so at most one row wrap per step
+  __device__ void advance(int Ho, int Wo, int col, int row, int img, bool single) {
+    ow += BPX;
+    e += col;
+    if (single) {
+      const bool wr = ow >= Wo;
+      ow = wr ? ow - Wo : ow;
+      e = wr ? e + row : e;
+      oh += wr ? 1 : 0;
+      const bool wi = oh == Ho;
+      oh = wi ? 0 : oh;
+      e = wi ? e + img : e;
+    } else {
+      while (ow >= Wo) {
+        ow -= Wo;
+        e += row;
+        if (++oh == Ho) oh = 0, e += img;
+      }
+    }
+  }
+};
+
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
@@ -168,9 +205,11 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p)
   const int kh = kc / (4 * p.Cin);
   const int rem = kc - kh * 4 * p.Cin;
   const int kw = rem / p.Cin, ci = rem - kw * p.Cin;
-  PixelCursor c0, c1;
-  c0.init(m_begin + xpx0, p.Ho, p.Wo);
-  c1.init(m_begin + xpx0 + 16, p.Ho, p.Wo);
+  XCursor c0, c1;
+  c0.init(m_begin + xpx0, p, kh, kw, ci);
+  c1.init(m_begin + xpx0 + 16, p, kh, kw, ci);
+  const int j_col = 2 * BPX * p.Cin, j_row = 2 * (p.W - p.Wo) * p.Cin, j_img = (p.H - 2 * p.Ho) * p.W * p.Cin;
+  const bool single = p.Wo >= BPX;
 
   const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(p.x, int64_t(p.N) * p.H * p.W * p.Cin * 2);
   const __amdgpu_buffer_rsrc_t rs_dy = make_rsrc(p.dy, p.M * p.Cout * 2);
@@ -186,23 +225,22 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p)
   int md = m_begin + dpx;                                           // this thread's dY pixel
   uint32_t dy_byte = uint32_t(md) * uint32_t(p.Cout * 2) + uint32_t((co0 + dch * 8) * 2);
   const uint32_t dy_step = uint32_t(BPX * p.Cout * 2);
-  int mx = m_begin + xpx0;                                          // X pixels mx, mx + 16
-  const int row_elems = p.W * p.Cin;
-  auto xload = [&](const PixelCursor& c, int m) {
+  // X needs no slice-end test: a pixel past the slice pairs with a zero dY
+  // chunk (out-of-range dY loads return 0), and past the tensor the X load is
+  // out of range too
+  auto xload = [&](const XCursor& c) {
     const int ih = 2 * c.oh - 1 + kh, iw = 2 * c.ow - 1 + kw;
-    const bool ok = m < m_end && unsigned(ih) < unsigned(p.H) && unsigned(iw) < unsigned(p.W);
-    const int e = (c.n * p.H + ih) * row_elems + iw * p.Cin + ci;
-    return bload(rs_x, ok ? uint32_t(e) * 2u : kOOB);
+    const bool ok = unsigned(ih) < unsigned(p.H) && unsigned(iw) < unsigned(p.W);
+    return bload(rs_x, ok ? uint32_t(c.e) * 2u : kOOB);
   };
   auto load = [&](Stage& r) {
     r.dy = bload(rs_dy, md < m_end ? dy_byte : kOOB);
-    r.x0 = xload(c0, mx);
-    r.x1 = xload(c1, mx + 16);
+    r.x0 = xload(c0);
+    r.x1 = xload(c1);
     md += BPX;
     dy_byte += dy_step;
-    mx += BPX;
-    c0.advance(p.Ho, p.Wo);
-    c1.advance(p.Ho, p.Wo);
+    c0.advance(p.Ho, p.Wo, j_col, j_row, j_img, single);
+    c1.advance(p.Ho, p.Wo, j_col, j_row, j_img, single);
   };
   const int st_dy = dy_off(dpx, dch * 16), st_x0 = DY_TILE + x_off(xpx0, xch * 16),
             st_x1 = DY_TILE + x_off(xpx0 + 16, xch * 16);
@@ -498,6 +536,23 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     base[j] = (n * p.SH + rb[j]) * p.SW + cb[j];
     obase[j] = DGRAD ? ((n * p.OH + 2 * a + ph) * p.OW + 2 * bb + pw) * p.NOUT : mm * p.NOUT;
   }
+  // per row: byte offset of its tap-origin pixel (mod 2^32: border rows start
+  // at -1, and only in-bounds taps are ever added to it) and a bitmask of the
+  // taps that land inside the image -- the k-loop then costs one add and one
+  // mask test per row instead of the full index and bounds arithmetic
+  uint32_t abase[4], vmask[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    abase[j] = uint32_t(base[j]) << (p.cshift + 1);
+    uint32_t mk = 0;
+#pragma unroll
+    for (int tp = 0; tp < NTAPS; ++tp) {
+      const int dr = DGRAD ? ph - (tp >> 1) : tp >> 2, dc = DGRAD ? pw - (tp & 1) : tp & 3;
+      const bool in = unsigned(rb[j] + dr) < unsigned(p.SH) && unsigned(cb[j] + dc) < unsigned(p.SW);
+      mk |= (pin[j] && in) ? (1u << tp) : 0u;
+    }
+    vmask[j] = mk;
+  }
   const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(p.src, int64_t(p.N) * p.SH * p.SW * p.C * 2);
   const uint16_t* wrow0 = p.w + (n0 + ar) * (16 * p.C);
   const uint16_t* wrow1 = p.w + (n0 + (BN == 64 ? ar + 32 : ar)) * (16 * p.C);
@@ -525,12 +580,16 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
                        uint32_t(q[3]) | (uint32_t(q[4]) << 16), uint32_t(q[5]));
     }
   };
+  const int nsteps = K / FBK;
   auto load = [&](int ks) {
     if constexpr (C4) {
       load_c4();
       return;
     }
-    const int kc = ks * FBK + ac * 8;
+    // steps past the end (the ring's padding) load zeros for A -- the MFMA then
+    // adds nothing -- and re-read the last step's weights (in bounds)
+    const bool live = ks < nsteps;
+    const int kc = (live ? ks : nsteps - 1) * FBK + ac * 8;
     const int tap = kc >> p.cshift, ch = kc & (p.C - 1);
     int dr, dc, wtap;
     if (DGRAD) {
@@ -542,12 +601,10 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
       dc = tap & 3;
       wtap = tap;
     }
-    const int toff = dr * p.SW + dc;
+    const uint32_t soff = uint32_t((((dr * p.SW + dc) << p.cshift) + ch) * 2);
+    const uint32_t tbit = live ? 1u << tap : 0u;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const bool ok = pin[j] && unsigned(rb[j] + dr) < unsigned(p.SH) && unsigned(cb[j] + dc) < unsigned(p.SW);
-      ra[j] = bload(rs_src, ok ? uint32_t((((base[j] + toff) << p.cshift) + ch) * 2) : kOOB);
-    }
+    for (int j = 0; j < 4; ++j) ra[j] = bload(rs_src, (vmask[j] & tbit) ? abase[j] + soff : kOOB);
     const int woff = wtap * p.C + ch;
     rb0 = *reinterpret_cast<const uint4*>(wrow0 + woff);
     if (BN == 64) rb1 = *reinterpret_cast<const uint4*>(wrow1 + woff);
@@ -578,13 +635,8 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) fb[j][kk] = FA_TILE + f_off(col0 + 16 * j + (lane & 15), chunk);
   }
-  const int nsteps = K / FBK;
-  load(0);
-  store(0);
-  __syncthreads();
-  for (int s = 0; s < nsteps; ++s) {
-    if (s + 1 < nsteps) load(s + 1);
-    const char* ai = smem + (s & 1) * F_STAGE;
+  auto mma = [&](int buf) {
+    const char* ai = smem + buf * F_STAGE;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 a[FM], bb[FN];
@@ -598,8 +650,47 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bb[j], acc[i][j], 0, 0, 0);
     }
-    if (s + 1 < nsteps) store((s + 1) & 1);
+  };
+  if constexpr (C4) {   // the first layer's K is one step
+    load(0);
+    store(0);
     __syncthreads();
+    mma(0);
+  } else {
+    // Loads run kDepth steps ahead of the MFMAs in a register ring: with one
+    // step of prefetch every k-step waited out a full global-load latency, and
+    // the deep-K layers (16-32 steps) were latency-bound.  The barrier is
+    // LDS-only, so the ring's later stages stay in flight across it (counted
+    // vmcnt waits on the stage being stored).
+    constexpr int kDepth = 2;
+    uint4 ring_a[kDepth][4], ring_b0[kDepth], ring_b1[kDepth];
+    int ks_next = 0;
+    auto fetch = [&](int u) {
+      load(ks_next++);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ring_a[u][j] = ra[j];
+      ring_b0[u] = rb0;
+      if (BN == 64) ring_b1[u] = rb1;
+    };
+#pragma unroll
+    for (int u = 0; u < kDepth; ++u) fetch(u);
+    const int padded = (nsteps + kDepth - 1) / kDepth * kDepth;
+    for (int s0 = 0; s0 < padded; s0 += kDepth) {
+#pragma unroll
+      for (int u = 0; u < kDepth; ++u) {
+        const int buf = u & 1;   // kDepth is even: (s0 + u) & 1
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ra[j] = ring_a[u][j];
+        rb0 = ring_b0[u];
+        if (BN == 64) rb1 = ring_b1[u];
+        store(buf);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        fetch(u);                // step s0 + u + kDepth
+        mma(buf);
+      }
+    }
+    __syncthreads();   // the epilogue reuses the staging LDS
   }
 
   // epilogue: round to bf16 (RNE) into an LDS tile [FBM][BN] (128-byte row
@@ -657,7 +748,8 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     float v = 0.f;
 #pragma unroll
     for (int g = 0; g < WGM; ++g) v += red[(g * 2 + which) * BN + c];
-    p.stats[mt * 2 * p.NOUT + which * p.NOUT + n0 + c] = v;
+    // channel-major [2][NOUT][tiles], the layout bn_finalize_rows folds
+    p.stats[(which * p.NOUT + n0 + c) * ((p.M + FBM - 1) / FBM) + mt] = v;
   }
 }
 

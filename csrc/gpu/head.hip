@@ -28,24 +28,56 @@ __device__ __forceinline__ int wend(int i, int in, int out) { return ((i + 1) * 
 __device__ __forceinline__ float bf(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
 
 // one block per (pooling cell, image): pooled values of the cell and the
-// cell's share of the image's logit
+// cell's share of the image's logit.  Lanes own 8 channels (one 16-byte load)
+// of a pixel; the PL = 256 / (C / 8) pixel lanes of a channel group stride the
+// window and meet in LDS.  (One lane per channel walking the window serially
+// was a chain of dependent 2-byte loads: 22 us for the bench's 8x30x40x256.)
 __global__ __launch_bounds__(kHeadThreads) void head_fwd_kernel(HeadParams p) {
   __shared__ float red[kHeadThreads / 64];
+  __shared__ float acc_l[kHeadThreads * 8];
   const int cell = int(blockIdx.x), n = int(blockIdx.y);
   const int i = cell / p.OW, j = cell - i * p.OW;
   const int h0 = wstart(i, p.H, p.OH), h1 = wend(i, p.H, p.OH);
   const int w0 = wstart(j, p.W, p.OW), w1 = wend(j, p.W, p.OW);
-  const float inv = 1.f / float((h1 - h0) * (w1 - w0));
+  const int ww = w1 - w0, npx = (h1 - h0) * ww;
+  const float inv = 1.f / float(npx);
+  const int t = int(threadIdx.x);
   float part = 0.f;
-  for (int c = int(threadIdx.x); c < p.C; c += kHeadThreads) {
-    float s = 0.f;
-    for (int h = h0; h < h1; ++h) {
-      const uint16_t* row = p.z + (int64_t(n * p.H + h) * p.W) * p.C + c;
-      for (int w = w0; w < w1; ++w) s += bf(row[int64_t(w) * p.C]);
+  const int G = p.C / 8;
+  if (p.C % 8 == 0 && G <= kHeadThreads && kHeadThreads % G == 0 && (reinterpret_cast<uintptr_t>(p.z) & 15) == 0) {
+    const int g = t % G, pl = t / G, PL = kHeadThreads / G;
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int k = pl; k < npx; k += PL) {
+      const int h = h0 + k / ww, w = w0 + k % ww;
+      const uint4 v = *reinterpret_cast<const uint4*>(p.z + (int64_t(n * p.H + h) * p.W + w) * p.C + g * 8);
+      const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        a[2 * q] += __uint_as_float(u[q] << 16);
+        a[2 * q + 1] += __uint_as_float(u[q] & 0xFFFF0000u);
+      }
     }
-    const float pooled = s * inv;
-    p.pooled[(int64_t(n) * p.OH * p.OW + cell) * p.C + c] = pooled;
-    part += pooled * p.w[c * p.ws_c + i * p.ws_i + j * p.ws_j];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc_l[pl * p.C + g * 8 + q] = a[q];
+    __syncthreads();
+    for (int c = t; c < p.C; c += kHeadThreads) {
+      float s = 0.f;
+      for (int l = 0; l < PL; ++l) s += acc_l[l * p.C + c];
+      const float pooled = s * inv;
+      p.pooled[(int64_t(n) * p.OH * p.OW + cell) * p.C + c] = pooled;
+      part += pooled * p.w[c * p.ws_c + i * p.ws_i + j * p.ws_j];
+    }
+  } else {
+    for (int c = t; c < p.C; c += kHeadThreads) {
+      float s = 0.f;
+      for (int h = h0; h < h1; ++h) {
+        const uint16_t* row = p.z + (int64_t(n * p.H + h) * p.W) * p.C + c;
+        for (int w = w0; w < w1; ++w) s += bf(row[int64_t(w) * p.C]);
+      }
+      const float pooled = s * inv;
+      p.pooled[(int64_t(n) * p.OH * p.OW + cell) * p.C + c] = pooled;
+      part += pooled * p.w[c * p.ws_c + i * p.ws_i + j * p.ws_j];
+    }
   }
   for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = part;
@@ -77,17 +109,19 @@ __global__ __launch_bounds__(64) void head_loss_kernel(HeadParams p) {
 
 // dz: 8 channels of one pixel per lane (one 16-byte store)
 __global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p) {
+  // 32-bit index math (the host checks N*H*W*C/8 < 2^31): 64-bit division
+  // and modulo made this an ALU-bound kernel
   const int groups = p.C / 8;
-  const int64_t total = int64_t(p.N) * p.H * p.W * groups;
+  const int total = p.N * p.H * p.W * groups;
   const float g = p.gscale[0];
-  for (int64_t e = int64_t(blockIdx.x) * kHeadThreads + threadIdx.x; e < total;
-       e += int64_t(gridDim.x) * kHeadThreads) {
-    const int c0 = int(e % groups) * 8;
-    int64_t r = e / groups;
-    const int w = int(r % p.W);
+  for (int e = int(blockIdx.x) * kHeadThreads + int(threadIdx.x); e < total; e += int(gridDim.x) * kHeadThreads) {
+    int r = e / groups;
+    const int c0 = (e - r * groups) * 8;
+    const int pix = r;
     r /= p.W;
-    const int h = int(r % p.H);
-    const int n = int(r / p.H);
+    const int w = pix - r * p.W;
+    const int n = r / p.H;
+    const int h = r - n * p.H;
     const float d = g * p.dlogit[n];
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const int i0 = (h * p.OH) / p.H, i1 = ((h + 1) * p.OH + p.H - 1) / p.H;
@@ -144,6 +178,7 @@ hipError_t head_backward(const HeadParams& p, hipStream_t stream) {
   if (p.C % 8 || !p.dz || !p.dw || !p.gscale || !p.dlogit || !p.pooled) return hipErrorInvalidValue;
   if (reinterpret_cast<uintptr_t>(p.dz) & 15) return hipErrorInvalidValue;
   const int64_t total = int64_t(p.N) * p.H * p.W * (p.C / 8);
+  if (total >= (int64_t(1) << 31) - int64_t(kHeadThreads) * 4096) return hipErrorInvalidValue;
   const int64_t blocks = (total + kHeadThreads - 1) / kHeadThreads;
   head_bwd_kernel<<<unsigned(blocks < 4096 ? blocks : 4096), kHeadThreads, 0, stream>>>(p);
   const int wtotal = p.C * p.OH * p.OW;

@@ -253,9 +253,9 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
 
 // Forward 4x4 / stride-2 / pad-1 convolution on the MFMA units (conv.hip):
 // x [N][H][W][Cin] bf16, w [Cout][4][4][Cin] bf16 (channels-last weight) ->
-// y [N][Ho][Wo][Cout] bf16.  stats (nullable): [conv_fwd_tiles(M)][2][Cout]
-// fp32 per-tile sum / sum of squares of the rounded y -- the partial rows
-// bn_finalize_tiles folds into BatchNorm statistics.
+// y [N][Ho][Wo][Cout] bf16.  stats (nullable): [2][Cout][conv_fwd_tiles(M)]
+// fp32 per-tile sum / sum of squares of the rounded y (channel-major) -- the
+// partials bn_finalize_rows folds into BatchNorm statistics.
 struct ConvFwdParams {
   const uint16_t* x = nullptr;
   const uint16_t* w = nullptr;

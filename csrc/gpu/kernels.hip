@@ -919,10 +919,11 @@ __global__ __launch_bounds__(kBlock) void bn_reduce_kernel(const void* __restric
   const int G = C / V, R = kBlock / G;
   const int g = int(threadIdx.x) % G, r0 = int(threadIdx.x) / G;
   const int c0 = g * V;
-  float mu[V], is[V], ww[V], bb[V];
+  float nm[V], is[V], ww[V], bb[V];   // xhat = v * is + nm, as bn_apply_kernel computes it
   if constexpr (BWD) {
 #pragma unroll
-    for (int i = 0; i < V; ++i) mu[i] = mean[c0 + i], is[i] = invstd[c0 + i], ww[i] = w[c0 + i], bb[i] = b[c0 + i];
+    for (int i = 0; i < V; ++i)
+      is[i] = invstd[c0 + i], nm[i] = -mean[c0 + i] * is[i], ww[i] = w[c0 + i], bb[i] = b[c0 + i];
   }
   float s[V], q[V];
 #pragma unroll
@@ -937,8 +938,8 @@ __global__ __launch_bounds__(kBlock) void bn_reduce_kernel(const void* __restric
       bn_load<DT>(gy, r * C + c0, gv);
 #pragma unroll
       for (int i = 0; i < V; ++i) {
-        const float xh = (v[i] - mu[i]) * is[i];
-        const float gz = (xh * ww[i] + bb[i]) > 0.f ? gv[i] : gv[i] * slope;
+        const float xh = fmaf(v[i], is[i], nm[i]);
+        const float gz = fmaf(xh, ww[i], bb[i]) > 0.f ? gv[i] : gv[i] * slope;
         s[i] += gz;
         q[i] += gz * xh;
       }
@@ -956,19 +957,25 @@ __global__ __launch_bounds__(kBlock) void bn_reduce_kernel(const void* __restric
     const float* pq = lq + (c % V) * LS + c / V;
     float a = 0.f, q2 = 0.f;
     for (int r = 0; r < R; ++r) a += ps[r * G], q2 += pq[r * G];
-    partial[int64_t(blockIdx.x) * 2 * C + c] = a;
-    partial[int64_t(blockIdx.x) * 2 * C + C + c] = q2;
+    // channel-major [2C][blocks]: the fold reads each channel's partials contiguously
+    partial[int64_t(c) * gridDim.x + blockIdx.x] = a;
+    partial[int64_t(C + c) * gridDim.x + blockIdx.x] = q2;
   }
 }
 
 // One block per channel folds the per-block partials (fp64, LDS tree); a
 // single lane per channel walking 1024 partials serially cost ~1 ms per step.
+// Partials are channel-major ([2C][nblocks]: sums, then sums of squares), so
+// the block's lanes read consecutive floats (the row-major layout cost one
+// cache-line request per partial).
 __device__ __forceinline__ void bn_fold(const float* __restrict__ partial, int nblocks, int C, int c, double& s,
                                         double& q) {
   __shared__ double ss[kBlock], qq[kBlock];
   double a = 0.0, b2 = 0.0;
-  for (int b = int(threadIdx.x); b < nblocks; b += kBlock)
-    a += partial[int64_t(b) * 2 * C + c], b2 += partial[int64_t(b) * 2 * C + C + c];
+  const float* ps = partial + int64_t(c) * nblocks;
+  const float* pq = partial + int64_t(C + c) * nblocks;
+#pragma unroll 4
+  for (int b = int(threadIdx.x); b < nblocks; b += kBlock) a += ps[b], b2 += pq[b];
   ss[threadIdx.x] = a;
   qq[threadIdx.x] = b2;
   __syncthreads();
@@ -1011,6 +1018,9 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_finalize_kernel(const float* __
 }
 
 // BWD = false: y = leaky(xhat * w + b).  BWD = true: gx = w * invstd * (gz - db/M - xhat * dw/M).
+// The grid-stride step is a multiple of kBlock and G = C / V divides kBlock,
+// so a lane keeps one channel group for the whole loop: its per-channel
+// coefficients are loaded once into registers, not per element.
 template <int DT, bool BWD>
 __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const void* __restrict__ x, const void* __restrict__ gy,
                                                           void* __restrict__ out, int64_t M, int C,
@@ -1023,8 +1033,23 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const void* __restrict
   const int G = C / V;
   const int64_t total = M * G;
   const float invM = 1.f / float(M);
+  const int c0 = (int(threadIdx.x) % G) * V;
+  // xhat = v * is + nm;  z = xhat * ww + bb;  backward: gx = P * (gz - dbm) - pdw * xhat
+  float is[V], nm[V], ww[V], bb[V], P[V], dbm[V], pdw[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int c = c0 + i;
+    is[i] = invstd[c];
+    nm[i] = -mean[c] * is[i];
+    ww[i] = w[c];
+    bb[i] = b[c];
+    if constexpr (BWD) {
+      P[i] = ww[i] * is[i];
+      dbm[i] = db[c] * invM;
+      pdw[i] = P[i] * dw[c] * invM;
+    }
+  }
   for (int64_t idx = int64_t(blockIdx.x) * kBlock + threadIdx.x; idx < total; idx += int64_t(gridDim.x) * kBlock) {
-    const int c0 = int(idx % G) * V;
     const int64_t e = idx * V;
     float v[V], o[V];
     bn_load<DT>(x, e, v);
@@ -1033,16 +1058,14 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const void* __restrict
       bn_load<DT>(gy, e, gv);
 #pragma unroll
       for (int i = 0; i < V; ++i) {
-        const int c = c0 + i;
-        const float xh = (v[i] - mean[c]) * invstd[c];
-        const float gz = (xh * w[c] + b[c]) > 0.f ? gv[i] : gv[i] * slope;
-        o[i] = w[c] * invstd[c] * (gz - db[c] * invM - xh * dw[c] * invM);
+        const float xh = fmaf(v[i], is[i], nm[i]);
+        const float gz = fmaf(xh, ww[i], bb[i]) > 0.f ? gv[i] : gv[i] * slope;
+        o[i] = fmaf(P[i], gz - dbm[i], -pdw[i] * xh);
       }
     } else {
 #pragma unroll
       for (int i = 0; i < V; ++i) {
-        const int c = c0 + i;
-        const float z = (v[i] - mean[c]) * invstd[c] * w[c] + b[c];
+        const float z = fmaf(fmaf(v[i], is[i], nm[i]), ww[i], bb[i]);
         o[i] = z > 0.f ? z : z * slope;
       }
     }

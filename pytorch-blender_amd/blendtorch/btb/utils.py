@@ -12,41 +12,35 @@ from mathutils import Vector
 
 def find_first_view3d():
     """``(area, space, region)`` of the first VIEW_3D area (widest WINDOW region)."""
-    areas = [a for a in bpy.context.screen.areas if a.type == 'VIEW_3D']
-    assert len(areas) > 0
-    area = areas[0]
-    region = max((r for r in area.regions if r.type == 'WINDOW'), key=lambda r: r.width)
-    spaces = [s for s in area.spaces if s.type == 'VIEW_3D']
-    assert len(spaces) > 0
-    return area, spaces[0], region
+    area = next((a for a in bpy.context.screen.areas if a.type == 'VIEW_3D'), None)
+    assert area is not None, 'no 3D view in the current screen'
+    space = next((s for s in area.spaces if s.type == 'VIEW_3D'), None)
+    assert space is not None, 'the 3D view area has no VIEW_3D space'
+    windows = [r for r in area.regions if r.type == 'WINDOW']
+    return area, space, max(windows, key=lambda r: r.width)
 
 
-def _eval(obj, depsgraph):
-    return obj.evaluated_get(depsgraph or bpy.context.evaluated_depsgraph_get())
+def _rows(objs, depsgraph, points):
+    """Stack ``points(evaluated_object)`` (an iterable of 3-vectors) over
+    ``objs``, evaluated after modifiers in ``depsgraph`` (default: the
+    context's)."""
+    dg = depsgraph or bpy.context.evaluated_depsgraph_get()
+    return np.stack([np.asarray(p) for o in objs for p in points(o.evaluated_get(dg))])
 
 
 def object_coordinates(*objs, depsgraph=None):
     """Nx3 local vertex coordinates of the evaluated objects."""
-    xyz = [np.asarray(v.co) for o in objs for v in _eval(o, depsgraph).data.vertices]
-    return np.stack(xyz)
+    return _rows(objs, depsgraph, lambda e: (v.co for v in e.data.vertices))
 
 
 def world_coordinates(*objs, depsgraph=None):
     """Nx3 world vertex coordinates (``matrix_world @ v.co``)."""
-    out = []
-    for o in objs:
-        e = _eval(o, depsgraph)
-        out.extend(np.asarray(e.matrix_world @ v.co) for v in e.data.vertices)
-    return np.stack(out)
+    return _rows(objs, depsgraph, lambda e: (e.matrix_world @ v.co for v in e.data.vertices))
 
 
 def bbox_world_coordinates(*objs, depsgraph=None):
     """8*len(objs) x 3 world coordinates of the objects' bounding boxes."""
-    out = []
-    for o in objs:
-        e = _eval(o, depsgraph)
-        out.extend(np.asarray(e.matrix_world @ Vector(c)) for c in e.bound_box)
-    return np.stack(out)
+    return _rows(objs, depsgraph, lambda e: (e.matrix_world @ Vector(c) for c in e.bound_box))
 
 
 def hom(x, v=1.):
@@ -71,22 +65,29 @@ def random_spherical_loc(radius_range=None, theta_range=None, phi_range=None):
 
 
 def compute_object_visibility(obj, cam, N=25, scene=None, view_layer=None, dist=None):
-    """Fraction of N random vertices of ``obj`` whose ray from the camera hits ``obj`` first."""
+    """Fraction of N random vertices of ``obj`` whose ray from the camera hits ``obj`` first.
+
+    Monte-Carlo estimate: a sampled vertex counts when it lies in front of
+    the camera (negative camera-space z) and the scene ray cast from the
+    camera origin towards it reports ``obj`` as the first hit."""
     scene = scene or bpy.context.scene
-    vl = view_layer or bpy.context.view_layer
-    src = cam.bpy_camera.matrix_world.translation
-    dist = dist or 1.70141e+38
-    caminv = cam.bpy_camera.matrix_world.inverted()
-    vis = 0
-    for idx in np.random.choice(len(obj.data.vertices), size=N):
-        dst_world = obj.matrix_world @ obj.data.vertices[idx].co
-        d = (dst_world - src).normalized()
-        dst_cam = caminv @ dst_world
-        if dst_cam.z <= 0. and np.isfinite(np.asarray(d)).all():
-            res, _, _, _, hit, _ = scene.ray_cast(vl, src, d, distance=dist)
-            if res and hit == obj:
-                vis += 1
-    return vis / N
+    layer = view_layer or bpy.context.view_layer
+    cam_world = cam.bpy_camera.matrix_world
+    origin, to_cam = cam_world.translation, cam_world.inverted()
+    max_dist = dist or 1.70141e+38
+
+    def visible(vertex_index):
+        target = obj.matrix_world @ obj.data.vertices[vertex_index].co
+        if (to_cam @ target).z > 0.:
+            return False                      # behind the camera
+        ray = (target - origin).normalized()
+        if not np.isfinite(np.asarray(ray)).all():
+            return False
+        hit, _loc, _normal, _face, first, _m = scene.ray_cast(layer, origin, ray, distance=max_dist)
+        return bool(hit) and first == obj
+
+    picks = np.random.choice(len(obj.data.vertices), size=N)
+    return sum(visible(i) for i in picks) / N
 
 
 def scene_stats():

@@ -6,7 +6,20 @@ running instances.  File-like objects work too (the reference's file-like
 branch referenced an un-imported ``nullcontext``; fixed here).
 """
 import json
-from contextlib import ExitStack, nullcontext
+from contextlib import contextmanager
+
+_SERIALISED = ('addresses', 'commands')
+
+
+@contextmanager
+def _stream(file, mode):
+    """Yield ``file`` itself when it is already a file object (left open),
+    otherwise the path opened in ``mode`` (closed on exit)."""
+    if hasattr(file, 'write' if 'w' in mode else 'read'):
+        yield file
+        return
+    with open(file, mode) as fp:
+        yield fp
 
 
 class LaunchInfo:
@@ -21,23 +34,22 @@ class LaunchInfo:
     def __repr__(self):
         return f'LaunchInfo(addresses={self.addresses!r}, commands={len(self.commands)} commands)'
 
-    @staticmethod
-    def _open(file, mode):
-        if hasattr(file, 'write' if 'w' in mode else 'read'):
-            return nullcontext(file)
-        return open(file, mode)
+    def to_dict(self):
+        """The JSON-serialisable part (no process handles)."""
+        return {k: getattr(self, k) for k in _SERIALISED}
+
+    @classmethod
+    def from_dict(cls, d):
+        return cls(*(d[k] for k in _SERIALISED))
 
     @staticmethod
     def save_json(file, launch_info):
         """Write addresses and commands as indented JSON to a path or file object."""
-        with ExitStack() as stack:
-            fp = stack.enter_context(LaunchInfo._open(file, 'w'))
-            json.dump({'addresses': launch_info.addresses, 'commands': launch_info.commands}, fp, indent=4)
+        with _stream(file, 'w') as fp:
+            json.dump(launch_info.to_dict(), fp, indent=4)
 
     @staticmethod
     def load_json(file):
         """Inverse of :meth:`save_json` (processes are not restored)."""
-        with ExitStack() as stack:
-            fp = stack.enter_context(LaunchInfo._open(file, 'r'))
-            data = json.load(fp)
-        return LaunchInfo(data['addresses'], data['commands'])
+        with _stream(file, 'r') as fp:
+            return LaunchInfo.from_dict(json.load(fp))

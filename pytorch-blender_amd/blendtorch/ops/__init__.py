@@ -846,7 +846,8 @@ def conv_fwd(x, w16, stats=None):
     [N, Cin, H, W] bf16 channels-last, ``w16`` [Cout, Cin, 4, 4] bf16
     channels-last; returns channels-last bf16 y.  ``stats`` (optional fp32
     tensor of ``conv_fwd_stats_rows(M) * 2 * Cout``) receives per-tile
-    BatchNorm sums of y (see :func:`batch_norm_from_stats`)."""
+    BatchNorm sums of y, channel-major: ``stats.view(2, Cout, rows)`` holds
+    the sums, then the sums of squares (see :func:`batch_norm_from_stats`)."""
     import torch
     ext = hip_ext()
     N, Cin, H, W = x.shape

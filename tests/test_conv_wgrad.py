@@ -115,7 +115,7 @@ def test_forward_matches_fp32_reference_and_stats(dev, N, Cin, H, W, Cout):
     assert y.is_contiguous(memory_format=cl) and y.dtype == torch.bfloat16
     # fp32 accumulation, one bf16 rounding: within one bf16 ulp of the fp32 result
     torch.testing.assert_close(y.float(), ref, rtol=2 ** -7, atol=1e-3 * float(ref.abs().max()))
-    st = stats.view(rows, 2, Cout).sum(0)
+    st = stats.view(2, Cout, rows).sum(-1)
     yf = y.float().permute(0, 2, 3, 1).reshape(-1, Cout)
     torch.testing.assert_close(st[0], yf.sum(0), rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(st[1], (yf * yf).sum(0), rtol=1e-4, atol=1e-3)
@@ -154,7 +154,7 @@ def test_first_layer_rgba_forward_and_wgrad(dev, N, H, W):
     ref = F.conv2d(x[:, :3].float(), w.float(), None, 2, 1)
     torch.testing.assert_close(y.float(), ref, rtol=2 ** -7, atol=1e-3 * float(ref.abs().max()))
     yf = y.float().permute(0, 2, 3, 1).reshape(-1, 32)
-    torch.testing.assert_close(stats.view(rows, 2, 32).sum(0)[0], yf.sum(0), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(stats.view(2, 32, rows).sum(-1)[0], yf.sum(0), rtol=1e-4, atol=1e-3)
     dy = torch.randn(N, 32, H // 2, W // 2, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
     for layout in (torch.contiguous_format, cl):
         out = torch.full((32, 3, 4, 4), float('nan'), device=dev).contiguous(memory_format=layout)

@@ -147,7 +147,8 @@ def test_discriminator_pool_runs_hip_kernel(dev):
     assert all(torch.isfinite(p.grad).all() for p in net.parameters())
 
 
-@pytest.mark.parametrize('shape', [(8, 32, 60, 80), (4, 256, 15, 20), (3, 64, 7, 9), (2, 128, 1, 1)])
+@pytest.mark.parametrize('shape', [(8, 32, 60, 80), (4, 256, 15, 20), (3, 64, 7, 9), (2, 128, 1, 1),
+                                   (8, 64, 120, 160), (2, 512, 6, 10)])
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('channels_last', [True, False])
 def test_batch_norm_leaky_relu(dev, shape, dtype, channels_last):
@@ -177,7 +178,14 @@ def test_batch_norm_leaky_relu(dev, shape, dtype, channels_last):
     assert torch.allclose(rm.cpu(), rmr, atol=1e-4, rtol=1e-4)
     assert torch.allclose(rv.cpu(), rvr, atol=1e-4, rtol=1e-4)
     gtol = 1e-3 if dtype == torch.float32 else 5e-2
-    assert torch.allclose(x.grad.float().cpu(), xr.grad, atol=gtol, rtol=gtol)
+    # elements at the LeakyReLU kink (pre-activation ~ 0) may take either
+    # slope: bf16 inputs repeat the same grid values thousands of times, so one
+    # value whose z rounds across 0 flips them all.  Compare the data gradient
+    # away from the kink (the flips still enter dw/db sums, within tolerance).
+    with torch.no_grad():
+        z = torch.nn.functional.batch_norm(xr.detach(), None, None, wr.detach(), br.detach(), training=True, eps=1e-5)
+    away = z.abs() > 1e-2
+    assert torch.allclose(x.grad.float().cpu()[away], xr.grad[away], atol=gtol, rtol=gtol)
     assert torch.allclose(w.grad.cpu(), wr.grad, atol=gtol * C, rtol=gtol)
     assert torch.allclose(b.grad.cpu(), br.grad, atol=gtol * C, rtol=gtol)
 
