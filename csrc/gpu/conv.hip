@@ -499,6 +499,7 @@ struct TapGemm {
   int GH = 0, GW = 0, M = 0;       // GEMM rows: m = (n * GH + a) * GW + b
   int NOUT = 0, OH = 0, OW = 0;    // dst [N][OH][OW][NOUT]
   int wc = 0;                      // C4 mode: weight input channels (3 or 4)
+  BnBwdFuse bn;                    // data gradient only: BN backward statistics in the epilogue (bn.part nullable)
 };
 
 // BN = output channels per block (64, or 32 for 32-channel outputs such as
@@ -693,6 +694,16 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     __syncthreads();   // the epilogue reuses the staging LDS
   }
 
+  // BN-backward fusion (below): issue the BN input loads now, so their
+  // latency hides under the epilogue's LDS round trip
+  const bool bnf = DGRAD && p.bn.part != nullptr;
+  uint4 xpre[4];
+  if (bnf && ac < BN / 8) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      xpre[j] = pin[j] ? *reinterpret_cast<const uint4*>(p.bn.x + obase[j] + n0 + ac * 8) : make_uint4(0, 0, 0, 0);
+  }
+
   // epilogue: round to bf16 (RNE) into an LDS tile [FBM][BN] (128-byte row
   // pitch, same swizzle), sum the rounded values per channel (forward), then
   // 16-byte stores of whole row chunks
@@ -735,12 +746,70 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     }
   }
   __syncthreads();
+  // data gradient feeding a BatchNorm+LeakyReLU backward (p.bn.part): the
+  // stored gradient IS that backward's gy.  Per channel, sum gz and gz * xhat
+  // over this tile (gz = gy * leaky'(z), z = xhat * w + b, xhat from the BN's
+  // saved input at the same offsets) -- the reduction pass over gy and x the
+  // BN backward would otherwise make.
+  float bs[8], bq[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) bs[q] = bq[q] = 0.f;
   if (ac < BN / 8) {
+    float is[8], nm[8], ww[8], bb[8];
+    if (bnf) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int c = n0 + ac * 8 + q;
+        is[q] = p.bn.invstd[c];
+        nm[q] = -p.bn.mean[c] * is[q];
+        ww[q] = p.bn.w[c];
+        bb[q] = p.bn.b[c];
+      }
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (!pin[j]) continue;
       const uint4 v = *reinterpret_cast<const uint4*>(smem + st_a + j * 32 * F_ROW);
       *reinterpret_cast<uint4*>(p.dst + obase[j] + n0 + ac * 8) = v;
+      if (bnf) {
+        const uint4 xv = xpre[j];
+        const uint32_t gw[4] = {v.x, v.y, v.z, v.w}, xw[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const uint32_t gb = q & 1 ? gw[q >> 1] & 0xFFFF0000u : gw[q >> 1] << 16;
+          const uint32_t xb = q & 1 ? xw[q >> 1] & 0xFFFF0000u : xw[q >> 1] << 16;
+          const float xh = fmaf(__uint_as_float(xb), is[q], nm[q]);
+          const float g = __uint_as_float(gb);
+          const float gz = fmaf(xh, ww[q], bb[q]) > 0.f ? g : g * p.bn.slope;
+          bs[q] += gz;
+          bq[q] += gz * xh;
+        }
+      }
+    }
+  }
+  if (bnf) {
+    // lanes l, l^8, l^16, ... (same ac) hold the same channels: fold them,
+    // then the 4 waves through LDS (the statistics area is free in backward)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+#pragma unroll
+      for (int o = 8; o < 64; o <<= 1) bs[q] += __shfl_xor(bs[q], o), bq[q] += __shfl_xor(bq[q], o);
+    }
+    if (lane < 8 && ac < BN / 8) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        red[(wave * 2 + 0) * BN + ac * 8 + q] = bs[q];
+        red[(wave * 2 + 1) * BN + ac * 8 + q] = bq[q];
+      }
+    }
+    __syncthreads();
+    if (t < 2 * BN) {
+      const int which = t / BN, c = t - which * BN;
+      float v = 0.f;
+#pragma unroll
+      for (int w4 = 0; w4 < 4; ++w4) v += red[(w4 * 2 + which) * BN + c];
+      // channel-major [2][NOUT][rows], row = (pixel tile, parity class)
+      p.bn.part[(which * p.NOUT + n0 + c) * p.bn.rows + mt * int(gridDim.y) + int(blockIdx.y)] = v;
     }
   }
   if (!DGRAD && p.stats && t < 2 * BN) {
@@ -896,8 +965,10 @@ hipError_t conv_weight_t_multi(const WeightTParams& p, hipStream_t stream) {
   return hipGetLastError();
 }
 
+int64_t conv_dgrad_bn_rows(int N, int H, int W) { return conv_fwd_tiles(int64_t(N) * (H / 2) * (W / 2)) * 4; }
+
 hipError_t conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int N, int H, int W, int Cin, int Cout,
-                      hipStream_t stream) {
+                      hipStream_t stream, const BnBwdFuse* bn) {
   if (!conv_dgrad_supported(Cin, Cout) || !dy || !wt || !dx || H % 2 || W % 2) return hipErrorInvalidValue;
   if ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(wt) | reinterpret_cast<uintptr_t>(dx)) & 15)
     return hipErrorInvalidValue;
@@ -909,6 +980,12 @@ hipError_t conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int 
   g.N = N, g.SH = Ho, g.SW = Wo, g.C = Cout, g.cshift = ilog2_exact(Cout);
   g.GH = Ho, g.GW = Wo, g.M = N * Ho * Wo;   // one parity class: every (a, b)
   g.NOUT = Cin, g.OH = H, g.OW = W;
+  if (bn && bn->part) {
+    if (!bn->x || !bn->mean || !bn->invstd || !bn->w || !bn->b || bn->rows != conv_dgrad_bn_rows(N, H, W) ||
+        (reinterpret_cast<uintptr_t>(bn->x) & 15))
+      return hipErrorInvalidValue;
+    g.bn = *bn;
+  }
   launch_tap_gemm<true>(g, 4, stream);
   return hipGetLastError();
 }

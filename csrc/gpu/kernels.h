@@ -181,6 +181,8 @@ hipError_t bn_bwd_reduce(const void* x, const void* gy, int64_t M, int C, int dt
                          const float* invstd, const float* w, const float* b, float slope, float* partial,
                          hipStream_t stream);
 hipError_t bn_bwd_finalize(const float* partial, int64_t M, int C, int dtype, float* dw, float* db, hipStream_t stream);
+// bn_bwd_finalize over `rows` channel-major partials produced elsewhere (conv_dgrad's BnBwdFuse epilogue)
+hipError_t bn_bwd_finalize_rows(const float* partial, int rows, int C, float* dw, float* db, hipStream_t stream);
 hipError_t bn_bwd_apply(const void* x, const void* gy, void* gx, int64_t M, int C, int dtype, const float* mean,
                         const float* invstd, const float* w, const float* b, const float* dw, const float* db,
                         float slope, hipStream_t stream);
@@ -284,8 +286,24 @@ struct WeightTParams {   // conv_weight_t for several weights in one launch
   int n = 0;
 };
 hipError_t conv_weight_t_multi(const WeightTParams& p, hipStream_t stream);
+// bn (nullable, part != null to enable): dx is the gy of a BatchNorm+LeakyReLU
+// backward whose saved input x ([N][H][W][Cin] bf16), batch mean / invstd,
+// affine w / b (fp32 [Cin]) and slope are given; the epilogue writes that
+// backward's per-tile sums of gz and gz * xhat, channel-major
+// [2][Cin][conv_dgrad_bn_rows(N, H, W)] fp32, for bn_backward_from_stats.
+struct BnBwdFuse {
+  const uint16_t* x = nullptr;
+  const float* mean = nullptr;
+  const float* invstd = nullptr;
+  const float* w = nullptr;
+  const float* b = nullptr;
+  float slope = 0.f;
+  float* part = nullptr;
+  int rows = 0;
+};
+int64_t conv_dgrad_bn_rows(int N, int H, int W);
 hipError_t conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int N, int H, int W, int Cin, int Cout,
-                      hipStream_t stream);
+                      hipStream_t stream, const BnBwdFuse* bn = nullptr);
 // bn_finalize over `nblocks` partial rows produced elsewhere (conv_fwd's epilogue)
 hipError_t bn_finalize_rows(const float* partial, int nblocks, int64_t M, int C, float eps, float momentum,
                             float* mean, float* invstd, float* running_mean, float* running_var, hipStream_t stream,

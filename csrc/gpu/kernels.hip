@@ -1175,6 +1175,12 @@ hipError_t bn_bwd_finalize(const float* partial, int64_t M, int C, int dtype, fl
   return hipGetLastError();
 }
 
+hipError_t bn_bwd_finalize_rows(const float* partial, int rows, int C, float* dw, float* db, hipStream_t stream) {
+  if (rows <= 0 || C <= 0 || !partial || !dw || !db) return hipErrorInvalidValue;
+  bn_bwd_finalize_kernel<<<C, kBlock, 0, stream>>>(partial, rows, C, dw, db);
+  return hipGetLastError();
+}
+
 hipError_t bn_bwd_apply(const void* x, const void* gy, void* gx, int64_t M, int C, int dtype, const float* mean,
                         const float* invstd, const float* w, const float* b, const float* dw, const float* db,
                         float slope, hipStream_t stream) {

@@ -255,12 +255,41 @@ PYBIND11_MODULE(_hip, m) {
     }
     check(conv_weight_t_multi(p, stream_of(stream)), "conv_weight_t_multi");
   });
-  m.def("conv_dgrad", [](uintptr_t dy, uintptr_t wt, uintptr_t dx, int N, int H, int W, int Cin, int Cout,
-                         uintptr_t stream) {
-    check(conv_dgrad(ptr<const uint16_t>(dy), ptr<const uint16_t>(wt), ptr<uint16_t>(dx), N, H, W, Cin, Cout,
-                     stream_of(stream)),
-          "conv_dgrad");
-  });
+  m.def(
+      "conv_dgrad",
+      [](uintptr_t dy, uintptr_t wt, uintptr_t dx, int N, int H, int W, int Cin, int Cout, uintptr_t stream,
+         uintptr_t bn_x, uintptr_t bn_mean, uintptr_t bn_invstd, uintptr_t bn_w, uintptr_t bn_b, float bn_slope,
+         uintptr_t bn_part, int bn_rows) {
+        BnBwdFuse bn;
+        bn.x = ptr<const uint16_t>(bn_x);
+        bn.mean = ptr<const float>(bn_mean);
+        bn.invstd = ptr<const float>(bn_invstd);
+        bn.w = ptr<const float>(bn_w);
+        bn.b = ptr<const float>(bn_b);
+        bn.slope = bn_slope;
+        bn.part = ptr<float>(bn_part);
+        bn.rows = bn_rows;
+        check(conv_dgrad(ptr<const uint16_t>(dy), ptr<const uint16_t>(wt), ptr<uint16_t>(dx), N, H, W, Cin, Cout,
+                         stream_of(stream), bn_part ? &bn : nullptr),
+              "conv_dgrad");
+      },
+      py::arg("dy"), py::arg("wt"), py::arg("dx"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("Cin"),
+      py::arg("Cout"), py::arg("stream"), py::arg("bn_x") = 0, py::arg("bn_mean") = 0, py::arg("bn_invstd") = 0,
+      py::arg("bn_w") = 0, py::arg("bn_b") = 0, py::arg("bn_slope") = 0.f, py::arg("bn_part") = 0,
+      py::arg("bn_rows") = 0);
+  m.def("conv_dgrad_bn_rows", &conv_dgrad_bn_rows);
+  m.def("bn_backward_from_stats",
+        [](uintptr_t x, uintptr_t gy, uintptr_t gx, int64_t M, int C, int dtype, uintptr_t part, int rows,
+           uintptr_t mean, uintptr_t invstd, uintptr_t w, uintptr_t b, uintptr_t dw, uintptr_t db, float slope,
+           uintptr_t stream) {
+          hipStream_t s = stream_of(stream);
+          check(bn_bwd_finalize_rows(ptr<const float>(part), rows, C, ptr<float>(dw), ptr<float>(db), s),
+                "bn_bwd_finalize_rows");
+          check(bn_bwd_apply(ptr<const void>(x), ptr<const void>(gy), ptr<void>(gx), M, C, dtype,
+                             ptr<const float>(mean), ptr<const float>(invstd), ptr<const float>(w),
+                             ptr<const float>(b), ptr<const float>(dw), ptr<const float>(db), slope, s),
+                "bn_bwd_apply");
+        });
   m.def("conv_fwd",
         [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, int N, int H, int W, int Cin, int Ho, int Wo,
            int Cout, uintptr_t stream, int w_channels) {

@@ -115,7 +115,7 @@ class Discriminator(nn.Module):
             if need:
                 wts = dict(zip(need, ops.conv_weights_t([w16s[k] for k in need])))
         ci = -1
-        stats = None
+        stats = link = None
         for i, m in enumerate(layers):
             if isinstance(m, nn.Conv2d):
                 w16 = next(weights)
@@ -125,16 +125,22 @@ class Discriminator(nn.Module):
                     nxt = layers[i + 1] if i + 1 < len(layers) else None
                     fuse = (isinstance(nxt, ops.BatchNormLeakyReLU2d) and ops.conv_fwd_supported(x, w16)
                             and nxt.fused_with_stats(x.new_empty((1, m.out_channels, 1, 1))))
+                    # the BN that produced x: this conv's data gradient does its backward reduction
+                    bl, link = link, None
                     if fuse:   # BN statistics come out of the conv kernel's epilogue
-                        x, stats = ops.conv4x4s2(x, m.weight, w16, with_stats=True, wt=wts.get(ci))
+                        x, stats = ops.conv4x4s2(x, m.weight, w16, with_stats=True, wt=wts.get(ci), bn_link=bl)
                     else:
-                        x = ops.conv4x4s2(x, m.weight, w16, wt=wts.get(ci))
+                        x = ops.conv4x4s2(x, m.weight, w16, wt=wts.get(ci), bn_link=bl)
                 else:
+                    link = None
                     x = F.conv2d(x, w16, None, m.stride, m.padding, m.dilation, m.groups)
             elif stats is not None and isinstance(m, ops.BatchNormLeakyReLU2d):
-                x = m.forward_from_stats(x, stats)
+                link = ops.BnLink() if torch.is_grad_enabled() else None
+                x = m.forward_from_stats(x, stats, link)
                 stats = None
             else:
+                if not isinstance(m, nn.Identity):
+                    link = None
                 x = m(x)
         return x
 

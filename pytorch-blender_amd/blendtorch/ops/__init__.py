@@ -640,13 +640,45 @@ def cast_bf16(*tensors):
 # ---------------------------------------------------------------------------
 # consumer-model op: training BatchNorm2d fused with LeakyReLU (channels-last)
 
+class BnLink:
+    """Hand-off between a training :class:`BatchNormLeakyReLU2d` and the
+    convolution that consumes its output (:func:`conv4x4s2` ``bn_link=``).
+
+    The BN forward records what its backward needs (its input ``x``, batch
+    ``mean``/``invstd``, affine ``w``/``b``, ``slope``).  The convolution's
+    backward, which runs first, computes the BN's gy as its data gradient and
+    has the MFMA kernel's epilogue sum gz and gz * xhat per tile into
+    ``part``; the BN backward then only finalizes and applies (one pass over
+    the activation fewer).  ``part`` is consumed once."""
+    __slots__ = ('x', 'mean', 'invstd', 'w', 'b', 'slope', 'part', 'rows', 'gy')
+
+    def __init__(self):
+        self.x = self.mean = self.invstd = self.w = self.b = self.part = self.gy = None
+        self.slope, self.rows = 0.0, 0
+
+    def ready(self, dx):
+        """True when the recorded BN input matches ``dx`` (shape, bf16 NHWC)."""
+        import torch
+        x = self.x
+        return (x is not None and x.dtype == torch.bfloat16 and dx.dtype == torch.bfloat16
+                and tuple(x.shape) == (dx.shape[0], dx.shape[2], dx.shape[3], dx.shape[1]) and x.is_contiguous())
+
+    def take(self, gys):
+        """The epilogue partials, if they were computed for exactly ``gys``."""
+        part, rows, gy = self.part, self.rows, self.gy
+        self.part = self.gy = None
+        if part is None or gy is None or gys.data_ptr() != gy.data_ptr():
+            return None, 0
+        return part, rows
+
+
 def _bn_function():
     import torch
 
     class _BatchNormLeakyReLU(torch.autograd.Function):
         @staticmethod
         def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, slope, tracked=None,
-                    stats=None):
+                    stats=None, link=None):
             ext = hip_ext()
             N, C, H, W = x.shape
             M = N * H * W
@@ -675,6 +707,10 @@ def _bn_function():
                                _stream(x.device), tr)
             ctx.save_for_backward(xs, w, b, mean, invstd)
             ctx.slope = float(slope)
+            ctx.link = link
+            if link is not None:
+                link.x, link.mean, link.invstd, link.w, link.b, link.slope = xs, mean, invstd, w, b, float(slope)
+                link.part = link.gy = None
             return y.permute(0, 3, 1, 2)
 
         @staticmethod
@@ -688,12 +724,20 @@ def _bn_function():
             gx = torch.empty_like(xs)
             dw = torch.empty(C, dtype=torch.float32, device=xs.device)
             db = torch.empty_like(dw)
-            part = torch.empty(ext.bn_partial_floats(M, C, dt), dtype=torch.float32, device=xs.device)
-            _count('bn_backward')
-            ext.bn_backward(xs.data_ptr(), gys.data_ptr(), gx.data_ptr(), M, C, dt, part.data_ptr(), mean.data_ptr(),
-                            invstd.data_ptr(), w.data_ptr(), b.data_ptr(), dw.data_ptr(), db.data_ptr(), ctx.slope,
-                            _stream(xs.device))
-            return gx.permute(0, 3, 1, 2), dw, db, None, None, None, None, None, None, None
+            part, rows = ctx.link.take(gys) if ctx.link is not None else (None, 0)
+            if part is not None:
+                # the consuming convolution's data-gradient epilogue already summed gz, gz * xhat
+                _count('bn_backward_from_stats')
+                ext.bn_backward_from_stats(xs.data_ptr(), gys.data_ptr(), gx.data_ptr(), M, C, dt, part.data_ptr(),
+                                           rows, mean.data_ptr(), invstd.data_ptr(), w.data_ptr(), b.data_ptr(),
+                                           dw.data_ptr(), db.data_ptr(), ctx.slope, _stream(xs.device))
+            else:
+                part = torch.empty(ext.bn_partial_floats(M, C, dt), dtype=torch.float32, device=xs.device)
+                _count('bn_backward')
+                ext.bn_backward(xs.data_ptr(), gys.data_ptr(), gx.data_ptr(), M, C, dt, part.data_ptr(),
+                                mean.data_ptr(), invstd.data_ptr(), w.data_ptr(), b.data_ptr(), dw.data_ptr(),
+                                db.data_ptr(), ctx.slope, _stream(xs.device))
+            return gx.permute(0, 3, 1, 2), dw, db, None, None, None, None, None, None, None, None
 
     return _BatchNormLeakyReLU
 
@@ -730,8 +774,8 @@ def batch_norm_leaky_relu(x, weight, bias, running_mean=None, running_var=None, 
 
 
 def _bn_apply_unchecked(x, weight, bias, running_mean, running_var, eps, momentum, slope, tracked=None,
-                        stats=None):
-    return _BN_FN.apply(x, weight, bias, running_mean, running_var, eps, momentum, slope, tracked, stats)
+                        stats=None, link=None):
+    return _BN_FN.apply(x, weight, bias, running_mean, running_var, eps, momentum, slope, tracked, stats, link)
 
 
 def reference_batch_norm_leaky_relu(x, weight, bias, running_mean=None, running_var=None, eps=1e-5, momentum=0.1,
@@ -775,15 +819,18 @@ def _bn_module():
             return (self.training and self.affine and self.track_running_stats and self.momentum is not None
                     and bn_supported(x))
 
-        def forward_from_stats(self, x, stats):
+        def forward_from_stats(self, x, stats, link=None):
             """Training forward with the batch statistics already summed by
             the producing kernel (``conv_fwd``'s epilogue rows, see
-            :func:`conv4x4s2`): finalize + apply only."""
+            :func:`conv4x4s2`): finalize + apply only.  ``link``: a
+            :class:`BnLink` shared with the convolution that consumes the
+            output (its data-gradient epilogue then does this op's backward
+            reduction)."""
             global _BN_FN
             if _BN_FN is None:
                 _BN_FN = _bn_function()
             return _bn_apply_unchecked(x, self.weight, self.bias, self.running_mean, self.running_var, self.eps,
-                                       self.momentum, self.slope, self.num_batches_tracked, stats)
+                                       self.momentum, self.slope, self.num_batches_tracked, stats, link)
 
         def extra_repr(self):
             return super().extra_repr() + f', slope={self.slope}'
@@ -885,11 +932,16 @@ def conv_weights_t(weights):
     return outs
 
 
-def conv_dgrad(dy, w16, in_shape, wt=None):
+def conv_dgrad(dy, w16, in_shape, wt=None, bn=None):
     """Data gradient of :func:`conv_fwd` on the same MFMA kernel (four
     stride-2 parity classes, 4 taps each): ``dy`` [N, Cout, H/2, W/2] bf16
     channels-last, ``w16`` [Cout, Cin, 4, 4] bf16 channels-last -> dx
-    [N, Cin, H, W] bf16 channels-last."""
+    [N, Cin, H, W] bf16 channels-last.
+
+    ``bn`` (a :class:`BnLink` whose BatchNorm+LeakyReLU produced this
+    convolution's input): dx is that BN backward's gy, and the kernel's
+    epilogue also writes the BN backward's per-tile sums (``bn.part``), so the
+    BN backward skips its reduction pass."""
     import torch
     ext = hip_ext()
     N, Cin, H, W = in_shape
@@ -906,7 +958,16 @@ def conv_dgrad(dy, w16, in_shape, wt=None):
         raise ValueError('conv_dgrad: wt is not this weight\'s transpose (conv_weights_t)')
     dx = torch.empty((N, Cin, H, W), dtype=torch.bfloat16, device=dy.device, memory_format=cl)
     _count('conv_dgrad')
-    ext.conv_dgrad(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), N, H, W, Cin, Cout, _stream(dy.device))
+    if bn is not None and bn.ready(dx):
+        rows = int(ext.conv_dgrad_bn_rows(N, H, W))
+        part = torch.empty(2 * Cin * rows, dtype=torch.float32, device=dy.device)
+        _count('conv_dgrad_bn')
+        ext.conv_dgrad(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), N, H, W, Cin, Cout, _stream(dy.device),
+                       bn.x.data_ptr(), bn.mean.data_ptr(), bn.invstd.data_ptr(), bn.w.data_ptr(), bn.b.data_ptr(),
+                       bn.slope, part.data_ptr(), rows)
+        bn.part, bn.rows, bn.gy = part, rows, dx
+    else:
+        ext.conv_dgrad(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), N, H, W, Cin, Cout, _stream(dy.device))
     return dx
 
 
@@ -943,10 +1004,10 @@ def _conv_function():
         into the master weight's gradient (no bf16 round trip, no cast)."""
 
         @staticmethod
-        def forward(ctx, x, w32, w16, with_stats=False, wt=None):
+        def forward(ctx, x, w32, w16, with_stats=False, wt=None, bn_link=None):
             ctx.set_materialize_grads(False)   # no zero-filled gradient for the stats output
             ctx.save_for_backward(x, w16)
-            ctx.w32, ctx.wt = w32, wt
+            ctx.w32, ctx.wt, ctx.bn_link = w32, wt, bn_link
             if with_stats:
                 N, _, H, W = x.shape
                 M = N * ((H - 2) // 2 + 1) * ((W - 2) // 2 + 1)
@@ -964,12 +1025,12 @@ def _conv_function():
         def backward(ctx, gy, gstats=None):
             x, w16 = ctx.saved_tensors
             if gy is None:
-                return None, None, None, None, None
+                return None, None, None, None, None, None
             gy = gy.contiguous(memory_format=torch.channels_last)
             gx = gw = None
             if ctx.needs_input_grad[0]:
                 if conv_dgrad_supported(x, w16):
-                    gx = conv_dgrad(gy, w16, tuple(x.shape), ctx.wt)
+                    gx = conv_dgrad(gy, w16, tuple(x.shape), ctx.wt, ctx.bn_link)
                 else:
                     wfull = w16
                     if w16.shape[1] != x.shape[1]:   # RGBA-fed RGB weight: zero weight on the extra channel
@@ -979,7 +1040,7 @@ def _conv_function():
                                                              [0, 0], 1, [True, False, False])[0]
             if ctx.needs_input_grad[1]:
                 gw = conv_wgrad(x, gy, torch.empty_like(ctx.w32))
-            return gx, gw, None, None, None
+            return gx, gw, None, None, None, None
 
     return _Conv4x4s2
 
@@ -987,18 +1048,20 @@ def _conv_function():
 _CONV_FN = None
 
 
-def conv4x4s2(x, w32, w16, with_stats=False, wt=None):
+def conv4x4s2(x, w32, w16, with_stats=False, wt=None, bn_link=None):
     """4x4 / stride-2 / pad-1 convolution of bf16 channels-last ``x`` with the
     bf16 copy ``w16`` of fp32 weight ``w32``; the gradient goes to ``w32``
     (fp32, from the MFMA weight-gradient kernel).  See :func:`conv_wgrad_supported`.
     ``with_stats``: return ``(y, stats)``, the per-tile BatchNorm sums of y
-    from the forward kernel's epilogue (for ``BatchNormLeakyReLU2d.forward_from_stats``)."""
+    from the forward kernel's epilogue (for ``BatchNormLeakyReLU2d.forward_from_stats``).
+    ``bn_link``: the :class:`BnLink` of the BatchNorm+LeakyReLU that produced
+    ``x``; the data gradient then also computes that BN's backward sums."""
     global _CONV_FN
     if _CONV_FN is None:
         _CONV_FN = _conv_function()
     if with_stats and not conv_fwd_supported(x, w16):
         raise ValueError('conv4x4s2(with_stats=True) needs the MFMA forward (see conv_fwd_supported)')
-    return _CONV_FN.apply(x, w32, w16.detach(), with_stats, wt)
+    return _CONV_FN.apply(x, w32, w16.detach(), with_stats, wt, bn_link)
 
 
 # ---------------------------------------------------------------------------

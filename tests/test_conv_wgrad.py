@@ -182,3 +182,25 @@ def test_discriminator_rgba_input_equals_rgb(dev):
     for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
         ga, gb = pa.grad.flatten().double(), pb.grad.flatten().double()
         assert float(ga @ gb / (ga.norm() * gb.norm())) > 0.99, n
+
+
+@pytest.mark.gpu
+def test_bn_backward_sums_from_dgrad_epilogue(dev, monkeypatch):
+    """A BN+LeakyReLU whose output feeds an MFMA conv takes its backward sums
+    from that conv's data-gradient epilogue (BnLink): same gradients as the
+    separate reduction pass, on the bench's RGBA-fed layer stack."""
+    from blendtorch.models import Discriminator
+    torch.manual_seed(3)
+    a = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=torch.channels_last)
+    b = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=torch.channels_last)
+    b.load_state_dict(a.state_dict())
+    x = torch.rand(4, 4, 96, 128, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    before = ops.KERNEL_CALLS.get('bn_backward_from_stats', 0)
+    a.bce_loss_bf16(x, 1.0).backward()
+    # BN1..BN3 feed conv2..conv4 (BN4 feeds the head)
+    assert ops.KERNEL_CALLS.get('bn_backward_from_stats', 0) == before + 3
+    monkeypatch.setattr(ops.BnLink, 'ready', lambda self, dx: False)
+    b.bce_loss_bf16(x, 1.0).backward()
+    assert ops.KERNEL_CALLS.get('bn_backward_from_stats', 0) == before + 3
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        torch.testing.assert_close(pa.grad, pb.grad, rtol=2e-2, atol=2e-2 * float(pb.grad.abs().max()), msg=n)
