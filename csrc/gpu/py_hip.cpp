@@ -561,8 +561,15 @@ PYBIND11_MODULE(_hip, m) {
           p.lut = lut;
           p.B = B, p.H = H, p.W = W, p.Cin = Cin, p.Cout = 3;
           p.max_grid = max_grid;
+          // "hybrid:<n>": the first n frames of a batch are read over PCIe by the
+          // decode kernel itself, the rest are DMA'd to staging first (both
+          // paths pulling over the link at once)
+          const bool hybrid = mode.rfind("hybrid:", 0) == 0;
+          const int ndirect = hybrid ? std::max(0, std::min(B, std::stoi(mode.substr(7)))) : 0;
           const bool direct = mode == "direct";
-          if (direct) {
+          if (hybrid) {
+            p.nsrcs = B;
+          } else if (direct) {
             p.nsrcs = B;
             for (int b = 0; b < B; ++b) p.srcs[b] = dev_host + size_t(b) * slot;
           } else {
@@ -572,10 +579,12 @@ PYBIND11_MODULE(_hip, m) {
             if (rewrite)
               for (int b = 0; b < B; ++b) host[size_t(b) * slot] = uint8_t(it);   // fresh content per batch
             uint8_t* st = (pipelined && (it & 1)) ? stage2 : stage;
+            if (hybrid)
+              for (int b = 0; b < B; ++b) p.srcs[b] = b < ndirect ? dev_host + size_t(b) * slot : st + size_t(b) * img;
             if (!direct) {
               p.src = st;
               for (int k = 1; k < K; ++k) check(hipStreamWaitEvent(cs[size_t(k)], kdone, 0), "wait");   // staging free
-              for (int b = 0; b < B; ++b)
+              for (int b = ndirect; b < B; ++b)
                 check(hipMemcpyAsync(st + size_t(b) * img, host + size_t(b) * slot, img, hipMemcpyHostToDevice,
                                      cs[size_t(b % K)]),
                       "memcpy");
