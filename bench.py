@@ -129,6 +129,9 @@ def parse_args(argv=None):
                     help='copy path: HIP streams a batch\'s frame copies are spread over (several DMA engines); '
                          'default 2, or 1 for the disc consumer (it needs ~12 GB/s, and one DMA stream '
                          'disturbs its step least: 9.72k vs 9.59k img/s, profiles/r2/host_sync.txt)')
+    ap.add_argument('--prefetch', type=int, default=None,
+                    help='output buffers posted to the loader (batches assembled/decoding/ready ahead of the consumer); '
+                         'default 16, or 6 for the disc consumer')
     ap.add_argument('--launch-depth', type=int, default=2,
                     help='direct-path decode launches queued before new batches coalesce into one launch')
     ap.add_argument('--backend', choices=['nccl', 'gloo'], default='nccl',
@@ -165,6 +168,8 @@ def parse_args(argv=None):
     args = ap.parse_args(argv)
     if args.h2d is None:
         args.h2d = 'copy' if args.consumer == 'disc' else 'auto'
+    if args.prefetch is None:
+        args.prefetch = 6 if args.consumer == 'disc' else 16
     return args
 
 
@@ -348,7 +353,7 @@ def main(argv=None):
                     # decode runs inside the captured training step
                     ldec = DecodeConfig.raw(channels=args.mode)
                 dl = DeviceLoader(addrs, batch_size=per_step, decode=ldec, device=device,
-                                  max_items=total_batches * per_step, prefetch=6,
+                                  max_items=total_batches * per_step, prefetch=args.prefetch,
                                   io_threads=args.io_threads or None, timeoutms=60000, h2d=args.h2d,
                                   launch_depth=args.launch_depth,
                                   copy_streams=copy_streams,
@@ -526,7 +531,7 @@ def main(argv=None):
                 'pinned_producers': pin,
                 'shm_slots': shm_slots,
                 'h2d': args.h2d,
-                'launch_depth': args.launch_depth,
+                'launch_depth': args.launch_depth, 'prefetch': args.prefetch,
                 'copy_streams': copy_streams if args.h2d == 'copy' else None,
                 'codec': args.codec if shm_slots else 'none',
                 'consumer_step': stepper.state if stepper is not None else None,
