@@ -76,10 +76,14 @@ def _run(cmd, verbose):
 
 def _compile(compiler, src: Path, obj: Path, flags, verbose):
     deps = [src] + _headers()
-    if not _newer(obj, deps):
+    # the command line is part of the object's identity: a flag change rebuilds
+    stamp = obj.with_suffix('.cmd')
+    cmd = ' '.join(str(a) for a in [compiler, *flags])
+    if not _newer(obj, deps) and stamp.exists() and stamp.read_text() == cmd:
         return obj
     obj.parent.mkdir(parents=True, exist_ok=True)
     _run([compiler, *flags, '-c', src, '-o', obj], verbose)
+    stamp.write_text(cmd)
     return obj
 
 
@@ -127,9 +131,11 @@ def build_hip(verbose=False, jobs=8):
     gpu_srcs = sorted((CSRC / 'gpu').glob('*.hip')) + sorted((CSRC / 'gpu').glob('*.cpp'))
     if not gpu_srcs:
         return None
+    # MFMA accumulators in VGPRs (gfx950 allows either file): in the unrolled
+    # MFMA loops the AGPR form left accumulator copies between the files
     hflags = ['-std=c++17', '-O3', '-fPIC', f'--offload-arch={HIP_ARCH}', '-Wall',
               '-Wno-unused-parameter', '-Wno-unused-result', '-mcode-object-version=5',
-              '-D__HIP_PLATFORM_AMD__'] + _py_includes()
+              '-mllvm', '-amdgpu-mfma-vgpr-form=1'] + _py_includes()
     cxx = os.environ.get('CXX', 'g++')
     cflags = CXXFLAGS
     with ThreadPoolExecutor(jobs) as ex:
