@@ -138,13 +138,32 @@ struct Group {
   const uint8_t* src;    // first source byte (flip applied)
 };
 
+// (image, first pixel, row, column) of pixel group g.  32-bit division when
+// the launch's group count fits (every real frame batch): a 64-bit divide is a
+// ~100-instruction sequence, two per lane and group.
+template <int PPT>
+__device__ __forceinline__ void split_group(int64_t g, int64_t groups_per_img, int W, bool small, int& b, int64_t& q,
+                                            int& y, int& x) {
+  if (small) {
+    const uint32_t g32 = uint32_t(g), gpi = uint32_t(groups_per_img);
+    const uint32_t b32 = g32 / gpi;
+    const uint32_t q32 = (g32 - b32 * gpi) * uint32_t(PPT);
+    const uint32_t y32 = q32 / uint32_t(W);
+    b = int(b32), q = int64_t(q32), y = int(y32), x = int(q32 - y32 * uint32_t(W));
+  } else {
+    b = int(g / groups_per_img);
+    q = (g - int64_t(b) * groups_per_img) * PPT;
+    y = int(q / W);
+    x = int(q - int64_t(y) * W);
+  }
+}
+
 template <int PPT, int CIN>
-__device__ __forceinline__ Group locate(const DecodeParams& p, int64_t g, int64_t groups_per_img, int64_t HW) {
+__device__ __forceinline__ Group locate(const DecodeParams& p, int64_t g, int64_t groups_per_img, int64_t HW,
+                                        bool small) {
   Group r;
-  r.b = int(g / groups_per_img);
-  r.q = (g - int64_t(r.b) * groups_per_img) * PPT;
-  const int y = int(r.q / p.W);
-  const int x = int(r.q - int64_t(y) * p.W);
+  int y, x;
+  split_group<PPT>(g, groups_per_img, p.W, small, r.b, r.q, y, x);
   const int b = r.b;
   const bool flip = p.flip_all || (p.flip && p.flip[b]) || (b < 256 && ((p.flip_bits[b >> 6] >> (b & 63)) & 1));
   const int sy = flip ? p.H - 1 - y : y;
@@ -214,16 +233,17 @@ __global__ __launch_bounds__(kBlock) void decode_vec_kernel(DecodeParams p) {
 #pragma unroll
   for (int c = 0; c < 4; ++c) cm[c] = p.cmap[c];
   const int64_t stride = int64_t(gridDim.x) * kBlock;
+  const bool small = total + U * stride < (int64_t(1) << 31) && HW < (int64_t(1) << 31);
 
   for (int64_t g0 = int64_t(blockIdx.x) * kBlock + threadIdx.x; g0 < total; g0 += U * stride) {
-    const Group gr0 = locate<PPT, CIN>(p, g0, groups_per_img, HW);
+    const Group gr0 = locate<PPT, CIN>(p, g0, groups_per_img, HW, small);
     Pixels<PPT, CIN> px0;
     load_pixels<PPT, CIN>(gr0.src, px0);
     if constexpr (U == 2) {
       const int64_t g1 = g0 + stride;
       const bool has1 = g1 < total;
       // second group's load goes out before the first group's lookups
-      const Group gr1 = locate<PPT, CIN>(p, has1 ? g1 : g0, groups_per_img, HW);
+      const Group gr1 = locate<PPT, CIN>(p, has1 ? g1 : g0, groups_per_img, HW, small);
       Pixels<PPT, CIN> px1;
       load_pixels<PPT, CIN>(gr1.src, px1);
       emit<PPT, CIN, OUTT, LAYOUT>(p, lut, cm, cout, HW, gr0, px0);
@@ -527,15 +547,15 @@ __global__ __launch_bounds__(kBlock) void replay_vec_kernel(DecodeParams p, Repl
 #pragma unroll
   for (int c = 0; c < 4; ++c) cm[c] = p.cmap[c];
   const int64_t stride = int64_t(gridDim.x) * kBlock;
+  const bool small = groups + meta_units + stride < (int64_t(1) << 31);
   for (int64_t g = int64_t(blockIdx.x) * kBlock + threadIdx.x; g < groups + meta_units; g += stride) {
     if (g >= groups) {
       replay_meta(r, sh, p.B, g - groups);
       continue;
     }
     Group gr;
-    gr.b = int(g / groups_per_img);
-    gr.q = (g - int64_t(gr.b) * groups_per_img) * PPT;
-    const int y = int(gr.q / p.W), x = int(gr.q - int64_t(y) * p.W);
+    int y, x;
+    split_group<PPT>(g, groups_per_img, p.W, small, gr.b, gr.q, y, x);
     const int sy = p.flip_all ? p.H - 1 - y : y;
     gr.src = p.src + sh.idx[gr.b] * r.frame_bytes + (int64_t(sy) * p.W + x) * CIN;
     Pixels<PPT, CIN> px;
