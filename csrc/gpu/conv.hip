@@ -694,14 +694,35 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     __syncthreads();   // the epilogue reuses the staging LDS
   }
 
+  // Epilogue stores: every thread takes whole 16-byte row chunks -- CPR
+  // chunks per row, RPP rows per pass, NJ rows per thread (for BN = 32 that
+  // is 2 rows of all 256 threads, not 4 rows of half of them).
+  constexpr int CPR = BN / 8, RPP = kThreads / CPR, NJ = FBM / RPP;
+  const int ec = t % CPR;
+  int eob[NJ];
+  bool epin[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    if constexpr (BN == 64) {   // the staging rows ar + 32 j
+      eob[j] = obase[j];
+      epin[j] = pin[j];
+    } else {
+      const int m = m0 + t / CPR + RPP * j;
+      epin[j] = m < p.M;
+      const int mm = epin[j] ? m : 0;
+      const int n = mm / (p.GH * p.GW), rem = mm - n * (p.GH * p.GW);
+      const int a = rem / p.GW, bb = rem - a * p.GW;
+      eob[j] = DGRAD ? ((n * p.OH + 2 * a + ph) * p.OW + 2 * bb + pw) * p.NOUT : mm * p.NOUT;
+    }
+  }
   // BN-backward fusion (below): issue the BN input loads now, so their
   // latency hides under the epilogue's LDS round trip
   const bool bnf = DGRAD && p.bn.part != nullptr;
-  uint4 xpre[4];
-  if (bnf && ac < BN / 8) {
+  uint4 xpre[NJ];
+  if (bnf) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      xpre[j] = pin[j] ? *reinterpret_cast<const uint4*>(p.bn.x + obase[j] + n0 + ac * 8) : make_uint4(0, 0, 0, 0);
+    for (int j = 0; j < NJ; ++j)
+      xpre[j] = epin[j] ? *reinterpret_cast<const uint4*>(p.bn.x + eob[j] + n0 + ec * 8) : make_uint4(0, 0, 0, 0);
   }
 
   // epilogue: round to bf16 (RNE) into an LDS tile [FBM][BN] (128-byte row
@@ -754,52 +775,50 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   float bs[8], bq[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) bs[q] = bq[q] = 0.f;
-  if (ac < BN / 8) {
-    float is[8], nm[8], ww[8], bb[8];
+  float is[8], nm[8], ww[8], bb[8];
+  if (bnf) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = n0 + ec * 8 + q;
+      is[q] = p.bn.invstd[c];
+      nm[q] = -p.bn.mean[c] * is[q];
+      ww[q] = p.bn.w[c];
+      bb[q] = p.bn.b[c];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    if (!epin[j]) continue;
+    const uint4 v = *reinterpret_cast<const uint4*>(smem + f_off(t / CPR + RPP * j, ec));
+    *reinterpret_cast<uint4*>(p.dst + eob[j] + n0 + ec * 8) = v;
     if (bnf) {
+      const uint4 xv = xpre[j];
+      const uint32_t gw[4] = {v.x, v.y, v.z, v.w}, xw[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const int c = n0 + ac * 8 + q;
-        is[q] = p.bn.invstd[c];
-        nm[q] = -p.bn.mean[c] * is[q];
-        ww[q] = p.bn.w[c];
-        bb[q] = p.bn.b[c];
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (!pin[j]) continue;
-      const uint4 v = *reinterpret_cast<const uint4*>(smem + st_a + j * 32 * F_ROW);
-      *reinterpret_cast<uint4*>(p.dst + obase[j] + n0 + ac * 8) = v;
-      if (bnf) {
-        const uint4 xv = xpre[j];
-        const uint32_t gw[4] = {v.x, v.y, v.z, v.w}, xw[4] = {xv.x, xv.y, xv.z, xv.w};
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const uint32_t gb = q & 1 ? gw[q >> 1] & 0xFFFF0000u : gw[q >> 1] << 16;
-          const uint32_t xb = q & 1 ? xw[q >> 1] & 0xFFFF0000u : xw[q >> 1] << 16;
-          const float xh = fmaf(__uint_as_float(xb), is[q], nm[q]);
-          const float g = __uint_as_float(gb);
-          const float gz = fmaf(xh, ww[q], bb[q]) > 0.f ? g : g * p.bn.slope;
-          bs[q] += gz;
-          bq[q] += gz * xh;
-        }
+        const uint32_t gb = q & 1 ? gw[q >> 1] & 0xFFFF0000u : gw[q >> 1] << 16;
+        const uint32_t xb = q & 1 ? xw[q >> 1] & 0xFFFF0000u : xw[q >> 1] << 16;
+        const float xh = fmaf(__uint_as_float(xb), is[q], nm[q]);
+        const float g = __uint_as_float(gb);
+        const float gz = fmaf(xh, ww[q], bb[q]) > 0.f ? g : g * p.bn.slope;
+        bs[q] += gz;
+        bq[q] += gz * xh;
       }
     }
   }
   if (bnf) {
-    // lanes l, l^8, l^16, ... (same ac) hold the same channels: fold them,
-    // then the 4 waves through LDS (the statistics area is free in backward)
+    // lanes with the same ec hold the same channels: fold them, then the 4
+    // waves through LDS (the statistics area is free in backward)
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
 #pragma unroll
-      for (int o = 8; o < 64; o <<= 1) bs[q] += __shfl_xor(bs[q], o), bq[q] += __shfl_xor(bq[q], o);
+      for (int o = CPR; o < 64; o <<= 1) bs[q] += __shfl_xor(bs[q], o), bq[q] += __shfl_xor(bq[q], o);
     }
-    if (lane < 8 && ac < BN / 8) {
+    if (lane < CPR) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        red[(wave * 2 + 0) * BN + ac * 8 + q] = bs[q];
-        red[(wave * 2 + 1) * BN + ac * 8 + q] = bq[q];
+        red[(wave * 2 + 0) * BN + ec * 8 + q] = bs[q];
+        red[(wave * 2 + 1) * BN + ec * 8 + q] = bq[q];
       }
     }
     __syncthreads();
