@@ -508,8 +508,14 @@ template <bool DGRAD, int BN, bool C4 = false>
 __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   constexpr int WGM = BN == 64 ? 2 : 4, WGN = 4 / WGM;
   constexpr int FM = FBM / WGM / 16, FN = BN / WGN / 16;   // 16x16 fragments per wave
-  __shared__ __attribute__((aligned(16))) char smem[2 * F_STAGE + 4 * 2 * 64 * 4];
-  float* red = reinterpret_cast<float*>(smem + 2 * F_STAGE);   // [WGM][2][BN]
+  // one stage = the A tile + a BN-row B tile; the epilogue's bf16 tile
+  // ([FBM][128 B] = FA_TILE) and the per-wave channel sums (red, [4][2][BN])
+  // reuse the staging space once the k-loop is done.  A 32-channel block
+  // therefore takes 40 KiB, and four fit a CU's LDS (50 KiB fit three).
+  constexpr int STG = FA_TILE + BN * F_ROW;
+  static_assert(2 * STG >= FA_TILE + 4 * 2 * BN * 4, "epilogue does not fit the staging LDS");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STG];
+  float* red = reinterpret_cast<float*>(smem + FA_TILE);   // [WGM][2][BN], after the epilogue tile
   const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
   constexpr int NTAPS = DGRAD ? 4 : 16;
   const int K = C4 ? FBK : NTAPS * p.C, NT = p.NOUT / BN;
@@ -612,7 +618,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   };
   const int st_a = f_off(ar, ac);   // rows ar + 32j keep the swizzle phase: (ar + 32j) & 7 == ar & 7
   auto store = [&](int buf) {
-    char* ai = smem + buf * F_STAGE;
+    char* ai = smem + buf * STG;
 #pragma unroll
     for (int j = 0; j < 4; ++j) *reinterpret_cast<uint4*>(ai + st_a + j * 32 * F_ROW) = ra[j];
     *reinterpret_cast<uint4*>(ai + FA_TILE + st_a) = rb0;
@@ -637,7 +643,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     for (int j = 0; j < FN; ++j) fb[j][kk] = FA_TILE + f_off(col0 + 16 * j + (lane & 15), chunk);
   }
   auto mma = [&](int buf) {
-    const char* ai = smem + buf * F_STAGE;
+    const char* ai = smem + buf * STG;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 a[FM], bb[FN];
@@ -657,6 +663,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     store(0);
     __syncthreads();
     mma(0);
+    __syncthreads();   // the epilogue tile overwrites stage 0
   } else {
     // Loads run kDepth steps ahead of the MFMAs in a register ring: with one
     // step of prefetch every k-step waited out a full global-load latency, and
