@@ -538,7 +538,6 @@ __device__ __forceinline__ void replay_meta(const ReplayParams& r, const ReplayS
 template <int PPT, int CIN, int OUTT, int LAYOUT>
 __global__ __launch_bounds__(kBlock) void replay_vec_kernel(DecodeParams p, ReplayParams r, int64_t meta_units) {
   __shared__ ReplayShared sh;
-  replay_prologue(p, r, sh);
   const int64_t HW = int64_t(p.H) * p.W;
   const int64_t groups_per_img = HW / PPT;
   const int64_t groups = groups_per_img * p.B;
@@ -548,9 +547,40 @@ __global__ __launch_bounds__(kBlock) void replay_vec_kernel(DecodeParams p, Repl
   for (int c = 0; c < 4; ++c) cm[c] = p.cmap[c];
   const int64_t stride = int64_t(gridDim.x) * kBlock;
   const bool small = groups + meta_units + stride < (int64_t(1) << 31);
-  for (int64_t g = int64_t(blockIdx.x) * kBlock + threadIdx.x; g < groups + meta_units; g += stride) {
+  // Every lane draws the frame index of its own first group (the same Philox
+  // word the block's table holds) and issues that group's pixel loads before
+  // the LUT staging and the block barrier: the HBM latency of the first
+  // loads overlaps the prologue instead of following it (one launch round
+  // for a batch of 8).
+  const uint64_t ctr = r.index_in ? 0 : (r.counter ? r.counter[0] : r.ctr_value);
+  auto frame_of = [&](int b) -> int64_t {
+    return r.index_in ? r.index_in[b]
+                      : int64_t((uint64_t(philox_word(r.seed, ctr, uint32_t(b))) * uint64_t(r.count)) >> 32);
+  };
+  const int64_t g0 = int64_t(blockIdx.x) * kBlock + threadIdx.x;
+  Group gr0;
+  Pixels<PPT, CIN> px0;
+  if (g0 < groups) {
+    int y, x;
+    split_group<PPT>(g0, groups_per_img, p.W, small, gr0.b, gr0.q, y, x);
+    const int sy = p.flip_all ? p.H - 1 - y : y;
+    gr0.src = p.src + frame_of(gr0.b) * r.frame_bytes + (int64_t(sy) * p.W + x) * CIN;
+    load_pixels<PPT, CIN>(gr0.src, px0);
+  }
+  for (int i = threadIdx.x; i < p.Cout * 256; i += kBlock) sh.lut[i] = p.lut[i];
+  for (int b = threadIdx.x; b < p.B; b += kBlock) {
+    const int64_t i = frame_of(b);
+    sh.idx[b] = i;
+    if (blockIdx.x == 0 && r.index_out) r.index_out[b] = i;
+  }
+  __syncthreads();
+  for (int64_t g = g0; g < groups + meta_units; g += stride) {
     if (g >= groups) {
       replay_meta(r, sh, p.B, g - groups);
+      continue;
+    }
+    if (g == g0) {
+      emit<PPT, CIN, OUTT, LAYOUT>(p, sh.lut, cm, cout, HW, gr0, px0);
       continue;
     }
     Group gr;
