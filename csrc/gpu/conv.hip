@@ -43,6 +43,8 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr int kThreads = 256;   // 4 waves: 2 (co) x 2 (kc), a 32 x 64 sub-tile each
@@ -547,18 +549,23 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   // at -1, and only in-bounds taps are ever added to it) and a bitmask of the
   // taps that land inside the image -- the k-loop then costs one add and one
   // mask test per row instead of the full index and bounds arithmetic
+  // (the mask is the outer product of the in-image tap rows and columns)
+  constexpr int TW = DGRAD ? 2 : 4;   // taps per row of the tap grid
   uint32_t abase[4], vmask[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     abase[j] = uint32_t(base[j]) << (p.cshift + 1);
+    uint32_t rows = 0, cols = 0;
+#pragma unroll
+    for (int k = 0; k < TW; ++k) {
+      const int dr = DGRAD ? ph - k : k, dc = DGRAD ? pw - k : k;
+      rows |= unsigned(rb[j] + dr) < unsigned(p.SH) ? 1u << k : 0u;
+      cols |= unsigned(cb[j] + dc) < unsigned(p.SW) ? 1u << k : 0u;
+    }
     uint32_t mk = 0;
 #pragma unroll
-    for (int tp = 0; tp < NTAPS; ++tp) {
-      const int dr = DGRAD ? ph - (tp >> 1) : tp >> 2, dc = DGRAD ? pw - (tp & 1) : tp & 3;
-      const bool in = unsigned(rb[j] + dr) < unsigned(p.SH) && unsigned(cb[j] + dc) < unsigned(p.SW);
-      mk |= (pin[j] && in) ? (1u << tp) : 0u;
-    }
-    vmask[j] = mk;
+    for (int k = 0; k < TW; ++k) mk |= (rows >> k) & 1u ? cols << (TW * k) : 0u;
+    vmask[j] = pin[j] ? mk : 0u;
   }
   const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(p.src, int64_t(p.N) * p.SH * p.SW * p.C * 2);
   const uint16_t* wrow0 = p.w + (n0 + ar) * (16 * p.C);
@@ -742,21 +749,28 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j)
+    for (int j = 0; j < FN; ++j) {
+      // RNE to bf16, two values per v_cvt_pk_bf16_f32
+      uint32_t pk[2];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const f32x2 pr = {acc[i][j][2 * h2], acc[i][j][2 * h2 + 1]};
+        pk[h2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2));
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = row0 + 16 * i + 4 * (lane >> 4) + r;
         const int col = col0 + 16 * j + (lane & 15);
-        uint32_t u = __float_as_uint(acc[i][j][r]);
-        u += 0x7FFFu + ((u >> 16) & 1u);
-        const uint16_t h = uint16_t(u >> 16);
+        const uint32_t w2 = pk[r >> 1];
+        const uint16_t h = uint16_t(r & 1 ? w2 >> 16 : w2);
         tile[(f_off(row, col >> 3) >> 1) + (col & 7)] = h;
         if (!DGRAD && m0 + row < p.M) {
-          const float vr = __uint_as_float(uint32_t(h) << 16);
+          const float vr = __uint_as_float(r & 1 ? w2 & 0xFFFF0000u : w2 << 16);
           sum[j] += vr;
           sq[j] += vr * vr;
         }
       }
+    }
   if (!DGRAD && p.stats) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {   // lanes l, l^16, l^32, l^48 hold the same channel

@@ -22,6 +22,8 @@ namespace gpu {
 namespace {
 
 constexpr int kHeadThreads = 256;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int wstart(int i, int in, int out) { return (i * in) / out; }
 __device__ __forceinline__ int wend(int i, int in, int out) { return ((i + 1) * in + out - 1) / out; }
@@ -140,10 +142,8 @@ __global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p) {
     uint32_t packed[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      uint32_t lo = __float_as_uint(acc[2 * k]), hi = __float_as_uint(acc[2 * k + 1]);
-      lo += 0x7FFFu + ((lo >> 16) & 1u);
-      hi += 0x7FFFu + ((hi >> 16) & 1u);
-      packed[k] = (lo >> 16) | (hi & 0xFFFF0000u);
+      const f32x2 pr = {acc[2 * k], acc[2 * k + 1]};
+      packed[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2));   // RNE, v_cvt_pk_bf16_f32
     }
     *reinterpret_cast<uint4*>(p.dz + ((int64_t(n * p.H + h) * p.W + w) * p.C + c0)) =
         make_uint4(packed[0], packed[1], packed[2], packed[3]);

@@ -33,10 +33,8 @@ namespace {
 constexpr int kBlock = 256;
 
 __device__ __forceinline__ uint16_t f2bf(float f) {
-  // round-to-nearest-even; table values are finite
-  uint32_t u = __float_as_uint(f);
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return uint16_t(u >> 16);
+  // round-to-nearest-even in one v_cvt_pk_bf16_f32 (gfx950)
+  return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f));
 }
 
 __device__ __forceinline__ uint16_t f2h(float f) {
