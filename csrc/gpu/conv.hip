@@ -202,14 +202,21 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p)
 
   // this thread's staging work: one dY chunk, two X chunks per k-step
   const int dpx = t >> 3, dch = t & 7;                 // dY: pixel, 16-byte chunk
-  const int xpx0 = t >> 4, xch = t & 15;               // X: pixels xpx0, xpx0+16, chunk
+  // X: one pixel per thread, its chunks xch and xch + 8 (im2col columns kc
+  // and kc + 64): one pixel cursor feeds both loads
+  const int xpx = t >> 3, xch = t & 7;
   const int kc = kt * BKC + xch * 8;
   const int kh = kc / (4 * p.Cin);
   const int rem = kc - kh * 4 * p.Cin;
   const int kw = rem / p.Cin, ci = rem - kw * p.Cin;
-  XCursor c0, c1;
-  c0.init(m_begin + xpx0, p, kh, kw, ci);
-  c1.init(m_begin + xpx0 + 16, p, kh, kw, ci);
+  const int kc1 = kc + 64;
+  const int kh1 = kc1 / (4 * p.Cin);
+  const int rem1 = kc1 - kh1 * 4 * p.Cin;
+  const int kw1 = rem1 / p.Cin, ci1 = rem1 - kw1 * p.Cin;
+  const int dkh = kh1 - kh, dkw = kw1 - kw;
+  const int de = (dkh * p.W + dkw) * p.Cin + (ci1 - ci);   // element offset of the second chunk
+  XCursor c0;
+  c0.init(m_begin + xpx, p, kh, kw, ci);
   const int j_col = 2 * BPX * p.Cin, j_row = 2 * (p.W - p.Wo) * p.Cin, j_img = (p.H - 2 * p.Ho) * p.W * p.Cin;
   const bool single = p.Wo >= BPX;
 
@@ -230,22 +237,19 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p)
   // X needs no slice-end test: a pixel past the slice pairs with a zero dY
   // chunk (out-of-range dY loads return 0), and past the tensor the X load is
   // out of range too
-  auto xload = [&](const XCursor& c) {
-    const int ih = 2 * c.oh - 1 + kh, iw = 2 * c.ow - 1 + kw;
-    const bool ok = unsigned(ih) < unsigned(p.H) && unsigned(iw) < unsigned(p.W);
-    return bload(rs_x, ok ? uint32_t(c.e) * 2u : kOOB);
-  };
   auto load = [&](Stage& r) {
     r.dy = bload(rs_dy, md < m_end ? dy_byte : kOOB);
-    r.x0 = xload(c0);
-    r.x1 = xload(c1);
+    const int ih = 2 * c0.oh - 1 + kh, iw = 2 * c0.ow - 1 + kw;
+    const bool ok0 = unsigned(ih) < unsigned(p.H) && unsigned(iw) < unsigned(p.W);
+    const bool ok1 = unsigned(ih + dkh) < unsigned(p.H) && unsigned(iw + dkw) < unsigned(p.W);
+    r.x0 = bload(rs_x, ok0 ? uint32_t(c0.e) * 2u : kOOB);
+    r.x1 = bload(rs_x, ok1 ? uint32_t(c0.e + de) * 2u : kOOB);
     md += BPX;
     dy_byte += dy_step;
     c0.advance(p.Ho, p.Wo, j_col, j_row, j_img, single);
-    c1.advance(p.Ho, p.Wo, j_col, j_row, j_img, single);
   };
-  const int st_dy = dy_off(dpx, dch * 16), st_x0 = DY_TILE + x_off(xpx0, xch * 16),
-            st_x1 = DY_TILE + x_off(xpx0 + 16, xch * 16);
+  const int st_dy = dy_off(dpx, dch * 16), st_x0 = DY_TILE + x_off(xpx, xch * 16),
+            st_x1 = DY_TILE + x_off(xpx, (xch + 8) * 16);
   auto store = [&](const Stage& r, int buf) {
     char* base = smem + buf * STAGE;
     *reinterpret_cast<uint4*>(base + st_dy) = r.dy;
