@@ -537,17 +537,32 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   const int ar = t >> 3, ac = t & 7;
   int rb[4], cb[4], base[4], obase[4];
   bool pin[4];
+  // (n, a, b) of row ar by division, the next rows 32 GEMM rows on by
+  // stepping (two integer divisions per row were a third of the kernel's VALU)
+  int gn, ga, gbb;
+  {
+    const int m = m0 + ar < p.M ? m0 + ar : 0;
+    gn = m / (p.GH * p.GW);
+    const int rem = m - gn * (p.GH * p.GW);
+    ga = rem / p.GW;
+    gbb = rem - ga * p.GW;
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int m = m0 + ar + 32 * j;
+    if (j > 0) {
+      gbb += 32;
+      while (gbb >= p.GW) {
+        gbb -= p.GW;
+        if (++ga == p.GH) ga = 0, ++gn;
+      }
+    }
     pin[j] = m < p.M;
     const int mm = pin[j] ? m : 0;
-    const int n = mm / (p.GH * p.GW), rem = mm - n * (p.GH * p.GW);
-    const int a = rem / p.GW, bb = rem - a * p.GW;
-    rb[j] = DGRAD ? a : 2 * a - 1;
-    cb[j] = DGRAD ? bb : 2 * bb - 1;
-    base[j] = (n * p.SH + rb[j]) * p.SW + cb[j];
-    obase[j] = DGRAD ? ((n * p.OH + 2 * a + ph) * p.OW + 2 * bb + pw) * p.NOUT : mm * p.NOUT;
+    rb[j] = DGRAD ? ga : 2 * ga - 1;
+    cb[j] = DGRAD ? gbb : 2 * gbb - 1;
+    base[j] = (gn * p.SH + rb[j]) * p.SW + cb[j];
+    obase[j] = DGRAD ? ((gn * p.OH + 2 * ga + ph) * p.OW + 2 * gbb + pw) * p.NOUT : mm * p.NOUT;
   }
   // per row: byte offset of its tap-origin pixel (mod 2^32: border rows start
   // at -1, and only in-bounds taps are ever added to it) and a bitmask of the
@@ -719,18 +734,31 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   const int ec = t % CPR;
   int eob[NJ];
   bool epin[NJ];
+  if constexpr (BN == 64) {   // the staging rows ar + 32 j
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    if constexpr (BN == 64) {   // the staging rows ar + 32 j
-      eob[j] = obase[j];
-      epin[j] = pin[j];
-    } else {
-      const int m = m0 + t / CPR + RPP * j;
+    for (int j = 0; j < NJ; ++j) eob[j] = obase[j], epin[j] = pin[j];
+  } else {                     // rows t / CPR + RPP j: divide once, then step
+    const int m_first = m0 + t / CPR;
+    int en = 0, ea = 0, eb = 0;
+    {
+      const int m = m_first < p.M ? m_first : 0;
+      en = m / (p.GH * p.GW);
+      const int rem = m - en * (p.GH * p.GW);
+      ea = rem / p.GW;
+      eb = rem - ea * p.GW;
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      if (j > 0) {
+        eb += RPP;
+        while (eb >= p.GW) {
+          eb -= p.GW;
+          if (++ea == p.GH) ea = 0, ++en;
+        }
+      }
+      const int m = m_first + RPP * j;
       epin[j] = m < p.M;
-      const int mm = epin[j] ? m : 0;
-      const int n = mm / (p.GH * p.GW), rem = mm - n * (p.GH * p.GW);
-      const int a = rem / p.GW, bb = rem - a * p.GW;
-      eob[j] = DGRAD ? ((n * p.OH + 2 * a + ph) * p.OW + 2 * bb + pw) * p.NOUT : mm * p.NOUT;
+      eob[j] = DGRAD ? ((en * p.OH + 2 * ea + ph) * p.OW + 2 * eb + pw) * p.NOUT : m * p.NOUT;
     }
   }
   // BN-backward fusion (below): issue the BN input loads now, so their
@@ -750,6 +778,19 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   float sum[FN], sq[FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) sum[j] = sq[j] = 0.f;
+  // LDS element offsets of this lane's values: row row0 + 16 i + lr + r has
+  // swizzle phase (lr + r) & 7 for every i (row0 and 16 i are multiples of 8),
+  // so the 4 x FN offsets are computed once and i only adds 16 rows
+  const int lr = 4 * (lane >> 4);
+  int toff[FN][4];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int col = col0 + 16 * j + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      toff[j][r] = (row0 + lr + r) * (F_ROW / 2) + ((((col >> 3) ^ ((lr + r) & 7)) << 4) >> 1) + (col & 7);
+  }
+  const bool all_rows = m0 + FBM <= p.M;   // the tile holds no row past the GEMM
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -763,12 +804,9 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = row0 + 16 * i + 4 * (lane >> 4) + r;
-        const int col = col0 + 16 * j + (lane & 15);
         const uint32_t w2 = pk[r >> 1];
-        const uint16_t h = uint16_t(r & 1 ? w2 >> 16 : w2);
-        tile[(f_off(row, col >> 3) >> 1) + (col & 7)] = h;
-        if (!DGRAD && m0 + row < p.M) {
+        tile[toff[j][r] + i * 16 * (F_ROW / 2)] = uint16_t(r & 1 ? w2 >> 16 : w2);
+        if (!DGRAD && (all_rows || m0 + row0 + 16 * i + lr + r < p.M)) {
           const float vr = __uint_as_float(r & 1 ? w2 & 0xFFFF0000u : w2 << 16);
           sum[j] += vr;
           sq[j] += vr * vr;
