@@ -205,14 +205,20 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p)
   // X: one pixel per thread, its chunks xch and xch + 8 (im2col columns kc
   // and kc + 64): one pixel cursor feeds both loads
   const int xpx = t >> 3, xch = t & 7;
-  const int kc = kt * BKC + xch * 8;
-  const int kh = kc / (4 * p.Cin);
-  const int rem = kc - kh * 4 * p.Cin;
-  const int kw = rem / p.Cin, ci = rem - kw * p.Cin;
-  const int kc1 = kc + 64;
-  const int kh1 = kc1 / (4 * p.Cin);
-  const int rem1 = kc1 - kh1 * 4 * p.Cin;
-  const int kw1 = rem1 / p.Cin, ci1 = rem1 - kw1 * p.Cin;
+  const int kc = kt * BKC + xch * 8, kc1 = kc + 64;
+  int kh, kw, ci, kh1, kw1, ci1;
+  if ((p.Cin & (p.Cin - 1)) == 0) {   // power-of-two channels (block-uniform): shifts, not divisions
+    const int cs = __builtin_ctz(unsigned(p.Cin));
+    kh = kc >> (cs + 2), kw = (kc >> cs) & 3, ci = kc & (p.Cin - 1);
+    kh1 = kc1 >> (cs + 2), kw1 = (kc1 >> cs) & 3, ci1 = kc1 & (p.Cin - 1);
+  } else {
+    kh = kc / (4 * p.Cin);
+    const int rem = kc - kh * 4 * p.Cin;
+    kw = rem / p.Cin, ci = rem - kw * p.Cin;
+    kh1 = kc1 / (4 * p.Cin);
+    const int rem1 = kc1 - kh1 * 4 * p.Cin;
+    kw1 = rem1 / p.Cin, ci1 = rem1 - kw1 * p.Cin;
+  }
   const int dkh = kh1 - kh, dkw = kw1 - kw;
   const int de = (dkh * p.W + dkw) * p.Cin + (ci1 - ci);   // element offset of the second chunk
   XCursor c0;
@@ -301,17 +307,16 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p)
 
   // C/D map of 16x16x32: column = lane & 15 (kc), row = 4 * (lane >> 4) + reg (co)
   zero_output(p);
-  float* out = p.partial + int64_t(slice) * p.Cout * KC;
+  // 32-bit offsets from the lane's first element (the slice's partial block
+  // is < 2^31 elements): one add per store instead of 64-bit address math
+  float* out = p.partial + int64_t(slice) * p.Cout * KC + (co0 + wco + 4 * (lane >> 4)) * KC +
+               (kt * BKC + wkc + (lane & 15));
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = co0 + wco + 16 * i + 4 * (lane >> 4) + r;
-        const int col = kt * BKC + wkc + 16 * j + (lane & 15);
-        out[int64_t(co) * KC + col] = acc[i][j][r];
-      }
+      for (int r = 0; r < 4; ++r) out[(16 * i + r) * KC + 16 * j] = acc[i][j][r];
 }
 
 // ---------------------------------------------------------------------------
