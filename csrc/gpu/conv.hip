@@ -575,20 +575,34 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   // mask test per row instead of the full index and bounds arithmetic
   // (the mask is the outer product of the in-image tap rows and columns)
   constexpr int TW = DGRAD ? 2 : 4;   // taps per row of the tap grid
+  // The in-image tap rows k (dr = k, or ph - k for the data gradient) form one
+  // interval, so do the columns: two clamps each, then the interval bits are
+  // spread over the tap grid with a multiply instead of a per-tap test.
+  auto span = [](int lo, int hi) -> uint32_t {   // bits [lo, hi) of [0, TW)
+    lo = lo < 0 ? 0 : lo;
+    hi = hi > TW ? TW : hi;
+    return hi > lo ? (1u << hi) - (1u << lo) : 0u;
+  };
   uint32_t abase[4], vmask[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     abase[j] = uint32_t(base[j]) << (p.cshift + 1);
-    uint32_t rows = 0, cols = 0;
-#pragma unroll
-    for (int k = 0; k < TW; ++k) {
-      const int dr = DGRAD ? ph - k : k, dc = DGRAD ? pw - k : k;
-      rows |= unsigned(rb[j] + dr) < unsigned(p.SH) ? 1u << k : 0u;
-      cols |= unsigned(cb[j] + dc) < unsigned(p.SW) ? 1u << k : 0u;
+    uint32_t rows, cols;
+    if (DGRAD) {   // 0 <= rb + ph - k < SH  <=>  rb + ph - SH < k <= rb + ph
+      rows = span(rb[j] + ph - p.SH + 1, rb[j] + ph + 1);
+      cols = span(cb[j] + pw - p.SW + 1, cb[j] + pw + 1);
+    } else {       // 0 <= rb + k < SH
+      rows = span(-rb[j], p.SH - rb[j]);
+      cols = span(-cb[j], p.SW - cb[j]);
     }
-    uint32_t mk = 0;
-#pragma unroll
-    for (int k = 0; k < TW; ++k) mk |= (rows >> k) & 1u ? cols << (TW * k) : 0u;
+    uint32_t mk;
+    if constexpr (TW == 4) {
+      const uint32_t x = (rows | (rows << 3) | (rows << 6) | (rows << 9)) & 0x1111u;   // row k -> bit 4k
+      mk = (x * 0xFu) & (cols * 0x1111u);
+    } else {
+      const uint32_t x = (rows | (rows << 1)) & 0x5u;                                   // row k -> bit 2k
+      mk = (x * 0x3u) & (cols * 0x5u);
+    }
     vmask[j] = pin[j] ? mk : 0u;
   }
   const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(p.src, int64_t(p.N) * p.SH * p.SW * p.C * 2);
