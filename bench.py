@@ -131,8 +131,9 @@ def parse_args(argv=None):
                          'disturbs its step least: 9.72k vs 9.59k img/s, profiles/r2/host_sync.txt)')
     ap.add_argument('--prefetch', type=int, default=None,
                     help='output buffers posted to the loader (batches assembled/decoding/ready ahead of the consumer); '
-                         'default 6.  Deeper queues gain ~1 %% on long runs, but a short timed window then ends '
-                         'with more in-flight decode work inside its closing device sync (20 steps: 34k vs 40k img/s)')
+                         'default 8.  Deeper queues coalesce larger decode launches (16: +1-2 %% on long runs), '
+                         'but a short timed window then ends with more in-flight decode work inside its closing '
+                         'device sync (20 steps: 34k vs 40k img/s); profiles/r2/loader_depth_ab.txt')
     ap.add_argument('--launch-depth', type=int, default=2,
                     help='direct-path decode launches queued before new batches coalesce into one launch')
     ap.add_argument('--backend', choices=['nccl', 'gloo'], default='nccl',
@@ -170,7 +171,7 @@ def parse_args(argv=None):
     if args.h2d is None:
         args.h2d = 'copy' if args.consumer == 'disc' else 'auto'
     if args.prefetch is None:
-        args.prefetch = 6
+        args.prefetch = 6 if args.consumer == 'disc' else 8
     return args
 
 
