@@ -131,9 +131,10 @@ def parse_args(argv=None):
                          'disturbs its step least: 9.72k vs 9.59k img/s, profiles/r2/host_sync.txt)')
     ap.add_argument('--prefetch', type=int, default=None,
                     help='output buffers posted to the loader (batches assembled/decoding/ready ahead of the consumer); '
-                         'default 8.  Deeper queues coalesce larger decode launches (16: +1-2 %% on long runs), '
-                         'but a short timed window then ends with more in-flight decode work inside its closing '
-                         'device sync (20 steps: 34k vs 40k img/s); profiles/r2/loader_depth_ab.txt')
+                         'default 6.  Deeper queues coalesce larger decode launches (8: +0.7 %%, 16: +1-2 %% on '
+                         'long runs), but a short timed window then ends with more in-flight decode work inside '
+                         'its closing device sync (20 steps, 8: 37.9k, 16: 34k vs 40.0k img/s); '
+                         'profiles/r2/loader_depth_ab.txt')
     ap.add_argument('--launch-depth', type=int, default=2,
                     help='direct-path decode launches queued before new batches coalesce into one launch')
     ap.add_argument('--backend', choices=['nccl', 'gloo'], default='nccl',
@@ -171,7 +172,7 @@ def parse_args(argv=None):
     if args.h2d is None:
         args.h2d = 'copy' if args.consumer == 'disc' else 'auto'
     if args.prefetch is None:
-        args.prefetch = 6 if args.consumer == 'disc' else 8
+        args.prefetch = 6
     return args
 
 
