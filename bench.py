@@ -229,7 +229,7 @@ def main(argv=None):
     gpu = local_rank % max(1, torch.cuda.device_count())    # == local_rank on a full node
     torch.cuda.set_device(gpu)
     device = torch.device('cuda', gpu)
-    world_seen, allreduce = 1, None
+    world_seen, allreduce, comm = 1, None, None
     if world == 1 and args.force_pg:
         # a 1-rank process group: rehearses the collective path (e.g. RCCL
         # all-reduce captured in the step graph) on a single GPU
@@ -250,6 +250,14 @@ def main(argv=None):
         allreduce = {'value': float(chk.item()), 'expected': world_seen * (world_seen + 1) / 2}
         if allreduce['value'] != allreduce['expected']:
             raise RuntimeError(f'all_reduce sanity check failed: {allreduce}')
+        # the communicator the training step and scatter mode use (RCCL called on
+        # the compute stream), checked before anything depends on it: a P2P ring
+        # over xGMI plus an all-reduce, each with a timeout that names this rank
+        # and its peers (blendtorch/parallel/comm.py)
+        from blendtorch.parallel import DeviceComm
+        comm = DeviceComm(device=device if args.backend == 'nccl' else None)
+        allreduce['selfcheck'] = {k: (round(v, 3) if isinstance(v, float) else v)
+                                  for k, v in comm.selfcheck().items()}
 
     # place each rank's producers on CPUs local to its GPU (same NUMA domain as
     # the GPU's PCIe root: frames are written there and read back by the GPU)
@@ -400,7 +408,7 @@ def main(argv=None):
         stepper = None
         if model is not None:
             from blendtorch.parallel.step import CapturedStep
-            stepper = CapturedStep(model, opt, loss_fn, graph=use_graph,
+            stepper = CapturedStep(model, opt, loss_fn, graph=use_graph, comm=comm,
                                    allreduce='always' if args.force_pg else dist.is_initialized(), split=dma_mid)
 
         def graphed(x):
@@ -545,6 +553,8 @@ def main(argv=None):
                 'head': args.head if model is not None else None,
                 'host_sync': args.host_sync,
                 'consumer_collectives_per_step': stepper.collectives if stepper is not None else None,
+                'collectives': ('rccl-direct' if comm is not None and comm.native else
+                                ('c10d' if comm is not None else None)),
             },
             'sec_per_image': round(tmax / images, 7),
             'sec_per_batch': round(tmax / args.steps, 6),

@@ -205,9 +205,12 @@ hipError_t multi_cast(const CastParams& p, hipStream_t stream);
 // Adam / AdamW over a list of fp32 parameters in ONE launch, graph-capturable:
 // the step counter and the bias corrections live on the device.
 //   adam_schedule (one lane): step += 1; sched = {lr / (1 - b1^step),
-//                             1 / sqrt(1 - b2^step), lr}   (hp = {lr})
+//                             1 / sqrt(1 - b2^step), lr, grad_scale, 1}
+//                             (hp = {lr, grad_scale}).  With a device `gate`
+//                             whose gate[0] == 0 nothing advances and
+//                             sched[4] = 0 turns the update into a no-op.
 //   adam_update: per element, PyTorch's Adam arithmetic
-//       g = grad (+ wd * p unless decoupled); decoupled: p *= 1 - lr * wd
+//       g = grad * grad_scale (+ wd * p unless decoupled); decoupled: p *= 1 - lr * wd
 //       m = b1 m + (1 - b1) g;  v = b2 v + (1 - b2) g^2
 //       p -= sched[0] * m / (sqrt(v) * sched[1] + eps)
 //     grads fp32 or bf16 (grad_bf16); optional bf16 shadow copy of the new
@@ -228,7 +231,7 @@ struct AdamParams {
   int decoupled = 0;   // AdamW
   int maximize = 0;
   float beta1 = 0.9f, beta2 = 0.999f, eps = 1e-8f, weight_decay = 0.f;
-  const float* sched = nullptr;   // device [3], written by adam_schedule
+  const float* sched = nullptr;   // device [5], written by adam_schedule
 };
 // Weight gradient of a 4x4 / stride-2 / pad-1 convolution over channels-last
 // bf16 activations on the MFMA units (conv.hip): x [N][H][W][Cin],
@@ -336,7 +339,8 @@ struct HeadParams {
 hipError_t head_forward(const HeadParams& p, hipStream_t stream);
 hipError_t head_backward(const HeadParams& p, hipStream_t stream);
 
-hipError_t adam_schedule(float* step, const float* hp, float* sched, float beta1, float beta2, hipStream_t stream);
+hipError_t adam_schedule(float* step, const float* hp, float* sched, float beta1, float beta2, hipStream_t stream,
+                         const float* gate = nullptr);
 hipError_t adam_update(const AdamParams& p, hipStream_t stream);
 
 }  // namespace gpu

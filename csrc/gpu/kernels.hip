@@ -1293,8 +1293,14 @@ namespace {
 
 // One lane: the step counter and the bias corrections, so that the update
 // kernel's blocks all read a value no block is writing.
-__global__ void adam_schedule_kernel(float* step, const float* hp, float* sched, float beta1, float beta2) {
+__global__ void adam_schedule_kernel(float* step, const float* hp, float* sched, float beta1, float beta2,
+                                     const float* gate) {
   if (threadIdx.x != 0) return;
+  // a closed gate (gate[0] == 0, computed on the device earlier in the same
+  // stream/graph) makes the whole step a no-op: counter, moments and weights
+  const bool active = !gate || gate[0] != 0.f;
+  sched[4] = active ? 1.f : 0.f;
+  if (!active) return;
   const float s = step[0] + 1.f;
   step[0] = s;
   const float lr = hp[0];
@@ -1303,17 +1309,18 @@ __global__ void adam_schedule_kernel(float* step, const float* hp, float* sched,
   sched[0] = float(double(lr) / bc1);
   sched[1] = float(1.0 / sqrt(bc2));
   sched[2] = lr;
+  sched[3] = hp[1];   // gradient scale (e.g. 1 / world after a summing all-reduce)
 }
 
 template <bool GBF16>
 __global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
   const int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x;   // 4-element group
-  if (q >= a.gstart[a.n]) return;
+  if (q >= a.gstart[a.n] || a.sched[4] == 0.f) return;
   int k = 0;
   while (q >= a.gstart[k + 1]) ++k;     // <= kMaxAdam compares, mostly uniform across a wave
   const int64_t e0 = (q - a.gstart[k]) * 4;
   const int64_t n = a.numel[k];
-  const float step_size = a.sched[0], inv_bc2 = a.sched[1], lr = a.sched[2];
+  const float step_size = a.sched[0], inv_bc2 = a.sched[1], lr = a.sched[2], gscale = a.sched[3];
   const float b1 = a.beta1, b2 = a.beta2, wd = a.weight_decay;
   float* P = a.p[k];
   float* M = a.m[k];
@@ -1350,7 +1357,7 @@ __global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    float g = a.maximize ? -gv[j] : gv[j];
+    float g = (a.maximize ? -gv[j] : gv[j]) * gscale;
     if (wd != 0.f) {
       if (a.decoupled) pv[j] *= 1.f - lr * wd;
       else g += wd * pv[j];
@@ -1380,9 +1387,10 @@ __global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
 
 }  // namespace
 
-hipError_t adam_schedule(float* step, const float* hp, float* sched, float beta1, float beta2, hipStream_t stream) {
+hipError_t adam_schedule(float* step, const float* hp, float* sched, float beta1, float beta2, hipStream_t stream,
+                         const float* gate) {
   if (!step || !hp || !sched) return hipErrorInvalidValue;
-  adam_schedule_kernel<<<1, 64, 0, stream>>>(step, hp, sched, beta1, beta2);
+  adam_schedule_kernel<<<1, 64, 0, stream>>>(step, hp, sched, beta1, beta2, gate);
   return hipGetLastError();
 }
 

@@ -189,12 +189,27 @@ bool StreamLoader::next(ReadyBatch* out, hipStream_t consumer, long timeout_ms) 
 }
 
 // host_sync: hand out, in order, the launched batches whose device work the
-// host has seen complete (worker thread).
+// host has seen complete (worker thread).  Their shm slots are re-validated
+// first: a HELD slot a dead-consumer lease took back while the DMA read it
+// fails the stream BEFORE the batch reaches the consumer (reap() counts it).
+// Without host_sync the batch is handed out at launch and the same check in
+// reap() raises on the consumer's next next() call.
 void StreamLoader::promote_ready() {
   bool any = false;
   while (!unready_.empty() && unready_.front().pending->done()) {
+    ReadyBatch& rb = unready_.front();
+    const bool torn = std::any_of(rb.slots.begin(), rb.slots.end(),
+                                  [](const ReadyBatch::SlotRef& s) { return !s.seg->valid(s.slot, s.gen); });
     std::lock_guard<std::mutex> lk(mu_);
-    ready_.push_back(std::move(unready_.front()));
+    if (torn && !cfg_.skip_bad) {
+      if (error_.empty())
+        error_ = "StreamLoader: shared-memory slot(s) were reclaimed by their producer while a batch read them";
+      stop_ = true;
+      any = true;
+      break;
+    }
+    rb.slots.clear();
+    ready_.push_back(std::move(rb));
     unready_.pop_front();
     any = true;
   }
@@ -389,6 +404,20 @@ bool StreamLoader::process(zmtp::Message&& msg) {
   };
   if (msg.size() != 1) return bad("expected a single-frame message");
   Item it;
+  // a claimed shm slot (and the key-frame reference of a tile16 frame) goes
+  // back on every exit that does not hand the item to cur_ -- the bad()
+  // returns and the throws alike: a rejected descriptor must not pin a ring
+  // slot for the HELD lease (minutes) nor keep a replaced key frame alive
+  struct ClaimGuard {
+    Item& it;
+    bool armed = false;
+    ~ClaimGuard() {
+      if (!armed) return;
+      it.seg->release(it.slot, it.gen);
+      if (it.key) it.key->refs--;
+      it.key = nullptr;
+    }
+  } guard{it};
   it.frame = std::move(msg[0]);
   const uint8_t* data = it.frame.data();
   const size_t n = it.frame.size;
@@ -435,6 +464,7 @@ bool StreamLoader::process(zmtp::Message&& msg) {
       stats_.shm_stale++;
       return false;
     }
+    guard.armed = true;   // claimed: every exit but the hand-over to cur_ gives it back
     it.src = it.seg->base() + off;
     if (dev_base) it.dsrc = dev_base + off;
     if (d.items.size() >= 9 && d.items[8]->kind == codec::Value::TUPLE) {
@@ -536,7 +566,6 @@ bool StreamLoader::process(zmtp::Message&& msg) {
     }
     cv_.notify_all();
   } else if (h != H_ || w != W_ || c != C_) {
-    if (it.seg) it.seg->release(it.slot, it.gen);
     return bad("image shape changed within the stream");
   }
   // metadata: the frame minus the image payload, tree re-based onto it
@@ -568,6 +597,7 @@ bool StreamLoader::process(zmtp::Message&& msg) {
     if (const codec::Value* b = root->get("btid"))
       if (b->kind == codec::Value::INT) stats_.frames_per_btid[b->i]++;
   }
+  guard.armed = false;
   cur_.push_back(std::move(it));
   if (int(cur_.size()) == cfg_.batch_size) launch();
   return true;
@@ -982,7 +1012,10 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
     rb.items.reserve(b.items.size());
     for (auto& it : b.items) {
       fl.frames.push_back(std::move(it.frame));
-      if (it.seg) fl.slots.push_back({it.seg, it.slot, it.gen});
+      if (it.seg) {
+        fl.slots.push_back({it.seg, it.slot, it.gen});
+        if (cfg_.host_sync) rb.slots.push_back({it.seg, it.slot, it.gen});
+      }
       if (!it.expanded.empty()) fl.expanded.push_back(std::move(it.expanded));
       rb.items.push_back(std::move(it.meta));
     }

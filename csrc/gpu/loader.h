@@ -166,6 +166,11 @@ struct ReadyBatch {
   hipEvent_t done = nullptr;         // GPU-side completion (host_sync = false)
   std::shared_ptr<EventSet> pending; // host-side completion (host_sync): ready once done()
   double recv_ms = 0;                // wall time spent assembling the batch
+  struct SlotRef {
+    shm::Segment* seg;
+    uint32_t slot, gen;
+  };
+  std::vector<SlotRef> slots;        // host_sync: shm slots re-validated before hand-out
 };
 
 struct LoaderStats {

@@ -15,6 +15,7 @@
 #include <sys/mman.h>
 
 #include "../python/pyvalue.h"
+#include "comm.h"
 #include "kernels.h"
 #include "loader.h"
 
@@ -352,12 +353,55 @@ PYBIND11_MODULE(_hip, m) {
           check(head_backward(p, stream_of(stream)), "head_backward");
         });
 
+  // direct RCCL on the caller's stream (comm.h); the GIL is released while
+  // RCCL enqueues (a group end may block until peers have posted theirs)
+  m.def("rccl_load", [](const std::string& path) { comm::load(path); });
+  m.def("rccl_loaded", [] { return comm::loaded(); });
+  m.def("rccl_count", [](uintptr_t c) { return comm::comm_count(c); });
+  m.def("rccl_rank", [](uintptr_t c) { return comm::comm_rank(c); });
+  m.def("rccl_async_error", [](uintptr_t c) { return comm::async_error(c); });
+  m.def(
+      "rccl_all_reduce",
+      [](uintptr_t send, uintptr_t recv, size_t count, int dtype, int op, uintptr_t c, uintptr_t stream) {
+        comm::all_reduce(ptr<const void>(send), ptr<void>(recv), count, dtype, op, c, stream_of(stream));
+      },
+      py::call_guard<py::gil_scoped_release>());
+  m.def(
+      "rccl_broadcast",
+      [](uintptr_t send, uintptr_t recv, size_t count, int dtype, int root, uintptr_t c, uintptr_t stream) {
+        comm::broadcast(ptr<const void>(send), ptr<void>(recv), count, dtype, root, c, stream_of(stream));
+      },
+      py::call_guard<py::gil_scoped_release>());
+  // one group of point-to-point transfers: ops = [(is_send, ptr, count, dtype, peer)]
+  m.def(
+      "rccl_p2p",
+      [](std::vector<std::tuple<int, uintptr_t, size_t, int, int>> ops, uintptr_t c, uintptr_t stream) {
+        comm::group_start();
+        try {
+          for (auto& [is_send, p, count, dtype, peer] : ops) {
+            if (is_send) comm::send(ptr<const void>(p), count, dtype, peer, c, stream_of(stream));
+            else comm::recv(ptr<void>(p), count, dtype, peer, c, stream_of(stream));
+          }
+        } catch (...) {
+          try {
+            comm::group_end();
+          } catch (...) {
+          }
+          throw;
+        }
+        comm::group_end();
+      },
+      py::call_guard<py::gil_scoped_release>());
+
   m.def("adam_schedule",
-        [](uintptr_t step, uintptr_t hp, uintptr_t sched, float beta1, float beta2, uintptr_t stream) {
+        [](uintptr_t step, uintptr_t hp, uintptr_t sched, float beta1, float beta2, uintptr_t stream,
+           uintptr_t gate) {
           check(adam_schedule(ptr<float>(step), ptr<const float>(hp), ptr<float>(sched), beta1, beta2,
-                              stream_of(stream)),
+                              stream_of(stream), ptr<const float>(gate)),
                 "adam_schedule");
-        });
+        },
+        py::arg("step"), py::arg("hp"), py::arg("sched"), py::arg("beta1"), py::arg("beta2"), py::arg("stream"),
+        py::arg("gate") = 0);
 
   m.def("adam_update",
         [](std::vector<uintptr_t> params, std::vector<uintptr_t> grads, std::vector<uintptr_t> exp_avg,

@@ -11,7 +11,15 @@ Byte layout (compatible with pkg_pytorch/blendtorch/btt/file.py:10-132)::
 
 The offset table is written (all -1) when recording starts and rewritten in
 place when it ends; shape and dtype never change, so its size does not.
+
+Messages the framework pickles itself (shared-memory frames materialised by
+``RemoteIterableDataset``, ``DeviceReplayBuffer.save_recordings``) go through
+:func:`dumps_numpy1`: protocol 3 with numpy's globals under their numpy 1.x
+module path (``numpy.core.multiarray``), like the reference's own writes
+(pkg_pytorch/blendtorch/btt/file.py:46-53 under numpy 1.x).  numpy 2 writes
+``numpy._core`` paths that numpy 1 cannot import.
 """
+import io
 import logging
 import pickle
 from pathlib import Path
@@ -19,6 +27,33 @@ from pathlib import Path
 import numpy as np
 
 log = logging.getLogger('blendtorch')
+
+
+class _Numpy1Pickler(pickle._Pickler):
+    """Protocol-3 pickler that names numpy 2's ``numpy._core.*`` globals by
+    their numpy 1.x path.  Both numpy generations resolve the result: numpy 2
+    still ships ``numpy.core`` as an alias package."""
+    _REMAP = {'numpy._core.multiarray': 'numpy.core.multiarray', 'numpy._core.numeric': 'numpy.core.numeric',
+              'numpy._core': 'numpy.core'}
+
+    def save_global(self, obj, name=None):
+        if name is None:
+            name = getattr(obj, '__qualname__', None) or obj.__name__
+        module = pickle.whichmodule(obj, name)
+        alias = self._REMAP.get(module)
+        if alias is None or self.proto >= 4:
+            return super().save_global(obj, name)
+        self.write(pickle.GLOBAL + f'{alias}\n{name}\n'.encode('utf-8'))
+        self.memoize(obj)
+
+    dispatch = dict(pickle._Pickler.dispatch)
+
+
+def dumps_numpy1(obj):
+    """``pickle.dumps(obj, protocol=3)`` readable by numpy 1.x (see module doc)."""
+    buf = io.BytesIO()
+    _Numpy1Pickler(buf, protocol=3).dump(obj)
+    return buf.getvalue()
 
 
 def _header(offsets):
@@ -29,7 +64,7 @@ def _header(offsets):
     except ImportError:
         # no native build: CPython's bytes with the module path swapped
         # (same byte count minus the underscore)
-        return pickle.dumps(table, protocol=3).replace(b'cnumpy._core.multiarray\n', b'cnumpy.core.multiarray\n', 1)
+        return dumps_numpy1(table)
     return _native.btr_header(table)
 
 
@@ -37,7 +72,8 @@ class FileRecorder:
     """Append messages to one ``.btr`` file (use as a context manager).
 
     ``save(data, is_pickled)`` stores raw pickled bytes as they are, or
-    pickles ``data`` (protocol 3: readable by Blender 2.8x's Python 3.7).
+    pickles ``data`` (protocol 3, numpy 1.x module paths: readable by Blender
+    2.8x's Python 3.7 and numpy 1 as well as numpy 2).
     Messages beyond ``max_messages`` are ignored."""
 
     def __init__(self, outpath='blendtorch.mpkl', max_messages=100000):
@@ -59,7 +95,7 @@ class FileRecorder:
     def save(self, data, is_pickled=False):
         if self.num_messages == self.capacity:
             return
-        payload = data if is_pickled else pickle.dumps(data, protocol=3)
+        payload = data if is_pickled else dumps_numpy1(data)
         self.offsets[self.num_messages] = self.file.tell()
         self.file.write(payload)
         self.num_messages += 1

@@ -577,6 +577,33 @@ def _pool_module():
 
 
 # ---------------------------------------------------------------------------
+# gradient sinks: parameters whose gradient lives in a persistent flat bucket
+# (parallel.GradBuckets) get it written there by the backward kernel itself
+
+def grad_sink(param):
+    """The persistent gradient view of ``param`` installed by
+    ``parallel.GradBuckets`` (same shape and strides), or None."""
+    return getattr(param, '_bt_grad_sink', None)
+
+
+def _grad_dest(param, like=None):
+    """(tensor the backward kernel writes ``param``'s gradient into, whether
+    that is the param's bucket view).  The first gradient after
+    ``GradBuckets.zero_()`` is written straight into the bucket and the op
+    returns None for that input (no AccumulateGrad kernel); any further one
+    in the same step (several backward passes before the optimizer step)
+    goes to a fresh tensor that autograd adds into ``param.grad`` -- the
+    usual accumulate semantics either way.  A bucket view that is no longer
+    ``param.grad`` (e.g. after ``zero_grad(set_to_none=True)``) is ignored."""
+    import torch
+    sink = grad_sink(param) if param is not None else None
+    if sink is not None and param.grad is sink and getattr(param, '_bt_grad_fresh', False):
+        param._bt_grad_fresh = False
+        return sink, True
+    return torch.empty_like(param if like is None else like), False
+
+
+# ---------------------------------------------------------------------------
 # consumer-model op: one-launch fp32 -> bf16 cast of a parameter list
 
 def _dense(t):
@@ -708,6 +735,7 @@ def _bn_function():
             ctx.save_for_backward(xs, w, b, mean, invstd)
             ctx.slope = float(slope)
             ctx.link = link
+            ctx.params = (weight, bias)
             if link is not None:
                 link.x, link.mean, link.invstd, link.w, link.b, link.slope = xs, mean, invstd, w, b, float(slope)
                 link.part = link.gy = None
@@ -722,8 +750,12 @@ def _bn_function():
             dt = _dt(xs)
             gys = _as_nhwc(gy if gy.dtype == xs.dtype else gy.to(xs.dtype))
             gx = torch.empty_like(xs)
-            dw = torch.empty(C, dtype=torch.float32, device=xs.device)
-            db = torch.empty_like(dw)
+            dw, w_sunk = _grad_dest(ctx.params[0], w)
+            db, b_sunk = _grad_dest(ctx.params[1], b)
+            if dw.dtype != torch.float32 or not dw.is_contiguous():
+                dw, w_sunk = torch.empty_like(w), False
+            if db.dtype != torch.float32 or not db.is_contiguous():
+                db, b_sunk = torch.empty_like(b), False
             part, rows = ctx.link.take(gys) if ctx.link is not None else (None, 0)
             if part is not None:
                 # the consuming convolution's data-gradient epilogue already summed gz, gz * xhat
@@ -737,7 +769,8 @@ def _bn_function():
                 ext.bn_backward(xs.data_ptr(), gys.data_ptr(), gx.data_ptr(), M, C, dt, part.data_ptr(),
                                 mean.data_ptr(), invstd.data_ptr(), w.data_ptr(), b.data_ptr(), dw.data_ptr(),
                                 db.data_ptr(), ctx.slope, _stream(xs.device))
-            return gx.permute(0, 3, 1, 2), dw, db, None, None, None, None, None, None, None, None
+            return (gx.permute(0, 3, 1, 2), None if w_sunk else dw, None if b_sunk else db,
+                    None, None, None, None, None, None, None, None)
 
     return _BatchNormLeakyReLU
 
@@ -1039,7 +1072,10 @@ def _conv_function():
                     gx = torch.ops.aten.convolution_backward(gy, x, wfull, None, [2, 2], [1, 1], [1, 1], False,
                                                              [0, 0], 1, [True, False, False])[0]
             if ctx.needs_input_grad[1]:
-                gw = conv_wgrad(x, gy, torch.empty_like(ctx.w32))
+                out, sunk = _grad_dest(ctx.w32)
+                gw = conv_wgrad(x, gy, out)
+                if sunk:
+                    gw = None      # written into the parameter's bucket view
             return gx, gw, None, None, None, None
 
     return _Conv4x4s2
@@ -1094,6 +1130,7 @@ def _head_function():
                              tptr, tval, pooled.data_ptr(), partial.data_ptr(), loss.data_ptr(), dlogit.data_ptr(),
                              logit.data_ptr(), _stream(dev))
             ctx.save_for_backward(w, pooled, dlogit)
+            ctx.wparam = w
             ctx.zshape, ctx.pool = (N, C, H, W), (oh, ow)
             ctx.mark_non_differentiable(logit)
             return loss, logit
@@ -1108,12 +1145,14 @@ def _head_function():
             oh, ow = ctx.pool
             g = gloss.to(torch.float32).reshape(1).contiguous()
             dz = torch.empty((N, C, H, W), dtype=torch.bfloat16, device=w.device, memory_format=torch.channels_last)
-            dw = torch.empty_like(w)
+            dw, sunk = _grad_dest(ctx.wparam, w)
+            if dw.stride() != w.stride():
+                dw, sunk = torch.empty_like(w), False
             _count('head_backward')
             ext.head_backward(w.data_ptr(), w.stride(1), w.stride(2), w.stride(3), N, H, W, C, oh, ow,
                               pooled.data_ptr(), dlogit.data_ptr(), g.data_ptr(), dz.data_ptr(), dw.data_ptr(),
                               _stream(w.device))
-            return dz, dw, None, None, None
+            return dz, None if sunk else dw, None, None, None
 
     return _DiscHeadBCE
 

@@ -15,6 +15,13 @@ Optional ``bf16_shadow``: the update also writes a bf16 copy of every new
 weight (``shadow(p)``), which a bf16 forward can read instead of casting the
 fp32 master weights on every step.
 
+Data parallel: ``grad_scale`` multiplies every gradient inside the update
+kernel, so a summing all-reduce of the gradients (``parallel.GradBuckets``)
+needs no separate ``div_`` by the world size.  ``step(gate=t)`` takes a device
+scalar: where ``t == 0`` the step is a no-op (counter, moments and weights
+untouched) -- a conditional optimizer step without a host synchronisation,
+capturable in a graph (densityopt's ``D_real - D_sim < 0.7`` rule).
+
 Arithmetic is PyTorch's Adam (torch/optim/adam.py, non-amsgrad): L2 weight
 decay added to the gradient, or decoupled (AdamW) when ``decoupled=True``.
 CPU tensors run the same formulas in PyTorch (reference path and tests).
@@ -34,40 +41,60 @@ _MAX_PER_LAUNCH = 32   # kMaxAdam (csrc/gpu/kernels.h)
 
 class FusedAdam(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, decoupled=False,
-                 maximize=False, bf16_shadow=False):
+                 maximize=False, bf16_shadow=False, grad_scale=1.0):
         if lr < 0 or eps < 0 or weight_decay < 0 or not (0 <= betas[0] < 1 and 0 <= betas[1] < 1):
             raise ValueError(f'invalid Adam hyper-parameters lr={lr} betas={betas} eps={eps} wd={weight_decay}')
         defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, decoupled=decoupled,
                         maximize=maximize, bf16_shadow=bf16_shadow)
         super().__init__(params, defaults)
-        self._dev = {}   # id(group) -> device scalars (kept out of param_groups / state_dict)
+        self._grad_scale = float(grad_scale)
+        # id(group) -> device scalars (kept out of param_groups / state_dict).
+        # Each entry holds its group, so an id cannot be reused while it lives.
+        self._dev = {}
 
     # -- per-group device scalars ------------------------------------------
     def _group_state(self, group):
         dev = group['params'][0].device
         gs = self._dev.get(id(group))
-        if gs is None or gs['step'].device != dev:
+        if gs is None or gs['group'] is not group or gs['step'].device != dev:
             # a loaded state_dict carries the counter as each parameter's 'step'
             prev = next((self.state[p]['step'] for p in group['params'] if 'step' in self.state.get(p, {})), None)
             step = torch.zeros(1, dtype=torch.float32, device=dev)
             if prev is not None:
                 step.fill_(float(prev.reshape(-1)[0]))
-            gs = {'step': step,
-                  'hp': torch.tensor([float(group['lr'])], dtype=torch.float32, device=dev),
-                  'sched': torch.zeros(3, dtype=torch.float32, device=dev),
-                  'lr': float(group['lr'])}
+            gs = {'step': step, 'group': group,
+                  'hp': torch.tensor([float(group['lr']), self._grad_scale], dtype=torch.float32, device=dev),
+                  'sched': torch.zeros(5, dtype=torch.float32, device=dev),
+                  'lr': float(group['lr']), 'grad_scale': self._grad_scale}
             self._dev[id(group)] = gs
             for p in group['params']:
                 if self.state.get(p):
                     self.state[p]['step'] = step
         return gs
 
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._dev.clear()     # the loaded groups are new dicts: rebuild their counters from the state
+
+    @property
+    def grad_scale(self):
+        return self._grad_scale
+
+    def set_grad_scale(self, scale):
+        """Factor every gradient is multiplied by in the update (e.g.
+        ``1 / world_size`` after a summing all-reduce); also for a captured
+        optimizer (the device copy is rewritten)."""
+        self._grad_scale = float(scale)
+        for gs in self._dev.values():
+            gs['hp'][1].fill_(self._grad_scale)
+            gs['grad_scale'] = self._grad_scale
+
     def set_lr(self, lr, group=0):
         """Change the learning rate, also for an optimizer captured in a graph."""
         g = self.param_groups[group]
         g['lr'] = float(lr)
         gs = self._group_state(g)
-        gs['hp'].fill_(float(lr))
+        gs['hp'][0].fill_(float(lr))
         gs['lr'] = float(lr)
 
     def _state(self, p, group):
@@ -89,7 +116,9 @@ class FusedAdam(torch.optim.Optimizer):
 
     # -- step -----------------------------------------------------------------
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, gate=None):
+        """One update; ``gate`` (optional 1-element float tensor on the
+        parameters' device): skip the step where it is 0."""
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -101,16 +130,18 @@ class FusedAdam(torch.optim.Optimizer):
             gs = self._group_state(group)
             capturing = params[0].is_cuda and torch.cuda.is_current_stream_capturing()
             if gs['lr'] != float(group['lr']) and not capturing:
-                gs['hp'].fill_(float(group['lr']))   # lr edited through param_groups
+                gs['hp'][0].fill_(float(group['lr']))   # lr edited through param_groups
                 gs['lr'] = float(group['lr'])
             states = [self._state(p, group) for p in params]
+            if gate is not None and (gate.numel() != 1 or gate.device != params[0].device):
+                raise ValueError('FusedAdam.step: gate must be a 1-element tensor on the parameters\' device')
             if params[0].is_cuda:
-                self._step_gpu(group, gs, params, states)
+                self._step_gpu(group, gs, params, states, gate)
             else:
-                self._step_reference(group, gs, params, states)
+                self._step_reference(group, gs, params, states, gate)
         return loss
 
-    def _step_gpu(self, group, gs, params, states):
+    def _step_gpu(self, group, gs, params, states, gate=None):
         ext = hip_ext()
         b1, b2 = group['betas']
         stream = _stream(params[0].device)
@@ -120,7 +151,10 @@ class FusedAdam(torch.optim.Optimizer):
             if p.dtype != torch.float32 or not _dense(p):
                 raise ValueError('FusedAdam (GPU) needs dense fp32 parameters (contiguous or channels-last)')
         _count('adam_schedule')
-        ext.adam_schedule(gs['step'].data_ptr(), gs['hp'].data_ptr(), gs['sched'].data_ptr(), b1, b2, stream)
+        if gate is not None and gate.dtype != torch.float32:
+            raise ValueError('FusedAdam.step: gate must be float32 on the GPU')
+        ext.adam_schedule(gs['step'].data_ptr(), gs['hp'].data_ptr(), gs['sched'].data_ptr(), b1, b2, stream,
+                          gate.data_ptr() if gate is not None else 0)
         for i in range(0, len(params), _MAX_PER_LAUNCH):
             ps, ss = params[i:i + _MAX_PER_LAUNCH], states[i:i + _MAX_PER_LAUNCH]
             grads = []
@@ -140,16 +174,21 @@ class FusedAdam(torch.optim.Optimizer):
                             int(group['maximize']), stream)
 
     @staticmethod
-    def _step_reference(group, gs, params, states):
+    def _step_reference(group, gs, params, states, gate=None):
         """fp32 PyTorch reference of the same update (CPU tensors)."""
+        if gate is not None and float(gate.reshape(-1)[0]) == 0.0:
+            return
         b1, b2 = group['betas']
         gs['step'] += 1
         s = float(gs['step'])
         lr, wd = float(gs['hp'][0]), group['weight_decay']
         step_size = lr / (1 - b1 ** s)
         inv_bc2 = 1.0 / (1 - b2 ** s) ** 0.5
+        scale = float(gs['hp'][1])
         for p, st in zip(params, states):
             g = p.grad.float()
+            if scale != 1.0:
+                g = g * scale
             if group['maximize']:
                 g = -g
             if wd:

@@ -1,0 +1,142 @@
+"""Persistent flat gradient buckets for data-parallel training steps.
+
+``DistributedDataParallel`` cannot live inside a captured HIP graph (its
+reducer does host-side bookkeeping per step), and packing gradients into a
+fresh flat buffer per step (``torch.cat``), all-reducing it, dividing and
+copying it back (``_foreach_copy_``) costs ~20 small kernels per step --
+measured as a 45 % tax on the DCGAN consumer step even on one GPU
+(profiles/r3/dp_tax.md).
+
+:class:`GradBuckets` instead allocates the gradients ONCE as views into a few
+flat buffers (one per dtype/device, at most ``bucket_mb`` each):
+
+* every ``p.grad`` is permanently a view of its bucket, with ``p``'s own
+  strides (channels-last conv weights stay channels-last);
+* the gfx950 backward kernels (``blendtorch.ops``: MFMA weight gradient, fused
+  BatchNorm, fused head) write the first gradient of a step straight into the
+  view (``ops._grad_dest``): no AccumulateGrad kernel, no copy;
+* the all-reduce runs in place on the flat bucket, directly on the compute
+  stream (:class:`~blendtorch.parallel.comm.DeviceComm`), and the ``1/world``
+  average folds into ``ops.FusedAdam(grad_scale=...)``: no ``div_`` kernel;
+* views are 256-byte aligned so the optimizer's 16-byte vector loads apply.
+
+Buckets are laid out in reverse parameter order (the order backward produces
+gradients), so with several buckets the first one is complete earliest.
+
+Reference loop being data-paralleled: examples/densityopt/densityopt.py:257-331
+(the reference itself trains single-process).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+__all__ = ['GradBuckets']
+
+_ALIGN_BYTES = 256
+
+
+def _dense(t):
+    return t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last))
+
+
+class GradBuckets:
+    """Flat persistent gradient storage for ``params``.
+
+    Params
+    ------
+    params: parameters (those with ``requires_grad``) of one or more models.
+    bucket_mb: maximum bucket size; a single parameter larger than this gets a
+        bucket of its own.
+    """
+
+    def __init__(self, params: Sequence[torch.nn.Parameter], bucket_mb: float = 256.0):
+        ps = [p for p in params if p.requires_grad]
+        seen = set()
+        self.params: List[torch.nn.Parameter] = []
+        for p in ps:
+            if id(p) not in seen:
+                seen.add(id(p))
+                self.params.append(p)
+        for p in self.params:
+            if not _dense(p):
+                raise ValueError(f'GradBuckets: parameter {tuple(p.shape)} is not dense (contiguous / channels-last)')
+        limit = max(1, int(bucket_mb * (1 << 20)))
+        # group by (device, dtype), reverse order: the last layers' gradients come first in backward
+        groups: Dict[tuple, List[torch.nn.Parameter]] = {}
+        for p in reversed(self.params):
+            groups.setdefault((p.device, p.dtype), []).append(p)
+        self.buckets: List[torch.Tensor] = []
+        self._members: List[List[torch.nn.Parameter]] = []
+        for (dev, dt), members in groups.items():
+            esz = torch.tensor([], dtype=dt).element_size()
+            align = max(1, _ALIGN_BYTES // esz)
+            cur, offs, size = [], [], 0
+            for p in members:
+                n = p.numel()
+                if cur and (size + n) * esz > limit:
+                    self._make(dev, dt, cur, offs, size)
+                    cur, offs, size = [], [], 0
+                offs.append(size)
+                cur.append(p)
+                size += -(-n // align) * align
+            if cur:
+                self._make(dev, dt, cur, offs, size)
+        self.zero_()
+
+    def _make(self, dev, dt, members, offs, size):
+        flat = torch.zeros(size, dtype=dt, device=dev)
+        for p, off in zip(members, offs):
+            view = flat.as_strided(p.shape, p.stride(), off)
+            p.grad = view
+            p._bt_grad_sink = view
+        self.buckets.append(flat)
+        self._members.append(list(members))
+
+    @property
+    def numel(self) -> int:
+        return sum(b.numel() for b in self.buckets)
+
+    def attached(self) -> bool:
+        """True while every parameter's ``.grad`` is still its bucket view."""
+        return all(getattr(p, '_bt_grad_sink', None) is not None and p.grad is p._bt_grad_sink
+                   for p in self.params)
+
+    def zero_(self, memset: bool = True):
+        """Start a step: the next gradient of each parameter overwrites its view.
+        ``memset`` also clears the buckets (needed when some parameter's
+        gradient comes from a kernel without a bucket sink, or not at all)."""
+        if not self.attached():
+            raise RuntimeError('GradBuckets: a parameter\'s .grad was replaced (zero_grad(set_to_none=True)?); '
+                               'bucketed gradients must stay attached')
+        if memset:
+            for b in self.buckets:
+                b.zero_()
+        for p in self.params:
+            p._bt_grad_fresh = True
+
+    def all_reduce(self, comm, op: str = 'sum') -> int:
+        """Reduce every bucket in place over ``comm``
+        (:class:`~blendtorch.parallel.comm.DeviceComm`).  Capturable when the
+        communicator is native.  Returns the number of collectives issued."""
+        if not self.attached():
+            raise RuntimeError('GradBuckets: gradients were detached from their buckets')
+        for b in self.buckets:
+            comm.all_reduce_(b, op)
+        return len(self.buckets)
+
+    def detach(self):
+        """Remove the buckets: parameters get ordinary gradients again."""
+        for p in self.params:
+            if getattr(p, '_bt_grad_sink', None) is not None:
+                if p.grad is p._bt_grad_sink:
+                    p.grad = p.grad.clone()
+                del p._bt_grad_sink
+            if hasattr(p, '_bt_grad_fresh'):
+                del p._bt_grad_fresh
+        self.buckets, self._members = [], []
+
+    def __repr__(self):
+        return (f'GradBuckets({len(self.params)} params, {len(self.buckets)} buckets, '
+                f'{self.numel} elements)')

@@ -1,19 +1,28 @@
 """Whole training steps as one HIP graph, data-parallel included.
 
 A consumer step on the streamed batches (DCGAN discriminator, keypoint CNN)
-is ~100 small kernels: eager PyTorch spends as long dispatching them as the
+is ~60-100 small kernels: eager PyTorch spends as long dispatching them as the
 GPU spends running them (profiles/consumer_step.md: 1.07 ms eager vs 0.81 ms
 graphed).  :class:`CapturedStep` captures forward, backward, the gradient
 all-reduce and the optimizer update once and replays the graph per batch.
 
 ``DistributedDataParallel`` cannot live inside a captured graph (its reducer
 hooks run host-side bookkeeping per step), so the data-parallel reduction is
-done here explicitly: the gradients are flattened into buckets of at most
-``bucket_mb`` and each bucket is one RCCL all-reduce enqueued on the capture
-stream -- a captured collective replays with the graph like any kernel.  A
-few large buckets suit xGMI's point-to-point ring (per-link bandwidth, fixed
-per-collective latency) better than DDP's default 25 MB-but-many-hooks
-pattern for a model this small (~0.7 M parameters = one bucket).
+done here explicitly, with nothing per step but the collective itself:
+
+* gradients live permanently in flat buckets (:class:`~.grads.GradBuckets`);
+  the gfx950 backward kernels write straight into them;
+* each bucket is ONE in-place RCCL all-reduce enqueued on the compute stream
+  (:class:`~.comm.DeviceComm`) -- inside the captured graph it is one more
+  node of the same linear queue, not a fork/join onto c10d's stream;
+* ``1/world`` is folded into ``ops.FusedAdam`` (``grad_scale``); other
+  optimizers get an averaging all-reduce (``ncclAvg``).
+
+A model of ~0.7 M parameters is one 2.8 MB bucket: one collective per step,
+which suits xGMI's point-to-point links (per-collective latency dominates).
+The previous per-step pack (``torch.cat``) / ``div_`` / ``_foreach_copy_``
+cost 45 % of the step on one GPU (profiles/r3/dp_tax.md);
+:func:`allreduce_gradients` keeps that path for callers without buckets.
 
 The reference trains on the CPU-collated batches in eager PyTorch
 (examples/densityopt/densityopt.py:257-331) and has no data parallelism.
@@ -70,15 +79,21 @@ class CapturedStep:
 
     Params
     ------
-    model, optimizer: the optimizer must be created with ``capturable=True``
-        (its step counters then live on the GPU).
+    model, optimizer: a torch optimizer must be created with
+        ``capturable=True`` (its step counters then live on the GPU);
+        ``ops.FusedAdam`` always is.
     loss_fn: ``loss_fn(model, x) -> scalar loss`` (forward + loss; may use
         autocast -- pass ``cache_enabled=False`` so replays recast live weights).
-    allreduce: average gradients over the default process group inside the
-        graph (data parallel without DDP); ``'always'`` also on a 1-rank group.
+    allreduce: average gradients over the process group inside the step
+        (data parallel without DDP); ``'always'`` also on a 1-rank group
+        (rehearses the collective path on one GPU).
     warmup: eager steps on a side stream before capture (allocator, MIOpen
         algorithm search, optimizer state).
     graph: False runs the same step eagerly (fallback / comparison).
+    comm: a :class:`~.comm.DeviceComm` to reduce over (default: one is
+        created on the world group -- a collective call on every rank).
+    buckets: False keeps the legacy per-step pack/all-reduce/copy-back path
+        (:func:`allreduce_gradients`; comparison only).
 
     split: capture forward+loss and backward+update as two graphs sharing one
         memory pool, so a caller can act between them: ``step(x, mid=fn)``
@@ -87,11 +102,13 @@ class CapturedStep:
         the memory-bound forward, see bench.py --dma-phase).
 
     ``state`` is ``'graph'`` after a successful capture, ``'eager'`` otherwise.
+    ``collectives`` is the number of all-reduces per step.
     """
 
     def __init__(self, model: torch.nn.Module, optimizer: torch.optim.Optimizer,
-                 loss_fn: Callable[[torch.nn.Module, torch.Tensor], torch.Tensor], allreduce: bool = True,
-                 warmup: int = 3, graph: bool = True, group=None, bucket_mb: float = 64.0, split: bool = False):
+                 loss_fn: Callable[[torch.nn.Module, torch.Tensor], torch.Tensor], allreduce=True,
+                 warmup: int = 3, graph: bool = True, group=None, bucket_mb: float = 256.0, split: bool = False,
+                 comm=None, buckets: bool = True):
         self.model, self.opt, self.loss_fn = model, optimizer, loss_fn
         self.split = split
         self.graph_bwd: Optional[torch.cuda.CUDAGraph] = None
@@ -102,14 +119,34 @@ class CapturedStep:
         self.loss = None
         self.collectives = 0
         self.error = None
+        self.comm = None
+        self.grads = None
+        self._op = 'sum'
+        active = bool(allreduce) and dist.is_available() and dist.is_initialized() and (
+            dist.get_world_size(group) > 1 or allreduce == 'always')
+        self._legacy = active and not buckets
+        if active and buckets:
+            from .comm import DeviceComm
+            from .grads import GradBuckets
+            self.comm = comm if comm is not None else DeviceComm(group)
+            self.grads = GradBuckets(model.parameters(), bucket_mb=bucket_mb)
+            if hasattr(optimizer, 'set_grad_scale'):
+                optimizer.set_grad_scale(1.0 / self.comm.world)   # folded into the update kernel
+            else:
+                self._op = 'avg'
 
     def _forward(self, x):
-        self.opt.zero_grad(set_to_none=True)
+        if self.grads is not None:
+            self.grads.zero_()
+        else:
+            self.opt.zero_grad(set_to_none=True)
         return self.loss_fn(self.model, x)
 
     def _backward(self, loss):
         loss.backward()
-        if self.allreduce:
+        if self.grads is not None and self.comm is not None:
+            self.collectives = self.grads.all_reduce(self.comm, self._op)
+        elif self._legacy:
             self.collectives = allreduce_gradients(self.model.parameters(), self.group, self.bucket_mb,
                                                    force=self.allreduce == 'always')
         self.opt.step()
@@ -129,7 +166,8 @@ class CapturedStep:
         torch.cuda.current_stream().wait_stream(side)
         g = torch.cuda.CUDAGraph()
         try:
-            self.opt.zero_grad(set_to_none=True)
+            if self.grads is None:
+                self.opt.zero_grad(set_to_none=True)
             if self.split:
                 with torch.cuda.graph(g):
                     loss = self._forward(self.x)

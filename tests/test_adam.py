@@ -186,3 +186,91 @@ def test_gpu_graph_replay_advances_step_and_follows_set_lr(dev):
     assert float(ours.state[next(a.parameters())]['step']) == 6
     for pa, pb in zip(a.parameters(), b.parameters()):
         torch.testing.assert_close(pa.detach().cpu(), pb.detach(), rtol=1e-5, atol=1e-6)
+
+
+def test_reference_grad_scale_and_gate():
+    """grad_scale multiplies the gradient inside the update; a closed gate
+    leaves counter, moments and weights untouched."""
+    a, b = _model(), _model()
+    ours = ops.FusedAdam(a.parameters(), lr=1e-2, grad_scale=0.25)
+    ref = torch.optim.Adam(b.parameters(), lr=1e-2)
+    for k in range(4):
+        _grads(a, k)
+        _grads(b, k)
+        for q in b.parameters():
+            q.grad.mul_(0.25)
+        ours.step(gate=torch.ones(1))
+        ref.step()
+        before = [p.detach().clone() for p in a.parameters()]
+        _grads(a, 50 + k)
+        ours.step(gate=torch.zeros(1))        # skipped entirely
+        assert all(torch.equal(x, p) for x, p in zip(before, a.parameters()))
+    assert float(ours.state[next(a.parameters())]['step']) == 4
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-6)
+    ours.set_grad_scale(1.0)
+    assert ours.grad_scale == 1.0
+
+
+def test_load_state_dict_twice_into_stepped_optimizer():
+    """Loading a state dict (twice, into an optimizer that already stepped)
+    takes the loaded step counter, never a stale per-group counter."""
+    a = _model()
+    opt = ops.FusedAdam(a.parameters(), lr=1e-2)
+    for k in range(3):
+        _grads(a, k)
+        opt.step()
+    sd3 = copy.deepcopy(opt.state_dict())
+    _grads(a, 3)
+    opt.step()
+    sd4 = copy.deepcopy(opt.state_dict())
+    b = _model()
+    opt2 = ops.FusedAdam(b.parameters(), lr=1e-2)
+    _grads(b, 9)
+    opt2.step()
+    opt2.load_state_dict(sd3)
+    opt2.load_state_dict(sd4)
+    b.load_state_dict(a.state_dict())
+    _grads(a, 5)
+    _grads(b, 5)
+    opt.step()
+    opt2.step()
+    assert float(opt2.state[next(b.parameters())]['step']) == 5
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        torch.testing.assert_close(pa, pb, rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+def test_gpu_grad_scale_and_gate_in_graph(dev):
+    """Captured: the gate tensor is read on every replay (skip without a host
+    sync), grad_scale matches the reference path."""
+    a, b = _model(device=dev), _model()
+    ours = ops.FusedAdam(a.parameters(), lr=1e-2, grad_scale=0.5)
+    ref = ops.FusedAdam(b.parameters(), lr=1e-2, grad_scale=0.5)
+    grads = [torch.zeros_like(p) for p in a.parameters()]
+    for p, g in zip(a.parameters(), grads):
+        p.grad = g
+    gate = torch.ones(1, device=dev)
+
+    def feed(k):
+        _grads(b, k)
+        for g, q in zip(grads, b.parameters()):
+            g.copy_(q.grad)
+
+    feed(0)
+    ours.step(gate=gate)
+    ref.step()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        ours.step(gate=gate)
+    for k in range(1, 7):
+        feed(k)
+        open_ = k % 2 == 0
+        gate.fill_(1.0 if open_ else 0.0)
+        graph.replay()
+        if open_:
+            ref.step()
+    torch.cuda.synchronize()
+    assert float(ours.state[next(a.parameters())]['step']) == 4
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        torch.testing.assert_close(pa.detach().cpu(), pb.detach(), rtol=1e-5, atol=1e-6)

@@ -184,10 +184,12 @@ def test_dataset_tile_codec_matches_raw(free_port, extra):
     dataset exactly the frames the raw shm path gives for the same seed."""
     from blendtorch.transport import shm
     frames = {}
+    pids = []
     for i, codec in enumerate(('none', 'tile16')):
         args = dict(producer='cubesim', num_instances=1, named_sockets=['DATA'], start_port=free_port + 5 * i,
                     proto='ipc', seed=11, instance_args=[extra + ['--shm', '6', '--codec', codec]])
         with btt.BlenderLauncher(**args) as bl:
+            pids += [p.pid for p in bl.launch_info.processes]
             ds = btt.RemoteIterableDataset(bl.launch_info.addresses['DATA'], max_items=24)
             frames[codec] = [(it['frameid'], it['image']) for it in ds]
     assert len(frames['tile16']) == 24
@@ -195,5 +197,7 @@ def test_dataset_tile_codec_matches_raw(free_port, extra):
         assert fa == fb and a.shape == b.shape and np.array_equal(a, b)
     # frames differ from each other (random poses), so tiles were really sent
     assert not np.array_equal(frames['tile16'][0][1], frames['tile16'][1][1])
-    assert not [f for f in __import__('os').listdir('/dev/shm') if f.startswith('blendtorch-')]
+    # this test's producers removed their rings (other tests may run concurrently)
+    mine = tuple(f'blendtorch-{pid}-' for pid in pids)
+    assert not [f for f in __import__('os').listdir('/dev/shm') if f.startswith(mine)]
     del shm

@@ -71,3 +71,52 @@ def test_reader_in_dataloader_workers(tmp_path):
     dl = tud.DataLoader(ds, batch_size=4, num_workers=2, shuffle=True)
     seen = sorted(int(v) for b in dl for v in b['x'][:, 0, 0])
     assert seen == list(range(16))
+
+
+class _Numpy1OnlyUnpickler(__import__('pickle').Unpickler):
+    """What a numpy 1.x reader can resolve: no ``numpy._core`` module path."""
+
+    def find_class(self, module, name):
+        if module.startswith('numpy._core'):
+            raise __import__('pickle').UnpicklingError(f'numpy 1.x cannot import {module}.{name}')
+        return super().find_class(module, name)
+
+
+def _load_all_numpy1(path):
+    import io
+    from blendtorch.btt.file import FileReader
+    data = open(path, 'rb').read()
+    assert b'numpy._core' not in data
+    hdr = _Numpy1OnlyUnpickler(io.BytesIO(data)).load()
+    offs = FileReader.read_offsets(path)
+    assert list(offs) == list(hdr[:len(offs)])
+    return [_Numpy1OnlyUnpickler(io.BytesIO(data[int(o):])).load() for o in offs]
+
+
+@pytest.mark.background
+def test_repickled_messages_are_numpy1_readable(tmp_path, free_port):
+    """Recordings of shared-memory producer frames (materialised, then
+    re-pickled) and DeviceReplayBuffer.save_recordings contain no numpy 2
+    module path: a numpy-1 reader loads every message."""
+    import numpy as np
+    import torch
+    from blendtorch import btt
+    from blendtorch.btt.replay import DeviceReplayBuffer
+    with btt.BlenderLauncher(producer='cubesim', num_instances=1, named_sockets=['DATA'], start_port=free_port,
+                             proto='ipc', seed=3,
+                             instance_args=[['--mode', 'rgb', '--resolution', '64x48', '--shm', '6']]) as bl:
+        ds = btt.RemoteIterableDataset(bl.launch_info.addresses['DATA'], max_items=6,
+                                       record_path_prefix=tmp_path / 'shm')
+        live = list(ds)
+    msgs = _load_all_numpy1(tmp_path / 'shm_00.btr')
+    assert len(msgs) == 6
+    for m, it in zip(msgs, live):
+        assert np.array_equal(m['image'], it['image']) and m['frameid'] == it['frameid']
+        assert m['xy'].dtype == np.float64 and m['xy'].shape == (8, 2)
+    rb = DeviceReplayBuffer(4, device='cpu')
+    rb.extend(torch.arange(4, dtype=torch.uint8).view(4, 1, 1, 1).expand(4, 3, 5, 4).contiguous(),
+              frameid=np.arange(4), xy=np.arange(16, dtype=np.float64).reshape(4, 2, 2))
+    [path] = rb.save_recordings(str(tmp_path / 'hbm'))
+    msgs = _load_all_numpy1(path)
+    assert [int(m['frameid']) for m in msgs] == [0, 1, 2, 3]
+    assert all(m['image'].shape == (3, 5, 4) and int(m['image'][0, 0, 0]) == i for i, m in enumerate(msgs))
