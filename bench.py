@@ -260,44 +260,26 @@ def main(argv=None):
                                   for k, v in comm.selfcheck().items()}
 
     # place each rank's producers on CPUs local to its GPU (same NUMA domain as
-    # the GPU's PCIe root: frames are written there and read back by the GPU)
-    from blendtorch.parallel import plan_rank_cpus
+    # the GPU's PCIe root: frames are written there and read back by the GPU),
+    # with disjoint port blocks and a /dev/shm share per rank
+    # (blendtorch/parallel/topology.py::plan_rank_resources)
+    from blendtorch.parallel import plan_rank_resources
     cpus, budget, pin = cpu_budget()
-    plan = plan_rank_cpus(local_rank, local_world, cpus[:budget] if pin else cpus)
-    share = max(1, budget // local_world)                 # CPUs this rank may keep busy
-    # one producer renders ~14k frames/s on the MI355X host (profiles/render_sweep.md):
-    # 4 saturate a GPU's PCIe link, 8 leave 2.5x headroom on a shared node
-    nprod = args.producers or max(1, min(8, share - 3))
-    if args.dist == 'scatter' and not args.producers:
-        # every frame crosses the ROOT's PCIe link (~42k RGBA frames/s, which 4-8
-        # producers saturate): 8 producers in total, launched NUMA-local on
-        # every rank, and the root connects to all of them
-        nprod = max(1, -(-8 // world))
-    mine = plan['cpus']
-    if pin:
-        affinity = [[mine[i % len(mine)]] for i in range(nprod)]
-    elif plan['numa_local']:
-        affinity = [plan['domain']] * nprod               # soft: any core of the GPU's domain
-    else:
-        affinity = None
+    res_w, res_h = (int(v) for v in args.resolution.lower().split('x'))
+    try:
+        st = os.statvfs('/dev/shm')
+        shm_free = st.f_bavail * st.f_frsize
+    except OSError:
+        shm_free = None
+    rp = plan_rank_resources(rank, local_rank, local_world, world, cpus, budget, pin, producers=args.producers,
+                             dist_mode=args.dist, shm_slots=args.shm, shm_free_bytes=shm_free,
+                             frame_bytes=res_w * res_h * (4 if args.mode == 'rgba' else 3))
+    plan = {'cpus': rp['cpus'], 'domain': rp['domain'], 'numa_local': rp['numa_local']}
+    share, nprod, affinity, shm_slots = rp['share'], rp['producers'], rp['affinity'], rp['shm_slots']
     if plan['numa_local']:
         os.sched_setaffinity(0, plan['domain'])           # loader threads next to the GPU too
-    start_port = args.start_port or (20000 + (os.getpid() % 200) * 50 if world == 1 else 21000 + rank * 64)
+    start_port = args.start_port or rp['start_port']
 
-    res_w, res_h = (int(v) for v in args.resolution.lower().split('x'))
-    # size the producers' shared-memory rings to what /dev/shm can hold for
-    # every local rank (a small /dev/shm would make ring creation fail and the
-    # producers fall back to inline frames)
-    shm_slots = args.shm
-    if shm_slots > 0:
-        try:
-            st = os.statvfs('/dev/shm')
-            free = st.f_bavail * st.f_frsize
-            frame = res_w * res_h * (4 if args.mode == 'rgba' else 3)
-            fit = int(0.6 * free / max(1, frame * max(1, nprod) * local_world))
-            shm_slots = min(shm_slots, fit) if fit >= 8 else 0
-        except OSError:
-            pass
     decode = DecodeConfig.unit(channels='rgb', gamma=2.2)
     amp = args.consumer == 'disc' and args.consumer_dtype == 'bf16'
     # decode inside the consumer's captured step (frames arrive by DMA only)

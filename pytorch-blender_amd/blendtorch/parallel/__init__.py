@@ -34,12 +34,12 @@ import torch.distributed as dist
 
 from .comm import DeviceComm  # noqa: E402
 from .grads import GradBuckets  # noqa: E402
-from .topology import parse_cpulist, plan_rank_cpus  # noqa: E402
+from .topology import parse_cpulist, plan_rank_cpus, plan_rank_resources  # noqa: E402
 
 __all__ = ['init_distributed', 'rank_world', 'shard_addresses', 'pool_addresses', 'partition_cpus', 'plan_rank_cpus',
            'parse_cpulist',
            'scatter_batch', 'broadcast_tensor', 'all_gather_stats', 'ScatterLoader', 'barrier', 'pack_meta',
-           'unpack_meta', 'DeviceComm', 'GradBuckets']
+           'unpack_meta', 'DeviceComm', 'GradBuckets', 'plan_rank_resources']
 
 
 def rank_world():

@@ -13,11 +13,15 @@ this pool, and the children need the devices to themselves), so it
    ``LOCAL_RANK``, ``WORLD_SIZE``, ``LOCAL_WORLD_SIZE``, ``MASTER_ADDR``,
    ``MASTER_PORT``), each in its own session so a whole rank (and the
    producer processes it launched) can be torn down as a group,
-4. relays their output (children share the parent's stdout/stderr, so rank
-   0's JSON line reaches the caller unchanged), and
+4. relays their output (children share the parent's stdout, so rank 0's
+   JSON line reaches the caller unchanged; each rank's stderr is relayed
+   line by line and its tail kept),
 5. returns the worst exit code.  If one rank fails the others are stopped
    after ``grace_s`` (a rank blocked in a collective on a dead peer would
-   otherwise hang until the RCCL timeout).
+   otherwise hang until the RCCL timeout), and
+6. prints, for every rank that failed, its exit status and the last lines
+   of its stderr in one block -- with 8 ranks interleaving their logs, the
+   failing rank's traceback is otherwise hard to find.
 
 The reference has no GPU ranks at all; its only scale axis is the number of
 Blender instances a single consumer process launches
@@ -25,15 +29,17 @@ Blender instances a single consumer process launches
 """
 from __future__ import annotations
 
+import collections
 import os
 import signal
 import socket
 import subprocess
 import sys
+import threading
 import time
 from typing import Dict, List, Optional, Sequence
 
-__all__ = ['visible_gpu_count', 'free_port', 'rank_env', 'spawn_ranks', 'worst_rc']
+__all__ = ['visible_gpu_count', 'free_port', 'rank_env', 'spawn_ranks', 'worst_rc', 'failure_report']
 
 
 def visible_gpu_count(timeout_s: float = 300.0) -> int:
@@ -91,9 +97,35 @@ def _kill_group(p: subprocess.Popen, sig: int):
         pass
 
 
+def _relay(stream, sink, tail: collections.deque):
+    """Copy a rank's stderr to ours line by line, keeping its last lines."""
+    for raw in iter(stream.readline, b''):
+        tail.append(raw.decode('utf-8', 'replace').rstrip('\n'))
+        try:
+            sink.write(raw)
+            sink.flush()
+        except (OSError, ValueError):
+            pass
+    stream.close()
+
+
+def failure_report(codes: Sequence[Optional[int]], tails: Sequence[Sequence[str]], first: Optional[int] = None) -> str:
+    """Text block naming every failed rank with the tail of its stderr
+    (the rank that failed first is marked: later ones were usually stopped)."""
+    out = []
+    for r, (c, tail) in enumerate(zip(codes, tails)):
+        if c in (0, None):
+            continue
+        sig = f' (signal {-c})' if c < 0 else ''
+        mark = ' [failed first]' if r == first else ''
+        out.append(f'[launch] rank {r} exited with {c}{sig}{mark}; last {len(tail)} stderr lines:')
+        out.extend(f'[launch]   rank {r}| {line}' for line in tail)
+    return '\n'.join(out)
+
+
 def spawn_ranks(cmd: Sequence[str], world: int, port: Optional[int] = None, grace_s: float = 30.0,
                 timeout_s: Optional[float] = None, env: Optional[Dict[str, str]] = None,
-                poll_s: float = 0.1):
+                poll_s: float = 0.1, tail_lines: int = 25, report=None):
     """Run ``cmd`` as ``world`` ranks on this node and wait for all of them.
 
     Returns ``(codes, rc)``: the per-rank exit codes and the job's exit status
@@ -101,14 +133,23 @@ def spawn_ranks(cmd: Sequence[str], world: int, port: Optional[int] = None, grac
     SIGTERM, which would hide the cause -- or 124 on ``timeout_s``).  When a rank exits non-zero (or
     ``timeout_s`` passes) the remaining ranks receive SIGTERM, then SIGKILL
     ``grace_s`` later; every rank runs in its own session and is signalled as
-    a process group."""
+    a process group.  Each rank's stderr is relayed to ours; the last
+    ``tail_lines`` of every failed rank are printed together at the end
+    (to ``report``, default ``sys.stderr``)."""
     port = port or free_port()
-    procs = [subprocess.Popen(list(cmd), env=rank_env(r, world, port, env), start_new_session=True)
+    procs = [subprocess.Popen(list(cmd), env=rank_env(r, world, port, env), start_new_session=True,
+                              stderr=subprocess.PIPE)
              for r in range(world)]
+    tails = [collections.deque(maxlen=tail_lines) for _ in range(world)]
+    sink = getattr(sys.stderr, 'buffer', None) or sys.stderr
+    relays = [threading.Thread(target=_relay, args=(p.stderr, sink, t), daemon=True) for p, t in zip(procs, tails)]
+    for t in relays:
+        t.start()
     codes: List[Optional[int]] = [None] * world
     t0 = time.monotonic()
     term_at = None
     rc = 0
+    first = None
     try:
         while any(c is None for c in codes):
             for i, p in enumerate(procs):
@@ -116,6 +157,7 @@ def spawn_ranks(cmd: Sequence[str], world: int, port: Optional[int] = None, grac
                     codes[i] = p.poll()
                     if codes[i] not in (None, 0) and rc == 0:
                         rc = worst_rc([codes[i]])
+                        first = i
             failed = rc != 0
             late = timeout_s is not None and time.monotonic() - t0 > timeout_s
             if late and rc == 0:
@@ -139,4 +181,11 @@ def spawn_ranks(cmd: Sequence[str], world: int, port: Optional[int] = None, grac
             except subprocess.TimeoutExpired:
                 _kill_group(p, signal.SIGKILL)
         raise
+    for t in relays:
+        t.join(5)
+    if rc:
+        text = failure_report(codes, [list(t) for t in tails], first)
+        if rc == 124 and first is None:
+            text = f'[launch] timed out after {timeout_s} s\n' + text
+        print(text, file=report or sys.stderr, flush=True)
     return codes, rc

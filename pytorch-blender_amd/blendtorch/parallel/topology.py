@@ -24,7 +24,7 @@ from typing import Dict, List, Optional, Sequence
 
 SYSFS_PCI = Path('/sys/bus/pci/devices')
 
-__all__ = ['parse_cpulist', 'gpu_pci_bus_id', 'pci_local_cpus', 'plan_rank_cpus']
+__all__ = ['parse_cpulist', 'gpu_pci_bus_id', 'pci_local_cpus', 'plan_rank_cpus', 'plan_rank_resources']
 
 
 def parse_cpulist(text: str) -> List[int]:
@@ -103,3 +103,56 @@ def plan_rank_cpus(local_rank: int, local_world: int, allowed: Sequence[int],
 
 def current_allowed_cpus() -> List[int]:
     return sorted(os.sched_getaffinity(0))
+
+
+def plan_rank_resources(rank: int, local_rank: int, local_world: int, world: int, allowed: Sequence[int],
+                        budget: int, pin: bool, producers: int = 0, dist_mode: str = 'shard', shm_slots: int = 48,
+                        shm_free_bytes: Optional[int] = None, frame_bytes: int = 640 * 480 * 4,
+                        named_sockets: int = 1, port_base: int = 21000, port_stride: int = 64,
+                        bus_ids: Optional[Sequence[Optional[str]]] = None, sysfs: Path = SYSFS_PCI,
+                        pid: Optional[int] = None) -> Dict[str, object]:
+    """Everything one rank of ``bench.py`` claims on the node, decided without
+    talking to the other ranks (so every rank computes the same, disjoint plan):
+
+    * ``cpus``/``domain``/``numa_local``: :func:`plan_rank_cpus` over the CPUs
+      the job may keep busy (``allowed`` trimmed to the cgroup ``budget`` when
+      per-core pinning isolates anything, i.e. ``pin``);
+    * ``producers``: producer processes this rank launches -- ``producers`` if
+      given, else one per spare CPU of its share (at most 8, at least 1; one
+      producer renders ~14k frames/s, profiles/render_sweep.md).  Scatter mode
+      spreads 8 producers over all ranks (the root's PCIe link is the bound);
+    * ``affinity``: per-producer CPU lists (single cores when pinning, the
+      GPU's NUMA domain otherwise, or None);
+    * ``start_port``: ``port_base + rank * port_stride`` (the launcher takes
+      ``producers`` consecutive ports per named socket), or a pid-derived base
+      for a single rank so concurrent jobs rarely collide;
+    * ``shm_slots``: ring slots per producer that fit 60 % of the free
+      ``/dev/shm`` shared by every local rank's producers (0 = inline frames
+      when fewer than 8 would fit).
+    """
+    plan = plan_rank_cpus(local_rank, local_world, list(allowed)[:budget] if pin else allowed, bus_ids, sysfs)
+    share = max(1, budget // max(1, local_world))
+    nprod = producers or max(1, min(8, share - 3))
+    if dist_mode == 'scatter' and not producers:
+        nprod = max(1, -(-8 // max(1, world)))
+    mine = plan['cpus']
+    if pin:
+        affinity = [[mine[i % len(mine)]] for i in range(nprod)]
+    elif plan['numa_local']:
+        affinity = [plan['domain']] * nprod
+    else:
+        affinity = None
+    if world == 1:
+        start_port = 20000 + ((os.getpid() if pid is None else pid) % 200) * 50
+    else:
+        start_port = port_base + rank * port_stride
+    span = nprod * max(1, named_sockets)
+    if span > port_stride and world > 1:
+        raise ValueError(f'{nprod} producers x {named_sockets} sockets exceed the {port_stride}-port block per rank')
+    slots = int(shm_slots)
+    if slots > 0 and shm_free_bytes is not None:
+        fit = int(0.6 * shm_free_bytes / max(1, frame_bytes * nprod * max(1, local_world)))
+        slots = min(slots, fit) if fit >= 8 else 0
+    return {'cpus': mine, 'domain': plan['domain'], 'numa_local': plan['numa_local'], 'share': share,
+            'producers': nprod, 'affinity': affinity, 'start_port': start_port, 'port_span': span,
+            'shm_slots': slots}

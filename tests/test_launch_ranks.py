@@ -26,7 +26,9 @@ RANK_PROG = textwrap.dedent('''
     if r == 0:
         print(json.dumps({'world': w, 'sum': t.item(), 'ranks': info}), flush=True)
     dist.destroy_process_group()
-    sys.exit(int(os.environ.get('FAIL_RANK', '-1')) == r and 7 or 0)
+    if int(os.environ.get('FAIL_RANK', '-1')) == r:
+        print(f'rank {r} says: simulated RCCL failure', file=sys.stderr, flush=True)
+        sys.exit(7)
 ''')
 
 
@@ -77,6 +79,57 @@ def test_spawn_two_gloo_ranks_relays_rank0(tmp_path):
 def test_failing_rank_sets_exit_code(tmp_path):
     r = _run_supervisor(tmp_path, 2, extra_env={'FAIL_RANK': '1'})
     assert r.returncode == 7, (r.stdout, r.stderr)
+    # the supervisor names the failed rank and repeats the tail of its stderr
+    assert '[launch] rank 1 exited with 7 [failed first]' in r.stderr, r.stderr
+    assert '[launch]   rank 1| rank 1 says: simulated RCCL failure' in r.stderr
+
+
+def test_failure_report_format():
+    text = launch.failure_report([0, -15, 3], [['ok'], ['stopped'], ['Traceback', 'RuntimeError: boom']], first=2)
+    assert 'rank 0' not in text
+    assert 'rank 1 exited with -15 (signal 15)' in text
+    assert 'rank 2 exited with 3 [failed first]' in text and 'rank 2| RuntimeError: boom' in text
+
+
+@pytest.mark.parametrize('mode', ['shard', 'pool', 'scatter'])
+def test_eight_rank_resource_plan_small_node(tmp_path, mode):
+    """8 ranks on a node whose cgroup allows 16 CPUs (of 256 visible) and a
+    256 MiB /dev/shm: every rank gets >= 1 producer, disjoint CPU slices and
+    port blocks, and the rings of all ranks fit /dev/shm together."""
+    from blendtorch.parallel import plan_rank_resources
+    allowed = list(range(256))
+    frame = 640 * 480 * 4
+    shm_free = 256 << 20
+    plans = [plan_rank_resources(r, r, 8, 8, allowed, budget=16, pin=False, dist_mode=mode, shm_slots=48,
+                                 shm_free_bytes=shm_free, frame_bytes=frame, bus_ids=[None] * 8, sysfs=tmp_path)
+             for r in range(8)]
+    assert all(p['producers'] >= 1 for p in plans)
+    if mode == 'scatter':
+        assert sum(p['producers'] for p in plans) >= 8
+    blocks = [range(p['start_port'], p['start_port'] + p['port_span']) for p in plans]
+    for i in range(8):
+        for j in range(i + 1, 8):
+            assert not set(blocks[i]) & set(blocks[j]), (i, j)
+    for i in range(8):
+        for j in range(i + 1, 8):
+            assert not set(plans[i]['cpus']) & set(plans[j]['cpus'])
+    used = sum(p['producers'] * p['shm_slots'] * frame for p in plans)
+    assert used <= shm_free
+    assert all(p['shm_slots'] == 0 or p['shm_slots'] >= 8 for p in plans)
+    # a roomy /dev/shm keeps the requested ring depth
+    big = plan_rank_resources(0, 0, 8, 8, allowed, 16, False, dist_mode=mode, shm_slots=48,
+                              shm_free_bytes=64 << 30, frame_bytes=frame, bus_ids=[None] * 8, sysfs=tmp_path)
+    assert big['shm_slots'] == 48
+
+
+def test_eight_rank_plan_pinned_quota():
+    """Pinned producers (the quota covers most of the affinity mask): every
+    producer gets one core of its own rank's slice."""
+    from blendtorch.parallel import plan_rank_resources
+    plans = [plan_rank_resources(r, r, 8, 8, list(range(64)), budget=64, pin=True, bus_ids=[None] * 8,
+                                 sysfs=Path('/nonexistent')) for r in range(8)]
+    for p in plans:
+        assert p['producers'] == 5 and all(len(a) == 1 and a[0] in p['cpus'] for a in p['affinity'])
 
 
 def test_hung_rank_is_stopped(tmp_path):
