@@ -77,28 +77,47 @@ class Discriminator(nn.Module):
 
     def bce_loss_bf16(self, x, target=1.0, mfma=True):
         """Mean binary cross-entropy of :meth:`forward_bf16`'s output against
-        ``target`` (scalar or [N]), with the adaptive head (pool -> 4x4 conv ->
-        sigmoid -> BCE) fused into ``ops.disc_head_bce`` (2 launches forward,
-        2 backward, instead of ~20 library kernels; fp32 weight and gradient).
+        ``target`` (scalar or [N]), with the head (pool -> 4x4 conv -> sigmoid
+        -> BCE) fused into ``ops.disc_head_bce`` (2 launches forward, 2
+        backward, instead of ~20 library kernels; fp32 weight and gradient).
         Falls back to :meth:`forward_bf16` + ``BCELoss`` off that shape.
         Returns the loss."""
+        return self.bce_bf16(x, target, mfma)[0]
+
+    def bce_bf16(self, x, target=1.0, mfma=True):
+        """``(mean BCE loss, per-sample probabilities)`` of the bf16 forward.
+
+        The fused head applies to the adaptive stack (pool -> conv -> sigmoid)
+        and to the plain DCGAN stack whose last conv consumes the whole
+        feature map (densityopt's 64x64 model: 4x4 features, 4x4 kernel --
+        the head kernel's pooling is then the identity)."""
         import torch.nn.functional as F
         from .. import ops
         layers = list(self.features)
-        head = layers[-3:]
-        fused = (len(head) == 3 and isinstance(head[0], ops.AdaptiveAvgPool2d) and isinstance(head[1], nn.Conv2d)
-                 and isinstance(head[2], nn.Sigmoid) and head[1].out_channels == 1 and head[1].bias is None
-                 and head[1].stride == (1, 1) and head[1].padding == (0, 0)
-                 and tuple(head[1].kernel_size) == _pair(head[0].output_size))
-        if not fused:
-            out = self.forward_bf16(x, mfma).float()
-            tgt = target if isinstance(target, torch.Tensor) else torch.full_like(out, float(target))
-            return F.binary_cross_entropy(out, tgt)
-        z = self._run_bf16(x, layers[:-3], mfma)
-        if not (z.is_cuda and z.is_contiguous(memory_format=torch.channels_last)):
-            z = z.contiguous(memory_format=torch.channels_last)
-        loss, _ = ops.disc_head_bce(z, head[1].weight, target, _pair(head[0].output_size))
-        return loss
+        head = body = pool = None
+        adaptive = (len(layers) >= 3 and isinstance(layers[-3], ops.AdaptiveAvgPool2d)
+                    and isinstance(layers[-2], nn.Conv2d) and isinstance(layers[-1], nn.Sigmoid)
+                    and tuple(layers[-2].kernel_size) == _pair(layers[-3].output_size))
+        if adaptive:
+            head, body, pool = layers[-2], layers[:-3], _pair(layers[-3].output_size)
+        elif len(layers) >= 2 and isinstance(layers[-2], nn.Conv2d) and isinstance(layers[-1], nn.Sigmoid):
+            head, body, pool = layers[-2], layers[:-2], tuple(layers[-2].kernel_size)
+        ok = (head is not None and x.is_cuda and head.out_channels == 1 and head.bias is None
+              and head.stride == (1, 1) and head.padding == (0, 0) and head.groups == 1
+              and head.in_channels % 8 == 0)
+        if ok:
+            z = self._run_bf16(x, body, mfma)
+            if adaptive or tuple(z.shape[2:]) == pool:
+                if not z.is_contiguous(memory_format=torch.channels_last):
+                    z = z.contiguous(memory_format=torch.channels_last)
+                loss, logits = ops.disc_head_bce(z, head.weight, target, pool)
+                return loss, torch.sigmoid(logits)
+            out = self._run_bf16(z, layers[len(body):], mfma)
+        else:
+            out = self._run_bf16(x, layers, mfma)
+        out = out.reshape(-1).float()
+        tgt = target if isinstance(target, torch.Tensor) else torch.full_like(out, float(target))
+        return F.binary_cross_entropy(out, tgt), out
 
     def _run_bf16(self, x, layers, mfma):
         import torch.nn.functional as F
@@ -162,9 +181,11 @@ class ProbModel(nn.Module):
 
     @property
     def dists(self):
-        # built on the fly so autograd sees fresh graphs every step
-        return (D.LogNormal(self.m1m2_mean[0], torch.exp(self.m1m2_log_std[0])),
-                D.LogNormal(self.m1m2_mean[1], torch.exp(self.m1m2_log_std[1])))
+        # built on the fly so autograd sees fresh graphs every step; no argument
+        # validation: its checks read device values back (a host sync per call,
+        # and not capturable in a HIP graph)
+        return (D.LogNormal(self.m1m2_mean[0], torch.exp(self.m1m2_log_std[0]), validate_args=False),
+                D.LogNormal(self.m1m2_mean[1], torch.exp(self.m1m2_log_std[1]), validate_args=False))
 
     def sample(self, n):
         m1, m2 = self.dists

@@ -184,15 +184,46 @@ def _meta_schema(batch, n, image_key):
     return tensors, objects
 
 
-def pack_meta(batch, schema, n):
-    """Per-item bytes of every tensor key, concatenated: u8 [n, M] (CPU)."""
+def _meta_row_bytes(schema):
+    row = 0
+    for _, dt, shp in schema:
+        per = torch.tensor([], dtype=getattr(torch, dt)).element_size()
+        for d in shp:
+            per *= int(d)
+        row += per
+    return row
+
+
+def pack_meta(batch, schema, n, out=None):
+    """Per-item bytes of every tensor key, concatenated: u8 [n, M] (CPU).
+
+    Every key must still match the agreed ``schema`` (dtype and per-item
+    shape): the peers' receive buffers were sized from it, and a row of a
+    different width would corrupt or hang the point-to-point round.
+    ``out``: an [n, M] u8 CPU tensor (e.g. pinned) to write into."""
     cols = []
-    for k, _, _ in schema:
-        v = batch[k].detach().to('cpu').contiguous()
+    for k, dt, shape in schema:
+        v = batch[k]
+        if not isinstance(v, torch.Tensor) or str(v.dtype).replace('torch.', '') != dt \
+                or tuple(v.shape[1:]) != tuple(shape) or v.shape[0] != n:
+            got = (tuple(v.shape), str(v.dtype)) if isinstance(v, torch.Tensor) else type(v).__name__
+            raise ValueError(f'scatter metadata {k!r} changed: agreed ({dt}, [{n}, *{tuple(shape)}]), got {got}')
+        v = v.detach().to('cpu').contiguous()
         cols.append(v.reshape(n, -1).view(torch.uint8).reshape(n, -1))
-    if not cols:
-        return torch.zeros((n, 0), dtype=torch.uint8)
-    return torch.cat(cols, dim=1).contiguous()
+    row = sum(c.shape[1] for c in cols)
+    if row != _meta_row_bytes(schema):
+        raise ValueError(f'scatter metadata row is {row} bytes, the agreed schema says {_meta_row_bytes(schema)}')
+    if out is None:
+        if not cols:
+            return torch.zeros((n, 0), dtype=torch.uint8)
+        return torch.cat(cols, dim=1).contiguous()
+    if tuple(out.shape) != (n, row):
+        raise ValueError(f'pack_meta: out is {tuple(out.shape)}, need {(n, row)}')
+    off = 0
+    for c in cols:
+        out[:, off:off + c.shape[1]].copy_(c)
+        off += c.shape[1]
+    return out
 
 
 def unpack_meta(packed, schema):
@@ -217,11 +248,18 @@ class ScatterLoader:
     What crosses xGMI is the undecoded u8 pixels (3-4 B/px instead of 12 B/px
     of fp32 planes) plus every fixed-size metadata tensor (btid, frameid,
     keypoints ...) packed into one byte row per item -- both in ONE grouped
-    ``batch_isend_irecv`` round: the root posts a send per peer at once, so
-    each point-to-point xGMI link carries its shard concurrently (a ring would
+    point-to-point round: the root posts a send per peer at once, so each
+    point-to-point xGMI link carries its shard concurrently (a ring would
     serialise them).  Every rank then runs the fused decode kernel on its own
-    shard.  The metadata schema is agreed once (first step); only keys that
-    are not fixed-size tensors (rare) fall back to a per-step object scatter.
+    shard.  The metadata schema is agreed once (first step) and every later
+    batch is checked against it; only keys that are not fixed-size tensors
+    (rare) fall back to a per-step object scatter.
+
+    No per-step host synchronisation on RCCL: the sends/receives are RCCL
+    calls on the compute stream (:class:`~.comm.DeviceComm`), the root's
+    metadata rows are packed into a reused pinned buffer and copied to the
+    device asynchronously, and receive buffers come from the caching
+    allocator.  The decode kernel follows on the same stream.
 
     Params
     ------
@@ -235,8 +273,10 @@ class ScatterLoader:
         (gloo rehearsals) the PyTorch reference -- bit-identical.
     device: where shards land and are decoded.
     num_batches: steps to deliver (all ranks must agree).
-    comm_device: device of the tensors handed to the process group (default:
-        ``device`` for NCCL/RCCL, CPU for gloo).
+    comm: a :class:`~.comm.DeviceComm` (default: one is created on the world
+        group when the first step runs -- collective).
+    comm_device: device of the tensors handed to a non-native (gloo) group
+        (default CPU for gloo, ``device`` otherwise).
 
     Reference semantics: the fan-out of PUSH/PULL round-robin across consumers
     (examples/datagen/Readme.md:168-177) and densityopt's partition of work
@@ -244,7 +284,7 @@ class ScatterLoader:
     """
 
     def __init__(self, source: Optional[Iterable], batch_size: int, decode, device: torch.device,
-                 num_batches: int, image_key: str = 'image', src: int = 0, comm_device=None):
+                 num_batches: int, image_key: str = 'image', src: int = 0, comm_device=None, comm=None):
         self.source = source
         self.batch_size = int(batch_size)
         self.decode = decode
@@ -253,6 +293,8 @@ class ScatterLoader:
         self.image_key = image_key
         self.src = src
         self.comm_device = comm_device
+        self.comm = comm
+        self._pinned = None
         self.stats = {'steps': 0, 'object_scatters': 0, 'bytes_sent': 0}
 
     def __len__(self):
@@ -273,11 +315,40 @@ class ScatterLoader:
             return ops.decode(shard, self.decode)
         return ops.reference_decode(shard, self.decode)
 
+    def _pack(self, batch, schema, n, cdev):
+        """Metadata rows on ``cdev``: packed into a reused (pinned) host
+        buffer, then one asynchronous copy."""
+        row = _meta_row_bytes(schema)
+        if cdev.type != 'cuda':
+            return pack_meta(batch, schema, n)
+        if self._pinned is None or tuple(self._pinned[0].shape) != (n, row):
+            # two host buffers used alternately: the async copy of step k may
+            # still read one while step k+1 packs the other
+            self._pinned = [torch.empty((n, row), dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+            self._pin_ev = [None, None]
+            self._pin_i = 0
+        i = self._pin_i
+        self._pin_i ^= 1
+        if self._pin_ev[i] is not None:
+            self._pin_ev[i].synchronize()      # the copy that read it two steps ago (long done)
+        host = pack_meta(batch, schema, n, out=self._pinned[i])
+        dev = torch.empty((n, row), dtype=torch.uint8, device=cdev)
+        dev.copy_(host, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(cdev))
+        self._pin_ev[i] = ev
+        return dev
+
     def __iter__(self):
         rank, world, _ = rank_world()
         multi = world > 1 and dist.is_available() and dist.is_initialized()
+        if multi and self.comm is None:
+            from .comm import DeviceComm
+            self.comm = DeviceComm(device=self.device if self.device.type == 'cuda' else None)
+        comm = self.comm
         it = iter(self.source) if rank == self.src else None
-        B, cdev = self.batch_size, self._comm_dev()
+        B = self.batch_size
+        cdev = self.device if (comm is not None and comm.native) else self._comm_dev()
         header = None          # (H, W, C, tensor schema, object keys), agreed on the first step
         for _ in range(self.num_batches):
             batch = next(it) if rank == self.src else None
@@ -292,35 +363,29 @@ class ScatterLoader:
                     box = [header]
                     dist.broadcast_object_list(box, src=self.src)
                     header = box[0]
+                row_bytes = _meta_row_bytes(header[1])
             shape, schema, objects = header
             if rank == self.src:
                 full = batch[self.image_key]
+                if tuple(full.shape) != (world * B,) + tuple(shape) or full.dtype != torch.uint8:
+                    raise ValueError(f'scatter source changed its image shape: {tuple(full.shape)}')
                 if full.device != cdev:
                     full = full.to(cdev)
-                meta = pack_meta(batch, schema, world * B).to(cdev, non_blocking=True)
+                meta = self._pack(batch, schema, world * B, cdev)
                 img = full[self.src * B:(self.src + 1) * B]
                 mrow = meta[self.src * B:(self.src + 1) * B]
                 if multi:
                     ops_ = []
                     for r in range(world):
                         if r != self.src:
-                            ops_.append(dist.P2POp(dist.isend, full[r * B:(r + 1) * B], r))
-                            ops_.append(dist.P2POp(dist.isend, meta[r * B:(r + 1) * B], r))
-                    for w in dist.batch_isend_irecv(ops_):
-                        w.wait()
-                    self.stats['bytes_sent'] += (world - 1) * B * (full[0].numel() + meta.shape[1])
+                            ops_.append((True, full[r * B:(r + 1) * B], r))
+                            ops_.append((True, meta[r * B:(r + 1) * B], r))
+                    comm.p2p(ops_)
+                    self.stats['bytes_sent'] += (world - 1) * B * (full[0].numel() + row_bytes)
             else:
-                row = 0
-                for _, dt, shp in schema:
-                    per = torch.tensor([], dtype=getattr(torch, dt)).element_size()
-                    for d in shp:
-                        per *= int(d)
-                    row += per
                 img = torch.empty((B,) + tuple(shape), dtype=torch.uint8, device=cdev)
-                mrow = torch.empty((B, row), dtype=torch.uint8, device=cdev)
-                for w in dist.batch_isend_irecv([dist.P2POp(dist.irecv, img, self.src),
-                                                 dist.P2POp(dist.irecv, mrow, self.src)]):
-                    w.wait()
+                mrow = torch.empty((B, row_bytes), dtype=torch.uint8, device=cdev)
+                comm.p2p([(False, img, self.src), (False, mrow, self.src)])
             if img.device != self.device:
                 img = img.to(self.device, non_blocking=True)
             out = {self.image_key: self._decode(img)}

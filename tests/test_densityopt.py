@@ -1,0 +1,135 @@
+"""densityopt (reference: examples/densityopt/densityopt.py:257-331) on the
+device-resident iteration (blendtorch.models.densityopt.DensityOptStep):
+gating semantics against a direct transcription of the reference rules, and
+data parallelism over gloo with 2 ranks (identical ProbModel and
+discriminator on both).  The GPU variant (bf16 MFMA discriminator, HIP graph,
+RCCL) runs in tests/test_gpu_consumer.py and profiles/r3/."""
+import importlib.util
+import json
+import os
+import socket
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _example():
+    spec = importlib.util.spec_from_file_location('densityopt_example', ROOT / 'examples' / 'densityopt' /
+                                                  'densityopt.py')
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_step_matches_reference_rules_cpu():
+    """Eager CPU iterations of DensityOptStep against the reference's host
+    logic (D step iff D_real - D_sim < 0.7; S step unless first and not yet
+    separated; baseline = first errS mean, then an EMA)."""
+    from blendtorch.models import Discriminator, ProbModel
+    from blendtorch.models.densityopt import DensityOptStep
+    import torch.nn as nn
+    B = 8
+    torch.manual_seed(0)
+    netA, netB = Discriminator(), Discriminator()
+    netB.load_state_dict(netA.state_dict())
+    pmA, pmB = ProbModel([1.2, 3.0], [0.4, 0.4]), ProbModel([1.2, 3.0], [0.4, 0.4])
+    g = torch.Generator().manual_seed(1)
+    real = torch.rand(B, 3, 64, 64, generator=g) * 2 - 1
+    step = DensityOptStep(netA, pmA, real.clone(), B, graph=False)
+    step.start()
+    optD = torch.optim.Adam(netB.parameters(), lr=5e-5, betas=(0.5, 0.999))
+    optS = torch.optim.Adam(pmB.parameters(), lr=5e-2, betas=(0.7, 0.999))
+    crit = nn.BCELoss(reduction='none')
+    b, first = 0.7, True
+    for it in range(6):
+        samples = {'m1': step.samples[0].clone(), 'm2': step.samples[1].clone()}
+        sim = torch.rand(B, 3, 64, 64, generator=g) * 2 - 1
+        sid = torch.randperm(B, generator=g)
+        step(sim, sid)
+        # reference transcription (densityopt.py:257-316)
+        netB.zero_grad()
+        out = netB(real)
+        crit(out, torch.ones(B)).mean().backward()
+        d_real = out.mean().item()
+        out = netB(sim)
+        crit(out, torch.zeros(B)).mean().backward()
+        d_sim = out.mean().item()
+        if d_real - d_sim < 0.7:
+            optD.step()
+        assert float(step.gate_d) == float(d_real - d_sim < 0.7)
+        if not first or d_real - d_sim >= 0.7:
+            optS.zero_grad()
+            with torch.no_grad():
+                errS = crit(netB(sim), torch.ones(B))
+            loss = pmB.log_prob(samples)[sid] * (errS - b)
+            loss.mean().backward()
+            optS.step()
+            b = errS.mean() if first else 0.9 * errS.mean() + 0.1 * b
+            first = False
+            assert float(step.gate_s) == 1.0
+        else:
+            assert float(step.gate_s) == 0.0
+        torch.testing.assert_close(step.b.reshape(()), torch.as_tensor(b, dtype=torch.float32).reshape(()),
+                                   rtol=1e-5, atol=1e-6)
+        for pa, pb in zip(pmA.parameters(), pmB.parameters()):
+            torch.testing.assert_close(pa, pb, rtol=1e-4, atol=1e-5)
+        for pa, pb in zip(netA.parameters(), netB.parameters()):
+            torch.testing.assert_close(pa, pb, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.background
+def test_densityopt_example_cpu(free_port):
+    mod = _example()
+    res = mod.main(['--device', 'cpu', '--num-epochs', '4', '--instances', '2', '--batch', '16',
+                    '--start-port', str(free_port)])
+    assert res['iterations'] == 5 and res['world'] == 1 and res['dtype'] == 'fp32'
+    assert all(d == d for d in res['abs_diff'])           # finite
+
+
+def _rank(rank, world, port, prod_port, out):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        mod = _example()
+        res = mod.main(['--device', 'cpu', '--backend', 'gloo', '--num-epochs', '3', '--instances', '2',
+                        '--batch', '8', '--start-port', str(prod_port), '--seed', str(rank)])
+        Path(out).write_text(json.dumps(res))
+    except Exception:
+        import traceback
+        Path(out).write_text(json.dumps({'error': traceback.format_exc()}))
+
+
+@pytest.mark.background
+def test_densityopt_data_parallel_gloo_world2(tmp_path):
+    """2 ranks, each with its own producers; rank 0's samples are broadcast,
+    gradients / gate statistics averaged: ProbModel and discriminator end
+    bit-identical on both ranks (different seeds would diverge them)."""
+    ctx = mp.get_context('spawn')
+    port = _free_port()
+    prod = 38000 + (os.getpid() % 400) * 10
+    outs = [tmp_path / f'r{r}.json' for r in range(2)]
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, prod, str(outs[r]))) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    res = [json.loads(o.read_text()) for o in outs]
+    for r in res:
+        assert 'error' not in r, r.get('error')
+    assert res[0]['world'] == 2 and res[0]['collectives'] == 'gloo'
+    assert res[0]['weights_sha'] == res[1]['weights_sha']
+    assert res[0]['final_params'] == res[1]['final_params']
+    assert res[0]['d_steps'] == res[1]['d_steps'] and res[0]['s_steps'] == res[1]['s_steps']

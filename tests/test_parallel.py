@@ -249,3 +249,17 @@ def test_captured_step_split_mid_hook_eager():
     sb(x)
     for p, q in zip(a.parameters(), b.parameters()):
         assert torch.equal(p, q)
+
+
+def test_pack_meta_rejects_schema_drift():
+    """A metadata tensor whose dtype or per-item shape changes after the
+    schema was agreed raises instead of sending rows of another width."""
+    b = {'btid': torch.arange(4), 'xy': torch.rand(4, 8, 2, dtype=torch.float64)}
+    schema, _ = parallel.__dict__['_meta_schema'](b, 4, 'image')
+    out = torch.empty((4, 8 + 128), dtype=torch.uint8)
+    assert parallel.pack_meta(b, schema, 4, out=out) is out
+    assert torch.equal(out, parallel.pack_meta(b, schema, 4))
+    with pytest.raises(ValueError, match="'xy' changed"):
+        parallel.pack_meta({'btid': torch.arange(4), 'xy': torch.rand(4, 9, 2, dtype=torch.float64)}, schema, 4)
+    with pytest.raises(ValueError, match="'btid' changed"):
+        parallel.pack_meta({'btid': torch.arange(4, dtype=torch.int32), 'xy': b['xy']}, schema, 4)
