@@ -198,10 +198,14 @@ void StreamLoader::promote_ready() {
   bool any = false;
   while (!unready_.empty() && unready_.front().pending->done()) {
     ReadyBatch& rb = unready_.front();
-    const bool torn = std::any_of(rb.slots.begin(), rb.slots.end(),
+    // a launch reap() has retired was validated there (before its slots were
+    // handed back: they may already belong to new frames); otherwise the
+    // slots are still held by this loader and are checked here
+    const bool torn = rb.launch_no > retired_launch_ &&
+                      std::any_of(rb.slots.begin(), rb.slots.end(),
                                   [](const ReadyBatch::SlotRef& s) { return !s.seg->valid(s.slot, s.gen); });
     std::lock_guard<std::mutex> lk(mu_);
-    if (torn && !cfg_.skip_bad) {
+    if ((torn || !error_.empty()) && !cfg_.skip_bad) {   // reap() may have failed the stream already
       if (error_.empty())
         error_ = "StreamLoader: shared-memory slot(s) were reclaimed by their producer while a batch read them";
       stop_ = true;
@@ -1009,6 +1013,7 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
   for (auto& b : group) {
     ReadyBatch rb;
     rb.index = batch_index_++;
+    rb.launch_no = launch_no;
     rb.items.reserve(b.items.size());
     for (auto& it : b.items) {
       fl.frames.push_back(std::move(it.frame));

@@ -171,6 +171,7 @@ struct ReadyBatch {
     uint32_t slot, gen;
   };
   std::vector<SlotRef> slots;        // host_sync: shm slots re-validated before hand-out
+  int64_t launch_no = 0;             // host_sync: the launch that read them
 };
 
 struct LoaderStats {

@@ -179,8 +179,9 @@ class DensityOptStep:
 
     def _capture_and_replay(self):
         g = torch.cuda.CUDAGraph()
-        # capture records without running: the iteration then runs as its first replay
-        with torch.cuda.graph(g):
+        # capture records without running: the iteration then runs as its first replay.
+        # thread_local: the stream loader's worker thread keeps making HIP calls
+        with torch.cuda.graph(g, capture_error_mode='thread_local'):
             self._iteration()
         self.graph = g
         g.replay()

@@ -169,15 +169,17 @@ class CapturedStep:
             if self.grads is None:
                 self.opt.zero_grad(set_to_none=True)
             if self.split:
-                with torch.cuda.graph(g):
+                with torch.cuda.graph(g, capture_error_mode='thread_local'):
                     loss = self._forward(self.x)
                 gb = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gb, pool=g.pool()):
+                with torch.cuda.graph(gb, pool=g.pool(), capture_error_mode='thread_local'):
                     self.loss = self._backward(loss)
                 del loss
                 self.graph_bwd = gb
             else:
-                with torch.cuda.graph(g):
+                # thread_local: the stream loader's worker thread keeps making
+                # HIP calls (event queries, copies) while this thread captures
+                with torch.cuda.graph(g, capture_error_mode='thread_local'):
                     self.loss = self._train(self.x)
             self.graph, self.state = g, 'graph'
         except RuntimeError as e:          # keep the run alive; callers report which mode ran

@@ -184,8 +184,11 @@ def _disc_steps(dev, buckets, graph, xs, grad_scale=None):
 @pytest.mark.parametrize('graph', [False, True])
 def test_bucketed_grads_written_in_place_train_identically(dev, graph):
     """The fused backward kernels (MFMA weight gradient, BN, head) write each
-    parameter's gradient straight into its GradBuckets view: training is
-    bit-identical to ordinary per-step gradient tensors, eager and graphed."""
+    parameter's gradient straight into its GradBuckets view: training matches
+    ordinary per-step gradient tensors, eager and graphed.  (Not bit-exact:
+    the weight-gradient slice reduce adds slice groups with float atomics, so
+    two runs differ by rounding; early Adam steps move each weight by ~lr,
+    so nearly every weight must agree far below lr.)"""
     g = torch.Generator(device=dev).manual_seed(7)
     xs = [torch.rand(4, 4, 96, 128, device=dev, generator=g).to(torch.bfloat16)
           .contiguous(memory_format=torch.channels_last) for _ in range(4)]
@@ -194,8 +197,10 @@ def test_bucketed_grads_written_in_place_train_identically(dev, graph):
     b, sb = _disc_steps(dev, True, graph, xs)
     assert ops.KERNEL_CALLS['conv_wgrad'] > before
     assert sb.state == ('graph' if graph else 'eager')
+    lr = 2e-4
     for pa, pb in zip(a.parameters(), b.parameters()):
-        torch.testing.assert_close(pb, pa, rtol=0, atol=0)
+        d = (pb - pa).detach().abs()
+        assert float(d.mean()) < 0.1 * lr and float((d > 0.5 * lr).float().mean()) < 0.02
 
 
 def test_rccl_direct_one_rank_process_group(dev, tmp_path):
@@ -221,5 +226,5 @@ def test_rccl_direct_one_rank_process_group(dev, tmp_path):
     res = json.loads(out.read_text())
     assert res['native'] and res['selfcheck']['native']
     assert res['collectives'] == 1 and res['state'] == 'graph'
-    assert res['max_abs_diff'] == 0.0
+    assert res['max_abs_diff'] < 1e-4                  # atomically-reduced weight gradients: rounding only
     assert res['allreduce_avg_ok'] and res['broadcast_ok'] and res['p2p_self_ok']
