@@ -29,9 +29,21 @@ enum Layout : int { NCHW = 0, NHWC = 1 };
 //               replay from an HBM-resident frame store), else at src + b*H*W*Cin.
 //   src_offsets_aligned  caller's promise that every src_offsets[b] is a
 //               multiple of 16 (frame-strided stores): keeps the vector path.
-//   lut         device float[4][256]: value for (output channel c, input u8 v).
-//               Gamma, scale and per-channel mean/std are folded into it on
-//               the host (bit-exact with the fp32 reference by construction).
+//   lut         device value table (kTableFloats floats, layout below): for
+//               every (output channel c, input u8 v) the fp32 value, plus an
+//               arithmetic form of the same table the kernels use instead of
+//               reading 1-KiB fp32 tables from LDS:
+//                 x = gamma[v] (channels fed by colour inputs when a gamma is
+//                     set) or v, then per channel one of
+//                 op 0: fma(x, a, b)   op 1: x*a - b   op 2: (x*a - b) / d
+//                 (each operation rounded separately, like numpy's float32).
+//               The host picks, per channel, an op it has VERIFIED to
+//               reproduce the fp32 table bit for bit for all 256 inputs
+//               (blendtorch.ops.build_table); mode 0 keeps the table lookup.
+//               The gamma bytes sit in LDS as a lane-private table (each of
+//               the 32 lanes of a ds_read_b32 group reads its own bank), so
+//               the data-dependent lookup is free of bank conflicts; without
+//               a gamma nothing is read from LDS at all.
 //   cmap[c]     input channel feeding output channel c (c < Cout).
 //   flip        nullable device u8[B]; 1 = image stored lower-left (GL order).
 //   flip_all    applies to every image (OR-ed with flip[b]).
@@ -43,6 +55,12 @@ enum Layout : int { NCHW = 0, NHWC = 1 };
 //               fused read, no staging copy and no DMA-engine round).
 //   max_grid    0: default grid cap; >0 overrides it (launch-shape sweeps).
 constexpr int kMaxSrcs = 64;
+// value-table layout (floats): [0, 1024) fp32 table [4][256]; header at
+// kXfHeader: mode, gamma_used, gam[4], op[4], a[4], b[4], d[4]; gamma u8[256]
+// packed little-endian at kXfGamma (64 floats' worth of bytes)
+constexpr int kXfHeader = 1024;
+constexpr int kXfGamma = 1088;
+constexpr int kTableFloats = 1152;
 struct DecodeParams {
   const uint8_t* src = nullptr;
   const int64_t* src_offsets = nullptr;

@@ -9,10 +9,12 @@
 //     contiguous run of the same pixels;
 //   * PPT is picked per output dtype so every plane store is exactly 16 B
 //     (f32: 4 px, bf16/f16: 8 px, u8: 16 px);
-//   * gamma + scale + per-channel mean/std are one 1-KiB-per-channel float
-//     table in LDS (one ds_read per element, no pow/div in the kernel, bit-
-//     exact with the fp32 reference because the host builds the table with
-//     the same fp32 expression);
+//   * gamma + scale + per-channel mean/std: the host verifies an arithmetic
+//     form of the fp32 reference table (fma, or mul/sub[/div] rounded like
+//     numpy) per channel, so the kernel computes the value; only the u8 gamma
+//     table is looked up, from a lane-private LDS copy (every lane of a
+//     ds_read group owns a bank: no conflicts, whatever the pixel values).
+//     Bit-exact with the fp32 reference (kernels.h: lut);
 //   * the vertical flip (GL lower-left readback) is a source-row remap.
 // color4x4: per-pixel 4x4 affine transform on the matrix cores with
 //   v_mfma_f32_4x4x1_16b_f32 (16 independent 4x4 blocks per wave, exact f32):
@@ -70,35 +72,121 @@ __device__ __forceinline__ void load_pixels(const uint8_t* p, Pixels<PPT, CIN>& 
   }
 }
 
-// Table lookup of input channel IC for the lane's PPT pixels.  The channel
-// map is a runtime value, but it is uniform across the wave: `lookup`
+// ---- value transform (kernels.h: lut) --------------------------------------
+// LDS holds either the fp32 table (fallback, <= 4 KiB) or the lane-private
+// gamma table: word (v >> 2) * 32 + (lane & 31) packs gamma[v & ~3 .. v | 3],
+// so lane l of a 32-lane ds_read group always hits bank l (8 KiB).
+constexpr int kTabWords = 2048;
+
+struct Xf {
+  int arith;               // 0: fp32 table lookups; 1: arithmetic
+  const float* lut;        // LDS fp32 table [c][256] (arith == 0)
+  const uint8_t* g;        // this lane's column of the LDS gamma table
+  int gam[4], op[4];
+  float a[4], b[4], d[4];
+};
+
+// Read the header (uniform: scalar loads) and stage the table; caller syncs.
+__device__ __forceinline__ Xf stage_xf(const float* T, uint32_t* tab, int nch) {
+  Xf x;
+  x.arith = T[kXfHeader] != 0.f;
+  x.lut = reinterpret_cast<const float*>(tab);
+  x.g = reinterpret_cast<const uint8_t*>(tab) + (threadIdx.x & 31) * 4;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    x.gam[c] = T[kXfHeader + 2 + c] != 0.f;
+    x.op[c] = int(T[kXfHeader + 6 + c]);
+    x.a[c] = T[kXfHeader + 10 + c];
+    x.b[c] = T[kXfHeader + 14 + c];
+    x.d[c] = T[kXfHeader + 18 + c];
+  }
+  if (!x.arith) {
+    for (int i = threadIdx.x; i < nch * 256; i += blockDim.x) reinterpret_cast<float*>(tab)[i] = T[i];
+  } else if (T[kXfHeader + 1] != 0.f) {
+    const uint32_t* gw = reinterpret_cast<const uint32_t*>(T + kXfGamma);
+    for (int i = threadIdx.x; i < kTabWords; i += blockDim.x) tab[i] = gw[i >> 5];
+  }
+  return x;
+}
+
+// op 1 / op 2 must round every operation on its own (numpy's float32 order),
+// never contract the multiply into an fma
+__device__ __forceinline__ float xf_mulsub(float x, float a, float b) {
+#pragma clang fp contract(off)
+  return x * a - b;
+}
+
+__device__ __forceinline__ float xf_apply(int op, float x, float a, float b, float d) {
+  if (op == 0) return __builtin_fmaf(x, a, b);
+  const float t = xf_mulsub(x, a, b);
+  return op == 1 ? t : t / d;   // correctly rounded fp32 division (HIP default)
+}
+
+__device__ __forceinline__ float xf_source(const Xf& xf, int c, uint32_t v) {
+  return xf.gam[c] ? float(xf.g[(v >> 2) * 128 + (v & 3)]) : float(v);
+}
+
+// Value of output channel c for input byte v (scalar paths).
+__device__ __forceinline__ float xf_value(const Xf& xf, int c, uint32_t v) {
+  if (!xf.arith) return xf.lut[c * 256 + v];
+  return xf_apply(xf.op[c], xf_source(xf, c, v), xf.a[c], xf.b[c], xf.d[c]);
+}
+
+// Output channel c from input channel IC for the lane's PPT pixels.  The
+// channel map is a runtime value, but it is uniform across the wave: `lookup`
 // branches on it once (scalar branch) into a fully static body, so every
 // byte of `px` is addressed with a compile-time index and `px` stays in
 // VGPRs (a dynamically indexed byte array would be spilled to scratch).
 template <int PPT, int CIN, int IC>
-__device__ __forceinline__ void lookup_static(const Pixels<PPT, CIN>& px, const float* l, float (&o)[PPT]) {
+__device__ __forceinline__ void lookup_static(const Pixels<PPT, CIN>& px, const Xf& xf, int c, float (&o)[PPT]) {
+  if (!xf.arith) {
+    const float* l = xf.lut + c * 256;
 #pragma unroll
-  for (int i = 0; i < PPT; ++i) o[i] = l[px.v[i * CIN + IC]];
+    for (int i = 0; i < PPT; ++i) o[i] = l[px.v[i * CIN + IC]];
+    return;
+  }
+  float x[PPT];
+  if (xf.gam[c]) {
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const uint32_t v = px.v[i * CIN + IC];
+      x[i] = float(xf.g[(v >> 2) * 128 + (v & 3)]);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) x[i] = float(px.v[i * CIN + IC]);
+  }
+  const float a = xf.a[c], b = xf.b[c], d = xf.d[c];
+  if (xf.op[c] == 0) {
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) o[i] = __builtin_fmaf(x[i], a, b);
+  } else if (xf.op[c] == 1) {
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) o[i] = xf_mulsub(x[i], a, b);
+  } else {
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) o[i] = xf_mulsub(x[i], a, b) / d;
+  }
 }
 
 template <int PPT, int CIN>
-__device__ __forceinline__ void lookup(const Pixels<PPT, CIN>& px, int ic, const float* l, float (&o)[PPT]) {
+__device__ __forceinline__ void lookup(const Pixels<PPT, CIN>& px, int ic, const Xf& xf, int c, float (&o)[PPT]) {
   switch (ic) {
-    case 0: lookup_static<PPT, CIN, 0>(px, l, o); break;
-    case 1: if constexpr (CIN > 1) lookup_static<PPT, CIN, 1>(px, l, o); break;
-    case 2: if constexpr (CIN > 2) lookup_static<PPT, CIN, 2>(px, l, o); break;
-    default: if constexpr (CIN > 3) lookup_static<PPT, CIN, 3>(px, l, o); break;
+    case 0: lookup_static<PPT, CIN, 0>(px, xf, c, o); break;
+    case 1: if constexpr (CIN > 1) lookup_static<PPT, CIN, 1>(px, xf, c, o); break;
+    case 2: if constexpr (CIN > 2) lookup_static<PPT, CIN, 2>(px, xf, c, o); break;
+    default: if constexpr (CIN > 3) lookup_static<PPT, CIN, 3>(px, xf, c, o); break;
   }
 }
 
 template <int PPT, int CIN, int OUTT, int COUT>
-__device__ __forceinline__ void store_nhwc(const DecodeParams& p, const float* lut, const int* cm,
+__device__ __forceinline__ void store_nhwc(const DecodeParams& p, const Xf& xf, const int* cm,
                                            const Pixels<PPT, CIN>& px, int b, int64_t q, int64_t HW) {
   constexpr int N = PPT * COUT;
   const int64_t off = q * COUT;   // within image b (NHWC)
   float v[COUT][PPT];
 #pragma unroll
-  for (int c = 0; c < COUT; ++c) lookup<PPT, CIN>(px, cm[c], lut + c * 256, v[c]);
+  for (int c = 0; c < COUT; ++c) lookup<PPT, CIN>(px, cm[c], xf, c, v[c]);
   if constexpr (OUTT == OUT_F32) {
     float o[N];
 #pragma unroll
@@ -171,7 +259,7 @@ __device__ __forceinline__ Group locate(const DecodeParams& p, int64_t g, int64_
 }
 
 template <int PPT, int CIN, int OUTT, int LAYOUT>
-__device__ __forceinline__ void emit(const DecodeParams& p, const float* lut, const int* cm, int cout, int64_t HW,
+__device__ __forceinline__ void emit(const DecodeParams& p, const Xf& xf, const int* cm, int cout, int64_t HW,
                                      const Group& gr, const Pixels<PPT, CIN>& px) {
   const int b = gr.b;
   const int64_t q = gr.q;
@@ -180,7 +268,7 @@ __device__ __forceinline__ void emit(const DecodeParams& p, const float* lut, co
     for (int c = 0; c < 4; ++c) {
       if (c >= cout) break;
       float v[PPT];
-      lookup<PPT, CIN>(px, cm[c], lut + c * 256, v);
+      lookup<PPT, CIN>(px, cm[c], xf, c, v);
       const int64_t off = int64_t(c) * HW + q;   // within image b (NCHW)
       if constexpr (OUTT == OUT_F32) {
         float* d = image_out<float>(p, b, HW * cout) + off;
@@ -206,10 +294,10 @@ __device__ __forceinline__ void emit(const DecodeParams& p, const float* lut, co
     // NHWC (channels_last): PPT*COUT contiguous elements, assembled in
     // registers and written as 16-byte stores (PPT*sizeof(T) == 16).
     switch (cout) {
-      case 1: store_nhwc<PPT, CIN, OUTT, 1>(p, lut, cm, px, b, q, HW); break;
-      case 2: store_nhwc<PPT, CIN, OUTT, 2>(p, lut, cm, px, b, q, HW); break;
-      case 3: store_nhwc<PPT, CIN, OUTT, 3>(p, lut, cm, px, b, q, HW); break;
-      default: store_nhwc<PPT, CIN, OUTT, 4>(p, lut, cm, px, b, q, HW); break;
+      case 1: store_nhwc<PPT, CIN, OUTT, 1>(p, xf, cm, px, b, q, HW); break;
+      case 2: store_nhwc<PPT, CIN, OUTT, 2>(p, xf, cm, px, b, q, HW); break;
+      case 3: store_nhwc<PPT, CIN, OUTT, 3>(p, xf, cm, px, b, q, HW); break;
+      default: store_nhwc<PPT, CIN, OUTT, 4>(p, xf, cm, px, b, q, HW); break;
     }
   }
 }
@@ -219,8 +307,8 @@ __device__ __forceinline__ void emit(const DecodeParams& p, const float* lut, co
 // flight (memory-level parallelism once the grid is smaller than the work).
 template <int PPT, int CIN, int OUTT, int LAYOUT, int U>
 __global__ __launch_bounds__(kBlock) void decode_vec_kernel(DecodeParams p) {
-  __shared__ float lut[4 * 256];
-  for (int i = threadIdx.x; i < p.Cout * 256; i += kBlock) lut[i] = p.lut[i];
+  __shared__ uint32_t tab[kTabWords];
+  const Xf xf = stage_xf(p.lut, tab, p.Cout);
   __syncthreads();
 
   const int64_t HW = int64_t(p.H) * p.W;
@@ -244,10 +332,10 @@ __global__ __launch_bounds__(kBlock) void decode_vec_kernel(DecodeParams p) {
       const Group gr1 = locate<PPT, CIN>(p, has1 ? g1 : g0, groups_per_img, HW, small);
       Pixels<PPT, CIN> px1;
       load_pixels<PPT, CIN>(gr1.src, px1);
-      emit<PPT, CIN, OUTT, LAYOUT>(p, lut, cm, cout, HW, gr0, px0);
-      if (has1) emit<PPT, CIN, OUTT, LAYOUT>(p, lut, cm, cout, HW, gr1, px1);
+      emit<PPT, CIN, OUTT, LAYOUT>(p, xf, cm, cout, HW, gr0, px0);
+      if (has1) emit<PPT, CIN, OUTT, LAYOUT>(p, xf, cm, cout, HW, gr1, px1);
     } else {
-      emit<PPT, CIN, OUTT, LAYOUT>(p, lut, cm, cout, HW, gr0, px0);
+      emit<PPT, CIN, OUTT, LAYOUT>(p, xf, cm, cout, HW, gr0, px0);
     }
   }
 }
@@ -270,8 +358,8 @@ __global__ __launch_bounds__(kBlock) void tile_fill_kernel(DecodeParams p, TileP
 // `idx` of a tile takes PPT pixels of tile row idx / (16 / PPT).
 template <int PPT, int CIN, int OUTT, int LAYOUT>
 __global__ __launch_bounds__(kBlock) void tile_scatter_kernel(DecodeParams p, TileParams t) {
-  __shared__ float lut[4 * 256];
-  for (int i = threadIdx.x; i < p.Cout * 256; i += kBlock) lut[i] = p.lut[i];
+  __shared__ uint32_t tab[kTabWords];
+  const Xf xf = stage_xf(p.lut, tab, p.Cout);
   __syncthreads();
   constexpr int T = 16, LPT = T * T / PPT, LPR = T / PPT;
   const int64_t HW = int64_t(p.H) * p.W;
@@ -298,15 +386,15 @@ __global__ __launch_bounds__(kBlock) void tile_scatter_kernel(DecodeParams p, Ti
     gr.b = b;
     gr.q = int64_t(flip ? p.H - 1 - sy : sy) * p.W + x;
     gr.src = nullptr;
-    emit<PPT, CIN, OUTT, LAYOUT>(p, lut, cm, cout, HW, gr, px);
+    emit<PPT, CIN, OUTT, LAYOUT>(p, xf, cm, cout, HW, gr, px);
   }
 }
 
 // Generic fallback: one pixel per thread (any W, any alignment).
 template <int OUTT>
 __global__ __launch_bounds__(kBlock) void decode_scalar_kernel(DecodeParams p) {
-  __shared__ float lut[4 * 256];
-  for (int i = threadIdx.x; i < p.Cout * 256; i += kBlock) lut[i] = p.lut[i];
+  __shared__ uint32_t tab[kTabWords];
+  const Xf xf = stage_xf(p.lut, tab, p.Cout);
   __syncthreads();
   const int64_t HW = int64_t(p.H) * p.W;
   const int64_t total = HW * p.B;
@@ -319,7 +407,7 @@ __global__ __launch_bounds__(kBlock) void decode_scalar_kernel(DecodeParams p) {
     const uint8_t* img = p.nsrcs ? p.srcs[b] : p.src + (p.src_offsets ? p.src_offsets[b] : int64_t(b) * HW * p.Cin);
     const uint8_t* s = img + (int64_t(sy) * p.W + x) * p.Cin;
     for (int c = 0; c < p.Cout; ++c) {
-      float v = lut[c * 256 + s[p.cmap[c]]];
+      const float v = xf_value(xf, c, s[p.cmap[c]]);
       const int64_t off = p.layout == NCHW ? int64_t(c) * HW + q : q * p.Cout + c;   // within image b
       const int64_t ie = HW * p.Cout;
       if constexpr (OUTT == OUT_F32) image_out<float>(p, b, ie)[off] = v;
@@ -489,13 +577,13 @@ __device__ __forceinline__ uint32_t philox_word(uint64_t seed, uint64_t ctr, uin
 // Block prologue shared by both replay kernels: the table, this launch's B
 // frame indices (drawn or given) in LDS, and the counter hand-over.
 struct ReplayShared {
-  float lut[4 * 256];
+  uint32_t tab[kTabWords];
   int64_t idx[kMaxReplayB];
   uint64_t ctr;
 };
 
-__device__ void replay_prologue(const DecodeParams& p, const ReplayParams& r, ReplayShared& sh) {
-  for (int i = threadIdx.x; i < p.Cout * 256; i += kBlock) sh.lut[i] = p.lut[i];
+__device__ Xf replay_prologue(const DecodeParams& p, const ReplayParams& r, ReplayShared& sh) {
+  const Xf xf = stage_xf(p.lut, sh.tab, p.Cout);
   if (threadIdx.x == 0) sh.ctr = r.index_in ? 0 : (r.counter ? r.counter[0] : r.ctr_value);
   __syncthreads();
   for (int b = threadIdx.x; b < p.B; b += kBlock) {
@@ -505,6 +593,7 @@ __device__ void replay_prologue(const DecodeParams& p, const ReplayParams& r, Re
     if (blockIdx.x == 0 && r.index_out) r.index_out[b] = i;
   }
   __syncthreads();
+  return xf;
 }
 
 // The counter moves on in a one-lane kernel queued right behind the sample:
@@ -565,7 +654,7 @@ __global__ __launch_bounds__(kBlock) void replay_vec_kernel(DecodeParams p, Repl
     gr0.src = p.src + frame_of(gr0.b) * r.frame_bytes + (int64_t(sy) * p.W + x) * CIN;
     load_pixels<PPT, CIN>(gr0.src, px0);
   }
-  for (int i = threadIdx.x; i < p.Cout * 256; i += kBlock) sh.lut[i] = p.lut[i];
+  const Xf xf = stage_xf(p.lut, sh.tab, p.Cout);
   for (int b = threadIdx.x; b < p.B; b += kBlock) {
     const int64_t i = frame_of(b);
     sh.idx[b] = i;
@@ -578,7 +667,7 @@ __global__ __launch_bounds__(kBlock) void replay_vec_kernel(DecodeParams p, Repl
       continue;
     }
     if (g == g0) {
-      emit<PPT, CIN, OUTT, LAYOUT>(p, sh.lut, cm, cout, HW, gr0, px0);
+      emit<PPT, CIN, OUTT, LAYOUT>(p, xf, cm, cout, HW, gr0, px0);
       continue;
     }
     Group gr;
@@ -588,7 +677,7 @@ __global__ __launch_bounds__(kBlock) void replay_vec_kernel(DecodeParams p, Repl
     gr.src = p.src + sh.idx[gr.b] * r.frame_bytes + (int64_t(sy) * p.W + x) * CIN;
     Pixels<PPT, CIN> px;
     load_pixels<PPT, CIN>(gr.src, px);
-    emit<PPT, CIN, OUTT, LAYOUT>(p, sh.lut, cm, cout, HW, gr, px);
+    emit<PPT, CIN, OUTT, LAYOUT>(p, xf, cm, cout, HW, gr, px);
   }
 }
 
@@ -596,7 +685,7 @@ __global__ __launch_bounds__(kBlock) void replay_vec_kernel(DecodeParams p, Repl
 template <int OUTT>
 __global__ __launch_bounds__(kBlock) void replay_scalar_kernel(DecodeParams p, ReplayParams r, int64_t meta_units) {
   __shared__ ReplayShared sh;
-  replay_prologue(p, r, sh);
+  const Xf xf = replay_prologue(p, r, sh);
   const int64_t HW = int64_t(p.H) * p.W;
   const int64_t total = HW * p.B;
   const int64_t ie = HW * p.Cout;
@@ -611,7 +700,7 @@ __global__ __launch_bounds__(kBlock) void replay_scalar_kernel(DecodeParams p, R
     const int sy = p.flip_all ? p.H - 1 - y : y;
     const uint8_t* s = p.src + sh.idx[b] * r.frame_bytes + (int64_t(sy) * p.W + x) * p.Cin;
     for (int c = 0; c < p.Cout; ++c) {
-      const float v = sh.lut[c * 256 + s[p.cmap[c]]];
+      const float v = xf_value(xf, c, s[p.cmap[c]]);
       const int64_t off = p.layout == NCHW ? int64_t(c) * HW + q : q * p.Cout + c;
       if constexpr (OUTT == OUT_F32) reinterpret_cast<float*>(p.dst)[int64_t(b) * ie + off] = v;
       else if constexpr (OUTT == OUT_BF16) reinterpret_cast<uint16_t*>(p.dst)[int64_t(b) * ie + off] = f2bf(v);
@@ -693,8 +782,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // reg, and for a fixed reg the 16 lanes of one channel cover 64 contiguous
 // pixels: every store instruction writes four 256-byte plane runs.
 __global__ __launch_bounds__(kBlock) void color4x4_kernel(Color4x4Params p) {
-  __shared__ float lut[4 * 256];
-  for (int i = threadIdx.x; i < 4 * 256; i += kBlock) lut[i] = p.lut[i];
+  __shared__ uint32_t tab[kTabWords];
+  const Xf xf = stage_xf(p.lut, tab, 4);   // indexed by INPUT channel here
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -723,8 +812,8 @@ __global__ __launch_bounds__(kBlock) void color4x4_kernel(Color4x4Params p) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const uint32_t px = w[s];
-      const float a0 = lut[0 * 256 + (px & 0xff)], a1 = lut[1 * 256 + ((px >> 8) & 0xff)];
-      const float a2 = lut[2 * 256 + ((px >> 16) & 0xff)], a3 = lut[3 * 256 + (px >> 24)];
+      const float a0 = xf_value(xf, 0, px & 0xff), a1 = xf_value(xf, 1, (px >> 8) & 0xff);
+      const float a2 = xf_value(xf, 2, (px >> 16) & 0xff), a3 = xf_value(xf, 3, px >> 24);
       f32x4 c = {bj, bj, bj, bj};
       c = __builtin_amdgcn_mfma_f32_4x4x1f32(a0, bm[0], c, 0, 0, 0);
       c = __builtin_amdgcn_mfma_f32_4x4x1f32(a1, bm[1], c, 0, 0, 0);

@@ -109,7 +109,11 @@ void PinnedPool::release(void* owner, Buffer* b) {
 StreamLoader::StreamLoader(const LoaderConfig& cfg) : cfg_(cfg) {
   if (cfg_.addresses.empty()) throw std::invalid_argument("StreamLoader: no addresses");
   if (cfg_.batch_size < 1) throw std::invalid_argument("StreamLoader: batch_size < 1");
-  if (cfg_.lut.size() != 4 * 256) throw std::invalid_argument("StreamLoader: lut must hold 4*256 floats");
+  // the value table (kernels.h): a bare [4][256] fp32 table is padded with a
+  // zero header (mode 0: table lookups)
+  if (cfg_.lut.size() == 4 * 256) cfg_.lut.resize(kTableFloats, 0.f);
+  if (cfg_.lut.size() != size_t(kTableFloats))
+    throw std::invalid_argument("StreamLoader: lut must hold 4*256 or kTableFloats floats");
   if (cfg_.cout < 1 || cfg_.cout > 4) throw std::invalid_argument("StreamLoader: cout must be 1..4");
   if (cfg_.color_matrix && (cfg_.matrix.size() != 16 || cfg_.bias.size() != 4))
     throw std::invalid_argument("StreamLoader: colour matrix needs 16 + 4 floats");
@@ -555,8 +559,8 @@ bool StreamLoader::process(zmtp::Message&& msg) {
       check(hipMalloc(reinterpret_cast<void**>(&p), img_bytes_ * size_t(cfg_.batch_size)), "hipMalloc(staging)");
       staging_.push_back(p);
     }
-    check(hipMalloc(reinterpret_cast<void**>(&d_lut_), 4 * 256 * sizeof(float)), "hipMalloc(lut)");
-    check(hipMemcpy(d_lut_, cfg_.lut.data(), 4 * 256 * sizeof(float), hipMemcpyHostToDevice), "upload lut");
+    check(hipMalloc(reinterpret_cast<void**>(&d_lut_), kTableFloats * sizeof(float)), "hipMalloc(lut)");
+    check(hipMemcpy(d_lut_, cfg_.lut.data(), kTableFloats * sizeof(float), hipMemcpyHostToDevice), "upload lut");
     if (cfg_.color_matrix) {
       check(hipMalloc(reinterpret_cast<void**>(&d_mat_), 20 * sizeof(float)), "hipMalloc(matrix)");
       std::vector<float> mb(cfg_.matrix);

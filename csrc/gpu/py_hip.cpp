@@ -577,7 +577,7 @@ PYBIND11_MODULE(_hip, m) {
           float *dst = nullptr, *lut = nullptr;
           check(hipMalloc(reinterpret_cast<void**>(&stage), img * B), "hipMalloc");
           check(hipMalloc(reinterpret_cast<void**>(&dst), size_t(B) * 3 * H * W * sizeof(float)), "hipMalloc");
-          std::vector<float> hl(4 * 256);
+          std::vector<float> hl(kTableFloats, 0.f);   // identity table, mode 0 header
           for (int i = 0; i < 4 * 256; ++i) hl[size_t(i)] = float(i & 255);
           check(hipMalloc(reinterpret_cast<void**>(&lut), hl.size() * sizeof(float)), "hipMalloc");
           check(hipMemcpy(lut, hl.data(), hl.size() * sizeof(float), hipMemcpyHostToDevice), "lut");

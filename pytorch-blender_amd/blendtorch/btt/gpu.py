@@ -175,7 +175,7 @@ class DeviceLoader:
     def _make(self):
         ext = ops.hip_ext()
         cfg = self.decode
-        lut = ops.build_lut(cfg).reshape(-1).tolist()
+        lut = ops.build_table(cfg).tolist()
         matrix = [] if cfg.color_matrix is None else np.asarray(cfg.color_matrix, np.float32).reshape(-1).tolist()
         bias = [] if cfg.color_matrix is None else list(cfg.color_bias or (0.0, 0.0, 0.0, 0.0))
         max_batches = -1 if self.max_items is None else self.max_items // self.batch_size

@@ -28,7 +28,8 @@ from typing import Optional, Sequence
 import numpy as np
 
 __all__ = [
-    'DecodeConfig', 'hip_ext', 'hip_available', 'gamma_lut', 'build_lut', 'decode', 'decode_gather', 'color4x4',
+    'DecodeConfig', 'hip_ext', 'hip_available', 'gamma_lut', 'build_lut', 'build_table', 'decode', 'decode_gather',
+    'color4x4',
     'project', 'adaptive_avg_pool_nhwc', 'AdaptiveAvgPool2d', 'batch_norm_leaky_relu', 'BatchNormLeakyReLU2d',
     'reference_decode', 'reference_color4x4', 'reference_project', 'reference_gamma',
 ]
@@ -201,6 +202,77 @@ def build_lut(cfg: DecodeConfig) -> np.ndarray:
     return lut
 
 
+# value table handed to the kernels (csrc/gpu/kernels.h: lut): the fp32 table
+# plus a per-channel arithmetic form the host has verified bit for bit
+XF_HEADER, XF_GAMMA, TABLE_FLOATS = 1024, 1088, 1152
+
+
+def _xform_channel(x, y, gam, normalize, scale, mean, std):
+    """(op, a, b, d) reproducing float32 table ``y`` from inputs ``x`` exactly,
+    or None.  Candidates are the reference expression itself, rounded like
+    numpy: op 1 ``x*scale - mean``, op 2 ``(x*scale - mean) / std``; op 0
+    (one fma) only where it is provably identical (``b == 0``: fma(x, a, 0)
+    is the correctly rounded product)."""
+    f32 = np.float32
+    cands = []
+    if not normalize:
+        cands.append((0, f32(1.0), f32(0.0), f32(1.0)))
+    else:
+        if mean == 0.0 and std == 1.0:
+            cands.append((0, f32(scale), f32(0.0), f32(1.0)))
+        if std == 1.0:
+            cands.append((1, f32(scale), f32(mean), f32(1.0)))
+        cands.append((2, f32(scale), f32(mean), f32(std)))
+    with np.errstate(all='ignore'):
+        for op, a, b, d in cands:
+            if op == 0:
+                z = x * a            # b == 0: the fma is this product, rounded once
+            elif op == 1:
+                z = x * a - b
+            else:
+                z = (x * a - b) / d
+            if np.array_equal(z.view(np.uint32), y.view(np.uint32)):
+                return op, float(a), float(b), float(d)
+    return None
+
+
+def build_table(cfg: DecodeConfig) -> np.ndarray:
+    """float32[TABLE_FLOATS]: :func:`build_lut` plus the header and u8 gamma
+    table of the kernels' arithmetic path (see csrc/gpu/kernels.h).  Falls
+    back to mode 0 (fp32 table lookups) if any channel has no verified form."""
+    lut = build_lut(cfg)
+    out = np.zeros(TABLE_FLOATS, dtype=np.float32)
+    out[:1024] = lut.reshape(-1)
+    g = gamma_lut(cfg.gamma)
+    gf = g.astype(np.float32)
+    ident = np.arange(256, dtype=np.float32)
+    if cfg.color_matrix is not None:
+        chans = [(k, k) for k in range(4)]          # indexed by input channel, no normalisation
+        normalize = False
+    else:
+        chans = list(enumerate(cfg.cmap))
+        normalize = not (cfg.mean is None and cfg.std is None and cfg.scale == 1.0)
+    mean = list(cfg.mean) if cfg.mean is not None else [0.0] * 4
+    std = list(cfg.std) if cfg.std is not None else [1.0] * 4
+    hdr = np.zeros(22, dtype=np.float32)
+    hdr[6:10] = 0
+    hdr[10:14] = 1.0
+    hdr[18:22] = 1.0
+    for c, ic in chans:
+        gam = bool(cfg.gamma) and ic < 3
+        x = gf if gam else ident
+        form = _xform_channel(x, lut[c], gam, normalize, np.float32(cfg.scale), mean[c], std[c])
+        if form is None:
+            return out                              # mode 0: table lookups
+        op, a, b, d = form
+        hdr[2 + c], hdr[6 + c], hdr[10 + c], hdr[14 + c], hdr[18 + c] = float(gam), op, a, b, d
+        hdr[1] = max(hdr[1], float(gam))
+    hdr[0] = 1.0
+    out[XF_HEADER:XF_HEADER + 22] = hdr
+    out[XF_GAMMA:XF_GAMMA + 64] = np.frombuffer(g.astype(np.uint8).tobytes(), dtype=np.float32)
+    return out
+
+
 # ---------------------------------------------------------------------------
 # references (plain PyTorch fp32)
 # ---------------------------------------------------------------------------
@@ -281,7 +353,7 @@ def device_lut(cfg: DecodeConfig, device):
     key = (cfg, str(device))
     t = _lut_cache.get(key)
     if t is None:
-        t = torch.from_numpy(build_lut(cfg)).to(device)
+        t = torch.from_numpy(build_table(cfg)).to(device)
         _lut_cache[key] = t
     return t
 

@@ -80,3 +80,41 @@ def test_utils_coordinates():
     cam = btb.Camera()
     vis = btb.utils.compute_object_visibility(cube, cam, N=10)
     assert 0.0 <= vis <= 1.0
+
+
+def test_value_table_arithmetic_forms_reproduce_reference_tables():
+    """ops.build_table: every common decode config gets the kernels'
+    arithmetic path (mode 1), and the verified per-channel form -- applied to
+    the lane-private gamma table exactly as the kernels index it -- equals
+    the fp32 reference table bit for bit (so the LDS-free / conflict-free
+    decode stays bit-exact)."""
+    import numpy as np
+    from blendtorch import ops
+    cfgs = [ops.DecodeConfig.unit(channels='rgb', gamma=2.2),
+            ops.DecodeConfig.unit(channels='rgba', gamma=2.2, dtype='bfloat16', layout='nhwc'),
+            ops.DecodeConfig.densityopt(channels='rgb'),
+            ops.DecodeConfig.densityopt(channels=(0, 1, 2, 2), dtype='bfloat16', layout='nhwc'),
+            ops.DecodeConfig.densityopt(channels='rgb', gamma=2.2),
+            ops.DecodeConfig.raw(), ops.DecodeConfig.raw(channels='rgb'),
+            ops.DecodeConfig(channels='bgr', mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225), scale=1 / 255),
+            ops.DecodeConfig(channels='rgba', gamma=1.8, color_matrix=np.eye(4).tolist())]
+    for cfg in cfgs:
+        t = ops.build_table(cfg)
+        assert t.shape == (ops.TABLE_FLOATS,) and t.dtype == np.float32
+        assert t[ops.XF_HEADER] == 1.0, cfg
+        lut = ops.build_lut(cfg)
+        hdr = t[ops.XF_HEADER:ops.XF_HEADER + 22]
+        gw = t[ops.XF_GAMMA:ops.XF_GAMMA + 64].view(np.uint32)
+        tab = np.repeat(gw, 32).view(np.uint8)                  # word i = gamma dword i >> 5
+        nch = 4 if cfg.color_matrix is not None else cfg.cout
+        v = np.arange(256)
+        for lane in (0, 7, 31):
+            for c in range(nch):
+                if hdr[2 + c]:
+                    x = tab[(v >> 2) * 128 + lane * 4 + (v & 3)].astype(np.float32)
+                else:
+                    x = v.astype(np.float32)
+                op, a, b, d = int(hdr[6 + c]), hdr[10 + c], hdr[14 + c], hdr[18 + c]
+                z = x * a + b if (op == 0 and b == 0) else (x * a - b if op == 1 else (x * a - b) / d)
+                assert op != 0 or b == 0
+                assert np.array_equal(z.view(np.uint32), lut[c].view(np.uint32)), (cfg, c, lane)
