@@ -188,8 +188,14 @@ class ProbModel(nn.Module):
                 D.LogNormal(self.m1m2_mean[1], torch.exp(self.m1m2_log_std[1]), validate_args=False))
 
     def sample(self, n):
-        m1, m2 = self.dists
-        return {'m1': m1.sample((n,)), 'm2': m2.sample((n,))}
+        """``n`` draws of (m1, m2): ``exp(mean + std * eps)``, eps ~ N(0, 1) --
+        the LogNormal's sample written out (torch.normal with tensor
+        arguments checks ``std >= 0`` on the host, which is a device sync and
+        cannot be captured in a HIP graph)."""
+        with torch.no_grad():
+            eps = torch.randn(2, n, device=self.m1m2_mean.device)
+            m = torch.exp(self.m1m2_mean.detach()[:, None] + torch.exp(self.m1m2_log_std.detach())[:, None] * eps)
+        return {'m1': m[0], 'm2': m[1]}
 
     def log_prob(self, samples):
         m1, m2 = self.dists

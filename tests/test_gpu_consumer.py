@@ -228,3 +228,31 @@ def test_rccl_direct_one_rank_process_group(dev, tmp_path):
     assert res['collectives'] == 1 and res['state'] == 'graph'
     assert res['max_abs_diff'] < 1e-4                  # atomically-reduced weight gradients: rounding only
     assert res['allreduce_avg_ok'] and res['broadcast_ok'] and res['p2p_self_ok']
+
+
+def test_densityopt_step_captures_and_replays(dev):
+    """The whole densityopt iteration (gated D step on the bf16 MFMA
+    discriminator, gated S step, baseline, resampling) captures into one HIP
+    graph and replays; the decisions stay device tensors (0/1) and the
+    parameter samples stay finite and positive (LogNormal)."""
+    from blendtorch.models import Discriminator, ProbModel
+    from blendtorch.models.densityopt import DensityOptStep
+    B = 64
+    torch.manual_seed(0)
+    netD = Discriminator().to(dev).to(memory_format=torch.channels_last)
+    pm = ProbModel([1.2, 3.0], [0.4, 0.4]).to(dev)
+    g = torch.Generator(device=dev).manual_seed(2)
+
+    def batch():
+        return (torch.rand(B, 64, 64, 4, device=dev, generator=g) * 2 - 1).to(torch.bfloat16).permute(0, 3, 1, 2)
+
+    step = DensityOptStep(netD, pm, batch().clone(), B, graph=True, warmup=2)
+    step.start()
+    before = ops.KERNEL_CALLS.get('conv_fwd', 0)
+    for i in range(6):
+        step(batch(), torch.randperm(B))
+    torch.cuda.synchronize()
+    assert step.graph is not None and ops.KERNEL_CALLS['conv_fwd'] > before
+    assert float(step.gate_d) in (0.0, 1.0) and float(step.gate_s) in (0.0, 1.0)
+    assert bool(torch.isfinite(step.samples).all()) and bool((step.samples > 0).all())
+    assert bool(torch.isfinite(step.params_out).all())
