@@ -36,7 +36,9 @@ enum Layout : int { NCHW = 0, NHWC = 1 };
 //                 x = gamma[v] (channels fed by colour inputs when a gamma is
 //                     set) or v, then per channel one of
 //                 op 0: fma(x, a, b)   op 1: x*a - b   op 2: (x*a - b) / d
-//                 (each operation rounded separately, like numpy's float32).
+//                 op 3: t = x*a - b, q = t*r, fma(fma(-q, d, t), r, q)
+//                 (each operation rounded separately, like numpy's float32;
+//                 csrc/codec/xform_fit.h).
 //               The host picks, per channel, an op it has VERIFIED to
 //               reproduce the fp32 table bit for bit for all 256 inputs
 //               (blendtorch.ops.build_table); mode 0 keeps the table lookup.
@@ -56,7 +58,7 @@ enum Layout : int { NCHW = 0, NHWC = 1 };
 //   max_grid    0: default grid cap; >0 overrides it (launch-shape sweeps).
 constexpr int kMaxSrcs = 64;
 // value-table layout (floats): [0, 1024) fp32 table [4][256]; header at
-// kXfHeader: mode, gamma_used, gam[4], op[4], a[4], b[4], d[4]; gamma u8[256]
+// kXfHeader: mode, gamma_used, gam[4], op[4], a[4], b[4], d[4], r[4]; gamma u8[256]
 // packed little-endian at kXfGamma (64 floats' worth of bytes)
 constexpr int kXfHeader = 1024;
 constexpr int kXfGamma = 1088;

@@ -73,17 +73,18 @@ __device__ __forceinline__ void load_pixels(const uint8_t* p, Pixels<PPT, CIN>& 
 }
 
 // ---- value transform (kernels.h: lut) --------------------------------------
-// LDS holds either the fp32 table (fallback, <= 4 KiB) or the lane-private
-// gamma table: word (v >> 2) * 32 + (lane & 31) packs gamma[v & ~3 .. v | 3],
-// so lane l of a 32-lane ds_read group always hits bank l (8 KiB).
+// LDS holds either the fp32 table (mode 0, <= 4 KiB) or R copies of the u8
+// gamma table: word (v >> 2) * R + (lane % R) packs gamma[v & ~3 .. v | 3],
+// so with R = 32 lane l of a 32-lane ds_read group always hits bank l (8 KiB).
 constexpr int kTabWords = 2048;
 
 struct Xf {
   int arith;               // 0: fp32 table lookups; 1: arithmetic
   const float* lut;        // LDS fp32 table [c][256] (arith == 0)
   const uint8_t* g;        // this lane's column of the LDS gamma table
+  int gshift;              // log2 of a gamma row's bytes (4 * copies)
   int gam[4], op[4];
-  float a[4], b[4], d[4];
+  float a[4], b[4], d[4], r[4];
 };
 
 // Read the header (uniform: scalar loads) and stage the table; caller syncs.
@@ -91,7 +92,6 @@ __device__ __forceinline__ Xf stage_xf(const float* T, uint32_t* tab, int nch) {
   Xf x;
   x.arith = T[kXfHeader] != 0.f;
   x.lut = reinterpret_cast<const float*>(tab);
-  x.g = reinterpret_cast<const uint8_t*>(tab) + (threadIdx.x & 31) * 4;
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     x.gam[c] = T[kXfHeader + 2 + c] != 0.f;
@@ -99,12 +99,24 @@ __device__ __forceinline__ Xf stage_xf(const float* T, uint32_t* tab, int nch) {
     x.a[c] = T[kXfHeader + 10 + c];
     x.b[c] = T[kXfHeader + 14 + c];
     x.d[c] = T[kXfHeader + 18 + c];
+    x.r[c] = T[kXfHeader + 22 + c];
   }
+  // gamma copies R (16 or 32): lane l reads copy l % R.  32 = every lane of a
+  // ds_read group owns a bank; 16 = half the fill, lanes l and l+16 share a
+  // bank (a 2-way conflict only when their values differ in the same column)
+  const int rep = int(T[kXfHeader + 1]);
+  x.gshift = rep == 32 ? 7 : 6;                 // bytes per gamma row: 4 * R
+  x.g = reinterpret_cast<const uint8_t*>(tab) + (threadIdx.x & (rep - 1)) * 4;
   if (!x.arith) {
     for (int i = threadIdx.x; i < nch * 256; i += blockDim.x) reinterpret_cast<float*>(tab)[i] = T[i];
-  } else if (T[kXfHeader + 1] != 0.f) {
+  } else if (rep > 0) {
+    // 16-byte stores: the 4 words of a quad sit in one row (same gamma dword)
     const uint32_t* gw = reinterpret_cast<const uint32_t*>(T + kXfGamma);
-    for (int i = threadIdx.x; i < kTabWords; i += blockDim.x) tab[i] = gw[i >> 5];
+    const int qshift = rep == 32 ? 3 : 2;       // quads per row: R / 4
+    for (int i = threadIdx.x; i < 16 * rep; i += blockDim.x) {
+      const uint32_t w = gw[i >> qshift];
+      reinterpret_cast<uint4*>(tab)[i] = make_uint4(w, w, w, w);
+    }
   }
   return x;
 }
@@ -116,20 +128,28 @@ __device__ __forceinline__ float xf_mulsub(float x, float a, float b) {
   return x * a - b;
 }
 
-__device__ __forceinline__ float xf_apply(int op, float x, float a, float b, float d) {
+// op 3: the quotient by the rounded reciprocal plus one fma correction --
+// the host proved it equals the correctly rounded division for every input
+__device__ __forceinline__ float xf_recip_div(float t, float d, float r) {
+  const float q = t * r;
+  return __builtin_fmaf(__builtin_fmaf(-q, d, t), r, q);
+}
+
+__device__ __forceinline__ float xf_apply(int op, float x, float a, float b, float d, float r) {
   if (op == 0) return __builtin_fmaf(x, a, b);
   const float t = xf_mulsub(x, a, b);
-  return op == 1 ? t : t / d;   // correctly rounded fp32 division (HIP default)
+  if (op == 1) return t;
+  return op == 3 ? xf_recip_div(t, d, r) : t / d;   // op 2: correctly rounded fp32 division (HIP default)
 }
 
 __device__ __forceinline__ float xf_source(const Xf& xf, int c, uint32_t v) {
-  return xf.gam[c] ? float(xf.g[(v >> 2) * 128 + (v & 3)]) : float(v);
+  return xf.gam[c] ? float(xf.g[((v >> 2) << xf.gshift) + (v & 3)]) : float(v);
 }
 
 // Value of output channel c for input byte v (scalar paths).
 __device__ __forceinline__ float xf_value(const Xf& xf, int c, uint32_t v) {
   if (!xf.arith) return xf.lut[c * 256 + v];
-  return xf_apply(xf.op[c], xf_source(xf, c, v), xf.a[c], xf.b[c], xf.d[c]);
+  return xf_apply(xf.op[c], xf_source(xf, c, v), xf.a[c], xf.b[c], xf.d[c], xf.r[c]);
 }
 
 // Output channel c from input channel IC for the lane's PPT pixels.  The
@@ -150,19 +170,22 @@ __device__ __forceinline__ void lookup_static(const Pixels<PPT, CIN>& px, const 
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
       const uint32_t v = px.v[i * CIN + IC];
-      x[i] = float(xf.g[(v >> 2) * 128 + (v & 3)]);
+      x[i] = float(xf.g[((v >> 2) << xf.gshift) + (v & 3)]);
     }
   } else {
 #pragma unroll
     for (int i = 0; i < PPT; ++i) x[i] = float(px.v[i * CIN + IC]);
   }
-  const float a = xf.a[c], b = xf.b[c], d = xf.d[c];
+  const float a = xf.a[c], b = xf.b[c], d = xf.d[c], r = xf.r[c];
   if (xf.op[c] == 0) {
 #pragma unroll
     for (int i = 0; i < PPT; ++i) o[i] = __builtin_fmaf(x[i], a, b);
   } else if (xf.op[c] == 1) {
 #pragma unroll
     for (int i = 0; i < PPT; ++i) o[i] = xf_mulsub(x[i], a, b);
+  } else if (xf.op[c] == 3) {
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) o[i] = xf_recip_div(xf_mulsub(x[i], a, b), d, r);
   } else {
 #pragma unroll
     for (int i = 0; i < PPT; ++i) o[i] = xf_mulsub(x[i], a, b) / d;

@@ -8,6 +8,7 @@
 #include <pybind11/stl.h>
 
 #include "../codec/pickle_codec.h"
+#include "../codec/xform_fit.h"
 #include "../sim/physics.h"
 #include "../sim/raster.h"
 #include "../transport/zmtp.h"
@@ -231,6 +232,22 @@ class NativeError(Exception):
     } catch (const codec::Unsupported& e) {
       throw py::value_error(std::string("unsupported pickle: ") + e.what());
     }
+  });
+  // decode value transform: the cheapest per-channel form that reproduces
+  // the fp32 table exactly (codec/xform_fit.h); None when there is none
+  m.def("xform_fit",
+        [](py::array_t<float, py::array::c_style | py::array::forcecast> x,
+           py::array_t<float, py::array::c_style | py::array::forcecast> y, float scale, float mean, float std,
+           bool normalize) -> py::object {
+          if (x.size() != 256 || y.size() != 256) throw std::invalid_argument("xform_fit: x and y need 256 values");
+          codec::XfChannel c;
+          if (!codec::fit_channel(x.data(), y.data(), scale, mean, std, normalize, &c)) return py::none();
+          return py::make_tuple(c.op, c.a, c.b, c.d, c.r);
+        });
+  m.def("xform_apply", [](int op, float a, float b, float d, float r, float x) {
+    codec::XfChannel c;
+    c.op = op, c.a = a, c.b = b, c.d = d, c.r = r;
+    return codec::apply_channel(c, x);
   });
   m.def("btr_header", [](py::array_t<int64_t, py::array::c_style | py::array::forcecast> offs) {
     std::vector<int64_t> o(offs.data(), offs.data() + offs.size());

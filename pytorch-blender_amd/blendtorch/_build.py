@@ -30,10 +30,11 @@ BIN = PKG / 'bin'
 HIP_ARCH = os.environ.get('BLENDTORCH_HIP_ARCH', 'gfx950')
 ROCM = Path(os.environ.get('ROCM_PATH', '/opt/rocm'))
 
-CXXFLAGS = ['-std=c++17', '-O3', '-fPIC', '-Wall', '-Wno-unused-parameter', '-pthread']
+# -ffp-contract=off: host float code (e.g. codec/xform_fit.cpp) rounds every operation on its own
+CXXFLAGS = ['-std=c++17', '-O3', '-fPIC', '-Wall', '-Wno-unused-parameter', '-pthread', '-ffp-contract=off']
 
 TRANSPORT = ['transport/zmtp.cpp', 'transport/shmring.cpp']
-CODEC = ['codec/pickle_codec.cpp']
+CODEC = ['codec/pickle_codec.cpp', 'codec/xform_fit.cpp']
 RASTER = ['sim/raster.cpp', 'sim/physics.cpp']
 
 

@@ -82,10 +82,12 @@ class Discriminator(nn.Module):
         backward, instead of ~20 library kernels; fp32 weight and gradient).
         Falls back to :meth:`forward_bf16` + ``BCELoss`` off that shape.
         Returns the loss."""
-        return self.bce_bf16(x, target, mfma)[0]
+        return self.bce_bf16(x, target, mfma, probs=False)[0]
 
-    def bce_bf16(self, x, target=1.0, mfma=True):
-        """``(mean BCE loss, per-sample probabilities)`` of the bf16 forward.
+    def bce_bf16(self, x, target=1.0, mfma=True, probs=True):
+        """``(mean BCE loss, per-sample probabilities)`` of the bf16 forward
+        (``probs=False``: the fused head's logits are not turned into
+        probabilities -- one kernel fewer when only the loss is used).
 
         The fused head applies to the adaptive stack (pool -> conv -> sigmoid)
         and to the plain DCGAN stack whose last conv consumes the whole
@@ -111,7 +113,7 @@ class Discriminator(nn.Module):
                 if not z.is_contiguous(memory_format=torch.channels_last):
                     z = z.contiguous(memory_format=torch.channels_last)
                 loss, logits = ops.disc_head_bce(z, head.weight, target, pool)
-                return loss, torch.sigmoid(logits)
+                return loss, (torch.sigmoid(logits) if probs else None)
             out = self._run_bf16(z, layers[len(body):], mfma)
         else:
             out = self._run_bf16(x, layers, mfma)

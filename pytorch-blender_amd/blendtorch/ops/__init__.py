@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import dataclasses
 import importlib
+import os
 from typing import Optional, Sequence
 
 import numpy as np
@@ -208,12 +209,18 @@ XF_HEADER, XF_GAMMA, TABLE_FLOATS = 1024, 1088, 1152
 
 
 def _xform_channel(x, y, gam, normalize, scale, mean, std):
-    """(op, a, b, d) reproducing float32 table ``y`` from inputs ``x`` exactly,
-    or None.  Candidates are the reference expression itself, rounded like
-    numpy: op 1 ``x*scale - mean``, op 2 ``(x*scale - mean) / std``; op 0
-    (one fma) only where it is provably identical (``b == 0``: fma(x, a, 0)
-    is the correctly rounded product)."""
+    """(op, a, b, d, r) reproducing float32 table ``y`` from inputs ``x``
+    exactly, or None (csrc/codec/xform_fit.h: op 0 fma, 1 mul-sub, 3 mul-sub
+    times the reciprocal with one fma correction, 2 division; each verified
+    over all 256 inputs).  Without the native module: the forms numpy can
+    emulate exactly (op 0 with b == 0, ops 1 and 2)."""
     f32 = np.float32
+    try:
+        from .. import _native
+        return _native.xform_fit(np.ascontiguousarray(x, f32), np.ascontiguousarray(y, f32), float(scale),
+                                 float(mean), float(std), bool(normalize))
+    except ImportError:
+        pass
     cands = []
     if not normalize:
         cands.append((0, f32(1.0), f32(0.0), f32(1.0)))
@@ -232,7 +239,7 @@ def _xform_channel(x, y, gam, normalize, scale, mean, std):
             else:
                 z = (x * a - b) / d
             if np.array_equal(z.view(np.uint32), y.view(np.uint32)):
-                return op, float(a), float(b), float(d)
+                return op, float(a), float(b), float(d), float(f32(1.0) / d)
     return None
 
 
@@ -243,6 +250,8 @@ def build_table(cfg: DecodeConfig) -> np.ndarray:
     lut = build_lut(cfg)
     out = np.zeros(TABLE_FLOATS, dtype=np.float32)
     out[:1024] = lut.reshape(-1)
+    if os.environ.get('BLENDTORCH_DECODE_XFORM', '1') == '0':
+        return out                                  # A/B switch: fp32 table lookups
     g = gamma_lut(cfg.gamma)
     gf = g.astype(np.float32)
     ident = np.arange(256, dtype=np.float32)
@@ -254,21 +263,24 @@ def build_table(cfg: DecodeConfig) -> np.ndarray:
         normalize = not (cfg.mean is None and cfg.std is None and cfg.scale == 1.0)
     mean = list(cfg.mean) if cfg.mean is not None else [0.0] * 4
     std = list(cfg.std) if cfg.std is not None else [1.0] * 4
-    hdr = np.zeros(22, dtype=np.float32)
-    hdr[6:10] = 0
+    hdr = np.zeros(26, dtype=np.float32)   # mode, gamma_used, gam[4], op[4], a[4], b[4], d[4], r[4]
     hdr[10:14] = 1.0
-    hdr[18:22] = 1.0
+    hdr[18:26] = 1.0
     for c, ic in chans:
         gam = bool(cfg.gamma) and ic < 3
         x = gf if gam else ident
         form = _xform_channel(x, lut[c], gam, normalize, np.float32(cfg.scale), mean[c], std[c])
         if form is None:
             return out                              # mode 0: table lookups
-        op, a, b, d = form
-        hdr[2 + c], hdr[6 + c], hdr[10 + c], hdr[14 + c], hdr[18 + c] = float(gam), op, a, b, d
+        op, a, b, d, r = form
+        hdr[2 + c], hdr[6 + c], hdr[10 + c], hdr[14 + c], hdr[18 + c], hdr[22 + c] = float(gam), op, a, b, d, r
         hdr[1] = max(hdr[1], float(gam))
+    if hdr[1]:
+        hdr[1] = float(int(os.environ.get('BLENDTORCH_GAMMA_COPIES', '32')))   # lane-private copies: 16 or 32
+        if hdr[1] not in (16.0, 32.0):
+            raise ValueError('BLENDTORCH_GAMMA_COPIES must be 16 or 32')
     hdr[0] = 1.0
-    out[XF_HEADER:XF_HEADER + 22] = hdr
+    out[XF_HEADER:XF_HEADER + 26] = hdr
     out[XF_GAMMA:XF_GAMMA + 64] = np.frombuffer(g.astype(np.uint8).tobytes(), dtype=np.float32)
     return out
 

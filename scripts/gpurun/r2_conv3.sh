@@ -1,7 +1,7 @@
 #!/bin/bash
 # conv kernel iteration: numerics, per-layer timings, disc consumer bench
 set -u
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 trap 'find gpurun_out -type f -size +8M -delete' EXIT

@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC passes over the conv kernels (scripts/conv_prof.py); summary to gpurun_out/conv_pmc/summary.txt
 set -u
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out/conv_pmc
 export TMPDIR=/tmp
 trap 'find gpurun_out -type f -size +8M -delete' EXIT

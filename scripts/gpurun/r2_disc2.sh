@@ -1,4 +1,4 @@
 set -u
 cd $GRAFT_REPO_ROOT
-bash scripts/r2_disc.sh || exit 1
+bash scripts/gpurun/r2_disc.sh || exit 1
 bash scripts/disc_ktrace.sh

@@ -2,7 +2,7 @@
 # headline bench vs loader depth: posted output buffers (--prefetch) and queued decode launches (--launch-depth),
 # on long and driver-style short timed windows
 set -u
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 for cfg in ${CFGS:-"4 2 20 5" "6 2 20 5" "8 2 20 5" "4 2 2000 50" "6 2 2000 50" "8 2 2000 50" "4 2 20 5" "6 2 20 5" "8 2 20 5"}; do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # posted loader buffers 6 vs 8, alternating, on driver-style short and long timed windows
 set -u
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 while read -r pf steps warm; do

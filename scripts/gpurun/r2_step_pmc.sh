@@ -2,7 +2,7 @@
 # PMC passes over the discriminator training step (eager, resident batch, bench config): per-kernel
 # MFMA / VALU / LDS instruction counts, bank conflicts, busy cycles and HBM bytes -> gpurun_out/step_pmc/summary.txt
 set -u
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out/step_pmc
 export TMPDIR=/tmp
 trap 'find gpurun_out -type f -size +8M -delete' EXIT

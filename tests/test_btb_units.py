@@ -103,18 +103,20 @@ def test_value_table_arithmetic_forms_reproduce_reference_tables():
         assert t.shape == (ops.TABLE_FLOATS,) and t.dtype == np.float32
         assert t[ops.XF_HEADER] == 1.0, cfg
         lut = ops.build_lut(cfg)
-        hdr = t[ops.XF_HEADER:ops.XF_HEADER + 22]
+        hdr = t[ops.XF_HEADER:ops.XF_HEADER + 26]
         gw = t[ops.XF_GAMMA:ops.XF_GAMMA + 64].view(np.uint32)
-        tab = np.repeat(gw, 32).view(np.uint8)                  # word i = gamma dword i >> 5
+        tab = np.repeat(gw, 32).view(np.uint8)                  # word i = gamma dword i >> 5 (32 copies)
+        assert hdr[1] in (0.0, 32.0)
         nch = 4 if cfg.color_matrix is not None else cfg.cout
         v = np.arange(256)
+        from blendtorch import _native
         for lane in (0, 7, 31):
             for c in range(nch):
                 if hdr[2 + c]:
                     x = tab[(v >> 2) * 128 + lane * 4 + (v & 3)].astype(np.float32)
                 else:
                     x = v.astype(np.float32)
-                op, a, b, d = int(hdr[6 + c]), hdr[10 + c], hdr[14 + c], hdr[18 + c]
-                z = x * a + b if (op == 0 and b == 0) else (x * a - b if op == 1 else (x * a - b) / d)
-                assert op != 0 or b == 0
+                op, a, b, d, r = int(hdr[6 + c]), hdr[10 + c], hdr[14 + c], hdr[18 + c], hdr[22 + c]
+                z = np.array([_native.xform_apply(op, a, b, d, r, float(xi)) for xi in x], dtype=np.float32)
+                assert op in (0, 1, 3) or cfg.std is not None, (cfg, op)     # division only as the last resort
                 assert np.array_equal(z.view(np.uint32), lut[c].view(np.uint32)), (cfg, c, lane)
