@@ -245,13 +245,19 @@ def _xform_channel(x, y, gam, normalize, scale, mean, std):
 
 def build_table(cfg: DecodeConfig) -> np.ndarray:
     """float32[TABLE_FLOATS]: :func:`build_lut` plus the header and u8 gamma
-    table of the kernels' arithmetic path (see csrc/gpu/kernels.h).  Falls
-    back to mode 0 (fp32 table lookups) if any channel has no verified form."""
+    table of the kernels' arithmetic path (see csrc/gpu/kernels.h).
+
+    ``BLENDTORCH_DECODE_XFORM``: ``auto`` (default) uses the arithmetic path
+    when it reads no LDS and needs no division (no gamma, ops 0/1), the fp32
+    table otherwise; ``1`` always the arithmetic path (bank-conflict-free
+    lane-private gamma copies, ``BLENDTORCH_GAMMA_COPIES`` 16/32); ``0``
+    always the table.  Mode 0 also whenever a channel has no verified form."""
     lut = build_lut(cfg)
     out = np.zeros(TABLE_FLOATS, dtype=np.float32)
     out[:1024] = lut.reshape(-1)
-    if os.environ.get('BLENDTORCH_DECODE_XFORM', '1') == '0':
-        return out                                  # A/B switch: fp32 table lookups
+    policy = os.environ.get('BLENDTORCH_DECODE_XFORM', 'auto')
+    if policy == '0':
+        return out                                  # fp32 table lookups
     g = gamma_lut(cfg.gamma)
     gf = g.astype(np.float32)
     ident = np.arange(256, dtype=np.float32)
@@ -275,6 +281,13 @@ def build_table(cfg: DecodeConfig) -> np.ndarray:
         op, a, b, d, r = form
         hdr[2 + c], hdr[6 + c], hdr[10 + c], hdr[14 + c], hdr[18 + c], hdr[22 + c] = float(gam), op, a, b, d, r
         hdr[1] = max(hdr[1], float(gam))
+    if policy == 'auto' and (hdr[1] or any(int(o) not in (0, 1) for o in hdr[6:6 + len(chans)])):
+        # measured (profiles/r3/decode_ab.md): with a gamma table or a division
+        # the arithmetic form costs ~35 % more VALU and 5-15 % more time than
+        # the fp32 table, whose bank conflicts (2.2 extra cycles per ds_read on
+        # uniform random pixels) are not what bounds the kernel; without
+        # either it reads no LDS at all at the table's speed
+        return out
     if hdr[1]:
         hdr[1] = float(int(os.environ.get('BLENDTORCH_GAMMA_COPIES', '32')))   # lane-private copies: 16 or 32
         if hdr[1] not in (16.0, 32.0):

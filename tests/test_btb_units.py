@@ -98,8 +98,15 @@ def test_value_table_arithmetic_forms_reproduce_reference_tables():
             ops.DecodeConfig.raw(), ops.DecodeConfig.raw(channels='rgb'),
             ops.DecodeConfig(channels='bgr', mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225), scale=1 / 255),
             ops.DecodeConfig(channels='rgba', gamma=1.8, color_matrix=np.eye(4).tolist())]
-    for cfg in cfgs:
-        t = ops.build_table(cfg)
+    import os
+    os.environ['BLENDTORCH_DECODE_XFORM'] = '1'      # the forced arithmetic path (auto keeps the table for gamma)
+    try:
+        tables = [ops.build_table(cfg) for cfg in cfgs]
+    finally:
+        del os.environ['BLENDTORCH_DECODE_XFORM']
+    assert ops.build_table(ops.DecodeConfig.unit(channels='rgb'))[ops.XF_HEADER] == 1.0          # auto: no LDS
+    assert ops.build_table(ops.DecodeConfig.unit(channels='rgb', gamma=2.2))[ops.XF_HEADER] == 0.0
+    for cfg, t in zip(cfgs, tables):
         assert t.shape == (ops.TABLE_FLOATS,) and t.dtype == np.float32
         assert t[ops.XF_HEADER] == 1.0, cfg
         lut = ops.build_lut(cfg)

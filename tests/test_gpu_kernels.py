@@ -206,3 +206,34 @@ def test_discriminator_fused_matches_unfused(dev):
         assert torch.allclose(pa.grad, pb.grad, atol=1e-3, rtol=1e-2), n
     for (n, ba), bb in zip(a.named_buffers(), b.buffers()):
         assert torch.allclose(ba.float(), bb.float(), atol=1e-4, rtol=1e-4), n
+
+
+@pytest.mark.parametrize('copies', ['16', '32'])
+def test_decode_forced_arithmetic_transform_bit_exact(monkeypatch, copies):
+    """BLENDTORCH_DECODE_XFORM=1: the verified arithmetic value transform with
+    a lane-private gamma table (no LDS bank conflicts) is bit-exact with the
+    fp32 reference for gamma, normalisation (reciprocal + fma correction) and
+    raw configs, in the stream decode, the gather decode and the replay sample."""
+    if not torch.cuda.is_available():
+        pytest.skip('needs a GPU')
+    monkeypatch.setenv('BLENDTORCH_DECODE_XFORM', '1')
+    monkeypatch.setenv('BLENDTORCH_GAMMA_COPIES', copies)
+    monkeypatch.setattr(ops, '_lut_cache', {})
+    dev = torch.device('cuda', 0)
+    g = torch.Generator(device=dev).manual_seed(4)
+    x = torch.randint(0, 256, (6, 48, 64, 4), dtype=torch.uint8, device=dev, generator=g)
+    cfgs = [ops.DecodeConfig.densityopt(channels='rgb', gamma=2.2),
+            ops.DecodeConfig.unit(channels='rgba', gamma=1.8, dtype='bfloat16', layout='nhwc'),
+            ops.DecodeConfig(channels='bgr', mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225), scale=1 / 255),
+            ops.DecodeConfig.raw(channels='rgb')]
+    for cfg in cfgs:
+        assert ops.build_table(cfg)[ops.XF_HEADER] == 1.0
+        ref = ops.reference_decode(x.cpu(), cfg)
+        assert torch.equal(ops.decode(x, cfg).cpu(), ref), cfg
+        idx = torch.tensor([5, 0, 3], device=dev)
+        assert torch.equal(ops.decode_gather(x, idx, cfg).cpu(), ref[idx.cpu()]), cfg
+        out, got_idx, _ = ops.replay_sample(x, 6, 4, cfg, seed=3, counter=11)
+        assert torch.equal(out.cpu(), ref[got_idx.cpu()]), cfg
+    y = ops.color4x4(x, np.eye(4), gamma=2.2)
+    torch.testing.assert_close(y.cpu(), ops.reference_color4x4(x.cpu(), np.eye(4), [0] * 4, gamma=2.2),
+                               rtol=0, atol=0)
