@@ -49,6 +49,7 @@ for step in "$@"; do
            timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29556 bench.py --gpus 1 --steps 300 --warmup 20 --consumer disc >> gpurun_out/dist1.log 2>&1; rc=$?; grep '^{' gpurun_out/dist1.log | tail -1;;
     sup2) timeout -k 10 300 python bench.py --gpus 2 --backend gloo --steps 1000 --warmup 20 > gpurun_out/sup2.log 2>&1; rc=$?; grep '^{' gpurun_out/sup2.log | cut -c1-600;;
     sup2:*) a="${step#sup2:}"; timeout -k 10 300 python bench.py --gpus 2 --backend gloo ${a//,/ } >> gpurun_out/sup2.log 2>&1; rc=$?; grep '^{' gpurun_out/sup2.log | tail -1 | cut -c1-600;;
+    supn:*) a="${step#supn:}"; n="${a%%,*}"; rest="${a#*,}"; timeout -k 10 400 python bench.py --gpus $n --backend gloo ${rest//,/ } >> gpurun_out/supn.log 2>&1; rc=$?; grep '^{' gpurun_out/supn.log | tail -1 | cut -c1-400;;
     gtests:*) a="${step#gtests:}"; timeout -k 10 500 python -u -m pytest ${a//,/ } -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu_sel.log 2>&1; rc=$?; grep -E "PASS|FAIL|ERROR|passed|failed" gpurun_out/pytest_gpu_sel.log | tail -30;;
     b:*) a="${step#b:}"; tag=$(echo "$a" | tr -c 'a-zA-Z0-9\n' '_' | cut -c1-60); timeout -k 10 300 python bench.py ${a//,/ } > gpurun_out/b_$tag.log 2>&1; rc=$?; grep '^{' gpurun_out/b_$tag.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$a', '->', d['value'], d['unit'], d['ms_per_step'], 'ms', d.get('h2d_gbytes_per_s'), 'GB/s', d['config'].get('consumer_step'), d.get('world_size_seen'))" || tail -5 gpurun_out/b_$tag.log;;
     ktrace:*) a="${step#ktrace:}"; tag=$(echo "$a" | tr -c 'a-zA-Z0-9\n' '_' | cut -c1-50); timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d /tmp/rp_kt_$tag -o run --output-format csv -- python bench.py ${a//,/ } > gpurun_out/kt_$tag.log 2>&1; rc=$?; grep '^{' gpurun_out/kt_$tag.log | cut -c1-300
