@@ -40,11 +40,43 @@ except ImportError:  # pragma: no cover - exercised only without the native buil
     _native_cas = None
 
 
+def _libatomic_cas():
+    """A lock-free 32-bit compare-and-swap from the GCC runtime's libatomic,
+    through ctypes -- for Pythons without the native module (Blender's own):
+    the producer's lease reclaim must not overwrite a slot a consumer has just
+    claimed (PUBLISHED -> HELD) between a read and a store."""
+    import ctypes
+    import ctypes.util
+    for name in ('libatomic.so.1', ctypes.util.find_library('atomic')):
+        if not name:
+            continue
+        try:
+            fn = ctypes.CDLL(name).__atomic_compare_exchange_4
+        except (OSError, AttributeError):
+            continue
+        fn.restype = ctypes.c_bool
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_bool, ctypes.c_int, ctypes.c_int]
+
+        def cas(states, i, expected, desired, _fn=fn, _c=ctypes):
+            exp = _c.c_uint32(int(expected))
+            addr = states.ctypes.data + 4 * int(i)
+            return bool(_fn(addr, _c.addressof(exp), int(desired) & 0xFFFFFFFF, False, 5, 5))   # seq_cst
+        return cas
+    return None
+
+
+_ctypes_cas = _libatomic_cas() if _native_cas is None else None
+
+
 def _cas(states, i, expected, desired):
-    """Compare-and-swap slot word ``i`` (atomic when the native module is
-    available; a plain check-then-store otherwise)."""
+    """Compare-and-swap slot word ``i``: the native module's atomic, else
+    libatomic's through ctypes; only without either a plain check-then-store
+    (then a consumer's claim racing a producer's lease reclaim can be
+    overwritten -- the loader reports that batch as torn)."""
     if _native_cas is not None:
         return _native_cas(states, int(i), int(expected), int(desired))
+    if _ctypes_cas is not None:
+        return _ctypes_cas(states, i, expected, desired)
     if int(states[i]) != expected:
         return False
     states[i] = desired

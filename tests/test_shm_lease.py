@@ -147,3 +147,18 @@ def test_set_key_frame_mid_stream_cpu(free_port):
     finally:
         pull.close()
         pub.close()
+
+
+def test_libatomic_cas_fallback_is_atomic_cas():
+    """Without the native module (Blender's Python) slot words still change
+    by a real compare-and-swap (libatomic through ctypes)."""
+    import numpy as np
+    from blendtorch.transport import shm
+    cas = shm._libatomic_cas()
+    assert cas is not None
+    words = np.zeros(4, dtype=np.uint32)
+    words[2] = (7 << 2) | shm.PUBLISHED
+    assert not cas(words, 2, (7 << 2) | shm.FREE, 1)           # wrong expectation: untouched
+    assert words[2] == (7 << 2) | shm.PUBLISHED
+    assert cas(words, 2, (7 << 2) | shm.PUBLISHED, (7 << 2) | shm.HELD)
+    assert words[2] == (7 << 2) | shm.HELD and words[1] == 0 and words[3] == 0
