@@ -256,10 +256,12 @@ class ScatterLoader:
     (rare) fall back to a per-step object scatter.
 
     No per-step host synchronisation on RCCL: the sends/receives are RCCL
-    calls on the compute stream (:class:`~.comm.DeviceComm`), the root's
+    calls on the compute stream (:class:`~.comm.DeviceComm`), the peers'
     metadata rows are packed into a reused pinned buffer and copied to the
-    device asynchronously, and receive buffers come from the caching
-    allocator.  The decode kernel follows on the same stream.
+    device asynchronously (the root keeps its own rows as the collated host
+    tensors, like shard mode; peers get device tensors), and receive buffers
+    come from the caching allocator.  The decode kernel follows on the same
+    stream.
 
     Params
     ------
@@ -371,10 +373,11 @@ class ScatterLoader:
                     raise ValueError(f'scatter source changed its image shape: {tuple(full.shape)}')
                 if full.device != cdev:
                     full = full.to(cdev)
-                meta = self._pack(batch, schema, world * B, cdev)
                 img = full[self.src * B:(self.src + 1) * B]
-                mrow = meta[self.src * B:(self.src + 1) * B]
                 if multi:
+                    # only the peers' metadata rows travel (packed, pinned, async H2D);
+                    # the root keeps its own rows as the collated host tensors
+                    meta = self._pack(batch, schema, world * B, cdev)
                     ops_ = []
                     for r in range(world):
                         if r != self.src:
@@ -382,14 +385,16 @@ class ScatterLoader:
                             ops_.append((True, meta[r * B:(r + 1) * B], r))
                     comm.p2p(ops_)
                     self.stats['bytes_sent'] += (world - 1) * B * (full[0].numel() + row_bytes)
+                own = {k: batch[k][self.src * B:(self.src + 1) * B] for k, _, _ in schema}
             else:
                 img = torch.empty((B,) + tuple(shape), dtype=torch.uint8, device=cdev)
                 mrow = torch.empty((B, row_bytes), dtype=torch.uint8, device=cdev)
                 comm.p2p([(False, img, self.src), (False, mrow, self.src)])
+                own = unpack_meta(mrow, schema)
             if img.device != self.device:
                 img = img.to(self.device, non_blocking=True)
             out = {self.image_key: self._decode(img)}
-            out.update(unpack_meta(mrow, schema))
+            out.update(own)
             if objects:
                 # keys that are not fixed-size tensors: the slow path, per step
                 self.stats['object_scatters'] += 1
