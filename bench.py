@@ -336,10 +336,11 @@ def main(argv=None):
                 from blendtorch.parallel import pool_addresses
                 addrs = pool_addresses(addrs)
             if args.dist != 'scatter' or rank == 0:
-                # scatter: the root's loader lands raw u8 frames (alpha dropped when
-                # the decode does not read it) -- the bytes that cross xGMI
-                ldec = decode if args.dist != 'scatter' else DecodeConfig.raw(
-                    channels='rgba' if 3 in decode.cmap else 'rgb')
+                # scatter: the root's loader lands raw u8 RGBA frames -- the bytes
+                # that cross xGMI (4-pixel lanes read host memory at the PCIe rate;
+                # dropping alpha would save 25 % of the xGMI bytes but forces
+                # 16-pixel lanes that read host memory ~30 % slower)
+                ldec = decode if args.dist != 'scatter' else DecodeConfig.raw(channels='rgba')
                 if step_decode:
                     # the loader only DMAs the frames into the consumer's tensor
                     # (identity decode = no kernel on the loader's queue); the

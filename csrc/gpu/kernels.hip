@@ -500,6 +500,14 @@ hipError_t launch_out(const DecodeParams& p, hipStream_t s) {
                                    : (reinterpret_cast<uintptr_t>(p.src) % 16) == 0 && (p.src_offsets == nullptr || p.src_offsets_aligned);
   const bool dst_aligned = p.ndsts ? dsts_ok(p.dsts, p.ndsts, p.B, 16) : (reinterpret_cast<uintptr_t>(p.dst) % 16) == 0;
   bool aligned = (p.W % PPT) == 0 && (int64_t(p.H) * p.W * p.Cin) % 16 == 0 && dst_aligned && src_aligned;
+  if constexpr (OUTT == OUT_U8) {
+    // RGBA -> RGBA u8 NHWC read from HOST memory (the scatter root's raw
+    // frames): 4 pixels per lane, one 16-byte load and one 16-byte store, so
+    // 4x the lanes of the 16-pixel shape keep PCIe read requests in flight
+    // (the 16-pixel shape read host frames at ~36 GB/s against ~50)
+    if (p.nsrcs && p.layout == NHWC && p.Cin == 4 && p.Cout == 4 && aligned && (p.W % 4) == 0)
+      return launch_vec<4, 4, OUTT>(p, s);
+  }
   if (aligned && p.Cin == 4) return launch_vec<PPT, 4, OUTT>(p, s);
   if (aligned && p.Cin == 3) return launch_vec<PPT, 3, OUTT>(p, s);
   int64_t work = int64_t(p.B) * p.H * p.W;
