@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdint>
 
 #include "kernels.h"
@@ -515,18 +516,22 @@ struct TapGemm {
 
 // BN = output channels per block (64, or 32 for 32-channel outputs such as
 // the first layer's data gradient); 4 waves as WGM (pixels) x WGN (channels).
-template <bool DGRAD, int BN, bool C4 = false>
+// BM = pixels per block: 128, or 64 when 128-pixel tiles would leave the
+// chip short of blocks (the deep-K layers: 300-600 tiles on 256 CUs).
+template <bool DGRAD, int BN, bool C4 = false, int BM = FBM>
 __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
+  constexpr int RJ = BM / 32;                  // staged A rows per thread (ar + 32 j)
+  constexpr int A_TILE = BM * F_ROW;
   constexpr int WGM = BN == 64 ? 2 : 4, WGN = 4 / WGM;
-  constexpr int FM = FBM / WGM / 16, FN = BN / WGN / 16;   // 16x16 fragments per wave
+  constexpr int FM = BM / WGM / 16, FN = BN / WGN / 16;   // 16x16 fragments per wave
   // one stage = the A tile + a BN-row B tile; the epilogue's bf16 tile
-  // ([FBM][128 B] = FA_TILE) and the per-wave channel sums (red, [4][2][BN])
+  // ([BM][128 B] = A_TILE) and the per-wave channel sums (red, [4][2][BN])
   // reuse the staging space once the k-loop is done.  A 32-channel block
   // therefore takes 40 KiB, and four fit a CU's LDS (50 KiB fit three).
-  constexpr int STG = FA_TILE + BN * F_ROW;
-  static_assert(2 * STG >= FA_TILE + 4 * 2 * BN * 4, "epilogue does not fit the staging LDS");
+  constexpr int STG = A_TILE + BN * F_ROW;
+  static_assert(2 * STG >= A_TILE + 4 * 2 * BN * 4, "epilogue does not fit the staging LDS");
   __shared__ __attribute__((aligned(16))) char smem[2 * STG];
-  float* red = reinterpret_cast<float*>(smem + FA_TILE);   // [WGM][2][BN], after the epilogue tile
+  float* red = reinterpret_cast<float*>(smem + A_TILE);   // [WGM][2][BN], after the epilogue tile
   const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
   constexpr int NTAPS = DGRAD ? 4 : 16;
   const int K = C4 ? FBK : NTAPS * p.C, NT = p.NOUT / BN;
@@ -536,12 +541,12 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
   const int mt = w / NT, n0 = (w - mt * NT) * BN;
-  const int m0 = mt * FBM;
+  const int m0 = mt * BM;
 
   // this thread's 4 GEMM rows (staging A, and the epilogue stores): ar + 32j
   const int ar = t >> 3, ac = t & 7;
-  int rb[4], cb[4], base[4], obase[4];
-  bool pin[4];
+  int rb[RJ], cb[RJ], base[RJ], obase[RJ];
+  bool pin[RJ];
   // (n, a, b) of row ar by division, the next rows 32 GEMM rows on by
   // stepping (two integer divisions per row were a third of the kernel's VALU)
   int gn, ga, gbb;
@@ -553,7 +558,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     gbb = rem - ga * p.GW;
   }
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < RJ; ++j) {
     const int m = m0 + ar + 32 * j;
     if (j > 0) {
       gbb += 32;
@@ -583,9 +588,9 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     hi = hi > TW ? TW : hi;
     return hi > lo ? (1u << hi) - (1u << lo) : 0u;
   };
-  uint32_t abase[4], vmask[4];
+  uint32_t abase[RJ], vmask[RJ];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < RJ; ++j) {
     abase[j] = uint32_t(base[j]) << (p.cshift + 1);
     uint32_t rows, cols;
     if (DGRAD) {   // 0 <= rb + ph - k < SH  <=>  rb + ph - SH < k <= rb + ph
@@ -608,14 +613,14 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(p.src, int64_t(p.N) * p.SH * p.SW * p.C * 2);
   const uint16_t* wrow0 = p.w + (n0 + ar) * (16 * p.C);
   const uint16_t* wrow1 = p.w + (n0 + (BN == 64 ? ar + 32 : ar)) * (16 * p.C);
-  uint4 ra[4], rb0, rb1;
+  uint4 ra[RJ], rb0, rb1;
   auto load_c4 = [&]() {
     // first layer, 4-channel input: K = 16 taps x 4 = one k-step; chunk ac is
     // taps (kh, kw) and (kh, kw + 1) of one row -- two adjacent input pixels,
     // each checked against the border on its own
     const int kh = ac >> 1, kw = (ac & 1) * 2;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < RJ; ++j) {
       const bool rok = pin[j] && unsigned(rb[j] + kh) < unsigned(p.SH);
       const int e = (base[j] + kh * p.SW + kw) * 4;
       const uint2 lo = bload8(rs_src, rok && unsigned(cb[j] + kw) < unsigned(p.SW) ? uint32_t(e) * 2u : kOOB);
@@ -656,7 +661,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     const uint32_t soff = uint32_t((((dr * p.SW + dc) << p.cshift) + ch) * 2);
     const uint32_t tbit = live ? 1u << tap : 0u;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) ra[j] = bload(rs_src, (vmask[j] & tbit) ? abase[j] + soff : kOOB);
+    for (int j = 0; j < RJ; ++j) ra[j] = bload(rs_src, (vmask[j] & tbit) ? abase[j] + soff : kOOB);
     const int woff = wtap * p.C + ch;
     rb0 = *reinterpret_cast<const uint4*>(wrow0 + woff);
     if (BN == 64) rb1 = *reinterpret_cast<const uint4*>(wrow1 + woff);
@@ -665,9 +670,9 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   auto store = [&](int buf) {
     char* ai = smem + buf * STG;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) *reinterpret_cast<uint4*>(ai + st_a + j * 32 * F_ROW) = ra[j];
-    *reinterpret_cast<uint4*>(ai + FA_TILE + st_a) = rb0;
-    if (BN == 64) *reinterpret_cast<uint4*>(ai + FA_TILE + st_a + 32 * F_ROW) = rb1;
+    for (int j = 0; j < RJ; ++j) *reinterpret_cast<uint4*>(ai + st_a + j * 32 * F_ROW) = ra[j];
+    *reinterpret_cast<uint4*>(ai + A_TILE + st_a) = rb0;
+    if (BN == 64) *reinterpret_cast<uint4*>(ai + A_TILE + st_a + 32 * F_ROW) = rb1;
   };
 
   f32x4 acc[FM][FN];
@@ -676,7 +681,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int wm = wave / WGN, wn = wave % WGN;
-  const int row0 = wm * (FBM / WGM), col0 = wn * (BN / WGN);
+  const int row0 = wm * (BM / WGM), col0 = wn * (BN / WGN);
   // fragment read offsets (loop invariant): row r, chunk 4 kk + lane / 16
   int fa[FM][2], fb[FN][2];
 #pragma unroll
@@ -685,7 +690,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
 #pragma unroll
     for (int i = 0; i < FM; ++i) fa[i][kk] = f_off(row0 + 16 * i + (lane & 15), chunk);
 #pragma unroll
-    for (int j = 0; j < FN; ++j) fb[j][kk] = FA_TILE + f_off(col0 + 16 * j + (lane & 15), chunk);
+    for (int j = 0; j < FN; ++j) fb[j][kk] = A_TILE + f_off(col0 + 16 * j + (lane & 15), chunk);
   }
   auto mma = [&](int buf) {
     const char* ai = smem + buf * STG;
@@ -716,12 +721,12 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     // LDS-only, so the ring's later stages stay in flight across it (counted
     // vmcnt waits on the stage being stored).
     constexpr int kDepth = 2;
-    uint4 ring_a[kDepth][4], ring_b0[kDepth], ring_b1[kDepth];
+    uint4 ring_a[kDepth][RJ], ring_b0[kDepth], ring_b1[kDepth];
     int ks_next = 0;
     auto fetch = [&](int u) {
       load(ks_next++);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) ring_a[u][j] = ra[j];
+      for (int j = 0; j < RJ; ++j) ring_a[u][j] = ra[j];
       ring_b0[u] = rb0;
       if (BN == 64) ring_b1[u] = rb1;
     };
@@ -733,7 +738,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
       for (int u = 0; u < kDepth; ++u) {
         const int buf = u & 1;   // kDepth is even: (s0 + u) & 1
 #pragma unroll
-        for (int j = 0; j < 4; ++j) ra[j] = ring_a[u][j];
+        for (int j = 0; j < RJ; ++j) ra[j] = ring_a[u][j];
         rb0 = ring_b0[u];
         if (BN == 64) rb1 = ring_b1[u];
         store(buf);
@@ -749,7 +754,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   // Epilogue stores: every thread takes whole 16-byte row chunks -- CPR
   // chunks per row, RPP rows per pass, NJ rows per thread (for BN = 32 that
   // is 2 rows of all 256 threads, not 4 rows of half of them).
-  constexpr int CPR = BN / 8, RPP = kThreads / CPR, NJ = FBM / RPP;
+  constexpr int CPR = BN / 8, RPP = kThreads / CPR, NJ = BM / RPP;
   const int ec = t % CPR;
   int eob[NJ];
   bool epin[NJ];
@@ -790,7 +795,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
       xpre[j] = epin[j] ? *reinterpret_cast<const uint4*>(p.bn.x + eob[j] + n0 + ec * 8) : make_uint4(0, 0, 0, 0);
   }
 
-  // epilogue: round to bf16 (RNE) into an LDS tile [FBM][BN] (128-byte row
+  // epilogue: round to bf16 (RNE) into an LDS tile [BM][BN] (128-byte row
   // pitch, same swizzle), sum the rounded values per channel (forward), then
   // 16-byte stores of whole row chunks
   uint16_t* tile = reinterpret_cast<uint16_t*>(smem);
@@ -809,7 +814,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     for (int r = 0; r < 4; ++r)
       toff[j][r] = (row0 + lr + r) * (F_ROW / 2) + ((((col >> 3) ^ ((lr + r) & 7)) << 4) >> 1) + (col & 7);
   }
-  const bool all_rows = m0 + FBM <= p.M;   // the tile holds no row past the GEMM
+  const bool all_rows = m0 + BM <= p.M;   // the tile holds no row past the GEMM
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -919,7 +924,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
 #pragma unroll
     for (int g = 0; g < WGM; ++g) v += red[(g * 2 + which) * BN + c];
     // channel-major [2][NOUT][tiles], the layout bn_finalize_rows folds
-    p.stats[(which * p.NOUT + n0 + c) * ((p.M + FBM - 1) / FBM) + mt] = v;
+    p.stats[(which * p.NOUT + n0 + c) * ((p.M + BM - 1) / BM) + mt] = v;
   }
 }
 
@@ -1008,23 +1013,40 @@ bool conv_dgrad_supported(int Cin, int Cout) {
 }
 
 namespace {
-template <bool DGRAD>
-void launch_tap_gemm(const TapGemm& g, unsigned ytiles, hipStream_t stream) {
+template <bool DGRAD, int BM>
+void launch_tap_gemm_bm(const TapGemm& g, unsigned ytiles, hipStream_t stream) {
   const bool wide = g.NOUT % 64 == 0;
-  const int64_t blocks = conv_fwd_tiles(g.M) * (g.NOUT / (wide ? 64 : 32));
+  const int64_t blocks = (g.M + BM - 1) / BM * (g.NOUT / (wide ? 64 : 32));
   const dim3 grid(unsigned(blocks), ytiles);
   if (!DGRAD && g.C == 4) {
-    if (wide) tap_gemm_kernel<false, 64, true><<<grid, kThreads, 0, stream>>>(g);
-    else tap_gemm_kernel<false, 32, true><<<grid, kThreads, 0, stream>>>(g);
+    if (wide) tap_gemm_kernel<false, 64, true, BM><<<grid, kThreads, 0, stream>>>(g);
+    else tap_gemm_kernel<false, 32, true, BM><<<grid, kThreads, 0, stream>>>(g);
   } else if (wide) {
-    tap_gemm_kernel<DGRAD, 64><<<grid, kThreads, 0, stream>>>(g);
+    tap_gemm_kernel<DGRAD, 64, false, BM><<<grid, kThreads, 0, stream>>>(g);
   } else {
-    tap_gemm_kernel<DGRAD, 32><<<grid, kThreads, 0, stream>>>(g);
+    tap_gemm_kernel<DGRAD, 32, false, BM><<<grid, kThreads, 0, stream>>>(g);
   }
+}
+
+template <bool DGRAD>
+void launch_tap_gemm(const TapGemm& g, unsigned ytiles, hipStream_t stream) {
+  if (conv_tile_pixels(g.M, g.NOUT, int(ytiles)) == 64) launch_tap_gemm_bm<DGRAD, 64>(g, ytiles, stream);
+  else launch_tap_gemm_bm<DGRAD, FBM>(g, ytiles, stream);
 }
 }  // namespace
 
-int64_t conv_fwd_tiles(int64_t M) { return (M + FBM - 1) / FBM; }
+int conv_tile_pixels(int64_t M, int NOUT, int ytiles) {
+  // fewer than 2 blocks per CU with 128-pixel tiles: halve the tile
+  static const int env = std::getenv("BT_CONV_BM") ? std::atoi(std::getenv("BT_CONV_BM")) : 0;
+  if (env == 64 || env == 128) return env;
+  const int64_t blocks = (M + FBM - 1) / FBM * (NOUT / (NOUT % 64 == 0 ? 64 : 32)) * ytiles;
+  return blocks < 512 ? 64 : FBM;
+}
+
+int64_t conv_fwd_tiles(int64_t M, int NOUT) {
+  const int bm = conv_tile_pixels(M, NOUT, 1);
+  return (M + bm - 1) / bm;
+}
 
 hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream) {
   if (!conv_fwd_supported(p.Cin, p.Cout) || !p.x || !p.w || !p.y) return hipErrorInvalidValue;
@@ -1066,7 +1088,11 @@ hipError_t conv_weight_t_multi(const WeightTParams& p, hipStream_t stream) {
   return hipGetLastError();
 }
 
-int64_t conv_dgrad_bn_rows(int N, int H, int W) { return conv_fwd_tiles(int64_t(N) * (H / 2) * (W / 2)) * 4; }
+int64_t conv_dgrad_bn_rows(int N, int H, int W, int Cin) {
+  const int64_t M = int64_t(N) * (H / 2) * (W / 2);
+  const int bm = conv_tile_pixels(M, Cin, 4);
+  return (M + bm - 1) / bm * 4;
+}
 
 hipError_t conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int N, int H, int W, int Cin, int Cout,
                       hipStream_t stream, const BnBwdFuse* bn) {
@@ -1082,7 +1108,7 @@ hipError_t conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int 
   g.GH = Ho, g.GW = Wo, g.M = N * Ho * Wo;   // one parity class: every (a, b)
   g.NOUT = Cin, g.OH = H, g.OW = W;
   if (bn && bn->part) {
-    if (!bn->x || !bn->mean || !bn->invstd || !bn->w || !bn->b || bn->rows != conv_dgrad_bn_rows(N, H, W) ||
+    if (!bn->x || !bn->mean || !bn->invstd || !bn->w || !bn->b || bn->rows != conv_dgrad_bn_rows(N, H, W, Cin) ||
         (reinterpret_cast<uintptr_t>(bn->x) & 15))
       return hipErrorInvalidValue;
     g.bn = *bn;

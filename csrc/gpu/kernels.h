@@ -278,7 +278,7 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
 
 // Forward 4x4 / stride-2 / pad-1 convolution on the MFMA units (conv.hip):
 // x [N][H][W][Cin] bf16, w [Cout][4][4][Cin] bf16 (channels-last weight) ->
-// y [N][Ho][Wo][Cout] bf16.  stats (nullable): [2][Cout][conv_fwd_tiles(M)]
+// y [N][Ho][Wo][Cout] bf16.  stats (nullable): [2][Cout][conv_fwd_tiles(M, Cout)]
 // fp32 per-tile sum / sum of squares of the rounded y (channel-major) -- the
 // partials bn_finalize_rows folds into BatchNorm statistics.
 struct ConvFwdParams {
@@ -292,7 +292,10 @@ struct ConvFwdParams {
 };
 // Cin a power of two >= 8, or Cin == 4 (first layer, RGBA-decoded frames); Cout % 32 == 0.
 bool conv_fwd_supported(int Cin, int Cout);
-int64_t conv_fwd_tiles(int64_t M);
+int64_t conv_fwd_tiles(int64_t M, int Cout);
+// pixels per tap-GEMM tile (64 or 128) for a GEMM of M rows, NOUT outputs and
+// `ytiles` parity classes (BT_CONV_BM=64/128 overrides, for sweeps)
+int conv_tile_pixels(int64_t M, int NOUT, int ytiles);
 hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream);
 // Data gradient of the same convolution (same tap-gather GEMM kernel, four
 // stride-2 parity classes in one launch): dy [N][H/2][W/2][Cout] bf16,
@@ -313,7 +316,7 @@ hipError_t conv_weight_t_multi(const WeightTParams& p, hipStream_t stream);
 // backward whose saved input x ([N][H][W][Cin] bf16), batch mean / invstd,
 // affine w / b (fp32 [Cin]) and slope are given; the epilogue writes that
 // backward's per-tile sums of gz and gz * xhat, channel-major
-// [2][Cin][conv_dgrad_bn_rows(N, H, W)] fp32, for bn_backward_from_stats.
+// [2][Cin][conv_dgrad_bn_rows(N, H, W, Cin)] fp32, for bn_backward_from_stats.
 struct BnBwdFuse {
   const uint16_t* x = nullptr;
   const float* mean = nullptr;
@@ -324,7 +327,7 @@ struct BnBwdFuse {
   float* part = nullptr;
   int rows = 0;
 };
-int64_t conv_dgrad_bn_rows(int N, int H, int W);
+int64_t conv_dgrad_bn_rows(int N, int H, int W, int Cin);
 hipError_t conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int N, int H, int W, int Cin, int Cout,
                       hipStream_t stream, const BnBwdFuse* bn = nullptr);
 // bn_finalize over `nblocks` partial rows produced elsewhere (conv_fwd's epilogue)

@@ -1022,7 +1022,7 @@ def conv_fwd(x, w16, stats=None):
     """y = conv2d(x, w16, stride 2, pad 1) on the gfx950 MFMA kernel: ``x``
     [N, Cin, H, W] bf16 channels-last, ``w16`` [Cout, Cin, 4, 4] bf16
     channels-last; returns channels-last bf16 y.  ``stats`` (optional fp32
-    tensor of ``conv_fwd_stats_rows(M) * 2 * Cout``) receives per-tile
+    tensor of ``conv_fwd_stats_rows(M, Cout) * 2 * Cout``) receives per-tile
     BatchNorm sums of y, channel-major: ``stats.view(2, Cout, rows)`` holds
     the sums, then the sums of squares (see :func:`batch_norm_from_stats`)."""
     import torch
@@ -1089,7 +1089,7 @@ def conv_dgrad(dy, w16, in_shape, wt=None, bn=None):
     dx = torch.empty((N, Cin, H, W), dtype=torch.bfloat16, device=dy.device, memory_format=cl)
     _count('conv_dgrad')
     if bn is not None and bn.ready(dx):
-        rows = int(ext.conv_dgrad_bn_rows(N, H, W))
+        rows = int(ext.conv_dgrad_bn_rows(N, H, W, Cin))
         part = torch.empty(2 * Cin * rows, dtype=torch.float32, device=dy.device)
         _count('conv_dgrad_bn')
         ext.conv_dgrad(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), N, H, W, Cin, Cout, _stream(dy.device),
@@ -1119,9 +1119,11 @@ def conv_fwd_supported(x, w):
             and w.is_contiguous(memory_format=torch.channels_last))
 
 
-def conv_fwd_stats_rows(M):
-    """Partial-statistics rows :func:`conv_fwd` writes for M output pixels."""
-    return int(hip_ext().conv_fwd_tiles(int(M)))
+def conv_fwd_stats_rows(M, Cout):
+    """Partial-statistics rows :func:`conv_fwd` writes for M output pixels
+    and Cout channels (one per pixel tile; the tile height depends on the
+    GEMM's size)."""
+    return int(hip_ext().conv_fwd_tiles(int(M), int(Cout)))
 
 
 def _conv_function():
@@ -1141,7 +1143,8 @@ def _conv_function():
             if with_stats:
                 N, _, H, W = x.shape
                 M = N * ((H - 2) // 2 + 1) * ((W - 2) // 2 + 1)
-                stats = torch.empty(conv_fwd_stats_rows(M) * 2 * w16.shape[0], dtype=torch.float32, device=x.device)
+                stats = torch.empty(conv_fwd_stats_rows(M, w16.shape[0]) * 2 * w16.shape[0], dtype=torch.float32,
+                                    device=x.device)
                 y = conv_fwd(x, w16, stats)
                 ctx.mark_non_differentiable(stats)
                 return y, stats

@@ -50,7 +50,7 @@ def main():
             dy, x, w16, None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False]), a.iters), 2)
         import torch.nn.functional as F
         row['miopen_fwd_us'] = round(timed(lambda: F.conv2d(x, w16, None, 2, 1), a.iters), 2)
-        rows = ops.conv_fwd_stats_rows(a.batch * (h // 2) * (w // 2))
+        rows = ops.conv_fwd_stats_rows(a.batch * (h // 2) * (w // 2), cout)
         stats = torch.empty(rows * 2 * cout, device=dev)
         row['mfma_fwd_us'] = round(timed(lambda: ops.conv_fwd(x, w16), a.iters), 2)
         row['mfma_fwd_stats_us'] = round(timed(lambda: ops.conv_fwd(x, w16, stats), a.iters), 2)

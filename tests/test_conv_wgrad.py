@@ -108,7 +108,7 @@ def test_forward_matches_fp32_reference_and_stats(dev, N, Cin, H, W, Cout):
     x = torch.randn(N, Cin, H, W, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
     w = (0.1 * torch.randn(Cout, Cin, 4, 4, device=dev, generator=g)).to(torch.bfloat16).contiguous(memory_format=cl)
     M = N * (H // 2) * (W // 2)
-    rows = ops.conv_fwd_stats_rows(M)
+    rows = ops.conv_fwd_stats_rows(M, Cout)
     stats = torch.full((rows * 2 * Cout,), float('nan'), device=dev)
     y = ops.conv_fwd(x, w, stats)
     ref = F.conv2d(x.float(), w.float(), None, 2, 1)
@@ -148,7 +148,7 @@ def test_first_layer_rgba_forward_and_wgrad(dev, N, H, W):
     cl = torch.channels_last
     x = torch.rand(N, 4, H, W, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
     w = (0.1 * torch.randn(32, 3, 4, 4, device=dev, generator=g)).to(torch.bfloat16).contiguous(memory_format=cl)
-    rows = ops.conv_fwd_stats_rows(N * (H // 2) * (W // 2))
+    rows = ops.conv_fwd_stats_rows(N * (H // 2) * (W // 2), 32)
     stats = torch.empty(rows * 2 * 32, device=dev)
     y = ops.conv_fwd(x, w, stats)
     ref = F.conv2d(x[:, :3].float(), w.float(), None, 2, 1)
