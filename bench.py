@@ -254,10 +254,11 @@ def main(argv=None):
         # the compute stream), checked before anything depends on it: a P2P ring
         # over xGMI plus an all-reduce, each with a timeout that names this rank
         # and its peers (blendtorch/parallel/comm.py)
-        from blendtorch.parallel import DeviceComm
-        comm = DeviceComm(device=device if args.backend == 'nccl' else None)
-        allreduce['selfcheck'] = {k: (round(v, 3) if isinstance(v, float) else v)
-                                  for k, v in comm.selfcheck().items()}
+        if os.environ.get('BT_NO_DEVICECOMM') != '1':      # (diagnostic switch)
+            from blendtorch.parallel import DeviceComm
+            comm = DeviceComm(device=device if args.backend == 'nccl' else None)
+            allreduce['selfcheck'] = {k: (round(v, 3) if isinstance(v, float) else v)
+                                      for k, v in comm.selfcheck().items()}
 
     # place each rank's producers on CPUs local to its GPU (same NUMA domain as
     # the GPU's PCIe root: frames are written there and read back by the GPU),
