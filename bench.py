@@ -82,6 +82,21 @@ def cpu_budget():
     return cpus, budget, budget * 2 > len(cpus)
 
 
+def thread_cpu():
+    """{tid: (name, utime + stime ticks)} of this process's threads (Linux)."""
+    out = {}
+    for tid in os.listdir('/proc/self/task'):
+        try:
+            with open(f'/proc/self/task/{tid}/stat') as f:
+                st = f.read()
+        except OSError:
+            continue
+        name = st[st.index('(') + 1:st.rindex(')')]
+        rest = st[st.rindex(')') + 2:].split()
+        out[int(tid)] = (name, int(rest[11]) + int(rest[12]))
+    return out
+
+
 def cgroup_cpu_stat():
     """cgroup v2 cpu.stat counters (usage/throttling) -- producer-bound runs
     are CPU-quota sensitive, so report them next to the throughput."""
@@ -256,7 +271,8 @@ def main(argv=None):
         # and its peers (blendtorch/parallel/comm.py)
         if os.environ.get('BT_NO_DEVICECOMM') != '1':      # (diagnostic switch)
             from blendtorch.parallel import DeviceComm
-            comm = DeviceComm(device=device if args.backend == 'nccl' else None)
+            comm = DeviceComm(device=device if args.backend == 'nccl' else None,
+                              dedicated=os.environ.get('BT_DEVICECOMM_SHARED') != '1')
             allreduce['selfcheck'] = {k: (round(v, 3) if isinstance(v, float) else v)
                                       for k, v in comm.selfcheck().items()}
 
@@ -438,6 +454,7 @@ def main(argv=None):
         if world > 1:
             dist.barrier()
         cg0 = cgroup_cpu_stat()
+        th0 = thread_cpu() if os.environ.get('BT_THREAD_REPORT') == '1' else None
         ru0 = os.times()
         snap0 = dl.snapshot() if dl is not None else {}
         t0 = time.perf_counter()
@@ -454,6 +471,11 @@ def main(argv=None):
         for k in ('usage_usec', 'throttled_usec', 'nr_throttled'):
             if k in cg0 and k in cg1:
                 cpu['cgroup_' + k] = cg1[k] - cg0[k]
+        if th0 is not None:
+            # (diagnostic) this process's busiest threads over the timed region
+            th1 = thread_cpu()
+            busy = sorted(((th1[t][1] - th0.get(t, ('', 0))[1], th1[t][0]) for t in th1), reverse=True)
+            cpu['threads_cpu_s'] = [[name, round(d / os.sysconf('SC_CLK_TCK'), 3)] for d, name in busy[:12] if d > 0]
         shape = tuple(img.shape)
         if args.dist == 'scatter':
             try:            # run the source to its end so its stats are final

@@ -514,24 +514,31 @@ struct TapGemm {
   BnBwdFuse bn;                    // data gradient only: BN backward statistics in the epilogue (bn.part nullable)
 };
 
-// BN = output channels per block (64, or 32 for 32-channel outputs such as
-// the first layer's data gradient); 4 waves as WGM (pixels) x WGN (channels).
+// BN = output channels per block (128 or 64, or 32 for 32-channel outputs
+// such as the first layer's data gradient); 4 waves as WGM (pixels) x WGN
+// (channels).  A wider BN re-reads the tap-gathered A tile for fewer channel
+// tiles (the deep layers' A traffic is the bound, not the MFMAs).
 // BM = pixels per block: 128, or 64 when 128-pixel tiles would leave the
 // chip short of blocks (the deep-K layers: 300-600 tiles on 256 CUs).
 template <bool DGRAD, int BN, bool C4 = false, int BM = FBM>
 __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   constexpr int RJ = BM / 32;                  // staged A rows per thread (ar + 32 j)
   constexpr int A_TILE = BM * F_ROW;
-  constexpr int WGM = BN == 64 ? 2 : 4, WGN = 4 / WGM;
+  constexpr int WGM = BN >= 64 ? 2 : 4, WGN = 4 / WGM;
+  constexpr int RB = BN / 32;                  // staged B rows per thread (ar + 32 j)
+  // epilogue tile row pitch (bytes): whole 128-byte rows at least, so the
+  // 8-chunk XOR swizzle stays inside its row (a 32-channel row uses half)
+  constexpr int T_ROW = BN >= 64 ? BN * 2 : F_ROW;
   constexpr int FM = BM / WGM / 16, FN = BN / WGN / 16;   // 16x16 fragments per wave
   // one stage = the A tile + a BN-row B tile; the epilogue's bf16 tile
-  // ([BM][128 B] = A_TILE) and the per-wave channel sums (red, [4][2][BN])
+  // ([BM][BN] bf16) and the per-wave channel sums (red, [4][2][BN])
   // reuse the staging space once the k-loop is done.  A 32-channel block
   // therefore takes 40 KiB, and four fit a CU's LDS (50 KiB fit three).
   constexpr int STG = A_TILE + BN * F_ROW;
-  static_assert(2 * STG >= A_TILE + 4 * 2 * BN * 4, "epilogue does not fit the staging LDS");
+  constexpr int E_TILE = BM * T_ROW;
+  static_assert(2 * STG >= E_TILE + 4 * 2 * BN * 4, "epilogue does not fit the staging LDS");
   __shared__ __attribute__((aligned(16))) char smem[2 * STG];
-  float* red = reinterpret_cast<float*>(smem + A_TILE);   // [WGM][2][BN], after the epilogue tile
+  float* red = reinterpret_cast<float*>(smem + E_TILE);   // [WGM][2][BN], after the epilogue tile
   const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
   constexpr int NTAPS = DGRAD ? 4 : 16;
   const int K = C4 ? FBK : NTAPS * p.C, NT = p.NOUT / BN;
@@ -611,9 +618,9 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     vmask[j] = pin[j] ? mk : 0u;
   }
   const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(p.src, int64_t(p.N) * p.SH * p.SW * p.C * 2);
-  const uint16_t* wrow0 = p.w + (n0 + ar) * (16 * p.C);
-  const uint16_t* wrow1 = p.w + (n0 + (BN == 64 ? ar + 32 : ar)) * (16 * p.C);
-  uint4 ra[RJ], rb0, rb1;
+  const uint16_t* wrow = p.w + (n0 + ar) * (16 * p.C);   // B rows ar + 32 j: 32 * 16 * C elements apart
+  uint4 ra[RJ + RB];   // staged A rows, then B rows (one array: SROA keeps it in registers)
+  uint4* const rbv = ra + RJ;
   auto load_c4 = [&]() {
     // first layer, 4-channel input: K = 16 taps x 4 = one k-step; chunk ac is
     // taps (kh, kw) and (kh, kw + 1) of one row -- two adjacent input pixels,
@@ -629,12 +636,16 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     }
     // weights: 4 input channels, or 3 (an RGB model fed RGBA: channel 3 gets weight 0)
     const int tap = kh * 4 + kw;
-    if (p.wc == 4) {
-      rb0 = *reinterpret_cast<const uint4*>(p.w + ((n0 + ar) * 16 + tap) * 4);
-    } else {
-      const uint16_t* q = p.w + ((n0 + ar) * 16 + tap) * 3;
-      rb0 = make_uint4(uint32_t(q[0]) | (uint32_t(q[1]) << 16), uint32_t(q[2]),
-                       uint32_t(q[3]) | (uint32_t(q[4]) << 16), uint32_t(q[5]));
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+      const int co = n0 + ar + 32 * j;
+      if (p.wc == 4) {
+        rbv[j] = *reinterpret_cast<const uint4*>(p.w + (co * 16 + tap) * 4);
+      } else {
+        const uint16_t* q = p.w + (co * 16 + tap) * 3;
+        rbv[j] = make_uint4(uint32_t(q[0]) | (uint32_t(q[1]) << 16), uint32_t(q[2]),
+                            uint32_t(q[3]) | (uint32_t(q[4]) << 16), uint32_t(q[5]));
+      }
     }
   };
   const int nsteps = K / FBK;
@@ -663,16 +674,16 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
 #pragma unroll
     for (int j = 0; j < RJ; ++j) ra[j] = bload(rs_src, (vmask[j] & tbit) ? abase[j] + soff : kOOB);
     const int woff = wtap * p.C + ch;
-    rb0 = *reinterpret_cast<const uint4*>(wrow0 + woff);
-    if (BN == 64) rb1 = *reinterpret_cast<const uint4*>(wrow1 + woff);
+#pragma unroll
+    for (int j = 0; j < RB; ++j) rbv[j] = *reinterpret_cast<const uint4*>(wrow + j * (32 * 16) * p.C + woff);
   };
   const int st_a = f_off(ar, ac);   // rows ar + 32j keep the swizzle phase: (ar + 32j) & 7 == ar & 7
   auto store = [&](int buf) {
     char* ai = smem + buf * STG;
 #pragma unroll
     for (int j = 0; j < RJ; ++j) *reinterpret_cast<uint4*>(ai + st_a + j * 32 * F_ROW) = ra[j];
-    *reinterpret_cast<uint4*>(ai + A_TILE + st_a) = rb0;
-    if (BN == 64) *reinterpret_cast<uint4*>(ai + A_TILE + st_a + 32 * F_ROW) = rb1;
+#pragma unroll
+    for (int j = 0; j < RB; ++j) *reinterpret_cast<uint4*>(ai + A_TILE + st_a + j * 32 * F_ROW) = rbv[j];
   };
 
   f32x4 acc[FM][FN];
@@ -721,14 +732,12 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     // LDS-only, so the ring's later stages stay in flight across it (counted
     // vmcnt waits on the stage being stored).
     constexpr int kDepth = 2;
-    uint4 ring_a[kDepth][RJ], ring_b0[kDepth], ring_b1[kDepth];
+    uint4 ring[kDepth][RJ + RB];
     int ks_next = 0;
     auto fetch = [&](int u) {
       load(ks_next++);
 #pragma unroll
-      for (int j = 0; j < RJ; ++j) ring_a[u][j] = ra[j];
-      ring_b0[u] = rb0;
-      if (BN == 64) ring_b1[u] = rb1;
+      for (int j = 0; j < RJ + RB; ++j) ring[u][j] = ra[j];
     };
 #pragma unroll
     for (int u = 0; u < kDepth; ++u) fetch(u);
@@ -738,9 +747,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
       for (int u = 0; u < kDepth; ++u) {
         const int buf = u & 1;   // kDepth is even: (s0 + u) & 1
 #pragma unroll
-        for (int j = 0; j < RJ; ++j) ra[j] = ring_a[u][j];
-        rb0 = ring_b0[u];
-        if (BN == 64) rb1 = ring_b1[u];
+        for (int j = 0; j < RJ + RB; ++j) ra[j] = ring[u][j];
         store(buf);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -812,7 +819,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     const int col = col0 + 16 * j + (lane & 15);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      toff[j][r] = (row0 + lr + r) * (F_ROW / 2) + ((((col >> 3) ^ ((lr + r) & 7)) << 4) >> 1) + (col & 7);
+      toff[j][r] = (row0 + lr + r) * (T_ROW / 2) + ((((col >> 3) ^ ((lr + r) & 7)) << 4) >> 1) + (col & 7);
   }
   const bool all_rows = m0 + BM <= p.M;   // the tile holds no row past the GEMM
 #pragma unroll
@@ -829,7 +836,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const uint32_t w2 = pk[r >> 1];
-        tile[toff[j][r] + i * 16 * (F_ROW / 2)] = uint16_t(r & 1 ? w2 >> 16 : w2);
+        tile[toff[j][r] + i * 16 * (T_ROW / 2)] = uint16_t(r & 1 ? w2 >> 16 : w2);
         if (!DGRAD && (all_rows || m0 + row0 + 16 * i + lr + r < p.M)) {
           const float vr = __uint_as_float(r & 1 ? w2 & 0xFFFF0000u : w2 << 16);
           sum[j] += vr;
@@ -876,7 +883,8 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     if (!epin[j]) continue;
-    const uint4 v = *reinterpret_cast<const uint4*>(smem + f_off(t / CPR + RPP * j, ec));
+    const int er = t / CPR + RPP * j;
+    const uint4 v = *reinterpret_cast<const uint4*>(smem + er * T_ROW + ((ec ^ (er & 7)) << 4));
     *reinterpret_cast<uint4*>(p.dst + eob[j] + n0 + ec * 8) = v;
     if (bnf) {
       const uint4 xv = xpre[j];
@@ -1014,14 +1022,15 @@ bool conv_dgrad_supported(int Cin, int Cout) {
 
 namespace {
 template <bool DGRAD, int BM>
-void launch_tap_gemm_bm(const TapGemm& g, unsigned ytiles, hipStream_t stream) {
-  const bool wide = g.NOUT % 64 == 0;
-  const int64_t blocks = (g.M + BM - 1) / BM * (g.NOUT / (wide ? 64 : 32));
+void launch_tap_gemm_bm(const TapGemm& g, int bn, unsigned ytiles, hipStream_t stream) {
+  const int64_t blocks = (g.M + BM - 1) / BM * (g.NOUT / bn);
   const dim3 grid(unsigned(blocks), ytiles);
   if (!DGRAD && g.C == 4) {
-    if (wide) tap_gemm_kernel<false, 64, true, BM><<<grid, kThreads, 0, stream>>>(g);
+    if (bn == 64) tap_gemm_kernel<false, 64, true, BM><<<grid, kThreads, 0, stream>>>(g);
     else tap_gemm_kernel<false, 32, true, BM><<<grid, kThreads, 0, stream>>>(g);
-  } else if (wide) {
+  } else if (bn == 128) {
+    tap_gemm_kernel<DGRAD, 128, false, BM><<<grid, kThreads, 0, stream>>>(g);
+  } else if (bn == 64) {
     tap_gemm_kernel<DGRAD, 64, false, BM><<<grid, kThreads, 0, stream>>>(g);
   } else {
     tap_gemm_kernel<DGRAD, 32, false, BM><<<grid, kThreads, 0, stream>>>(g);
@@ -1030,16 +1039,39 @@ void launch_tap_gemm_bm(const TapGemm& g, unsigned ytiles, hipStream_t stream) {
 
 template <bool DGRAD>
 void launch_tap_gemm(const TapGemm& g, unsigned ytiles, hipStream_t stream) {
-  if (conv_tile_pixels(g.M, g.NOUT, int(ytiles)) == 64) launch_tap_gemm_bm<DGRAD, 64>(g, ytiles, stream);
-  else launch_tap_gemm_bm<DGRAD, FBM>(g, ytiles, stream);
+  const int bn = conv_tile_channels(g.NOUT, g.C == 4 && !DGRAD);
+  if (conv_tile_pixels(g.M, g.NOUT, int(ytiles)) == 64) launch_tap_gemm_bm<DGRAD, 64>(g, bn, ytiles, stream);
+  else launch_tap_gemm_bm<DGRAD, FBM>(g, bn, ytiles, stream);
 }
+
+// tile-size overrides (0 = the automatic rule); set from tests and sweeps,
+// first from BT_CONV_BM / BT_CONV_BN
+int env_int(const char* name) {
+  const char* v = std::getenv(name);
+  return v ? std::atoi(v) : 0;
+}
+int g_force_bm = env_int("BT_CONV_BM");
+int g_force_bn = env_int("BT_CONV_BN");
 }  // namespace
+
+void conv_set_tiles(int bm, int bn) {
+  g_force_bm = bm == 64 || bm == 128 ? bm : 0;
+  g_force_bn = bn == 32 || bn == 64 || bn == 128 ? bn : 0;
+}
+
+int conv_tile_channels(int NOUT, bool c4) {
+  // 64 by default; 128 (an override) halves how often the tap-gathered A
+  // tile is re-read; 32 for 32-channel outputs.  The first layer's one-step K
+  // has no use for 128.
+  const int f = g_force_bn;
+  if (f && NOUT % f == 0 && !(c4 && f == 128)) return f;
+  return NOUT % 64 == 0 ? 64 : 32;
+}
 
 int conv_tile_pixels(int64_t M, int NOUT, int ytiles) {
   // fewer than 2 blocks per CU with 128-pixel tiles: halve the tile
-  static const int env = std::getenv("BT_CONV_BM") ? std::atoi(std::getenv("BT_CONV_BM")) : 0;
-  if (env == 64 || env == 128) return env;
-  const int64_t blocks = (M + FBM - 1) / FBM * (NOUT / (NOUT % 64 == 0 ? 64 : 32)) * ytiles;
+  if (g_force_bm) return g_force_bm;
+  const int64_t blocks = (M + FBM - 1) / FBM * (NOUT / conv_tile_channels(NOUT, false)) * ytiles;
   return blocks < 512 ? 64 : FBM;
 }
 

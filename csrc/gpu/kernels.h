@@ -294,8 +294,13 @@ struct ConvFwdParams {
 bool conv_fwd_supported(int Cin, int Cout);
 int64_t conv_fwd_tiles(int64_t M, int Cout);
 // pixels per tap-GEMM tile (64 or 128) for a GEMM of M rows, NOUT outputs and
-// `ytiles` parity classes (BT_CONV_BM=64/128 overrides, for sweeps)
+// `ytiles` parity classes, and output channels per tile (32, 64 or 128).
 int conv_tile_pixels(int64_t M, int NOUT, int ytiles);
+int conv_tile_channels(int NOUT, bool first_layer);
+// Force the tile sizes (0 = automatic; initially BT_CONV_BM / BT_CONV_BN).
+// Row counts of the statistics buffers follow the tile size: change it only
+// between steps, never between sizing a buffer and the launch that fills it.
+void conv_set_tiles(int bm, int bn);
 hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream);
 // Data gradient of the same convolution (same tap-gather GEMM kernel, four
 // stride-2 parity classes in one launch): dy [N][H/2][W/2][Cout] bf16,

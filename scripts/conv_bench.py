@@ -1,4 +1,4 @@
-"""Weight-gradient kernel timing on the bench discriminator's layers (batch 8,
+"""Tap-GEMM forward / data-gradient and weight-gradient kernel timing on the bench discriminator's layers (batch 8,
 640x480 input): gfx950 MFMA ``ops.conv_wgrad`` (over several grid sizes) vs
 MIOpen's bf16 weight gradient (``aten.convolution_backward``, weight only).
 
@@ -19,24 +19,49 @@ LAYERS = [(32, 240, 320, 64), (64, 120, 160, 128), (128, 60, 80, 256)]
    # Cin, H, W, Cout (input side)
 
 
+GRAPH = True
+
+
 def timed(fn, iters):
+    """Device time per call: ``fn`` captured 20 times in a HIP graph and the
+    graph replayed (eager calls measure the host's launch path instead --
+    ~20 us per call, more than most of these kernels take)."""
     for _ in range(5):
         fn()
     torch.cuda.synchronize()
+    reps = 20
+    g = None
+    if GRAPH:
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(reps):
+                fn()
+        g.replay()
+        torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = max(1, iters // reps)
     e0.record()
-    for _ in range(iters):
-        fn()
+    if g is not None:
+        for _ in range(n):
+            g.replay()
+    else:
+        for _ in range(n * reps):
+            fn()
     e1.record()
     torch.cuda.synchronize()
-    return e0.elapsed_time(e1) * 1000 / iters
+    return e0.elapsed_time(e1) * 1000 / (n * reps)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--iters', type=int, default=200)
     ap.add_argument('--batch', type=int, default=8)
+    ap.add_argument('--eager', action='store_true', help='time eager calls (host launch path included)')
     a = ap.parse_args()
+    global GRAPH
+    GRAPH = not a.eager
     torch.backends.cudnn.benchmark = True
     dev = torch.device('cuda', 0)
     cl = torch.channels_last

@@ -24,5 +24,6 @@ for cin, h, w, cout in [(32, 240, 320, 64), (64, 120, 160, 128), (128, 60, 80, 2
     for _ in range(a.iters):
         ops.conv_wgrad(x, dy, out, target_blocks=a.blocks)
         ops.conv_fwd(x, w16)
+        ops.conv_dgrad(dy, w16, tuple(x.shape))
 torch.cuda.synchronize()
 print('done')

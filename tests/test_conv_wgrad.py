@@ -204,3 +204,52 @@ def test_bn_backward_sums_from_dgrad_epilogue(dev, monkeypatch):
     assert ops.KERNEL_CALLS.get('bn_backward_from_stats', 0) == before + 3
     for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
         torch.testing.assert_close(pa.grad, pb.grad, rtol=2e-2, atol=2e-2 * float(pb.grad.abs().max()), msg=n)
+
+
+@pytest.fixture
+def tiles(request):
+    bm, bn = request.param
+    ops.conv_set_tiles(bm, bn)
+    yield bm, bn
+    ops.conv_set_tiles(0, 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('tiles', [(64, 64), (128, 64), (64, 128), (128, 128), (64, 32), (128, 32)],
+                         indirect=True, ids=lambda t: f'bm{t[0]}_bn{t[1]}')
+def test_tap_gemm_tile_variants(dev, tiles):
+    """Every tile shape of the tap-gather GEMM (pixels x output channels)
+    against the fp32 reference: forward with statistics, data gradient, and
+    the data gradient with the BN-backward epilogue (Discriminator backward)."""
+    import torch.nn.functional as F
+    from blendtorch.models import Discriminator
+    bm, bn = tiles
+    cl = torch.channels_last
+    g = torch.Generator(device=dev).manual_seed(bm + bn)
+    for N, Cin, H, W, Cout in [(2, 64, 30, 40, 128), (1, 128, 8, 10, 256), (3, 32, 14, 18, 64)]:
+        x = torch.randn(N, Cin, H, W, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+        w = (0.1 * torch.randn(Cout, Cin, 4, 4, device=dev, generator=g)).to(torch.bfloat16).contiguous(memory_format=cl)
+        M = N * (H // 2) * (W // 2)
+        rows = ops.conv_fwd_stats_rows(M, Cout)
+        stats = torch.full((rows * 2 * Cout,), float('nan'), device=dev)
+        y = ops.conv_fwd(x, w, stats)
+        ref = F.conv2d(x.float(), w.float(), None, 2, 1)
+        torch.testing.assert_close(y.float(), ref, rtol=2 ** -7, atol=1e-3 * float(ref.abs().max()))
+        yf = y.float().permute(0, 2, 3, 1).reshape(-1, Cout)
+        st = stats.view(2, Cout, rows).sum(-1)
+        torch.testing.assert_close(st[0], yf.sum(0), rtol=1e-4, atol=1e-3)
+        torch.testing.assert_close(st[1], (yf * yf).sum(0), rtol=1e-4, atol=1e-3)
+        dy = torch.randn(N, Cout, H // 2, W // 2, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+        dx = ops.conv_dgrad(dy, w, (N, Cin, H, W))
+        dref = torch.nn.grad.conv2d_input((N, Cin, H, W), w.float(), dy.float(), stride=2, padding=1)
+        torch.testing.assert_close(dx.float(), dref, rtol=2 ** -7, atol=1e-3 * float(dref.abs().max()))
+    torch.manual_seed(5)
+    a = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
+    xin = torch.rand(4, 4, 96, 128, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    a.bce_loss_bf16(xin, 1.0).backward()
+    got = [p.grad.clone() for p in a.parameters()]
+    ops.conv_set_tiles(0, 0)
+    a.zero_grad(set_to_none=True)
+    a.bce_loss_bf16(xin, 1.0).backward()
+    for (n, p), g0 in zip(a.named_parameters(), got):
+        torch.testing.assert_close(g0, p.grad, rtol=2e-2, atol=2e-2 * float(p.grad.abs().max()), msg=n)
