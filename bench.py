@@ -272,7 +272,7 @@ def main(argv=None):
         if os.environ.get('BT_NO_DEVICECOMM') != '1':      # (diagnostic switch)
             from blendtorch.parallel import DeviceComm
             comm = DeviceComm(device=device if args.backend == 'nccl' else None,
-                              dedicated=os.environ.get('BT_DEVICECOMM_SHARED') != '1')
+                              dedicated=os.environ.get('BT_DEVICECOMM_DEDICATED') == '1')
             allreduce['selfcheck'] = {k: (round(v, 3) if isinstance(v, float) else v)
                                       for k, v in comm.selfcheck().items()}
 

@@ -520,7 +520,11 @@ struct TapGemm {
 // tiles (the deep layers' A traffic is the bound, not the MFMAs).
 // BM = pixels per block: 128, or 64 when 128-pixel tiles would leave the
 // chip short of blocks (the deep-K layers: 300-600 tiles on 256 CUs).
-template <bool DGRAD, int BN, bool C4 = false, int BM = FBM>
+// NST = staging: 0 = loads into a register ring then ds_write_b128 into two
+// LDS buffers; 2 or 3 = LDS-DMA (buffer_load ... lds) straight into NST LDS
+// stages -- the 16-byte LDS stores of the register path run at ~79 B/clk/CU
+// (a third of what the fragment reads get) and were the kernel's bound.
+template <bool DGRAD, int BN, bool C4 = false, int BM = FBM, int NST = 0>
 __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   constexpr int RJ = BM / 32;                  // staged A rows per thread (ar + 32 j)
   constexpr int A_TILE = BM * F_ROW;
@@ -536,8 +540,10 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   // therefore takes 40 KiB, and four fit a CU's LDS (50 KiB fit three).
   constexpr int STG = A_TILE + BN * F_ROW;
   constexpr int E_TILE = BM * T_ROW;
-  static_assert(2 * STG >= E_TILE + 4 * 2 * BN * 4, "epilogue does not fit the staging LDS");
-  __shared__ __attribute__((aligned(16))) char smem[2 * STG];
+  constexpr int NBUF = (C4 || NST == 0) ? 2 : NST;
+  static_assert(NST == 0 || NST == 2 || NST == 3, "staging: register ring, or 2-3 LDS-DMA stages");
+  static_assert(NBUF * STG >= E_TILE + 4 * 2 * BN * 4, "epilogue does not fit the staging LDS");
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * STG];
   float* red = reinterpret_cast<float*>(smem + E_TILE);   // [WGM][2][BN], after the epilogue tile
   const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
   constexpr int NTAPS = DGRAD ? 4 : 16;
@@ -618,6 +624,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     vmask[j] = pin[j] ? mk : 0u;
   }
   const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(p.src, int64_t(p.N) * p.SH * p.SW * p.C * 2);
+  const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(p.w, int64_t(p.NOUT) * 16 * p.C * 2);
   const uint16_t* wrow = p.w + (n0 + ar) * (16 * p.C);   // B rows ar + 32 j: 32 * 16 * C elements apart
   uint4 ra[RJ + RB];   // staged A rows, then B rows (one array: SROA keeps it in registers)
   uint4* const rbv = ra + RJ;
@@ -685,6 +692,42 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
 #pragma unroll
     for (int j = 0; j < RB; ++j) *reinterpret_cast<uint4*>(ai + A_TILE + st_a + j * 32 * F_ROW) = rbv[j];
   };
+  // LDS-DMA staging: one wave-instruction writes 1 KiB of LDS linearly (lane l
+  // at 16 l), i.e. rows 8 w + 32 j .. + 7 of the tile, lane l on row 8 w +
+  // 32 j + l / 8 at PHYSICAL chunk l & 7.  The XOR swizzle of the image
+  // (logical chunk c at c ^ (row & 7)) therefore moves to the source: lane l
+  // fetches logical chunk (l & 7) ^ (l / 8).  Border taps load out of range
+  // (zeros).  All LDS in one array (a second __shared__ object makes hipcc
+  // drain vmcnt before the fragment reads).
+  const int acs = ac ^ (ar & 7);
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const uint32_t wrow_b = uint32_t((n0 + ar) * 16 * p.C) * 2u;   // byte offset of B row ar
+  auto issue = [&](int ks, int buf) {
+    const int kc = ks * FBK + acs * 8;
+    const int tap = kc >> p.cshift, ch = kc & (p.C - 1);
+    int dr, dc, wtap;
+    if (DGRAD) {
+      dr = ph - (tap >> 1);
+      dc = pw - (tap & 1);
+      wtap = (1 - ph + 2 * (tap >> 1)) * 4 + (1 - pw + 2 * (tap & 1));
+    } else {
+      dr = tap >> 2;
+      dc = tap & 3;
+      wtap = tap;
+    }
+    const uint32_t soff = uint32_t((((dr * p.SW + dc) << p.cshift) + ch) * 2);
+    const uint32_t tbit = 1u << tap;
+    char* st = smem + buf * STG + wv * 1024;
+#pragma unroll
+    for (int j = 0; j < RJ; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_src, (__attribute__((address_space(3))) void*)(st + j * 4096), 16,
+                                               int((vmask[j] & tbit) ? abase[j] + soff : kOOB), 0, 0, 0);
+    const uint32_t woff = wrow_b + uint32_t(wtap * p.C + ch) * 2u;
+#pragma unroll
+    for (int j = 0; j < RB; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w, (__attribute__((address_space(3))) void*)(st + A_TILE + j * 4096),
+                                               16, int(woff + uint32_t(j * 32 * 16 * p.C) * 2u), 0, 0, 0);
+  };
 
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -725,6 +768,30 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     __syncthreads();
     mma(0);
     __syncthreads();   // the epilogue tile overwrites stage 0
+  } else if constexpr (NST > 0) {
+    // NST - 1 stages in flight: at step ks wait for stage ks (the NST - 2
+    // younger stages' NL loads each may stay out), barrier (stage ks is
+    // visible to every wave, and every wave is done reading stage ks - 1),
+    // refill stage ks - 1's buffer with step ks + NST - 1, then the MFMAs
+    constexpr int NL = RJ + RB;   // LDS-DMA instructions per stage per thread
+    constexpr uint32_t kWaitAll = (7u << 4) | (0xFu << 8);   // vmcnt(0), no lgkm / exp wait
+    constexpr uint32_t kWaitOne = kWaitAll | uint32_t(NL & 15) | (uint32_t(NL >> 4) << 14);
+#pragma unroll
+    for (int u = 0; u < NST - 1; ++u)
+      if (u < nsteps) issue(u, u);
+    int cur = 0;
+    for (int ks = 0; ks < nsteps; ++ks) {
+      if (NST == 3 && ks + 1 < nsteps) __builtin_amdgcn_s_waitcnt(kWaitOne);
+      else __builtin_amdgcn_s_waitcnt(kWaitAll);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const int nxt = ks + NST - 1;
+      if (nxt < nsteps) issue(nxt, cur == 0 ? NST - 1 : cur - 1);
+      mma(cur);
+      cur = cur == NST - 1 ? 0 : cur + 1;
+    }
+    __syncthreads();   // the epilogue reuses the staging LDS
   } else {
     // Loads run kDepth steps ahead of the MFMAs in a register ring: with one
     // step of prefetch every k-step waited out a full global-load latency, and
@@ -1021,7 +1088,7 @@ bool conv_dgrad_supported(int Cin, int Cout) {
 }
 
 namespace {
-template <bool DGRAD, int BM>
+template <bool DGRAD, int BM, int NST>
 void launch_tap_gemm_bm(const TapGemm& g, int bn, unsigned ytiles, hipStream_t stream) {
   const int64_t blocks = (g.M + BM - 1) / BM * (g.NOUT / bn);
   const dim3 grid(unsigned(blocks), ytiles);
@@ -1029,19 +1096,39 @@ void launch_tap_gemm_bm(const TapGemm& g, int bn, unsigned ytiles, hipStream_t s
     if (bn == 64) tap_gemm_kernel<false, 64, true, BM><<<grid, kThreads, 0, stream>>>(g);
     else tap_gemm_kernel<false, 32, true, BM><<<grid, kThreads, 0, stream>>>(g);
   } else if (bn == 128) {
-    tap_gemm_kernel<DGRAD, 128, false, BM><<<grid, kThreads, 0, stream>>>(g);
+    tap_gemm_kernel<DGRAD, 128, false, BM, NST><<<grid, kThreads, 0, stream>>>(g);
   } else if (bn == 64) {
-    tap_gemm_kernel<DGRAD, 64, false, BM><<<grid, kThreads, 0, stream>>>(g);
+    tap_gemm_kernel<DGRAD, 64, false, BM, NST><<<grid, kThreads, 0, stream>>>(g);
   } else {
-    tap_gemm_kernel<DGRAD, 32, false, BM><<<grid, kThreads, 0, stream>>>(g);
+    tap_gemm_kernel<DGRAD, 32, false, BM, NST><<<grid, kThreads, 0, stream>>>(g);
+  }
+}
+
+int g_staging = -1;   // 0 register ring, 2/3 LDS-DMA stages; -1 = BT_CONV_STAGING or the default
+
+int staging() {
+  if (g_staging < 0) {
+    const char* v = std::getenv("BT_CONV_STAGING");
+    const int e = v ? std::atoi(v) : 2;
+    g_staging = e == 0 || e == 2 || e == 3 ? e : 2;
+  }
+  return g_staging;
+}
+
+template <bool DGRAD, int BM>
+void launch_tap_gemm_st(const TapGemm& g, int bn, unsigned ytiles, hipStream_t stream) {
+  switch (staging()) {
+    case 0: launch_tap_gemm_bm<DGRAD, BM, 0>(g, bn, ytiles, stream); break;
+    case 3: launch_tap_gemm_bm<DGRAD, BM, 3>(g, bn, ytiles, stream); break;
+    default: launch_tap_gemm_bm<DGRAD, BM, 2>(g, bn, ytiles, stream); break;
   }
 }
 
 template <bool DGRAD>
 void launch_tap_gemm(const TapGemm& g, unsigned ytiles, hipStream_t stream) {
   const int bn = conv_tile_channels(g.NOUT, g.C == 4 && !DGRAD);
-  if (conv_tile_pixels(g.M, g.NOUT, int(ytiles)) == 64) launch_tap_gemm_bm<DGRAD, 64>(g, bn, ytiles, stream);
-  else launch_tap_gemm_bm<DGRAD, FBM>(g, bn, ytiles, stream);
+  if (conv_tile_pixels(g.M, g.NOUT, int(ytiles)) == 64) launch_tap_gemm_st<DGRAD, 64>(g, bn, ytiles, stream);
+  else launch_tap_gemm_st<DGRAD, FBM>(g, bn, ytiles, stream);
 }
 
 // tile-size overrides (0 = the automatic rule); set from tests and sweeps,
@@ -1054,9 +1141,10 @@ int g_force_bm = env_int("BT_CONV_BM");
 int g_force_bn = env_int("BT_CONV_BN");
 }  // namespace
 
-void conv_set_tiles(int bm, int bn) {
+void conv_set_tiles(int bm, int bn, int staging) {
   g_force_bm = bm == 64 || bm == 128 ? bm : 0;
   g_force_bn = bn == 32 || bn == 64 || bn == 128 ? bn : 0;
+  g_staging = staging == 0 || staging == 2 || staging == 3 ? staging : -1;
 }
 
 int conv_tile_channels(int NOUT, bool c4) {

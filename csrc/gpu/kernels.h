@@ -297,10 +297,12 @@ int64_t conv_fwd_tiles(int64_t M, int Cout);
 // `ytiles` parity classes, and output channels per tile (32, 64 or 128).
 int conv_tile_pixels(int64_t M, int NOUT, int ytiles);
 int conv_tile_channels(int NOUT, bool first_layer);
-// Force the tile sizes (0 = automatic; initially BT_CONV_BM / BT_CONV_BN).
+// Force the tile sizes (0 = automatic; initially BT_CONV_BM / BT_CONV_BN) and
+// the staging (0 = register ring, 2 / 3 = LDS-DMA stages; -1 = default,
+// BT_CONV_STAGING).
 // Row counts of the statistics buffers follow the tile size: change it only
 // between steps, never between sizing a buffer and the launch that fills it.
-void conv_set_tiles(int bm, int bn);
+void conv_set_tiles(int bm, int bn, int staging = -1);
 hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream);
 // Data gradient of the same convolution (same tap-gather GEMM kernel, four
 // stride-2 parity classes in one launch): dy [N][H/2][W/2][Cout] bf16,

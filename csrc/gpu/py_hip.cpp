@@ -237,7 +237,7 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("s_co"), py::arg("s_ci"), py::arg("s_kh"), py::arg("s_kw"), py::arg("stream"), py::arg("cin_out") = 0);
 
   m.def("conv_fwd_tiles", &conv_fwd_tiles);
-  m.def("conv_set_tiles", &conv_set_tiles, py::arg("bm") = 0, py::arg("bn") = 0);
+  m.def("conv_set_tiles", &conv_set_tiles, py::arg("bm") = 0, py::arg("bn") = 0, py::arg("staging") = -1);
   m.def("conv_tile_pixels", &conv_tile_pixels);
   m.def("conv_tile_channels", &conv_tile_channels);
   m.def("conv_dgrad_supported", &conv_dgrad_supported);

@@ -1126,12 +1126,13 @@ def conv_fwd_stats_rows(M, Cout):
     return int(hip_ext().conv_fwd_tiles(int(M), int(Cout)))
 
 
-def conv_set_tiles(bm=0, bn=0):
+def conv_set_tiles(bm=0, bn=0, staging=-1):
     """Force the tap-GEMM tile: ``bm`` pixels (64/128) by ``bn`` output
-    channels (32/64/128); 0 restores the automatic choice.  For tests and
+    channels (32/64/128), and its staging (0 = register ring, 2/3 = LDS-DMA
+    stages); 0 (-1 for staging) restores the automatic choice.  For tests and
     sweeps: call it between steps, never between sizing a statistics buffer
     (:func:`conv_fwd_stats_rows`) and the launch that fills it."""
-    hip_ext().conv_set_tiles(int(bm), int(bn))
+    hip_ext().conv_set_tiles(int(bm), int(bn), int(staging))
 
 
 def _conv_function():

@@ -17,8 +17,15 @@ current HIP stream through the ``_hip`` extension (csrc/gpu/comm.cpp):
 * no cross-stream events: an eager step pays one RCCL enqueue;
 * capturable: inside ``torch.cuda.graph`` the collective becomes a node of the
   same linear queue as the step's kernels;
-* a **dedicated** communicator (``dist.new_group``) so these calls never
-  interleave with c10d's own collectives on one communicator.
+* by default the process group's OWN communicator: a second one
+  (``dedicated=True``, a ``dist.new_group``) cost 25 % of the 1-GPU streaming
+  throughput with no collective in the timed loop at all (29.9k vs 39.4k
+  img/s, same box, profiles/r3/pg_ab.md) -- RCCL's per-communicator streams
+  and buffers, not CPU time.  Sharing is safe because both users serialise on
+  the compute stream: a blocking c10d collective first waits for the caller's
+  stream and the caller's stream then waits for it, so every rank sees one
+  order of operations on the communicator.  Keep c10d calls on that group
+  blocking (``async_op=False``) while a :class:`DeviceComm` uses it.
 
 With gloo (CPU rehearsals) or without the extension every method falls back
 to the equivalent ``torch.distributed`` call, so the same training code runs
@@ -51,7 +58,8 @@ def _rccl_path():
 
 
 class DeviceComm:
-    """Collectives on the caller's stream over a dedicated communicator.
+    """Collectives on the caller's stream over the process group's communicator (or, with
+    ``dedicated=True``, a communicator of its own).
 
     Collective to construct: every rank of ``group`` (default: the whole
     world) must create it, in the same order relative to other collectives.
@@ -61,7 +69,7 @@ class DeviceComm:
     ``force_native=False`` keeps the c10d path even on RCCL (comparison).
     """
 
-    def __init__(self, group=None, device: Optional[torch.device] = None, dedicated: bool = True,
+    def __init__(self, group=None, device: Optional[torch.device] = None, dedicated: bool = False,
                  force_native: Optional[bool] = None):
         if not (dist.is_available() and dist.is_initialized()):
             raise RuntimeError('DeviceComm needs an initialised process group')

@@ -9,6 +9,6 @@ import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_ste
 run() { echo "== $1"; shift; timeout -k 10 200 env BT_THREAD_REPORT=1 "$@" python bench.py $a --force-pg > gpurun_out/pgab.log 2>&1 || { tail -5 gpurun_out/pgab.log; return 1; }; show; }
 echo "== no pg"
 timeout -k 10 200 env BT_THREAD_REPORT=1 python bench.py $a > gpurun_out/pgab.log 2>&1 && show
-run "pg default" X=1
+run "pg default (shared DeviceComm)" X=1
 run "pg no DeviceComm" BT_NO_DEVICECOMM=1
-run "pg shared DeviceComm" BT_DEVICECOMM_SHARED=1
+run "pg dedicated DeviceComm" BT_DEVICECOMM_DEDICATED=1

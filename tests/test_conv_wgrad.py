@@ -208,22 +208,22 @@ def test_bn_backward_sums_from_dgrad_epilogue(dev, monkeypatch):
 
 @pytest.fixture
 def tiles(request):
-    bm, bn = request.param
-    ops.conv_set_tiles(bm, bn)
-    yield bm, bn
-    ops.conv_set_tiles(0, 0)
+    ops.conv_set_tiles(*request.param)
+    yield request.param
+    ops.conv_set_tiles(0, 0, -1)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('tiles', [(64, 64), (128, 64), (64, 128), (128, 128), (64, 32), (128, 32)],
-                         indirect=True, ids=lambda t: f'bm{t[0]}_bn{t[1]}')
+@pytest.mark.parametrize('tiles', [(bm, bn, st) for st in (0, 2, 3) for bm in (64, 128) for bn in (32, 64, 128)],
+                         indirect=True, ids=lambda t: f'bm{t[0]}_bn{t[1]}_st{t[2]}')
 def test_tap_gemm_tile_variants(dev, tiles):
-    """Every tile shape of the tap-gather GEMM (pixels x output channels)
-    against the fp32 reference: forward with statistics, data gradient, and
-    the data gradient with the BN-backward epilogue (Discriminator backward)."""
+    """Every tile shape of the tap-gather GEMM (pixels x output channels) and
+    staging (register ring, 2 or 3 LDS-DMA stages) against the fp32
+    reference: forward with statistics, data gradient, and the data gradient
+    with the BN-backward epilogue (Discriminator backward)."""
     import torch.nn.functional as F
     from blendtorch.models import Discriminator
-    bm, bn = tiles
+    bm, bn, _ = tiles
     cl = torch.channels_last
     g = torch.Generator(device=dev).manual_seed(bm + bn)
     for N, Cin, H, W, Cout in [(2, 64, 30, 40, 128), (1, 128, 8, 10, 256), (3, 32, 14, 18, 64)]:
@@ -248,7 +248,7 @@ def test_tap_gemm_tile_variants(dev, tiles):
     xin = torch.rand(4, 4, 96, 128, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
     a.bce_loss_bf16(xin, 1.0).backward()
     got = [p.grad.clone() for p in a.parameters()]
-    ops.conv_set_tiles(0, 0)
+    ops.conv_set_tiles(0, 0, 0)     # reference: default tiles, register staging
     a.zero_grad(set_to_none=True)
     a.bce_loss_bf16(xin, 1.0).backward()
     for (n, p), g0 in zip(a.named_parameters(), got):
