@@ -271,8 +271,12 @@ def main(argv=None):
         # and its peers (blendtorch/parallel/comm.py)
         if os.environ.get('BT_NO_DEVICECOMM') != '1':      # (diagnostic switch)
             from blendtorch.parallel import DeviceComm
-            comm = DeviceComm(device=device if args.backend == 'nccl' else None,
-                              dedicated=os.environ.get('BT_DEVICECOMM_DEDICATED') == '1')
+            # a communicator of its own for the training step's in-graph all-reduce
+            # (16 % step tax on the group's shared one); streaming alone has no
+            # per-step collective and a second communicator costs it 25 %
+            # (profiles/r3/pg_ab.md)
+            ded = os.environ.get('BT_DEVICECOMM_DEDICATED', '1' if args.consumer == 'disc' else '0') == '1'
+            comm = DeviceComm(device=device if args.backend == 'nccl' else None, dedicated=ded)
             allreduce['selfcheck'] = {k: (round(v, 3) if isinstance(v, float) else v)
                                       for k, v in comm.selfcheck().items()}
 

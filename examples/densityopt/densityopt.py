@@ -87,7 +87,7 @@ def run(args):
     rank, world, dev = parallel.init_distributed(backend=args.backend)
     if args.device == 'cpu':
         dev = torch.device('cpu')
-    comm = parallel.DeviceComm(device=dev if dev.type == 'cuda' else None) if world > 1 else None
+    comm = parallel.DeviceComm(device=dev if dev.type == 'cuda' else None, dedicated=True) if world > 1 else None
     if comm is not None and comm.backend == 'nccl':
         comm.selfcheck()
     B = args.batch

@@ -17,15 +17,18 @@ current HIP stream through the ``_hip`` extension (csrc/gpu/comm.cpp):
 * no cross-stream events: an eager step pays one RCCL enqueue;
 * capturable: inside ``torch.cuda.graph`` the collective becomes a node of the
   same linear queue as the step's kernels;
-* by default the process group's OWN communicator: a second one
-  (``dedicated=True``, a ``dist.new_group``) cost 25 % of the 1-GPU streaming
-  throughput with no collective in the timed loop at all (29.9k vs 39.4k
-  img/s, same box, profiles/r3/pg_ab.md) -- RCCL's per-communicator streams
-  and buffers, not CPU time.  Sharing is safe because both users serialise on
-  the compute stream: a blocking c10d collective first waits for the caller's
-  stream and the caller's stream then waits for it, so every rank sees one
-  order of operations on the communicator.  Keep c10d calls on that group
-  blocking (``async_op=False``) while a :class:`DeviceComm` uses it.
+* the communicator is the process group's own (default) or, with
+  ``dedicated=True``, one of its own (a ``dist.new_group``).  Measured on one
+  MI355X with a 1-rank group (profiles/r3/pg_ab.md): the graphed training
+  step's in-graph all-reduce costs 1.6 % on a dedicated communicator and 20 %
+  on the shared one -- so the training step (:class:`~.step.CapturedStep`,
+  densityopt) uses a dedicated one; streaming with no per-step collective
+  loses 25 % to a second communicator existing at all -- so loaders share.
+  Sharing is safe because both users serialise on the compute stream: a
+  blocking c10d collective first waits for the caller's stream and the
+  caller's stream then waits for it, so every rank sees one order of
+  operations on the communicator.  Keep c10d calls on that group blocking
+  (``async_op=False``) while a shared :class:`DeviceComm` uses it.
 
 With gloo (CPU rehearsals) or without the extension every method falls back
 to the equivalent ``torch.distributed`` call, so the same training code runs

@@ -128,7 +128,7 @@ class CapturedStep:
         if active and buckets:
             from .comm import DeviceComm
             from .grads import GradBuckets
-            self.comm = comm if comm is not None else DeviceComm(group)
+            self.comm = comm if comm is not None else DeviceComm(group, dedicated=True)
             self.grads = GradBuckets(model.parameters(), bucket_mb=bucket_mb)
             if hasattr(optimizer, 'set_grad_scale'):
                 optimizer.set_grad_scale(1.0 / self.comm.world)   # folded into the update kernel
