@@ -543,7 +543,9 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   constexpr int NBUF = (C4 || NST == 0) ? 2 : NST;
   static_assert(NST == 0 || NST == 2 || NST == 3, "staging: register ring, or 2-3 LDS-DMA stages");
   static_assert(NBUF * STG >= E_TILE + 4 * 2 * BN * 4, "epilogue does not fit the staging LDS");
-  __shared__ __attribute__((aligned(16))) char smem[NBUF * STG];
+  // the tile's row table after the staging space (not C4): {abase, vmask, obase, in range} per GEMM row
+  constexpr int RT_OFF = NBUF * STG, RT = C4 ? 0 : BM * 16;
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * STG + RT];
   float* red = reinterpret_cast<float*>(smem + E_TILE);   // [WGM][2][BN], after the epilogue tile
   const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
   constexpr int NTAPS = DGRAD ? 4 : 16;
@@ -556,37 +558,10 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   const int mt = w / NT, n0 = (w - mt * NT) * BN;
   const int m0 = mt * BM;
 
-  // this thread's 4 GEMM rows (staging A, and the epilogue stores): ar + 32j
+  // this thread's RJ GEMM rows (staging A, and the epilogue stores): ar + 32j
   const int ar = t >> 3, ac = t & 7;
   int rb[RJ], cb[RJ], base[RJ], obase[RJ];
   bool pin[RJ];
-  // (n, a, b) of row ar by division, the next rows 32 GEMM rows on by
-  // stepping (two integer divisions per row were a third of the kernel's VALU)
-  int gn, ga, gbb;
-  {
-    const int m = m0 + ar < p.M ? m0 + ar : 0;
-    gn = m / (p.GH * p.GW);
-    const int rem = m - gn * (p.GH * p.GW);
-    ga = rem / p.GW;
-    gbb = rem - ga * p.GW;
-  }
-#pragma unroll
-  for (int j = 0; j < RJ; ++j) {
-    const int m = m0 + ar + 32 * j;
-    if (j > 0) {
-      gbb += 32;
-      while (gbb >= p.GW) {
-        gbb -= p.GW;
-        if (++ga == p.GH) ga = 0, ++gn;
-      }
-    }
-    pin[j] = m < p.M;
-    const int mm = pin[j] ? m : 0;
-    rb[j] = DGRAD ? ga : 2 * ga - 1;
-    cb[j] = DGRAD ? gbb : 2 * gbb - 1;
-    base[j] = (gn * p.SH + rb[j]) * p.SW + cb[j];
-    obase[j] = DGRAD ? ((gn * p.OH + 2 * ga + ph) * p.OW + 2 * gbb + pw) * p.NOUT : mm * p.NOUT;
-  }
   // per row: byte offset of its tap-origin pixel (mod 2^32: border rows start
   // at -1, and only in-bounds taps are ever added to it) and a bitmask of the
   // taps that land inside the image -- the k-loop then costs one add and one
@@ -601,27 +576,77 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     hi = hi > TW ? TW : hi;
     return hi > lo ? (1u << hi) - (1u << lo) : 0u;
   };
-  uint32_t abase[RJ], vmask[RJ];
-#pragma unroll
-  for (int j = 0; j < RJ; ++j) {
-    abase[j] = uint32_t(base[j]) << (p.cshift + 1);
+  auto tap_mask = [&](int r0, int c0) -> uint32_t {
     uint32_t rows, cols;
     if (DGRAD) {   // 0 <= rb + ph - k < SH  <=>  rb + ph - SH < k <= rb + ph
-      rows = span(rb[j] + ph - p.SH + 1, rb[j] + ph + 1);
-      cols = span(cb[j] + pw - p.SW + 1, cb[j] + pw + 1);
+      rows = span(r0 + ph - p.SH + 1, r0 + ph + 1);
+      cols = span(c0 + pw - p.SW + 1, c0 + pw + 1);
     } else {       // 0 <= rb + k < SH
-      rows = span(-rb[j], p.SH - rb[j]);
-      cols = span(-cb[j], p.SW - cb[j]);
+      rows = span(-r0, p.SH - r0);
+      cols = span(-c0, p.SW - c0);
     }
-    uint32_t mk;
     if constexpr (TW == 4) {
       const uint32_t x = (rows | (rows << 3) | (rows << 6) | (rows << 9)) & 0x1111u;   // row k -> bit 4k
-      mk = (x * 0xFu) & (cols * 0x1111u);
+      return (x * 0xFu) & (cols * 0x1111u);
     } else {
       const uint32_t x = (rows | (rows << 1)) & 0x5u;                                   // row k -> bit 2k
-      mk = (x * 0x3u) & (cols * 0x5u);
+      return (x * 0x3u) & (cols * 0x5u);
     }
-    vmask[j] = pin[j] ? mk : 0u;
+  };
+  uint32_t abase[RJ], vmask[RJ];
+  if constexpr (!C4) {
+    // Row table: thread t < BM works out row m0 + t once (two divisions, the
+    // base offset, the tap mask, the output offset) and every thread reads
+    // the RJ rows it stages from LDS.  Each row was worked out by all 8 lanes
+    // that stage its chunks -- 8x the index math, most of the kernel's VALU.
+    int4* rt = reinterpret_cast<int4*>(smem + RT_OFF);
+    if (t < BM) {
+      const int m = m0 + t;
+      const bool in = m < p.M;
+      const int mm = in ? m : 0;
+      const int gn = mm / (p.GH * p.GW);
+      const int rem = mm - gn * (p.GH * p.GW);
+      const int ga = rem / p.GW, gbb = rem - ga * p.GW;
+      const int r0 = DGRAD ? ga : 2 * ga - 1, c0 = DGRAD ? gbb : 2 * gbb - 1;
+      const uint32_t ab = uint32_t((gn * p.SH + r0) * p.SW + c0) << (p.cshift + 1);
+      const int ob = DGRAD ? ((gn * p.OH + 2 * ga + ph) * p.OW + 2 * gbb + pw) * p.NOUT : mm * p.NOUT;
+      rt[t] = make_int4(int(ab), int(in ? tap_mask(r0, c0) : 0u), ob, in ? 1 : 0);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RJ; ++j) {
+      const int4 r = rt[ar + 32 * j];
+      abase[j] = uint32_t(r.x), vmask[j] = uint32_t(r.y), obase[j] = r.z, pin[j] = r.w != 0;
+    }
+  } else {
+    // (n, a, b) of row ar by division, the next rows 32 GEMM rows on by stepping
+    int gn, ga, gbb;
+    {
+      const int m = m0 + ar < p.M ? m0 + ar : 0;
+      gn = m / (p.GH * p.GW);
+      const int rem = m - gn * (p.GH * p.GW);
+      ga = rem / p.GW;
+      gbb = rem - ga * p.GW;
+    }
+#pragma unroll
+    for (int j = 0; j < RJ; ++j) {
+      const int m = m0 + ar + 32 * j;
+      if (j > 0) {
+        gbb += 32;
+        while (gbb >= p.GW) {
+          gbb -= p.GW;
+          if (++ga == p.GH) ga = 0, ++gn;
+        }
+      }
+      pin[j] = m < p.M;
+      const int mm = pin[j] ? m : 0;
+      rb[j] = 2 * ga - 1;
+      cb[j] = 2 * gbb - 1;
+      base[j] = (gn * p.SH + rb[j]) * p.SW + cb[j];
+      obase[j] = mm * p.NOUT;
+      abase[j] = uint32_t(base[j]) << (p.cshift + 1);
+      vmask[j] = pin[j] ? tap_mask(rb[j], cb[j]) : 0u;
+    }
   }
   const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(p.src, int64_t(p.N) * p.SH * p.SW * p.C * 2);
   const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(p.w, int64_t(p.NOUT) * 16 * p.C * 2);
@@ -835,7 +860,14 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   if constexpr (BN == 64) {   // the staging rows ar + 32 j
 #pragma unroll
     for (int j = 0; j < NJ; ++j) eob[j] = obase[j], epin[j] = pin[j];
-  } else {                     // rows t / CPR + RPP j: divide once, then step
+  } else if constexpr (!C4) {  // rows t / CPR + RPP j: from the row table
+    const int4* rt = reinterpret_cast<const int4*>(smem + RT_OFF);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int4 r = rt[t / CPR + RPP * j];
+      eob[j] = r.z, epin[j] = r.w != 0;
+    }
+  } else {                     // (C4, forward) rows t / CPR + RPP j: divide once, then step
     const int m_first = m0 + t / CPR;
     int en = 0, ea = 0, eb = 0;
     {
@@ -856,7 +888,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
       }
       const int m = m_first + RPP * j;
       epin[j] = m < p.M;
-      eob[j] = DGRAD ? ((en * p.OH + 2 * ea + ph) * p.OW + 2 * eb + pw) * p.NOUT : m * p.NOUT;
+      eob[j] = m * p.NOUT;
     }
   }
   // BN-backward fusion (below): issue the BN input loads now, so their
