@@ -334,10 +334,14 @@ def main(argv=None):
         # fused Adam: one multi-tensor kernel for the whole update (0.95 -> 0.84 ms graphed step,
         # profiles/consumer_step.md); capturable keeps its step counters on the GPU for the graph
         if args.optim == 'gfx950':
-            # ops.FusedAdam: one 1-lane schedule kernel + one update kernel over all
-            # parameters (device step counter: capturable)
+            # ops.FusedAdam: ONE update kernel over all parameters (device step
+            # counter: capturable), which also rewrites the bf16 conv weights and
+            # their data-gradient transposes the next forward reads (no per-step
+            # cast / transpose launches) and clears the gradients it consumed
             from blendtorch import ops
             opt = ops.FusedAdam(model.parameters(), lr=2e-4)
+            if args.cast == 'fused':
+                model.use_optimizer_shadows(opt)
         else:
             opt = torch.optim.Adam(model.parameters(), lr=2e-4, capturable=use_graph, fused=True)
         crit = torch.nn.BCELoss()

@@ -511,6 +511,7 @@ struct TapGemm {
   int GH = 0, GW = 0, M = 0;       // GEMM rows: m = (n * GH + a) * GW + b
   int NOUT = 0, OH = 0, OW = 0;    // dst [N][OH][OW][NOUT]
   int wc = 0;                      // C4 mode: weight input channels (3 or 4)
+  int acc_r = 0;                   // forward: > 0 = stats points at a BnAcc accumulator (fp64 [acc_r][2][NOUT])
   BnBwdFuse bn;                    // data gradient only: BN backward statistics in the epilogue (bn.part nullable)
 };
 
@@ -1021,8 +1022,13 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
       float v = 0.f;
 #pragma unroll
       for (int w4 = 0; w4 < 4; ++w4) v += red[(w4 * 2 + which) * BN + c];
-      // channel-major [2][NOUT][rows], row = (pixel tile, parity class)
-      p.bn.part[(which * p.NOUT + n0 + c) * p.bn.rows + mt * int(gridDim.y) + int(blockIdx.y)] = v;
+      // channel-major [2][NOUT][rows], row = (pixel tile, parity class); or
+      // added into replica row % R of an accumulator [R][2][NOUT] (bn_bwd_apply_acc folds it)
+      const int row = mt * int(gridDim.y) + int(blockIdx.y);
+      if (p.bn.acc_r > 0)
+        unsafeAtomicAdd(reinterpret_cast<double*>(p.bn.part) + ((row % p.bn.acc_r) * 2 + which) * p.NOUT + n0 + c,
+                        double(v));
+      else p.bn.part[(which * p.NOUT + n0 + c) * p.bn.rows + row] = v;
     }
   }
   if (!DGRAD && p.stats && t < 2 * BN) {
@@ -1030,8 +1036,11 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     float v = 0.f;
 #pragma unroll
     for (int g = 0; g < WGM; ++g) v += red[(g * 2 + which) * BN + c];
-    // channel-major [2][NOUT][tiles], the layout bn_finalize_rows folds
-    p.stats[(which * p.NOUT + n0 + c) * ((p.M + BM - 1) / BM) + mt] = v;
+    // channel-major [2][NOUT][tiles], the layout bn_finalize_rows folds; or
+    // added into replica mt % R of an accumulator [R][2][NOUT] (bn_apply_acc folds it)
+    if (p.acc_r > 0)
+      unsafeAtomicAdd(reinterpret_cast<double*>(p.stats) + ((mt % p.acc_r) * 2 + which) * p.NOUT + n0 + c, double(v));
+    else p.stats[(which * p.NOUT + n0 + c) * ((p.M + BM - 1) / BM) + mt] = v;
   }
 }
 
@@ -1214,6 +1223,8 @@ hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream) {
   g.GH = p.Ho, g.GW = p.Wo, g.M = int(p.M);
   g.NOUT = p.Cout, g.OH = p.Ho, g.OW = p.Wo;
   g.wc = p.Cin == 4 ? (p.w_channels > 0 ? p.w_channels : 4) : p.Cin;
+  g.acc_r = p.stats ? p.acc_r : 0;
+  if (g.acc_r < 0 || g.acc_r > 64) return hipErrorInvalidValue;
   if (p.Cin == 4 && g.wc != 3 && g.wc != 4) return hipErrorInvalidValue;
   launch_tap_gemm<false>(g, 1, stream);
   return hipGetLastError();
@@ -1260,8 +1271,8 @@ hipError_t conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int 
   g.GH = Ho, g.GW = Wo, g.M = N * Ho * Wo;   // one parity class: every (a, b)
   g.NOUT = Cin, g.OH = H, g.OW = W;
   if (bn && bn->part) {
-    if (!bn->x || !bn->mean || !bn->invstd || !bn->w || !bn->b || bn->rows != conv_dgrad_bn_rows(N, H, W, Cin) ||
-        (reinterpret_cast<uintptr_t>(bn->x) & 15))
+    if (!bn->x || !bn->mean || !bn->invstd || !bn->w || !bn->b || bn->acc_r < 0 || bn->acc_r > 64 ||
+        (bn->acc_r == 0 && bn->rows != conv_dgrad_bn_rows(N, H, W, Cin)) || (reinterpret_cast<uintptr_t>(bn->x) & 15))
       return hipErrorInvalidValue;
     g.bn = *bn;
   }

@@ -13,6 +13,8 @@
 // examples/densityopt/densityopt.py:139-190 (conv4x4 -> sigmoid, BCELoss).
 #include <hip/hip_runtime.h>
 
+#include <hip/amd_detail/amd_hip_unsafe_atomics.h>
+
 #include <cstdint>
 
 #include "kernels.h"
@@ -28,6 +30,8 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ int wstart(int i, int in, int out) { return (i * in) / out; }
 __device__ __forceinline__ int wend(int i, int in, int out) { return ((i + 1) * in + out - 1) / out; }
 __device__ __forceinline__ float bf(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
+
+__device__ void head_loss_wave(const HeadParams& p, bool write_through);
 
 // one block per (pooling cell, image): pooled values of the cell and the
 // cell's share of the image's logit.  Lanes own 8 channels (one 16-byte load)
@@ -84,20 +88,42 @@ __global__ __launch_bounds__(kHeadThreads) void head_fwd_kernel(HeadParams p) {
   for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = part;
   __syncthreads();
+  if (!p.ticket) {
+    if (threadIdx.x == 0) {
+      float v = 0.f;
+      for (int k = 0; k < kHeadThreads / 64; ++k) v += red[k];
+      p.partial[n * p.OH * p.OW + cell] = v;
+    }
+    return;
+  }
+  // one-launch form: lane 0 publishes the block's partial write-through,
+  // waits for it, then takes a ticket; the block that takes the last ticket
+  // computes the loss in its first wave, reading the partials write-through
+  // (agent-scope relaxed atomics: sc1 stores and loads -- no fences)
+  if (threadIdx.x >= 64) return;
+  uint32_t last = 0;
   if (threadIdx.x == 0) {
     float v = 0.f;
     for (int k = 0; k < kHeadThreads / 64; ++k) v += red[k];
-    p.partial[n * p.OH * p.OW + cell] = v;
+    __hip_atomic_store(p.partial + n * p.OH * p.OW + cell, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t tk = __hip_atomic_fetch_add(p.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = tk == gridDim.x * gridDim.y - 1;
+    if (last) __hip_atomic_store(p.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  if (!__shfl(last, 0)) return;
+  head_loss_wave(p, true);
 }
 
 // one wave: logits, sigmoid, mean BCE, and dlogit/g for the backward
-__global__ __launch_bounds__(64) void head_loss_kernel(HeadParams p) {
+__device__ void head_loss_wave(const HeadParams& p, bool wt) {
   const int cells = p.OH * p.OW;
   float total = 0.f;
   for (int n = int(threadIdx.x); n < p.N; n += 64) {
     float logit = 0.f;
-    for (int k = 0; k < cells; ++k) logit += p.partial[n * cells + k];
+    for (int k = 0; k < cells; ++k)
+      logit += wt ? __hip_atomic_load(p.partial + n * cells + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                  : p.partial[n * cells + k];
     const float y = p.target ? p.target[n] : p.target_value;
     const float pr = 1.f / (1.f + expf(-logit));
     const float lp = fmaxf(logf(pr), -100.f), lq = fmaxf(logf(1.f - pr), -100.f);
@@ -109,14 +135,49 @@ __global__ __launch_bounds__(64) void head_loss_kernel(HeadParams p) {
   if (threadIdx.x == 0) p.loss[0] = total / float(p.N);
 }
 
-// dz: 8 channels of one pixel per lane (one 16-byte store)
-__global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p) {
+__global__ __launch_bounds__(64) void head_loss_kernel(HeadParams p) { head_loss_wave(p, false); }
+
+// Backward in ONE launch: blocks [0, nbwd) write dz (8 channels of one pixel
+// per lane, one 16-byte store), blocks [nbwd, ...) the weight gradient.
+// With p.bn_acc the dz blocks also sum the producing BatchNorm+LeakyReLU
+// backward's gz and gz * xhat per channel: a lane keeps one channel group
+// over the whole grid-stride loop (the stride is a multiple of C / 8), the
+// block folds its lanes through LDS and adds its 2 C sums into replica
+// blockIdx % R of the fp64 accumulator.
+__global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p, int nbwd) {
+  const int t = int(threadIdx.x);
+  const float g = p.gscale[0];
+  if (int(blockIdx.x) >= nbwd) {   // weight gradient
+    const int cells = p.OH * p.OW;
+    const int total = p.C * cells;
+    const int nw = int(gridDim.x) - nbwd;
+    for (int e = (int(blockIdx.x) - nbwd) * kHeadThreads + t; e < total; e += nw * kHeadThreads) {
+      const int c = e % p.C, cell = e / p.C;
+      float s = 0.f;
+      for (int n = 0; n < p.N; ++n) s += p.dlogit[n] * p.pooled[(int64_t(n) * cells + cell) * p.C + c];
+      const int i = cell / p.OW, j = cell - i * p.OW;
+      p.dw[c * p.ws_c + i * p.ws_i + j * p.ws_j] = g * s;
+    }
+    return;
+  }
   // 32-bit index math (the host checks N*H*W*C/8 < 2^31): 64-bit division
   // and modulo made this an ALU-bound kernel
   const int groups = p.C / 8;
   const int total = p.N * p.H * p.W * groups;
-  const float g = p.gscale[0];
-  for (int e = int(blockIdx.x) * kHeadThreads + int(threadIdx.x); e < total; e += int(gridDim.x) * kHeadThreads) {
+  const bool bnf = p.bn_acc != nullptr;
+  const int c0l = (t % groups) * 8;   // this lane's channel group (fixed: the stride is a multiple of groups)
+  float is[8], nm[8], bw[8], bb[8], bs[8], bq[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    bs[q] = bq[q] = 0.f;
+    if (bnf) {
+      is[q] = p.bn_invstd[c0l + q];
+      nm[q] = -p.bn_mean[c0l + q] * is[q];
+      bw[q] = p.bn_w[c0l + q];
+      bb[q] = p.bn_b[c0l + q];
+    }
+  }
+  for (int e = int(blockIdx.x) * kHeadThreads + t; e < total; e += nbwd * kHeadThreads) {
     int r = e / groups;
     const int c0 = (e - r * groups) * 8;
     const int pix = r;
@@ -125,6 +186,8 @@ __global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p) {
     const int n = r / p.H;
     const int h = r - n * p.H;
     const float d = g * p.dlogit[n];
+    uint4 xv = make_uint4(0, 0, 0, 0);
+    if (bnf) xv = *reinterpret_cast<const uint4*>(p.bn_x + (int64_t(pix) * p.C + c0));
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const int i0 = (h * p.OH) / p.H, i1 = ((h + 1) * p.OH + p.H - 1) / p.H;
     const int j0 = (w * p.OW) / p.W, j1 = ((w + 1) * p.OW + p.W - 1) / p.W;
@@ -147,19 +210,33 @@ __global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p) {
     }
     *reinterpret_cast<uint4*>(p.dz + ((int64_t(n * p.H + h) * p.W + w) * p.C + c0)) =
         make_uint4(packed[0], packed[1], packed[2], packed[3]);
+    if (bnf) {   // the BN backward reads the stored (bf16) dz as its gy
+      const uint32_t xw[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const uint32_t gb = q & 1 ? packed[q >> 1] & 0xFFFF0000u : packed[q >> 1] << 16;
+        const uint32_t xb = q & 1 ? xw[q >> 1] & 0xFFFF0000u : xw[q >> 1] << 16;
+        const float xh = fmaf(__uint_as_float(xb), is[q], nm[q]);
+        const float gy = __uint_as_float(gb);
+        const float gz = fmaf(xh, bw[q], bb[q]) > 0.f ? gy : gy * p.bn_slope;
+        bs[q] += gz;
+        bq[q] += gz * xh;
+      }
+    }
   }
-}
-
-__global__ __launch_bounds__(kHeadThreads) void head_wgrad_kernel(HeadParams p) {
-  const int cells = p.OH * p.OW;
-  const int total = p.C * cells;
-  const float g = p.gscale[0];
-  for (int e = int(blockIdx.x) * kHeadThreads + int(threadIdx.x); e < total; e += int(gridDim.x) * kHeadThreads) {
-    const int c = e % p.C, cell = e / p.C;
-    float s = 0.f;
-    for (int n = 0; n < p.N; ++n) s += p.dlogit[n] * p.pooled[(int64_t(n) * cells + cell) * p.C + c];
-    const int i = cell / p.OW, j = cell - i * p.OW;
-    p.dw[c * p.ws_c + i * p.ws_i + j * p.ws_j] = g * s;
+  if (!bnf) return;
+  // fold the lanes of each channel group (lanes t, t + groups, ...) in LDS
+  __shared__ float red[2][kHeadThreads * 8];   // [PL][C] per sum, PL * C = 8 * 256
+  const int PL = kHeadThreads / groups;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) red[0][(t / groups) * p.C + c0l + q] = bs[q], red[1][(t / groups) * p.C + c0l + q] = bq[q];
+  __syncthreads();
+  double* row = p.bn_acc + int64_t(int(blockIdx.x) % p.bn_acc_r) * 2 * p.C;
+  for (int c = t; c < p.C; c += kHeadThreads) {
+    float s0 = 0.f, s1 = 0.f;
+    for (int l = 0; l < PL; ++l) s0 += red[0][l * p.C + c], s1 += red[1][l * p.C + c];
+    unsafeAtomicAdd(row + c, double(s0));
+    unsafeAtomicAdd(row + p.C + c, double(s1));
   }
 }
 
@@ -170,7 +247,7 @@ hipError_t head_forward(const HeadParams& p, hipStream_t stream) {
       !p.partial || !p.loss || !p.dlogit)
     return hipErrorInvalidValue;
   head_fwd_kernel<<<dim3(unsigned(p.OH * p.OW), unsigned(p.N)), kHeadThreads, 0, stream>>>(p);
-  head_loss_kernel<<<1, 64, 0, stream>>>(p);
+  if (!p.ticket) head_loss_kernel<<<1, 64, 0, stream>>>(p);
   return hipGetLastError();
 }
 
@@ -179,10 +256,17 @@ hipError_t head_backward(const HeadParams& p, hipStream_t stream) {
   if (reinterpret_cast<uintptr_t>(p.dz) & 15) return hipErrorInvalidValue;
   const int64_t total = int64_t(p.N) * p.H * p.W * (p.C / 8);
   if (total >= (int64_t(1) << 31) - int64_t(kHeadThreads) * 4096) return hipErrorInvalidValue;
+  const int groups = p.C / 8;
+  if (p.bn_acc) {   // lanes keep one channel group: the block stride must be a multiple of C / 8
+    if (groups > kHeadThreads || kHeadThreads % groups || p.bn_acc_r <= 0 || !p.bn_x || !p.bn_mean ||
+        !p.bn_invstd || !p.bn_w || !p.bn_b || (reinterpret_cast<uintptr_t>(p.bn_x) & 15))
+      return hipErrorInvalidValue;
+  }
   const int64_t blocks = (total + kHeadThreads - 1) / kHeadThreads;
-  head_bwd_kernel<<<unsigned(blocks < 4096 ? blocks : 4096), kHeadThreads, 0, stream>>>(p);
+  const int nbwd = int(blocks < 2048 ? blocks : 2048);
   const int wtotal = p.C * p.OH * p.OW;
-  head_wgrad_kernel<<<(wtotal + kHeadThreads - 1) / kHeadThreads, kHeadThreads, 0, stream>>>(p);
+  const int nw = (wtotal + kHeadThreads - 1) / kHeadThreads;
+  head_bwd_kernel<<<unsigned(nbwd + nw), kHeadThreads, 0, stream>>>(p, nbwd);
   return hipGetLastError();
 }
 

@@ -207,6 +207,33 @@ hipError_t bn_bwd_apply(const void* x, const void* gy, void* gx, int64_t M, int 
                         const float* invstd, const float* w, const float* b, const float* dw, const float* db,
                         float slope, hipStream_t stream);
 
+// Accumulator form of the statistics hand-off.  The producer -- conv_fwd's
+// or conv_dgrad's epilogue, or bn_bwd_reduce -- adds each tile's channel sums
+// into acc [R][2][C] with fp64 atomics (replica = tile % R, R =
+// bn_acc_replicas(C); fp64 so the sums do not depend on the adders' order
+// at fp32 precision), and ONE finalize block folds the R replicas, writes the
+// finalized outputs (forward: mean, invstd, running stats,
+// num_batches_tracked; backward: dw, db) and clears acc for the next
+// producer.  acc must be all-zero when the producer runs: allocate it zeroed
+// (bn_acc_elems(C) doubles) and let the finalize keep it that way.
+int bn_acc_replicas(int C);
+int64_t bn_acc_elems(int C);
+struct BnAcc {
+  double* acc = nullptr;
+  int R = 0;
+};
+hipError_t bn_apply_acc(const void* x, void* y, int64_t M, int C, int dtype, BnAcc acc, float eps, float momentum,
+                        float* mean, float* invstd, float* running_mean, float* running_var,
+                        int64_t* num_batches_tracked, const float* w, const float* b, float slope,
+                        hipStream_t stream);
+hipError_t bn_bwd_apply_acc(const void* x, const void* gy, void* gx, int64_t M, int C, int dtype, BnAcc acc,
+                            const float* mean, const float* invstd, const float* w, const float* b, float* dw,
+                            float* db, float slope, hipStream_t stream);
+// bn_bwd_reduce adding into an accumulator (bn_bwd_apply_acc consumes it)
+hipError_t bn_bwd_reduce_acc(const void* x, const void* gy, int64_t M, int C, int dtype, const float* mean,
+                             const float* invstd, const float* w, const float* b, float slope, BnAcc acc,
+                             hipStream_t stream);
+
 // Multi-tensor dtype cast in ONE launch (the consumer step's weight casts
 // for bf16 compute and the cast of the bf16 weight gradients back to fp32 --
 // a dozen tiny launches otherwise).  mode CAST_F32_TO_BF16 (RNE) or
@@ -252,6 +279,24 @@ struct AdamParams {
   int maximize = 0;
   float beta1 = 0.9f, beta2 = 0.999f, eps = 1e-8f, weight_decay = 0.f;
   const float* sched = nullptr;   // device [5], written by adam_schedule
+  // One-launch form (no adam_schedule): with step != nullptr every block
+  // works the schedule out itself from step / hp / gate (one lane, shared
+  // through LDS), and the block that takes the last ticket (*ticket, zero
+  // between launches) stores the advanced counter.  sched is then unused.
+  float* step = nullptr;
+  const float* hp = nullptr;
+  const float* gate = nullptr;
+  uint32_t* ticket = nullptr;
+  // zero_grad: clear each gradient after reading it (also when a gate closes
+  // the step), so a training loop with persistent gradient buffers needs no
+  // separate zero-fill launch before its next backward.  fp32 grads only.
+  int zero_grad = 0;
+  // shadow_t[k] (nullable): a bf16 copy of the new weight transposed from
+  // channels-last [tcout][4][4][tcin] to [tcin][4][4][tcout] (a 4x4
+  // convolution's data-gradient operand, conv_weight_t).
+  uint16_t* shadow_t[kMaxAdam] = {};
+  int tcout[kMaxAdam] = {};
+  int tcin[kMaxAdam] = {};
 };
 // Weight gradient of a 4x4 / stride-2 / pad-1 convolution over channels-last
 // bf16 activations on the MFMA units (conv.hip): x [N][H][W][Cin],
@@ -289,6 +334,7 @@ struct ConvFwdParams {
   int N = 0, H = 0, W = 0, Cin = 0, Ho = 0, Wo = 0, Cout = 0;
   int64_t M = 0;
   int w_channels = 0;   // Cin == 4 (first layer): 3 = an RGB weight [Cout][4][4][3], input channel 3 ignored
+  int acc_r = 0;        // > 0: stats points at a bn_apply_acc accumulator (fp64 [acc_r][2][Cout], atomic adds)
 };
 // Cin a power of two >= 8, or Cin == 4 (first layer, RGBA-decoded frames); Cout % 32 == 0.
 bool conv_fwd_supported(int Cin, int Cout);
@@ -333,6 +379,7 @@ struct BnBwdFuse {
   float slope = 0.f;
   float* part = nullptr;
   int rows = 0;
+  int acc_r = 0;   // > 0: part points at a bn_bwd_apply_acc accumulator (fp64 [acc_r][2][Cin], atomic adds), rows unused
 };
 int64_t conv_dgrad_bn_rows(int N, int H, int W, int Cin);
 hipError_t conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int N, int H, int W, int Cin, int Cout,
@@ -365,6 +412,21 @@ struct HeadParams {
   const float* gscale = nullptr;
   uint16_t* dz = nullptr;
   float* dw = nullptr;
+  // forward: with ticket (a zeroed word) the pooling blocks hand their
+  // partial logits to the block that finishes last, which computes the loss
+  // (one launch instead of two)
+  uint32_t* ticket = nullptr;
+  // backward: bn_acc (nullable) = the BnAcc accumulator of the BatchNorm +
+  // LeakyReLU that produced z: the dz pass also sums that backward's gz and
+  // gz * xhat (x = the BN's saved input) -- no bn_bwd_reduce launch
+  const uint16_t* bn_x = nullptr;
+  const float* bn_mean = nullptr;
+  const float* bn_invstd = nullptr;
+  const float* bn_w = nullptr;
+  const float* bn_b = nullptr;
+  float bn_slope = 0.f;
+  double* bn_acc = nullptr;
+  int bn_acc_r = 0;
 };
 hipError_t head_forward(const HeadParams& p, hipStream_t stream);
 hipError_t head_backward(const HeadParams& p, hipStream_t stream);

@@ -906,661 +906,5 @@ hipError_t project(const float* pts, int64_t N, const float* PV, const float* V,
   return hipGetLastError();
 }
 
-// ---------------------------------------------------------------------------
-// Adaptive average pooling, NHWC.  The pooled maps are small (the DCGAN
-// consumer pools 8 x 30 x 40 x 256 bf16 down to 4 x 4), so the kernels are
-// shaped for parallelism, not bandwidth: forward = one lane per output
-// element, lanes of a wave walk adjacent channels (every window load is one
-// coalesced 128/256-byte row segment); backward = one lane per input element
-// gathering the (at most a few) output cells whose window covers it -- no
-// atomics, every gradient written once.
-
-template <int DT>
-__device__ __forceinline__ float load_act(const void* p, int64_t i) {
-  if constexpr (DT == OUT_BF16)
-    return __uint_as_float(uint32_t(reinterpret_cast<const uint16_t*>(p)[i]) << 16);
-  else
-    return reinterpret_cast<const float*>(p)[i];
-}
-
-template <int DT>
-__device__ __forceinline__ void store_act(void* p, int64_t i, float v) {
-  if constexpr (DT == OUT_BF16)
-    reinterpret_cast<uint16_t*>(p)[i] = f2bf(v);
-  else
-    reinterpret_cast<float*>(p)[i] = v;
-}
-
-__device__ __forceinline__ int win_start(int i, int in, int out) { return int((int64_t(i) * in) / out); }
-__device__ __forceinline__ int win_end(int i, int in, int out) { return int((int64_t(i + 1) * in + out - 1) / out); }
-
-template <int DT>
-__global__ __launch_bounds__(kBlock) void avgpool_fwd_kernel(const void* __restrict__ x, void* __restrict__ y, int N,
-                                                             int H, int W, int C, int OH, int OW) {
-  const int64_t total = int64_t(N) * OH * OW * C;
-  for (int64_t o = int64_t(blockIdx.x) * kBlock + threadIdx.x; o < total; o += int64_t(gridDim.x) * kBlock) {
-    const int c = int(o % C);
-    int64_t r = o / C;
-    const int j = int(r % OW);
-    r /= OW;
-    const int i = int(r % OH);
-    const int n = int(r / OH);
-    const int h0 = win_start(i, H, OH), h1 = win_end(i, H, OH);
-    const int w0 = win_start(j, W, OW), w1 = win_end(j, W, OW);
-    float acc = 0.f;
-    for (int h = h0; h < h1; ++h) {
-      const int64_t row = ((int64_t(n) * H + h) * W) * C + c;
-#pragma unroll 4
-      for (int w = w0; w < w1; ++w) acc += load_act<DT>(x, row + int64_t(w) * C);
-    }
-    store_act<DT>(y, o, acc / float((h1 - h0) * (w1 - w0)));
-  }
-}
-
-template <int DT>
-__global__ __launch_bounds__(kBlock) void avgpool_bwd_kernel(const void* __restrict__ gy, void* __restrict__ gx, int N,
-                                                             int H, int W, int C, int OH, int OW) {
-  const int64_t total = int64_t(N) * H * W * C;
-  for (int64_t e = int64_t(blockIdx.x) * kBlock + threadIdx.x; e < total; e += int64_t(gridDim.x) * kBlock) {
-    const int c = int(e % C);
-    int64_t r = e / C;
-    const int w = int(r % W);
-    r /= W;
-    const int h = int(r % H);
-    const int n = int(r / H);
-    // output rows whose window covers h: floor(h*OH/H) .. ceil((h+1)*OH/H)-1
-    const int i0 = int((int64_t(h) * OH) / H), i1 = int((int64_t(h + 1) * OH + H - 1) / H);
-    const int j0 = int((int64_t(w) * OW) / W), j1 = int((int64_t(w + 1) * OW + W - 1) / W);
-    float acc = 0.f;
-    for (int i = i0; i < i1 && i < OH; ++i) {
-      const int hs = win_start(i, H, OH), he = win_end(i, H, OH);
-      if (h < hs || h >= he) continue;
-      for (int j = j0; j < j1 && j < OW; ++j) {
-        const int ws = win_start(j, W, OW), we = win_end(j, W, OW);
-        if (w < ws || w >= we) continue;
-        acc += load_act<DT>(gy, ((int64_t(n) * OH + i) * OW + j) * C + c) / float((he - hs) * (we - ws));
-      }
-    }
-    store_act<DT>(gx, e, acc);
-  }
-}
-
-namespace {
-int pool_grid(int64_t total) {
-  const int64_t blocks = (total + kBlock - 1) / kBlock;
-  return int(blocks < 8192 ? (blocks < 1 ? 1 : blocks) : 8192);
-}
-}  // namespace
-
-hipError_t adaptive_avgpool_nhwc(const void* x, void* y, int N, int H, int W, int C, int OH, int OW, int dtype,
-                                 hipStream_t stream) {
-  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || OH <= 0 || OW <= 0) return hipErrorInvalidValue;
-  const int grid = pool_grid(int64_t(N) * OH * OW * C);
-  if (dtype == OUT_BF16)
-    avgpool_fwd_kernel<OUT_BF16><<<grid, kBlock, 0, stream>>>(x, y, N, H, W, C, OH, OW);
-  else if (dtype == OUT_F32)
-    avgpool_fwd_kernel<OUT_F32><<<grid, kBlock, 0, stream>>>(x, y, N, H, W, C, OH, OW);
-  else
-    return hipErrorInvalidValue;
-  return hipGetLastError();
-}
-
-hipError_t adaptive_avgpool_nhwc_bwd(const void* gy, void* gx, int N, int H, int W, int C, int OH, int OW, int dtype,
-                                     hipStream_t stream) {
-  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || OH <= 0 || OW <= 0) return hipErrorInvalidValue;
-  const int grid = pool_grid(int64_t(N) * H * W * C);
-  if (dtype == OUT_BF16)
-    avgpool_bwd_kernel<OUT_BF16><<<grid, kBlock, 0, stream>>>(gy, gx, N, H, W, C, OH, OW);
-  else if (dtype == OUT_F32)
-    avgpool_bwd_kernel<OUT_F32><<<grid, kBlock, 0, stream>>>(gy, gx, N, H, W, C, OH, OW);
-  else
-    return hipErrorInvalidValue;
-  return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
-// Training-mode BatchNorm2d + LeakyReLU, channels-last.  The consumer's
-// BN -> LeakyReLU pairs were 7 MIOpen/PyTorch kernels per layer and step
-// (mean/variance, final, normalise, leaky; and the same backwards), each a
-// full pass over the activation.  Here: forward = one statistics pass + one
-// normalise-and-activate pass; backward = one reduction pass + one gradient
-// pass, with the activation's derivative recomputed from x (z > 0 <=> y > 0
-// for a positive slope), so nothing but x is kept for backward.
-//
-// Reductions: a lane owns V = 16 B of channels of a row (8 bf16 / 4 fp32),
-// the G = C / V lanes of one row read it as one contiguous segment and
-// R = 256 / G rows are in flight per block; per-block partial sums go through
-// LDS to a [blocks, 2C] scratch that one lane per channel folds in fp64.
-
-constexpr int kBnMaxBlocks = 1024;
-
-template <int DT>
-struct BnVec {
-  static constexpr int V = DT == OUT_BF16 ? 8 : 4;
-  static constexpr int ES = DT == OUT_BF16 ? 2 : 4;
-};
-
-template <int DT>
-__device__ __forceinline__ void bn_load(const void* p, int64_t e, float (&v)[BnVec<DT>::V]) {
-  const uint4 raw = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(p) + e * BnVec<DT>::ES);
-  const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
-  if constexpr (DT == OUT_BF16) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      v[2 * i] = __uint_as_float(w[i] << 16);
-      v[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = __uint_as_float(w[i]);
-  }
-}
-
-template <int DT>
-__device__ __forceinline__ void bn_store(void* p, int64_t e, const float (&v)[BnVec<DT>::V]) {
-  uint4 raw;
-  if constexpr (DT == OUT_BF16) {
-    raw.x = uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16);
-    raw.y = uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16);
-    raw.z = uint32_t(f2bf(v[4])) | (uint32_t(f2bf(v[5])) << 16);
-    raw.w = uint32_t(f2bf(v[6])) | (uint32_t(f2bf(v[7])) << 16);
-  } else {
-    raw = make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3]));
-  }
-  *reinterpret_cast<uint4*>(reinterpret_cast<char*>(p) + e * BnVec<DT>::ES) = raw;
-}
-
-// BWD = false: sums of x and x^2.  BWD = true: sums of gz and gz * xhat.
-template <int DT, bool BWD>
-__global__ __launch_bounds__(kBlock) void bn_reduce_kernel(const void* __restrict__ x, const void* __restrict__ gy,
-                                                           int64_t M, int C, int64_t rows_per_block,
-                                                           const float* __restrict__ mean,
-                                                           const float* __restrict__ invstd,
-                                                           const float* __restrict__ w, const float* __restrict__ b,
-                                                           float slope, float* __restrict__ partial) {
-  constexpr int V = BnVec<DT>::V;
-  // partials laid out [V][kBlock + 1]: lane t's V values land in V different
-  // rows at column t, so the write is bank-conflict free (a [row][C] layout
-  // put the lanes' 8-float runs on the same banks)
-  constexpr int LS = kBlock + 1;
-  __shared__ float ls[V * LS], lq[V * LS];
-  const int G = C / V, R = kBlock / G;
-  const int g = int(threadIdx.x) % G, r0 = int(threadIdx.x) / G;
-  const int c0 = g * V;
-  float nm[V], is[V], ww[V], bb[V];   // xhat = v * is + nm, as bn_apply_kernel computes it
-  if constexpr (BWD) {
-#pragma unroll
-    for (int i = 0; i < V; ++i)
-      is[i] = invstd[c0 + i], nm[i] = -mean[c0 + i] * is[i], ww[i] = w[c0 + i], bb[i] = b[c0 + i];
-  }
-  float s[V], q[V];
-#pragma unroll
-  for (int i = 0; i < V; ++i) s[i] = 0.f, q[i] = 0.f;
-  const int64_t row_begin = int64_t(blockIdx.x) * rows_per_block;
-  const int64_t row_end = row_begin + rows_per_block < M ? row_begin + rows_per_block : M;
-  for (int64_t r = row_begin + r0; r < row_end; r += R) {
-    float v[V];
-    bn_load<DT>(x, r * C + c0, v);
-    if constexpr (BWD) {
-      float gv[V];
-      bn_load<DT>(gy, r * C + c0, gv);
-#pragma unroll
-      for (int i = 0; i < V; ++i) {
-        const float xh = fmaf(v[i], is[i], nm[i]);
-        const float gz = fmaf(xh, ww[i], bb[i]) > 0.f ? gv[i] : gv[i] * slope;
-        s[i] += gz;
-        q[i] += gz * xh;
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < V; ++i) s[i] += v[i], q[i] += v[i] * v[i];
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < V; ++i) ls[i * LS + threadIdx.x] = s[i], lq[i * LS + threadIdx.x] = q[i];
-  __syncthreads();
-  for (int c = int(threadIdx.x); c < C; c += kBlock) {
-    // channel c = group c / V, element c % V; its R partials sit in lanes r * G + c / V
-    const float* ps = ls + (c % V) * LS + c / V;
-    const float* pq = lq + (c % V) * LS + c / V;
-    float a = 0.f, q2 = 0.f;
-    for (int r = 0; r < R; ++r) a += ps[r * G], q2 += pq[r * G];
-    // channel-major [2C][blocks]: the fold reads each channel's partials contiguously
-    partial[int64_t(c) * gridDim.x + blockIdx.x] = a;
-    partial[int64_t(C + c) * gridDim.x + blockIdx.x] = q2;
-  }
-}
-
-// One WAVE per channel folds the per-block partials in fp64 (a single lane
-// per channel walking 1024 partials serially cost ~1 ms per step; a 256-lane
-// block per channel with an LDS tree and 8 barriers ~6.5 us per call).
-// Partials are channel-major ([2C][nblocks]: sums, then sums of squares), so
-// a wave's lanes read consecutive floats.  Lane 0 of the wave returns.
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
-
-__device__ __forceinline__ void bn_fold(const float* __restrict__ partial, int nblocks, int C, int c, double& s,
-                                        double& q) {
-  const int lane = int(threadIdx.x) & 63;
-  double a = 0.0, b2 = 0.0;
-  const float* ps = partial + int64_t(c) * nblocks;
-  const float* pq = partial + int64_t(C + c) * nblocks;
-#pragma unroll 4
-  for (int b = lane; b < nblocks; b += 64) a += ps[b], b2 += pq[b];
-  s = wave_sum(a);
-  q = wave_sum(b2);
-}
-
-constexpr int kFoldWaves = 4;   // channels per finalize block (one wave each)
-
-__global__ __launch_bounds__(64 * kFoldWaves) void bn_finalize_kernel(const float* __restrict__ partial, int nblocks,
-                                                                      int64_t M, int C, float eps, float momentum,
-                                                                      float* mean, float* invstd, float* rm,
-                                                                      float* rv, int64_t* tracked) {
-  const int c = int(blockIdx.x) * kFoldWaves + (int(threadIdx.x) >> 6);
-  if (c >= C) return;
-  double s, q;
-  bn_fold(partial, nblocks, C, c, s, q);
-  if ((threadIdx.x & 63) != 0) return;
-  if (tracked && c == 0) tracked[0] += 1;   // BatchNorm2d.num_batches_tracked (saves a launch)
-  const double mu = s / double(M);
-  double var = q / double(M) - mu * mu;
-  var = var < 0.0 ? 0.0 : var;
-  mean[c] = float(mu);
-  invstd[c] = float(1.0 / sqrt(var + double(eps)));
-  if (rm) {
-    rm[c] = float((1.0 - momentum) * rm[c] + momentum * mu);
-    rv[c] = float((1.0 - momentum) * rv[c] + momentum * var * double(M) / double(M > 1 ? M - 1 : 1));
-  }
-}
-
-__global__ __launch_bounds__(64 * kFoldWaves) void bn_bwd_finalize_kernel(const float* __restrict__ partial,
-                                                                          int nblocks, int C, float* dw, float* db) {
-  const int c = int(blockIdx.x) * kFoldWaves + (int(threadIdx.x) >> 6);
-  if (c >= C) return;
-  double s, q;
-  bn_fold(partial, nblocks, C, c, s, q);
-  if ((threadIdx.x & 63) != 0) return;
-  db[c] = float(s);
-  dw[c] = float(q);
-}
-
-// BWD = false: y = leaky(xhat * w + b).  BWD = true: gx = w * invstd * (gz - db/M - xhat * dw/M).
-// The grid-stride step is a multiple of kBlock and G = C / V divides kBlock,
-// so a lane keeps one channel group for the whole loop: its per-channel
-// coefficients are loaded once into registers, not per element.  Each lane
-// takes kBnUnroll vectors kBlock apart per pass with every load issued before
-// any math: one 16-byte vector per lane per pass left the kernel waiting out a
-// load latency per 16 bytes (9.9 / 12.4 us per call where the bytes take 1-4).
-constexpr int kBnUnroll = 4;
-
-template <int DT, bool BWD>
-__global__ __launch_bounds__(kBlock) void bn_apply_kernel(const void* __restrict__ x, const void* __restrict__ gy,
-                                                          void* __restrict__ out, int64_t M, int C,
-                                                          const float* __restrict__ mean,
-                                                          const float* __restrict__ invstd,
-                                                          const float* __restrict__ w, const float* __restrict__ b,
-                                                          const float* __restrict__ dw, const float* __restrict__ db,
-                                                          float slope) {
-  constexpr int V = BnVec<DT>::V, U = kBnUnroll;
-  const int G = C / V;
-  const int64_t total = M * G;
-  const float invM = 1.f / float(M);
-  const int c0 = (int(threadIdx.x) % G) * V;
-  // xhat = v * is + nm;  z = xhat * ww + bb;  backward: gx = P * (gz - dbm) - pdw * xhat
-  float is[V], nm[V], ww[V], bb[V], P[V], dbm[V], pdw[V];
-#pragma unroll
-  for (int i = 0; i < V; ++i) {
-    const int c = c0 + i;
-    is[i] = invstd[c];
-    nm[i] = -mean[c] * is[i];
-    ww[i] = w[c];
-    bb[i] = b[c];
-    if constexpr (BWD) {
-      P[i] = ww[i] * is[i];
-      dbm[i] = db[c] * invM;
-      pdw[i] = P[i] * dw[c] * invM;
-    }
-  }
-  auto apply = [&](const float (&v)[V], const float (&gv)[V], float (&o)[V]) {
-    if constexpr (BWD) {
-#pragma unroll
-      for (int i = 0; i < V; ++i) {
-        const float xh = fmaf(v[i], is[i], nm[i]);
-        const float gz = fmaf(xh, ww[i], bb[i]) > 0.f ? gv[i] : gv[i] * slope;
-        o[i] = fmaf(P[i], gz - dbm[i], -pdw[i] * xh);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < V; ++i) {
-        const float z = fmaf(fmaf(v[i], is[i], nm[i]), ww[i], bb[i]);
-        o[i] = z > 0.f ? z : z * slope;
-      }
-    }
-  };
-  const int64_t pass = int64_t(gridDim.x) * kBlock * U;
-  int64_t idx = int64_t(blockIdx.x) * kBlock * U + threadIdx.x;
-  for (; idx + (U - 1) * kBlock < total; idx += pass) {   // whole passes: U loads in flight
-    float v[U][V], gv[U][V];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      bn_load<DT>(x, (idx + u * kBlock) * V, v[u]);
-      if constexpr (BWD) bn_load<DT>(gy, (idx + u * kBlock) * V, gv[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      float o[V];
-      apply(v[u], gv[u], o);
-      bn_store<DT>(out, (idx + u * kBlock) * V, o);
-    }
-  }
-  for (; idx < total; idx += kBlock) {   // the tail: at most U - 1 vectors per lane
-    float v[V], gv[V], o[V];
-    bn_load<DT>(x, idx * V, v);
-    if constexpr (BWD) bn_load<DT>(gy, idx * V, gv);
-    apply(v, gv, o);
-    bn_store<DT>(out, idx * V, o);
-  }
-}
-
-namespace {
-bool bn_shape_ok(int64_t M, int C, int dtype) {
-  if (M <= 0 || C <= 0 || (dtype != OUT_F32 && dtype != OUT_BF16)) return false;
-  const int V = dtype == OUT_BF16 ? 8 : 4;
-  return C % V == 0 && kBlock % (C / V) == 0;
-}
-
-void bn_blocks(int64_t M, int C, int dtype, int& nblocks, int64_t& rows_per_block) {
-  const int V = dtype == OUT_BF16 ? 8 : 4;
-  const int R = kBlock / (C / V);
-  const int64_t want = (M + R - 1) / R;
-  nblocks = int(want < kBnMaxBlocks ? want : kBnMaxBlocks);
-  rows_per_block = (M + nblocks - 1) / nblocks;
-}
-
-int bn_grid(int64_t work) {   // work = 16-byte vectors; kBnUnroll per lane per pass
-  const int64_t blocks = (work + kBlock * kBnUnroll - 1) / (kBlock * kBnUnroll);
-  return int(blocks < 4096 ? (blocks < 1 ? 1 : blocks) : 4096);
-}
-}  // namespace
-
-int64_t bn_partial_floats(int64_t M, int C, int dtype) {
-  if (!bn_shape_ok(M, C, dtype)) return -1;
-  int nb;
-  int64_t rpb;
-  bn_blocks(M, C, dtype, nb, rpb);
-  return int64_t(nb) * 2 * C;
-}
-
-hipError_t bn_stats(const void* x, int64_t M, int C, int dtype, float* partial, hipStream_t stream) {
-  if (!bn_shape_ok(M, C, dtype)) return hipErrorInvalidValue;
-  int nb;
-  int64_t rpb;
-  bn_blocks(M, C, dtype, nb, rpb);
-  if (dtype == OUT_BF16)
-    bn_reduce_kernel<OUT_BF16, false><<<nb, kBlock, 0, stream>>>(x, nullptr, M, C, rpb, nullptr, nullptr, nullptr,
-                                                                 nullptr, 0.f, partial);
-  else
-    bn_reduce_kernel<OUT_F32, false><<<nb, kBlock, 0, stream>>>(x, nullptr, M, C, rpb, nullptr, nullptr, nullptr,
-                                                                nullptr, 0.f, partial);
-  return hipGetLastError();
-}
-
-hipError_t bn_finalize(const float* partial, int64_t M, int C, int dtype, float eps, float momentum, float* mean,
-                       float* invstd, float* running_mean, float* running_var, hipStream_t stream,
-                       int64_t* num_batches_tracked) {
-  if (!bn_shape_ok(M, C, dtype)) return hipErrorInvalidValue;
-  int nb;
-  int64_t rpb;
-  bn_blocks(M, C, dtype, nb, rpb);
-  bn_finalize_kernel<<<(C + kFoldWaves - 1) / kFoldWaves, 64 * kFoldWaves, 0, stream>>>(partial, nb, M, C, eps, momentum, mean, invstd, running_mean,
-                                                running_var, num_batches_tracked);
-  return hipGetLastError();
-}
-
-hipError_t bn_finalize_rows(const float* partial, int nblocks, int64_t M, int C, float eps, float momentum,
-                            float* mean, float* invstd, float* running_mean, float* running_var, hipStream_t stream,
-                            int64_t* num_batches_tracked) {
-  if (nblocks <= 0 || M <= 0 || C <= 0 || !partial || !mean || !invstd) return hipErrorInvalidValue;
-  bn_finalize_kernel<<<(C + kFoldWaves - 1) / kFoldWaves, 64 * kFoldWaves, 0, stream>>>(partial, nblocks, M, C, eps, momentum, mean, invstd, running_mean,
-                                                running_var, num_batches_tracked);
-  return hipGetLastError();
-}
-
-hipError_t bn_apply(const void* x, void* y, int64_t M, int C, int dtype, const float* mean, const float* invstd,
-                    const float* w, const float* b, float slope, hipStream_t stream) {
-  if (!bn_shape_ok(M, C, dtype)) return hipErrorInvalidValue;
-  const int V = dtype == OUT_BF16 ? 8 : 4;
-  const int grid = bn_grid(M * (C / V));
-  if (dtype == OUT_BF16)
-    bn_apply_kernel<OUT_BF16, false><<<grid, kBlock, 0, stream>>>(x, nullptr, y, M, C, mean, invstd, w, b, nullptr,
-                                                                  nullptr, slope);
-  else
-    bn_apply_kernel<OUT_F32, false><<<grid, kBlock, 0, stream>>>(x, nullptr, y, M, C, mean, invstd, w, b, nullptr,
-                                                                 nullptr, slope);
-  return hipGetLastError();
-}
-
-hipError_t bn_bwd_reduce(const void* x, const void* gy, int64_t M, int C, int dtype, const float* mean,
-                         const float* invstd, const float* w, const float* b, float slope, float* partial,
-                         hipStream_t stream) {
-  if (!bn_shape_ok(M, C, dtype)) return hipErrorInvalidValue;
-  int nb;
-  int64_t rpb;
-  bn_blocks(M, C, dtype, nb, rpb);
-  if (dtype == OUT_BF16)
-    bn_reduce_kernel<OUT_BF16, true><<<nb, kBlock, 0, stream>>>(x, gy, M, C, rpb, mean, invstd, w, b, slope, partial);
-  else
-    bn_reduce_kernel<OUT_F32, true><<<nb, kBlock, 0, stream>>>(x, gy, M, C, rpb, mean, invstd, w, b, slope, partial);
-  return hipGetLastError();
-}
-
-hipError_t bn_bwd_finalize(const float* partial, int64_t M, int C, int dtype, float* dw, float* db,
-                           hipStream_t stream) {
-  if (!bn_shape_ok(M, C, dtype)) return hipErrorInvalidValue;
-  int nb;
-  int64_t rpb;
-  bn_blocks(M, C, dtype, nb, rpb);
-  bn_bwd_finalize_kernel<<<(C + kFoldWaves - 1) / kFoldWaves, 64 * kFoldWaves, 0, stream>>>(partial, nb, C, dw, db);
-  return hipGetLastError();
-}
-
-hipError_t bn_bwd_finalize_rows(const float* partial, int rows, int C, float* dw, float* db, hipStream_t stream) {
-  if (rows <= 0 || C <= 0 || !partial || !dw || !db) return hipErrorInvalidValue;
-  bn_bwd_finalize_kernel<<<(C + kFoldWaves - 1) / kFoldWaves, 64 * kFoldWaves, 0, stream>>>(partial, rows, C, dw, db);
-  return hipGetLastError();
-}
-
-hipError_t bn_bwd_apply(const void* x, const void* gy, void* gx, int64_t M, int C, int dtype, const float* mean,
-                        const float* invstd, const float* w, const float* b, const float* dw, const float* db,
-                        float slope, hipStream_t stream) {
-  if (!bn_shape_ok(M, C, dtype)) return hipErrorInvalidValue;
-  const int V = dtype == OUT_BF16 ? 8 : 4;
-  const int grid = bn_grid(M * (C / V));
-  if (dtype == OUT_BF16)
-    bn_apply_kernel<OUT_BF16, true><<<grid, kBlock, 0, stream>>>(x, gy, gx, M, C, mean, invstd, w, b, dw, db, slope);
-  else
-    bn_apply_kernel<OUT_F32, true><<<grid, kBlock, 0, stream>>>(x, gy, gx, M, C, mean, invstd, w, b, dw, db, slope);
-  return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
-// multi-tensor cast (fp32 <-> bf16)
-// ---------------------------------------------------------------------------
-namespace {
-
-// blockIdx.y = tensor, blockIdx.x strides over its elements, 4 per lane
-template <int MODE>
-__global__ __launch_bounds__(kBlock) void multi_cast_kernel(CastParams p) {
-  const int k = int(blockIdx.y);
-  const int64_t n = p.numel[k];
-  for (int64_t i = (int64_t(blockIdx.x) * kBlock + threadIdx.x) * 4; i < n; i += int64_t(gridDim.x) * kBlock * 4) {
-    if constexpr (MODE == CAST_F32_TO_BF16) {
-      const float* s = static_cast<const float*>(p.src[k]);
-      uint16_t* d = static_cast<uint16_t*>(p.dst[k]);
-      for (int j = 0; j < 4 && i + j < n; ++j) {
-        const float f = s[i + j];
-        d[i + j] = f != f ? uint16_t(0x7FC0) : f2bf(f);   // NaN stays a quiet NaN (as torch)
-      }
-    } else {
-      const uint16_t* s = static_cast<const uint16_t*>(p.src[k]);
-      float* d = static_cast<float*>(p.dst[k]);
-      for (int j = 0; j < 4 && i + j < n; ++j) d[i + j] = __uint_as_float(uint32_t(s[i + j]) << 16);
-    }
-  }
-}
-
-}  // namespace
-
-hipError_t multi_cast(const CastParams& p, hipStream_t stream) {
-  if (p.n <= 0) return hipSuccess;
-  if (p.n > kMaxCast) return hipErrorInvalidValue;
-  int64_t most = 0;
-  for (int k = 0; k < p.n; ++k) {
-    if (p.numel[k] < 0 || (p.numel[k] > 0 && (!p.src[k] || !p.dst[k]))) return hipErrorInvalidValue;
-    most = p.numel[k] > most ? p.numel[k] : most;
-  }
-  const int64_t blocks = (most + 4 * kBlock - 1) / (4 * kBlock);
-  const dim3 grid(unsigned(blocks < 1024 ? (blocks > 0 ? blocks : 1) : 1024), unsigned(p.n));
-  if (p.mode == CAST_F32_TO_BF16) multi_cast_kernel<CAST_F32_TO_BF16><<<grid, kBlock, 0, stream>>>(p);
-  else if (p.mode == CAST_BF16_TO_F32) multi_cast_kernel<CAST_BF16_TO_F32><<<grid, kBlock, 0, stream>>>(p);
-  else return hipErrorInvalidValue;
-  return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
-// Adam / AdamW
-// ---------------------------------------------------------------------------
-namespace {
-
-// One lane: the step counter and the bias corrections, so that the update
-// kernel's blocks all read a value no block is writing.
-__global__ void adam_schedule_kernel(float* step, const float* hp, float* sched, float beta1, float beta2,
-                                     const float* gate) {
-  if (threadIdx.x != 0) return;
-  // a closed gate (gate[0] == 0, computed on the device earlier in the same
-  // stream/graph) makes the whole step a no-op: counter, moments and weights
-  const bool active = !gate || gate[0] != 0.f;
-  sched[4] = active ? 1.f : 0.f;
-  if (!active) return;
-  const float s = step[0] + 1.f;
-  step[0] = s;
-  const float lr = hp[0];
-  const double bc1 = 1.0 - pow(double(beta1), double(s));
-  const double bc2 = 1.0 - pow(double(beta2), double(s));
-  sched[0] = float(double(lr) / bc1);
-  sched[1] = float(1.0 / sqrt(bc2));
-  sched[2] = lr;
-  sched[3] = hp[1];   // gradient scale (e.g. 1 / world after a summing all-reduce)
-}
-
-template <bool GBF16>
-__global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
-  const int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x;   // 4-element group
-  if (q >= a.gstart[a.n] || a.sched[4] == 0.f) return;
-  int k = 0;
-  while (q >= a.gstart[k + 1]) ++k;     // <= kMaxAdam compares, mostly uniform across a wave
-  const int64_t e0 = (q - a.gstart[k]) * 4;
-  const int64_t n = a.numel[k];
-  const float step_size = a.sched[0], inv_bc2 = a.sched[1], lr = a.sched[2], gscale = a.sched[3];
-  const float b1 = a.beta1, b2 = a.beta2, wd = a.weight_decay;
-  float* P = a.p[k];
-  float* M = a.m[k];
-  float* V = a.v[k];
-  float pv[4], gv[4], mv[4], vv[4];
-  const bool full = e0 + 4 <= n;   // tensors are 16-byte aligned (host-checked), so a full group is one dwordx4
-  if (full) {
-    const float4 p4 = *reinterpret_cast<const float4*>(P + e0);
-    const float4 m4 = *reinterpret_cast<const float4*>(M + e0);
-    const float4 v4 = *reinterpret_cast<const float4*>(V + e0);
-    pv[0] = p4.x, pv[1] = p4.y, pv[2] = p4.z, pv[3] = p4.w;
-    mv[0] = m4.x, mv[1] = m4.y, mv[2] = m4.z, mv[3] = m4.w;
-    vv[0] = v4.x, vv[1] = v4.y, vv[2] = v4.z, vv[3] = v4.w;
-    if constexpr (GBF16) {
-      const uint2 g2 = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(a.g[k]) + e0);
-      gv[0] = __uint_as_float(g2.x << 16), gv[1] = __uint_as_float(g2.x & 0xFFFF0000u);
-      gv[2] = __uint_as_float(g2.y << 16), gv[3] = __uint_as_float(g2.y & 0xFFFF0000u);
-    } else {
-      const float4 g4 = *reinterpret_cast<const float4*>(static_cast<const float*>(a.g[k]) + e0);
-      gv[0] = g4.x, gv[1] = g4.y, gv[2] = g4.z, gv[3] = g4.w;
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const bool in = e0 + j < n;
-      pv[j] = in ? P[e0 + j] : 0.f;
-      mv[j] = in ? M[e0 + j] : 0.f;
-      vv[j] = in ? V[e0 + j] : 0.f;
-      if constexpr (GBF16)
-        gv[j] = in ? __uint_as_float(uint32_t(static_cast<const uint16_t*>(a.g[k])[e0 + j]) << 16) : 0.f;
-      else
-        gv[j] = in ? static_cast<const float*>(a.g[k])[e0 + j] : 0.f;
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    float g = (a.maximize ? -gv[j] : gv[j]) * gscale;
-    if (wd != 0.f) {
-      if (a.decoupled) pv[j] *= 1.f - lr * wd;
-      else g += wd * pv[j];
-    }
-    mv[j] = b1 * mv[j] + (1.f - b1) * g;
-    vv[j] = b2 * vv[j] + (1.f - b2) * g * g;
-    pv[j] -= step_size * mv[j] / (sqrtf(vv[j]) * inv_bc2 + a.eps);
-  }
-  uint16_t* S = a.shadow[k];
-  if (full) {
-    *reinterpret_cast<float4*>(P + e0) = make_float4(pv[0], pv[1], pv[2], pv[3]);
-    *reinterpret_cast<float4*>(M + e0) = make_float4(mv[0], mv[1], mv[2], mv[3]);
-    *reinterpret_cast<float4*>(V + e0) = make_float4(vv[0], vv[1], vv[2], vv[3]);
-    if (S) {
-      uint2 s2;
-      s2.x = uint32_t(f2bf(pv[0])) | (uint32_t(f2bf(pv[1])) << 16);
-      s2.y = uint32_t(f2bf(pv[2])) | (uint32_t(f2bf(pv[3])) << 16);
-      *reinterpret_cast<uint2*>(S + e0) = s2;
-    }
-  } else {
-    for (int j = 0; j < 4 && e0 + j < n; ++j) {
-      P[e0 + j] = pv[j], M[e0 + j] = mv[j], V[e0 + j] = vv[j];
-      if (S) S[e0 + j] = f2bf(pv[j]);
-    }
-  }
-}
-
-}  // namespace
-
-hipError_t adam_schedule(float* step, const float* hp, float* sched, float beta1, float beta2, hipStream_t stream,
-                         const float* gate) {
-  if (!step || !hp || !sched) return hipErrorInvalidValue;
-  adam_schedule_kernel<<<1, 64, 0, stream>>>(step, hp, sched, beta1, beta2, gate);
-  return hipGetLastError();
-}
-
-hipError_t adam_update(const AdamParams& p, hipStream_t stream) {
-  if (p.n <= 0) return hipSuccess;
-  if (p.n > kMaxAdam || !p.sched) return hipErrorInvalidValue;
-  if (p.gstart[0] != 0) return hipErrorInvalidValue;
-  for (int k = 0; k < p.n; ++k) {
-    if (p.numel[k] < 0 || p.gstart[k + 1] - p.gstart[k] != (p.numel[k] + 3) / 4) return hipErrorInvalidValue;
-    if (p.numel[k] > 0 && (!p.p[k] || !p.g[k] || !p.m[k] || !p.v[k])) return hipErrorInvalidValue;
-    // full groups are read and written as 16-byte (8-byte for bf16) vectors
-    const uintptr_t mis = reinterpret_cast<uintptr_t>(p.p[k]) | reinterpret_cast<uintptr_t>(p.m[k]) |
-                          reinterpret_cast<uintptr_t>(p.v[k]) |
-                          (reinterpret_cast<uintptr_t>(p.g[k]) << (p.grad_bf16 ? 1 : 0)) |
-                          (reinterpret_cast<uintptr_t>(p.shadow[k]) << 1);
-    if (mis & 15) return hipErrorInvalidValue;
-  }
-  const int64_t groups = p.gstart[p.n];
-  if (groups == 0) return hipSuccess;
-  const int64_t blocks = (groups + kBlock - 1) / kBlock;
-  if (blocks > int64_t(1) << 30) return hipErrorInvalidValue;
-  if (p.grad_bf16) adam_update_kernel<true><<<unsigned(blocks), kBlock, 0, stream>>>(p);
-  else adam_update_kernel<false><<<unsigned(blocks), kBlock, 0, stream>>>(p);
-  return hipGetLastError();
-}
-
 }  // namespace gpu
 }  // namespace btn

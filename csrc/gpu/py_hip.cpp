@@ -263,8 +263,9 @@ PYBIND11_MODULE(_hip, m) {
       "conv_dgrad",
       [](uintptr_t dy, uintptr_t wt, uintptr_t dx, int N, int H, int W, int Cin, int Cout, uintptr_t stream,
          uintptr_t bn_x, uintptr_t bn_mean, uintptr_t bn_invstd, uintptr_t bn_w, uintptr_t bn_b, float bn_slope,
-         uintptr_t bn_part, int bn_rows) {
+         uintptr_t bn_part, int bn_rows, int bn_acc_r) {
         BnBwdFuse bn;
+        bn.acc_r = bn_acc_r;
         bn.x = ptr<const uint16_t>(bn_x);
         bn.mean = ptr<const float>(bn_mean);
         bn.invstd = ptr<const float>(bn_invstd);
@@ -280,7 +281,7 @@ PYBIND11_MODULE(_hip, m) {
       py::arg("dy"), py::arg("wt"), py::arg("dx"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("Cin"),
       py::arg("Cout"), py::arg("stream"), py::arg("bn_x") = 0, py::arg("bn_mean") = 0, py::arg("bn_invstd") = 0,
       py::arg("bn_w") = 0, py::arg("bn_b") = 0, py::arg("bn_slope") = 0.f, py::arg("bn_part") = 0,
-      py::arg("bn_rows") = 0);
+      py::arg("bn_rows") = 0, py::arg("bn_acc_r") = 0);
   m.def("conv_dgrad_bn_rows", &conv_dgrad_bn_rows);
   m.def("bn_backward_from_stats",
         [](uintptr_t x, uintptr_t gy, uintptr_t gx, int64_t M, int C, int dtype, uintptr_t part, int rows,
@@ -296,9 +297,10 @@ PYBIND11_MODULE(_hip, m) {
         });
   m.def("conv_fwd",
         [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, int N, int H, int W, int Cin, int Ho, int Wo,
-           int Cout, uintptr_t stream, int w_channels) {
+           int Cout, uintptr_t stream, int w_channels, int acc_r) {
           ConvFwdParams p;
           p.w_channels = w_channels;
+          p.acc_r = acc_r;
           p.x = ptr<const uint16_t>(x);
           p.w = ptr<const uint16_t>(w);
           p.y = ptr<uint16_t>(y);
@@ -308,7 +310,8 @@ PYBIND11_MODULE(_hip, m) {
           check(conv_fwd(p, stream_of(stream)), "conv_fwd");
         },
         py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"), py::arg("N"), py::arg("H"), py::arg("W"),
-        py::arg("Cin"), py::arg("Ho"), py::arg("Wo"), py::arg("Cout"), py::arg("stream"), py::arg("w_channels") = 0);
+        py::arg("Cin"), py::arg("Ho"), py::arg("Wo"), py::arg("Cout"), py::arg("stream"), py::arg("w_channels") = 0,
+        py::arg("acc_r") = 0);
   // BatchNorm+LeakyReLU forward from conv_fwd's per-tile statistics: finalize + apply
   m.def("bn_forward_from_stats",
         [](uintptr_t x, uintptr_t y, int64_t M, int C, int dtype, uintptr_t stats, int nrows, float eps,
@@ -326,8 +329,9 @@ PYBIND11_MODULE(_hip, m) {
   m.def("head_forward",
         [](uintptr_t z, uintptr_t w, int64_t ws_c, int64_t ws_i, int64_t ws_j, int N, int H, int W, int C, int OH,
            int OW, uintptr_t target, float target_value, uintptr_t pooled, uintptr_t partial, uintptr_t loss,
-           uintptr_t dlogit, uintptr_t logit, uintptr_t stream) {
+           uintptr_t dlogit, uintptr_t logit, uintptr_t stream, uintptr_t ticket) {
           HeadParams p;
+          p.ticket = ptr<uint32_t>(ticket);
           p.z = ptr<const uint16_t>(z);
           p.w = ptr<const float>(w);
           p.ws_c = ws_c, p.ws_i = ws_i, p.ws_j = ws_j;
@@ -340,11 +344,25 @@ PYBIND11_MODULE(_hip, m) {
           p.dlogit = ptr<float>(dlogit);
           p.logit = ptr<float>(logit);
           check(head_forward(p, stream_of(stream)), "head_forward");
-        });
+        },
+        py::arg("z"), py::arg("w"), py::arg("ws_c"), py::arg("ws_i"), py::arg("ws_j"), py::arg("N"), py::arg("H"),
+        py::arg("W"), py::arg("C"), py::arg("OH"), py::arg("OW"), py::arg("target"), py::arg("target_value"),
+        py::arg("pooled"), py::arg("partial"), py::arg("loss"), py::arg("dlogit"), py::arg("logit"),
+        py::arg("stream"), py::arg("ticket") = 0);
   m.def("head_backward",
         [](uintptr_t w, int64_t ws_c, int64_t ws_i, int64_t ws_j, int N, int H, int W, int C, int OH, int OW,
-           uintptr_t pooled, uintptr_t dlogit, uintptr_t gscale, uintptr_t dz, uintptr_t dw, uintptr_t stream) {
+           uintptr_t pooled, uintptr_t dlogit, uintptr_t gscale, uintptr_t dz, uintptr_t dw, uintptr_t stream,
+           uintptr_t bn_x, uintptr_t bn_mean, uintptr_t bn_invstd, uintptr_t bn_w, uintptr_t bn_b, float bn_slope,
+           uintptr_t bn_acc, int bn_acc_r) {
           HeadParams p;
+          p.bn_x = ptr<const uint16_t>(bn_x);
+          p.bn_mean = ptr<const float>(bn_mean);
+          p.bn_invstd = ptr<const float>(bn_invstd);
+          p.bn_w = ptr<const float>(bn_w);
+          p.bn_b = ptr<const float>(bn_b);
+          p.bn_slope = bn_slope;
+          p.bn_acc = ptr<double>(bn_acc);
+          p.bn_acc_r = bn_acc_r;
           p.w = ptr<const float>(w);
           p.ws_c = ws_c, p.ws_i = ws_i, p.ws_j = ws_j;
           p.N = N, p.H = H, p.W = W, p.C = C, p.OH = OH, p.OW = OW;
@@ -354,7 +372,12 @@ PYBIND11_MODULE(_hip, m) {
           p.dz = ptr<uint16_t>(dz);
           p.dw = ptr<float>(dw);
           check(head_backward(p, stream_of(stream)), "head_backward");
-        });
+        },
+        py::arg("w"), py::arg("ws_c"), py::arg("ws_i"), py::arg("ws_j"), py::arg("N"), py::arg("H"), py::arg("W"),
+        py::arg("C"), py::arg("OH"), py::arg("OW"), py::arg("pooled"), py::arg("dlogit"), py::arg("gscale"),
+        py::arg("dz"), py::arg("dw"), py::arg("stream"), py::arg("bn_x") = 0, py::arg("bn_mean") = 0,
+        py::arg("bn_invstd") = 0, py::arg("bn_w") = 0, py::arg("bn_b") = 0, py::arg("bn_slope") = 0.f,
+        py::arg("bn_acc") = 0, py::arg("bn_acc_r") = 0);
 
   // direct RCCL on the caller's stream (comm.h); the GIL is released while
   // RCCL enqueues (a group end may block until peers have posted theirs)
@@ -410,11 +433,14 @@ PYBIND11_MODULE(_hip, m) {
         [](std::vector<uintptr_t> params, std::vector<uintptr_t> grads, std::vector<uintptr_t> exp_avg,
            std::vector<uintptr_t> exp_avg_sq, std::vector<uintptr_t> shadow, std::vector<int64_t> numel,
            uintptr_t sched, int grad_bf16, float beta1, float beta2, float eps, float weight_decay, int decoupled,
-           int maximize, uintptr_t stream) {
+           int maximize, uintptr_t stream, uintptr_t step, uintptr_t hp, uintptr_t gate, uintptr_t ticket,
+           int zero_grad, std::vector<uintptr_t> shadow_t, std::vector<int> tcout, std::vector<int> tcin) {
           const size_t n = params.size();
           if (grads.size() != n || exp_avg.size() != n || exp_avg_sq.size() != n || shadow.size() != n ||
               numel.size() != n || n > size_t(kMaxAdam))
             throw std::invalid_argument("adam_update: list lengths differ or exceed kMaxAdam");
+          if (!shadow_t.empty() && (shadow_t.size() != n || tcout.size() != n || tcin.size() != n))
+            throw std::invalid_argument("adam_update: shadow_t / tcout / tcin must match params");
           AdamParams a;
           a.n = int(n);
           for (size_t k = 0; k < n; ++k) {
@@ -426,11 +452,27 @@ PYBIND11_MODULE(_hip, m) {
             a.numel[k] = numel[k];
             a.gstart[k + 1] = a.gstart[k] + (numel[k] + 3) / 4;
           }
+          for (size_t k = 0; k < shadow_t.size(); ++k) {
+            a.shadow_t[k] = ptr<uint16_t>(shadow_t[k]);
+            a.tcout[k] = tcout[k];
+            a.tcin[k] = tcin[k];
+          }
           a.sched = ptr<const float>(sched);
+          a.step = ptr<float>(step);
+          a.hp = ptr<const float>(hp);
+          a.gate = ptr<const float>(gate);
+          a.ticket = ptr<uint32_t>(ticket);
+          a.zero_grad = zero_grad;
           a.grad_bf16 = grad_bf16, a.decoupled = decoupled, a.maximize = maximize;
           a.beta1 = beta1, a.beta2 = beta2, a.eps = eps, a.weight_decay = weight_decay;
           check(adam_update(a, stream_of(stream)), "adam_update");
-        });
+        },
+        py::arg("params"), py::arg("grads"), py::arg("exp_avg"), py::arg("exp_avg_sq"), py::arg("shadow"),
+        py::arg("numel"), py::arg("sched"), py::arg("grad_bf16"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"),
+        py::arg("weight_decay"), py::arg("decoupled"), py::arg("maximize"), py::arg("stream"), py::arg("step") = 0,
+        py::arg("hp") = 0, py::arg("gate") = 0, py::arg("ticket") = 0, py::arg("zero_grad") = 0,
+        py::arg("shadow_t") = std::vector<uintptr_t>(), py::arg("tcout") = std::vector<int>(),
+        py::arg("tcin") = std::vector<int>());
 
   m.def("color4x4",
         [](uintptr_t src, uintptr_t dst, uintptr_t lut, uintptr_t M, uintptr_t bias, uintptr_t flip, int B, int H,
@@ -501,6 +543,38 @@ PYBIND11_MODULE(_hip, m) {
                              ptr<const float>(mean), ptr<const float>(invstd), ptr<const float>(w),
                              ptr<const float>(b), ptr<const float>(dw), ptr<const float>(db), slope, s),
                 "bn_bwd_apply");
+        });
+
+  // accumulator hand-off (kernels.h BnAcc): no finalize launches
+  m.def("bn_acc_replicas", &bn_acc_replicas);
+  m.def("bn_acc_elems", &bn_acc_elems);
+  m.def("bn_forward_acc",
+        [](uintptr_t x, uintptr_t y, int64_t M, int C, int dtype, uintptr_t acc, int R, float eps, float momentum,
+           uintptr_t mean, uintptr_t invstd, uintptr_t rm, uintptr_t rv, uintptr_t w, uintptr_t b, float slope,
+           uintptr_t stream, uintptr_t tracked) {
+          BnAcc a;
+          a.acc = ptr<double>(acc), a.R = R;
+          check(bn_apply_acc(ptr<const void>(x), ptr<void>(y), M, C, dtype, a, eps, momentum, ptr<float>(mean),
+                             ptr<float>(invstd), ptr<float>(rm), ptr<float>(rv), ptr<int64_t>(tracked),
+                             ptr<const float>(w), ptr<const float>(b), slope, stream_of(stream)),
+                "bn_apply_acc");
+        });
+  m.def("bn_backward_acc",
+        [](uintptr_t x, uintptr_t gy, uintptr_t gx, int64_t M, int C, int dtype, uintptr_t acc, int R, uintptr_t mean,
+           uintptr_t invstd, uintptr_t w, uintptr_t b, uintptr_t dw, uintptr_t db, float slope, uintptr_t stream,
+           bool reduce) {
+          // reduce: sum gz, gz * xhat here first (no producer epilogue did)
+          BnAcc a;
+          a.acc = ptr<double>(acc), a.R = R;
+          hipStream_t s = stream_of(stream);
+          if (reduce)
+            check(bn_bwd_reduce_acc(ptr<const void>(x), ptr<const void>(gy), M, C, dtype, ptr<const float>(mean),
+                                    ptr<const float>(invstd), ptr<const float>(w), ptr<const float>(b), slope, a, s),
+                  "bn_bwd_reduce_acc");
+          check(bn_bwd_apply_acc(ptr<const void>(x), ptr<const void>(gy), ptr<void>(gx), M, C, dtype, a,
+                                 ptr<const float>(mean), ptr<const float>(invstd), ptr<const float>(w),
+                                 ptr<const float>(b), ptr<float>(dw), ptr<float>(db), slope, s),
+                "bn_bwd_apply_acc");
         });
 
   // Diagnostics: H2D bandwidth of one `nbytes` copy repeated `iters` times

@@ -59,6 +59,20 @@ class Discriminator(nn.Module):
     def forward(self, x):
         return self.features(x).view(-1, 1).squeeze(1)
 
+    def use_optimizer_shadows(self, opt):
+        """Read the bf16 conv weights (and their data-gradient transposes)
+        from ``opt``'s shadows (``ops.FusedAdam.enable_conv_shadows``: the
+        update kernel rewrites them) instead of casting and transposing the
+        fp32 weights in two launches every step.  Only the 4x4 / stride-2
+        layers (the MFMA path, whose weight gradient goes to the fp32 weight
+        directly) use them.  ``opt=None`` switches back."""
+        self._shadow_opt = None
+        if opt is not None:
+            ws = [m.weight for m in self.features if isinstance(m, nn.Conv2d) and m.stride == (2, 2)
+                  and tuple(m.kernel_size) == (4, 4)]
+            opt.enable_conv_shadows(ws)
+            self._shadow_opt = opt
+
     def forward_bf16(self, x, mfma=True):
         """bf16 forward without autocast.  ``x`` may carry a 4th (alpha)
         channel that the first convolution ignores (RGBA-decoded frames feed
@@ -108,11 +122,11 @@ class Discriminator(nn.Module):
               and head.stride == (1, 1) and head.padding == (0, 0) and head.groups == 1
               and head.in_channels % 8 == 0)
         if ok:
-            z = self._run_bf16(x, body, mfma)
+            z, link = self._run_bf16(x, body, mfma, want_link=True)
             if adaptive or tuple(z.shape[2:]) == pool:
                 if not z.is_contiguous(memory_format=torch.channels_last):
-                    z = z.contiguous(memory_format=torch.channels_last)
-                loss, logits = ops.disc_head_bce(z, head.weight, target, pool)
+                    z, link = z.contiguous(memory_format=torch.channels_last), None
+                loss, logits = ops.disc_head_bce(z, head.weight, target, pool, bn_link=link)
                 return loss, (torch.sigmoid(logits) if probs else None)
             out = self._run_bf16(z, layers[len(body):], mfma)
         else:
@@ -121,16 +135,18 @@ class Discriminator(nn.Module):
         tgt = target if isinstance(target, torch.Tensor) else torch.full_like(out, float(target))
         return F.binary_cross_entropy(out, tgt), out
 
-    def _run_bf16(self, x, layers, mfma):
+    def _run_bf16(self, x, layers, mfma, want_link=False):
         import torch.nn.functional as F
         from .. import ops
         convs = [m for m in layers if isinstance(m, nn.Conv2d)]
-        w16s = ops.cast_bf16(*[c.weight for c in convs])
-        weights = iter(w16s)
+        shadows = self.__dict__.get('_shadow_opt') if (mfma and x.is_cuda) else None
+        # with optimizer shadows only the layers off the MFMA path are cast (usually none)
+        w16s = ops.cast_bf16(*[c.weight for c in convs]) if shadows is None else None
+        weights = iter(w16s) if w16s is not None else None
         # data-gradient operands of the MFMA layers that need one (not the first:
         # its input is the batch), transposed in one launch per step
         wts = {}
-        if mfma and torch.is_grad_enabled() and x.is_cuda:
+        if shadows is None and mfma and torch.is_grad_enabled() and x.is_cuda:
             need = [k for k, c in enumerate(convs) if k > 0 and c.in_channels % 32 == 0 and c.stride == (2, 2)
                     and tuple(c.kernel_size) == (4, 4) and c.out_channels % 32 == 0]
             if need:
@@ -139,16 +155,29 @@ class Discriminator(nn.Module):
         stats = link = None
         for i, m in enumerate(layers):
             if isinstance(m, nn.Conv2d):
-                w16 = next(weights)
                 ci += 1
-                if (mfma and m.stride == (2, 2) and m.padding == (1, 1) and m.bias is None and m.groups == 1
-                        and m.dilation == (1, 1) and ops.conv_wgrad_supported(x, m.weight)):
+                on_mfma = (mfma and m.stride == (2, 2) and m.padding == (1, 1) and m.bias is None
+                           and m.groups == 1 and m.dilation == (1, 1) and ops.conv_wgrad_supported(x, m.weight))
+                if shadows is None:
+                    w16 = next(weights)
+                elif on_mfma and 'shadow' in shadows.state.get(m.weight, {}):
+                    w16 = shadows.shadow(m.weight)
+                    if ci > 0 and torch.is_grad_enabled():
+                        wts[ci] = shadows.shadow_t(m.weight)
+                else:
+                    w16 = ops.cast_bf16(m.weight)[0]
+                if on_mfma:
                     nxt = layers[i + 1] if i + 1 < len(layers) else None
                     fuse = (isinstance(nxt, ops.BatchNormLeakyReLU2d) and ops.conv_fwd_supported(x, w16)
                             and nxt.fused_with_stats(x.new_empty((1, m.out_channels, 1, 1))))
                     # the BN that produced x: this conv's data gradient does its backward reduction
                     bl, link = link, None
-                    if fuse:   # BN statistics come out of the conv kernel's epilogue
+                    if fuse and ops.bn_acc_supported(m.out_channels):
+                        # BN statistics come out of the conv kernel's epilogue, added into
+                        # the BN call's zeroed accumulator (its apply kernel folds them)
+                        stats = nxt.accumulator(x.device)
+                        x = ops.conv4x4s2(x, m.weight, w16, with_stats=stats, wt=wts.get(ci), bn_link=bl)
+                    elif fuse:   # per-tile partial rows + a finalize launch
                         x, stats = ops.conv4x4s2(x, m.weight, w16, with_stats=True, wt=wts.get(ci), bn_link=bl)
                     else:
                         x = ops.conv4x4s2(x, m.weight, w16, wt=wts.get(ci), bn_link=bl)
@@ -163,7 +192,9 @@ class Discriminator(nn.Module):
                 if not isinstance(m, nn.Identity):
                     link = None
                 x = m(x)
-        return x
+        # want_link: also the BnLink of a BN whose output is returned (its consumer
+        # -- the fused head -- can then do that BN's backward reduction)
+        return (x, link) if want_link else x
 
 
 class ProbModel(nn.Module):

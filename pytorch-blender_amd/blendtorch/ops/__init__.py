@@ -764,6 +764,33 @@ def cast_bf16(*tensors):
 # ---------------------------------------------------------------------------
 # consumer-model op: training BatchNorm2d fused with LeakyReLU (channels-last)
 
+class BnAccumulator:
+    """Zeroed fp64 statistics accumulators of one BatchNorm+LeakyReLU call
+    (csrc/gpu/kernels.h ``BnAcc``): the producing kernel -- the convolution's
+    forward epilogue (``fwd``) or the consuming convolution's data-gradient
+    epilogue (``bwd``) -- adds its per-tile channel sums into them with fp64
+    atomics (order-independent at fp32 precision), and one finalize block
+    folds and clears them again: no per-tile partial rows, no per-step
+    memset, and the finalize is one memory latency instead of a walk over
+    ~4800 rows per channel.  ``R`` replicas per channel spread the atomics."""
+    __slots__ = ('fwd', 'bwd', 'R')
+
+    def __init__(self, C, device):
+        import torch
+        ext = hip_ext()
+        self.R = int(ext.bn_acc_replicas(int(C)))
+        n = int(ext.bn_acc_elems(int(C)))
+        if self.R <= 0 or n <= 0:
+            raise ValueError(f'BnAccumulator: unsupported channel count {C}')
+        self.fwd = torch.zeros(n, dtype=torch.float64, device=device)
+        self.bwd = torch.zeros(n, dtype=torch.float64, device=device)
+
+
+def bn_acc_supported(C):
+    """True when :class:`BnAccumulator` takes ``C`` channels."""
+    return int(hip_ext().bn_acc_replicas(int(C))) > 0
+
+
 class BnLink:
     """Hand-off between a training :class:`BatchNormLeakyReLU2d` and the
     convolution that consumes its output (:func:`conv4x4s2` ``bn_link=``).
@@ -774,11 +801,12 @@ class BnLink:
     has the MFMA kernel's epilogue sum gz and gz * xhat per tile into
     ``part``; the BN backward then only finalizes and applies (one pass over
     the activation fewer).  ``part`` is consumed once."""
-    __slots__ = ('x', 'mean', 'invstd', 'w', 'b', 'slope', 'part', 'rows', 'gy')
+    __slots__ = ('x', 'mean', 'invstd', 'w', 'b', 'slope', 'part', 'rows', 'gy', 'acc')
 
     def __init__(self):
         self.x = self.mean = self.invstd = self.w = self.b = self.part = self.gy = None
         self.slope, self.rows = 0.0, 0
+        self.acc = None      # BnAccumulator of the BN call (accumulator mode: part = acc.bwd, rows = -R)
 
     def ready(self, dx):
         """True when the recorded BN input matches ``dx`` (shape, bf16 NHWC)."""
@@ -788,10 +816,14 @@ class BnLink:
                 and tuple(x.shape) == (dx.shape[0], dx.shape[2], dx.shape[3], dx.shape[1]) and x.is_contiguous())
 
     def take(self, gys):
-        """The epilogue partials, if they were computed for exactly ``gys``."""
+        """The epilogue partials, if they were computed for exactly ``gys``
+        (``rows < 0``: accumulator mode, ``part`` = the ``-rows``-replica
+        accumulator).  An accumulator filled for another gradient is cleared."""
         part, rows, gy = self.part, self.rows, self.gy
         self.part = self.gy = None
         if part is None or gy is None or gys.data_ptr() != gy.data_ptr():
+            if part is not None and rows < 0:
+                part.zero_()
             return None, 0
         return part, rows
 
@@ -816,7 +848,14 @@ def _bn_function():
             rm = running_mean.data_ptr() if running_mean is not None else 0
             rv = running_var.data_ptr() if running_var is not None else 0
             tr = tracked.data_ptr() if tracked is not None else 0
-            if stats is not None:
+            if isinstance(stats, BnAccumulator):
+                # sums accumulated by the producing conv's epilogue; folded by the apply kernel
+                _count('bn_forward_from_stats')
+                _count('bn_forward_acc')
+                ext.bn_forward_acc(xs.data_ptr(), y.data_ptr(), M, C, dt, stats.fwd.data_ptr(), stats.R, float(eps),
+                                   float(momentum), mean.data_ptr(), invstd.data_ptr(), rm, rv, w.data_ptr(),
+                                   b.data_ptr(), float(slope), _stream(x.device), tr)
+            elif stats is not None:
                 # per-tile sums from the producing conv's epilogue (conv_fwd): no reduction pass over x
                 _count('bn_forward_from_stats')
                 ext.bn_forward_from_stats(xs.data_ptr(), y.data_ptr(), M, C, dt, stats.data_ptr(),
@@ -833,9 +872,11 @@ def _bn_function():
             ctx.slope = float(slope)
             ctx.link = link
             ctx.params = (weight, bias)
+            ctx.acc = stats if isinstance(stats, BnAccumulator) else None
             if link is not None:
                 link.x, link.mean, link.invstd, link.w, link.b, link.slope = xs, mean, invstd, w, b, float(slope)
                 link.part = link.gy = None
+                link.acc = ctx.acc
             return y.permute(0, 3, 1, 2)
 
         @staticmethod
@@ -854,7 +895,15 @@ def _bn_function():
             if db.dtype != torch.float32 or not db.is_contiguous():
                 db, b_sunk = torch.empty_like(b), False
             part, rows = ctx.link.take(gys) if ctx.link is not None else (None, 0)
-            if part is not None:
+            if ctx.acc is not None and (part is None or rows < 0):
+                # accumulator mode: the consuming conv's dgrad epilogue summed into
+                # acc.bwd (part), or this launch reduces into it first
+                _count('bn_backward_from_stats' if part is not None else 'bn_backward')
+                _count('bn_backward_acc')
+                ext.bn_backward_acc(xs.data_ptr(), gys.data_ptr(), gx.data_ptr(), M, C, dt, ctx.acc.bwd.data_ptr(),
+                                    ctx.acc.R, mean.data_ptr(), invstd.data_ptr(), w.data_ptr(), b.data_ptr(),
+                                    dw.data_ptr(), db.data_ptr(), ctx.slope, _stream(xs.device), part is None)
+            elif part is not None:
                 # the consuming convolution's data-gradient epilogue already summed gz, gz * xhat
                 _count('bn_backward_from_stats')
                 ext.bn_backward_from_stats(xs.data_ptr(), gys.data_ptr(), gx.data_ptr(), M, C, dt, part.data_ptr(),
@@ -949,10 +998,24 @@ def _bn_module():
             return (self.training and self.affine and self.track_running_stats and self.momentum is not None
                     and bn_supported(x))
 
+        def accumulator(self, device):
+            """The next :class:`BnAccumulator` of this module's ring (4 per
+            device): each training call takes its own, so the backward sums of
+            up to 4 calls in flight (e.g. a real and a simulated batch through
+            the same discriminator) never share one.  Not part of the state."""
+            ring = self.__dict__.get('_bt_acc_ring')
+            if ring is None or ring[0][0].fwd.device != device:
+                ring = self.__dict__['_bt_acc_ring'] = [[BnAccumulator(self.num_features, device) for _ in range(4)],
+                                                        0]
+            accs, i = ring
+            ring[1] = (i + 1) % len(accs)
+            return accs[i]
+
         def forward_from_stats(self, x, stats, link=None):
             """Training forward with the batch statistics already summed by
             the producing kernel (``conv_fwd``'s epilogue rows, see
-            :func:`conv4x4s2`): finalize + apply only.  ``link``: a
+            :func:`conv4x4s2`, or a :class:`BnAccumulator` it added into:
+            then one apply launch folds them): finalize + apply only.  ``link``: a
             :class:`BnLink` shared with the convolution that consumes the
             output (its data-gradient epilogue then does this op's backward
             reduction)."""
@@ -1018,13 +1081,15 @@ def conv_wgrad(x, dy, out, target_blocks=None):
     return out
 
 
-def conv_fwd(x, w16, stats=None):
+def conv_fwd(x, w16, stats=None, acc_r=0):
     """y = conv2d(x, w16, stride 2, pad 1) on the gfx950 MFMA kernel: ``x``
     [N, Cin, H, W] bf16 channels-last, ``w16`` [Cout, Cin, 4, 4] bf16
     channels-last; returns channels-last bf16 y.  ``stats`` (optional fp32
     tensor of ``conv_fwd_stats_rows(M, Cout) * 2 * Cout``) receives per-tile
     BatchNorm sums of y, channel-major: ``stats.view(2, Cout, rows)`` holds
-    the sums, then the sums of squares (see :func:`batch_norm_from_stats`)."""
+    the sums, then the sums of squares (see :func:`batch_norm_from_stats`).
+    ``acc_r`` > 0: ``stats`` is a :class:`BnAccumulator`'s zeroed fp64
+    ``fwd`` tensor with ``acc_r`` replicas, added into with atomics."""
     import torch
     ext = hip_ext()
     N, Cin, H, W = x.shape
@@ -1039,8 +1104,10 @@ def conv_fwd(x, w16, stats=None):
     Ho, Wo = (H - 2) // 2 + 1, (W - 2) // 2 + 1
     y = torch.empty((N, Cout, Ho, Wo), dtype=torch.bfloat16, device=x.device, memory_format=cl)
     _count('conv_fwd')
+    if acc_r and (stats is None or stats.dtype != torch.float64 or stats.numel() < 2 * Cout * acc_r):
+        raise ValueError('conv_fwd: acc_r needs an fp64 accumulator of 2 * Cout * acc_r elements')
     ext.conv_fwd(x.data_ptr(), w16.data_ptr(), y.data_ptr(), stats.data_ptr() if stats is not None else 0,
-                 N, H, W, Cin, Ho, Wo, Cout, _stream(x.device), wc if Cin == 4 else 0)
+                 N, H, W, Cin, Ho, Wo, Cout, _stream(x.device), wc if Cin == 4 else 0, int(acc_r))
     return y
 
 
@@ -1089,12 +1156,16 @@ def conv_dgrad(dy, w16, in_shape, wt=None, bn=None):
     dx = torch.empty((N, Cin, H, W), dtype=torch.bfloat16, device=dy.device, memory_format=cl)
     _count('conv_dgrad')
     if bn is not None and bn.ready(dx):
-        rows = int(ext.conv_dgrad_bn_rows(N, H, W, Cin))
-        part = torch.empty(2 * Cin * rows, dtype=torch.float32, device=dy.device)
         _count('conv_dgrad_bn')
+        if bn.acc is not None:
+            # add into the BN call's zeroed backward accumulator (no partial rows, no finalize)
+            part, acc_r, rows = bn.acc.bwd, bn.acc.R, -bn.acc.R
+        else:
+            acc_r, rows = 0, int(ext.conv_dgrad_bn_rows(N, H, W, Cin))
+            part = torch.empty(2 * Cin * rows, dtype=torch.float32, device=dy.device)
         ext.conv_dgrad(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), N, H, W, Cin, Cout, _stream(dy.device),
                        bn.x.data_ptr(), bn.mean.data_ptr(), bn.invstd.data_ptr(), bn.w.data_ptr(), bn.b.data_ptr(),
-                       bn.slope, part.data_ptr(), rows)
+                       bn.slope, part.data_ptr(), max(rows, 0), acc_r)
         bn.part, bn.rows, bn.gy = part, rows, dx
     else:
         ext.conv_dgrad(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), N, H, W, Cin, Cout, _stream(dy.device))
@@ -1149,6 +1220,8 @@ def _conv_function():
             ctx.set_materialize_grads(False)   # no zero-filled gradient for the stats output
             ctx.save_for_backward(x, w16)
             ctx.w32, ctx.wt, ctx.bn_link = w32, wt, bn_link
+            if isinstance(with_stats, BnAccumulator):
+                return conv_fwd(x, w16, with_stats.fwd, with_stats.R)
             if with_stats:
                 N, _, H, W = x.shape
                 M = N * ((H - 2) // 2 + 1) * ((W - 2) // 2 + 1)
@@ -1198,7 +1271,8 @@ def conv4x4s2(x, w32, w16, with_stats=False, wt=None, bn_link=None):
     bf16 copy ``w16`` of fp32 weight ``w32``; the gradient goes to ``w32``
     (fp32, from the MFMA weight-gradient kernel).  See :func:`conv_wgrad_supported`.
     ``with_stats``: return ``(y, stats)``, the per-tile BatchNorm sums of y
-    from the forward kernel's epilogue (for ``BatchNormLeakyReLU2d.forward_from_stats``).
+    from the forward kernel's epilogue (for ``BatchNormLeakyReLU2d.forward_from_stats``);
+    or a :class:`BnAccumulator` that the epilogue adds the sums into (returns y only).
     ``bn_link``: the :class:`BnLink` of the BatchNorm+LeakyReLU that produced
     ``x``; the data gradient then also computes that BN's backward sums."""
     global _CONV_FN
@@ -1218,7 +1292,7 @@ def _head_function():
 
     class _DiscHeadBCE(torch.autograd.Function):
         @staticmethod
-        def forward(ctx, z, w, target, oh, ow):
+        def forward(ctx, z, w, target, oh, ow, bn_link=None):
             ctx.set_materialize_grads(False)   # no zero-filled gradient for the logits output
             ext = hip_ext()
             N, C, H, W = z.shape
@@ -1237,9 +1311,10 @@ def _head_function():
             _count('head_forward')
             ext.head_forward(z.data_ptr(), w.data_ptr(), w.stride(1), w.stride(2), w.stride(3), N, H, W, C, oh, ow,
                              tptr, tval, pooled.data_ptr(), partial.data_ptr(), loss.data_ptr(), dlogit.data_ptr(),
-                             logit.data_ptr(), _stream(dev))
+                             logit.data_ptr(), _stream(dev), _head_ticket(dev).data_ptr())
             ctx.save_for_backward(w, pooled, dlogit)
             ctx.wparam = w
+            ctx.bn_link = bn_link
             ctx.zshape, ctx.pool = (N, C, H, W), (oh, ow)
             ctx.mark_non_differentiable(logit)
             return loss, logit
@@ -1247,7 +1322,7 @@ def _head_function():
         @staticmethod
         def backward(ctx, gloss, glogit=None):
             if gloss is None:
-                return None, None, None, None, None
+                return None, None, None, None, None, None
             ext = hip_ext()
             w, pooled, dlogit = ctx.saved_tensors
             N, C, H, W = ctx.zshape
@@ -1258,10 +1333,21 @@ def _head_function():
             if dw.stride() != w.stride():
                 dw, sunk = torch.empty_like(w), False
             _count('head_backward')
-            ext.head_backward(w.data_ptr(), w.stride(1), w.stride(2), w.stride(3), N, H, W, C, oh, ow,
-                              pooled.data_ptr(), dlogit.data_ptr(), g.data_ptr(), dz.data_ptr(), dw.data_ptr(),
-                              _stream(w.device))
-            return dz, None if sunk else dw, None, None, None
+            bn = ctx.bn_link
+            if bn is not None and bn.acc is not None and bn.ready(dz) and (C // 8) <= 256 and 256 % (C // 8) == 0:
+                # dz is the gy of the BN+LeakyReLU that produced z: sum its backward
+                # statistics here, into the BN call's accumulator
+                _count('head_backward_bn')
+                ext.head_backward(w.data_ptr(), w.stride(1), w.stride(2), w.stride(3), N, H, W, C, oh, ow,
+                                  pooled.data_ptr(), dlogit.data_ptr(), g.data_ptr(), dz.data_ptr(), dw.data_ptr(),
+                                  _stream(w.device), bn.x.data_ptr(), bn.mean.data_ptr(), bn.invstd.data_ptr(),
+                                  bn.w.data_ptr(), bn.b.data_ptr(), bn.slope, bn.acc.bwd.data_ptr(), bn.acc.R)
+                bn.part, bn.rows, bn.gy = bn.acc.bwd, -bn.acc.R, dz
+            else:
+                ext.head_backward(w.data_ptr(), w.stride(1), w.stride(2), w.stride(3), N, H, W, C, oh, ow,
+                                  pooled.data_ptr(), dlogit.data_ptr(), g.data_ptr(), dz.data_ptr(), dw.data_ptr(),
+                                  _stream(w.device))
+            return dz, None if sunk else dw, None, None, None, None
 
     return _DiscHeadBCE
 
@@ -1269,12 +1355,28 @@ def _head_function():
 _HEAD_FN = None
 
 
-def disc_head_bce(z, w, target=1.0, pool=(4, 4)):
+_HEAD_TICKETS = {}
+
+
+def _head_ticket(dev):
+    """The zeroed ticket word the one-launch head forward hands its partial
+    logits over with (reset by the kernel's last block)."""
+    import torch
+    t = _HEAD_TICKETS.get(dev)
+    if t is None:
+        t = _HEAD_TICKETS[dev] = torch.zeros(4, dtype=torch.int32, device=dev)
+    return t
+
+
+def disc_head_bce(z, w, target=1.0, pool=(4, 4), bn_link=None):
     """``BCELoss()(sigmoid(conv2d(adaptive_avg_pool2d(z, pool), w)).view(-1), target)``
     for a head conv that consumes the whole pooled map (``w``: fp32
     [1, C, pool_h, pool_w]); ``z`` bf16 channels-last [N, C, H, W] on the GPU.
     Returns ``(loss, logits)``; gradients flow to ``z`` (bf16) and ``w``
-    (fp32).  Pool, dot products and loss run in fp32."""
+    (fp32).  Pool, dot products and loss run in fp32.  ``bn_link``: the
+    :class:`BnLink` of the BatchNorm+LeakyReLU that produced ``z`` (in
+    accumulator mode): the backward then also sums that BN's backward
+    statistics."""
     import torch
     global _HEAD_FN
     if _HEAD_FN is None:
@@ -1284,7 +1386,7 @@ def disc_head_bce(z, w, target=1.0, pool=(4, 4)):
         raise ValueError('disc_head_bce needs bf16 channels-last GPU features')
     if tuple(w.shape) != (1, z.shape[1], oh, ow) or w.dtype != torch.float32 or z.shape[1] % 8:
         raise ValueError(f'disc_head_bce: weight {tuple(w.shape)} {w.dtype} does not fit features {tuple(z.shape)}')
-    return _HEAD_FN.apply(z, w, target, oh, ow)
+    return _HEAD_FN.apply(z, w, target, oh, ow, bn_link)
 
 
 def __getattr__(name):

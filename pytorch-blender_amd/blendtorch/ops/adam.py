@@ -13,7 +13,17 @@ optimizer (it writes the device copy the schedule kernel reads).
 
 Optional ``bf16_shadow``: the update also writes a bf16 copy of every new
 weight (``shadow(p)``), which a bf16 forward can read instead of casting the
-fp32 master weights on every step.
+fp32 master weights on every step.  :meth:`FusedAdam.enable_conv_shadows`
+adds, for 4x4 convolution weights, the transposed bf16 copy a data-gradient
+kernel reads (``shadow_t(p)``, ``conv_weights_t`` layout) -- the consumer
+step's per-step cast and transpose launches then disappear.
+
+One launch per step where a group fits one launch (<= 32 tensors): every
+block of the update kernel works the schedule out itself and the last block
+to finish stores the counter (no ``adam_schedule`` launch).
+:meth:`set_zero_grads` makes the update clear each gradient after reading it,
+so persistent gradient buffers (``parallel.GradBuckets``) need no zero-fill
+launch before the next backward.
 
 Data parallel: ``grad_scale`` multiplies every gradient inside the update
 kernel, so a summing all-reduce of the gradients (``parallel.GradBuckets``)
@@ -51,6 +61,8 @@ class FusedAdam(torch.optim.Optimizer):
         # id(group) -> device scalars (kept out of param_groups / state_dict).
         # Each entry holds its group, so an id cannot be reused while it lives.
         self._dev = {}
+        self._zero_grads = False
+        self._one_launch = True
 
     # -- per-group device scalars ------------------------------------------
     def _group_state(self, group):
@@ -65,6 +77,7 @@ class FusedAdam(torch.optim.Optimizer):
             gs = {'step': step, 'group': group,
                   'hp': torch.tensor([float(group['lr']), self._grad_scale], dtype=torch.float32, device=dev),
                   'sched': torch.zeros(5, dtype=torch.float32, device=dev),
+                  'ticket': torch.zeros(4, dtype=torch.int32, device=dev),
                   'lr': float(group['lr']), 'grad_scale': self._grad_scale}
             self._dev[id(group)] = gs
             for p in group['params']:
@@ -111,8 +124,47 @@ class FusedAdam(torch.optim.Optimizer):
         return st
 
     def shadow(self, p):
-        """The bf16 copy of ``p`` the last update wrote (``bf16_shadow=True``)."""
+        """The bf16 copy of ``p`` the last update wrote (``bf16_shadow=True``
+        or :meth:`enable_conv_shadows`)."""
         return self.state[p]['shadow']
+
+    def shadow_t(self, p):
+        """The transposed bf16 copy of conv weight ``p`` (:meth:`enable_conv_shadows`)."""
+        return self.state[p]['shadow_t']
+
+    def enable_conv_shadows(self, weights):
+        """Keep, for each fp32 4x4 convolution weight in ``weights`` (channels-
+        last [Cout, Cin, 4, 4], on the GPU), a bf16 copy and its data-gradient
+        transpose up to date: made now from the current weights and rewritten
+        by every update.  A weight changed outside this optimizer (e.g. a
+        model ``load_state_dict``) needs :meth:`refresh_shadows`."""
+        from . import conv_weights_t
+        found = {id(p) for g in self.param_groups for p in g['params']}
+        for p in weights:
+            if id(p) not in found:
+                raise ValueError('enable_conv_shadows: a weight is not a parameter of this optimizer')
+            if not (p.is_cuda and p.dtype == torch.float32 and p.dim() == 4 and tuple(p.shape[2:]) == (4, 4)
+                    and p.is_contiguous(memory_format=torch.channels_last)):
+                raise ValueError('enable_conv_shadows: needs channels-last fp32 [Cout, Cin, 4, 4] GPU weights')
+            st = self.state[p]
+            st['shadow'] = p.detach().to(torch.bfloat16)
+            st['shadow_t'] = conv_weights_t([st['shadow']])[0]
+
+    def refresh_shadows(self):
+        """Rewrite every bf16 shadow from the current fp32 weights."""
+        from . import conv_weights_t
+        for g in self.param_groups:
+            for p in g['params']:
+                st = self.state.get(p, {})
+                if 'shadow' in st:
+                    st['shadow'].copy_(p.detach())
+                if 'shadow_t' in st:
+                    st['shadow_t'].copy_(conv_weights_t([st['shadow']])[0])
+
+    def set_zero_grads(self, on=True):
+        """Clear every (fp32) gradient inside the update kernel after reading
+        it, also when a gate skips the step."""
+        self._zero_grads = bool(on)
 
     # -- step -----------------------------------------------------------------
     @torch.no_grad()
@@ -139,6 +191,9 @@ class FusedAdam(torch.optim.Optimizer):
                 self._step_gpu(group, gs, params, states, gate)
             else:
                 self._step_reference(group, gs, params, states, gate)
+                if self._zero_grads:
+                    for p in params:
+                        p.grad.zero_()
         return loss
 
     def _step_gpu(self, group, gs, params, states, gate=None):
@@ -150,11 +205,14 @@ class FusedAdam(torch.optim.Optimizer):
             # exp_avg and exp_avg_sq share it (the state is allocated like p)
             if p.dtype != torch.float32 or not _dense(p):
                 raise ValueError('FusedAdam (GPU) needs dense fp32 parameters (contiguous or channels-last)')
-        _count('adam_schedule')
         if gate is not None and gate.dtype != torch.float32:
             raise ValueError('FusedAdam.step: gate must be float32 on the GPU')
-        ext.adam_schedule(gs['step'].data_ptr(), gs['hp'].data_ptr(), gs['sched'].data_ptr(), b1, b2, stream,
-                          gate.data_ptr() if gate is not None else 0)
+        one = self._one_launch and len(params) <= _MAX_PER_LAUNCH
+        if not one:
+            _count('adam_schedule')
+            ext.adam_schedule(gs['step'].data_ptr(), gs['hp'].data_ptr(), gs['sched'].data_ptr(), b1, b2, stream,
+                              gate.data_ptr() if gate is not None else 0)
+        zero = self._zero_grads and all(p.grad.dtype == torch.float32 for p in params)
         for i in range(0, len(params), _MAX_PER_LAUNCH):
             ps, ss = params[i:i + _MAX_PER_LAUNCH], states[i:i + _MAX_PER_LAUNCH]
             grads = []
@@ -166,12 +224,23 @@ class FusedAdam(torch.optim.Optimizer):
                     g = torch.empty_like(p, dtype=g.dtype).copy_(g)   # same memory order as the parameter
                 grads.append(g)
             _count('adam_update')
+            trans = any('shadow_t' in s for s in ss)
             ext.adam_update([p.data_ptr() for p in ps], [g.data_ptr() for g in grads],
                             [s['exp_avg'].data_ptr() for s in ss], [s['exp_avg_sq'].data_ptr() for s in ss],
                             [s['shadow'].data_ptr() if 'shadow' in s else 0 for s in ss],
                             [p.numel() for p in ps], gs['sched'].data_ptr(), int(grads[0].dtype == torch.bfloat16),
                             b1, b2, group['eps'], group['weight_decay'], int(group['decoupled']),
-                            int(group['maximize']), stream)
+                            int(group['maximize']), stream,
+                            step=gs['step'].data_ptr() if one else 0, hp=gs['hp'].data_ptr() if one else 0,
+                            gate=gate.data_ptr() if (one and gate is not None) else 0,
+                            ticket=gs['ticket'].data_ptr() if one else 0, zero_grad=int(zero),
+                            shadow_t=[s['shadow_t'].data_ptr() if 'shadow_t' in s else 0 for s in ss] if trans else [],
+                            tcout=[int(p.shape[0]) if 'shadow_t' in s else 0 for p, s in zip(ps, ss)] if trans else [],
+                            tcin=[int(p.shape[1]) if 'shadow_t' in s else 0 for p, s in zip(ps, ss)] if trans else [])
+            if zero:
+                for p, g in zip(ps, grads):
+                    if g is not p.grad:      # a re-strided copy was read and cleared: clear the real one
+                        p.grad.zero_()
 
     @staticmethod
     def _step_reference(group, gs, params, states, gate=None):
@@ -201,3 +270,6 @@ class FusedAdam(torch.optim.Optimizer):
             p.addcdiv_(st['exp_avg'], st['exp_avg_sq'].sqrt().mul_(inv_bc2).add_(group['eps']), value=-step_size)
             if 'shadow' in st:
                 st['shadow'].copy_(p)
+            if 'shadow_t' in st:
+                from . import conv_weights_t
+                st['shadow_t'].copy_(conv_weights_t([st['shadow']])[0])

@@ -125,11 +125,21 @@ class CapturedStep:
         active = bool(allreduce) and dist.is_available() and dist.is_initialized() and (
             dist.get_world_size(group) > 1 or allreduce == 'always')
         self._legacy = active and not buckets
+        self._memset = True
+        self._seed = None
+        # persistent gradient buckets: always for a collective; without one too
+        # when the optimizer clears the gradients it consumes (ops.FusedAdam):
+        # then the step needs neither per-step gradient allocations nor a fill
+        zeroing = hasattr(optimizer, 'set_zero_grads')
+        if buckets and (active or zeroing):
+            from .grads import GradBuckets
+            self.grads = GradBuckets(model.parameters(), bucket_mb=bucket_mb)
+            if zeroing:
+                optimizer.set_zero_grads(True)
+                self._memset = False
         if active and buckets:
             from .comm import DeviceComm
-            from .grads import GradBuckets
             self.comm = comm if comm is not None else DeviceComm(group, dedicated=True)
-            self.grads = GradBuckets(model.parameters(), bucket_mb=bucket_mb)
             if hasattr(optimizer, 'set_grad_scale'):
                 optimizer.set_grad_scale(1.0 / self.comm.world)   # folded into the update kernel
             else:
@@ -137,13 +147,18 @@ class CapturedStep:
 
     def _forward(self, x):
         if self.grads is not None:
-            self.grads.zero_()
+            self.grads.zero_(memset=self._memset)
         else:
             self.opt.zero_grad(set_to_none=True)
         return self.loss_fn(self.model, x)
 
     def _backward(self, loss):
-        loss.backward()
+        # the backward's seed gradient: one persistent tensor of ones, not a
+        # fill kernel per step
+        if self._seed is None or self._seed.shape != loss.shape or self._seed.device != loss.device \
+                or self._seed.dtype != loss.dtype:
+            self._seed = torch.ones_like(loss)
+        loss.backward(self._seed)
         if self.grads is not None and self.comm is not None:
             self.collectives = self.grads.all_reduce(self.comm, self._op)
         elif self._legacy:

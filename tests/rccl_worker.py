@@ -53,6 +53,9 @@ def main(path):
             res['state'] = step.state
             res['error'] = step.error
     res['max_abs_diff'] = max(float((p - q).abs().max()) for p, q in zip(nets[0].parameters(), nets[1].parameters()))
+    d = torch.cat([(p - q).detach().abs().flatten() for p, q in zip(nets[0].parameters(), nets[1].parameters())])
+    res['mean_abs_diff'] = float(d.mean())
+    res['frac_above_half_lr'] = float((d > 1e-4).float().mean())
     Path(path).write_text(json.dumps(res))
     dist.destroy_process_group()
 

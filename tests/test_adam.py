@@ -274,3 +274,92 @@ def test_gpu_grad_scale_and_gate_in_graph(dev):
     assert float(ours.state[next(a.parameters())]['step']) == 4
     for pa, pb in zip(a.parameters(), b.parameters()):
         torch.testing.assert_close(pa.detach().cpu(), pb.detach(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_gpu_one_launch_zero_grads_and_conv_shadows(dev):
+    """One update launch per step (the schedule worked out in-kernel, the last
+    block storing the counter), gradients cleared after use (also behind a
+    closed gate), and the bf16 conv-weight shadow plus its data-gradient
+    transpose kept equal to cast + conv_weights_t of the new weights --
+    eager and replayed from a graph."""
+    a, b = _model(device=dev), _model()
+    a = a.to(memory_format=torch.channels_last)
+    ours = ops.FusedAdam(a.parameters(), lr=1e-2, betas=(0.8, 0.95))
+    ref = ops.FusedAdam(b.parameters(), lr=1e-2, betas=(0.8, 0.95))
+    conv = [m.weight for m in a if isinstance(m, torch.nn.Conv2d) and tuple(m.kernel_size) == (4, 4)]
+    ours.enable_conv_shadows(conv)
+    ours.set_zero_grads(True)
+    grads = [torch.zeros_like(p) for p in a.parameters()]
+    for p, g in zip(a.parameters(), grads):
+        p.grad = g
+    gate = torch.ones(1, device=dev)
+
+    def feed(k):
+        _grads(b, k)
+        for g, q in zip(grads, b.parameters()):
+            g.copy_(q.grad)
+
+    before = (ops.KERNEL_CALLS.get('adam_update', 0), ops.KERNEL_CALLS.get('adam_schedule', 0))
+    feed(0)
+    ours.step(gate=gate)
+    ref.step()
+    assert ops.KERNEL_CALLS['adam_update'] == before[0] + 1
+    assert ops.KERNEL_CALLS.get('adam_schedule', 0) == before[1]          # no schedule launch
+    assert all(int(torch.count_nonzero(g)) == 0 for g in grads)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        ours.step(gate=gate)
+    steps = 1
+    for k in range(1, 8):
+        feed(k)
+        open_ = k % 3 != 0
+        gate.fill_(1.0 if open_ else 0.0)
+        graph.replay()
+        if open_:
+            ref.step()
+            steps += 1
+        torch.cuda.synchronize()
+        assert all(int(torch.count_nonzero(g)) == 0 for g in grads), k    # consumed, also when gated
+    assert float(ours.state[next(a.parameters())]['step']) == steps
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        torch.testing.assert_close(pa.detach().cpu(), pb.detach(), rtol=1e-5, atol=1e-6)
+    for w in conv:
+        w16 = w.detach().to(torch.bfloat16)
+        assert torch.equal(ours.shadow(w), w16)
+        assert torch.equal(ours.shadow_t(w), ops.conv_weights_t([w16])[0])
+
+
+@pytest.mark.gpu
+def test_gpu_discriminator_step_with_optimizer_shadows(dev):
+    """The bench's disc step with the conv weights read from FusedAdam's
+    shadows (no cast / transpose launches) and persistent gradient buckets
+    cleared by the update (no fill) trains like the cast-every-step path."""
+    from blendtorch.models import Discriminator
+    from blendtorch.parallel.step import CapturedStep
+    cl = torch.channels_last
+    g = torch.Generator(device=dev).manual_seed(3)
+    xs = [torch.rand(4, 4, 96, 128, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+          for _ in range(4)]
+    nets = []
+    for shadow in (False, True):
+        torch.manual_seed(0)
+        m = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
+        opt = ops.FusedAdam(m.parameters(), lr=2e-4)
+        if shadow:
+            m.use_optimizer_shadows(opt)
+        step = CapturedStep(m, opt, lambda mm, x: mm.bce_loss_bf16(x, 1.0), allreduce=False, graph=True,
+                            buckets=shadow)
+        casts = ops.KERNEL_CALLS.get('multi_cast', 0)
+        for x in xs:
+            step(x)
+        torch.cuda.synchronize()
+        assert step.state == 'graph'
+        if shadow:
+            assert ops.KERNEL_CALLS.get('multi_cast', 0) == casts    # no per-step weight casts captured
+            assert step.grads is not None
+        nets.append(m)
+    lr = 2e-4
+    for pa, pb in zip(nets[0].parameters(), nets[1].parameters()):
+        d = (pb - pa).detach().abs()
+        assert float(d.mean()) < 0.15 * lr and float((d > 0.5 * lr).float().mean()) < 0.03

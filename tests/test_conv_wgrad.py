@@ -197,11 +197,11 @@ def test_bn_backward_sums_from_dgrad_epilogue(dev, monkeypatch):
     x = torch.rand(4, 4, 96, 128, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     before = ops.KERNEL_CALLS.get('bn_backward_from_stats', 0)
     a.bce_loss_bf16(x, 1.0).backward()
-    # BN1..BN3 feed conv2..conv4 (BN4 feeds the head)
-    assert ops.KERNEL_CALLS.get('bn_backward_from_stats', 0) == before + 3
+    # BN1..BN3 feed conv2..conv4, BN4 the fused head: all four take their sums from the consumer
+    assert ops.KERNEL_CALLS.get('bn_backward_from_stats', 0) == before + 4
     monkeypatch.setattr(ops.BnLink, 'ready', lambda self, dx: False)
     b.bce_loss_bf16(x, 1.0).backward()
-    assert ops.KERNEL_CALLS.get('bn_backward_from_stats', 0) == before + 3
+    assert ops.KERNEL_CALLS.get('bn_backward_from_stats', 0) == before + 4
     for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
         torch.testing.assert_close(pa.grad, pb.grad, rtol=2e-2, atol=2e-2 * float(pb.grad.abs().max()), msg=n)
 
@@ -253,3 +253,42 @@ def test_tap_gemm_tile_variants(dev, tiles):
     a.bce_loss_bf16(xin, 1.0).backward()
     for (n, p), g0 in zip(a.named_parameters(), got):
         torch.testing.assert_close(g0, p.grad, rtol=2e-2, atol=2e-2 * float(p.grad.abs().max()), msg=n)
+
+
+@pytest.mark.gpu
+def test_bn_accumulators_fold_and_clear(dev, monkeypatch):
+    """Accumulator hand-off (BnAccumulator): the conv epilogues add BN sums
+    into zeroed accumulators that the apply kernels fold and clear -- same
+    loss, gradients and running statistics as the partial-row + finalize
+    path, over several steps, and every accumulator is zero after each step."""
+    from blendtorch.models import Discriminator
+    torch.manual_seed(7)
+    cl = torch.channels_last
+    a = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
+    b = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
+    b.load_state_dict(a.state_dict())
+    x = torch.rand(4, 4, 96, 128, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    acc_supported = ops.bn_acc_supported
+    for step in range(3):
+        a.zero_grad(set_to_none=True)
+        b.zero_grad(set_to_none=True)
+        before = ops.KERNEL_CALLS.get('bn_forward_acc', 0), ops.KERNEL_CALLS.get('bn_backward_acc', 0)
+        la = a.bce_loss_bf16(x, 1.0)
+        la.backward()
+        # 4 BN layers forward; backward: BN1..3 from the dgrad epilogues, BN4 from the head's
+        assert ops.KERNEL_CALLS['bn_forward_acc'] == before[0] + 4
+        assert ops.KERNEL_CALLS['bn_backward_acc'] == before[1] + 4
+        monkeypatch.setattr(ops, 'bn_acc_supported', lambda C: False)
+        lb = b.bce_loss_bf16(x, 1.0)
+        lb.backward()
+        monkeypatch.setattr(ops, 'bn_acc_supported', acc_supported)
+        torch.testing.assert_close(la, lb, rtol=1e-3, atol=1e-4)
+        for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+            torch.testing.assert_close(pa.grad, pb.grad, rtol=2e-2, atol=2e-2 * float(pb.grad.abs().max()), msg=n)
+        for ma, mb in zip(a.modules(), b.modules()):
+            if isinstance(ma, ops.BatchNormLeakyReLU2d):
+                torch.testing.assert_close(ma.running_mean, mb.running_mean, rtol=1e-3, atol=1e-5)
+                torch.testing.assert_close(ma.running_var, mb.running_var, rtol=1e-3, atol=1e-5)
+                assert int(ma.num_batches_tracked) == int(mb.num_batches_tracked) == step + 1
+                for acc in ma.__dict__['_bt_acc_ring'][0]:
+                    assert int(torch.count_nonzero(acc.fwd)) == 0 and int(torch.count_nonzero(acc.bwd)) == 0
