@@ -129,7 +129,8 @@ def _pool_worker(rank, world, port, prod_port, q):
             addrs = parallel.pool_addresses(bl.launch_info.addresses['DATA'])
             ds = btt.RemoteIterableDataset(addrs, max_items=40, timeoutms=30000)
             import time
-            time.sleep(1.0)            # both ranks connected before frames flow
+            torch.distributed.barrier()   # both ranks' producers launched (a loaded host starts them late)
+            time.sleep(2.0)               # both ranks connected before frames flow
             sources = [int(item['frameid']) // 1000 for item in ds]   # which rank's producer
             torch.distributed.barrier()   # keep producers alive until both ranks are done
         q.put((rank, len(addrs), sorted(set(sources)), len(sources)))
