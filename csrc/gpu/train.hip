@@ -570,7 +570,7 @@ int bn_acc_replicas(int C) {
 
 int64_t bn_acc_elems(int C) {
   const int r = bn_acc_replicas(C);
-  return r > 0 ? int64_t(2) * C * r : -1;
+  return r > 0 ? int64_t(2) * C * r + 2 : -1;   // + the producer-finalize ticket (bn_acc.h), 16-byte padded
 }
 
 hipError_t bn_apply_acc(const void* x, void* y, int64_t M, int C, int dtype, BnAcc acc, float eps, float momentum,
@@ -696,55 +696,37 @@ __global__ void adam_schedule_kernel(float* step, const float* hp, float* sched,
 template <bool GBF16>
 __global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
   const int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x;   // 4-element group
-  float step_size, inv_bc2, lr, gscale;
-  bool active;
-  if (a.step) {
-    // one-launch schedule: lane 0 reads the counter, works out the bias
-    // corrections and shares them; it has read the counter before it takes
-    // its ticket, so the block taking the last ticket may store the new value
-    __shared__ float sh[5];
-    if (threadIdx.x == 0) {
-      const bool on = !a.gate || a.gate[0] != 0.f;
-      const float s = a.step[0] + 1.f;
-      const double bc1 = 1.0 - pow(double(a.beta1), double(s));
-      const double bc2 = 1.0 - pow(double(a.beta2), double(s));
-      sh[0] = float(double(a.hp[0]) / bc1);
-      sh[1] = float(1.0 / sqrt(bc2));
-      sh[2] = a.hp[0];
-      sh[3] = a.hp[1];
-      sh[4] = on ? 1.f : 0.f;
-      const uint32_t tk = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (tk == gridDim.x - 1) {
-        if (on) a.step[0] = s;
-        __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    __syncthreads();
-    step_size = sh[0], inv_bc2 = sh[1], lr = sh[2], gscale = sh[3], active = sh[4] != 0.f;
-  } else {
-    step_size = a.sched[0], inv_bc2 = a.sched[1], lr = a.sched[2], gscale = a.sched[3];
-    active = a.sched[4] != 0.f;
-  }
-  if (q >= a.gstart[a.n]) return;
+  const bool in = q < a.gstart[a.n];
   int k = 0;
-  while (q >= a.gstart[k + 1]) ++k;     // <= kMaxAdam compares, mostly uniform across a wave
-  const int64_t e0 = (q - a.gstart[k]) * 4;
-  const int64_t n = a.numel[k];
-  const bool full = e0 + 4 <= n;   // tensors are 16-byte aligned (host-checked), so a full group is one dwordx4
-  if (!active) {   // a closed gate: nothing moves, but the gradients are still consumed
-    if (a.zero_grad) {
-      float* G = static_cast<float*>(const_cast<void*>(a.g[k]));
-      if (full) *reinterpret_cast<float4*>(G + e0) = make_float4(0.f, 0.f, 0.f, 0.f);
-      else for (int j = 0; j < 4 && e0 + j < n; ++j) G[e0 + j] = 0.f;
-    }
-    return;
+  if (in)
+    while (q >= a.gstart[k + 1]) ++k;     // <= kMaxAdam compares, mostly uniform across a wave
+  const int64_t gi = in ? q - a.gstart[k] : 0;
+  // element offset of the group.  A tensor with a transposed shadow starts
+  // on a block boundary and is walked in 32 x 32 (co, ci) tiles of one tap,
+  // a block per tile: lane t = row t / 8 (co), 4 input channels 4 (t % 8) --
+  // 128-byte runs in, and through an LDS transpose 64-byte runs of the
+  // [ci][tap][co] shadow out.
+  int64_t e0 = gi * 4;
+  uint16_t* T = in ? a.shadow_t[k] : nullptr;   // block-uniform (host-checked tiling)
+  int tco0 = 0, ttap = 0, tci0 = 0;
+  if (T) {
+    const int cin = a.tcin[k], cit = cin >> 5;
+    const int tile = int(gi >> 8), t = int(threadIdx.x);
+    tci0 = (tile % cit) * 32;
+    ttap = (tile / cit) & 15;
+    tco0 = (tile / (cit * 16)) * 32;
+    e0 = (int64_t(tco0 + (t >> 3)) * 16 + ttap) * cin + tci0 + 4 * (t & 7);
   }
-  const float b1 = a.beta1, b2 = a.beta2, wd = a.weight_decay;
-  float* P = a.p[k];
-  float* M = a.m[k];
-  float* V = a.v[k];
-  float pv[4], gv[4], mv[4], vv[4];
-  if (full) {
+  const int64_t n = in ? a.numel[k] : 0;
+  const bool full = e0 + 4 <= n;   // tensors are 16-byte aligned (host-checked), so a full group is one dwordx4
+  float* P = in ? a.p[k] : nullptr;
+  float* M = in ? a.m[k] : nullptr;
+  float* V = in ? a.v[k] : nullptr;
+  float pv[4] = {0.f, 0.f, 0.f, 0.f}, gv[4] = {0.f, 0.f, 0.f, 0.f}, mv[4] = {0.f, 0.f, 0.f, 0.f},
+        vv[4] = {0.f, 0.f, 0.f, 0.f};
+  // every load is issued before the schedule below (its fp64 math and the
+  // block barrier then overlap the memory latency)
+  if (in && full) {
     const float4 p4 = *reinterpret_cast<const float4*>(P + e0);
     const float4 m4 = *reinterpret_cast<const float4*>(M + e0);
     const float4 v4 = *reinterpret_cast<const float4*>(V + e0);
@@ -758,59 +740,101 @@ __global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
     } else {
       const float4 g4 = *reinterpret_cast<const float4*>(static_cast<const float*>(a.g[k]) + e0);
       gv[0] = g4.x, gv[1] = g4.y, gv[2] = g4.z, gv[3] = g4.w;
-      if (a.zero_grad)
-        *reinterpret_cast<float4*>(static_cast<float*>(const_cast<void*>(a.g[k])) + e0) = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-  } else {
+  } else if (in) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const bool in = e0 + j < n;
-      pv[j] = in ? P[e0 + j] : 0.f;
-      mv[j] = in ? M[e0 + j] : 0.f;
-      vv[j] = in ? V[e0 + j] : 0.f;
+      const bool ok = e0 + j < n;
+      pv[j] = ok ? P[e0 + j] : 0.f;
+      mv[j] = ok ? M[e0 + j] : 0.f;
+      vv[j] = ok ? V[e0 + j] : 0.f;
       if constexpr (GBF16)
-        gv[j] = in ? __uint_as_float(uint32_t(static_cast<const uint16_t*>(a.g[k])[e0 + j]) << 16) : 0.f;
+        gv[j] = ok ? __uint_as_float(uint32_t(static_cast<const uint16_t*>(a.g[k])[e0 + j]) << 16) : 0.f;
       else
-        gv[j] = in ? static_cast<const float*>(a.g[k])[e0 + j] : 0.f;
+        gv[j] = ok ? static_cast<const float*>(a.g[k])[e0 + j] : 0.f;
     }
-    if (!GBF16 && a.zero_grad)
-      for (int j = 0; j < 4 && e0 + j < n; ++j) static_cast<float*>(const_cast<void*>(a.g[k]))[e0 + j] = 0.f;
   }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    float g = (a.maximize ? -gv[j] : gv[j]) * gscale;
-    if (wd != 0.f) {
-      if (a.decoupled) pv[j] *= 1.f - lr * wd;
-      else g += wd * pv[j];
+  float step_size, inv_bc2, lr, gscale;
+  bool active;
+  float s_new = 0.f;
+  if (a.step) {
+    // one-launch schedule: lane 0 reads the counter, works out the bias
+    // corrections and shares them; it reads the counter before it takes its
+    // ticket (end of the kernel), so the block taking the last ticket may
+    // store the new value
+    __shared__ float sh[5];
+    if (threadIdx.x == 0) {
+      const bool on = !a.gate || a.gate[0] != 0.f;
+      s_new = a.step[0] + 1.f;
+      const double bc1 = 1.0 - pow(double(a.beta1), double(s_new));
+      const double bc2 = 1.0 - pow(double(a.beta2), double(s_new));
+      sh[0] = float(double(a.hp[0]) / bc1);
+      sh[1] = float(1.0 / sqrt(bc2));
+      sh[2] = a.hp[0];
+      sh[3] = a.hp[1];
+      sh[4] = on ? 1.f : 0.f;
     }
-    mv[j] = b1 * mv[j] + (1.f - b1) * g;
-    vv[j] = b2 * vv[j] + (1.f - b2) * g * g;
-    pv[j] -= step_size * mv[j] / (sqrtf(vv[j]) * inv_bc2 + a.eps);
-  }
-  uint16_t* S = a.shadow[k];
-  if (full) {
-    *reinterpret_cast<float4*>(P + e0) = make_float4(pv[0], pv[1], pv[2], pv[3]);
-    *reinterpret_cast<float4*>(M + e0) = make_float4(mv[0], mv[1], mv[2], mv[3]);
-    *reinterpret_cast<float4*>(V + e0) = make_float4(vv[0], vv[1], vv[2], vv[3]);
-    if (S) {
-      uint2 s2;
-      s2.x = uint32_t(f2bf(pv[0])) | (uint32_t(f2bf(pv[1])) << 16);
-      s2.y = uint32_t(f2bf(pv[2])) | (uint32_t(f2bf(pv[3])) << 16);
-      *reinterpret_cast<uint2*>(S + e0) = s2;
-    }
+    __syncthreads();
+    step_size = sh[0], inv_bc2 = sh[1], lr = sh[2], gscale = sh[3], active = sh[4] != 0.f;
   } else {
-    for (int j = 0; j < 4 && e0 + j < n; ++j) {
-      P[e0 + j] = pv[j], M[e0 + j] = mv[j], V[e0 + j] = vv[j];
-      if (S) S[e0 + j] = f2bf(pv[j]);
+    step_size = a.sched[0], inv_bc2 = a.sched[1], lr = a.sched[2], gscale = a.sched[3];
+    active = a.sched[4] != 0.f;
+  }
+  if (in) {
+    if (!GBF16 && a.zero_grad) {   // consumed (also when a closed gate skips the update)
+      float* G = static_cast<float*>(const_cast<void*>(a.g[k]));
+      if (full) *reinterpret_cast<float4*>(G + e0) = make_float4(0.f, 0.f, 0.f, 0.f);
+      else for (int j = 0; j < 4 && e0 + j < n; ++j) G[e0 + j] = 0.f;
+    }
+    if (active) {
+      const float b1 = a.beta1, b2 = a.beta2, wd = a.weight_decay;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float g = (a.maximize ? -gv[j] : gv[j]) * gscale;
+        if (wd != 0.f) {
+          if (a.decoupled) pv[j] *= 1.f - lr * wd;
+          else g += wd * pv[j];
+        }
+        mv[j] = b1 * mv[j] + (1.f - b1) * g;
+        vv[j] = b2 * vv[j] + (1.f - b2) * g * g;
+        pv[j] -= step_size * mv[j] / (sqrtf(vv[j]) * inv_bc2 + a.eps);
+      }
+      uint16_t* S = a.shadow[k];
+      if (full) {
+        *reinterpret_cast<float4*>(P + e0) = make_float4(pv[0], pv[1], pv[2], pv[3]);
+        *reinterpret_cast<float4*>(M + e0) = make_float4(mv[0], mv[1], mv[2], mv[3]);
+        *reinterpret_cast<float4*>(V + e0) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+        if (S) {
+          uint2 s2;
+          s2.x = uint32_t(f2bf(pv[0])) | (uint32_t(f2bf(pv[1])) << 16);
+          s2.y = uint32_t(f2bf(pv[2])) | (uint32_t(f2bf(pv[3])) << 16);
+          *reinterpret_cast<uint2*>(S + e0) = s2;
+        }
+      } else {
+        for (int j = 0; j < 4 && e0 + j < n; ++j) {
+          P[e0 + j] = pv[j], M[e0 + j] = mv[j], V[e0 + j] = vv[j];
+          if (S) S[e0 + j] = f2bf(pv[j]);
+        }
+      }
+      if (T) {   // (co, tap, ci) -> [ci][tap][co] through LDS (T, active: block-uniform)
+        __shared__ uint16_t tl[32][34];
+        const int t = int(threadIdx.x), cout = a.tcout[k];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) tl[4 * (t & 7) + j][t >> 3] = f2bf(pv[j]);
+        __syncthreads();
+        const int rr = t >> 3, cc = 4 * (t & 7);
+        uint2 o;
+        o.x = uint32_t(tl[rr][cc]) | (uint32_t(tl[rr][cc + 1]) << 16);
+        o.y = uint32_t(tl[rr][cc + 2]) | (uint32_t(tl[rr][cc + 3]) << 16);
+        *reinterpret_cast<uint2*>(T + (int64_t(tci0 + rr) * 16 + ttap) * cout + tco0 + cc) = o;
+      }
     }
   }
-  uint16_t* T = a.shadow_t[k];
-  if (T) {   // channels-last (co, tap, ci) -> (ci, tap, co)
-    const int cin = a.tcin[k], cout = a.tcout[k], kc = 16 * cin;
-    for (int j = 0; j < 4 && e0 + j < n; ++j) {
-      const int e = int(e0) + j;
-      const int co = e / kc, r = e - co * kc, tap = r / cin, ci = r - tap * cin;
-      T[(ci * 16 + tap) * cout + co] = f2bf(pv[j]);
+  if (a.step && threadIdx.x == 0) {
+    const uint32_t tk = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tk == gridDim.x - 1) {
+      if (active) a.step[0] = s_new;
+      __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -831,7 +855,8 @@ hipError_t adam_update(const AdamParams& p, hipStream_t stream) {
   if (p.zero_grad && p.grad_bf16) return hipErrorInvalidValue;
   if (p.gstart[0] != 0) return hipErrorInvalidValue;
   for (int k = 0; k < p.n; ++k) {
-    if (p.numel[k] < 0 || p.gstart[k + 1] - p.gstart[k] != (p.numel[k] + 3) / 4) return hipErrorInvalidValue;
+    // a tensor's group range may be padded (blocks never straddle tensors)
+    if (p.numel[k] < 0 || p.gstart[k + 1] - p.gstart[k] < (p.numel[k] + 3) / 4) return hipErrorInvalidValue;
     if (p.numel[k] > 0 && (!p.p[k] || !p.g[k] || !p.m[k] || !p.v[k])) return hipErrorInvalidValue;
     // full groups are read and written as 16-byte (8-byte for bf16) vectors
     const uintptr_t mis = reinterpret_cast<uintptr_t>(p.p[k]) | reinterpret_cast<uintptr_t>(p.m[k]) |
@@ -839,7 +864,10 @@ hipError_t adam_update(const AdamParams& p, hipStream_t stream) {
                           (reinterpret_cast<uintptr_t>(p.g[k]) << (p.grad_bf16 ? 1 : 0)) |
                           (reinterpret_cast<uintptr_t>(p.shadow[k]) << 1);
     if (mis & 15) return hipErrorInvalidValue;
-    if (p.shadow_t[k] && (p.tcout[k] <= 0 || p.tcin[k] <= 0 || int64_t(p.tcout[k]) * 16 * p.tcin[k] != p.numel[k]))
+    // transposed shadows: whole 32 x 32 tiles, one block each
+    if (p.shadow_t[k] && (p.tcout[k] <= 0 || p.tcin[k] <= 0 || p.tcout[k] % 32 || p.tcin[k] % 32 ||
+                          int64_t(p.tcout[k]) * 16 * p.tcin[k] != p.numel[k] || p.gstart[k] % kBlock ||
+                          p.gstart[k + 1] - p.gstart[k] != p.numel[k] / 4))
       return hipErrorInvalidValue;
   }
   const int64_t groups = p.gstart[p.n];

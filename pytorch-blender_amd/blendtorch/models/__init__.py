@@ -70,7 +70,8 @@ class Discriminator(nn.Module):
         if opt is not None:
             ws = [m.weight for m in self.features if isinstance(m, nn.Conv2d) and m.stride == (2, 2)
                   and tuple(m.kernel_size) == (4, 4)]
-            opt.enable_conv_shadows(ws)
+            # the first layer's input is the batch: no data gradient, no transpose
+            opt.enable_conv_shadows(ws, transpose=[i > 0 for i in range(len(ws))])
             self._shadow_opt = opt
 
     def forward_bf16(self, x, mfma=True):

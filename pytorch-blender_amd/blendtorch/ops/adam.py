@@ -18,9 +18,13 @@ adds, for 4x4 convolution weights, the transposed bf16 copy a data-gradient
 kernel reads (``shadow_t(p)``, ``conv_weights_t`` layout) -- the consumer
 step's per-step cast and transpose launches then disappear.
 
-One launch per step where a group fits one launch (<= 32 tensors): every
+``one_launch=True``: where a group fits one launch (<= 32 tensors) every
 block of the update kernel works the schedule out itself and the last block
-to finish stores the counter (no ``adam_schedule`` launch).
+to finish stores the counter (no ``adam_schedule`` launch).  Off by default:
+measured on the bench discriminator's 0.7 M parameters (scripts/adam_bench.py,
+graph replays) it is 3.7 us SLOWER than the two launches -- every block then
+waits on one lane's fp64 bias corrections behind a barrier, and on its
+ticket -- where the separate one-lane launch costs less than that.
 :meth:`set_zero_grads` makes the update clear each gradient after reading it,
 so persistent gradient buffers (``parallel.GradBuckets``) need no zero-fill
 launch before the next backward.
@@ -51,7 +55,7 @@ _MAX_PER_LAUNCH = 32   # kMaxAdam (csrc/gpu/kernels.h)
 
 class FusedAdam(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, decoupled=False,
-                 maximize=False, bf16_shadow=False, grad_scale=1.0):
+                 maximize=False, bf16_shadow=False, grad_scale=1.0, one_launch=False):
         if lr < 0 or eps < 0 or weight_decay < 0 or not (0 <= betas[0] < 1 and 0 <= betas[1] < 1):
             raise ValueError(f'invalid Adam hyper-parameters lr={lr} betas={betas} eps={eps} wd={weight_decay}')
         defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, decoupled=decoupled,
@@ -62,7 +66,7 @@ class FusedAdam(torch.optim.Optimizer):
         # Each entry holds its group, so an id cannot be reused while it lives.
         self._dev = {}
         self._zero_grads = False
-        self._one_launch = True
+        self._one_launch = bool(one_launch)
 
     # -- per-group device scalars ------------------------------------------
     def _group_state(self, group):
@@ -132,23 +136,32 @@ class FusedAdam(torch.optim.Optimizer):
         """The transposed bf16 copy of conv weight ``p`` (:meth:`enable_conv_shadows`)."""
         return self.state[p]['shadow_t']
 
-    def enable_conv_shadows(self, weights):
+    def enable_conv_shadows(self, weights, transpose=None):
         """Keep, for each fp32 4x4 convolution weight in ``weights`` (channels-
-        last [Cout, Cin, 4, 4], on the GPU), a bf16 copy and its data-gradient
+        last [Cout, Cin, 4, 4], on the GPU), a bf16 copy and -- where
+        ``transpose[i]`` (default: Cout and Cin multiples of 32) -- its data-gradient
         transpose up to date: made now from the current weights and rewritten
         by every update.  A weight changed outside this optimizer (e.g. a
         model ``load_state_dict``) needs :meth:`refresh_shadows`."""
         from . import conv_weights_t
         found = {id(p) for g in self.param_groups for p in g['params']}
-        for p in weights:
+        weights = list(weights)
+        if transpose is None:
+            transpose = [int(p.shape[0]) % 32 == 0 and int(p.shape[1]) % 32 == 0 for p in weights]
+        for p, tr in zip(weights, transpose):
             if id(p) not in found:
                 raise ValueError('enable_conv_shadows: a weight is not a parameter of this optimizer')
             if not (p.is_cuda and p.dtype == torch.float32 and p.dim() == 4 and tuple(p.shape[2:]) == (4, 4)
                     and p.is_contiguous(memory_format=torch.channels_last)):
                 raise ValueError('enable_conv_shadows: needs channels-last fp32 [Cout, Cin, 4, 4] GPU weights')
+            if tr and (int(p.shape[0]) % 32 or int(p.shape[1]) % 32):
+                raise ValueError('enable_conv_shadows: a transposed shadow needs Cout % 32 == Cin % 32 == 0')
             st = self.state[p]
             st['shadow'] = p.detach().to(torch.bfloat16)
-            st['shadow_t'] = conv_weights_t([st['shadow']])[0]
+            if tr:
+                st['shadow_t'] = conv_weights_t([st['shadow']])[0]
+            else:
+                st.pop('shadow_t', None)
 
     def refresh_shadows(self):
         """Rewrite every bf16 shadow from the current fp32 weights."""
