@@ -34,7 +34,6 @@
 #include <cstdlib>
 #include <cstdint>
 
-#include "bn_acc.h"
 #include "kernels.h"
 
 namespace btn {
@@ -513,7 +512,6 @@ struct TapGemm {
   int NOUT = 0, OH = 0, OW = 0;    // dst [N][OH][OW][NOUT]
   int wc = 0;                      // C4 mode: weight input channels (3 or 4)
   int acc_r = 0;                   // forward: > 0 = stats points at a BnAcc accumulator (fp64 [acc_r][2][NOUT])
-  BnFin fin;                       // fin.acc: the last block finalizes the accumulator (bn_acc.h)
   BnBwdFuse bn;                    // data gradient only: BN backward statistics in the epilogue (bn.part nullable)
 };
 
@@ -1044,10 +1042,6 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
       unsafeAtomicAdd(reinterpret_cast<double*>(p.stats) + ((mt % p.acc_r) * 2 + which) * p.NOUT + n0 + c, double(v));
     else p.stats[(which * p.NOUT + n0 + c) * ((p.M + BM - 1) / BM) + mt] = v;
   }
-  if (p.fin.acc) {   // every thread: the block that finishes last finalizes the BN statistics
-    __syncthreads();   // the statistics area (red) is read above; the tail reuses the LDS
-    bn_fin_tail(p.fin, reinterpret_cast<double*>(smem), reinterpret_cast<int*>(smem + 8192 + 64));
-  }
 }
 
 // several weights at once (blockIdx.y = tensor): the data gradients' operands for every layer in one launch
@@ -1231,14 +1225,6 @@ hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream) {
   g.wc = p.Cin == 4 ? (p.w_channels > 0 ? p.w_channels : 4) : p.Cin;
   g.acc_r = p.stats ? p.acc_r : 0;
   if (g.acc_r < 0 || g.acc_r > 64) return hipErrorInvalidValue;
-  if (g.acc_r > 0 && p.fin_mean) {
-    if (!p.fin_invstd || 2 * p.Cout > 1024) return hipErrorInvalidValue;
-    g.fin.acc = reinterpret_cast<double*>(p.stats);
-    g.fin.R = g.acc_r, g.fin.C = p.Cout, g.fin.M = p.M, g.fin.bwd = 0;
-    g.fin.eps = p.fin_eps, g.fin.momentum = p.fin_momentum;
-    g.fin.o0 = p.fin_mean, g.fin.o1 = p.fin_invstd;
-    g.fin.rm = p.fin_rm, g.fin.rv = p.fin_rv, g.fin.tracked = p.fin_tracked;
-  }
   if (p.Cin == 4 && g.wc != 3 && g.wc != 4) return hipErrorInvalidValue;
   launch_tap_gemm<false>(g, 1, stream);
   return hipGetLastError();
@@ -1289,12 +1275,6 @@ hipError_t conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int 
         (bn->acc_r == 0 && bn->rows != conv_dgrad_bn_rows(N, H, W, Cin)) || (reinterpret_cast<uintptr_t>(bn->x) & 15))
       return hipErrorInvalidValue;
     g.bn = *bn;
-    if (bn->acc_r > 0 && bn->dw) {
-      if (!bn->db || 2 * Cin > 1024) return hipErrorInvalidValue;
-      g.fin.acc = reinterpret_cast<double*>(bn->part);
-      g.fin.R = bn->acc_r, g.fin.C = Cin, g.fin.M = int64_t(N) * H * W, g.fin.bwd = 1;
-      g.fin.o0 = bn->db, g.fin.o1 = bn->dw;
-    }
   }
   launch_tap_gemm<true>(g, 4, stream);
   return hipGetLastError();

@@ -17,7 +17,6 @@
 
 #include <cstdint>
 
-#include "bn_acc.h"
 #include "kernels.h"
 
 namespace btn {
@@ -227,7 +226,7 @@ __global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p, in
   }
   if (!bnf) return;
   // fold the lanes of each channel group (lanes t, t + groups, ...) in LDS
-  __shared__ __attribute__((aligned(16))) float red[2][kHeadThreads * 8];   // [PL][C] per sum, PL * C = 8 * 256
+  __shared__ float red[2][kHeadThreads * 8];   // [PL][C] per sum, PL * C = 8 * 256
   const int PL = kHeadThreads / groups;
 #pragma unroll
   for (int q = 0; q < 8; ++q) red[0][(t / groups) * p.C + c0l + q] = bs[q], red[1][(t / groups) * p.C + c0l + q] = bq[q];
@@ -238,14 +237,6 @@ __global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p, in
     for (int l = 0; l < PL; ++l) s0 += red[0][l * p.C + c], s1 += red[1][l * p.C + c];
     unsafeAtomicAdd(row + c, double(s0));
     unsafeAtomicAdd(row + p.C + c, double(s1));
-  }
-  if (p.bn_dw) {   // the last of the dz blocks finalizes (db, dw) and clears the accumulator
-    BnFin f;
-    f.acc = p.bn_acc, f.R = p.bn_acc_r, f.C = p.C, f.M = int64_t(p.N) * p.H * p.W, f.bwd = 1;
-    f.o0 = p.bn_db, f.o1 = p.bn_dw;
-    __syncthreads();   // red is read above; the tail reuses it
-    bn_fin_tail_n(f, reinterpret_cast<double*>(&red[0][0]), reinterpret_cast<int*>(&red[1][kHeadThreads * 8 - 4]),
-                  uint32_t(nbwd));
   }
 }
 
@@ -272,10 +263,7 @@ hipError_t head_backward(const HeadParams& p, hipStream_t stream) {
       return hipErrorInvalidValue;
   }
   const int64_t blocks = (total + kHeadThreads - 1) / kHeadThreads;
-  // BN-fused: one block per CU, lanes loop -- each block adds 2 C fp64 sums
-  // into the accumulator, so fewer, fuller blocks keep that traffic small
-  const int cap = p.bn_acc ? 256 : 2048;
-  const int nbwd = int(blocks < cap ? blocks : cap);
+  const int nbwd = int(blocks < 2048 ? blocks : 2048);
   const int wtotal = p.C * p.OH * p.OW;
   const int nw = (wtotal + kHeadThreads - 1) / kHeadThreads;
   head_bwd_kernel<<<unsigned(nbwd + nw), kHeadThreads, 0, stream>>>(p, nbwd);

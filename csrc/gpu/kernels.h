@@ -335,15 +335,6 @@ struct ConvFwdParams {
   int64_t M = 0;
   int w_channels = 0;   // Cin == 4 (first layer): 3 = an RGB weight [Cout][4][4][3], input channel 3 ignored
   int acc_r = 0;        // > 0: stats points at a bn_apply_acc accumulator (fp64 [acc_r][2][Cout], atomic adds)
-  // acc_r > 0 and fin_mean != nullptr: the kernel's last block also finalizes
-  // (bn_acc.h): mean / invstd (+ running stats, num_batches_tracked) written,
-  // accumulator cleared -- the BN then needs only bn_apply
-  float* fin_mean = nullptr;
-  float* fin_invstd = nullptr;
-  float* fin_rm = nullptr;
-  float* fin_rv = nullptr;
-  int64_t* fin_tracked = nullptr;
-  float fin_eps = 0.f, fin_momentum = 0.f;
 };
 // Cin a power of two >= 8, or Cin == 4 (first layer, RGBA-decoded frames); Cout % 32 == 0.
 bool conv_fwd_supported(int Cin, int Cout);
@@ -389,10 +380,6 @@ struct BnBwdFuse {
   float* part = nullptr;
   int rows = 0;
   int acc_r = 0;   // > 0: part points at a bn_bwd_apply_acc accumulator (fp64 [acc_r][2][Cin], atomic adds), rows unused
-  // acc_r > 0 and dw != nullptr: the last block also finalizes (bn_acc.h):
-  // db = sum gz, dw = sum gz * xhat written, accumulator cleared
-  float* dw = nullptr;
-  float* db = nullptr;
 };
 int64_t conv_dgrad_bn_rows(int N, int H, int W, int Cin);
 hipError_t conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int N, int H, int W, int Cin, int Cout,
@@ -440,8 +427,6 @@ struct HeadParams {
   float bn_slope = 0.f;
   double* bn_acc = nullptr;
   int bn_acc_r = 0;
-  float* bn_dw = nullptr;   // non-null: the last block finalizes too (bn_acc.h): db = sum gz, dw = sum gz * xhat
-  float* bn_db = nullptr;
 };
 hipError_t head_forward(const HeadParams& p, hipStream_t stream);
 hipError_t head_backward(const HeadParams& p, hipStream_t stream);

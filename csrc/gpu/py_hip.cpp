@@ -263,11 +263,9 @@ PYBIND11_MODULE(_hip, m) {
       "conv_dgrad",
       [](uintptr_t dy, uintptr_t wt, uintptr_t dx, int N, int H, int W, int Cin, int Cout, uintptr_t stream,
          uintptr_t bn_x, uintptr_t bn_mean, uintptr_t bn_invstd, uintptr_t bn_w, uintptr_t bn_b, float bn_slope,
-         uintptr_t bn_part, int bn_rows, int bn_acc_r, uintptr_t bn_dw, uintptr_t bn_db) {
+         uintptr_t bn_part, int bn_rows, int bn_acc_r) {
         BnBwdFuse bn;
         bn.acc_r = bn_acc_r;
-        bn.dw = ptr<float>(bn_dw);
-        bn.db = ptr<float>(bn_db);
         bn.x = ptr<const uint16_t>(bn_x);
         bn.mean = ptr<const float>(bn_mean);
         bn.invstd = ptr<const float>(bn_invstd);
@@ -283,7 +281,7 @@ PYBIND11_MODULE(_hip, m) {
       py::arg("dy"), py::arg("wt"), py::arg("dx"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("Cin"),
       py::arg("Cout"), py::arg("stream"), py::arg("bn_x") = 0, py::arg("bn_mean") = 0, py::arg("bn_invstd") = 0,
       py::arg("bn_w") = 0, py::arg("bn_b") = 0, py::arg("bn_slope") = 0.f, py::arg("bn_part") = 0,
-      py::arg("bn_rows") = 0, py::arg("bn_acc_r") = 0, py::arg("bn_dw") = 0, py::arg("bn_db") = 0);
+      py::arg("bn_rows") = 0, py::arg("bn_acc_r") = 0);
   m.def("conv_dgrad_bn_rows", &conv_dgrad_bn_rows);
   m.def("bn_backward_from_stats",
         [](uintptr_t x, uintptr_t gy, uintptr_t gx, int64_t M, int C, int dtype, uintptr_t part, int rows,
@@ -299,17 +297,10 @@ PYBIND11_MODULE(_hip, m) {
         });
   m.def("conv_fwd",
         [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, int N, int H, int W, int Cin, int Ho, int Wo,
-           int Cout, uintptr_t stream, int w_channels, int acc_r, uintptr_t fin_mean, uintptr_t fin_invstd,
-           uintptr_t fin_rm, uintptr_t fin_rv, uintptr_t fin_tracked, float fin_eps, float fin_momentum) {
+           int Cout, uintptr_t stream, int w_channels, int acc_r) {
           ConvFwdParams p;
           p.w_channels = w_channels;
           p.acc_r = acc_r;
-          p.fin_mean = ptr<float>(fin_mean);
-          p.fin_invstd = ptr<float>(fin_invstd);
-          p.fin_rm = ptr<float>(fin_rm);
-          p.fin_rv = ptr<float>(fin_rv);
-          p.fin_tracked = ptr<int64_t>(fin_tracked);
-          p.fin_eps = fin_eps, p.fin_momentum = fin_momentum;
           p.x = ptr<const uint16_t>(x);
           p.w = ptr<const uint16_t>(w);
           p.y = ptr<uint16_t>(y);
@@ -320,8 +311,7 @@ PYBIND11_MODULE(_hip, m) {
         },
         py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"), py::arg("N"), py::arg("H"), py::arg("W"),
         py::arg("Cin"), py::arg("Ho"), py::arg("Wo"), py::arg("Cout"), py::arg("stream"), py::arg("w_channels") = 0,
-        py::arg("acc_r") = 0, py::arg("fin_mean") = 0, py::arg("fin_invstd") = 0, py::arg("fin_rm") = 0,
-        py::arg("fin_rv") = 0, py::arg("fin_tracked") = 0, py::arg("fin_eps") = 0.f, py::arg("fin_momentum") = 0.f);
+        py::arg("acc_r") = 0);
   // BatchNorm+LeakyReLU forward from conv_fwd's per-tile statistics: finalize + apply
   m.def("bn_forward_from_stats",
         [](uintptr_t x, uintptr_t y, int64_t M, int C, int dtype, uintptr_t stats, int nrows, float eps,
@@ -363,10 +353,8 @@ PYBIND11_MODULE(_hip, m) {
         [](uintptr_t w, int64_t ws_c, int64_t ws_i, int64_t ws_j, int N, int H, int W, int C, int OH, int OW,
            uintptr_t pooled, uintptr_t dlogit, uintptr_t gscale, uintptr_t dz, uintptr_t dw, uintptr_t stream,
            uintptr_t bn_x, uintptr_t bn_mean, uintptr_t bn_invstd, uintptr_t bn_w, uintptr_t bn_b, float bn_slope,
-           uintptr_t bn_acc, int bn_acc_r, uintptr_t bn_dw, uintptr_t bn_db) {
+           uintptr_t bn_acc, int bn_acc_r) {
           HeadParams p;
-          p.bn_dw = ptr<float>(bn_dw);
-          p.bn_db = ptr<float>(bn_db);
           p.bn_x = ptr<const uint16_t>(bn_x);
           p.bn_mean = ptr<const float>(bn_mean);
           p.bn_invstd = ptr<const float>(bn_invstd);
@@ -389,7 +377,7 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("C"), py::arg("OH"), py::arg("OW"), py::arg("pooled"), py::arg("dlogit"), py::arg("gscale"),
         py::arg("dz"), py::arg("dw"), py::arg("stream"), py::arg("bn_x") = 0, py::arg("bn_mean") = 0,
         py::arg("bn_invstd") = 0, py::arg("bn_w") = 0, py::arg("bn_b") = 0, py::arg("bn_slope") = 0.f,
-        py::arg("bn_acc") = 0, py::arg("bn_acc_r") = 0, py::arg("bn_dw") = 0, py::arg("bn_db") = 0);
+        py::arg("bn_acc") = 0, py::arg("bn_acc_r") = 0);
 
   // direct RCCL on the caller's stream (comm.h); the GIL is released while
   // RCCL enqueues (a group end may block until peers have posted theirs)
@@ -462,9 +450,7 @@ PYBIND11_MODULE(_hip, m) {
             a.v[k] = ptr<float>(exp_avg_sq[k]);
             a.shadow[k] = ptr<uint16_t>(shadow[k]);
             a.numel[k] = numel[k];
-            // every tensor starts on a 256-group block boundary (transposed
-            // shadows are walked a block per tile; the padding groups are no-ops)
-            a.gstart[k + 1] = (a.gstart[k] + (numel[k] + 3) / 4 + 255) / 256 * 256;
+            a.gstart[k + 1] = a.gstart[k] + (numel[k] + 3) / 4;
           }
           for (size_t k = 0; k < shadow_t.size(); ++k) {
             a.shadow_t[k] = ptr<uint16_t>(shadow_t[k]);
@@ -559,23 +545,6 @@ PYBIND11_MODULE(_hip, m) {
                 "bn_bwd_apply");
         });
 
-  // apply passes alone (the statistics finalized by their producer, bn_acc.h)
-  m.def("bn_apply",
-        [](uintptr_t x, uintptr_t y, int64_t M, int C, int dtype, uintptr_t mean, uintptr_t invstd, uintptr_t w,
-           uintptr_t b, float slope, uintptr_t stream) {
-          check(bn_apply(ptr<const void>(x), ptr<void>(y), M, C, dtype, ptr<const float>(mean),
-                         ptr<const float>(invstd), ptr<const float>(w), ptr<const float>(b), slope, stream_of(stream)),
-                "bn_apply");
-        });
-  m.def("bn_bwd_apply",
-        [](uintptr_t x, uintptr_t gy, uintptr_t gx, int64_t M, int C, int dtype, uintptr_t mean, uintptr_t invstd,
-           uintptr_t w, uintptr_t b, uintptr_t dw, uintptr_t db, float slope, uintptr_t stream) {
-          check(bn_bwd_apply(ptr<const void>(x), ptr<const void>(gy), ptr<void>(gx), M, C, dtype,
-                             ptr<const float>(mean), ptr<const float>(invstd), ptr<const float>(w),
-                             ptr<const float>(b), ptr<const float>(dw), ptr<const float>(db), slope,
-                             stream_of(stream)),
-                "bn_bwd_apply");
-        });
   // accumulator hand-off (kernels.h BnAcc): no finalize launches
   m.def("bn_acc_replicas", &bn_acc_replicas);
   m.def("bn_acc_elems", &bn_acc_elems);

@@ -570,7 +570,7 @@ int bn_acc_replicas(int C) {
 
 int64_t bn_acc_elems(int C) {
   const int r = bn_acc_replicas(C);
-  return r > 0 ? int64_t(2) * C * r + 2 : -1;   // + the producer-finalize ticket (bn_acc.h), 16-byte padded
+  return r > 0 ? int64_t(2) * C * r : -1;
 }
 
 hipError_t bn_apply_acc(const void* x, void* y, int64_t M, int C, int dtype, BnAcc acc, float eps, float momentum,

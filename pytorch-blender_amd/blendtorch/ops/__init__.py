@@ -773,9 +773,9 @@ class BnAccumulator:
     folds and clears them again: no per-tile partial rows, no per-step
     memset, and the finalize is one memory latency instead of a walk over
     ~4800 rows per channel.  ``R`` replicas per channel spread the atomics."""
-    __slots__ = ('fwd', 'bwd', 'R', 'module', 'mean', 'invstd')
+    __slots__ = ('fwd', 'bwd', 'R')
 
-    def __init__(self, C, device, module=None):
+    def __init__(self, C, device):
         import torch
         ext = hip_ext()
         self.R = int(ext.bn_acc_replicas(int(C)))
@@ -784,10 +784,6 @@ class BnAccumulator:
             raise ValueError(f'BnAccumulator: unsupported channel count {C}')
         self.fwd = torch.zeros(n, dtype=torch.float64, device=device)
         self.bwd = torch.zeros(n, dtype=torch.float64, device=device)
-        # the BatchNorm module (running statistics) and the current call's batch
-        # statistics when the producer finalized them (bn_acc.h)
-        self.module = module
-        self.mean = self.invstd = None
 
 
 def bn_acc_supported(C):
@@ -805,32 +801,12 @@ class BnLink:
     has the MFMA kernel's epilogue sum gz and gz * xhat per tile into
     ``part``; the BN backward then only finalizes and applies (one pass over
     the activation fewer).  ``part`` is consumed once."""
-    __slots__ = ('x', 'mean', 'invstd', 'w', 'b', 'slope', 'part', 'rows', 'gy', 'acc', 'params', 'dw', 'db',
-                 'dw_sunk', 'db_sunk')
+    __slots__ = ('x', 'mean', 'invstd', 'w', 'b', 'slope', 'part', 'rows', 'gy', 'acc')
 
     def __init__(self):
         self.x = self.mean = self.invstd = self.w = self.b = self.part = self.gy = None
         self.slope, self.rows = 0.0, 0
         self.acc = None      # BnAccumulator of the BN call (accumulator mode: part = acc.bwd, rows = -R)
-        self.params = None   # the BN's (weight, bias) parameters
-        # accumulator mode: where the consumer's kernel finalized the BN's weight /
-        # bias gradients (bn_acc.h), and whether those are the parameters' bucket views
-        self.dw = self.db = None
-        self.dw_sunk = self.db_sunk = False
-
-    def finalize_dests(self):
-        """Pick (and remember) the tensors a consumer kernel finalizes this
-        BN's weight and bias gradients into: the parameters' gradient bucket
-        views when they are fresh (``parallel.GradBuckets``), else new fp32
-        tensors the BN backward returns."""
-        import torch
-        self.dw, self.dw_sunk = _grad_dest(self.params[0], self.w)
-        self.db, self.db_sunk = _grad_dest(self.params[1], self.b)
-        if self.dw.dtype != torch.float32 or not self.dw.is_contiguous():
-            self.dw, self.dw_sunk = torch.empty_like(self.w), False
-        if self.db.dtype != torch.float32 or not self.db.is_contiguous():
-            self.db, self.db_sunk = torch.empty_like(self.b), False
-        return self.dw, self.db
 
     def ready(self, dx):
         """True when the recorded BN input matches ``dx`` (shape, bf16 NHWC)."""
@@ -872,16 +848,8 @@ def _bn_function():
             rm = running_mean.data_ptr() if running_mean is not None else 0
             rv = running_var.data_ptr() if running_var is not None else 0
             tr = tracked.data_ptr() if tracked is not None else 0
-            if isinstance(stats, BnAccumulator) and stats.mean is not None:
-                # the producing conv's last block finalized the statistics (bn_acc.h): apply only
-                _count('bn_forward_from_stats')
-                _count('bn_forward_acc')
-                mean, invstd = stats.mean, stats.invstd
-                stats.mean = stats.invstd = None
-                ext.bn_apply(xs.data_ptr(), y.data_ptr(), M, C, dt, mean.data_ptr(), invstd.data_ptr(), w.data_ptr(),
-                             b.data_ptr(), float(slope), _stream(x.device))
-            elif isinstance(stats, BnAccumulator):
-                # sums accumulated by the producing conv's epilogue; one finalize block, then the apply
+            if isinstance(stats, BnAccumulator):
+                # sums accumulated by the producing conv's epilogue; folded by the apply kernel
                 _count('bn_forward_from_stats')
                 _count('bn_forward_acc')
                 ext.bn_forward_acc(xs.data_ptr(), y.data_ptr(), M, C, dt, stats.fwd.data_ptr(), stats.R, float(eps),
@@ -909,8 +877,6 @@ def _bn_function():
                 link.x, link.mean, link.invstd, link.w, link.b, link.slope = xs, mean, invstd, w, b, float(slope)
                 link.part = link.gy = None
                 link.acc = ctx.acc
-                link.params = (weight, bias)
-                link.dw = link.db = None
             return y.permute(0, 3, 1, 2)
 
         @staticmethod
@@ -929,18 +895,6 @@ def _bn_function():
             if db.dtype != torch.float32 or not db.is_contiguous():
                 db, b_sunk = torch.empty_like(b), False
             part, rows = ctx.link.take(gys) if ctx.link is not None else (None, 0)
-            if part is not None and rows < 0 and ctx.link.dw is not None:
-                # the consumer's kernel also finalized dw, db (bn_acc.h): apply only
-                _count('bn_backward_from_stats')
-                _count('bn_backward_acc')
-                lk = ctx.link
-                ext.bn_bwd_apply(xs.data_ptr(), gys.data_ptr(), gx.data_ptr(), M, C, dt, mean.data_ptr(),
-                                 invstd.data_ptr(), w.data_ptr(), b.data_ptr(), lk.dw.data_ptr(), lk.db.data_ptr(),
-                                 ctx.slope, _stream(xs.device))
-                out_w = None if lk.dw_sunk else lk.dw
-                out_b = None if lk.db_sunk else lk.db
-                lk.dw = lk.db = None
-                return (gx.permute(0, 3, 1, 2), out_w, out_b, None, None, None, None, None, None, None, None)
             if ctx.acc is not None and (part is None or rows < 0):
                 # accumulator mode: the consuming conv's dgrad epilogue summed into
                 # acc.bwd (part), or this launch reduces into it first
@@ -1051,8 +1005,8 @@ def _bn_module():
             the same discriminator) never share one.  Not part of the state."""
             ring = self.__dict__.get('_bt_acc_ring')
             if ring is None or ring[0][0].fwd.device != device:
-                ring = self.__dict__['_bt_acc_ring'] = [[BnAccumulator(self.num_features, device, self)
-                                                         for _ in range(4)], 0]
+                ring = self.__dict__['_bt_acc_ring'] = [[BnAccumulator(self.num_features, device) for _ in range(4)],
+                                                        0]
             accs, i = ring
             ring[1] = (i + 1) % len(accs)
             return accs[i]
@@ -1127,7 +1081,7 @@ def conv_wgrad(x, dy, out, target_blocks=None):
     return out
 
 
-def conv_fwd(x, w16, stats=None, acc_r=0, fin=None):
+def conv_fwd(x, w16, stats=None, acc_r=0):
     """y = conv2d(x, w16, stride 2, pad 1) on the gfx950 MFMA kernel: ``x``
     [N, Cin, H, W] bf16 channels-last, ``w16`` [Cout, Cin, 4, 4] bf16
     channels-last; returns channels-last bf16 y.  ``stats`` (optional fp32
@@ -1135,10 +1089,7 @@ def conv_fwd(x, w16, stats=None, acc_r=0, fin=None):
     BatchNorm sums of y, channel-major: ``stats.view(2, Cout, rows)`` holds
     the sums, then the sums of squares (see :func:`batch_norm_from_stats`).
     ``acc_r`` > 0: ``stats`` is a :class:`BnAccumulator`'s zeroed fp64
-    ``fwd`` tensor with ``acc_r`` replicas, added into with atomics;
-    ``fin`` (that :class:`BnAccumulator`, its ``module`` set): the kernel's
-    last block also finalizes the batch statistics into new ``fin.mean`` /
-    ``fin.invstd`` tensors and updates the module's running statistics."""
+    ``fwd`` tensor with ``acc_r`` replicas, added into with atomics."""
     import torch
     ext = hip_ext()
     N, Cin, H, W = x.shape
@@ -1155,20 +1106,8 @@ def conv_fwd(x, w16, stats=None, acc_r=0, fin=None):
     _count('conv_fwd')
     if acc_r and (stats is None or stats.dtype != torch.float64 or stats.numel() < 2 * Cout * acc_r):
         raise ValueError('conv_fwd: acc_r needs an fp64 accumulator of 2 * Cout * acc_r elements')
-    fk = {}
-    if fin is not None and acc_r:
-        mod = fin.module
-        fin.mean = torch.empty(Cout, dtype=torch.float32, device=x.device)
-        fin.invstd = torch.empty_like(fin.mean)
-        rm = mod.running_mean if mod.track_running_stats else None
-        rv = mod.running_var if mod.track_running_stats else None
-        tr = mod.num_batches_tracked if mod.track_running_stats else None
-        fk = dict(fin_mean=fin.mean.data_ptr(), fin_invstd=fin.invstd.data_ptr(),
-                  fin_rm=rm.data_ptr() if rm is not None else 0, fin_rv=rv.data_ptr() if rv is not None else 0,
-                  fin_tracked=tr.data_ptr() if tr is not None else 0, fin_eps=float(mod.eps),
-                  fin_momentum=float(mod.momentum))
     ext.conv_fwd(x.data_ptr(), w16.data_ptr(), y.data_ptr(), stats.data_ptr() if stats is not None else 0,
-                 N, H, W, Cin, Ho, Wo, Cout, _stream(x.device), wc if Cin == 4 else 0, int(acc_r), **fk)
+                 N, H, W, Cin, Ho, Wo, Cout, _stream(x.device), wc if Cin == 4 else 0, int(acc_r))
     return y
 
 
@@ -1218,20 +1157,15 @@ def conv_dgrad(dy, w16, in_shape, wt=None, bn=None):
     _count('conv_dgrad')
     if bn is not None and bn.ready(dx):
         _count('conv_dgrad_bn')
-        fd = {}
         if bn.acc is not None:
-            # add into the BN call's zeroed backward accumulator; the kernel's last
-            # block finalizes the BN's weight / bias gradients (bn_acc.h)
+            # add into the BN call's zeroed backward accumulator (no partial rows, no finalize)
             part, acc_r, rows = bn.acc.bwd, bn.acc.R, -bn.acc.R
-            if bn.params is not None:
-                dw, db = bn.finalize_dests()
-                fd = dict(bn_dw=dw.data_ptr(), bn_db=db.data_ptr())
         else:
             acc_r, rows = 0, int(ext.conv_dgrad_bn_rows(N, H, W, Cin))
             part = torch.empty(2 * Cin * rows, dtype=torch.float32, device=dy.device)
         ext.conv_dgrad(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), N, H, W, Cin, Cout, _stream(dy.device),
                        bn.x.data_ptr(), bn.mean.data_ptr(), bn.invstd.data_ptr(), bn.w.data_ptr(), bn.b.data_ptr(),
-                       bn.slope, part.data_ptr(), max(rows, 0), acc_r, **fd)
+                       bn.slope, part.data_ptr(), max(rows, 0), acc_r)
         bn.part, bn.rows, bn.gy = part, rows, dx
     else:
         ext.conv_dgrad(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), N, H, W, Cin, Cout, _stream(dy.device))
@@ -1287,8 +1221,7 @@ def _conv_function():
             ctx.save_for_backward(x, w16)
             ctx.w32, ctx.wt, ctx.bn_link = w32, wt, bn_link
             if isinstance(with_stats, BnAccumulator):
-                fin = with_stats if with_stats.module is not None else None
-                return conv_fwd(x, w16, with_stats.fwd, with_stats.R, fin=fin)
+                return conv_fwd(x, w16, with_stats.fwd, with_stats.R)
             if with_stats:
                 N, _, H, W = x.shape
                 M = N * ((H - 2) // 2 + 1) * ((W - 2) // 2 + 1)
@@ -1405,14 +1338,10 @@ def _head_function():
                 # dz is the gy of the BN+LeakyReLU that produced z: sum its backward
                 # statistics here, into the BN call's accumulator
                 _count('head_backward_bn')
-                fd = {}
-                if bn.params is not None:
-                    bdw, bdb = bn.finalize_dests()
-                    fd = dict(bn_dw=bdw.data_ptr(), bn_db=bdb.data_ptr())
                 ext.head_backward(w.data_ptr(), w.stride(1), w.stride(2), w.stride(3), N, H, W, C, oh, ow,
                                   pooled.data_ptr(), dlogit.data_ptr(), g.data_ptr(), dz.data_ptr(), dw.data_ptr(),
                                   _stream(w.device), bn.x.data_ptr(), bn.mean.data_ptr(), bn.invstd.data_ptr(),
-                                  bn.w.data_ptr(), bn.b.data_ptr(), bn.slope, bn.acc.bwd.data_ptr(), bn.acc.R, **fd)
+                                  bn.w.data_ptr(), bn.b.data_ptr(), bn.slope, bn.acc.bwd.data_ptr(), bn.acc.R)
                 bn.part, bn.rows, bn.gy = bn.acc.bwd, -bn.acc.R, dz
             else:
                 ext.head_backward(w.data_ptr(), w.stride(1), w.stride(2), w.stride(3), N, H, W, C, oh, ow,
