@@ -122,11 +122,66 @@ __device__ __forceinline__ uint2 bload8(__amdgpu_buffer_rsrc_t r, uint32_t off) 
 // start at zero: the weight-gradient kernel clears it (every block a share,
 // plain stores) -- the reduce runs after it on the stream, so no separate
 // memset launch is needed.
+__device__ __forceinline__ int main_blocks(const ConvWgradParams& p) {
+  return p.main_blocks > 0 ? p.main_blocks : int(gridDim.x);
+}
+
 __device__ __forceinline__ void zero_output(const ConvWgradParams& p) {
   if (!p.zero_out) return;
-  const int per = (p.zero_count + int(gridDim.x) - 1) / int(gridDim.x);
+  const int per = (p.zero_count + main_blocks(p) - 1) / main_blocks(p);
   const int e0 = int(blockIdx.x) * per, e1 = e0 + per < p.zero_count ? e0 + per : p.zero_count;
   for (int e = e0 + int(threadIdx.x); e < e1; e += int(blockDim.x)) p.zero_out[e] = 0.f;
+}
+
+// Sum the S slices into fp32 dW[co][kh][kw][ci] at the parameter's strides.
+// blockIdx.y takes a group of kSliceGroup slices and each lane four
+// consecutive elements (one 16-byte load per slice, all of a group's loads
+// independent and in flight together); groups add into the zeroed output
+// with float atomics (S / kSliceGroup adds per element).  One lane per
+// element walking all S slices serially was latency-bound (17 us at S = 64).
+constexpr int kSliceGroup = 8;
+
+__device__ __forceinline__ void wgrad_reduce_block(const ConvWgradParams::Reduce& r, int bx, int by) {
+  const float* __restrict__ partial = r.partial;
+  const int S = r.S, Cin = r.Cin, cin_out = r.cin_out;
+  float* __restrict__ out = r.out;
+  const int KC = 16 * Cin;
+  const int total = r.Cout * KC;
+  const int e0 = (bx * kThreads + int(threadIdx.x)) * 4;
+  if (e0 >= total) return;
+  const int k0 = by * kSliceGroup;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int k = 0; k < kSliceGroup; ++k) {
+    if (k0 + k < S) {
+      const float4 v = *reinterpret_cast<const float4*>(partial + int64_t(k0 + k) * total + e0);
+      acc.x += v.x, acc.y += v.y, acc.z += v.z, acc.w += v.w;
+    }
+  }
+  const float vals[4] = {acc.x, acc.y, acc.z, acc.w};
+  const bool single = S <= kSliceGroup;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int e = e0 + j;
+    const int co = e / KC, kc = e - co * KC;
+    const int tap = kc / Cin, ci = kc - tap * Cin;
+    if (ci >= cin_out) continue;   // padded input channel (4-channel first layer)
+    float* dst = out + co * r.s_co + ci * r.s_ci + (tap >> 2) * r.s_kh + (tap & 3) * r.s_kw;
+    if (single) *dst = vals[j];
+    else atomicAdd(dst, vals[j]);
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void conv_wgrad_reduce_kernel(ConvWgradParams::Reduce r) {
+  wgrad_reduce_block(r, int(blockIdx.x), int(blockIdx.y));
+}
+
+// blocks past the main grid: a previous layer's deferred reduce (the side job)
+__device__ __forceinline__ bool run_side(const ConvWgradParams& p) {
+  const int b = int(blockIdx.x) - main_blocks(p);
+  if (b < 0) return false;
+  wgrad_reduce_block(p.side, b % p.side.rx, b / p.side.rx);
+  return true;
 }
 
 struct PixelCursor {   // (n, oh, ow) of pixel m, advanced by BPX per k-step
@@ -186,11 +241,12 @@ struct XCursor {
 
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  if (run_side(p)) return;
   const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
   const int KC = 16 * p.Cin, KT = KC / BKC, T = (p.Cout / BCO) * KT;
 
   // XCD-aware bijective remap: consecutive work ids share an XCD (blockIdx % 8)
-  const int nwg = int(gridDim.x), b = int(blockIdx.x);
+  const int nwg = main_blocks(p), b = int(blockIdx.x);
   const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
   const int slice = w / T, tile = w - slice * T;
@@ -343,9 +399,10 @@ __device__ __forceinline__ int c4x_off(int r, int byte) { return dy_off(r, byte)
 
 __global__ __launch_bounds__(kThreads) void conv_wgrad_c4_kernel(ConvWgradParams p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * C4_STAGE];
+  if (run_side(p)) return;
   const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
   const int T = p.Cout / 32;
-  const int nwg = int(gridDim.x), b = int(blockIdx.x);
+  const int nwg = main_blocks(p), b = int(blockIdx.x);
   const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
   const int slice = w / T, co0 = (w - slice * T) * 32;
@@ -426,47 +483,6 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4_kernel(ConvWgradParams
       out[co * 64 + fkc + 16 * j + (lane & 15)] = acc[j][r];
     }
 }
-
-// Sum the S slices into fp32 dW[co][kh][kw][ci] at the parameter's strides.
-// blockIdx.y takes a group of kSliceGroup slices and each lane four
-// consecutive elements (one 16-byte load per slice, all of a group's loads
-// independent and in flight together); groups add into the zeroed output
-// with float atomics (S / kSliceGroup adds per element).  One lane per
-// element walking all S slices serially was latency-bound (17 us at S = 64).
-constexpr int kSliceGroup = 8;
-
-__global__ __launch_bounds__(kThreads) void conv_wgrad_reduce_kernel(const float* __restrict__ partial, int S,
-                                                                     int Cout, int Cin, int cin_out,
-                                                                     float* __restrict__ out,
-                                                                     int64_t s_co, int64_t s_ci, int64_t s_kh,
-                                                                     int64_t s_kw) {
-  const int KC = 16 * Cin;
-  const int total = Cout * KC;
-  const int e0 = (int(blockIdx.x) * kThreads + int(threadIdx.x)) * 4;
-  if (e0 >= total) return;
-  const int k0 = int(blockIdx.y) * kSliceGroup;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-  for (int k = 0; k < kSliceGroup; ++k) {
-    if (k0 + k < S) {
-      const float4 v = *reinterpret_cast<const float4*>(partial + int64_t(k0 + k) * total + e0);
-      acc.x += v.x, acc.y += v.y, acc.z += v.z, acc.w += v.w;
-    }
-  }
-  const float vals[4] = {acc.x, acc.y, acc.z, acc.w};
-  const bool single = S <= kSliceGroup;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int e = e0 + j;
-    const int co = e / KC, kc = e - co * KC;
-    const int tap = kc / Cin, ci = kc - tap * Cin;
-    if (ci >= cin_out) continue;   // padded input channel (4-channel first layer)
-    float* dst = out + co * s_co + ci * s_ci + (tap >> 2) * s_kh + (tap & 3) * s_kw;
-    if (single) *dst = vals[j];
-    else atomicAdd(dst, vals[j]);
-  }
-}
-
 
 // ---------------------------------------------------------------------------
 // Tap-gather GEMM: the forward convolution AND the data gradient.
@@ -1080,8 +1096,14 @@ int conv_wgrad_slices(int64_t M, int Cin, int Cout, int target_blocks) {
   return int(s);
 }
 
+hipError_t conv_wgrad_reduce(const ConvWgradParams::Reduce& r, hipStream_t stream) {
+  if (!r.partial || !r.out || r.S <= 0 || r.rx <= 0 || r.ry <= 0) return hipErrorInvalidValue;
+  conv_wgrad_reduce_kernel<<<dim3(unsigned(r.rx), unsigned(r.ry)), kThreads, 0, stream>>>(r);
+  return hipGetLastError();
+}
+
 hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_t s_ci, int64_t s_kh, int64_t s_kw,
-                      hipStream_t stream) {
+                      hipStream_t stream, ConvWgradParams::Reduce* defer, const ConvWgradParams::Reduce* side) {
   if (!conv_wgrad_supported(p.Cin, p.Cout) || p.slices <= 0 || !p.x || !p.dy || !p.partial || !out ||
       p.cin_out < 0 || p.cin_out > p.Cin)
     return hipErrorInvalidValue;
@@ -1101,14 +1123,27 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
     q.zero_out = out;
     q.zero_count = p.Cout * 16 * (p.cin_out > 0 ? p.cin_out : p.Cin);
   }
-  if (c4) conv_wgrad_c4_kernel<<<unsigned(blocks), kThreads, 0, stream>>>(q);
-  else conv_wgrad_kernel<<<unsigned(blocks), kThreads, 0, stream>>>(q);
+  int64_t grid = blocks;
+  if (side) {
+    if (!side->partial || !side->out || side->S <= 0 || side->rx <= 0 || side->ry <= 0) return hipErrorInvalidValue;
+    q.main_blocks = int(blocks);
+    q.side = *side;
+    grid += int64_t(side->rx) * side->ry;
+  }
+  if (c4) conv_wgrad_c4_kernel<<<unsigned(grid), kThreads, 0, stream>>>(q);
+  else conv_wgrad_kernel<<<unsigned(grid), kThreads, 0, stream>>>(q);
   const int64_t total = int64_t(p.Cout) * 16 * p.Cin;   // partial elements per slice
-  const int cin_out = p.cin_out > 0 ? p.cin_out : p.Cin;
-  const dim3 rgrid(unsigned((total / 4 + kThreads - 1) / kThreads), unsigned((p.slices + kSliceGroup - 1) / kSliceGroup));
-  conv_wgrad_reduce_kernel<<<rgrid, kThreads, 0, stream>>>(p.partial, p.slices, p.Cout, p.Cin,
-                                                           p.cin_out > 0 ? p.cin_out : p.Cin, out, s_co, s_ci, s_kh,
-                                                           s_kw);
+  ConvWgradParams::Reduce r;
+  r.partial = p.partial, r.S = p.slices, r.Cout = p.Cout, r.Cin = p.Cin;
+  r.cin_out = p.cin_out > 0 ? p.cin_out : p.Cin;
+  r.out = out, r.s_co = s_co, r.s_ci = s_ci, r.s_kh = s_kh, r.s_kw = s_kw;
+  r.rx = int((total / 4 + kThreads - 1) / kThreads);
+  r.ry = (p.slices + kSliceGroup - 1) / kSliceGroup;
+  if (defer) {
+    *defer = r;
+    return hipGetLastError();
+  }
+  conv_wgrad_reduce_kernel<<<dim3(unsigned(r.rx), unsigned(r.ry)), kThreads, 0, stream>>>(r);
   return hipGetLastError();
 }
 

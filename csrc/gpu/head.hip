@@ -263,7 +263,10 @@ hipError_t head_backward(const HeadParams& p, hipStream_t stream) {
       return hipErrorInvalidValue;
   }
   const int64_t blocks = (total + kHeadThreads - 1) / kHeadThreads;
-  const int nbwd = int(blocks < 2048 ? blocks : 2048);
+  // BN-fused: one block per CU, lanes loop -- each block adds 2 C fp64 sums
+  // into the accumulator, so fewer, fuller blocks keep that traffic small
+  const int cap = p.bn_acc ? 256 : 2048;
+  const int nbwd = int(blocks < cap ? blocks : cap);
   const int wtotal = p.C * p.OH * p.OW;
   const int nw = (wtotal + kHeadThreads - 1) / kHeadThreads;
   head_bwd_kernel<<<unsigned(nbwd + nw), kHeadThreads, 0, stream>>>(p, nbwd);

@@ -314,12 +314,31 @@ struct ConvWgradParams {
   int cin_out = 0;   // dW input channels written (0: Cin); 3 for a 4-channel (RGBA-fed) first layer
   float* zero_out = nullptr;   // set by conv_wgrad: the kernel clears the output for the atomic reduce
   int zero_count = 0;
+  // set by conv_wgrad: blocks [0, main_blocks) compute this layer, blocks
+  // [main_blocks, grid) run `side`, a previous layer's deferred slice reduce
+  int main_blocks = 0;
+  struct Reduce {
+    const float* partial = nullptr;
+    int S = 0, Cout = 0, Cin = 0, cin_out = 0;
+    float* out = nullptr;
+    int64_t s_co = 0, s_ci = 0, s_kh = 0, s_kw = 0;
+    int rx = 0, ry = 0;   // its grid: element blocks x slice groups
+  } side;
 };
 // Cin % 32 == 0 with Cout % 64 == 0, or Cin == 4 (the first layer) with Cout % 32 == 0.
 bool conv_wgrad_supported(int Cin, int Cout);
 int conv_wgrad_slices(int64_t M, int Cin, int Cout, int target_blocks);
+// The slice reduce normally follows the main kernel as its own launch.
+// defer != nullptr: it is NOT launched but described in *defer, for the
+// next conv_wgrad to run as extra blocks of its own launch (`side`; the
+// partial scratch must stay alive until then) -- a layer chain then pays one
+// reduce launch in all, the last layer's.  The deferred output was already
+// cleared by its main kernel.
 hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_t s_ci, int64_t s_kh, int64_t s_kw,
-                      hipStream_t stream);
+                      hipStream_t stream, ConvWgradParams::Reduce* defer = nullptr,
+                      const ConvWgradParams::Reduce* side = nullptr);
+// a deferred reduce on its own (a chain that ends without another conv_wgrad)
+hipError_t conv_wgrad_reduce(const ConvWgradParams::Reduce& r, hipStream_t stream);
 
 // Forward 4x4 / stride-2 / pad-1 convolution on the MFMA units (conv.hip):
 // x [N][H][W][Cin] bf16, w [Cout][4][4][Cin] bf16 (channels-last weight) ->

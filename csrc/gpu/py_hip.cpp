@@ -116,6 +116,24 @@ void fill_cmap(int* dst, const std::vector<int>& cmap) {
 
 }  // namespace
 
+// a deferred weight-gradient slice reduce (ConvWgradParams::Reduce) as a
+// plain tuple: (partial, S, Cout, Cin, cin_out, out, s_co, s_ci, s_kh, s_kw, rx, ry)
+py::tuple reduce_to_tuple(const ConvWgradParams::Reduce& r) {
+  return py::make_tuple(reinterpret_cast<uintptr_t>(r.partial), r.S, r.Cout, r.Cin, r.cin_out,
+                        reinterpret_cast<uintptr_t>(r.out), r.s_co, r.s_ci, r.s_kh, r.s_kw, r.rx, r.ry);
+}
+
+ConvWgradParams::Reduce reduce_from_tuple(const py::tuple& t) {
+  if (t.size() != 12) throw std::invalid_argument("conv_wgrad: a deferred reduce is a 12-tuple");
+  ConvWgradParams::Reduce r;
+  r.partial = reinterpret_cast<const float*>(t[0].cast<uintptr_t>());
+  r.S = t[1].cast<int>(), r.Cout = t[2].cast<int>(), r.Cin = t[3].cast<int>(), r.cin_out = t[4].cast<int>();
+  r.out = reinterpret_cast<float*>(t[5].cast<uintptr_t>());
+  r.s_co = t[6].cast<int64_t>(), r.s_ci = t[7].cast<int64_t>(), r.s_kh = t[8].cast<int64_t>();
+  r.s_kw = t[9].cast<int64_t>(), r.rx = t[10].cast<int>(), r.ry = t[11].cast<int>();
+  return r;
+}
+
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "blendtorch gfx950 kernels + GPU stream loader";
 
@@ -220,7 +238,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("conv_wgrad",
         [](uintptr_t x, uintptr_t dy, uintptr_t partial, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
            int slices, int64_t px_per_slice, uintptr_t out, int64_t s_co, int64_t s_ci, int64_t s_kh, int64_t s_kw,
-           uintptr_t stream, int cin_out) {
+           uintptr_t stream, int cin_out, bool defer, py::object side) -> py::object {
           ConvWgradParams p;
           p.cin_out = cin_out;
           p.x = ptr<const uint16_t>(x);
@@ -230,11 +248,23 @@ PYBIND11_MODULE(_hip, m) {
           p.M = int64_t(N) * Ho * Wo;
           p.slices = slices;
           p.px_per_slice = px_per_slice;
-          check(conv_wgrad(p, ptr<float>(out), s_co, s_ci, s_kh, s_kw, stream_of(stream)), "conv_wgrad");
+          ConvWgradParams::Reduce sd, df;
+          const bool has_side = !side.is_none();
+          if (has_side) sd = reduce_from_tuple(side.cast<py::tuple>());
+          check(conv_wgrad(p, ptr<float>(out), s_co, s_ci, s_kh, s_kw, stream_of(stream), defer ? &df : nullptr,
+                           has_side ? &sd : nullptr),
+                "conv_wgrad");
+          if (!defer) return py::none();
+          return reduce_to_tuple(df);
         },
         py::arg("x"), py::arg("dy"), py::arg("partial"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("Cin"),
         py::arg("Ho"), py::arg("Wo"), py::arg("Cout"), py::arg("slices"), py::arg("px_per_slice"), py::arg("out"),
-        py::arg("s_co"), py::arg("s_ci"), py::arg("s_kh"), py::arg("s_kw"), py::arg("stream"), py::arg("cin_out") = 0);
+        py::arg("s_co"), py::arg("s_ci"), py::arg("s_kh"), py::arg("s_kw"), py::arg("stream"), py::arg("cin_out") = 0,
+        py::arg("defer") = false, py::arg("side") = py::none());
+  // a deferred slice reduce on its own (a weight-gradient chain that ended early)
+  m.def("conv_wgrad_reduce", [](py::tuple r, uintptr_t stream) {
+    check(conv_wgrad_reduce(reduce_from_tuple(r), stream_of(stream)), "conv_wgrad_reduce");
+  });
 
   m.def("conv_fwd_tiles", &conv_fwd_tiles);
   m.def("conv_set_tiles", &conv_set_tiles, py::arg("bm") = 0, py::arg("bn") = 0, py::arg("staging") = -1);
@@ -450,7 +480,9 @@ PYBIND11_MODULE(_hip, m) {
             a.v[k] = ptr<float>(exp_avg_sq[k]);
             a.shadow[k] = ptr<uint16_t>(shadow[k]);
             a.numel[k] = numel[k];
-            a.gstart[k + 1] = a.gstart[k] + (numel[k] + 3) / 4;
+            // every tensor starts on a 256-group block boundary (transposed
+            // shadows are walked a block per tile; the padding groups are no-ops)
+            a.gstart[k + 1] = (a.gstart[k] + (numel[k] + 3) / 4 + 255) / 256 * 256;
           }
           for (size_t k = 0; k < shadow_t.size(); ++k) {
             a.shadow_t[k] = ptr<uint16_t>(shadow_t[k]);

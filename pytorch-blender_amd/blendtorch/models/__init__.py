@@ -154,6 +154,10 @@ class Discriminator(nn.Module):
                 wts = dict(zip(need, ops.conv_weights_t([w16s[k] for k in need])))
         ci = -1
         stats = link = None
+        # the MFMA weight gradients of one backward hand their slice reduce to the
+        # next one (ops.WgradChain): the first such layer's runs last and closes it
+        wchain = ops.WgradChain() if (mfma and torch.is_grad_enabled() and x.is_cuda) else None
+        first_mfma = True
         for i, m in enumerate(layers):
             if isinstance(m, nn.Conv2d):
                 ci += 1
@@ -173,15 +177,17 @@ class Discriminator(nn.Module):
                             and nxt.fused_with_stats(x.new_empty((1, m.out_channels, 1, 1))))
                     # the BN that produced x: this conv's data gradient does its backward reduction
                     bl, link = link, None
+                    wk = dict(wt=wts.get(ci), bn_link=bl, wchain=wchain, wlast=first_mfma)
+                    first_mfma = False
                     if fuse and ops.bn_acc_supported(m.out_channels):
                         # BN statistics come out of the conv kernel's epilogue, added into
                         # the BN call's zeroed accumulator (its apply kernel folds them)
                         stats = nxt.accumulator(x.device)
-                        x = ops.conv4x4s2(x, m.weight, w16, with_stats=stats, wt=wts.get(ci), bn_link=bl)
+                        x = ops.conv4x4s2(x, m.weight, w16, with_stats=stats, **wk)
                     elif fuse:   # per-tile partial rows + a finalize launch
-                        x, stats = ops.conv4x4s2(x, m.weight, w16, with_stats=True, wt=wts.get(ci), bn_link=bl)
+                        x, stats = ops.conv4x4s2(x, m.weight, w16, with_stats=True, **wk)
                     else:
-                        x = ops.conv4x4s2(x, m.weight, w16, wt=wts.get(ci), bn_link=bl)
+                        x = ops.conv4x4s2(x, m.weight, w16, **wk)
                 else:
                     link = None
                     x = F.conv2d(x, w16, None, m.stride, m.padding, m.dilation, m.groups)

@@ -1049,11 +1049,32 @@ def conv_wgrad_supported(x, weight):
     return (kh, kw) == (4, 4) and (big or first) and x.is_contiguous(memory_format=torch.channels_last)
 
 
-def conv_wgrad(x, dy, out, target_blocks=None):
+class WgradChain:
+    """Weight-gradient launches of one backward pass that hand their slice
+    reduce forward: each :func:`conv_wgrad` in the chain leaves its reduce to
+    the next one, which runs it as extra blocks of its own launch; the call
+    marked ``last`` runs its own (and the one handed to it) -- one reduce
+    launch per chain instead of one per layer.  ``flush()`` runs a reduce
+    left pending (a chain that ended before its ``last`` call)."""
+    __slots__ = ('pending', 'keep')
+
+    def __init__(self):
+        self.pending = None   # the deferred reduce (ext tuple)
+        self.keep = None      # its partial scratch and output, alive until run
+
+    def flush(self, device):
+        if self.pending is not None:
+            hip_ext().conv_wgrad_reduce(self.pending, _stream(device))
+            self.pending = self.keep = None
+
+
+def conv_wgrad(x, dy, out, target_blocks=None, chain=None, last=True):
     """fp32 weight gradient of a 4x4/s2/p1 convolution into ``out`` ([Cout, Cin,
     4, 4], any strides): MFMA tiles over pixel slices + one slice-reduce
     launch.  ``x`` [N, Cin, H, W] and ``dy`` [N, Cout, H/2, W/2] are bf16 with
-    channels-last memory."""
+    channels-last memory.  ``chain`` (:class:`WgradChain`): run the chain's
+    pending reduce inside this launch, and leave this layer's to the next
+    call unless ``last`` -- ``out`` is then complete only after that call."""
     import torch
     ext = hip_ext()
     N, Cin, H, W = x.shape
@@ -1075,9 +1096,15 @@ def conv_wgrad(x, dy, out, target_blocks=None):
     slices = -(-M // px)
     partial = torch.empty(slices * Cout * 16 * Cin, dtype=torch.float32, device=x.device)
     _count('conv_wgrad')
-    ext.conv_wgrad(x.data_ptr(), dy.data_ptr(), partial.data_ptr(), N, H, W, Cin, Ho, Wo, Cout, slices, px,
-                   out.data_ptr(), out.stride(0), out.stride(1), out.stride(2), out.stride(3), _stream(x.device),
-                   cin_out)
+    side = chain.pending if chain is not None else None
+    defer = chain is not None and not last
+    res = ext.conv_wgrad(x.data_ptr(), dy.data_ptr(), partial.data_ptr(), N, H, W, Cin, Ho, Wo, Cout, slices, px,
+                         out.data_ptr(), out.stride(0), out.stride(1), out.stride(2), out.stride(3), _stream(x.device),
+                         cin_out, defer, side)
+    if chain is not None:
+        if side is not None:
+            _count('conv_wgrad_side_reduce')
+        chain.pending, chain.keep = (res, (partial, out)) if defer else (None, None)
     return out
 
 
@@ -1216,10 +1243,11 @@ def _conv_function():
         into the master weight's gradient (no bf16 round trip, no cast)."""
 
         @staticmethod
-        def forward(ctx, x, w32, w16, with_stats=False, wt=None, bn_link=None):
+        def forward(ctx, x, w32, w16, with_stats=False, wt=None, bn_link=None, wchain=None, wlast=True):
             ctx.set_materialize_grads(False)   # no zero-filled gradient for the stats output
             ctx.save_for_backward(x, w16)
             ctx.w32, ctx.wt, ctx.bn_link = w32, wt, bn_link
+            ctx.wchain, ctx.wlast = wchain, wlast
             if isinstance(with_stats, BnAccumulator):
                 return conv_fwd(x, w16, with_stats.fwd, with_stats.R)
             if with_stats:
@@ -1240,7 +1268,9 @@ def _conv_function():
         def backward(ctx, gy, gstats=None):
             x, w16 = ctx.saved_tensors
             if gy is None:
-                return None, None, None, None, None, None
+                if ctx.wchain is not None and ctx.wlast:
+                    ctx.wchain.flush(x.device)
+                return None, None, None, None, None, None, None, None
             gy = gy.contiguous(memory_format=torch.channels_last)
             gx = gw = None
             if ctx.needs_input_grad[0]:
@@ -1255,10 +1285,17 @@ def _conv_function():
                                                              [0, 0], 1, [True, False, False])[0]
             if ctx.needs_input_grad[1]:
                 out, sunk = _grad_dest(ctx.w32)
-                gw = conv_wgrad(x, gy, out)
+                # a chained (deferred) reduce only into a bucket view: a returned
+                # gradient must be complete when autograd accumulates it
+                chain = ctx.wchain if (sunk or ctx.wlast) else None
+                if ctx.wchain is not None and chain is None:
+                    ctx.wchain.flush(x.device)
+                gw = conv_wgrad(x, gy, out, chain=chain, last=ctx.wlast or chain is None)
                 if sunk:
                     gw = None      # written into the parameter's bucket view
-            return gx, gw, None, None, None, None
+            elif ctx.wchain is not None:
+                ctx.wchain.flush(x.device)
+            return gx, gw, None, None, None, None, None, None
 
     return _Conv4x4s2
 
@@ -1266,7 +1303,7 @@ def _conv_function():
 _CONV_FN = None
 
 
-def conv4x4s2(x, w32, w16, with_stats=False, wt=None, bn_link=None):
+def conv4x4s2(x, w32, w16, with_stats=False, wt=None, bn_link=None, wchain=None, wlast=True):
     """4x4 / stride-2 / pad-1 convolution of bf16 channels-last ``x`` with the
     bf16 copy ``w16`` of fp32 weight ``w32``; the gradient goes to ``w32``
     (fp32, from the MFMA weight-gradient kernel).  See :func:`conv_wgrad_supported`.
@@ -1274,13 +1311,16 @@ def conv4x4s2(x, w32, w16, with_stats=False, wt=None, bn_link=None):
     from the forward kernel's epilogue (for ``BatchNormLeakyReLU2d.forward_from_stats``);
     or a :class:`BnAccumulator` that the epilogue adds the sums into (returns y only).
     ``bn_link``: the :class:`BnLink` of the BatchNorm+LeakyReLU that produced
-    ``x``; the data gradient then also computes that BN's backward sums."""
+    ``x``; the data gradient then also computes that BN's backward sums.
+    ``wchain`` / ``wlast``: the :class:`WgradChain` of the model's backward;
+    ``wlast`` marks the layer whose weight gradient is computed last (the
+    first layer)."""
     global _CONV_FN
     if _CONV_FN is None:
         _CONV_FN = _conv_function()
     if with_stats and not conv_fwd_supported(x, w16):
         raise ValueError('conv4x4s2(with_stats=True) needs the MFMA forward (see conv_fwd_supported)')
-    return _CONV_FN.apply(x, w32, w16.detach(), with_stats, wt, bn_link)
+    return _CONV_FN.apply(x, w32, w16.detach(), with_stats, wt, bn_link, wchain, wlast)
 
 
 # ---------------------------------------------------------------------------

@@ -292,3 +292,27 @@ def test_bn_accumulators_fold_and_clear(dev, monkeypatch):
                 assert int(ma.num_batches_tracked) == int(mb.num_batches_tracked) == step + 1
                 for acc in ma.__dict__['_bt_acc_ring'][0]:
                     assert int(torch.count_nonzero(acc.fwd)) == 0 and int(torch.count_nonzero(acc.bwd)) == 0
+
+
+@pytest.mark.gpu
+def test_wgrad_chain_defers_slice_reduces(dev):
+    """With bucketed gradients the MFMA weight gradients hand their slice
+    reduce to the next layer's launch (3 side reduces, one reduce launch in
+    all): same gradients as the unchained per-layer reduces."""
+    from blendtorch.models import Discriminator
+    from blendtorch.parallel.grads import GradBuckets
+    torch.manual_seed(11)
+    cl = torch.channels_last
+    a = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
+    b = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
+    b.load_state_dict(a.state_dict())
+    x = torch.rand(4, 4, 96, 128, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    gb = GradBuckets(a.parameters())
+    gb.zero_()
+    before = ops.KERNEL_CALLS.get('conv_wgrad_side_reduce', 0)
+    a.bce_loss_bf16(x, 1.0).backward()
+    assert ops.KERNEL_CALLS.get('conv_wgrad_side_reduce', 0) == before + 3
+    b.bce_loss_bf16(x, 1.0).backward()                      # plain .grad tensors: no chaining
+    assert ops.KERNEL_CALLS.get('conv_wgrad_side_reduce', 0) == before + 3
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-4, atol=1e-6 + 1e-4 * float(pb.grad.abs().max()), msg=n)
