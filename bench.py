@@ -175,6 +175,10 @@ def parse_args(argv=None):
                     help='disc consumer with --h2d copy: on = the loader only DMAs raw frames into the batch '
                          'tensor and the decode kernel runs inside the captured training step (one queue, no '
                          'loader kernels competing with the step); off = the loader decodes')
+    ap.add_argument('--fuse-decode', choices=['on', 'off'], default='on',
+                    help='disc consumer with the in-step decode (bf16, fused cast and head): on = the first '
+                         'convolution reads the raw u8 RGBA frames through the decode table inside its MFMA '
+                         'kernels; off = a decode launch writes bf16 frames first')
     ap.add_argument('--consumer-input', choices=['stream', 'resident'], default='stream',
                     help='diagnostic: resident = the consumer trains on one fixed batch while the stream keeps running')
     ap.add_argument('--force-pg', action='store_true',
@@ -312,6 +316,9 @@ def main(argv=None):
     if amp:
         # the decode kernel writes what the model's first conv reads: bf16, channels-last
         decode = DecodeConfig.unit(channels='rgba' if rgba_in else 'rgb', gamma=2.2, dtype='bfloat16', layout='nhwc')
+    # the in-step decode folded into the first convolution's MFMA kernels (raw u8 frames in)
+    fuse_decode = (step_decode and args.fuse_decode == 'on' and amp and args.cast == 'fused'
+                   and args.head == 'fused' and decode.channels == 'rgba' and decode.dtype == 'bfloat16')
     launch = dict(producer='cubesim', num_instances=nprod, named_sockets=['DATA'], start_port=start_port,
                   proto=args.proto, seed=1000 * rank, cpu_affinity=affinity,
                   instance_args=[['--mode', args.mode, '--sndhwm', '10', '--resolution', f'{res_w}x{res_h}'] + (['--shm', str(shm_slots), '--codec', args.codec] if shm_slots else [])]
@@ -390,6 +397,11 @@ def main(argv=None):
             return img.permute(0, 3, 1, 2) if amp else img.contiguous(memory_format=torch.channels_last)
 
         def loss_fn(m, x):
+            if fuse_decode:
+                # the raw u8 RGBA frames go straight into the first convolution,
+                # which decodes them in its MFMA kernels' tile loads (no decode
+                # launch, no bf16 copy of the batch)
+                return m.bce_loss_bf16(x.permute(0, 3, 1, 2), 1.0, decode=decode)
             if step_decode:
                 from blendtorch import ops
                 x = ops.decode(x, decode)   # gfx950 decode, captured with the step
@@ -561,6 +573,7 @@ def main(argv=None):
                 'codec': args.codec if shm_slots else 'none',
                 'consumer_step': stepper.state if stepper is not None else None,
                 'decode_in_step': step_decode,
+                'decode_fused_in_conv': fuse_decode,
                 'cast': args.cast if amp else None,
                 'optim': args.optim if model is not None else None,
                 'dma_phase': args.dma_phase if model is not None else None,

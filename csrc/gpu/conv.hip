@@ -117,6 +117,26 @@ __device__ __forceinline__ uint2 bload8(__amdgpu_buffer_rsrc_t r, uint32_t off) 
   const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, int(off), 0, 0);
   return make_uint2(v[0], v[1]);
 }
+__device__ __forceinline__ uint32_t bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, int(off), 0, 0);
+}
+
+// First layer fed the RAW u8 RGBA frames (decode fused into the convolution):
+// a pixel's 4 bytes become 4 bf16 values through the decode's value table,
+// RNE-rounded to bf16 ([4][256], 2 KB, staged in LDS per block) -- exactly
+// what the decode kernel writes for a bf16 NHWC RGBA output.  Padding pixels
+// stay zero (not table[0]).
+constexpr int kLutBytes = 4 * 256 * 2;
+__device__ __forceinline__ void stage_lut(const uint16_t* lut, char* lds) {
+  const int t = int(threadIdx.x);   // 256 threads x 8 bytes
+  *reinterpret_cast<uint2*>(lds + 8 * t) = *reinterpret_cast<const uint2*>(lut + 4 * t);
+}
+__device__ __forceinline__ uint2 lut_px(const char* lds, uint32_t w, bool ok) {
+  const uint16_t* l = reinterpret_cast<const uint16_t*>(lds);
+  if (!ok) return make_uint2(0u, 0u);
+  return make_uint2(uint32_t(l[w & 255u]) | (uint32_t(l[256 + ((w >> 8) & 255u)]) << 16),
+                    uint32_t(l[512 + ((w >> 16) & 255u)]) | (uint32_t(l[768 + (w >> 24)]) << 16));
+}
 
 // The slice-reduce adds slice groups atomically into the gradient, which must
 // start at zero: the weight-gradient kernel clears it (every block a share,
@@ -398,8 +418,14 @@ __device__ __forceinline__ int c4dy_off(int r, int byte) {
 __device__ __forceinline__ int c4x_off(int r, int byte) { return dy_off(r, byte); }
 
 __global__ __launch_bounds__(kThreads) void conv_wgrad_c4_kernel(ConvWgradParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * C4_STAGE];
+  __shared__ __attribute__((aligned(16))) char smem[2 * C4_STAGE + kLutBytes];
   if (run_side(p)) return;
+  const bool u8in = p.lut != nullptr;   // raw u8 RGBA input, decoded through the table (see stage_lut)
+  char* const lutl = smem + 2 * C4_STAGE;
+  if (u8in) {
+    stage_lut(p.lut, lutl);
+    __syncthreads();
+  }
   const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
   const int T = p.Cout / 32;
   const int nwg = main_blocks(p), b = int(blockIdx.x);
@@ -416,12 +442,12 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4_kernel(ConvWgradParams
   const int kh = xch >> 1, kw = (xch & 1) * 2;
   PixelCursor c;
   c.init(m_begin + xpx, p.Ho, p.Wo);
-  const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(p.x, int64_t(p.N) * p.H * p.W * 4 * 2);
+  const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(p.x, int64_t(p.N) * p.H * p.W * 4 * (u8in ? 1 : 2));
   const __amdgpu_buffer_rsrc_t rs_dy = make_rsrc(p.dy, p.M * p.Cout * 2);
   constexpr int kDepth = 4;
   struct Stage {
     uint4 dy;
-    uint2 x0, x1;
+    uint2 x0, x1;    // bf16 pixels; u8 input: x0.x / x1.x the raw bytes, x0.y / x1.y in-image flags
   };
   Stage ring[kDepth];
   int md = m_begin + dpx, mx = m_begin + xpx;
@@ -432,8 +458,14 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4_kernel(ConvWgradParams
     const int ih = 2 * c.oh - 1 + kh, iw = 2 * c.ow - 1 + kw;
     const bool row_ok = mx < m_end && unsigned(ih) < unsigned(p.H);
     const int e = ((c.n * p.H + ih) * p.W + iw) * 4;
-    r.x0 = bload8(rs_x, row_ok && unsigned(iw) < unsigned(p.W) ? uint32_t(e) * 2u : kOOB);
-    r.x1 = bload8(rs_x, row_ok && unsigned(iw + 1) < unsigned(p.W) ? uint32_t(e + 4) * 2u : kOOB);
+    const bool ok0 = row_ok && unsigned(iw) < unsigned(p.W), ok1 = row_ok && unsigned(iw + 1) < unsigned(p.W);
+    if (u8in) {   // converted when stored (the ring keeps its loads in flight)
+      r.x0 = make_uint2(bload4(rs_x, ok0 ? uint32_t(e) : kOOB), ok0 ? 1u : 0u);
+      r.x1 = make_uint2(bload4(rs_x, ok1 ? uint32_t(e + 4) : kOOB), ok1 ? 1u : 0u);
+    } else {
+      r.x0 = bload8(rs_x, ok0 ? uint32_t(e) * 2u : kOOB);
+      r.x1 = bload8(rs_x, ok1 ? uint32_t(e + 4) * 2u : kOOB);
+    }
     md += BPX;
     mx += BPX;
     dy_byte += dy_step;
@@ -443,7 +475,12 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4_kernel(ConvWgradParams
   auto store = [&](const Stage& r, int buf) {
     char* base = smem + buf * C4_STAGE;
     if (dy_loader) *reinterpret_cast<uint4*>(base + st_dy) = r.dy;
-    *reinterpret_cast<uint4*>(base + st_x) = make_uint4(r.x0.x, r.x0.y, r.x1.x, r.x1.y);
+    if (u8in) {
+      const uint2 a = lut_px(lutl, r.x0.x, r.x0.y != 0u), b = lut_px(lutl, r.x1.x, r.x1.y != 0u);
+      *reinterpret_cast<uint4*>(base + st_x) = make_uint4(a.x, a.y, b.x, b.y);
+    } else {
+      *reinterpret_cast<uint4*>(base + st_x) = make_uint4(r.x0.x, r.x0.y, r.x1.x, r.x1.y);
+    }
   };
   // wave: co fragment wave / 2, kc fragments 2 (wave % 2) + {0, 1}
   const int fco = (wave >> 1) * 16, fkc = (wave & 1) * 32;
@@ -527,6 +564,7 @@ struct TapGemm {
   int GH = 0, GW = 0, M = 0;       // GEMM rows: m = (n * GH + a) * GW + b
   int NOUT = 0, OH = 0, OW = 0;    // dst [N][OH][OW][NOUT]
   int wc = 0;                      // C4 mode: weight input channels (3 or 4)
+  const uint16_t* lut = nullptr;   // C4 mode: src is raw u8 RGBA, decoded through this bf16 table [4][256]
   int acc_r = 0;                   // forward: > 0 = stats points at a BnAcc accumulator (fp64 [acc_r][2][NOUT])
   BnBwdFuse bn;                    // data gradient only: BN backward statistics in the epilogue (bn.part nullable)
 };
@@ -562,7 +600,8 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   static_assert(NBUF * STG >= E_TILE + 4 * 2 * BN * 4, "epilogue does not fit the staging LDS");
   // the tile's row table after the staging space (not C4): {abase, vmask, obase, in range} per GEMM row
   constexpr int RT_OFF = NBUF * STG, RT = C4 ? 0 : BM * 16;
-  __shared__ __attribute__((aligned(16))) char smem[NBUF * STG + RT];
+  constexpr int LUT_OFF = NBUF * STG + RT, LUTB = C4 ? kLutBytes : 0;   // C4: the u8 decode table
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * STG + RT + LUTB];
   float* red = reinterpret_cast<float*>(smem + E_TILE);   // [WGM][2][BN], after the epilogue tile
   const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
   constexpr int NTAPS = DGRAD ? 4 : 16;
@@ -665,7 +704,12 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
       vmask[j] = pin[j] ? tap_mask(rb[j], cb[j]) : 0u;
     }
   }
-  const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(p.src, int64_t(p.N) * p.SH * p.SW * p.C * 2);
+  const bool u8in = C4 && p.lut != nullptr;
+  const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(p.src, int64_t(p.N) * p.SH * p.SW * p.C * (u8in ? 1 : 2));
+  if (u8in) {
+    stage_lut(p.lut, smem + LUT_OFF);
+    __syncthreads();
+  }
   const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(p.w, int64_t(p.NOUT) * 16 * p.C * 2);
   const uint16_t* wrow = p.w + (n0 + ar) * (16 * p.C);   // B rows ar + 32 j: 32 * 16 * C elements apart
   uint4 ra[RJ + RB];   // staged A rows, then B rows (one array: SROA keeps it in registers)
@@ -675,13 +719,32 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     // taps (kh, kw) and (kh, kw + 1) of one row -- two adjacent input pixels,
     // each checked against the border on its own
     const int kh = ac >> 1, kw = (ac & 1) * 2;
+    if (u8in) {   // raw RGBA bytes -> bf16 through the LDS table (loads first, then the lookups)
+      uint32_t w0[RJ], w1[RJ];
+      bool k0[RJ], k1[RJ];
 #pragma unroll
-    for (int j = 0; j < RJ; ++j) {
-      const bool rok = pin[j] && unsigned(rb[j] + kh) < unsigned(p.SH);
-      const int e = (base[j] + kh * p.SW + kw) * 4;
-      const uint2 lo = bload8(rs_src, rok && unsigned(cb[j] + kw) < unsigned(p.SW) ? uint32_t(e) * 2u : kOOB);
-      const uint2 hi = bload8(rs_src, rok && unsigned(cb[j] + kw + 1) < unsigned(p.SW) ? uint32_t(e + 4) * 2u : kOOB);
-      ra[j] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      for (int j = 0; j < RJ; ++j) {
+        const bool rok = pin[j] && unsigned(rb[j] + kh) < unsigned(p.SH);
+        const int e = (base[j] + kh * p.SW + kw) * 4;
+        k0[j] = rok && unsigned(cb[j] + kw) < unsigned(p.SW);
+        k1[j] = rok && unsigned(cb[j] + kw + 1) < unsigned(p.SW);
+        w0[j] = bload4(rs_src, k0[j] ? uint32_t(e) : kOOB);
+        w1[j] = bload4(rs_src, k1[j] ? uint32_t(e + 4) : kOOB);
+      }
+#pragma unroll
+      for (int j = 0; j < RJ; ++j) {
+        const uint2 lo = lut_px(smem + LUT_OFF, w0[j], k0[j]), hi = lut_px(smem + LUT_OFF, w1[j], k1[j]);
+        ra[j] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < RJ; ++j) {
+        const bool rok = pin[j] && unsigned(rb[j] + kh) < unsigned(p.SH);
+        const int e = (base[j] + kh * p.SW + kw) * 4;
+        const uint2 lo = bload8(rs_src, rok && unsigned(cb[j] + kw) < unsigned(p.SW) ? uint32_t(e) * 2u : kOOB);
+        const uint2 hi = bload8(rs_src, rok && unsigned(cb[j] + kw + 1) < unsigned(p.SW) ? uint32_t(e + 4) * 2u : kOOB);
+        ra[j] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      }
     }
     // weights: 4 input channels, or 3 (an RGB model fed RGBA: channel 3 gets weight 0)
     const int tap = kh * 4 + kw;
@@ -1112,6 +1175,7 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
   if (p.px_per_slice <= 0 || p.px_per_slice % BPX != 0 || int64_t(p.slices) * p.px_per_slice < p.M)
     return hipErrorInvalidValue;
   if ((reinterpret_cast<uintptr_t>(p.x) | reinterpret_cast<uintptr_t>(p.dy)) & 15) return hipErrorInvalidValue;
+  if (p.lut && (p.Cin != 4 || (reinterpret_cast<uintptr_t>(p.lut) & 7))) return hipErrorInvalidValue;
   if (int64_t(p.N) * p.H * p.W * p.Cin * 2 >= int64_t(kOOB) || p.M * p.Cout * 2 >= int64_t(kOOB))
     return hipErrorInvalidValue;   // 32-bit buffer offsets
   const bool c4 = p.Cin == 4;
@@ -1258,6 +1322,8 @@ hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream) {
   g.GH = p.Ho, g.GW = p.Wo, g.M = int(p.M);
   g.NOUT = p.Cout, g.OH = p.Ho, g.OW = p.Wo;
   g.wc = p.Cin == 4 ? (p.w_channels > 0 ? p.w_channels : 4) : p.Cin;
+  g.lut = p.Cin == 4 ? p.lut : nullptr;
+  if (p.lut && (p.Cin != 4 || (reinterpret_cast<uintptr_t>(p.lut) & 7))) return hipErrorInvalidValue;
   g.acc_r = p.stats ? p.acc_r : 0;
   if (g.acc_r < 0 || g.acc_r > 64) return hipErrorInvalidValue;
   if (p.Cin == 4 && g.wc != 3 && g.wc != 4) return hipErrorInvalidValue;

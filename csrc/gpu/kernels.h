@@ -312,6 +312,7 @@ struct ConvWgradParams {
   int slices = 0;
   int64_t px_per_slice = 0;
   int cin_out = 0;   // dW input channels written (0: Cin); 3 for a 4-channel (RGBA-fed) first layer
+  const uint16_t* lut = nullptr;   // Cin == 4: x is raw u8 RGBA decoded through this bf16 table (ConvFwdParams)
   float* zero_out = nullptr;   // set by conv_wgrad: the kernel clears the output for the atomic reduce
   int zero_count = 0;
   // set by conv_wgrad: blocks [0, main_blocks) compute this layer, blocks
@@ -353,6 +354,10 @@ struct ConvFwdParams {
   int N = 0, H = 0, W = 0, Cin = 0, Ho = 0, Wo = 0, Cout = 0;
   int64_t M = 0;
   int w_channels = 0;   // Cin == 4 (first layer): 3 = an RGB weight [Cout][4][4][3], input channel 3 ignored
+  // Cin == 4: x is the RAW u8 RGBA frames [N][H][W][4] and lut their decode
+  // table as bf16 [4][256] (RNE of the fp32 table): the decode runs inside
+  // the convolution's tile loads (padding stays 0)
+  const uint16_t* lut = nullptr;
   int acc_r = 0;        // > 0: stats points at a bn_apply_acc accumulator (fp64 [acc_r][2][Cout], atomic adds)
 };
 // Cin a power of two >= 8, or Cin == 4 (first layer, RGBA-decoded frames); Cout % 32 == 0.

@@ -238,9 +238,10 @@ PYBIND11_MODULE(_hip, m) {
   m.def("conv_wgrad",
         [](uintptr_t x, uintptr_t dy, uintptr_t partial, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
            int slices, int64_t px_per_slice, uintptr_t out, int64_t s_co, int64_t s_ci, int64_t s_kh, int64_t s_kw,
-           uintptr_t stream, int cin_out, bool defer, py::object side) -> py::object {
+           uintptr_t stream, int cin_out, bool defer, py::object side, uintptr_t lut) -> py::object {
           ConvWgradParams p;
           p.cin_out = cin_out;
+          p.lut = ptr<const uint16_t>(lut);
           p.x = ptr<const uint16_t>(x);
           p.dy = ptr<const uint16_t>(dy);
           p.partial = ptr<float>(partial);
@@ -260,7 +261,7 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("x"), py::arg("dy"), py::arg("partial"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("Cin"),
         py::arg("Ho"), py::arg("Wo"), py::arg("Cout"), py::arg("slices"), py::arg("px_per_slice"), py::arg("out"),
         py::arg("s_co"), py::arg("s_ci"), py::arg("s_kh"), py::arg("s_kw"), py::arg("stream"), py::arg("cin_out") = 0,
-        py::arg("defer") = false, py::arg("side") = py::none());
+        py::arg("defer") = false, py::arg("side") = py::none(), py::arg("lut") = 0);
   // a deferred slice reduce on its own (a weight-gradient chain that ended early)
   m.def("conv_wgrad_reduce", [](py::tuple r, uintptr_t stream) {
     check(conv_wgrad_reduce(reduce_from_tuple(r), stream_of(stream)), "conv_wgrad_reduce");
@@ -327,8 +328,9 @@ PYBIND11_MODULE(_hip, m) {
         });
   m.def("conv_fwd",
         [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, int N, int H, int W, int Cin, int Ho, int Wo,
-           int Cout, uintptr_t stream, int w_channels, int acc_r) {
+           int Cout, uintptr_t stream, int w_channels, int acc_r, uintptr_t lut) {
           ConvFwdParams p;
+          p.lut = ptr<const uint16_t>(lut);
           p.w_channels = w_channels;
           p.acc_r = acc_r;
           p.x = ptr<const uint16_t>(x);
@@ -341,7 +343,7 @@ PYBIND11_MODULE(_hip, m) {
         },
         py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"), py::arg("N"), py::arg("H"), py::arg("W"),
         py::arg("Cin"), py::arg("Ho"), py::arg("Wo"), py::arg("Cout"), py::arg("stream"), py::arg("w_channels") = 0,
-        py::arg("acc_r") = 0);
+        py::arg("acc_r") = 0, py::arg("lut") = 0);
   // BatchNorm+LeakyReLU forward from conv_fwd's per-tile statistics: finalize + apply
   m.def("bn_forward_from_stats",
         [](uintptr_t x, uintptr_t y, int64_t M, int C, int dtype, uintptr_t stats, int nrows, float eps,

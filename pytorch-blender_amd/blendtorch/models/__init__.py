@@ -90,16 +90,20 @@ class Discriminator(nn.Module):
         ``mfma=False`` is bit-identical to autocast over :meth:`forward`."""
         return self._run_bf16(x, list(self.features), mfma).view(-1, 1).squeeze(1)
 
-    def bce_loss_bf16(self, x, target=1.0, mfma=True):
+    def bce_loss_bf16(self, x, target=1.0, mfma=True, decode=None):
         """Mean binary cross-entropy of :meth:`forward_bf16`'s output against
         ``target`` (scalar or [N]), with the head (pool -> 4x4 conv -> sigmoid
         -> BCE) fused into ``ops.disc_head_bce`` (2 launches forward, 2
         backward, instead of ~20 library kernels; fp32 weight and gradient).
         Falls back to :meth:`forward_bf16` + ``BCELoss`` off that shape.
-        Returns the loss."""
-        return self.bce_bf16(x, target, mfma, probs=False)[0]
+        ``decode`` (an RGBA ``ops.DecodeConfig``): ``x`` is the RAW u8 RGBA
+        frames ([N, 4, H, W] channels-last, i.e. NHWC bytes) and the first
+        convolution decodes them inside its MFMA kernels' loads -- the same
+        values as ``ops.decode`` to bf16 NHWC, without the decode pass and its
+        bf16 copy of the batch.  Returns the loss."""
+        return self.bce_bf16(x, target, mfma, probs=False, decode=decode)[0]
 
-    def bce_bf16(self, x, target=1.0, mfma=True, probs=True):
+    def bce_bf16(self, x, target=1.0, mfma=True, probs=True, decode=None):
         """``(mean BCE loss, per-sample probabilities)`` of the bf16 forward
         (``probs=False``: the fused head's logits are not turned into
         probabilities -- one kernel fewer when only the loss is used).
@@ -122,8 +126,13 @@ class Discriminator(nn.Module):
         ok = (head is not None and x.is_cuda and head.out_channels == 1 and head.bias is None
               and head.stride == (1, 1) and head.padding == (0, 0) and head.groups == 1
               and head.in_channels % 8 == 0)
+        lut = None
+        if decode is not None:
+            if not (ok and mfma and x.dtype == torch.uint8):
+                raise ValueError('bce_bf16(decode=): raw u8 RGBA frames on the fused-head MFMA path only')
+            lut = ops.decode_lut_bf16(decode, x.device)
         if ok:
-            z, link = self._run_bf16(x, body, mfma, want_link=True)
+            z, link = self._run_bf16(x, body, mfma, want_link=True, lut=lut)
             if adaptive or tuple(z.shape[2:]) == pool:
                 if not z.is_contiguous(memory_format=torch.channels_last):
                     z, link = z.contiguous(memory_format=torch.channels_last), None
@@ -136,7 +145,7 @@ class Discriminator(nn.Module):
         tgt = target if isinstance(target, torch.Tensor) else torch.full_like(out, float(target))
         return F.binary_cross_entropy(out, tgt), out
 
-    def _run_bf16(self, x, layers, mfma, want_link=False):
+    def _run_bf16(self, x, layers, mfma, want_link=False, lut=None):
         import torch.nn.functional as F
         from .. import ops
         convs = [m for m in layers if isinstance(m, nn.Conv2d)]
@@ -174,10 +183,12 @@ class Discriminator(nn.Module):
                 if on_mfma:
                     nxt = layers[i + 1] if i + 1 < len(layers) else None
                     fuse = (isinstance(nxt, ops.BatchNormLeakyReLU2d) and ops.conv_fwd_supported(x, w16)
-                            and nxt.fused_with_stats(x.new_empty((1, m.out_channels, 1, 1))))
+                            and nxt.fused_with_stats(x.new_empty((1, m.out_channels, 1, 1), dtype=torch.bfloat16)))
                     # the BN that produced x: this conv's data gradient does its backward reduction
                     bl, link = link, None
                     wk = dict(wt=wts.get(ci), bn_link=bl, wchain=wchain, wlast=first_mfma)
+                    if ci == 0 and lut is not None:
+                        wk['lut'] = lut    # raw u8 frames: decoded in this layer's kernels
                     first_mfma = False
                     if fuse and ops.bn_acc_supported(m.out_channels):
                         # BN statistics come out of the conv kernel's epilogue, added into
@@ -189,6 +200,8 @@ class Discriminator(nn.Module):
                     else:
                         x = ops.conv4x4s2(x, m.weight, w16, **wk)
                 else:
+                    if ci == 0 and lut is not None:
+                        raise ValueError('raw u8 frames need the MFMA first layer')
                     link = None
                     x = F.conv2d(x, w16, None, m.stride, m.padding, m.dilation, m.groups)
             elif stats is not None and isinstance(m, ops.BatchNormLeakyReLU2d):

@@ -1040,13 +1040,32 @@ def conv_wgrad_supported(x, weight):
     """True when :func:`conv4x4s2` can take ``x`` (bf16 channels-last GPU
     activations) and ``weight`` ([Cout, Cin, 4, 4] fp32) on the MFMA path."""
     import torch
-    if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and weight.dim() == 4):
+    if not (x.is_cuda and x.dtype in (torch.bfloat16, torch.uint8) and x.dim() == 4 and weight.dim() == 4):
         return False
     cout, cin, kh, kw = weight.shape
     xc = x.shape[1]
-    big = xc == cin and cin % 32 == 0 and cout % 64 == 0
-    first = xc == 4 and cin in (3, 4) and cout % 32 == 0     # RGBA-fed first layer
+    big = xc == cin and cin % 32 == 0 and cout % 64 == 0 and x.dtype == torch.bfloat16
+    # RGBA-fed first layer: decoded bf16 frames, or the raw u8 frames (decode fused, lut=)
+    first = xc == 4 and cin in (3, 4) and cout % 32 == 0
     return (kh, kw) == (4, 4) and (big or first) and x.is_contiguous(memory_format=torch.channels_last)
+
+
+_LUTS = {}
+
+
+def decode_lut_bf16(cfg: DecodeConfig, device):
+    """bf16 [4 * 256] value table of ``cfg`` (RNE of :func:`build_lut`'s fp32
+    table) on ``device``: what the first convolution reads raw u8 RGBA frames
+    through (``conv4x4s2(..., lut=)``) -- the same values the decode kernel
+    writes for a bf16 NHWC RGBA output.  Cached per (config, device)."""
+    import torch
+    if cfg.cmap != [0, 1, 2, 3] or cfg.flip or cfg.color_matrix is not None:
+        raise ValueError('decode_lut_bf16: RGBA identity channel map, no flip, no colour matrix')
+    key = (cfg, str(device))
+    t = _LUTS.get(key)
+    if t is None:
+        t = _LUTS[key] = torch.from_numpy(build_lut(cfg).reshape(-1).copy()).to(torch.bfloat16).to(device)
+    return t
 
 
 class WgradChain:
@@ -1068,13 +1087,15 @@ class WgradChain:
             self.pending = self.keep = None
 
 
-def conv_wgrad(x, dy, out, target_blocks=None, chain=None, last=True):
+def conv_wgrad(x, dy, out, target_blocks=None, chain=None, last=True, lut=None):
     """fp32 weight gradient of a 4x4/s2/p1 convolution into ``out`` ([Cout, Cin,
     4, 4], any strides): MFMA tiles over pixel slices + one slice-reduce
     launch.  ``x`` [N, Cin, H, W] and ``dy`` [N, Cout, H/2, W/2] are bf16 with
     channels-last memory.  ``chain`` (:class:`WgradChain`): run the chain's
     pending reduce inside this launch, and leave this layer's to the next
-    call unless ``last`` -- ``out`` is then complete only after that call."""
+    call unless ``last`` -- ``out`` is then complete only after that call.
+    ``lut``: ``x`` is raw u8 RGBA frames read through this decode table
+    (:func:`decode_lut_bf16`)."""
     import torch
     ext = hip_ext()
     N, Cin, H, W = x.shape
@@ -1098,9 +1119,11 @@ def conv_wgrad(x, dy, out, target_blocks=None, chain=None, last=True):
     _count('conv_wgrad')
     side = chain.pending if chain is not None else None
     defer = chain is not None and not last
+    if (lut is not None) != (x.dtype == torch.uint8) or (lut is not None and Cin != 4):
+        raise ValueError('conv_wgrad: u8 input (4 channels) needs its decode table lut, and only u8 takes one')
     res = ext.conv_wgrad(x.data_ptr(), dy.data_ptr(), partial.data_ptr(), N, H, W, Cin, Ho, Wo, Cout, slices, px,
                          out.data_ptr(), out.stride(0), out.stride(1), out.stride(2), out.stride(3), _stream(x.device),
-                         cin_out, defer, side)
+                         cin_out, defer, side, lut.data_ptr() if lut is not None else 0)
     if chain is not None:
         if side is not None:
             _count('conv_wgrad_side_reduce')
@@ -1108,7 +1131,7 @@ def conv_wgrad(x, dy, out, target_blocks=None, chain=None, last=True):
     return out
 
 
-def conv_fwd(x, w16, stats=None, acc_r=0):
+def conv_fwd(x, w16, stats=None, acc_r=0, lut=None):
     """y = conv2d(x, w16, stride 2, pad 1) on the gfx950 MFMA kernel: ``x``
     [N, Cin, H, W] bf16 channels-last, ``w16`` [Cout, Cin, 4, 4] bf16
     channels-last; returns channels-last bf16 y.  ``stats`` (optional fp32
@@ -1116,7 +1139,10 @@ def conv_fwd(x, w16, stats=None, acc_r=0):
     BatchNorm sums of y, channel-major: ``stats.view(2, Cout, rows)`` holds
     the sums, then the sums of squares (see :func:`batch_norm_from_stats`).
     ``acc_r`` > 0: ``stats`` is a :class:`BnAccumulator`'s zeroed fp64
-    ``fwd`` tensor with ``acc_r`` replicas, added into with atomics."""
+    ``fwd`` tensor with ``acc_r`` replicas, added into with atomics.
+    ``lut`` (first layer): ``x`` is the raw u8 RGBA frames ([N, 4, H, W],
+    channels-last) and ``lut`` their bf16 decode table (:func:`decode_lut_bf16`):
+    the decode happens in the convolution's tile loads."""
     import torch
     ext = hip_ext()
     N, Cin, H, W = x.shape
@@ -1124,8 +1150,11 @@ def conv_fwd(x, w16, stats=None, acc_r=0):
     cl = torch.channels_last
     # first layer fed RGBA: a 3-input-channel weight, the 4th input channel ignored
     wc = 3 if (Cin == 4 and w16.shape[1] == 3) else Cin
-    if tuple(w16.shape) != (Cout, wc, 4, 4) or w16.dtype != torch.bfloat16 or x.dtype != torch.bfloat16:
+    xdt = torch.uint8 if lut is not None else torch.bfloat16
+    if tuple(w16.shape) != (Cout, wc, 4, 4) or w16.dtype != torch.bfloat16 or x.dtype != xdt:
         raise ValueError(f'conv_fwd: x {x.dtype} {tuple(x.shape)} / w {w16.dtype} {tuple(w16.shape)}')
+    if lut is not None and (Cin != 4 or lut.dtype != torch.bfloat16 or lut.numel() != 1024 or lut.device != x.device):
+        raise ValueError('conv_fwd: u8 input takes 4 channels and a bf16 [1024] decode table (decode_lut_bf16)')
     if not (x.is_contiguous(memory_format=cl) and w16.is_contiguous(memory_format=cl)):
         raise ValueError('conv_fwd needs channels-last x and weight')
     Ho, Wo = (H - 2) // 2 + 1, (W - 2) // 2 + 1
@@ -1134,7 +1163,8 @@ def conv_fwd(x, w16, stats=None, acc_r=0):
     if acc_r and (stats is None or stats.dtype != torch.float64 or stats.numel() < 2 * Cout * acc_r):
         raise ValueError('conv_fwd: acc_r needs an fp64 accumulator of 2 * Cout * acc_r elements')
     ext.conv_fwd(x.data_ptr(), w16.data_ptr(), y.data_ptr(), stats.data_ptr() if stats is not None else 0,
-                 N, H, W, Cin, Ho, Wo, Cout, _stream(x.device), wc if Cin == 4 else 0, int(acc_r))
+                 N, H, W, Cin, Ho, Wo, Cout, _stream(x.device), wc if Cin == 4 else 0, int(acc_r),
+                 lut.data_ptr() if lut is not None else 0)
     return y
 
 
@@ -1207,7 +1237,9 @@ def conv_dgrad_supported(x, w):
 
 def conv_fwd_supported(x, w):
     import torch
-    if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and w.dim() == 4):
+    if not (x.is_cuda and x.dim() == 4 and w.dim() == 4):
+        return False
+    if not (x.dtype == torch.bfloat16 or (x.dtype == torch.uint8 and x.shape[1] == 4)):
         return False
     cout, cin, kh, kw = w.shape
     xc = x.shape[1]
@@ -1243,11 +1275,17 @@ def _conv_function():
         into the master weight's gradient (no bf16 round trip, no cast)."""
 
         @staticmethod
-        def forward(ctx, x, w32, w16, with_stats=False, wt=None, bn_link=None, wchain=None, wlast=True):
+        def forward(ctx, x, w32, w16, with_stats=False, wt=None, bn_link=None, wchain=None, wlast=True, lut=None):
             ctx.set_materialize_grads(False)   # no zero-filled gradient for the stats output
             ctx.save_for_backward(x, w16)
             ctx.w32, ctx.wt, ctx.bn_link = w32, wt, bn_link
-            ctx.wchain, ctx.wlast = wchain, wlast
+            ctx.wchain, ctx.wlast, ctx.lut = wchain, wlast, lut
+            if lut is not None:   # raw u8 frames: the decode runs in the MFMA kernels' loads
+                if isinstance(with_stats, BnAccumulator):
+                    return conv_fwd(x, w16, with_stats.fwd, with_stats.R, lut=lut)
+                if with_stats:
+                    raise ValueError('conv4x4s2: u8 input takes accumulator statistics only')
+                return conv_fwd(x, w16, lut=lut)
             if isinstance(with_stats, BnAccumulator):
                 return conv_fwd(x, w16, with_stats.fwd, with_stats.R)
             if with_stats:
@@ -1270,7 +1308,7 @@ def _conv_function():
             if gy is None:
                 if ctx.wchain is not None and ctx.wlast:
                     ctx.wchain.flush(x.device)
-                return None, None, None, None, None, None, None, None
+                return None, None, None, None, None, None, None, None, None
             gy = gy.contiguous(memory_format=torch.channels_last)
             gx = gw = None
             if ctx.needs_input_grad[0]:
@@ -1290,12 +1328,12 @@ def _conv_function():
                 chain = ctx.wchain if (sunk or ctx.wlast) else None
                 if ctx.wchain is not None and chain is None:
                     ctx.wchain.flush(x.device)
-                gw = conv_wgrad(x, gy, out, chain=chain, last=ctx.wlast or chain is None)
+                gw = conv_wgrad(x, gy, out, chain=chain, last=ctx.wlast or chain is None, lut=ctx.lut)
                 if sunk:
                     gw = None      # written into the parameter's bucket view
             elif ctx.wchain is not None:
                 ctx.wchain.flush(x.device)
-            return gx, gw, None, None, None, None, None, None
+            return gx, gw, None, None, None, None, None, None, None
 
     return _Conv4x4s2
 
@@ -1303,7 +1341,7 @@ def _conv_function():
 _CONV_FN = None
 
 
-def conv4x4s2(x, w32, w16, with_stats=False, wt=None, bn_link=None, wchain=None, wlast=True):
+def conv4x4s2(x, w32, w16, with_stats=False, wt=None, bn_link=None, wchain=None, wlast=True, lut=None):
     """4x4 / stride-2 / pad-1 convolution of bf16 channels-last ``x`` with the
     bf16 copy ``w16`` of fp32 weight ``w32``; the gradient goes to ``w32``
     (fp32, from the MFMA weight-gradient kernel).  See :func:`conv_wgrad_supported`.
@@ -1314,13 +1352,14 @@ def conv4x4s2(x, w32, w16, with_stats=False, wt=None, bn_link=None, wchain=None,
     ``x``; the data gradient then also computes that BN's backward sums.
     ``wchain`` / ``wlast``: the :class:`WgradChain` of the model's backward;
     ``wlast`` marks the layer whose weight gradient is computed last (the
-    first layer)."""
+    first layer).  ``lut``: ``x`` is raw u8 RGBA frames decoded through this
+    table inside the kernels (:func:`decode_lut_bf16`; no gradient for ``x``)."""
     global _CONV_FN
     if _CONV_FN is None:
         _CONV_FN = _conv_function()
     if with_stats and not conv_fwd_supported(x, w16):
         raise ValueError('conv4x4s2(with_stats=True) needs the MFMA forward (see conv_fwd_supported)')
-    return _CONV_FN.apply(x, w32, w16.detach(), with_stats, wt, bn_link, wchain, wlast)
+    return _CONV_FN.apply(x, w32, w16.detach(), with_stats, wt, bn_link, wchain, wlast, lut)
 
 
 # ---------------------------------------------------------------------------

@@ -316,3 +316,39 @@ def test_wgrad_chain_defers_slice_reduces(dev):
     assert ops.KERNEL_CALLS.get('conv_wgrad_side_reduce', 0) == before + 3
     for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
         torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-4, atol=1e-6 + 1e-4 * float(pb.grad.abs().max()), msg=n)
+
+
+@pytest.mark.gpu
+def test_first_layer_reads_raw_u8_frames_through_decode_table(dev):
+    """Decode fused into the first convolution: raw u8 RGBA frames through the
+    bf16 decode table give bit-identical forward outputs and weight gradients
+    to ops.decode -> bf16 NHWC -> the same layer; and the whole disc step
+    (bce_loss_bf16(decode=)) matches the decode-first step."""
+    from blendtorch.models import Discriminator
+    cl = torch.channels_last
+    cfg = ops.DecodeConfig.unit(channels='rgba', gamma=2.2, dtype='bfloat16', layout='nhwc')
+    g = torch.Generator(device=dev).manual_seed(4)
+    raw = torch.randint(0, 256, (3, 48, 64, 4), dtype=torch.uint8, device=dev, generator=g)
+    xu8 = raw.permute(0, 3, 1, 2)                         # [N, 4, H, W], NHWC bytes
+    xdec = ops.decode(raw, cfg).permute(0, 3, 1, 2)       # bf16 NHWC as [N, 4, H, W]
+    lut = ops.decode_lut_bf16(cfg, dev)
+    w = (0.1 * torch.randn(32, 3, 4, 4, device=dev, generator=g)).to(torch.bfloat16).contiguous(memory_format=cl)
+    ya = ops.conv_fwd(xu8, w, lut=lut)
+    yb = ops.conv_fwd(xdec, w)
+    assert torch.equal(ya, yb)
+    dy = torch.randn(3, 32, 24, 32, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    oa = ops.conv_wgrad(xu8, dy, torch.empty(32, 3, 4, 4, device=dev), lut=lut)
+    ob = ops.conv_wgrad(xdec, dy, torch.empty(32, 3, 4, 4, device=dev))
+    # slice groups add with float atomics: equal up to the adds' order
+    torch.testing.assert_close(oa, ob, rtol=1e-4, atol=1e-4 * float(ob.abs().max()))
+    torch.manual_seed(2)
+    a = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
+    b = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
+    b.load_state_dict(a.state_dict())
+    la = a.bce_loss_bf16(xu8, 1.0, decode=cfg)
+    lb = b.bce_loss_bf16(xdec, 1.0)
+    torch.testing.assert_close(la, lb, rtol=1e-5, atol=1e-6)
+    la.backward()
+    lb.backward()
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-3, atol=1e-5 + 1e-3 * float(pb.grad.abs().max()), msg=n)
