@@ -328,7 +328,7 @@ def test_first_layer_reads_raw_u8_frames_through_decode_table(dev):
     cl = torch.channels_last
     cfg = ops.DecodeConfig.unit(channels='rgba', gamma=2.2, dtype='bfloat16', layout='nhwc')
     g = torch.Generator(device=dev).manual_seed(4)
-    raw = torch.randint(0, 256, (3, 48, 64, 4), dtype=torch.uint8, device=dev, generator=g)
+    raw = torch.randint(0, 256, (3, 96, 128, 4), dtype=torch.uint8, device=dev, generator=g)
     xu8 = raw.permute(0, 3, 1, 2)                         # [N, 4, H, W], NHWC bytes
     xdec = ops.decode(raw, cfg).permute(0, 3, 1, 2)       # bf16 NHWC as [N, 4, H, W]
     lut = ops.decode_lut_bf16(cfg, dev)
@@ -336,7 +336,7 @@ def test_first_layer_reads_raw_u8_frames_through_decode_table(dev):
     ya = ops.conv_fwd(xu8, w, lut=lut)
     yb = ops.conv_fwd(xdec, w)
     assert torch.equal(ya, yb)
-    dy = torch.randn(3, 32, 24, 32, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    dy = torch.randn(3, 32, 48, 64, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
     oa = ops.conv_wgrad(xu8, dy, torch.empty(32, 3, 4, 4, device=dev), lut=lut)
     ob = ops.conv_wgrad(xdec, dy, torch.empty(32, 3, 4, 4, device=dev))
     # slice groups add with float atomics: equal up to the adds' order
