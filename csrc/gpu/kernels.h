@@ -85,6 +85,7 @@ struct DecodeParams {
   uint64_t flip_bits[4] = {0, 0, 0, 0};   // per-image flip for b < 256
   int out_dtype = OUT_F32;
   int layout = NCHW;
+  int xf_table_only = 0;   // 1: the caller built `lut` in table mode (header mode 0); replay picks its table-only kernel
 };
 hipError_t decode(const DecodeParams& p, hipStream_t stream);
 

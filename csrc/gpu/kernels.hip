@@ -157,9 +157,9 @@ __device__ __forceinline__ float xf_value(const Xf& xf, int c, uint32_t v) {
 // branches on it once (scalar branch) into a fully static body, so every
 // byte of `px` is addressed with a compile-time index and `px` stays in
 // VGPRs (a dynamically indexed byte array would be spilled to scratch).
-template <int PPT, int CIN, int IC>
+template <int PPT, int CIN, int IC, bool TBL = false>
 __device__ __forceinline__ void lookup_static(const Pixels<PPT, CIN>& px, const Xf& xf, int c, float (&o)[PPT]) {
-  if (!xf.arith) {
+  if (TBL || !xf.arith) {   // TBL: the host promised a table-mode value table (no arithmetic code at all)
     const float* l = xf.lut + c * 256;
 #pragma unroll
     for (int i = 0; i < PPT; ++i) o[i] = l[px.v[i * CIN + IC]];
@@ -192,24 +192,24 @@ __device__ __forceinline__ void lookup_static(const Pixels<PPT, CIN>& px, const 
   }
 }
 
-template <int PPT, int CIN>
+template <int PPT, int CIN, bool TBL = false>
 __device__ __forceinline__ void lookup(const Pixels<PPT, CIN>& px, int ic, const Xf& xf, int c, float (&o)[PPT]) {
   switch (ic) {
-    case 0: lookup_static<PPT, CIN, 0>(px, xf, c, o); break;
-    case 1: if constexpr (CIN > 1) lookup_static<PPT, CIN, 1>(px, xf, c, o); break;
-    case 2: if constexpr (CIN > 2) lookup_static<PPT, CIN, 2>(px, xf, c, o); break;
-    default: if constexpr (CIN > 3) lookup_static<PPT, CIN, 3>(px, xf, c, o); break;
+    case 0: lookup_static<PPT, CIN, 0, TBL>(px, xf, c, o); break;
+    case 1: if constexpr (CIN > 1) lookup_static<PPT, CIN, 1, TBL>(px, xf, c, o); break;
+    case 2: if constexpr (CIN > 2) lookup_static<PPT, CIN, 2, TBL>(px, xf, c, o); break;
+    default: if constexpr (CIN > 3) lookup_static<PPT, CIN, 3, TBL>(px, xf, c, o); break;
   }
 }
 
-template <int PPT, int CIN, int OUTT, int COUT>
+template <int PPT, int CIN, int OUTT, int COUT, bool TBL = false>
 __device__ __forceinline__ void store_nhwc(const DecodeParams& p, const Xf& xf, const int* cm,
                                            const Pixels<PPT, CIN>& px, int b, int64_t q, int64_t HW) {
   constexpr int N = PPT * COUT;
   const int64_t off = q * COUT;   // within image b (NHWC)
   float v[COUT][PPT];
 #pragma unroll
-  for (int c = 0; c < COUT; ++c) lookup<PPT, CIN>(px, cm[c], xf, c, v[c]);
+  for (int c = 0; c < COUT; ++c) lookup<PPT, CIN, TBL>(px, cm[c], xf, c, v[c]);
   if constexpr (OUTT == OUT_F32) {
     float o[N];
 #pragma unroll
@@ -281,7 +281,7 @@ __device__ __forceinline__ Group locate(const DecodeParams& p, int64_t g, int64_
   return r;
 }
 
-template <int PPT, int CIN, int OUTT, int LAYOUT>
+template <int PPT, int CIN, int OUTT, int LAYOUT, bool TBL = false>
 __device__ __forceinline__ void emit(const DecodeParams& p, const Xf& xf, const int* cm, int cout, int64_t HW,
                                      const Group& gr, const Pixels<PPT, CIN>& px) {
   const int b = gr.b;
@@ -291,7 +291,7 @@ __device__ __forceinline__ void emit(const DecodeParams& p, const Xf& xf, const 
     for (int c = 0; c < 4; ++c) {
       if (c >= cout) break;
       float v[PPT];
-      lookup<PPT, CIN>(px, cm[c], xf, c, v);
+      lookup<PPT, CIN, TBL>(px, cm[c], xf, c, v);
       const int64_t off = int64_t(c) * HW + q;   // within image b (NCHW)
       if constexpr (OUTT == OUT_F32) {
         float* d = image_out<float>(p, b, HW * cout) + off;
@@ -317,10 +317,10 @@ __device__ __forceinline__ void emit(const DecodeParams& p, const Xf& xf, const 
     // NHWC (channels_last): PPT*COUT contiguous elements, assembled in
     // registers and written as 16-byte stores (PPT*sizeof(T) == 16).
     switch (cout) {
-      case 1: store_nhwc<PPT, CIN, OUTT, 1>(p, xf, cm, px, b, q, HW); break;
-      case 2: store_nhwc<PPT, CIN, OUTT, 2>(p, xf, cm, px, b, q, HW); break;
-      case 3: store_nhwc<PPT, CIN, OUTT, 3>(p, xf, cm, px, b, q, HW); break;
-      default: store_nhwc<PPT, CIN, OUTT, 4>(p, xf, cm, px, b, q, HW); break;
+      case 1: store_nhwc<PPT, CIN, OUTT, 1, TBL>(p, xf, cm, px, b, q, HW); break;
+      case 2: store_nhwc<PPT, CIN, OUTT, 2, TBL>(p, xf, cm, px, b, q, HW); break;
+      case 3: store_nhwc<PPT, CIN, OUTT, 3, TBL>(p, xf, cm, px, b, q, HW); break;
+      default: store_nhwc<PPT, CIN, OUTT, 4, TBL>(p, xf, cm, px, b, q, HW); break;
     }
   }
 }
@@ -653,7 +653,10 @@ __device__ __forceinline__ void replay_meta(const ReplayParams& r, const ReplayS
   }
 }
 
-template <int PPT, int CIN, int OUTT, int LAYOUT>
+// TBL: the value table is in table mode (p.xf_table_only): the lookups are
+// plain LDS reads and the kernel carries none of the arithmetic-form code
+// (whose registers cut the general kernel to 4 waves per SIMD)
+template <int PPT, int CIN, int OUTT, int LAYOUT, bool TBL>
 __global__ __launch_bounds__(kBlock) void replay_vec_kernel(DecodeParams p, ReplayParams r, int64_t meta_units) {
   __shared__ ReplayShared sh;
   const int64_t HW = int64_t(p.H) * p.W;
@@ -698,7 +701,7 @@ __global__ __launch_bounds__(kBlock) void replay_vec_kernel(DecodeParams p, Repl
       continue;
     }
     if (g == g0) {
-      emit<PPT, CIN, OUTT, LAYOUT>(p, xf, cm, cout, HW, gr0, px0);
+      emit<PPT, CIN, OUTT, LAYOUT, TBL>(p, xf, cm, cout, HW, gr0, px0);
       continue;
     }
     Group gr;
@@ -708,7 +711,7 @@ __global__ __launch_bounds__(kBlock) void replay_vec_kernel(DecodeParams p, Repl
     gr.src = p.src + sh.idx[gr.b] * r.frame_bytes + (int64_t(sy) * p.W + x) * CIN;
     Pixels<PPT, CIN> px;
     load_pixels<PPT, CIN>(gr.src, px);
-    emit<PPT, CIN, OUTT, LAYOUT>(p, xf, cm, cout, HW, gr, px);
+    emit<PPT, CIN, OUTT, LAYOUT, TBL>(p, xf, cm, cout, HW, gr, px);
   }
 }
 
@@ -749,7 +752,11 @@ hipError_t launch_replay(const DecodeParams& p, const ReplayParams& r, int64_t m
                    (int64_t(p.H) * p.W * p.Cin) % 16 == 0;
   if (vec) {
     const int grid = grid_for(int64_t(p.B) * p.H * p.W / PPT + meta_units, p.max_grid);
-#define BT_REPLAY(CIN, LAY) replay_vec_kernel<PPT, CIN, OUTT, LAY><<<grid, kBlock, 0, s>>>(p, r, meta_units)
+#define BT_REPLAY(CIN, LAY)                                                                  \
+  do {                                                                                       \
+    if (p.xf_table_only) replay_vec_kernel<PPT, CIN, OUTT, LAY, true><<<grid, kBlock, 0, s>>>(p, r, meta_units); \
+    else replay_vec_kernel<PPT, CIN, OUTT, LAY, false><<<grid, kBlock, 0, s>>>(p, r, meta_units);               \
+  } while (0)
     if (p.Cin == 4) {
       if (p.layout == NCHW) BT_REPLAY(4, NCHW);
       else BT_REPLAY(4, NHWC);

@@ -184,8 +184,9 @@ PYBIND11_MODULE(_hip, m) {
         [](uintptr_t store, int64_t count, uintptr_t dst, uintptr_t lut, int B, int H, int W, int Cin, int Cout,
            std::vector<int> cmap, int flip_all, int out_dtype, int layout, uint64_t seed, uintptr_t counter,
            uint64_t ctr_value, uintptr_t index_in, uintptr_t index_out, std::vector<uintptr_t> meta_src, std::vector<uintptr_t> meta_dst,
-           std::vector<int> meta_bytes, uintptr_t stream) {
+           std::vector<int> meta_bytes, uintptr_t stream, int xf_table_only) {
           DecodeParams p;
+          p.xf_table_only = xf_table_only;
           p.src = ptr<const uint8_t>(store);
           p.dst = ptr<void>(dst);
           p.lut = ptr<const float>(lut);
@@ -216,7 +217,7 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("store"), py::arg("count"), py::arg("dst"), py::arg("lut"), py::arg("B"), py::arg("H"), py::arg("W"),
         py::arg("Cin"), py::arg("Cout"), py::arg("cmap"), py::arg("flip_all"), py::arg("out_dtype"), py::arg("layout"),
         py::arg("seed"), py::arg("counter"), py::arg("ctr_value"), py::arg("index_in"), py::arg("index_out"), py::arg("meta_src"),
-        py::arg("meta_dst"), py::arg("meta_bytes"), py::arg("stream"));
+        py::arg("meta_dst"), py::arg("meta_bytes"), py::arg("stream"), py::arg("xf_table_only") = 0);
 
   m.def("multi_cast",
         [](std::vector<uintptr_t> src, std::vector<uintptr_t> dst, std::vector<int64_t> numel, int mode,

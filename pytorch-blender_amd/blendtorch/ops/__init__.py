@@ -378,9 +378,18 @@ def device_lut(cfg: DecodeConfig, device):
     key = (cfg, str(device))
     t = _lut_cache.get(key)
     if t is None:
-        t = torch.from_numpy(build_table(cfg)).to(device)
+        tab = build_table(cfg)
+        t = torch.from_numpy(tab).to(device)
         _lut_cache[key] = t
+        _lut_cache[('mode',) + key] = int(tab[XF_HEADER])
     return t
+
+
+def table_only(cfg: DecodeConfig, device) -> int:
+    """1 when ``device_lut(cfg, device)`` is in table mode (header mode 0):
+    kernels may then take their table-only variant."""
+    device_lut(cfg, device)
+    return int(_lut_cache[('mode', cfg, str(device))] == 0)
 
 
 def _stream(device):
@@ -516,7 +525,7 @@ def replay_sample(store, count: int, batch: int, cfg: DecodeConfig = DecodeConfi
     ext.replay_sample(store.data_ptr(), int(count), out.data_ptr(), lut.data_ptr(), batch, H, W, C, cfg.cout,
                       cfg.cmap, int(cfg.flip), OUT_DTYPES[cfg.dtype], LAYOUTS[cfg.layout], int(seed) & (2 ** 64 - 1),
                       ctr_ptr, ctr_value, idx_in, idx_out.data_ptr(), src, dst, nbytes,
-                      _stream(dev))
+                      _stream(dev), table_only(cfg, dev))
     return out, idx_out, mout
 
 
