@@ -34,6 +34,7 @@
 #include <cstdlib>
 #include <cstdint>
 
+#include "bn_fold.h"
 #include "kernels.h"
 
 namespace btn {
@@ -196,11 +197,21 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_reduce_kernel(ConvWgradPa
   wgrad_reduce_block(r, int(blockIdx.x), int(blockIdx.y));
 }
 
-// blocks past the main grid: a previous layer's deferred reduce (the side job)
-__device__ __forceinline__ bool run_side(const ConvWgradParams& p) {
-  const int b = int(blockIdx.x) - main_blocks(p);
+// blocks past the main grid: a previous layer's deferred reduce (the side
+// job), then -- one block -- the BN statistics fold the preceding data
+// gradient's epilogue accumulated (ConvWgradParams::fold)
+__device__ __forceinline__ bool run_side(const ConvWgradParams& p, char* lds) {
+  int b = int(blockIdx.x) - main_blocks(p);
   if (b < 0) return false;
-  wgrad_reduce_block(p.side, b % p.side.rx, b / p.side.rx);
+  const int nred = p.side.partial ? p.side.rx * p.side.ry : 0;
+  if (b < nred) {
+    wgrad_reduce_block(p.side, b % p.side.rx, b / p.side.rx);
+    return true;
+  }
+  BnFold f;
+  f.acc = p.fold.acc, f.R = p.fold.R, f.C = p.fold.C, f.M = p.fold.M, f.bwd = 1;
+  f.o0 = p.fold.db, f.o1 = p.fold.dw;
+  bn_fold_block(f, reinterpret_cast<double*>(lds));
   return true;
 }
 
@@ -261,7 +272,7 @@ struct XCursor {
 
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
-  if (run_side(p)) return;
+  if (run_side(p, smem)) return;
   const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
   const int KC = 16 * p.Cin, KT = KC / BKC, T = (p.Cout / BCO) * KT;
 
@@ -419,7 +430,7 @@ __device__ __forceinline__ int c4x_off(int r, int byte) { return dy_off(r, byte)
 
 __global__ __launch_bounds__(kThreads) void conv_wgrad_c4_kernel(ConvWgradParams p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * C4_STAGE + kLutBytes];
-  if (run_side(p)) return;
+  if (run_side(p, smem)) return;
   const bool u8in = p.lut != nullptr;   // raw u8 RGBA input, decoded through the table (see stage_lut)
   char* const lutl = smem + 2 * C4_STAGE;
   if (u8in) {
@@ -1188,11 +1199,18 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
     q.zero_count = p.Cout * 16 * (p.cin_out > 0 ? p.cin_out : p.Cin);
   }
   int64_t grid = blocks;
+  q.main_blocks = int(blocks);
   if (side) {
     if (!side->partial || !side->out || side->S <= 0 || side->rx <= 0 || side->ry <= 0) return hipErrorInvalidValue;
-    q.main_blocks = int(blocks);
     q.side = *side;
     grid += int64_t(side->rx) * side->ry;
+  } else {
+    q.side = ConvWgradParams::Reduce();
+  }
+  if (p.fold.acc) {   // + one block: the BN fold (its LDS: 2 C doubles of the kernel's staging array)
+    if (c4 || p.fold.R <= 0 || p.fold.C <= 0 || 2 * p.fold.C * 8 > 2 * STAGE || !p.fold.dw || !p.fold.db)
+      return hipErrorInvalidValue;
+    grid += 1;
   }
   if (c4) conv_wgrad_c4_kernel<<<unsigned(grid), kThreads, 0, stream>>>(q);
   else conv_wgrad_kernel<<<unsigned(grid), kThreads, 0, stream>>>(q);

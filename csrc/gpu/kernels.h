@@ -326,6 +326,17 @@ struct ConvWgradParams {
     int64_t s_co = 0, s_ci = 0, s_kh = 0, s_kw = 0;
     int rx = 0, ry = 0;   // its grid: element blocks x slice groups
   } side;
+  // fold.acc != nullptr (not the 4-channel first layer): one more block folds
+  // the BatchNorm backward accumulator the preceding data gradient's epilogue
+  // filled (bn_fold.h) into db = sum gz, dw = sum gz * xhat, and clears it --
+  // the BN backward then needs no finalize launch
+  struct Fold {
+    double* acc = nullptr;
+    int R = 0, C = 0;
+    int64_t M = 0;
+    float* dw = nullptr;
+    float* db = nullptr;
+  } fold;
 };
 // Cin % 32 == 0 with Cout % 64 == 0, or Cin == 4 (the first layer) with Cout % 32 == 0.
 bool conv_wgrad_supported(int Cin, int Cout);

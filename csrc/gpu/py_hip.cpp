@@ -239,9 +239,17 @@ PYBIND11_MODULE(_hip, m) {
   m.def("conv_wgrad",
         [](uintptr_t x, uintptr_t dy, uintptr_t partial, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
            int slices, int64_t px_per_slice, uintptr_t out, int64_t s_co, int64_t s_ci, int64_t s_kh, int64_t s_kw,
-           uintptr_t stream, int cin_out, bool defer, py::object side, uintptr_t lut) -> py::object {
+           uintptr_t stream, int cin_out, bool defer, py::object side, uintptr_t lut, py::object fold) -> py::object {
           ConvWgradParams p;
           p.cin_out = cin_out;
+          if (!fold.is_none()) {   // (acc, R, C, M, dw, db)
+            const py::tuple f = fold.cast<py::tuple>();
+            if (f.size() != 6) throw std::invalid_argument("conv_wgrad: fold is (acc, R, C, M, dw, db)");
+            p.fold.acc = reinterpret_cast<double*>(f[0].cast<uintptr_t>());
+            p.fold.R = f[1].cast<int>(), p.fold.C = f[2].cast<int>(), p.fold.M = f[3].cast<int64_t>();
+            p.fold.dw = reinterpret_cast<float*>(f[4].cast<uintptr_t>());
+            p.fold.db = reinterpret_cast<float*>(f[5].cast<uintptr_t>());
+          }
           p.lut = ptr<const uint16_t>(lut);
           p.x = ptr<const uint16_t>(x);
           p.dy = ptr<const uint16_t>(dy);
@@ -262,7 +270,7 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("x"), py::arg("dy"), py::arg("partial"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("Cin"),
         py::arg("Ho"), py::arg("Wo"), py::arg("Cout"), py::arg("slices"), py::arg("px_per_slice"), py::arg("out"),
         py::arg("s_co"), py::arg("s_ci"), py::arg("s_kh"), py::arg("s_kw"), py::arg("stream"), py::arg("cin_out") = 0,
-        py::arg("defer") = false, py::arg("side") = py::none(), py::arg("lut") = 0);
+        py::arg("defer") = false, py::arg("side") = py::none(), py::arg("lut") = 0, py::arg("fold") = py::none());
   // a deferred slice reduce on its own (a weight-gradient chain that ended early)
   m.def("conv_wgrad_reduce", [](py::tuple r, uintptr_t stream) {
     check(conv_wgrad_reduce(reduce_from_tuple(r), stream_of(stream)), "conv_wgrad_reduce");
@@ -580,6 +588,16 @@ PYBIND11_MODULE(_hip, m) {
                 "bn_bwd_apply");
         });
 
+  // the BN backward's apply pass alone (dw, db folded elsewhere: conv_wgrad fold=)
+  m.def("bn_bwd_apply",
+        [](uintptr_t x, uintptr_t gy, uintptr_t gx, int64_t M, int C, int dtype, uintptr_t mean, uintptr_t invstd,
+           uintptr_t w, uintptr_t b, uintptr_t dw, uintptr_t db, float slope, uintptr_t stream) {
+          check(bn_bwd_apply(ptr<const void>(x), ptr<const void>(gy), ptr<void>(gx), M, C, dtype,
+                             ptr<const float>(mean), ptr<const float>(invstd), ptr<const float>(w),
+                             ptr<const float>(b), ptr<const float>(dw), ptr<const float>(db), slope,
+                             stream_of(stream)),
+                "bn_bwd_apply");
+        });
   // accumulator hand-off (kernels.h BnAcc): no finalize launches
   m.def("bn_acc_replicas", &bn_acc_replicas);
   m.def("bn_acc_elems", &bn_acc_elems);

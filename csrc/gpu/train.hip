@@ -8,6 +8,7 @@
 
 #include <cstdlib>
 
+#include "bn_fold.h"
 #include "kernels.h"
 
 namespace btn {
@@ -322,54 +323,20 @@ __global__ __launch_bounds__(64 * kFoldWaves) void bn_bwd_finalize_kernel(const 
 // load latency per 16 bytes (9.9 / 12.4 us per call where the bytes take 1-4).
 constexpr int kBnUnroll = 4;
 
-// BnAcc finalize (kernels.h): ONE block folds the fp64 accumulator [R][2C]
-// (<= 2048 doubles, copied to LDS with all loads in flight at once) in fp64 --
-// G = 256 / 2C lane groups each summing every G-th replica, then one lane per
-// (sum, channel) adding the G group sums -- finalizes, and clears the
-// accumulator for the next producer.  The per-tile-row finalize this replaces
-// walked ~4800 rows per channel (6-8 us a call); this is one memory latency.
+// BnAcc finalize (kernels.h): ONE block folds, finalizes and clears the fp64
+// accumulator (bn_fold.h).  The per-tile-row finalize this replaces walked
+// ~4800 rows per channel (6-8 us a call); this is one memory latency.
 constexpr int kBnAccMaxC = 512;
 
 template <bool BWD>
 __global__ __launch_bounds__(kBlock) void bn_acc_finalize_kernel(double* __restrict__ acc, int R, int64_t M, int C,
                                                                  float eps, float momentum, float* o0, float* o1,
                                                                  float* rm, float* rv, int64_t* tracked) {
-  __shared__ double raw[2048];
   __shared__ double part[2 * kBnAccMaxC];
-  const int t = int(threadIdx.x);
-  const int J = 2 * C, n = J * R;   // n: a multiple of 4 (host-checked), <= 2048
-  typedef double d2 __attribute__((ext_vector_type(2)));
-  for (int e = 2 * t; e < n; e += 2 * kBlock) *reinterpret_cast<d2*>(raw + e) = *reinterpret_cast<const d2*>(acc + e);
-  __syncthreads();
-  // read: clear for the next producer (its atomics run at the memory side)
-  for (int e = 2 * t; e < n; e += 2 * kBlock) *reinterpret_cast<d2*>(acc + e) = d2{0.0, 0.0};
-  const int G = J >= kBlock ? 1 : kBlock / J;
-  for (int u = t; u < G * J; u += kBlock) {
-    const int j = u % J, g = u / J;
-    double s = 0.0;
-    for (int r = g; r < R; r += G) s += raw[r * J + j];
-    part[g * J + j] = s;
-  }
-  __syncthreads();
-  for (int c = t; c < C; c += kBlock) {
-    double s0 = 0.0, s1 = 0.0;
-    for (int g = 0; g < G; ++g) s0 += part[g * J + c], s1 += part[g * J + C + c];
-    if constexpr (BWD) {   // o0 = db (sum gz), o1 = dw (sum gz * xhat)
-      o0[c] = float(s0);
-      o1[c] = float(s1);
-    } else {               // o0 = mean, o1 = invstd
-      const double mu = s0 / double(M);
-      double var = s1 / double(M) - mu * mu;
-      var = var < 0.0 ? 0.0 : var;
-      o0[c] = float(mu);
-      o1[c] = float(1.0 / sqrt(var + double(eps)));
-      if (rm) {
-        rm[c] = float((1.0 - momentum) * rm[c] + momentum * mu);
-        rv[c] = float((1.0 - momentum) * rv[c] + momentum * var * double(M) / double(M > 1 ? M - 1 : 1));
-      }
-      if (tracked && c == 0) tracked[0] += 1;
-    }
-  }
+  BnFold f;
+  f.acc = acc, f.R = R, f.C = C, f.M = M, f.bwd = BWD ? 1 : 0, f.eps = eps, f.momentum = momentum;
+  f.o0 = o0, f.o1 = o1, f.rm = rm, f.rv = rv, f.tracked = tracked;
+  bn_fold_block(f, part);
 }
 
 template <int DT, bool BWD>

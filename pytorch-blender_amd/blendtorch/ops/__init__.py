@@ -810,12 +810,34 @@ class BnLink:
     has the MFMA kernel's epilogue sum gz and gz * xhat per tile into
     ``part``; the BN backward then only finalizes and applies (one pass over
     the activation fewer).  ``part`` is consumed once."""
-    __slots__ = ('x', 'mean', 'invstd', 'w', 'b', 'slope', 'part', 'rows', 'gy', 'acc')
+    __slots__ = ('x', 'mean', 'invstd', 'w', 'b', 'slope', 'part', 'rows', 'gy', 'acc', 'params', 'dw', 'db',
+                 'dw_sunk', 'db_sunk', 'folded')
 
     def __init__(self):
         self.x = self.mean = self.invstd = self.w = self.b = self.part = self.gy = None
         self.slope, self.rows = 0.0, 0
         self.acc = None      # BnAccumulator of the BN call (accumulator mode: part = acc.bwd, rows = -R)
+        self.params = None   # the BN's (weight, bias) parameters
+        # accumulator mode: the BN's weight / bias gradients when the consuming
+        # conv's weight-gradient launch already folded the accumulator into them
+        self.dw = self.db = None
+        self.dw_sunk = self.db_sunk = self.folded = False
+
+    def fold_args(self, M):
+        """``(acc, R, C, M, dw, db)`` for ``conv_wgrad(fold=)``: fold this BN's
+        backward accumulator into its weight / bias gradients -- their
+        bucket views when fresh (``parallel.GradBuckets``), else new tensors
+        the BN backward returns.  Marks the link folded."""
+        import torch
+        self.dw, self.dw_sunk = _grad_dest(self.params[0], self.w)
+        self.db, self.db_sunk = _grad_dest(self.params[1], self.b)
+        if self.dw.dtype != torch.float32 or not self.dw.is_contiguous():
+            self.dw, self.dw_sunk = torch.empty_like(self.w), False
+        if self.db.dtype != torch.float32 or not self.db.is_contiguous():
+            self.db, self.db_sunk = torch.empty_like(self.b), False
+        self.folded = True
+        return (self.acc.bwd.data_ptr(), self.acc.R, int(self.w.numel()), int(M), self.dw.data_ptr(),
+                self.db.data_ptr())
 
     def ready(self, dx):
         """True when the recorded BN input matches ``dx`` (shape, bf16 NHWC)."""
@@ -886,6 +908,9 @@ def _bn_function():
                 link.x, link.mean, link.invstd, link.w, link.b, link.slope = xs, mean, invstd, w, b, float(slope)
                 link.part = link.gy = None
                 link.acc = ctx.acc
+                link.params = (weight, bias)
+                link.dw = link.db = None
+                link.folded = False
             return y.permute(0, 3, 1, 2)
 
         @staticmethod
@@ -903,7 +928,24 @@ def _bn_function():
                 dw, w_sunk = torch.empty_like(w), False
             if db.dtype != torch.float32 or not db.is_contiguous():
                 db, b_sunk = torch.empty_like(b), False
-            part, rows = ctx.link.take(gys) if ctx.link is not None else (None, 0)
+            lk = ctx.link
+            folded = lk is not None and lk.folded
+            part, rows = lk.take(gys) if lk is not None else (None, 0)
+            if folded and part is not None and rows < 0:
+                # the consuming conv's weight-gradient launch folded dw, db: apply only
+                _count('bn_backward_from_stats')
+                _count('bn_backward_acc')
+                _count('bn_backward_folded')
+                ext.bn_bwd_apply(xs.data_ptr(), gys.data_ptr(), gx.data_ptr(), M, C, dt, mean.data_ptr(),
+                                 invstd.data_ptr(), w.data_ptr(), b.data_ptr(), lk.dw.data_ptr(), lk.db.data_ptr(),
+                                 ctx.slope, _stream(xs.device))
+                out_w = None if lk.dw_sunk else lk.dw
+                out_b = None if lk.db_sunk else lk.db
+                lk.dw = lk.db = None
+                lk.folded = False
+                return (gx.permute(0, 3, 1, 2), out_w, out_b, None, None, None, None, None, None, None, None)
+            if folded:
+                raise RuntimeError('BatchNormLeakyReLU2d: its statistics were folded for another gradient')
             if ctx.acc is not None and (part is None or rows < 0):
                 # accumulator mode: the consuming conv's dgrad epilogue summed into
                 # acc.bwd (part), or this launch reduces into it first
@@ -1096,7 +1138,7 @@ class WgradChain:
             self.pending = self.keep = None
 
 
-def conv_wgrad(x, dy, out, target_blocks=None, chain=None, last=True, lut=None):
+def conv_wgrad(x, dy, out, target_blocks=None, chain=None, last=True, lut=None, fold=None):
     """fp32 weight gradient of a 4x4/s2/p1 convolution into ``out`` ([Cout, Cin,
     4, 4], any strides): MFMA tiles over pixel slices + one slice-reduce
     launch.  ``x`` [N, Cin, H, W] and ``dy`` [N, Cout, H/2, W/2] are bf16 with
@@ -1132,7 +1174,9 @@ def conv_wgrad(x, dy, out, target_blocks=None, chain=None, last=True, lut=None):
         raise ValueError('conv_wgrad: u8 input (4 channels) needs its decode table lut, and only u8 takes one')
     res = ext.conv_wgrad(x.data_ptr(), dy.data_ptr(), partial.data_ptr(), N, H, W, Cin, Ho, Wo, Cout, slices, px,
                          out.data_ptr(), out.stride(0), out.stride(1), out.stride(2), out.stride(3), _stream(x.device),
-                         cin_out, defer, side, lut.data_ptr() if lut is not None else 0)
+                         cin_out, defer, side, lut.data_ptr() if lut is not None else 0, fold)
+    if fold is not None:
+        _count('conv_wgrad_bn_fold')
     if chain is not None:
         if side is not None:
             _count('conv_wgrad_side_reduce')
@@ -1330,6 +1374,13 @@ def _conv_function():
                         wfull = wfull.contiguous(memory_format=torch.channels_last)
                     gx = torch.ops.aten.convolution_backward(gy, x, wfull, None, [2, 2], [1, 1], [1, 1], False,
                                                              [0, 0], 1, [True, False, False])[0]
+            fold = None
+            bl = ctx.bn_link
+            if gx is not None and bl is not None and bl.acc is not None and bl.part is not None and bl.rows < 0 \
+                    and bl.params is not None and ctx.needs_input_grad[1] and x.shape[1] != 4:
+                # the data gradient just filled the BN's backward accumulator: the
+                # weight-gradient launch folds it in one extra block
+                fold = bl.fold_args(x.shape[0] * x.shape[2] * x.shape[3])
             if ctx.needs_input_grad[1]:
                 out, sunk = _grad_dest(ctx.w32)
                 # a chained (deferred) reduce only into a bucket view: a returned
@@ -1337,7 +1388,7 @@ def _conv_function():
                 chain = ctx.wchain if (sunk or ctx.wlast) else None
                 if ctx.wchain is not None and chain is None:
                     ctx.wchain.flush(x.device)
-                gw = conv_wgrad(x, gy, out, chain=chain, last=ctx.wlast or chain is None, lut=ctx.lut)
+                gw = conv_wgrad(x, gy, out, chain=chain, last=ctx.wlast or chain is None, lut=ctx.lut, fold=fold)
                 if sunk:
                     gw = None      # written into the parameter's bucket view
             elif ctx.wchain is not None:

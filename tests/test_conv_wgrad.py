@@ -272,12 +272,15 @@ def test_bn_accumulators_fold_and_clear(dev, monkeypatch):
     for step in range(3):
         a.zero_grad(set_to_none=True)
         b.zero_grad(set_to_none=True)
-        before = ops.KERNEL_CALLS.get('bn_forward_acc', 0), ops.KERNEL_CALLS.get('bn_backward_acc', 0)
+        before = (ops.KERNEL_CALLS.get('bn_forward_acc', 0), ops.KERNEL_CALLS.get('bn_backward_acc', 0),
+                  ops.KERNEL_CALLS.get('bn_backward_folded', 0))
         la = a.bce_loss_bf16(x, 1.0)
         la.backward()
         # 4 BN layers forward; backward: BN1..3 from the dgrad epilogues, BN4 from the head's
         assert ops.KERNEL_CALLS['bn_forward_acc'] == before[0] + 4
         assert ops.KERNEL_CALLS['bn_backward_acc'] == before[1] + 4
+        # BN1..3's sums are folded by the next conv's weight-gradient launch
+        assert ops.KERNEL_CALLS.get('bn_backward_folded', 0) == before[2] + 3
         monkeypatch.setattr(ops, 'bn_acc_supported', lambda C: False)
         lb = b.bce_loss_bf16(x, 1.0)
         lb.backward()
