@@ -175,6 +175,10 @@ def parse_args(argv=None):
                     help='disc consumer with --h2d copy: on = the loader only DMAs raw frames into the batch '
                          'tensor and the decode kernel runs inside the captured training step (one queue, no '
                          'loader kernels competing with the step); off = the loader decodes')
+    ap.add_argument('--static-inputs', choices=['on', 'off'], default='on',
+                    help='disc consumer: on = the loader cycles a fixed ring of output tensors and the captured '
+                         'step has a graph per tensor that reads the batch in place; off = each batch is copied '
+                         'into the graph\'s static input buffer')
     ap.add_argument('--fuse-decode', choices=['on', 'off'], default='on',
                     help='disc consumer with the in-step decode (bf16, fused cast and head): on = the first '
                          'convolution reads the raw u8 RGBA frames through the decode table inside its MFMA '
@@ -316,6 +320,10 @@ def main(argv=None):
     if amp:
         # the decode kernel writes what the model's first conv reads: bf16, channels-last
         decode = DecodeConfig.unit(channels='rgba' if rgba_in else 'rgb', gamma=2.2, dtype='bfloat16', layout='nhwc')
+    # graphs per loader output tensor (disc consumer, one graph per step): the
+    # step reads each batch where the loader put it
+    static_in = (args.prefetch + 2) if (args.consumer == 'disc' and args.static_inputs == 'on'
+                                        and args.dma_phase != 'mid' and args.dist != 'scatter') else 0
     # the in-step decode folded into the first convolution's MFMA kernels (raw u8 frames in)
     fuse_decode = (step_decode and args.fuse_decode == 'on' and amp and args.cast == 'fused'
                    and args.head == 'fused' and decode.channels == 'rgba' and decode.dtype == 'bfloat16')
@@ -384,7 +392,10 @@ def main(argv=None):
                                   launch_depth=args.launch_depth,
                                   copy_streams=copy_streams,
                                   defer_post=dma_mid,
-                                  host_sync=None if args.host_sync == 'auto' else args.host_sync == 'on')
+                                  host_sync=None if args.host_sync == 'auto' else args.host_sync == 'on',
+                                  # a fixed ring of output tensors: the captured step keeps a
+                                  # graph per tensor and reads the batch in place (no copy)
+                                  reuse_buffers=static_in > 0)
         if args.dist == 'scatter':
             it = iter(ScatterLoader(dl, args.batch, decode, device, total_batches))
         else:
@@ -429,7 +440,8 @@ def main(argv=None):
         if model is not None:
             from blendtorch.parallel.step import CapturedStep
             stepper = CapturedStep(model, opt, loss_fn, graph=use_graph, comm=comm,
-                                   allreduce='always' if args.force_pg else dist.is_initialized(), split=dma_mid)
+                                   allreduce='always' if args.force_pg else dist.is_initialized(), split=dma_mid,
+                                   static_inputs=static_in)
 
         def graphed(x):
             stepper(x, mid=dl.release if (dma_mid and dl is not None) else None)
@@ -574,6 +586,7 @@ def main(argv=None):
                 'consumer_step': stepper.state if stepper is not None else None,
                 'decode_in_step': step_decode,
                 'decode_fused_in_conv': fuse_decode,
+                'static_input_graphs': static_in,
                 'cast': args.cast if amp else None,
                 'optim': args.optim if model is not None else None,
                 'dma_phase': args.dma_phase if model is not None else None,

@@ -112,7 +112,7 @@ class DeviceLoader:
                  rcvhwm: int = 10, prefetch: int = 4, io_threads: Optional[int] = None, image_key: str = 'image',
                  skip_bad: bool = False, meta_to_device: bool = False, staging_depth: int = 3, h2d: str = 'auto',
                  launch_depth: int = 2, log_every: Optional[float] = None, copy_streams: int = 2,
-                 defer_post: bool = False, host_sync: Optional[bool] = None):
+                 defer_post: bool = False, host_sync: Optional[bool] = None, reuse_buffers: bool = False):
         if h2d not in ('auto', 'copy'):
             raise ValueError("h2d must be 'auto' or 'copy'")
         self.h2d = h2d
@@ -155,6 +155,14 @@ class DeviceLoader:
         self.host_sync = (h2d == 'copy') if host_sync is None else bool(host_sync)
         self._owed = 0             # deferred posts not yet made
         self._post_fn = None
+        # reuse_buffers: output tensors come from a fixed ring of prefetch + 2
+        # (a batch's tensor is refilled prefetch + 2 batches later, behind the
+        # consumer's stream work on it), so a consumer that captures one graph
+        # per input tensor (parallel.step.CapturedStep static_inputs) reads
+        # them in place -- it must not keep batches longer than that
+        self.reuse_buffers = bool(reuse_buffers)
+        self._ring = []
+        self._ring_i = 0
 
     @classmethod
     def from_config(cls, addresses: Sequence[str], config, decode: DecodeConfig = DecodeConfig(), device=None,
@@ -186,8 +194,17 @@ class DeviceLoader:
             self.h2d == 'auto', self.launch_depth, self.copy_streams, self.host_sync)
 
     def _post(self, loader, stream):
-        out = torch.empty(self.decode.out_shape(self.batch_size, *self.shape[:2]), dtype=self.decode.torch_dtype(),
-                          device=self.device)
+        shape = self.decode.out_shape(self.batch_size, *self.shape[:2])
+        if self.reuse_buffers:
+            if len(self._ring) < self.prefetch + 2:
+                self._ring.append(torch.empty(shape, dtype=self.decode.torch_dtype(), device=self.device))
+                out = self._ring[-1]
+            else:
+                out = self._ring[self._ring_i % len(self._ring)]
+                self._ring_i += 1
+            loader.post(out.data_ptr(), stream.cuda_stream)
+            return out
+        out = torch.empty(shape, dtype=self.decode.torch_dtype(), device=self.device)
         loader.post(out.data_ptr(), stream.cuda_stream)
         return out
 

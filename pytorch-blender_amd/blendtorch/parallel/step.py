@@ -95,6 +95,13 @@ class CapturedStep:
     buckets: False keeps the legacy per-step pack/all-reduce/copy-back path
         (:func:`allreduce_gradients`; comparison only).
 
+    static_inputs: up to this many input tensors get a graph of their own
+        that reads the tensor in place (captured the first time its storage
+        shows up, sharing the first graph's memory pool) -- no per-step copy
+        into a static buffer.  For a loader that cycles a fixed set of output
+        tensors (``btt.DeviceLoader(reuse_buffers=True)``); further inputs
+        are copied into a private buffer with a graph of its own.  Not with
+        ``split``.
     split: capture forward+loss and backward+update as two graphs sharing one
         memory pool, so a caller can act between them: ``step(x, mid=fn)``
         runs ``fn()`` after enqueuing the forward (e.g. to gate the next
@@ -108,9 +115,11 @@ class CapturedStep:
     def __init__(self, model: torch.nn.Module, optimizer: torch.optim.Optimizer,
                  loss_fn: Callable[[torch.nn.Module, torch.Tensor], torch.Tensor], allreduce=True,
                  warmup: int = 3, graph: bool = True, group=None, bucket_mb: float = 256.0, split: bool = False,
-                 comm=None, buckets: bool = True):
+                 comm=None, buckets: bool = True, static_inputs: int = 0):
         self.model, self.opt, self.loss_fn = model, optimizer, loss_fn
         self.split = split
+        self.static_inputs = 0 if split else max(0, int(static_inputs))
+        self._by_input = {}   # input data_ptr -> (graph, input tensor, loss)
         self.graph_bwd: Optional[torch.cuda.CUDAGraph] = None
         self.allreduce, self.warmup, self.group, self.bucket_mb = allreduce, warmup, group, bucket_mb
         self.state = 'pending' if graph else 'eager'
@@ -171,8 +180,11 @@ class CapturedStep:
         return self._backward(self._forward(x))
 
     def _capture(self, x):
-        self.x = torch.empty_like(x)         # same strides (channels-last stays channels-last)
-        self.x.copy_(x)
+        if self.static_inputs:
+            self.x = x                       # read in place (the caller keeps it alive and unchanged)
+        else:
+            self.x = torch.empty_like(x)     # same strides (channels-last stays channels-last)
+            self.x.copy_(x)
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -197,9 +209,30 @@ class CapturedStep:
                 with torch.cuda.graph(g, capture_error_mode='thread_local'):
                     self.loss = self._train(self.x)
             self.graph, self.state = g, 'graph'
+            if self.static_inputs:
+                self._by_input[self.x.data_ptr()] = (g, self.x, self.loss)
         except RuntimeError as e:          # keep the run alive; callers report which mode ran
             self.error = str(e)
             self.state = 'eager'
+
+    def _same_layout(self, x):
+        return (x.shape == self.x.shape and x.stride() == self.x.stride() and x.dtype == self.x.dtype
+                and x.device == self.x.device)
+
+    def _capture_for(self, x, key=None):
+        """One more graph of the step, reading ``x`` in place, in the first
+        graph's memory pool (the graphs replay one at a time on one stream)."""
+        g = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(g, pool=self.graph.pool(), capture_error_mode='thread_local'):
+                loss = self._train(x)
+        except RuntimeError as e:
+            self.error = str(e)
+            self.static_inputs = len(self._by_input)     # no more captures; copy into the first graph's input
+            return None
+        ent = (g, x, loss)
+        self._by_input[x.data_ptr() if key is None else key] = ent
+        return ent
 
     def _replay(self, mid):
         self.graph.replay()
@@ -217,6 +250,24 @@ class CapturedStep:
                 self._replay(mid)
                 return self.loss
         if self.state == 'graph':
+            if self.static_inputs:
+                ent = self._by_input.get(x.data_ptr())
+                if ent is None and len(self._by_input) - ('copy' in self._by_input) < self.static_inputs \
+                        and self._same_layout(x):
+                    ent = self._capture_for(x)
+                if ent is None and self._same_layout(x):
+                    # past the cap: copy into a private buffer with a graph of its own
+                    # (the first graph's input is a caller's tensor, never written)
+                    ent = self._by_input.get('copy')
+                    if ent is None:
+                        ent = self._capture_for(torch.empty_like(x), key='copy')
+                    if ent is not None:
+                        ent[1].copy_(x)
+                if ent is not None:
+                    ent[0].replay()
+                    if mid is not None:
+                        mid()
+                    return ent[2]
             if x.data_ptr() != self.x.data_ptr():
                 self.x.copy_(x)
             self._replay(mid)

@@ -258,3 +258,36 @@ def test_densityopt_step_captures_and_replays(dev):
     assert float(step.gate_d) in (0.0, 1.0) and float(step.gate_s) in (0.0, 1.0)
     assert bool(torch.isfinite(step.samples).all()) and bool((step.samples > 0).all())
     assert bool(torch.isfinite(step.params_out).all())
+
+
+def test_captured_step_static_inputs_read_in_place(dev):
+    """CapturedStep(static_inputs=N): one graph per input tensor, reading it
+    in place (no copy into a static buffer) -- trains like the copy path over
+    alternating inputs, and an input past N falls back to the copy."""
+    from blendtorch.models import Discriminator
+    from blendtorch.parallel.step import CapturedStep
+    cl = torch.channels_last
+    g = torch.Generator(device=dev).manual_seed(5)
+    bufs = [torch.rand(4, 4, 96, 128, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+            for _ in range(3)]
+    nets, losses = [], []
+    for static in (0, 2):
+        torch.manual_seed(0)
+        m = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
+        opt = ops.FusedAdam(m.parameters(), lr=2e-4)
+        step = CapturedStep(m, opt, lambda mm, x: mm.bce_loss_bf16(x, 1.0), allreduce=False, graph=True,
+                            static_inputs=static)
+        ls = []
+        for k in range(7):
+            ls.append(float(step(bufs[k % 3])))
+        torch.cuda.synchronize()
+        assert step.state == 'graph'
+        if static:                                     # the third tensor took the copy path
+            assert len(step._by_input) == 3 and 'copy' in step._by_input
+        nets.append(m)
+        losses.append(ls)
+    torch.testing.assert_close(torch.tensor(losses[0]), torch.tensor(losses[1]), rtol=2e-3, atol=1e-4)
+    lr = 2e-4
+    for pa, pb in zip(nets[0].parameters(), nets[1].parameters()):
+        d = (pb - pa).detach().abs()
+        assert float(d.mean()) < 0.15 * lr
