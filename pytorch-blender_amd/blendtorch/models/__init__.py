@@ -186,10 +186,15 @@ class Discriminator(nn.Module):
                             and nxt.fused_with_stats(x.new_empty((1, m.out_channels, 1, 1), dtype=torch.bfloat16)))
                     # the BN that produced x: this conv's data gradient does its backward reduction
                     bl, link = link, None
-                    wk = dict(wt=wts.get(ci), bn_link=bl, wchain=wchain, wlast=first_mfma)
+                    # the chain closes at the first MFMA layer whose weight takes a gradient:
+                    # its backward node exists whatever the input, so the deferred reduces
+                    # handed down to it always run (frozen layers flush, see ops.conv4x4s2)
+                    closes = first_mfma and m.weight.requires_grad
+                    wk = dict(wt=wts.get(ci), bn_link=bl, wchain=wchain, wlast=closes)
                     if ci == 0 and lut is not None:
                         wk['lut'] = lut    # raw u8 frames: decoded in this layer's kernels
-                    first_mfma = False
+                    if closes:
+                        first_mfma = False
                     if fuse and ops.bn_acc_supported(m.out_channels):
                         # BN statistics come out of the conv kernel's epilogue, added into
                         # the BN call's zeroed accumulator (its apply kernel folds them)

@@ -355,3 +355,28 @@ def test_first_layer_reads_raw_u8_frames_through_decode_table(dev):
     lb.backward()
     for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
         torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-3, atol=1e-5 + 1e-3 * float(pb.grad.abs().max()), msg=n)
+
+
+@pytest.mark.gpu
+def test_wgrad_chain_with_frozen_first_layer(dev):
+    """A frozen first layer (no weight gradient, no input gradient: no
+    backward node) must not strand the reduces handed down the chain: the
+    chain closes at the first layer that does take a weight gradient."""
+    from blendtorch.models import Discriminator
+    from blendtorch.parallel.grads import GradBuckets
+    torch.manual_seed(12)
+    cl = torch.channels_last
+    a = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
+    b = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
+    b.load_state_dict(a.state_dict())
+    for m in (a, b):
+        m.features[0].weight.requires_grad_(False)
+    x = torch.rand(4, 4, 96, 128, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    gb = GradBuckets([p for p in a.parameters() if p.requires_grad])
+    gb.zero_()
+    a.bce_loss_bf16(x, 1.0).backward()
+    b.bce_loss_bf16(x, 1.0).backward()
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        if pa.requires_grad:
+            torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-4, atol=1e-6 + 1e-4 * float(pb.grad.abs().max()),
+                                       msg=n)
