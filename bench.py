@@ -187,6 +187,12 @@ def parse_args(argv=None):
                     help='diagnostic: resident = the consumer trains on one fixed batch while the stream keeps running')
     ap.add_argument('--force-pg', action='store_true',
                     help='initialise a process group even for one rank (rehearses the collective code paths)')
+    ap.add_argument('--pg-backend', choices=['auto', 'nccl', 'gloo'], default='auto',
+                    help='process-group backend: auto = nccl only where a device collective runs (disc '
+                         'consumer, scatter), else a gloo control plane (barriers, timing); nccl = always RCCL')
+    ap.add_argument('--rccl-selfcheck', choices=['on', 'off'], default='on',
+                    help='with a gloo control plane and --backend nccl: run the RCCL P2P-ring + all-reduce '
+                         'self-check on a temporary nccl group at start-up, then destroy it')
     ap.add_argument('--dist', choices=['shard', 'pool', 'scatter'], default='shard',
                     help='shard: every rank owns its producers; pool: every rank launches producers and connects '
                          'to all of them (PUSH round-robin across GPUs); scatter: rank 0 receives world*B per step '
@@ -243,6 +249,10 @@ def main(argv=None):
     local_world = int(os.environ.get('LOCAL_WORLD_SIZE', str(world)))
 
     ensure_built()
+    # before the HIP runtime starts: 8 hardware queues, so the loader's copy /
+    # decode streams never share one with RCCL's (blendtorch.utils.ensure_hw_queues)
+    from blendtorch.utils import ensure_hw_queues
+    hw_queues = ensure_hw_queues()
     import torch
     import torch.distributed as dist
     from blendtorch import btt
@@ -261,16 +271,35 @@ def main(argv=None):
         os.environ.setdefault('MASTER_PORT', str(free_port()))
         os.environ.setdefault('RANK', '0')
         os.environ['WORLD_SIZE'] = '1'
+    # Which backend the process group needs.  Streaming in shard / pool mode
+    # runs no device collective: the ranks only meet at the barriers around
+    # the timed region and for the timing all-reduce, which a gloo control
+    # plane carries.  A live RCCL communicator costs streaming 4-8 % on one
+    # GPU even when it is never used (profiles/r3/pg_ab.md; why:
+    # profiles/r4/pg_tax.md), so nccl is only built where a device
+    # collective runs (the training step's gradient all-reduce, scatter).
+    # With --backend nccl a shard/pool run still proves RCCL over xGMI at
+    # start-up: a temporary nccl group runs the P2P-ring + all-reduce
+    # self-check and is destroyed before streaming starts.
+    device_coll = args.consumer == 'disc' or args.dist == 'scatter'
+    if args.pg_backend == 'auto':
+        pg_backend = args.backend if device_coll else 'gloo'
+    else:
+        pg_backend = args.pg_backend
+    if pg_backend == 'nccl' and args.backend != 'nccl':
+        pg_backend = 'gloo'
+    pg_dev = device if pg_backend == 'nccl' else torch.device('cpu')
     if world > 1 or args.force_pg:
-        if args.backend == 'nccl':
+        if pg_backend == 'nccl':
             dist.init_process_group('nccl', device_id=device)
         else:
             dist.init_process_group('gloo')
         world_seen = dist.get_world_size()
         # collective sanity check: sum over ranks of (rank + 1) == w (w + 1) / 2
-        chk = torch.tensor([float(rank + 1)], device=device if args.backend == 'nccl' else 'cpu')
+        chk = torch.tensor([float(rank + 1)], device=pg_dev)
         dist.all_reduce(chk)
-        allreduce = {'value': float(chk.item()), 'expected': world_seen * (world_seen + 1) / 2}
+        allreduce = {'value': float(chk.item()), 'expected': world_seen * (world_seen + 1) / 2,
+                     'pg_backend': pg_backend}
         if allreduce['value'] != allreduce['expected']:
             raise RuntimeError(f'all_reduce sanity check failed: {allreduce}')
         # the communicator the training step and scatter mode use (RCCL called on
@@ -279,14 +308,23 @@ def main(argv=None):
         # and its peers (blendtorch/parallel/comm.py)
         if os.environ.get('BT_NO_DEVICECOMM') != '1':      # (diagnostic switch)
             from blendtorch.parallel import DeviceComm
-            # a communicator of its own for the training step's in-graph all-reduce
-            # (16 % step tax on the group's shared one); streaming alone has no
-            # per-step collective and a second communicator costs it 25 %
-            # (profiles/r3/pg_ab.md)
-            ded = os.environ.get('BT_DEVICECOMM_DEDICATED', '1' if args.consumer == 'disc' else '0') == '1'
-            comm = DeviceComm(device=device if args.backend == 'nccl' else None, dedicated=ded)
-            allreduce['selfcheck'] = {k: (round(v, 3) if isinstance(v, float) else v)
-                                      for k, v in comm.selfcheck().items()}
+            if pg_backend == 'nccl':
+                # a communicator of its own for the training step's in-graph all-reduce
+                # (16 % step tax on the group's shared one; profiles/r3/pg_ab.md)
+                ded = os.environ.get('BT_DEVICECOMM_DEDICATED', '1' if args.consumer == 'disc' else '0') == '1'
+                comm = DeviceComm(device=device, dedicated=ded)
+                allreduce['selfcheck'] = {k: (round(v, 3) if isinstance(v, float) else v)
+                                          for k, v in comm.selfcheck().items()}
+            elif args.backend == 'nccl' and args.rccl_selfcheck == 'on':
+                # streaming needs no device collective: prove RCCL anyway, then tear it down
+                sub = dist.new_group(backend='nccl')
+                tmp = DeviceComm(group=sub, device=device)
+                res = tmp.selfcheck()
+                tmp.close()
+                torch.cuda.synchronize()
+                dist.destroy_process_group(sub)
+                res['torn_down'] = True
+                allreduce['selfcheck'] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in res.items()}
 
     # place each rank's producers on CPUs local to its GPU (same NUMA domain as
     # the GPU's PCIe root: frames are written there and read back by the GPU),
@@ -522,7 +560,7 @@ def main(argv=None):
             dist.barrier()   # other ranks may still be drawing on this rank's producers
 
     win = DeviceLoader.window(snap0, snap1)
-    t = torch.tensor([elapsed], dtype=torch.float64, device=device if args.backend == 'nccl' else 'cpu')
+    t = torch.tensor([elapsed], dtype=torch.float64, device=pg_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     tmax = float(t.item())
@@ -559,6 +597,8 @@ def main(argv=None):
             'baseline_note': BASELINE_NOTE,
             'world_size_seen': world_seen,
             'backend': (args.backend if world > 1 else None),
+            'pg_backend': (pg_backend if dist.is_initialized() else None),
+            'hw_queues': hw_queues,
             'allreduce_check': allreduce,
             'rank_time_s': {'min': round(min(r['elapsed_s'] for r in per_rank), 6),
                             'max': round(max(r['elapsed_s'] for r in per_rank), 6)},

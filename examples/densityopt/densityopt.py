@@ -37,6 +37,10 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT / 'pytorch-blender_amd'))
 
+from blendtorch.utils import ensure_hw_queues  # noqa: E402
+
+ensure_hw_queues()   # before the HIP runtime starts (loader + compute + RCCL streams)
+
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
@@ -44,6 +48,7 @@ from blendtorch import btt, parallel  # noqa: E402
 from blendtorch.models import Discriminator, ProbModel  # noqa: E402
 from blendtorch.models.densityopt import DensityOptStep  # noqa: E402
 from blendtorch.ops import DecodeConfig  # noqa: E402
+from blendtorch.utils.images import save_image  # noqa: E402
 
 BATCH = 64
 SIM_INSTANCES = 4
@@ -167,18 +172,45 @@ def run(args):
         update_simulations(remotes, s[0], s[1], ids)
         history = []
         d_steps = s_steps = 0
+        # rank 0 writes the reference's outputs: image grids of the target and
+        # the simulated batch every --image-every epochs (densityopt.py:321-323),
+        # encoded on a writer thread so the loop does not wait for zlib
+        out_dir = Path(args.out_dir) if args.out_dir else None
+        writer = None
+        if out_dir is not None and rank == 0:
+            out_dir.mkdir(parents=True, exist_ok=True)
+            from concurrent.futures import ThreadPoolExecutor
+            writer = ThreadPoolExecutor(max_workers=1)
+        pending = []
+        # steady state: iterations after the warm-up / capture ones, timed per phase
+        steady_from = max(args.steady_skip, step.warmup + 2)
+        ph = dict.fromkeys(('sim_wait', 'step_enqueue', 'fetch', 'send', 'images', 'gpu_iteration'), 0.0)
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if pin else None
+        n_steady, t_steady = 0, None
         t0 = time.time()
         wait_s = 0.0
         epoch = 0
         while True:
-            tw = time.time()
+            steady = epoch >= steady_from
+            if steady and t_steady is None:
+                t_steady = time.perf_counter()
+            ta = time.perf_counter()
             batch = next(gen_sim)
-            wait_s += time.time() - tw
+            tb = time.perf_counter()
+            wait_s += tb - ta
             sid = batch['shape_id']
             sid = sid if isinstance(sid, torch.Tensor) else torch.as_tensor(np.asarray(sid))
-            step(as_input(batch['image']), sid)
+            sim_img = as_input(batch['image'])
+            if ev is not None and steady:
+                ev[0].record()
+            step(sim_img, sid)
+            if ev is not None and steady:
+                ev[1].record()
+            tc = time.perf_counter()
             s = fetch()
+            td = time.perf_counter()
             update_simulations(remotes, s[0], s[1], ids)
+            te = time.perf_counter()
             d_steps += int(host_stats[2] > 0)
             s_steps += int(host_stats[3] > 0)
             history.append(host_params.clone())
@@ -187,9 +219,29 @@ def run(args):
                       f'D step {int(host_stats[2])} S step {int(host_stats[3])} params {host_params.tolist()}',
                       flush=True)
             epoch += 1
+            if writer is not None and args.image_every > 0 and epoch % args.image_every == 0:
+                r_img, s_img = real[:, :3].float().cpu(), sim_img[:, :3].float().cpu()
+                pending.append(writer.submit(save_image, r_img, out_dir / f'real_{epoch:03d}.png', normalize=True))
+                pending.append(writer.submit(save_image, s_img, out_dir / f'sim_samples_{epoch:03d}.png',
+                                             normalize=True))
+            tf = time.perf_counter()
+            if steady:
+                n_steady += 1
+                ph['sim_wait'] += tb - ta
+                ph['step_enqueue'] += tc - tb
+                ph['fetch'] += td - tc
+                ph['send'] += te - td
+                ph['images'] += tf - te
+                if ev is not None:
+                    ph['gpu_iteration'] += ev[0].elapsed_time(ev[1]) * 1e-3   # fetch() synchronised
             if epoch > args.num_epochs:
                 break
+        t_end = time.perf_counter()
         dt = time.time() - t0
+        for f in pending:
+            f.result()
+        if writer is not None:
+            writer.shutdown()
         tgt = torch.tensor(np.concatenate((mu_target, std_target))).float()
         diff = (tgt - history[-1]).abs()
         if rank == 0:
@@ -200,6 +252,31 @@ def run(args):
                'd_steps': d_steps, 's_steps': s_steps, 'graph': step.graph is not None,
                'dtype': 'bf16' if bf16 else 'fp32', 'collectives': ('rccl-direct' if comm is not None and comm.native
                                                                    else ('gloo' if comm is not None else None))}
+        if n_steady:
+            st = t_end - t_steady
+            res['steady'] = {
+                'first_iteration': steady_from, 'iterations': n_steady, 'seconds': st,
+                'iterations_per_s': n_steady / st, 'images_per_s': n_steady * B * world / st,
+                # per-iteration means (ms): host time blocked on the next simulated batch, enqueueing
+                # the (graph-replayed) iteration, the D->H fetch incl. waiting for the GPU, duplex
+                # sends, image bookkeeping; gpu_iteration = device time of the iteration (events)
+                'ms_per_iteration': {k: round(v * 1e3 / n_steady, 4) for k, v in ph.items()},
+                'ms_per_iteration_total': round(st * 1e3 / n_steady, 4),
+            }
+            if ev is None:
+                res['steady']['ms_per_iteration'].pop('gpu_iteration')
+        # the reference's record of convergence: parameter history with the
+        # target appended as the last row (densityopt.py:326-331, 350-354)
+        hist = torch.stack(history + [tgt]).numpy()
+        res['history_rows'] = int(hist.shape[0])
+        if out_dir is not None and rank == 0:
+            hp = out_dir / f'run_{args.timestr}_{args.run_index:02d}_densityopt.txt'
+            # the reference's call as it stands (densityopt.py:350-354): its note is
+            # savetxt's comments= prefix, so the first line reads
+            # 'last entry corresponds to target paramsmu_m1, ...' (np.loadtxt(skiprows=1))
+            np.savetxt(hp, hist, header='mu_m1, mu_m2, std_m1, std_m2',
+                       comments='last entry corresponds to target params')
+            res['history_file'] = str(hp)
         if comm is not None:
             w = torch.cat([p.detach().reshape(-1).float() for p in list(netD.parameters()) + list(pm.parameters())])
             res['weights_checksum'] = float(w.double().sum())
@@ -223,12 +300,29 @@ def main(argv=None):
     ap.add_argument('--no-graph', action='store_true', help='eager iterations (no HIP graph)')
     ap.add_argument('--no-fused-bn', action='store_true',
                     help='discriminator with MIOpen BatchNorm + PyTorch LeakyReLU instead of the fused gfx950 op')
+    ap.add_argument('--num-runs', default=1, type=int, help='independent runs (one history file each)')
+    ap.add_argument('--out-dir', default='tmp',
+                    help='where the parameter history and image grids go (reference: tmp/); "" writes nothing')
+    ap.add_argument('--image-every', default=5, type=int,
+                    help='write real_/sim_samples_ PNG grids every N epochs (reference: 5; 0 = never)')
+    ap.add_argument('--steady-skip', default=5, type=int,
+                    help='iterations excluded from the steady-state rate (at least warm-up + capture + 1)')
     ap.add_argument('--verbose', action='store_true')
     args = ap.parse_args(argv)
-    res = run(args)
+    args.timestr = time.strftime('%Y%m%d_%H%M%S')
     rank = int(os.environ.get('RANK', '0'))
+    runs = []
+    for i in range(args.num_runs):
+        args.run_index = i
+        if i > 0:
+            args.seed += 1
+            args.start_port += 7     # fresh producer ports (the previous ones may linger in TIME_WAIT)
+        res = run(args)
+        runs.append(res)
+        if rank == 0:
+            print(json.dumps(res), flush=True)
+    res = runs[-1] if len(runs) == 1 else dict(runs[-1], runs=runs)
     if rank == 0:
-        print(json.dumps(res), flush=True)
         if args.json:
             Path(args.json).write_text(json.dumps(res, indent=2))
     elif args.json:

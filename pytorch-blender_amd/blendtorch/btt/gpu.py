@@ -155,11 +155,15 @@ class DeviceLoader:
         self.host_sync = (h2d == 'copy') if host_sync is None else bool(host_sync)
         self._owed = 0             # deferred posts not yet made
         self._post_fn = None
-        # reuse_buffers: output tensors come from a fixed ring of prefetch + 2
-        # (a batch's tensor is refilled prefetch + 2 batches later, behind the
-        # consumer's stream work on it), so a consumer that captures one graph
-        # per input tensor (parallel.step.CapturedStep static_inputs) reads
-        # them in place -- it must not keep batches longer than that
+        # reuse_buffers: output tensors come from a fixed ring of prefetch + 2,
+        # so a consumer that captures one graph per input tensor
+        # (parallel.step.CapturedStep static_inputs) reads them in place.  The
+        # tensor of batch j is posted again when batch j + 2 is handed out (its
+        # refill is ordered behind the consumer's stream work on it): a
+        # consumer may keep the previous batch, never the one before that.
+        # The ring is rebuilt at every __iter__ and whenever the output shape
+        # or dtype changes (another frame size), so no differently sized
+        # tensor is ever posted to the native decode
         self.reuse_buffers = bool(reuse_buffers)
         self._ring = []
         self._ring_i = 0
@@ -196,6 +200,10 @@ class DeviceLoader:
     def _post(self, loader, stream):
         shape = self.decode.out_shape(self.batch_size, *self.shape[:2])
         if self.reuse_buffers:
+            dt = self.decode.torch_dtype()
+            if self._ring and (tuple(self._ring[0].shape) != tuple(shape) or self._ring[0].dtype != dt
+                               or self._ring[0].device != self.device):
+                self._ring, self._ring_i = [], 0
             if len(self._ring) < self.prefetch + 2:
                 self._ring.append(torch.empty(shape, dtype=self.decode.torch_dtype(), device=self.device))
                 out = self._ring[-1]
@@ -323,6 +331,7 @@ class DeviceLoader:
         loader = self._make()
         loader.start()
         self._live = loader
+        self._ring, self._ring_i = [], 0     # a new stream: a fresh output ring
         self._t_start = self._t_end = None
         self._wait_s = 0.0
         try:

@@ -56,6 +56,11 @@ _C10D_OPS = {'sum': dist.ReduceOp.SUM, 'prod': dist.ReduceOp.PRODUCT, 'max': dis
              'min': dist.ReduceOp.MIN}
 
 
+def _nonblocking():
+    v = os.environ.get('TORCH_NCCL_USE_COMM_NONBLOCKING', '0').strip().lower()
+    return v not in ('', '0', 'false', 'no', 'off')
+
+
 def _rccl_path():
     return os.path.join(os.path.dirname(torch.__file__), 'lib', 'librccl.so')
 
@@ -86,7 +91,12 @@ class DeviceComm:
             torch.device('cuda', torch.cuda.current_device()) if self.backend == 'nccl' else torch.device('cpu'))
         self._ext = None
         self._comm = 0
+        self._backend_obj = None
         want = self.backend == 'nccl' if force_native is None else bool(force_native)
+        if want and force_native is None and _nonblocking():
+            # a nonblocking communicator returns ncclInProgress from enqueue calls,
+            # which the direct path does not poll: keep the c10d path then
+            want = False
         if want and self.backend == 'nccl':
             self._attach()
         elif want:
@@ -110,6 +120,29 @@ class DeviceComm:
             raise RuntimeError(f'DeviceComm: communicator is rank {r} of {n}, process group says '
                                f'{self.rank} of {self.world}')
         self._ext, self._comm = ext, comm
+        # the borrowed communicator lives as long as this backend object (and
+        # the process group it belongs to): keep a reference, and check the
+        # group is still registered before every direct call (_live)
+        self._backend_obj = be
+
+    def _live(self):
+        """Raise instead of calling RCCL through a communicator whose process
+        group was destroyed (``dist.destroy_process_group``): the borrowed
+        pointer would dangle."""
+        ok = dist.is_initialized()
+        if ok:
+            try:
+                from torch.distributed import distributed_c10d as c10d
+                ok = self.group in c10d._world.pg_map
+            except (AttributeError, ImportError):   # private registry moved: trust is_initialized
+                pass
+        if not ok:
+            self._comm, self._ext, self._backend_obj = 0, None, None
+            raise RuntimeError('DeviceComm: its process group was destroyed; the RCCL communicator is gone')
+
+    def close(self):
+        """Drop the borrowed communicator (before destroying the process group)."""
+        self._comm, self._ext, self._backend_obj = 0, None, None
 
     @property
     def native(self) -> bool:
@@ -119,6 +152,7 @@ class DeviceComm:
         return torch.cuda.current_stream(t.device).cuda_stream
 
     def _check(self, t):
+        self._live()
         if not t.is_cuda or t.device != self.device:
             raise ValueError(f'DeviceComm: tensor on {t.device}, communicator on {self.device}')
         if not t.is_contiguous():

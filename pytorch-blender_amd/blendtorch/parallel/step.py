@@ -109,7 +109,14 @@ class CapturedStep:
         the memory-bound forward, see bench.py --dma-phase).
 
     ``state`` is ``'graph'`` after a successful capture, ``'eager'`` otherwise.
+    An input whose layout (shape, strides, dtype, offset) differs from the
+    captured one runs an eager step; a graph is never replayed for it.
     ``collectives`` is the number of all-reduces per step.
+
+    Gradients of a bucketed step are never ``None``: a parameter that gets no
+    gradient in some step sees a zero gradient, and Adam's moments still move
+    it (``torch.optim.Adam`` after ``zero_grad(set_to_none=True)`` would skip
+    it).  Keep such parameters out of the optimizer, or use ``buckets=False``.
     """
 
     def __init__(self, model: torch.nn.Module, optimizer: torch.optim.Optimizer,
@@ -145,7 +152,13 @@ class CapturedStep:
             self.grads = GradBuckets(model.parameters(), bucket_mb=bucket_mb)
             if zeroing:
                 optimizer.set_zero_grads(True)
-                self._memset = False
+                # the optimizer clears only the gradients it consumes: a model
+                # parameter outside it would accumulate across steps, so the
+                # buckets are then cleared per step as well
+                opt_ids = {id(p) for grp in optimizer.param_groups for p in grp['params']}
+                self._memset = any(id(p) not in opt_ids for p in self.grads.params)
+        self._static_mode = bool(self.static_inputs)
+        self._copy_failed = False
         if active and buckets:
             from .comm import DeviceComm
             self.comm = comm if comm is not None else DeviceComm(group, dedicated=True)
@@ -217,7 +230,7 @@ class CapturedStep:
 
     def _same_layout(self, x):
         return (x.shape == self.x.shape and x.stride() == self.x.stride() and x.dtype == self.x.dtype
-                and x.device == self.x.device)
+                and x.device == self.x.device and x.storage_offset() == self.x.storage_offset())
 
     def _capture_for(self, x, key=None):
         """One more graph of the step, reading ``x`` in place, in the first
@@ -228,11 +241,43 @@ class CapturedStep:
                 loss = self._train(x)
         except RuntimeError as e:
             self.error = str(e)
-            self.static_inputs = len(self._by_input)     # no more captures; copy into the first graph's input
+            self.static_inputs = self._n_static()        # no more in-place captures
+            if key == 'copy':
+                self._copy_failed = True                 # recorded once: later misses run eagerly
             return None
         ent = (g, x, loss)
         self._by_input[x.data_ptr() if key is None else key] = ent
         return ent
+
+    def _n_static(self):
+        return len(self._by_input) - ('copy' in self._by_input)
+
+    def _lookup(self, x):
+        """The graph that runs the step on ``x`` in static-input mode, or None
+        (the caller then steps eagerly).  A graph is only ever replayed for
+        an input of exactly the captured layout: a cache hit on the data
+        pointer alone (e.g. ``x[:4]`` or a dtype view of a captured buffer)
+        would replay the step for the captured shape."""
+        if not self._same_layout(x):
+            return None
+        ent = self._by_input.get(x.data_ptr())
+        if ent is None and self._n_static() < self.static_inputs:
+            ent = self._capture_for(x)
+        if ent is None and not self._copy_failed:
+            # past the cap: copy into a private buffer with a graph of its own
+            # (the captured inputs are callers' tensors, never written)
+            ent = self._by_input.get('copy')
+            if ent is None:
+                ent = self._capture_for(torch.empty_like(x), key='copy')
+            if ent is not None:
+                ent[1].copy_(x)
+        return ent
+
+    def _eager(self, x, mid):
+        loss = self._forward(x)
+        if mid is not None:
+            mid()
+        return self._backward(loss)
 
     def _replay(self, mid):
         self.graph.replay()
@@ -250,29 +295,19 @@ class CapturedStep:
                 self._replay(mid)
                 return self.loss
         if self.state == 'graph':
-            if self.static_inputs:
-                ent = self._by_input.get(x.data_ptr())
-                if ent is None and len(self._by_input) - ('copy' in self._by_input) < self.static_inputs \
-                        and self._same_layout(x):
-                    ent = self._capture_for(x)
-                if ent is None and self._same_layout(x):
-                    # past the cap: copy into a private buffer with a graph of its own
-                    # (the first graph's input is a caller's tensor, never written)
-                    ent = self._by_input.get('copy')
-                    if ent is None:
-                        ent = self._capture_for(torch.empty_like(x), key='copy')
-                    if ent is not None:
-                        ent[1].copy_(x)
-                if ent is not None:
-                    ent[0].replay()
-                    if mid is not None:
-                        mid()
-                    return ent[2]
+            if self._static_mode:
+                # self.x is a caller's tensor (e.g. a loader ring buffer): never written
+                ent = self._lookup(x)
+                if ent is None:
+                    return self._eager(x, mid)
+                ent[0].replay()
+                if mid is not None:
+                    mid()
+                return ent[2]
+            if x.shape != self.x.shape or x.dtype != self.x.dtype or x.device != self.x.device:
+                return self._eager(x, mid)       # the graph is for the captured shape only (copy_ converts strides)
             if x.data_ptr() != self.x.data_ptr():
                 self.x.copy_(x)
             self._replay(mid)
             return self.loss
-        loss = self._forward(x)
-        if mid is not None:
-            mid()
-        return self._backward(loss)
+        return self._eager(x, mid)

@@ -55,12 +55,15 @@ def _libatomic_cas():
         except (OSError, AttributeError):
             continue
         fn.restype = ctypes.c_bool
-        fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_bool, ctypes.c_int, ctypes.c_int]
+        # the out-of-line libatomic entry point is (ptr, expected*, desired,
+        # success_order, failure_order) -- no 'weak' argument (that one exists
+        # only in the compiler builtin)
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_int]
 
         def cas(states, i, expected, desired, _fn=fn, _c=ctypes):
             exp = _c.c_uint32(int(expected))
             addr = states.ctypes.data + 4 * int(i)
-            return bool(_fn(addr, _c.addressof(exp), int(desired) & 0xFFFFFFFF, False, 5, 5))   # seq_cst
+            return bool(_fn(addr, _c.addressof(exp), int(desired) & 0xFFFFFFFF, 5, 5))   # seq_cst, seq_cst
         return cas
     return None
 

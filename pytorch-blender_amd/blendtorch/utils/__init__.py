@@ -10,19 +10,49 @@ benchmarks/benchmark.py:33-47 and the ``'blendtorch'`` logger (SURVEY.md
   --marker-trace`` timelines) around host-side stages, no-op without a GPU;
 * :class:`StreamConfig` -- one place for the GPU streaming knobs whose
   defaults reproduce the reference's behaviour (HWM 10, 10 s timeout, batch
-  of dicts).
+  of dicts);
+* :func:`ensure_hw_queues` -- enough HIP hardware queues per process for
+  the loader's streams, the compute stream and RCCL's.
 """
 from __future__ import annotations
 
 import contextlib
 import dataclasses
 import logging
+import os
 import time
 from typing import Dict, Optional
 
 logger = logging.getLogger('blendtorch')
 
-__all__ = ['Meter', 'trace_range', 'StreamConfig', 'get_logger']
+__all__ = ['Meter', 'trace_range', 'StreamConfig', 'get_logger', 'ensure_hw_queues']
+
+# HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues per process (4 by
+# default) round-robin.  A rank's loader uses 2-3 streams (decode, copies),
+# the consumer one, and an RCCL communicator adds its own: with 4 queues the
+# loader's streams then share queues with RCCL's and serialise behind them.
+# Measured on one MI355X (profiles/r4/pg_tax.md): a live 1-rank RCCL process
+# group cost streaming 3.6 % (shard) / 5.3 % (scatter) at 4 queues and 0.0 % /
+# 0.7 % at 8.
+DEFAULT_HW_QUEUES = 8
+
+
+def ensure_hw_queues(n: int = DEFAULT_HW_QUEUES) -> int:
+    """Raise ``GPU_MAX_HW_QUEUES`` to at least ``n`` for this process (and
+    the processes it starts) unless ``BT_HW_QUEUES`` pins a value.  Only
+    effective before the HIP runtime initialises (the first GPU call), so
+    call it at program start.  Returns the value in force."""
+    pinned = os.environ.get('BT_HW_QUEUES')
+    if pinned:
+        os.environ['GPU_MAX_HW_QUEUES'] = str(int(pinned))
+    else:
+        try:
+            cur = int(os.environ.get('GPU_MAX_HW_QUEUES', '4'))
+        except ValueError:
+            cur = 4
+        if cur < n:
+            os.environ['GPU_MAX_HW_QUEUES'] = str(int(n))
+    return int(os.environ['GPU_MAX_HW_QUEUES'])
 
 
 def get_logger():

@@ -91,12 +91,33 @@ def test_step_matches_reference_rules_cpu():
 
 
 @pytest.mark.background
-def test_densityopt_example_cpu(free_port):
+def test_densityopt_example_cpu(free_port, tmp_path):
+    """The example runs end to end on the CPU path and writes the reference's
+    outputs (densityopt.py:321-331, 350-354): the parameter history as text,
+    one row per epoch plus the target as the last row, and image grids of
+    the target and simulated batch every 5 epochs."""
+    import numpy as np
+    from blendtorch.utils.images import read_png
     mod = _example()
-    res = mod.main(['--device', 'cpu', '--num-epochs', '4', '--instances', '2', '--batch', '16',
-                    '--start-port', str(free_port)])
-    assert res['iterations'] == 5 and res['world'] == 1 and res['dtype'] == 'fp32'
+    res = mod.main(['--device', 'cpu', '--num-epochs', '5', '--instances', '2', '--batch', '16',
+                    '--start-port', str(free_port), '--out-dir', str(tmp_path), '--steady-skip', '1'])
+    assert res['iterations'] == 6 and res['world'] == 1 and res['dtype'] == 'fp32'
     assert all(d == d for d in res['abs_diff'])           # finite
+    # the reference passes its note as savetxt's comments= (the header's
+    # prefix, not a comment line): mirrored byte for byte, so skip that line
+    hist = np.loadtxt(res['history_file'], skiprows=1)
+    assert hist.shape == (7, 4) and res['history_rows'] == 7
+    np.testing.assert_allclose(hist[-1], res['target'], rtol=1e-6)
+    np.testing.assert_allclose(hist[-2], res['final_params'], rtol=1e-5)
+    head = Path(res['history_file']).read_text().splitlines()
+    assert head[0] == 'last entry corresponds to target paramsmu_m1, mu_m2, std_m1, std_m2'
+    # 16 images of 64x64 in rows of 8 with 2-pixel padding: 2 x 8 tiles
+    for name in ('real_005.png', 'sim_samples_005.png'):
+        img = read_png(tmp_path / name)
+        assert img.shape == (2 * 66 + 2, 8 * 66 + 2, 3) and img.max() > img.min()
+    st = res['steady']
+    assert st['iterations'] >= 1 and st['iterations_per_s'] > 0
+    assert set(st['ms_per_iteration']) >= {'sim_wait', 'step_enqueue', 'fetch', 'send'}
 
 
 def _rank(rank, world, port, prod_port, out):
@@ -105,7 +126,7 @@ def _rank(rank, world, port, prod_port, out):
     try:
         mod = _example()
         res = mod.main(['--device', 'cpu', '--backend', 'gloo', '--num-epochs', '3', '--instances', '2',
-                        '--batch', '8', '--start-port', str(prod_port), '--seed', str(rank)])
+                        '--batch', '8', '--start-port', str(prod_port), '--seed', str(rank), '--out-dir', ''])
         Path(out).write_text(json.dumps(res))
     except Exception:
         import traceback

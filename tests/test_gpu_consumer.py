@@ -291,3 +291,36 @@ def test_captured_step_static_inputs_read_in_place(dev):
     for pa, pb in zip(nets[0].parameters(), nets[1].parameters()):
         d = (pb - pa).detach().abs()
         assert float(d.mean()) < 0.15 * lr
+
+
+def test_captured_step_never_replays_for_another_layout(dev):
+    """A cache hit on the data pointer alone must not replay a graph: a view
+    of a captured buffer with another shape (``x[:2]``: same data pointer;
+    ``x[2:]``: same storage) runs an eager step -- visible as host-side op calls, which a replay makes
+    none of -- and the captured input is never written."""
+    from blendtorch.models import Discriminator
+    from blendtorch.parallel.step import CapturedStep
+    cl = torch.channels_last
+    g = torch.Generator(device=dev).manual_seed(9)
+    buf = torch.rand(4, 4, 96, 128, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    keep = buf.clone()
+    for static in (0, 2):
+        torch.manual_seed(0)
+        m = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
+        opt = ops.FusedAdam(m.parameters(), lr=2e-4)
+        step = CapturedStep(m, opt, lambda mm, x: mm.bce_loss_bf16(x, 1.0), allreduce=False, graph=True,
+                            static_inputs=static)
+        step(buf)
+        step(buf)
+        torch.cuda.synchronize()
+        assert step.state == 'graph'
+        calls = ops.KERNEL_CALLS.get('conv_fwd', 0)
+        step(buf)                                           # replay: no host-side op calls
+        assert ops.KERNEL_CALLS.get('conv_fwd', 0) == calls
+        for x in (buf[:2], buf[2:]):      # same pointer / same storage, other shape
+            loss = step(x)
+            torch.cuda.synchronize()
+            assert ops.KERNEL_CALLS.get('conv_fwd', 0) > calls, 'replayed a graph for another layout'
+            calls = ops.KERNEL_CALLS.get('conv_fwd', 0)
+            assert bool(torch.isfinite(loss))
+        assert torch.equal(buf, keep)                       # the caller's tensor was never written

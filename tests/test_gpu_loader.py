@@ -571,3 +571,25 @@ def test_host_sync_many_small_batches_match_cpu(dev, free_port, h2d, decode):
             fids += b['frameid'].tolist()
             assert torch.equal(b['image'].cpu(), ref[len(fids) - 4:len(fids)]), f'batch ending at {len(fids)}'
     assert fids == [m['frameid'] for m in cpu]
+
+
+def test_reuse_buffers_ring_rebuilt_per_stream_and_shape(dev, free_port):
+    """``reuse_buffers=True``: a second iteration over producers of another
+    frame size gets a fresh output ring of the new shape (an old, differently
+    sized tensor posted to the native decode would be written out of bounds),
+    and within one stream the ring cycles prefetch + 2 tensors."""
+    cfg = ops.DecodeConfig.unit(channels='rgb', gamma=2.2)
+    dl = DeviceLoader([], batch_size=4, max_items=48, decode=cfg, device=dev, prefetch=2, reuse_buffers=True)
+    for k, (w, h) in enumerate(((320, 240), (160, 120))):
+        with btt.BlenderLauncher(producer='cubesim', num_instances=1, named_sockets=['DATA'],
+                                 start_port=free_port + 5 * k, seed=4,
+                                 instance_args=[['--mode', 'rgba', '--resolution', f'{w}x{h}']]) as bl:
+            dl.addresses = bl.launch_info.addresses['DATA']
+            ptrs = set()
+            for b in dl:
+                img = b['image']
+                assert img.shape == (4, 3, h, w)
+                assert float(img.min()) >= 0.0 and float(img.max()) <= 1.0
+                ptrs.add(img.data_ptr())
+            assert len(ptrs) == dl.prefetch + 2
+            assert all(tuple(t.shape) == (4, 3, h, w) for t in dl._ring)

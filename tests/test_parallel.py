@@ -268,3 +268,31 @@ def test_pack_meta_rejects_schema_drift():
         parallel.pack_meta({'btid': torch.arange(4), 'xy': torch.rand(4, 9, 2, dtype=torch.float64)}, schema, 4)
     with pytest.raises(ValueError, match="'btid' changed"):
         parallel.pack_meta({'btid': torch.arange(4, dtype=torch.int32), 'xy': b['xy']}, schema, 4)
+
+
+def test_device_comm_refuses_a_destroyed_process_group(monkeypatch):
+    """A DeviceComm whose process group was destroyed raises instead of
+    calling RCCL through the dangling borrowed communicator; a nonblocking
+    communicator (TORCH_NCCL_USE_COMM_NONBLOCKING) is never borrowed."""
+    import os
+    import torch
+    import torch.distributed as dist
+    from blendtorch.parallel import comm as commmod
+    from blendtorch.parallel.launch import free_port
+    os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+    monkeypatch.setenv('MASTER_PORT', str(free_port()))
+    dist.init_process_group('gloo', rank=0, world_size=1)
+    try:
+        c = commmod.DeviceComm()
+        assert not c.native
+        c._comm = 1                      # pretend a borrowed communicator
+        c._live()                        # group alive: fine
+    finally:
+        dist.destroy_process_group()
+    with pytest.raises(RuntimeError, match='destroyed'):
+        c._live()
+    assert not c.native
+    monkeypatch.setenv('TORCH_NCCL_USE_COMM_NONBLOCKING', '1')
+    assert commmod._nonblocking()
+    monkeypatch.setenv('TORCH_NCCL_USE_COMM_NONBLOCKING', '0')
+    assert not commmod._nonblocking()

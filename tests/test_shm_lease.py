@@ -162,3 +162,34 @@ def test_libatomic_cas_fallback_is_atomic_cas():
     assert words[2] == (7 << 2) | shm.PUBLISHED
     assert cas(words, 2, (7 << 2) | shm.PUBLISHED, (7 << 2) | shm.HELD)
     assert words[2] == (7 << 2) | shm.HELD and words[1] == 0 and words[3] == 0
+
+
+def test_cas_through_ctypes_path_with_native_forced_off(monkeypatch):
+    """``shm._cas`` with the native module forced off goes through libatomic's
+    out-of-line ``__atomic_compare_exchange_4(ptr, expected*, desired,
+    success_order, failure_order)``; threads racing CAS-increments on one
+    word (ctypes drops the GIL around the call) lose no update."""
+    import threading
+    import numpy as np
+    from blendtorch.transport import shm
+    monkeypatch.setattr(shm, '_native_cas', None)
+    monkeypatch.setattr(shm, '_ctypes_cas', shm._libatomic_cas())
+    assert shm._ctypes_cas is not None
+    words = np.zeros(2, dtype=np.uint32)
+    assert shm._cas(words, 1, 0, 5) and words[1] == 5
+    assert not shm._cas(words, 1, 0, 9) and words[1] == 5
+    n_threads, per = 4, 2000
+
+    def bump():
+        for _ in range(per):
+            while True:
+                cur = int(words[0])
+                if shm._cas(words, 0, cur, cur + 1):
+                    break
+
+    ts = [threading.Thread(target=bump) for _ in range(n_threads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert int(words[0]) == n_threads * per and int(words[1]) == 5

@@ -1,5 +1,8 @@
 """Observability / configuration helpers."""
 import inspect
+import os
+
+import torch
 
 import pytest
 
@@ -35,3 +38,30 @@ def test_meter_rates():
         pass
     d = m.summary()
     assert d['frames'] == 10 and d['frames_per_s'] > 0 and d['recv_ms_avg'] >= 0
+
+
+def test_ensure_hw_queues_raises_but_never_lowers(monkeypatch):
+    from blendtorch.utils import ensure_hw_queues
+    monkeypatch.delenv('BT_HW_QUEUES', raising=False)
+    monkeypatch.setenv('GPU_MAX_HW_QUEUES', '4')
+    assert ensure_hw_queues(8) == 8 and os.environ['GPU_MAX_HW_QUEUES'] == '8'
+    monkeypatch.setenv('GPU_MAX_HW_QUEUES', '16')
+    assert ensure_hw_queues(8) == 16
+    monkeypatch.setenv('BT_HW_QUEUES', '4')          # an explicit pin wins
+    assert ensure_hw_queues(8) == 4 and os.environ['GPU_MAX_HW_QUEUES'] == '4'
+
+
+def test_save_image_matches_torchvision_grid_rules(tmp_path):
+    """PNG grids as torchvision.utils.save_image(normalize=True) writes them
+    (the densityopt example's image output): min-max over the batch, tiles in
+    rows of nrow with 2-pixel zero padding, x * 255 + 0.5 truncated."""
+    import numpy as np
+    from blendtorch.utils.images import read_png, save_image
+    x = torch.arange(3 * 3 * 2 * 2, dtype=torch.float32).reshape(3, 3, 2, 2) - 5
+    u8 = save_image(x, tmp_path / 'g.png', nrow=2, normalize=True)
+    back = read_png(tmp_path / 'g.png')
+    assert back.shape == (2 * 4 + 2, 2 * 4 + 2, 3) and np.array_equal(back, u8)
+    lo, hi = float(x.min()), float(x.max())
+    want = np.clip((x[1].numpy() - lo) / (hi - lo) * 255 + 0.5, 0, 255).astype(np.uint8).transpose(1, 2, 0)
+    assert np.array_equal(back[2:4, 6:8], want)         # tile 1: row 0, column 1
+    assert back[:2].max() == 0 and back[8:, 6:].max() == 0   # padding and the empty 4th tile stay 0
