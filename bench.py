@@ -183,6 +183,9 @@ def parse_args(argv=None):
                     help='disc consumer with the in-step decode (bf16, fused cast and head): on = the first '
                          'convolution reads the raw u8 RGBA frames through the decode table inside its MFMA '
                          'kernels; off = a decode launch writes bf16 frames first')
+    ap.add_argument('--grad-overlap', choices=['on', 'off'], default='on',
+                    help='disc consumer, data parallel: on = two gradient buckets, each all-reduced as soon as its '
+                         'gradients are written; off = one bucket after the whole backward')
     ap.add_argument('--consumer-input', choices=['stream', 'resident'], default='stream',
                     help='diagnostic: resident = the consumer trains on one fixed batch while the stream keeps running')
     ap.add_argument('--force-pg', action='store_true',
@@ -477,9 +480,11 @@ def main(argv=None):
         stepper = None
         if model is not None:
             from blendtorch.parallel.step import CapturedStep
+            # data parallel: two gradient buckets, the last layers' all-reduced as soon as
+            # written, ahead of the first layers' weight gradients (GradBuckets.arm)
             stepper = CapturedStep(model, opt, loss_fn, graph=use_graph, comm=comm,
                                    allreduce='always' if args.force_pg else dist.is_initialized(), split=dma_mid,
-                                   static_inputs=static_in)
+                                   static_inputs=static_in, overlap=args.grad_overlap == 'on')
 
         def graphed(x):
             stepper(x, mid=dl.release if (dma_mid and dl is not None) else None)
@@ -633,6 +638,8 @@ def main(argv=None):
                 'head': args.head if model is not None else None,
                 'host_sync': args.host_sync,
                 'consumer_collectives_per_step': stepper.collectives if stepper is not None else None,
+                'grad_buckets_issue_order': (stepper.grads.order if stepper is not None and stepper.overlap
+                                             and stepper.grads is not None else None),
                 'collectives': ('rccl-direct' if comm is not None and comm.native else
                                 ('c10d' if comm is not None else None)),
             },

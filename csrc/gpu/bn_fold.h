@@ -73,5 +73,88 @@ __device__ inline void bn_fold_block(const BnFold& f, double* part) {
   }
 }
 
+// BatchNorm + LeakyReLU backward for one element, given the BN input v and
+// the gradient g of the activation's output: gx = P (gz - db / M) - P dw / M
+// xhat, xhat = v is + nm, gz = g leaky'(xhat w + b).  ONE definition for the
+// apply kernel (train.hip) and the first layer's weight gradient, which
+// computes its dY operand this way instead of reading a materialised gx
+// (conv.hip, ConvWgradParams::bn_dy): both round the same fp32 value to bf16.
+struct BnBwdCoef {
+  float is, nm, ww, bb, P, dbm, pdw;
+  __device__ void init(float mean, float invstd, float w, float b, float dw, float db, float invM) {
+    is = invstd;
+    nm = -mean * is;
+    ww = w;
+    bb = b;
+    P = ww * is;
+    dbm = db * invM;
+    pdw = P * dw * invM;
+  }
+  __device__ float gx(float v, float g, float slope) const {
+    const float xh = fmaf(v, is, nm);
+    const float gz = fmaf(xh, ww, bb) > 0.f ? g : g * slope;
+    return fmaf(P, gz - dbm, -pdw * xh);
+  }
+};
+
+// The apply kernels' own fold (bn_apply_fold_kernel, train.hip): EVERY block
+// of the apply launch folds the accumulator it consumes -- one memory latency
+// at the block's start, overlapped with its first pass of loads -- so no
+// one-block finalize launch (and its kernel boundary) sits between the
+// producer and the apply.  The accumulator is cleared for the next producer
+// by whichever block arrives last (a ticket word after the [R][2][C]
+// replicas: blocks take a ticket only once their reads have returned, so the
+// last ticket holder clears after every reader), and block 0 writes the
+// finalized outputs (mean / invstd and running statistics, or dw / db).
+//
+// Sums of column j of [R][J] (J = 2C) over the replicas into part[j] (every
+// thread of the block; part: >= max(nt, J) doubles of LDS).
+__device__ inline void bn_acc_column_sums(const double* acc, int R, int J, double* part) {
+  const int t = int(threadIdx.x), nt = int(blockDim.x);
+  const int G = J >= nt ? 1 : nt / J;
+  for (int u = t; u < G * J; u += nt) {
+    const int j = u % J, g = u / J;
+    double v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = g + G * i;
+      v[i] = r < R ? acc[int64_t(r) * J + j] : 0.0;
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += v[i];
+    for (int r = g + 8 * G; r < R; r += G) s += acc[int64_t(r) * J + j];
+    part[g * J + j] = s;
+  }
+  __syncthreads();
+  // fold the G groups into part[j] (column j is owned by one thread: no race)
+  for (int j = t; j < J; j += nt) {
+    double s = part[j];
+    for (int g = 1; g < G; ++g) s += part[g * J + j];
+    part[j] = s;
+  }
+  __syncthreads();
+}
+
+// The ticket word of a [R][2][C] accumulator (kernels.h: bn_acc_elems leaves room for it)
+__device__ inline unsigned* bn_acc_ticket(double* acc, int R, int C) {
+  return reinterpret_cast<unsigned*>(acc + int64_t(R) * 2 * C);
+}
+
+// After every reader of this block has its values (call after the block's
+// last use of them, behind a barrier): take a ticket; the block with the
+// last one clears the replicas and resets the ticket.  `flag`: one int of LDS.
+__device__ inline void bn_acc_release(double* acc, int R, int C, int* flag) {
+  const int t = int(threadIdx.x), nt = int(blockDim.x);
+  unsigned* ticket = bn_acc_ticket(acc, R, C);
+  if (t == 0) *flag = atomicAdd(ticket, 1u) == gridDim.x * gridDim.y - 1 ? 1 : 0;
+  __syncthreads();
+  if (*flag) {
+    const int n = R * 2 * C;
+    for (int i = t; i < n; i += nt) acc[i] = 0.0;
+    if (t == 0) *ticket = 0u;
+  }
+}
+
 }  // namespace gpu
 }  // namespace btn

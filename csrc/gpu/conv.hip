@@ -408,6 +408,159 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p)
 }
 
 // ---------------------------------------------------------------------------
+// The same weight gradient with LDS-DMA staging (buffer_load ... lds) and
+// 64-pixel k-steps: the register path above stages every 16-byte chunk through
+// VGPRs and ds_write (the kernel's VALU and LDS-store bound: 6.4 VALU per
+// MFMA, 24 us per layer in the disc step) and barriers every 8 MFMAs.
+//
+// LDS image per stage: COLUMN blocks -- one 16-byte chunk column (8 channels)
+// of the 64 pixels, 1 KiB, padded to 1088 B -- so one wave-instruction of
+// LDS-DMA (lane l -> bytes 16 l of 1 KiB) lands 64 pixels of one chunk: lane l
+// is pixel l of the step, every lane keeps ONE pixel cursor, and a wave's
+// instructions are whole chunk columns (wave-uniform (kh, kw, ci), scalar).
+// The transposing fragment read of 4 pixels x 16 columns (two column blocks)
+// is conflict-free: within 32 lanes the 8-byte pieces sit at 128 g + 16 q
+// (pixel) + 64 (block, from the 1088-byte pitch) + 8 (half chunk) mod 256.
+constexpr int W2_BPX = 64;                        // pixels per k-step
+constexpr int W2_COL = W2_BPX * 16 + 64;          // one column block, padded
+constexpr int W2_DY = (BCO / 8) * W2_COL;         // dY: 8 blocks (64 output channels)
+constexpr int W2_X = (BKC / 8) * W2_COL;          // X: 16 blocks (128 im2col columns)
+constexpr int W2_STAGE = W2_DY + W2_X;
+
+__device__ __forceinline__ int w2_off(int px, int col) { return (col >> 3) * W2_COL + px * 16 + (col & 7) * 2; }
+
+template <int NST>
+__global__ __launch_bounds__(kThreads) void conv_wgrad_dma_kernel(ConvWgradParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[NST * W2_STAGE];
+  if (run_side(p, smem)) return;
+  const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const int KC = 16 * p.Cin, KT = KC / BKC, T = (p.Cout / BCO) * KT;
+  const int nwg = main_blocks(p), b = int(blockIdx.x);
+  const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  const int slice = w / T, tile = w - slice * T;
+  const int co0 = (tile / KT) * BCO, kt = tile - (tile / KT) * KT;
+  const int m_begin = slice * int(p.px_per_slice);
+  const int m_end = m_begin + int(p.px_per_slice) < int(p.M) ? m_begin + int(p.px_per_slice) : int(p.M);
+  const int nsteps = m_end > m_begin ? (m_end - m_begin + W2_BPX - 1) / W2_BPX : 0;
+
+  // this wave's chunk columns: X blocks 4 wv + j (j < 4), dY blocks 2 wv + j (j < 2);
+  // (kh, kw, ci) and the element delta from the pixel's tap-(0, 0) origin are wave-uniform
+  int xkh[4], xkw[4], xde[4];
+  const int cs = __builtin_ctz(unsigned(p.Cin));   // Cin is a power of two (host check)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int kc = kt * BKC + (4 * wv + j) * 8;
+    xkh[j] = kc >> (cs + 2);
+    xkw[j] = (kc >> cs) & 3;
+    xde[j] = (xkh[j] * p.W + xkw[j]) * p.Cin + (kc & (p.Cin - 1));
+  }
+  // lane = pixel m of the step: (oh, ow) and the element offset of its tap-(0, 0) origin
+  int m = m_begin + lane;
+  int oh, ow, e;
+  {
+    const int hw = p.Ho * p.Wo;
+    const int n = m / hw, r = m - n * hw;
+    oh = r / p.Wo;
+    ow = r - oh * p.Wo;
+    e = (n * p.H + 2 * oh - 1) * (p.W * p.Cin) + (2 * ow - 1) * p.Cin;
+  }
+  const int j_col = 2 * W2_BPX * p.Cin, j_row = 2 * (p.W - p.Wo) * p.Cin, j_img = (p.H - 2 * p.Ho) * p.W * p.Cin;
+  const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(p.x, int64_t(p.N) * p.H * p.W * p.Cin * 2);
+  const __amdgpu_buffer_rsrc_t rs_dy = make_rsrc(p.dy, p.M * p.Cout * 2);
+  const uint32_t dy_co = uint32_t((co0 + 2 * wv * 8) * 2);
+
+  // one stage: 4 X + 2 dY LDS-DMA instructions per wave; stages past the slice
+  // load out of range (zeros, no memory traffic), so every stage counts the same
+  auto issue = [&](int buf) {
+    char* st = smem + buf * W2_STAGE;
+    const int ih = 2 * oh - 1, iw = 2 * ow - 1;
+    const bool live = m < m_end;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool ok = live && unsigned(ih + xkh[j]) < unsigned(p.H) && unsigned(iw + xkw[j]) < unsigned(p.W);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs_x, (__attribute__((address_space(3))) void*)(st + W2_DY + (4 * wv + j) * W2_COL), 16,
+          int(ok ? uint32_t(e + xde[j]) * 2u : kOOB), 0, 0, 0);
+    }
+    const uint32_t doff = uint32_t(m) * uint32_t(p.Cout * 2) + dy_co;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs_dy, (__attribute__((address_space(3))) void*)(st + (2 * wv + j) * W2_COL), 16,
+          int(live ? doff + uint32_t(j * 16) : kOOB), 0, 0, 0);
+    // advance the pixel by 64 (at most two row wraps for Wo >= 32)
+    m += W2_BPX;
+    ow += W2_BPX;
+    e += j_col;
+    while (ow >= p.Wo) {
+      ow -= p.Wo;
+      e += j_row;
+      if (++oh == p.Ho) oh = 0, e += j_img;
+    }
+  };
+
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int wco = (wave >> 1) * 32, wkc = (wave & 1) * 64;
+  // fragment read offsets (loop invariant): rows (pixels) 8 g + q (+4, +32 kk), columns col + 4 pp
+  int ra[2], rb[4];
+  {
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) ra[i] = w2_off(8 * g + q, wco + 16 * i + 4 * pp);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) rb[j] = W2_DY + w2_off(8 * g + q, wkc + 16 * j + 4 * pp);
+  }
+  constexpr int NL = 6;   // LDS-DMA instructions per stage per lane
+  constexpr uint32_t kWaitAll = (7u << 4) | (0xFu << 8);
+  constexpr uint32_t kWaitNewer = kWaitAll | uint32_t((NL * (NST - 2)) & 15) | (uint32_t((NL * (NST - 2)) >> 4) << 14);
+#pragma unroll
+  for (int u = 0; u < NST - 1; ++u) issue(u);
+  int cur = 0;
+  for (int s = 0; s < nsteps; ++s) {
+    // stage s landed (the NST - 2 younger stages may stay in flight), visible
+    // to every wave; every wave is done reading stage s - 1's buffer
+    __builtin_amdgcn_s_waitcnt(kWaitNewer);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    issue(cur == 0 ? NST - 1 : cur - 1);   // step s + NST - 1
+    const char* base = smem + cur * W2_STAGE;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ko = kk * 32 * 16;          // 32 pixels further down the column blocks
+      bf16x8 a[2], bm[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = frag_at(base, ra[i] + ko, 4 * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bm[j] = frag_at(base, rb[j] + ko, 4 * 16);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bm[j], acc[i][j], 0, 0, 0);
+    }
+    cur = cur == NST - 1 ? 0 : cur + 1;
+  }
+  __builtin_amdgcn_s_waitcnt(kWaitAll);   // the padding stages' DMAs are done before the block exits
+
+  zero_output(p);
+  float* out = p.partial + int64_t(slice) * p.Cout * KC + (co0 + wco + 4 * (lane >> 4)) * KC +
+               (kt * BKC + wkc + (lane & 15));
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[(16 * i + r) * KC + 16 * j] = acc[i][j][r];
+}
+
+// ---------------------------------------------------------------------------
 // Weight gradient of the FIRST layer: 4-channel input (RGB frames decoded as
 // RGBA bf16; the alpha channel's gradient is computed and discarded), Cout %
 // 32 == 0.  KC = 16 taps x 4 channels = 64, one 32 x 64 tile per block and
@@ -455,9 +608,22 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4_kernel(ConvWgradParams
   c.init(m_begin + xpx, p.Ho, p.Wo);
   const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(p.x, int64_t(p.N) * p.H * p.W * 4 * (u8in ? 1 : 2));
   const __amdgpu_buffer_rsrc_t rs_dy = make_rsrc(p.dy, p.M * p.Cout * 2);
+  // BN backward applied while staging dY (ConvWgradParams::bn_dy): the lane's
+  // 8 channels are fixed, so their coefficients live in registers
+  const bool bnd = p.bn_dy.y != nullptr;
+  const __amdgpu_buffer_rsrc_t rs_by = make_rsrc(bnd ? p.bn_dy.y : p.dy, p.M * p.Cout * 2);
+  BnBwdCoef bc[8];
+  if (bnd) {
+    const float invM = 1.f / float(p.M);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = co0 + dch * 8 + i;
+      bc[i].init(p.bn_dy.mean[c], p.bn_dy.invstd[c], p.bn_dy.w[c], p.bn_dy.b[c], p.bn_dy.dw[c], p.bn_dy.db[c], invM);
+    }
+  }
   constexpr int kDepth = 4;
   struct Stage {
-    uint4 dy;
+    uint4 dy, by;    // by: the BN input chunk (bnd)
     uint2 x0, x1;    // bf16 pixels; u8 input: x0.x / x1.x the raw bytes, x0.y / x1.y in-image flags
   };
   Stage ring[kDepth];
@@ -465,7 +631,9 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4_kernel(ConvWgradParams
   uint32_t dy_byte = uint32_t(md) * uint32_t(p.Cout * 2) + uint32_t((co0 + dch * 8) * 2);
   const uint32_t dy_step = uint32_t(BPX * p.Cout * 2);
   auto load = [&](Stage& r) {
-    r.dy = bload(rs_dy, dy_loader && md < m_end ? dy_byte : kOOB);
+    const uint32_t doff = dy_loader && md < m_end ? dy_byte : kOOB;
+    r.dy = bload(rs_dy, doff);
+    if (bnd) r.by = bload(rs_by, doff);
     const int ih = 2 * c.oh - 1 + kh, iw = 2 * c.ow - 1 + kw;
     const bool row_ok = mx < m_end && unsigned(ih) < unsigned(p.H);
     const int e = ((c.n * p.H + ih) * p.W + iw) * 4;
@@ -483,9 +651,27 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4_kernel(ConvWgradParams
     c.advance(p.Ho, p.Wo);
   };
   const int st_dy = c4dy_off(dpx, dch * 16), st_x = C4_DY_TILE + c4x_off(xpx, xch * 16);
+  const float slope = p.bn_dy.slope;
   auto store = [&](const Stage& r, int buf) {
     char* base = smem + buf * C4_STAGE;
-    if (dy_loader) *reinterpret_cast<uint4*>(base + st_dy) = r.dy;
+    if (dy_loader) {
+      uint4 d = r.dy;
+      if (bnd) {   // gx of the BN from its input (by) and its output gradient (dy)
+        const uint32_t gw[4] = {r.dy.x, r.dy.y, r.dy.z, r.dy.w}, yw[4] = {r.by.x, r.by.y, r.by.z, r.by.w};
+        uint32_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float2 g = make_float2(__uint_as_float(gw[k] << 16), __uint_as_float(gw[k] & 0xFFFF0000u));
+          const float2 v = make_float2(__uint_as_float(yw[k] << 16), __uint_as_float(yw[k] & 0xFFFF0000u));
+          const f32x2 pr = {bc[2 * k].gx(v.x, g.x, slope), bc[2 * k + 1].gx(v.y, g.y, slope)};
+          o[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2));
+        }
+        // a row past the slice loaded zeros for both and gets a nonzero gx: its X
+        // row is past the slice too and staged as zeros, so it adds nothing
+        d = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+      *reinterpret_cast<uint4*>(base + st_dy) = d;
+    }
     if (u8in) {
       const uint2 a = lut_px(lutl, r.x0.x, r.x0.y != 0u), b = lut_px(lutl, r.x1.x, r.x1.y != 0u);
       *reinterpret_cast<uint4*>(base + st_x) = make_uint4(a.x, a.y, b.x, b.y);
@@ -578,6 +764,7 @@ struct TapGemm {
   const uint16_t* lut = nullptr;   // C4 mode: src is raw u8 RGBA, decoded through this bf16 table [4][256]
   int acc_r = 0;                   // forward: > 0 = stats points at a BnAcc accumulator (fp64 [acc_r][2][NOUT])
   BnBwdFuse bn;                    // data gradient only: BN backward statistics in the epilogue (bn.part nullable)
+  int cls_per_block = 1;           // data gradient: parity classes per block (1, or 4 = all; grid.y = 4 / this)
 };
 
 // BN = output channels per block (128 or 64, or 32 for 32-channel outputs
@@ -617,13 +804,34 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
   constexpr int NTAPS = DGRAD ? 4 : 16;
   const int K = C4 ? FBK : NTAPS * p.C, NT = p.NOUT / BN;
-  const int ph = DGRAD ? int(blockIdx.y) >> 1 : 0, pw = DGRAD ? int(blockIdx.y) & 1 : 0;
+  // data gradient: blockIdx.y is one stride-2 parity class (ph, pw), or with
+  // p.cls_per_block == 4 the block runs all four classes of its pixel tile in
+  // turn (the 32-channel layer: 4x fewer, 4x longer blocks -- its 4800
+  // one-class blocks of 16 MFMAs per wave were prologue- and epilogue-bound)
+  const int ncls = DGRAD ? p.cls_per_block : 1;
+  int ph = 0, pw = 0;
 
   const int nwg = int(gridDim.x), b = int(blockIdx.x);
   const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
   const int mt = w / NT, n0 = (w - mt * NT) * BN;
   const int m0 = mt * BM;
+  // epilogue geometry: every thread takes whole 16-byte row chunks -- CPR
+  // chunks per row, RPP rows per pass, NJ rows per thread (for BN = 32 that
+  // is 2 rows of all 256 threads, not 4 rows of half of them)
+  constexpr int CPR = BN / 8, RPP = kThreads / CPR, NJ = BM / RPP;
+  const int ec = t % CPR;
+  const bool bnf = DGRAD && p.bn.part != nullptr;
+  float bs[8], bq[8];   // BN-backward sums (bnf), over every class this block runs
+#pragma unroll
+  for (int q = 0; q < 8; ++q) bs[q] = bq[q] = 0.f;
+  for (int cls_i = 0; cls_i < ncls; ++cls_i) {
+  if constexpr (DGRAD) {
+    const int cls = int(blockIdx.y) * ncls + cls_i;
+    ph = cls >> 1;
+    pw = cls & 1;
+  }
+  if (cls_i > 0) __syncthreads();   // the previous class's epilogue is done with the LDS
 
   // this thread's RJ GEMM rows (staging A, and the epilogue stores): ar + 32j
   const int ar = t >> 3, ac = t & 7;
@@ -941,11 +1149,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     __syncthreads();   // the epilogue reuses the staging LDS
   }
 
-  // Epilogue stores: every thread takes whole 16-byte row chunks -- CPR
-  // chunks per row, RPP rows per pass, NJ rows per thread (for BN = 32 that
-  // is 2 rows of all 256 threads, not 4 rows of half of them).
-  constexpr int CPR = BN / 8, RPP = kThreads / CPR, NJ = BM / RPP;
-  const int ec = t % CPR;
+  // Epilogue stores (geometry above)
   int eob[NJ];
   bool epin[NJ];
   if constexpr (BN == 64) {   // the staging rows ar + 32 j
@@ -984,7 +1188,6 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   }
   // BN-backward fusion (below): issue the BN input loads now, so their
   // latency hides under the epilogue's LDS round trip
-  const bool bnf = DGRAD && p.bn.part != nullptr;
   uint4 xpre[NJ];
   if (bnf) {
 #pragma unroll
@@ -1056,9 +1259,6 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   // over this tile (gz = gy * leaky'(z), z = xhat * w + b, xhat from the BN's
   // saved input at the same offsets) -- the reduction pass over gy and x the
   // BN backward would otherwise make.
-  float bs[8], bq[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) bs[q] = bq[q] = 0.f;
   float is[8], nm[8], ww[8], bb[8];
   if (bnf) {
 #pragma unroll
@@ -1091,6 +1291,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
       }
     }
   }
+  }   // parity classes
   if (bnf) {
     // lanes with the same ec hold the same channels: fold them, then the 4
     // waves through LDS (the statistics area is free in backward)
@@ -1114,11 +1315,14 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
       for (int w4 = 0; w4 < 4; ++w4) v += red[(w4 * 2 + which) * BN + c];
       // channel-major [2][NOUT][rows], row = (pixel tile, parity class); or
       // added into replica row % R of an accumulator [R][2][NOUT] (bn_bwd_apply_acc folds it)
-      const int row = mt * int(gridDim.y) + int(blockIdx.y);
-      if (p.bn.acc_r > 0)
+      const int row = mt * 4 + int(blockIdx.y) * ncls;
+      if (p.bn.acc_r > 0) {
         unsafeAtomicAdd(reinterpret_cast<double*>(p.bn.part) + ((row % p.bn.acc_r) * 2 + which) * p.NOUT + n0 + c,
                         double(v));
-      else p.bn.part[(which * p.NOUT + n0 + c) * p.bn.rows + row] = v;
+      } else {
+        p.bn.part[(which * p.NOUT + n0 + c) * p.bn.rows + row] = v;
+        for (int k = 1; k < ncls; ++k) p.bn.part[(which * p.NOUT + n0 + c) * p.bn.rows + row + k] = 0.f;
+      }
     }
   }
   if (!DGRAD && p.stats && t < 2 * BN) {
@@ -1157,6 +1361,22 @@ __global__ __launch_bounds__(kThreads) void weight_t_kernel(const uint16_t* __re
 
 }  // namespace
 
+namespace {
+// weight-gradient staging: 0 = register ring (conv_wgrad_kernel), 2 / 3 =
+// LDS-DMA stages of 64 pixels (conv_wgrad_dma_kernel); BT_WGRAD_STAGING
+int g_wgrad_staging = -1;
+int wgrad_staging() {
+  if (g_wgrad_staging < 0) {
+    const char* v = std::getenv("BT_WGRAD_STAGING");
+    const int e = v ? std::atoi(v) : 2;
+    g_wgrad_staging = e == 0 || e == 2 || e == 3 ? e : 2;
+  }
+  return g_wgrad_staging;
+}
+}  // namespace
+
+void conv_set_wgrad_staging(int staging) { g_wgrad_staging = staging == 0 || staging == 2 || staging == 3 ? staging : -1; }
+
 bool conv_wgrad_supported(int Cin, int Cout) {
   return (Cin >= 32 && Cin % 32 == 0 && Cout >= 64 && Cout % 64 == 0) || (Cin == 4 && Cout % 32 == 0 && Cout > 0);
 }
@@ -1187,6 +1407,9 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
     return hipErrorInvalidValue;
   if ((reinterpret_cast<uintptr_t>(p.x) | reinterpret_cast<uintptr_t>(p.dy)) & 15) return hipErrorInvalidValue;
   if (p.lut && (p.Cin != 4 || (reinterpret_cast<uintptr_t>(p.lut) & 7))) return hipErrorInvalidValue;
+  if (p.bn_dy.y && (p.Cin != 4 || (reinterpret_cast<uintptr_t>(p.bn_dy.y) & 15) || !p.bn_dy.mean || !p.bn_dy.invstd ||
+                    !p.bn_dy.w || !p.bn_dy.b || !p.bn_dy.dw || !p.bn_dy.db))
+    return hipErrorInvalidValue;   // the 4-channel first layer's kernel only
   if (int64_t(p.N) * p.H * p.W * p.Cin * 2 >= int64_t(kOOB) || p.M * p.Cout * 2 >= int64_t(kOOB))
     return hipErrorInvalidValue;   // 32-bit buffer offsets
   const bool c4 = p.Cin == 4;
@@ -1213,6 +1436,10 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
     grid += 1;
   }
   if (c4) conv_wgrad_c4_kernel<<<unsigned(grid), kThreads, 0, stream>>>(q);
+  else if (wgrad_staging() == 2 && (p.Cin & (p.Cin - 1)) == 0 && p.Wo >= 32)
+    conv_wgrad_dma_kernel<2><<<unsigned(grid), kThreads, 0, stream>>>(q);
+  else if (wgrad_staging() == 3 && (p.Cin & (p.Cin - 1)) == 0 && p.Wo >= 32)
+    conv_wgrad_dma_kernel<3><<<unsigned(grid), kThreads, 0, stream>>>(q);
   else conv_wgrad_kernel<<<unsigned(grid), kThreads, 0, stream>>>(q);
   const int64_t total = int64_t(p.Cout) * 16 * p.Cin;   // partial elements per slice
   ConvWgradParams::Reduce r;
@@ -1249,7 +1476,7 @@ namespace {
 template <bool DGRAD, int BM, int NST>
 void launch_tap_gemm_bm(const TapGemm& g, int bn, unsigned ytiles, hipStream_t stream) {
   const int64_t blocks = (g.M + BM - 1) / BM * (g.NOUT / bn);
-  const dim3 grid(unsigned(blocks), ytiles);
+  const dim3 grid(unsigned(blocks), ytiles / unsigned(DGRAD ? g.cls_per_block : 1));
   if (!DGRAD && g.C == 4) {
     if (bn == 64) tap_gemm_kernel<false, 64, true, BM><<<grid, kThreads, 0, stream>>>(g);
     else tap_gemm_kernel<false, 32, true, BM><<<grid, kThreads, 0, stream>>>(g);
@@ -1297,12 +1524,23 @@ int env_int(const char* name) {
 }
 int g_force_bm = env_int("BT_CONV_BM");
 int g_force_bn = env_int("BT_CONV_BN");
+int g_dgrad_cls = env_int("BT_CONV_DGRAD_CLS");   // 1 / 4: force the data gradient's classes per block
 }  // namespace
 
-void conv_set_tiles(int bm, int bn, int staging) {
+int conv_dgrad_classes_per_block(int64_t M, int NOUT) {
+  // one parity class per block unless that makes >= 4096 blocks (the
+  // 32-channel layer: 4800); then a block runs all four (1200 blocks)
+  if (g_dgrad_cls == 1 || g_dgrad_cls == 4) return g_dgrad_cls;
+  const int bm = conv_tile_pixels(M, NOUT, 4);
+  const int64_t blocks = (M + bm - 1) / bm * (NOUT / conv_tile_channels(NOUT, false)) * 4;
+  return blocks >= 4096 ? 4 : 1;
+}
+
+void conv_set_tiles(int bm, int bn, int staging, int dgrad_cls) {
   g_force_bm = bm == 64 || bm == 128 ? bm : 0;
   g_force_bn = bn == 32 || bn == 64 || bn == 128 ? bn : 0;
   g_staging = staging == 0 || staging == 2 || staging == 3 ? staging : -1;
+  g_dgrad_cls = dgrad_cls == 1 || dgrad_cls == 4 ? dgrad_cls : 0;
 }
 
 int conv_tile_channels(int NOUT, bool c4) {
@@ -1395,6 +1633,7 @@ hipError_t conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int 
       return hipErrorInvalidValue;
     g.bn = *bn;
   }
+  g.cls_per_block = conv_dgrad_classes_per_block(g.M, g.NOUT);
   launch_tap_gemm<true>(g, 4, stream);
   return hipGetLastError();
 }

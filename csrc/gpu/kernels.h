@@ -337,10 +337,29 @@ struct ConvWgradParams {
     float* dw = nullptr;
     float* db = nullptr;
   } fold;
+  // bn_dy.y != nullptr (the 4-channel first layer only): dy is NOT the
+  // convolution's output gradient but the gradient of the BatchNorm +
+  // LeakyReLU that follows it, whose input is bn_dy.y ([M][Cout] bf16); the
+  // kernel applies that BN's backward while staging dY (bn_fold.h BnBwdCoef,
+  // bit-identical to bn_bwd_apply), so no bn_bwd_apply pass runs.  dw / db:
+  // the BN's folded backward sums (db = sum gz, dw = sum gz * xhat).
+  struct BnDy {
+    const uint16_t* y = nullptr;
+    const float* mean = nullptr;
+    const float* invstd = nullptr;
+    const float* w = nullptr;
+    const float* b = nullptr;
+    const float* dw = nullptr;
+    const float* db = nullptr;
+    float slope = 0.f;
+  } bn_dy;
 };
 // Cin % 32 == 0 with Cout % 64 == 0, or Cin == 4 (the first layer) with Cout % 32 == 0.
 bool conv_wgrad_supported(int Cin, int Cout);
 int conv_wgrad_slices(int64_t M, int Cin, int Cout, int target_blocks);
+// Weight-gradient staging (not the 4-channel layer): 0 = register ring,
+// 2 / 3 = LDS-DMA stages of 64 pixels (default 2; -1 = BT_WGRAD_STAGING or default).
+void conv_set_wgrad_staging(int staging);
 // The slice reduce normally follows the main kernel as its own launch.
 // defer != nullptr: it is NOT launched but described in *defer, for the
 // next conv_wgrad to run as extra blocks of its own launch (`side`; the
@@ -384,7 +403,10 @@ int conv_tile_channels(int NOUT, bool first_layer);
 // BT_CONV_STAGING).
 // Row counts of the statistics buffers follow the tile size: change it only
 // between steps, never between sizing a buffer and the launch that fills it.
-void conv_set_tiles(int bm, int bn, int staging = -1);
+void conv_set_tiles(int bm, int bn, int staging = -1, int dgrad_cls = 0);
+// Parity classes per data-gradient block (1, or 4 when one class per block
+// would give >= 4096 blocks; BT_CONV_DGRAD_CLS / conv_set_tiles force it).
+int conv_dgrad_classes_per_block(int64_t M, int NOUT);
 hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream);
 // Data gradient of the same convolution (same tap-gather GEMM kernel, four
 // stride-2 parity classes in one launch): dy [N][H/2][W/2][Cout] bf16,

@@ -239,9 +239,22 @@ PYBIND11_MODULE(_hip, m) {
   m.def("conv_wgrad",
         [](uintptr_t x, uintptr_t dy, uintptr_t partial, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
            int slices, int64_t px_per_slice, uintptr_t out, int64_t s_co, int64_t s_ci, int64_t s_kh, int64_t s_kw,
-           uintptr_t stream, int cin_out, bool defer, py::object side, uintptr_t lut, py::object fold) -> py::object {
+           uintptr_t stream, int cin_out, bool defer, py::object side, uintptr_t lut, py::object fold,
+           py::object bn_dy) -> py::object {
           ConvWgradParams p;
           p.cin_out = cin_out;
+          if (!bn_dy.is_none()) {   // (y, mean, invstd, w, b, dw, db, slope)
+            const py::tuple f = bn_dy.cast<py::tuple>();
+            if (f.size() != 8) throw std::invalid_argument("conv_wgrad: bn_dy is (y, mean, invstd, w, b, dw, db, slope)");
+            p.bn_dy.y = ptr<const uint16_t>(f[0].cast<uintptr_t>());
+            p.bn_dy.mean = ptr<const float>(f[1].cast<uintptr_t>());
+            p.bn_dy.invstd = ptr<const float>(f[2].cast<uintptr_t>());
+            p.bn_dy.w = ptr<const float>(f[3].cast<uintptr_t>());
+            p.bn_dy.b = ptr<const float>(f[4].cast<uintptr_t>());
+            p.bn_dy.dw = ptr<const float>(f[5].cast<uintptr_t>());
+            p.bn_dy.db = ptr<const float>(f[6].cast<uintptr_t>());
+            p.bn_dy.slope = f[7].cast<float>();
+          }
           if (!fold.is_none()) {   // (acc, R, C, M, dw, db)
             const py::tuple f = fold.cast<py::tuple>();
             if (f.size() != 6) throw std::invalid_argument("conv_wgrad: fold is (acc, R, C, M, dw, db)");
@@ -270,14 +283,18 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("x"), py::arg("dy"), py::arg("partial"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("Cin"),
         py::arg("Ho"), py::arg("Wo"), py::arg("Cout"), py::arg("slices"), py::arg("px_per_slice"), py::arg("out"),
         py::arg("s_co"), py::arg("s_ci"), py::arg("s_kh"), py::arg("s_kw"), py::arg("stream"), py::arg("cin_out") = 0,
-        py::arg("defer") = false, py::arg("side") = py::none(), py::arg("lut") = 0, py::arg("fold") = py::none());
+        py::arg("defer") = false, py::arg("side") = py::none(), py::arg("lut") = 0, py::arg("fold") = py::none(),
+        py::arg("bn_dy") = py::none());
   // a deferred slice reduce on its own (a weight-gradient chain that ended early)
   m.def("conv_wgrad_reduce", [](py::tuple r, uintptr_t stream) {
     check(conv_wgrad_reduce(reduce_from_tuple(r), stream_of(stream)), "conv_wgrad_reduce");
   });
 
   m.def("conv_fwd_tiles", &conv_fwd_tiles);
-  m.def("conv_set_tiles", &conv_set_tiles, py::arg("bm") = 0, py::arg("bn") = 0, py::arg("staging") = -1);
+  m.def("conv_set_tiles", &conv_set_tiles, py::arg("bm") = 0, py::arg("bn") = 0, py::arg("staging") = -1,
+        py::arg("dgrad_cls") = 0);
+  m.def("conv_dgrad_classes_per_block", &conv_dgrad_classes_per_block);
+  m.def("conv_set_wgrad_staging", &conv_set_wgrad_staging);
   m.def("conv_tile_pixels", &conv_tile_pixels);
   m.def("conv_tile_channels", &conv_tile_channels);
   m.def("conv_dgrad_supported", &conv_dgrad_supported);

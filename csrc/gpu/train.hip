@@ -339,14 +339,28 @@ __global__ __launch_bounds__(kBlock) void bn_acc_finalize_kernel(double* __restr
   bn_fold_block(f, part);
 }
 
-template <int DT, bool BWD>
+// FOLD: the coefficients come from the BnAcc accumulator the producer added
+// into, folded by every block itself (bn_fold.h: bn_acc_column_sums /
+// bn_acc_release) -- no finalize launch before the apply.
+struct BnApplyFold {
+  double* acc = nullptr;
+  int R = 0;
+  float eps = 0.f, momentum = 0.f;
+  float* o0 = nullptr;         // forward: mean; backward: db  (block 0 writes)
+  float* o1 = nullptr;         // forward: invstd; backward: dw
+  float* rm = nullptr;         // forward: running statistics, num_batches_tracked
+  float* rv = nullptr;
+  int64_t* tracked = nullptr;
+};
+
+template <int DT, bool BWD, bool FOLD = false>
 __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const void* __restrict__ x, const void* __restrict__ gy,
                                                           void* __restrict__ out, int64_t M, int C,
                                                           const float* __restrict__ mean,
                                                           const float* __restrict__ invstd,
                                                           const float* __restrict__ w, const float* __restrict__ b,
                                                           const float* __restrict__ dw, const float* __restrict__ db,
-                                                          float slope) {
+                                                          float slope, BnApplyFold fa = BnApplyFold()) {
   constexpr int V = BnVec<DT>::V, U = kBnUnroll;
   const int G = C / V;
   const int64_t total = M * G;
@@ -367,29 +381,68 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const void* __restrict
   };
   bool have = idx + (U - 1) * kBlock < total;   // a whole pass: U vectors per lane
   if (have) load_pass();
-  // xhat = v * is + nm;  z = xhat * ww + bb;  backward: gx = P * (gz - dbm) - pdw * xhat
-  float is[V], nm[V], ww[V], bb[V], P[V], dbm[V], pdw[V];
+  // xhat = v * is + nm;  z = xhat * ww + bb;  backward: gx = P * (gz - dbm) - pdw * xhat (BnBwdCoef)
+  float is[V], nm[V], ww[V], bb[V];
+  BnBwdCoef bc[BWD ? V : 1];
+  const float* s_mean = mean;
+  const float* s_inv = invstd;
+  const float* s_db = db;
+  const float* s_dw = dw;
+  if constexpr (FOLD) {
+    __shared__ double part[2 * kBnAccMaxC > kBlock ? 2 * kBnAccMaxC : kBlock];
+    __shared__ float coef[2 * kBnAccMaxC];
+    __shared__ int flag;
+    bn_acc_column_sums(fa.acc, fa.R, 2 * C, part);
+    const bool first = blockIdx.x == 0;
+    for (int c = int(threadIdx.x); c < C; c += kBlock) {
+      if constexpr (BWD) {   // db = sum gz, dw = sum gz * xhat (bn_fold_block, bwd)
+        coef[c] = float(part[c]);
+        coef[C + c] = float(part[C + c]);
+        if (first) fa.o0[c] = coef[c], fa.o1[c] = coef[C + c];
+      } else {               // exactly bn_fold_block's forward finalize
+        const double mu = part[c] / double(M);
+        double var = part[C + c] / double(M) - mu * mu;
+        var = var < 0.0 ? 0.0 : var;
+        coef[c] = float(mu);
+        coef[C + c] = float(1.0 / sqrt(var + double(fa.eps)));
+        if (first) {
+          fa.o0[c] = coef[c];
+          fa.o1[c] = coef[C + c];
+          if (fa.rm) {
+            fa.rm[c] = float((1.0 - fa.momentum) * fa.rm[c] + fa.momentum * mu);
+            fa.rv[c] = float((1.0 - fa.momentum) * fa.rv[c] +
+                             fa.momentum * var * double(M) / double(M > 1 ? M - 1 : 1));
+          }
+          if (fa.tracked && c == 0) fa.tracked[0] += 1;
+        }
+      }
+    }
+    __syncthreads();
+    bn_acc_release(fa.acc, fa.R, C, &flag);
+    if constexpr (BWD) {
+      s_db = coef;
+      s_dw = coef + C;
+    } else {
+      s_mean = coef;
+      s_inv = coef + C;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < V; ++i) {
     const int c = c0 + i;
-    is[i] = invstd[c];
-    nm[i] = -mean[c] * is[i];
-    ww[i] = w[c];
-    bb[i] = b[c];
     if constexpr (BWD) {
-      P[i] = ww[i] * is[i];
-      dbm[i] = db[c] * invM;
-      pdw[i] = P[i] * dw[c] * invM;
+      bc[i].init(s_mean[c], s_inv[c], w[c], b[c], s_dw[c], s_db[c], invM);
+    } else {
+      is[i] = s_inv[c];
+      nm[i] = -s_mean[c] * is[i];
+      ww[i] = w[c];
+      bb[i] = b[c];
     }
   }
   auto apply = [&](const float (&v)[V], const float (&gv)[V], float (&o)[V]) {
     if constexpr (BWD) {
 #pragma unroll
-      for (int i = 0; i < V; ++i) {
-        const float xh = fmaf(v[i], is[i], nm[i]);
-        const float gz = fmaf(xh, ww[i], bb[i]) > 0.f ? gv[i] : gv[i] * slope;
-        o[i] = fmaf(P[i], gz - dbm[i], -pdw[i] * xh);
-      }
+      for (int i = 0; i < V; ++i) o[i] = bc[i].gx(v[i], gv[i], slope);
     } else {
 #pragma unroll
       for (int i = 0; i < V; ++i) {
@@ -436,6 +489,13 @@ void bn_blocks(int64_t M, int C, int dtype, int& nblocks, int64_t& rows_per_bloc
 int bn_grid(int64_t work) {   // work = 16-byte vectors; kBnUnroll per lane per pass
   const int64_t blocks = (work + kBlock * kBnUnroll - 1) / (kBlock * kBnUnroll);
   return int(blocks < 4096 ? (blocks < 1 ? 1 : blocks) : 4096);
+}
+
+// apply launches that fold their accumulator: every block reads the 16 KB of
+// replicas once, so fewer, longer-running blocks (4 per CU)
+int bn_fold_grid(int64_t work) {
+  const int g = bn_grid(work);
+  return g < 1024 ? g : 1024;
 }
 }  // namespace
 
@@ -536,8 +596,9 @@ int bn_acc_replicas(int C) {
 }
 
 int64_t bn_acc_elems(int C) {
+  // [R][2][C] replicas + one double's room for the apply launches' ticket word (bn_fold.h)
   const int r = bn_acc_replicas(C);
-  return r > 0 ? int64_t(2) * C * r : -1;
+  return r > 0 ? int64_t(2) * C * r + 1 : -1;
 }
 
 hipError_t bn_apply_acc(const void* x, void* y, int64_t M, int C, int dtype, BnAcc acc, float eps, float momentum,
@@ -545,9 +606,19 @@ hipError_t bn_apply_acc(const void* x, void* y, int64_t M, int C, int dtype, BnA
                         const float* w, const float* b, float slope, hipStream_t stream) {
   if (!bn_shape_ok(M, C, dtype) || !acc.acc || acc.R != bn_acc_replicas(C) || !mean || !invstd || !w || !b)
     return hipErrorInvalidValue;
-  bn_acc_finalize_kernel<false><<<1, kBlock, 0, stream>>>(acc.acc, acc.R, M, C, eps, momentum, mean, invstd,
-                                                          running_mean, running_var, tracked);
-  return bn_apply(x, y, M, C, dtype, mean, invstd, w, b, slope, stream);
+  // every apply block folds the accumulator itself (bn_fold.h): no finalize launch
+  BnApplyFold fa;
+  fa.acc = acc.acc, fa.R = acc.R, fa.eps = eps, fa.momentum = momentum;
+  fa.o0 = mean, fa.o1 = invstd, fa.rm = running_mean, fa.rv = running_var, fa.tracked = tracked;
+  const int V = dtype == OUT_BF16 ? 8 : 4;
+  const int grid = bn_fold_grid(M * (C / V));
+  if (dtype == OUT_BF16)
+    bn_apply_kernel<OUT_BF16, false, true><<<grid, kBlock, 0, stream>>>(x, nullptr, y, M, C, nullptr, nullptr, w, b,
+                                                                        nullptr, nullptr, slope, fa);
+  else
+    bn_apply_kernel<OUT_F32, false, true><<<grid, kBlock, 0, stream>>>(x, nullptr, y, M, C, nullptr, nullptr, w, b,
+                                                                       nullptr, nullptr, slope, fa);
+  return hipGetLastError();
 }
 
 hipError_t bn_bwd_apply_acc(const void* x, const void* gy, void* gx, int64_t M, int C, int dtype, BnAcc acc,
@@ -556,9 +627,17 @@ hipError_t bn_bwd_apply_acc(const void* x, const void* gy, void* gx, int64_t M, 
   if (!bn_shape_ok(M, C, dtype) || !acc.acc || acc.R != bn_acc_replicas(C) || !mean || !invstd || !w || !b || !dw ||
       !db)
     return hipErrorInvalidValue;
-  bn_acc_finalize_kernel<true><<<1, kBlock, 0, stream>>>(acc.acc, acc.R, M, C, 0.f, 0.f, db, dw, nullptr, nullptr,
-                                                         nullptr);
-  return bn_bwd_apply(x, gy, gx, M, C, dtype, mean, invstd, w, b, dw, db, slope, stream);
+  BnApplyFold fa;
+  fa.acc = acc.acc, fa.R = acc.R, fa.o0 = db, fa.o1 = dw;
+  const int V = dtype == OUT_BF16 ? 8 : 4;
+  const int grid = bn_fold_grid(M * (C / V));
+  if (dtype == OUT_BF16)
+    bn_apply_kernel<OUT_BF16, true, true><<<grid, kBlock, 0, stream>>>(x, gy, gx, M, C, mean, invstd, w, b, nullptr,
+                                                                       nullptr, slope, fa);
+  else
+    bn_apply_kernel<OUT_F32, true, true><<<grid, kBlock, 0, stream>>>(x, gy, gx, M, C, mean, invstd, w, b, nullptr,
+                                                                      nullptr, slope, fa);
+  return hipGetLastError();
 }
 
 hipError_t bn_bwd_reduce_acc(const void* x, const void* gy, int64_t M, int C, int dtype, const float* mean,

@@ -33,6 +33,11 @@ def _weights_init(m):
 class Discriminator(nn.Module):
     """DCGAN discriminator: N x nc x H x W -> N probabilities."""
 
+    # bf16 path with raw u8 frames (decode fused into the first conv): the first
+    # BN's backward apply runs inside the first conv's weight-gradient kernel
+    # (ops.BnDeferred); False keeps the separate apply launch (A/B, tests)
+    defer_first_bn = True
+
     def __init__(self, nc=3, ndf=32, adaptive=False, fused=True):
         super().__init__()
         from .. import ops
@@ -162,7 +167,7 @@ class Discriminator(nn.Module):
             if need:
                 wts = dict(zip(need, ops.conv_weights_t([w16s[k] for k in need])))
         ci = -1
-        stats = link = None
+        stats = link = defer = None
         # the MFMA weight gradients of one backward hand their slice reduce to the
         # next one (ops.WgradChain): the first such layer's runs last and closes it
         wchain = ops.WgradChain() if (mfma and torch.is_grad_enabled() and x.is_cuda) else None
@@ -193,6 +198,10 @@ class Discriminator(nn.Module):
                     wk = dict(wt=wts.get(ci), bn_link=bl, wchain=wchain, wlast=closes)
                     if ci == 0 and lut is not None:
                         wk['lut'] = lut    # raw u8 frames: decoded in this layer's kernels
+                        if fuse and torch.is_grad_enabled() and self.defer_first_bn:
+                            # no data gradient here: the following BN's backward apply runs
+                            # inside this layer's weight-gradient kernel (ops.BnDeferred)
+                            defer = wk['bn_out'] = ops.BnDeferred()
                     if closes:
                         first_mfma = False
                     if fuse and ops.bn_acc_supported(m.out_channels):
@@ -211,8 +220,8 @@ class Discriminator(nn.Module):
                     x = F.conv2d(x, w16, None, m.stride, m.padding, m.dilation, m.groups)
             elif stats is not None and isinstance(m, ops.BatchNormLeakyReLU2d):
                 link = ops.BnLink() if torch.is_grad_enabled() else None
-                x = m.forward_from_stats(x, stats, link)
-                stats = None
+                x = m.forward_from_stats(x, stats, link, defer)
+                stats = defer = None
             else:
                 if not isinstance(m, nn.Identity):
                     link = None

@@ -686,6 +686,23 @@ def _pool_module():
 # gradient sinks: parameters whose gradient lives in a persistent flat bucket
 # (parallel.GradBuckets) get it written there by the backward kernel itself
 
+# Gradient-completion listener (parallel.GradBuckets.arm): called with a
+# parameter right after the launch that writes its bucket-view gradient for
+# the last time in this backward is enqueued, so a data-parallel step can
+# enqueue a bucket's all-reduce as soon as every gradient in it is written,
+# ahead of the rest of the backward.  _GRAD_LATE is called when a parameter
+# whose bucket view was already written gets another contribution.
+_GRAD_DONE = None
+_GRAD_LATE = None
+
+
+def _grad_done(*params):
+    if _GRAD_DONE is not None:
+        for p in params:
+            if p is not None:
+                _GRAD_DONE(p)
+
+
 def grad_sink(param):
     """The persistent gradient view of ``param`` installed by
     ``parallel.GradBuckets`` (same shape and strides), or None."""
@@ -706,6 +723,8 @@ def _grad_dest(param, like=None):
     if sink is not None and param.grad is sink and getattr(param, '_bt_grad_fresh', False):
         param._bt_grad_fresh = False
         return sink, True
+    if sink is not None and _GRAD_LATE is not None:
+        _GRAD_LATE(param)
     return torch.empty_like(param if like is None else like), False
 
 
@@ -859,13 +878,35 @@ class BnLink:
         return part, rows
 
 
+class BnDeferred:
+    """Hand-off of a BatchNorm+LeakyReLU backward to the 4-channel first
+    convolution that produced the BN's input (:func:`conv4x4s2` ``bn_out=``).
+
+    That convolution's input is the frames (no data gradient), so the BN's
+    input gradient gx feeds nothing but its weight-gradient kernel, which
+    can compute gx itself while staging it (``conv_wgrad(bn_dy=)``): the BN
+    backward then skips its apply pass -- one read of the activation and of
+    its gradient and one write fewer -- and passes its output gradient on.
+    ``armed``: set by the convolution (it accepts the hand-off); ``pending``:
+    the BN's saved tensors and folded sums, set by its backward, taken once."""
+    __slots__ = ('armed', 'pending')
+
+    def __init__(self):
+        self.armed = False
+        self.pending = None
+
+    def take(self):
+        p, self.pending = self.pending, None
+        return p
+
+
 def _bn_function():
     import torch
 
     class _BatchNormLeakyReLU(torch.autograd.Function):
         @staticmethod
         def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, slope, tracked=None,
-                    stats=None, link=None):
+                    stats=None, link=None, defer=None):
             ext = hip_ext()
             N, C, H, W = x.shape
             M = N * H * W
@@ -902,6 +943,7 @@ def _bn_function():
             ctx.save_for_backward(xs, w, b, mean, invstd)
             ctx.slope = float(slope)
             ctx.link = link
+            ctx.defer = defer if (defer is not None and defer.armed and dt == OUT_DTYPES['bfloat16']) else None
             ctx.params = (weight, bias)
             ctx.acc = stats if isinstance(stats, BnAccumulator) else None
             if link is not None:
@@ -922,12 +964,6 @@ def _bn_function():
             dt = _dt(xs)
             gys = _as_nhwc(gy if gy.dtype == xs.dtype else gy.to(xs.dtype))
             gx = torch.empty_like(xs)
-            dw, w_sunk = _grad_dest(ctx.params[0], w)
-            db, b_sunk = _grad_dest(ctx.params[1], b)
-            if dw.dtype != torch.float32 or not dw.is_contiguous():
-                dw, w_sunk = torch.empty_like(w), False
-            if db.dtype != torch.float32 or not db.is_contiguous():
-                db, b_sunk = torch.empty_like(b), False
             lk = ctx.link
             folded = lk is not None and lk.folded
             part, rows = lk.take(gys) if lk is not None else (None, 0)
@@ -936,16 +972,30 @@ def _bn_function():
                 _count('bn_backward_from_stats')
                 _count('bn_backward_acc')
                 _count('bn_backward_folded')
-                ext.bn_bwd_apply(xs.data_ptr(), gys.data_ptr(), gx.data_ptr(), M, C, dt, mean.data_ptr(),
-                                 invstd.data_ptr(), w.data_ptr(), b.data_ptr(), lk.dw.data_ptr(), lk.db.data_ptr(),
-                                 ctx.slope, _stream(xs.device))
                 out_w = None if lk.dw_sunk else lk.dw
                 out_b = None if lk.db_sunk else lk.db
+                if ctx.defer is not None:
+                    # the producing first convolution applies this backward while it
+                    # stages its weight gradient's dY (BnDeferred): pass gy on unchanged
+                    _count('bn_backward_deferred')
+                    ctx.defer.pending = (xs, mean, invstd, w, b, lk.dw, lk.db, ctx.slope)
+                    gx = gys
+                else:
+                    ext.bn_bwd_apply(xs.data_ptr(), gys.data_ptr(), gx.data_ptr(), M, C, dt, mean.data_ptr(),
+                                     invstd.data_ptr(), w.data_ptr(), b.data_ptr(), lk.dw.data_ptr(),
+                                     lk.db.data_ptr(), ctx.slope, _stream(xs.device))
                 lk.dw = lk.db = None
                 lk.folded = False
-                return (gx.permute(0, 3, 1, 2), out_w, out_b, None, None, None, None, None, None, None, None)
+                return (gx.permute(0, 3, 1, 2), out_w, out_b, None, None, None, None, None, None, None, None, None)
             if folded:
                 raise RuntimeError('BatchNormLeakyReLU2d: its statistics were folded for another gradient')
+            # (not before the folded branch: the fold already took the bucket views)
+            dw, w_sunk = _grad_dest(ctx.params[0], w)
+            db, b_sunk = _grad_dest(ctx.params[1], b)
+            if dw.dtype != torch.float32 or not dw.is_contiguous():
+                dw, w_sunk = torch.empty_like(w), False
+            if db.dtype != torch.float32 or not db.is_contiguous():
+                db, b_sunk = torch.empty_like(b), False
             if ctx.acc is not None and (part is None or rows < 0):
                 # accumulator mode: the consuming conv's dgrad epilogue summed into
                 # acc.bwd (part), or this launch reduces into it first
@@ -966,8 +1016,9 @@ def _bn_function():
                 ext.bn_backward(xs.data_ptr(), gys.data_ptr(), gx.data_ptr(), M, C, dt, part.data_ptr(),
                                 mean.data_ptr(), invstd.data_ptr(), w.data_ptr(), b.data_ptr(), dw.data_ptr(),
                                 db.data_ptr(), ctx.slope, _stream(xs.device))
+            _grad_done(ctx.params[0] if w_sunk else None, ctx.params[1] if b_sunk else None)
             return (gx.permute(0, 3, 1, 2), None if w_sunk else dw, None if b_sunk else db,
-                    None, None, None, None, None, None, None, None)
+                    None, None, None, None, None, None, None, None, None)
 
     return _BatchNormLeakyReLU
 
@@ -1004,8 +1055,9 @@ def batch_norm_leaky_relu(x, weight, bias, running_mean=None, running_var=None, 
 
 
 def _bn_apply_unchecked(x, weight, bias, running_mean, running_var, eps, momentum, slope, tracked=None,
-                        stats=None, link=None):
-    return _BN_FN.apply(x, weight, bias, running_mean, running_var, eps, momentum, slope, tracked, stats, link)
+                        stats=None, link=None, defer=None):
+    return _BN_FN.apply(x, weight, bias, running_mean, running_var, eps, momentum, slope, tracked, stats, link,
+                        defer)
 
 
 def reference_batch_norm_leaky_relu(x, weight, bias, running_mean=None, running_var=None, eps=1e-5, momentum=0.1,
@@ -1062,19 +1114,21 @@ def _bn_module():
             ring[1] = (i + 1) % len(accs)
             return accs[i]
 
-        def forward_from_stats(self, x, stats, link=None):
+        def forward_from_stats(self, x, stats, link=None, defer=None):
             """Training forward with the batch statistics already summed by
             the producing kernel (``conv_fwd``'s epilogue rows, see
             :func:`conv4x4s2`, or a :class:`BnAccumulator` it added into:
             then one apply launch folds them): finalize + apply only.  ``link``: a
             :class:`BnLink` shared with the convolution that consumes the
             output (its data-gradient epilogue then does this op's backward
-            reduction)."""
+            reduction).  ``defer``: a :class:`BnDeferred` armed by the first
+            convolution that produced ``x`` (it then applies this op's
+            backward itself)."""
             global _BN_FN
             if _BN_FN is None:
                 _BN_FN = _bn_function()
             return _bn_apply_unchecked(x, self.weight, self.bias, self.running_mean, self.running_var, self.eps,
-                                       self.momentum, self.slope, self.num_batches_tracked, stats, link)
+                                       self.momentum, self.slope, self.num_batches_tracked, stats, link, defer)
 
         def extra_repr(self):
             return super().extra_repr() + f', slope={self.slope}'
@@ -1126,19 +1180,22 @@ class WgradChain:
     marked ``last`` runs its own (and the one handed to it) -- one reduce
     launch per chain instead of one per layer.  ``flush()`` runs a reduce
     left pending (a chain that ended before its ``last`` call)."""
-    __slots__ = ('pending', 'keep')
+    __slots__ = ('pending', 'keep', 'param')
 
     def __init__(self):
         self.pending = None   # the deferred reduce (ext tuple)
         self.keep = None      # its partial scratch and output, alive until run
+        self.param = None     # the parameter whose (bucket-view) gradient it completes
 
     def flush(self, device):
         if self.pending is not None:
             hip_ext().conv_wgrad_reduce(self.pending, _stream(device))
-            self.pending = self.keep = None
+            _grad_done(self.param)
+            self.pending = self.keep = self.param = None
 
 
-def conv_wgrad(x, dy, out, target_blocks=None, chain=None, last=True, lut=None, fold=None):
+def conv_wgrad(x, dy, out, target_blocks=None, chain=None, last=True, lut=None, fold=None, bn_dy=None, param=None,
+               fold_params=()):
     """fp32 weight gradient of a 4x4/s2/p1 convolution into ``out`` ([Cout, Cin,
     4, 4], any strides): MFMA tiles over pixel slices + one slice-reduce
     launch.  ``x`` [N, Cin, H, W] and ``dy`` [N, Cout, H/2, W/2] are bf16 with
@@ -1146,7 +1203,13 @@ def conv_wgrad(x, dy, out, target_blocks=None, chain=None, last=True, lut=None, 
     pending reduce inside this launch, and leave this layer's to the next
     call unless ``last`` -- ``out`` is then complete only after that call.
     ``lut``: ``x`` is raw u8 RGBA frames read through this decode table
-    (:func:`decode_lut_bf16`)."""
+    (:func:`decode_lut_bf16`).  ``bn_dy`` (4-channel first layer): ``dy`` is
+    the output gradient of the BatchNorm+LeakyReLU that follows this
+    convolution and ``bn_dy`` that BN's ``(x, mean, invstd, w, b, dw, db,
+    slope)`` (:class:`BnDeferred`): the kernel applies the BN backward to
+    ``dy`` while staging it.  ``param`` / ``fold_params``: the parameters
+    whose bucket-view gradients ``out`` / the fold complete (reported to
+    the gradient-completion listener once their launch is enqueued)."""
     import torch
     ext = hip_ext()
     N, Cin, H, W = x.shape
@@ -1172,15 +1235,31 @@ def conv_wgrad(x, dy, out, target_blocks=None, chain=None, last=True, lut=None, 
     defer = chain is not None and not last
     if (lut is not None) != (x.dtype == torch.uint8) or (lut is not None and Cin != 4):
         raise ValueError('conv_wgrad: u8 input (4 channels) needs its decode table lut, and only u8 takes one')
+    bnt = None
+    if bn_dy is not None:
+        by, bmean, binv, bw, bb, bdw, bdb, bslope = bn_dy
+        if Cin != 4 or tuple(by.shape) != (N, Ho, Wo, Cout) or by.dtype != torch.bfloat16 or not by.is_contiguous():
+            raise ValueError('conv_wgrad(bn_dy=): the 4-channel first layer, BN input [N, Ho, Wo, Cout] bf16 NHWC')
+        for t in (bmean, binv, bw, bb, bdw, bdb):
+            if t.dtype != torch.float32 or t.numel() != Cout or not t.is_contiguous():
+                raise ValueError('conv_wgrad(bn_dy=): fp32 [Cout] BN statistics / parameters / sums')
+        _count('conv_wgrad_bn_dy')
+        bnt = (by.data_ptr(), bmean.data_ptr(), binv.data_ptr(), bw.data_ptr(), bb.data_ptr(), bdw.data_ptr(),
+               bdb.data_ptr(), float(bslope))
     res = ext.conv_wgrad(x.data_ptr(), dy.data_ptr(), partial.data_ptr(), N, H, W, Cin, Ho, Wo, Cout, slices, px,
                          out.data_ptr(), out.stride(0), out.stride(1), out.stride(2), out.stride(3), _stream(x.device),
-                         cin_out, defer, side, lut.data_ptr() if lut is not None else 0, fold)
+                         cin_out, defer, side, lut.data_ptr() if lut is not None else 0, fold, bnt)
     if fold is not None:
         _count('conv_wgrad_bn_fold')
+        _grad_done(*fold_params)
     if chain is not None:
         if side is not None:
             _count('conv_wgrad_side_reduce')
+            _grad_done(chain.param)
         chain.pending, chain.keep = (res, (partial, out)) if defer else (None, None)
+        chain.param = param if defer else None
+    if not defer:
+        _grad_done(param)
     return out
 
 
@@ -1309,13 +1388,14 @@ def conv_fwd_stats_rows(M, Cout):
     return int(hip_ext().conv_fwd_tiles(int(M), int(Cout)))
 
 
-def conv_set_tiles(bm=0, bn=0, staging=-1):
+def conv_set_tiles(bm=0, bn=0, staging=-1, dgrad_cls=0):
     """Force the tap-GEMM tile: ``bm`` pixels (64/128) by ``bn`` output
-    channels (32/64/128), and its staging (0 = register ring, 2/3 = LDS-DMA
-    stages); 0 (-1 for staging) restores the automatic choice.  For tests and
-    sweeps: call it between steps, never between sizing a statistics buffer
+    channels (32/64/128), its staging (0 = register ring, 2/3 = LDS-DMA
+    stages) and the data gradient's parity classes per block (1 or 4); 0
+    (-1 for staging) restores the automatic choice.  For tests and sweeps:
+    call it between steps, never between sizing a statistics buffer
     (:func:`conv_fwd_stats_rows`) and the launch that fills it."""
-    hip_ext().conv_set_tiles(int(bm), int(bn), int(staging))
+    hip_ext().conv_set_tiles(int(bm), int(bn), int(staging), int(dgrad_cls))
 
 
 def _conv_function():
@@ -1328,11 +1408,18 @@ def _conv_function():
         into the master weight's gradient (no bf16 round trip, no cast)."""
 
         @staticmethod
-        def forward(ctx, x, w32, w16, with_stats=False, wt=None, bn_link=None, wchain=None, wlast=True, lut=None):
+        def forward(ctx, x, w32, w16, with_stats=False, wt=None, bn_link=None, wchain=None, wlast=True, lut=None,
+                    bn_out=None):
             ctx.set_materialize_grads(False)   # no zero-filled gradient for the stats output
             ctx.save_for_backward(x, w16)
             ctx.w32, ctx.wt, ctx.bn_link = w32, wt, bn_link
             ctx.wchain, ctx.wlast, ctx.lut = wchain, wlast, lut
+            # the BN that consumes the output may hand its backward to this layer's
+            # weight gradient (BnDeferred): only without a data gradient (frames in)
+            ctx.bn_out = None
+            if bn_out is not None and lut is not None:
+                bn_out.armed = True
+                ctx.bn_out = bn_out
             if lut is not None:   # raw u8 frames: the decode runs in the MFMA kernels' loads
                 if isinstance(with_stats, BnAccumulator):
                     return conv_fwd(x, w16, with_stats.fwd, with_stats.R, lut=lut)
@@ -1358,10 +1445,13 @@ def _conv_function():
         @staticmethod
         def backward(ctx, gy, gstats=None):
             x, w16 = ctx.saved_tensors
+            bn_dy = ctx.bn_out.take() if ctx.bn_out is not None else None
             if gy is None:
                 if ctx.wchain is not None and ctx.wlast:
                     ctx.wchain.flush(x.device)
-                return None, None, None, None, None, None, None, None, None
+                return None, None, None, None, None, None, None, None, None, None
+            if bn_dy is not None and ctx.needs_input_grad[0]:
+                raise RuntimeError('conv4x4s2: a deferred BN backward needs a layer without a data gradient')
             gy = gy.contiguous(memory_format=torch.channels_last)
             gx = gw = None
             if ctx.needs_input_grad[0]:
@@ -1388,12 +1478,16 @@ def _conv_function():
                 chain = ctx.wchain if (sunk or ctx.wlast) else None
                 if ctx.wchain is not None and chain is None:
                     ctx.wchain.flush(x.device)
-                gw = conv_wgrad(x, gy, out, chain=chain, last=ctx.wlast or chain is None, lut=ctx.lut, fold=fold)
+                fold_params = ()
+                if fold is not None:
+                    fold_params = tuple(p for p, sk in zip(bl.params, (bl.dw_sunk, bl.db_sunk)) if sk)
+                gw = conv_wgrad(x, gy, out, chain=chain, last=ctx.wlast or chain is None, lut=ctx.lut, fold=fold,
+                                bn_dy=bn_dy, param=ctx.w32 if sunk else None, fold_params=fold_params)
                 if sunk:
                     gw = None      # written into the parameter's bucket view
             elif ctx.wchain is not None:
                 ctx.wchain.flush(x.device)
-            return gx, gw, None, None, None, None, None, None, None
+            return gx, gw, None, None, None, None, None, None, None, None
 
     return _Conv4x4s2
 
@@ -1401,7 +1495,8 @@ def _conv_function():
 _CONV_FN = None
 
 
-def conv4x4s2(x, w32, w16, with_stats=False, wt=None, bn_link=None, wchain=None, wlast=True, lut=None):
+def conv4x4s2(x, w32, w16, with_stats=False, wt=None, bn_link=None, wchain=None, wlast=True, lut=None,
+              bn_out=None):
     """4x4 / stride-2 / pad-1 convolution of bf16 channels-last ``x`` with the
     bf16 copy ``w16`` of fp32 weight ``w32``; the gradient goes to ``w32``
     (fp32, from the MFMA weight-gradient kernel).  See :func:`conv_wgrad_supported`.
@@ -1413,13 +1508,16 @@ def conv4x4s2(x, w32, w16, with_stats=False, wt=None, bn_link=None, wchain=None,
     ``wchain`` / ``wlast``: the :class:`WgradChain` of the model's backward;
     ``wlast`` marks the layer whose weight gradient is computed last (the
     first layer).  ``lut``: ``x`` is raw u8 RGBA frames decoded through this
-    table inside the kernels (:func:`decode_lut_bf16`; no gradient for ``x``)."""
+    table inside the kernels (:func:`decode_lut_bf16`; no gradient for ``x``).
+    ``bn_out`` (with ``lut``): a :class:`BnDeferred` shared with the
+    BatchNorm+LeakyReLU that consumes the output -- its backward apply then
+    runs inside this layer's weight-gradient kernel."""
     global _CONV_FN
     if _CONV_FN is None:
         _CONV_FN = _conv_function()
     if with_stats and not conv_fwd_supported(x, w16):
         raise ValueError('conv4x4s2(with_stats=True) needs the MFMA forward (see conv_fwd_supported)')
-    return _CONV_FN.apply(x, w32, w16.detach(), with_stats, wt, bn_link, wchain, wlast, lut)
+    return _CONV_FN.apply(x, w32, w16.detach(), with_stats, wt, bn_link, wchain, wlast, lut, bn_out)
 
 
 # ---------------------------------------------------------------------------
@@ -1486,6 +1584,8 @@ def _head_function():
                 ext.head_backward(w.data_ptr(), w.stride(1), w.stride(2), w.stride(3), N, H, W, C, oh, ow,
                                   pooled.data_ptr(), dlogit.data_ptr(), g.data_ptr(), dz.data_ptr(), dw.data_ptr(),
                                   _stream(w.device))
+            if sunk:
+                _grad_done(ctx.wparam)
             return dz, None if sunk else dw, None, None, None, None
 
     return _DiscHeadBCE

@@ -21,7 +21,14 @@ flat buffers (one per dtype/device, at most ``bucket_mb`` each):
 * views are 256-byte aligned so the optimizer's 16-byte vector loads apply.
 
 Buckets are laid out in reverse parameter order (the order backward produces
-gradients), so with several buckets the first one is complete earliest.
+gradients), so with several buckets the first one is complete earliest, and
+:meth:`GradBuckets.arm` enqueues each bucket's all-reduce as soon as every
+gradient in it has been written: the gfx950 backward kernels report each
+bucket-view gradient they complete (``ops._GRAD_DONE``), and the collective
+goes onto the compute stream right there, ahead of the rest of the backward
+-- in a captured step, a node of the same linear queue before the first
+layers' weight gradients (``n_buckets=2`` splits the DCGAN's 2.8 MB after the
+last two layers).
 
 Reference loop being data-paralleled: examples/densityopt/densityopt.py:257-331
 (the reference itself trains single-process).
@@ -51,7 +58,8 @@ class GradBuckets:
         bucket of its own.
     """
 
-    def __init__(self, params: Sequence[torch.nn.Parameter], bucket_mb: float = 256.0):
+    def __init__(self, params: Sequence[torch.nn.Parameter], bucket_mb: float = 256.0, n_buckets: int = 0,
+                 first_fraction: float = 0.7):
         ps = [p for p in params if p.requires_grad]
         seen = set()
         self.params: List[torch.nn.Parameter] = []
@@ -63,6 +71,19 @@ class GradBuckets:
             if not _dense(p):
                 raise ValueError(f'GradBuckets: parameter {tuple(p.shape)} is not dense (contiguous / channels-last)')
         limit = max(1, int(bucket_mb * (1 << 20)))
+        cut = None
+        if n_buckets == 2:
+            # two buckets: the first (the last layers' gradients, written first in
+            # backward) ends once it holds first_fraction of the bytes, the second
+            # takes the rest
+            total = sum(p.numel() * p.element_size() for p in self.params)
+            acc, cut = 0, set()
+            for p in reversed(self.params):
+                acc += p.numel() * p.element_size()
+                cut.add(id(p))
+                if acc >= first_fraction * total:
+                    break
+            limit = 1 << 62
         # group by (device, dtype), reverse order: the last layers' gradients come first in backward
         groups: Dict[tuple, List[torch.nn.Parameter]] = {}
         for p in reversed(self.params):
@@ -75,7 +96,8 @@ class GradBuckets:
             cur, offs, size = [], [], 0
             for p in members:
                 n = p.numel()
-                if cur and (size + n) * esz > limit:
+                if cur and ((size + n) * esz > limit or (cut is not None and id(cur[-1]) in cut
+                                                         and id(p) not in cut)):
                     self._make(dev, dt, cur, offs, size)
                     cur, offs, size = [], [], 0
                 offs.append(size)
@@ -115,6 +137,60 @@ class GradBuckets:
                 b.zero_()
         for p in self.params:
             p._bt_grad_fresh = True
+
+    # -- all-reduce as soon as a bucket is complete ---------------------------------
+    def arm(self, comm, op: str = 'sum'):
+        """Before ONE backward pass: enqueue each bucket's all-reduce the
+        moment its last gradient is reported written (``ops._GRAD_DONE``);
+        :meth:`finish` (after the backward) reduces the rest.  Every gradient
+        must come from exactly one contribution in this backward: a second one
+        into an already reduced bucket raises."""
+        from .. import ops
+        if not self.attached():
+            raise RuntimeError('GradBuckets: gradients were detached from their buckets')
+        self._comm, self._op = comm, op
+        self._where = {id(p): i for i, m in enumerate(self._members) for p in m}
+        self._left = [{id(p) for p in m} for m in self._members]
+        self._issued = [False] * len(self.buckets)
+        self.order = []
+        ops._GRAD_DONE = self._on_done
+        ops._GRAD_LATE = self._on_late
+
+    def _issue(self, i):
+        from .. import ops
+        self._issued[i] = True
+        # (bucket, weight-gradient launches enqueued before its all-reduce): where it went
+        self.order.append((i, ops.KERNEL_CALLS.get('conv_wgrad', 0)))
+        self._comm.all_reduce_(self.buckets[i], self._op)
+
+    def _on_done(self, p):
+        i = self._where.get(id(p))
+        if i is None or self._issued[i]:
+            return
+        self._left[i].discard(id(p))
+        if not self._left[i]:
+            self._issue(i)
+
+    def _on_late(self, p):
+        i = self._where.get(id(p))
+        if i is not None and self._issued[i]:
+            raise RuntimeError('GradBuckets: a gradient arrived after its bucket was all-reduced '
+                               '(several contributions per step need finish-time reduction: no arm())')
+
+    def finish(self) -> int:
+        """After the backward: reduce the buckets not reduced yet (gradients
+        that never reported, or none at all); disarm.  Returns the number of
+        collectives of the step."""
+        from .. import ops
+        ops._GRAD_DONE = ops._GRAD_LATE = None
+        for i, done in enumerate(self._issued):
+            if not done:
+                self._issue(i)
+        return len(self.buckets)
+
+    def disarm(self):
+        from .. import ops
+        ops._GRAD_DONE = ops._GRAD_LATE = None
 
     def all_reduce(self, comm, op: str = 'sum') -> int:
         """Reduce every bucket in place over ``comm``

@@ -102,6 +102,11 @@ class CapturedStep:
         tensors (``btt.DeviceLoader(reuse_buffers=True)``); further inputs
         are copied into a private buffer with a graph of its own.  Not with
         ``split``.
+    overlap: (data parallel with buckets) two gradient buckets, and each
+        bucket's all-reduce enqueued as soon as its gradients are written
+        (:meth:`~.grads.GradBuckets.arm`): the last layers' bucket goes ahead of
+        the first layers' weight gradients.  Only for a ``loss_fn`` whose
+        parameters each get one gradient contribution per backward.
     split: capture forward+loss and backward+update as two graphs sharing one
         memory pool, so a caller can act between them: ``step(x, mid=fn)``
         runs ``fn()`` after enqueuing the forward (e.g. to gate the next
@@ -122,7 +127,7 @@ class CapturedStep:
     def __init__(self, model: torch.nn.Module, optimizer: torch.optim.Optimizer,
                  loss_fn: Callable[[torch.nn.Module, torch.Tensor], torch.Tensor], allreduce=True,
                  warmup: int = 3, graph: bool = True, group=None, bucket_mb: float = 256.0, split: bool = False,
-                 comm=None, buckets: bool = True, static_inputs: int = 0):
+                 comm=None, buckets: bool = True, static_inputs: int = 0, overlap: bool = False):
         self.model, self.opt, self.loss_fn = model, optimizer, loss_fn
         self.split = split
         self.static_inputs = 0 if split else max(0, int(static_inputs))
@@ -141,6 +146,7 @@ class CapturedStep:
         active = bool(allreduce) and dist.is_available() and dist.is_initialized() and (
             dist.get_world_size(group) > 1 or allreduce == 'always')
         self._legacy = active and not buckets
+        self.overlap = bool(overlap) and active and buckets
         self._memset = True
         self._seed = None
         # persistent gradient buckets: always for a collective; without one too
@@ -149,7 +155,7 @@ class CapturedStep:
         zeroing = hasattr(optimizer, 'set_zero_grads')
         if buckets and (active or zeroing):
             from .grads import GradBuckets
-            self.grads = GradBuckets(model.parameters(), bucket_mb=bucket_mb)
+            self.grads = GradBuckets(model.parameters(), bucket_mb=bucket_mb, n_buckets=2 if self.overlap else 0)
             if zeroing:
                 optimizer.set_zero_grads(True)
                 # the optimizer clears only the gradients it consumes: a model
@@ -180,12 +186,25 @@ class CapturedStep:
         if self._seed is None or self._seed.shape != loss.shape or self._seed.device != loss.device \
                 or self._seed.dtype != loss.dtype:
             self._seed = torch.ones_like(loss)
-        loss.backward(self._seed)
-        if self.grads is not None and self.comm is not None:
+        if self.overlap and self.grads is not None and self.comm is not None:
+            # each bucket's all-reduce is enqueued the moment its last gradient is
+            # (the last layers' bucket ahead of the first layers' weight gradients)
+            self.grads.arm(self.comm, self._op)
+            try:
+                loss.backward(self._seed)
+            except BaseException:
+                self.grads.disarm()
+                raise
+            self.collectives = self.grads.finish()
+        elif self.grads is not None and self.comm is not None:
+            loss.backward(self._seed)
             self.collectives = self.grads.all_reduce(self.comm, self._op)
         elif self._legacy:
+            loss.backward(self._seed)
             self.collectives = allreduce_gradients(self.model.parameters(), self.group, self.bucket_mb,
                                                    force=self.allreduce == 'always')
+        else:
+            loss.backward(self._seed)
         self.opt.step()
         return loss.detach()
 

@@ -38,20 +38,28 @@ def main(path):
     xs = [torch.rand(4, 4, 96, 128, device=dev, generator=g).to(torch.bfloat16)
           .contiguous(memory_format=torch.channels_last) for _ in range(5)]
     nets = []
-    for pg in (False, True):
+    for pg in (False, True, 'overlap'):
         torch.manual_seed(0)
         m = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=torch.channels_last)
         opt = ops.FusedAdam(m.parameters(), lr=2e-4)
         step = CapturedStep(m, opt, lambda mod, x: mod.bce_loss_bf16(x, 1.0), warmup=2,
-                            allreduce='always' if pg else False, comm=comm if pg else None)
+                            allreduce='always' if pg else False, comm=comm if pg else None, overlap=pg == 'overlap')
+        w0 = ops.KERNEL_CALLS.get('conv_wgrad', 0)
         for x in xs:
             step(x)
         torch.cuda.synchronize()
         nets.append(m)
-        if pg:
+        if pg is True:
             res['collectives'] = step.collectives
             res['state'] = step.state
             res['error'] = step.error
+        elif pg == 'overlap':
+            # (bucket, weight-gradient launches before its all-reduce) of the captured step
+            res['overlap'] = {'collectives': step.collectives, 'state': step.state, 'error': step.error,
+                              'order': [(i, n - w0) for i, n in step.grads.order],
+                              'first_bucket_params': len(step.grads._members[0]),
+                              'max_abs_diff': max(float((p - q).abs().max())
+                                                  for p, q in zip(nets[0].parameters(), m.parameters()))}
     res['max_abs_diff'] = max(float((p - q).abs().max()) for p, q in zip(nets[0].parameters(), nets[1].parameters()))
     d = torch.cat([(p - q).detach().abs().flatten() for p, q in zip(nets[0].parameters(), nets[1].parameters())])
     res['mean_abs_diff'] = float(d.mean())

@@ -24,11 +24,21 @@ def _ref(x, dy, cout):
     return torch.nn.grad.conv2d_weight(x.float(), (cout, x.shape[1], 4, 4), dy.float(), stride=2, padding=1)
 
 
+@pytest.fixture(params=[0, 2, 3], ids=lambda s: f'staging{s}')
+def wgrad_staging(request):
+    """Weight-gradient staging: register ring (0) or LDS-DMA stages of 64
+    pixels (2, 3; layers with Wo >= 32 -- narrower ones take the register ring)."""
+    ops.hip_ext().conv_set_wgrad_staging(request.param)
+    yield request.param
+    ops.hip_ext().conv_set_wgrad_staging(-1)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize('N,Cin,H,W,Cout', [(2, 32, 30, 40, 64), (2, 64, 16, 20, 128), (1, 128, 8, 10, 256),
-                                            (3, 32, 14, 18, 64), (8, 32, 240, 320, 64)])
+                                            (3, 32, 14, 18, 64), (8, 32, 240, 320, 64), (2, 64, 60, 80, 128),
+                                            (1, 128, 60, 64, 256), (3, 32, 10, 66, 64)])
 @pytest.mark.parametrize('layout', ['channels_last', 'contiguous'])
-def test_wgrad_matches_fp32_reference(dev, N, Cin, H, W, Cout, layout):
+def test_wgrad_matches_fp32_reference(dev, N, Cin, H, W, Cout, layout, wgrad_staging):
     g = torch.Generator(device=dev).manual_seed(N * Cin + H)
     cl = torch.channels_last
     x = torch.randn(N, Cin, H, W, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
@@ -45,7 +55,7 @@ def test_wgrad_matches_fp32_reference(dev, N, Cin, H, W, Cout, layout):
 
 
 @pytest.mark.gpu
-def test_wgrad_asymmetric_operands(dev):
+def test_wgrad_asymmetric_operands(dev, wgrad_staging):
     """Structured (non-random) operands: a transposed or mis-swizzled tile
     cannot pass by symmetry."""
     cl = torch.channels_last
@@ -210,20 +220,22 @@ def test_bn_backward_sums_from_dgrad_epilogue(dev, monkeypatch):
 def tiles(request):
     ops.conv_set_tiles(*request.param)
     yield request.param
-    ops.conv_set_tiles(0, 0, -1)
+    ops.conv_set_tiles(0, 0, -1, 0)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('tiles', [(bm, bn, st) for st in (0, 2, 3) for bm in (64, 128) for bn in (32, 64, 128)],
-                         indirect=True, ids=lambda t: f'bm{t[0]}_bn{t[1]}_st{t[2]}')
+@pytest.mark.parametrize('tiles', [(bm, bn, st, 0) for st in (0, 2, 3) for bm in (64, 128) for bn in (32, 64, 128)]
+                         + [(bm, bn, 2, cls) for cls in (1, 4) for bm in (64, 128) for bn in (32, 64)],
+                         indirect=True, ids=lambda t: f'bm{t[0]}_bn{t[1]}_st{t[2]}_cls{t[3]}')
 def test_tap_gemm_tile_variants(dev, tiles):
-    """Every tile shape of the tap-gather GEMM (pixels x output channels) and
-    staging (register ring, 2 or 3 LDS-DMA stages) against the fp32
-    reference: forward with statistics, data gradient, and the data gradient
-    with the BN-backward epilogue (Discriminator backward)."""
+    """Every tile shape of the tap-gather GEMM (pixels x output channels),
+    staging (register ring, 2 or 3 LDS-DMA stages) and data-gradient parity
+    classes per block (1, 4; 0 = automatic) against the fp32 reference:
+    forward with statistics, data gradient, and the data gradient with the
+    BN-backward epilogue (Discriminator backward)."""
     import torch.nn.functional as F
     from blendtorch.models import Discriminator
-    bm, bn, _ = tiles
+    bm, bn = tiles[0], tiles[1]
     cl = torch.channels_last
     g = torch.Generator(device=dev).manual_seed(bm + bn)
     for N, Cin, H, W, Cout in [(2, 64, 30, 40, 128), (1, 128, 8, 10, 256), (3, 32, 14, 18, 64)]:
@@ -248,7 +260,7 @@ def test_tap_gemm_tile_variants(dev, tiles):
     xin = torch.rand(4, 4, 96, 128, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
     a.bce_loss_bf16(xin, 1.0).backward()
     got = [p.grad.clone() for p in a.parameters()]
-    ops.conv_set_tiles(0, 0, 0)     # reference: default tiles, register staging
+    ops.conv_set_tiles(0, 0, 0, 1)  # reference: default tiles, register staging, one class per block
     a.zero_grad(set_to_none=True)
     a.bce_loss_bf16(xin, 1.0).backward()
     for (n, p), g0 in zip(a.named_parameters(), got):
@@ -376,6 +388,50 @@ def test_wgrad_chain_with_frozen_first_layer(dev):
     gb.zero_()
     a.bce_loss_bf16(x, 1.0).backward()
     b.bce_loss_bf16(x, 1.0).backward()
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        if pa.requires_grad:
+            torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-4, atol=1e-6 + 1e-4 * float(pb.grad.abs().max()),
+                                       msg=n)
+
+
+@pytest.mark.gpu
+def test_first_bn_backward_deferred_into_first_wgrad(dev):
+    """With raw u8 frames the first BN's backward apply runs inside the first
+    convolution's weight-gradient kernel (ops.BnDeferred): its dY operand is
+    gx computed from the BN input and output gradient while staging, with the
+    same formula and bf16 rounding as bn_bwd_apply.  Every gradient matches
+    the step with the separate apply launch (the slice reduce adds with float
+    atomics: equal up to the order of those adds), and the apply launch is
+    gone."""
+    from blendtorch.models import Discriminator
+    cl = torch.channels_last
+    cfg = ops.DecodeConfig.unit(channels='rgba', gamma=2.2, dtype='bfloat16', layout='nhwc')
+    g = torch.Generator(device=dev).manual_seed(21)
+    xu8 = torch.randint(0, 256, (4, 96, 128, 4), dtype=torch.uint8, device=dev, generator=g).permute(0, 3, 1, 2)
+    torch.manual_seed(3)
+    a = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
+    b = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
+    b.load_state_dict(a.state_dict())
+    b.defer_first_bn = False
+    d0 = ops.KERNEL_CALLS.get('bn_backward_deferred', 0)
+    w0 = ops.KERNEL_CALLS.get('conv_wgrad_bn_dy', 0)
+    la = a.bce_loss_bf16(xu8, 1.0, decode=cfg)
+    la.backward()
+    assert ops.KERNEL_CALLS.get('bn_backward_deferred', 0) == d0 + 1
+    assert ops.KERNEL_CALLS.get('conv_wgrad_bn_dy', 0) == w0 + 1
+    lb = b.bce_loss_bf16(xu8, 1.0, decode=cfg)
+    lb.backward()
+    assert ops.KERNEL_CALLS.get('bn_backward_deferred', 0) == d0 + 1      # b took the apply launch
+    torch.testing.assert_close(la, lb, rtol=0, atol=0)
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-4, atol=1e-6 + 1e-4 * float(pb.grad.abs().max()), msg=n)
+    # a frozen first layer never takes the hand-off: the other gradients are unchanged
+    a.zero_grad(set_to_none=True)
+    b.zero_grad(set_to_none=True)
+    for m in (a, b):
+        m.features[0].weight.requires_grad_(False)
+    a.bce_loss_bf16(xu8, 1.0, decode=cfg).backward()
+    b.bce_loss_bf16(xu8, 1.0, decode=cfg).backward()
     for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
         if pa.requires_grad:
             torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-4, atol=1e-6 + 1e-4 * float(pb.grad.abs().max()),

@@ -230,6 +230,14 @@ def test_rccl_direct_one_rank_process_group(dev, tmp_path):
     assert res['collectives'] == 1 and res['state'] == 'graph'
     assert res['max_abs_diff'] < 1e-3 and res['mean_abs_diff'] < 2e-5 and res['frac_above_half_lr'] < 0.02
     assert res['allreduce_avg_ok'] and res['broadcast_ok'] and res['p2p_self_ok']
+    # two buckets, the last layers' all-reduced ahead of the first layers' weight
+    # gradients: captured (the last recorded step is the capture), issued after
+    # 2 of the 4 weight-gradient launches, trains like the one-bucket step
+    ov = res['overlap']
+    assert ov['collectives'] == 2 and ov['state'] == 'graph', ov
+    (b0, n0), (b1, n1) = ov['order'][-2:]
+    assert (b0, b1) == (0, 1) and n1 - n0 == 2, ov['order']
+    assert ov['max_abs_diff'] < 1e-3
 
 
 def test_densityopt_step_captures_and_replays(dev):

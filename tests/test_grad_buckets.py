@@ -67,7 +67,7 @@ def _free_port():
     return p
 
 
-def _dp_worker(rank, world, port, q):
+def _dp_worker(rank, world, port, q, overlap=False):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     try:
@@ -75,7 +75,7 @@ def _dp_worker(rank, world, port, q):
         parallel.init_distributed(backend='gloo')
         m = _net()
         opt = ops.FusedAdam(m.parameters(), lr=1e-2)
-        step = CapturedStep(m, opt, lambda mod, x: mod(x).pow(2).mean(), graph=False)
+        step = CapturedStep(m, opt, lambda mod, x: mod(x).pow(2).mean(), graph=False, overlap=overlap)
         ok_scale = opt.grad_scale == 1.0 / world and step.grads is not None and not step.comm.native
         xs = [torch.randn(4, 3, 16, 16, generator=torch.Generator().manual_seed(10 * r + i))
               for r in range(world) for i in range(3)]
@@ -92,7 +92,7 @@ def _dp_worker(rank, world, port, q):
         w = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
         allw = [torch.empty_like(w) for _ in range(world)]
         torch.distributed.all_gather(allw, w)
-        ok_sync = all(torch.equal(allw[0], x) for x in allw) and step.collectives == 1
+        ok_sync = all(torch.equal(allw[0], x) for x in allw) and step.collectives == len(step.grads.buckets)
         wr = torch.cat([p.detach().reshape(-1) for p in ref.parameters()])
         ok_ref = torch.allclose(w, wr, rtol=1e-4, atol=1e-5)
         q.put((rank, ok_scale, ok_sync, ok_ref))
@@ -102,14 +102,16 @@ def _dp_worker(rank, world, port, q):
         q.put((rank, traceback.format_exc()))
 
 
-def test_bucketed_dp_step_gloo_world2():
+@pytest.mark.parametrize('overlap', [False, True])
+def test_bucketed_dp_step_gloo_world2(overlap):
     """CapturedStep on GradBuckets + FusedAdam(grad_scale=1/world): weights
     stay bit-identical across ranks and equal single-process training on the
-    union of the ranks' batches."""
+    union of the ranks' batches -- also with two buckets reduced as soon as
+    they are complete (overlap)."""
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q, overlap)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]
@@ -117,3 +119,39 @@ def test_bucketed_dp_step_gloo_world2():
         p.join(timeout=60)
     for r in res:
         assert r[1:] == (True, True, True), r
+
+
+def test_armed_buckets_reduce_as_soon_as_complete():
+    """GradBuckets.arm: a bucket's all-reduce is enqueued the moment the last
+    of its gradients is reported written (ops._GRAD_DONE, as the gfx950
+    backward kernels do), the rest at finish(); a second contribution into a
+    bucket already reduced raises."""
+    m = torch.nn.Sequential(torch.nn.Linear(64, 64), torch.nn.Linear(64, 256), torch.nn.Linear(256, 8))
+    gb = parallel.GradBuckets(m.parameters(), n_buckets=2)
+    assert len(gb.buckets) == 2
+    first = {id(p) for p in gb._members[0]}
+    # reverse order, 70 % of the bytes: the last two layers
+    assert first == {id(p) for p in list(m[2].parameters()) + list(m[1].parameters())}
+
+    class Comm:
+        calls = []
+
+        def all_reduce_(self, t, op):
+            self.calls.append(t.data_ptr())
+
+    c = Comm()
+    gb.zero_()
+    gb.arm(c)
+    for p in m[2].parameters():
+        ops._grad_done(p)
+    assert c.calls == []                      # bucket 0 still has m[1]'s gradients to come
+    ops._grad_done(m[1].weight)
+    ops._grad_done(m[1].bias)
+    assert c.calls == [gb.buckets[0].data_ptr()]
+    ops._grad_done(m[1].bias)                 # reported twice: no second collective
+    assert len(c.calls) == 1
+    with pytest.raises(RuntimeError, match='after its bucket'):
+        ops._GRAD_LATE(m[2].weight)
+    ops._GRAD_LATE(m[0].weight)               # bucket 1 not reduced yet: fine
+    assert gb.finish() == 2 and c.calls[1] == gb.buckets[1].data_ptr()
+    assert ops._GRAD_DONE is None and ops._GRAD_LATE is None
