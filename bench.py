@@ -546,6 +546,16 @@ def main(argv=None):
         for k in ('usage_usec', 'throttled_usec', 'nr_throttled'):
             if k in cg0 and k in cg1:
                 cpu['cgroup_' + k] = cg1[k] - cg0[k]
+        # CPU per delivered frame (what plan_rank_resources budgets with): the
+        # cgroup holds every local rank's consumer and producers; the consumer
+        # process (loader IO threads + the Python main thread) is this rank's
+        frames_here = args.steps * args.batch
+        per = {'consumer': round(cpu['consumer_cpu_s'] * 1e6 / max(1, frames_here), 2)}
+        if 'cgroup_usage_usec' in cpu:
+            node_frames = frames_here * (local_world if args.dist != 'scatter' else 1)
+            per['total'] = round(cpu['cgroup_usage_usec'] / max(1, node_frames), 2)
+            per['producers'] = round(per['total'] - per['consumer'], 2)
+        cpu['us_per_frame'] = per
         if th0 is not None:
             # (diagnostic) this process's busiest threads over the timed region
             th1 = thread_cpu()

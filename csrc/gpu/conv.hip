@@ -1338,6 +1338,220 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// The first layer's forward (4-channel RGBA input, raw u8 through the decode
+// table or decoded bf16; K = 16 taps x 4 = one MFMA k-step) over T
+// consecutive 128-pixel tiles per block.  As one tile per block (the C4 path
+// of tap_gemm_kernel, 4,800 blocks of 4 MFMAs per wave at 640x480 x 8) the
+// kernel was all prologue and epilogue: table staging, weight tile, row
+// arithmetic, a load -> wait -> compute -> store chain per block and 64 fp64
+// atomics per tile.  Here the table and the weight tile are staged once, the
+// next tile's frame loads are in flight while this tile computes and stores,
+// and the BatchNorm sums stay in registers until the block's last tile.
+template <int BN>
+__global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tiles_per_block) {
+  constexpr int BM = FBM, RJ = BM / 32, RB = BN / 32;
+  constexpr int WGM = BN >= 64 ? 2 : 4, WGN = 4 / WGM;
+  constexpr int FM = BM / WGM / 16, FN = BN / WGN / 16;
+  constexpr int A_TILE = BM * F_ROW;                 // 16 KB, reused as the epilogue tile
+  constexpr int T_ROW = BN >= 64 ? BN * 2 : F_ROW;
+  static_assert(BM * T_ROW <= A_TILE, "epilogue tile");
+  constexpr int B_OFF = A_TILE, LUT_OFF = B_OFF + BN * F_ROW, RED_OFF = LUT_OFF + kLutBytes;
+  __shared__ __attribute__((aligned(16))) char smem[RED_OFF + WGM * 2 * BN * 4];
+  float* red = reinterpret_cast<float*>(smem + RED_OFF);
+  const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
+  const int ntiles = (p.M + BM - 1) / BM;
+  const int tile0 = int(blockIdx.x) * tiles_per_block;
+  const int tile1 = tile0 + tiles_per_block < ntiles ? tile0 + tiles_per_block : ntiles;
+  const bool u8in = p.lut != nullptr;
+  const int ar = t >> 3, ac = t & 7;
+  const int kh = ac >> 1, kw = (ac & 1) * 2;          // this thread's tap pair of its rows
+  if (u8in) stage_lut(p.lut, smem + LUT_OFF);
+  {   // the weight tile, once: rows co = ar + 32 j, chunk ac = taps (kh, kw), (kh, kw + 1)
+    const int tap = kh * 4 + kw;
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+      const int co = ar + 32 * j;
+      uint4 v;
+      if (p.wc == 4) {
+        v = *reinterpret_cast<const uint4*>(p.w + (co * 16 + tap) * 4);
+      } else {   // an RGB weight on RGBA input: channel 3 gets weight 0
+        const uint16_t* q = p.w + (co * 16 + tap) * 3;
+        v = make_uint4(uint32_t(q[0]) | (uint32_t(q[1]) << 16), uint32_t(q[2]),
+                       uint32_t(q[3]) | (uint32_t(q[4]) << 16), uint32_t(q[5]));
+      }
+      *reinterpret_cast<uint4*>(smem + B_OFF + f_off(co, ac)) = v;
+    }
+  }
+  const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(p.src, int64_t(p.N) * p.SH * p.SW * p.C * (u8in ? 1 : 2));
+  // the thread's rows ar + 32 j of the tile being loaded: (n, a, b) of the first by
+  // division, the others by stepping; the next tile's by stepping 128 pixels
+  int gn, ga, gb;
+  {
+    const int m = tile0 * BM + ar < p.M ? tile0 * BM + ar : 0;
+    gn = m / (p.GH * p.GW);
+    const int rem = m - gn * (p.GH * p.GW);
+    ga = rem / p.GW;
+    gb = rem - ga * p.GW;
+  }
+  auto step = [&](int& n, int& a, int& b, int by) {
+    b += by;
+    while (b >= p.GW) {
+      b -= p.GW;
+      if (++a == p.GH) a = 0, ++n;
+    }
+  };
+  uint32_t w0[RJ], w1[RJ];   // raw pixels (u8: RGBA word; bf16: low half), in flight across a tile
+  uint32_t h0[RJ], h1[RJ];   // bf16 input: the high half
+  bool k0[RJ], k1[RJ];
+  auto load_raw = [&](int tile) {
+    int n = gn, a = ga, b = gb;
+#pragma unroll
+    for (int j = 0; j < RJ; ++j) {
+      if (j > 0) step(n, a, b, 32);
+      const int m = tile * BM + ar + 32 * j;
+      const int r0 = 2 * a - 1, c0 = 2 * b - 1;
+      const bool rok = m < p.M && unsigned(r0 + kh) < unsigned(p.SH);
+      const int e = ((n * p.SH + r0 + kh) * p.SW + c0 + kw) * 4;
+      k0[j] = rok && unsigned(c0 + kw) < unsigned(p.SW);
+      k1[j] = rok && unsigned(c0 + kw + 1) < unsigned(p.SW);
+      if (u8in) {
+        w0[j] = bload4(rs_src, k0[j] ? uint32_t(e) : kOOB);
+        w1[j] = bload4(rs_src, k1[j] ? uint32_t(e + 4) : kOOB);
+      } else {
+        const uint2 lo = bload8(rs_src, k0[j] ? uint32_t(e) * 2u : kOOB);
+        const uint2 hi = bload8(rs_src, k1[j] ? uint32_t(e + 4) * 2u : kOOB);
+        w0[j] = lo.x, h0[j] = lo.y, w1[j] = hi.x, h1[j] = hi.y;
+      }
+    }
+    step(gn, ga, gb, BM);   // the next tile's first row
+  };
+  const int st_a = f_off(ar, ac);
+  auto store_a = [&]() {
+#pragma unroll
+    for (int j = 0; j < RJ; ++j) {
+      uint4 v;
+      if (u8in) {
+        const uint2 lo = lut_px(smem + LUT_OFF, w0[j], k0[j]), hi = lut_px(smem + LUT_OFF, w1[j], k1[j]);
+        v = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      } else {
+        v = make_uint4(w0[j], h0[j], w1[j], h1[j]);
+      }
+      *reinterpret_cast<uint4*>(smem + st_a + j * 32 * F_ROW) = v;
+    }
+  };
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int row0 = wm * (BM / WGM), col0 = wn * (BN / WGN);
+  int fa[FM][2], fb[FN][2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int chunk = 4 * kk + (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) fa[i][kk] = f_off(row0 + 16 * i + (lane & 15), chunk);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) fb[j][kk] = B_OFF + f_off(col0 + 16 * j + (lane & 15), chunk);
+  }
+  const int lr = 4 * (lane >> 4);
+  int toff[FN][4];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int col = col0 + 16 * j + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      toff[j][r] = (row0 + lr + r) * (T_ROW / 2) + ((((col >> 3) ^ ((lr + r) & 7)) << 4) >> 1) + (col & 7);
+  }
+  constexpr int CPR = BN / 8, RPP = kThreads / CPR, NJ = BM / RPP;
+  const int ec = t % CPR;
+  float sum[FN], sq[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) sum[j] = sq[j] = 0.f;
+  uint16_t* tile_lds = reinterpret_cast<uint16_t*>(smem);
+
+  if (tile0 < tile1) load_raw(tile0);
+  for (int tile = tile0; tile < tile1; ++tile) {
+    __syncthreads();                 // previous tile's epilogue done with the LDS (and, first, the tables)
+    store_a();                       // decode (LUT lookups wait for this tile's loads)
+    if (tile + 1 < tile1) load_raw(tile + 1);   // in flight while this tile computes and stores
+    __syncthreads();
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 a[FM], bb[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const bf16x8*>(smem + fa[i][kk]);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bb[j] = *reinterpret_cast<const bf16x8*>(smem + fb[j][kk]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bb[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();                 // every wave has its fragments: the A tile becomes the output tile
+    const int m0 = tile * BM;
+    const bool all_rows = m0 + BM <= p.M;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        uint32_t pk[2];
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const f32x2 pr = {acc[i][j][2 * h2], acc[i][j][2 * h2 + 1]};
+          pk[h2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2));
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t w2 = pk[r >> 1];
+          tile_lds[toff[j][r] + i * 16 * (T_ROW / 2)] = uint16_t(r & 1 ? w2 >> 16 : w2);
+          if (all_rows || m0 + row0 + 16 * i + lr + r < p.M) {
+            const float vr = __uint_as_float(r & 1 ? w2 & 0xFFFF0000u : w2 << 16);
+            sum[j] += vr;
+            sq[j] += vr * vr;
+          }
+        }
+      }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int er = t / CPR + RPP * j, m = m0 + er;
+      if (m < p.M) {
+        const uint4 v = *reinterpret_cast<const uint4*>(smem + er * T_ROW + ((ec ^ (er & 7)) << 4));
+        *reinterpret_cast<uint4*>(p.dst + int64_t(m) * p.NOUT + ec * 8) = v;
+      }
+    }
+  }
+  if (!p.stats) return;
+  // the block's BatchNorm sums: lanes l, l^16, l^32, l^48 hold a channel, then the WGM row groups
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    sum[j] += __shfl_xor(sum[j], 16);
+    sum[j] += __shfl_xor(sum[j], 32);
+    sq[j] += __shfl_xor(sq[j], 16);
+    sq[j] += __shfl_xor(sq[j], 32);
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      red[(wm * 2 + 0) * BN + col0 + 16 * j + lane] = sum[j];
+      red[(wm * 2 + 1) * BN + col0 + 16 * j + lane] = sq[j];
+    }
+  }
+  __syncthreads();
+  if (t < 2 * BN) {
+    const int which = t / BN, c = t - which * BN;
+    float v = 0.f;
+#pragma unroll
+    for (int g = 0; g < WGM; ++g) v += red[(g * 2 + which) * BN + c];
+    unsafeAtomicAdd(reinterpret_cast<double*>(p.stats) + ((int(blockIdx.x) % p.acc_r) * 2 + which) * p.NOUT + c,
+                    double(v));
+  }
+}
+
 // several weights at once (blockIdx.y = tensor): the data gradients' operands for every layer in one launch
 __global__ __launch_bounds__(kThreads) void weight_t_multi_kernel(WeightTParams p) {
   const int k = int(blockIdx.y);
@@ -1525,7 +1739,11 @@ int env_int(const char* name) {
 int g_force_bm = env_int("BT_CONV_BM");
 int g_force_bn = env_int("BT_CONV_BN");
 int g_dgrad_cls = env_int("BT_CONV_DGRAD_CLS");   // 1 / 4: force the data gradient's classes per block
+int g_conv1_tiles = env_int("BT_CONV1_TILES");     // first-layer forward: tiles per block (1 = the tap-GEMM path)
+int conv1_tiles() { return g_conv1_tiles > 0 ? g_conv1_tiles : 4; }
 }  // namespace
+
+void conv_set_conv1_tiles(int tiles) { g_conv1_tiles = tiles > 0 ? tiles : 0; }
 
 int conv_dgrad_classes_per_block(int64_t M, int NOUT) {
   // one parity class per block unless that makes >= 4096 blocks (the
@@ -1583,6 +1801,17 @@ hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream) {
   g.acc_r = p.stats ? p.acc_r : 0;
   if (g.acc_r < 0 || g.acc_r > 64) return hipErrorInvalidValue;
   if (p.Cin == 4 && g.wc != 3 && g.wc != 4) return hipErrorInvalidValue;
+  // the first layer over several tiles per block (conv1_fwd_kernel): BN sums
+  // into an accumulator (or none), 128-pixel tiles, Cout 32 / 64
+  const int64_t t128 = (g.M + FBM - 1) / FBM;
+  const int bn1 = conv_tile_channels(p.Cout, true);
+  if (p.Cin == 4 && (!p.stats || g.acc_r > 0) && p.Cout == bn1 && t128 >= 1024 && conv1_tiles() > 1) {
+    const int tpb = conv1_tiles();
+    const int64_t blocks = (t128 + tpb - 1) / tpb;
+    if (bn1 == 64) conv1_fwd_kernel<64><<<unsigned(blocks), kThreads, 0, stream>>>(g, tpb);
+    else conv1_fwd_kernel<32><<<unsigned(blocks), kThreads, 0, stream>>>(g, tpb);
+    return hipGetLastError();
+  }
   launch_tap_gemm<false>(g, 1, stream);
   return hipGetLastError();
 }

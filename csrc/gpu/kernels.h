@@ -407,6 +407,9 @@ void conv_set_tiles(int bm, int bn, int staging = -1, int dgrad_cls = 0);
 // Parity classes per data-gradient block (1, or 4 when one class per block
 // would give >= 4096 blocks; BT_CONV_DGRAD_CLS / conv_set_tiles force it).
 int conv_dgrad_classes_per_block(int64_t M, int NOUT);
+// First-layer (4-channel) forward: 128-pixel tiles per block of the multi-tile
+// kernel (default 4; 1 = the one-tile tap-GEMM path; BT_CONV1_TILES).
+void conv_set_conv1_tiles(int tiles);
 hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream);
 // Data gradient of the same convolution (same tap-gather GEMM kernel, four
 // stride-2 parity classes in one launch): dy [N][H/2][W/2][Cout] bf16,

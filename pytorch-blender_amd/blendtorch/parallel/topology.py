@@ -105,6 +105,36 @@ def current_allowed_cpus() -> List[int]:
     return sorted(os.sched_getaffinity(0))
 
 
+# Measured CPU cost per delivered 640x480 RGBA frame on the headline path
+# (bench.py, 8 cubesim producers -> shm ring -> zero-copy decode, one MI355X;
+# profiles/r3/final/bench_headline.log: 2.31 s of cgroup CPU for 16,000 frames,
+# 0.71 s of it in the consumer process).  bench.py reports the current values
+# as ``cpu_us_per_frame`` on every run.
+PRODUCER_US_PER_FRAME = 100.0
+CONSUMER_US_PER_FRAME = 44.0
+# host->device read ceiling of one MI355X PCIe link (profiles/direct_host_read.md)
+LINK_GBYTES_PER_S = 51.5
+
+
+def producers_for_share(share: float, frame_bytes: int = 640 * 480 * 4,
+                        producer_us: float = PRODUCER_US_PER_FRAME, consumer_us: float = CONSUMER_US_PER_FRAME,
+                        link_gbytes: float = LINK_GBYTES_PER_S, cap: int = 8) -> int:
+    """Producer processes one rank should run on ``share`` CPUs: the frame
+    rate the rank can sustain is the smaller of its PCIe link's and its CPU
+    share's (every frame costs ``producer_us`` in some producer and
+    ``consumer_us`` in the rank's own process); the producers need
+    ``rate * producer_us`` cores of it, rounded up.  When the link is the
+    bound a 1.5x margin keeps producers ahead of it (backpressure absorbs
+    the surplus); when the CPU is, more producers would only steal the
+    consumer's cores."""
+    link_rate = link_gbytes * 1e9 / max(1, frame_bytes)
+    cpu_rate = max(0.0, share) * 1e6 / (producer_us + consumer_us)
+    rate = min(link_rate, cpu_rate)
+    need = rate * producer_us / 1e6
+    n = need * 1.5 if link_rate <= cpu_rate else need
+    return int(max(1, min(cap, -(-n // 1))))
+
+
 def plan_rank_resources(rank: int, local_rank: int, local_world: int, world: int, allowed: Sequence[int],
                         budget: int, pin: bool, producers: int = 0, dist_mode: str = 'shard', shm_slots: int = 48,
                         shm_free_bytes: Optional[int] = None, frame_bytes: int = 640 * 480 * 4,
@@ -118,9 +148,11 @@ def plan_rank_resources(rank: int, local_rank: int, local_world: int, world: int
       the job may keep busy (``allowed`` trimmed to the cgroup ``budget`` when
       per-core pinning isolates anything, i.e. ``pin``);
     * ``producers``: producer processes this rank launches -- ``producers`` if
-      given, else one per spare CPU of its share (at most 8, at least 1; one
-      producer renders ~14k frames/s, profiles/render_sweep.md).  Scatter mode
-      spreads 8 producers over all ranks (the root's PCIe link is the bound);
+      given, else what the measured per-frame CPU costs justify on the rank's
+      CPU share (:func:`producers_for_share`: 7 on 16 CPUs, where the PCIe
+      link is the bound; 2 on the 2 CPUs a rank gets when 8 ranks share a
+      16-CPU quota, where the CPU is).  Scatter mode spreads 8 producers over
+      all ranks (the root's PCIe link is the bound);
     * ``affinity``: per-producer CPU lists (single cores when pinning, the
       GPU's NUMA domain otherwise, or None);
     * ``start_port``: ``port_base + rank * port_stride`` (the launcher takes
@@ -132,7 +164,7 @@ def plan_rank_resources(rank: int, local_rank: int, local_world: int, world: int
     """
     plan = plan_rank_cpus(local_rank, local_world, list(allowed)[:budget] if pin else allowed, bus_ids, sysfs)
     share = max(1, budget // max(1, local_world))
-    nprod = producers or max(1, min(8, share - 3))
+    nprod = producers or producers_for_share(budget / max(1, local_world), frame_bytes)
     if dist_mode == 'scatter' and not producers:
         nprod = max(1, -(-8 // max(1, world)))
     mine = plan['cpus']

@@ -15,3 +15,5 @@ for v in "X=0" "X=0 --force-pg" "X=0 --force-pg --grad-overlap off"; do
   grep '^{' gpurun_out/dp_ab.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'v':'$v','value':d['value'],'ms':d['ms_per_step'],'coll':d['config']['consumer_collectives_per_step'],'order':d['config'].get('grad_buckets_issue_order')}))" | tee -a gpurun_out/dp_ab.jsonl
 done
 bash scripts/gpurun/dopt_steady.sh
+BT_THREAD_REPORT=1 timeout -k 10 200 python bench.py --steps 2000 > gpurun_out/headline.log 2>&1 || { tail -5 gpurun_out/headline.log; exit 1; }
+grep '^{' gpurun_out/headline.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'value':d['value'],'ms':d['ms_per_step'],'producers':d['config']['producers_per_gpu'],'cpu':d['cpu']}))"
