@@ -777,7 +777,7 @@ struct TapGemm {
 // LDS buffers; 2 or 3 = LDS-DMA (buffer_load ... lds) straight into NST LDS
 // stages -- the 16-byte LDS stores of the register path run at ~79 B/clk/CU
 // (a third of what the fragment reads get) and were the kernel's bound.
-template <bool DGRAD, int BN, bool C4 = false, int BM = FBM, int NST = 0>
+template <bool DGRAD, int BN, bool C4 = false, int BM = FBM, int NST = 0, int CLS = 1>
 __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   constexpr int RJ = BM / 32;                  // staged A rows per thread (ar + 32 j)
   constexpr int A_TILE = BM * F_ROW;
@@ -808,7 +808,9 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   // p.cls_per_block == 4 the block runs all four classes of its pixel tile in
   // turn (the 32-channel layer: 4x fewer, 4x longer blocks -- its 4800
   // one-class blocks of 16 MFMAs per wave were prologue- and epilogue-bound)
-  const int ncls = DGRAD ? p.cls_per_block : 1;
+  // (a compile-time count: with a runtime one the BN-backward sums stayed live
+  // across the whole k-loop of every data gradient, 24 -> 32 us per layer)
+  constexpr int ncls = DGRAD ? CLS : 1;
   int ph = 0, pw = 0;
 
   const int nwg = int(gridDim.x), b = int(blockIdx.x);
@@ -1576,14 +1578,15 @@ __global__ __launch_bounds__(kThreads) void weight_t_kernel(const uint16_t* __re
 }  // namespace
 
 namespace {
-// weight-gradient staging: 0 = register ring (conv_wgrad_kernel), 2 / 3 =
-// LDS-DMA stages of 64 pixels (conv_wgrad_dma_kernel); BT_WGRAD_STAGING
+// weight-gradient staging: 0 = register ring (conv_wgrad_kernel, default), 2 /
+// 3 = LDS-DMA stages of 64 pixels (conv_wgrad_dma_kernel: 33 us against 24 us
+// per layer in the disc step, profiles/r4/disc_kernels.md); BT_WGRAD_STAGING
 int g_wgrad_staging = -1;
 int wgrad_staging() {
   if (g_wgrad_staging < 0) {
     const char* v = std::getenv("BT_WGRAD_STAGING");
-    const int e = v ? std::atoi(v) : 2;
-    g_wgrad_staging = e == 0 || e == 2 || e == 3 ? e : 2;
+    const int e = v ? std::atoi(v) : 0;
+    g_wgrad_staging = e == 0 || e == 2 || e == 3 ? e : 0;
   }
   return g_wgrad_staging;
 }
@@ -1690,10 +1693,15 @@ namespace {
 template <bool DGRAD, int BM, int NST>
 void launch_tap_gemm_bm(const TapGemm& g, int bn, unsigned ytiles, hipStream_t stream) {
   const int64_t blocks = (g.M + BM - 1) / BM * (g.NOUT / bn);
-  const dim3 grid(unsigned(blocks), ytiles / unsigned(DGRAD ? g.cls_per_block : 1));
+  const bool all_cls = DGRAD && g.cls_per_block == 4;
+  const dim3 grid(unsigned(blocks), all_cls ? 1u : ytiles);
   if (!DGRAD && g.C == 4) {
     if (bn == 64) tap_gemm_kernel<false, 64, true, BM><<<grid, kThreads, 0, stream>>>(g);
     else tap_gemm_kernel<false, 32, true, BM><<<grid, kThreads, 0, stream>>>(g);
+  } else if (all_cls) {   // (the 32-channel data gradient; other widths as well for tests / sweeps)
+    if (bn == 128) tap_gemm_kernel<DGRAD, 128, false, BM, NST, 4><<<grid, kThreads, 0, stream>>>(g);
+    else if (bn == 64) tap_gemm_kernel<DGRAD, 64, false, BM, NST, 4><<<grid, kThreads, 0, stream>>>(g);
+    else tap_gemm_kernel<DGRAD, 32, false, BM, NST, 4><<<grid, kThreads, 0, stream>>>(g);
   } else if (bn == 128) {
     tap_gemm_kernel<DGRAD, 128, false, BM, NST><<<grid, kThreads, 0, stream>>>(g);
   } else if (bn == 64) {
@@ -1740,7 +1748,7 @@ int g_force_bm = env_int("BT_CONV_BM");
 int g_force_bn = env_int("BT_CONV_BN");
 int g_dgrad_cls = env_int("BT_CONV_DGRAD_CLS");   // 1 / 4: force the data gradient's classes per block
 int g_conv1_tiles = env_int("BT_CONV1_TILES");     // first-layer forward: tiles per block (1 = the tap-GEMM path)
-int conv1_tiles() { return g_conv1_tiles > 0 ? g_conv1_tiles : 4; }
+int conv1_tiles() { return g_conv1_tiles > 0 ? g_conv1_tiles : 1; }   // default: the tap-GEMM path
 }  // namespace
 
 void conv_set_conv1_tiles(int tiles) { g_conv1_tiles = tiles > 0 ? tiles : 0; }

@@ -53,14 +53,27 @@ __global__ __launch_bounds__(kHeadThreads) void head_fwd_kernel(HeadParams p) {
   if (p.C % 8 == 0 && G <= kHeadThreads && kHeadThreads % G == 0 && (reinterpret_cast<uintptr_t>(p.z) & 15) == 0) {
     const int g = t % G, pl = t / G, PL = kHeadThreads / G;
     float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int k = pl; k < npx; k += PL) {
-      const int h = h0 + k / ww, w = w0 + k % ww;
-      const uint4 v = *reinterpret_cast<const uint4*>(p.z + (int64_t(n * p.H + h) * p.W + w) * p.C + g * 8);
-      const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+    // 4 window pixels per lane per pass, every load issued before any add: the
+    // one-pixel loop waited out a load latency per pixel (~10 per lane)
+    constexpr int UN = 4;
+    for (int k0 = pl; k0 < npx; k0 += UN * PL) {
+      uint4 v[UN];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        a[2 * q] += __uint_as_float(u[q] << 16);
-        a[2 * q + 1] += __uint_as_float(u[q] & 0xFFFF0000u);
+      for (int u = 0; u < UN; ++u) {
+        const int k = k0 + u * PL;
+        const int kk = k < npx ? k : k0;   // past the window: re-read the first pixel, added as 0 below
+        const int h = h0 + kk / ww, w = w0 + kk % ww;
+        v[u] = *reinterpret_cast<const uint4*>(p.z + (int64_t(n * p.H + h) * p.W + w) * p.C + g * 8);
+      }
+#pragma unroll
+      for (int u = 0; u < UN; ++u) {
+        if (k0 + u * PL >= npx) break;
+        const uint32_t uu[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          a[2 * q] += __uint_as_float(uu[q] << 16);
+          a[2 * q + 1] += __uint_as_float(uu[q] & 0xFFFF0000u);
+        }
       }
     }
 #pragma unroll

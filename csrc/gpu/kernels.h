@@ -358,7 +358,7 @@ struct ConvWgradParams {
 bool conv_wgrad_supported(int Cin, int Cout);
 int conv_wgrad_slices(int64_t M, int Cin, int Cout, int target_blocks);
 // Weight-gradient staging (not the 4-channel layer): 0 = register ring,
-// 2 / 3 = LDS-DMA stages of 64 pixels (default 2; -1 = BT_WGRAD_STAGING or default).
+// 2 / 3 = LDS-DMA stages of 64 pixels (default 0; -1 = BT_WGRAD_STAGING or default).
 void conv_set_wgrad_staging(int staging);
 // The slice reduce normally follows the main kernel as its own launch.
 // defer != nullptr: it is NOT launched but described in *defer, for the
@@ -408,7 +408,7 @@ void conv_set_tiles(int bm, int bn, int staging = -1, int dgrad_cls = 0);
 // would give >= 4096 blocks; BT_CONV_DGRAD_CLS / conv_set_tiles force it).
 int conv_dgrad_classes_per_block(int64_t M, int NOUT);
 // First-layer (4-channel) forward: 128-pixel tiles per block of the multi-tile
-// kernel (default 4; 1 = the one-tile tap-GEMM path; BT_CONV1_TILES).
+// kernel (default 1 = the one-tile tap-GEMM path; BT_CONV1_TILES).
 void conv_set_conv1_tiles(int tiles);
 hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream);
 // Data gradient of the same convolution (same tap-gather GEMM kernel, four

@@ -17,3 +17,4 @@ done
 bash scripts/gpurun/dopt_steady.sh
 BT_THREAD_REPORT=1 timeout -k 10 200 python bench.py --steps 2000 > gpurun_out/headline.log 2>&1 || { tail -5 gpurun_out/headline.log; exit 1; }
 grep '^{' gpurun_out/headline.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'value':d['value'],'ms':d['ms_per_step'],'producers':d['config']['producers_per_gpu'],'cpu':d['cpu']}))"
+find gpurun_out -type f -size +4M -print -delete; du -sh gpurun_out

@@ -467,7 +467,8 @@ def test_first_layer_multi_tile_forward(dev, u8, cout, wc):
         outs.append((y, s))
     ops.hip_ext().conv_set_conv1_tiles(0)
     assert torch.equal(outs[0][0], outs[1][0])
-    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-9, atol=1e-6)
+    # per-block fp32 partials over 4 tiles instead of 1: equal to fp32 rounding of those partials
+    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-6, atol=1e-3)
     wref = w.float() if wc == 4 else torch.cat([w.float(), torch.zeros(cout, 1, 4, 4, device=dev)], 1)
     ref = F.conv2d(xdec.float(), wref, None, 2, 1)
     torch.testing.assert_close(outs[0][0].float(), ref, rtol=2 ** -7, atol=1e-3 * float(ref.abs().max()))
