@@ -252,10 +252,12 @@ def main(argv=None):
     local_world = int(os.environ.get('LOCAL_WORLD_SIZE', str(world)))
 
     ensure_built()
-    # before the HIP runtime starts: 8 hardware queues, so the loader's copy /
-    # decode streams never share one with RCCL's (blendtorch.utils.ensure_hw_queues)
+    # before the HIP runtime starts: streaming alone gets 8 hardware queues, so
+    # the loader's copy / decode streams never share one with RCCL's; a training
+    # consumer keeps HIP's 4 -- its captured step with the in-graph all-reduce
+    # ran 27 % slower with 8 (profiles/r4/pg_tax.md; blendtorch.utils.ensure_hw_queues)
     from blendtorch.utils import ensure_hw_queues
-    hw_queues = ensure_hw_queues()
+    hw_queues = ensure_hw_queues(8 if args.consumer == 'none' else 4)
     import torch
     import torch.distributed as dist
     from blendtorch import btt

@@ -136,23 +136,41 @@ __device__ inline void bn_acc_column_sums(const double* acc, int R, int J, doubl
   __syncthreads();
 }
 
-// The ticket word of a [R][2][C] accumulator (kernels.h: bn_acc_elems leaves room for it)
+// The ticket words of a [R][2][C] accumulator (kernels.h: bn_acc_elems leaves
+// room for them): 8 shard counters, then the top counter.  One counter for
+// every block of a 1,024-block apply launch serialised ~1,000 returning
+// atomics on one word (~88 per us): ~12 us of a 25 us kernel.  Blocks take a
+// ticket on the shard of their blockIdx % 8 (8 words, 8 channels in
+// parallel); the last block of each shard takes one on the top counter.
+constexpr int kBnTicketShards = 8;
+constexpr int kBnTicketStride = 32;   // words: one 128-byte line per counter (atomics contend per line)
 __device__ inline unsigned* bn_acc_ticket(double* acc, int R, int C) {
   return reinterpret_cast<unsigned*>(acc + int64_t(R) * 2 * C);
 }
 
 // After every reader of this block has its values (call after the block's
 // last use of them, behind a barrier): take a ticket; the block with the
-// last one clears the replicas and resets the ticket.  `flag`: one int of LDS.
+// last one clears the replicas and resets the tickets.  `flag`: one int of
+// LDS.  1-D grids.
 __device__ inline void bn_acc_release(double* acc, int R, int C, int* flag) {
   const int t = int(threadIdx.x), nt = int(blockDim.x);
   unsigned* ticket = bn_acc_ticket(acc, R, C);
-  if (t == 0) *flag = atomicAdd(ticket, 1u) == gridDim.x * gridDim.y - 1 ? 1 : 0;
+  if (t == 0) {
+    const unsigned G = gridDim.x, s = blockIdx.x % kBnTicketShards;
+    const unsigned in_shard = (G - s + kBnTicketShards - 1) / kBnTicketShards;   // blocks s, s + 8, ...
+    const unsigned shards = G < unsigned(kBnTicketShards) ? G : unsigned(kBnTicketShards);
+    int last = 0;
+    if (atomicAdd(ticket + s * kBnTicketStride, 1u) == in_shard - 1) {
+      ticket[s * kBnTicketStride] = 0u;   // every block of this shard has taken its ticket
+      last = atomicAdd(ticket + kBnTicketShards * kBnTicketStride, 1u) == shards - 1 ? 1 : 0;
+    }
+    *flag = last;
+  }
   __syncthreads();
   if (*flag) {
     const int n = R * 2 * C;
     for (int i = t; i < n; i += nt) acc[i] = 0.0;
-    if (t == 0) *ticket = 0u;
+    if (t == 0) ticket[kBnTicketShards * kBnTicketStride] = 0u;
   }
 }
 

@@ -719,6 +719,192 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4_kernel(ConvWgradParams
 }
 
 // ---------------------------------------------------------------------------
+// The first layer's weight gradient with WAVE-PRIVATE staging.  Its 32 x 64
+// tile is 2 MFMAs per wave per 32-pixel step, so the block-shared staging of
+// conv_wgrad_c4_kernel spent its time in the per-step block barrier, with
+// the dY loaders (128 threads) doing all of the BN-backward arithmetic while
+// the other two waves waited.  Here each wave streams its own pixel steps
+// (wave w takes steps w, w + 4, ...) through its own 6 KiB of LDS: no block
+// barrier in the loop (a wave's LDS writes and reads are ordered by its own
+// lgkmcnt), every lane stages dY (and applies the BN backward to its 8
+// channels) and X, and a step is 8 MFMAs (the whole 32 x 64 tile).  The
+// four waves' tiles meet in LDS at the end.  Same slices, same reduce.
+constexpr int C4W_DY = BPX * C4_DY_ROW;          // 2 KiB: [32 px][32 co]
+constexpr int C4W_X = BPX * C4_X_ROW;            // 4 KiB: [32 px][64 kc]
+constexpr int C4W_WAVE = C4W_DY + C4W_X;
+constexpr int C4W_LDS = 4 * 32 * 64 * 4;         // the combine: 4 waves x [32][64] fp32 (32 KiB)
+static_assert(4 * C4W_WAVE + kLutBytes <= C4W_LDS, "staging fits the combine area");
+
+__global__ __launch_bounds__(kThreads) void conv_wgrad_c4w_kernel(ConvWgradParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[C4W_LDS];
+  if (run_side(p, smem)) return;
+  const bool u8in = p.lut != nullptr;
+  char* const lutl = smem + 4 * C4W_WAVE;
+  if (u8in) {
+    stage_lut(p.lut, lutl);
+    __syncthreads();
+  }
+  const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
+  const int T = p.Cout / 32;
+  const int nwg = main_blocks(p), b = int(blockIdx.x);
+  const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  const int slice = w / T, co0 = (w - slice * T) * 32;
+  const int m_begin = slice * int(p.px_per_slice);
+  const int m_end = m_begin + int(p.px_per_slice) < int(p.M) ? m_begin + int(p.px_per_slice) : int(p.M);
+  const int nsteps = m_end > m_begin ? (m_end - m_begin + BPX - 1) / BPX : 0;
+  const int mysteps = nsteps > wave ? (nsteps - wave + 3) / 4 : 0;   // steps wave, wave + 4, ...
+  char* const ws = smem + wave * C4W_WAVE;
+
+  // dY: lane -> channel chunk dc (8 channels), pixels dp and dp + 16 of the step
+  const int dc = lane & 3, dp = lane >> 2;
+  // X: lane -> pixel xp of the step, chunks xc0 .. xc0 + 3 (taps kh0, kh0 + 1 by kw 0, 2)
+  const int xp = lane & 31, kh0 = (lane >> 5) * 2;
+  const bool bnd = p.bn_dy.y != nullptr;
+  BnBwdCoef bc[8];
+  if (bnd) {
+    const float invM = 1.f / float(p.M);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = co0 + dc * 8 + i;
+      bc[i].init(p.bn_dy.mean[c], p.bn_dy.invstd[c], p.bn_dy.w[c], p.bn_dy.b[c], p.bn_dy.dw[c], p.bn_dy.db[c], invM);
+    }
+  }
+  const float slope = p.bn_dy.slope;
+  const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(p.x, int64_t(p.N) * p.H * p.W * 4 * (u8in ? 1 : 2));
+  const __amdgpu_buffer_rsrc_t rs_dy = make_rsrc(p.dy, p.M * p.Cout * 2);
+  const __amdgpu_buffer_rsrc_t rs_by = make_rsrc(bnd ? p.bn_dy.y : p.dy, p.M * p.Cout * 2);
+  PixelCursor c;
+  c.init(m_begin + wave * BPX + xp, p.Ho, p.Wo);
+  int md = m_begin + wave * BPX + dp, mx = m_begin + wave * BPX + xp;
+  uint32_t dy_byte = uint32_t(md) * uint32_t(p.Cout * 2) + uint32_t((co0 + dc * 8) * 2);
+  const uint32_t dy_step = uint32_t(4 * BPX * p.Cout * 2), dy_half = uint32_t(16 * p.Cout * 2);
+  constexpr int kDepth = 2;
+  struct Stage {
+    uint4 g[2], y[2];   // dY chunks of pixels dp, dp + 16 (y: the BN input, bnd)
+    uint32_t x[4][2];   // u8: RGBA words of the 2 pixels of each chunk; bf16: low halves
+    uint32_t xh[4][2];  // bf16: high halves
+    uint32_t ok;        // per-pixel in-image bits (u8)
+  };
+  Stage ring[kDepth];
+  auto load = [&](Stage& r) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t off = md + 16 * h < m_end ? dy_byte + uint32_t(h) * dy_half : kOOB;
+      r.g[h] = bload(rs_dy, off);
+      if (bnd) r.y[h] = bload(rs_by, off);
+    }
+    r.ok = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int kh = kh0 + (k >> 1), kw = (k & 1) * 2;
+      const int ih = 2 * c.oh - 1 + kh, iw = 2 * c.ow - 1 + kw;
+      const bool row_ok = mx < m_end && unsigned(ih) < unsigned(p.H);
+      const int e = ((c.n * p.H + ih) * p.W + iw) * 4;
+      const bool ok0 = row_ok && unsigned(iw) < unsigned(p.W), ok1 = row_ok && unsigned(iw + 1) < unsigned(p.W);
+      if (u8in) {
+        r.x[k][0] = bload4(rs_x, ok0 ? uint32_t(e) : kOOB);
+        r.x[k][1] = bload4(rs_x, ok1 ? uint32_t(e + 4) : kOOB);
+        r.ok |= (ok0 ? 1u : 0u) << (2 * k) | (ok1 ? 2u : 0u) << (2 * k);
+      } else {
+        const uint2 lo = bload8(rs_x, ok0 ? uint32_t(e) * 2u : kOOB), hi = bload8(rs_x, ok1 ? uint32_t(e + 4) * 2u : kOOB);
+        r.x[k][0] = lo.x, r.xh[k][0] = lo.y, r.x[k][1] = hi.x, r.xh[k][1] = hi.y;
+      }
+    }
+    md += 4 * BPX;
+    mx += 4 * BPX;
+    dy_byte += dy_step;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c.advance(p.Ho, p.Wo);   // 4 x 32 pixels: this wave's next step
+  };
+  auto store = [&](const Stage& r) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      uint4 d = r.g[h];
+      if (bnd) {
+        const uint32_t gw[4] = {r.g[h].x, r.g[h].y, r.g[h].z, r.g[h].w};
+        const uint32_t yw[4] = {r.y[h].x, r.y[h].y, r.y[h].z, r.y[h].w};
+        uint32_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const f32x2 pr = {bc[2 * k].gx(__uint_as_float(yw[k] << 16), __uint_as_float(gw[k] << 16), slope),
+                            bc[2 * k + 1].gx(__uint_as_float(yw[k] & 0xFFFF0000u),
+                                             __uint_as_float(gw[k] & 0xFFFF0000u), slope)};
+          o[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2));
+        }
+        // (a pixel past the slice gets a nonzero gx from its zero loads; its X
+        // row is past the slice too and staged as zeros: it adds nothing)
+        d = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+      *reinterpret_cast<uint4*>(ws + c4dy_off(dp + 16 * h, dc * 16)) = d;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int chunk = (kh0 + (k >> 1)) * 2 + (k & 1);   // im2col columns 8 chunk .. + 7
+      uint4 v;
+      if (u8in) {
+        const uint2 lo = lut_px(lutl, r.x[k][0], (r.ok >> (2 * k)) & 1u), hi = lut_px(lutl, r.x[k][1], (r.ok >> (2 * k + 1)) & 1u);
+        v = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      } else {
+        v = make_uint4(r.x[k][0], r.xh[k][0], r.x[k][1], r.xh[k][1]);
+      }
+      *reinterpret_cast<uint4*>(ws + C4W_DY + c4x_off(xp, chunk * 16)) = v;
+    }
+  };
+  int ra[2], rb[4];
+  {
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) ra[i] = c4dy_off(8 * g + q, (16 * i + 4 * pp) * 2);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) rb[j] = C4W_DY + c4x_off(8 * g + q, (16 * j + 4 * pp) * 2);
+  }
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < kDepth; ++u) load(ring[u]);
+  const int padded = (mysteps + kDepth - 1) / kDepth * kDepth;
+  for (int s0 = 0; s0 < padded; s0 += kDepth) {
+#pragma unroll
+    for (int u = 0; u < kDepth; ++u) {
+      asm volatile("" ::: "memory");
+      store(ring[u]);                            // waits for this stage's loads (counted vmcnt)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      load(ring[u]);                             // step + 2 (past the end: out of range, zeros)
+      bf16x8 a[2], bm[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = frag_at(ws, ra[i], 4 * C4_DY_ROW);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bm[j] = frag_at(ws, rb[j], 4 * C4_X_ROW);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bm[j], acc[i][j], 0, 0, 0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // fragments in registers before the next store
+    }
+  }
+  // combine the four waves' tiles: [wave][co 32][kc 64] fp32 in LDS
+  __syncthreads();
+  float* cmb = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        cmb[(wave * 32 + 16 * i + 4 * (lane >> 4) + r) * 64 + 16 * j + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+  zero_output(p);
+  float* out = p.partial + int64_t(slice) * p.Cout * 64 + co0 * 64;
+  for (int e = t; e < 32 * 64; e += kThreads)
+    out[e] = cmb[e] + cmb[32 * 64 + e] + cmb[2 * 32 * 64 + e] + cmb[3 * 32 * 64 + e];
+}
+
+// ---------------------------------------------------------------------------
 // Tap-gather GEMM: the forward convolution AND the data gradient.
 //
 //   out[pixel m][col] = sum over taps t, channels c of
@@ -1592,6 +1778,19 @@ int wgrad_staging() {
 }
 }  // namespace
 
+namespace {
+int g_c4w = -1;   // first-layer weight gradient: 1 = wave-private staging (default), 0 = block-shared; BT_C4_WAVE
+bool c4_wave_private() {
+  if (g_c4w < 0) {
+    const char* v = std::getenv("BT_C4_WAVE");
+    g_c4w = v ? (std::atoi(v) != 0 ? 1 : 0) : 1;
+  }
+  return g_c4w == 1;
+}
+}  // namespace
+
+void conv_set_c4_wave_private(int on) { g_c4w = on < 0 ? -1 : (on ? 1 : 0); }
+
 void conv_set_wgrad_staging(int staging) { g_wgrad_staging = staging == 0 || staging == 2 || staging == 3 ? staging : -1; }
 
 bool conv_wgrad_supported(int Cin, int Cout) {
@@ -1652,7 +1851,8 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
       return hipErrorInvalidValue;
     grid += 1;
   }
-  if (c4) conv_wgrad_c4_kernel<<<unsigned(grid), kThreads, 0, stream>>>(q);
+  if (c4 && c4_wave_private()) conv_wgrad_c4w_kernel<<<unsigned(grid), kThreads, 0, stream>>>(q);
+  else if (c4) conv_wgrad_c4_kernel<<<unsigned(grid), kThreads, 0, stream>>>(q);
   else if (wgrad_staging() == 2 && (p.Cin & (p.Cin - 1)) == 0 && p.Wo >= 32)
     conv_wgrad_dma_kernel<2><<<unsigned(grid), kThreads, 0, stream>>>(q);
   else if (wgrad_staging() == 3 && (p.Cin & (p.Cin - 1)) == 0 && p.Wo >= 32)

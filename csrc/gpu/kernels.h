@@ -360,6 +360,8 @@ int conv_wgrad_slices(int64_t M, int Cin, int Cout, int target_blocks);
 // Weight-gradient staging (not the 4-channel layer): 0 = register ring,
 // 2 / 3 = LDS-DMA stages of 64 pixels (default 0; -1 = BT_WGRAD_STAGING or default).
 void conv_set_wgrad_staging(int staging);
+// First-layer weight gradient: 1 = wave-private staging (default), 0 = block-shared, -1 = BT_C4_WAVE / default.
+void conv_set_c4_wave_private(int on);
 // The slice reduce normally follows the main kernel as its own launch.
 // defer != nullptr: it is NOT launched but described in *defer, for the
 // next conv_wgrad to run as extra blocks of its own launch (`side`; the

@@ -296,6 +296,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("conv_dgrad_classes_per_block", &conv_dgrad_classes_per_block);
   m.def("conv_set_wgrad_staging", &conv_set_wgrad_staging);
   m.def("conv_set_conv1_tiles", &conv_set_conv1_tiles);
+  m.def("conv_set_c4_wave_private", &conv_set_c4_wave_private);
   m.def("conv_tile_pixels", &conv_tile_pixels);
   m.def("conv_tile_channels", &conv_tile_channels);
   m.def("conv_dgrad_supported", &conv_dgrad_supported);

@@ -596,9 +596,10 @@ int bn_acc_replicas(int C) {
 }
 
 int64_t bn_acc_elems(int C) {
-  // [R][2][C] replicas + one double's room for the apply launches' ticket word (bn_fold.h)
+  // [R][2][C] replicas + the apply launches' ticket words, one 128-byte line
+  // each (bn_fold.h: 8 shards + the top counter)
   const int r = bn_acc_replicas(C);
-  return r > 0 ? int64_t(2) * C * r + 1 : -1;
+  return r > 0 ? int64_t(2) * C * r + (kBnTicketShards * kBnTicketStride + 1 + 1) / 2 : -1;
 }
 
 hipError_t bn_apply_acc(const void* x, void* y, int64_t M, int C, int dtype, BnAcc acc, float eps, float momentum,

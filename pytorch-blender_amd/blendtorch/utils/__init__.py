@@ -33,7 +33,9 @@ __all__ = ['Meter', 'trace_range', 'StreamConfig', 'get_logger', 'ensure_hw_queu
 # loader's streams then share queues with RCCL's and serialise behind them.
 # Measured on one MI355X (profiles/r4/pg_tax.md): a live 1-rank RCCL process
 # group cost streaming 3.6 % (shard) / 5.3 % (scatter) at 4 queues and 0.0 % /
-# 0.7 % at 8.
+# 0.7 % at 8 -- but the graphed training step with its in-graph RCCL
+# all-reduce ran 27 % SLOWER at 8 queues (0.6 % tax at 4), so training
+# consumers keep 4 (bench.py picks per run).
 DEFAULT_HW_QUEUES = 8
 
 

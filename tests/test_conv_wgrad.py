@@ -148,9 +148,17 @@ def test_dgrad_matches_fp32_reference(dev, N, Cin, H, W, Cout):
     torch.testing.assert_close(dx.float(), ref, rtol=2 ** -7, atol=1e-3 * float(ref.abs().max()))
 
 
+@pytest.fixture(params=[1, 0], ids=['c4wave', 'c4block'])
+def c4_staging(request):
+    """First-layer weight gradient: wave-private (1, default) or block-shared (0) staging."""
+    ops.hip_ext().conv_set_c4_wave_private(request.param)
+    yield request.param
+    ops.hip_ext().conv_set_c4_wave_private(-1)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize('N,H,W', [(2, 30, 40), (8, 480, 640), (3, 14, 18)])
-def test_first_layer_rgba_forward_and_wgrad(dev, N, H, W):
+def test_first_layer_rgba_forward_and_wgrad(dev, N, H, W, c4_staging):
     """RGBA-decoded frames into an RGB first layer: the 4-channel MFMA paths
     ignore the alpha channel (weight 0) and produce the 3-channel gradient."""
     import torch.nn.functional as F
@@ -334,7 +342,7 @@ def test_wgrad_chain_defers_slice_reduces(dev):
 
 
 @pytest.mark.gpu
-def test_first_layer_reads_raw_u8_frames_through_decode_table(dev):
+def test_first_layer_reads_raw_u8_frames_through_decode_table(dev, c4_staging):
     """Decode fused into the first convolution: raw u8 RGBA frames through the
     bf16 decode table give bit-identical forward outputs and weight gradients
     to ops.decode -> bf16 NHWC -> the same layer; and the whole disc step
@@ -395,7 +403,7 @@ def test_wgrad_chain_with_frozen_first_layer(dev):
 
 
 @pytest.mark.gpu
-def test_first_bn_backward_deferred_into_first_wgrad(dev):
+def test_first_bn_backward_deferred_into_first_wgrad(dev, c4_staging):
     """With raw u8 frames the first BN's backward apply runs inside the first
     convolution's weight-gradient kernel (ops.BnDeferred): its dY operand is
     gx computed from the BN input and output gradient while staging, with the
