@@ -980,7 +980,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   constexpr int STG = A_TILE + BN * F_ROW;
   constexpr int E_TILE = BM * T_ROW;
   constexpr int NBUF = (C4 || NST == 0) ? 2 : NST;
-  static_assert(NST == 0 || NST == 2 || NST == 3, "staging: register ring, or 2-3 LDS-DMA stages");
+  static_assert(NST == 0 || NST == 2 || NST == 3 || NST == 4, "staging: register ring, or 2-4 LDS-DMA stages");
   static_assert(NBUF * STG >= E_TILE + 4 * 2 * BN * 4, "epilogue does not fit the staging LDS");
   // the tile's row table after the staging space (not C4): {abase, vmask, obase, in range} per GEMM row
   constexpr int RT_OFF = NBUF * STG, RT = C4 ? 0 : BM * 16;
@@ -1288,12 +1288,16 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     constexpr int NL = RJ + RB;   // LDS-DMA instructions per stage per thread
     constexpr uint32_t kWaitAll = (7u << 4) | (0xFu << 8);   // vmcnt(0), no lgkm / exp wait
     constexpr uint32_t kWaitOne = kWaitAll | uint32_t(NL & 15) | (uint32_t(NL >> 4) << 14);
+    constexpr uint32_t kWaitTwo = kWaitAll | uint32_t((2 * NL) & 15) | (uint32_t((2 * NL) >> 4) << 14);
 #pragma unroll
     for (int u = 0; u < NST - 1; ++u)
       if (u < nsteps) issue(u, u);
     int cur = 0;
     for (int ks = 0; ks < nsteps; ++ks) {
-      if (NST == 3 && ks + 1 < nsteps) __builtin_amdgcn_s_waitcnt(kWaitOne);
+      // the stages younger than ks that were issued (the last steps issue none)
+      const int younger = nsteps - 1 - ks < NST - 2 ? nsteps - 1 - ks : NST - 2;
+      if (younger >= 2) __builtin_amdgcn_s_waitcnt(kWaitTwo);
+      else if (younger == 1) __builtin_amdgcn_s_waitcnt(kWaitOne);
       else __builtin_amdgcn_s_waitcnt(kWaitAll);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -1917,7 +1921,7 @@ int staging() {
   if (g_staging < 0) {
     const char* v = std::getenv("BT_CONV_STAGING");
     const int e = v ? std::atoi(v) : 2;
-    g_staging = e == 0 || e == 2 || e == 3 ? e : 2;
+    g_staging = e == 0 || e == 2 || e == 3 || e == 4 ? e : 2;
   }
   return g_staging;
 }
@@ -1927,6 +1931,7 @@ void launch_tap_gemm_st(const TapGemm& g, int bn, unsigned ytiles, hipStream_t s
   switch (staging()) {
     case 0: launch_tap_gemm_bm<DGRAD, BM, 0>(g, bn, ytiles, stream); break;
     case 3: launch_tap_gemm_bm<DGRAD, BM, 3>(g, bn, ytiles, stream); break;
+    case 4: launch_tap_gemm_bm<DGRAD, BM, 4>(g, bn, ytiles, stream); break;
     default: launch_tap_gemm_bm<DGRAD, BM, 2>(g, bn, ytiles, stream); break;
   }
 }
@@ -1965,7 +1970,7 @@ int conv_dgrad_classes_per_block(int64_t M, int NOUT) {
 void conv_set_tiles(int bm, int bn, int staging, int dgrad_cls) {
   g_force_bm = bm == 64 || bm == 128 ? bm : 0;
   g_force_bn = bn == 32 || bn == 64 || bn == 128 ? bn : 0;
-  g_staging = staging == 0 || staging == 2 || staging == 3 ? staging : -1;
+  g_staging = staging == 0 || staging == 2 || staging == 3 || staging == 4 ? staging : -1;
   g_dgrad_cls = dgrad_cls == 1 || dgrad_cls == 4 ? dgrad_cls : 0;
 }
 

@@ -232,7 +232,7 @@ def tiles(request):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('tiles', [(bm, bn, st, 0) for st in (0, 2, 3) for bm in (64, 128) for bn in (32, 64, 128)]
+@pytest.mark.parametrize('tiles', [(bm, bn, st, 0) for st in (0, 2, 3, 4) for bm in (64, 128) for bn in (32, 64, 128)]
                          + [(bm, bn, 2, cls) for cls in (1, 4) for bm in (64, 128) for bn in (32, 64)],
                          indirect=True, ids=lambda t: f'bm{t[0]}_bn{t[1]}_st{t[2]}_cls{t[3]}')
 def test_tap_gemm_tile_variants(dev, tiles):
