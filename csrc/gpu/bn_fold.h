@@ -151,12 +151,12 @@ __device__ inline unsigned* bn_acc_ticket(double* acc, int R, int C) {
 // After every reader of this block has its values (call after the block's
 // last use of them, behind a barrier): take a ticket; the block with the
 // last one clears the replicas and resets the tickets.  `flag`: one int of
-// LDS.  1-D grids.
-__device__ inline void bn_acc_release(double* acc, int R, int C, int* flag) {
+// LDS.  `blk` / `nblk`: this block's linear index and the grid's block count.
+__device__ inline void bn_acc_release(double* acc, int R, int C, int* flag, unsigned blk, unsigned nblk) {
   const int t = int(threadIdx.x), nt = int(blockDim.x);
   unsigned* ticket = bn_acc_ticket(acc, R, C);
   if (t == 0) {
-    const unsigned G = gridDim.x, s = blockIdx.x % kBnTicketShards;
+    const unsigned G = nblk, s = blk % kBnTicketShards;
     const unsigned in_shard = (G - s + kBnTicketShards - 1) / kBnTicketShards;   // blocks s, s + 8, ...
     const unsigned shards = G < unsigned(kBnTicketShards) ? G : unsigned(kBnTicketShards);
     int last = 0;
@@ -171,6 +171,39 @@ __device__ inline void bn_acc_release(double* acc, int R, int C, int* flag) {
     const int n = R * 2 * C;
     for (int i = t; i < n; i += nt) acc[i] = 0.0;
     if (t == 0) ticket[kBnTicketShards * kBnTicketStride] = 0u;
+  }
+}
+__device__ inline void bn_acc_release(double* acc, int R, int C, int* flag) {   // 1-D grids
+  bn_acc_release(acc, R, C, flag, blockIdx.x, gridDim.x);
+}
+
+// The forward finalize of a folded accumulator (part[c] = sum, part[C + c] =
+// sum of squares over M elements; bn_acc_column_sums), exactly as
+// bn_fold_block computes it: mean and invstd of channel c; the block that
+// passes `first` also writes the outputs and running statistics.
+struct BnFwdFinal {
+  float eps = 0.f, momentum = 0.f;
+  float* mean = nullptr;
+  float* invstd = nullptr;
+  float* rm = nullptr;
+  float* rv = nullptr;
+  int64_t* tracked = nullptr;
+};
+__device__ inline void bn_fwd_finalize(const BnFwdFinal& f, const double* part, int C, int64_t M, int c, bool first,
+                                       float& mean, float& invstd) {
+  const double mu = part[c] / double(M);
+  double var = part[C + c] / double(M) - mu * mu;
+  var = var < 0.0 ? 0.0 : var;
+  mean = float(mu);
+  invstd = float(1.0 / sqrt(var + double(f.eps)));
+  if (first) {
+    f.mean[c] = mean;
+    f.invstd[c] = invstd;
+    if (f.rm) {
+      f.rm[c] = float((1.0 - f.momentum) * f.rm[c] + f.momentum * mu);
+      f.rv[c] = float((1.0 - f.momentum) * f.rv[c] + f.momentum * var * double(M) / double(M > 1 ? M - 1 : 1));
+    }
+    if (f.tracked && c == 0) f.tracked[0] += 1;
   }
 }
 

@@ -1532,38 +1532,59 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
 
 // ---------------------------------------------------------------------------
 // The first layer's forward (4-channel RGBA input, raw u8 through the decode
-// table or decoded bf16; K = 16 taps x 4 = one MFMA k-step) over T
-// consecutive 128-pixel tiles per block.  As one tile per block (the C4 path
-// of tap_gemm_kernel, 4,800 blocks of 4 MFMAs per wave at 640x480 x 8) the
-// kernel was all prologue and epilogue: table staging, weight tile, row
-// arithmetic, a load -> wait -> compute -> store chain per block and 64 fp64
-// atomics per tile.  Here the table and the weight tile are staged once, the
-// next tile's frame loads are in flight while this tile computes and stores,
-// and the BatchNorm sums stay in registers until the block's last tile.
-template <int BN>
+// table or decoded bf16; K = 16 taps x 4 channels = 64) from a decoded input
+// PATCH.  As an im2col GEMM (the C4 path of tap_gemm_kernel) each output
+// pixel gathers its 16 input pixels -- a stride-2 4x4 window re-reads every
+// input pixel 4 times, so the LUT decode and the A-tile stores ran 4x per
+// input pixel, and the kernel was VALU/LDS bound at ~51 VALU per MFMA
+// (profiles/r4/disc_pmc_b2.txt).  Here a block decodes the (2 TR + 2) x 130
+// input pixels under a TR x 64 output tile ONCE into LDS (8 bytes a pixel,
+// rows of 1,040 bytes) and reads each MFMA operand straight out of it: the
+// k-chunk (kh, kw..kw+1) of output pixel (r, c) is the 16 bytes at patch
+// (2r + kh, 2c + kw), 16-byte aligned because the patch starts one pixel
+// left of the tile's first input column.
+//
+// The weights are the MFMA's A operand (rows = output channels, held in
+// registers for the whole block) and the patch the B operand (columns =
+// pixels), so a lane's accumulator holds 4 channels of ONE pixel; fragment
+// pairs map their rows to channels 8g..8g+7 of a 32-channel group (lane group
+// g), and the lane writes them with one 16-byte store -- no LDS epilogue.
+// T tiles per block: the table and weights are staged once, the next tile's
+// frame loads are in flight while this tile computes, and the BatchNorm sums
+// stay in registers until the block's last tile.
+constexpr int kC1Cols = 64;   // output columns per tile
+
+__device__ __forceinline__ int c1_row_chan(int f, int rho) {   // A row rho of channel fragment f
+  return 32 * (f >> 1) + 8 * (rho >> 2) + 4 * (f & 1) + (rho & 3);
+}
+
+template <int BN, int TR, bool U8>
 __global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tiles_per_block) {
-  constexpr int BM = FBM, RJ = BM / 32, RB = BN / 32;
-  constexpr int WGM = BN >= 64 ? 2 : 4, WGN = 4 / WGM;
-  constexpr int FM = BM / WGM / 16, FN = BN / WGN / 16;
-  constexpr int A_TILE = BM * F_ROW;                 // 16 KB, reused as the epilogue tile
-  constexpr int T_ROW = BN >= 64 ? BN * 2 : F_ROW;
-  static_assert(BM * T_ROW <= A_TILE, "epilogue tile");
-  constexpr int B_OFF = A_TILE, LUT_OFF = B_OFF + BN * F_ROW, RED_OFF = LUT_OFF + kLutBytes;
-  __shared__ __attribute__((aligned(16))) char smem[RED_OFF + WGM * 2 * BN * 4];
+  constexpr int PR = 2 * TR + 2, PC = 2 * kC1Cols + 2, PX = PR * PC;
+  constexpr int NL = (PX + kThreads - 1) / kThreads;   // patch pixels per thread
+  constexpr int FC = BN / 16, CP = BN / 32;            // channel fragments, 32-channel groups
+  constexpr int PF = TR * kC1Cols / 16 / 4;            // 16-pixel fragments per wave
+  constexpr int LUT_OFF = PX * 8, RED_OFF = LUT_OFF + kLutBytes;
+  static_assert(PF >= 1 && (TR * kC1Cols) % 64 == 0, "tile");
+  __shared__ __attribute__((aligned(16))) char smem[RED_OFF + 4 * 2 * BN * 4];
   float* red = reinterpret_cast<float*>(smem + RED_OFF);
   const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
-  const int ntiles = (p.M + BM - 1) / BM;
+  const int tiles_r = (p.OH + TR - 1) / TR, tiles_c = (p.OW + kC1Cols - 1) / kC1Cols;
+  const int ntiles = p.N * tiles_r * tiles_c;
   const int tile0 = int(blockIdx.x) * tiles_per_block;
   const int tile1 = tile0 + tiles_per_block < ntiles ? tile0 + tiles_per_block : ntiles;
-  const bool u8in = p.lut != nullptr;
-  const int ar = t >> 3, ac = t & 7;
-  const int kh = ac >> 1, kw = (ac & 1) * 2;          // this thread's tap pair of its rows
+  constexpr bool u8in = U8;   // raw u8 frames through the table (a template parameter: a runtime branch
+                              // between the load kinds put the in-flight words in scratch)
   if (u8in) stage_lut(p.lut, smem + LUT_OFF);
-  {   // the weight tile, once: rows co = ar + 32 j, chunk ac = taps (kh, kw), (kh, kw + 1)
-    const int tap = kh * 4 + kw;
+  // the weights, once, as A fragments: row rho of fragment f = channel c1_row_chan(f, rho);
+  // k-chunk 4 kk + (lane >> 4) = taps (kh, kw), (kh, kw + 1), kh = chunk >> 1, kw = 2 (chunk & 1)
+  bf16x8 wa[FC][2];
 #pragma unroll
-    for (int j = 0; j < RB; ++j) {
-      const int co = ar + 32 * j;
+  for (int f = 0; f < FC; ++f)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int co = c1_row_chan(f, lane & 15), chunk = 4 * kk + (lane >> 4);
+      const int tap = (chunk >> 1) * 4 + (chunk & 1) * 2;
       uint4 v;
       if (p.wc == 4) {
         v = *reinterpret_cast<const uint4*>(p.w + (co * 16 + tap) * 4);
@@ -1572,173 +1593,134 @@ __global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tile
         v = make_uint4(uint32_t(q[0]) | (uint32_t(q[1]) << 16), uint32_t(q[2]),
                        uint32_t(q[3]) | (uint32_t(q[4]) << 16), uint32_t(q[5]));
       }
-      *reinterpret_cast<uint4*>(smem + B_OFF + f_off(co, ac)) = v;
+      wa[f][kk] = __builtin_bit_cast(bf16x8, v);
     }
-  }
   const __amdgpu_buffer_rsrc_t rs_src = make_rsrc(p.src, int64_t(p.N) * p.SH * p.SW * p.C * (u8in ? 1 : 2));
-  // the thread's rows ar + 32 j of the tile being loaded: (n, a, b) of the first by
-  // division, the others by stepping; the next tile's by stepping 128 pixels
-  int gn, ga, gb;
-  {
-    const int m = tile0 * BM + ar < p.M ? tile0 * BM + ar : 0;
-    gn = m / (p.GH * p.GW);
-    const int rem = m - gn * (p.GH * p.GW);
-    ga = rem / p.GW;
-    gb = rem - ga * p.GW;
-  }
-  auto step = [&](int& n, int& a, int& b, int by) {
-    b += by;
-    while (b >= p.GW) {
-      b -= p.GW;
-      if (++a == p.GH) a = 0, ++n;
-    }
-  };
-  uint32_t w0[RJ], w1[RJ];   // raw pixels (u8: RGBA word; bf16: low half), in flight across a tile
-  uint32_t h0[RJ], h1[RJ];   // bf16 input: the high half
-  bool k0[RJ], k1[RJ];
-  auto load_raw = [&](int tile) {
-    int n = gn, a = ga, b = gb;
+  // this thread's patch pixels u = t + 256 i: (row, column) within the patch
+  int pr[NL], pc[NL];
 #pragma unroll
-    for (int j = 0; j < RJ; ++j) {
-      if (j > 0) step(n, a, b, 32);
-      const int m = tile * BM + ar + 32 * j;
-      const int r0 = 2 * a - 1, c0 = 2 * b - 1;
-      const bool rok = m < p.M && unsigned(r0 + kh) < unsigned(p.SH);
-      const int e = ((n * p.SH + r0 + kh) * p.SW + c0 + kw) * 4;
-      k0[j] = rok && unsigned(c0 + kw) < unsigned(p.SW);
-      k1[j] = rok && unsigned(c0 + kw + 1) < unsigned(p.SW);
-      if (u8in) {
-        w0[j] = bload4(rs_src, k0[j] ? uint32_t(e) : kOOB);
-        w1[j] = bload4(rs_src, k1[j] ? uint32_t(e + 4) : kOOB);
+  for (int i = 0; i < NL; ++i) {
+    const int u = t + kThreads * i;
+    pr[i] = u < PX ? u / PC : -8;   // past the patch: never in range
+    pc[i] = u - (u / PC) * PC;
+  }
+  uint32_t w0[NL], w1[NL];   // raw pixels in flight (u8: the RGBA word; bf16: two words)
+  bool ok[NL];
+  auto load_patch = [&](int tile) __attribute__((always_inline)) {
+    const int n = tile / (tiles_r * tiles_c), rem = tile - n * (tiles_r * tiles_c);
+    const int r0 = 2 * (rem / tiles_c) * TR - 1, c0 = 2 * (rem % tiles_c) * kC1Cols - 1;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int ir = r0 + pr[i], ic = c0 + pc[i];
+      ok[i] = unsigned(ir) < unsigned(p.SH) && unsigned(ic) < unsigned(p.SW);
+      const uint32_t e = uint32_t(((n * p.SH + ir) * p.SW + ic) * 4);
+      if constexpr (u8in) {
+        w0[i] = bload4(rs_src, ok[i] ? e : kOOB);
       } else {
-        const uint2 lo = bload8(rs_src, k0[j] ? uint32_t(e) * 2u : kOOB);
-        const uint2 hi = bload8(rs_src, k1[j] ? uint32_t(e + 4) * 2u : kOOB);
-        w0[j] = lo.x, h0[j] = lo.y, w1[j] = hi.x, h1[j] = hi.y;
+        const uint2 v = bload8(rs_src, ok[i] ? e * 2u : kOOB);
+        w0[i] = v.x, w1[i] = v.y;
       }
     }
-    step(gn, ga, gb, BM);   // the next tile's first row
   };
-  const int st_a = f_off(ar, ac);
-  auto store_a = [&]() {
+  auto store_patch = [&]() __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < RJ; ++j) {
-      uint4 v;
-      if (u8in) {
-        const uint2 lo = lut_px(smem + LUT_OFF, w0[j], k0[j]), hi = lut_px(smem + LUT_OFF, w1[j], k1[j]);
-        v = make_uint4(lo.x, lo.y, hi.x, hi.y);
-      } else {
-        v = make_uint4(w0[j], h0[j], w1[j], h1[j]);
-      }
-      *reinterpret_cast<uint4*>(smem + st_a + j * 32 * F_ROW) = v;
+    for (int i = 0; i < NL; ++i) {
+      const uint2 v = u8in ? lut_px(smem + LUT_OFF, w0[i], ok[i]) : make_uint2(w0[i], w1[i]);
+      if ((i + 1) * kThreads <= PX || t + kThreads * i < PX) *reinterpret_cast<uint2*>(smem + (t + kThreads * i) * 8) = v;
     }
   };
-  const int wm = wave / WGN, wn = wave % WGN;
-  const int row0 = wm * (BM / WGM), col0 = wn * (BN / WGN);
-  int fa[FM][2], fb[FN][2];
+  // the B fragments' patch offsets (tile-invariant): pixel fragment j of this
+  // wave = output row fi / 4, columns 16 (fi % 4) .. +15
+  int boff[PF][2];
 #pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    const int chunk = 4 * kk + (lane >> 4);
-#pragma unroll
-    for (int i = 0; i < FM; ++i) fa[i][kk] = f_off(row0 + 16 * i + (lane & 15), chunk);
-#pragma unroll
-    for (int j = 0; j < FN; ++j) fb[j][kk] = B_OFF + f_off(col0 + 16 * j + (lane & 15), chunk);
-  }
-  const int lr = 4 * (lane >> 4);
-  int toff[FN][4];
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int col = col0 + 16 * j + (lane & 15);
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      toff[j][r] = (row0 + lr + r) * (T_ROW / 2) + ((((col >> 3) ^ ((lr + r) & 7)) << 4) >> 1) + (col & 7);
-  }
-  constexpr int CPR = BN / 8, RPP = kThreads / CPR, NJ = BM / RPP;
-  const int ec = t % CPR;
-  float sum[FN], sq[FN];
-#pragma unroll
-  for (int j = 0; j < FN; ++j) sum[j] = sq[j] = 0.f;
-  uint16_t* tile_lds = reinterpret_cast<uint16_t*>(smem);
-
-  if (tile0 < tile1) load_raw(tile0);
-  for (int tile = tile0; tile < tile1; ++tile) {
-    __syncthreads();                 // previous tile's epilogue done with the LDS (and, first, the tables)
-    store_a();                       // decode (LUT lookups wait for this tile's loads)
-    if (tile + 1 < tile1) load_raw(tile + 1);   // in flight while this tile computes and stores
-    __syncthreads();
-    f32x4 acc[FM][FN];
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < PF; ++j) {
+    const int fi = wave * PF + j, r = fi >> 2, c = 16 * (fi & 3) + (lane & 15);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 a[FM], bb[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const bf16x8*>(smem + fa[i][kk]);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) bb[j] = *reinterpret_cast<const bf16x8*>(smem + fb[j][kk]);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bb[j], acc[i][j], 0, 0, 0);
+      const int chunk = 4 * kk + (lane >> 4);
+      boff[j][kk] = ((2 * r + (chunk >> 1)) * PC + 2 * c + 2 * (chunk & 1)) * 8;
     }
-    __syncthreads();                 // every wave has its fragments: the A tile becomes the output tile
-    const int m0 = tile * BM;
-    const bool all_rows = m0 + BM <= p.M;
+  }
+  const int g = lane >> 4;
+  float sum[CP][8], sq[CP][8];
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+  for (int q = 0; q < CP; ++q)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        uint32_t pk[2];
-#pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2) {
-          const f32x2 pr = {acc[i][j][2 * h2], acc[i][j][2 * h2 + 1]};
-          pk[h2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2));
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const uint32_t w2 = pk[r >> 1];
-          tile_lds[toff[j][r] + i * 16 * (T_ROW / 2)] = uint16_t(r & 1 ? w2 >> 16 : w2);
-          if (all_rows || m0 + row0 + 16 * i + lr + r < p.M) {
-            const float vr = __uint_as_float(r & 1 ? w2 & 0xFFFF0000u : w2 << 16);
-            sum[j] += vr;
-            sq[j] += vr * vr;
-          }
-        }
-      }
+    for (int e = 0; e < 8; ++e) sum[q][e] = sq[q][e] = 0.f;
+
+  if (tile0 < tile1) load_patch(tile0);
+  for (int tile = tile0; tile < tile1; ++tile) {
+    __syncthreads();                 // the previous tile's fragment reads are done (and, first, the table)
+    store_patch();                   // decode (the table lookups wait for this tile's loads)
+    if (tile + 1 < tile1) load_patch(tile + 1);   // in flight while this tile computes and stores
     __syncthreads();
+    f32x4 acc[FC][PF];
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int er = t / CPR + RPP * j, m = m0 + er;
-      if (m < p.M) {
-        const uint4 v = *reinterpret_cast<const uint4*>(smem + er * T_ROW + ((ec ^ (er & 7)) << 4));
-        *reinterpret_cast<uint4*>(p.dst + int64_t(m) * p.NOUT + ec * 8) = v;
+    for (int f = 0; f < FC; ++f)
+#pragma unroll
+      for (int j = 0; j < PF; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 b[PF];
+#pragma unroll
+      for (int j = 0; j < PF; ++j) b[j] = *reinterpret_cast<const bf16x8*>(smem + boff[j][kk]);
+#pragma unroll
+      for (int f = 0; f < FC; ++f)
+#pragma unroll
+        for (int j = 0; j < PF; ++j)
+          acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[f][kk], b[j], acc[f][j], 0, 0, 0);
+    }
+    const int n = tile / (tiles_r * tiles_c), rem = tile - n * (tiles_r * tiles_c);
+    const int orow0 = (rem / tiles_c) * TR, ocol0 = (rem % tiles_c) * kC1Cols;
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      const int fi = wave * PF + j;
+      const int orow = orow0 + (fi >> 2), ocol = ocol0 + 16 * (fi & 3) + (lane & 15);
+      if (orow >= p.OH || ocol >= p.OW) continue;
+      uint16_t* out = p.dst + (int64_t(n * p.OH + orow) * p.OW + ocol) * p.NOUT + 8 * g;
+#pragma unroll
+      for (int q = 0; q < CP; ++q) {
+        uint32_t pk[4];
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {   // channels 8g + 2h, +1: fragment 2q + (h >> 1), rows 2 (h & 1), +1
+          const f32x4& a = acc[2 * q + (h >> 1)][j];
+          const f32x2 pr2 = {a[2 * (h & 1)], a[2 * (h & 1) + 1]};
+          pk[h] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr2, bf16x2));
+          const float lo = __uint_as_float(pk[h] << 16), hi = __uint_as_float(pk[h] & 0xFFFF0000u);
+          sum[q][2 * h] += lo, sq[q][2 * h] += lo * lo;
+          sum[q][2 * h + 1] += hi, sq[q][2 * h + 1] += hi * hi;
+        }
+        *reinterpret_cast<uint4*>(out + 32 * q) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
       }
     }
   }
   if (!p.stats) return;
-  // the block's BatchNorm sums: lanes l, l^16, l^32, l^48 hold a channel, then the WGM row groups
+  // the block's BatchNorm sums: the 16 lanes of a group hold the same 8 channels
 #pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    sum[j] += __shfl_xor(sum[j], 16);
-    sum[j] += __shfl_xor(sum[j], 32);
-    sq[j] += __shfl_xor(sq[j], 16);
-    sq[j] += __shfl_xor(sq[j], 32);
-  }
-  if (lane < 16) {
+  for (int q = 0; q < CP; ++q)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      red[(wm * 2 + 0) * BN + col0 + 16 * j + lane] = sum[j];
-      red[(wm * 2 + 1) * BN + col0 + 16 * j + lane] = sq[j];
+    for (int e = 0; e < 8; ++e) {
+#pragma unroll
+      for (int s = 1; s < 16; s <<= 1) {
+        sum[q][e] += __shfl_xor(sum[q][e], s);
+        sq[q][e] += __shfl_xor(sq[q][e], s);
+      }
     }
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int q = 0; q < CP; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(wave * 2 + 0) * BN + 32 * q + 8 * g + e] = sum[q][e];
+        red[(wave * 2 + 1) * BN + 32 * q + 8 * g + e] = sq[q][e];
+      }
   }
   __syncthreads();
   if (t < 2 * BN) {
     const int which = t / BN, c = t - which * BN;
     float v = 0.f;
 #pragma unroll
-    for (int g = 0; g < WGM; ++g) v += red[(g * 2 + which) * BN + c];
+    for (int w = 0; w < 4; ++w) v += red[(w * 2 + which) * BN + c];
     unsafeAtomicAdd(reinterpret_cast<double*>(p.stats) + ((int(blockIdx.x) % p.acc_r) * 2 + which) * p.NOUT + c,
                     double(v));
   }
@@ -1952,11 +1934,17 @@ int env_int(const char* name) {
 int g_force_bm = env_int("BT_CONV_BM");
 int g_force_bn = env_int("BT_CONV_BN");
 int g_dgrad_cls = env_int("BT_CONV_DGRAD_CLS");   // 1 / 4: force the data gradient's classes per block
-int g_conv1_tiles = env_int("BT_CONV1_TILES");     // first-layer forward: tiles per block (1 = the tap-GEMM path)
-int conv1_tiles() { return g_conv1_tiles > 0 ? g_conv1_tiles : 1; }   // default: the tap-GEMM path
+// first-layer forward: tiles per block of the patch kernel (0 = the im2col tap-GEMM path), output rows per tile
+int g_conv1_tiles = env_int("BT_CONV1_TILES");
+int g_conv1_rows = env_int("BT_CONV1_ROWS");
+int conv1_tiles() { return g_conv1_tiles > 0 ? g_conv1_tiles : g_conv1_tiles < 0 ? 0 : 4; }
+int conv1_rows() { return g_conv1_rows == 4 ? 4 : 2; }
 }  // namespace
 
-void conv_set_conv1_tiles(int tiles) { g_conv1_tiles = tiles > 0 ? tiles : 0; }
+void conv_set_conv1_tiles(int tiles, int rows) {   // tiles: > 0 patch kernel, -1 the tap-GEMM path, 0 default
+  g_conv1_tiles = tiles;
+  g_conv1_rows = rows;
+}
 
 int conv_dgrad_classes_per_block(int64_t M, int NOUT) {
   // one parity class per block unless that makes >= 4096 blocks (the
@@ -2014,15 +2002,25 @@ hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream) {
   g.acc_r = p.stats ? p.acc_r : 0;
   if (g.acc_r < 0 || g.acc_r > 64) return hipErrorInvalidValue;
   if (p.Cin == 4 && g.wc != 3 && g.wc != 4) return hipErrorInvalidValue;
-  // the first layer over several tiles per block (conv1_fwd_kernel): BN sums
-  // into an accumulator (or none), 128-pixel tiles, Cout 32 / 64
-  const int64_t t128 = (g.M + FBM - 1) / FBM;
+  // the first layer from a decoded input patch (conv1_fwd_kernel): BN sums
+  // into an accumulator (or none), Cout 32 / 64
   const int bn1 = conv_tile_channels(p.Cout, true);
-  if (p.Cin == 4 && (!p.stats || g.acc_r > 0) && p.Cout == bn1 && t128 >= 1024 && conv1_tiles() > 1) {
-    const int tpb = conv1_tiles();
-    const int64_t blocks = (t128 + tpb - 1) / tpb;
-    if (bn1 == 64) conv1_fwd_kernel<64><<<unsigned(blocks), kThreads, 0, stream>>>(g, tpb);
-    else conv1_fwd_kernel<32><<<unsigned(blocks), kThreads, 0, stream>>>(g, tpb);
+  if (p.Cin == 4 && (!p.stats || g.acc_r > 0) && p.Cout == bn1 && conv1_tiles() > 0) {
+    const int tr = conv1_rows(), tpb = conv1_tiles();
+    const int64_t ntiles = int64_t(p.N) * ((p.Ho + tr - 1) / tr) * ((p.Wo + kC1Cols - 1) / kC1Cols);
+    const unsigned blocks = unsigned((ntiles + tpb - 1) / tpb);
+    const dim3 grid(blocks);
+    const bool u8 = g.lut != nullptr;
+#define BT_CONV1(BN_, TR_)                                                   \
+    do {                                                                     \
+      if (u8) conv1_fwd_kernel<BN_, TR_, true><<<grid, kThreads, 0, stream>>>(g, tpb);  \
+      else conv1_fwd_kernel<BN_, TR_, false><<<grid, kThreads, 0, stream>>>(g, tpb);    \
+    } while (0)
+    if (bn1 == 64 && tr == 4) BT_CONV1(64, 4);
+    else if (bn1 == 64) BT_CONV1(64, 2);
+    else if (tr == 4) BT_CONV1(32, 4);
+    else BT_CONV1(32, 2);
+#undef BT_CONV1
     return hipGetLastError();
   }
   launch_tap_gemm<false>(g, 1, stream);

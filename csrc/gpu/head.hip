@@ -17,6 +17,7 @@
 
 #include <cstdint>
 
+#include "bn_fold.h"
 #include "kernels.h"
 
 namespace btn {
@@ -53,6 +54,41 @@ __global__ __launch_bounds__(kHeadThreads) void head_fwd_kernel(HeadParams p) {
   if (p.C % 8 == 0 && G <= kHeadThreads && kHeadThreads % G == 0 && (reinterpret_cast<uintptr_t>(p.z) & 15) == 0) {
     const int g = t % G, pl = t / G, PL = kHeadThreads / G;
     float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    // act.on(): fold the BN statistics (every block; block (0, 0) writes the
+    // outputs, the last block clears the accumulator) into this lane's 8
+    // channels' xhat = v is + nm, z = xhat w + b
+    const bool act = p.act.on();
+    float is[8], nm[8], aw[8], ab[8];
+    if (act) {
+      __shared__ double fold[2 * kBnFoldMaxC];
+      __shared__ float coef[2 * kBnFoldMaxC];
+      __shared__ int flag;
+      bn_acc_column_sums(p.act.acc, p.act.R, 2 * p.C, fold);
+      BnFwdFinal f;
+      f.eps = p.act.eps, f.momentum = p.act.momentum, f.mean = p.act.mean, f.invstd = p.act.invstd;
+      f.rm = p.act.rm, f.rv = p.act.rv, f.tracked = p.act.tracked;
+      const bool first = blockIdx.x == 0 && blockIdx.y == 0;
+      for (int c = t; c < p.C; c += kHeadThreads) bn_fwd_finalize(f, fold, p.C, p.act.M, c, first, coef[c], coef[p.C + c]);
+      __syncthreads();
+      bn_acc_release(p.act.acc, p.act.R, p.C, &flag, blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        is[q] = coef[p.C + g * 8 + q];
+        nm[q] = -coef[g * 8 + q] * is[q];
+        aw[q] = p.act.w[g * 8 + q];
+        ab[q] = p.act.b[g * 8 + q];
+      }
+    }
+    // leaky(bn(v)) of channels q, q + 1 rounded to bf16 (RNE, v_cvt_pk_bf16_f32) -- the
+    // values the apply kernel would have stored -- added into a[q], a[q + 1]
+    auto act_add = [&](uint32_t word, int q) {
+      const float z0 = fmaf(fmaf(__uint_as_float(word << 16), is[q], nm[q]), aw[q], ab[q]);
+      const float z1 = fmaf(fmaf(__uint_as_float(word & 0xFFFF0000u), is[q + 1], nm[q + 1]), aw[q + 1], ab[q + 1]);
+      const f32x2 pr = {z0 > 0.f ? z0 : z0 * p.act.slope, z1 > 0.f ? z1 : z1 * p.act.slope};
+      const uint32_t r = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2));
+      a[q] += __uint_as_float(r << 16);
+      a[q + 1] += __uint_as_float(r & 0xFFFF0000u);
+    };
     // 4 window pixels per lane per pass, every load issued before any add: the
     // one-pixel loop waited out a load latency per pixel (~10 per lane)
     constexpr int UN = 4;
@@ -69,10 +105,15 @@ __global__ __launch_bounds__(kHeadThreads) void head_fwd_kernel(HeadParams p) {
       for (int u = 0; u < UN; ++u) {
         if (k0 + u * PL >= npx) break;
         const uint32_t uu[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+        if (act) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          a[2 * q] += __uint_as_float(uu[q] << 16);
-          a[2 * q + 1] += __uint_as_float(uu[q] & 0xFFFF0000u);
+          for (int q = 0; q < 4; ++q) act_add(uu[q], 2 * q);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            a[2 * q] += __uint_as_float(uu[q] << 16);
+            a[2 * q + 1] += __uint_as_float(uu[q] & 0xFFFF0000u);
+          }
         }
       }
     }
@@ -150,13 +191,20 @@ __device__ void head_loss_wave(const HeadParams& p, bool wt) {
 
 __global__ __launch_bounds__(64) void head_loss_kernel(HeadParams p) { head_loss_wave(p, false); }
 
-// Backward in ONE launch: blocks [0, nbwd) write dz (8 channels of one pixel
-// per lane, one 16-byte store), blocks [nbwd, ...) the weight gradient.
+// Backward in ONE launch: blocks [0, nbwd) write dz, blocks [nbwd, ...) the
+// weight gradient.  dz[n][h][w][c] = g dlogit_n * M[h][w][c], where M (the
+// pooling-folded head weight seen by pixel (h, w): the sum of w[c][i][j] /
+// |window(i, j)| over the windows holding it) does not depend on the image:
+// a dz block takes PXB consecutive pixels of one row (PXB = 256 / (C / 8)
+// lanes of 8 channels each), works out its lanes' M once and walks the N
+// images with all their loads in flight (one pixel per lane per image was
+// the old form: window search, divisions and weight gathers per element,
+// 17.5 us for 8x30x40x256 at 0.56 TB/s).
 // With p.bn_acc the dz blocks also sum the producing BatchNorm+LeakyReLU
-// backward's gz and gz * xhat per channel: a lane keeps one channel group
-// over the whole grid-stride loop (the stride is a multiple of C / 8), the
-// block folds its lanes through LDS and adds its 2 C sums into replica
-// blockIdx % R of the fp64 accumulator.
+// backward's gz and gz * xhat per channel; the block folds its lanes through
+// LDS and adds its 2 C sums into replica blockIdx % R of the fp64 accumulator.
+constexpr int kHeadImgs = 4;   // images per pass (loads in flight per lane)
+
 __global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p, int nbwd) {
   const int t = int(threadIdx.x);
   const float g = p.gscale[0];
@@ -173,35 +221,14 @@ __global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p, in
     }
     return;
   }
-  // 32-bit index math (the host checks N*H*W*C/8 < 2^31): 64-bit division
-  // and modulo made this an ALU-bound kernel
-  const int groups = p.C / 8;
-  const int total = p.N * p.H * p.W * groups;
+  const int groups = p.C / 8, PXB = kHeadThreads / groups;
+  const int wblocks = (p.W + PXB - 1) / PXB;
+  const int h = int(blockIdx.x) / wblocks, w = (int(blockIdx.x) - h * wblocks) * PXB + t / groups;
+  const int c0 = (t % groups) * 8;
+  const bool live = t < PXB * groups && w < p.W;
   const bool bnf = p.bn_acc != nullptr;
-  const int c0l = (t % groups) * 8;   // this lane's channel group (fixed: the stride is a multiple of groups)
-  float is[8], nm[8], bw[8], bb[8], bs[8], bq[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    bs[q] = bq[q] = 0.f;
-    if (bnf) {
-      is[q] = p.bn_invstd[c0l + q];
-      nm[q] = -p.bn_mean[c0l + q] * is[q];
-      bw[q] = p.bn_w[c0l + q];
-      bb[q] = p.bn_b[c0l + q];
-    }
-  }
-  for (int e = int(blockIdx.x) * kHeadThreads + t; e < total; e += nbwd * kHeadThreads) {
-    int r = e / groups;
-    const int c0 = (e - r * groups) * 8;
-    const int pix = r;
-    r /= p.W;
-    const int w = pix - r * p.W;
-    const int n = r / p.H;
-    const int h = r - n * p.H;
-    const float d = g * p.dlogit[n];
-    uint4 xv = make_uint4(0, 0, 0, 0);
-    if (bnf) xv = *reinterpret_cast<const uint4*>(p.bn_x + (int64_t(pix) * p.C + c0));
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (live) {
     const int i0 = (h * p.OH) / p.H, i1 = ((h + 1) * p.OH + p.H - 1) / p.H;
     const int j0 = (w * p.OW) / p.W, j1 = ((w + 1) * p.OW + p.W - 1) / p.W;
     for (int i = i0; i < i1 && i < p.OH; ++i) {
@@ -210,44 +237,71 @@ __global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p, in
       for (int j = j0; j < j1 && j < p.OW; ++j) {
         const int ws = wstart(j, p.W, p.OW), we = wend(j, p.W, p.OW);
         if (w < ws || w >= we) continue;
-        const float inv = d / float((he - hs) * (we - ws));
+        const float area = float((he - hs) * (we - ws));
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] += inv * p.w[(c0 + k) * p.ws_c + i * p.ws_i + j * p.ws_j];
+        for (int k = 0; k < 8; ++k) m[k] += p.w[(c0 + k) * p.ws_c + i * p.ws_i + j * p.ws_j] / area;
       }
     }
-    uint32_t packed[4];
+  }
+  float is[8], nm[8], bw[8], bb[8], bs[8], bq[8];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const f32x2 pr = {acc[2 * k], acc[2 * k + 1]};
-      packed[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2));   // RNE, v_cvt_pk_bf16_f32
+  for (int q = 0; q < 8; ++q) {
+    bs[q] = bq[q] = 0.f;
+    if (bnf) {
+      is[q] = p.bn_invstd[c0 + q];
+      nm[q] = -p.bn_mean[c0 + q] * is[q];
+      bw[q] = p.bn_w[c0 + q];
+      bb[q] = p.bn_b[c0 + q];
     }
-    *reinterpret_cast<uint4*>(p.dz + ((int64_t(n * p.H + h) * p.W + w) * p.C + c0)) =
-        make_uint4(packed[0], packed[1], packed[2], packed[3]);
-    if (bnf) {   // the BN backward reads the stored (bf16) dz as its gy
-      const uint32_t xw[4] = {xv.x, xv.y, xv.z, xv.w};
+  }
+  const int64_t img = int64_t(p.H) * p.W * p.C;
+  const int64_t off = (int64_t(h) * p.W + w) * p.C + c0;
+  for (int n0 = 0; live && n0 < p.N; n0 += kHeadImgs) {
+    uint4 xv[kHeadImgs];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const uint32_t gb = q & 1 ? packed[q >> 1] & 0xFFFF0000u : packed[q >> 1] << 16;
-        const uint32_t xb = q & 1 ? xw[q >> 1] & 0xFFFF0000u : xw[q >> 1] << 16;
-        const float xh = fmaf(__uint_as_float(xb), is[q], nm[q]);
-        const float gy = __uint_as_float(gb);
-        const float gz = fmaf(xh, bw[q], bb[q]) > 0.f ? gy : gy * p.bn_slope;
-        bs[q] += gz;
-        bq[q] += gz * xh;
+    for (int u = 0; u < kHeadImgs; ++u)
+      xv[u] = bnf && n0 + u < p.N ? *reinterpret_cast<const uint4*>(p.bn_x + (n0 + u) * img + off)
+                                  : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < kHeadImgs; ++u) {
+      if (n0 + u >= p.N) break;
+      const float d = g * p.dlogit[n0 + u];
+      uint32_t packed[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const f32x2 pr = {d * m[2 * k], d * m[2 * k + 1]};
+        packed[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2));   // RNE, v_cvt_pk_bf16_f32
+      }
+      *reinterpret_cast<uint4*>(p.dz + (n0 + u) * img + off) = make_uint4(packed[0], packed[1], packed[2], packed[3]);
+      if (bnf) {   // the BN backward reads the stored (bf16) dz as its gy
+        const uint32_t xw[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const uint32_t gb = q & 1 ? packed[q >> 1] & 0xFFFF0000u : packed[q >> 1] << 16;
+          const uint32_t xb = q & 1 ? xw[q >> 1] & 0xFFFF0000u : xw[q >> 1] << 16;
+          const float xh = fmaf(__uint_as_float(xb), is[q], nm[q]);
+          const float gy = __uint_as_float(gb);
+          const float gz = fmaf(xh, bw[q], bb[q]) > 0.f ? gy : gy * p.bn_slope;
+          bs[q] += gz;
+          bq[q] += gz * xh;
+        }
       }
     }
   }
   if (!bnf) return;
-  // fold the lanes of each channel group (lanes t, t + groups, ...) in LDS
-  __shared__ float red[2][kHeadThreads * 8];   // [PL][C] per sum, PL * C = 8 * 256
-  const int PL = kHeadThreads / groups;
+  // fold the PXB pixel lanes of each channel group in LDS ([PXB][C] per sum,
+  // PXB * C = 8 * 256); a 9-float pitch per lane spreads the 8-float runs over the banks
+  __shared__ float red[2][kHeadThreads * 9];
+  if (t < PXB * groups) {
 #pragma unroll
-  for (int q = 0; q < 8; ++q) red[0][(t / groups) * p.C + c0l + q] = bs[q], red[1][(t / groups) * p.C + c0l + q] = bq[q];
+    for (int q = 0; q < 8; ++q) red[0][t * 9 + q] = bs[q], red[1][t * 9 + q] = bq[q];
+  }
   __syncthreads();
   double* row = p.bn_acc + int64_t(int(blockIdx.x) % p.bn_acc_r) * 2 * p.C;
   for (int c = t; c < p.C; c += kHeadThreads) {
+    const int gq = c >> 3, q = c & 7;
     float s0 = 0.f, s1 = 0.f;
-    for (int l = 0; l < PL; ++l) s0 += red[0][l * p.C + c], s1 += red[1][l * p.C + c];
+    for (int l = 0; l < PXB; ++l) s0 += red[0][(l * groups + gq) * 9 + q], s1 += red[1][(l * groups + gq) * 9 + q];
     unsafeAtomicAdd(row + c, double(s0));
     unsafeAtomicAdd(row + p.C + c, double(s1));
   }
@@ -259,6 +313,13 @@ hipError_t head_forward(const HeadParams& p, hipStream_t stream) {
   if (p.N <= 0 || p.C <= 0 || p.OH <= 0 || p.OW <= 0 || p.H < p.OH || p.W < p.OW || !p.z || !p.w || !p.pooled ||
       !p.partial || !p.loss || !p.dlogit)
     return hipErrorInvalidValue;
+  if (p.act.on()) {   // the fast path only: C / 8 lane groups tiling the block, 16-byte aligned rows
+    const int G = p.C / 8;
+    if (p.C % 8 || G > kHeadThreads || kHeadThreads % G || (reinterpret_cast<uintptr_t>(p.z) & 15) ||
+        p.C > kBnFoldMaxC || !p.act.acc || p.act.R <= 0 || !p.act.b || !p.act.mean || !p.act.invstd ||
+        p.act.M != int64_t(p.N) * p.H * p.W)
+      return hipErrorInvalidValue;
+  }
   head_fwd_kernel<<<dim3(unsigned(p.OH * p.OW), unsigned(p.N)), kHeadThreads, 0, stream>>>(p);
   if (!p.ticket) head_loss_kernel<<<1, 64, 0, stream>>>(p);
   return hipGetLastError();
@@ -271,15 +332,13 @@ hipError_t head_backward(const HeadParams& p, hipStream_t stream) {
   if (total >= (int64_t(1) << 31) - int64_t(kHeadThreads) * 4096) return hipErrorInvalidValue;
   const int groups = p.C / 8;
   if (p.bn_acc) {   // lanes keep one channel group: the block stride must be a multiple of C / 8
-    if (groups > kHeadThreads || kHeadThreads % groups || p.bn_acc_r <= 0 || !p.bn_x || !p.bn_mean ||
+    if (p.bn_acc_r <= 0 || !p.bn_x || !p.bn_mean ||
         !p.bn_invstd || !p.bn_w || !p.bn_b || (reinterpret_cast<uintptr_t>(p.bn_x) & 15))
       return hipErrorInvalidValue;
   }
-  const int64_t blocks = (total + kHeadThreads - 1) / kHeadThreads;
-  // BN-fused: one block per CU, lanes loop -- each block adds 2 C fp64 sums
-  // into the accumulator, so fewer, fuller blocks keep that traffic small
-  const int cap = p.bn_acc ? 256 : 2048;
-  const int nbwd = int(blocks < cap ? blocks : cap);
+  if (groups > kHeadThreads) return hipErrorInvalidValue;
+  const int pxb = kHeadThreads / groups;
+  const int nbwd = p.H * ((p.W + pxb - 1) / pxb);   // one row segment of pxb pixels per block, all images
   const int wtotal = p.C * p.OH * p.OW;
   const int nw = (wtotal + kHeadThreads - 1) / kHeadThreads;
   head_bwd_kernel<<<unsigned(nbwd + nw), kHeadThreads, 0, stream>>>(p, nbwd);

@@ -411,7 +411,7 @@ void conv_set_tiles(int bm, int bn, int staging = -1, int dgrad_cls = 0);
 int conv_dgrad_classes_per_block(int64_t M, int NOUT);
 // First-layer (4-channel) forward: 128-pixel tiles per block of the multi-tile
 // kernel (default 1 = the one-tile tap-GEMM path; BT_CONV1_TILES).
-void conv_set_conv1_tiles(int tiles);
+void conv_set_conv1_tiles(int tiles, int rows);
 hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream);
 // Data gradient of the same convolution (same tap-gather GEMM kernel, four
 // stride-2 parity classes in one launch): dy [N][H/2][W/2][Cout] bf16,
@@ -445,6 +445,30 @@ struct BnBwdFuse {
   int acc_r = 0;   // > 0: part points at a bn_bwd_apply_acc accumulator (fp64 [acc_r][2][Cin], atomic adds), rows unused
 };
 int64_t conv_dgrad_bn_rows(int N, int H, int W, int Cin);
+
+// A training BatchNorm+LeakyReLU applied by its CONSUMER as it reads the BN's
+// input (the conv forward's operand staging, its weight gradient's re-read,
+// the head's pooling): no apply pass and no activation tensor.  The batch
+// statistics sit in the BnAcc accumulator the producer added into (acc,
+// fp64 [R][2][C]); every consumer block folds them, block 0 writes mean /
+// invstd and the running statistics, and the last block clears the
+// accumulator (bn_fold.h).  With acc == nullptr the consumer reads mean /
+// invstd as given (the weight gradient, after the forward wrote them).
+struct BnActIn {
+  double* acc = nullptr;
+  int R = 0;
+  int64_t M = 0;                   // elements per channel
+  float eps = 0.f, momentum = 0.f;
+  const float* w = nullptr;        // affine weight / bias, fp32 [C]
+  const float* b = nullptr;
+  float slope = 0.f;
+  float* mean = nullptr;           // fp32 [C]: written (acc) or read
+  float* invstd = nullptr;
+  float* rm = nullptr;             // running statistics (nullable)
+  float* rv = nullptr;
+  int64_t* tracked = nullptr;
+  __host__ __device__ bool on() const { return w != nullptr; }
+};
 hipError_t conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int N, int H, int W, int Cin, int Cout,
                       hipStream_t stream, const BnBwdFuse* bn = nullptr);
 // bn_finalize over `nblocks` partial rows produced elsewhere (conv_fwd's epilogue)
@@ -490,6 +514,9 @@ struct HeadParams {
   float bn_slope = 0.f;
   double* bn_acc = nullptr;
   int bn_acc_r = 0;
+  // forward: z is the INPUT of the BatchNorm+LeakyReLU whose output the head
+  // pools (act.on()): the pooling reads leaky(bn(z)) rounded to bf16
+  BnActIn act;
 };
 hipError_t head_forward(const HeadParams& p, hipStream_t stream);
 hipError_t head_backward(const HeadParams& p, hipStream_t stream);

@@ -12,6 +12,7 @@
 #include <tuple>
 #include <cstring>
 #include <stdexcept>
+#include <string>
 #include <sys/mman.h>
 
 #include "../python/pyvalue.h"
@@ -28,6 +29,32 @@ namespace {
 template <typename T>
 T* ptr(uintptr_t p) {
   return reinterpret_cast<T*>(p);
+}
+
+// BnActIn from Python: None, or (acc, R, M, eps, momentum, w, b, slope, mean, invstd, rm, rv, tracked) --
+// integers are device pointers (0 = none)
+BnActIn act_from(const py::object& o, const char* what) {
+  BnActIn a;
+  if (o.is_none()) return a;
+  const py::tuple f = o.cast<py::tuple>();
+  if (f.size() != 13)
+    throw std::invalid_argument(std::string(what) +
+                                ": act is (acc, R, M, eps, momentum, w, b, slope, mean, invstd, rm, rv, tracked)");
+  a.acc = ptr<double>(f[0].cast<uintptr_t>());
+  a.R = f[1].cast<int>();
+  a.M = f[2].cast<int64_t>();
+  a.eps = f[3].cast<float>();
+  a.momentum = f[4].cast<float>();
+  a.w = ptr<const float>(f[5].cast<uintptr_t>());
+  a.b = ptr<const float>(f[6].cast<uintptr_t>());
+  a.slope = f[7].cast<float>();
+  a.mean = ptr<float>(f[8].cast<uintptr_t>());
+  a.invstd = ptr<float>(f[9].cast<uintptr_t>());
+  a.rm = ptr<float>(f[10].cast<uintptr_t>());
+  a.rv = ptr<float>(f[11].cast<uintptr_t>());
+  a.tracked = ptr<int64_t>(f[12].cast<uintptr_t>());
+  if (!a.w) throw std::invalid_argument(std::string(what) + ": act needs the BN weight");
+  return a;
 }
 
 hipStream_t stream_of(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
@@ -295,7 +322,7 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("dgrad_cls") = 0);
   m.def("conv_dgrad_classes_per_block", &conv_dgrad_classes_per_block);
   m.def("conv_set_wgrad_staging", &conv_set_wgrad_staging);
-  m.def("conv_set_conv1_tiles", &conv_set_conv1_tiles);
+  m.def("conv_set_conv1_tiles", &conv_set_conv1_tiles, py::arg("tiles"), py::arg("rows") = 0);
   m.def("conv_set_c4_wave_private", &conv_set_c4_wave_private);
   m.def("conv_tile_pixels", &conv_tile_pixels);
   m.def("conv_tile_channels", &conv_tile_channels);
@@ -389,8 +416,9 @@ PYBIND11_MODULE(_hip, m) {
   m.def("head_forward",
         [](uintptr_t z, uintptr_t w, int64_t ws_c, int64_t ws_i, int64_t ws_j, int N, int H, int W, int C, int OH,
            int OW, uintptr_t target, float target_value, uintptr_t pooled, uintptr_t partial, uintptr_t loss,
-           uintptr_t dlogit, uintptr_t logit, uintptr_t stream, uintptr_t ticket) {
+           uintptr_t dlogit, uintptr_t logit, uintptr_t stream, uintptr_t ticket, py::object act) {
           HeadParams p;
+          p.act = act_from(act, "head_forward");
           p.ticket = ptr<uint32_t>(ticket);
           p.z = ptr<const uint16_t>(z);
           p.w = ptr<const float>(w);
@@ -408,7 +436,7 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("z"), py::arg("w"), py::arg("ws_c"), py::arg("ws_i"), py::arg("ws_j"), py::arg("N"), py::arg("H"),
         py::arg("W"), py::arg("C"), py::arg("OH"), py::arg("OW"), py::arg("target"), py::arg("target_value"),
         py::arg("pooled"), py::arg("partial"), py::arg("loss"), py::arg("dlogit"), py::arg("logit"),
-        py::arg("stream"), py::arg("ticket") = 0);
+        py::arg("stream"), py::arg("ticket") = 0, py::arg("act") = py::none());
   m.def("head_backward",
         [](uintptr_t w, int64_t ws_c, int64_t ws_i, int64_t ws_j, int N, int H, int W, int C, int OH, int OW,
            uintptr_t pooled, uintptr_t dlogit, uintptr_t gscale, uintptr_t dz, uintptr_t dw, uintptr_t stream,

@@ -37,6 +37,8 @@ class Discriminator(nn.Module):
     # BN's backward apply runs inside the first conv's weight-gradient kernel
     # (ops.BnDeferred); False keeps the separate apply launch (A/B, tests)
     defer_first_bn = True
+    # the last BatchNorm+LeakyReLU's forward apply runs in the fused head's pooling (ops.BnActLazy)
+    lazy_head_bn = True
 
     def __init__(self, nc=3, ndf=32, adaptive=False, fused=True):
         super().__init__()
@@ -137,11 +139,15 @@ class Discriminator(nn.Module):
                 raise ValueError('bce_bf16(decode=): raw u8 RGBA frames on the fused-head MFMA path only')
             lut = ops.decode_lut_bf16(decode, x.device)
         if ok:
-            z, link = self._run_bf16(x, body, mfma, want_link=True, lut=lut)
+            # adaptive stack: the last BN's apply runs in the head's pooling (BnActLazy)
+            z, link, lazy = self._run_bf16(x, body, mfma, want_link=True, lut=lut,
+                                           lazy_tail=adaptive and self.lazy_head_bn)
             if adaptive or tuple(z.shape[2:]) == pool:
                 if not z.is_contiguous(memory_format=torch.channels_last):
+                    if lazy is not None:
+                        raise RuntimeError('bce_bf16: the lazily applied BN input is not channels-last')
                     z, link = z.contiguous(memory_format=torch.channels_last), None
-                loss, logits = ops.disc_head_bce(z, head.weight, target, pool, bn_link=link)
+                loss, logits = ops.disc_head_bce(z, head.weight, target, pool, bn_link=link, act=lazy)
                 return loss, (torch.sigmoid(logits) if probs else None)
             out = self._run_bf16(z, layers[len(body):], mfma)
         else:
@@ -150,7 +156,7 @@ class Discriminator(nn.Module):
         tgt = target if isinstance(target, torch.Tensor) else torch.full_like(out, float(target))
         return F.binary_cross_entropy(out, tgt), out
 
-    def _run_bf16(self, x, layers, mfma, want_link=False, lut=None):
+    def _run_bf16(self, x, layers, mfma, want_link=False, lut=None, lazy_tail=False):
         import torch.nn.functional as F
         from .. import ops
         convs = [m for m in layers if isinstance(m, nn.Conv2d)]
@@ -167,7 +173,7 @@ class Discriminator(nn.Module):
             if need:
                 wts = dict(zip(need, ops.conv_weights_t([w16s[k] for k in need])))
         ci = -1
-        stats = link = defer = None
+        stats = link = defer = lazy = None
         # the MFMA weight gradients of one backward hand their slice reduce to the
         # next one (ops.WgradChain): the first such layer's runs last and closes it
         wchain = ops.WgradChain() if (mfma and torch.is_grad_enabled() and x.is_cuda) else None
@@ -220,14 +226,20 @@ class Discriminator(nn.Module):
                     x = F.conv2d(x, w16, None, m.stride, m.padding, m.dilation, m.groups)
             elif stats is not None and isinstance(m, ops.BatchNormLeakyReLU2d):
                 link = ops.BnLink() if torch.is_grad_enabled() else None
-                x = m.forward_from_stats(x, stats, link, defer)
+                if (lazy_tail and i == len(layers) - 1 and isinstance(stats, ops.BnAccumulator)
+                        and x.dtype == torch.bfloat16):
+                    lazy = ops.BnActLazy()   # the caller's consumer applies this BN
+                x = m.forward_from_stats(x, stats, link, defer, lazy)
                 stats = defer = None
             else:
                 if not isinstance(m, nn.Identity):
                     link = None
                 x = m(x)
         # want_link: also the BnLink of a BN whose output is returned (its consumer
-        # -- the fused head -- can then do that BN's backward reduction)
+        # -- the fused head -- can then do that BN's backward reduction), and with
+        # lazy_tail that BN's BnActLazy (None: x is the BN's output, not its input)
+        if lazy_tail:
+            return x, link, lazy
         return (x, link) if want_link else x
 
 

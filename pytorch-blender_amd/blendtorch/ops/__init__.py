@@ -900,13 +900,36 @@ class BnDeferred:
         return p
 
 
+class BnActLazy:
+    """Hand-off of a training BatchNorm+LeakyReLU's FORWARD apply to the op
+    that consumes its output (the fused discriminator head,
+    :func:`disc_head_bce` ``act=``): the BN call returns its input ``y``
+    unchanged and records here what the consumer needs to compute
+    ``leaky(bn(y))`` itself while it reads ``y`` -- the statistics
+    accumulator its blocks fold (block 0 writes mean / invstd and the running
+    statistics, the last clears it), the affine parameters and the slope
+    (``csrc/gpu/kernels.h`` ``BnActIn``).  No apply pass, no activation
+    tensor.  ``args`` is consumed once."""
+    __slots__ = ('args', 'keep')
+
+    def __init__(self):
+        self.args = None
+        self.keep = None
+
+    def take(self):
+        a, self.args = self.args, None
+        if a is None:
+            raise RuntimeError('BnActLazy: no pending BatchNorm apply (never set, or already consumed)')
+        return a
+
+
 def _bn_function():
     import torch
 
     class _BatchNormLeakyReLU(torch.autograd.Function):
         @staticmethod
         def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, slope, tracked=None,
-                    stats=None, link=None, defer=None):
+                    stats=None, link=None, defer=None, lazy=None):
             ext = hip_ext()
             N, C, H, W = x.shape
             M = N * H * W
@@ -916,11 +939,19 @@ def _bn_function():
             b = bias.detach().float().contiguous()
             mean = torch.empty(C, dtype=torch.float32, device=x.device)
             invstd = torch.empty_like(mean)
-            y = torch.empty_like(xs)
             rm = running_mean.data_ptr() if running_mean is not None else 0
             rv = running_var.data_ptr() if running_var is not None else 0
             tr = tracked.data_ptr() if tracked is not None else 0
-            if isinstance(stats, BnAccumulator):
+            if lazy is not None and not (isinstance(stats, BnAccumulator) and dt == OUT_DTYPES['bfloat16']):
+                raise ValueError('BatchNormLeakyReLU2d(lazy=): bf16 input with accumulated statistics only')
+            y = xs if lazy is not None else torch.empty_like(xs)
+            if lazy is not None:
+                # the consumer applies this op while it reads x (BnActLazy): no launch here
+                _count('bn_forward_lazy')
+                lazy.args = (stats.fwd.data_ptr(), stats.R, M, float(eps), float(momentum), w.data_ptr(),
+                             b.data_ptr(), float(slope), mean.data_ptr(), invstd.data_ptr(), rm, rv, tr)
+                lazy.keep = (stats, w, b, mean, invstd)
+            elif isinstance(stats, BnAccumulator):
                 # sums accumulated by the producing conv's epilogue; folded by the apply kernel
                 _count('bn_forward_from_stats')
                 _count('bn_forward_acc')
@@ -953,7 +984,7 @@ def _bn_function():
                 link.params = (weight, bias)
                 link.dw = link.db = None
                 link.folded = False
-            return y.permute(0, 3, 1, 2)
+            return y.permute(0, 3, 1, 2)   # (lazy: a view of the input, the pre-BN values)
 
         @staticmethod
         def backward(ctx, gy):
@@ -986,7 +1017,8 @@ def _bn_function():
                                      lk.db.data_ptr(), ctx.slope, _stream(xs.device))
                 lk.dw = lk.db = None
                 lk.folded = False
-                return (gx.permute(0, 3, 1, 2), out_w, out_b, None, None, None, None, None, None, None, None, None)
+                return (gx.permute(0, 3, 1, 2), out_w, out_b, None, None, None, None, None, None, None, None, None,
+                        None)
             if folded:
                 raise RuntimeError('BatchNormLeakyReLU2d: its statistics were folded for another gradient')
             # (not before the folded branch: the fold already took the bucket views)
@@ -1018,7 +1050,7 @@ def _bn_function():
                                 db.data_ptr(), ctx.slope, _stream(xs.device))
             _grad_done(ctx.params[0] if w_sunk else None, ctx.params[1] if b_sunk else None)
             return (gx.permute(0, 3, 1, 2), None if w_sunk else dw, None if b_sunk else db,
-                    None, None, None, None, None, None, None, None, None)
+                    None, None, None, None, None, None, None, None, None, None)
 
     return _BatchNormLeakyReLU
 
@@ -1055,9 +1087,9 @@ def batch_norm_leaky_relu(x, weight, bias, running_mean=None, running_var=None, 
 
 
 def _bn_apply_unchecked(x, weight, bias, running_mean, running_var, eps, momentum, slope, tracked=None,
-                        stats=None, link=None, defer=None):
+                        stats=None, link=None, defer=None, lazy=None):
     return _BN_FN.apply(x, weight, bias, running_mean, running_var, eps, momentum, slope, tracked, stats, link,
-                        defer)
+                        defer, lazy)
 
 
 def reference_batch_norm_leaky_relu(x, weight, bias, running_mean=None, running_var=None, eps=1e-5, momentum=0.1,
@@ -1114,7 +1146,7 @@ def _bn_module():
             ring[1] = (i + 1) % len(accs)
             return accs[i]
 
-        def forward_from_stats(self, x, stats, link=None, defer=None):
+        def forward_from_stats(self, x, stats, link=None, defer=None, lazy=None):
             """Training forward with the batch statistics already summed by
             the producing kernel (``conv_fwd``'s epilogue rows, see
             :func:`conv4x4s2`, or a :class:`BnAccumulator` it added into:
@@ -1123,12 +1155,14 @@ def _bn_module():
             output (its data-gradient epilogue then does this op's backward
             reduction).  ``defer``: a :class:`BnDeferred` armed by the first
             convolution that produced ``x`` (it then applies this op's
-            backward itself)."""
+            backward itself).  ``lazy``: a :class:`BnActLazy` -- the
+            consumer applies this op itself; returns ``x`` (pre-BN)."""
             global _BN_FN
             if _BN_FN is None:
                 _BN_FN = _bn_function()
             return _bn_apply_unchecked(x, self.weight, self.bias, self.running_mean, self.running_var, self.eps,
-                                       self.momentum, self.slope, self.num_batches_tracked, stats, link, defer)
+                                       self.momentum, self.slope, self.num_batches_tracked, stats, link, defer,
+                                       lazy)
 
         def extra_repr(self):
             return super().extra_repr() + f', slope={self.slope}'
@@ -1529,7 +1563,7 @@ def _head_function():
 
     class _DiscHeadBCE(torch.autograd.Function):
         @staticmethod
-        def forward(ctx, z, w, target, oh, ow, bn_link=None):
+        def forward(ctx, z, w, target, oh, ow, bn_link=None, act=None):
             ctx.set_materialize_grads(False)   # no zero-filled gradient for the logits output
             ext = hip_ext()
             N, C, H, W = z.shape
@@ -1548,7 +1582,8 @@ def _head_function():
             _count('head_forward')
             ext.head_forward(z.data_ptr(), w.data_ptr(), w.stride(1), w.stride(2), w.stride(3), N, H, W, C, oh, ow,
                              tptr, tval, pooled.data_ptr(), partial.data_ptr(), loss.data_ptr(), dlogit.data_ptr(),
-                             logit.data_ptr(), _stream(dev), _head_ticket(dev).data_ptr())
+                             logit.data_ptr(), _stream(dev), _head_ticket(dev).data_ptr(),
+                             act.take() if act is not None else None)
             ctx.save_for_backward(w, pooled, dlogit)
             ctx.wparam = w
             ctx.bn_link = bn_link
@@ -1559,7 +1594,7 @@ def _head_function():
         @staticmethod
         def backward(ctx, gloss, glogit=None):
             if gloss is None:
-                return None, None, None, None, None, None
+                return None, None, None, None, None, None, None
             ext = hip_ext()
             w, pooled, dlogit = ctx.saved_tensors
             N, C, H, W = ctx.zshape
@@ -1586,7 +1621,7 @@ def _head_function():
                                   _stream(w.device))
             if sunk:
                 _grad_done(ctx.wparam)
-            return dz, None if sunk else dw, None, None, None, None
+            return dz, None if sunk else dw, None, None, None, None, None
 
     return _DiscHeadBCE
 
@@ -1607,7 +1642,7 @@ def _head_ticket(dev):
     return t
 
 
-def disc_head_bce(z, w, target=1.0, pool=(4, 4), bn_link=None):
+def disc_head_bce(z, w, target=1.0, pool=(4, 4), bn_link=None, act=None):
     """``BCELoss()(sigmoid(conv2d(adaptive_avg_pool2d(z, pool), w)).view(-1), target)``
     for a head conv that consumes the whole pooled map (``w``: fp32
     [1, C, pool_h, pool_w]); ``z`` bf16 channels-last [N, C, H, W] on the GPU.
@@ -1615,7 +1650,9 @@ def disc_head_bce(z, w, target=1.0, pool=(4, 4), bn_link=None):
     (fp32).  Pool, dot products and loss run in fp32.  ``bn_link``: the
     :class:`BnLink` of the BatchNorm+LeakyReLU that produced ``z`` (in
     accumulator mode): the backward then also sums that BN's backward
-    statistics."""
+    statistics.  ``act``: that BN's :class:`BnActLazy` -- ``z`` is then the
+    BN's INPUT and the head's pooling applies the BN (its forward launch
+    skipped the apply)."""
     import torch
     global _HEAD_FN
     if _HEAD_FN is None:
@@ -1625,7 +1662,7 @@ def disc_head_bce(z, w, target=1.0, pool=(4, 4), bn_link=None):
         raise ValueError('disc_head_bce needs bf16 channels-last GPU features')
     if tuple(w.shape) != (1, z.shape[1], oh, ow) or w.dtype != torch.float32 or z.shape[1] % 8:
         raise ValueError(f'disc_head_bce: weight {tuple(w.shape)} {w.dtype} does not fit features {tuple(z.shape)}')
-    return _HEAD_FN.apply(z, w, target, oh, ow, bn_link)
+    return _HEAD_FN.apply(z, w, target, oh, ow, bn_link, act)
 
 
 def __getattr__(name):

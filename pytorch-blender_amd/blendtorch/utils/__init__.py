@@ -54,6 +54,8 @@ def ensure_hw_queues(n: int = DEFAULT_HW_QUEUES) -> int:
             cur = 4
         if cur < n:
             os.environ['GPU_MAX_HW_QUEUES'] = str(int(n))
+        else:
+            return cur   # (unset: HIP's default, 4)
     return int(os.environ['GPU_MAX_HW_QUEUES'])
 
 

@@ -449,16 +449,19 @@ def test_first_bn_backward_deferred_into_first_wgrad(dev, c4_staging):
 @pytest.mark.gpu
 @pytest.mark.parametrize('u8', [True, False])
 @pytest.mark.parametrize('cout,wc', [(32, 3), (64, 4)])
-def test_first_layer_multi_tile_forward(dev, u8, cout, wc):
-    """The first layer's multi-tile forward kernel (4 x 128-pixel tiles per
-    block, BN sums into a BnAccumulator) against the one-tile tap-GEMM path:
-    bit-identical outputs, the same channel sums (fp64 atomics in another
-    order), both equal to the fp32 reference."""
+@pytest.mark.parametrize('tiles,rows', [(4, 2), (1, 4), (3, 4)])
+def test_first_layer_patch_forward(dev, u8, cout, wc, tiles, rows):
+    """The first layer's patch kernel (input decoded once into LDS, rows x 64
+    output tiles, several tiles per block, BN sums into a BnAccumulator)
+    against the im2col tap-GEMM path: bit-identical outputs (the same MFMA
+    dot products with the operands swapped), the same channel sums (fp64
+    atomics over other partials), both equal to the fp32 reference.  644
+    columns: a ragged last column tile; 482 rows: a ragged last row tile."""
     import torch.nn.functional as F
     cl = torch.channels_last
     g = torch.Generator(device=dev).manual_seed(cout + wc)
     cfg = ops.DecodeConfig.unit(channels='rgba', gamma=2.2, dtype='bfloat16', layout='nhwc')
-    raw = torch.randint(0, 256, (4, 480, 644, 4), dtype=torch.uint8, device=dev, generator=g)  # 2415 tiles, ragged end
+    raw = torch.randint(0, 256, (3, 482, 644, 4), dtype=torch.uint8, device=dev, generator=g)
     if u8:
         x, lut = raw.permute(0, 3, 1, 2), ops.decode_lut_bf16(cfg, dev)
         xdec = ops.decode(raw, cfg).permute(0, 3, 1, 2)
@@ -467,19 +470,21 @@ def test_first_layer_multi_tile_forward(dev, u8, cout, wc):
         lut = None
     w = (0.1 * torch.randn(cout, wc, 4, 4, device=dev, generator=g)).to(torch.bfloat16).contiguous(memory_format=cl)
     outs = []
-    for tiles in (4, 1):
-        ops.hip_ext().conv_set_conv1_tiles(tiles)
-        acc = ops.BnAccumulator(cout, dev)
-        y = ops.conv_fwd(x, w, acc.fwd, acc.R, lut=lut)
-        s = acc.fwd[:acc.R * 2 * cout].view(acc.R, 2, cout).sum(0)
-        outs.append((y, s))
-    ops.hip_ext().conv_set_conv1_tiles(0)
+    try:
+        for t in (tiles, -1):
+            ops.hip_ext().conv_set_conv1_tiles(t, rows)
+            acc = ops.BnAccumulator(cout, dev)
+            y = ops.conv_fwd(x, w, acc.fwd, acc.R, lut=lut)
+            s = acc.fwd[:acc.R * 2 * cout].view(acc.R, 2, cout).sum(0)
+            outs.append((y, s))
+    finally:
+        ops.hip_ext().conv_set_conv1_tiles(0, 0)
     assert torch.equal(outs[0][0], outs[1][0])
-    # per-block fp32 partials over 4 tiles instead of 1: equal to fp32 rounding of those partials
     torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-6, atol=1e-3)
     wref = w.float() if wc == 4 else torch.cat([w.float(), torch.zeros(cout, 1, 4, 4, device=dev)], 1)
     ref = F.conv2d(xdec.float(), wref, None, 2, 1)
     torch.testing.assert_close(outs[0][0].float(), ref, rtol=2 ** -7, atol=1e-3 * float(ref.abs().max()))
     yf = outs[0][0].float().permute(0, 2, 3, 1).reshape(-1, cout).double()
     torch.testing.assert_close(outs[0][1][0], yf.sum(0), rtol=1e-6, atol=1e-3)
+    torch.testing.assert_close(outs[0][1][1], (yf * yf).sum(0), rtol=1e-6, atol=1e-3)
     torch.testing.assert_close(outs[0][1][1], (yf * yf).sum(0), rtol=1e-6, atol=1e-3)

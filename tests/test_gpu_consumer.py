@@ -162,6 +162,38 @@ def test_discriminator_bce_loss_bf16(dev):
         assert float(ga @ gb / (ga.norm() * gb.norm())) > 0.98, n
 
 
+def test_head_applies_last_bn_bit_identical(dev):
+    """The last BatchNorm+LeakyReLU's forward apply inside the fused head's
+    pooling (ops.BnActLazy: no apply launch, no activation tensor) gives the
+    SAME loss, gradients and running statistics as the apply pass: the head
+    computes the same bf16 activation values from the same folded statistics."""
+    from blendtorch.models import Discriminator
+    torch.manual_seed(0)
+    nets = []
+    for lazy in (True, False):
+        torch.manual_seed(0)
+        m = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=torch.channels_last)
+        m.lazy_head_bn = lazy
+        nets.append(m)
+    g = torch.Generator(device=dev).manual_seed(2)
+    before = ops.KERNEL_CALLS.get('bn_forward_lazy', 0)
+    for _ in range(2):   # the second step re-uses the accumulators the first step's head cleared
+        x = torch.rand(4, 3, 120, 160, device=dev, generator=g).to(torch.bfloat16)
+        x = x.contiguous(memory_format=torch.channels_last)
+        losses = []
+        for m in nets:
+            m.zero_grad(set_to_none=True)
+            loss = m.bce_loss_bf16(x, 1.0)
+            loss.backward()
+            losses.append(loss.detach())
+        assert torch.equal(losses[0], losses[1])
+        for (n, pa), pb in zip(nets[0].named_parameters(), nets[1].parameters()):
+            assert torch.equal(pa.grad, pb.grad), n
+        for (n, ba), bb in zip(nets[0].named_buffers(), nets[1].buffers()):
+            assert torch.equal(ba, bb), n
+    assert ops.KERNEL_CALLS['bn_forward_lazy'] == before + 2
+
+
 def _disc_steps(dev, buckets, graph, xs, grad_scale=None):
     from blendtorch.models import Discriminator
     from blendtorch.parallel import GradBuckets

@@ -49,6 +49,9 @@ def test_ensure_hw_queues_raises_but_never_lowers(monkeypatch):
     assert ensure_hw_queues(8) == 16
     monkeypatch.setenv('BT_HW_QUEUES', '4')          # an explicit pin wins
     assert ensure_hw_queues(8) == 4 and os.environ['GPU_MAX_HW_QUEUES'] == '4'
+    monkeypatch.delenv('BT_HW_QUEUES')
+    monkeypatch.delenv('GPU_MAX_HW_QUEUES')
+    assert ensure_hw_queues(4) == 4 and 'GPU_MAX_HW_QUEUES' not in os.environ   # HIP's default already
 
 
 def test_save_image_matches_torchvision_grid_rules(tmp_path):
