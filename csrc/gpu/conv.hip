@@ -33,6 +33,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstdint>
+#include <type_traits>
 
 #include "bn_fold.h"
 #include "kernels.h"
@@ -270,6 +271,8 @@ struct XCursor {
   }
 };
 
+template <bool BND>   // BND: the BN backward applied to dY (ConvWgradParams::bn_dy) -- its coefficients and
+                     // ring cost ~80 VGPRs, so the plain variant stays lean
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   if (run_side(p, smem)) return;
@@ -316,13 +319,27 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p)
 
   const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(p.x, int64_t(p.N) * p.H * p.W * p.Cin * 2);
   const __amdgpu_buffer_rsrc_t rs_dy = make_rsrc(p.dy, p.M * p.Cout * 2);
+  // bn_dy: dy is the gradient of the BatchNorm+LeakyReLU that follows this
+  // layer; its backward (BnBwdCoef, the apply kernel's arithmetic) is applied
+  // to the staged dY chunk, which the first column tile's blocks also store
+  // to gx_out (the next data gradient's operand)
+  constexpr bool bnd = BND;
+  BnBwdCoef bc[8];
+  if (bnd) {   // (LDS scratch: the staging area, free until the loop)
+    bn_dy_coefs(p.bn_dy, p.Cout, p.M, co0 + dch * 8, reinterpret_cast<double*>(smem),
+                reinterpret_cast<int*>(smem + 4096), unsigned(b), unsigned(nwg), bc);
+    __syncthreads();
+  }
+  const __amdgpu_buffer_rsrc_t rs_by = make_rsrc(bnd ? p.bn_dy.y : p.dy, p.M * p.Cout * 2);
+  uint16_t* const gx_out = bnd && kt == 0 ? p.bn_dy.gx_out : nullptr;
   // Stage loads run kDepth stages ahead of the MFMAs in a register ring (one
   // block per CU: nothing else would hide the ~0.8 us load latency).  Stages
   // past the slice load out of range (zeros, no memory traffic), so the loop
   // has no tail and the compiler keeps counted vmcnt waits.
   constexpr int kDepth = 4;
   struct Stage {
-    uint4 dy, x0, x1;
+    uint4 dy, x0, x1, y;   // y: the BN input at the dY chunk (bn_dy)
+    uint32_t off;          // the dY chunk's byte offset, kOOB past the slice
   };
   Stage ring[kDepth];
   int md = m_begin + dpx;                                           // this thread's dY pixel
@@ -332,7 +349,9 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p)
   // chunk (out-of-range dY loads return 0), and past the tensor the X load is
   // out of range too
   auto load = [&](Stage& r) {
-    r.dy = bload(rs_dy, md < m_end ? dy_byte : kOOB);
+    r.off = md < m_end ? dy_byte : kOOB;
+    r.dy = bload(rs_dy, r.off);
+    if (bnd) r.y = bload(rs_by, r.off);
     const int ih = 2 * c0.oh - 1 + kh, iw = 2 * c0.ow - 1 + kw;
     const bool ok0 = unsigned(ih) < unsigned(p.H) && unsigned(iw) < unsigned(p.W);
     const bool ok1 = unsigned(ih + dkh) < unsigned(p.H) && unsigned(iw + dkw) < unsigned(p.W);
@@ -344,9 +363,26 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p)
   };
   const int st_dy = dy_off(dpx, dch * 16), st_x0 = DY_TILE + x_off(xpx, xch * 16),
             st_x1 = DY_TILE + x_off(xpx, (xch + 8) * 16);
+  const float slope = p.bn_dy.slope;
   auto store = [&](const Stage& r, int buf) {
     char* base = smem + buf * STAGE;
-    *reinterpret_cast<uint4*>(base + st_dy) = r.dy;
+    uint4 d = r.dy;
+    if (bnd) {   // gx of the 8 channels (rows past the slice stay zero, not gx(0, 0))
+      if (r.off != kOOB) {
+        const uint32_t gw[4] = {r.dy.x, r.dy.y, r.dy.z, r.dy.w}, yw[4] = {r.y.x, r.y.y, r.y.z, r.y.w};
+        uint32_t o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x2 pr = {bc[2 * q].gx(__uint_as_float(yw[q] << 16), __uint_as_float(gw[q] << 16), slope),
+                            bc[2 * q + 1].gx(__uint_as_float(yw[q] & 0xFFFF0000u),
+                                             __uint_as_float(gw[q] & 0xFFFF0000u), slope)};
+          o[q] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2));
+        }
+        d = make_uint4(o[0], o[1], o[2], o[3]);
+        if (gx_out) *reinterpret_cast<uint4*>(reinterpret_cast<char*>(gx_out) + r.off) = d;
+      }
+    }
+    *reinterpret_cast<uint4*>(base + st_dy) = d;
     *reinterpret_cast<uint4*>(base + st_x0) = r.x0;
     *reinterpret_cast<uint4*>(base + st_x1) = r.x1;
   };
@@ -762,13 +798,10 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4w_kernel(ConvWgradParam
   const int xp = lane & 31, kh0 = (lane >> 5) * 2;
   const bool bnd = p.bn_dy.y != nullptr;
   BnBwdCoef bc[8];
-  if (bnd) {
-    const float invM = 1.f / float(p.M);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int c = co0 + dc * 8 + i;
-      bc[i].init(p.bn_dy.mean[c], p.bn_dy.invstd[c], p.bn_dy.w[c], p.bn_dy.b[c], p.bn_dy.dw[c], p.bn_dy.db[c], invM);
-    }
+  if (bnd) {   // (LDS scratch: the staging area, free until the loop)
+    bn_dy_coefs(p.bn_dy, p.Cout, p.M, co0 + dc * 8, reinterpret_cast<double*>(smem),
+                reinterpret_cast<int*>(smem + 4096), unsigned(b), unsigned(nwg), bc);
+    __syncthreads();
   }
   const float slope = p.bn_dy.slope;
   const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(p.x, int64_t(p.N) * p.H * p.W * 4 * (u8in ? 1 : 2));
@@ -938,6 +971,15 @@ constexpr int F_STAGE = FA_TILE + FB_TILE;
 
 __device__ __forceinline__ int f_off(int r, int chunk) { return r * F_ROW + ((chunk ^ (r & 7)) << 4); }
 
+// Channels-as-rows MFMA tiles (the weights as the A operand, the pixels as B):
+// a lane's accumulator then holds 4 channels of ONE pixel.  Row rho of channel
+// fragment f is channel 32 (f >> 1) + 8 (rho >> 2) + 4 (f & 1) + (rho & 3), so
+// fragments 2q and 2q + 1 give lane group g = lane >> 4 the 8 consecutive
+// channels 32 q + 8 g .. + 7: one 16-byte store per lane and pixel.
+__device__ __forceinline__ int c1_row_chan(int f, int rho) {
+  return 32 * (f >> 1) + 8 * (rho >> 2) + 4 * (f & 1) + (rho & 3);
+}
+
 struct TapGemm {
   const uint16_t* src = nullptr;
   const uint16_t* w = nullptr;     // [NOUT][16][C]
@@ -951,6 +993,10 @@ struct TapGemm {
   int acc_r = 0;                   // forward: > 0 = stats points at a BnAcc accumulator (fp64 [acc_r][2][NOUT])
   BnBwdFuse bn;                    // data gradient only: BN backward statistics in the epilogue (bn.part nullable)
   int cls_per_block = 1;           // data gradient: parity classes per block (1, or 4 = all; grid.y = 4 / this)
+  // forward: src is the INPUT of a BatchNorm+LeakyReLU (act.on()) applied to the A tile as it is
+  // staged; act_out (nullable) receives the activation itself (every input element once)
+  BnActIn act;
+  uint16_t* act_out = nullptr;
 };
 
 // BN = output channels per block (128 or 64, or 32 for 32-channel outputs
@@ -963,8 +1009,21 @@ struct TapGemm {
 // LDS buffers; 2 or 3 = LDS-DMA (buffer_load ... lds) straight into NST LDS
 // stages -- the 16-byte LDS stores of the register path run at ~79 B/clk/CU
 // (a third of what the fragment reads get) and were the kernel's bound.
-template <bool DGRAD, int BN, bool C4 = false, int BM = FBM, int NST = 0, int CLS = 1>
+// ACT (forward, LDS-DMA staging): the BatchNorm+LeakyReLU that produced src
+// is applied here (BnActIn): every block folds the statistics accumulator in
+// its prologue (overlapping its first stage's loads), and after its own
+// LDS-DMA chunks of a stage have landed each thread rewrites them in place
+// as leaky(bn(x)) rounded to bf16 -- before the barrier that publishes the
+// stage, so no extra barrier and no register staging.  Padding chunks stay
+// zero.  The chunks of the 4 centre taps (kh, kw in {1, 2}) cover every input
+// element exactly once, so blocks of the first channel tile also store those
+// to act_out: the activation the weight gradient reads, written without a
+// pass of its own.  ACT = coefficient sets per thread: a thread's chunk is
+// always the same 8 channels when C <= 64 (1), or alternates between two with
+// the k-step when C = 128 (2).
+template <bool DGRAD, int BN, bool C4 = false, int BM = FBM, int NST = 0, int CLS = 1, int ACT = 0>
 __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
+  static_assert(ACT == 0 || (!DGRAD && !C4 && NST >= 2), "the BN apply rides on the forward's LDS-DMA staging");
   constexpr int RJ = BM / 32;                  // staged A rows per thread (ar + 32 j)
   constexpr int A_TILE = BM * F_ROW;
   constexpr int WGM = BN >= 64 ? 2 : 4, WGN = 4 / WGM;
@@ -989,6 +1048,13 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   float* red = reinterpret_cast<float*>(smem + E_TILE);   // [WGM][2][BN], after the epilogue tile
   const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
   constexpr int NTAPS = DGRAD ? 4 : 16;
+  // DIRECT (every layer but the im2col first layer): channels-as-rows tiles
+  // (c1_row_chan) and an epilogue straight from the accumulators -- each lane
+  // rounds its pixel's 8 channels and stores them with one 16-byte store, the
+  // BatchNorm sums stay in registers.  The LDS round trip it replaces wrote
+  // every value with a 2-byte ds_write (16 per lane per tile) behind a barrier.
+  constexpr bool DIRECT = !C4;
+  static_assert(!DIRECT || FN % 2 == 0, "channel fragments pair up");
   const int K = C4 ? FBK : NTAPS * p.C, NT = p.NOUT / BN;
   // data gradient: blockIdx.y is one stride-2 parity class (ph, pw), or with
   // p.cls_per_block == 4 the block runs all four classes of its pixel tile in
@@ -1010,9 +1076,14 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   constexpr int CPR = BN / 8, RPP = kThreads / CPR, NJ = BM / RPP;
   const int ec = t % CPR;
   const bool bnf = DGRAD && p.bn.part != nullptr;
-  float bs[8], bq[8];   // BN-backward sums (bnf), over every class this block runs
+  // BN-backward sums (bnf), over every class this block runs: 8 channels per
+  // 32-channel group of the wave (DIRECT), or the 8 of the lane's row chunk
+  constexpr int NQ = DIRECT ? FN / 2 : 1;
+  float bs[NQ][8], bq[NQ][8];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) bs[q] = bq[q] = 0.f;
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bs[q][e] = bq[q][e] = 0.f;
   for (int cls_i = 0; cls_i < ncls; ++cls_i) {
   if constexpr (DGRAD) {
     const int cls = int(blockIdx.y) * ncls + cls_i;
@@ -1256,7 +1327,8 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
 #pragma unroll
     for (int i = 0; i < FM; ++i) fa[i][kk] = f_off(row0 + 16 * i + (lane & 15), chunk);
 #pragma unroll
-    for (int j = 0; j < FN; ++j) fb[j][kk] = A_TILE + f_off(col0 + 16 * j + (lane & 15), chunk);
+    for (int j = 0; j < FN; ++j)
+      fb[j][kk] = A_TILE + f_off(col0 + (DIRECT ? c1_row_chan(j, lane & 15) : 16 * j + (lane & 15)), chunk);
   }
   auto mma = [&](int buf) {
     const char* ai = smem + buf * STG;
@@ -1271,7 +1343,8 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bb[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = DIRECT ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[j], a[i], acc[i][j], 0, 0, 0)
+                             : __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bb[j], acc[i][j], 0, 0, 0);
     }
   };
   if constexpr (C4) {   // the first layer's K is one step
@@ -1292,6 +1365,62 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
 #pragma unroll
     for (int u = 0; u < NST - 1; ++u)
       if (u < nsteps) issue(u, u);
+    // ACT: fold the BN statistics while the first stages load (scratch: the
+    // last stage's buffer, issued only after the k-loop's first barrier)
+    constexpr int NSET = ACT > 0 ? ACT : 1;
+    float cis[NSET][8], cnm[NSET][8], cw[NSET][8], cb[NSET][8];
+    if constexpr (ACT > 0) {
+      double* part = reinterpret_cast<double*>(smem + (NST - 1) * STG);
+      float* coef = reinterpret_cast<float*>(smem + (NST - 1) * STG + kThreads * 8);
+      int* flag = reinterpret_cast<int*>(coef + 2 * p.C);
+      bn_acc_column_sums(p.act.acc, p.act.R, 2 * p.C, part);
+      BnFwdFinal f;
+      f.eps = p.act.eps, f.momentum = p.act.momentum, f.mean = p.act.mean, f.invstd = p.act.invstd;
+      f.rm = p.act.rm, f.rv = p.act.rv, f.tracked = p.act.tracked;
+      for (int c = t; c < p.C; c += kThreads)
+        bn_fwd_finalize(f, part, p.C, p.act.M, c, blockIdx.x == 0, coef[c], coef[p.C + c]);
+      __syncthreads();
+      bn_acc_release(p.act.acc, p.act.R, p.C, flag);
+#pragma unroll
+      for (int u = 0; u < NSET; ++u) {
+        const int cbase = (u * FBK + acs * 8) & (p.C - 1);   // this thread's chunk channels at k-steps u, u + NSET, ...
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          cis[u][e] = coef[p.C + cbase + e];
+          cnm[u][e] = -coef[cbase + e] * cis[u][e];
+          cw[u][e] = p.act.w[cbase + e];
+          cb[u][e] = p.act.b[cbase + e];
+        }
+      }
+    }
+    // leaky(bn(.)) of this thread's own chunks of stage ks, in place (coefficient set U)
+    auto act_stage = [&](int ks, int buf, auto U) {
+      constexpr int u = decltype(U)::value;
+      const int kc = ks * FBK + acs * 8;
+      const int tap = kc >> p.cshift, ch = kc & (p.C - 1);
+      const uint32_t tbit = 1u << tap;
+      const bool centre = p.act_out && n0 == 0 && unsigned((tap >> 2) - 1) < 2u && unsigned((tap & 3) - 1) < 2u;
+      const uint32_t soff = uint32_t(((((tap >> 2) * p.SW + (tap & 3)) << p.cshift) + ch) * 2);
+      char* st = smem + buf * STG + wv * 1024 + lane * 16;
+#pragma unroll
+      for (int j = 0; j < RJ; ++j) {
+        if (!(vmask[j] & tbit)) continue;   // padding: stays zero
+        uint4 v = *reinterpret_cast<const uint4*>(st + j * 4096);
+        uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float z0 = fmaf(fmaf(__uint_as_float(w4[q] << 16), cis[u][2 * q], cnm[u][2 * q]), cw[u][2 * q],
+                                cb[u][2 * q]);
+          const float z1 = fmaf(fmaf(__uint_as_float(w4[q] & 0xFFFF0000u), cis[u][2 * q + 1], cnm[u][2 * q + 1]),
+                                cw[u][2 * q + 1], cb[u][2 * q + 1]);
+          const f32x2 pr = {z0 > 0.f ? z0 : z0 * p.act.slope, z1 > 0.f ? z1 : z1 * p.act.slope};
+          w4[q] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2));
+        }
+        v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        *reinterpret_cast<uint4*>(st + j * 4096) = v;
+        if (centre) *reinterpret_cast<uint4*>(reinterpret_cast<char*>(p.act_out) + (abase[j] + soff)) = v;
+      }
+    };
     int cur = 0;
     for (int ks = 0; ks < nsteps; ++ks) {
       // the stages younger than ks that were issued (the last steps issue none)
@@ -1299,6 +1428,12 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
       if (younger >= 2) __builtin_amdgcn_s_waitcnt(kWaitTwo);
       else if (younger == 1) __builtin_amdgcn_s_waitcnt(kWaitOne);
       else __builtin_amdgcn_s_waitcnt(kWaitAll);
+      if constexpr (ACT == 1) {
+        act_stage(ks, cur, std::integral_constant<int, 0>());
+      } else if constexpr (ACT == 2) {
+        if (ks & 1) act_stage(ks, cur, std::integral_constant<int, 1>());
+        else act_stage(ks, cur, std::integral_constant<int, 0>());
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
@@ -1341,6 +1476,99 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     __syncthreads();   // the epilogue reuses the staging LDS
   }
 
+  if constexpr (DIRECT) {
+    // this lane's pixel of fragment i: GEMM row row0 + 16 i + (lane & 15), its
+    // output offset and range flag from the row table; its channels: 32 q + 8 g .. + 7
+    const int g = lane >> 4;
+    const int4* rtab = reinterpret_cast<const int4*>(smem + RT_OFF);
+    int ob[FM];
+    bool pv[FM];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int4 r = rtab[row0 + 16 * i + (lane & 15)];
+      ob[i] = r.z + n0 + col0 + 8 * g, pv[i] = r.w != 0;
+    }
+    uint4 xq[FM][NQ];   // BN-backward fusion: the BN input at the same offsets, loads issued first
+    if (bnf) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+          xq[i][q] = pv[i] ? *reinterpret_cast<const uint4*>(p.bn.x + ob[i] + 32 * q) : make_uint4(0, 0, 0, 0);
+    }
+    float is[NQ][8], nm[NQ][8], ww[NQ][8], bb[NQ][8];
+    if (bnf) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int c = n0 + col0 + 32 * q + 8 * g + e;
+          is[q][e] = p.bn.invstd[c];
+          nm[q][e] = -p.bn.mean[c] * is[q][e];
+          ww[q][e] = p.bn.w[c];
+          bb[q][e] = p.bn.b[c];
+        }
+    }
+    float sum[NQ][8], sq[NQ][8];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sum[q][e] = sq[q][e] = 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        uint32_t pk[4];
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {   // channels 8 g + 2 h, + 1: fragment 2 q + (h >> 1), rows 2 (h & 1), + 1
+          const f32x4& a = acc[i][2 * q + (h >> 1)];
+          const f32x2 pr = {a[2 * (h & 1)], a[2 * (h & 1) + 1]};
+          pk[h] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2));   // RNE
+        }
+        if (!pv[i]) continue;
+        *reinterpret_cast<uint4*>(p.dst + ob[i] + 32 * q) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+        if (!DGRAD && p.stats) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float v = __uint_as_float(e & 1 ? pk[e >> 1] & 0xFFFF0000u : pk[e >> 1] << 16);
+            sum[q][e] += v;
+            sq[q][e] += v * v;
+          }
+        }
+        if (bnf) {
+          const uint32_t xw[4] = {xq[i][q].x, xq[i][q].y, xq[i][q].z, xq[i][q].w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float gv = __uint_as_float(e & 1 ? pk[e >> 1] & 0xFFFF0000u : pk[e >> 1] << 16);
+            const float xh = fmaf(__uint_as_float(e & 1 ? xw[e >> 1] & 0xFFFF0000u : xw[e >> 1] << 16),
+                                  is[q][e], nm[q][e]);
+            const float gz = fmaf(xh, ww[q][e], bb[q][e]) > 0.f ? gv : gv * p.bn.slope;
+            bs[q][e] += gz;
+            bq[q][e] += gz * xh;
+          }
+        }
+      }
+    if (!DGRAD && p.stats) {
+      // the 16 lanes of a group hold the same channels; then the WGN waves of a
+      // row group write disjoint channel ranges of row wm
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) sum[q][e] += __shfl_xor(sum[q][e], o), sq[q][e] += __shfl_xor(sq[q][e], o);
+      if ((lane & 15) == 0) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            red[(wm * 2 + 0) * BN + col0 + 32 * q + 8 * g + e] = sum[q][e];
+            red[(wm * 2 + 1) * BN + col0 + 32 * q + 8 * g + e] = sq[q][e];
+          }
+      }
+      __syncthreads();
+    }
+  } else {
   // Epilogue stores (geometry above)
   int eob[NJ];
   bool epin[NJ];
@@ -1478,25 +1706,48 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
         const float xh = fmaf(__uint_as_float(xb), is[q], nm[q]);
         const float g = __uint_as_float(gb);
         const float gz = fmaf(xh, ww[q], bb[q]) > 0.f ? g : g * p.bn.slope;
-        bs[q] += gz;
-        bq[q] += gz * xh;
+        bs[0][q] += gz;
+        bq[0][q] += gz * xh;
       }
     }
   }
+  }
   }   // parity classes
   if (bnf) {
-    // lanes with the same ec hold the same channels: fold them, then the 4
-    // waves through LDS (the statistics area is free in backward)
+    // lanes holding the same channels fold, then the row groups through LDS
+    // (the statistics area is free in backward): DIRECT -- the 16 lanes of a
+    // group, waves (wm, wn) writing row wm; else lanes with the same ec, 4 waves
+    constexpr int RG = DIRECT ? WGM : 4;
+    if constexpr (DIRECT) {
+      const int g = lane >> 4, wm = wave / WGN, col0 = (wave % WGN) * (BN / WGN);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
+      for (int q = 0; q < NQ; ++q)
 #pragma unroll
-      for (int o = CPR; o < 64; o <<= 1) bs[q] += __shfl_xor(bs[q], o), bq[q] += __shfl_xor(bq[q], o);
-    }
-    if (lane < CPR) {
+        for (int e = 0; e < 8; ++e)
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) bs[q][e] += __shfl_xor(bs[q][e], o), bq[q][e] += __shfl_xor(bq[q][e], o);
+      __syncthreads();   // every wave is done with the last class's LDS
+      if ((lane & 15) == 0) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            red[(wm * 2 + 0) * BN + col0 + 32 * q + 8 * g + e] = bs[q][e];
+            red[(wm * 2 + 1) * BN + col0 + 32 * q + 8 * g + e] = bq[q][e];
+          }
+      }
+    } else {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        red[(wave * 2 + 0) * BN + ec * 8 + q] = bs[q];
-        red[(wave * 2 + 1) * BN + ec * 8 + q] = bq[q];
+#pragma unroll
+        for (int o = CPR; o < 64; o <<= 1) bs[0][q] += __shfl_xor(bs[0][q], o), bq[0][q] += __shfl_xor(bq[0][q], o);
+      }
+      if (lane < CPR) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          red[(wave * 2 + 0) * BN + ec * 8 + q] = bs[0][q];
+          red[(wave * 2 + 1) * BN + ec * 8 + q] = bq[0][q];
+        }
       }
     }
     __syncthreads();
@@ -1504,7 +1755,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
       const int which = t / BN, c = t - which * BN;
       float v = 0.f;
 #pragma unroll
-      for (int w4 = 0; w4 < 4; ++w4) v += red[(w4 * 2 + which) * BN + c];
+      for (int w4 = 0; w4 < RG; ++w4) v += red[(w4 * 2 + which) * BN + c];
       // channel-major [2][NOUT][rows], row = (pixel tile, parity class); or
       // added into replica row % R of an accumulator [R][2][NOUT] (bn_bwd_apply_acc folds it)
       const int row = mt * 4 + int(blockIdx.y) * ncls;
@@ -1554,9 +1805,6 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
 // stay in registers until the block's last tile.
 constexpr int kC1Cols = 64;   // output columns per tile
 
-__device__ __forceinline__ int c1_row_chan(int f, int rho) {   // A row rho of channel fragment f
-  return 32 * (f >> 1) + 8 * (rho >> 2) + 4 * (f & 1) + (rho & 3);
-}
 
 template <int BN, int TR, bool U8>
 __global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tiles_per_block) {
@@ -1809,9 +2057,14 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
     return hipErrorInvalidValue;
   if ((reinterpret_cast<uintptr_t>(p.x) | reinterpret_cast<uintptr_t>(p.dy)) & 15) return hipErrorInvalidValue;
   if (p.lut && (p.Cin != 4 || (reinterpret_cast<uintptr_t>(p.lut) & 7))) return hipErrorInvalidValue;
-  if (p.bn_dy.y && (p.Cin != 4 || (reinterpret_cast<uintptr_t>(p.bn_dy.y) & 15) || !p.bn_dy.mean || !p.bn_dy.invstd ||
-                    !p.bn_dy.w || !p.bn_dy.b || !p.bn_dy.dw || !p.bn_dy.db))
-    return hipErrorInvalidValue;   // the 4-channel first layer's kernel only
+  if (p.bn_dy.y) {
+    const bool given = p.bn_dy.dw && p.bn_dy.db;                               // folded elsewhere
+    const bool folds = p.bn_dy.acc && p.bn_dy.R > 0 && p.bn_dy.dw_out && p.bn_dy.db_out;   // folded here
+    if ((reinterpret_cast<uintptr_t>(p.bn_dy.y) | reinterpret_cast<uintptr_t>(p.bn_dy.gx_out)) & 15 ||
+        !p.bn_dy.mean || !p.bn_dy.invstd || !p.bn_dy.w || !p.bn_dy.b || given == folds || p.fold.acc ||
+        (p.Cin != 4 && !folds) || (p.Cin == 4 && p.bn_dy.gx_out) || 2 * p.Cout > 512)   // fold scratch: 4 KiB
+      return hipErrorInvalidValue;
+  }
   if (int64_t(p.N) * p.H * p.W * p.Cin * 2 >= int64_t(kOOB) || p.M * p.Cout * 2 >= int64_t(kOOB))
     return hipErrorInvalidValue;   // 32-bit buffer offsets
   const bool c4 = p.Cin == 4;
@@ -1837,13 +2090,16 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
       return hipErrorInvalidValue;
     grid += 1;
   }
-  if (c4 && c4_wave_private()) conv_wgrad_c4w_kernel<<<unsigned(grid), kThreads, 0, stream>>>(q);
+  // (a BN backward folded in-kernel: the wave-private first-layer kernel or the register-staged one)
+  const bool bn_folds = p.bn_dy.acc != nullptr;
+  if (c4 && (c4_wave_private() || bn_folds)) conv_wgrad_c4w_kernel<<<unsigned(grid), kThreads, 0, stream>>>(q);
   else if (c4) conv_wgrad_c4_kernel<<<unsigned(grid), kThreads, 0, stream>>>(q);
+  else if (bn_folds) conv_wgrad_kernel<true><<<unsigned(grid), kThreads, 0, stream>>>(q);
   else if (wgrad_staging() == 2 && (p.Cin & (p.Cin - 1)) == 0 && p.Wo >= 32)
     conv_wgrad_dma_kernel<2><<<unsigned(grid), kThreads, 0, stream>>>(q);
   else if (wgrad_staging() == 3 && (p.Cin & (p.Cin - 1)) == 0 && p.Wo >= 32)
     conv_wgrad_dma_kernel<3><<<unsigned(grid), kThreads, 0, stream>>>(q);
-  else conv_wgrad_kernel<<<unsigned(grid), kThreads, 0, stream>>>(q);
+  else conv_wgrad_kernel<false><<<unsigned(grid), kThreads, 0, stream>>>(q);
   const int64_t total = int64_t(p.Cout) * 16 * p.Cin;   // partial elements per slice
   ConvWgradParams::Reduce r;
   r.partial = p.partial, r.S = p.slices, r.Cout = p.Cout, r.Cin = p.Cin;
@@ -1918,9 +2174,29 @@ void launch_tap_gemm_st(const TapGemm& g, int bn, unsigned ytiles, hipStream_t s
   }
 }
 
+// forward with the input BatchNorm applied in the staging (TapGemm::act): 2 LDS-DMA stages
+template <int BM, int ACT>
+void launch_tap_gemm_act(const TapGemm& g, int bn, hipStream_t stream) {
+  const dim3 grid(unsigned((g.M + BM - 1) / BM * (g.NOUT / bn)));
+  if (bn == 128) tap_gemm_kernel<false, 128, false, BM, 2, 1, ACT><<<grid, kThreads, 0, stream>>>(g);
+  else if (bn == 64) tap_gemm_kernel<false, 64, false, BM, 2, 1, ACT><<<grid, kThreads, 0, stream>>>(g);
+  else tap_gemm_kernel<false, 32, false, BM, 2, 1, ACT><<<grid, kThreads, 0, stream>>>(g);
+}
+
 template <bool DGRAD>
 void launch_tap_gemm(const TapGemm& g, unsigned ytiles, hipStream_t stream) {
   const int bn = conv_tile_channels(g.NOUT, g.C == 4 && !DGRAD);
+  if (!DGRAD && g.act.on()) {
+    const bool two = g.C > FBK;   // a thread's chunk alternates between two channel sets (C = 128)
+    if (conv_tile_pixels(g.M, g.NOUT, int(ytiles)) == 64) {
+      if (two) launch_tap_gemm_act<64, 2>(g, bn, stream);
+      else launch_tap_gemm_act<64, 1>(g, bn, stream);
+    } else {
+      if (two) launch_tap_gemm_act<FBM, 2>(g, bn, stream);
+      else launch_tap_gemm_act<FBM, 1>(g, bn, stream);
+    }
+    return;
+  }
   if (conv_tile_pixels(g.M, g.NOUT, int(ytiles)) == 64) launch_tap_gemm_st<DGRAD, 64>(g, bn, ytiles, stream);
   else launch_tap_gemm_st<DGRAD, FBM>(g, bn, ytiles, stream);
 }
@@ -2001,6 +2277,14 @@ hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream) {
   if (p.lut && (p.Cin != 4 || (reinterpret_cast<uintptr_t>(p.lut) & 7))) return hipErrorInvalidValue;
   g.acc_r = p.stats ? p.acc_r : 0;
   if (g.acc_r < 0 || g.acc_r > 64) return hipErrorInvalidValue;
+  if (p.act.on()) {   // the input BN applied in the staging: C <= 128 (two coefficient sets), accumulator given
+    if (p.Cin == 4 || p.Cin > 2 * FBK || !p.act.acc || p.act.R <= 0 || !p.act.b || !p.act.mean || !p.act.invstd ||
+        p.act.M != int64_t(p.N) * p.H * p.W || (reinterpret_cast<uintptr_t>(p.act_out) & 15) ||
+        (p.act_out && (p.H % 2 || p.W % 2)))   // the centre taps cover every input element: even sides
+      return hipErrorInvalidValue;
+    g.act = p.act;
+    g.act_out = p.act_out;
+  }
   if (p.Cin == 4 && g.wc != 3 && g.wc != 4) return hipErrorInvalidValue;
   // the first layer from a decoded input patch (conv1_fwd_kernel): BN sums
   // into an accumulator (or none), Cout 32 / 64

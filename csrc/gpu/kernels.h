@@ -337,12 +337,20 @@ struct ConvWgradParams {
     float* dw = nullptr;
     float* db = nullptr;
   } fold;
-  // bn_dy.y != nullptr (the 4-channel first layer only): dy is NOT the
+  // bn_dy.y != nullptr: dy is NOT the
   // convolution's output gradient but the gradient of the BatchNorm +
   // LeakyReLU that follows it, whose input is bn_dy.y ([M][Cout] bf16); the
   // kernel applies that BN's backward while staging dY (bn_fold.h BnBwdCoef,
   // bit-identical to bn_bwd_apply), so no bn_bwd_apply pass runs.  dw / db:
   // the BN's folded backward sums (db = sum gz, dw = sum gz * xhat).
+  // With bn_dy.acc (any layer): dw / db are not given but folded by every
+  // block from the BN's backward accumulator (fp64 [R][2][Cout], filled by
+  // the following layer's data-gradient epilogue); block 0 writes them to
+  // dw_out / db_out (the BN's parameter gradients), the last block clears the
+  // accumulator; gx_out (nullable) receives the BN's input gradient gx (the
+  // blocks of the first column tile store their staged dY chunks: every
+  // element once) -- the operand of this layer's data gradient, which then
+  // runs after this kernel.  Not the DMA-staged kernel.
   struct BnDy {
     const uint16_t* y = nullptr;
     const float* mean = nullptr;
@@ -352,6 +360,11 @@ struct ConvWgradParams {
     const float* dw = nullptr;
     const float* db = nullptr;
     float slope = 0.f;
+    double* acc = nullptr;
+    int R = 0;
+    float* dw_out = nullptr;
+    float* db_out = nullptr;
+    uint16_t* gx_out = nullptr;
   } bn_dy;
 };
 // Cin % 32 == 0 with Cout % 64 == 0, or Cin == 4 (the first layer) with Cout % 32 == 0.
@@ -379,6 +392,30 @@ hipError_t conv_wgrad_reduce(const ConvWgradParams::Reduce& r, hipStream_t strea
 // y [N][Ho][Wo][Cout] bf16.  stats (nullable): [2][Cout][conv_fwd_tiles(M, Cout)]
 // fp32 per-tile sum / sum of squares of the rounded y (channel-major) -- the
 // partials bn_finalize_rows folds into BatchNorm statistics.
+// A training BatchNorm+LeakyReLU applied by its CONSUMER as it reads the BN's
+// input (the conv forward's operand staging, its weight gradient's re-read,
+// the head's pooling): no apply pass and no activation tensor.  The batch
+// statistics sit in the BnAcc accumulator the producer added into (acc,
+// fp64 [R][2][C]); every consumer block folds them, block 0 writes mean /
+// invstd and the running statistics, and the last block clears the
+// accumulator (bn_fold.h).  With acc == nullptr the consumer reads mean /
+// invstd as given (the weight gradient, after the forward wrote them).
+struct BnActIn {
+  double* acc = nullptr;
+  int R = 0;
+  int64_t M = 0;                   // elements per channel
+  float eps = 0.f, momentum = 0.f;
+  const float* w = nullptr;        // affine weight / bias, fp32 [C]
+  const float* b = nullptr;
+  float slope = 0.f;
+  float* mean = nullptr;           // fp32 [C]: written (acc) or read
+  float* invstd = nullptr;
+  float* rm = nullptr;             // running statistics (nullable)
+  float* rv = nullptr;
+  int64_t* tracked = nullptr;
+  __host__ __device__ bool on() const { return w != nullptr; }
+};
+
 struct ConvFwdParams {
   const uint16_t* x = nullptr;
   const uint16_t* w = nullptr;
@@ -392,6 +429,12 @@ struct ConvFwdParams {
   // the convolution's tile loads (padding stays 0)
   const uint16_t* lut = nullptr;
   int acc_r = 0;        // > 0: stats points at a bn_apply_acc accumulator (fp64 [acc_r][2][Cout], atomic adds)
+  // act.on(): x is the input of a BatchNorm+LeakyReLU applied inside this
+  // convolution's operand staging (Cin <= 128); act_out (nullable) receives
+  // that activation, [N][H][W][Cin] bf16 -- written by the convolution, no
+  // apply pass (BnActIn)
+  BnActIn act;
+  uint16_t* act_out = nullptr;
 };
 // Cin a power of two >= 8, or Cin == 4 (first layer, RGBA-decoded frames); Cout % 32 == 0.
 bool conv_fwd_supported(int Cin, int Cout);
@@ -446,29 +489,6 @@ struct BnBwdFuse {
 };
 int64_t conv_dgrad_bn_rows(int N, int H, int W, int Cin);
 
-// A training BatchNorm+LeakyReLU applied by its CONSUMER as it reads the BN's
-// input (the conv forward's operand staging, its weight gradient's re-read,
-// the head's pooling): no apply pass and no activation tensor.  The batch
-// statistics sit in the BnAcc accumulator the producer added into (acc,
-// fp64 [R][2][C]); every consumer block folds them, block 0 writes mean /
-// invstd and the running statistics, and the last block clears the
-// accumulator (bn_fold.h).  With acc == nullptr the consumer reads mean /
-// invstd as given (the weight gradient, after the forward wrote them).
-struct BnActIn {
-  double* acc = nullptr;
-  int R = 0;
-  int64_t M = 0;                   // elements per channel
-  float eps = 0.f, momentum = 0.f;
-  const float* w = nullptr;        // affine weight / bias, fp32 [C]
-  const float* b = nullptr;
-  float slope = 0.f;
-  float* mean = nullptr;           // fp32 [C]: written (acc) or read
-  float* invstd = nullptr;
-  float* rm = nullptr;             // running statistics (nullable)
-  float* rv = nullptr;
-  int64_t* tracked = nullptr;
-  __host__ __device__ bool on() const { return w != nullptr; }
-};
 hipError_t conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int N, int H, int W, int Cin, int Cout,
                       hipStream_t stream, const BnBwdFuse* bn = nullptr);
 // bn_finalize over `nblocks` partial rows produced elsewhere (conv_fwd's epilogue)

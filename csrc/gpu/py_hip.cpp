@@ -270,9 +270,18 @@ PYBIND11_MODULE(_hip, m) {
            py::object bn_dy) -> py::object {
           ConvWgradParams p;
           p.cin_out = cin_out;
-          if (!bn_dy.is_none()) {   // (y, mean, invstd, w, b, dw, db, slope)
+          if (!bn_dy.is_none()) {   // (y, mean, invstd, w, b, dw, db, slope[, acc, R, dw_out, db_out, gx_out])
             const py::tuple f = bn_dy.cast<py::tuple>();
-            if (f.size() != 8) throw std::invalid_argument("conv_wgrad: bn_dy is (y, mean, invstd, w, b, dw, db, slope)");
+            if (f.size() != 8 && f.size() != 13)
+              throw std::invalid_argument(
+                  "conv_wgrad: bn_dy is (y, mean, invstd, w, b, dw, db, slope[, acc, R, dw_out, db_out, gx_out])");
+            if (f.size() == 13) {
+              p.bn_dy.acc = ptr<double>(f[8].cast<uintptr_t>());
+              p.bn_dy.R = f[9].cast<int>();
+              p.bn_dy.dw_out = ptr<float>(f[10].cast<uintptr_t>());
+              p.bn_dy.db_out = ptr<float>(f[11].cast<uintptr_t>());
+              p.bn_dy.gx_out = ptr<uint16_t>(f[12].cast<uintptr_t>());
+            }
             p.bn_dy.y = ptr<const uint16_t>(f[0].cast<uintptr_t>());
             p.bn_dy.mean = ptr<const float>(f[1].cast<uintptr_t>());
             p.bn_dy.invstd = ptr<const float>(f[2].cast<uintptr_t>());
@@ -383,8 +392,11 @@ PYBIND11_MODULE(_hip, m) {
         });
   m.def("conv_fwd",
         [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, int N, int H, int W, int Cin, int Ho, int Wo,
-           int Cout, uintptr_t stream, int w_channels, int acc_r, uintptr_t lut) {
+           int Cout, uintptr_t stream, int w_channels, int acc_r, uintptr_t lut, py::object act,
+           uintptr_t act_out) {
           ConvFwdParams p;
+          p.act = act_from(act, "conv_fwd");
+          p.act_out = ptr<uint16_t>(act_out);
           p.lut = ptr<const uint16_t>(lut);
           p.w_channels = w_channels;
           p.acc_r = acc_r;
@@ -398,7 +410,7 @@ PYBIND11_MODULE(_hip, m) {
         },
         py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"), py::arg("N"), py::arg("H"), py::arg("W"),
         py::arg("Cin"), py::arg("Ho"), py::arg("Wo"), py::arg("Cout"), py::arg("stream"), py::arg("w_channels") = 0,
-        py::arg("acc_r") = 0, py::arg("lut") = 0);
+        py::arg("acc_r") = 0, py::arg("lut") = 0, py::arg("act") = py::none(), py::arg("act_out") = 0);
   // BatchNorm+LeakyReLU forward from conv_fwd's per-tile statistics: finalize + apply
   m.def("bn_forward_from_stats",
         [](uintptr_t x, uintptr_t y, int64_t M, int C, int dtype, uintptr_t stats, int nrows, float eps,

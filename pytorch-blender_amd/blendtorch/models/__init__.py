@@ -39,6 +39,10 @@ class Discriminator(nn.Module):
     defer_first_bn = True
     # the last BatchNorm+LeakyReLU's forward apply runs in the fused head's pooling (ops.BnActLazy)
     lazy_head_bn = True
+    # the other BatchNorm+LeakyReLU applies run in the next MFMA convolution's operand staging
+    lazy_conv_bn = True
+    # every BatchNorm+LeakyReLU backward apply runs in the producing convolution's weight gradient
+    defer_bn_bwd = True
 
     def __init__(self, nc=3, ndf=32, adaptive=False, fused=True):
         super().__init__()
@@ -140,7 +144,7 @@ class Discriminator(nn.Module):
             lut = ops.decode_lut_bf16(decode, x.device)
         if ok:
             # adaptive stack: the last BN's apply runs in the head's pooling (BnActLazy)
-            z, link, lazy = self._run_bf16(x, body, mfma, want_link=True, lut=lut,
+            z, link, lazy = self._run_bf16(x, body, mfma, want_link=True, lut=lut, want_lazy=True,
                                            lazy_tail=adaptive and self.lazy_head_bn)
             if adaptive or tuple(z.shape[2:]) == pool:
                 if not z.is_contiguous(memory_format=torch.channels_last):
@@ -156,7 +160,26 @@ class Discriminator(nn.Module):
         tgt = target if isinstance(target, torch.Tensor) else torch.full_like(out, float(target))
         return F.binary_cross_entropy(out, tgt), out
 
-    def _run_bf16(self, x, layers, mfma, want_link=False, lut=None, lazy_tail=False):
+    @staticmethod
+    def _conv_applies_bn(x, layers, j, mfma):
+        """True when layers[j] is an MFMA convolution that can apply the
+        BatchNorm+LeakyReLU producing its input ``x`` in its own operand
+        staging (ops.BnActLazy): the accumulator-statistics path (a fused BN
+        follows it) on a bf16 input of 8-128 channels."""
+        from .. import ops
+        if not mfma or j >= len(layers) or not isinstance(layers[j], nn.Conv2d):
+            return False
+        m = layers[j]
+        nxt = layers[j + 1] if j + 1 < len(layers) else None
+        cin = m.in_channels
+        # even input sides: the centre taps that write the activation cover every input row / column
+        return (x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0 and m.stride == (2, 2) and m.padding == (1, 1) and m.bias is None and m.groups == 1
+                and m.dilation == (1, 1) and tuple(m.kernel_size) == (4, 4) and ops.conv_wgrad_supported(x, m.weight)
+                and 8 <= cin <= 128 and cin & (cin - 1) == 0 and m.out_channels % 32 == 0
+                and isinstance(nxt, ops.BatchNormLeakyReLU2d) and ops.bn_acc_supported(m.out_channels)
+                and nxt.fused_with_stats(x.new_empty((1, m.out_channels, 1, 1), dtype=torch.bfloat16)))
+
+    def _run_bf16(self, x, layers, mfma, want_link=False, lut=None, lazy_tail=False, want_lazy=False):
         import torch.nn.functional as F
         from .. import ops
         convs = [m for m in layers if isinstance(m, nn.Conv2d)]
@@ -173,7 +196,7 @@ class Discriminator(nn.Module):
             if need:
                 wts = dict(zip(need, ops.conv_weights_t([w16s[k] for k in need])))
         ci = -1
-        stats = link = defer = lazy = None
+        stats = link = defer = lazy = act_next = None
         # the MFMA weight gradients of one backward hand their slice reduce to the
         # next one (ops.WgradChain): the first such layer's runs last and closes it
         wchain = ops.WgradChain() if (mfma and torch.is_grad_enabled() and x.is_cuda) else None
@@ -202,12 +225,17 @@ class Discriminator(nn.Module):
                     # handed down to it always run (frozen layers flush, see ops.conv4x4s2)
                     closes = first_mfma and m.weight.requires_grad
                     wk = dict(wt=wts.get(ci), bn_link=bl, wchain=wchain, wlast=closes)
+                    if act_next is not None:   # x is the previous BN's input: apply it in the staging
+                        wk['act'], act_next = act_next, None
                     if ci == 0 and lut is not None:
                         wk['lut'] = lut    # raw u8 frames: decoded in this layer's kernels
-                        if fuse and torch.is_grad_enabled() and self.defer_first_bn:
-                            # no data gradient here: the following BN's backward apply runs
-                            # inside this layer's weight-gradient kernel (ops.BnDeferred)
-                            defer = wk['bn_out'] = ops.BnDeferred()
+                    if (fuse and torch.is_grad_enabled() and ops.bn_acc_supported(m.out_channels)
+                            and (self.defer_bn_bwd or (ci == 0 and lut is not None and self.defer_first_bn))):
+                        # the following BN's backward apply runs inside this layer's
+                        # weight-gradient kernel (ops.BnDeferred / BnBwdFold): it folds the
+                        # BN's backward sums, applies the BN backward to the staged dY and
+                        # writes the BN's input gradient for this layer's data gradient
+                        defer = wk['bn_out'] = ops.BnDeferred()
                     if closes:
                         first_mfma = False
                     if fuse and ops.bn_acc_supported(m.out_channels):
@@ -222,14 +250,23 @@ class Discriminator(nn.Module):
                 else:
                     if ci == 0 and lut is not None:
                         raise ValueError('raw u8 frames need the MFMA first layer')
+                    if act_next is not None:
+                        raise RuntimeError('_run_bf16: a lazily applied BN feeds a layer off the MFMA path')
                     link = None
                     x = F.conv2d(x, w16, None, m.stride, m.padding, m.dilation, m.groups)
             elif stats is not None and isinstance(m, ops.BatchNormLeakyReLU2d):
                 link = ops.BnLink() if torch.is_grad_enabled() else None
-                if (lazy_tail and i == len(layers) - 1 and isinstance(stats, ops.BnAccumulator)
-                        and x.dtype == torch.bfloat16):
+                acc_bf16 = isinstance(stats, ops.BnAccumulator) and x.dtype == torch.bfloat16
+                j = i + 1   # the consumer: the next layer that is not an Identity
+                while j < len(layers) and isinstance(layers[j], nn.Identity):
+                    j += 1
+                if lazy_tail and j == len(layers) and acc_bf16:
                     lazy = ops.BnActLazy()   # the caller's consumer applies this BN
+                elif acc_bf16 and self.lazy_conv_bn and self._conv_applies_bn(x, layers, j, mfma):
+                    lazy = act_next = ops.BnActLazy()   # the next convolution applies this BN
                 x = m.forward_from_stats(x, stats, link, defer, lazy)
+                if lazy is act_next:
+                    lazy = None
                 stats = defer = None
             else:
                 if not isinstance(m, nn.Identity):
@@ -237,8 +274,9 @@ class Discriminator(nn.Module):
                 x = m(x)
         # want_link: also the BnLink of a BN whose output is returned (its consumer
         # -- the fused head -- can then do that BN's backward reduction), and with
-        # lazy_tail that BN's BnActLazy (None: x is the BN's output, not its input)
-        if lazy_tail:
+        # want_lazy the BnActLazy of that BN when lazy_tail let it skip its apply
+        # (None: x is the BN's output, not its input)
+        if want_lazy:
             return x, link, lazy
         return (x, link) if want_link else x
 

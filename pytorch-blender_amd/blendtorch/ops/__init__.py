@@ -830,7 +830,7 @@ class BnLink:
     ``part``; the BN backward then only finalizes and applies (one pass over
     the activation fewer).  ``part`` is consumed once."""
     __slots__ = ('x', 'mean', 'invstd', 'w', 'b', 'slope', 'part', 'rows', 'gy', 'acc', 'params', 'dw', 'db',
-                 'dw_sunk', 'db_sunk', 'folded')
+                 'dw_sunk', 'db_sunk', 'folded', 'defer_fold')
 
     def __init__(self):
         self.x = self.mean = self.invstd = self.w = self.b = self.part = self.gy = None
@@ -841,6 +841,9 @@ class BnLink:
         # conv's weight-gradient launch already folded the accumulator into them
         self.dw = self.db = None
         self.dw_sunk = self.db_sunk = self.folded = False
+        # the BN hands its backward to the convolution that produced its input
+        # (BnDeferred, BnBwdFold): that one folds the accumulator, not the consumer
+        self.defer_fold = False
 
     def fold_args(self, M):
         """``(acc, R, C, M, dw, db)`` for ``conv_wgrad(fold=)``: fold this BN's
@@ -878,6 +881,23 @@ class BnLink:
         return part, rows
 
 
+class BnBwdFold:
+    """A BatchNorm+LeakyReLU backward handed to the weight gradient of the
+    convolution that produced the BN's input (:class:`BnDeferred`,
+    ``conv_wgrad(bn_dy=)``): the BN's saved input ``x`` (NHWC), batch
+    ``mean``/``invstd``, affine ``w``/``b``, ``slope``, its accumulator
+    ``acc`` (the backward sums the consumer's data gradient -- or the head --
+    added), the destinations of its ``dw``/``db`` gradients (``done``: the
+    parameters whose bucket views they are) and ``gx_out``, the BN's input
+    gradient (set by the convolution for its data gradient)."""
+    __slots__ = ('x', 'mean', 'invstd', 'w', 'b', 'slope', 'acc', 'dw', 'db', 'done', 'gx_out')
+
+    def __init__(self, x, mean, invstd, w, b, slope, acc, dw, db, done):
+        self.x, self.mean, self.invstd, self.w, self.b, self.slope = x, mean, invstd, w, b, slope
+        self.acc, self.dw, self.db, self.done = acc, dw, db, done
+        self.gx_out = None
+
+
 class BnDeferred:
     """Hand-off of a BatchNorm+LeakyReLU backward to the 4-channel first
     convolution that produced the BN's input (:func:`conv4x4s2` ``bn_out=``).
@@ -902,8 +922,9 @@ class BnDeferred:
 
 class BnActLazy:
     """Hand-off of a training BatchNorm+LeakyReLU's FORWARD apply to the op
-    that consumes its output (the fused discriminator head,
-    :func:`disc_head_bce` ``act=``): the BN call returns its input ``y``
+    that consumes its output (the next MFMA convolution, :func:`conv4x4s2`
+    ``act=``, or the fused discriminator head, :func:`disc_head_bce`
+    ``act=``): the BN call returns its input ``y``
     unchanged and records here what the consumer needs to compute
     ``leaky(bn(y))`` itself while it reads ``y`` -- the statistics
     accumulator its blocks fold (block 0 writes mean / invstd and the running
@@ -984,6 +1005,7 @@ def _bn_function():
                 link.params = (weight, bias)
                 link.dw = link.db = None
                 link.folded = False
+                link.defer_fold = ctx.defer is not None and ctx.acc is not None
             return y.permute(0, 3, 1, 2)   # (lazy: a view of the input, the pre-BN values)
 
         @staticmethod
@@ -1019,6 +1041,24 @@ def _bn_function():
                 lk.folded = False
                 return (gx.permute(0, 3, 1, 2), out_w, out_b, None, None, None, None, None, None, None, None, None,
                         None)
+            if (not folded and ctx.defer is not None and ctx.acc is not None and part is not None and rows < 0
+                    and part.data_ptr() == ctx.acc.bwd.data_ptr()):
+                # the consumer filled the backward accumulator: the convolution that produced x
+                # folds it and applies this backward while staging its weight gradient's dY
+                # (BnBwdFold) -- gy passes on unchanged.  The dw / db it writes must not be
+                # accumulated into an existing .grad before that launch: bucket views or unset.
+                dw, w_sunk = _grad_dest(ctx.params[0], w)
+                db, b_sunk = _grad_dest(ctx.params[1], b)
+                if dw.dtype != torch.float32 or not dw.is_contiguous():
+                    dw, w_sunk = torch.empty_like(w), False
+                if db.dtype != torch.float32 or not db.is_contiguous():
+                    db, b_sunk = torch.empty_like(b), False
+                if (w_sunk or ctx.params[0].grad is None) and (b_sunk or ctx.params[1].grad is None):
+                    _count('bn_backward_deferred_fold')
+                    ctx.defer.pending = BnBwdFold(xs, mean, invstd, w, b, ctx.slope, ctx.acc, dw, db,
+                                                  tuple(p for p, sk in zip(ctx.params, (w_sunk, b_sunk)) if sk))
+                    return (gys.permute(0, 3, 1, 2), None if w_sunk else dw, None if b_sunk else db, None, None,
+                            None, None, None, None, None, None, None, None)
             if folded:
                 raise RuntimeError('BatchNormLeakyReLU2d: its statistics were folded for another gradient')
             # (not before the folded branch: the fold already took the bucket views)
@@ -1228,6 +1268,9 @@ class WgradChain:
             self.pending = self.keep = self.param = None
 
 
+_WGRAD_BLOCKS = int(os.environ.get('BT_WGRAD_BLOCKS', '512'))
+
+
 def conv_wgrad(x, dy, out, target_blocks=None, chain=None, last=True, lut=None, fold=None, bn_dy=None, param=None,
                fold_params=()):
     """fp32 weight gradient of a 4x4/s2/p1 convolution into ``out`` ([Cout, Cin,
@@ -1237,11 +1280,13 @@ def conv_wgrad(x, dy, out, target_blocks=None, chain=None, last=True, lut=None, 
     pending reduce inside this launch, and leave this layer's to the next
     call unless ``last`` -- ``out`` is then complete only after that call.
     ``lut``: ``x`` is raw u8 RGBA frames read through this decode table
-    (:func:`decode_lut_bf16`).  ``bn_dy`` (4-channel first layer): ``dy`` is
-    the output gradient of the BatchNorm+LeakyReLU that follows this
-    convolution and ``bn_dy`` that BN's ``(x, mean, invstd, w, b, dw, db,
-    slope)`` (:class:`BnDeferred`): the kernel applies the BN backward to
-    ``dy`` while staging it.  ``param`` / ``fold_params``: the parameters
+    (:func:`decode_lut_bf16`).  ``bn_dy``: ``dy`` is the output gradient of
+    the BatchNorm+LeakyReLU that follows this convolution, whose backward the
+    kernel applies to ``dy`` while staging it (:class:`BnDeferred`) -- a
+    :class:`BnBwdFold` (the kernel folds the BN's backward accumulator
+    itself, writes the BN's dw / db and, for a layer with a data gradient,
+    gx into ``gx_out``), or on the 4-channel first layer that BN's ``(x,
+    mean, invstd, w, b, dw, db, slope)`` with the sums already folded.  ``param`` / ``fold_params``: the parameters
     whose bucket-view gradients ``out`` / the fold complete (reported to
     the gradient-completion listener once their launch is enqueued)."""
     import torch
@@ -1256,7 +1301,8 @@ def conv_wgrad(x, dy, out, target_blocks=None, chain=None, last=True, lut=None, 
         raise ValueError('conv_wgrad needs channels-last x and dy')
     M = N * Ho * Wo
     if target_blocks is None:
-        target_blocks = 512   # 2 blocks per CU (profiles/r2/conv_bench_v2.jsonl)
+        # 2 blocks per CU (profiles/r2/conv_bench_v2.jsonl); BT_WGRAD_BLOCKS overrides (sweeps)
+        target_blocks = _WGRAD_BLOCKS
     slices = ext.conv_wgrad_slices(M, Cin, Cout, target_blocks)
     if slices <= 0:
         raise ValueError(f'conv_wgrad: unsupported channels Cin={Cin} Cout={Cout} (Cin % 32, Cout % 64)')
@@ -1270,22 +1316,43 @@ def conv_wgrad(x, dy, out, target_blocks=None, chain=None, last=True, lut=None, 
     if (lut is not None) != (x.dtype == torch.uint8) or (lut is not None and Cin != 4):
         raise ValueError('conv_wgrad: u8 input (4 channels) needs its decode table lut, and only u8 takes one')
     bnt = None
+    bn_done = ()
     if bn_dy is not None:
-        by, bmean, binv, bw, bb, bdw, bdb, bslope = bn_dy
-        if Cin != 4 or tuple(by.shape) != (N, Ho, Wo, Cout) or by.dtype != torch.bfloat16 or not by.is_contiguous():
-            raise ValueError('conv_wgrad(bn_dy=): the 4-channel first layer, BN input [N, Ho, Wo, Cout] bf16 NHWC')
-        for t in (bmean, binv, bw, bb, bdw, bdb):
+        if isinstance(bn_dy, BnBwdFold):   # sums folded in the kernel, gx written for the data gradient
+            by, bmean, binv, bw, bb, bslope = bn_dy.x, bn_dy.mean, bn_dy.invstd, bn_dy.w, bn_dy.b, bn_dy.slope
+            sums = (bn_dy.dw, bn_dy.db)
+            gxo = bn_dy.gx_out
+            if gxo is not None and (gxo.shape != dy.shape or gxo.dtype != torch.bfloat16
+                                    or not gxo.is_contiguous(memory_format=cl) or Cin == 4):
+                raise ValueError('conv_wgrad(bn_dy=): gx_out is shaped like dy (a layer with a data gradient)')
+        else:
+            by, bmean, binv, bw, bb, bdw, bdb, bslope = bn_dy
+            sums = (bdw, bdb)
+            if Cin != 4:
+                raise ValueError('conv_wgrad(bn_dy=): given sums on the 4-channel first layer only')
+        if tuple(by.shape) != (N, Ho, Wo, Cout) or by.dtype != torch.bfloat16 or not by.is_contiguous():
+            raise ValueError('conv_wgrad(bn_dy=): BN input [N, Ho, Wo, Cout] bf16 NHWC')
+        for t in (bmean, binv, bw, bb) + sums:
             if t.dtype != torch.float32 or t.numel() != Cout or not t.is_contiguous():
                 raise ValueError('conv_wgrad(bn_dy=): fp32 [Cout] BN statistics / parameters / sums')
         _count('conv_wgrad_bn_dy')
-        bnt = (by.data_ptr(), bmean.data_ptr(), binv.data_ptr(), bw.data_ptr(), bb.data_ptr(), bdw.data_ptr(),
-               bdb.data_ptr(), float(bslope))
+        if isinstance(bn_dy, BnBwdFold):
+            _count('conv_wgrad_bn_dy_fold')
+            bnt = (by.data_ptr(), bmean.data_ptr(), binv.data_ptr(), bw.data_ptr(), bb.data_ptr(), 0, 0,
+                   float(bslope), bn_dy.acc.bwd.data_ptr(), bn_dy.acc.R, bn_dy.dw.data_ptr(), bn_dy.db.data_ptr(),
+                   gxo.data_ptr() if gxo is not None else 0)
+            bn_done = bn_dy.done
+        else:
+            bnt = (by.data_ptr(), bmean.data_ptr(), binv.data_ptr(), bw.data_ptr(), bb.data_ptr(), bdw.data_ptr(),
+                   bdb.data_ptr(), float(bslope))
     res = ext.conv_wgrad(x.data_ptr(), dy.data_ptr(), partial.data_ptr(), N, H, W, Cin, Ho, Wo, Cout, slices, px,
                          out.data_ptr(), out.stride(0), out.stride(1), out.stride(2), out.stride(3), _stream(x.device),
                          cin_out, defer, side, lut.data_ptr() if lut is not None else 0, fold, bnt)
     if fold is not None:
         _count('conv_wgrad_bn_fold')
         _grad_done(*fold_params)
+    if bn_done:
+        _grad_done(*bn_done)
     if chain is not None:
         if side is not None:
             _count('conv_wgrad_side_reduce')
@@ -1297,7 +1364,7 @@ def conv_wgrad(x, dy, out, target_blocks=None, chain=None, last=True, lut=None, 
     return out
 
 
-def conv_fwd(x, w16, stats=None, acc_r=0, lut=None):
+def conv_fwd(x, w16, stats=None, acc_r=0, lut=None, act=None, act_out=None):
     """y = conv2d(x, w16, stride 2, pad 1) on the gfx950 MFMA kernel: ``x``
     [N, Cin, H, W] bf16 channels-last, ``w16`` [Cout, Cin, 4, 4] bf16
     channels-last; returns channels-last bf16 y.  ``stats`` (optional fp32
@@ -1308,10 +1375,16 @@ def conv_fwd(x, w16, stats=None, acc_r=0, lut=None):
     ``fwd`` tensor with ``acc_r`` replicas, added into with atomics.
     ``lut`` (first layer): ``x`` is the raw u8 RGBA frames ([N, 4, H, W],
     channels-last) and ``lut`` their bf16 decode table (:func:`decode_lut_bf16`):
-    the decode happens in the convolution's tile loads."""
+    the decode happens in the convolution's tile loads.  ``act``: the
+    :class:`BnActLazy` of the BatchNorm+LeakyReLU whose INPUT ``x`` is -- the
+    convolution applies it to its operand tiles; ``act_out`` (same shape as
+    ``x``, optional) receives that activation."""
     import torch
     ext = hip_ext()
     N, Cin, H, W = x.shape
+    if act_out is not None and (act is None or act_out.shape != x.shape or act_out.dtype != torch.bfloat16
+                                or not act_out.is_contiguous(memory_format=torch.channels_last)):
+        raise ValueError('conv_fwd: act_out is the activation of act, shaped and laid out like x')
     Cout = w16.shape[0]
     cl = torch.channels_last
     # first layer fed RGBA: a 3-input-channel weight, the 4th input channel ignored
@@ -1328,9 +1401,12 @@ def conv_fwd(x, w16, stats=None, acc_r=0, lut=None):
     _count('conv_fwd')
     if acc_r and (stats is None or stats.dtype != torch.float64 or stats.numel() < 2 * Cout * acc_r):
         raise ValueError('conv_fwd: acc_r needs an fp64 accumulator of 2 * Cout * acc_r elements')
+    if act is not None:
+        _count('conv_fwd_act')
     ext.conv_fwd(x.data_ptr(), w16.data_ptr(), y.data_ptr(), stats.data_ptr() if stats is not None else 0,
                  N, H, W, Cin, Ho, Wo, Cout, _stream(x.device), wc if Cin == 4 else 0, int(acc_r),
-                 lut.data_ptr() if lut is not None else 0)
+                 lut.data_ptr() if lut is not None else 0, act.take() if act is not None else None,
+                 act_out.data_ptr() if act_out is not None else 0)
     return y
 
 
@@ -1443,15 +1519,29 @@ def _conv_function():
 
         @staticmethod
         def forward(ctx, x, w32, w16, with_stats=False, wt=None, bn_link=None, wchain=None, wlast=True, lut=None,
-                    bn_out=None):
+                    bn_out=None, act=None):
             ctx.set_materialize_grads(False)   # no zero-filled gradient for the stats output
+            if act is not None:
+                # x is the input of the BN that produced this layer's input (BnActLazy): the
+                # kernel applies it and writes the activation, which the weight gradient reads
+                if not (isinstance(with_stats, BnAccumulator) and lut is None):
+                    raise ValueError('conv4x4s2(act=): accumulator statistics on bf16 input only')
+                xa = torch.empty_like(x, memory_format=torch.channels_last)
+                ctx.save_for_backward(xa, w16)
+                ctx.w32, ctx.wt, ctx.bn_link = w32, wt, bn_link
+                ctx.wchain, ctx.wlast, ctx.lut, ctx.bn_out = wchain, wlast, None, None
+                if bn_out is not None and w32.requires_grad:
+                    bn_out.armed = True
+                    ctx.bn_out = bn_out
+                return conv_fwd(x, w16, with_stats.fwd, with_stats.R, act=act, act_out=xa)
             ctx.save_for_backward(x, w16)
             ctx.w32, ctx.wt, ctx.bn_link = w32, wt, bn_link
             ctx.wchain, ctx.wlast, ctx.lut = wchain, wlast, lut
             # the BN that consumes the output may hand its backward to this layer's
-            # weight gradient (BnDeferred): only without a data gradient (frames in)
+            # weight gradient (BnDeferred): with the sums already folded only without a
+            # data gradient (frames in), else folded by the kernel (BnBwdFold)
             ctx.bn_out = None
-            if bn_out is not None and lut is not None:
+            if bn_out is not None and w32.requires_grad:
                 bn_out.armed = True
                 ctx.bn_out = bn_out
             if lut is not None:   # raw u8 frames: the decode runs in the MFMA kernels' loads
@@ -1483,45 +1573,60 @@ def _conv_function():
             if gy is None:
                 if ctx.wchain is not None and ctx.wlast:
                     ctx.wchain.flush(x.device)
-                return None, None, None, None, None, None, None, None, None, None
-            if bn_dy is not None and ctx.needs_input_grad[0]:
-                raise RuntimeError('conv4x4s2: a deferred BN backward needs a layer without a data gradient')
+                return None, None, None, None, None, None, None, None, None, None, None
+            fold_bn = isinstance(bn_dy, BnBwdFold)
+            if bn_dy is not None and ctx.needs_input_grad[0] and not fold_bn:
+                raise RuntimeError('conv4x4s2: a deferred BN backward with folded sums needs a layer without a '
+                                   'data gradient')
             gy = gy.contiguous(memory_format=torch.channels_last)
             gx = gw = None
+            gy_dgrad = gy
+            if fold_bn and ctx.needs_input_grad[0]:
+                # the weight gradient runs first: it applies the BN backward to gy and writes
+                # the BN's input gradient, this layer's true output gradient, for the data gradient
+                bn_dy.gx_out = gy_dgrad = torch.empty_like(gy, memory_format=torch.channels_last)
+                gw = _Conv4x4s2._wgrad(ctx, x, gy, None, None, bn_dy)
+                bn_dy = None
             if ctx.needs_input_grad[0]:
                 if conv_dgrad_supported(x, w16):
-                    gx = conv_dgrad(gy, w16, tuple(x.shape), ctx.wt, ctx.bn_link)
+                    gx = conv_dgrad(gy_dgrad, w16, tuple(x.shape), ctx.wt, ctx.bn_link)
                 else:
                     wfull = w16
                     if w16.shape[1] != x.shape[1]:   # RGBA-fed RGB weight: zero weight on the extra channel
                         wfull = torch.cat([w16, w16.new_zeros(w16.shape[0], x.shape[1] - w16.shape[1], 4, 4)], 1)
                         wfull = wfull.contiguous(memory_format=torch.channels_last)
-                    gx = torch.ops.aten.convolution_backward(gy, x, wfull, None, [2, 2], [1, 1], [1, 1], False,
-                                                             [0, 0], 1, [True, False, False])[0]
-            fold = None
-            bl = ctx.bn_link
-            if gx is not None and bl is not None and bl.acc is not None and bl.part is not None and bl.rows < 0 \
-                    and bl.params is not None and ctx.needs_input_grad[1] and x.shape[1] != 4:
-                # the data gradient just filled the BN's backward accumulator: the
-                # weight-gradient launch folds it in one extra block
-                fold = bl.fold_args(x.shape[0] * x.shape[2] * x.shape[3])
-            if ctx.needs_input_grad[1]:
-                out, sunk = _grad_dest(ctx.w32)
-                # a chained (deferred) reduce only into a bucket view: a returned
-                # gradient must be complete when autograd accumulates it
-                chain = ctx.wchain if (sunk or ctx.wlast) else None
-                if ctx.wchain is not None and chain is None:
+                    gx = torch.ops.aten.convolution_backward(gy_dgrad, x, wfull, None, [2, 2], [1, 1], [1, 1],
+                                                             False, [0, 0], 1, [True, False, False])[0]
+            if gy_dgrad is gy:   # (not already run before the data gradient)
+                fold = None
+                bl = ctx.bn_link
+                if gx is not None and bl is not None and bl.acc is not None and bl.part is not None and bl.rows < 0 \
+                        and bl.params is not None and ctx.needs_input_grad[1] and x.shape[1] != 4 \
+                        and not bl.defer_fold:
+                    # the data gradient just filled the BN's backward accumulator: the
+                    # weight-gradient launch folds it in one extra block
+                    fold = bl.fold_args(x.shape[0] * x.shape[2] * x.shape[3])
+                gw = _Conv4x4s2._wgrad(ctx, x, gy, fold, bl, bn_dy)
+            return gx, gw, None, None, None, None, None, None, None, None, None
+
+        @staticmethod
+        def _wgrad(ctx, x, gy, fold, bl, bn_dy):
+            if not ctx.needs_input_grad[1]:
+                if ctx.wchain is not None:
                     ctx.wchain.flush(x.device)
-                fold_params = ()
-                if fold is not None:
-                    fold_params = tuple(p for p, sk in zip(bl.params, (bl.dw_sunk, bl.db_sunk)) if sk)
-                gw = conv_wgrad(x, gy, out, chain=chain, last=ctx.wlast or chain is None, lut=ctx.lut, fold=fold,
-                                bn_dy=bn_dy, param=ctx.w32 if sunk else None, fold_params=fold_params)
-                if sunk:
-                    gw = None      # written into the parameter's bucket view
-            elif ctx.wchain is not None:
+                return None
+            out, sunk = _grad_dest(ctx.w32)
+            # a chained (deferred) reduce only into a bucket view: a returned
+            # gradient must be complete when autograd accumulates it
+            chain = ctx.wchain if (sunk or ctx.wlast) else None
+            if ctx.wchain is not None and chain is None:
                 ctx.wchain.flush(x.device)
-            return gx, gw, None, None, None, None, None, None, None, None
+            fold_params = ()
+            if fold is not None:
+                fold_params = tuple(p for p, sk in zip(bl.params, (bl.dw_sunk, bl.db_sunk)) if sk)
+            gw = conv_wgrad(x, gy, out, chain=chain, last=ctx.wlast or chain is None, lut=ctx.lut, fold=fold,
+                            bn_dy=bn_dy, param=ctx.w32 if sunk else None, fold_params=fold_params)
+            return None if sunk else gw   # (sunk: written into the parameter's bucket view)
 
     return _Conv4x4s2
 
@@ -1530,7 +1635,7 @@ _CONV_FN = None
 
 
 def conv4x4s2(x, w32, w16, with_stats=False, wt=None, bn_link=None, wchain=None, wlast=True, lut=None,
-              bn_out=None):
+              bn_out=None, act=None):
     """4x4 / stride-2 / pad-1 convolution of bf16 channels-last ``x`` with the
     bf16 copy ``w16`` of fp32 weight ``w32``; the gradient goes to ``w32``
     (fp32, from the MFMA weight-gradient kernel).  See :func:`conv_wgrad_supported`.
@@ -1545,13 +1650,16 @@ def conv4x4s2(x, w32, w16, with_stats=False, wt=None, bn_link=None, wchain=None,
     table inside the kernels (:func:`decode_lut_bf16`; no gradient for ``x``).
     ``bn_out`` (with ``lut``): a :class:`BnDeferred` shared with the
     BatchNorm+LeakyReLU that consumes the output -- its backward apply then
-    runs inside this layer's weight-gradient kernel."""
+    runs inside this layer's weight-gradient kernel.  ``act``: the
+    :class:`BnActLazy` of the BatchNorm+LeakyReLU whose input ``x`` is (it
+    skipped its apply): the forward kernel applies it while staging its
+    operand tiles and writes the activation for the weight gradient."""
     global _CONV_FN
     if _CONV_FN is None:
         _CONV_FN = _conv_function()
     if with_stats and not conv_fwd_supported(x, w16):
         raise ValueError('conv4x4s2(with_stats=True) needs the MFMA forward (see conv_fwd_supported)')
-    return _CONV_FN.apply(x, w32, w16.detach(), with_stats, wt, bn_link, wchain, wlast, lut, bn_out)
+    return _CONV_FN.apply(x, w32, w16.detach(), with_stats, wt, bn_link, wchain, wlast, lut, bn_out, act)
 
 
 # ---------------------------------------------------------------------------

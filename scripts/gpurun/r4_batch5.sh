@@ -14,3 +14,9 @@ for v in "X=0" "X=1"; do
 done
 bash scripts/gpurun/disc_trace.sh r4f > /dev/null || exit 1
 grep -A30 'per kernel, summed' gpurun_out/trace_r4f/step_sequence.txt
+# per-kernel effect of the staging depth and the weight-gradient block count
+for v in BT_CONV_STAGING=3 BT_CONV_STAGING=4 BT_WGRAD_BLOCKS=1024 BT_WGRAD_BLOCKS=2048; do
+  tag=r4f_${v/=/_}
+  env $v bash scripts/gpurun/disc_trace.sh $tag > /dev/null || exit 1
+  echo "== $v"; grep -A24 'mean over' gpurun_out/trace_$tag/step_sequence.txt
+done

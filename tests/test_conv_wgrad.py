@@ -488,3 +488,125 @@ def test_first_layer_patch_forward(dev, u8, cout, wc, tiles, rows):
     torch.testing.assert_close(outs[0][1][0], yf.sum(0), rtol=1e-6, atol=1e-3)
     torch.testing.assert_close(outs[0][1][1], (yf * yf).sum(0), rtol=1e-6, atol=1e-3)
     torch.testing.assert_close(outs[0][1][1], (yf * yf).sum(0), rtol=1e-6, atol=1e-3)
+
+
+def _fill_acc(acc, x):
+    """A BnAccumulator's forward replicas as a producer leaves them: replica 0
+    holds the fp64 channel sums and sums of squares of x, the rest zero."""
+    C = x.shape[1]
+    xf = x.permute(0, 2, 3, 1).reshape(-1, C).double()
+    acc.fwd.zero_()
+    v = acc.fwd[:acc.R * 2 * C].view(acc.R, 2, C)
+    v[0, 0] = xf.sum(0)
+    v[0, 1] = (xf * xf).sum(0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('cin,cout,hw', [(32, 64, (48, 64)), (64, 128, (32, 40)), (128, 256, (16, 24))])
+def test_forward_applies_input_bn(dev, cin, cout, hw):
+    """A convolution that applies the BatchNorm+LeakyReLU producing its input
+    in its own operand staging (ops.BnActLazy: the BN call skips its apply)
+    against the apply pass + plain convolution: bit-identical output, output
+    statistics, activation side output (act_out: every input element, from
+    the centre taps), BN mean / invstd and running statistics; the
+    accumulator cleared for the next producer either way.  cin 128: a
+    thread's chunk alternates between two channel sets."""
+    cl = torch.channels_last
+    g = torch.Generator(device=dev).manual_seed(cin)
+    H, W = hw
+    x = (torch.randn(2, cin, H, W, device=dev, generator=g) * 0.7 + 0.2).to(torch.bfloat16).contiguous(memory_format=cl)
+    w16 = (0.05 * torch.randn(cout, cin, 4, 4, device=dev, generator=g)).to(torch.bfloat16).contiguous(memory_format=cl)
+    bns = []
+    for _ in range(2):
+        bn = ops.BatchNormLeakyReLU2d(cin).to(dev)
+        with torch.no_grad():
+            bn.weight.copy_(1 + 0.1 * torch.randn(cin, device=dev, generator=torch.Generator(device=dev).manual_seed(1)))
+            bn.bias.copy_(0.1 * torch.randn(cin, device=dev, generator=torch.Generator(device=dev).manual_seed(2)))
+        bns.append(bn)
+    # reference: apply pass, then the convolution
+    acc_in, acc_out = ops.BnAccumulator(cin, dev), ops.BnAccumulator(cout, dev)
+    _fill_acc(acc_in, x)
+    with torch.no_grad():
+        a = bns[0].forward_from_stats(x, acc_in)
+        y_ref = ops.conv_fwd(a.contiguous(memory_format=cl), w16, acc_out.fwd, acc_out.R)
+    s_ref = acc_out.fwd.clone()
+    assert float(acc_in.fwd.abs().sum()) == 0.0
+    # the convolution applies the BN
+    acc_in2, acc_out2 = ops.BnAccumulator(cin, dev), ops.BnAccumulator(cout, dev)
+    _fill_acc(acc_in2, x)
+    lazy = ops.BnActLazy()
+    before = ops.KERNEL_CALLS.get('conv_fwd_act', 0)
+    with torch.no_grad():
+        xo = bns[1].forward_from_stats(x, acc_in2, lazy=lazy)
+        assert xo.data_ptr() == x.data_ptr()   # the BN's input, no apply launch
+        xa = torch.empty_like(x, memory_format=cl)
+        y = ops.conv_fwd(xo, w16, acc_out2.fwd, acc_out2.R, act=lazy, act_out=xa)
+    torch.cuda.synchronize()
+    assert ops.KERNEL_CALLS['conv_fwd_act'] == before + 1
+    assert float(acc_in2.fwd.abs().sum()) == 0.0          # cleared by the last block
+    assert torch.equal(xa, a)                               # the activation, every element
+    assert torch.equal(y, y_ref)
+    torch.testing.assert_close(acc_out2.fwd, s_ref, rtol=1e-9, atol=1e-6)
+    for ba, bb in zip(bns[0].buffers(), bns[1].buffers()):
+        assert torch.equal(ba, bb)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('cin,cout,hw', [(32, 64, (64, 80)), (128, 256, (32, 40)), (4, 32, (96, 128))])
+def test_wgrad_applies_bn_backward_folded(dev, cin, cout, hw):
+    """The weight gradient that applies the following BatchNorm+LeakyReLU's
+    backward to its staged dY (ops.BnBwdFold): it folds the BN's backward
+    accumulator itself (dw / db equal to the fp64 sums rounded once), its gx
+    side output is bit-identical to the apply kernel's (bn_bwd_apply: the same
+    BnBwdCoef arithmetic), the weight gradient equals the one computed from
+    that gx, and the accumulator is left cleared.  cin 4: the first layer's
+    wave-private kernel (no data gradient, no gx output)."""
+    cl = torch.channels_last
+    g = torch.Generator(device=dev).manual_seed(cin + cout)
+    H, W = hw
+    N, Ho, Wo = 2, H // 2, W // 2
+    x = torch.randn(N, cin, H, W, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    y = (torch.randn(N, Ho, Wo, cout, device=dev, generator=g) * 0.8 + 0.1).to(torch.bfloat16)   # BN input, NHWC
+    gy = (torch.randn(N, cout, Ho, Wo, device=dev, generator=g) * 1e-2).to(torch.bfloat16).contiguous(memory_format=cl)
+    yf = y.float().reshape(-1, cout)
+    mean = yf.mean(0)
+    invstd = torch.rsqrt(yf.var(0, unbiased=False) + 1e-5)
+    w = 1 + 0.1 * torch.randn(cout, device=dev, generator=g)
+    b = 0.1 * torch.randn(cout, device=dev, generator=g)
+    slope = 0.2
+    acc = ops.BnAccumulator(cout, dev)
+    # the backward sums as the consumer leaves them (any values do: both paths read them)
+    xh = (yf - mean) * invstd
+    gz = torch.where(xh * w + b > 0, 1.0, slope) * gy.permute(0, 2, 3, 1).reshape(-1, cout).float()
+    acc.bwd.zero_()
+    v = acc.bwd[:acc.R * 2 * cout].view(acc.R, 2, cout)
+    v[0, 0] = gz.double().sum(0)
+    v[0, 1] = (gz.double() * xh.double()).sum(0)
+    db_ref = v[0, 0].float().clone()
+    dw_ref = v[0, 1].float().clone()
+    # reference: the apply kernel, then the weight gradient of its output
+    gx_ref = torch.empty_like(y)
+    ops.hip_ext().bn_bwd_apply(y.data_ptr(), gy.data_ptr(), gx_ref.data_ptr(), N * Ho * Wo, cout,
+                               ops.OUT_DTYPES['bfloat16'], mean.data_ptr(), invstd.data_ptr(), w.data_ptr(),
+                               b.data_ptr(), dw_ref.data_ptr(), db_ref.data_ptr(), slope,
+                               ops._stream(dev))
+    gx_ref = gx_ref.permute(0, 3, 1, 2)
+    wout = 3 if cin == 4 else cin
+    out_ref = torch.zeros(cout, wout, 4, 4, device=dev)
+    xin = x if cin != 4 else x
+    ops.conv_wgrad(xin, gx_ref.contiguous(memory_format=cl), out_ref)
+    # the weight gradient folds and applies
+    dw, db = torch.empty(cout, device=dev), torch.empty(cout, device=dev)
+    pend = ops.BnBwdFold(y, mean, invstd, w, b, slope, acc, dw, db, ())
+    if cin != 4:
+        pend.gx_out = torch.empty_like(gy, memory_format=cl)
+    out = torch.zeros(cout, wout, 4, 4, device=dev)
+    before = ops.KERNEL_CALLS.get('conv_wgrad_bn_dy_fold', 0)
+    ops.conv_wgrad(xin, gy, out, bn_dy=pend)
+    torch.cuda.synchronize()
+    assert ops.KERNEL_CALLS['conv_wgrad_bn_dy_fold'] == before + 1
+    assert torch.equal(dw, dw_ref) and torch.equal(db, db_ref)
+    assert float(acc.bwd.abs().sum()) == 0.0
+    if cin != 4:
+        assert torch.equal(pend.gx_out, gx_ref)
+    torch.testing.assert_close(out, out_ref, rtol=1e-5, atol=1e-5 * float(out_ref.abs().max()))
