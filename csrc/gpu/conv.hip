@@ -271,8 +271,12 @@ struct XCursor {
   }
 };
 
-template <bool BND>   // BND: the BN backward applied to dY (ConvWgradParams::bn_dy) -- its coefficients and
-                     // ring cost ~80 VGPRs, so the plain variant stays lean
+// BND: the BN backward applied to dY (ConvWgradParams::bn_dy) -- its
+// coefficients and ring cost ~80 VGPRs, so the plain variant stays lean.
+// PIPE: the next step's fragments are read right after the barrier that
+// publishes them, while this step's MFMAs run (two fragment sets, +24 VGPRs):
+// without it every step waited out barrier -> LDS read latency -> MFMAs in turn.
+template <bool BND, bool PIPE = false>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   if (run_side(p, smem)) return;
@@ -406,26 +410,63 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p)
 #pragma unroll
   for (int u = 0; u < kDepth; ++u) load(ring[u]);
   const int padded = (nsteps + kDepth - 1) / kDepth * kDepth;
-  for (int s0 = 0; s0 < padded; s0 += kDepth) {
+  auto frags = [&](int buf, bf16x8 (&a)[2], bf16x8 (&bm)[4]) {
+    const char* base = smem + buf * STAGE;
 #pragma unroll
-    for (int u = 0; u < kDepth; ++u) {
-      const int buf = u & 1;   // kDepth is even: (s0 + u) & 1
-      store(ring[u], buf);     // waits for this stage's loads only (counted vmcnt)
-      // LDS-only barrier: the ring's later stages stay in flight across it
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      load(ring[u]);           // stage s + kDepth
-      const char* base = smem + buf * STAGE;
-      bf16x8 a[2], bm[4];
+    for (int i = 0; i < 2; ++i) a[i] = frag_at(base, ra[i], 4 * DY_ROW);
 #pragma unroll
-      for (int i = 0; i < 2; ++i) a[i] = frag_at(base, ra[i], 4 * DY_ROW);
+    for (int j = 0; j < 4; ++j) bm[j] = frag_at(base + DY_TILE, rb[j], 4 * X_ROW);
+  };
+  auto mma = [&](const bf16x8 (&a)[2], const bf16x8 (&bm)[4]) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bm[j] = frag_at(base + DY_TILE, rb[j], 4 * X_ROW);
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bm[j], acc[i][j], 0, 0, 0);
+  };
+  if constexpr (PIPE) {
+    // ring slot k holds step s0 + k; iteration (s0, u) stores step s0 + u + 1,
+    // refills its slot with step s0 + u + 1 + kDepth, reads its fragments and
+    // runs step s0 + u's MFMAs (fragments read one iteration earlier).  The
+    // lgkmcnt(0) before each barrier also retires every wave's fragment reads
+    // of the buffer the next store overwrites.  Past the slice the steps are
+    // zeros (and the final extra store / load is never multiplied in).
+    bf16x8 ac[2], bc4[4], an[2], bn[4];
+    store(ring[0], 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    load(ring[0]);   // step kDepth
+    frags(0, ac, bc4);
+    for (int s0 = 0; s0 < padded; s0 += kDepth) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bm[j], acc[i][j], 0, 0, 0);
+      for (int u = 0; u < kDepth; ++u) {
+        Stage& nx = ring[(u + 1) % kDepth];
+        store(nx, (u + 1) & 1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        load(nx);
+        frags((u + 1) & 1, an, bn);
+        mma(ac, bc4);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) ac[i] = an[i];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bc4[j] = bn[j];
+      }
+    }
+  } else {
+    for (int s0 = 0; s0 < padded; s0 += kDepth) {
+#pragma unroll
+      for (int u = 0; u < kDepth; ++u) {
+        const int buf = u & 1;   // kDepth is even: (s0 + u) & 1
+        store(ring[u], buf);     // waits for this stage's loads only (counted vmcnt)
+        // LDS-only barrier: the ring's later stages stay in flight across it
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        load(ring[u]);           // stage s + kDepth
+        bf16x8 a[2], bm[4];
+        frags(buf, a, bm);
+        mma(a, bm);
+      }
     }
   }
 
@@ -979,6 +1020,11 @@ __device__ __forceinline__ int f_off(int r, int chunk) { return r * F_ROW + ((ch
 __device__ __forceinline__ int c1_row_chan(int f, int rho) {
   return 32 * (f >> 1) + 8 * (rho >> 2) + 4 * (f & 1) + (rho & 3);
 }
+// The swizzle key of such a channel tile's LDS rows: the 16 rows one fragment
+// read touches (c1_row_chan(f, 0..15): bits 0-1 and 3-4 vary) must land on
+// 16 different 16-byte bank slots; with the pixel tiles' key (r & 7) they
+// shared 4 and the reads ran 4-way conflicted (PMC: 60-124 % conflict cycles)
+__device__ __forceinline__ int bkey(int r) { return ((r >> 1) & 1) | (((r >> 3) & 3) << 1); }
 
 struct TapGemm {
   const uint16_t* src = nullptr;
@@ -1268,12 +1314,14 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     for (int j = 0; j < RB; ++j) rbv[j] = *reinterpret_cast<const uint4*>(wrow + j * (32 * 16) * p.C + woff);
   };
   const int st_a = f_off(ar, ac);   // rows ar + 32j keep the swizzle phase: (ar + 32j) & 7 == ar & 7
+  // the B (channel) tile: DIRECT reads its rows in c1_row_chan order -> bkey swizzle (also ar + 32j invariant)
+  const int st_b = DIRECT ? ar * F_ROW + ((ac ^ bkey(ar)) << 4) : st_a;
   auto store = [&](int buf) {
     char* ai = smem + buf * STG;
 #pragma unroll
     for (int j = 0; j < RJ; ++j) *reinterpret_cast<uint4*>(ai + st_a + j * 32 * F_ROW) = ra[j];
 #pragma unroll
-    for (int j = 0; j < RB; ++j) *reinterpret_cast<uint4*>(ai + A_TILE + st_a + j * 32 * F_ROW) = rbv[j];
+    for (int j = 0; j < RB; ++j) *reinterpret_cast<uint4*>(ai + A_TILE + st_b + j * 32 * F_ROW) = rbv[j];
   };
   // LDS-DMA staging: one wave-instruction writes 1 KiB of LDS linearly (lane l
   // at 16 l), i.e. rows 8 w + 32 j .. + 7 of the tile, lane l on row 8 w +
@@ -1283,21 +1331,23 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   // (zeros).  All LDS in one array (a second __shared__ object makes hipcc
   // drain vmcnt before the fragment reads).
   const int acs = ac ^ (ar & 7);
+  const int acs_b = DIRECT ? ac ^ bkey(ar) : acs;   // the B tile's logical chunk (its own swizzle)
   const int wv = __builtin_amdgcn_readfirstlane(wave);
   const uint32_t wrow_b = uint32_t((n0 + ar) * 16 * p.C) * 2u;   // byte offset of B row ar
   auto issue = [&](int ks, int buf) {
     const int kc = ks * FBK + acs * 8;
     const int tap = kc >> p.cshift, ch = kc & (p.C - 1);
-    int dr, dc, wtap;
+    int dr, dc;
     if (DGRAD) {
       dr = ph - (tap >> 1);
       dc = pw - (tap & 1);
-      wtap = (1 - ph + 2 * (tap >> 1)) * 4 + (1 - pw + 2 * (tap & 1));
     } else {
       dr = tap >> 2;
       dc = tap & 3;
-      wtap = tap;
     }
+    const int kcb = ks * FBK + acs_b * 8;
+    const int tapb = kcb >> p.cshift, chb = kcb & (p.C - 1);
+    const int wtap = DGRAD ? (1 - ph + 2 * (tapb >> 1)) * 4 + (1 - pw + 2 * (tapb & 1)) : tapb;
     const uint32_t soff = uint32_t((((dr * p.SW + dc) << p.cshift) + ch) * 2);
     const uint32_t tbit = 1u << tap;
     char* st = smem + buf * STG + wv * 1024;
@@ -1305,7 +1355,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     for (int j = 0; j < RJ; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_src, (__attribute__((address_space(3))) void*)(st + j * 4096), 16,
                                                int((vmask[j] & tbit) ? abase[j] + soff : kOOB), 0, 0, 0);
-    const uint32_t woff = wrow_b + uint32_t(wtap * p.C + ch) * 2u;
+    const uint32_t woff = wrow_b + uint32_t(wtap * p.C + chb) * 2u;
 #pragma unroll
     for (int j = 0; j < RB; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w, (__attribute__((address_space(3))) void*)(st + A_TILE + j * 4096),
@@ -1327,8 +1377,10 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
 #pragma unroll
     for (int i = 0; i < FM; ++i) fa[i][kk] = f_off(row0 + 16 * i + (lane & 15), chunk);
 #pragma unroll
-    for (int j = 0; j < FN; ++j)
-      fb[j][kk] = A_TILE + f_off(col0 + (DIRECT ? c1_row_chan(j, lane & 15) : 16 * j + (lane & 15)), chunk);
+    for (int j = 0; j < FN; ++j) {
+      const int r = col0 + (DIRECT ? c1_row_chan(j, lane & 15) : 16 * j + (lane & 15));
+      fb[j][kk] = A_TILE + (DIRECT ? r * F_ROW + ((chunk ^ bkey(r)) << 4) : f_off(r, chunk));
+    }
   }
   auto mma = [&](int buf) {
     const char* ai = smem + buf * STG;
@@ -1974,6 +2026,158 @@ __global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tile
   }
 }
 
+// ---------------------------------------------------------------------------
+// The data gradient of the 32-channel layer (conv 32 -> 64: dY 64 channels,
+// dx 32) from a dY PATCH.  As a tap GEMM (tap_gemm_kernel<true, 32, ..., 4>)
+// every class pixel re-stages its 4 taps x 64 channels through LDS-DMA each
+// k-step: 16 x the dY tensor of LDS traffic, 5 DMA pieces per wave per 8
+// MFMAs, 16 latency-bound k-steps per block (47 us, 13.9 VALU per MFMA).
+// Here a block loads the (4 + 2) x (32 + 2) dY pixels under a 4 x 32 tile of
+// the class grid ONCE into LDS (26 KB, 16-byte chunks XOR-swizzled by pixel so
+// a 16-lane fragment read of 16 consecutive pixels hits 16 bank slots) and
+// runs all four parity classes' 8 K=32 steps straight from it: the weights
+// (the class's [ci][tap][co] rows) are the MFMA's A operand, loaded into
+// registers per class, and the patch pixels its B operand -- so a lane's
+// accumulators hold 8 consecutive dx channels of one pixel (c1_row_chan) and
+// the epilogue stores 16 bytes and sums the BN-backward terms from registers.
+constexpr int DP_TA = 4, DP_TB = 32;                  // class-grid rows x columns per block
+constexpr int DP_PR = DP_TA + 2, DP_PC = DP_TB + 2;   // the dY patch: one pixel of halo each side
+constexpr int DP_C = 64, DP_NOUT = 32;                 // dY channels, dx channels
+constexpr int DP_NP = DP_PR * DP_PC;                   // 204 patch pixels, 128 bytes each
+__device__ __forceinline__ int dp_off(int px, int q) { return px * (DP_C * 2) + ((q ^ ((px >> 1) & 7)) << 4); }
+
+__global__ __launch_bounds__(kThreads) void dgrad_patch_kernel(TapGemm p) {
+  constexpr int NCH = DP_NP * 8, NL = (NCH + kThreads - 1) / kThreads;
+  __shared__ __attribute__((aligned(16))) char smem[DP_NP * DP_C * 2 + 4 * 2 * DP_NOUT * 4];
+  float* red = reinterpret_cast<float*>(smem + DP_NP * DP_C * 2);
+  const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6, g = lane >> 4;
+  const int tb = (p.GW + DP_TB - 1) / DP_TB, ta = (p.GH + DP_TA - 1) / DP_TA;
+  const int blk = int(blockIdx.x);
+  const int n = blk / (ta * tb), rem = blk - n * (ta * tb);
+  const int a0 = (rem / tb) * DP_TA, b0 = (rem % tb) * DP_TB;
+  // the patch: chunk u = t + 256 i is chunk u & 7 of patch pixel u >> 3
+  {
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.src, int64_t(p.N) * p.SH * p.SW * DP_C * 2);
+    uint4 v[NL];
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int u = t + kThreads * i, pix = u >> 3, q = u & 7;
+      const int pr = pix / DP_PC, pc = pix - pr * DP_PC;
+      const int ya = a0 - 1 + pr, yb = b0 - 1 + pc;
+      const bool ok = u < NCH && unsigned(ya) < unsigned(p.SH) && unsigned(yb) < unsigned(p.SW);
+      v[i] = bload(rs, ok ? uint32_t(((n * p.SH + ya) * p.SW + yb) * (DP_C * 2) + q * 16) : kOOB);
+    }
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int u = t + kThreads * i;
+      if ((i + 1) * kThreads <= NCH || u < NCH) *reinterpret_cast<uint4*>(smem + dp_off(u >> 3, u & 7)) = v[i];
+    }
+  }
+  // this wave: class-grid row a0 + wave, columns b0 + 16 j + (lane & 15), j = 0, 1
+  const int ra = a0 + wave;
+  const bool bnf = p.bn.part != nullptr;
+  float is[8], nm[8], ww[8], bb[8], bs[8], bq[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    bs[e] = bq[e] = 0.f;
+    if (bnf) {
+      const int c = 8 * g + e;
+      is[e] = p.bn.invstd[c];
+      nm[e] = -p.bn.mean[c] * is[e];
+      ww[e] = p.bn.w[c];
+      bb[e] = p.bn.b[c];
+    }
+  }
+  __syncthreads();
+  for (int cls = 0; cls < 4; ++cls) {
+    const int ph = cls >> 1, pw = cls & 1;
+    // A: the class's weight rows, ci = c1_row_chan(f, lane & 15); K step s = tap s / 2,
+    // dY channels 32 (s & 1) + 8 (lane >> 4) .. + 7 -> wt[ci][kh][kw][co]
+    bf16x8 wa[2][8];
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const int ci = c1_row_chan(f, lane & 15), tap = s >> 1;
+        const int kh = 1 - ph + 2 * (tap >> 1), kw = 1 - pw + 2 * (tap & 1);
+        const int co = 32 * (s & 1) + 8 * g;
+        wa[f][s] = *reinterpret_cast<const bf16x8*>(p.w + (ci * 16 + kh * 4 + kw) * DP_C + co);
+      }
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int tap = s >> 1, dr = ph - (tap >> 1), dc = pw - (tap & 1);
+      const int q = 4 * (s & 1) + g;
+      bf16x8 bm[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int px = (wave + dr + 1) * DP_PC + 16 * j + (lane & 15) + dc + 1;
+        bm[j] = *reinterpret_cast<const bf16x8*>(smem + dp_off(px, q));
+      }
+#pragma unroll
+      for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[f][s], bm[j], acc[f][j], 0, 0, 0);
+    }
+    // epilogue: dx pixel (2 a + ph, 2 b + pw), channels 8 g .. + 7
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int bcol = b0 + 16 * j + (lane & 15);
+      if (ra < p.GH && bcol < p.GW) {
+      const int off = ((n * p.OH + 2 * ra + ph) * p.OW + 2 * bcol + pw) * DP_NOUT + 8 * g;
+      uint4 xv = make_uint4(0, 0, 0, 0);
+      if (bnf) xv = *reinterpret_cast<const uint4*>(p.bn.x + off);
+      uint32_t pk[4];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {   // channels 8 g + 2 h, + 1: fragment h >> 1, rows 2 (h & 1), + 1
+        const f32x4& a = acc[h >> 1][j];
+        const f32x2 pr = {a[2 * (h & 1)], a[2 * (h & 1) + 1]};
+        pk[h] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2));
+      }
+      *reinterpret_cast<uint4*>(p.dst + off) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+      if (bnf) {
+        const uint32_t xw[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float gv = __uint_as_float(e & 1 ? pk[e >> 1] & 0xFFFF0000u : pk[e >> 1] << 16);
+          const float xh = fmaf(__uint_as_float(e & 1 ? xw[e >> 1] & 0xFFFF0000u : xw[e >> 1] << 16), is[e], nm[e]);
+          const float gz = fmaf(xh, ww[e], bb[e]) > 0.f ? gv : gv * p.bn.slope;
+          bs[e] += gz;
+          bq[e] += gz * xh;
+        }
+      }
+      }
+    }
+  }
+  if (!bnf) return;
+  // the 16 lanes of a group hold the same channels; then the 4 waves through LDS
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) bs[e] += __shfl_xor(bs[e], o), bq[e] += __shfl_xor(bq[e], o);
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(wave * 2 + 0) * DP_NOUT + 8 * g + e] = bs[e];
+      red[(wave * 2 + 1) * DP_NOUT + 8 * g + e] = bq[e];
+    }
+  }
+  __syncthreads();
+  if (t < 2 * DP_NOUT) {
+    const int which = t / DP_NOUT, c = t - which * DP_NOUT;
+    float v = 0.f;
+#pragma unroll
+    for (int w4 = 0; w4 < 4; ++w4) v += red[(w4 * 2 + which) * DP_NOUT + c];
+    unsafeAtomicAdd(reinterpret_cast<double*>(p.bn.part) + ((blk % p.bn.acc_r) * 2 + which) * DP_NOUT + c,
+                    double(v));
+  }
+}
+
 // several weights at once (blockIdx.y = tensor): the data gradients' operands for every layer in one launch
 __global__ __launch_bounds__(kThreads) void weight_t_multi_kernel(WeightTParams p) {
   const int k = int(blockIdx.y);
@@ -2001,6 +2205,22 @@ namespace {
 // weight-gradient staging: 0 = register ring (conv_wgrad_kernel, default), 2 /
 // 3 = LDS-DMA stages of 64 pixels (conv_wgrad_dma_kernel: 33 us against 24 us
 // per layer in the disc step, profiles/r4/disc_kernels.md); BT_WGRAD_STAGING
+int g_dgrad_patch = -1;   // the 32-channel data gradient from a dY patch (BT_DGRAD_PATCH, default on)
+int dgrad_patch() {
+  if (g_dgrad_patch < 0) {
+    const char* v = std::getenv("BT_DGRAD_PATCH");
+    g_dgrad_patch = v ? (std::atoi(v) ? 1 : 0) : 1;
+  }
+  return g_dgrad_patch;
+}
+int g_wgrad_pipe = -1;   // register-staged weight gradient: fragments read a step ahead (BT_WGRAD_PIPE)
+int wgrad_pipe() {
+  if (g_wgrad_pipe < 0) {
+    const char* v = std::getenv("BT_WGRAD_PIPE");
+    g_wgrad_pipe = v ? (std::atoi(v) ? 1 : 0) : 0;
+  }
+  return g_wgrad_pipe;
+}
 int g_wgrad_staging = -1;
 int wgrad_staging() {
   if (g_wgrad_staging < 0) {
@@ -2025,6 +2245,8 @@ bool c4_wave_private() {
 
 void conv_set_c4_wave_private(int on) { g_c4w = on < 0 ? -1 : (on ? 1 : 0); }
 
+void conv_set_dgrad_patch(int on) { g_dgrad_patch = on < 0 ? -1 : (on ? 1 : 0); }
+void conv_set_wgrad_pipe(int on) { g_wgrad_pipe = on < 0 ? -1 : (on ? 1 : 0); }
 void conv_set_wgrad_staging(int staging) { g_wgrad_staging = staging == 0 || staging == 2 || staging == 3 ? staging : -1; }
 
 bool conv_wgrad_supported(int Cin, int Cout) {
@@ -2094,11 +2316,13 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
   const bool bn_folds = p.bn_dy.acc != nullptr;
   if (c4 && (c4_wave_private() || bn_folds)) conv_wgrad_c4w_kernel<<<unsigned(grid), kThreads, 0, stream>>>(q);
   else if (c4) conv_wgrad_c4_kernel<<<unsigned(grid), kThreads, 0, stream>>>(q);
+  else if (bn_folds && wgrad_pipe()) conv_wgrad_kernel<true, true><<<unsigned(grid), kThreads, 0, stream>>>(q);
   else if (bn_folds) conv_wgrad_kernel<true><<<unsigned(grid), kThreads, 0, stream>>>(q);
   else if (wgrad_staging() == 2 && (p.Cin & (p.Cin - 1)) == 0 && p.Wo >= 32)
     conv_wgrad_dma_kernel<2><<<unsigned(grid), kThreads, 0, stream>>>(q);
   else if (wgrad_staging() == 3 && (p.Cin & (p.Cin - 1)) == 0 && p.Wo >= 32)
     conv_wgrad_dma_kernel<3><<<unsigned(grid), kThreads, 0, stream>>>(q);
+  else if (wgrad_pipe()) conv_wgrad_kernel<false, true><<<unsigned(grid), kThreads, 0, stream>>>(q);
   else conv_wgrad_kernel<false><<<unsigned(grid), kThreads, 0, stream>>>(q);
   const int64_t total = int64_t(p.Cout) * 16 * p.Cin;   // partial elements per slice
   ConvWgradParams::Reduce r;
@@ -2356,6 +2580,13 @@ hipError_t conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int 
         (bn->acc_r == 0 && bn->rows != conv_dgrad_bn_rows(N, H, W, Cin)) || (reinterpret_cast<uintptr_t>(bn->x) & 15))
       return hipErrorInvalidValue;
     g.bn = *bn;
+  }
+  // the 32-channel layer (dY 64 channels -> dx 32): from a dY patch, all four classes per block
+  // (BN-backward sums into an accumulator, or none)
+  if (Cout == DP_C && Cin == DP_NOUT && dgrad_patch() && (!g.bn.part || g.bn.acc_r > 0)) {
+    const int64_t blocks = int64_t(N) * ((Ho + DP_TA - 1) / DP_TA) * ((Wo + DP_TB - 1) / DP_TB);
+    dgrad_patch_kernel<<<unsigned(blocks), kThreads, 0, stream>>>(g);
+    return hipGetLastError();
   }
   g.cls_per_block = conv_dgrad_classes_per_block(g.M, g.NOUT);
   launch_tap_gemm<true>(g, 4, stream);

@@ -331,6 +331,8 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("dgrad_cls") = 0);
   m.def("conv_dgrad_classes_per_block", &conv_dgrad_classes_per_block);
   m.def("conv_set_wgrad_staging", &conv_set_wgrad_staging);
+  m.def("conv_set_wgrad_pipe", &conv_set_wgrad_pipe);
+  m.def("conv_set_dgrad_patch", &conv_set_dgrad_patch);
   m.def("conv_set_conv1_tiles", &conv_set_conv1_tiles, py::arg("tiles"), py::arg("rows") = 0);
   m.def("conv_set_c4_wave_private", &conv_set_c4_wave_private);
   m.def("conv_tile_pixels", &conv_tile_pixels);

@@ -12,6 +12,8 @@
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.distributions as D
@@ -30,6 +32,11 @@ def _weights_init(m):
         nn.init.zeros_(m.bias)
 
 
+def _env_flag(name, default):
+    v = os.environ.get(name)
+    return default if v is None or v == '' else v not in ('0', 'false', 'False', 'off')
+
+
 class Discriminator(nn.Module):
     """DCGAN discriminator: N x nc x H x W -> N probabilities."""
 
@@ -37,12 +44,17 @@ class Discriminator(nn.Module):
     # BN's backward apply runs inside the first conv's weight-gradient kernel
     # (ops.BnDeferred); False keeps the separate apply launch (A/B, tests)
     defer_first_bn = True
-    # the last BatchNorm+LeakyReLU's forward apply runs in the fused head's pooling (ops.BnActLazy)
-    lazy_head_bn = True
-    # the other BatchNorm+LeakyReLU applies run in the next MFMA convolution's operand staging
-    lazy_conv_bn = True
-    # every BatchNorm+LeakyReLU backward apply runs in the producing convolution's weight gradient
-    defer_bn_bwd = True
+    # Where the BatchNorm+LeakyReLU applies run (profiles/r4/bn_placement.md has the per-kernel A/B):
+    # the last BN's forward apply in the fused head's pooling (ops.BnActLazy): -6.4 us per step
+    lazy_head_bn = _env_flag('BT_LAZY_HEAD_BN', True)
+    # the other forward applies in the next MFMA convolution's operand staging: measured +15 us
+    # per step (each such convolution doubles; its per-k-step rewrite of the staged tile sits
+    # between the stage's arrival and the barrier of latency-bound k-loops), so off by default
+    lazy_conv_bn = _env_flag('BT_LAZY_CONV_BN', False)
+    # every backward apply in the producing convolution's weight gradient (in-kernel fold, gx side
+    # output): measured +9 us per step against the apply launches, so off by default (the first
+    # layer, which has no data gradient, always takes its BN's backward: defer_first_bn)
+    defer_bn_bwd = _env_flag('BT_DEFER_BN_BWD', False)
 
     def __init__(self, nc=3, ndf=32, adaptive=False, fused=True):
         super().__init__()

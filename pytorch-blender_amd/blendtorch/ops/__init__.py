@@ -890,11 +890,15 @@ class BnBwdFold:
     added), the destinations of its ``dw``/``db`` gradients (``done``: the
     parameters whose bucket views they are) and ``gx_out``, the BN's input
     gradient (set by the convolution for its data gradient)."""
-    __slots__ = ('x', 'mean', 'invstd', 'w', 'b', 'slope', 'acc', 'dw', 'db', 'done', 'gx_out')
+    __slots__ = ('x', 'mean', 'invstd', 'w', 'b', 'slope', 'acc', 'dw', 'db', 'done', 'gx_out', 'assign')
 
-    def __init__(self, x, mean, invstd, w, b, slope, acc, dw, db, done):
+    def __init__(self, x, mean, invstd, w, b, slope, acc, dw, db, done, assign=()):
         self.x, self.mean, self.invstd, self.w, self.b, self.slope = x, mean, invstd, w, b, slope
         self.acc, self.dw, self.db, self.done = acc, dw, db, done
+        # (param, tensor): gradients that are not bucket views, set on the parameters once the kernel
+        # that writes them is enqueued (returning them from the BN backward would let autograd copy
+        # them before they are written)
+        self.assign = assign
         self.gx_out = None
 
 
@@ -1054,11 +1058,15 @@ def _bn_function():
                 if db.dtype != torch.float32 or not db.is_contiguous():
                     db, b_sunk = torch.empty_like(b), False
                 if (w_sunk or ctx.params[0].grad is None) and (b_sunk or ctx.params[1].grad is None):
+                    _count('bn_backward_from_stats')   # (the sums: from the consumer's epilogue)
                     _count('bn_backward_deferred_fold')
+                    sunk = (w_sunk, b_sunk)
                     ctx.defer.pending = BnBwdFold(xs, mean, invstd, w, b, ctx.slope, ctx.acc, dw, db,
-                                                  tuple(p for p, sk in zip(ctx.params, (w_sunk, b_sunk)) if sk))
-                    return (gys.permute(0, 3, 1, 2), None if w_sunk else dw, None if b_sunk else db, None, None,
-                            None, None, None, None, None, None, None, None)
+                                                  tuple(p for p, sk in zip(ctx.params, sunk) if sk),
+                                                  tuple((p, g) for p, g, sk in zip(ctx.params, (dw, db), sunk)
+                                                        if not sk and p.requires_grad))
+                    return (gys.permute(0, 3, 1, 2), None, None, None, None, None, None, None, None, None, None,
+                            None, None)
             if folded:
                 raise RuntimeError('BatchNormLeakyReLU2d: its statistics were folded for another gradient')
             # (not before the folded branch: the fold already took the bucket views)
@@ -1353,6 +1361,9 @@ def conv_wgrad(x, dy, out, target_blocks=None, chain=None, last=True, lut=None, 
         _grad_done(*fold_params)
     if bn_done:
         _grad_done(*bn_done)
+    if isinstance(bn_dy, BnBwdFold):
+        for prm, grad in bn_dy.assign:   # (unset .grad, checked by the BN backward)
+            prm.grad = grad if prm.grad is None else prm.grad + grad
     if chain is not None:
         if side is not None:
             _count('conv_wgrad_side_reduce')

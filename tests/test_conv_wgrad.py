@@ -24,6 +24,14 @@ def _ref(x, dy, cout):
     return torch.nn.grad.conv2d_weight(x.float(), (cout, x.shape[1], 4, 4), dy.float(), stride=2, padding=1)
 
 
+@pytest.fixture(params=[0, 1], ids=['pipe0', 'pipe1'])
+def wgrad_pipe(request):
+    """Register-staged weight gradient: fragments read a step ahead of the MFMAs (1) or not (0)."""
+    ops.hip_ext().conv_set_wgrad_pipe(request.param)
+    yield request.param
+    ops.hip_ext().conv_set_wgrad_pipe(-1)
+
+
 @pytest.fixture(params=[0, 2, 3], ids=lambda s: f'staging{s}')
 def wgrad_staging(request):
     """Weight-gradient staging: register ring (0) or LDS-DMA stages of 64
@@ -38,7 +46,7 @@ def wgrad_staging(request):
                                             (3, 32, 14, 18, 64), (8, 32, 240, 320, 64), (2, 64, 60, 80, 128),
                                             (1, 128, 60, 64, 256), (3, 32, 10, 66, 64)])
 @pytest.mark.parametrize('layout', ['channels_last', 'contiguous'])
-def test_wgrad_matches_fp32_reference(dev, N, Cin, H, W, Cout, layout, wgrad_staging):
+def test_wgrad_matches_fp32_reference(dev, N, Cin, H, W, Cout, layout, wgrad_staging, wgrad_pipe):
     g = torch.Generator(device=dev).manual_seed(N * Cin + H)
     cl = torch.channels_last
     x = torch.randn(N, Cin, H, W, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
@@ -55,7 +63,7 @@ def test_wgrad_matches_fp32_reference(dev, N, Cin, H, W, Cout, layout, wgrad_sta
 
 
 @pytest.mark.gpu
-def test_wgrad_asymmetric_operands(dev, wgrad_staging):
+def test_wgrad_asymmetric_operands(dev, wgrad_staging, wgrad_pipe):
     """Structured (non-random) operands: a transposed or mis-swizzled tile
     cannot pass by symmetry."""
     cl = torch.channels_last
@@ -85,10 +93,12 @@ def test_discriminator_backward_with_mfma_convs(dev):
         n.load_state_dict(nets[0].state_dict())
     x = torch.rand(4, 3, 240, 320, device=dev).contiguous(memory_format=torch.channels_last)
     before = ops.KERNEL_CALLS.get('conv_wgrad', 0)
-    bn_before = ops.KERNEL_CALLS.get('bn_forward_from_stats', 0)
+    def stats_bns():   # BN calls that took the convolution epilogue's sums (applied, or lazily by a consumer)
+        return ops.KERNEL_CALLS.get('bn_forward_from_stats', 0) + ops.KERNEL_CALLS.get('bn_forward_lazy', 0)
+    bn_before = stats_bns()
     nets[0].forward_bf16(x.to(torch.bfloat16), mfma=True).float().sum().backward()
     assert ops.KERNEL_CALLS['conv_wgrad'] == before + 3          # conv 2, 3 and 4 (conv 1 has Cin = 3)
-    assert ops.KERNEL_CALLS['bn_forward_from_stats'] == bn_before + 3   # their BNs take the epilogue sums
+    assert stats_bns() == bn_before + 3   # their BNs take the epilogue sums
     nets[1].forward_bf16(x.to(torch.bfloat16), mfma=False).float().sum().backward()
     nets[2](x).sum().backward()                                   # fp32 reference
     for (n, pa), pb, pr in zip(nets[0].named_parameters(), nets[1].parameters(), nets[2].parameters()):
@@ -287,6 +297,8 @@ def test_bn_accumulators_fold_and_clear(dev, monkeypatch):
     a = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
     b = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
     b.load_state_dict(a.state_dict())
+    for m in (a, b):   # the apply kernels' path (the BN applies moved into their neighbours:
+        m.lazy_head_bn = m.lazy_conv_bn = m.defer_bn_bwd = False   # test_lazy_bn_applies_match_apply_pass)
     x = torch.rand(4, 4, 96, 128, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
     acc_supported = ops.bn_acc_supported
     for step in range(3):
@@ -420,16 +432,17 @@ def test_first_bn_backward_deferred_into_first_wgrad(dev, c4_staging):
     a = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
     b = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
     b.load_state_dict(a.state_dict())
-    b.defer_first_bn = False
-    d0 = ops.KERNEL_CALLS.get('bn_backward_deferred', 0)
+    a.defer_bn_bwd = False                      # only the first BN hands its backward on
+    b.defer_first_bn = b.defer_bn_bwd = False   # none
+    d0 = ops.KERNEL_CALLS.get('bn_backward_deferred_fold', 0)
     w0 = ops.KERNEL_CALLS.get('conv_wgrad_bn_dy', 0)
     la = a.bce_loss_bf16(xu8, 1.0, decode=cfg)
     la.backward()
-    assert ops.KERNEL_CALLS.get('bn_backward_deferred', 0) == d0 + 1
+    assert ops.KERNEL_CALLS.get('bn_backward_deferred_fold', 0) == d0 + 1
     assert ops.KERNEL_CALLS.get('conv_wgrad_bn_dy', 0) == w0 + 1
     lb = b.bce_loss_bf16(xu8, 1.0, decode=cfg)
     lb.backward()
-    assert ops.KERNEL_CALLS.get('bn_backward_deferred', 0) == d0 + 1      # b took the apply launch
+    assert ops.KERNEL_CALLS.get('bn_backward_deferred_fold', 0) == d0 + 1      # b took the apply launch
     torch.testing.assert_close(la, lb, rtol=0, atol=0)
     for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
         torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-4, atol=1e-6 + 1e-4 * float(pb.grad.abs().max()), msg=n)
@@ -553,7 +566,7 @@ def test_forward_applies_input_bn(dev, cin, cout, hw):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('cin,cout,hw', [(32, 64, (64, 80)), (128, 256, (32, 40)), (4, 32, (96, 128))])
-def test_wgrad_applies_bn_backward_folded(dev, cin, cout, hw):
+def test_wgrad_applies_bn_backward_folded(dev, cin, cout, hw, wgrad_pipe):
     """The weight gradient that applies the following BatchNorm+LeakyReLU's
     backward to its staged dY (ops.BnBwdFold): it folds the BN's backward
     accumulator itself (dw / db equal to the fp64 sums rounded once), its gx
@@ -610,3 +623,45 @@ def test_wgrad_applies_bn_backward_folded(dev, cin, cout, hw):
     if cin != 4:
         assert torch.equal(pend.gx_out, gx_ref)
     torch.testing.assert_close(out, out_ref, rtol=1e-5, atol=1e-5 * float(out_ref.abs().max()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('shape', [(2, 64, 80), (3, 50, 72)])
+@pytest.mark.parametrize('with_bn', [False, True])
+def test_dgrad_patch_matches_tap_gemm(dev, shape, with_bn):
+    """The 32-channel layer's data gradient from a dY patch (all four parity
+    classes per block, weights as the MFMA A operand) against the tap-GEMM
+    path: bit-identical dx (the same K-step order), the same BN-backward sums
+    (fp64 adds in another grouping), both equal to the fp32 reference.  50 x
+    72: ragged class-grid tiles (25 x 36 against 4 x 32)."""
+    import torch.nn.functional as F
+    cl = torch.channels_last
+    N, H, W = shape
+    g = torch.Generator(device=dev).manual_seed(H + W)
+    dy = torch.randn(N, 64, H // 2, W // 2, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    w = (0.05 * torch.randn(64, 32, 4, 4, device=dev, generator=g)).to(torch.bfloat16).contiguous(memory_format=cl)
+    outs = []
+    for patch in (1, 0):
+        ops.hip_ext().conv_set_dgrad_patch(patch)
+        try:
+            link = None
+            if with_bn:
+                link = ops.BnLink()
+                x = torch.randn(N, H, W, 32, device=dev, generator=torch.Generator(device=dev).manual_seed(5))
+                link.x = x.to(torch.bfloat16)
+                link.mean = torch.full((32,), 0.1, device=dev)
+                link.invstd = torch.full((32,), 1.3, device=dev)
+                link.w = torch.linspace(0.5, 1.5, 32, device=dev)
+                link.b = torch.linspace(-0.2, 0.2, 32, device=dev)
+                link.slope = 0.2
+                link.acc = ops.BnAccumulator(32, dev)
+            dx = ops.conv_dgrad(dy, w, (N, 32, H, W), bn=link)
+            sums = link.acc.bwd[:link.acc.R * 64].view(link.acc.R, 2, 32).sum(0) if with_bn else None
+            outs.append((dx, sums))
+        finally:
+            ops.hip_ext().conv_set_dgrad_patch(-1)
+    assert torch.equal(outs[0][0], outs[1][0])
+    if with_bn:
+        torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-9, atol=1e-6)
+    ref = F.conv_transpose2d(dy.float(), w.float(), None, 2, 1)
+    torch.testing.assert_close(outs[0][0].float(), ref, rtol=2 ** -7, atol=1e-3 * float(ref.abs().max()))

@@ -196,6 +196,10 @@ def test_lazy_bn_applies_match_apply_pass(dev):
         assert torch.equal(losses[0], losses[1])
         for (n, ba), bb in zip(nets[0].named_buffers(), nets[1].buffers()):
             assert torch.equal(ba, bb), n
+        for mod in nets[0].modules():   # every accumulator cleared by the kernels that folded it
+            if isinstance(mod, ops.BatchNormLeakyReLU2d):
+                for acc in mod.__dict__['_bt_acc_ring'][0]:
+                    assert int(torch.count_nonzero(acc.fwd)) == 0 and int(torch.count_nonzero(acc.bwd)) == 0
         # the weight gradients' slice groups add with fp32 atomics (conv_wgrad_reduce): their
         # order, not the lazy apply, varies between runs -- equal up to that reordering
         for (n, pa), pb in zip(nets[0].named_parameters(), nets[1].parameters()):
