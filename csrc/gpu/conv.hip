@@ -1906,6 +1906,10 @@ __global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tile
   }
   uint32_t w0[NL], w1[NL];   // raw pixels in flight (u8: the RGBA word; bf16: two words)
   bool ok[NL];
+  // act_out (u8 input): the decoded frame, bf16 NHWC RGBA -- each tile stores the 2 TR x 128 input
+  // pixels it owns (patch rows 1 .. 2 TR, columns 1 .. 128; even sides: every pixel once), the
+  // weight gradient's operand without a decode of its own
+  uint32_t eo[NL];
   auto load_patch = [&](int tile) __attribute__((always_inline)) {
     const int n = tile / (tiles_r * tiles_c), rem = tile - n * (tiles_r * tiles_c);
     const int r0 = 2 * (rem / tiles_c) * TR - 1, c0 = 2 * (rem % tiles_c) * kC1Cols - 1;
@@ -1914,6 +1918,7 @@ __global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tile
       const int ir = r0 + pr[i], ic = c0 + pc[i];
       ok[i] = unsigned(ir) < unsigned(p.SH) && unsigned(ic) < unsigned(p.SW);
       const uint32_t e = uint32_t(((n * p.SH + ir) * p.SW + ic) * 4);
+      eo[i] = ok[i] && unsigned(pr[i] - 1) < unsigned(2 * TR) && unsigned(pc[i] - 1) < unsigned(2 * kC1Cols) ? e : ~0u;
       if constexpr (u8in) {
         w0[i] = bload4(rs_src, ok[i] ? e : kOOB);
       } else {
@@ -1927,6 +1932,7 @@ __global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tile
     for (int i = 0; i < NL; ++i) {
       const uint2 v = u8in ? lut_px(smem + LUT_OFF, w0[i], ok[i]) : make_uint2(w0[i], w1[i]);
       if ((i + 1) * kThreads <= PX || t + kThreads * i < PX) *reinterpret_cast<uint2*>(smem + (t + kThreads * i) * 8) = v;
+      if (u8in && p.act_out && eo[i] != ~0u) *reinterpret_cast<uint2*>(reinterpret_cast<char*>(p.act_out) + eo[i] * 2u) = v;
     }
   };
   // the B fragments' patch offsets (tile-invariant): pixel fragment j of this
@@ -2501,6 +2507,12 @@ hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream) {
   if (p.lut && (p.Cin != 4 || (reinterpret_cast<uintptr_t>(p.lut) & 7))) return hipErrorInvalidValue;
   g.acc_r = p.stats ? p.acc_r : 0;
   if (g.acc_r < 0 || g.acc_r > 64) return hipErrorInvalidValue;
+  if (p.act_out && !p.act.on()) {   // u8 first layer: the decoded frame as a side output (patch kernel)
+    if (p.Cin != 4 || !p.lut || conv1_tiles() <= 0 || p.H % 2 || p.W % 2 || (reinterpret_cast<uintptr_t>(p.act_out) & 7) ||
+        (p.stats && p.acc_r <= 0) || p.Cout != conv_tile_channels(p.Cout, true))
+      return hipErrorInvalidValue;   // (the conditions of the patch kernel's dispatch below)
+    g.act_out = p.act_out;
+  }
   if (p.act.on()) {   // the input BN applied in the staging: C <= 128 (two coefficient sets), accumulator given
     if (p.Cin == 4 || p.Cin > 2 * FBK || !p.act.acc || p.act.R <= 0 || !p.act.b || !p.act.mean || !p.act.invstd ||
         p.act.M != int64_t(p.N) * p.H * p.W || (reinterpret_cast<uintptr_t>(p.act_out) & 15) ||

@@ -1277,6 +1277,8 @@ class WgradChain:
 
 
 _WGRAD_BLOCKS = int(os.environ.get('BT_WGRAD_BLOCKS', '512'))
+# first layer on raw u8 frames: its forward writes the decoded frames for its weight gradient (BT_C4_DECODED)
+_C4_DECODED = os.environ.get('BT_C4_DECODED', '0') not in ('', '0')
 
 
 def conv_wgrad(x, dy, out, target_blocks=None, chain=None, last=True, lut=None, fold=None, bn_dy=None, param=None,
@@ -1386,16 +1388,19 @@ def conv_fwd(x, w16, stats=None, acc_r=0, lut=None, act=None, act_out=None):
     ``fwd`` tensor with ``acc_r`` replicas, added into with atomics.
     ``lut`` (first layer): ``x`` is the raw u8 RGBA frames ([N, 4, H, W],
     channels-last) and ``lut`` their bf16 decode table (:func:`decode_lut_bf16`):
-    the decode happens in the convolution's tile loads.  ``act``: the
+    the decode happens in the convolution's tile loads (``act_out``, bf16 like
+    ``x``: also receives the decoded frames, for the weight gradient).  ``act``: the
     :class:`BnActLazy` of the BatchNorm+LeakyReLU whose INPUT ``x`` is -- the
     convolution applies it to its operand tiles; ``act_out`` (same shape as
     ``x``, optional) receives that activation."""
     import torch
     ext = hip_ext()
     N, Cin, H, W = x.shape
-    if act_out is not None and (act is None or act_out.shape != x.shape or act_out.dtype != torch.bfloat16
+    if act_out is not None and (act is None and lut is None or act_out.shape != x.shape
+                                or act_out.dtype != torch.bfloat16
                                 or not act_out.is_contiguous(memory_format=torch.channels_last)):
-        raise ValueError('conv_fwd: act_out is the activation of act, shaped and laid out like x')
+        raise ValueError('conv_fwd: act_out is the activation of act (or, with lut, the decoded frames), '
+                         'shaped and laid out like x')
     Cout = w16.shape[0]
     cl = torch.channels_last
     # first layer fed RGBA: a 3-input-channel weight, the 4th input channel ignored
@@ -1557,6 +1562,16 @@ def _conv_function():
                 ctx.bn_out = bn_out
             if lut is not None:   # raw u8 frames: the decode runs in the MFMA kernels' loads
                 if isinstance(with_stats, BnAccumulator):
+                    if _C4_DECODED and w32.requires_grad and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0 \
+                            and int(hip_ext().conv_tile_channels(int(w16.shape[0]), True)) == w16.shape[0]:
+                        # the forward also writes the decoded frames: the weight gradient reads
+                        # those (bf16) instead of decoding the u8 frames again
+                        xd = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device,
+                                         memory_format=torch.channels_last)
+                        y = conv_fwd(x, w16, with_stats.fwd, with_stats.R, lut=lut, act_out=xd)
+                        ctx.save_for_backward(xd, w16)
+                        ctx.lut = None
+                        return y
                     return conv_fwd(x, w16, with_stats.fwd, with_stats.R, lut=lut)
                 if with_stats:
                     raise ValueError('conv4x4s2: u8 input takes accumulator statistics only')

@@ -665,3 +665,36 @@ def test_dgrad_patch_matches_tap_gemm(dev, shape, with_bn):
         torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-9, atol=1e-6)
     ref = F.conv_transpose2d(dy.float(), w.float(), None, 2, 1)
     torch.testing.assert_close(outs[0][0].float(), ref, rtol=2 ** -7, atol=1e-3 * float(ref.abs().max()))
+
+
+@pytest.mark.gpu
+def test_first_layer_decoded_side_output(dev, monkeypatch):
+    """The first layer's patch forward also writes the decoded frames
+    (act_out) and the weight gradient reads those bf16 frames instead of
+    decoding the u8 frames again: the decoded tensor equals ops.decode's,
+    and the step gives the same loss and gradients (up to the weight
+    reduce's atomic order) as decoding in the weight gradient."""
+    from blendtorch.models import Discriminator
+    cl = torch.channels_last
+    cfg = ops.DecodeConfig.unit(channels='rgba', gamma=2.2, dtype='bfloat16', layout='nhwc')
+    g = torch.Generator(device=dev).manual_seed(9)
+    raw = torch.randint(0, 256, (4, 96, 128, 4), dtype=torch.uint8, device=dev, generator=g)
+    xu8 = raw.permute(0, 3, 1, 2)
+    lut = ops.decode_lut_bf16(cfg, dev)
+    w16 = (0.1 * torch.randn(32, 3, 4, 4, device=dev, generator=g)).to(torch.bfloat16).contiguous(memory_format=cl)
+    xd = torch.full(xu8.shape, float('nan'), dtype=torch.bfloat16, device=dev).contiguous(memory_format=cl)
+    acc = ops.BnAccumulator(32, dev)
+    ops.conv_fwd(xu8, w16, acc.fwd, acc.R, lut=lut, act_out=xd)
+    assert torch.equal(xd, ops.decode(raw, cfg).permute(0, 3, 1, 2))
+    torch.manual_seed(3)
+    nets = [Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl) for _ in range(2)]
+    nets[1].load_state_dict(nets[0].state_dict())
+    losses = []
+    for m, dec in zip(nets, (True, False)):
+        monkeypatch.setattr(ops, '_C4_DECODED', dec)
+        loss = m.bce_loss_bf16(xu8, 1.0, decode=cfg)
+        loss.backward()
+        losses.append(loss.detach())
+    assert torch.equal(losses[0], losses[1])
+    for (n, pa), pb in zip(nets[0].named_parameters(), nets[1].parameters()):
+        torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-4, atol=1e-6 + 1e-4 * float(pb.grad.abs().max()), msg=n)
