@@ -2041,26 +2041,61 @@ __global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tile
 // Here a block loads the (4 + 2) x (32 + 2) dY pixels under a 4 x 32 tile of
 // the class grid ONCE into LDS (26 KB, 16-byte chunks XOR-swizzled by pixel so
 // a 16-lane fragment read of 16 consecutive pixels hits 16 bank slots) and
-// runs all four parity classes' 8 K=32 steps straight from it: the weights
-// (the class's [ci][tap][co] rows) are the MFMA's A operand, loaded into
-// registers per class, and the patch pixels its B operand -- so a lane's
-// accumulators hold 8 consecutive dx channels of one pixel (c1_row_chan) and
-// the epilogue stores 16 bytes and sums the BN-backward terms from registers.
+// runs all four parity classes' 8 K=32 steps straight from it.  The weights
+// -- a class's [32 ci][4 taps x 64 co] rows, 16 KB -- are the MFMA's A
+// operand, staged in LDS once per class for all 4 waves (double-buffered: the
+// next class's load is in flight while this class computes), and the patch
+// pixels its B operand: a lane's accumulators hold 8 consecutive dx channels
+// of one pixel (c1_row_chan), so the epilogue stores 16 bytes and sums the
+// BN-backward terms from registers.  (Weights loaded into every lane's
+// registers instead: 4 x the L2 traffic, 65-67 us.)
 constexpr int DP_TA = 4, DP_TB = 32;                  // class-grid rows x columns per block
 constexpr int DP_PR = DP_TA + 2, DP_PC = DP_TB + 2;   // the dY patch: one pixel of halo each side
 constexpr int DP_C = 64, DP_NOUT = 32;                 // dY channels, dx channels
 constexpr int DP_NP = DP_PR * DP_PC;                   // 204 patch pixels, 128 bytes each
+constexpr int DP_PATCH = DP_NP * DP_C * 2;             // 26,112 bytes
+constexpr int DP_WROW = 4 * DP_C * 2;                  // one weight row: 4 taps x 64 co, 512 bytes (32 chunks)
+constexpr int DP_W = DP_NOUT * DP_WROW;                // one class's weights, 16 KiB
 __device__ __forceinline__ int dp_off(int px, int q) { return px * (DP_C * 2) + ((q ^ ((px >> 1) & 7)) << 4); }
+// weight row ci, chunk kc (k = 8 kc): the 16 rows a fragment reads (c1_row_chan: bits 0-1, 3-4 of ci)
+// take 16 different chunk slots
+__device__ __forceinline__ int dpw_off(int ci, int kc) {
+  return ci * DP_WROW + ((kc ^ ((ci & 3) | (((ci >> 3) & 3) << 2))) << 4);
+}
 
 __global__ __launch_bounds__(kThreads) void dgrad_patch_kernel(TapGemm p) {
   constexpr int NCH = DP_NP * 8, NL = (NCH + kThreads - 1) / kThreads;
-  __shared__ __attribute__((aligned(16))) char smem[DP_NP * DP_C * 2 + 4 * 2 * DP_NOUT * 4];
-  float* red = reinterpret_cast<float*>(smem + DP_NP * DP_C * 2);
+  constexpr int WCH = DP_W / 16, WL = WCH / kThreads;   // 1024 weight chunks, 4 per thread
+  __shared__ __attribute__((aligned(16))) char smem[DP_PATCH + 2 * DP_W + 4 * 2 * DP_NOUT * 4];
+  char* const wl = smem + DP_PATCH;
+  float* red = reinterpret_cast<float*>(smem + DP_PATCH + 2 * DP_W);
   const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6, g = lane >> 4;
   const int tb = (p.GW + DP_TB - 1) / DP_TB, ta = (p.GH + DP_TA - 1) / DP_TA;
   const int blk = int(blockIdx.x);
   const int n = blk / (ta * tb), rem = blk - n * (ta * tb);
   const int a0 = (rem / tb) * DP_TA, b0 = (rem % tb) * DP_TB;
+  // a class's weight chunks: chunk c = t + 256 i -> row ci = c / 32, chunk kc = c % 32
+  // (k = 8 kc: tap kc / 8, co 8 (kc % 8)) <- wt[ci][kh][kw][co]
+  static_assert(WL == 4, "4 weight chunks per thread");
+  // (four named registers, not an array: an array live across the class loop was promoted to LDS)
+  uint4 wv0, wv1, wv2, wv3;
+  auto wsrc = [&](int cls, int i) -> const uint4* {
+    const int ph = cls >> 1, pw = cls & 1;
+    const int c = t + kThreads * i, ci = c >> 5, kc = c & 31, tap = kc >> 3;
+    const int kh = 1 - ph + 2 * (tap >> 1), kw = 1 - pw + 2 * (tap & 1);
+    return reinterpret_cast<const uint4*>(p.w + (ci * 16 + kh * 4 + kw) * DP_C + 8 * (kc & 7));
+  };
+  auto load_w = [&](int cls) __attribute__((always_inline)) {
+    wv0 = *wsrc(cls, 0), wv1 = *wsrc(cls, 1), wv2 = *wsrc(cls, 2), wv3 = *wsrc(cls, 3);
+  };
+  auto wdst = [&](int buf, int i) -> uint4* {
+    const int c = t + kThreads * i;
+    return reinterpret_cast<uint4*>(wl + buf * DP_W + dpw_off(c >> 5, c & 31));
+  };
+  auto store_w = [&](int buf) __attribute__((always_inline)) {
+    *wdst(buf, 0) = wv0, *wdst(buf, 1) = wv1, *wdst(buf, 2) = wv2, *wdst(buf, 3) = wv3;
+  };
+  load_w(0);
   // the patch: chunk u = t + 256 i is chunk u & 7 of patch pixel u >> 3
   {
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.src, int64_t(p.N) * p.SH * p.SW * DP_C * 2);
@@ -2079,6 +2114,7 @@ __global__ __launch_bounds__(kThreads) void dgrad_patch_kernel(TapGemm p) {
       if ((i + 1) * kThreads <= NCH || u < NCH) *reinterpret_cast<uint4*>(smem + dp_off(u >> 3, u & 7)) = v[i];
     }
   }
+  store_w(0);
   // this wave: class-grid row a0 + wave, columns b0 + 16 j + (lane & 15), j = 0, 1
   const int ra = a0 + wave;
   const bool bnf = p.bn.part != nullptr;
@@ -2094,21 +2130,15 @@ __global__ __launch_bounds__(kThreads) void dgrad_patch_kernel(TapGemm p) {
       bb[e] = p.bn.b[c];
     }
   }
+  // A fragment offsets (class-invariant): row c1_row_chan(f, lane & 15), chunk 4 s + g
+  int aoff[2];
+#pragma unroll
+  for (int f = 0; f < 2; ++f) aoff[f] = c1_row_chan(f, lane & 15);
   __syncthreads();
   for (int cls = 0; cls < 4; ++cls) {
     const int ph = cls >> 1, pw = cls & 1;
-    // A: the class's weight rows, ci = c1_row_chan(f, lane & 15); K step s = tap s / 2,
-    // dY channels 32 (s & 1) + 8 (lane >> 4) .. + 7 -> wt[ci][kh][kw][co]
-    bf16x8 wa[2][8];
-#pragma unroll
-    for (int f = 0; f < 2; ++f)
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        const int ci = c1_row_chan(f, lane & 15), tap = s >> 1;
-        const int kh = 1 - ph + 2 * (tap >> 1), kw = 1 - pw + 2 * (tap & 1);
-        const int co = 32 * (s & 1) + 8 * g;
-        wa[f][s] = *reinterpret_cast<const bf16x8*>(p.w + (ci * 16 + kh * 4 + kw) * DP_C + co);
-      }
+    if (cls < 3) load_w(cls + 1);   // in flight while this class computes
+    const char* wb = wl + (cls & 1) * DP_W;
     f32x4 acc[2][2];
 #pragma unroll
     for (int f = 0; f < 2; ++f)
@@ -2118,7 +2148,9 @@ __global__ __launch_bounds__(kThreads) void dgrad_patch_kernel(TapGemm p) {
     for (int s = 0; s < 8; ++s) {
       const int tap = s >> 1, dr = ph - (tap >> 1), dc = pw - (tap & 1);
       const int q = 4 * (s & 1) + g;
-      bf16x8 bm[2];
+      bf16x8 wa[2], bm[2];
+#pragma unroll
+      for (int f = 0; f < 2; ++f) wa[f] = *reinterpret_cast<const bf16x8*>(wb + dpw_off(aoff[f], 4 * s + g));
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int px = (wave + dr + 1) * DP_PC + 16 * j + (lane & 15) + dc + 1;
@@ -2128,36 +2160,40 @@ __global__ __launch_bounds__(kThreads) void dgrad_patch_kernel(TapGemm p) {
       for (int f = 0; f < 2; ++f)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[f][s], bm[j], acc[f][j], 0, 0, 0);
+          acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[f], bm[j], acc[f][j], 0, 0, 0);
     }
     // epilogue: dx pixel (2 a + ph, 2 b + pw), channels 8 g .. + 7
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int bcol = b0 + 16 * j + (lane & 15);
       if (ra < p.GH && bcol < p.GW) {
-      const int off = ((n * p.OH + 2 * ra + ph) * p.OW + 2 * bcol + pw) * DP_NOUT + 8 * g;
-      uint4 xv = make_uint4(0, 0, 0, 0);
-      if (bnf) xv = *reinterpret_cast<const uint4*>(p.bn.x + off);
-      uint32_t pk[4];
+        const int off = ((n * p.OH + 2 * ra + ph) * p.OW + 2 * bcol + pw) * DP_NOUT + 8 * g;
+        uint4 xv = make_uint4(0, 0, 0, 0);
+        if (bnf) xv = *reinterpret_cast<const uint4*>(p.bn.x + off);
+        uint32_t pk[4];
 #pragma unroll
-      for (int h = 0; h < 4; ++h) {   // channels 8 g + 2 h, + 1: fragment h >> 1, rows 2 (h & 1), + 1
-        const f32x4& a = acc[h >> 1][j];
-        const f32x2 pr = {a[2 * (h & 1)], a[2 * (h & 1) + 1]};
-        pk[h] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2));
-      }
-      *reinterpret_cast<uint4*>(p.dst + off) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-      if (bnf) {
-        const uint32_t xw[4] = {xv.x, xv.y, xv.z, xv.w};
+        for (int h = 0; h < 4; ++h) {   // channels 8 g + 2 h, + 1: fragment h >> 1, rows 2 (h & 1), + 1
+          const f32x4& a = acc[h >> 1][j];
+          const f32x2 pr = {a[2 * (h & 1)], a[2 * (h & 1) + 1]};
+          pk[h] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2));
+        }
+        *reinterpret_cast<uint4*>(p.dst + off) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+        if (bnf) {
+          const uint32_t xw[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float gv = __uint_as_float(e & 1 ? pk[e >> 1] & 0xFFFF0000u : pk[e >> 1] << 16);
-          const float xh = fmaf(__uint_as_float(e & 1 ? xw[e >> 1] & 0xFFFF0000u : xw[e >> 1] << 16), is[e], nm[e]);
-          const float gz = fmaf(xh, ww[e], bb[e]) > 0.f ? gv : gv * p.bn.slope;
-          bs[e] += gz;
-          bq[e] += gz * xh;
+          for (int e = 0; e < 8; ++e) {
+            const float gv = __uint_as_float(e & 1 ? pk[e >> 1] & 0xFFFF0000u : pk[e >> 1] << 16);
+            const float xh = fmaf(__uint_as_float(e & 1 ? xw[e >> 1] & 0xFFFF0000u : xw[e >> 1] << 16), is[e], nm[e]);
+            const float gz = fmaf(xh, ww[e], bb[e]) > 0.f ? gv : gv * p.bn.slope;
+            bs[e] += gz;
+            bq[e] += gz * xh;
+          }
         }
       }
-      }
+    }
+    if (cls < 3) {   // the next class's weights into the other buffer (last read by class cls - 1)
+      store_w((cls + 1) & 1);
+      __syncthreads();
     }
   }
   if (!bnf) return;
@@ -2211,11 +2247,11 @@ namespace {
 // weight-gradient staging: 0 = register ring (conv_wgrad_kernel, default), 2 /
 // 3 = LDS-DMA stages of 64 pixels (conv_wgrad_dma_kernel: 33 us against 24 us
 // per layer in the disc step, profiles/r4/disc_kernels.md); BT_WGRAD_STAGING
-int g_dgrad_patch = -1;   // the 32-channel data gradient from a dY patch (BT_DGRAD_PATCH, default on)
+int g_dgrad_patch = -1;   // the 32-channel data gradient from a dY patch (BT_DGRAD_PATCH; off until it measures faster)
 int dgrad_patch() {
   if (g_dgrad_patch < 0) {
     const char* v = std::getenv("BT_DGRAD_PATCH");
-    g_dgrad_patch = v ? (std::atoi(v) ? 1 : 0) : 1;
+    g_dgrad_patch = v ? (std::atoi(v) ? 1 : 0) : 0;
   }
   return g_dgrad_patch;
 }

@@ -1,0 +1,17 @@
+#!/bin/bash
+# GPU session 13: the 32-channel data gradient from a dY patch, weights shared through LDS -- tests, A/B, trace.
+set -u
+cd "$(dirname "$0")/../.."
+mkdir -p gpurun_out/b13
+export TMPDIR=/tmp
+trap 'find gpurun_out -type f -size +4M -print -delete; du -sh gpurun_out' EXIT
+timeout -k 10 300 python -u -m pytest -x -q --timeout 150 --timeout-method thread -p no:cacheprovider \
+  tests/test_conv_wgrad.py -m gpu -k "dgrad or discriminator or bn" > gpurun_out/b13/pytest.log 2>&1
+rc=$?; tail -2 gpurun_out/b13/pytest.log; grep -E "^(FAILED|E  )" gpurun_out/b13/pytest.log | head -20; [ $rc -eq 0 ] || exit $rc
+for v in "BT_DGRAD_PATCH=1" "BT_DGRAD_PATCH=0" "BT_DGRAD_PATCH=1" "BT_DGRAD_PATCH=0"; do
+  timeout -k 10 200 env $v python bench.py --consumer disc --steps 2000 > gpurun_out/b13/sweep.log 2>&1 || { tail -5 gpurun_out/b13/sweep.log; exit 1; }
+  grep '^{' gpurun_out/b13/sweep.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'v':'$v','value':d['value'],'ms':d['ms_per_step']}))" | tee -a gpurun_out/b13/sweep.jsonl
+done
+BT_DGRAD_PATCH=1 bash scripts/gpurun/disc_trace.sh r4m > /dev/null || exit 1
+cp gpurun_out/trace_r4m/step_sequence.txt gpurun_out/b13/
+sed -n '/mean over/,$p' gpurun_out/trace_r4m/step_sequence.txt | head -40

@@ -661,8 +661,8 @@ def test_dgrad_patch_matches_tap_gemm(dev, shape, with_bn):
         finally:
             ops.hip_ext().conv_set_dgrad_patch(-1)
     assert torch.equal(outs[0][0], outs[1][0])
-    if with_bn:
-        torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-9, atol=1e-6)
+    if with_bn:   # (fp32 per-block partials over other pixel groupings, then fp64 adds)
+        torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-5 * float(outs[1][1].abs().max()))
     ref = F.conv_transpose2d(dy.float(), w.float(), None, 2, 1)
     torch.testing.assert_close(outs[0][0].float(), ref, rtol=2 ** -7, atol=1e-3 * float(ref.abs().max()))
 
