@@ -161,7 +161,8 @@ __device__ __forceinline__ void zero_output(const ConvWgradParams& p) {
 // independent and in flight together); groups add into the zeroed output
 // with float atomics (S / kSliceGroup adds per element).  One lane per
 // element walking all S slices serially was latency-bound (17 us at S = 64).
-constexpr int kSliceGroup = 8;
+constexpr int kSliceGroup = 8;   // (groups of 32 for the first layer's 512 slices -- 16 atomics per
+                                 // element instead of 64 -- measured slower: 8.4 -> 11.0 us)
 
 __device__ __forceinline__ void wgrad_reduce_block(const ConvWgradParams::Reduce& r, int bx, int by) {
   const float* __restrict__ partial = r.partial;
@@ -2043,8 +2044,8 @@ __global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tile
 // a 16-lane fragment read of 16 consecutive pixels hits 16 bank slots) and
 // runs all four parity classes' 8 K=32 steps straight from it.  The weights
 // -- a class's [32 ci][4 taps x 64 co] rows, 16 KB -- are the MFMA's A
-// operand, staged in LDS once per class for all 4 waves (double-buffered: the
-// next class's load is in flight while this class computes), and the patch
+// operand, staged in LDS once per class for all 4 waves (the next class's
+// global loads are in flight while this class computes), and the patch
 // pixels its B operand: a lane's accumulators hold 8 consecutive dx channels
 // of one pixel (c1_row_chan), so the epilogue stores 16 bytes and sums the
 // BN-backward terms from registers.  (Weights loaded into every lane's
@@ -2066,9 +2067,10 @@ __device__ __forceinline__ int dpw_off(int ci, int kc) {
 __global__ __launch_bounds__(kThreads) void dgrad_patch_kernel(TapGemm p) {
   constexpr int NCH = DP_NP * 8, NL = (NCH + kThreads - 1) / kThreads;
   constexpr int WCH = DP_W / 16, WL = WCH / kThreads;   // 1024 weight chunks, 4 per thread
-  __shared__ __attribute__((aligned(16))) char smem[DP_PATCH + 2 * DP_W + 4 * 2 * DP_NOUT * 4];
+  // one weight buffer (43 KB of LDS: 3 blocks per CU; double-buffered, 59 KB, fit 2 and ran slower)
+  __shared__ __attribute__((aligned(16))) char smem[DP_PATCH + DP_W + 4 * 2 * DP_NOUT * 4];
   char* const wl = smem + DP_PATCH;
-  float* red = reinterpret_cast<float*>(smem + DP_PATCH + 2 * DP_W);
+  float* red = reinterpret_cast<float*>(smem + DP_PATCH + DP_W);
   const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6, g = lane >> 4;
   const int tb = (p.GW + DP_TB - 1) / DP_TB, ta = (p.GH + DP_TA - 1) / DP_TA;
   const int blk = int(blockIdx.x);
@@ -2138,7 +2140,16 @@ __global__ __launch_bounds__(kThreads) void dgrad_patch_kernel(TapGemm p) {
   for (int cls = 0; cls < 4; ++cls) {
     const int ph = cls >> 1, pw = cls & 1;
     if (cls < 3) load_w(cls + 1);   // in flight while this class computes
-    const char* wb = wl + (cls & 1) * DP_W;
+    // the epilogue's BN inputs, also in flight during the MFMAs
+    int eoff[2];
+    uint4 xv[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int bcol = b0 + 16 * j + (lane & 15);
+      eoff[j] = ra < p.GH && bcol < p.GW ? ((n * p.OH + 2 * ra + ph) * p.OW + 2 * bcol + pw) * DP_NOUT + 8 * g : -1;
+      xv[j] = bnf && eoff[j] >= 0 ? *reinterpret_cast<const uint4*>(p.bn.x + eoff[j]) : make_uint4(0, 0, 0, 0);
+    }
+    const char* wb = wl;
     f32x4 acc[2][2];
 #pragma unroll
     for (int f = 0; f < 2; ++f)
@@ -2165,11 +2176,8 @@ __global__ __launch_bounds__(kThreads) void dgrad_patch_kernel(TapGemm p) {
     // epilogue: dx pixel (2 a + ph, 2 b + pw), channels 8 g .. + 7
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int bcol = b0 + 16 * j + (lane & 15);
-      if (ra < p.GH && bcol < p.GW) {
-        const int off = ((n * p.OH + 2 * ra + ph) * p.OW + 2 * bcol + pw) * DP_NOUT + 8 * g;
-        uint4 xv = make_uint4(0, 0, 0, 0);
-        if (bnf) xv = *reinterpret_cast<const uint4*>(p.bn.x + off);
+      if (eoff[j] >= 0) {
+        const int off = eoff[j];
         uint32_t pk[4];
 #pragma unroll
         for (int h = 0; h < 4; ++h) {   // channels 8 g + 2 h, + 1: fragment h >> 1, rows 2 (h & 1), + 1
@@ -2179,7 +2187,7 @@ __global__ __launch_bounds__(kThreads) void dgrad_patch_kernel(TapGemm p) {
         }
         *reinterpret_cast<uint4*>(p.dst + off) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
         if (bnf) {
-          const uint32_t xw[4] = {xv.x, xv.y, xv.z, xv.w};
+          const uint32_t xw[4] = {xv[j].x, xv[j].y, xv[j].z, xv[j].w};
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             const float gv = __uint_as_float(e & 1 ? pk[e >> 1] & 0xFFFF0000u : pk[e >> 1] << 16);
@@ -2191,8 +2199,9 @@ __global__ __launch_bounds__(kThreads) void dgrad_patch_kernel(TapGemm p) {
         }
       }
     }
-    if (cls < 3) {   // the next class's weights into the other buffer (last read by class cls - 1)
-      store_w((cls + 1) & 1);
+    if (cls < 3) {   // the next class's weights, once every wave is done with this class's
+      __syncthreads();
+      store_w(0);
       __syncthreads();
     }
   }
@@ -2247,11 +2256,11 @@ namespace {
 // weight-gradient staging: 0 = register ring (conv_wgrad_kernel, default), 2 /
 // 3 = LDS-DMA stages of 64 pixels (conv_wgrad_dma_kernel: 33 us against 24 us
 // per layer in the disc step, profiles/r4/disc_kernels.md); BT_WGRAD_STAGING
-int g_dgrad_patch = -1;   // the 32-channel data gradient from a dY patch (BT_DGRAD_PATCH; off until it measures faster)
+int g_dgrad_patch = -1;   // the 32-channel data gradient from a dY patch (BT_DGRAD_PATCH, default on: 47 -> 36.5 us)
 int dgrad_patch() {
   if (g_dgrad_patch < 0) {
     const char* v = std::getenv("BT_DGRAD_PATCH");
-    g_dgrad_patch = v ? (std::atoi(v) ? 1 : 0) : 0;
+    g_dgrad_patch = v ? (std::atoi(v) ? 1 : 0) : 1;
   }
   return g_dgrad_patch;
 }
