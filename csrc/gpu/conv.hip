@@ -486,6 +486,139 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p)
 }
 
 // ---------------------------------------------------------------------------
+// The weight gradient with 256-column im2col tiles (BT_WGRAD_WIDE).  The
+// register-staged kernel above (128 columns, waves of 32 x 64) runs one
+// barrier and 12 transposing fragment reads per 8 MFMAs per wave; here the
+// waves are 2 (co) x 2 (kc) tiles of 32 x 128: 16 MFMAs and 20 reads per
+// barrier, half the block tiles (and slices of the same length, so the
+// same MFMAs per block).  X rows are 512 bytes: 16 windows of 32 bytes whose
+// low 3 bits take the same XOR swizzle as x_off (every row starts at bank 0,
+// so the 8 rows of a transposing read land on 8 windows).  Each thread
+// stages one dY chunk and four X chunks (im2col columns 64 apart) per step
+// from one pixel cursor.  Non-BN variant (the default path).
+constexpr int BKC2 = 256;
+constexpr int X2_ROW = BKC2 * 2;              // 512-byte LDS rows
+constexpr int X2_TILE = BPX * X2_ROW;         // 16 KiB
+constexpr int STAGE2 = DY_TILE + X2_TILE;     // 20 KiB
+__device__ __forceinline__ int x2_off(int r, int byte) {
+  const int f = (r & 3) | (((r >> 3) & 1) << 2);
+  return r * X2_ROW + ((((byte >> 5) ^ f) << 5) | (byte & 31));
+}
+
+__global__ __launch_bounds__(kThreads) void conv_wgrad_wide_kernel(ConvWgradParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE2];
+  if (run_side(p, smem)) return;
+  const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
+  const int KC = 16 * p.Cin, KT = KC / BKC2, T = (p.Cout / BCO) * KT;
+  const int nwg = main_blocks(p), b = int(blockIdx.x);
+  const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  const int slice = w / T, tile = w - slice * T;
+  const int co0 = (tile / KT) * BCO, kt = tile - (tile / KT) * KT;
+  const int m_begin = slice * int(p.px_per_slice);
+  const int m_end = m_begin + int(p.px_per_slice) < int(p.M) ? m_begin + int(p.px_per_slice) : int(p.M);
+  const int nsteps = m_end > m_begin ? (m_end - m_begin + BPX - 1) / BPX : 0;
+
+  const int dpx = t >> 3, dch = t & 7;   // dY: pixel, 16-byte chunk
+  const int xpx = t >> 3, xch = t & 7;   // X: pixel, chunks xch + 8 i (columns kc0 + 64 i)
+  const int cs = __builtin_ctz(unsigned(p.Cin));   // (host: power-of-two Cin)
+  const int kc0 = kt * BKC2 + xch * 8;
+  int dkh[4], dkw[4], de[4];
+  const int kh = kc0 >> (cs + 2), kw = (kc0 >> cs) & 3, ci = kc0 & (p.Cin - 1);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int kc = kc0 + 64 * i;
+    dkh[i] = (kc >> (cs + 2)) - kh;
+    dkw[i] = ((kc >> cs) & 3) - kw;
+    de[i] = (dkh[i] * p.W + dkw[i]) * p.Cin + ((kc & (p.Cin - 1)) - ci);
+  }
+  XCursor c0;
+  c0.init(m_begin + xpx, p, kh, kw, ci);
+  const int j_col = 2 * BPX * p.Cin, j_row = 2 * (p.W - p.Wo) * p.Cin, j_img = (p.H - 2 * p.Ho) * p.W * p.Cin;
+  const bool single = p.Wo >= BPX;
+  const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(p.x, int64_t(p.N) * p.H * p.W * p.Cin * 2);
+  const __amdgpu_buffer_rsrc_t rs_dy = make_rsrc(p.dy, p.M * p.Cout * 2);
+  constexpr int kDepth = 2;   // (4 stages of 5 chunks: 276 registers, one wave per SIMD)
+  struct Stage {
+    uint4 dy, x[4];
+  };
+  Stage ring[kDepth];
+  int md = m_begin + dpx;
+  uint32_t dy_byte = uint32_t(md) * uint32_t(p.Cout * 2) + uint32_t((co0 + dch * 8) * 2);
+  const uint32_t dy_step = uint32_t(BPX * p.Cout * 2);
+  auto load = [&](Stage& r) __attribute__((always_inline)) {
+    r.dy = bload(rs_dy, md < m_end ? dy_byte : kOOB);
+    const int ih = 2 * c0.oh - 1 + kh, iw = 2 * c0.ow - 1 + kw;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool ok = unsigned(ih + dkh[i]) < unsigned(p.H) && unsigned(iw + dkw[i]) < unsigned(p.W);
+      r.x[i] = bload(rs_x, ok ? uint32_t(c0.e + de[i]) * 2u : kOOB);
+    }
+    md += BPX;
+    dy_byte += dy_step;
+    c0.advance(p.Ho, p.Wo, j_col, j_row, j_img, single);
+  };
+  const int st_dy = dy_off(dpx, dch * 16);
+  int st_x[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) st_x[i] = DY_TILE + x2_off(xpx, (xch + 8 * i) * 16);
+  auto store = [&](const Stage& r, int buf) __attribute__((always_inline)) {
+    char* base = smem + buf * STAGE2;
+    *reinterpret_cast<uint4*>(base + st_dy) = r.dy;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(base + st_x[i]) = r.x[i];
+  };
+
+  f32x4 acc[2][8];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int wco = (wave >> 1) * 32, wkc = (wave & 1) * 128;
+  int ra[2], rb[8];
+  {
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) ra[i] = dy_off(8 * g + q, (wco + 16 * i + 4 * pp) * 2);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) rb[j] = x2_off(8 * g + q, (wkc + 16 * j + 4 * pp) * 2);
+  }
+#pragma unroll
+  for (int u = 0; u < kDepth; ++u) load(ring[u]);
+  const int padded = (nsteps + kDepth - 1) / kDepth * kDepth;
+  for (int s0 = 0; s0 < padded; s0 += kDepth) {
+#pragma unroll
+    for (int u = 0; u < kDepth; ++u) {
+      const int buf = u & 1;
+      store(ring[u], buf);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      load(ring[u]);
+      const char* base = smem + buf * STAGE2;
+      bf16x8 a[2], bm[8];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = frag_at(base, ra[i], 4 * DY_ROW);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bm[j] = frag_at(base + DY_TILE, rb[j], 4 * X2_ROW);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bm[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  zero_output(p);
+  float* out = p.partial + int64_t(slice) * p.Cout * KC + (co0 + wco + 4 * (lane >> 4)) * KC +
+               (kt * BKC2 + wkc + (lane & 15));
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[(16 * i + r) * KC + 16 * j] = acc[i][j][r];
+}
+
+// ---------------------------------------------------------------------------
 // The same weight gradient with LDS-DMA staging (buffer_load ... lds) and
 // 64-pixel k-steps: the register path above stages every 16-byte chunk through
 // VGPRs and ds_write (the kernel's VALU and LDS-store bound: 6.4 VALU per
@@ -2264,6 +2397,16 @@ int dgrad_patch() {
   }
   return g_dgrad_patch;
 }
+int g_wgrad_wide = -1;   // register-staged weight gradient over 256-column tiles (BT_WGRAD_WIDE)
+int wgrad_wide() {
+  if (g_wgrad_wide < 0) {
+    const char* v = std::getenv("BT_WGRAD_WIDE");
+    g_wgrad_wide = v ? (std::atoi(v) ? 1 : 0) : 0;
+  }
+  return g_wgrad_wide;
+}
+// the wide kernel's layers: power-of-two Cin with whole 256-column tiles, plain dY
+bool wgrad_wide_ok(int Cin, int Cout) { return wgrad_wide() && Cin >= 16 && (Cin & (Cin - 1)) == 0 && Cout % BCO == 0; }
 int g_wgrad_pipe = -1;   // register-staged weight gradient: fragments read a step ahead (BT_WGRAD_PIPE)
 int wgrad_pipe() {
   if (g_wgrad_pipe < 0) {
@@ -2297,6 +2440,7 @@ bool c4_wave_private() {
 void conv_set_c4_wave_private(int on) { g_c4w = on < 0 ? -1 : (on ? 1 : 0); }
 
 void conv_set_dgrad_patch(int on) { g_dgrad_patch = on < 0 ? -1 : (on ? 1 : 0); }
+void conv_set_wgrad_wide(int on) { g_wgrad_wide = on < 0 ? -1 : (on ? 1 : 0); }
 void conv_set_wgrad_pipe(int on) { g_wgrad_pipe = on < 0 ? -1 : (on ? 1 : 0); }
 void conv_set_wgrad_staging(int staging) { g_wgrad_staging = staging == 0 || staging == 2 || staging == 3 ? staging : -1; }
 
@@ -2306,7 +2450,7 @@ bool conv_wgrad_supported(int Cin, int Cout) {
 
 int conv_wgrad_slices(int64_t M, int Cin, int Cout, int target_blocks) {
   if (!conv_wgrad_supported(Cin, Cout) || M <= 0) return 0;
-  const int64_t tiles = Cin == 4 ? Cout / 32 : int64_t(Cout / BCO) * (16 * Cin / BKC);
+  const int64_t tiles = Cin == 4 ? Cout / 32 : int64_t(Cout / BCO) * (16 * Cin / (wgrad_wide_ok(Cin, Cout) ? BKC2 : BKC));
   int64_t s = (target_blocks + tiles - 1) / tiles;
   const int64_t max_s = (M + BPX - 1) / BPX;
   s = s < 1 ? 1 : (s > max_s ? max_s : s);
@@ -2341,7 +2485,9 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
   if (int64_t(p.N) * p.H * p.W * p.Cin * 2 >= int64_t(kOOB) || p.M * p.Cout * 2 >= int64_t(kOOB))
     return hipErrorInvalidValue;   // 32-bit buffer offsets
   const bool c4 = p.Cin == 4;
-  const int64_t tiles = c4 ? p.Cout / 32 : int64_t(p.Cout / BCO) * (16 * p.Cin / BKC);
+  // 256-column tiles (BT_WGRAD_WIDE): the plain register-staged path only
+  const bool wide = !c4 && wgrad_wide_ok(p.Cin, p.Cout) && !p.bn_dy.y && wgrad_staging() == 0;
+  const int64_t tiles = c4 ? p.Cout / 32 : int64_t(p.Cout / BCO) * (16 * p.Cin / (wide ? BKC2 : BKC));
   const int64_t blocks = tiles * p.slices;
   if (blocks > (int64_t(1) << 31) - 1) return hipErrorInvalidValue;
   ConvWgradParams q = p;
@@ -2373,6 +2519,7 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
     conv_wgrad_dma_kernel<2><<<unsigned(grid), kThreads, 0, stream>>>(q);
   else if (wgrad_staging() == 3 && (p.Cin & (p.Cin - 1)) == 0 && p.Wo >= 32)
     conv_wgrad_dma_kernel<3><<<unsigned(grid), kThreads, 0, stream>>>(q);
+  else if (wide) conv_wgrad_wide_kernel<<<unsigned(grid), kThreads, 0, stream>>>(q);
   else if (wgrad_pipe()) conv_wgrad_kernel<false, true><<<unsigned(grid), kThreads, 0, stream>>>(q);
   else conv_wgrad_kernel<false><<<unsigned(grid), kThreads, 0, stream>>>(q);
   const int64_t total = int64_t(p.Cout) * 16 * p.Cin;   // partial elements per slice
@@ -2483,6 +2630,8 @@ int env_int(const char* name) {
   return v ? std::atoi(v) : 0;
 }
 int g_force_bm = env_int("BT_CONV_BM");
+// 128-pixel tiles unless that leaves fewer blocks than this (BT_CONV_BM64_BELOW; 512 = 2 per CU)
+int g_bm64_below = env_int("BT_CONV_BM64_BELOW") > 0 ? env_int("BT_CONV_BM64_BELOW") : 512;
 int g_force_bn = env_int("BT_CONV_BN");
 int g_dgrad_cls = env_int("BT_CONV_DGRAD_CLS");   // 1 / 4: force the data gradient's classes per block
 // first-layer forward: tiles per block of the patch kernel (0 = the im2col tap-GEMM path), output rows per tile
@@ -2526,7 +2675,7 @@ int conv_tile_pixels(int64_t M, int NOUT, int ytiles) {
   // fewer than 2 blocks per CU with 128-pixel tiles: halve the tile
   if (g_force_bm) return g_force_bm;
   const int64_t blocks = (M + FBM - 1) / FBM * (NOUT / conv_tile_channels(NOUT, false)) * ytiles;
-  return blocks < 512 ? 64 : FBM;
+  return blocks < g_bm64_below ? 64 : FBM;
 }
 
 int64_t conv_fwd_tiles(int64_t M, int NOUT) {

@@ -376,6 +376,8 @@ void conv_set_wgrad_staging(int staging);
 // Register-staged weight gradient: 1 = read the next step's fragments while this step's MFMAs run
 // (two fragment sets), 0 = one set (default), -1 = BT_WGRAD_PIPE / default.
 void conv_set_wgrad_pipe(int on);
+// Register-staged weight gradient over 256-column im2col tiles (waves of 32 x 128): 1 on, 0 off (default), -1 env.
+void conv_set_wgrad_wide(int on);
 // The 32-channel data gradient (dY 64 -> dx 32): 1 = from a dY patch (default), 0 = the tap GEMM, -1 = BT_DGRAD_PATCH.
 void conv_set_dgrad_patch(int on);
 // First-layer weight gradient: 1 = wave-private staging (default), 0 = block-shared, -1 = BT_C4_WAVE / default.

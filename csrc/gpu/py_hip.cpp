@@ -332,6 +332,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("conv_dgrad_classes_per_block", &conv_dgrad_classes_per_block);
   m.def("conv_set_wgrad_staging", &conv_set_wgrad_staging);
   m.def("conv_set_wgrad_pipe", &conv_set_wgrad_pipe);
+  m.def("conv_set_wgrad_wide", &conv_set_wgrad_wide);
   m.def("conv_set_dgrad_patch", &conv_set_dgrad_patch);
   m.def("conv_set_conv1_tiles", &conv_set_conv1_tiles, py::arg("tiles"), py::arg("rows") = 0);
   m.def("conv_set_c4_wave_private", &conv_set_c4_wave_private);

@@ -24,12 +24,15 @@ def _ref(x, dy, cout):
     return torch.nn.grad.conv2d_weight(x.float(), (cout, x.shape[1], 4, 4), dy.float(), stride=2, padding=1)
 
 
-@pytest.fixture(params=[0, 1], ids=['pipe0', 'pipe1'])
+@pytest.fixture(params=['plain', 'pipe', 'wide'])
 def wgrad_pipe(request):
-    """Register-staged weight gradient: fragments read a step ahead of the MFMAs (1) or not (0)."""
-    ops.hip_ext().conv_set_wgrad_pipe(request.param)
+    """Register-staged weight gradient: plain, fragments read a step ahead of the MFMAs
+    (pipe), or 256-column tiles (wide; layers with Cin >= 16, plain dY)."""
+    ops.hip_ext().conv_set_wgrad_pipe(1 if request.param == 'pipe' else 0)
+    ops.hip_ext().conv_set_wgrad_wide(1 if request.param == 'wide' else 0)
     yield request.param
     ops.hip_ext().conv_set_wgrad_pipe(-1)
+    ops.hip_ext().conv_set_wgrad_wide(-1)
 
 
 @pytest.fixture(params=[0, 2, 3], ids=lambda s: f'staging{s}')
