@@ -92,6 +92,8 @@ def thread_cpu():
         except OSError:
             continue
         name = st[st.index('(') + 1:st.rindex(')')]
+        if int(tid) == os.getpid():
+            name = 'main'       # the Python thread (native threads name themselves bt-*)
         rest = st[st.rindex(')') + 2:].split()
         out[int(tid)] = (name, int(rest[11]) + int(rest[12]))
     return out

@@ -1,6 +1,8 @@
 // StreamLoader implementation (see loader.h).
 #include "loader.h"
 
+#include <pthread.h>
+
 #include "../codec/tiledelta.h"
 #include "../common/trace.h"
 
@@ -128,11 +130,26 @@ StreamLoader::StreamLoader(const LoaderConfig& cfg) : cfg_(cfg) {
   for (size_t i = 0; i < cfg_.addresses.size(); ++i) socks_[i % socks_.size()]->connect(cfg_.addresses[i]);
 }
 
+namespace {
+// Completion polling grain of the worker thread while launched batches are in
+// flight (BT_LOADER_POLL_US, default 10): finer hands batches over sooner,
+// coarser costs less CPU per delivered frame.
+std::chrono::microseconds poll_grain() {
+  static const long us = [] {
+    const char* e = std::getenv("BT_LOADER_POLL_US");
+    const long v = e ? std::atol(e) : 10;
+    return v > 0 ? v : 10;
+  }();
+  return std::chrono::microseconds(us);
+}
+}  // namespace
+
 StreamLoader::~StreamLoader() { stop(); }
 
 void StreamLoader::start() {
   if (worker_.joinable()) return;
   worker_ = std::thread([this] {
+    pthread_setname_np(pthread_self(), "bt-loader");
     try {
       run();
     } catch (const std::exception& e) {
@@ -367,7 +384,7 @@ void StreamLoader::run() {
       ev = zmtp::Socket::poll(items, inflight_.empty() && pending_.empty() && unready_.empty() ? 100 : (unready_.empty() ? 1 : 0),
                               intr);
       if (!unready_.empty() && std::none_of(ev.begin(), ev.end(), [](int e) { return e != 0; }))
-        std::this_thread::sleep_for(std::chrono::microseconds(10));   // nothing to receive: poll completions
+        std::this_thread::sleep_for(poll_grain());   // nothing to receive: poll completions
     } catch (const zmtp::Error& e) {
       if (e.code == zmtp::E_INTR) break;
       throw;
@@ -753,7 +770,7 @@ void StreamLoader::launch() {
         // the consumer is most likely waiting for one of these: keep
         // promoting at a fine grain instead of sleeping through a post
         lk.unlock();
-        std::this_thread::sleep_for(std::chrono::microseconds(10));
+        std::this_thread::sleep_for(poll_grain());
         lk.lock();
         continue;
       }

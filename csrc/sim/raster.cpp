@@ -29,10 +29,12 @@ inline double dot(const Vec3& a, const Vec3& b) { return a.x * b.x + a.y * b.y +
 // linear radiance -> display 8 bit (power 1/2.2), 4096-entry table over [0,1]
 struct ToneLut {
   uint8_t v[4097];
+  uint32_t gray4[4097];   // v[i] in R, G and B, alpha 255: one load per pixel of a grey box
   ToneLut() {
     for (int i = 0; i <= 4096; ++i) {
       double x = i / 4096.0;
       v[i] = uint8_t(std::min(255.0, std::floor(255.0 * std::pow(x, 1.0 / 2.2) + 0.5)));
+      gray4[i] = uint32_t(v[i]) * 0x010101u | 0xff000000u;
     }
   }
   inline uint8_t operator()(double x) const {
@@ -297,16 +299,25 @@ void Renderer::render(const Scene& s, uint8_t* out, DirtyRect* dirty) {
   if (dirty && dirty->known) {
     // only the previous frame's boxes and shadows differ from the background
     if (!dirty->empty()) {
-      const size_t off = size_t(dirty->x0) * C, n = size_t(dirty->x1 - dirty->x0 + 1) * C;
+      const bool rows = dirty->lo.size() == size_t(H);
       for (int y = dirty->y0; y <= dirty->y1; ++y) {
+        const int a = rows ? dirty->lo[size_t(y)] : dirty->x0, b = rows ? dirty->hi[size_t(y)] : dirty->x1;
+        if (a > b) continue;
         uint8_t* r = row_ptr(y);
-        std::memcpy(r + off, background_.data() + (r - out) + off, n);
+        const size_t off = size_t(a) * C;
+        std::memcpy(r + off, background_.data() + (r - out) + off, size_t(b - a + 1) * C);
       }
     }
   } else {
     std::memcpy(out, background_.data(), background_.size());
   }
   DirtyRect touched;
+  if (dirty) {   // reuse the previous record's row arrays (no allocation per frame)
+    touched.lo.swap(dirty->lo);
+    touched.hi.swap(dirty->hi);
+    touched.lo.assign(size_t(H), 1 << 30);
+    touched.hi.assign(size_t(H), -1);
+  }
 
   // ---- shadows: each box's shadow hull on the ground plane, projected to
   // the image (a projective map keeps it convex) and span-filled ----
@@ -404,6 +415,8 @@ void Renderer::render(const Scene& s, uint8_t* out, DirtyRect* dirty) {
           inten[i] = amb + e;
         }
         if (!vis) continue;
+        // grey albedo (the Cube scene's): the three channels share one table index
+        const bool gray = b.albedo[0] == b.albedo[1] && b.albedo[1] == b.albedo[2];
         const float a0 = b.albedo[0] * 4096.f, a1 = b.albedo[1] * 4096.f, a2 = b.albedo[2] * 4096.f;
         static const int tri[2][3] = {{0, 1, 2}, {0, 2, 3}};
         for (const auto& t : tri) {
@@ -436,6 +449,7 @@ void Renderer::render(const Scene& s, uint8_t* out, DirtyRect* dirty) {
                 const __m128 I = _mm_add_ps(vI0, _mm_mul_ps(vdI, kv));
                 _mm_store_si128(reinterpret_cast<__m128i*>(i0 + k),
                                 _mm_cvttps_epi32(_mm_min_ps(_mm_max_ps(_mm_mul_ps(va0, I), lo), hi)));
+                if (gray) continue;
                 _mm_store_si128(reinterpret_cast<__m128i*>(i1 + k),
                                 _mm_cvttps_epi32(_mm_min_ps(_mm_max_ps(_mm_mul_ps(va1, I), lo), hi)));
                 _mm_store_si128(reinterpret_cast<__m128i*>(i2 + k),
@@ -448,14 +462,19 @@ void Renderer::render(const Scene& s, uint8_t* out, DirtyRect* dirty) {
                   const float Z = Z0 + dZ * (kb + float(k));
                   if (Z <= zr[k]) continue;
                   zr[k] = Z;
-                  p[0] = T.v[i0[k]], p[1] = T.v[i1[k]], p[2] = T.v[i2[k]];
+                  if (gray) p[0] = p[1] = p[2] = T.v[i0[k]];
+                  else p[0] = T.v[i0[k]], p[1] = T.v[i1[k]], p[2] = T.v[i2[k]];
                 }
+              } else if (C == 4 && gray) {
+                for (int k = 0; k < n; ++k) std::memcpy(p + size_t(k) * 4, &T.gray4[i0[k]], 4);
               } else if (C == 4) {
                 for (int k = 0; k < n; ++k) {
                   const uint32_t v = uint32_t(T.v[i0[k]]) | uint32_t(T.v[i1[k]]) << 8 |
                                      uint32_t(T.v[i2[k]]) << 16 | 0xff000000u;
                   std::memcpy(p + size_t(k) * 4, &v, 4);
                 }
+              } else if (gray) {
+                for (int k = 0; k < n; ++k, p += C) p[0] = p[1] = p[2] = T.v[i0[k]];
               } else {
                 for (int k = 0; k < n; ++k, p += C) p[0] = T.v[i0[k]], p[1] = T.v[i1[k]], p[2] = T.v[i2[k]];
               }
@@ -467,7 +486,7 @@ void Renderer::render(const Scene& s, uint8_t* out, DirtyRect* dirty) {
   }
   if (dirty) {
     touched.known = true;
-    *dirty = touched;
+    *dirty = std::move(touched);
   }
 }
 

@@ -83,14 +83,23 @@ Scene falling_cubes_scene();
 // frame left; the next render restores the background inside it only,
 // instead of copying the whole background.  `known` false = the buffer's
 // content is unknown (fresh slot): full background copy.
+// With `lo` / `hi` sized to the image height, each row also keeps the span
+// it wrote (a box and its shadow cover ~57 % of their bounding rectangle, so
+// a restore over the row spans moves that much less memory).
 struct DirtyRect {
   int x0 = 1 << 30, y0 = 1 << 30, x1 = -1, y1 = -1;
   bool known = false;
+  std::vector<int> lo, hi;   // per image row [lo, hi]; empty = rectangle only
   bool empty() const { return x1 < x0 || y1 < y0; }
   void reset() { x0 = y0 = 1 << 30, x1 = y1 = -1; }
   void add(int y, int a, int b) {
     y0 = y < y0 ? y : y0, y1 = y > y1 ? y : y1;
     x0 = a < x0 ? a : x0, x1 = b > x1 ? b : x1;
+    if (!lo.empty()) {
+      int& l = lo[static_cast<unsigned>(y)];
+      int& h = hi[static_cast<unsigned>(y)];
+      l = a < l ? a : l, h = b > h ? b : h;
+    }
   }
 };
 
