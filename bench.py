@@ -560,10 +560,16 @@ def main(argv=None):
             per['total'] = round(cpu['cgroup_usage_usec'] / max(1, node_frames), 2)
             per['producers'] = round(per['total'] - per['consumer'], 2)
         cpu['us_per_frame'] = per
+        if snap1.get('cpu_recv_ms'):
+            # BT_LOADER_CPU=1: the loader worker's thread CPU per loop stage, per frame
+            cpu['loader_us_per_frame'] = {k[4:-3]: round((snap1[k] - snap0.get(k, 0)) * 1e3 / max(1, frames_here), 2)
+                                          for k in ('cpu_poll_ms', 'cpu_recv_ms', 'cpu_launch_ms', 'cpu_reap_ms')}
         if th0 is not None:
             # (diagnostic) this process's busiest threads over the timed region
             th1 = thread_cpu()
-            busy = sorted(((th1[t][1] - th0.get(t, ('', 0))[1], th1[t][0]) for t in th1), reverse=True)
+            wt = snap1.get('worker_tid')
+            name = {t: ('bt-loader(worker)' if t == wt else th1[t][0]) for t in th1}
+            busy = sorted(((th1[t][1] - th0.get(t, ('', 0))[1], name[t]) for t in th1), reverse=True)
             cpu['threads_cpu_s'] = [[name, round(d / os.sysconf('SC_CLK_TCK'), 3)] for d, name in busy[:12] if d > 0]
         shape = tuple(img.shape)
         if args.dist == 'scatter':

@@ -2,11 +2,15 @@
 #include "loader.h"
 
 #include <pthread.h>
+#include <sys/syscall.h>
+#include <time.h>
+#include <unistd.h>
 
 #include "../codec/tiledelta.h"
 #include "../common/trace.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <chrono>
 #include <cstring>
 #include <stdexcept>
@@ -131,6 +135,30 @@ StreamLoader::StreamLoader(const LoaderConfig& cfg) : cfg_(cfg) {
 }
 
 namespace {
+uint64_t thread_cpu_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return uint64_t(ts.tv_sec) * 1000000000ull + uint64_t(ts.tv_nsec);
+}
+// BT_LOADER_CPU=1: the worker accounts its thread CPU per loop stage (the
+// thread clock is a system call, ~0.3 us, a few per loop turn: off by default)
+bool cpu_accounting() {
+  static const bool on = [] {
+    const char* e = std::getenv("BT_LOADER_CPU");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+// adds the calling thread's CPU time over its scope to one counter
+struct CpuScope {
+  std::atomic<uint64_t>& acc;
+  const bool on = cpu_accounting();
+  const uint64_t t0 = on ? thread_cpu_ns() : 0;
+  explicit CpuScope(std::atomic<uint64_t>& a) : acc(a) {}
+  ~CpuScope() {
+    if (on) acc.fetch_add(thread_cpu_ns() - t0, std::memory_order_relaxed);
+  }
+};
 // Completion polling grain of the worker thread while launched batches are in
 // flight (BT_LOADER_POLL_US, default 10): finer hands batches over sooner,
 // coarser costs less CPU per delivered frame.
@@ -150,6 +178,7 @@ void StreamLoader::start() {
   if (worker_.joinable()) return;
   worker_ = std::thread([this] {
     pthread_setname_np(pthread_self(), "bt-loader");
+    worker_tid_ = int64_t(syscall(SYS_gettid));
     try {
       run();
     } catch (const std::exception& e) {
@@ -346,6 +375,11 @@ void StreamLoader::drain_sockets() {
 LoaderStats StreamLoader::stats() {
   std::lock_guard<std::mutex> lk(mu_);
   LoaderStats s = stats_;
+  s.cpu_poll_ms = double(cpu_ns_[kCpuPoll].load()) * 1e-6;
+  s.cpu_recv_ms = double(cpu_ns_[kCpuRecv].load()) * 1e-6;
+  s.cpu_launch_ms = double(cpu_ns_[kCpuLaunch].load()) * 1e-6;
+  s.cpu_reap_ms = double(cpu_ns_[kCpuReap].load()) * 1e-6;
+  s.worker_tid = worker_tid_.load();
   s.pool_fallbacks = pool_ ? pool_->fallbacks() : 0;
   s.ring_slots = s.ring_published = s.ring_held = 0;
   for (const shm::Segment* g : seg_list_) {
@@ -373,11 +407,15 @@ void StreamLoader::run() {
   const int64_t max_frames = cfg_.max_batches < 0 ? -1 : cfg_.max_batches * cfg_.batch_size;
   int64_t taken = 0;
   while (!stop_) {
-    promote_ready();
-    reap();
+    {
+      CpuScope cs(cpu_ns_[kCpuReap]);
+      promote_ready();
+      reap();
+    }
     if (max_frames >= 0 && taken >= max_frames) break;
     std::vector<int> ev;
     try {
+      CpuScope cs(cpu_ns_[kCpuPoll]);
       // with copies in flight, wake up often enough to recycle their slots
       // promptly (producers / IO threads may be waiting for them)
       trace::Range tp("btn.loader.poll");
@@ -389,6 +427,7 @@ void StreamLoader::run() {
       if (e.code == zmtp::E_INTR) break;
       throw;
     }
+    CpuScope cs(cpu_ns_[kCpuRecv]);
     flush_pending(max_frames >= 0 && taken >= max_frames);
     for (size_t i = 0; i < ev.size() && !stop_; ++i) {
       if (!(ev[i] & zmtp::POLLIN)) continue;
@@ -839,6 +878,7 @@ void StreamLoader::flush_pending(bool force) {
 
 void StreamLoader::launch_group(std::vector<Pending>& group) {
   trace::Range tr("btn.loader.launch");
+  CpuScope cpu(cpu_ns_[kCpuLaunch]);
   const double t_issue = now_ms();
   const bool direct = group.front().direct;
   int total = 0;

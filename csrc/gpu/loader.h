@@ -193,6 +193,12 @@ struct LoaderStats {
   uint64_t ring_slots = 0, ring_published = 0, ring_held = 0;
   uint64_t passthrough_batches = 0;        // copy path, identity decode: DMA only, no kernel
   std::map<int64_t, uint64_t> frames_per_btid;   // provenance: frames per producer id
+  // worker-thread CPU (thread clock, ms) per stage of its loop -- where the
+  // consumer process's CPU per delivered frame goes: socket poll, receive +
+  // descriptor parse + batch assembly, decode launches (a subset of the
+  // previous), completion checks (reap + promote)
+  double cpu_poll_ms = 0, cpu_recv_ms = 0, cpu_launch_ms = 0, cpu_reap_ms = 0;
+  int64_t worker_tid = 0;
 };
 
 class StreamLoader {
@@ -260,6 +266,10 @@ class StreamLoader {
   std::shared_ptr<PinnedPool> pool_;
   std::thread worker_;
   std::atomic<bool> stop_{false};
+  // LoaderStats::cpu_*_ms, in ns (written by the worker, read by stats())
+  enum CpuStage { kCpuPoll, kCpuRecv, kCpuLaunch, kCpuReap, kCpuStages };
+  std::atomic<uint64_t> cpu_ns_[kCpuStages] = {};
+  std::atomic<int64_t> worker_tid_{0};
 
   std::mutex mu_;
   std::condition_variable cv_;

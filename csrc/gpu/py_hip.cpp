@@ -1050,6 +1050,11 @@ PYBIND11_MODULE(_hip, m) {
         d["ring_slots"] = s.ring_slots;
         d["ring_published"] = s.ring_published;
         d["ring_held"] = s.ring_held;
+        d["cpu_poll_ms"] = s.cpu_poll_ms;
+        d["cpu_recv_ms"] = s.cpu_recv_ms;
+        d["cpu_launch_ms"] = s.cpu_launch_ms;
+        d["cpu_reap_ms"] = s.cpu_reap_ms;
+        d["worker_tid"] = s.worker_tid;
         py::dict per;
         for (const auto& kv : s.frames_per_btid) per[py::int_(kv.first)] = kv.second;
         d["frames_per_btid"] = per;
