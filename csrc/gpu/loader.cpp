@@ -730,6 +730,16 @@ StreamLoader::MappedSegment& StreamLoader::segment(const std::string& name) {
 void StreamLoader::reap(bool wait_all) {
   // drop the frames of batches whose H2D copies completed: their pinned
   // slots return to the pool (and unblock an IO thread waiting for one)
+  // (diagnostic BT_LOADER_REAP_US: at most one completion query per interval)
+  static const long reap_us = [] {
+    const char* e = std::getenv("BT_LOADER_REAP_US");
+    return e ? std::atol(e) : 0L;
+  }();
+  if (reap_us > 0 && !wait_all && !inflight_.empty()) {
+    const double t = now_ms();
+    if (t - last_reap_ms_ < reap_us * 1e-3) return;
+    last_reap_ms_ = t;
+  }
   while (!inflight_.empty()) {
     Inflight& f = inflight_.front();
     if (wait_all) f.copied->wait();

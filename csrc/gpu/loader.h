@@ -293,6 +293,7 @@ class StreamLoader {
   static constexpr int kTimedSkip = 8;         // cold launches never sampled
   static constexpr int64_t kKeyIdleLaunches = 64;
   int64_t launch_no_ = 0, retired_launch_ = 0;
+  double last_reap_ms_ = 0;
   std::vector<hipStream_t> copy_streams_;      // copy path fan-out (cfg_.copy_streams > 1)
   std::vector<hipEvent_t> copy_done_;          // one per copy stream, reused
   std::vector<hipEvent_t> stage_free_;         // per staging buffer: last kernel reading it
