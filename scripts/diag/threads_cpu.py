@@ -40,31 +40,36 @@ def idle(label, secs=1.0, worker=None):
     report(label, a, threads(), time.perf_counter() - t, worker)
 
 
-dev = torch.device('cuda', 0)
-torch.ones(8, device=dev).sum().item()
-idle('torch idle')
-dec = ops.DecodeConfig.unit(channels='rgba', gamma=2.2)
-probe = DeviceLoader(['tcp://127.0.0.1:9'], batch_size=8, device=dev, decode=dec)
-ld = probe._make()
-ld.start()
-time.sleep(0.3)
-idle('loader started, no producer', worker=ld.stats().get('worker_tid'))
-ld.stop()
-idle('loader stopped')
-port = 24000 + os.getpid() % 1000
-with btt.BlenderLauncher(producer='cubesim', num_instances=4, named_sockets=['DATA'], start_port=port,
-                         instance_args=[['--mode', 'rgba', '--shm', '64']] * 4) as bl:
-    dl = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=8, device=dev, decode=dec, timeoutms=60000)
-    it = iter(dl)
-    for _ in range(50):
-        next(it)
-    torch.cuda.synchronize()
-    a, t = threads(), time.perf_counter()
-    for _ in range(1000):
-        next(it)
-    torch.cuda.synchronize()
-    wt = dl._live.stats().get('worker_tid')
-    report('streaming 1000 batches', a, threads(), time.perf_counter() - t, wt)
-    idle('stream paused (loader alive, buffers full)', worker=wt)
-    it.close()
-    idle('after close')
+def main():
+    dev = torch.device('cuda', 0)
+    torch.ones(8, device=dev).sum().item()
+    idle('torch idle')
+    dec = ops.DecodeConfig.unit(channels='rgba', gamma=2.2)
+    probe = DeviceLoader(['tcp://127.0.0.1:9'], batch_size=8, device=dev, decode=dec)
+    ld = probe._make()
+    ld.start()
+    time.sleep(0.3)
+    idle('loader started, no producer', worker=ld.stats().get('worker_tid'))
+    ld.stop()
+    idle('loader stopped')
+    port = 24000 + os.getpid() % 1000
+    with btt.BlenderLauncher(producer='cubesim', num_instances=4, named_sockets=['DATA'], start_port=port,
+                             instance_args=[['--mode', 'rgba', '--shm', '64']] * 4) as bl:
+        dl = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=8, device=dev, decode=dec, timeoutms=60000)
+        it = iter(dl)
+        for _ in range(50):
+            next(it)
+        torch.cuda.synchronize()
+        a, t = threads(), time.perf_counter()
+        for _ in range(1000):
+            next(it)
+        torch.cuda.synchronize()
+        wt = dl._live.stats().get('worker_tid')
+        report('streaming 1000 batches', a, threads(), time.perf_counter() - t, wt)
+        idle('stream paused (loader alive, buffers full)', worker=wt)
+        it.close()
+        idle('after close')
+
+
+if __name__ == '__main__':
+    main()
