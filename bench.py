@@ -148,7 +148,7 @@ def parse_args(argv=None):
                          'disturbs its step least: 9.72k vs 9.59k img/s, profiles/r2/host_sync.txt)')
     ap.add_argument('--prefetch', type=int, default=None,
                     help='output buffers posted to the loader (batches assembled/decoding/ready ahead of the consumer); '
-                         'default 6.  Deeper queues coalesce larger decode launches (8: +0.7 %%, 16: +1-2 %% on '
+                         'default 8 (host-ordered hand-off, profiles/r4/cpu_per_frame.md), 6 for the disc consumer.  Deeper queues coalesce larger decode launches (8: +0.7 %%, 16: +1-2 %% on '
                          'long runs), but a short timed window then ends with more in-flight decode work inside '
                          'its closing device sync (20 steps, 8: 37.9k, 16: 34k vs 40.0k img/s); '
                          'profiles/r2/loader_depth_ab.txt')
@@ -159,7 +159,8 @@ def parse_args(argv=None):
     ap.add_argument('--start-port', type=int, default=0)
     ap.add_argument('--host-sync', choices=['auto', 'on', 'off'], default='auto',
                     help='loader/consumer ordering by host-side event checks (on) or cross-stream waits (off); '
-                         'auto = on for the DMA copy path (--h2d copy, the disc consumer), off for the direct path')
+                         'auto = on (a stream of cross-stream waits keeps a HIP runtime thread busy: 43 -> 20 '
+                         'consumer CPU-us per frame, profiles/r4/cpu_per_frame.md)')
     ap.add_argument('--dma-phase', choices=['start', 'mid'], default='start',
                     help='disc consumer: when the next frames\' host->device DMA may start -- start = when the '
                          'step begins (overlapping the memory-bound forward); mid = between the forward and the '
@@ -206,7 +207,7 @@ def parse_args(argv=None):
     if args.h2d is None:
         args.h2d = 'copy' if args.consumer == 'disc' else 'auto'
     if args.prefetch is None:
-        args.prefetch = 6
+        args.prefetch = 6 if args.consumer == 'disc' else 8
     return args
 
 

@@ -89,14 +89,16 @@ class DeviceLoader:
         Log :meth:`metrics` on the ``'blendtorch'`` logger every that many
         seconds while iterating.
     host_sync: bool, optional
-        (default: True for ``h2d='copy'``, False otherwise.)
+        (default: True.)
         Order the loader against the consumer on the host (event queries)
         rather than with cross-stream waits: a posted buffer is written once
         its post event has completed, and a batch is handed out once its
         copies/kernel have completed -- the consumer's stream never waits on
         the loader's.  ROCm's hipStreamWaitEvent costs 28-430 us of host time
-        per call (profiles/r2/hip_api_cost.json); False restores the
-        GPU-side waits.
+        per call (profiles/r2/hip_api_cost.json), and a stream of
+        cross-stream waits keeps a HIP runtime thread busy for a whole core
+        (profiles/r4/cpu_per_frame.md: 23 of the consumer's 43 CPU-us per
+        frame); False restores the GPU-side waits.
     defer_post: bool
         Hand the loader a fresh output buffer only when the consumer calls
         :meth:`release` (or, failing that, when it asks for the next batch)
@@ -148,11 +150,11 @@ class DeviceLoader:
         self._t_start = self._t_end = None
         self._wait_s = 0.0
         self.defer_post = bool(defer_post)
-        # default: host ordering for the DMA path (where the consumer's step
-        # and the copies overlap), GPU-side waits for the direct path (its
-        # decode kernel is the batch's last device work; measured 42.0k vs
-        # 38.7k img/s with host ordering)
-        self.host_sync = (h2d == 'copy') if host_sync is None else bool(host_sync)
+        # default: host ordering on both paths.  (Round 2 measured the direct
+        # path 42.0k vs 38.7k img/s with GPU-side waits; with 8 posted buffers
+        # the two are level, 42.1-42.3k, and host ordering halves the
+        # consumer process's CPU per frame: profiles/r4/cpu_per_frame.md)
+        self.host_sync = True if host_sync is None else bool(host_sync)
         self._owed = 0             # deferred posts not yet made
         self._post_fn = None
         # reuse_buffers: output tensors come from a fixed ring of prefetch + 2,

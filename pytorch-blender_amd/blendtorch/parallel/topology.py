@@ -106,12 +106,13 @@ def current_allowed_cpus() -> List[int]:
 
 
 # Measured CPU cost per delivered 640x480 RGBA frame on the headline path
-# (bench.py, 8 cubesim producers -> shm ring -> zero-copy decode, one MI355X;
-# profiles/r3/final/bench_headline.log: 2.31 s of cgroup CPU for 16,000 frames,
-# 0.71 s of it in the consumer process).  bench.py reports the current values
-# as ``cpu_us_per_frame`` on every run.
-PRODUCER_US_PER_FRAME = 100.0
-CONSUMER_US_PER_FRAME = 44.0
+# (bench.py, cubesim producers -> shm ring -> zero-copy decode, one MI355X;
+# profiles/r4/cpu_per_frame.md: 62-67 us in the producers -- render with
+# per-row dirty spans, 45 us of it -- and 19-21 us in the consumer process
+# with the host-ordered loader hand-off; round 3 measured 100 + 44).
+# bench.py reports the current values as ``cpu.us_per_frame`` on every run.
+PRODUCER_US_PER_FRAME = 65.0
+CONSUMER_US_PER_FRAME = 20.0
 # host->device read ceiling of one MI355X PCIe link (profiles/direct_host_read.md)
 LINK_GBYTES_PER_S = 51.5
 
@@ -149,7 +150,7 @@ def plan_rank_resources(rank: int, local_rank: int, local_world: int, world: int
       per-core pinning isolates anything, i.e. ``pin``);
     * ``producers``: producer processes this rank launches -- ``producers`` if
       given, else what the measured per-frame CPU costs justify on the rank's
-      CPU share (:func:`producers_for_share`: 7 on 16 CPUs, where the PCIe
+      CPU share (:func:`producers_for_share`: 5 on 16 CPUs, where the PCIe
       link is the bound; 2 on the 2 CPUs a rank gets when 8 ranks share a
       16-CPU quota, where the CPU is).  Scatter mode spreads 8 producers over
       all ranks (the root's PCIe link is the bound);

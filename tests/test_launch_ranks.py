@@ -126,20 +126,23 @@ def test_eight_rank_plan_pinned_quota():
     """Pinned producers (the quota covers most of the affinity mask): every
     producer gets one core of its own rank's slice."""
     from blendtorch.parallel import plan_rank_resources
+    from blendtorch.parallel.topology import producers_for_share
     plans = [plan_rank_resources(r, r, 8, 8, list(range(64)), budget=64, pin=True, bus_ids=[None] * 8,
                                  sysfs=Path('/nonexistent')) for r in range(8)]
     for p in plans:
         # 8 CPUs per rank: the link, not the CPU, is the bound (producers_for_share)
-        assert p['producers'] == 7 and all(len(a) == 1 and a[0] in p['cpus'] for a in p['affinity'])
+        assert p['producers'] == producers_for_share(8) and all(len(a) == 1 and a[0] in p['cpus']
+                                                                for a in p['affinity'])
 
 
 def test_eight_ranks_under_16_cpu_quota_get_cost_justified_producers(tmp_path):
     """8 ranks under a 16-CPU quota (2 CPUs each): at the measured costs of
-    ~100 us of producer CPU and ~44 us of consumer-process CPU per frame a
-    rank sustains 2e6 / 144 = 13.9k frames/s, for which its producers need
-    1.39 cores: 2 producers each (the old ``share - 3`` rule gave 1, i.e.
-    ~12k frames/s per rank, README round 3).  One rank with all 16 CPUs is
-    link-bound (42k RGBA frames/s need 4.2 producer cores): 7 with margin."""
+    ~65 us of producer CPU and ~20 us of consumer-process CPU per frame
+    (profiles/r4/cpu_per_frame.md) a rank sustains 2e6 / 85 = 23.5k
+    frames/s, for which its producers need 1.53 cores: 2 producers each (the
+    round-2 ``share - 3`` rule gave 1, i.e. ~12k frames/s per rank).  One
+    rank with all 16 CPUs is link-bound (42k RGBA frames/s need 2.7
+    producer cores): 5 with the 1.5x margin."""
     from blendtorch.parallel import plan_rank_resources
     from blendtorch.parallel.topology import producers_for_share, CONSUMER_US_PER_FRAME, PRODUCER_US_PER_FRAME
     frame = 640 * 480 * 4
@@ -151,7 +154,7 @@ def test_eight_ranks_under_16_cpu_quota_get_cost_justified_producers(tmp_path):
     assert want == 2 and all(p['producers'] == want for p in plans)
     one = plan_rank_resources(0, 0, 1, 1, list(range(16)), budget=16, pin=True, shm_slots=48,
                               shm_free_bytes=64 << 30, frame_bytes=frame, bus_ids=[None], sysfs=tmp_path)
-    assert one['producers'] == 7
+    assert one['producers'] == 5
     # more CPU per frame in the consumer leaves fewer cores to producers
     assert producers_for_share(2, frame, consumer_us=150.0) == 1
 
