@@ -140,6 +140,21 @@ uint64_t thread_cpu_ns() {
   clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
   return uint64_t(ts.tv_sec) * 1000000000ull + uint64_t(ts.tv_nsec);
 }
+// Host-ordered hand-off (host_sync): with BT_LOADER_BLOCKING=1 the events
+// that mark a batch's device work are blocking-sync events, and a worker that
+// cannot go on until the oldest launched batch completes (every posted
+// buffer in use) sleeps in hipEventSynchronize instead of polling it every
+// few microseconds.
+bool blocking_waits() {
+  static const bool on = [] {
+    const char* e = std::getenv("BT_LOADER_BLOCKING");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+unsigned completion_event_flags() {
+  return hipEventDisableTiming | (blocking_waits() ? hipEventBlockingSync : 0u);
+}
 // BT_LOADER_CPU=1: the worker accounts its thread CPU per loop stage (the
 // thread clock is a system call, ~0.3 us, a few per loop turn: off by default)
 bool cpu_accounting() {
@@ -435,12 +450,7 @@ void StreamLoader::run() {
       for (int n = 0; n < 64 && !stop_; ++n) {
         if (max_frames >= 0 && taken >= max_frames) break;
         zmtp::Message m;
-        try {
-          m = socks_[i]->recv(zmtp::DONTWAIT);
-        } catch (const zmtp::Error& e) {
-          if (e.code == zmtp::E_AGAIN) break;
-          throw;
-        }
+        if (!socks_[i]->try_recv(m)) break;
         if (process(std::move(m))) ++taken;
       }
     }
@@ -818,8 +828,10 @@ void StreamLoader::launch() {
       if (!unready_.empty()) {
         // the consumer is most likely waiting for one of these: keep
         // promoting at a fine grain instead of sleeping through a post
+        // (blocking: sleep until the oldest completes, then promote it)
         lk.unlock();
-        std::this_thread::sleep_for(poll_grain());
+        if (blocking_waits()) unready_.front().pending->wait();
+        else std::this_thread::sleep_for(poll_grain());
         lk.lock();
         continue;
       }
@@ -930,7 +942,7 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
   auto copied = std::make_shared<EventSet>();
   auto add_event = [&](hipStream_t st) {
     hipEvent_t ev;
-    check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate(copied)");
+    check(hipEventCreateWithFlags(&ev, completion_event_flags()), "hipEventCreate(copied)");
     check(hipEventRecord(ev, st), "hipEventRecord(copied)");
     copied->ev.push_back(ev);
   };
@@ -1100,7 +1112,7 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
     } else if (cfg_.host_sync) {
       auto fin = std::make_shared<EventSet>();
       hipEvent_t ev;
-      check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate(done)");
+      check(hipEventCreateWithFlags(&ev, completion_event_flags()), "hipEventCreate(done)");
       check(hipEventRecord(ev, stream_), "hipEventRecord(done)");
       fin->ev.push_back(ev);
       rb.pending = fin;

@@ -1470,6 +1470,15 @@ Message Socket::recv(int flags, const Interrupt& intr) {
   }
 }
 
+bool Socket::try_recv(Message& out) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (closing_) throw Error(E_TERM, "socket closed");
+  if (type_ == PUSH) throw Error(E_INVAL, "PUSH sockets cannot recv");
+  if (type_ == REQ && !req_expect_reply_) throw Error(E_FSM, "REQ: must send before recv");
+  if (type_ == REP && rep_replying_) throw Error(E_FSM, "REP: must send reply before next recv");
+  return try_recv_locked(out);
+}
+
 void Socket::wait_slice(std::unique_lock<std::mutex>& lk, const Clock::time_point* deadline,
                         const Interrupt& intr) {
   auto until = Clock::now() + std::chrono::milliseconds(intr ? 100 : 1000);
