@@ -79,7 +79,32 @@ def idle():
     time.sleep(1e-3)
 
 
+# a captured graph of 20 small kernels, replayed like the disc consumer's step
+gs = torch.cuda.Stream(dev)
+gs.wait_stream(torch.cuda.current_stream())
+with torch.cuda.stream(gs):
+    for _ in range(3):
+        for _ in range(20):
+            a.add_(1.0)
+torch.cuda.current_stream().wait_stream(gs)
+graph = torch.cuda.CUDAGraph()
+with torch.cuda.graph(graph):
+    for _ in range(20):
+        a.add_(1.0)
+
+
+def graph_replay():
+    graph.replay()
+    time.sleep(200e-6)
+
+
+def graph_replay_sync():
+    graph.replay()
+    torch.cuda.current_stream().synchronize()
+
+
 for label, body in [('idle', idle), ('kernels', kernels), ('event record+destroy while pending', ev_destroy_pending),
                     ('event reuse', ev_reuse), ('cross-stream wait', ev_wait_cross), ('event query poll', ev_query),
+                    ('graph replay', graph_replay), ('graph replay + stream sync', graph_replay_sync),
                     ('idle again', idle)]:
     phase(label, body)
