@@ -493,9 +493,15 @@ int bn_grid(int64_t work) {   // work = 16-byte vectors; kBnUnroll per lane per 
 
 // apply launches that fold their accumulator: every block reads the 16 KB of
 // replicas once, so fewer, longer-running blocks (4 per CU)
+// (BT_BN_FOLD_GRID: the cap, default 1024)
 int bn_fold_grid(int64_t work) {
+  static const int cap = [] {
+    const char* e = std::getenv("BT_BN_FOLD_GRID");
+    const int v = e ? std::atoi(e) : 1024;
+    return v > 0 ? v : 1024;
+  }();
   const int g = bn_grid(work);
-  return g < 1024 ? g : 1024;
+  return g < cap ? g : cap;
 }
 }  // namespace
 
