@@ -493,15 +493,24 @@ int bn_grid(int64_t work) {   // work = 16-byte vectors; kBnUnroll per lane per 
 
 // apply launches that fold their accumulator: every block reads the 16 KB of
 // replicas once, so fewer, longer-running blocks (4 per CU)
-// (BT_BN_FOLD_GRID: the cap, default 1024)
+// (BT_BN_FOLD_GRID: the cap, default 1024; BT_BN_FOLD_BALANCE=1: the grid
+// divides the passes evenly -- a cap of 1024 left 1.17 passes per block on a
+// 1200-block tensor, i.e. 2 passes for some blocks and 1 for the rest)
 int bn_fold_grid(int64_t work) {
   static const int cap = [] {
     const char* e = std::getenv("BT_BN_FOLD_GRID");
     const int v = e ? std::atoi(e) : 1024;
     return v > 0 ? v : 1024;
   }();
+  static const bool balance = [] {
+    const char* e = std::getenv("BT_BN_FOLD_BALANCE");
+    return e && e[0] == '1';
+  }();
   const int g = bn_grid(work);
-  return g < cap ? g : cap;
+  if (g <= cap) return g;
+  if (!balance) return cap;
+  const int passes = (g + cap - 1) / cap;
+  return (g + passes - 1) / passes;
 }
 }  // namespace
 
