@@ -492,19 +492,21 @@ int bn_grid(int64_t work) {   // work = 16-byte vectors; kBnUnroll per lane per 
 }
 
 // apply launches that fold their accumulator: every block reads the 16 KB of
-// replicas once, so fewer, longer-running blocks (4 per CU)
-// (BT_BN_FOLD_GRID: the cap, default 1024; BT_BN_FOLD_BALANCE=1: the grid
-// divides the passes evenly -- a cap of 1024 left 1.17 passes per block on a
-// 1200-block tensor, i.e. 2 passes for some blocks and 1 for the rest)
+// replicas once, so fewer, longer-running blocks -- at most 512 (2 per CU),
+// sized so every block runs the same number of passes (a cap of 1024 left
+// 1.17 passes per block on the 1200-block second layer, i.e. 2 passes for
+// some blocks and 1 for the rest).  Disc step: 18.8k -> 19.1-19.3k img/s,
+// forward applies 42.2 -> 37.3 us (profiles/r4/b33/).  BT_BN_FOLD_GRID: the
+// cap; BT_BN_FOLD_BALANCE=0: plain capping.
 int bn_fold_grid(int64_t work) {
   static const int cap = [] {
     const char* e = std::getenv("BT_BN_FOLD_GRID");
-    const int v = e ? std::atoi(e) : 1024;
-    return v > 0 ? v : 1024;
+    const int v = e ? std::atoi(e) : 512;
+    return v > 0 ? v : 512;
   }();
   static const bool balance = [] {
     const char* e = std::getenv("BT_BN_FOLD_BALANCE");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   const int g = bn_grid(work);
   if (g <= cap) return g;
