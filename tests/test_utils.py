@@ -40,6 +40,32 @@ def test_meter_rates():
     assert d['frames'] == 10 and d['frames_per_s'] > 0 and d['recv_ms_avg'] >= 0
 
 
+def test_trace_range_is_a_shared_no_op_unless_enabled(monkeypatch):
+    """The per-batch loops call trace_range: without BLENDTORCH_ROCTX=1 (or
+    without a GPU) it must hand back one shared no-op context, not build a
+    generator and push roctx ranges (~6 us per call)."""
+    import blendtorch.utils as u
+    monkeypatch.delenv('BLENDTORCH_ROCTX', raising=False)
+    monkeypatch.setattr(u, '_roctx_on', None)
+    a, b = u.trace_range('x'), u.trace_range('y')
+    assert a is b
+    with a:
+        pass
+    monkeypatch.setenv('BLENDTORCH_ROCTX', '1')
+    monkeypatch.setattr(u, '_roctx_on', None)
+    assert (u.trace_range('x') is a) == (not torch.cuda.is_available())
+
+
+def test_bench_thread_report_names_the_python_thread():
+    import importlib.util
+    from pathlib import Path
+    spec = importlib.util.spec_from_file_location('bench_mod', Path(__file__).resolve().parents[1] / 'bench.py')
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    th = bench.thread_cpu()
+    assert th[os.getpid()][0] == 'main' and all(isinstance(v[1], int) for v in th.values())
+
+
 def test_ensure_hw_queues_raises_but_never_lowers(monkeypatch):
     from blendtorch.utils import ensure_hw_queues
     monkeypatch.delenv('BT_HW_QUEUES', raising=False)
