@@ -38,10 +38,11 @@ def main():
     ends = [i for i, r in enumerate(rows) if a.marker in r['k']]
     if len(ends) < 3:
         raise SystemExit(f'fewer than 3 {a.marker!r} kernels in the trace')
-    steps = []
+    steps, lead = [], []
     for i0, i1 in zip(ends[:-1], ends[1:]):
         steps.append(rows[i0 + 1:i1 + 1])
-    steps = steps[-a.steps:]
+        lead.append(rows[i0 + 1]['s'] - rows[i0]['e'])   # idle GPU time before the step's first kernel
+    steps, lead = steps[-a.steps:], lead[-a.steps:]
     # the median-length step, printed in order
     spans = [s[-1]['e'] - s[0]['s'] for s in steps]
     med = sorted(range(len(steps)), key=lambda i: spans[i])[len(steps) // 2]
@@ -57,6 +58,9 @@ def main():
         prev = r['e']
     busy = sum(r['e'] - r['s'] for r in st) / 1e3
     print(f'busy {busy:.1f} us of {spans[med] / 1e3:.1f} us')
+    period = [e1[-1]['e'] - e0[-1]['e'] for e0, e1 in zip(steps[:-1], steps[1:])]
+    print(f'between steps: median {statistics.median(lead) / 1e3:.1f} us idle before a step\'s first kernel; '
+          f'median step period {statistics.median(period) / 1e3:.1f} us')
     # mean per (position in step) over all steps with the same kernel count
     n = len(st)
     same = [s for s in steps if len(s) == n]
