@@ -186,6 +186,9 @@ def parse_args(argv=None):
                     help='disc consumer with the in-step decode (bf16, fused cast and head): on = the first '
                          'convolution reads the raw u8 RGBA frames through the decode table inside its MFMA '
                          'kernels; off = a decode launch writes bf16 frames first')
+    ap.add_argument('--graph-steps', type=int, choices=[1, 2], default=1,
+                    help='disc consumer with static inputs: training steps per graph replay (2: consecutive '
+                         'batches run in pairs from one captured graph -- halves the GPU idle between replays)')
     ap.add_argument('--grad-overlap', choices=['on', 'off'], default='on',
                     help='disc consumer, data parallel: on = two gradient buckets, each all-reduced as soon as its '
                          'gradients are written; off = one bucket after the whole backward')
@@ -489,7 +492,8 @@ def main(argv=None):
             # written, ahead of the first layers' weight gradients (GradBuckets.arm)
             stepper = CapturedStep(model, opt, loss_fn, graph=use_graph, comm=comm,
                                    allreduce='always' if args.force_pg else dist.is_initialized(), split=dma_mid,
-                                   static_inputs=static_in, overlap=args.grad_overlap == 'on')
+                                   static_inputs=static_in, overlap=args.grad_overlap == 'on',
+                                   pair_steps=args.graph_steps == 2)
 
         def graphed(x):
             stepper(x, mid=dl.release if (dma_mid and dl is not None) else None)
@@ -530,6 +534,8 @@ def main(argv=None):
             n_warm += 1
             if last['btid'] is not None:
                 seen.update(int(x) for x in last['btid'])
+        if stepper is not None:
+            stepper.flush()          # --graph-steps 2: no warm-up step carried into the timed region
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -540,6 +546,8 @@ def main(argv=None):
         t0 = time.perf_counter()
         for _ in range(args.steps):
             img = step()
+        if stepper is not None:
+            stepper.flush()          # --graph-steps 2: the last step of an odd count runs on its own
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -656,6 +664,7 @@ def main(argv=None):
                 'cast': args.cast if amp else None,
                 'optim': args.optim if model is not None else None,
                 'dma_phase': args.dma_phase if model is not None else None,
+                'graph_steps': args.graph_steps if model is not None else None,
                 'head': args.head if model is not None else None,
                 'host_sync': args.host_sync,
                 'consumer_collectives_per_step': stepper.collectives if stepper is not None else None,

@@ -107,6 +107,12 @@ class CapturedStep:
         (:meth:`~.grads.GradBuckets.arm`): the last layers' bucket goes ahead of
         the first layers' weight gradients.  Only for a ``loss_fn`` whose
         parameters each get one gradient contribution per backward.
+    pair_steps: (with ``static_inputs``) two consecutive steps per replay: a
+        step is held until the next one's input arrives, then both run from one
+        graph captured for that pair of input tensors (the GPU idles ~13 us
+        between two replays, profiles/r4/SUMMARY.md).  A held step returns
+        ``None``; :meth:`flush` runs a held step on its own -- call it before
+        reading results or synchronising.
     split: capture forward+loss and backward+update as two graphs sharing one
         memory pool, so a caller can act between them: ``step(x, mid=fn)``
         runs ``fn()`` after enqueuing the forward (e.g. to gate the next
@@ -127,7 +133,8 @@ class CapturedStep:
     def __init__(self, model: torch.nn.Module, optimizer: torch.optim.Optimizer,
                  loss_fn: Callable[[torch.nn.Module, torch.Tensor], torch.Tensor], allreduce=True,
                  warmup: int = 3, graph: bool = True, group=None, bucket_mb: float = 256.0, split: bool = False,
-                 comm=None, buckets: bool = True, static_inputs: int = 0, overlap: bool = False):
+                 comm=None, buckets: bool = True, static_inputs: int = 0, overlap: bool = False,
+                 pair_steps: bool = False):
         self.model, self.opt, self.loss_fn = model, optimizer, loss_fn
         self.split = split
         self.static_inputs = 0 if split else max(0, int(static_inputs))
@@ -165,6 +172,10 @@ class CapturedStep:
                 self._memset = any(id(p) not in opt_ids for p in self.grads.params)
         self._static_mode = bool(self.static_inputs)
         self._copy_failed = False
+        self.pair_steps = bool(pair_steps) and self._static_mode
+        self._held = None          # pair_steps: the input of a step not yet enqueued
+        self._pairs = {}           # (data_ptr a, data_ptr b) -> (graph, a, b, loss of b)
+        self._pair_failed = False
         if active and buckets:
             from .comm import DeviceComm
             self.comm = comm if comm is not None else DeviceComm(group, dedicated=True)
@@ -292,6 +303,42 @@ class CapturedStep:
                 ent[1].copy_(x)
         return ent
 
+    def _pair_entry(self, xa, xb):
+        """The graph that runs the steps on ``xa`` then ``xb`` (captured on
+        first use, in the first graph's pool), or None."""
+        key = (xa.data_ptr(), xb.data_ptr())
+        ent = self._pairs.get(key)
+        if ent is None and not self._pair_failed and len(self._pairs) < self.static_inputs:
+            g = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(g, pool=self.graph.pool(), capture_error_mode='thread_local'):
+                    self._train(xa)
+                    loss = self._train(xb)
+            except RuntimeError as e:
+                self.error = str(e)
+                self._pair_failed = True       # recorded once: single steps from here on
+                return None
+            ent = (g, xa, xb, loss)
+            self._pairs[key] = ent
+        return ent
+
+    def _static_step(self, x, mid):
+        # x is a caller's tensor (e.g. a loader ring buffer): never written
+        ent = self._lookup(x)
+        if ent is None:
+            return self._eager(x, mid)
+        ent[0].replay()
+        if mid is not None:
+            mid()
+        return ent[2]
+
+    def flush(self) -> Optional[torch.Tensor]:
+        """pair_steps: enqueue a held step on its own (no-op otherwise)."""
+        if self._held is None:
+            return None
+        x, self._held = self._held, None
+        return self._static_step(x, None)
+
     def _eager(self, x, mid):
         loss = self._forward(x)
         if mid is not None:
@@ -315,14 +362,19 @@ class CapturedStep:
                 return self.loss
         if self.state == 'graph':
             if self._static_mode:
-                # self.x is a caller's tensor (e.g. a loader ring buffer): never written
-                ent = self._lookup(x)
-                if ent is None:
-                    return self._eager(x, mid)
-                ent[0].replay()
-                if mid is not None:
-                    mid()
-                return ent[2]
+                if self.pair_steps and mid is None and self._same_layout(x):
+                    if self._held is None:
+                        self._held = x
+                        return None
+                    xa, self._held = self._held, None
+                    ent = self._pair_entry(xa, x)
+                    if ent is not None:
+                        ent[0].replay()
+                        return ent[3]
+                    self._static_step(xa, None)
+                    return self._static_step(x, None)
+                self.flush()                   # keep the steps in order
+                return self._static_step(x, mid)
             if x.shape != self.x.shape or x.dtype != self.x.dtype or x.device != self.x.device:
                 return self._eager(x, mid)       # the graph is for the captured shape only (copy_ converts strides)
             if x.data_ptr() != self.x.data_ptr():

@@ -349,6 +349,43 @@ def test_captured_step_static_inputs_read_in_place(dev):
         assert float(d.mean()) < 0.15 * lr
 
 
+def test_captured_step_pair_steps_train_like_single_steps(dev):
+    """CapturedStep(pair_steps=True): consecutive steps run in pairs from one
+    graph per pair of input tensors; a held step runs when the next arrives or
+    at flush().  Same training as one graph per step (7 steps: three pairs,
+    then a flushed single)."""
+    from blendtorch.models import Discriminator
+    from blendtorch.parallel.step import CapturedStep
+    cl = torch.channels_last
+    g = torch.Generator(device=dev).manual_seed(7)
+    bufs = [torch.rand(4, 4, 96, 128, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+            for _ in range(4)]
+    keep = [b.clone() for b in bufs]
+    nets = []
+    for pair in (False, True):
+        torch.manual_seed(0)
+        m = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
+        opt = ops.FusedAdam(m.parameters(), lr=2e-4)
+        step = CapturedStep(m, opt, lambda mm, x: mm.bce_loss_bf16(x, 1.0), allreduce=False, graph=True,
+                            static_inputs=4, pair_steps=pair)
+        held = 0
+        for k in range(7):
+            held += step(bufs[k % 4]) is None
+        step.flush()
+        torch.cuda.synchronize()
+        assert step.state == 'graph' and step.error is None
+        if pair:
+            # step 0 captures the single graph; steps 1-6 pair up (1, 2), (3, 0), (1, 2)
+            assert held == 3 and len(step._pairs) == 2 and step._held is None
+        nets.append(m)
+    for b, k in zip(bufs, keep):
+        assert torch.equal(b, k)                            # inputs read in place, never written
+    lr = 2e-4
+    for pa, pb in zip(nets[0].parameters(), nets[1].parameters()):
+        d = (pb - pa).detach().abs()
+        assert float(d.mean()) < 0.15 * lr
+
+
 def test_captured_step_never_replays_for_another_layout(dev):
     """A cache hit on the data pointer alone must not replay a graph: a view
     of a captured buffer with another shape (``x[:2]``: same data pointer;
