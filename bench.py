@@ -189,7 +189,9 @@ def parse_args(argv=None):
     ap.add_argument('--graph-steps', type=int, choices=[1, 2], default=2,
                     help='disc consumer with static inputs: training steps per graph replay (2: consecutive '
                          'batches run in pairs from one captured graph -- halves the GPU idle between replays; '
-                         '+0.4-1.3 %% in three same-call A/Bs, profiles/r4/b38/)')
+                         '+0.4-1.3 %% in three same-call A/Bs, profiles/r4/b38/).  Not more than 2: the '
+                         'loader re-posts a ring tensor two batches after handing it out, so a held step must '
+                         'be enqueued by then')
     ap.add_argument('--grad-overlap', choices=['on', 'off'], default='on',
                     help='disc consumer, data parallel: on = two gradient buckets, each all-reduced as soon as its '
                          'gradients are written; off = one bucket after the whole backward')
@@ -494,7 +496,7 @@ def main(argv=None):
             stepper = CapturedStep(model, opt, loss_fn, graph=use_graph, comm=comm,
                                    allreduce='always' if args.force_pg else dist.is_initialized(), split=dma_mid,
                                    static_inputs=static_in, overlap=args.grad_overlap == 'on',
-                                   pair_steps=args.graph_steps == 2)
+                                   group_steps=args.graph_steps)
 
         def graphed(x):
             stepper(x, mid=dl.release if (dma_mid and dl is not None) else None)

@@ -107,12 +107,16 @@ class CapturedStep:
         (:meth:`~.grads.GradBuckets.arm`): the last layers' bucket goes ahead of
         the first layers' weight gradients.  Only for a ``loss_fn`` whose
         parameters each get one gradient contribution per backward.
-    pair_steps: (with ``static_inputs``) two consecutive steps per replay: a
-        step is held until the next one's input arrives, then both run from one
-        graph captured for that pair of input tensors (the GPU idles ~13 us
-        between two replays, profiles/r4/SUMMARY.md).  A held step returns
-        ``None``; :meth:`flush` runs a held step on its own -- call it before
-        reading results or synchronising.
+    group_steps: (with ``static_inputs``) that many consecutive steps per
+        replay: steps are held until the group's last input arrives, then all
+        run from one graph captured for that tuple of input tensors (the GPU
+        idles ~13 us between two replays, profiles/r4/SUMMARY.md).  A held
+        step returns ``None``; :meth:`flush` runs held steps one by one --
+        call it before reading results or synchronising.  ``pair_steps=True``
+        is ``group_steps=2``.  A held input must stay unchanged until its group
+        replays: ``btt.DeviceLoader(reuse_buffers=True)`` re-posts a ring
+        tensor for refilling two batches after handing it out, so with it at
+        most 2 steps per group are safe.
     split: capture forward+loss and backward+update as two graphs sharing one
         memory pool, so a caller can act between them: ``step(x, mid=fn)``
         runs ``fn()`` after enqueuing the forward (e.g. to gate the next
@@ -134,7 +138,7 @@ class CapturedStep:
                  loss_fn: Callable[[torch.nn.Module, torch.Tensor], torch.Tensor], allreduce=True,
                  warmup: int = 3, graph: bool = True, group=None, bucket_mb: float = 256.0, split: bool = False,
                  comm=None, buckets: bool = True, static_inputs: int = 0, overlap: bool = False,
-                 pair_steps: bool = False):
+                 pair_steps: bool = False, group_steps: int = 1):
         self.model, self.opt, self.loss_fn = model, optimizer, loss_fn
         self.split = split
         self.static_inputs = 0 if split else max(0, int(static_inputs))
@@ -172,10 +176,11 @@ class CapturedStep:
                 self._memset = any(id(p) not in opt_ids for p in self.grads.params)
         self._static_mode = bool(self.static_inputs)
         self._copy_failed = False
-        self.pair_steps = bool(pair_steps) and self._static_mode
-        self._held = None          # pair_steps: the input of a step not yet enqueued
-        self._pairs = {}           # (data_ptr a, data_ptr b) -> (graph, a, b, loss of b)
-        self._pair_failed = False
+        n = max(int(group_steps), 2 if pair_steps else 1)
+        self.group_steps = n if self._static_mode else 1
+        self._held = []            # group_steps: inputs of steps not yet enqueued
+        self._groups = {}          # (data_ptr, ...) -> (graph, inputs, loss of the last step)
+        self._group_failed = False
         if active and buckets:
             from .comm import DeviceComm
             self.comm = comm if comm is not None else DeviceComm(group, dedicated=True)
@@ -303,23 +308,23 @@ class CapturedStep:
                 ent[1].copy_(x)
         return ent
 
-    def _pair_entry(self, xa, xb):
-        """The graph that runs the steps on ``xa`` then ``xb`` (captured on
+    def _group_entry(self, xs):
+        """The graph that runs the steps on ``xs`` in order (captured on
         first use, in the first graph's pool), or None."""
-        key = (xa.data_ptr(), xb.data_ptr())
-        ent = self._pairs.get(key)
-        if ent is None and not self._pair_failed and len(self._pairs) < self.static_inputs:
+        key = tuple(x.data_ptr() for x in xs)
+        ent = self._groups.get(key)
+        if ent is None and not self._group_failed and len(self._groups) < self.static_inputs:
             g = torch.cuda.CUDAGraph()
             try:
                 with torch.cuda.graph(g, pool=self.graph.pool(), capture_error_mode='thread_local'):
-                    self._train(xa)
-                    loss = self._train(xb)
+                    for x in xs:
+                        loss = self._train(x)
             except RuntimeError as e:
                 self.error = str(e)
-                self._pair_failed = True       # recorded once: single steps from here on
+                self._group_failed = True      # recorded once: single steps from here on
                 return None
-            ent = (g, xa, xb, loss)
-            self._pairs[key] = ent
+            ent = (g, tuple(xs), loss)
+            self._groups[key] = ent
         return ent
 
     def _static_step(self, x, mid):
@@ -333,11 +338,12 @@ class CapturedStep:
         return ent[2]
 
     def flush(self) -> Optional[torch.Tensor]:
-        """pair_steps: enqueue a held step on its own (no-op otherwise)."""
-        if self._held is None:
-            return None
-        x, self._held = self._held, None
-        return self._static_step(x, None)
+        """group_steps: enqueue the held steps one by one (no-op otherwise)."""
+        held, self._held = self._held, []
+        loss = None
+        for x in held:
+            loss = self._static_step(x, None)
+        return loss
 
     def _eager(self, x, mid):
         loss = self._forward(x)
@@ -362,17 +368,18 @@ class CapturedStep:
                 return self.loss
         if self.state == 'graph':
             if self._static_mode:
-                if self.pair_steps and mid is None and self._same_layout(x):
-                    if self._held is None:
-                        self._held = x
+                if self.group_steps > 1 and mid is None and self._same_layout(x):
+                    self._held.append(x)
+                    if len(self._held) < self.group_steps:
                         return None
-                    xa, self._held = self._held, None
-                    ent = self._pair_entry(xa, x)
+                    xs, self._held = self._held, []
+                    ent = self._group_entry(xs)
                     if ent is not None:
                         ent[0].replay()
-                        return ent[3]
-                    self._static_step(xa, None)
-                    return self._static_step(x, None)
+                        return ent[2]
+                    for xi in xs[:-1]:
+                        self._static_step(xi, None)
+                    return self._static_step(xs[-1], None)
                 self.flush()                   # keep the steps in order
                 return self._static_step(x, mid)
             if x.shape != self.x.shape or x.dtype != self.x.dtype or x.device != self.x.device:

@@ -376,7 +376,7 @@ def test_captured_step_pair_steps_train_like_single_steps(dev):
         assert step.state == 'graph' and step.error is None
         if pair:
             # step 0 captures the single graph; steps 1-6 pair up (1, 2), (3, 0), (1, 2)
-            assert held == 3 and len(step._pairs) == 2 and step._held is None
+            assert held == 3 and len(step._groups) == 2 and not step._held
         nets.append(m)
     for b, k in zip(bufs, keep):
         assert torch.equal(b, k)                            # inputs read in place, never written
@@ -384,6 +384,34 @@ def test_captured_step_pair_steps_train_like_single_steps(dev):
     for pa, pb in zip(nets[0].parameters(), nets[1].parameters()):
         d = (pb - pa).detach().abs()
         assert float(d.mean()) < 0.15 * lr
+
+
+def test_captured_step_group_of_four_steps_trains_like_single_steps(dev):
+    """group_steps=4: steps 1-4 run from one graph, steps 5-6 stay held
+    until flush() runs them one by one."""
+    from blendtorch.models import Discriminator
+    from blendtorch.parallel.step import CapturedStep
+    cl = torch.channels_last
+    g = torch.Generator(device=dev).manual_seed(11)
+    bufs = [torch.rand(4, 4, 96, 128, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+            for _ in range(4)]
+    nets = []
+    for n in (1, 4):
+        torch.manual_seed(0)
+        m = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
+        opt = ops.FusedAdam(m.parameters(), lr=2e-4)
+        step = CapturedStep(m, opt, lambda mm, x: mm.bce_loss_bf16(x, 1.0), allreduce=False, graph=True,
+                            static_inputs=4, group_steps=n)
+        held = sum(step(bufs[k % 4]) is None for k in range(7))
+        if n == 4:
+            assert held == 5 and len(step._groups) == 1 and len(step._held) == 2
+        step.flush()
+        torch.cuda.synchronize()
+        assert step.state == 'graph' and step.error is None and not step._held
+        nets.append(m)
+    lr = 2e-4
+    for pa, pb in zip(nets[0].parameters(), nets[1].parameters()):
+        assert float((pb - pa).detach().abs().mean()) < 0.15 * lr
 
 
 def test_captured_step_never_replays_for_another_layout(dev):
