@@ -688,6 +688,10 @@ def main(argv=None):
             'h2d_gbytes_per_s': _r(win.get('h2d_gbytes_per_s'), 2),
             'loader_frames_per_s': _r(win.get('frames_per_s'), 1),
             'producer_frames_per_s': win.get('producer_frames_per_s'),
+            'producer_share_max_over_min': win.get('producer_share_max_over_min'),
+            'producers_starved': win.get('producers_starved'),
+            'window_frames': win.get('frames'),
+            'backlog_covers_window': win.get('backlog_covers_window'),
             'ring_t0': win.get('ring_t0'),
             'ring_t1': win.get('ring_t1'),
             'consumer_wait_ms_per_batch': _r(win.get('consumer_wait_ms_per_batch'), 4),

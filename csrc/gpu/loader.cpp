@@ -361,29 +361,34 @@ void StreamLoader::drain_sockets() {
     for (int n = 0; n < 4096; ++n) {
       zmtp::Message m;
       try {
-        m = s->recv(zmtp::DONTWAIT);
+        if (!s->try_recv(m)) break;
       } catch (const zmtp::Error&) {
         break;
       }
-      if (m.size() != 1) continue;
-      try {
-        codec::VPtr root = codec::parse(m[0].data(), m[0].size);
-        if (!root || root->kind != codec::Value::DICT) continue;
-        const codec::Value* d = root->get("_btshm");
-        if (!d || d->kind != codec::Value::TUPLE || d->items.size() < 8 || d->items[0]->kind != codec::Value::STR)
-          continue;
-        const uint32_t slot = uint32_t(d->items[1]->i), gen = uint32_t(d->items[7]->i);
-        auto it = segments_.find(d->items[0]->s);
-        if (it != segments_.end()) {
-          it->second.seg->release(slot, gen);
-        } else {
-          std::unique_ptr<shm::Segment> seg(shm::Segment::open(d->items[0]->s));
-          seg->release(slot, gen);
-        }
-      } catch (const std::exception&) {
-        continue;   // producer gone / not a descriptor: nothing to hand back
-      }
+      release_descriptor(m);
     }
+  }
+}
+
+// A received but unprocessed shm descriptor: hand its (still PUBLISHED) slot
+// back to the producer.  Anything else needs nothing.
+void StreamLoader::release_descriptor(const zmtp::Message& m) {
+  if (m.size() != 1) return;
+  try {
+    codec::VPtr root = codec::parse(m[0].data(), m[0].size);
+    if (!root || root->kind != codec::Value::DICT) return;
+    const codec::Value* d = root->get("_btshm");
+    if (!d || d->kind != codec::Value::TUPLE || d->items.size() < 8 || d->items[0]->kind != codec::Value::STR) return;
+    const uint32_t slot = uint32_t(d->items[1]->i), gen = uint32_t(d->items[7]->i);
+    auto it = segments_.find(d->items[0]->s);
+    if (it != segments_.end()) {
+      it->second.seg->release(slot, gen);
+    } else {
+      std::unique_ptr<shm::Segment> seg(shm::Segment::open(d->items[0]->s));
+      seg->release(slot, gen);
+    }
+  } catch (const std::exception&) {
+    // producer gone / not a descriptor: nothing to hand back
   }
 }
 
@@ -418,6 +423,8 @@ void StreamLoader::run() {
   }
   std::vector<std::pair<zmtp::Socket*, int>> items;
   for (auto& s : socks_) items.emplace_back(s.get(), zmtp::POLLIN);
+  std::vector<zmtp::Socket*> ready;
+  std::vector<zmtp::Message> round;
   const auto intr = [this] { return stop_.load(); };
   const int64_t max_frames = cfg_.max_batches < 0 ? -1 : cfg_.max_batches * cfg_.batch_size;
   int64_t taken = 0;
@@ -444,13 +451,27 @@ void StreamLoader::run() {
     }
     CpuScope cs(cpu_ns_[kCpuRecv]);
     flush_pending(max_frames >= 0 && taken >= max_frames);
-    for (size_t i = 0; i < ev.size() && !stop_; ++i) {
-      if (!(ev[i] & zmtp::POLLIN)) continue;
-      // drain what is queued on this socket (bounded, to stay fair)
-      for (int n = 0; n < 64 && !stop_; ++n) {
-        if (max_frames >= 0 && taken >= max_frames) break;
-        zmtp::Message m;
-        if (!socks_[i]->try_recv(m)) break;
+    ready.clear();
+    for (size_t i = 0; i < ev.size(); ++i)
+      if (ev[i] & zmtp::POLLIN) ready.push_back(socks_[i].get());
+    // Fair fan-in (the reference's PULL contract, examples/datagen/Readme.md:
+    // 168-177): every round takes at most ONE message per producer pipe,
+    // across all IO sockets, whatever the producer -> socket spread (5
+    // producers on 4 sockets put 2 on one).  Draining a socket at a time let
+    // a lone producer's socket deliver twice its share.  Rounds repeat until
+    // one comes back empty or ~64 frames were taken (amortises the poll).
+    size_t woke = 0;
+    while (!stop_ && !ready.empty() && woke < 64) {
+      const size_t room = max_frames >= 0 ? size_t(std::max<int64_t>(0, max_frames - taken)) : size_t(-1);
+      if (room == 0) break;
+      round.clear();
+      if (zmtp::Socket::recv_round(ready, round, room) == 0) break;
+      woke += round.size();
+      for (auto& m : round) {
+        if (stop_) {
+          release_descriptor(m);   // the stream failed / stopped mid-round: hand its shm slot back
+          continue;
+        }
         if (process(std::move(m))) ++taken;
       }
     }

@@ -259,6 +259,7 @@ class StreamLoader {
   void reap(bool wait_all = false);   // release pinned slots of completed H2D copies
   void evict_keys();
   void drain_sockets();               // stop(): hand back ring slots of still-queued descriptors
+  void release_descriptor(const zmtp::Message& m);   // an unprocessed descriptor: slot back to its producer
 
   LoaderConfig cfg_;
   std::vector<std::unique_ptr<zmtp::Context>> ctxs_;

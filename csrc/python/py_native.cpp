@@ -190,6 +190,32 @@ class NativeError(Exception):
           return guarded([&] { return Socket::poll(raw, timeout_ms, signal_check()); });
         });
 
+  // One fair fan-in round over several sockets (the GPU loader's receive
+  // policy): at most one message per producer pipe; list of multipart lists.
+  m.def("recv_round",
+        [](const std::vector<std::shared_ptr<Socket>>& socks, size_t max) {
+          std::vector<Socket*> raw;
+          for (auto& s : socks) raw.push_back(s.get());
+          std::vector<Message> msgs;
+          {
+            py::gil_scoped_release nogil;
+            guarded([&] { return Socket::recv_round(raw, msgs, max); });
+          }
+          py::list out;
+          for (auto& msg : msgs) {
+            py::list parts;
+            for (size_t i = 0; i < msg.size(); ++i) {
+              PyFrame pf;
+              pf.f = std::move(msg[i]);
+              pf.more = i + 1 < msg.size();
+              parts.append(py::cast(std::move(pf)));
+            }
+            out.append(parts);
+          }
+          return out;
+        },
+        py::arg("sockets"), py::arg("max") = size_t(-1));
+
   m.def("greeting_bytes", [](bool as_server) { return py::bytes(zmtp::greeting_bytes(as_server)); });
   m.def("ready_command", [](int t, const std::string& id) { return py::bytes(zmtp::ready_command(t, id)); },
         py::arg("socket_type"), py::arg("identity") = "");

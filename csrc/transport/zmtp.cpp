@@ -1479,6 +1479,49 @@ bool Socket::try_recv(Message& out) {
   return try_recv_locked(out);
 }
 
+size_t Socket::recv_round(std::vector<Message>& out, size_t max) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (closing_) throw Error(E_TERM, "socket closed");
+  if (type_ != PULL && type_ != PAIR && type_ != DEALER) throw Error(E_INVAL, "recv_round: PULL/PAIR/DEALER only");
+  // purge drained pipes of dead peers (as try_recv_locked does)
+  for (size_t i = 0; i < pipes_.size();) {
+    Pipe* p = pipes_[i].get();
+    if (p->gone && p->inq.empty() && p->state == Pipe::DEAD) {
+      detach_pipe_locked(p);
+      continue;
+    }
+    ++i;
+  }
+  const size_t n = pipes_.size();
+  size_t got = 0;
+  std::vector<Pipe*> dead;
+  const size_t start = rr_in_;
+  for (size_t k = 0; k < n && got < max; ++k) {
+    const size_t idx = (start + k) % n;
+    Pipe* p = pipes_[idx].get();
+    if (p->inq.empty()) continue;
+    out.push_back(std::move(p->inq.front()));
+    p->inq.pop_front();
+    resume_reads_locked(p);
+    ++got;
+    if (p->gone && p->inq.empty() && p->state == Pipe::DEAD) dead.push_back(p);
+    // the next round starts behind the last pipe served: a round cut short
+    // by `max` continues where it stopped instead of favouring pipe 0
+    rr_in_ = (idx + 1) % n;
+  }
+  for (Pipe* p : dead) detach_pipe_locked(p);
+  return got;
+}
+
+size_t Socket::recv_round(const std::vector<Socket*>& socks, std::vector<Message>& out, size_t max) {
+  size_t got = 0;
+  for (Socket* s : socks) {
+    if (got >= max) break;
+    got += s->recv_round(out, max - got);
+  }
+  return got;
+}
+
 void Socket::wait_slice(std::unique_lock<std::mutex>& lk, const Clock::time_point* deadline,
                         const Interrupt& intr) {
   auto until = Clock::now() + std::chrono::milliseconds(intr ? 100 : 1000);

@@ -148,6 +148,15 @@ class Socket : public std::enable_shared_from_this<Socket> {
   // empty queue cost the loader worker ~1-3 us per poll wake-up).
   bool try_recv(Message& out);
 
+  // One fair-queue round (PULL/PAIR/DEALER): appends at most ONE queued
+  // message per connected pipe (= per producer), visiting the pipes in
+  // round-robin order, and at most `max` in all.  Returns the count.
+  size_t recv_round(std::vector<Message>& out, size_t max);
+  // One round over several sockets: at most one message per pipe of every
+  // socket -- fair across producers however they are spread over the
+  // sockets (a socket holding 2 producers yields 2, one holding 1 yields 1).
+  static size_t recv_round(const std::vector<Socket*>& socks, std::vector<Message>& out, size_t max);
+
   // Readiness for poll(): bit POLLIN / POLLOUT.
   int events();
   // Multi-socket poll; returns readiness per socket.

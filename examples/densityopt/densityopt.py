@@ -86,6 +86,10 @@ def cpu_stream(addresses, batch):
     """CPU fallback: RemoteIterableDataset + DataLoader, as the reference does."""
     from torch.utils import data
     ds = btt.RemoteIterableDataset(addresses, item_transform=item_transform, timeoutms=30000)
+    # the dataset's default max_items=100000 (reference dataset.py:22) ends the
+    # stream after 1562 iterations of 64 with a short batch of 32: the
+    # reference's own loop cannot run past epoch 1562; stream without bound
+    ds.stream_length(1 << 62)
     for img, sid in data.DataLoader(ds, batch_size=batch, num_workers=0):
         yield {'image': img, 'shape_id': sid}
 

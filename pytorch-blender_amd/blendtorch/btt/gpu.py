@@ -299,7 +299,12 @@ class DeviceLoader:
                                                       'timed_gpu_ms', 'shm_stale', 'shm_torn', 'bad')}
         p0 = {int(k): int(v) for k, v in s0.get('frames_per_btid', {}).items()}
         p1 = {int(k): int(v) for k, v in s1.get('frames_per_btid', {}).items()}
-        per = {k: round((v - p0.get(k, 0)) / dt, 1) for k, v in sorted(p1.items())}
+        cnt = {k: v - p0.get(k, 0) for k, v in sorted(p1.items())}
+        per = {k: round(c / dt, 1) for k, c in cnt.items()}
+        # fair fan-in check (reference: every consumer interleaves all producers
+        # fairly, examples/datagen/Readme.md:177): max/min of the producers'
+        # frame counts in the window; None when a known producer sent nothing
+        lo = min(cnt.values()) if cnt else 0
         out = {
             'window_s': dt,
             'frames': d['frames'],
@@ -309,6 +314,9 @@ class DeviceLoader:
             'timed_images': d['timed_images'],
             'images_per_launch': d['frames'] / d['launches'] if d['launches'] else None,
             'producer_frames_per_s': per,
+            'producer_frames': cnt,
+            'producer_share_max_over_min': (round(max(cnt.values()) / lo, 4) if lo > 0 else None),
+            'producers_starved': sum(1 for c in cnt.values() if c == 0),
             'consumer_wait_ms_per_batch': ((s1['consumer_wait_s'] - s0['consumer_wait_s']) * 1e3 / d['batches']
                                            if d['batches'] else None),
             'shm_stale': d['shm_stale'], 'shm_torn': d['shm_torn'], 'bad': d['bad'],
@@ -319,6 +327,11 @@ class DeviceLoader:
             if 'ring_slots' in s:
                 out[f'ring_{tag}'] = {'published': s.get('ring_published', 0), 'held': s.get('ring_held', 0),
                                       'slots': s['ring_slots']}
+        # a window no longer than the frames already rendered at its start could
+        # have been served from that backlog alone: it proves the loader's rate,
+        # not the producers' sustained rate
+        if 'ring_t0' in out:
+            out['backlog_covers_window'] = out['ring_t0']['published'] >= d['frames']
         return out
 
     def _log_metrics(self):

@@ -42,6 +42,40 @@ def test_device_loader_cubesim(dev, free_port):
         assert dl.stats['frames'] == 512 and dl.stats['bad'] == 0
 
 
+@pytest.mark.parametrize('nprod', [5, 8])
+def test_device_loader_fair_across_producers(dev, free_port, nprod):
+    """Fair fan-in (reference: examples/datagen/Readme.md:168-177, every
+    consumer interleaves all connected producers fairly).  5 producers on the
+    loader's 4 IO sockets is the uneven case ({p0,p4},{p1},{p2},{p3}); with
+    every producer backpressured (a consumer slower than 5 producers' render
+    rate, shm rings full) each producer's share of >= 2000 frames must be
+    within +-10 % of 1/P (round 4 drained 64 per socket: 2.04:1)."""
+    import time
+    args = ['--mode', 'rgba', '--sndhwm', '10', '--shm', '16']
+    with btt.BlenderLauncher(producer='cubesim', num_instances=nprod, named_sockets=['DATA'], start_port=free_port,
+                             proto='ipc', seed=5, instance_args=[args] * nprod) as bl:
+        dl = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=8, device=dev,
+                          decode=ops.DecodeConfig.unit(channels='rgb', gamma=2.2))
+        it = iter(dl)
+        seen, t0 = set(), time.time()
+        while len(seen) < nprod and time.time() - t0 < 60:   # every producer up
+            seen.update(next(it)['btid'].tolist())
+        assert len(seen) == nprod, seen
+        time.sleep(0.5)                                       # rings fill: all backpressured
+        s0 = dl.snapshot()
+        for _ in range(300):                                  # 2400 frames
+            next(it)
+            time.sleep(0.0004)                                # <= 20k frames/s: producers stay ahead
+        s1 = dl.snapshot()
+        it.close()
+    w = DeviceLoader.window(s0, s1)
+    cnt = w['producer_frames']
+    total = sum(cnt.values())
+    assert total >= 2000 and sorted(cnt) == list(range(nprod)), cnt
+    assert all(abs(c / total - 1 / nprod) <= 0.1 / nprod for c in cnt.values()), cnt
+    assert w['producer_share_max_over_min'] is not None and w['producer_share_max_over_min'] <= 1.25, w
+
+
 def test_device_loader_matches_cpu_decode(dev, free_port):
     """Same frames through the CPU path (pyobj recv + reference decode) and the
     GPU loader must agree bit-exactly: run one producer with a fixed seed

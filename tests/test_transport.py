@@ -273,3 +273,69 @@ def test_writer_aligned_payload(n, align):
         assert off > 0 and off % align == 0
         for r in (_pickle.loads(b), _native.fast_loads(b)):
             assert np.array_equal(r['image'], img) and r[key] == 2.5 and np.array_equal(r['xy'], d['xy'])
+
+
+def test_recv_round_fair_across_uneven_sockets(tmp_path):
+    """The GPU loader's fan-in policy (csrc/gpu/loader.cpp run(): one
+    Socket::recv_round per pass, at most ONE message per producer pipe across
+    all IO sockets).  5 backpressured producers spread over 4 PULL sockets as
+    the loader spreads them ({p0,p4}, {p1}, {p2}, {p3}): every producer's share
+    stays within +-10 % of 1/5 over >= 2000 messages (the reference's contract:
+    examples/datagen/Readme.md:177, workers interleave producers fairly).
+    Draining a socket at a time would give p1..p3 twice p0's and p4's share."""
+    P, K = 5, 4
+    ctx = zmq.Context()
+    addrs = [f'ipc://{tmp_path}/p{i}' for i in range(P)]
+    stop = threading.Event()
+    sent = [0] * P
+
+    def produce(i, s):
+        while not stop.is_set():
+            try:
+                s.send(bytes([i]) * 256, zmq.NOBLOCK)
+                sent[i] += 1
+            except zmq.Again:
+                time.sleep(0.0002)
+
+    pushes = []
+    for a in addrs:
+        s = ctx.socket(zmq.PUSH)
+        s.setsockopt(zmq.SNDHWM, 4)
+        s.setsockopt(zmq.LINGER, 0)
+        s.bind(a)
+        pushes.append(s)
+    pulls = []
+    for _ in range(K):
+        s = ctx.socket(zmq.PULL)
+        s.setsockopt(zmq.RCVHWM, 4)
+        s.setsockopt(zmq.LINGER, 0)
+        pulls.append(s)
+    for i, a in enumerate(addrs):
+        pulls[i % K].connect(a)
+    threads = [threading.Thread(target=produce, args=(i, pushes[i]), daemon=True) for i in range(P)]
+    for t in threads:
+        t.start()
+    try:
+        deadline = time.time() + 10
+        while min(sent) < 50 and time.time() < deadline:   # every pipe backlogged
+            time.sleep(0.01)
+        counts = [0] * P
+        rounds = 0
+        while sum(counts) < 2500 and time.time() < deadline + 30:
+            got = _native.recv_round([p._sock for p in pulls])
+            rounds += 1
+            ids = [bytes(parts[0])[0] for parts in got]
+            assert len(ids) == len(set(ids)), ids      # one message per producer per round
+            for i in ids:
+                counts[i] += 1
+            time.sleep(0.0005)            # a consumer slower than its producers
+        total = sum(counts)
+        assert total >= 2000, counts
+        shares = [c / total for c in counts]
+        assert all(abs(s - 1 / P) <= 0.1 / P for s in shares), (counts, rounds)
+    finally:
+        stop.set()
+        for t in threads:
+            t.join(2)
+        for s in pulls + pushes:
+            s.close(0)

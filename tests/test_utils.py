@@ -94,3 +94,24 @@ def test_save_image_matches_torchvision_grid_rules(tmp_path):
     want = np.clip((x[1].numpy() - lo) / (hi - lo) * 255 + 0.5, 0, 255).astype(np.uint8).transpose(1, 2, 0)
     assert np.array_equal(back[2:4, 6:8], want)         # tile 1: row 0, column 1
     assert back[:2].max() == 0 and back[8:, 6:].max() == 0   # padding and the empty 4th tile stay 0
+
+
+def test_loader_window_fairness_and_backlog_fields():
+    """DeviceLoader.window: per-producer counts in the timed window, their
+    max/min share (bench.py's producer_share_max_over_min) and whether the
+    ring's backlog at t0 alone could have served the window."""
+    from blendtorch.btt.gpu import DeviceLoader
+    s0 = {'t': 0.0, 'frames': 100, 'batches': 10, 'launches': 5, 'image_bytes': 0, 'timed_images': 0,
+          'timed_gpu_ms': 0.0, 'consumer_wait_s': 0.0, 'frames_per_btid': {0: 50, 1: 50, 2: 0},
+          'ring_slots': 96, 'ring_published': 40, 'ring_held': 8}
+    s1 = dict(s0, t=1.0, frames=400, batches=40, frames_per_btid={0: 150, 1: 160, 2: 90},
+              ring_published=30)
+    w = DeviceLoader.window(s0, s1)
+    assert w['producer_frames'] == {0: 100, 1: 110, 2: 90}
+    assert w['producer_share_max_over_min'] == round(110 / 90, 4)
+    assert w['producers_starved'] == 0
+    assert w['backlog_covers_window'] is False            # 40 published < 300 frames
+    s1b = dict(s1, frames=130, frames_per_btid={0: 80, 1: 80, 2: 0})
+    w = DeviceLoader.window(s0, s1b)
+    assert w['producer_share_max_over_min'] is None and w['producers_starved'] == 1
+    assert w['backlog_covers_window'] is True             # 40 published >= 30 frames
