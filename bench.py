@@ -266,7 +266,7 @@ def main(argv=None):
     # consumer keeps HIP's 4 -- its captured step with the in-graph all-reduce
     # ran 27 % slower with 8 (profiles/r4/pg_tax.md; blendtorch.utils.ensure_hw_queues)
     from blendtorch.utils import ensure_hw_queues
-    hw_queues = ensure_hw_queues(8 if args.consumer == 'none' else 4)
+    hw_queues = ensure_hw_queues(8 if args.consumer == 'none' else 4, exact=args.consumer != 'none')
     import torch
     import torch.distributed as dist
     from blendtorch import btt

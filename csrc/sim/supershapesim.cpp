@@ -220,7 +220,17 @@ int main(int argc, char** argv) {
     }
     if (pending.empty() || pending.front().next >= pending.front().ids.size()) {
       pending.clear();
-      if (!got) std::this_thread::sleep_for(std::chrono::microseconds(500));
+      // idle: block until the next parameters arrive (a 500 us sleep between
+      // polls added 0-0.5 ms to the start of every densityopt iteration).
+      // The reference's Blender keeps animating and polls once per frame
+      // (supershape.blend.py:26-36); a headless producer has no frame to draw
+      if (!got) {
+        try {
+          (void)zmtp::Socket::poll({{ctrl.get(), zmtp::POLLIN}}, 100, intr);
+        } catch (const zmtp::Error&) {
+          break;   // interrupted: g_stop
+        }
+      }
       continue;
     }
     Work& w = pending.front();

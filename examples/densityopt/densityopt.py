@@ -41,7 +41,7 @@ from blendtorch.utils import ensure_hw_queues  # noqa: E402
 
 # before the HIP runtime starts: HIP's 4 queues for a training step with in-graph
 # RCCL collectives (8 slowed the bench's graphed DP step by 27 %, profiles/r4/pg_tax.md)
-ensure_hw_queues(4)
+ensure_hw_queues(4, exact=True)
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

@@ -55,6 +55,16 @@ def _torch_lib():
     return Path(spec.origin).parent / 'lib'
 
 
+# what the last build_all() did per target: 'compiled' (objects recompiled
+# and/or relinked) or 'up to date' -- build() prints it so a driver's build on
+# another machine is observable (prebuilt .so files travel with the tree)
+REPORT = {}
+
+
+def _note(target: Path, changed: bool):
+    REPORT[str(target)] = 'compiled' if changed else 'up to date'
+
+
 def _newer(target: Path, deps):
     if not target.exists():
         return True
@@ -81,11 +91,11 @@ def _compile(compiler, src: Path, obj: Path, flags, verbose):
     stamp = obj.with_suffix('.cmd')
     cmd = ' '.join(str(a) for a in [compiler, *flags])
     if not _newer(obj, deps) and stamp.exists() and stamp.read_text() == cmd:
-        return obj
+        return obj, False
     obj.parent.mkdir(parents=True, exist_ok=True)
     _run([compiler, *flags, '-c', src, '-o', obj], verbose)
     stamp.write_text(cmd)
-    return obj
+    return obj, True
 
 
 def _obj_path(src: Path, tag: str):
@@ -104,18 +114,24 @@ def build_native(verbose=False, jobs=8):
         sim_srcs = [CSRC / 'sim' / n for n in ('cubesim.cpp', 'cartpolesim.cpp', 'supershapesim.cpp')]
         sim_srcs = [s for s in sim_srcs if s.exists()]
         futs += [ex.submit(_compile, cxx, s, _obj_path(s, 'cpu'), CXXFLAGS, verbose) for s in sim_srcs]
-        objs = [f.result() for f in futs]
+        res = [f.result() for f in futs]
+    objs = [r[0] for r in res]
+    fresh = [r[1] for r in res]
     core = objs[:len(srcs)]
     py_obj = objs[len(srcs)]
     target = PKG / f'_native{_ext_suffix()}'
-    if _newer(target, core + [py_obj]):
+    link = _newer(target, core + [py_obj])
+    if link:
         _run([cxx, '-shared', '-pthread', '-Wl,-Bsymbolic', *core, py_obj, '-o', target], verbose)
+    _note(target, link or any(fresh[:len(srcs) + 1]))
     BIN.mkdir(exist_ok=True)
-    for s, o in zip(sim_srcs, objs[len(srcs) + 1:]):
+    for s, o, f in zip(sim_srcs, objs[len(srcs) + 1:], fresh[len(srcs) + 1:]):
         exe = BIN / s.stem
         deps = core + [o]
-        if _newer(exe, deps):
+        link = _newer(exe, deps)
+        if link:
             _run([cxx, '-pthread', '-O3', *deps, '-o', exe, '-lrt'], verbose)
+        _note(exe, link or f)
     return target
 
 
@@ -143,9 +159,12 @@ def build_hip(verbose=False, jobs=8):
         futs = [ex.submit(_compile, hipcc, s, _obj_path(s, 'hip'), hflags, verbose) for s in gpu_srcs]
         futs += [ex.submit(_compile, cxx, CSRC / s, _obj_path(CSRC / s, 'cpu'), cflags + _py_includes(), verbose)
                  for s in TRANSPORT + CODEC]
-        objs = [f.result() for f in futs]
+        res = [f.result() for f in futs]
+    objs = [r[0] for r in res]
     target = PKG / f'_hip{_ext_suffix()}'
-    if _newer(target, objs):
+    relink = _newer(target, objs)
+    _note(target, relink or any(r[1] for r in res))
+    if relink:
         link = [hipcc, '-shared', '-fPIC', f'--offload-arch={HIP_ARCH}', '-Wl,-Bsymbolic', *objs, '-o', target, '-ldl']
         if tl is not None:
             # resolve libamdhip64 to the runtime torch already loaded
@@ -155,6 +174,7 @@ def build_hip(verbose=False, jobs=8):
 
 
 def build_all(verbose=False, hip=True):
+    REPORT.clear()
     out = [build_native(verbose)]
     if hip and hip_available():
         out.append(build_hip(verbose))
@@ -167,5 +187,6 @@ if __name__ == '__main__':
     ap.add_argument('--no-hip', action='store_true')
     ap.add_argument('-v', '--verbose', action='store_true')
     a = ap.parse_args()
-    for t in build_all(verbose=a.verbose, hip=not a.no_hip):
-        print('built', t)
+    build_all(verbose=a.verbose, hip=not a.no_hip)
+    for t, st in REPORT.items():
+        print(f'{st}: {t}')

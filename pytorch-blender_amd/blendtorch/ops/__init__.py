@@ -709,6 +709,15 @@ def grad_sink(param):
     return getattr(param, '_bt_grad_sink', None)
 
 
+def _grad_sink_ready(param):
+    """Would :func:`_grad_dest` write ``param``'s gradient into its bucket view
+    (fp32, contiguous)?  Consumes nothing."""
+    import torch
+    sink = grad_sink(param) if param is not None else None
+    return (sink is not None and param.grad is sink and getattr(param, '_bt_grad_fresh', False)
+            and sink.dtype == torch.float32 and sink.is_contiguous())
+
+
 def _grad_dest(param, like=None):
     """(tensor the backward kernel writes ``param``'s gradient into, whether
     that is the param's bucket view).  The first gradient after
@@ -1051,13 +1060,12 @@ def _bn_function():
                 # folds it and applies this backward while staging its weight gradient's dY
                 # (BnBwdFold) -- gy passes on unchanged.  The dw / db it writes must not be
                 # accumulated into an existing .grad before that launch: bucket views or unset.
-                dw, w_sunk = _grad_dest(ctx.params[0], w)
-                db, b_sunk = _grad_dest(ctx.params[1], b)
-                if dw.dtype != torch.float32 or not dw.is_contiguous():
-                    dw, w_sunk = torch.empty_like(w), False
-                if db.dtype != torch.float32 or not db.is_contiguous():
-                    db, b_sunk = torch.empty_like(b), False
-                if (w_sunk or ctx.params[0].grad is None) and (b_sunk or ctx.params[1].grad is None):
+                # eligibility first, without consuming the bucket views' fresh flags: a
+                # fall-through must leave both for the general path's _grad_dest below
+                # (else its parameter reports late and its bucket loses the overlap)
+                if all(p.grad is None or _grad_sink_ready(p) for p in ctx.params):
+                    dw, w_sunk = _grad_dest(ctx.params[0], w)
+                    db, b_sunk = _grad_dest(ctx.params[1], b)
                     _count('bn_backward_from_stats')   # (the sums: from the consumer's epilogue)
                     _count('bn_backward_deferred_fold')
                     sunk = (w_sunk, b_sunk)

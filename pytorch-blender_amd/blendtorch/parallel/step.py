@@ -111,12 +111,19 @@ class CapturedStep:
         replay: steps are held until the group's last input arrives, then all
         run from one graph captured for that tuple of input tensors (the GPU
         idles ~13 us between two replays, profiles/r4/SUMMARY.md).  A held
-        step returns ``None``; :meth:`flush` runs held steps one by one --
-        call it before reading results or synchronising.  ``pair_steps=True``
-        is ``group_steps=2``.  A held input must stay unchanged until its group
-        replays: ``btt.DeviceLoader(reuse_buffers=True)`` re-posts a ring
-        tensor for refilling two batches after handing it out, so with it at
-        most 2 steps per group are safe.
+        step returns ``None``; :meth:`flush` runs held steps one by one -- it
+        runs by itself before the model's or the optimizer's ``state_dict()``
+        and a step object dropped with steps held warns.  ``pair_steps=True``
+        is ``group_steps=2``.  Every step's loss of the last call that ran
+        steps is in :meth:`last_losses`.
+    reuse_distance: how many later inputs the caller hands in before it may
+        rewrite an input tensor in place (``btt.DeviceLoader(reuse_buffers=
+        True)`` re-posts a ring tensor for refilling when the batch two
+        behind it is handed out: 2, the default).  A held input must stay
+        unchanged until its group replays, so ``group_steps`` may not exceed
+        it.  An input modified in place while held (``x.copy_(batch);
+        step(x)``, seen through the tensor's version counter) raises instead
+        of training twice on the last batch.
     split: capture forward+loss and backward+update as two graphs sharing one
         memory pool, so a caller can act between them: ``step(x, mid=fn)``
         runs ``fn()`` after enqueuing the forward (e.g. to gate the next
@@ -138,7 +145,7 @@ class CapturedStep:
                  loss_fn: Callable[[torch.nn.Module, torch.Tensor], torch.Tensor], allreduce=True,
                  warmup: int = 3, graph: bool = True, group=None, bucket_mb: float = 256.0, split: bool = False,
                  comm=None, buckets: bool = True, static_inputs: int = 0, overlap: bool = False,
-                 pair_steps: bool = False, group_steps: int = 1):
+                 pair_steps: bool = False, group_steps: int = 1, reuse_distance: int = 2):
         self.model, self.opt, self.loss_fn = model, optimizer, loss_fn
         self.split = split
         self.static_inputs = 0 if split else max(0, int(static_inputs))
@@ -177,10 +184,28 @@ class CapturedStep:
         self._static_mode = bool(self.static_inputs)
         self._copy_failed = False
         n = max(int(group_steps), 2 if pair_steps else 1)
+        if n > 1 and self._static_mode and n > int(reuse_distance):
+            raise ValueError(f'CapturedStep: group_steps={n} holds inputs longer than their reuse distance '
+                             f'({reuse_distance}): a held buffer would be refilled before its group replays')
         self.group_steps = n if self._static_mode else 1
-        self._held = []            # group_steps: inputs of steps not yet enqueued
-        self._groups = {}          # (data_ptr, ...) -> (graph, inputs, loss of the last step)
+        self._held = []            # group_steps: (input, its version counter) of steps not yet enqueued
+        self._groups = {}          # (data_ptr, ...) -> (graph, inputs, per-step losses)
         self._group_failed = False
+        self._last_losses = []
+        self._ran = None
+        if self.group_steps > 1:
+            # a checkpoint must not miss held steps: flush before either state_dict
+            import weakref
+            ref = weakref.ref(self)
+
+            def _flush_hook(*_a, **_k):
+                st = ref()
+                if st is not None and st._held:
+                    st.flush()
+            for obj in (model, optimizer):
+                reg = getattr(obj, 'register_state_dict_pre_hook', None)
+                if reg is not None:
+                    reg(_flush_hook)
         if active and buckets:
             from .comm import DeviceComm
             self.comm = comm if comm is not None else DeviceComm(group, dedicated=True)
@@ -317,13 +342,12 @@ class CapturedStep:
             g = torch.cuda.CUDAGraph()
             try:
                 with torch.cuda.graph(g, pool=self.graph.pool(), capture_error_mode='thread_local'):
-                    for x in xs:
-                        loss = self._train(x)
+                    losses = [self._train(x) for x in xs]
             except RuntimeError as e:
                 self.error = str(e)
                 self._group_failed = True      # recorded once: single steps from here on
                 return None
-            ent = (g, tuple(xs), loss)
+            ent = (g, tuple(xs), losses)
             self._groups[key] = ent
         return ent
 
@@ -338,12 +362,44 @@ class CapturedStep:
         return ent[2]
 
     def flush(self) -> Optional[torch.Tensor]:
-        """group_steps: enqueue the held steps one by one (no-op otherwise)."""
+        """group_steps: enqueue the held steps one by one (no-op otherwise).
+        Returns the last step's loss (every step's in :meth:`last_losses`)."""
         held, self._held = self._held, []
-        loss = None
-        for x in held:
+        if not held:
+            return None
+        self._check_held(held)
+        inside = self._ran is not None      # flushed by a call that runs a step of its own next
+        losses = []
+        for i, (x, _) in enumerate(held):
             loss = self._static_step(x, None)
-        return loss
+            # two steps on one input replay one graph: keep the earlier value
+            losses.append(loss.clone() if (inside or i + 1 < len(held)) and loss is not None else loss)
+        if inside:
+            self._ran.extend(losses)
+        else:
+            self._last_losses = losses
+        return losses[-1]
+
+    def last_losses(self) -> List[torch.Tensor]:
+        """The loss of every step run by the last call that ran steps (a
+        group replay runs ``group_steps``, :meth:`flush` the held ones), in
+        step order.  Graph outputs: valid until the same graph replays again
+        -- clone what must outlive that."""
+        return list(self._last_losses)
+
+    @staticmethod
+    def _check_held(held):
+        for x, ver in held:
+            if x._version != ver:
+                raise RuntimeError('CapturedStep: an input held for a grouped replay was modified in place before '
+                                   'its group ran (e.g. x.copy_(batch); step(x)): its step would train on the '
+                                   'later data.  Pass a distinct tensor per step, or use group_steps=1')
+
+    def __del__(self):
+        if getattr(self, '_held', None):
+            import warnings
+            warnings.warn(f'CapturedStep dropped with {len(self._held)} held step(s) never run: call flush()',
+                          RuntimeWarning, stacklevel=2)
 
     def _eager(self, x, mid):
         loss = self._forward(x)
@@ -360,7 +416,22 @@ class CapturedStep:
         elif mid is not None:
             mid()
 
-    def __call__(self, x: torch.Tensor, mid: Optional[Callable[[], None]] = None) -> torch.Tensor:
+    def __call__(self, x: torch.Tensor, mid: Optional[Callable[[], None]] = None) -> Optional[torch.Tensor]:
+        """Run (or, grouped, hold) one step on ``x``.  Returns the step's loss,
+        or ``None`` for a step held for a grouped replay (``group_steps > 1``):
+        it runs with the group's last input or at :meth:`flush`."""
+        self._ran = []                 # losses of every step this call runs, in order
+        try:
+            loss = self._call(x, mid)
+        finally:
+            ran, self._ran = self._ran, None
+        if not ran and loss is not None:
+            ran = [loss]
+        if ran:
+            self._last_losses = ran
+        return loss
+
+    def _call(self, x, mid):
         if self.state == 'pending':
             self._capture(x)
             if self.state == 'graph':
@@ -369,19 +440,25 @@ class CapturedStep:
         if self.state == 'graph':
             if self._static_mode:
                 if self.group_steps > 1 and mid is None and self._same_layout(x):
-                    self._held.append(x)
+                    self._held.append((x, x._version))
                     if len(self._held) < self.group_steps:
                         return None
-                    xs, self._held = self._held, []
+                    held, self._held = self._held, []
+                    self._check_held(held)
+                    xs = [h[0] for h in held]
                     ent = self._group_entry(xs)
                     if ent is not None:
                         ent[0].replay()
-                        return ent[2]
-                    for xi in xs[:-1]:
-                        self._static_step(xi, None)
-                    return self._static_step(xs[-1], None)
+                        self._ran.extend(ent[2])
+                        return ent[2][-1]
+                    self._held = held
+                    loss = self.flush()
+                    self._ran[-1] = loss       # the call's result itself needs no copy
+                    return loss
                 self.flush()                   # keep the steps in order
-                return self._static_step(x, mid)
+                loss = self._static_step(x, mid)
+                self._ran.append(loss)
+                return loss
             if x.shape != self.x.shape or x.dtype != self.x.dtype or x.device != self.x.device:
                 return self._eager(x, mid)       # the graph is for the captured shape only (copy_ converts strides)
             if x.data_ptr() != self.x.data_ptr():

@@ -20,7 +20,7 @@ from __future__ import annotations
 
 import os
 from pathlib import Path
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 SYSFS_PCI = Path('/sys/bus/pci/devices')
 
@@ -113,21 +113,40 @@ def current_allowed_cpus() -> List[int]:
 # bench.py reports the current values as ``cpu.us_per_frame`` on every run.
 PRODUCER_US_PER_FRAME = 65.0
 CONSUMER_US_PER_FRAME = 20.0
+HEADLINE_FRAME_BYTES = 640 * 480 * 4
+# Per-message part of those costs (pickle/descriptor, socket, scan, batch
+# bookkeeping: independent of the pixel count); the rest scales with the
+# frame's bytes.  Estimates, not measurements: for other frame sizes pass the
+# measured ``cpu.us_per_frame`` of a bench run as producer_us / consumer_us.
+PRODUCER_FIXED_US = 10.0
+CONSUMER_FIXED_US = 10.0
 # host->device read ceiling of one MI355X PCIe link (profiles/direct_host_read.md)
 LINK_GBYTES_PER_S = 51.5
 
 
-def producers_for_share(share: float, frame_bytes: int = 640 * 480 * 4,
-                        producer_us: float = PRODUCER_US_PER_FRAME, consumer_us: float = CONSUMER_US_PER_FRAME,
+def frame_costs_us(frame_bytes: int = HEADLINE_FRAME_BYTES) -> Tuple[float, float]:
+    """(producer, consumer) CPU microseconds per frame of ``frame_bytes``:
+    the headline frame's measured costs, the per-message part fixed and the
+    rest scaled by the frame size (exact at 640x480 RGBA)."""
+    k = max(0, int(frame_bytes)) / HEADLINE_FRAME_BYTES
+    return (PRODUCER_FIXED_US + (PRODUCER_US_PER_FRAME - PRODUCER_FIXED_US) * k,
+            CONSUMER_FIXED_US + (CONSUMER_US_PER_FRAME - CONSUMER_FIXED_US) * k)
+
+
+def producers_for_share(share: float, frame_bytes: int = HEADLINE_FRAME_BYTES,
+                        producer_us: Optional[float] = None, consumer_us: Optional[float] = None,
                         link_gbytes: float = LINK_GBYTES_PER_S, cap: int = 8) -> int:
     """Producer processes one rank should run on ``share`` CPUs: the frame
     rate the rank can sustain is the smaller of its PCIe link's and its CPU
     share's (every frame costs ``producer_us`` in some producer and
-    ``consumer_us`` in the rank's own process); the producers need
-    ``rate * producer_us`` cores of it, rounded up.  When the link is the
-    bound a 1.5x margin keeps producers ahead of it (backpressure absorbs
-    the surplus); when the CPU is, more producers would only steal the
-    consumer's cores."""
+    ``consumer_us`` in the rank's own process; default :func:`frame_costs_us`
+    for this frame size); the producers need ``rate * producer_us`` cores of
+    it, rounded up.  When the link is the bound a 1.5x margin keeps producers
+    ahead of it (backpressure absorbs the surplus); when the CPU is, more
+    producers would only steal the consumer's cores."""
+    p_def, c_def = frame_costs_us(frame_bytes)
+    producer_us = p_def if producer_us is None else float(producer_us)
+    consumer_us = c_def if consumer_us is None else float(consumer_us)
     link_rate = link_gbytes * 1e9 / max(1, frame_bytes)
     cpu_rate = max(0.0, share) * 1e6 / (producer_us + consumer_us)
     rate = min(link_rate, cpu_rate)
@@ -141,7 +160,8 @@ def plan_rank_resources(rank: int, local_rank: int, local_world: int, world: int
                         shm_free_bytes: Optional[int] = None, frame_bytes: int = 640 * 480 * 4,
                         named_sockets: int = 1, port_base: int = 21000, port_stride: int = 64,
                         bus_ids: Optional[Sequence[Optional[str]]] = None, sysfs: Path = SYSFS_PCI,
-                        pid: Optional[int] = None) -> Dict[str, object]:
+                        pid: Optional[int] = None, producer_us: Optional[float] = None,
+                        consumer_us: Optional[float] = None) -> Dict[str, object]:
     """Everything one rank of ``bench.py`` claims on the node, decided without
     talking to the other ranks (so every rank computes the same, disjoint plan):
 
@@ -165,7 +185,7 @@ def plan_rank_resources(rank: int, local_rank: int, local_world: int, world: int
     """
     plan = plan_rank_cpus(local_rank, local_world, list(allowed)[:budget] if pin else allowed, bus_ids, sysfs)
     share = max(1, budget // max(1, local_world))
-    nprod = producers or producers_for_share(budget / max(1, local_world), frame_bytes)
+    nprod = producers or producers_for_share(budget / max(1, local_world), frame_bytes, producer_us, consumer_us)
     if dist_mode == 'scatter' and not producers:
         nprod = max(1, -(-8 // max(1, world)))
     mine = plan['cpus']

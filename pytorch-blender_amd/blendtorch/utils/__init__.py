@@ -39,24 +39,36 @@ __all__ = ['Meter', 'trace_range', 'StreamConfig', 'get_logger', 'ensure_hw_queu
 DEFAULT_HW_QUEUES = 8
 
 
-def ensure_hw_queues(n: int = DEFAULT_HW_QUEUES) -> int:
-    """Raise ``GPU_MAX_HW_QUEUES`` to at least ``n`` for this process (and
-    the processes it starts) unless ``BT_HW_QUEUES`` pins a value.  Only
+def ensure_hw_queues(n: int = DEFAULT_HW_QUEUES, exact: bool = False) -> int:
+    """Set ``GPU_MAX_HW_QUEUES`` for this process (and the processes it
+    starts) unless ``BT_HW_QUEUES`` pins a value (1..32, the runtime refuses
+    more).  ``exact=False`` raises an inherited count to at least ``n``;
+    ``exact=True`` sets exactly ``n`` -- for a graphed training step, which an
+    inherited 8 slows by 27 % (the warning names the override).  Only
     effective before the HIP runtime initialises (the first GPU call), so
     call it at program start.  Returns the value in force."""
     pinned = os.environ.get('BT_HW_QUEUES')
     if pinned:
-        os.environ['GPU_MAX_HW_QUEUES'] = str(int(pinned))
-    else:
         try:
-            cur = int(os.environ.get('GPU_MAX_HW_QUEUES', '4'))
+            v = int(pinned)
         except ValueError:
-            cur = 4
-        if cur < n:
-            os.environ['GPU_MAX_HW_QUEUES'] = str(int(n))
-        else:
-            return cur   # (unset: HIP's default, 4)
-    return int(os.environ['GPU_MAX_HW_QUEUES'])
+            raise ValueError(f'BT_HW_QUEUES={pinned!r}: expected an integer 1..32') from None
+        if not 1 <= v <= 32:
+            raise ValueError(f'BT_HW_QUEUES={v}: the HIP runtime accepts 1..32 hardware queues')
+        os.environ['GPU_MAX_HW_QUEUES'] = str(v)
+        return v
+    n = max(1, min(32, int(n)))
+    raw = os.environ.get('GPU_MAX_HW_QUEUES')
+    try:
+        cur = int(raw) if raw else 4     # unset: HIP's default, 4
+    except ValueError:
+        cur = 4
+    if exact and raw and cur != n:
+        logger.warning('GPU_MAX_HW_QUEUES=%s inherited; this process uses %d (BT_HW_QUEUES pins a value)', raw, n)
+    if cur < n or (exact and cur != n):
+        os.environ['GPU_MAX_HW_QUEUES'] = str(n)
+        return n
+    return cur
 
 
 def get_logger():

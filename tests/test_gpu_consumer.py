@@ -401,7 +401,7 @@ def test_captured_step_group_of_four_steps_trains_like_single_steps(dev):
         m = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
         opt = ops.FusedAdam(m.parameters(), lr=2e-4)
         step = CapturedStep(m, opt, lambda mm, x: mm.bce_loss_bf16(x, 1.0), allreduce=False, graph=True,
-                            static_inputs=4, group_steps=n)
+                            static_inputs=4, group_steps=n, reuse_distance=4)   # bufs are never rewritten
         held = sum(step(bufs[k % 4]) is None for k in range(7))
         if n == 4:
             assert held == 5 and len(step._groups) == 1 and len(step._held) == 2
@@ -412,6 +412,54 @@ def test_captured_step_group_of_four_steps_trains_like_single_steps(dev):
     lr = 2e-4
     for pa, pb in zip(nets[0].parameters(), nets[1].parameters()):
         assert float((pb - pa).detach().abs().mean()) < 0.15 * lr
+
+
+def test_captured_step_group_keeps_every_loss_and_guards_held_inputs(dev):
+    """group_steps=2: last_losses() holds both steps' losses of a pair replay,
+    equal to single steps' losses; an input rewritten in place while held
+    (``x.copy_(batch); step(x)``) raises instead of training twice on the
+    later data; group_steps above the reuse distance is refused; a pending
+    held step runs before state_dict()."""
+    from blendtorch.models import Discriminator
+    from blendtorch.parallel.step import CapturedStep
+    cl = torch.channels_last
+    g = torch.Generator(device=dev).manual_seed(5)
+    bufs = [torch.rand(4, 4, 96, 128, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+            for _ in range(2)]
+    per_step = {}
+    for n in (1, 2):
+        torch.manual_seed(0)
+        m = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
+        opt = ops.FusedAdam(m.parameters(), lr=2e-4)
+        step = CapturedStep(m, opt, lambda mm, x: mm.bce_loss_bf16(x, 1.0), allreduce=False, graph=True,
+                            static_inputs=4, group_steps=n)
+        got = []
+        for k in range(5):
+            out = step(bufs[k % 2])
+            if out is not None:
+                got.extend(float(v) for v in step.last_losses())
+        assert step.flush() is None           # 5 steps: capture + two pairs, nothing held
+        per_step[n] = got
+    assert len(per_step[1]) == len(per_step[2]) == 5, per_step
+    torch.testing.assert_close(torch.tensor(per_step[2]), torch.tensor(per_step[1]), rtol=2e-3, atol=1e-4)
+    # in-place rewrite of a held input
+    torch.manual_seed(0)
+    m = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
+    opt = ops.FusedAdam(m.parameters(), lr=2e-4)
+    step = CapturedStep(m, opt, lambda mm, x: mm.bce_loss_bf16(x, 1.0), allreduce=False, graph=True,
+                        static_inputs=4, group_steps=2)
+    x = bufs[0].clone()
+    step(x)                                   # capture + first step
+    assert step(x) is None                    # held
+    x.copy_(bufs[1])
+    with pytest.raises(RuntimeError, match='modified in place'):
+        step(x)
+    # a held step runs before the checkpoint
+    assert step(bufs[0]) is None and step._held
+    m.state_dict()
+    assert not step._held and len(step.last_losses()) == 1
+    with pytest.raises(ValueError, match='reuse distance'):
+        CapturedStep(m, opt, lambda mm, x: mm.bce_loss_bf16(x, 1.0), allreduce=False, static_inputs=4, group_steps=3)
 
 
 def test_captured_step_never_replays_for_another_layout(dev):

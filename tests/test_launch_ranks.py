@@ -157,6 +157,14 @@ def test_eight_ranks_under_16_cpu_quota_get_cost_justified_producers(tmp_path):
     assert one['producers'] == 5
     # more CPU per frame in the consumer leaves fewer cores to producers
     assert producers_for_share(2, frame, consumer_us=150.0) == 1
+    # the costs follow the frame size: exact at the headline frame, per-message
+    # part fixed (a 4x larger frame needs more producer cores on the same share)
+    from blendtorch.parallel.topology import frame_costs_us
+    assert frame_costs_us(frame) == (PRODUCER_US_PER_FRAME, CONSUMER_US_PER_FRAME)
+    big, small = frame_costs_us(4 * frame), frame_costs_us(64 * 64 * 3)
+    assert big[0] > 3 * PRODUCER_US_PER_FRAME and 10.0 <= small[0] < 11.0
+    # 4 CPUs, 4x frames: link-bound at 10.5k frames/s x 230 us = 2.4 cores, x1.5 -> 4
+    assert producers_for_share(4, 4 * frame) == 4
 
 
 def test_hung_rank_is_stopped(tmp_path):

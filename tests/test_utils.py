@@ -80,6 +80,22 @@ def test_ensure_hw_queues_raises_but_never_lowers(monkeypatch):
     assert ensure_hw_queues(4) == 4 and 'GPU_MAX_HW_QUEUES' not in os.environ   # HIP's default already
 
 
+def test_ensure_hw_queues_exact_and_pin_range(monkeypatch):
+    """exact=True (graphed training steps) overrides an inherited larger count;
+    BT_HW_QUEUES outside 1..32 is refused (the runtime would reject it)."""
+    import pytest
+    from blendtorch.utils import ensure_hw_queues
+    monkeypatch.delenv('BT_HW_QUEUES', raising=False)
+    monkeypatch.setenv('GPU_MAX_HW_QUEUES', '8')
+    assert ensure_hw_queues(4, exact=True) == 4 and os.environ['GPU_MAX_HW_QUEUES'] == '4'
+    monkeypatch.delenv('GPU_MAX_HW_QUEUES')
+    assert ensure_hw_queues(4, exact=True) == 4
+    for bad in ('0', '33', 'x'):
+        monkeypatch.setenv('BT_HW_QUEUES', bad)
+        with pytest.raises(ValueError):
+            ensure_hw_queues(4)
+
+
 def test_save_image_matches_torchvision_grid_rules(tmp_path):
     """PNG grids as torchvision.utils.save_image(normalize=True) writes them
     (the densityopt example's image output): min-max over the batch, tiles in
