@@ -355,7 +355,10 @@ def test_device_loader_end_to_end_integrity(dev, free_port, launch_depth):
     for btid, seqs in seen.items():
         assert len(seqs) == len(set(seqs))             # no duplicates
         assert sorted(seqs) == seqs                     # per-producer order preserved
-    assert st['direct_batches'] > 0
+    # fair fan-in puts inline frames (heap-received: below the pinned pool's
+    # 64 KB threshold) into every batch, so batches take the copy path; the
+    # shm frames were read in place or DMA'd from the registered ring
+    assert st['shm_frames'] > 0 and st['batches'] == 750
 
 
 _MATRIX = [
