@@ -176,6 +176,7 @@ def run(args):
         step.start()
         s = fetch()
         update_simulations(remotes, s[0], s[1], ids)
+        step.prefetch()        # the D step's real-batch half runs while the producers render
         history = []
         d_steps = s_steps = 0
         # rank 0 writes the reference's outputs: image grids of the target and
@@ -190,9 +191,11 @@ def run(args):
         pending = []
         # steady state: iterations after the warm-up / capture ones, timed per phase
         steady_from = max(args.steady_skip, step.warmup + 2)
-        ph = dict.fromkeys(('sim_wait', 'step_enqueue', 'fetch', 'send', 'images', 'gpu_iteration'), 0.0)
-        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if pin else None
+        ph = dict.fromkeys(('sim_wait', 'step_enqueue', 'fetch', 'send', 'prefetch', 'images', 'gpu_iteration',
+                            'gpu_real_half'), 0.0)
+        ev = tuple(torch.cuda.Event(enable_timing=True) for _ in range(4)) if pin else None
         n_steady, t_steady = 0, None
+        real_rec = False       # ev[2:] hold a prefetched real half whose time is not yet read
         t0 = time.time()
         wait_s = 0.0
         epoch = 0
@@ -215,8 +218,18 @@ def run(args):
             tc = time.perf_counter()
             s = fetch()
             td = time.perf_counter()
+            if real_rec:       # fetch() synchronised: the real half prefetched last iteration is done
+                ph['gpu_real_half'] += ev[2].elapsed_time(ev[3]) * 1e-3
+                real_rec = False
             update_simulations(remotes, s[0], s[1], ids)
             te = time.perf_counter()
+            if ev is not None and steady:
+                ev[2].record()
+            step.prefetch()
+            if ev is not None and steady:
+                ev[3].record()
+                real_rec = True
+            tp = time.perf_counter()
             d_steps += int(host_stats[2] > 0)
             s_steps += int(host_stats[3] > 0)
             history.append(host_params.clone())
@@ -237,7 +250,8 @@ def run(args):
                 ph['step_enqueue'] += tc - tb
                 ph['fetch'] += td - tc
                 ph['send'] += te - td
-                ph['images'] += tf - te
+                ph['prefetch'] += tp - te
+                ph['images'] += tf - tp
                 if ev is not None:
                     ph['gpu_iteration'] += ev[0].elapsed_time(ev[1]) * 1e-3   # fetch() synchronised
             if epoch > args.num_epochs:
@@ -271,6 +285,7 @@ def run(args):
             }
             if ev is None:
                 res['steady']['ms_per_iteration'].pop('gpu_iteration')
+                res['steady']['ms_per_iteration'].pop('gpu_real_half')
         # the reference's record of convergence: parameter history with the
         # target appended as the last row (densityopt.py:326-331, 350-354)
         hist = torch.stack(history + [tgt]).numpy()

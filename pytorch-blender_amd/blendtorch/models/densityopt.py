@@ -25,9 +25,11 @@ The reference loop (examples/densityopt/densityopt.py:257-331) per iteration:
   way, so every rank takes identical decisions; rank 0's parameter samples
   are broadcast (the reference's ``torch.chunk`` partition of work over
   instances, with one chunk per rank -- densityopt.py:95-107);
-* after warm-up iterations the whole iteration is captured in one HIP graph
-  and replayed; the caller makes ONE device->host copy per iteration: the
-  parameters its producers must render next.
+* after warm-up iterations the iteration is captured as two HIP graphs and
+  replayed: the real-batch half of the D step (it needs only the previous
+  iteration's weights: :meth:`prefetch` enqueues it while the producers
+  render) and the rest; the caller makes ONE device->host copy per
+  iteration: the parameters its producers must render next.
 
 Everything also runs eagerly on the CPU (fp32, gloo) for the test suite.
 """
@@ -87,7 +89,10 @@ class DensityOptStep:
         self.params_out = torch.zeros(4, device=dev)    # pm.readable_params() after the step
         self.graph_enabled = graph and dev.type == 'cuda'
         self.warmup = int(warmup)
-        self.graph = None
+        self.graph = None          # the sim half (the iteration's remainder) once captured
+        self.graph_real = None     # the real half
+        self._real_done = False    # prefetch() ran the real half of the coming iteration
+        self.p_real_mean = torch.zeros(1, device=dev)
         self.iterations = 0
 
     # -- helpers ------------------------------------------------------------------
@@ -112,15 +117,23 @@ class DensityOptStep:
                 self.comm.broadcast_(self.samples, 0)
 
     # -- the iteration ---------------------------------------------------------------
-    def _iteration(self):
-        # 1. discriminator step, gated on the device
+    def _real_half(self):
+        """The D step's target-batch half: forward + backward on the resident
+        real batch.  It depends only on the weights the previous iteration
+        left, not on the simulated batch, so :meth:`prefetch` can run it while
+        the producers still render (reference order kept: real, then sim)."""
         self.gd.zero_()
         loss_r, p_real = self._score(self.real, 1.0)
         loss_r.backward()
+        with torch.no_grad():
+            self.p_real_mean.copy_(p_real.mean().reshape(1))
+
+    def _sim_half(self):
+        # 1. discriminator step (sim half), gated on the device
         loss_s, p_sim = self._score(self.sim, 0.0)
         loss_s.backward()
         with torch.no_grad():
-            self.stats.copy_(torch.stack([p_real.mean(), p_sim.mean()]))
+            self.stats.copy_(torch.cat([self.p_real_mean, p_sim.mean().reshape(1)]))
             self._avg(self.stats)
             self.gate_d.copy_((self.stats[0:1] - self.stats[1:2] < self.threshold).float())
         if self.comm is not None:
@@ -148,10 +161,37 @@ class DensityOptStep:
         # 3. parameters for the next images
         self._sample_into()
 
+    def _iteration(self):
+        self._real_half()
+        self._sim_half()
+
     def start(self):
         """Draw the first parameter samples (before any sim batch exists)."""
         self._sample_into()
         return self.samples
+
+    def _side(self, fn):
+        """Warm-up work on a side stream (allocator pools, first-use setup)."""
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            fn()
+        torch.cuda.current_stream(self.device).wait_stream(side)
+
+    def prefetch(self):
+        """Enqueue the next iteration's real-batch half now (call it after
+        sending the parameters, while the producers render): its GPU time
+        leaves the critical path between the sim batch's arrival and the
+        next parameters.  Optional -- :meth:`__call__` runs it otherwise."""
+        if self._real_done:
+            return
+        if self.graph is not None:
+            self.graph_real.replay()
+        elif self.graph_enabled:
+            self._side(self._real_half)
+        else:
+            self._real_half()
+        self._real_done = True
 
     def __call__(self, sim: torch.Tensor, shape_id: torch.Tensor):
         """One iteration on a simulated batch and its global sample ids.
@@ -162,29 +202,33 @@ class DensityOptStep:
         self.sim.copy_(sim)
         self.shape_id.copy_(shape_id, non_blocking=True)
         if self.graph is not None:
+            self.prefetch()
             self.graph.replay()
         elif self.graph_enabled and self.iterations >= self.warmup:
             self._capture_and_replay()
         elif self.graph_enabled:
-            # warm-up iterations on a side stream (allocator pools, first-use setup)
-            side = torch.cuda.Stream(self.device)
-            side.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(side):
-                self._iteration()
-            torch.cuda.current_stream(self.device).wait_stream(side)
+            self.prefetch()
+            self._side(self._sim_half)
         else:
-            self._iteration()
+            self.prefetch()
+            self._sim_half()
+        self._real_done = False
         self.iterations += 1
         return self.samples
 
     def _capture_and_replay(self):
-        g = torch.cuda.CUDAGraph()
-        # capture records without running: the iteration then runs as its first replay.
+        # capture records without running: each half then runs as its first replay
+        # (the real half only if prefetch() has not run it for this iteration).
         # thread_local: the stream loader's worker thread keeps making HIP calls
-        with torch.cuda.graph(g, capture_error_mode='thread_local'):
-            self._iteration()
-        self.graph = g
-        g.replay()
+        ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(ga, capture_error_mode='thread_local'):
+            self._real_half()
+        with torch.cuda.graph(gb, pool=ga.pool(), capture_error_mode='thread_local'):
+            self._sim_half()
+        self.graph_real, self.graph = ga, gb
+        if not self._real_done:
+            ga.replay()
+        gb.replay()
 
     def my_samples(self, samples: Optional[torch.Tensor] = None):
         """This rank's chunk of the samples ([2, B]) and their global ids."""

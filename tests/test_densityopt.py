@@ -37,7 +37,8 @@ def _free_port():
 def test_step_matches_reference_rules_cpu():
     """Eager CPU iterations of DensityOptStep against the reference's host
     logic (D step iff D_real - D_sim < 0.7; S step unless first and not yet
-    separated; baseline = first errS mean, then an EMA)."""
+    separated; baseline = first errS mean, then an EMA).  Every other
+    iteration runs its real-batch half ahead through prefetch()."""
     from blendtorch.models import Discriminator, ProbModel
     from blendtorch.models.densityopt import DensityOptStep
     import torch.nn as nn
@@ -58,6 +59,8 @@ def test_step_matches_reference_rules_cpu():
         samples = {'m1': step.samples[0].clone(), 'm2': step.samples[1].clone()}
         sim = torch.rand(B, 3, 64, 64, generator=g) * 2 - 1
         sid = torch.randperm(B, generator=g)
+        if it % 2:
+            step.prefetch()     # the real half enqueued ahead (while producers render): same iteration
         step(sim, sid)
         # reference transcription (densityopt.py:257-316)
         netB.zero_grad()
