@@ -316,6 +316,42 @@ def test_densityopt_step_captures_and_replays(dev):
     assert bool(torch.isfinite(step.params_out).all())
 
 
+def test_densityopt_step_prefetch_matches_inline(dev):
+    """DensityOptStep.prefetch(): the real-batch half replayed from its own
+    graph ahead of the sim batch trains exactly like the inline iteration
+    (warm-up, capture and replays; same inputs, same seeds)."""
+    from blendtorch.models import Discriminator, ProbModel
+    from blendtorch.models.densityopt import DensityOptStep
+    B = 64
+    outs = []
+    for pre in (False, True):
+        torch.manual_seed(0)
+        netD = Discriminator().to(dev).to(memory_format=torch.channels_last)
+        pm = ProbModel([1.2, 3.0], [0.4, 0.4]).to(dev)
+        g = torch.Generator(device=dev).manual_seed(3)
+
+        def batch():
+            return (torch.rand(B, 64, 64, 4, device=dev, generator=g) * 2 - 1).to(torch.bfloat16).permute(0, 3, 1, 2)
+
+        step = DensityOptStep(netD, pm, batch().clone(), B, graph=True, warmup=2)
+        torch.manual_seed(1)
+        step.start()
+        sids = torch.Generator().manual_seed(4)
+        hist = []
+        for i in range(7):
+            sim = batch()
+            if pre:
+                step.prefetch()
+            step(sim, torch.randperm(B, generator=sids))
+            hist.append(step.params_out.clone())
+        torch.cuda.synchronize()
+        assert step.graph is not None and step.graph_real is not None
+        outs.append((torch.stack(hist), [p.detach().clone() for p in netD.parameters()]))
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-5, atol=1e-6)
+    for a, b in zip(outs[0][1], outs[1][1]):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+
+
 def test_captured_step_static_inputs_read_in_place(dev):
     """CapturedStep(static_inputs=N): one graph per input tensor, reading it
     in place (no copy into a static buffer) -- trains like the copy path over
