@@ -69,6 +69,13 @@ def short(name):
     return re.sub(r'\(.*$', '', n).strip()
 
 
+def base(name):
+    """Kernel name without template arguments (the eager step's variants of a
+    graphed kernel, e.g. conv1_fwd_kernel<32, 2, false> for <32, 2, true>,
+    stand in for it: the PMC passes run eager steps)."""
+    return name.split('<')[0]
+
+
 def read_sequence(path):
     seq = []
     with open(path) as f:
@@ -98,7 +105,7 @@ def per_position(seq, pmc):
     """Average counters per step position: in every pass, dispatches in order
     are matched greedily against the position sequence (steps start at the
     first kernel's name; other kernels of the eager step are skipped)."""
-    names = [n for n, _ in seq]
+    names = [base(n) for n, _ in seq]
     acc = [collections.defaultdict(float) for _ in names]
     cnt = [collections.defaultdict(int) for _ in names]
     by_pass = collections.defaultdict(list)
@@ -109,6 +116,7 @@ def per_position(seq, pmc):
         pos = None
         steps = 0
         for _, (nm, ctr) in items:
+            nm = base(nm)
             if nm == names[0]:
                 pos, steps = 0, steps + 1
             if pos is None or pos >= len(names) or steps < 2:   # first step: warm-up
