@@ -176,7 +176,8 @@ def run(args):
         step.start()
         s = fetch()
         update_simulations(remotes, s[0], s[1], ids)
-        step.prefetch()        # the D step's real-batch half runs while the producers render
+        if not args.no_prefetch:
+            step.prefetch()    # the D step's real-batch half runs while the producers render
         history = []
         d_steps = s_steps = 0
         # rank 0 writes the reference's outputs: image grids of the target and
@@ -223,12 +224,13 @@ def run(args):
                 real_rec = False
             update_simulations(remotes, s[0], s[1], ids)
             te = time.perf_counter()
-            if ev is not None and steady:
-                ev[2].record()
-            step.prefetch()
-            if ev is not None and steady:
-                ev[3].record()
-                real_rec = True
+            if not args.no_prefetch:
+                if ev is not None and steady:
+                    ev[2].record()
+                step.prefetch()
+                if ev is not None and steady:
+                    ev[3].record()
+                    real_rec = True
             tp = time.perf_counter()
             d_steps += int(host_stats[2] > 0)
             s_steps += int(host_stats[3] > 0)
@@ -328,6 +330,9 @@ def main(argv=None):
                     help='write real_/sim_samples_ PNG grids every N epochs (reference: 5; 0 = never)')
     ap.add_argument('--steady-skip', default=5, type=int,
                     help='iterations excluded from the steady-state rate (at least warm-up + capture + 1)')
+    ap.add_argument('--no-prefetch', action='store_true',
+                    help='run the D step\'s real-batch half with the rest of the iteration, after the sim batch '
+                         'arrives (round 4\'s order; default: enqueued while the producers render)')
     ap.add_argument('--verbose', action='store_true')
     args = ap.parse_args(argv)
     args.timestr = time.strftime('%Y%m%d_%H%M%S')

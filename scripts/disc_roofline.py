@@ -10,7 +10,7 @@ Inputs:
 
 Per position it prints: analytic FLOPs and minimum HBM bytes (every operand
 read once, every output written once), measured FETCH_SIZE / WRITE_SIZE per
-DISPATCH (KB counters -> MB), achieved TFLOP/s and TB/s against the MI355X's
+DISPATCH (KB counters -> MB; FETCH_SIZE doubled, see below), achieved TFLOP/s and TB/s against the MI355X's
 dense bf16 peak (2.5 PFLOP/s) and HBM (8 TB/s), VALU and LDS instructions
 per MFMA, and LDS bank conflicts as SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
 (extra cycles over all LDS-array cycles, MI355X_MICROARCH.md section LDS).
@@ -150,7 +150,10 @@ def main():
     for i, (nm, us) in enumerate(seq):
         what, fl, mb = MODEL[i] if i < len(MODEL) else ('?', 0, 0)
         c = ctrs[i] if i < len(ctrs) else {}
-        fetch = c.get('FETCH_SIZE', 0.0) / 1024.0      # KB -> MB
+        # FETCH_SIZE x 2: on this gfx950 / rocprofv3 the counter reads half the
+        # bytes a streaming kernel must read (BN1 apply: 18.9 -> 37.8 MB of the
+        # 39.3 MB it reads; WRITE_SIZE matches the analytic writes as is)
+        fetch = 2.0 * c.get('FETCH_SIZE', 0.0) / 1024.0      # KB -> MB
         write = c.get('WRITE_SIZE', 0.0) / 1024.0
         mf = c.get('SQ_INSTS_MFMA', 0.0)
         lds_act = c.get('SQ_LDS_IDX_ACTIVE', 0.0)
