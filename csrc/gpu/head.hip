@@ -15,7 +15,9 @@
 
 #include <hip/amd_detail/amd_hip_unsafe_atomics.h>
 
+#include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "bn_fold.h"
 #include "kernels.h"
@@ -28,8 +30,8 @@ constexpr int kHeadThreads = 256;
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ int wstart(int i, int in, int out) { return (i * in) / out; }
-__device__ __forceinline__ int wend(int i, int in, int out) { return ((i + 1) * in + out - 1) / out; }
+__host__ __device__ __forceinline__ int wstart(int i, int in, int out) { return (i * in) / out; }
+__host__ __device__ __forceinline__ int wend(int i, int in, int out) { return ((i + 1) * in + out - 1) / out; }
 __device__ __forceinline__ float bf(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
 
 __device__ void head_loss_wave(const HeadParams& p, bool write_through);
@@ -169,6 +171,165 @@ __global__ __launch_bounds__(kHeadThreads) void head_fwd_kernel(HeadParams p) {
   head_loss_wave(p, true);
 }
 
+// The same forward with the BatchNorm applied (act.on()) and the loss ticket,
+// laid out as few memory round trips as possible -- one block per (cell,
+// image), so the kernel is ONE wave of ~128 blocks and its time is a block's
+// latency chain, not bandwidth (round 4: 14.7 us for 4.9 MB).  head_fwd_kernel
+// ran ~8 dependent round trips: the accumulator fold one column at a time,
+// the release ticket, the window in passes of 4 pixels, the partial store, the
+// loss ticket, the release's second counter.  Here:
+//  1. every window pixel of the lane is loaded up front (KMAX 16-byte loads);
+//  2. the accumulator's [R][2C] replicas are read as one flat array, 8 doubles
+//     per thread, all in flight with the pixels; LDS folds the replicas;
+//  3. the release's shard ticket goes out as soon as those reads are back,
+//     its answer is only needed at the end;
+//  4. the partial logit's store and the loss ticket (and, for the last block
+//     of a shard, the release's top counter) are one more round trip.
+// Same arithmetic per element as head_fwd_kernel (bit-identical pooled values
+// and partials: the per-channel sums run in the same lane / pixel order).
+constexpr int kHeadFlat = 8;   // accumulator doubles per thread: 2 C R = 2048 (bn_acc_replicas) over 256 threads
+
+template <int KMAX>
+__global__ __launch_bounds__(kHeadThreads) void head_fwd_act_kernel(HeadParams p) {
+  __shared__ float red[kHeadThreads / 64];
+  __shared__ float acc_l[kHeadThreads * 8];
+  __shared__ double fold[kHeadThreads * kHeadFlat];   // the [R][2C] replicas, then the column sums
+  __shared__ __attribute__((aligned(16))) float coef[2 * kBnFoldMaxC];
+  __shared__ int flags[2];
+  const int cell = int(blockIdx.x), n = int(blockIdx.y);
+  const int i = cell / p.OW, j = cell - i * p.OW;
+  const int h0 = wstart(i, p.H, p.OH), h1 = wend(i, p.H, p.OH);
+  const int w0 = wstart(j, p.W, p.OW), w1 = wend(j, p.W, p.OW);
+  const int ww = w1 - w0, npx = (h1 - h0) * ww;
+  const float inv = 1.f / float(npx);
+  const int t = int(threadIdx.x);
+  const int G = p.C / 8, g = t % G, pl = t / G, PL = kHeadThreads / G;
+  // 1. the lane's window pixels (k = pl + PL u), all loads in flight
+  uint4 v[KMAX];
+#pragma unroll
+  for (int u = 0; u < KMAX; ++u) {
+    const int k = pl + u * PL;
+    const int kk = k < npx ? k : pl;   // past the window: a re-read, added as 0 below
+    const int h = h0 + kk / ww, w = w0 + kk % ww;
+    v[u] = *reinterpret_cast<const uint4*>(p.z + (int64_t(n * p.H + h) * p.W + w) * p.C + g * 8);
+  }
+  // 2. the accumulator, flat: element e = t + 256 q of [R][2C]
+  const int J = 2 * p.C, RJ = p.act.R * J;
+  double a8[kHeadFlat];
+#pragma unroll
+  for (int q = 0; q < kHeadFlat; ++q) {
+    const int e = t + kHeadThreads * q;
+    a8[q] = e < RJ ? p.act.acc[e] : 0.0;
+  }
+#pragma unroll
+  for (int q = 0; q < kHeadFlat; ++q) fold[t + kHeadThreads * q] = a8[q];
+  __syncthreads();
+  // 3. every read of the accumulator is back: the release's shard ticket (answer used at the end)
+  const unsigned nblk = gridDim.x * gridDim.y, blk = blockIdx.y * gridDim.x + blockIdx.x;
+  unsigned* ticket = bn_acc_ticket(p.act.acc, p.act.R, p.C);
+  const unsigned shard = blk % kBnTicketShards;
+  unsigned shard_old = 0;
+  if (t == 0) shard_old = atomicAdd(ticket + shard * kBnTicketStride, 1u);
+  // column sums in bn_acc_column_sums' order (groups g of replicas g, g + GR, ..., then the groups in
+  // order: the same fp64 values, so the same mean / invstd as the other fold sites)
+  {
+    const int GR = J >= kHeadThreads ? 1 : kHeadThreads / J;
+    for (int c = t; c < J; c += kHeadThreads) {
+      double s = 0.0;
+      for (int gg = 0; gg < GR; ++gg) {
+        double sg = 0.0;
+        for (int r = gg; r < p.act.R; r += GR) sg += fold[r * J + c];
+        s = gg == 0 ? sg : s + sg;
+      }
+      fold[c] = s;   // row 0 of the replicas, column c: read only by this thread (above)
+    }
+  }
+  __syncthreads();
+  BnFwdFinal f;
+  f.eps = p.act.eps, f.momentum = p.act.momentum, f.mean = p.act.mean, f.invstd = p.act.invstd;
+  f.rm = p.act.rm, f.rv = p.act.rv, f.tracked = p.act.tracked;
+  const bool first = blockIdx.x == 0 && blockIdx.y == 0;
+  // mean / invstd in a lane-major order (channel 8 g + k at 4 g + k, k < 4, or
+  // 4 G + 4 g + k - 4): a lane's 8 channels are two conflict-free 16-byte reads
+  for (int c = t; c < p.C; c += kHeadThreads) {
+    const int gg = c >> 3, k = c & 7, pc = k < 4 ? 4 * gg + k : 4 * G + 4 * gg + k - 4;
+    bn_fwd_finalize(f, fold, p.C, p.act.M, c, first, coef[pc], coef[p.C + pc]);
+  }
+  __syncthreads();
+  float is[8], nm[8], aw[8], ab[8];
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    const float4 mu = *reinterpret_cast<const float4*>(coef + 4 * hh * G + 4 * g);
+    const float4 iv = *reinterpret_cast<const float4*>(coef + p.C + 4 * hh * G + 4 * g);
+    const float m4[4] = {mu.x, mu.y, mu.z, mu.w}, i4[4] = {iv.x, iv.y, iv.z, iv.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int q = 4 * hh + k;
+      is[q] = i4[k];
+      nm[q] = -m4[k] * is[q];
+      aw[q] = p.act.w[g * 8 + q];
+      ab[q] = p.act.b[g * 8 + q];
+    }
+  }
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < KMAX; ++u) {
+    if (pl + u * PL >= npx) break;
+    const uint32_t uu[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float z0 = fmaf(fmaf(__uint_as_float(uu[q] << 16), is[2 * q], nm[2 * q]), aw[2 * q], ab[2 * q]);
+      const float z1 = fmaf(fmaf(__uint_as_float(uu[q] & 0xFFFF0000u), is[2 * q + 1], nm[2 * q + 1]), aw[2 * q + 1],
+                            ab[2 * q + 1]);
+      const f32x2 pr = {z0 > 0.f ? z0 : z0 * p.act.slope, z1 > 0.f ? z1 : z1 * p.act.slope};
+      const uint32_t r = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2));
+      a[2 * q] += __uint_as_float(r << 16);
+      a[2 * q + 1] += __uint_as_float(r & 0xFFFF0000u);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) acc_l[pl * p.C + g * 8 + q] = a[q];
+  __syncthreads();
+  float part = 0.f;
+  for (int c = t; c < p.C; c += kHeadThreads) {
+    float s = 0.f;
+    for (int l = 0; l < PL; ++l) s += acc_l[l * p.C + c];
+    const float pooled = s * inv;
+    p.pooled[(int64_t(n) * p.OH * p.OW + cell) * p.C + c] = pooled;
+    part += pooled * p.w[c * p.ws_c + i * p.ws_i + j * p.ws_j];
+  }
+  for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+  if ((t & 63) == 0) red[t >> 6] = part;
+  __syncthreads();
+  // 4. partial logit (write-through), then the loss ticket and -- for the
+  // shard's last block -- the release's top counter, in one round trip
+  if (t == 0) {
+    float s = 0.f;
+    for (int k = 0; k < kHeadThreads / 64; ++k) s += red[k];
+    __hip_atomic_store(p.partial + n * p.OH * p.OW + cell, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the partial is visible; the shard ticket is back
+    const unsigned in_shard = (nblk - shard + kBnTicketShards - 1) / kBnTicketShards;
+    const unsigned shards = nblk < unsigned(kBnTicketShards) ? nblk : unsigned(kBnTicketShards);
+    const bool shard_last = shard_old == in_shard - 1;
+    const uint32_t tk = __hip_atomic_fetch_add(p.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned top_old = 0;
+    if (shard_last) {
+      ticket[shard * kBnTicketStride] = 0u;   // every block of this shard has taken its ticket
+      top_old = atomicAdd(ticket + kBnTicketShards * kBnTicketStride, 1u);
+    }
+    const bool loss_last = tk == nblk - 1;
+    if (loss_last) __hip_atomic_store(p.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flags[0] = shard_last && top_old == shards - 1;
+    flags[1] = loss_last;
+  }
+  __syncthreads();
+  if (flags[0]) {   // every block has read the accumulator: clear it for the next producer
+    for (int e = t; e < RJ; e += kHeadThreads) p.act.acc[e] = 0.0;
+    if (t == 0) ticket[kBnTicketShards * kBnTicketStride] = 0u;
+  }
+  if (flags[1] && t < 64) head_loss_wave(p, true);
+}
+
 // one wave: logits, sigmoid, mean BCE, and dlogit/g for the backward
 __device__ void head_loss_wave(const HeadParams& p, bool wt) {
   const int cells = p.OH * p.OW;
@@ -203,7 +364,7 @@ __global__ __launch_bounds__(64) void head_loss_kernel(HeadParams p) { head_loss
 // With p.bn_acc the dz blocks also sum the producing BatchNorm+LeakyReLU
 // backward's gz and gz * xhat per channel; the block folds its lanes through
 // LDS and adds its 2 C sums into replica blockIdx % R of the fp64 accumulator.
-constexpr int kHeadImgs = 4;   // images per pass (loads in flight per lane)
+constexpr int kHeadImgs = 8;   // images per pass (loads in flight per lane: the bench's whole batch)
 
 __global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p, int nbwd) {
   const int t = int(threadIdx.x);
@@ -215,7 +376,20 @@ __global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p, in
     for (int e = (int(blockIdx.x) - nbwd) * kHeadThreads + t; e < total; e += nw * kHeadThreads) {
       const int c = e % p.C, cell = e / p.C;
       float s = 0.f;
-      for (int n = 0; n < p.N; ++n) s += p.dlogit[n] * p.pooled[(int64_t(n) * cells + cell) * p.C + c];
+      // 8 images per pass with every load in flight (a rolled loop waited out
+      // one load latency per image), summed in image order as before
+      for (int n0 = 0; n0 < p.N; n0 += 8) {
+        float dl[8], pv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int n = n0 + u < p.N ? n0 + u : n0;
+          dl[u] = p.dlogit[n];
+          pv[u] = p.pooled[(int64_t(n) * cells + cell) * p.C + c];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (n0 + u < p.N) s += dl[u] * pv[u];
+      }
       const int i = cell / p.OW, j = cell - i * p.OW;
       p.dw[c * p.ws_c + i * p.ws_i + j * p.ws_j] = g * s;
     }
@@ -229,19 +403,32 @@ __global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p, in
   const bool bnf = p.bn_acc != nullptr;
   float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (live) {
+    // the pooling windows holding (h, w): with OH <= H (OW <= W) at most two
+    // per dimension, i0 and i0 + 1 (j0, j0 + 1) -- all four candidates' weights
+    // are loaded at once (a window at a time waited out a load latency each),
+    // then added in the window order of the loop this replaces
     const int i0 = (h * p.OH) / p.H, i1 = ((h + 1) * p.OH + p.H - 1) / p.H;
     const int j0 = (w * p.OW) / p.W, j1 = ((w + 1) * p.OW + p.W - 1) / p.W;
-    for (int i = i0; i < i1 && i < p.OH; ++i) {
-      const int hs = wstart(i, p.H, p.OH), he = wend(i, p.H, p.OH);
-      if (h < hs || h >= he) continue;
-      for (int j = j0; j < j1 && j < p.OW; ++j) {
-        const int ws = wstart(j, p.W, p.OW), we = wend(j, p.W, p.OW);
-        if (w < ws || w >= we) continue;
-        const float area = float((he - hs) * (we - ws));
+    float wv[4][8];
+    bool in[4];
+    float area[4];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) m[k] += p.w[(c0 + k) * p.ws_c + i * p.ws_i + j * p.ws_j] / area;
-      }
+    for (int q = 0; q < 4; ++q) {
+      const int i = i0 + (q >> 1), j = j0 + (q & 1);
+      const int hs = wstart(i, p.H, p.OH), he = wend(i, p.H, p.OH);
+      const int ws = wstart(j, p.W, p.OW), we = wend(j, p.W, p.OW);
+      in[q] = i < i1 && i < p.OH && j < j1 && j < p.OW && h >= hs && h < he && w >= ws && w < we;
+      area[q] = float((he - hs) * (we - ws));
+      const int ic = in[q] ? i : 0, jc = in[q] ? j : 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) wv[q][k] = p.w[(c0 + k) * p.ws_c + ic * p.ws_i + jc * p.ws_j];
     }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (in[q]) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) m[k] += wv[q][k] / area[q];
+      }
   }
   float is[8], nm[8], bw[8], bb[8], bs[8], bq[8];
 #pragma unroll
@@ -307,7 +494,19 @@ __global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p, in
   }
 }
 
+// BT_HEAD_FWD=0 (or head_set_fast(0)): round 4's head_fwd_kernel for the BN-applying forward too (A/B)
+int g_head_fast = -1;
+bool head_fwd_fast() {
+  if (g_head_fast < 0) {
+    const char* e = std::getenv("BT_HEAD_FWD");
+    g_head_fast = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_head_fast != 0;
+}
+
 }  // namespace
+
+void head_set_fast(int on) { g_head_fast = on < 0 ? -1 : (on ? 1 : 0); }
 
 hipError_t head_forward(const HeadParams& p, hipStream_t stream) {
   if (p.N <= 0 || p.C <= 0 || p.OH <= 0 || p.OW <= 0 || p.H < p.OH || p.W < p.OW || !p.z || !p.w || !p.pooled ||
@@ -320,13 +519,27 @@ hipError_t head_forward(const HeadParams& p, hipStream_t stream) {
         p.act.M != int64_t(p.N) * p.H * p.W)
       return hipErrorInvalidValue;
   }
-  head_fwd_kernel<<<dim3(unsigned(p.OH * p.OW), unsigned(p.N)), kHeadThreads, 0, stream>>>(p);
+  const dim3 grid(unsigned(p.OH * p.OW), unsigned(p.N));
+  if (p.act.on() && p.ticket && head_fwd_fast() && int64_t(2) * p.C * p.act.R <= kHeadThreads * kHeadFlat) {
+    // the round-trip-lean form: every window pixel of a lane loaded up front
+    int most = 0;   // the largest pooling window
+    for (int i = 0; i < p.OH; ++i)
+      for (int j = 0; j < p.OW; ++j)
+        most = std::max(most, (wend(i, p.H, p.OH) - wstart(i, p.H, p.OH)) * (wend(j, p.W, p.OW) - wstart(j, p.W, p.OW)));
+    const int pl = kHeadThreads / (p.C / 8);
+    if (most <= 16 * pl) {
+      head_fwd_act_kernel<16><<<grid, kHeadThreads, 0, stream>>>(p);
+      return hipGetLastError();
+    }
+  }
+  head_fwd_kernel<<<grid, kHeadThreads, 0, stream>>>(p);
   if (!p.ticket) head_loss_kernel<<<1, 64, 0, stream>>>(p);
   return hipGetLastError();
 }
 
 hipError_t head_backward(const HeadParams& p, hipStream_t stream) {
   if (p.C % 8 || !p.dz || !p.dw || !p.gscale || !p.dlogit || !p.pooled) return hipErrorInvalidValue;
+  if (p.OH <= 0 || p.OW <= 0 || p.H < p.OH || p.W < p.OW) return hipErrorInvalidValue;   // <= 2 windows per pixel and dimension
   if (reinterpret_cast<uintptr_t>(p.dz) & 15) return hipErrorInvalidValue;
   const int64_t total = int64_t(p.N) * p.H * p.W * (p.C / 8);
   if (total >= (int64_t(1) << 31) - int64_t(kHeadThreads) * 4096) return hipErrorInvalidValue;

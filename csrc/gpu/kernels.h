@@ -546,6 +546,7 @@ struct HeadParams {
   BnActIn act;
 };
 hipError_t head_forward(const HeadParams& p, hipStream_t stream);
+void head_set_fast(int on);   // BN-applying forward: 1 the round-trip-lean kernel (default), 0 round 4's, -1 BT_HEAD_FWD
 hipError_t head_backward(const HeadParams& p, hipStream_t stream);
 
 hipError_t adam_schedule(float* step, const float* hp, float* sched, float beta1, float beta2, hipStream_t stream,

@@ -384,30 +384,41 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const void* __restrict
   // xhat = v * is + nm;  z = xhat * ww + bb;  backward: gx = P * (gz - dbm) - pdw * xhat (BnBwdCoef)
   float is[V], nm[V], ww[V], bb[V];
   BnBwdCoef bc[BWD ? V : 1];
-  const float* s_mean = mean;
-  const float* s_inv = invstd;
-  const float* s_db = db;
-  const float* s_dw = dw;
   if constexpr (FOLD) {
+    // coef holds the two folded per-channel arrays (forward: mean, invstd;
+    // backward: db, dw) in a lane-major order: channel c = V g + k at
+    // 4 g + k (k < 4) or 4 G + 4 g + k - 4 (bf16, V = 8), so the G lanes of a
+    // row read their V channels as 16-byte vectors at consecutive 16-byte
+    // slots -- conflict-free ds_read_b128 (a lane reading its 8 floats one by
+    // one at a 32-byte stride ran 2-4 way conflicted: PMC 30-69 % for C >= 64)
     __shared__ double part[2 * kBnAccMaxC > kBlock ? 2 * kBnAccMaxC : kBlock];
-    __shared__ float coef[2 * kBnAccMaxC];
+    __shared__ __attribute__((aligned(16))) float coef[2 * kBnAccMaxC];
     __shared__ int flag;
+    auto pos = [&](int c) {
+      if constexpr (V == 8) {
+        const int gg = c >> 3, k = c & 7;
+        return k < 4 ? 4 * gg + k : 4 * G + 4 * gg + k - 4;
+      } else {
+        return c;
+      }
+    };
     bn_acc_column_sums(fa.acc, fa.R, 2 * C, part);
     const bool first = blockIdx.x == 0;
     for (int c = int(threadIdx.x); c < C; c += kBlock) {
+      float c0v, c1v;
       if constexpr (BWD) {   // db = sum gz, dw = sum gz * xhat (bn_fold_block, bwd)
-        coef[c] = float(part[c]);
-        coef[C + c] = float(part[C + c]);
-        if (first) fa.o0[c] = coef[c], fa.o1[c] = coef[C + c];
+        c0v = float(part[c]);
+        c1v = float(part[C + c]);
+        if (first) fa.o0[c] = c0v, fa.o1[c] = c1v;
       } else {               // exactly bn_fold_block's forward finalize
         const double mu = part[c] / double(M);
         double var = part[C + c] / double(M) - mu * mu;
         var = var < 0.0 ? 0.0 : var;
-        coef[c] = float(mu);
-        coef[C + c] = float(1.0 / sqrt(var + double(fa.eps)));
+        c0v = float(mu);
+        c1v = float(1.0 / sqrt(var + double(fa.eps)));
         if (first) {
-          fa.o0[c] = coef[c];
-          fa.o1[c] = coef[C + c];
+          fa.o0[c] = c0v;
+          fa.o1[c] = c1v;
           if (fa.rm) {
             fa.rm[c] = float((1.0 - fa.momentum) * fa.rm[c] + fa.momentum * mu);
             fa.rv[c] = float((1.0 - fa.momentum) * fa.rv[c] +
@@ -416,27 +427,44 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const void* __restrict
           if (fa.tracked && c == 0) fa.tracked[0] += 1;
         }
       }
+      coef[pos(c)] = c0v;
+      coef[C + pos(c)] = c1v;
     }
     __syncthreads();
     bn_acc_release(fa.acc, fa.R, C, &flag);
-    if constexpr (BWD) {
-      s_db = coef;
-      s_dw = coef + C;
-    } else {
-      s_mean = coef;
-      s_inv = coef + C;
-    }
-  }
+    const int gl = int(threadIdx.x) % G;   // this lane's channel group: channels V gl .. + V - 1
+    float a0[V], a1[V];
 #pragma unroll
-  for (int i = 0; i < V; ++i) {
-    const int c = c0 + i;
-    if constexpr (BWD) {
-      bc[i].init(s_mean[c], s_inv[c], w[c], b[c], s_dw[c], s_db[c], invM);
-    } else {
-      is[i] = s_inv[c];
-      nm[i] = -s_mean[c] * is[i];
-      ww[i] = w[c];
-      bb[i] = b[c];
+    for (int h = 0; h < V / 4; ++h) {
+      const float4 x0 = *reinterpret_cast<const float4*>(coef + 4 * h * G + 4 * gl);
+      const float4 x1 = *reinterpret_cast<const float4*>(coef + C + 4 * h * G + 4 * gl);
+      a0[4 * h] = x0.x, a0[4 * h + 1] = x0.y, a0[4 * h + 2] = x0.z, a0[4 * h + 3] = x0.w;
+      a1[4 * h] = x1.x, a1[4 * h + 1] = x1.y, a1[4 * h + 2] = x1.z, a1[4 * h + 3] = x1.w;
+    }
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      const int c = c0 + i;
+      if constexpr (BWD) {
+        bc[i].init(mean[c], invstd[c], w[c], b[c], a1[i], a0[i], invM);
+      } else {
+        is[i] = a1[i];
+        nm[i] = -a0[i] * is[i];
+        ww[i] = w[c];
+        bb[i] = b[c];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      const int c = c0 + i;
+      if constexpr (BWD) {
+        bc[i].init(mean[c], invstd[c], w[c], b[c], dw[c], db[c], invM);
+      } else {
+        is[i] = invstd[c];
+        nm[i] = -mean[c] * is[i];
+        ww[i] = w[c];
+        bb[i] = b[c];
+      }
     }
   }
   auto apply = [&](const float (&v)[V], const float (&gv)[V], float (&o)[V]) {

@@ -142,6 +142,43 @@ def test_disc_head_bce_matches_fp32_reference(dev, target, wlayout):
     torch.testing.assert_close(z.grad.float(), zr.grad, rtol=2 ** -7, atol=1e-3 * float(zr.grad.abs().max()))
 
 
+def test_head_fwd_lean_kernel_matches_round4_kernel(dev):
+    """The BN-applying head forward's round-trip-lean kernel (all window loads
+    and the accumulator read up front, combined tickets) gives bit-identical
+    losses, running statistics and gradients to round 4's head_fwd_kernel, and
+    leaves the accumulators cleared (two steps: the second reuses them)."""
+    from blendtorch.models import Discriminator
+    ext = ops.hip_ext()
+    runs = []
+    try:
+        for fast in (1, 0):
+            ext.head_set_fast(fast)
+            torch.manual_seed(0)
+            m = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=torch.channels_last)
+            m.lazy_head_bn = True
+            g = torch.Generator(device=dev).manual_seed(4)
+            out = []
+            for _ in range(2):
+                x = torch.rand(4, 3, 240, 320, device=dev, generator=g).to(torch.bfloat16)
+                x = x.contiguous(memory_format=torch.channels_last)
+                m.zero_grad(set_to_none=True)
+                loss = m.bce_loss_bf16(x, 1.0)
+                loss.backward()
+                out.append(loss.detach().clone())
+            for mod in m.modules():   # every accumulator cleared by the kernels that folded it
+                if isinstance(mod, ops.BatchNormLeakyReLU2d):
+                    for acc in mod.__dict__['_bt_acc_ring'][0]:
+                        assert int(torch.count_nonzero(acc.fwd)) == 0 and int(torch.count_nonzero(acc.bwd)) == 0
+            runs.append((out, [b.clone() for b in m.buffers()], [p.grad.clone() for p in m.parameters()]))
+    finally:
+        ext.head_set_fast(-1)
+    (la, ba, ga), (lb, bb, gb) = runs
+    assert all(torch.equal(x, y) for x, y in zip(la, lb)), (la, lb)
+    assert all(torch.equal(x, y) for x, y in zip(ba, bb))
+    for x, y in zip(ga, gb):   # (the weight-gradient reduce adds with fp32 atomics: order varies)
+        assert float((x - y).abs().max()) <= 1e-2 * float(y.abs().max())
+
+
 def test_discriminator_bce_loss_bf16(dev):
     """The fused-head loss of the whole discriminator equals the unfused
     bf16 forward + BCELoss, and trains the same parameters."""
