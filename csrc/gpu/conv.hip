@@ -130,8 +130,8 @@ __device__ __forceinline__ uint32_t bload4(__amdgpu_buffer_rsrc_t r, uint32_t of
 // stay zero (not table[0]).
 constexpr int kLutBytes = 4 * 256 * 2;
 __device__ __forceinline__ void stage_lut(const uint16_t* lut, char* lds) {
-  const int t = int(threadIdx.x);   // 256 threads x 8 bytes
-  *reinterpret_cast<uint2*>(lds + 8 * t) = *reinterpret_cast<const uint2*>(lut + 4 * t);
+  const int t = int(threadIdx.x);   // 256 threads x 8 bytes (threads past 256: nothing)
+  if (t < 256) *reinterpret_cast<uint2*>(lds + 8 * t) = *reinterpret_cast<const uint2*>(lut + 4 * t);
 }
 __device__ __forceinline__ uint2 lut_px(const char* lds, uint32_t w, bool ok) {
   const uint16_t* l = reinterpret_cast<const uint16_t*>(lds);
@@ -170,6 +170,7 @@ __device__ __forceinline__ void wgrad_reduce_block(const ConvWgradParams::Reduce
   float* __restrict__ out = r.out;
   const int KC = 16 * Cin;
   const int total = r.Cout * KC;
+  if (int(threadIdx.x) >= kThreads) return;   // (a side job of a wider block: 256 lanes do it)
   const int e0 = (bx * kThreads + int(threadIdx.x)) * 4;
   if (e0 >= total) return;
   const int k0 = by * kSliceGroup;
@@ -943,14 +944,21 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4_kernel(ConvWgradParams
 constexpr int C4W_DY = BPX * C4_DY_ROW;          // 2 KiB: [32 px][32 co]
 constexpr int C4W_X = BPX * C4_X_ROW;            // 4 KiB: [32 px][64 kc]
 constexpr int C4W_WAVE = C4W_DY + C4W_X;
-constexpr int C4W_LDS = 4 * 32 * 64 * 4;         // the combine: 4 waves x [32][64] fp32 (32 KiB)
-static_assert(4 * C4W_WAVE + kLutBytes <= C4W_LDS, "staging fits the combine area");
+// NW waves per block (BT_C4W_WAVES, 4 or 8): the kernel is latency-bound --
+// 512 blocks of 4 waves are 2 waves per SIMD, each walking ~9 pixel steps
+// whose loads, LUT lookups and BN-backward arithmetic form one chain -- so 8
+// waves per block double the chains in flight with the same slices (the
+// same partials, the same reduce, the same per-block fold).
+template <int NW>
+constexpr int c4w_lds() { return NW * 32 * 64 * 4; }   // the combine: NW waves x [32][64] fp32
+static_assert(4 * C4W_WAVE + kLutBytes <= c4w_lds<4>(), "staging fits the combine area");
 
-__global__ __launch_bounds__(kThreads) void conv_wgrad_c4w_kernel(ConvWgradParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[C4W_LDS];
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void conv_wgrad_c4w_kernel(ConvWgradParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[c4w_lds<NW>()];
   if (run_side(p, smem)) return;
   const bool u8in = p.lut != nullptr;
-  char* const lutl = smem + 4 * C4W_WAVE;
+  char* const lutl = smem + NW * C4W_WAVE;
   if (u8in) {
     stage_lut(p.lut, lutl);
     __syncthreads();
@@ -964,7 +972,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4w_kernel(ConvWgradParam
   const int m_begin = slice * int(p.px_per_slice);
   const int m_end = m_begin + int(p.px_per_slice) < int(p.M) ? m_begin + int(p.px_per_slice) : int(p.M);
   const int nsteps = m_end > m_begin ? (m_end - m_begin + BPX - 1) / BPX : 0;
-  const int mysteps = nsteps > wave ? (nsteps - wave + 3) / 4 : 0;   // steps wave, wave + 4, ...
+  const int mysteps = nsteps > wave ? (nsteps - wave + NW - 1) / NW : 0;   // steps wave, wave + NW, ...
   char* const ws = smem + wave * C4W_WAVE;
 
   // dY: lane -> channel chunk dc (8 channels), pixels dp and dp + 16 of the step
@@ -986,7 +994,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4w_kernel(ConvWgradParam
   c.init(m_begin + wave * BPX + xp, p.Ho, p.Wo);
   int md = m_begin + wave * BPX + dp, mx = m_begin + wave * BPX + xp;
   uint32_t dy_byte = uint32_t(md) * uint32_t(p.Cout * 2) + uint32_t((co0 + dc * 8) * 2);
-  const uint32_t dy_step = uint32_t(4 * BPX * p.Cout * 2), dy_half = uint32_t(16 * p.Cout * 2);
+  const uint32_t dy_step = uint32_t(NW * BPX * p.Cout * 2), dy_half = uint32_t(16 * p.Cout * 2);
   constexpr int kDepth = 2;
   struct Stage {
     uint4 g[2], y[2];   // dY chunks of pixels dp, dp + 16 (y: the BN input, bnd)
@@ -1019,11 +1027,11 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4w_kernel(ConvWgradParam
         r.x[k][0] = lo.x, r.xh[k][0] = lo.y, r.x[k][1] = hi.x, r.xh[k][1] = hi.y;
       }
     }
-    md += 4 * BPX;
-    mx += 4 * BPX;
+    md += NW * BPX;
+    mx += NW * BPX;
     dy_byte += dy_step;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) c.advance(p.Ho, p.Wo);   // 4 x 32 pixels: this wave's next step
+    for (int k = 0; k < NW; ++k) c.advance(p.Ho, p.Wo);   // NW x 32 pixels: this wave's next step
   };
   auto store = [&](const Stage& r) {
 #pragma unroll
@@ -1095,7 +1103,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4w_kernel(ConvWgradParam
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // fragments in registers before the next store
     }
   }
-  // combine the four waves' tiles: [wave][co 32][kc 64] fp32 in LDS
+  // combine the NW waves' tiles: [wave][co 32][kc 64] fp32 in LDS
   __syncthreads();
   float* cmb = reinterpret_cast<float*>(smem);
 #pragma unroll
@@ -1108,8 +1116,12 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4w_kernel(ConvWgradParam
   __syncthreads();
   zero_output(p);
   float* out = p.partial + int64_t(slice) * p.Cout * 64 + co0 * 64;
-  for (int e = t; e < 32 * 64; e += kThreads)
-    out[e] = cmb[e] + cmb[32 * 64 + e] + cmb[2 * 32 * 64 + e] + cmb[3 * 32 * 64 + e];
+  for (int e = t; e < 32 * 64; e += 64 * NW) {
+    float v = cmb[e];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) v += cmb[w * 32 * 64 + e];   // (wave order: NW = 4 sums as before)
+    out[e] = v;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2428,6 +2440,16 @@ int wgrad_staging() {
 
 namespace {
 int g_c4w = -1;   // first-layer weight gradient: 1 = wave-private staging (default), 0 = block-shared; BT_C4_WAVE
+int g_c4w_waves = -1;   // waves per block of the first layer's weight gradient; -1: BT_C4W_WAVES or the default
+int c4w_waves() {
+  if (g_c4w_waves < 0) {
+    const char* e = std::getenv("BT_C4W_WAVES");
+    const int v = e ? std::atoi(e) : 4;
+    g_c4w_waves = v == 8 ? 8 : 4;
+  }
+  return g_c4w_waves;
+}
+
 bool c4_wave_private() {
   if (g_c4w < 0) {
     const char* v = std::getenv("BT_C4_WAVE");
@@ -2438,6 +2460,7 @@ bool c4_wave_private() {
 }  // namespace
 
 void conv_set_c4_wave_private(int on) { g_c4w = on < 0 ? -1 : (on ? 1 : 0); }
+void conv_set_c4w_waves(int nw) { g_c4w_waves = nw == 4 || nw == 8 ? nw : -1; }
 
 void conv_set_dgrad_patch(int on) { g_dgrad_patch = on < 0 ? -1 : (on ? 1 : 0); }
 void conv_set_wgrad_wide(int on) { g_wgrad_wide = on < 0 ? -1 : (on ? 1 : 0); }
@@ -2511,7 +2534,10 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
   }
   // (a BN backward folded in-kernel: the wave-private first-layer kernel or the register-staged one)
   const bool bn_folds = p.bn_dy.acc != nullptr;
-  if (c4 && (c4_wave_private() || bn_folds)) conv_wgrad_c4w_kernel<<<unsigned(grid), kThreads, 0, stream>>>(q);
+  if (c4 && (c4_wave_private() || bn_folds)) {
+    if (c4w_waves() == 8) conv_wgrad_c4w_kernel<8><<<unsigned(grid), 512, 0, stream>>>(q);
+    else conv_wgrad_c4w_kernel<4><<<unsigned(grid), kThreads, 0, stream>>>(q);
+  }
   else if (c4) conv_wgrad_c4_kernel<<<unsigned(grid), kThreads, 0, stream>>>(q);
   else if (bn_folds && wgrad_pipe()) conv_wgrad_kernel<true, true><<<unsigned(grid), kThreads, 0, stream>>>(q);
   else if (bn_folds) conv_wgrad_kernel<true><<<unsigned(grid), kThreads, 0, stream>>>(q);

@@ -382,6 +382,7 @@ void conv_set_wgrad_wide(int on);
 void conv_set_dgrad_patch(int on);
 // First-layer weight gradient: 1 = wave-private staging (default), 0 = block-shared, -1 = BT_C4_WAVE / default.
 void conv_set_c4_wave_private(int on);
+void conv_set_c4w_waves(int nw);   // first-layer weight gradient: 4 or 8 waves per block (-1: BT_C4W_WAVES / default)
 // The slice reduce normally follows the main kernel as its own launch.
 // defer != nullptr: it is NOT launched but described in *defer, for the
 // next conv_wgrad to run as extra blocks of its own launch (`side`; the

@@ -336,6 +336,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("conv_set_dgrad_patch", &conv_set_dgrad_patch);
   m.def("conv_set_conv1_tiles", &conv_set_conv1_tiles, py::arg("tiles"), py::arg("rows") = 0);
   m.def("conv_set_c4_wave_private", &conv_set_c4_wave_private);
+  m.def("conv_set_c4w_waves", &conv_set_c4w_waves);
   m.def("head_set_fast", &head_set_fast);
   m.def("conv_tile_pixels", &conv_tile_pixels);
   m.def("conv_tile_channels", &conv_tile_channels);
