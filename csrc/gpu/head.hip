@@ -336,9 +336,25 @@ __device__ void head_loss_wave(const HeadParams& p, bool wt) {
   float total = 0.f;
   for (int n = int(threadIdx.x); n < p.N; n += 64) {
     float logit = 0.f;
-    for (int k = 0; k < cells; ++k)
-      logit += wt ? __hip_atomic_load(p.partial + n * cells + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+    // 16 partials at a time, every load issued before the adds (summed in cell
+    // order): one cell per round trip made this wave -- the kernel's tail -- a
+    // chain of `cells` write-through loads
+    // (write-through reads: sc1 buffer loads -- what an agent-scope relaxed
+    // atomic load compiles to, but ordinary loads the compiler keeps in flight
+    // together; atomic loads it waited out one at a time)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p.partial, 0, p.N * cells * 4, 0x00020000);
+    for (int k0 = 0; k0 < cells; k0 += 16) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int k = k0 + u < cells ? k0 + u : k0;
+        v[u] = wt ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (n * cells + k) * 4, 0, 16))
                   : p.partial[n * cells + k];
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (k0 + u < cells) logit += v[u];
+    }
     const float y = p.target ? p.target[n] : p.target_value;
     const float pr = 1.f / (1.f + expf(-logit));
     const float lp = fmaxf(logf(pr), -100.f), lq = fmaxf(logf(1.f - pr), -100.f);
@@ -364,7 +380,7 @@ __global__ __launch_bounds__(64) void head_loss_kernel(HeadParams p) { head_loss
 // With p.bn_acc the dz blocks also sum the producing BatchNorm+LeakyReLU
 // backward's gz and gz * xhat per channel; the block folds its lanes through
 // LDS and adds its 2 C sums into replica blockIdx % R of the fp64 accumulator.
-constexpr int kHeadImgs = 8;   // images per pass (loads in flight per lane: the bench's whole batch)
+constexpr int kHeadImgs = 4;   // images per pass (loads in flight per lane)
 
 __global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p, int nbwd) {
   const int t = int(threadIdx.x);
@@ -376,20 +392,7 @@ __global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p, in
     for (int e = (int(blockIdx.x) - nbwd) * kHeadThreads + t; e < total; e += nw * kHeadThreads) {
       const int c = e % p.C, cell = e / p.C;
       float s = 0.f;
-      // 8 images per pass with every load in flight (a rolled loop waited out
-      // one load latency per image), summed in image order as before
-      for (int n0 = 0; n0 < p.N; n0 += 8) {
-        float dl[8], pv[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int n = n0 + u < p.N ? n0 + u : n0;
-          dl[u] = p.dlogit[n];
-          pv[u] = p.pooled[(int64_t(n) * cells + cell) * p.C + c];
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (n0 + u < p.N) s += dl[u] * pv[u];
-      }
+      for (int n = 0; n < p.N; ++n) s += p.dlogit[n] * p.pooled[(int64_t(n) * cells + cell) * p.C + c];
       const int i = cell / p.OW, j = cell - i * p.OW;
       p.dw[c * p.ws_c + i * p.ws_i + j * p.ws_j] = g * s;
     }
@@ -403,32 +406,19 @@ __global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p, in
   const bool bnf = p.bn_acc != nullptr;
   float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (live) {
-    // the pooling windows holding (h, w): with OH <= H (OW <= W) at most two
-    // per dimension, i0 and i0 + 1 (j0, j0 + 1) -- all four candidates' weights
-    // are loaded at once (a window at a time waited out a load latency each),
-    // then added in the window order of the loop this replaces
     const int i0 = (h * p.OH) / p.H, i1 = ((h + 1) * p.OH + p.H - 1) / p.H;
     const int j0 = (w * p.OW) / p.W, j1 = ((w + 1) * p.OW + p.W - 1) / p.W;
-    float wv[4][8];
-    bool in[4];
-    float area[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int i = i0 + (q >> 1), j = j0 + (q & 1);
+    for (int i = i0; i < i1 && i < p.OH; ++i) {
       const int hs = wstart(i, p.H, p.OH), he = wend(i, p.H, p.OH);
-      const int ws = wstart(j, p.W, p.OW), we = wend(j, p.W, p.OW);
-      in[q] = i < i1 && i < p.OH && j < j1 && j < p.OW && h >= hs && h < he && w >= ws && w < we;
-      area[q] = float((he - hs) * (we - ws));
-      const int ic = in[q] ? i : 0, jc = in[q] ? j : 0;
+      if (h < hs || h >= he) continue;
+      for (int j = j0; j < j1 && j < p.OW; ++j) {
+        const int ws = wstart(j, p.W, p.OW), we = wend(j, p.W, p.OW);
+        if (w < ws || w >= we) continue;
+        const float area = float((he - hs) * (we - ws));
 #pragma unroll
-      for (int k = 0; k < 8; ++k) wv[q][k] = p.w[(c0 + k) * p.ws_c + ic * p.ws_i + jc * p.ws_j];
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (in[q]) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) m[k] += wv[q][k] / area[q];
+        for (int k = 0; k < 8; ++k) m[k] += p.w[(c0 + k) * p.ws_c + i * p.ws_i + j * p.ws_j] / area;
       }
+    }
   }
   float is[8], nm[8], bw[8], bb[8], bs[8], bq[8];
 #pragma unroll

@@ -280,10 +280,11 @@ struct AdamParams {
   int maximize = 0;
   float beta1 = 0.9f, beta2 = 0.999f, eps = 1e-8f, weight_decay = 0.f;
   const float* sched = nullptr;   // device [5], written by adam_schedule
-  // One-launch form (no adam_schedule): with step != nullptr every block
-  // works the schedule out itself from step / hp / gate (one lane, shared
-  // through LDS), and the block that takes the last ticket (*ticket, zero
-  // between launches) stores the advanced counter.  sched is then unused.
+  // One-launch form (no adam_schedule): with step != nullptr, sched holds
+  // THIS step's schedule, worked out ahead (adam_schedule_prime, then each
+  // launch's last block); every block reads it and the gate, and the block
+  // that takes the last ticket (*ticket, zero between launches) advances the
+  // counter and writes the next step's schedule from hp.
   float* step = nullptr;
   const float* hp = nullptr;
   const float* gate = nullptr;
@@ -553,6 +554,8 @@ hipError_t head_backward(const HeadParams& p, hipStream_t stream);
 hipError_t adam_schedule(float* step, const float* hp, float* sched, float beta1, float beta2, hipStream_t stream,
                          const float* gate = nullptr);
 hipError_t adam_update(const AdamParams& p, hipStream_t stream);
+hipError_t adam_schedule_prime(const float* step, const float* hp, float* sched, float beta1, float beta2,
+                               hipStream_t stream);
 
 }  // namespace gpu
 }  // namespace btn

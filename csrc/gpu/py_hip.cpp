@@ -534,6 +534,14 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("step"), py::arg("hp"), py::arg("sched"), py::arg("beta1"), py::arg("beta2"), py::arg("stream"),
         py::arg("gate") = 0);
 
+  m.def("adam_schedule_prime",
+        [](uintptr_t step, uintptr_t hp, uintptr_t sched, float beta1, float beta2, uintptr_t stream) {
+          check(adam_schedule_prime(ptr<const float>(step), ptr<const float>(hp), ptr<float>(sched), beta1, beta2,
+                                    stream_of(stream)),
+                "adam_schedule_prime");
+        },
+        py::arg("step"), py::arg("hp"), py::arg("sched"), py::arg("beta1"), py::arg("beta2"), py::arg("stream"));
+
   m.def("adam_update",
         [](std::vector<uintptr_t> params, std::vector<uintptr_t> grads, std::vector<uintptr_t> exp_avg,
            std::vector<uintptr_t> exp_avg_sq, std::vector<uintptr_t> shadow, std::vector<int64_t> numel,

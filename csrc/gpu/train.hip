@@ -766,6 +766,23 @@ namespace {
 
 // One lane: the step counter and the bias corrections, so that the update
 // kernel's blocks all read a value no block is writing.
+// the schedule of step s (bias corrections in fp64, as torch.optim.Adam)
+__device__ void adam_schedule_write(float s, const float* hp, float* sched, float beta1, float beta2) {
+  const float lr = hp[0];
+  const double bc1 = 1.0 - pow(double(beta1), double(s));
+  const double bc2 = 1.0 - pow(double(beta2), double(s));
+  sched[0] = float(double(lr) / bc1);
+  sched[1] = float(1.0 / sqrt(bc2));
+  sched[2] = lr;
+  sched[3] = hp[1];   // gradient scale (e.g. 1 / world after a summing all-reduce)
+}
+
+// the one-launch update's schedule for the coming step (step + 1), without
+// advancing the counter: after the counter, lr or gradient scale changed on the host side
+__global__ void adam_schedule_prime_kernel(const float* step, const float* hp, float* sched, float beta1, float beta2) {
+  if (threadIdx.x == 0) adam_schedule_write(step[0] + 1.f, hp, sched, beta1, beta2);
+}
+
 __global__ void adam_schedule_kernel(float* step, const float* hp, float* sched, float beta1, float beta2,
                                      const float* gate) {
   if (threadIdx.x != 0) return;
@@ -776,13 +793,7 @@ __global__ void adam_schedule_kernel(float* step, const float* hp, float* sched,
   if (!active) return;
   const float s = step[0] + 1.f;
   step[0] = s;
-  const float lr = hp[0];
-  const double bc1 = 1.0 - pow(double(beta1), double(s));
-  const double bc2 = 1.0 - pow(double(beta2), double(s));
-  sched[0] = float(double(lr) / bc1);
-  sched[1] = float(1.0 / sqrt(bc2));
-  sched[2] = lr;
-  sched[3] = hp[1];   // gradient scale (e.g. 1 / world after a summing all-reduce)
+  adam_schedule_write(s, hp, sched, beta1, beta2);
 }
 
 template <bool GBF16>
@@ -848,26 +859,14 @@ __global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
   }
   float step_size, inv_bc2, lr, gscale;
   bool active;
-  float s_new = 0.f;
   if (a.step) {
-    // one-launch schedule: lane 0 reads the counter, works out the bias
-    // corrections and shares them; it reads the counter before it takes its
-    // ticket (end of the kernel), so the block taking the last ticket may
-    // store the new value
-    __shared__ float sh[5];
-    if (threadIdx.x == 0) {
-      const bool on = !a.gate || a.gate[0] != 0.f;
-      s_new = a.step[0] + 1.f;
-      const double bc1 = 1.0 - pow(double(a.beta1), double(s_new));
-      const double bc2 = 1.0 - pow(double(a.beta2), double(s_new));
-      sh[0] = float(double(a.hp[0]) / bc1);
-      sh[1] = float(1.0 / sqrt(bc2));
-      sh[2] = a.hp[0];
-      sh[3] = a.hp[1];
-      sh[4] = on ? 1.f : 0.f;
-    }
-    __syncthreads();
-    step_size = sh[0], inv_bc2 = sh[1], lr = sh[2], gscale = sh[3], active = sh[4] != 0.f;
+    // one-launch form: the schedule of THIS step was worked out ahead -- by
+    // the previous launch's last block, or adam_schedule_prime -- so a block
+    // only reads it (no lane computing fp64 powers behind a barrier); the gate
+    // is read directly.  The block taking the last ticket advances the counter
+    // and works out the next step's schedule (below).
+    step_size = a.sched[0], inv_bc2 = a.sched[1], lr = a.sched[2], gscale = a.sched[3];
+    active = !a.gate || a.gate[0] != 0.f;
   } else {
     step_size = a.sched[0], inv_bc2 = a.sched[1], lr = a.sched[2], gscale = a.sched[3];
     active = a.sched[4] != 0.f;
@@ -923,15 +922,27 @@ __global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
     }
   }
   if (a.step && threadIdx.x == 0) {
+    // every block has read this step's schedule (its update used it) before its ticket
     const uint32_t tk = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tk == gridDim.x - 1) {
-      if (active) a.step[0] = s_new;
+      if (active) {
+        const float s = a.step[0] + 1.f;
+        a.step[0] = s;
+        adam_schedule_write(s + 1.f, a.hp, const_cast<float*>(a.sched), a.beta1, a.beta2);
+      }
       __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
 
 }  // namespace
+
+hipError_t adam_schedule_prime(const float* step, const float* hp, float* sched, float beta1, float beta2,
+                               hipStream_t stream) {
+  if (!step || !hp || !sched) return hipErrorInvalidValue;
+  adam_schedule_prime_kernel<<<1, 64, 0, stream>>>(step, hp, sched, beta1, beta2);
+  return hipGetLastError();
+}
 
 hipError_t adam_schedule(float* step, const float* hp, float* sched, float beta1, float beta2, hipStream_t stream,
                          const float* gate) {

@@ -18,13 +18,14 @@ adds, for 4x4 convolution weights, the transposed bf16 copy a data-gradient
 kernel reads (``shadow_t(p)``, ``conv_weights_t`` layout) -- the consumer
 step's per-step cast and transpose launches then disappear.
 
-``one_launch=True``: where a group fits one launch (<= 32 tensors) every
-block of the update kernel works the schedule out itself and the last block
-to finish stores the counter (no ``adam_schedule`` launch).  Off by default:
-measured on the bench discriminator's 0.7 M parameters (scripts/adam_bench.py,
-graph replays) it is 3.7 us SLOWER than the two launches -- every block then
-waits on one lane's fp64 bias corrections behind a barrier, and on its
-ticket -- where the separate one-lane launch costs less than that.
+``one_launch=True`` (or ``BT_ADAM_ONE_LAUNCH=1``): where a group fits one
+launch (<= 32 tensors) there is no ``adam_schedule`` launch.  The schedule of
+the coming step is worked out AHEAD -- once when the group's device state is
+made (and after ``set_lr`` / ``set_grad_scale``), then by the block of each
+update that takes the last ticket, which also advances the counter -- so the
+update's blocks only read it.  (Round 3's one-launch form had every block work
+the schedule out itself: one lane's fp64 powers behind a barrier, 3.7 us
+slower than two launches on the bench discriminator, scripts/adam_bench.py.)
 :meth:`set_zero_grads` makes the update clear each gradient after reading it,
 so persistent gradient buffers (``parallel.GradBuckets``) need no zero-fill
 launch before the next backward.
@@ -50,12 +51,16 @@ from . import _count, _dense, _stream, hip_ext
 
 __all__ = ['FusedAdam']
 
+import os  # noqa: E402
+
+_ONE_LAUNCH_DEFAULT = os.environ.get('BT_ADAM_ONE_LAUNCH', '0') == '1'
+
 _MAX_PER_LAUNCH = 32   # kMaxAdam (csrc/gpu/kernels.h)
 
 
 class FusedAdam(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, decoupled=False,
-                 maximize=False, bf16_shadow=False, grad_scale=1.0, one_launch=False):
+                 maximize=False, bf16_shadow=False, grad_scale=1.0, one_launch=None):
         if lr < 0 or eps < 0 or weight_decay < 0 or not (0 <= betas[0] < 1 and 0 <= betas[1] < 1):
             raise ValueError(f'invalid Adam hyper-parameters lr={lr} betas={betas} eps={eps} wd={weight_decay}')
         defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, decoupled=decoupled,
@@ -66,7 +71,7 @@ class FusedAdam(torch.optim.Optimizer):
         # Each entry holds its group, so an id cannot be reused while it lives.
         self._dev = {}
         self._zero_grads = False
-        self._one_launch = bool(one_launch)
+        self._one_launch = _ONE_LAUNCH_DEFAULT if one_launch is None else bool(one_launch)
 
     # -- per-group device scalars ------------------------------------------
     def _group_state(self, group):
@@ -84,10 +89,19 @@ class FusedAdam(torch.optim.Optimizer):
                   'ticket': torch.zeros(4, dtype=torch.int32, device=dev),
                   'lr': float(group['lr']), 'grad_scale': self._grad_scale}
             self._dev[id(group)] = gs
+            self._prime(group, gs)
             for p in group['params']:
                 if self.state.get(p):
                     self.state[p]['step'] = step
         return gs
+
+    def _prime(self, group, gs):
+        """One-launch form: work out the coming step's schedule now (the
+        counter, lr or gradient scale changed outside an update)."""
+        if self._one_launch and gs['step'].is_cuda:
+            b1, b2 = group['betas']
+            hip_ext().adam_schedule_prime(gs['step'].data_ptr(), gs['hp'].data_ptr(), gs['sched'].data_ptr(),
+                                          b1, b2, _stream(gs['step'].device))
 
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
@@ -105,6 +119,7 @@ class FusedAdam(torch.optim.Optimizer):
         for gs in self._dev.values():
             gs['hp'][1].fill_(self._grad_scale)
             gs['grad_scale'] = self._grad_scale
+            self._prime(gs['group'], gs)
 
     def set_lr(self, lr, group=0):
         """Change the learning rate, also for an optimizer captured in a graph."""
@@ -113,6 +128,7 @@ class FusedAdam(torch.optim.Optimizer):
         gs = self._group_state(g)
         gs['hp'][0].fill_(float(lr))
         gs['lr'] = float(lr)
+        self._prime(g, gs)
 
     def _state(self, p, group):
         st = self.state[p]
@@ -197,6 +213,7 @@ class FusedAdam(torch.optim.Optimizer):
             if gs['lr'] != float(group['lr']) and not capturing:
                 gs['hp'][0].fill_(float(group['lr']))   # lr edited through param_groups
                 gs['lr'] = float(group['lr'])
+                self._prime(group, gs)
             states = [self._state(p, group) for p in params]
             if gate is not None and (gate.numel() != 1 or gate.device != params[0].device):
                 raise ValueError('FusedAdam.step: gate must be a 1-element tensor on the parameters\' device')

@@ -372,3 +372,33 @@ def test_gpu_discriminator_step_with_optimizer_shadows(dev):
     for pa, pb in zip(nets[0].parameters(), nets[1].parameters()):
         d = (pb - pa).detach().abs()
         assert float(d.mean()) < 0.15 * lr and float((d > 0.5 * lr).float().mean()) < 0.03
+
+
+@pytest.mark.gpu
+def test_gpu_one_launch_schedule_ahead_follows_lr_changes(dev):
+    """One-launch form: the schedule worked out ahead (by the previous
+    update's last block) stays right across lr and gradient-scale changes and
+    closed gates -- identical to the two-launch form step by step."""
+    torch.manual_seed(3)
+    ps = [torch.randn(n, device=dev) for n in (1000, 4096, 7)]
+    runs = []
+    for one in (True, False):
+        params = [torch.nn.Parameter(p.clone()) for p in ps]
+        opt = ops.FusedAdam(params, lr=1e-2, betas=(0.9, 0.99), one_launch=one)
+        gate = torch.ones(1, device=dev)
+        g = torch.Generator(device=dev).manual_seed(7)
+        for k in range(9):
+            for p in params:
+                p.grad = torch.randn(p.shape, device=dev, generator=g)
+            if k == 3:
+                opt.set_lr(3e-3)
+            if k == 5:
+                opt.set_grad_scale(0.5)
+            if k == 6:
+                opt.param_groups[0]['lr'] = 5e-3          # edited through param_groups
+            gate.fill_(0.0 if k == 4 else 1.0)
+            opt.step(gate=gate)
+        torch.cuda.synchronize()
+        runs.append([p.detach().clone() for p in params] + [opt._group_state(opt.param_groups[0])['step'].clone()])
+    for x, y in zip(*runs):
+        assert torch.equal(x, y)
