@@ -38,15 +38,18 @@ __device__ inline void bn_fold_block(const BnFold& f, double* part) {
   const int G = J >= nt ? 1 : nt / J;
   for (int u = t; u < G * J; u += nt) {
     const int j = u % J, g = u / J;
+    // every replica load issued unconditionally (an out-of-range one re-reads
+    // replica 0 and adds 0.0): a guarded load per replica compiled to a branch
+    // and a full memory wait each -- 8 round trips instead of one
     double v[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int r = g + G * i;
-      v[i] = r < f.R ? f.acc[int64_t(r) * J + j] : 0.0;
+      v[i] = f.acc[int64_t(r < f.R ? r : 0) * J + j];
     }
     double s = 0.0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) s += v[i];
+    for (int i = 0; i < 8; ++i) s += g + G * i < f.R ? v[i] : 0.0;
     for (int r = g + 8 * G; r < f.R; r += G) s += f.acc[int64_t(r) * J + j];   // R > 8 G: not with R = 1024 / C
     for (int r = g; r < f.R; r += G) f.acc[int64_t(r) * J + j] = 0.0;          // read: cleared for the next producer
     part[g * J + j] = s;
@@ -114,15 +117,15 @@ __device__ inline void bn_acc_column_sums(const double* acc, int R, int J, doubl
   const int G = J >= nt ? 1 : nt / J;
   for (int u = t; u < G * J; u += nt) {
     const int j = u % J, g = u / J;
-    double v[8];
+    double v[8];   // (unconditional loads, as bn_fold_block)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int r = g + G * i;
-      v[i] = r < R ? acc[int64_t(r) * J + j] : 0.0;
+      v[i] = acc[int64_t(r < R ? r : 0) * J + j];
     }
     double s = 0.0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) s += v[i];
+    for (int i = 0; i < 8; ++i) s += g + G * i < R ? v[i] : 0.0;
     for (int r = g + 8 * G; r < R; r += G) s += acc[int64_t(r) * J + j];
     part[g * J + j] = s;
   }

@@ -175,13 +175,16 @@ __device__ __forceinline__ void wgrad_reduce_block(const ConvWgradParams::Reduce
   if (e0 >= total) return;
   const int k0 = by * kSliceGroup;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  // all of the group's loads in flight at once (past the last slice: re-read
+  // slice k0, not added); a guarded load per slice compiled to a branch and a
+  // memory wait each -- 8 round trips
+  float4 v[kSliceGroup];
 #pragma unroll
-  for (int k = 0; k < kSliceGroup; ++k) {
-    if (k0 + k < S) {
-      const float4 v = *reinterpret_cast<const float4*>(partial + int64_t(k0 + k) * total + e0);
-      acc.x += v.x, acc.y += v.y, acc.z += v.z, acc.w += v.w;
-    }
-  }
+  for (int k = 0; k < kSliceGroup; ++k)
+    v[k] = *reinterpret_cast<const float4*>(partial + int64_t(k0 + k < S ? k0 + k : k0) * total + e0);
+#pragma unroll
+  for (int k = 0; k < kSliceGroup; ++k)
+    if (k0 + k < S) acc.x += v[k].x, acc.y += v[k].y, acc.z += v[k].z, acc.w += v[k].w;
   const float vals[4] = {acc.x, acc.y, acc.z, acc.w};
   const bool single = S <= kSliceGroup;
 #pragma unroll

@@ -160,6 +160,26 @@ struct BnVec {
 };
 
 template <int DT>
+__device__ __forceinline__ uint4 bn_load_raw(const void* p, int64_t e) {
+  return *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(p) + e * BnVec<DT>::ES);
+}
+
+template <int DT>
+__device__ __forceinline__ void bn_unpack(const uint4 raw, float (&v)[BnVec<DT>::V]) {
+  const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+  if constexpr (DT == OUT_BF16) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = __uint_as_float(w[i]);
+  }
+}
+
+template <int DT>
 __device__ __forceinline__ void bn_load(const void* p, int64_t e, float (&v)[BnVec<DT>::V]) {
   const uint4 raw = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(p) + e * BnVec<DT>::ES);
   const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
@@ -368,15 +388,17 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const void* __restrict
   const int c0 = (int(threadIdx.x) % G) * V;
   // The block's first pass of loads goes out before the coefficients are
   // read, so their latencies overlap; later passes load at the end of the
-  // previous one (one register set).
+  // previous one (one register set).  The loads stay raw until the apply
+  // unpacks them: unpacking at load time made the compiler wait for the
+  // first pass before the accumulator fold even started.
   const int64_t pass = int64_t(gridDim.x) * kBlock * U;
   int64_t idx = int64_t(blockIdx.x) * kBlock * U + threadIdx.x;
-  float v[U][V], gv[U][V];
+  uint4 rv[U], rg[U];
   auto load_pass = [&]() {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      bn_load<DT>(x, (idx + u * kBlock) * V, v[u]);
-      if constexpr (BWD) bn_load<DT>(gy, (idx + u * kBlock) * V, gv[u]);
+      rv[u] = bn_load_raw<DT>(x, (idx + u * kBlock) * V);
+      if constexpr (BWD) rg[u] = bn_load_raw<DT>(gy, (idx + u * kBlock) * V);
     }
   };
   bool have = idx + (U - 1) * kBlock < total;   // a whole pass: U vectors per lane
@@ -482,8 +504,10 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const void* __restrict
   while (have) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      float o[V];
-      apply(v[u], gv[u], o);
+      float v[V], gv[V], o[V];
+      bn_unpack<DT>(rv[u], v);
+      if constexpr (BWD) bn_unpack<DT>(rg[u], gv);
+      apply(v, gv, o);
       bn_store<DT>(out, (idx + u * kBlock) * V, o);
     }
     idx += pass;
@@ -796,35 +820,64 @@ __global__ void adam_schedule_kernel(float* step, const float* hp, float* sched,
   adam_schedule_write(s, hp, sched, beta1, beta2);
 }
 
+// One tensor's slot of the launch, gathered into LDS by the block's first
+// lanes (one parallel read of the kernel arguments): indexing the argument
+// arrays with a lane's k read them from memory one dependent load at a time
+// -- ~6 round trips before any parameter load could start.
+struct AdamSlot {
+  float* p;
+  const void* g;
+  float* m;
+  float* v;
+  uint16_t* shadow;
+  uint16_t* shadow_t;
+  int64_t numel;
+  int tcin, tcout;
+};
+
 template <bool GBF16>
 __global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
+  __shared__ AdamSlot slot[kMaxAdam];
+  __shared__ int64_t gst[kMaxAdam + 1];
+  {
+    const int t = int(threadIdx.x);
+    if (t < a.n) {
+      AdamSlot sl;
+      sl.p = a.p[t], sl.g = a.g[t], sl.m = a.m[t], sl.v = a.v[t], sl.shadow = a.shadow[t];
+      sl.shadow_t = a.shadow_t[t], sl.numel = a.numel[t], sl.tcin = a.tcin[t], sl.tcout = a.tcout[t];
+      slot[t] = sl;
+    }
+    if (t <= a.n) gst[t] = a.gstart[t];
+    __syncthreads();
+  }
   const int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x;   // 4-element group
-  const bool in = q < a.gstart[a.n];
+  const bool in = q < gst[a.n];
   int k = 0;
   if (in)
-    while (q >= a.gstart[k + 1]) ++k;     // <= kMaxAdam compares, mostly uniform across a wave
-  const int64_t gi = in ? q - a.gstart[k] : 0;
+    while (q >= gst[k + 1]) ++k;          // <= kMaxAdam compares (LDS), mostly uniform across a wave
+  const int64_t gi = in ? q - gst[k] : 0;
   // element offset of the group.  A tensor with a transposed shadow starts
   // on a block boundary and is walked in 32 x 32 (co, ci) tiles of one tap,
   // a block per tile: lane t = row t / 8 (co), 4 input channels 4 (t % 8) --
   // 128-byte runs in, and through an LDS transpose 64-byte runs of the
   // [ci][tap][co] shadow out.
   int64_t e0 = gi * 4;
-  uint16_t* T = in ? a.shadow_t[k] : nullptr;   // block-uniform (host-checked tiling)
+  uint16_t* T = in ? slot[k].shadow_t : nullptr;   // block-uniform (host-checked tiling)
   int tco0 = 0, ttap = 0, tci0 = 0;
   if (T) {
-    const int cin = a.tcin[k], cit = cin >> 5;
+    const int cin = slot[k].tcin, cit = cin >> 5;
     const int tile = int(gi >> 8), t = int(threadIdx.x);
     tci0 = (tile % cit) * 32;
     ttap = (tile / cit) & 15;
     tco0 = (tile / (cit * 16)) * 32;
     e0 = (int64_t(tco0 + (t >> 3)) * 16 + ttap) * cin + tci0 + 4 * (t & 7);
   }
-  const int64_t n = in ? a.numel[k] : 0;
+  const int64_t n = in ? slot[k].numel : 0;
   const bool full = e0 + 4 <= n;   // tensors are 16-byte aligned (host-checked), so a full group is one dwordx4
-  float* P = in ? a.p[k] : nullptr;
-  float* M = in ? a.m[k] : nullptr;
-  float* V = in ? a.v[k] : nullptr;
+  float* P = in ? slot[k].p : nullptr;
+  float* M = in ? slot[k].m : nullptr;
+  float* V = in ? slot[k].v : nullptr;
+  const void* GR = in ? slot[k].g : nullptr;
   float pv[4] = {0.f, 0.f, 0.f, 0.f}, gv[4] = {0.f, 0.f, 0.f, 0.f}, mv[4] = {0.f, 0.f, 0.f, 0.f},
         vv[4] = {0.f, 0.f, 0.f, 0.f};
   // every load is issued before the schedule below (its fp64 math and the
@@ -837,11 +890,11 @@ __global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
     mv[0] = m4.x, mv[1] = m4.y, mv[2] = m4.z, mv[3] = m4.w;
     vv[0] = v4.x, vv[1] = v4.y, vv[2] = v4.z, vv[3] = v4.w;
     if constexpr (GBF16) {
-      const uint2 g2 = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(a.g[k]) + e0);
+      const uint2 g2 = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(GR) + e0);
       gv[0] = __uint_as_float(g2.x << 16), gv[1] = __uint_as_float(g2.x & 0xFFFF0000u);
       gv[2] = __uint_as_float(g2.y << 16), gv[3] = __uint_as_float(g2.y & 0xFFFF0000u);
     } else {
-      const float4 g4 = *reinterpret_cast<const float4*>(static_cast<const float*>(a.g[k]) + e0);
+      const float4 g4 = *reinterpret_cast<const float4*>(static_cast<const float*>(GR) + e0);
       gv[0] = g4.x, gv[1] = g4.y, gv[2] = g4.z, gv[3] = g4.w;
     }
   } else if (in) {
@@ -852,9 +905,9 @@ __global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
       mv[j] = ok ? M[e0 + j] : 0.f;
       vv[j] = ok ? V[e0 + j] : 0.f;
       if constexpr (GBF16)
-        gv[j] = ok ? __uint_as_float(uint32_t(static_cast<const uint16_t*>(a.g[k])[e0 + j]) << 16) : 0.f;
+        gv[j] = ok ? __uint_as_float(uint32_t(static_cast<const uint16_t*>(GR)[e0 + j]) << 16) : 0.f;
       else
-        gv[j] = ok ? static_cast<const float*>(a.g[k])[e0 + j] : 0.f;
+        gv[j] = ok ? static_cast<const float*>(GR)[e0 + j] : 0.f;
     }
   }
   float step_size, inv_bc2, lr, gscale;
@@ -873,7 +926,7 @@ __global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
   }
   if (in) {
     if (!GBF16 && a.zero_grad) {   // consumed (also when a closed gate skips the update)
-      float* G = static_cast<float*>(const_cast<void*>(a.g[k]));
+      float* G = static_cast<float*>(const_cast<void*>(GR));
       if (full) *reinterpret_cast<float4*>(G + e0) = make_float4(0.f, 0.f, 0.f, 0.f);
       else for (int j = 0; j < 4 && e0 + j < n; ++j) G[e0 + j] = 0.f;
     }
@@ -890,7 +943,7 @@ __global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
         vv[j] = b2 * vv[j] + (1.f - b2) * g * g;
         pv[j] -= step_size * mv[j] / (sqrtf(vv[j]) * inv_bc2 + a.eps);
       }
-      uint16_t* S = a.shadow[k];
+      uint16_t* S = slot[k].shadow;
       if (full) {
         *reinterpret_cast<float4*>(P + e0) = make_float4(pv[0], pv[1], pv[2], pv[3]);
         *reinterpret_cast<float4*>(M + e0) = make_float4(mv[0], mv[1], mv[2], mv[3]);
@@ -909,7 +962,7 @@ __global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
       }
       if (T) {   // (co, tap, ci) -> [ci][tap][co] through LDS (T, active: block-uniform)
         __shared__ uint16_t tl[32][34];
-        const int t = int(threadIdx.x), cout = a.tcout[k];
+        const int t = int(threadIdx.x), cout = slot[k].tcout;
 #pragma unroll
         for (int j = 0; j < 4; ++j) tl[4 * (t & 7) + j][t >> 3] = f2bf(pv[j]);
         __syncthreads();
