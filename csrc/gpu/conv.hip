@@ -99,8 +99,15 @@ __device__ __forceinline__ bf16x8 frag(const char* img, int lane, int col) {
 constexpr uint32_t kOOB = 0x80000000u;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+// (base and size are block-uniform at every call site; readfirstlane makes
+// that visible to the compiler -- where its divergence analysis could not
+// prove it (the first layer's `lut ? 1 : 2` byte size), every buffer load of
+// the kernel became a waterfall loop with a full memory wait)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int64_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, int(bytes), 0x00020000);
+  const uint64_t b = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(b)), hi = __builtin_amdgcn_readfirstlane(uint32_t(b >> 32));
+  const int n = __builtin_amdgcn_readfirstlane(int(bytes));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((uint64_t(hi) << 32) | lo), 0, n, 0x00020000);
 }
 __device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, int(off), 0, 0);

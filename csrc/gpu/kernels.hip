@@ -108,7 +108,21 @@ __device__ __forceinline__ Xf stage_xf(const float* T, uint32_t* tab, int nch) {
   x.gshift = rep == 32 ? 7 : 6;                 // bytes per gamma row: 4 * R
   x.g = reinterpret_cast<const uint8_t*>(tab) + (threadIdx.x & (rep - 1)) * 4;
   if (!x.arith) {
-    for (int i = threadIdx.x; i < nch * 256; i += blockDim.x) reinterpret_cast<float*>(tab)[i] = T[i];
+    // every load first (4 x 256 threads cover the 4 x 256 table): a
+    // load-store loop waited out one round trip per 256 entries
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = int(threadIdx.x) + u * int(blockDim.x);
+      v[u] = T[i < nch * 256 ? i : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = int(threadIdx.x) + u * int(blockDim.x);
+      if (i < nch * 256) reinterpret_cast<float*>(tab)[i] = v[u];
+    }
+    for (int i = int(threadIdx.x) + 4 * int(blockDim.x); i < nch * 256; i += blockDim.x)   // (blocks < 256 threads)
+      reinterpret_cast<float*>(tab)[i] = T[i];
   } else if (rep > 0) {
     // 16-byte stores: the 4 words of a quad sit in one row (same gamma dword)
     const uint32_t* gw = reinterpret_cast<const uint32_t*>(T + kXfGamma);
