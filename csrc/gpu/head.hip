@@ -209,7 +209,11 @@ __global__ __launch_bounds__(kHeadThreads) void head_fwd_act_kernel(HeadParams p
 #pragma unroll
   for (int u = 0; u < KMAX; ++u) {
     const int k = pl + u * PL;
-    const int kk = k < npx ? k : pl;   // past the window: a re-read, added as 0 below
+    // past the window: a re-read of its first pixel, added as 0 below (not pixel
+    // pl: with fewer window pixels than lanes per pixel group -- a 6 x 8 input
+    // pooled to 4 x 4 has 4 -- that lands rows below the window, past the last
+    // image's end)
+    const int kk = k < npx ? k : 0;
     const int h = h0 + kk / ww, w = w0 + kk % ww;
     v[u] = *reinterpret_cast<const uint4*>(p.z + (int64_t(n * p.H + h) * p.W + w) * p.C + g * 8);
   }

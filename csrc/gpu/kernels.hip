@@ -295,7 +295,9 @@ __device__ __forceinline__ Group locate(const DecodeParams& p, int64_t g, int64_
   return r;
 }
 
-template <int PPT, int CIN, int OUTT, int LAYOUT, bool TBL = false>
+// NT: streaming (non-temporal) stores -- output written once and read by a
+// later kernel, kept out of the L2's write-back set (replay sample A/B)
+template <int PPT, int CIN, int OUTT, int LAYOUT, bool TBL = false, bool NT = false>
 __device__ __forceinline__ void emit(const DecodeParams& p, const Xf& xf, const int* cm, int cout, int64_t HW,
                                      const Group& gr, const Pixels<PPT, CIN>& px) {
   const int b = gr.b;
@@ -309,8 +311,16 @@ __device__ __forceinline__ void emit(const DecodeParams& p, const Xf& xf, const 
       const int64_t off = int64_t(c) * HW + q;   // within image b (NCHW)
       if constexpr (OUTT == OUT_F32) {
         float* d = image_out<float>(p, b, HW * cout) + off;
+        if constexpr (NT) {
+          typedef float f4v __attribute__((ext_vector_type(4)));
 #pragma unroll
-        for (int i = 0; i < PPT / 4; ++i) reinterpret_cast<float4*>(d)[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+          for (int i = 0; i < PPT / 4; ++i)
+            __builtin_nontemporal_store(f4v{v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]},
+                                        reinterpret_cast<f4v*>(d) + i);
+        } else {
+#pragma unroll
+          for (int i = 0; i < PPT / 4; ++i) reinterpret_cast<float4*>(d)[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+        }
       } else if constexpr (OUTT == OUT_BF16 || OUTT == OUT_F16) {
         uint16_t o[PPT];
 #pragma unroll
@@ -670,7 +680,7 @@ __device__ __forceinline__ void replay_meta(const ReplayParams& r, const ReplayS
 // TBL: the value table is in table mode (p.xf_table_only): the lookups are
 // plain LDS reads and the kernel carries none of the arithmetic-form code
 // (whose registers cut the general kernel to 4 waves per SIMD)
-template <int PPT, int CIN, int OUTT, int LAYOUT, bool TBL>
+template <int PPT, int CIN, int OUTT, int LAYOUT, bool TBL, bool NT = false>
 __global__ __launch_bounds__(kBlock) void replay_vec_kernel(DecodeParams p, ReplayParams r, int64_t meta_units) {
   __shared__ ReplayShared sh;
   const int64_t HW = int64_t(p.H) * p.W;
@@ -715,7 +725,7 @@ __global__ __launch_bounds__(kBlock) void replay_vec_kernel(DecodeParams p, Repl
       continue;
     }
     if (g == g0) {
-      emit<PPT, CIN, OUTT, LAYOUT, TBL>(p, xf, cm, cout, HW, gr0, px0);
+      emit<PPT, CIN, OUTT, LAYOUT, TBL, NT>(p, xf, cm, cout, HW, gr0, px0);
       continue;
     }
     Group gr;
@@ -725,7 +735,7 @@ __global__ __launch_bounds__(kBlock) void replay_vec_kernel(DecodeParams p, Repl
     gr.src = p.src + sh.idx[gr.b] * r.frame_bytes + (int64_t(sy) * p.W + x) * CIN;
     Pixels<PPT, CIN> px;
     load_pixels<PPT, CIN>(gr.src, px);
-    emit<PPT, CIN, OUTT, LAYOUT, TBL>(p, xf, cm, cout, HW, gr, px);
+    emit<PPT, CIN, OUTT, LAYOUT, TBL, NT>(p, xf, cm, cout, HW, gr, px);
   }
 }
 
@@ -766,9 +776,13 @@ hipError_t launch_replay(const DecodeParams& p, const ReplayParams& r, int64_t m
                    (int64_t(p.H) * p.W * p.Cin) % 16 == 0;
   if (vec) {
     const int grid = grid_for(int64_t(p.B) * p.H * p.W / PPT + meta_units, p.max_grid);
+    // BT_REPLAY_NT=1: fp32 NCHW table-mode output through non-temporal stores (A/B)
+    static const bool nt_env = std::getenv("BT_REPLAY_NT") && std::atoi(std::getenv("BT_REPLAY_NT")) > 0;
+    const bool nt = nt_env && OUTT == OUT_F32 && p.layout == NCHW && p.xf_table_only;
 #define BT_REPLAY(CIN, LAY)                                                                  \
   do {                                                                                       \
-    if (p.xf_table_only) replay_vec_kernel<PPT, CIN, OUTT, LAY, true><<<grid, kBlock, 0, s>>>(p, r, meta_units); \
+    if (nt) replay_vec_kernel<PPT, CIN, OUTT, LAY, true, true><<<grid, kBlock, 0, s>>>(p, r, meta_units); \
+    else if (p.xf_table_only) replay_vec_kernel<PPT, CIN, OUTT, LAY, true><<<grid, kBlock, 0, s>>>(p, r, meta_units); \
     else replay_vec_kernel<PPT, CIN, OUTT, LAY, false><<<grid, kBlock, 0, s>>>(p, r, meta_units);               \
   } while (0)
     if (p.Cin == 4) {

@@ -670,6 +670,14 @@ PYBIND11_MODULE(_hip, m) {
                              stream_of(stream)),
                 "bn_bwd_apply");
         });
+  // the BN forward's apply pass alone (mean, invstd given)
+  m.def("bn_fwd_apply",
+        [](uintptr_t x, uintptr_t y, int64_t M, int C, int dtype, uintptr_t mean, uintptr_t invstd, uintptr_t w,
+           uintptr_t b, float slope, uintptr_t stream) {
+          check(bn_apply(ptr<const void>(x), ptr<void>(y), M, C, dtype, ptr<const float>(mean),
+                         ptr<const float>(invstd), ptr<const float>(w), ptr<const float>(b), slope, stream_of(stream)),
+                "bn_apply");
+        });
   // accumulator hand-off (kernels.h BnAcc): no finalize launches
   m.def("bn_acc_replicas", &bn_acc_replicas);
   m.def("bn_acc_elems", &bn_acc_elems);

@@ -371,6 +371,7 @@ struct BnApplyFold {
   float* rm = nullptr;         // forward: running statistics, num_batches_tracked
   float* rv = nullptr;
   int64_t* tracked = nullptr;
+  int release = 1;             // 0: no ticket / clear (BT_BN_RELEASE=0: timing diagnostics only)
 };
 
 template <int DT, bool BWD, bool FOLD = false>
@@ -453,7 +454,7 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const void* __restrict
       coef[C + pos(c)] = c1v;
     }
     __syncthreads();
-    bn_acc_release(fa.acc, fa.R, C, &flag);
+    if (fa.release) bn_acc_release(fa.acc, fa.R, C, &flag);
     const int gl = int(threadIdx.x) % G;   // this lane's channel group: channels V gl .. + V - 1
     float a0[V], a1[V];
 #pragma unroll
@@ -671,6 +672,16 @@ int64_t bn_acc_elems(int C) {
   return r > 0 ? int64_t(2) * C * r + (kBnTicketShards * kBnTicketStride + 1 + 1) / 2 : -1;
 }
 
+namespace {
+// BT_BN_RELEASE=0: the accumulator apply kernels skip the release (tickets and
+// clear) -- wrong for a second use of the accumulator; for the per-phase timing
+// of scripts/bn_apply_bench.py only
+int bn_release_env() {
+  static const int v = std::getenv("BT_BN_RELEASE") && std::getenv("BT_BN_RELEASE")[0] == '0' ? 0 : 1;
+  return v;
+}
+}  // namespace
+
 hipError_t bn_apply_acc(const void* x, void* y, int64_t M, int C, int dtype, BnAcc acc, float eps, float momentum,
                         float* mean, float* invstd, float* running_mean, float* running_var, int64_t* tracked,
                         const float* w, const float* b, float slope, hipStream_t stream) {
@@ -680,6 +691,7 @@ hipError_t bn_apply_acc(const void* x, void* y, int64_t M, int C, int dtype, BnA
   BnApplyFold fa;
   fa.acc = acc.acc, fa.R = acc.R, fa.eps = eps, fa.momentum = momentum;
   fa.o0 = mean, fa.o1 = invstd, fa.rm = running_mean, fa.rv = running_var, fa.tracked = tracked;
+  fa.release = bn_release_env();
   const int V = dtype == OUT_BF16 ? 8 : 4;
   const int grid = bn_fold_grid(M * (C / V));
   if (dtype == OUT_BF16)
@@ -699,6 +711,7 @@ hipError_t bn_bwd_apply_acc(const void* x, const void* gy, void* gx, int64_t M, 
     return hipErrorInvalidValue;
   BnApplyFold fa;
   fa.acc = acc.acc, fa.R = acc.R, fa.o0 = db, fa.o1 = dw;
+  fa.release = bn_release_env();
   const int V = dtype == OUT_BF16 ? 8 : 4;
   const int grid = bn_fold_grid(M * (C / V));
   if (dtype == OUT_BF16)

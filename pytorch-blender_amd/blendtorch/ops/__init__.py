@@ -1279,12 +1279,36 @@ class WgradChain:
 
     def flush(self, device):
         if self.pending is not None:
+            side = _SIDE_STREAMS.get(device)
+            if side is not None:   # the pending reduce's partials may have been written on the side stream
+                import torch
+                torch.cuda.current_stream(device).wait_stream(side)
             hip_ext().conv_wgrad_reduce(self.pending, _stream(device))
             _grad_done(self.param)
             self.pending = self.keep = self.param = None
 
 
 _WGRAD_BLOCKS = int(os.environ.get('BT_WGRAD_BLOCKS', '512'))
+# weight gradients on a side stream, concurrent with the data-gradient chain (BT_WGRAD_SIDE=0: in line)
+_SIDE_WGRAD = os.environ.get('BT_WGRAD_SIDE', '1') not in ('', '0')
+_SIDE_STREAMS = {}
+_SIDE_KEEP = []   # main-stream tensors the side stream reads, until it joins the main stream
+
+
+def _side_stream(device):
+    import torch
+    s = _SIDE_STREAMS.get(device)
+    if s is None:
+        s = _SIDE_STREAMS[device] = torch.cuda.Stream(device)
+    return s
+
+
+def set_side_wgrad(on):
+    """Weight gradients on a side stream (True, the default) or in line with
+    the data gradients (False); returns the previous setting."""
+    global _SIDE_WGRAD
+    prev, _SIDE_WGRAD = _SIDE_WGRAD, bool(on)
+    return prev
 # first layer on raw u8 frames: its forward writes the decoded frames for its weight gradient (BT_C4_DECODED)
 _C4_DECODED = os.environ.get('BT_C4_DECODED', '0') not in ('', '0')
 
@@ -1615,6 +1639,26 @@ def _conv_function():
             gy = gy.contiguous(memory_format=torch.channels_last)
             gx = gw = None
             gy_dgrad = gy
+            # the weight gradient on a side stream, concurrent with the data
+            # gradient and the backward chain that follows it: both kernels are
+            # latency-bound at a few waves per SIMD, so the other one's waves
+            # fill the idle issue slots (a chain of weight gradients -- one
+            # deferred reduce riding in the next launch -- stays on the side
+            # stream).  The BN backward's statistics fold then runs in its own
+            # apply launch instead of as an extra block of this weight
+            # gradient (which would put it back on the critical path).  A
+            # data-parallel bucket completed here is all-reduced on the side
+            # stream, behind its weight gradients (GradBuckets._issue).
+            side = None
+            wg_done = False
+            if (_SIDE_WGRAD and x.is_cuda and ctx.needs_input_grad[1] and ctx.wchain is not None
+                    and not (fold_bn and ctx.needs_input_grad[0])):
+                side = _side_stream(x.device)
+                side.wait_stream(torch.cuda.current_stream(x.device))   # gy (and everything before it) is ready
+                if ctx.needs_input_grad[0]:
+                    # fork now: the weight gradient is enqueued before the data gradient
+                    gw = _Conv4x4s2._wgrad_side(ctx, x, gy, bn_dy, side)
+                    wg_done = True
             if fold_bn and ctx.needs_input_grad[0]:
                 # the weight gradient runs first: it applies the BN backward to gy and writes
                 # the BN's input gradient, this layer's true output gradient, for the data gradient
@@ -1631,7 +1675,15 @@ def _conv_function():
                         wfull = wfull.contiguous(memory_format=torch.channels_last)
                     gx = torch.ops.aten.convolution_backward(gy_dgrad, x, wfull, None, [2, 2], [1, 1], [1, 1],
                                                              False, [0, 0], 1, [True, False, False])[0]
-            if gy_dgrad is gy:   # (not already run before the data gradient)
+            if wg_done:
+                pass
+            elif gy_dgrad is gy and side is not None:   # (no data gradient: the chain's last, the first layer)
+                gw = _Conv4x4s2._wgrad_side(ctx, x, gy, bn_dy, side)
+            elif gy_dgrad is gy:   # (not already run before the data gradient)
+                prior = _SIDE_STREAMS.get(x.device) if x.is_cuda else None
+                if prior is not None and ctx.wchain is not None and ctx.wchain.pending is not None:
+                    # the chain's pending reduce reads partials an earlier launch wrote on the side stream
+                    torch.cuda.current_stream(x.device).wait_stream(prior)
                 fold = None
                 bl = ctx.bn_link
                 if gx is not None and bl is not None and bl.acc is not None and bl.part is not None and bl.rows < 0 \
@@ -1642,6 +1694,25 @@ def _conv_function():
                     fold = bl.fold_args(x.shape[0] * x.shape[2] * x.shape[3])
                 gw = _Conv4x4s2._wgrad(ctx, x, gy, fold, bl, bn_dy)
             return gx, gw, None, None, None, None, None, None, None, None, None
+
+        @staticmethod
+        def _wgrad_side(ctx, x, gy, bn_dy, side):
+            """The weight gradient on the side stream (forked before the data
+            gradient was enqueued, see backward): the stream joins the main one
+            after the chain's last launch, or at once for a gradient autograd
+            accumulates itself."""
+            main = torch.cuda.current_stream(x.device)
+            with torch.cuda.stream(side):
+                gw = _Conv4x4s2._wgrad(ctx, x, gy, None, ctx.bn_link, bn_dy)
+            # x and gy live in main-stream memory the side stream still reads: they
+            # stay referenced until the join (a block freed earlier could be handed
+            # to a later main-stream tensor -- also inside a graph capture, where
+            # record_stream does not order the reuse)
+            _SIDE_KEEP.extend((x, gy))
+            if ctx.wlast or gw is not None:
+                main.wait_stream(side)
+                _SIDE_KEEP.clear()
+            return gw
 
         @staticmethod
         def _wgrad(ctx, x, gy, fold, bl, bn_dy):

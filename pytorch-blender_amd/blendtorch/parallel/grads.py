@@ -161,7 +161,16 @@ class GradBuckets:
         self._issued[i] = True
         # (bucket, weight-gradient launches enqueued before its all-reduce): where it went
         self.order.append((i, ops.KERNEL_CALLS.get('conv_wgrad', 0)))
-        self._comm.all_reduce_(self.buckets[i], self._op)
+        b = self.buckets[i]
+        if b.is_cuda:
+            # weight gradients run on a side stream (ops.set_side_wgrad): a bucket
+            # completed from the main stream also waits for the side stream's
+            # launches; one completed from the side stream reduces there, behind them
+            side = ops._SIDE_STREAMS.get(b.device)
+            cur = torch.cuda.current_stream(b.device)
+            if side is not None and cur != side:
+                cur.wait_stream(side)
+        self._comm.all_reduce_(b, self._op)
 
     def _on_done(self, p):
         i = self._where.get(id(p))

@@ -289,12 +289,16 @@ def test_tap_gemm_tile_variants(dev, tiles):
 
 
 @pytest.mark.gpu
-def test_bn_accumulators_fold_and_clear(dev, monkeypatch):
+@pytest.mark.parametrize('side', [False, True])
+def test_bn_accumulators_fold_and_clear(dev, monkeypatch, side):
     """Accumulator hand-off (BnAccumulator): the conv epilogues add BN sums
     into zeroed accumulators that the apply kernels fold and clear -- same
     loss, gradients and running statistics as the partial-row + finalize
-    path, over several steps, and every accumulator is zero after each step."""
+    path, over several steps, and every accumulator is zero after each step.
+    In line, the weight-gradient launches fold BN1..3's backward sums; with
+    the weight gradients on the side stream the BN applies fold them."""
     from blendtorch.models import Discriminator
+    monkeypatch.setattr(ops, '_SIDE_WGRAD', side)
     torch.manual_seed(7)
     cl = torch.channels_last
     a = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
@@ -314,8 +318,8 @@ def test_bn_accumulators_fold_and_clear(dev, monkeypatch):
         # 4 BN layers forward; backward: BN1..3 from the dgrad epilogues, BN4 from the head's
         assert ops.KERNEL_CALLS['bn_forward_acc'] == before[0] + 4
         assert ops.KERNEL_CALLS['bn_backward_acc'] == before[1] + 4
-        # BN1..3's sums are folded by the next conv's weight-gradient launch
-        assert ops.KERNEL_CALLS.get('bn_backward_folded', 0) == before[2] + 3
+        # BN1..3's sums are folded by the next conv's weight-gradient launch (in line)
+        assert ops.KERNEL_CALLS.get('bn_backward_folded', 0) == before[2] + (0 if side else 3)
         monkeypatch.setattr(ops, 'bn_acc_supported', lambda C: False)
         lb = b.bce_loss_bf16(x, 1.0)
         lb.backward()
@@ -701,3 +705,48 @@ def test_first_layer_decoded_side_output(dev, monkeypatch):
     assert torch.equal(losses[0], losses[1])
     for (n, pa), pb in zip(nets[0].named_parameters(), nets[1].parameters()):
         torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-4, atol=1e-6 + 1e-4 * float(pb.grad.abs().max()), msg=n)
+
+
+@pytest.mark.gpu
+def test_side_stream_weight_gradients(dev):
+    """Weight gradients on the side stream (ops.set_side_wgrad(True), forked
+    before each data gradient and joined after the chain's last launch) give
+    the gradients of the in-line order -- eager, and in the bench's captured
+    step (FusedAdam bucket views, so the deferred-reduce chain rides on the
+    side stream) where the weights after three steps agree far below lr."""
+    from blendtorch.models import Discriminator
+    from blendtorch.parallel.step import CapturedStep
+    cl = torch.channels_last
+    cfg = ops.DecodeConfig.unit(channels='rgba', gamma=2.2, dtype='bfloat16', layout='nhwc')
+    g = torch.Generator(device=dev).manual_seed(21)
+    xs = [torch.randint(0, 256, (4, 96, 128, 4), dtype=torch.uint8, device=dev, generator=g) for _ in range(3)]
+    torch.manual_seed(5)
+    nets = [Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl) for _ in range(4)]
+    for m in nets[1:]:
+        m.load_state_dict(nets[0].state_dict())
+    prev = ops.set_side_wgrad(True)
+    try:
+        for m, side in zip(nets[:2], (True, False)):   # eager
+            ops.set_side_wgrad(side)
+            m.bce_loss_bf16(xs[0].permute(0, 3, 1, 2), 1.0, decode=cfg).backward()
+        torch.cuda.synchronize()
+        for (n, pa), pb in zip(nets[0].named_parameters(), nets[1].parameters()):
+            torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-4, atol=1e-6 + 1e-4 * float(pb.grad.abs().max()),
+                                       msg=n)
+        lr = 2e-4
+        steps = []
+        for m, side in zip(nets[2:], (True, False)):   # captured (the setting is read while capturing)
+            ops.set_side_wgrad(side)
+            st = CapturedStep(m, ops.FusedAdam(m.parameters(), lr=lr),
+                              lambda mm, x: mm.bce_loss_bf16(x.permute(0, 3, 1, 2), 1.0, decode=cfg),
+                              allreduce=False, warmup=1)
+            for x in xs:
+                st(x)
+            steps.append(st)
+        torch.cuda.synchronize()
+        assert all(st.state == 'graph' for st in steps)
+    finally:
+        ops.set_side_wgrad(prev)
+    for pa, pb in zip(nets[2].parameters(), nets[3].parameters()):
+        d = (pa - pb).detach().abs()
+        assert float(d.mean()) < 0.1 * lr and float((d > 0.5 * lr).float().mean()) < 0.02
