@@ -216,11 +216,9 @@ __device__ inline void bn_fwd_finalize(const BnFwdFinal& f, const double* part, 
 // block; part: >= max(nt, 2 C) doubles of LDS, flag: one int; blk / nblk:
 // this block among the nblk that fold), block 0 writes db / dw, the last
 // block clears it; else dw / db are read as given.  M: elements per channel.
-// release false: the caller releases the accumulator itself later
-// (bn_acc_release with the same blk / nblk, every thread of the block).
 template <class BnDy>
 __device__ inline void bn_dy_coefs(const BnDy& d, int C, int64_t M, int chan0, double* part, int* flag, unsigned blk,
-                                   unsigned nblk, BnBwdCoef (&bc)[8], bool release = true) {
+                                   unsigned nblk, BnBwdCoef (&bc)[8]) {
   const float invM = 1.f / float(M);
   if (d.acc) {
     bn_acc_column_sums(d.acc, d.R, 2 * C, part);   // part[c] = db = sum gz, part[C + c] = dw = sum gz xhat
@@ -235,10 +233,8 @@ __device__ inline void bn_dy_coefs(const BnDy& d, int C, int64_t M, int chan0, d
       const int c = chan0 + i;
       bc[i].init(d.mean[c], d.invstd[c], d.w[c], d.b[c], float(part[C + c]), float(part[c]), invM);
     }
-    if (release) {
-      __syncthreads();
-      bn_acc_release(d.acc, d.R, C, flag, blk, nblk);
-    }
+    __syncthreads();
+    bn_acc_release(d.acc, d.R, C, flag, blk, nblk);
   } else {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {

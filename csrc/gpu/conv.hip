@@ -140,13 +140,11 @@ __device__ __forceinline__ void stage_lut(const uint16_t* lut, char* lds) {
   const int t = int(threadIdx.x);   // 256 threads x 8 bytes (threads past 256: nothing)
   if (t < 256) *reinterpret_cast<uint2*>(lds + 8 * t) = *reinterpret_cast<const uint2*>(lut + 4 * t);
 }
-__device__ __forceinline__ uint2 lut_px(const char* lds, uint32_t w, bool ok, bool alpha = true) {
+__device__ __forceinline__ uint2 lut_px(const char* lds, uint32_t w, bool ok) {
   const uint16_t* l = reinterpret_cast<const uint16_t*>(lds);
   if (!ok) return make_uint2(0u, 0u);
-  // alpha false: the 4th channel is staged as zero (an RGB weight on RGBA frames
-  // has no column for it) -- one table read in four saved
   return make_uint2(uint32_t(l[w & 255u]) | (uint32_t(l[256 + ((w >> 8) & 255u)]) << 16),
-                    uint32_t(l[512 + ((w >> 16) & 255u)]) | (alpha ? uint32_t(l[768 + (w >> 24)]) << 16 : 0u));
+                    uint32_t(l[512 + ((w >> 16) & 255u)]) | (uint32_t(l[768 + (w >> 24)]) << 16));
 }
 
 // The slice-reduce adds slice groups atomically into the gradient, which must
@@ -968,11 +966,13 @@ static_assert(4 * C4W_WAVE + kLutBytes <= c4w_lds<4>(), "staging fits the combin
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void conv_wgrad_c4w_kernel(ConvWgradParams p) {
   __shared__ __attribute__((aligned(16))) char smem[c4w_lds<NW>()];
-  __shared__ int rel_flag;
   if (run_side(p, smem)) return;
   const bool u8in = p.lut != nullptr;
-  const bool alpha = p.cin_out != 3;   // (cin_out 3: the RGB weight's gradient only -- alpha staged as zero)
   char* const lutl = smem + NW * C4W_WAVE;
+  if (u8in) {
+    stage_lut(p.lut, lutl);
+    __syncthreads();
+  }
   const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
   const int T = p.Cout / 32;
   const int nwg = main_blocks(p), b = int(blockIdx.x);
@@ -991,6 +991,11 @@ __global__ __launch_bounds__(64 * NW) void conv_wgrad_c4w_kernel(ConvWgradParams
   const int xp = lane & 31, kh0 = (lane >> 5) * 2;
   const bool bnd = p.bn_dy.y != nullptr;
   BnBwdCoef bc[8];
+  if (bnd) {   // (LDS scratch: the staging area, free until the loop)
+    bn_dy_coefs(p.bn_dy, p.Cout, p.M, co0 + dc * 8, reinterpret_cast<double*>(smem),
+                reinterpret_cast<int*>(smem + 4096), unsigned(b), unsigned(nwg), bc);
+    __syncthreads();
+  }
   const float slope = p.bn_dy.slope;
   const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(p.x, int64_t(p.N) * p.H * p.W * 4 * (u8in ? 1 : 2));
   const __amdgpu_buffer_rsrc_t rs_dy = make_rsrc(p.dy, p.M * p.Cout * 2);
@@ -1064,8 +1069,7 @@ __global__ __launch_bounds__(64 * NW) void conv_wgrad_c4w_kernel(ConvWgradParams
       const int chunk = (kh0 + (k >> 1)) * 2 + (k & 1);   // im2col columns 8 chunk .. + 7
       uint4 v;
       if (u8in) {
-        const uint2 lo = lut_px(lutl, r.x[k][0], (r.ok >> (2 * k)) & 1u, alpha),
-                    hi = lut_px(lutl, r.x[k][1], (r.ok >> (2 * k + 1)) & 1u, alpha);
+        const uint2 lo = lut_px(lutl, r.x[k][0], (r.ok >> (2 * k)) & 1u), hi = lut_px(lutl, r.x[k][1], (r.ok >> (2 * k + 1)) & 1u);
         v = make_uint4(lo.x, lo.y, hi.x, hi.y);
       } else {
         v = make_uint4(r.x[k][0], r.xh[k][0], r.x[k][1], r.xh[k][1]);
@@ -1086,15 +1090,8 @@ __global__ __launch_bounds__(64 * NW) void conv_wgrad_c4w_kernel(ConvWgradParams
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // the first stages' loads go out before the prologue (table staging, the BN
-  // accumulator fold): their latencies overlap it instead of following it
 #pragma unroll
   for (int u = 0; u < kDepth; ++u) load(ring[u]);
-  if (u8in) stage_lut(p.lut, lutl);
-  if (bnd)   // (LDS scratch: the staging area, free until the loop; the release waits for the kernel's end)
-    bn_dy_coefs(p.bn_dy, p.Cout, p.M, co0 + dc * 8, reinterpret_cast<double*>(smem), nullptr, unsigned(b),
-                unsigned(nwg), bc, false);
-  if (u8in || bnd) __syncthreads();
   const int padded = (mysteps + kDepth - 1) / kDepth * kDepth;
   for (int s0 = 0; s0 < padded; s0 += kDepth) {
 #pragma unroll
@@ -1135,9 +1132,6 @@ __global__ __launch_bounds__(64 * NW) void conv_wgrad_c4w_kernel(ConvWgradParams
     for (int w = 1; w < NW; ++w) v += cmb[w * 32 * 64 + e];   // (wave order: NW = 4 sums as before)
     out[e] = v;
   }
-  // every read of the BN accumulator came back in the prologue: its release
-  // ticket (and, for the last block, the clear) at the end, off the loads' path
-  if (bnd && p.bn_dy.acc) bn_acc_release(p.bn_dy.acc, p.bn_dy.R, p.Cout, &rel_flag, unsigned(b), unsigned(nwg));
 }
 
 // ---------------------------------------------------------------------------

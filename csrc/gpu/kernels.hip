@@ -776,8 +776,9 @@ hipError_t launch_replay(const DecodeParams& p, const ReplayParams& r, int64_t m
                    (int64_t(p.H) * p.W * p.Cin) % 16 == 0;
   if (vec) {
     const int grid = grid_for(int64_t(p.B) * p.H * p.W / PPT + meta_units, p.max_grid);
-    // BT_REPLAY_NT=1: fp32 NCHW table-mode output through non-temporal stores (A/B)
-    static const bool nt_env = std::getenv("BT_REPLAY_NT") && std::atoi(std::getenv("BT_REPLAY_NT")) > 0;
+    // fp32 NCHW table-mode output through non-temporal stores: batch 64 of
+    // 640x480 58.5 us against 62.8 (profiles/r5/b6; BT_REPLAY_NT=0: plain stores)
+    static const bool nt_env = !(std::getenv("BT_REPLAY_NT") && std::getenv("BT_REPLAY_NT")[0] == '0');
     const bool nt = nt_env && OUTT == OUT_F32 && p.layout == NCHW && p.xf_table_only;
 #define BT_REPLAY(CIN, LAY)                                                                  \
   do {                                                                                       \

@@ -454,6 +454,8 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const void* __restrict
       coef[C + pos(c)] = c1v;
     }
     __syncthreads();
+    // (the release at the kernel's end instead, after the stores: measured no
+    // faster -- profiles/r5/b7/bn_apply_bench.jsonl)
     if (fa.release) bn_acc_release(fa.acc, fa.R, C, &flag);
     const int gl = int(threadIdx.x) % G;   // this lane's channel group: channels V gl .. + V - 1
     float a0[V], a1[V];

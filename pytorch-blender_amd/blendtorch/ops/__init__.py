@@ -1289,8 +1289,10 @@ class WgradChain:
 
 
 _WGRAD_BLOCKS = int(os.environ.get('BT_WGRAD_BLOCKS', '512'))
-# weight gradients on a side stream, concurrent with the data-gradient chain (BT_WGRAD_SIDE=0: in line)
-_SIDE_WGRAD = os.environ.get('BT_WGRAD_SIDE', '1') not in ('', '0')
+# weight gradients on a side stream, concurrent with the data-gradient chain (BT_WGRAD_SIDE=1).  Off:
+# measured 13.7k img/s against 19.5k in line -- each concurrent pair of latency-bound kernels ran ~1.8x
+# its solo time (profiles/r5/b6: wgrad 44 us, dgrad 43 us side by side, 24 / 22 us alone)
+_SIDE_WGRAD = os.environ.get('BT_WGRAD_SIDE', '0') not in ('', '0')
 _SIDE_STREAMS = {}
 _SIDE_KEEP = []   # main-stream tensors the side stream reads, until it joins the main stream
 
@@ -1304,8 +1306,8 @@ def _side_stream(device):
 
 
 def set_side_wgrad(on):
-    """Weight gradients on a side stream (True, the default) or in line with
-    the data gradients (False); returns the previous setting."""
+    """Weight gradients on a side stream (True) or in line with the data
+    gradients (False, the default); returns the previous setting."""
     global _SIDE_WGRAD
     prev, _SIDE_WGRAD = _SIDE_WGRAD, bool(on)
     return prev

@@ -1,0 +1,30 @@
+#!/bin/bash
+# Round 5, GPU session 8: the disc step's roofline data (trace + PMC passes:
+# LDS bank conflicts, VALU/MFMA, HBM bytes) on the current kernels, the replay
+# sampler's LDS counters, and the disc bench after the c4w revert.
+set -u
+cd "$(dirname "$0")/../.."
+O=gpurun_out/r5b8
+mkdir -p $O
+export TMPDIR=/tmp
+trap 'find gpurun_out -type f -size +4M -print -delete; du -sh gpurun_out' EXIT
+for i in 1 2; do
+  timeout -k 10 200 python bench.py --consumer disc --steps 2000 > $O/disc.log 2>&1 || { tail -5 $O/disc.log; exit 1; }
+  grep '^{' $O/disc.log | tee -a $O/disc.jsonl | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'disc':d['value'],'ms':d['ms_per_step']}))"
+done
+bash scripts/gpurun/disc_roofline.sh r5b8 > $O/roofline.log 2>&1 || { tail -20 $O/roofline.log; exit 1; }
+cat gpurun_out/roof_r5b8/roofline.md
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --kernel-trace -d /tmp/rpmc_replay -o run --output-format csv -- python benchmarks/bench_replay.py --batch 64 --steps 100 --warmup 5 > $O/replay_pmc.log 2>&1 || { tail -5 $O/replay_pmc.log; exit 1; }
+f=$(find /tmp/rpmc_replay -name '*counter_collection.csv' | head -1)
+cp "$f" $O/replay_pmc.csv
+python - <<'PY'
+import csv, collections
+rows = list(csv.DictReader(open('gpurun_out/r5b8/replay_pmc.csv')))
+agg = collections.defaultdict(lambda: collections.defaultdict(float))
+for r in rows:
+    k = r['Kernel_Name'][:60]
+    agg[k][r['Counter_Name']] += float(r['Counter_Value'])
+for k, v in agg.items():
+    if v.get('SQ_LDS_IDX_ACTIVE'):
+        print(k, {c: round(x) for c, x in v.items()}, 'conflict %', round(100 * v['SQ_LDS_BANK_CONFLICT'] / max(1, v['SQ_LDS_IDX_ACTIVE'] - v['SQ_LDS_BANK_CONFLICT']), 1))
+PY
