@@ -963,11 +963,13 @@ template <int NW>
 constexpr int c4w_lds() { return NW * 32 * 64 * 4; }   // the combine: NW waves x [32][64] fp32
 static_assert(4 * C4W_WAVE + kLutBytes <= c4w_lds<4>(), "staging fits the combine area");
 
-template <int NW>
+// U8: the input is raw u8 frames read through the decode table (p.lut): a
+// compile-time switch, so neither form carries the other's stage registers
+template <int NW, bool U8>
 __global__ __launch_bounds__(64 * NW) void conv_wgrad_c4w_kernel(ConvWgradParams p) {
   __shared__ __attribute__((aligned(16))) char smem[c4w_lds<NW>()];
   if (run_side(p, smem)) return;
-  const bool u8in = p.lut != nullptr;
+  constexpr bool u8in = U8;
   char* const lutl = smem + NW * C4W_WAVE;
   if (u8in) {
     stage_lut(p.lut, lutl);
@@ -1028,7 +1030,7 @@ __global__ __launch_bounds__(64 * NW) void conv_wgrad_c4w_kernel(ConvWgradParams
       const bool row_ok = mx < m_end && unsigned(ih) < unsigned(p.H);
       const int e = ((c.n * p.H + ih) * p.W + iw) * 4;
       const bool ok0 = row_ok && unsigned(iw) < unsigned(p.W), ok1 = row_ok && unsigned(iw + 1) < unsigned(p.W);
-      if (u8in) {
+      if constexpr (u8in) {
         r.x[k][0] = bload4(rs_x, ok0 ? uint32_t(e) : kOOB);
         r.x[k][1] = bload4(rs_x, ok1 ? uint32_t(e + 4) : kOOB);
         r.ok |= (ok0 ? 1u : 0u) << (2 * k) | (ok1 ? 2u : 0u) << (2 * k);
@@ -1068,7 +1070,7 @@ __global__ __launch_bounds__(64 * NW) void conv_wgrad_c4w_kernel(ConvWgradParams
     for (int k = 0; k < 4; ++k) {
       const int chunk = (kh0 + (k >> 1)) * 2 + (k & 1);   // im2col columns 8 chunk .. + 7
       uint4 v;
-      if (u8in) {
+      if constexpr (u8in) {
         const uint2 lo = lut_px(lutl, r.x[k][0], (r.ok >> (2 * k)) & 1u), hi = lut_px(lutl, r.x[k][1], (r.ok >> (2 * k + 1)) & 1u);
         v = make_uint4(lo.x, lo.y, hi.x, hi.y);
       } else {
@@ -2545,8 +2547,11 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
   // (a BN backward folded in-kernel: the wave-private first-layer kernel or the register-staged one)
   const bool bn_folds = p.bn_dy.acc != nullptr;
   if (c4 && (c4_wave_private() || bn_folds)) {
-    if (c4w_waves() == 8) conv_wgrad_c4w_kernel<8><<<unsigned(grid), 512, 0, stream>>>(q);
-    else conv_wgrad_c4w_kernel<4><<<unsigned(grid), kThreads, 0, stream>>>(q);
+    const bool u8 = p.lut != nullptr;
+    if (c4w_waves() == 8 && u8) conv_wgrad_c4w_kernel<8, true><<<unsigned(grid), 512, 0, stream>>>(q);
+    else if (c4w_waves() == 8) conv_wgrad_c4w_kernel<8, false><<<unsigned(grid), 512, 0, stream>>>(q);
+    else if (u8) conv_wgrad_c4w_kernel<4, true><<<unsigned(grid), kThreads, 0, stream>>>(q);
+    else conv_wgrad_c4w_kernel<4, false><<<unsigned(grid), kThreads, 0, stream>>>(q);
   }
   else if (c4) conv_wgrad_c4_kernel<<<unsigned(grid), kThreads, 0, stream>>>(q);
   else if (bn_folds && wgrad_pipe()) conv_wgrad_kernel<true, true><<<unsigned(grid), kThreads, 0, stream>>>(q);

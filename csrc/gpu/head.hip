@@ -192,7 +192,10 @@ constexpr int kHeadFlat = 8;   // accumulator doubles per thread: 2 C R = 2048 (
 template <int KMAX>
 __global__ __launch_bounds__(kHeadThreads) void head_fwd_act_kernel(HeadParams p) {
   __shared__ float red[kHeadThreads / 64];
-  __shared__ float acc_l[kHeadThreads * 8];
+  // per-lane-group channel sums, [pl][g][9]: 9 words per channel group (8 +
+  // one of padding) so the 32 lanes of a row write 32 distinct banks (at 8 a
+  // row's 8 stores each ran 8-way conflicted)
+  __shared__ float acc_l[kHeadThreads * 9];
   __shared__ double fold[kHeadThreads * kHeadFlat];   // the [R][2C] replicas, then the column sums
   __shared__ __attribute__((aligned(16))) float coef[2 * kBnFoldMaxC];
   __shared__ int flags[2];
@@ -292,12 +295,12 @@ __global__ __launch_bounds__(kHeadThreads) void head_fwd_act_kernel(HeadParams p
     }
   }
 #pragma unroll
-  for (int q = 0; q < 8; ++q) acc_l[pl * p.C + g * 8 + q] = a[q];
+  for (int q = 0; q < 8; ++q) acc_l[pl * 9 * G + g * 9 + q] = a[q];
   __syncthreads();
   float part = 0.f;
   for (int c = t; c < p.C; c += kHeadThreads) {
     float s = 0.f;
-    for (int l = 0; l < PL; ++l) s += acc_l[l * p.C + c];
+    for (int l = 0; l < PL; ++l) s += acc_l[l * 9 * G + (c >> 3) * 9 + (c & 7)];
     const float pooled = s * inv;
     p.pooled[(int64_t(n) * p.OH * p.OW + cell) * p.C + c] = pooled;
     part += pooled * p.w[c * p.ws_c + i * p.ws_i + j * p.ws_j];

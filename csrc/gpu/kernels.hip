@@ -171,8 +171,13 @@ __device__ __forceinline__ float xf_value(const Xf& xf, int c, uint32_t v) {
 // branches on it once (scalar branch) into a fully static body, so every
 // byte of `px` is addressed with a compile-time index and `px` stays in
 // VGPRs (a dynamically indexed byte array would be spilled to scratch).
-template <int PPT, int CIN, int IC, bool TBL = false>
+template <int PPT, int CIN, int IC, int TBL = 0>
 __device__ __forceinline__ void lookup_static(const Pixels<PPT, CIN>& px, const Xf& xf, int c, float (&o)[PPT]) {
+  if constexpr (TBL == 2) {   // one table for every output channel, 32 copies: xf.lut is this lane's copy
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) o[i] = xf.lut[px.v[i * CIN + IC] * 32u];
+    return;
+  }
   if (TBL || !xf.arith) {   // TBL: the host promised a table-mode value table (no arithmetic code at all)
     const float* l = xf.lut + c * 256;
 #pragma unroll
@@ -206,7 +211,7 @@ __device__ __forceinline__ void lookup_static(const Pixels<PPT, CIN>& px, const 
   }
 }
 
-template <int PPT, int CIN, bool TBL = false>
+template <int PPT, int CIN, int TBL = 0>
 __device__ __forceinline__ void lookup(const Pixels<PPT, CIN>& px, int ic, const Xf& xf, int c, float (&o)[PPT]) {
   switch (ic) {
     case 0: lookup_static<PPT, CIN, 0, TBL>(px, xf, c, o); break;
@@ -216,7 +221,7 @@ __device__ __forceinline__ void lookup(const Pixels<PPT, CIN>& px, int ic, const
   }
 }
 
-template <int PPT, int CIN, int OUTT, int COUT, bool TBL = false>
+template <int PPT, int CIN, int OUTT, int COUT, int TBL = 0>
 __device__ __forceinline__ void store_nhwc(const DecodeParams& p, const Xf& xf, const int* cm,
                                            const Pixels<PPT, CIN>& px, int b, int64_t q, int64_t HW) {
   constexpr int N = PPT * COUT;
@@ -297,7 +302,7 @@ __device__ __forceinline__ Group locate(const DecodeParams& p, int64_t g, int64_
 
 // NT: streaming (non-temporal) stores -- output written once and read by a
 // later kernel, kept out of the L2's write-back set (replay sample A/B)
-template <int PPT, int CIN, int OUTT, int LAYOUT, bool TBL = false, bool NT = false>
+template <int PPT, int CIN, int OUTT, int LAYOUT, int TBL = 0, bool NT = false>
 __device__ __forceinline__ void emit(const DecodeParams& p, const Xf& xf, const int* cm, int cout, int64_t HW,
                                      const Group& gr, const Pixels<PPT, CIN>& px) {
   const int b = gr.b;
@@ -631,11 +636,13 @@ __device__ __forceinline__ uint32_t philox_word(uint64_t seed, uint64_t ctr, uin
 
 // Block prologue shared by both replay kernels: the table, this launch's B
 // frame indices (drawn or given) in LDS, and the counter hand-over.
-struct ReplayShared {
-  uint32_t tab[kTabWords];
+template <int TW>
+struct ReplaySharedT {
+  uint32_t tab[TW];
   int64_t idx[kMaxReplayB];
   uint64_t ctr;
 };
+using ReplayShared = ReplaySharedT<kTabWords>;
 
 __device__ Xf replay_prologue(const DecodeParams& p, const ReplayParams& r, ReplayShared& sh) {
   const Xf xf = stage_xf(p.lut, sh.tab, p.Cout);
@@ -659,7 +666,8 @@ __global__ void replay_advance_kernel(uint64_t* counter, int B) { counter[0] += 
 
 // metadata unit m of the launch: 4-byte words of 4-byte-multiple columns,
 // single bytes otherwise
-__device__ __forceinline__ void replay_meta(const ReplayParams& r, const ReplayShared& sh, int B, int64_t m) {
+template <class Shared>
+__device__ __forceinline__ void replay_meta(const ReplayParams& r, const Shared& sh, int B, int64_t m) {
   for (int k = 0; k < r.nmeta; ++k) {
     const int nb = r.meta_bytes[k];
     const int w = (nb % 4 == 0) ? 4 : 1;
@@ -679,10 +687,15 @@ __device__ __forceinline__ void replay_meta(const ReplayParams& r, const ReplayS
 
 // TBL: the value table is in table mode (p.xf_table_only): the lookups are
 // plain LDS reads and the kernel carries none of the arithmetic-form code
-// (whose registers cut the general kernel to 4 waves per SIMD)
-template <int PPT, int CIN, int OUTT, int LAYOUT, bool TBL, bool NT = false>
+// (whose registers cut the general kernel to 4 waves per SIMD).  TBL 2: every
+// output channel has the same table (xf_table_only 2) -- staged as 32 copies
+// interleaved by word, [value][copy], and lane l reads copy l % 32: the 32
+// lanes of a ds_read group always hit 32 distinct banks (one 1 KiB table read
+// at random bytes ran ~3.4-way conflicted)
+constexpr int kUniWords = 256 * 32;
+template <int PPT, int CIN, int OUTT, int LAYOUT, int TBL, bool NT = false>
 __global__ __launch_bounds__(kBlock) void replay_vec_kernel(DecodeParams p, ReplayParams r, int64_t meta_units) {
-  __shared__ ReplayShared sh;
+  __shared__ ReplaySharedT<TBL == 2 ? kUniWords : kTabWords> sh;
   const int64_t HW = int64_t(p.H) * p.W;
   const int64_t groups_per_img = HW / PPT;
   const int64_t groups = groups_per_img * p.B;
@@ -712,7 +725,20 @@ __global__ __launch_bounds__(kBlock) void replay_vec_kernel(DecodeParams p, Repl
     gr0.src = p.src + frame_of(gr0.b) * r.frame_bytes + (int64_t(sy) * p.W + x) * CIN;
     load_pixels<PPT, CIN>(gr0.src, px0);
   }
-  const Xf xf = stage_xf(p.lut, sh.tab, p.Cout);
+  Xf xf;
+  if constexpr (TBL == 2) {
+    // header scalars as stage_xf reads them; the table expanded into its 32
+    // copies (word w = 32 value + copy: consecutive lanes, consecutive words)
+    xf.arith = 0;
+    float v[kUniWords / kBlock];
+#pragma unroll
+    for (int i = 0; i < kUniWords / kBlock; ++i) v[i] = p.lut[(int(threadIdx.x) + kBlock * i) >> 5];
+#pragma unroll
+    for (int i = 0; i < kUniWords / kBlock; ++i) sh.tab[int(threadIdx.x) + kBlock * i] = __float_as_uint(v[i]);
+    xf.lut = reinterpret_cast<const float*>(sh.tab) + (threadIdx.x & 31);
+  } else {
+    xf = stage_xf(p.lut, sh.tab, p.Cout);
+  }
   for (int b = threadIdx.x; b < p.B; b += kBlock) {
     const int64_t i = frame_of(b);
     sh.idx[b] = i;
@@ -780,11 +806,17 @@ hipError_t launch_replay(const DecodeParams& p, const ReplayParams& r, int64_t m
     // 640x480 58.5 us against 62.8 (profiles/r5/b6; BT_REPLAY_NT=0: plain stores)
     static const bool nt_env = !(std::getenv("BT_REPLAY_NT") && std::getenv("BT_REPLAY_NT")[0] == '0');
     const bool nt = nt_env && OUTT == OUT_F32 && p.layout == NCHW && p.xf_table_only;
+    // one table for all channels (xf_table_only 2): the 32-copy conflict-free form
+    // (BT_REPLAY_UNI=0: the 1 KiB table per channel instead)
+    static const bool uni_env = !(std::getenv("BT_REPLAY_UNI") && std::getenv("BT_REPLAY_UNI")[0] == '0');
+    const bool uni = uni_env && p.xf_table_only == 2;
 #define BT_REPLAY(CIN, LAY)                                                                  \
   do {                                                                                       \
-    if (nt) replay_vec_kernel<PPT, CIN, OUTT, LAY, true, true><<<grid, kBlock, 0, s>>>(p, r, meta_units); \
-    else if (p.xf_table_only) replay_vec_kernel<PPT, CIN, OUTT, LAY, true><<<grid, kBlock, 0, s>>>(p, r, meta_units); \
-    else replay_vec_kernel<PPT, CIN, OUTT, LAY, false><<<grid, kBlock, 0, s>>>(p, r, meta_units);               \
+    if (uni && nt) replay_vec_kernel<PPT, CIN, OUTT, LAY, 2, true><<<grid, kBlock, 0, s>>>(p, r, meta_units); \
+    else if (uni) replay_vec_kernel<PPT, CIN, OUTT, LAY, 2><<<grid, kBlock, 0, s>>>(p, r, meta_units); \
+    else if (nt) replay_vec_kernel<PPT, CIN, OUTT, LAY, 1, true><<<grid, kBlock, 0, s>>>(p, r, meta_units); \
+    else if (p.xf_table_only) replay_vec_kernel<PPT, CIN, OUTT, LAY, 1><<<grid, kBlock, 0, s>>>(p, r, meta_units); \
+    else replay_vec_kernel<PPT, CIN, OUTT, LAY, 0><<<grid, kBlock, 0, s>>>(p, r, meta_units);               \
   } while (0)
     if (p.Cin == 4) {
       if (p.layout == NCHW) BT_REPLAY(4, NCHW);

@@ -381,15 +381,23 @@ def device_lut(cfg: DecodeConfig, device):
         tab = build_table(cfg)
         t = torch.from_numpy(tab).to(device)
         _lut_cache[key] = t
-        _lut_cache[('mode',) + key] = int(tab[XF_HEADER])
+        mode = int(tab[XF_HEADER])
+        # table mode with the same 256 values for every output channel: the
+        # replay kernel's conflict-free 32-copy table form takes it (table_only 2)
+        uni = mode == 0 and all(np.array_equal(tab[:256], tab[256 * c:256 * (c + 1)]) for c in range(1, cfg.cout))
+        _lut_cache[('mode',) + key] = mode
+        _lut_cache[('uni',) + key] = uni
     return t
 
 
 def table_only(cfg: DecodeConfig, device) -> int:
     """1 when ``device_lut(cfg, device)`` is in table mode (header mode 0):
-    kernels may then take their table-only variant."""
+    kernels may then take their table-only variant; 2 when besides every
+    output channel has the same table."""
     device_lut(cfg, device)
-    return int(_lut_cache[('mode', cfg, str(device))] == 0)
+    if _lut_cache[('mode', cfg, str(device))] != 0:
+        return 0
+    return 2 if _lut_cache[('uni', cfg, str(device))] else 1
 
 
 def _stream(device):

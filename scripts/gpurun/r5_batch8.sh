@@ -8,6 +8,9 @@ O=gpurun_out/r5b8
 mkdir -p $O
 export TMPDIR=/tmp
 trap 'find gpurun_out -type f -size +4M -print -delete; du -sh gpurun_out' EXIT
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider \
+  tests/test_conv_wgrad.py tests/test_gpu_consumer.py tests/test_replay.py -m gpu > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
 for i in 1 2; do
   timeout -k 10 200 python bench.py --consumer disc --steps 2000 > $O/disc.log 2>&1 || { tail -5 $O/disc.log; exit 1; }
   grep '^{' $O/disc.log | tee -a $O/disc.jsonl | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'disc':d['value'],'ms':d['ms_per_step']}))"
@@ -26,5 +29,12 @@ for r in rows:
     agg[k][r['Counter_Name']] += float(r['Counter_Value'])
 for k, v in agg.items():
     if v.get('SQ_LDS_IDX_ACTIVE'):
-        print(k, {c: round(x) for c, x in v.items()}, 'conflict %', round(100 * v['SQ_LDS_BANK_CONFLICT'] / max(1, v['SQ_LDS_IDX_ACTIVE'] - v['SQ_LDS_BANK_CONFLICT']), 1))
+        print(k, {c: round(x) for c, x in v.items()}, 'conflict %', round(100 * v['SQ_LDS_BANK_CONFLICT'] / v['SQ_LDS_IDX_ACTIVE'], 1))
 PY
+for v in "uni:" "tbl:BT_REPLAY_UNI=0" "uni:" "tbl:BT_REPLAY_UNI=0"; do
+  name=${v%%:*}; e=${v#*:}
+  for b in 64 8; do
+    timeout -k 10 120 env $e python benchmarks/bench_replay.py --batch $b --steps 2000 > $O/replay.log 2>&1 || { tail -5 $O/replay.log; exit 1; }
+    grep '^{' $O/replay.log | tee -a $O/replay_${name}_b$b.jsonl | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'v':'$name','B':$b,'us':d['us_per_batch'],'tbps':d['effective_tbps']}))"
+  done
+done

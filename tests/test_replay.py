@@ -192,3 +192,23 @@ def test_replay_buffer_uses_fused_sampler():
     for b in (b1, b2):
         assert torch.equal(b['image'], ops.decode(rb.store[b['index']], cfg))
         assert torch.equal(b['frameid'], b['index']) and torch.equal(b['xy'], rb.meta['xy'][b['index']])
+
+
+def test_table_only_flags_channel_uniform_tables():
+    """table_only: 2 (the replay kernel's 32-copy conflict-free table form)
+    exactly when the table is in table mode and every output channel has the
+    same 256 values; 1 for per-channel tables; 0 for the arithmetic form."""
+    import numpy as np
+    for cfg in (ops.DecodeConfig.unit(channels='rgb', gamma=2.2),
+                ops.DecodeConfig.unit(channels='bgr', dtype='bfloat16', layout='nhwc'),
+                ops.DecodeConfig.densityopt(channels='rgb', gamma=2.2),
+                ops.DecodeConfig(channels='rgb', mean=[0.1, 0.2, 0.3], std=[1.0, 2.0, 3.0]),
+                ops.DecodeConfig(channels='rgba')):
+        tab = ops.build_table(cfg)
+        if int(tab[ops.XF_HEADER]) != 0:
+            want = 0
+        else:
+            same = all(np.array_equal(tab[:256], tab[256 * c:256 * (c + 1)]) for c in range(1, cfg.cout))
+            want = 2 if same else 1
+        assert ops.table_only(cfg, torch.device('cpu')) == want, cfg
+    assert ops.table_only(ops.DecodeConfig.unit(channels='rgb', gamma=2.2), torch.device('cpu')) == 2
