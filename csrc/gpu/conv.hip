@@ -155,12 +155,15 @@ __device__ __forceinline__ int main_blocks(const ConvWgradParams& p) {
   return p.main_blocks > 0 ? p.main_blocks : int(gridDim.x);
 }
 
-__device__ __forceinline__ void zero_output(const ConvWgradParams& p) {
+// bid: the block's index in the weight gradient's own grid (blockIdx.x, or its
+// place in a launch shared with a data gradient: dgrad_wgrad_kernel)
+__device__ __forceinline__ void zero_output(const ConvWgradParams& p, int bid) {
   if (!p.zero_out) return;
   const int per = (p.zero_count + main_blocks(p) - 1) / main_blocks(p);
-  const int e0 = int(blockIdx.x) * per, e1 = e0 + per < p.zero_count ? e0 + per : p.zero_count;
+  const int e0 = bid * per, e1 = e0 + per < p.zero_count ? e0 + per : p.zero_count;
   for (int e = e0 + int(threadIdx.x); e < e1; e += int(blockDim.x)) p.zero_out[e] = 0.f;
 }
+__device__ __forceinline__ void zero_output(const ConvWgradParams& p) { zero_output(p, int(blockIdx.x)); }
 
 // Sum the S slices into fp32 dW[co][kh][kw][ci] at the parameter's strides.
 // blockIdx.y takes a group of kSliceGroup slices and each lane four
@@ -213,8 +216,8 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_reduce_kernel(ConvWgradPa
 // blocks past the main grid: a previous layer's deferred reduce (the side
 // job), then -- one block -- the BN statistics fold the preceding data
 // gradient's epilogue accumulated (ConvWgradParams::fold)
-__device__ __forceinline__ bool run_side(const ConvWgradParams& p, char* lds) {
-  int b = int(blockIdx.x) - main_blocks(p);
+__device__ __forceinline__ bool run_side(const ConvWgradParams& p, char* lds, int bid) {
+  int b = bid - main_blocks(p);
   if (b < 0) return false;
   const int nred = p.side.partial ? p.side.rx * p.side.ry : 0;
   if (b < nred) {
@@ -226,6 +229,9 @@ __device__ __forceinline__ bool run_side(const ConvWgradParams& p, char* lds) {
   f.o0 = p.fold.db, f.o1 = p.fold.dw;
   bn_fold_block(f, reinterpret_cast<double*>(lds));
   return true;
+}
+__device__ __forceinline__ bool run_side(const ConvWgradParams& p, char* lds) {
+  return run_side(p, lds, int(blockIdx.x));
 }
 
 struct PixelCursor {   // (n, oh, ow) of pixel m, advanced by BPX per k-step
@@ -288,15 +294,15 @@ struct XCursor {
 // PIPE: the next step's fragments are read right after the barrier that
 // publishes them, while this step's MFMAs run (two fragment sets, +24 VGPRs):
 // without it every step waited out barrier -> LDS read latency -> MFMAs in turn.
+constexpr int kWgradLds = 2 * STAGE;
 template <bool BND, bool PIPE = false>
-__global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
-  if (run_side(p, smem)) return;
+__device__ __forceinline__ void conv_wgrad_body(const ConvWgradParams& p, char* smem, int bid) {
+  if (run_side(p, smem, bid)) return;
   const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
   const int KC = 16 * p.Cin, KT = KC / BKC, T = (p.Cout / BCO) * KT;
 
   // XCD-aware bijective remap: consecutive work ids share an XCD (blockIdx % 8)
-  const int nwg = main_blocks(p), b = int(blockIdx.x);
+  const int nwg = main_blocks(p), b = bid;
   const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
   const int slice = w / T, tile = w - slice * T;
@@ -483,7 +489,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p)
   }
 
   // C/D map of 16x16x32: column = lane & 15 (kc), row = 4 * (lane >> 4) + reg (co)
-  zero_output(p);
+  zero_output(p, bid);
   // 32-bit offsets from the lane's first element (the slice's partial block
   // is < 2^31 elements): one add per store instead of 64-bit address math
   float* out = p.partial + int64_t(slice) * p.Cout * KC + (co0 + wco + 4 * (lane >> 4)) * KC +
@@ -494,6 +500,12 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p)
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) out[(16 * i + r) * KC + 16 * j] = acc[i][j][r];
+}
+
+template <bool BND, bool PIPE = false>
+__global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[kWgradLds];
+  conv_wgrad_body<BND, PIPE>(p, smem, int(blockIdx.x));
 }
 
 // ---------------------------------------------------------------------------
@@ -1225,8 +1237,17 @@ struct TapGemm {
 // pass of its own.  ACT = coefficient sets per thread: a thread's chunk is
 // always the same 8 channels when C <= 64 (1), or alternates between two with
 // the k-step when C = 128 (2).
+// LDS of a tap GEMM block (the formulas of tap_gemm_body's STG / NBUF / RT / LUTB)
+template <bool DGRAD, int BN, bool C4, int BM, int NST>
+constexpr int tap_gemm_lds() {
+  return ((C4 || NST == 0) ? 2 : NST) * (BM * F_ROW + BN * F_ROW) + (C4 ? 0 : BM * 16) + (C4 ? kLutBytes : 0);
+}
+
+// bx, by, nwg: the block's place in the GEMM's own grid (blockIdx.x / .y and
+// gridDim.x, or its place in a launch shared with a weight gradient:
+// dgrad_wgrad_kernel); smem: tap_gemm_lds() bytes
 template <bool DGRAD, int BN, bool C4 = false, int BM = FBM, int NST = 0, int CLS = 1, int ACT = 0>
-__global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
+__device__ __forceinline__ void tap_gemm_body(const TapGemm& p, char* smem, int bx, int by, int nwg) {
   static_assert(ACT == 0 || (!DGRAD && !C4 && NST >= 2), "the BN apply rides on the forward's LDS-DMA staging");
   constexpr int RJ = BM / 32;                  // staged A rows per thread (ar + 32 j)
   constexpr int A_TILE = BM * F_ROW;
@@ -1248,7 +1269,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   // the tile's row table after the staging space (not C4): {abase, vmask, obase, in range} per GEMM row
   constexpr int RT_OFF = NBUF * STG, RT = C4 ? 0 : BM * 16;
   constexpr int LUT_OFF = NBUF * STG + RT, LUTB = C4 ? kLutBytes : 0;   // C4: the u8 decode table
-  __shared__ __attribute__((aligned(16))) char smem[NBUF * STG + RT + LUTB];
+  static_assert(tap_gemm_lds<DGRAD, BN, C4, BM, NST>() == NBUF * STG + RT + LUTB, "tap_gemm_lds matches");
   float* red = reinterpret_cast<float*>(smem + E_TILE);   // [WGM][2][BN], after the epilogue tile
   const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
   constexpr int NTAPS = DGRAD ? 4 : 16;
@@ -1269,7 +1290,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   constexpr int ncls = DGRAD ? CLS : 1;
   int ph = 0, pw = 0;
 
-  const int nwg = int(gridDim.x), b = int(blockIdx.x);
+  const int b = bx;
   const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
   const int mt = w / NT, n0 = (w - mt * NT) * BN;
@@ -1290,7 +1311,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
     for (int e = 0; e < 8; ++e) bs[q][e] = bq[q][e] = 0.f;
   for (int cls_i = 0; cls_i < ncls; ++cls_i) {
   if constexpr (DGRAD) {
-    const int cls = int(blockIdx.y) * ncls + cls_i;
+    const int cls = by * ncls + cls_i;
     ph = cls >> 1;
     pw = cls & 1;
   }
@@ -1588,9 +1609,9 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
       f.eps = p.act.eps, f.momentum = p.act.momentum, f.mean = p.act.mean, f.invstd = p.act.invstd;
       f.rm = p.act.rm, f.rv = p.act.rv, f.tracked = p.act.tracked;
       for (int c = t; c < p.C; c += kThreads)
-        bn_fwd_finalize(f, part, p.C, p.act.M, c, blockIdx.x == 0, coef[c], coef[p.C + c]);
+        bn_fwd_finalize(f, part, p.C, p.act.M, c, bx == 0, coef[c], coef[p.C + c]);
       __syncthreads();
-      bn_acc_release(p.act.acc, p.act.R, p.C, flag);
+      bn_acc_release(p.act.acc, p.act.R, p.C, flag, unsigned(bx), unsigned(nwg));
 #pragma unroll
       for (int u = 0; u < NSET; ++u) {
         const int cbase = (u * FBK + acs * 8) & (p.C - 1);   // this thread's chunk channels at k-steps u, u + NSET, ...
@@ -1968,7 +1989,7 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
       for (int w4 = 0; w4 < RG; ++w4) v += red[(w4 * 2 + which) * BN + c];
       // channel-major [2][NOUT][rows], row = (pixel tile, parity class); or
       // added into replica row % R of an accumulator [R][2][NOUT] (bn_bwd_apply_acc folds it)
-      const int row = mt * 4 + int(blockIdx.y) * ncls;
+      const int row = mt * 4 + by * ncls;
       if (p.bn.acc_r > 0) {
         unsafeAtomicAdd(reinterpret_cast<double*>(p.bn.part) + ((row % p.bn.acc_r) * 2 + which) * p.NOUT + n0 + c,
                         double(v));
@@ -1989,6 +2010,12 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
       unsafeAtomicAdd(reinterpret_cast<double*>(p.stats) + ((mt % p.acc_r) * 2 + which) * p.NOUT + n0 + c, double(v));
     else p.stats[(which * p.NOUT + n0 + c) * ((p.M + BM - 1) / BM) + mt] = v;
   }
+}
+
+template <bool DGRAD, int BN, bool C4 = false, int BM = FBM, int NST = 0, int CLS = 1, int ACT = 0>
+__global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
+  __shared__ __attribute__((aligned(16))) char smem[tap_gemm_lds<DGRAD, BN, C4, BM, NST>()];
+  tap_gemm_body<DGRAD, BN, C4, BM, NST, CLS, ACT>(p, smem, int(blockIdx.x), int(blockIdx.y), int(gridDim.x));
 }
 
 // ---------------------------------------------------------------------------
@@ -2221,16 +2248,17 @@ __device__ __forceinline__ int dpw_off(int ci, int kc) {
   return ci * DP_WROW + ((kc ^ ((ci & 3) | (((ci >> 3) & 3) << 2))) << 4);
 }
 
-__global__ __launch_bounds__(kThreads) void dgrad_patch_kernel(TapGemm p) {
+// one weight buffer (43 KB of LDS: 3 blocks per CU; double-buffered, 59 KB, fit 2 and ran slower)
+constexpr int kDpatchLds = DP_PATCH + DP_W + 4 * 2 * DP_NOUT * 4;
+// blk: the block's index in its own grid (blockIdx.x, or its place in a launch
+// shared with the weight gradient: dpatch_wgrad_kernel)
+__device__ __forceinline__ void dgrad_patch_body(const TapGemm& p, char* smem, int blk) {
   constexpr int NCH = DP_NP * 8, NL = (NCH + kThreads - 1) / kThreads;
   constexpr int WCH = DP_W / 16, WL = WCH / kThreads;   // 1024 weight chunks, 4 per thread
-  // one weight buffer (43 KB of LDS: 3 blocks per CU; double-buffered, 59 KB, fit 2 and ran slower)
-  __shared__ __attribute__((aligned(16))) char smem[DP_PATCH + DP_W + 4 * 2 * DP_NOUT * 4];
   char* const wl = smem + DP_PATCH;
   float* red = reinterpret_cast<float*>(smem + DP_PATCH + DP_W);
   const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6, g = lane >> 4;
   const int tb = (p.GW + DP_TB - 1) / DP_TB, ta = (p.GH + DP_TA - 1) / DP_TA;
-  const int blk = int(blockIdx.x);
   const int n = blk / (ta * tb), rem = blk - n * (ta * tb);
   const int a0 = (rem / tb) * DP_TA, b0 = (rem % tb) * DP_TB;
   // a class's weight chunks: chunk c = t + 256 i -> row ci = c / 32, chunk kc = c % 32
@@ -2386,6 +2414,11 @@ __global__ __launch_bounds__(kThreads) void dgrad_patch_kernel(TapGemm p) {
   }
 }
 
+__global__ __launch_bounds__(kThreads) void dgrad_patch_kernel(TapGemm p) {
+  __shared__ __attribute__((aligned(16))) char smem[kDpatchLds];
+  dgrad_patch_body(p, smem, int(blockIdx.x));
+}
+
 // several weights at once (blockIdx.y = tensor): the data gradients' operands for every layer in one launch
 __global__ __launch_bounds__(kThreads) void weight_t_multi_kernel(WeightTParams p) {
   const int k = int(blockIdx.y);
@@ -2420,6 +2453,15 @@ int dgrad_patch() {
     g_dgrad_patch = v ? (std::atoi(v) ? 1 : 0) : 1;
   }
   return g_dgrad_patch;
+}
+// the patch data gradient held for a shared launch with the weight gradient
+// (dpatch_wgrad_kernel) when conv_dgrad_hold is on; BT_FUSE_PATCH=0: never
+int fuse_patch() {
+  static const int v = [] {
+    const char* e = std::getenv("BT_FUSE_PATCH");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return v;
 }
 int g_wgrad_wide = -1;   // register-staged weight gradient over 256-column tiles (BT_WGRAD_WIDE)
 int wgrad_wide() {
@@ -2498,6 +2540,83 @@ hipError_t conv_wgrad_reduce(const ConvWgradParams::Reduce& r, hipStream_t strea
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// A layer's data gradient and weight gradient in ONE launch.  Both are
+// latency-bound at 3 blocks per CU (tap GEMM: 16-64 k-steps of LDS-DMA
+// stages; weight gradient: ~40 pixel steps per slice), and both read the
+// same dY: sharing the CUs fills each other's memory waits, and the kernel
+// boundary between them goes away.  Blocks alternate in runs of 8 (a data-
+// gradient run, then a weight-gradient run, ... then the longer kind's
+// rest), so each part's XCD-aware tile order still sees consecutive ids on
+// one XCD.  The weight-gradient part may carry its chain's deferred reduce
+// (its side blocks) but not a BN fold: the fold would read the accumulator
+// this launch's data gradient is still filling (the BN backward then folds
+// it in its own apply).  conv_dgrad holds its tap-GEMM launch while
+// conv_dgrad_hold(1) is set; the next conv_wgrad on that stream launches
+// both, or conv_dgrad_flush launches the data gradient alone.
+template <int BM, bool PIPE>
+__global__ __launch_bounds__(kThreads) void dgrad_wgrad_kernel(TapGemm g, ConvWgradParams q, int gx, int nd, int nw) {
+  constexpr int TL = tap_gemm_lds<true, 64, false, BM, 2>();
+  __shared__ __attribute__((aligned(16))) char smem[TL > kWgradLds ? TL : kWgradLds];
+  const int b = int(blockIdx.x);
+  const int nd8 = (nd + 7) & ~7, nw8 = (nw + 7) & ~7, m8 = nd8 < nw8 ? nd8 : nw8;
+  int kind, idx;
+  if (b < 2 * m8) {
+    const int run = b >> 3;
+    kind = run & 1;
+    idx = ((run >> 1) << 3) | (b & 7);
+  } else {
+    kind = nd8 > nw8 ? 0 : 1;
+    idx = m8 + (b - 2 * m8);
+  }
+  if (kind == 0) {
+    if (idx >= nd) return;   // (padding of the run: block-uniform, before any barrier)
+    tap_gemm_body<true, 64, false, BM, 2, 1, 0>(g, smem, idx % gx, idx / gx, gx);
+  } else {
+    if (idx >= nw) return;
+    conv_wgrad_body<false, PIPE>(q, smem, idx);
+  }
+}
+
+// the same for the 32-channel layer's patch data gradient (dgrad_patch_body)
+template <bool PIPE>
+__global__ __launch_bounds__(kThreads) void dpatch_wgrad_kernel(TapGemm g, ConvWgradParams q, int nd, int nw) {
+  __shared__ __attribute__((aligned(16))) char smem[kDpatchLds > kWgradLds ? kDpatchLds : kWgradLds];
+  const int b = int(blockIdx.x);
+  const int nd8 = (nd + 7) & ~7, nw8 = (nw + 7) & ~7, m8 = nd8 < nw8 ? nd8 : nw8;
+  int kind, idx;
+  if (b < 2 * m8) {
+    const int run = b >> 3;
+    kind = run & 1;
+    idx = ((run >> 1) << 3) | (b & 7);
+  } else {
+    kind = nd8 > nw8 ? 0 : 1;
+    idx = m8 + (b - 2 * m8);
+  }
+  if (kind == 0) {
+    if (idx >= nd) return;
+    dgrad_patch_body(g, smem, idx);
+  } else {
+    if (idx >= nw) return;
+    conv_wgrad_body<false, PIPE>(q, smem, idx);
+  }
+}
+
+namespace {
+struct HeldDgrad {
+  bool on = false;
+  bool patch = false;   // dgrad_patch_kernel's grid (gx blocks), else the tap GEMM's (gx x 4 classes)
+  TapGemm g;
+  int bm = 0;
+  unsigned gx = 0;   // the data gradient's x grid (4 parity classes in y)
+  hipStream_t s = nullptr;
+};
+HeldDgrad g_held;
+bool g_hold = false;
+}  // namespace
+
+bool conv_dgrad_held() { return g_held.on; }
+
 hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_t s_ci, int64_t s_kh, int64_t s_kw,
                       hipStream_t stream, ConvWgradParams::Reduce* defer, const ConvWgradParams::Reduce* side) {
   if (!conv_wgrad_supported(p.Cin, p.Cout) || p.slices <= 0 || !p.x || !p.dy || !p.partial || !out ||
@@ -2546,7 +2665,35 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
   }
   // (a BN backward folded in-kernel: the wave-private first-layer kernel or the register-staged one)
   const bool bn_folds = p.bn_dy.acc != nullptr;
-  if (c4 && (c4_wave_private() || bn_folds)) {
+  bool fused = false;
+  if (g_held.on) {   // a held data gradient: one launch for both when this is the plain kernel's case
+    const bool dma = (wgrad_staging() == 2 || wgrad_staging() == 3) && (p.Cin & (p.Cin - 1)) == 0 && p.Wo >= 32;
+    const bool plain = !c4 && !bn_folds && !p.bn_dy.y && !p.fold.acc && !dma && !wide;
+    const int64_t nd = int64_t(g_held.gx) * (g_held.patch ? 1 : 4);
+    if (plain && stream == g_held.s && nd + grid + 16 < (int64_t(1) << 31)) {
+      const unsigned total = unsigned(((nd + 7) & ~int64_t(7)) + ((grid + 7) & ~int64_t(7)));
+      const int gx = int(g_held.gx), ndi = int(nd), nwi = int(grid);
+      if (g_held.patch && wgrad_pipe())
+        dpatch_wgrad_kernel<true><<<total, kThreads, 0, stream>>>(g_held.g, q, ndi, nwi);
+      else if (g_held.patch)
+        dpatch_wgrad_kernel<false><<<total, kThreads, 0, stream>>>(g_held.g, q, ndi, nwi);
+      else if (g_held.bm == 64 && wgrad_pipe())
+        dgrad_wgrad_kernel<64, true><<<total, kThreads, 0, stream>>>(g_held.g, q, gx, ndi, nwi);
+      else if (g_held.bm == 64)
+        dgrad_wgrad_kernel<64, false><<<total, kThreads, 0, stream>>>(g_held.g, q, gx, ndi, nwi);
+      else if (wgrad_pipe())
+        dgrad_wgrad_kernel<FBM, true><<<total, kThreads, 0, stream>>>(g_held.g, q, gx, ndi, nwi);
+      else
+        dgrad_wgrad_kernel<FBM, false><<<total, kThreads, 0, stream>>>(g_held.g, q, gx, ndi, nwi);
+      g_held.on = false;
+      fused = true;
+    } else {
+      const hipError_t e = conv_dgrad_flush();
+      if (e != hipSuccess) return e;
+    }
+  }
+  if (fused) {
+  } else if (c4 && (c4_wave_private() || bn_folds)) {
     const bool u8 = p.lut != nullptr;
     if (c4w_waves() == 8 && u8) conv_wgrad_c4w_kernel<8, true><<<unsigned(grid), 512, 0, stream>>>(q);
     else if (c4w_waves() == 8) conv_wgrad_c4w_kernel<8, false><<<unsigned(grid), 512, 0, stream>>>(q);
@@ -2832,11 +2979,46 @@ hipError_t conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int 
   // (BN-backward sums into an accumulator, or none)
   if (Cout == DP_C && Cin == DP_NOUT && dgrad_patch() && (!g.bn.part || g.bn.acc_r > 0)) {
     const int64_t blocks = int64_t(N) * ((Ho + DP_TA - 1) / DP_TA) * ((Wo + DP_TB - 1) / DP_TB);
+    if (g_hold && fuse_patch()) {   // held for the weight gradient that follows (dpatch_wgrad_kernel)
+      const hipError_t e = conv_dgrad_flush();
+      if (e != hipSuccess) return e;
+      g_held.g = g;
+      g_held.patch = true;
+      g_held.bm = 0;
+      g_held.gx = unsigned(blocks);
+      g_held.s = stream;
+      g_held.on = true;
+      return hipSuccess;
+    }
     dgrad_patch_kernel<<<unsigned(blocks), kThreads, 0, stream>>>(g);
     return hipGetLastError();
   }
   g.cls_per_block = conv_dgrad_classes_per_block(g.M, g.NOUT);
+  if (g_hold) {   // held for the weight gradient that follows (dgrad_wgrad_kernel)
+    const hipError_t e = conv_dgrad_flush();
+    if (e != hipSuccess) return e;
+    const int bn = conv_tile_channels(g.NOUT, false), bm = conv_tile_pixels(g.M, g.NOUT, 4);
+    if (g.cls_per_block == 1 && bn == 64 && staging() == 2 && (bm == 64 || bm == FBM)) {
+      g_held.g = g;
+      g_held.patch = false;
+      g_held.bm = bm;
+      g_held.gx = unsigned((g.M + bm - 1) / bm * (g.NOUT / bn));
+      g_held.s = stream;
+      g_held.on = true;
+      return hipSuccess;
+    }
+  }
   launch_tap_gemm<true>(g, 4, stream);
+  return hipGetLastError();
+}
+
+void conv_dgrad_hold(int on) { g_hold = on != 0; }
+
+hipError_t conv_dgrad_flush() {
+  if (!g_held.on) return hipSuccess;
+  g_held.on = false;
+  if (g_held.patch) dgrad_patch_kernel<<<g_held.gx, kThreads, 0, g_held.s>>>(g_held.g);
+  else launch_tap_gemm<true>(g_held.g, 4, g_held.s);
   return hipGetLastError();
 }
 

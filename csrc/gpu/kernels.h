@@ -500,6 +500,14 @@ int64_t conv_dgrad_bn_rows(int N, int H, int W, int Cin);
 
 hipError_t conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int N, int H, int W, int Cin, int Cout,
                       hipStream_t stream, const BnBwdFuse* bn = nullptr);
+// Hold the next tap-GEMM data gradient (on) for the weight gradient that
+// follows on its stream: conv_wgrad launches both in one kernel
+// (dgrad_wgrad_kernel) when it is the plain weight-gradient kernel's case,
+// else launches the held one first.  conv_dgrad_flush launches a held data
+// gradient alone; conv_dgrad_held reports whether one is held.
+void conv_dgrad_hold(int on);
+hipError_t conv_dgrad_flush();
+bool conv_dgrad_held();
 // bn_finalize over `nblocks` partial rows produced elsewhere (conv_fwd's epilogue)
 hipError_t bn_finalize_rows(const float* partial, int nblocks, int64_t M, int C, float eps, float momentum,
                             float* mean, float* invstd, float* running_mean, float* running_var, hipStream_t stream,

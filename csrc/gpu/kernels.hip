@@ -639,7 +639,7 @@ __device__ __forceinline__ uint32_t philox_word(uint64_t seed, uint64_t ctr, uin
 template <int TW>
 struct ReplaySharedT {
   uint32_t tab[TW];
-  int64_t idx[kMaxReplayB];
+  uint32_t idx[kMaxReplayB];   // frame indices (< 2^32: replay_sample checks the count)
   uint64_t ctr;
 };
 using ReplayShared = ReplaySharedT<kTabWords>;
@@ -675,7 +675,7 @@ __device__ __forceinline__ void replay_meta(const ReplayParams& r, const Shared&
     if (m < units) {
       const int b = int(m / per);
       const int64_t j = (m - int64_t(b) * per) * w;
-      const uint8_t* s = r.meta_src[k] + sh.idx[b] * nb + j;
+      const uint8_t* s = r.meta_src[k] + int64_t(sh.idx[b]) * nb + j;
       uint8_t* d = r.meta_dst[k] + int64_t(b) * nb + j;
       if (w == 4) *reinterpret_cast<uint32_t*>(d) = *reinterpret_cast<const uint32_t*>(s);
       else *d = *s;
@@ -693,6 +693,7 @@ __device__ __forceinline__ void replay_meta(const ReplayParams& r, const Shared&
 // lanes of a ds_read group always hit 32 distinct banks (one 1 KiB table read
 // at random bytes ran ~3.4-way conflicted)
 constexpr int kUniWords = 256 * 32;
+constexpr int kUniU = 4;   // groups in flight per lane (TBL 2)
 template <int PPT, int CIN, int OUTT, int LAYOUT, int TBL, bool NT = false>
 __global__ __launch_bounds__(kBlock) void replay_vec_kernel(DecodeParams p, ReplayParams r, int64_t meta_units) {
   __shared__ ReplaySharedT<TBL == 2 ? kUniWords : kTabWords> sh;
@@ -718,7 +719,24 @@ __global__ __launch_bounds__(kBlock) void replay_vec_kernel(DecodeParams p, Repl
   const int64_t g0 = int64_t(blockIdx.x) * kBlock + threadIdx.x;
   Group gr0;
   Pixels<PPT, CIN> px0;
-  if (g0 < groups) {
+  // TBL 2 runs a grid of few blocks (the table staging is per block): each
+  // lane keeps kUniU groups' loads in flight per pass
+  Group gru[kUniU];
+  Pixels<PPT, CIN> pxu[kUniU];
+#define BT_UNI_ISSUE(GB, FIRST)                                                                   \
+  _Pragma("unroll") for (int u = 0; u < kUniU; ++u) {                                             \
+    const int64_t g_ = (GB) + u * stride;                                                         \
+    int y_ = 0, x_ = 0;                                                                           \
+    split_group<PPT>(g_ < groups ? g_ : 0, groups_per_img, p.W, small, gru[u].b, gru[u].q, y_, x_); \
+    const int sy_ = p.flip_all ? p.H - 1 - y_ : y_;                                               \
+    const int64_t fi_ = (FIRST) ? frame_of(gru[u].b) : int64_t(sh.idx[gru[u].b]);                \
+    gru[u].src = p.src + fi_ * r.frame_bytes + (int64_t(sy_) * p.W + x_) * CIN;                   \
+    load_pixels<PPT, CIN>(gru[u].src, pxu[u]);                                                    \
+  }
+  // (a group past the end re-reads group 0 and is not emitted: no branch around the loads)
+  if constexpr (TBL == 2) {
+    BT_UNI_ISSUE(g0, true)
+  } else if (g0 < groups) {
     int y, x;
     split_group<PPT>(g0, groups_per_img, p.W, small, gr0.b, gr0.q, y, x);
     const int sy = p.flip_all ? p.H - 1 - y : y;
@@ -745,6 +763,20 @@ __global__ __launch_bounds__(kBlock) void replay_vec_kernel(DecodeParams p, Repl
     if (blockIdx.x == 0 && r.index_out) r.index_out[b] = i;
   }
   __syncthreads();
+  if constexpr (TBL == 2) {
+    for (int64_t gb = g0; gb < groups; gb += kUniU * stride) {
+      if (gb != g0) {
+        BT_UNI_ISSUE(gb, false)
+      }
+#pragma unroll
+      for (int u = 0; u < kUniU; ++u)
+        if (gb + u * stride < groups) emit<PPT, CIN, OUTT, LAYOUT, TBL, NT>(p, xf, cm, cout, HW, gru[u], pxu[u]);
+    }
+    for (int64_t g = g0; g < groups + meta_units; g += stride)
+      if (g >= groups) replay_meta(r, sh, p.B, g - groups);
+    return;
+  }
+#undef BT_UNI_ISSUE
   for (int64_t g = g0; g < groups + meta_units; g += stride) {
     if (g >= groups) {
       replay_meta(r, sh, p.B, g - groups);
@@ -758,7 +790,7 @@ __global__ __launch_bounds__(kBlock) void replay_vec_kernel(DecodeParams p, Repl
     int y, x;
     split_group<PPT>(g, groups_per_img, p.W, small, gr.b, gr.q, y, x);
     const int sy = p.flip_all ? p.H - 1 - y : y;
-    gr.src = p.src + sh.idx[gr.b] * r.frame_bytes + (int64_t(sy) * p.W + x) * CIN;
+    gr.src = p.src + int64_t(sh.idx[gr.b]) * r.frame_bytes + (int64_t(sy) * p.W + x) * CIN;
     Pixels<PPT, CIN> px;
     load_pixels<PPT, CIN>(gr.src, px);
     emit<PPT, CIN, OUTT, LAYOUT, TBL, NT>(p, xf, cm, cout, HW, gr, px);
@@ -782,7 +814,7 @@ __global__ __launch_bounds__(kBlock) void replay_scalar_kernel(DecodeParams p, R
     const int64_t q = g - int64_t(b) * HW;
     const int y = int(q / p.W), x = int(q - int64_t(y) * p.W);
     const int sy = p.flip_all ? p.H - 1 - y : y;
-    const uint8_t* s = p.src + sh.idx[b] * r.frame_bytes + (int64_t(sy) * p.W + x) * p.Cin;
+    const uint8_t* s = p.src + int64_t(sh.idx[b]) * r.frame_bytes + (int64_t(sy) * p.W + x) * p.Cin;
     for (int c = 0; c < p.Cout; ++c) {
       const float v = xf_value(xf, c, s[p.cmap[c]]);
       const int64_t off = p.layout == NCHW ? int64_t(c) * HW + q : q * p.Cout + c;
@@ -801,15 +833,21 @@ hipError_t launch_replay(const DecodeParams& p, const ReplayParams& r, int64_t m
                    (reinterpret_cast<uintptr_t>(p.src) % 16) == 0 && (reinterpret_cast<uintptr_t>(p.dst) % 16) == 0 &&
                    (int64_t(p.H) * p.W * p.Cin) % 16 == 0;
   if (vec) {
-    const int grid = grid_for(int64_t(p.B) * p.H * p.W / PPT + meta_units, p.max_grid);
+    int grid = grid_for(int64_t(p.B) * p.H * p.W / PPT + meta_units, p.max_grid);
     // fp32 NCHW table-mode output through non-temporal stores: batch 64 of
     // 640x480 58.5 us against 62.8 (profiles/r5/b6; BT_REPLAY_NT=0: plain stores)
     static const bool nt_env = !(std::getenv("BT_REPLAY_NT") && std::getenv("BT_REPLAY_NT")[0] == '0');
     const bool nt = nt_env && OUTT == OUT_F32 && p.layout == NCHW && p.xf_table_only;
-    // one table for all channels (xf_table_only 2): the 32-copy conflict-free form
-    // (BT_REPLAY_UNI=0: the 1 KiB table per channel instead)
-    static const bool uni_env = !(std::getenv("BT_REPLAY_UNI") && std::getenv("BT_REPLAY_UNI")[0] == '0');
+    // one table for all channels (xf_table_only 2): the 32-copy conflict-free
+    // form with BT_REPLAY_UNI=1 -- 0 % bank conflicts (PMC) but 83.4 us against
+    // 58.4 per batch of 64 (profiles/r5/b8): its 32 KiB table per block halves
+    // the resident waves and every one of the 8192 blocks stages it
+    static const bool uni_env = std::getenv("BT_REPLAY_UNI") && std::getenv("BT_REPLAY_UNI")[0] == '1';
     const bool uni = uni_env && p.xf_table_only == 2;
+    if (uni && p.max_grid <= 0) {   // 4 blocks per CU, the table staged once per block (BT_REPLAY_UNI_GRID)
+      static const int ug = std::getenv("BT_REPLAY_UNI_GRID") ? std::atoi(std::getenv("BT_REPLAY_UNI_GRID")) : 1024;
+      grid = std::min(grid, ug > 0 ? ug : 1024);
+    }
 #define BT_REPLAY(CIN, LAY)                                                                  \
   do {                                                                                       \
     if (uni && nt) replay_vec_kernel<PPT, CIN, OUTT, LAY, 2, true><<<grid, kBlock, 0, s>>>(p, r, meta_units); \

@@ -263,6 +263,9 @@ PYBIND11_MODULE(_hip, m) {
         });
 
   m.def("conv_wgrad_slices", &conv_wgrad_slices);
+  m.def("conv_dgrad_hold", [](int on) { conv_dgrad_hold(on); });
+  m.def("conv_dgrad_flush", []() { check(conv_dgrad_flush(), "conv_dgrad_flush"); });
+  m.def("conv_dgrad_held", []() { return conv_dgrad_held(); });
   m.def("conv_wgrad",
         [](uintptr_t x, uintptr_t dy, uintptr_t partial, int N, int H, int W, int Cin, int Ho, int Wo, int Cout,
            int slices, int64_t px_per_slice, uintptr_t out, int64_t s_co, int64_t s_ci, int64_t s_kh, int64_t s_kw,

@@ -330,11 +330,16 @@ def main(argv=None):
                     help='write real_/sim_samples_ PNG grids every N epochs (reference: 5; 0 = never)')
     ap.add_argument('--steady-skip', default=5, type=int,
                     help='iterations excluded from the steady-state rate (at least warm-up + capture + 1)')
+    ap.add_argument('--prefetch', action='store_true',
+                    help='enqueue the D step\'s real-batch half while the producers render (DensityOptStep.'
+                         'prefetch); default off: in a same-box A/B the inline iteration ran 179 / 166 it/s '
+                         'against 166 / 150 (profiles/r5/b8/dopt_ab.jsonl)')
     ap.add_argument('--no-prefetch', action='store_true',
-                    help='run the D step\'s real-batch half with the rest of the iteration, after the sim batch '
-                         'arrives (round 4\'s order; default: enqueued while the producers render)')
+                    help='the real-batch half with the rest of the iteration, after the sim batch arrives '
+                         '(the default; kept for scripts)')
     ap.add_argument('--verbose', action='store_true')
     args = ap.parse_args(argv)
+    args.no_prefetch = args.no_prefetch or not args.prefetch
     args.timestr = time.strftime('%Y%m%d_%H%M%S')
     rank = int(os.environ.get('RANK', '0'))
     runs = []

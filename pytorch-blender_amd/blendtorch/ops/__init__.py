@@ -1319,6 +1319,18 @@ def set_side_wgrad(on):
     global _SIDE_WGRAD
     prev, _SIDE_WGRAD = _SIDE_WGRAD, bool(on)
     return prev
+# a layer's data and weight gradients in one launch (dgrad_wgrad_kernel; BT_FUSE_DW=0: two launches)
+_FUSE_DW = os.environ.get('BT_FUSE_DW', '1') not in ('', '0')
+
+
+def set_fuse_dw(on):
+    """Data and weight gradients of a tap-GEMM layer in one launch (True, the
+    default) or two (False); returns the previous setting."""
+    global _FUSE_DW
+    prev, _FUSE_DW = _FUSE_DW, bool(on)
+    return prev
+
+
 # first layer on raw u8 frames: its forward writes the decoded frames for its weight gradient (BT_C4_DECODED)
 _C4_DECODED = os.environ.get('BT_C4_DECODED', '0') not in ('', '0')
 
@@ -1675,9 +1687,24 @@ def _conv_function():
                 bn_dy.gx_out = gy_dgrad = torch.empty_like(gy, memory_format=torch.channels_last)
                 gw = _Conv4x4s2._wgrad(ctx, x, gy, None, None, bn_dy)
                 bn_dy = None
+            held = False
             if ctx.needs_input_grad[0]:
                 if conv_dgrad_supported(x, w16):
-                    gx = conv_dgrad(gy_dgrad, w16, tuple(x.shape), ctx.wt, ctx.bn_link)
+                    # the data gradient held for the weight gradient below: both in one launch
+                    # (dgrad_wgrad_kernel), unless the weight gradient runs elsewhere
+                    hold = (_FUSE_DW and side is None and gy_dgrad is gy and ctx.needs_input_grad[1]
+                            and x.is_cuda)
+                    ext = hip_ext()
+                    if hold:
+                        ext.conv_dgrad_hold(1)
+                    try:
+                        gx = conv_dgrad(gy_dgrad, w16, tuple(x.shape), ctx.wt, ctx.bn_link)
+                    finally:
+                        if hold:
+                            ext.conv_dgrad_hold(0)
+                    held = hold and bool(ext.conv_dgrad_held())
+                    if held:
+                        _count('conv_dgrad_held')
                 else:
                     wfull = w16
                     if w16.shape[1] != x.shape[1]:   # RGBA-fed RGB weight: zero weight on the extra channel
@@ -1698,11 +1725,16 @@ def _conv_function():
                 bl = ctx.bn_link
                 if gx is not None and bl is not None and bl.acc is not None and bl.part is not None and bl.rows < 0 \
                         and bl.params is not None and ctx.needs_input_grad[1] and x.shape[1] != 4 \
-                        and not bl.defer_fold:
+                        and not bl.defer_fold and not held:
                     # the data gradient just filled the BN's backward accumulator: the
-                    # weight-gradient launch folds it in one extra block
+                    # weight-gradient launch folds it in one extra block (not when both
+                    # share a launch: the BN backward's apply folds it then)
                     fold = bl.fold_args(x.shape[0] * x.shape[2] * x.shape[3])
-                gw = _Conv4x4s2._wgrad(ctx, x, gy, fold, bl, bn_dy)
+                try:
+                    gw = _Conv4x4s2._wgrad(ctx, x, gy, fold, bl, bn_dy)
+                finally:
+                    if held:
+                        hip_ext().conv_dgrad_flush()   # (no-op once the weight gradient launched both)
             return gx, gw, None, None, None, None, None, None, None, None, None
 
         @staticmethod

@@ -64,6 +64,17 @@ MODEL = [
 ]
 
 
+# the same step with each tap-GEMM layer's data and weight gradient in one launch
+# (dgrad_wgrad_kernel, BT_FUSE_DW): 20 kernels
+MODEL_FUSED = MODEL[:10] + [
+    ('conv4 dgrad + wgrad (one launch)', 2 * G, 2 * (A4 + A3)),
+    ('BN3 apply bwd (folds)', 0, 3 * A3),
+    ('conv3 dgrad + wgrad (one launch)', 2 * G, 2 * (A3 + A2)),
+] + MODEL[15:]
+# ... and the 32-channel layer's patch data gradient with its weight gradient (dpatch_wgrad_kernel): 19
+MODEL_FUSED2 = MODEL_FUSED[:14] + [('conv2 dgrad (patch) + wgrad (one launch)', 2 * G, 2 * (A2 + A1))] + MODEL_FUSED[16:]
+
+
 def short(name):
     n = name.replace('(anonymous namespace)::', '').replace('btn::gpu::', '').replace('void ', '')
     return re.sub(r'\(.*$', '', n).strip()
@@ -139,8 +150,11 @@ def main():
     a = ap.parse_args()
     seq = read_sequence(a.seq)
     ctrs = per_position(seq, read_pmc(a.pmc)) if a.pmc != '-' else [{} for _ in seq]
-    if len(seq) != len(MODEL):
-        print(f'warning: {len(seq)} kernels per step, the model has {len(MODEL)}', file=sys.stderr)
+    model = MODEL_FUSED if any(base(n) == 'dgrad_wgrad_kernel' for n, _ in seq) else MODEL
+    if any(base(n) == 'dpatch_wgrad_kernel' for n, _ in seq):
+        model = MODEL_FUSED2
+    if len(seq) != len(model):
+        print(f'warning: {len(seq)} kernels per step, the model has {len(model)}', file=sys.stderr)
     rows = []
     tot = collections.defaultdict(float)
     hdr = ('| # | kernel | what | us | GFLOP | TFLOP/s | % bf16 peak | min MB | fetch MB | write MB | TB/s (meas.) '
@@ -148,7 +162,7 @@ def main():
     rows.append(hdr)
     rows.append('|' + '---|' * 15)
     for i, (nm, us) in enumerate(seq):
-        what, fl, mb = MODEL[i] if i < len(MODEL) else ('?', 0, 0)
+        what, fl, mb = model[i] if i < len(model) else ('?', 0, 0)
         c = ctrs[i] if i < len(ctrs) else {}
         # FETCH_SIZE x 2: on this gfx950 / rocprofv3 the counter reads half the
         # bytes a streaming kernel must read (BN1 apply: 18.9 -> 37.8 MB of the

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5, GPU session 8: the disc step's roofline data (trace + PMC passes:
+# Round 5, GPU session 8: fused data+weight gradient launch (A/B), the disc step's roofline data (trace + PMC passes:
 # LDS bank conflicts, VALU/MFMA, HBM bytes) on the current kernels, the replay
 # sampler's LDS counters, and the disc bench after the c4w revert.
 set -u
@@ -11,9 +11,10 @@ trap 'find gpurun_out -type f -size +4M -print -delete; du -sh gpurun_out' EXIT
 timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider \
   tests/test_conv_wgrad.py tests/test_gpu_consumer.py tests/test_replay.py -m gpu > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
-for i in 1 2; do
-  timeout -k 10 200 python bench.py --consumer disc --steps 2000 > $O/disc.log 2>&1 || { tail -5 $O/disc.log; exit 1; }
-  grep '^{' $O/disc.log | tee -a $O/disc.jsonl | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'disc':d['value'],'ms':d['ms_per_step']}))"
+for v in "fused:" "twolaunch:BT_FUSE_DW=0" "fused:" "twolaunch:BT_FUSE_DW=0"; do
+  name=${v%%:*}; e=${v#*:}
+  timeout -k 10 200 env $e python bench.py --consumer disc --steps 2000 > $O/disc.log 2>&1 || { tail -5 $O/disc.log; exit 1; }
+  grep '^{' $O/disc.log | tee -a $O/disc_$name.jsonl | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'v':'$name','disc':d['value'],'ms':d['ms_per_step']}))"
 done
 bash scripts/gpurun/disc_roofline.sh r5b8 > $O/roofline.log 2>&1 || { tail -20 $O/roofline.log; exit 1; }
 cat gpurun_out/roof_r5b8/roofline.md
@@ -37,4 +38,13 @@ for v in "uni:" "tbl:BT_REPLAY_UNI=0" "uni:" "tbl:BT_REPLAY_UNI=0"; do
     timeout -k 10 120 env $e python benchmarks/bench_replay.py --batch $b --steps 2000 > $O/replay.log 2>&1 || { tail -5 $O/replay.log; exit 1; }
     grep '^{' $O/replay.log | tee -a $O/replay_${name}_b$b.jsonl | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'v':'$name','B':$b,'us':d['us_per_batch'],'tbps':d['effective_tbps']}))"
   done
+done
+# densityopt: the real-half prefetch against the inline iteration, same box, alternating
+for v in "prefetch:" "inline:--no-prefetch" "prefetch:" "inline:--no-prefetch"; do
+  name=${v%%:*}; flags=${v#*:}
+  timeout -k 10 200 python examples/densityopt/densityopt.py --num-epochs 1000 --seed 0 --image-every 0 $flags \
+    --out-dir '' --json $O/dopt_$name.json > $O/dopt.log 2>&1 || { tail -5 $O/dopt.log; exit 1; }
+  python -c "
+import json; d=json.load(open('$O/dopt_$name.json')); s=d['steady']; m=s['ms_per_iteration']
+print(json.dumps({'v':'$name','it_s':round(s['iterations_per_s'],1),'wait_fetch_send_ms':round(m['sim_wait']+m['fetch']+m['send'],3),'ms':m,'abs_diff':[round(x,3) for x in d.get('abs_diff',[])]}))" | tee -a $O/dopt_ab.jsonl
 done

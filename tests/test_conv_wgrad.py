@@ -312,14 +312,16 @@ def test_bn_accumulators_fold_and_clear(dev, monkeypatch, side):
         a.zero_grad(set_to_none=True)
         b.zero_grad(set_to_none=True)
         before = (ops.KERNEL_CALLS.get('bn_forward_acc', 0), ops.KERNEL_CALLS.get('bn_backward_acc', 0),
-                  ops.KERNEL_CALLS.get('bn_backward_folded', 0))
+                  ops.KERNEL_CALLS.get('bn_backward_folded', 0), ops.KERNEL_CALLS.get('conv_dgrad_held', 0))
         la = a.bce_loss_bf16(x, 1.0)
         la.backward()
+        held = ops.KERNEL_CALLS.get('conv_dgrad_held', 0) - before[3]   # data gradients sharing a launch
         # 4 BN layers forward; backward: BN1..3 from the dgrad epilogues, BN4 from the head's
         assert ops.KERNEL_CALLS['bn_forward_acc'] == before[0] + 4
         assert ops.KERNEL_CALLS['bn_backward_acc'] == before[1] + 4
-        # BN1..3's sums are folded by the next conv's weight-gradient launch (in line)
-        assert ops.KERNEL_CALLS.get('bn_backward_folded', 0) == before[2] + (0 if side else 3)
+        # BN1..3's sums are folded by the next conv's weight-gradient launch (in line), unless
+        # that launch also runs the data gradient filling them (held: the apply folds them)
+        assert ops.KERNEL_CALLS.get('bn_backward_folded', 0) == before[2] + (0 if side else 3 - held)
         monkeypatch.setattr(ops, 'bn_acc_supported', lambda C: False)
         lb = b.bce_loss_bf16(x, 1.0)
         lb.backward()
@@ -750,3 +752,86 @@ def test_side_stream_weight_gradients(dev):
     for pa, pb in zip(nets[2].parameters(), nets[3].parameters()):
         d = (pa - pb).detach().abs()
         assert float(d.mean()) < 0.1 * lr and float((d > 0.5 * lr).float().mean()) < 0.02
+
+
+@pytest.mark.gpu
+def test_fused_data_and_weight_gradient_launch(dev):
+    """ops.set_fuse_dw(True): a tap-GEMM layer's data gradient is held and
+    launched with its weight gradient in one kernel (dgrad_wgrad_kernel) --
+    two such layers per disc backward -- and the step's gradients, BN
+    statistics and (captured, FusedAdam) weights match the two-launch order."""
+    from blendtorch.models import Discriminator
+    from blendtorch.parallel.step import CapturedStep
+    cl = torch.channels_last
+    cfg = ops.DecodeConfig.unit(channels='rgba', gamma=2.2, dtype='bfloat16', layout='nhwc')
+    g = torch.Generator(device=dev).manual_seed(31)
+    xs = [torch.randint(0, 256, (4, 96, 128, 4), dtype=torch.uint8, device=dev, generator=g) for _ in range(3)]
+    torch.manual_seed(6)
+    nets = [Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl) for _ in range(4)]
+    for m in nets[1:]:
+        m.load_state_dict(nets[0].state_dict())
+    prev = ops.set_fuse_dw(True)
+    try:
+        for m, fuse in zip(nets[:2], (True, False)):   # eager
+            ops.set_fuse_dw(fuse)
+            before = ops.KERNEL_CALLS.get('conv_dgrad_held', 0)
+            m.bce_loss_bf16(xs[0].permute(0, 3, 1, 2), 1.0, decode=cfg).backward()
+            # conv3, conv4 (tap GEMM) and conv2 (patch data gradient, unless BT_FUSE_PATCH=0)
+            assert ops.KERNEL_CALLS.get('conv_dgrad_held', 0) - before in ((3, 2) if fuse else (0,))
+        torch.cuda.synchronize()
+        assert not ops.hip_ext().conv_dgrad_held()
+        for (n, pa), pb in zip(nets[0].named_parameters(), nets[1].parameters()):
+            torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-4, atol=1e-6 + 1e-4 * float(pb.grad.abs().max()),
+                                       msg=n)
+        for ba, bb in zip(nets[0].buffers(), nets[1].buffers()):
+            torch.testing.assert_close(ba, bb, rtol=1e-5, atol=1e-6)
+        lr = 2e-4
+        steps = []
+        for m, fuse in zip(nets[2:], (True, False)):   # captured (the setting is read while capturing)
+            ops.set_fuse_dw(fuse)
+            st = CapturedStep(m, ops.FusedAdam(m.parameters(), lr=lr),
+                              lambda mm, x: mm.bce_loss_bf16(x.permute(0, 3, 1, 2), 1.0, decode=cfg),
+                              allreduce=False, warmup=1)
+            for x in xs:
+                st(x)
+            steps.append(st)
+        torch.cuda.synchronize()
+        assert all(st.state == 'graph' for st in steps)
+    finally:
+        ops.set_fuse_dw(prev)
+    for pa, pb in zip(nets[2].parameters(), nets[3].parameters()):
+        d = (pa - pb).detach().abs()
+        assert float(d.mean()) < 0.1 * lr and float((d > 0.5 * lr).float().mean()) < 0.02
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('cin,cout,hw', [(64, 128, (60, 80)), (128, 256, (30, 40)), (64, 128, (12, 18))])
+def test_dgrad_wgrad_kernel_matches_separate_launches(dev, cin, cout, hw):
+    """One layer, direct ops: conv_dgrad held + conv_wgrad (one launch) give
+    the bit-identical data gradient and the same weight gradient as the two
+    launches (odd shapes: partial tiles and runs of 8 padded with exiting
+    blocks)."""
+    cl = torch.channels_last
+    g = torch.Generator(device=dev).manual_seed(cin + cout + hw[0])
+    H, W = hw
+    x = torch.randn(8, cin, H, W, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    dy = torch.randn(8, cout, H // 2, W // 2, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    w = (0.05 * torch.randn(cout, cin, 4, 4, device=dev, generator=g)).to(torch.bfloat16).contiguous(memory_format=cl)
+    ext = ops.hip_ext()
+    outs = []
+    for fuse in (False, True):
+        if fuse:
+            ext.conv_dgrad_hold(1)
+        try:
+            dx = ops.conv_dgrad(dy, w, tuple(x.shape))
+        finally:
+            ext.conv_dgrad_hold(0)
+        assert bool(ext.conv_dgrad_held()) == fuse
+        gw = ops.conv_wgrad(x, dy, torch.empty(cout, cin, 4, 4, device=dev))
+        assert not ext.conv_dgrad_held()
+        torch.cuda.synchronize()
+        outs.append((dx, gw))
+    assert torch.equal(outs[0][0], outs[1][0])
+    torch.testing.assert_close(outs[1][1], outs[0][1], rtol=1e-5, atol=1e-5 * float(outs[0][1].abs().max()))
+    ref = torch.nn.grad.conv2d_weight(x.float(), (cout, cin, 4, 4), dy.float(), stride=2, padding=1)
+    torch.testing.assert_close(outs[1][1], ref, rtol=1e-3, atol=1e-3 * float(ref.abs().max()))
