@@ -35,6 +35,7 @@
 #include <cstdint>
 #include <type_traits>
 
+#include "adam_sched.h"
 #include "bn_fold.h"
 #include "kernels.h"
 
@@ -209,8 +210,35 @@ __device__ __forceinline__ void wgrad_reduce_block(const ConvWgradParams::Reduce
   }
 }
 
-__global__ __launch_bounds__(kThreads) void conv_wgrad_reduce_kernel(ConvWgradParams::Reduce r) {
+// job: an attached Adam schedule (adam_sched.h), run by the first lane
+__global__ __launch_bounds__(kThreads) void conv_wgrad_reduce_kernel(ConvWgradParams::Reduce r, AdamSchedJob job) {
+  if (job.step && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) adam_schedule_run(job);
   wgrad_reduce_block(r, int(blockIdx.x), int(blockIdx.y));
+}
+
+namespace {
+AdamSchedJob g_sched_job;     // attached, not yet launched
+bool g_sched_taken = false;   // a launch ran the attached job
+AdamSchedJob take_sched_job() {
+  AdamSchedJob j = g_sched_job;
+  if (j.step) g_sched_taken = true;
+  g_sched_job = AdamSchedJob();
+  return j;
+}
+}  // namespace
+
+void conv_attach_adam_schedule(const AdamSchedJob& j) {
+  g_sched_job = j;
+  g_sched_taken = false;
+}
+bool conv_adam_schedule_taken() {
+  const bool t = g_sched_taken;
+  g_sched_taken = false;
+  return t;
+}
+void conv_detach_adam_schedule() {
+  g_sched_job = AdamSchedJob();
+  g_sched_taken = false;
 }
 
 // blocks past the main grid: a previous layer's deferred reduce (the side
@@ -977,8 +1005,12 @@ static_assert(4 * C4W_WAVE + kLutBytes <= c4w_lds<4>(), "staging fits the combin
 
 // U8: the input is raw u8 frames read through the decode table (p.lut): a
 // compile-time switch, so neither form carries the other's stage registers
-template <int NW, bool U8>
+// LDSC: the BN-backward coefficients (7 floats x 8 channels of a lane's dY
+// chunk, 56 VGPRs) live in LDS and are read per staged stage, freeing the
+// registers that held the kernel at 2 waves per SIMD (BT_C4W_LDS_COEF)
+template <int NW, bool U8, bool LDSC = false>
 __global__ __launch_bounds__(64 * NW) void conv_wgrad_c4w_kernel(ConvWgradParams p) {
+  static_assert(NW * C4W_WAVE + kLutBytes + 32 * 8 * 4 <= c4w_lds<NW>(), "the coefficient table fits");
   __shared__ __attribute__((aligned(16))) char smem[c4w_lds<NW>()];
   if (run_side(p, smem)) return;
   constexpr bool u8in = U8;
@@ -1004,10 +1036,25 @@ __global__ __launch_bounds__(64 * NW) void conv_wgrad_c4w_kernel(ConvWgradParams
   // X: lane -> pixel xp of the step, chunks xc0 .. xc0 + 3 (taps kh0, kh0 + 1 by kw 0, 2)
   const int xp = lane & 31, kh0 = (lane >> 5) * 2;
   const bool bnd = p.bn_dy.y != nullptr;
-  BnBwdCoef bc[8];
+  BnBwdCoef bc[LDSC ? 1 : 8];
+  float* const coefl = reinterpret_cast<float*>(smem + NW * C4W_WAVE + kLutBytes);   // [32 co][8] (LDSC)
   if (bnd) {   // (LDS scratch: the staging area, free until the loop)
-    bn_dy_coefs(p.bn_dy, p.Cout, p.M, co0 + dc * 8, reinterpret_cast<double*>(smem),
-                reinterpret_cast<int*>(smem + 4096), unsigned(b), unsigned(nwg), bc);
+    if constexpr (LDSC) {
+      BnBwdCoef t8[8];
+      bn_dy_coefs(p.bn_dy, p.Cout, p.M, co0 + dc * 8, reinterpret_cast<double*>(smem),
+                  reinterpret_cast<int*>(smem + 4096), unsigned(b), unsigned(nwg), t8);
+      if (wave == 0 && lane < 4) {   // lanes 0-3 hold the 4 chunks of the block's 32 channels
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float4* q = reinterpret_cast<float4*>(coefl + (dc * 8 + i) * 8);
+          q[0] = make_float4(t8[i].is, t8[i].nm, t8[i].ww, t8[i].bb);
+          q[1] = make_float4(t8[i].P, t8[i].dbm, t8[i].pdw, 0.f);
+        }
+      }
+    } else {
+      bn_dy_coefs(p.bn_dy, p.Cout, p.M, co0 + dc * 8, reinterpret_cast<double*>(smem),
+                  reinterpret_cast<int*>(smem + 4096), unsigned(b), unsigned(nwg), bc);
+    }
     __syncthreads();
   }
   const float slope = p.bn_dy.slope;
@@ -1058,24 +1105,34 @@ __global__ __launch_bounds__(64 * NW) void conv_wgrad_c4w_kernel(ConvWgradParams
     for (int k = 0; k < NW; ++k) c.advance(p.Ho, p.Wo);   // NW x 32 pixels: this wave's next step
   };
   auto store = [&](const Stage& r) {
+    uint32_t o[2][4];
+    if (bnd) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {   // channels 2 k, 2 k + 1 of the chunk, both pixels
+        BnBwdCoef e0, e1;
+        if constexpr (LDSC) {
+          const float4* q = reinterpret_cast<const float4*>(coefl + (dc * 8 + 2 * k) * 8);
+          const float4 a0 = q[0], b0 = q[1], a1 = q[2], b1 = q[3];
+          e0.is = a0.x, e0.nm = a0.y, e0.ww = a0.z, e0.bb = a0.w, e0.P = b0.x, e0.dbm = b0.y, e0.pdw = b0.z;
+          e1.is = a1.x, e1.nm = a1.y, e1.ww = a1.z, e1.bb = a1.w, e1.P = b1.x, e1.dbm = b1.y, e1.pdw = b1.z;
+        } else {
+          e0 = bc[2 * k], e1 = bc[2 * k + 1];
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t gw = k == 0 ? r.g[h].x : k == 1 ? r.g[h].y : k == 2 ? r.g[h].z : r.g[h].w;
+          const uint32_t yw = k == 0 ? r.y[h].x : k == 1 ? r.y[h].y : k == 2 ? r.y[h].z : r.y[h].w;
+          const f32x2 pr = {e0.gx(__uint_as_float(yw << 16), __uint_as_float(gw << 16), slope),
+                            e1.gx(__uint_as_float(yw & 0xFFFF0000u), __uint_as_float(gw & 0xFFFF0000u), slope)};
+          o[h][k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2));
+        }
+      }
+    }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      uint4 d = r.g[h];
-      if (bnd) {
-        const uint32_t gw[4] = {r.g[h].x, r.g[h].y, r.g[h].z, r.g[h].w};
-        const uint32_t yw[4] = {r.y[h].x, r.y[h].y, r.y[h].z, r.y[h].w};
-        uint32_t o[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const f32x2 pr = {bc[2 * k].gx(__uint_as_float(yw[k] << 16), __uint_as_float(gw[k] << 16), slope),
-                            bc[2 * k + 1].gx(__uint_as_float(yw[k] & 0xFFFF0000u),
-                                             __uint_as_float(gw[k] & 0xFFFF0000u), slope)};
-          o[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2));
-        }
-        // (a pixel past the slice gets a nonzero gx from its zero loads; its X
-        // row is past the slice too and staged as zeros: it adds nothing)
-        d = make_uint4(o[0], o[1], o[2], o[3]);
-      }
+      // (a pixel past the slice gets a nonzero gx from its zero loads; its X
+      // row is past the slice too and staged as zeros: it adds nothing)
+      const uint4 d = bnd ? make_uint4(o[h][0], o[h][1], o[h][2], o[h][3]) : r.g[h];
       *reinterpret_cast<uint4*>(ws + c4dy_off(dp + 16 * h, dc * 16)) = d;
     }
 #pragma unroll
@@ -2536,7 +2593,7 @@ int conv_wgrad_slices(int64_t M, int Cin, int Cout, int target_blocks) {
 
 hipError_t conv_wgrad_reduce(const ConvWgradParams::Reduce& r, hipStream_t stream) {
   if (!r.partial || !r.out || r.S <= 0 || r.rx <= 0 || r.ry <= 0) return hipErrorInvalidValue;
-  conv_wgrad_reduce_kernel<<<dim3(unsigned(r.rx), unsigned(r.ry)), kThreads, 0, stream>>>(r);
+  conv_wgrad_reduce_kernel<<<dim3(unsigned(r.rx), unsigned(r.ry)), kThreads, 0, stream>>>(r, take_sched_job());
   return hipGetLastError();
 }
 
@@ -2695,9 +2752,12 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
   if (fused) {
   } else if (c4 && (c4_wave_private() || bn_folds)) {
     const bool u8 = p.lut != nullptr;
+    static const bool ldsc = std::getenv("BT_C4W_LDS_COEF") && std::getenv("BT_C4W_LDS_COEF")[0] == '1';
     if (c4w_waves() == 8 && u8) conv_wgrad_c4w_kernel<8, true><<<unsigned(grid), 512, 0, stream>>>(q);
     else if (c4w_waves() == 8) conv_wgrad_c4w_kernel<8, false><<<unsigned(grid), 512, 0, stream>>>(q);
+    else if (u8 && ldsc) conv_wgrad_c4w_kernel<4, true, true><<<unsigned(grid), kThreads, 0, stream>>>(q);
     else if (u8) conv_wgrad_c4w_kernel<4, true><<<unsigned(grid), kThreads, 0, stream>>>(q);
+    else if (ldsc) conv_wgrad_c4w_kernel<4, false, true><<<unsigned(grid), kThreads, 0, stream>>>(q);
     else conv_wgrad_c4w_kernel<4, false><<<unsigned(grid), kThreads, 0, stream>>>(q);
   }
   else if (c4) conv_wgrad_c4_kernel<<<unsigned(grid), kThreads, 0, stream>>>(q);
@@ -2721,7 +2781,7 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
     *defer = r;
     return hipGetLastError();
   }
-  conv_wgrad_reduce_kernel<<<dim3(unsigned(r.rx), unsigned(r.ry)), kThreads, 0, stream>>>(r);
+  conv_wgrad_reduce_kernel<<<dim3(unsigned(r.rx), unsigned(r.ry)), kThreads, 0, stream>>>(r, take_sched_job());
   return hipGetLastError();
 }
 

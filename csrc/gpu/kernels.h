@@ -563,7 +563,22 @@ hipError_t adam_schedule(float* step, const float* hp, float* sched, float beta1
                          const float* gate = nullptr);
 hipError_t adam_update(const AdamParams& p, hipStream_t stream);
 hipError_t adam_schedule_prime(const float* step, const float* hp, float* sched, float beta1, float beta2,
-                               hipStream_t stream);
+                               hipStream_t stream, float off = 1.f);
+
+// The Adam step schedule as a one-lane job (adam_sched.h): run by
+// adam_schedule, or attached ahead of the backward to the next weight-gradient
+// slice-reduce launch.  taken() reports -- and clears -- whether a launch ran
+// the attached job; detach drops an unused one.
+struct AdamSchedJob {
+  float* step = nullptr;        // null: no job
+  const float* hp = nullptr;    // lr, gradient scale
+  float* sched = nullptr;       // step size, 1 / sqrt(bc2), lr, gradient scale, active
+  float beta1 = 0.f, beta2 = 0.f;
+  const float* gate = nullptr;  // optional: 0 closes the step
+};
+void conv_attach_adam_schedule(const AdamSchedJob& j);
+bool conv_adam_schedule_taken();
+void conv_detach_adam_schedule();
 
 }  // namespace gpu
 }  // namespace btn

@@ -538,12 +538,23 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("gate") = 0);
 
   m.def("adam_schedule_prime",
-        [](uintptr_t step, uintptr_t hp, uintptr_t sched, float beta1, float beta2, uintptr_t stream) {
+        [](uintptr_t step, uintptr_t hp, uintptr_t sched, float beta1, float beta2, uintptr_t stream, float off) {
           check(adam_schedule_prime(ptr<const float>(step), ptr<const float>(hp), ptr<float>(sched), beta1, beta2,
-                                    stream_of(stream)),
+                                    stream_of(stream), off),
                 "adam_schedule_prime");
         },
-        py::arg("step"), py::arg("hp"), py::arg("sched"), py::arg("beta1"), py::arg("beta2"), py::arg("stream"));
+        py::arg("step"), py::arg("hp"), py::arg("sched"), py::arg("beta1"), py::arg("beta2"), py::arg("stream"),
+        py::arg("off") = 1.0f);
+  // the Adam schedule attached to the next weight-gradient slice-reduce launch (adam_sched.h)
+  m.def("adam_attach_schedule",
+        [](uintptr_t step, uintptr_t hp, uintptr_t sched, float beta1, float beta2) {
+          AdamSchedJob j;
+          j.step = ptr<float>(step), j.hp = ptr<const float>(hp), j.sched = ptr<float>(sched);
+          j.beta1 = beta1, j.beta2 = beta2;
+          conv_attach_adam_schedule(j);
+        });
+  m.def("adam_schedule_taken", []() { return conv_adam_schedule_taken(); });
+  m.def("adam_detach_schedule", []() { conv_detach_adam_schedule(); });
 
   m.def("adam_update",
         [](std::vector<uintptr_t> params, std::vector<uintptr_t> grads, std::vector<uintptr_t> exp_avg,

@@ -8,6 +8,7 @@
 
 #include <cstdlib>
 
+#include "adam_sched.h"
 #include "bn_fold.h"
 #include "kernels.h"
 
@@ -804,35 +805,23 @@ hipError_t multi_cast(const CastParams& p, hipStream_t stream) {
 namespace {
 
 // One lane: the step counter and the bias corrections, so that the update
-// kernel's blocks all read a value no block is writing.
-// the schedule of step s (bias corrections in fp64, as torch.optim.Adam)
-__device__ void adam_schedule_write(float s, const float* hp, float* sched, float beta1, float beta2) {
-  const float lr = hp[0];
-  const double bc1 = 1.0 - pow(double(beta1), double(s));
-  const double bc2 = 1.0 - pow(double(beta2), double(s));
-  sched[0] = float(double(lr) / bc1);
-  sched[1] = float(1.0 / sqrt(bc2));
-  sched[2] = lr;
-  sched[3] = hp[1];   // gradient scale (e.g. 1 / world after a summing all-reduce)
-}
+// kernel's blocks all read a value no block is writing (adam_sched.h).
 
-// the one-launch update's schedule for the coming step (step + 1), without
-// advancing the counter: after the counter, lr or gradient scale changed on the host side
-__global__ void adam_schedule_prime_kernel(const float* step, const float* hp, float* sched, float beta1, float beta2) {
-  if (threadIdx.x == 0) adam_schedule_write(step[0] + 1.f, hp, sched, beta1, beta2);
+// the schedule of step counter + off, without advancing the counter: the
+// one-launch update's coming step (off 1) after the counter, lr or gradient
+// scale changed on the host side; or this step's (off 0) when the lr changed
+// after an attached schedule already ran
+__global__ void adam_schedule_prime_kernel(const float* step, const float* hp, float* sched, float beta1, float beta2,
+                                           float off) {
+  if (threadIdx.x == 0) adam_schedule_write(step[0] + off, hp, sched, beta1, beta2);
 }
 
 __global__ void adam_schedule_kernel(float* step, const float* hp, float* sched, float beta1, float beta2,
                                      const float* gate) {
   if (threadIdx.x != 0) return;
-  // a closed gate (gate[0] == 0, computed on the device earlier in the same
-  // stream/graph) makes the whole step a no-op: counter, moments and weights
-  const bool active = !gate || gate[0] != 0.f;
-  sched[4] = active ? 1.f : 0.f;
-  if (!active) return;
-  const float s = step[0] + 1.f;
-  step[0] = s;
-  adam_schedule_write(s, hp, sched, beta1, beta2);
+  AdamSchedJob j;
+  j.step = step, j.hp = hp, j.sched = sched, j.beta1 = beta1, j.beta2 = beta2, j.gate = gate;
+  adam_schedule_run(j);
 }
 
 // One tensor's slot of the launch, gathered into LDS by the block's first
@@ -1006,9 +995,9 @@ __global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
 }  // namespace
 
 hipError_t adam_schedule_prime(const float* step, const float* hp, float* sched, float beta1, float beta2,
-                               hipStream_t stream) {
+                               hipStream_t stream, float off) {
   if (!step || !hp || !sched) return hipErrorInvalidValue;
-  adam_schedule_prime_kernel<<<1, 64, 0, stream>>>(step, hp, sched, beta1, beta2);
+  adam_schedule_prime_kernel<<<1, 64, 0, stream>>>(step, hp, sched, beta1, beta2, off);
   return hipGetLastError();
 }
 

@@ -1297,6 +1297,7 @@ class WgradChain:
 
 
 _WGRAD_BLOCKS = int(os.environ.get('BT_WGRAD_BLOCKS', '512'))
+_C4W_BLOCKS = int(os.environ.get('BT_C4W_BLOCKS', str(_WGRAD_BLOCKS)))
 # weight gradients on a side stream, concurrent with the data-gradient chain (BT_WGRAD_SIDE=1).  Off:
 # measured 13.7k img/s against 19.5k in line -- each concurrent pair of latency-bound kernels ran ~1.8x
 # its solo time (profiles/r5/b6: wgrad 44 us, dgrad 43 us side by side, 24 / 22 us alone)
@@ -1365,8 +1366,9 @@ def conv_wgrad(x, dy, out, target_blocks=None, chain=None, last=True, lut=None, 
         raise ValueError('conv_wgrad needs channels-last x and dy')
     M = N * Ho * Wo
     if target_blocks is None:
-        # 2 blocks per CU (profiles/r2/conv_bench_v2.jsonl); BT_WGRAD_BLOCKS overrides (sweeps)
-        target_blocks = _WGRAD_BLOCKS
+        # 2 blocks per CU (profiles/r2/conv_bench_v2.jsonl); BT_WGRAD_BLOCKS overrides (sweeps);
+        # the first layer's kernel: BT_C4W_BLOCKS
+        target_blocks = _C4W_BLOCKS if Cin == 4 else _WGRAD_BLOCKS
     slices = ext.conv_wgrad_slices(M, Cin, Cout, target_blocks)
     if slices <= 0:
         raise ValueError(f'conv_wgrad: unsupported channels Cin={Cin} Cout={Cout} (Cin % 32, Cout % 64)')

@@ -54,6 +54,8 @@ __all__ = ['FusedAdam']
 import os  # noqa: E402
 
 _ONE_LAUNCH_DEFAULT = os.environ.get('BT_ADAM_ONE_LAUNCH', '0') == '1'
+# the schedule handed to the backward's last slice-reduce launch by CapturedStep (BT_ADAM_ATTACH=0: its own launch)
+_ATTACH = os.environ.get('BT_ADAM_ATTACH', '1') not in ('', '0')
 
 _MAX_PER_LAUNCH = 32   # kMaxAdam (csrc/gpu/kernels.h)
 
@@ -72,6 +74,7 @@ class FusedAdam(torch.optim.Optimizer):
         self._dev = {}
         self._zero_grads = False
         self._one_launch = _ONE_LAUNCH_DEFAULT if one_launch is None else bool(one_launch)
+        self._attached = None   # (group id, lr) of a schedule handed to the backward (attach_schedule)
 
     # -- per-group device scalars ------------------------------------------
     def _group_state(self, group):
@@ -102,6 +105,39 @@ class FusedAdam(torch.optim.Optimizer):
             b1, b2 = group['betas']
             hip_ext().adam_schedule_prime(gs['step'].data_ptr(), gs['hp'].data_ptr(), gs['sched'].data_ptr(),
                                           b1, b2, _stream(gs['step'].device))
+
+    def attach_schedule(self):
+        """Hand this step's schedule (the step counter and bias corrections)
+        to the next weight-gradient slice-reduce launch of the backward about to
+        run (its first lane computes it): the update then needs no schedule
+        launch.  Call right before the backward, then :meth:`step` without a
+        gate; a backward without such a launch leaves the job to :meth:`step`.
+        Only for one GPU parameter group outside the one-launch form; returns
+        whether it attached."""
+        self._attached = None
+        if not _ATTACH or self._one_launch:
+            return False
+        groups = [g for g in self.param_groups if g['params']]
+        if len(groups) != 1 or not groups[0]['params'][0].is_cuda:
+            return False
+        group = groups[0]
+        gs = self._group_state(group)
+        if gs['lr'] != float(group['lr']):
+            if torch.cuda.is_current_stream_capturing():
+                return False
+            gs['hp'][0].fill_(float(group['lr']))
+            gs['lr'] = float(group['lr'])
+        b1, b2 = group['betas']
+        hip_ext().adam_attach_schedule(gs['step'].data_ptr(), gs['hp'].data_ptr(), gs['sched'].data_ptr(), b1, b2)
+        self._attached = (id(group), gs['lr'])
+        return True
+
+    def detach_schedule(self):
+        """Drop a schedule :meth:`attach_schedule` handed out and no launch ran
+        (e.g. the backward raised)."""
+        if self._attached is not None:
+            hip_ext().adam_detach_schedule()
+            self._attached = None
 
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
@@ -238,7 +274,20 @@ class FusedAdam(torch.optim.Optimizer):
         if gate is not None and gate.dtype != torch.float32:
             raise ValueError('FusedAdam.step: gate must be float32 on the GPU')
         one = self._one_launch and len(params) <= _MAX_PER_LAUNCH
-        if not one:
+        att, self._attached = getattr(self, '_attached', None), None
+        taken = att is not None and att[0] == id(group) and bool(ext.adam_schedule_taken())
+        if att is not None:
+            ext.adam_detach_schedule()
+        if taken:
+            # a slice-reduce launch of the backward already advanced the counter and
+            # wrote this step's schedule (attach_schedule)
+            if gate is not None:
+                raise RuntimeError('FusedAdam.step: a gate after attach_schedule (the schedule already ran ungated)')
+            _count('adam_schedule_attached')
+            if gs['lr'] != att[1]:   # lr edited after the attach: this step's schedule again, counter as is
+                ext.adam_schedule_prime(gs['step'].data_ptr(), gs['hp'].data_ptr(), gs['sched'].data_ptr(), b1, b2,
+                                        stream, 0.0)
+        elif not one:
             _count('adam_schedule')
             ext.adam_schedule(gs['step'].data_ptr(), gs['hp'].data_ptr(), gs['sched'].data_ptr(), b1, b2, stream,
                               gate.data_ptr() if gate is not None else 0)

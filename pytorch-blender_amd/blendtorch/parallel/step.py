@@ -227,6 +227,21 @@ class CapturedStep:
         if self._seed is None or self._seed.shape != loss.shape or self._seed.device != loss.device \
                 or self._seed.dtype != loss.dtype:
             self._seed = torch.ones_like(loss)
+        # ops.FusedAdam: the step's schedule rides in the backward's last weight-gradient
+        # slice-reduce launch (one launch fewer per step)
+        attach = getattr(self.opt, 'attach_schedule', None)
+        if attach is not None:
+            attach()
+        try:
+            self._backward_only(loss)
+        except BaseException:
+            if attach is not None:
+                self.opt.detach_schedule()
+            raise
+        self.opt.step()
+        return loss.detach()
+
+    def _backward_only(self, loss):
         if self.overlap and self.grads is not None and self.comm is not None:
             # each bucket's all-reduce is enqueued the moment its last gradient is
             # (the last layers' bucket ahead of the first layers' weight gradients)
@@ -246,8 +261,6 @@ class CapturedStep:
                                                    force=self.allreduce == 'always')
         else:
             loss.backward(self._seed)
-        self.opt.step()
-        return loss.detach()
 
     def _train(self, x):
         return self._backward(self._forward(x))

@@ -50,7 +50,7 @@ def main():
     for bn in (False, True):
         for u8 in (True, False):
             for nw in (4, 8):
-                for tb in (256, 512, 1024):
+                for tb in (256, 512, 768, 1024):
                     ext.conv_set_c4w_waves(nw)
                     x = x_u8 if u8 else x_bf
                     bnd = (y, mean, invstd, bw, bb, dw, db, 0.2) if bn else None

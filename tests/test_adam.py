@@ -402,3 +402,51 @@ def test_gpu_one_launch_schedule_ahead_follows_lr_changes(dev):
         runs.append([p.detach().clone() for p in params] + [opt._group_state(opt.param_groups[0])['step'].clone()])
     for x, y in zip(*runs):
         assert torch.equal(x, y)
+
+
+@pytest.mark.gpu
+def test_schedule_attached_to_backward_reduce(monkeypatch):
+    """CapturedStep hands FusedAdam's schedule to the backward's last weight-
+    gradient slice-reduce launch (FusedAdam.attach_schedule): no schedule
+    launch, and the weights and step counter are bit-identical to the
+    schedule kernel's -- eager and captured.  A model whose backward has no
+    such launch (an MLP) falls back to the schedule kernel."""
+    from blendtorch import ops
+    from blendtorch.models import Discriminator
+    from blendtorch.parallel.step import CapturedStep
+    import blendtorch.ops.adam as adam_mod
+    dev = torch.device('cuda', 0)
+    cl = torch.channels_last
+    g = torch.Generator(device=dev).manual_seed(3)
+    xs = [torch.rand(4, 3, 96, 128, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+          for _ in range(4)]
+    outs = []
+    for attach in (True, False):
+        monkeypatch.setattr(adam_mod, '_ATTACH', attach)
+        torch.manual_seed(8)
+        m = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
+        opt = ops.FusedAdam(m.parameters(), lr=2e-4)
+        st = CapturedStep(m, opt, lambda mm, x: mm.bce_loss_bf16(x, 1.0), allreduce=False, warmup=1)
+        before = (ops.KERNEL_CALLS.get('adam_schedule', 0), ops.KERNEL_CALLS.get('adam_schedule_attached', 0))
+        for x in xs:
+            st(x)
+        torch.cuda.synchronize()
+        assert st.state == 'graph'
+        sched = ops.KERNEL_CALLS.get('adam_schedule', 0) - before[0]
+        att = ops.KERNEL_CALLS.get('adam_schedule_attached', 0) - before[1]
+        assert (att > 0 and sched == 0) if attach else (att == 0 and sched > 0)
+        outs.append(([p.detach().clone() for p in m.parameters()], float(opt._group_state(opt.param_groups[0])['step'])))
+    (pa, sa), (pb, sb) = outs
+    assert sa == sb
+    for a, b in zip(pa, pb):
+        assert torch.equal(a, b)
+    monkeypatch.setattr(adam_mod, '_ATTACH', True)
+    mlp = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.ReLU(), torch.nn.Linear(32, 1)).to(dev)
+    opt = ops.FusedAdam(mlp.parameters(), lr=1e-3)
+    st = CapturedStep(mlp, opt, lambda mm, x: mm(x).pow(2).mean(), allreduce=False, warmup=1)
+    before = ops.KERNEL_CALLS.get('adam_schedule', 0)
+    for _ in range(3):
+        st(torch.randn(8, 16, device=dev))
+    torch.cuda.synchronize()
+    assert ops.KERNEL_CALLS.get('adam_schedule', 0) > before
+    assert not ops.hip_ext().adam_schedule_taken()
