@@ -227,19 +227,7 @@ AdamSchedJob take_sched_job() {
 }
 }  // namespace
 
-void conv_attach_adam_schedule(const AdamSchedJob& j) {
-  g_sched_job = j;
-  g_sched_taken = false;
-}
-bool conv_adam_schedule_taken() {
-  const bool t = g_sched_taken;
-  g_sched_taken = false;
-  return t;
-}
-void conv_detach_adam_schedule() {
-  g_sched_job = AdamSchedJob();
-  g_sched_taken = false;
-}
+// (conv_attach_adam_schedule / _taken / _detach: after this file's internal namespace)
 
 // blocks past the main grid: a previous layer's deferred reduce (the side
 // job), then -- one block -- the BN statistics fold the preceding data
@@ -2498,6 +2486,20 @@ __global__ __launch_bounds__(kThreads) void weight_t_kernel(const uint16_t* __re
 }
 
 }  // namespace
+
+void conv_attach_adam_schedule(const AdamSchedJob& j) {
+  g_sched_job = j;
+  g_sched_taken = false;
+}
+bool conv_adam_schedule_taken() {
+  const bool t = g_sched_taken;
+  g_sched_taken = false;
+  return t;
+}
+void conv_detach_adam_schedule() {
+  g_sched_job = AdamSchedJob();
+  g_sched_taken = false;
+}
 
 namespace {
 // weight-gradient staging: 0 = register ring (conv_wgrad_kernel, default), 2 /
