@@ -17,7 +17,7 @@ timeout -k 10 300 env BT_C4W_LDS_COEF=1 python scripts/c4w_bench.py --iters 200 
 timeout -k 10 300 python scripts/c4w_bench.py --iters 200 > $O/c4w_bench.jsonl 2>&1 || { tail -5 $O/c4w_bench.jsonl; exit 1; }
 grep '"bn_dy": true, "u8": true, "waves": 4' $O/c4w_bench_ldsc.jsonl | sed 's/^/ldsc /'
 grep '"bn_dy": true, "u8": true, "waves": 4' $O/c4w_bench.jsonl | sed 's/^/base /'
-for v in "attach:" "own:BT_ADAM_ATTACH=0" "ldsc768:BT_C4W_LDS_COEF=1 BT_C4W_BLOCKS=768" "ldsc512:BT_C4W_LDS_COEF=1" "attach:" "own:BT_ADAM_ATTACH=0" "ldsc768:BT_C4W_LDS_COEF=1 BT_C4W_BLOCKS=768" "ldsc512:BT_C4W_LDS_COEF=1"; do
+for v in "attach:" "own:BT_ADAM_ATTACH=0" "ldsc768:BT_C4W_LDS_COEF=1 BT_C4W_BLOCKS=768" "ldsc512:BT_C4W_LDS_COEF=1" "w8:BT_C4W_WAVES=8 BT_C4W_BLOCKS=256" "attach:" "own:BT_ADAM_ATTACH=0" "ldsc768:BT_C4W_LDS_COEF=1 BT_C4W_BLOCKS=768" "ldsc512:BT_C4W_LDS_COEF=1" "w8:BT_C4W_WAVES=8 BT_C4W_BLOCKS=256"; do
   name=${v%%:*}; e=${v#*:}
   timeout -k 10 200 env $e python bench.py --consumer disc --steps 2000 > $O/disc.log 2>&1 || { tail -5 $O/disc.log; exit 1; }
   grep '^{' $O/disc.log | tee -a $O/disc_$name.jsonl | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'v':'$name','disc':d['value'],'ms':d['ms_per_step']}))"
