@@ -189,9 +189,12 @@ __global__ __launch_bounds__(kHeadThreads) void head_fwd_kernel(HeadParams p) {
 // and partials: the per-channel sums run in the same lane / pixel order).
 constexpr int kHeadFlat = 8;   // accumulator doubles per thread: 2 C R = 2048 (bn_acc_replicas) over 256 threads
 
-template <int KMAX>
+// BNB: also the BN's backward sums, factored through dlogit (HeadParams::bn_ab)
+template <int KMAX, bool BNB = false>
 __global__ __launch_bounds__(kHeadThreads) void head_fwd_act_kernel(HeadParams p) {
   __shared__ float red[kHeadThreads / 64];
+  // (BNB) per lane group: sums of s and s * xhat over the lane's window pixels, [pl][g][9]
+  __shared__ float sa_l[BNB ? kHeadThreads * 9 : 1], sb_l[BNB ? kHeadThreads * 9 : 1];
   // per-lane-group channel sums, [pl][g][9]: 9 words per channel group (8 +
   // one of padding) so the 32 lanes of a row write 32 distinct banks (at 8 a
   // row's 8 stores each ran 8-way conflicted)
@@ -279,23 +282,34 @@ __global__ __launch_bounds__(kHeadThreads) void head_fwd_act_kernel(HeadParams p
     }
   }
   float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float sa[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, sb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int u = 0; u < KMAX; ++u) {
     if (pl + u * PL >= npx) break;
     const uint32_t uu[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float z0 = fmaf(fmaf(__uint_as_float(uu[q] << 16), is[2 * q], nm[2 * q]), aw[2 * q], ab[2 * q]);
-      const float z1 = fmaf(fmaf(__uint_as_float(uu[q] & 0xFFFF0000u), is[2 * q + 1], nm[2 * q + 1]), aw[2 * q + 1],
-                            ab[2 * q + 1]);
+      const float xh0 = fmaf(__uint_as_float(uu[q] << 16), is[2 * q], nm[2 * q]);
+      const float xh1 = fmaf(__uint_as_float(uu[q] & 0xFFFF0000u), is[2 * q + 1], nm[2 * q + 1]);
+      const float z0 = fmaf(xh0, aw[2 * q], ab[2 * q]);
+      const float z1 = fmaf(xh1, aw[2 * q + 1], ab[2 * q + 1]);
       const f32x2 pr = {z0 > 0.f ? z0 : z0 * p.act.slope, z1 > 0.f ? z1 : z1 * p.act.slope};
       const uint32_t r = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2));
       a[2 * q] += __uint_as_float(r << 16);
       a[2 * q + 1] += __uint_as_float(r & 0xFFFF0000u);
+      if constexpr (BNB) {   // the LeakyReLU's derivative s at the pixel, and s * xhat
+        const float s0 = z0 > 0.f ? 1.f : p.act.slope, s1 = z1 > 0.f ? 1.f : p.act.slope;
+        sa[2 * q] += s0, sa[2 * q + 1] += s1;
+        sb[2 * q] += s0 * xh0, sb[2 * q + 1] += s1 * xh1;
+      }
     }
   }
 #pragma unroll
   for (int q = 0; q < 8; ++q) acc_l[pl * 9 * G + g * 9 + q] = a[q];
+  if constexpr (BNB) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) sa_l[pl * 9 * G + g * 9 + q] = sa[q], sb_l[pl * 9 * G + g * 9 + q] = sb[q];
+  }
   __syncthreads();
   float part = 0.f;
   for (int c = t; c < p.C; c += kHeadThreads) {
@@ -303,10 +317,20 @@ __global__ __launch_bounds__(kHeadThreads) void head_fwd_act_kernel(HeadParams p
     for (int l = 0; l < PL; ++l) s += acc_l[l * 9 * G + (c >> 3) * 9 + (c & 7)];
     const float pooled = s * inv;
     p.pooled[(int64_t(n) * p.OH * p.OW + cell) * p.C + c] = pooled;
-    part += pooled * p.w[c * p.ws_c + i * p.ws_i + j * p.ws_j];
+    const float wc = p.w[c * p.ws_c + i * p.ws_i + j * p.ws_j];
+    part += pooled * wc;
+    if constexpr (BNB) {   // this window's share of A[n][c], B[n][c]: w[c][i][j] / |window| times the pixel sums
+      float s0 = 0.f, s1 = 0.f;
+      for (int l = 0; l < PL; ++l) s0 += sa_l[l * 9 * G + (c >> 3) * 9 + (c & 7)], s1 += sb_l[l * 9 * G + (c >> 3) * 9 + (c & 7)];
+      const float m = wc * inv;
+      __hip_atomic_fetch_add(p.bn_ab + int64_t(n) * p.C + c, s0 * m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(p.bn_ab + (int64_t(p.N) + n) * p.C + c, s1 * m, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
   if ((t & 63) == 0) red[t >> 6] = part;
+  if constexpr (BNB) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the block's adds are done before its ticket
   __syncthreads();
   // 4. partial logit (write-through), then the loss ticket and -- for the
   // shard's last block -- the release's top counter, in one round trip
@@ -335,6 +359,30 @@ __global__ __launch_bounds__(kHeadThreads) void head_fwd_act_kernel(HeadParams p
     if (t == 0) ticket[kBnTicketShards * kBnTicketStride] = 0u;
   }
   if (flags[1] && t < 64) head_loss_wave(p, true);
+  if constexpr (BNB) {
+    if (!flags[1]) return;
+    // the last block: every block's A / B adds are done (they preceded its ticket),
+    // dlogit is written by this block's first wave
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int NC = p.N * p.C;
+    const __amdgpu_buffer_rsrc_t rab = __builtin_amdgcn_make_buffer_rsrc(p.bn_ab, 0, 2 * NC * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rdl = __builtin_amdgcn_make_buffer_rsrc(p.dlogit, 0, p.N * 4, 0x00020000);
+    for (int c = t; c < p.C; c += kHeadThreads) {
+      float s0 = 0.f, s1 = 0.f;
+      for (int n = 0; n < p.N; ++n) {   // (write-through reads: sc1 buffer loads)
+        const float dl = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rdl, n * 4, 0, 16));
+        const float av = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rab, (n * p.C + c) * 4, 0, 16));
+        const float bv =
+            __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rab, (NC + n * p.C + c) * 4, 0, 16));
+        s0 += dl * av;
+        s1 += dl * bv;
+      }
+      p.bn_sums[c] = s0;
+      p.bn_sums[p.C + c] = s1;
+      for (int n = 0; n < p.N; ++n) p.bn_ab[n * p.C + c] = 0.f, p.bn_ab[NC + n * p.C + c] = 0.f;   // for the next step
+    }
+  }
 }
 
 // one wave: logits, sigmoid, mean BCE, and dlogit/g for the backward
@@ -438,14 +486,27 @@ __global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p, in
       bb[q] = p.bn_b[c0 + q];
     }
   }
+  // the BN backward applied here (its sums worked out by the forward, HeadParams::bn_sums):
+  // dz becomes the BN's input gradient gx, from the same bf16-rounded gy as the apply kernel reads
+  const bool bna = p.bn_sums != nullptr;
+  BnBwdCoef bc[8];
+  if (bna) {
+    const float invM = 1.f / float(int64_t(p.N) * p.H * p.W);
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      bc[q].init(p.bn_mean[c0 + q], p.bn_invstd[c0 + q], p.bn_w[c0 + q], p.bn_b[c0 + q], g * p.bn_sums[p.C + c0 + q],
+                 g * p.bn_sums[c0 + q], invM);
+    if (blockIdx.x == 0)
+      for (int c = t; c < p.C; c += kHeadThreads) p.bn_dw_out[c] = g * p.bn_sums[p.C + c], p.bn_db_out[c] = g * p.bn_sums[c];
+  }
   const int64_t img = int64_t(p.H) * p.W * p.C;
   const int64_t off = (int64_t(h) * p.W + w) * p.C + c0;
   for (int n0 = 0; live && n0 < p.N; n0 += kHeadImgs) {
     uint4 xv[kHeadImgs];
 #pragma unroll
     for (int u = 0; u < kHeadImgs; ++u)
-      xv[u] = bnf && n0 + u < p.N ? *reinterpret_cast<const uint4*>(p.bn_x + (n0 + u) * img + off)
-                                  : make_uint4(0, 0, 0, 0);
+      xv[u] = (bnf || bna) && n0 + u < p.N ? *reinterpret_cast<const uint4*>(p.bn_x + (n0 + u) * img + off)
+                                           : make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int u = 0; u < kHeadImgs; ++u) {
       if (n0 + u >= p.N) break;
@@ -455,6 +516,16 @@ __global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p, in
       for (int k = 0; k < 4; ++k) {
         const f32x2 pr = {d * m[2 * k], d * m[2 * k + 1]};
         packed[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2));   // RNE, v_cvt_pk_bf16_f32
+      }
+      if (bna) {   // gx = the BN+LeakyReLU backward of gy = the rounded dz (bn_fold.h: BnBwdCoef)
+        const uint32_t xw[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const f32x2 pr = {bc[2 * k].gx(__uint_as_float(xw[k] << 16), __uint_as_float(packed[k] << 16), p.bn_slope),
+                            bc[2 * k + 1].gx(__uint_as_float(xw[k] & 0xFFFF0000u),
+                                             __uint_as_float(packed[k] & 0xFFFF0000u), p.bn_slope)};
+          packed[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2));
+        }
       }
       *reinterpret_cast<uint4*>(p.dz + (n0 + u) * img + off) = make_uint4(packed[0], packed[1], packed[2], packed[3]);
       if (bnf) {   // the BN backward reads the stored (bf16) dz as its gy
@@ -505,6 +576,17 @@ bool head_fwd_fast() {
 
 void head_set_fast(int on) { g_head_fast = on < 0 ? -1 : (on ? 1 : 0); }
 
+bool head_bn_bwd_supported(int N, int H, int W, int C, int OH, int OW, int R) {
+  // the lean forward's conditions (head_forward below), which the BN-backward sums ride in
+  if (N <= 0 || C <= 0 || C % 8 || C / 8 > kHeadThreads || kHeadThreads % (C / 8) || C > kBnFoldMaxC ||
+      OH <= 0 || OW <= 0 || H < OH || W < OW || !head_fwd_fast() || int64_t(2) * C * R > kHeadThreads * kHeadFlat)
+    return false;
+  int most = 0;
+  for (int i = 0; i < OH; ++i)
+    for (int j = 0; j < OW; ++j) most = std::max(most, (wend(i, H, OH) - wstart(i, H, OH)) * (wend(j, W, OW) - wstart(j, W, OW)));
+  return most <= 16 * (kHeadThreads / (C / 8));
+}
+
 hipError_t head_forward(const HeadParams& p, hipStream_t stream) {
   if (p.N <= 0 || p.C <= 0 || p.OH <= 0 || p.OW <= 0 || p.H < p.OH || p.W < p.OW || !p.z || !p.w || !p.pooled ||
       !p.partial || !p.loss || !p.dlogit)
@@ -517,6 +599,9 @@ hipError_t head_forward(const HeadParams& p, hipStream_t stream) {
       return hipErrorInvalidValue;
   }
   const dim3 grid(unsigned(p.OH * p.OW), unsigned(p.N));
+  if (p.bn_ab && (!p.bn_sums || !p.act.on() || !p.ticket ||
+                  !head_bn_bwd_supported(p.N, p.H, p.W, p.C, p.OH, p.OW, p.act.R)))
+    return hipErrorInvalidValue;
   if (p.act.on() && p.ticket && head_fwd_fast() && int64_t(2) * p.C * p.act.R <= kHeadThreads * kHeadFlat) {
     // the round-trip-lean form: every window pixel of a lane loaded up front
     int most = 0;   // the largest pooling window
@@ -525,7 +610,8 @@ hipError_t head_forward(const HeadParams& p, hipStream_t stream) {
         most = std::max(most, (wend(i, p.H, p.OH) - wstart(i, p.H, p.OH)) * (wend(j, p.W, p.OW) - wstart(j, p.W, p.OW)));
     const int pl = kHeadThreads / (p.C / 8);
     if (most <= 16 * pl) {
-      head_fwd_act_kernel<16><<<grid, kHeadThreads, 0, stream>>>(p);
+      if (p.bn_ab) head_fwd_act_kernel<16, true><<<grid, kHeadThreads, 0, stream>>>(p);
+      else head_fwd_act_kernel<16><<<grid, kHeadThreads, 0, stream>>>(p);
       return hipGetLastError();
     }
   }
@@ -546,6 +632,9 @@ hipError_t head_backward(const HeadParams& p, hipStream_t stream) {
         !p.bn_invstd || !p.bn_w || !p.bn_b || (reinterpret_cast<uintptr_t>(p.bn_x) & 15))
       return hipErrorInvalidValue;
   }
+  if (p.bn_sums && (p.bn_acc || !p.bn_x || !p.bn_mean || !p.bn_invstd || !p.bn_w || !p.bn_b || !p.bn_dw_out ||
+                    !p.bn_db_out || (reinterpret_cast<uintptr_t>(p.bn_x) & 15)))
+    return hipErrorInvalidValue;   // (the BN backward applied here, or its sums summed here: not both)
   if (groups > kHeadThreads) return hipErrorInvalidValue;
   const int pxb = kHeadThreads / groups;
   const int nbwd = p.H * ((p.W + pxb - 1) / pxb);   // one row segment of pxb pixels per block, all images

@@ -554,8 +554,23 @@ struct HeadParams {
   // forward: z is the INPUT of the BatchNorm+LeakyReLU whose output the head
   // pools (act.on()): the pooling reads leaky(bn(z)) rounded to bf16
   BnActIn act;
+  // forward with act.on() and bn_ab (the BN's backward worked out in the head,
+  // head_fwd_act_kernel): dz = g dlogit_n M[h][w][c] factors, so the BN
+  // backward's sums are sum_n dlogit_n A[n][c] (db) and sum_n dlogit_n B[n][c]
+  // (dw), A / B = sum over the pixels of M s (s = the LeakyReLU slope at the
+  // pixel) and M s xhat.  bn_ab: [2][N][C] fp32 scratch, zero before the launch
+  // and cleared again by it; bn_sums: [2][C] the two sums (db, dw) before the
+  // backward's loss gradient g
+  float* bn_ab = nullptr;
+  float* bn_sums = nullptr;
+  // backward with bn_sums: write the BN's INPUT gradient gx (not dz) into dz,
+  // and the BN's dw / db (g times the sums) into bn_dw_out / bn_db_out
+  float* bn_dw_out = nullptr;
+  float* bn_db_out = nullptr;
 };
 hipError_t head_forward(const HeadParams& p, hipStream_t stream);
+// whether head_forward can work out the BN backward's sums (HeadParams::bn_ab) for this shape
+bool head_bn_bwd_supported(int N, int H, int W, int C, int OH, int OW, int R);
 void head_set_fast(int on);   // BN-applying forward: 1 the round-trip-lean kernel (default), 0 round 4's, -1 BT_HEAD_FWD
 hipError_t head_backward(const HeadParams& p, hipStream_t stream);
 

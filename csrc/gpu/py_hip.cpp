@@ -436,9 +436,12 @@ PYBIND11_MODULE(_hip, m) {
   m.def("head_forward",
         [](uintptr_t z, uintptr_t w, int64_t ws_c, int64_t ws_i, int64_t ws_j, int N, int H, int W, int C, int OH,
            int OW, uintptr_t target, float target_value, uintptr_t pooled, uintptr_t partial, uintptr_t loss,
-           uintptr_t dlogit, uintptr_t logit, uintptr_t stream, uintptr_t ticket, py::object act) {
+           uintptr_t dlogit, uintptr_t logit, uintptr_t stream, uintptr_t ticket, py::object act, uintptr_t bn_ab,
+           uintptr_t bn_sums) {
           HeadParams p;
           p.act = act_from(act, "head_forward");
+          p.bn_ab = ptr<float>(bn_ab);
+          p.bn_sums = ptr<float>(bn_sums);
           p.ticket = ptr<uint32_t>(ticket);
           p.z = ptr<const uint16_t>(z);
           p.w = ptr<const float>(w);
@@ -456,13 +459,18 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("z"), py::arg("w"), py::arg("ws_c"), py::arg("ws_i"), py::arg("ws_j"), py::arg("N"), py::arg("H"),
         py::arg("W"), py::arg("C"), py::arg("OH"), py::arg("OW"), py::arg("target"), py::arg("target_value"),
         py::arg("pooled"), py::arg("partial"), py::arg("loss"), py::arg("dlogit"), py::arg("logit"),
-        py::arg("stream"), py::arg("ticket") = 0, py::arg("act") = py::none());
+        py::arg("stream"), py::arg("ticket") = 0, py::arg("act") = py::none(), py::arg("bn_ab") = 0,
+        py::arg("bn_sums") = 0);
+  m.def("head_bn_bwd_supported", &head_bn_bwd_supported);
   m.def("head_backward",
         [](uintptr_t w, int64_t ws_c, int64_t ws_i, int64_t ws_j, int N, int H, int W, int C, int OH, int OW,
            uintptr_t pooled, uintptr_t dlogit, uintptr_t gscale, uintptr_t dz, uintptr_t dw, uintptr_t stream,
            uintptr_t bn_x, uintptr_t bn_mean, uintptr_t bn_invstd, uintptr_t bn_w, uintptr_t bn_b, float bn_slope,
-           uintptr_t bn_acc, int bn_acc_r) {
+           uintptr_t bn_acc, int bn_acc_r, uintptr_t bn_sums, uintptr_t bn_dw_out, uintptr_t bn_db_out) {
           HeadParams p;
+          p.bn_sums = ptr<float>(bn_sums);
+          p.bn_dw_out = ptr<float>(bn_dw_out);
+          p.bn_db_out = ptr<float>(bn_db_out);
           p.bn_x = ptr<const uint16_t>(bn_x);
           p.bn_mean = ptr<const float>(bn_mean);
           p.bn_invstd = ptr<const float>(bn_invstd);
@@ -485,7 +493,8 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("C"), py::arg("OH"), py::arg("OW"), py::arg("pooled"), py::arg("dlogit"), py::arg("gscale"),
         py::arg("dz"), py::arg("dw"), py::arg("stream"), py::arg("bn_x") = 0, py::arg("bn_mean") = 0,
         py::arg("bn_invstd") = 0, py::arg("bn_w") = 0, py::arg("bn_b") = 0, py::arg("bn_slope") = 0.f,
-        py::arg("bn_acc") = 0, py::arg("bn_acc_r") = 0);
+        py::arg("bn_acc") = 0, py::arg("bn_acc_r") = 0, py::arg("bn_sums") = 0, py::arg("bn_dw_out") = 0,
+        py::arg("bn_db_out") = 0);
 
   // direct RCCL on the caller's stream (comm.h); the GIL is released while
   // RCCL enqueues (a group end may block until peers have posted theirs)

@@ -847,7 +847,7 @@ class BnLink:
     ``part``; the BN backward then only finalizes and applies (one pass over
     the activation fewer).  ``part`` is consumed once."""
     __slots__ = ('x', 'mean', 'invstd', 'w', 'b', 'slope', 'part', 'rows', 'gy', 'acc', 'params', 'dw', 'db',
-                 'dw_sunk', 'db_sunk', 'folded', 'defer_fold')
+                 'dw_sunk', 'db_sunk', 'folded', 'defer_fold', 'applied')
 
     def __init__(self):
         self.x = self.mean = self.invstd = self.w = self.b = self.part = self.gy = None
@@ -861,6 +861,9 @@ class BnLink:
         # the BN hands its backward to the convolution that produced its input
         # (BnDeferred, BnBwdFold): that one folds the accumulator, not the consumer
         self.defer_fold = False
+        # the consumer (the fused head) applied this BN's backward itself: its
+        # gradient IS the BN's input gradient, dw / db are in dw / db
+        self.applied = False
 
     def fold_args(self, M):
         """``(acc, R, C, M, dw, db)`` for ``conv_wgrad(fold=)``: fold this BN's
@@ -1026,6 +1029,7 @@ def _bn_function():
                 link.params = (weight, bias)
                 link.dw = link.db = None
                 link.folded = False
+                link.applied = False
                 link.defer_fold = ctx.defer is not None and ctx.acc is not None
             return y.permute(0, 3, 1, 2)   # (lazy: a view of the input, the pre-BN values)
 
@@ -1039,6 +1043,17 @@ def _bn_function():
             gys = _as_nhwc(gy if gy.dtype == xs.dtype else gy.to(xs.dtype))
             gx = torch.empty_like(xs)
             lk = ctx.link
+            if lk is not None and lk.applied:
+                # the fused head applied this backward (disc_head_bce with the BN's sums
+                # worked out in its forward): gy is the input gradient already
+                lk.applied = False
+                out_w = None if lk.dw_sunk else lk.dw
+                out_b = None if lk.db_sunk else lk.db
+                lk.dw = lk.db = None
+                lk.part = lk.gy = None
+                _count('bn_backward_by_head')
+                return (gys.permute(0, 3, 1, 2), out_w, out_b, None, None, None, None, None, None, None, None, None,
+                        None)
             folded = lk is not None and lk.folded
             part, rows = lk.take(gys) if lk is not None else (None, 0)
             if folded and part is not None and rows < 0:
@@ -1837,10 +1852,22 @@ def _head_function():
             else:
                 tval = float(target)
             _count('head_forward')
+            # the BN's backward sums worked out here, factored through dlogit (head_fwd_act_kernel):
+            # the backward then applies that BN's backward itself (no apply launch)
+            bn_ab = bn_sums = None
+            if (act is not None and _HEAD_BN_BWD and bn_link is not None and bn_link.acc is not None
+                    and bn_link.params is not None and act.args is not None
+                    and ext.head_bn_bwd_supported(N, H, W, C, oh, ow, int(act.args[1]))):
+                bn_ab = _head_bn_scratch(dev, N, C)
+                bn_sums = torch.empty(2 * C, dtype=torch.float32, device=dev)
+                _count('head_bn_sums')
             ext.head_forward(z.data_ptr(), w.data_ptr(), w.stride(1), w.stride(2), w.stride(3), N, H, W, C, oh, ow,
                              tptr, tval, pooled.data_ptr(), partial.data_ptr(), loss.data_ptr(), dlogit.data_ptr(),
                              logit.data_ptr(), _stream(dev), _head_ticket(dev).data_ptr(),
-                             act.take() if act is not None else None)
+                             act.take() if act is not None else None,
+                             bn_ab.data_ptr() if bn_ab is not None else 0,
+                             bn_sums.data_ptr() if bn_sums is not None else 0)
+            ctx.bn_sums = bn_sums
             ctx.save_for_backward(w, pooled, dlogit)
             ctx.wparam = w
             ctx.bn_link = bn_link
@@ -1863,7 +1890,25 @@ def _head_function():
                 dw, sunk = torch.empty_like(w), False
             _count('head_backward')
             bn = ctx.bn_link
-            if bn is not None and bn.acc is not None and bn.ready(dz) and (C // 8) <= 256 and 256 % (C // 8) == 0:
+            if ctx.bn_sums is not None and bn is not None and bn.ready(dz) and bn.params is not None:
+                # the BN's backward applied here: dz receives its INPUT gradient gx, the
+                # BN backward passes it on (BnLink.applied)
+                _count('head_backward_bn_apply')
+                bdw, w_sunk = _grad_dest(bn.params[0], bn.w)
+                bdb, b_sunk = _grad_dest(bn.params[1], bn.b)
+                if bdw.dtype != torch.float32 or not bdw.is_contiguous():
+                    bdw, w_sunk = torch.empty_like(bn.w), False
+                if bdb.dtype != torch.float32 or not bdb.is_contiguous():
+                    bdb, b_sunk = torch.empty_like(bn.b), False
+                ext.head_backward(w.data_ptr(), w.stride(1), w.stride(2), w.stride(3), N, H, W, C, oh, ow,
+                                  pooled.data_ptr(), dlogit.data_ptr(), g.data_ptr(), dz.data_ptr(), dw.data_ptr(),
+                                  _stream(w.device), bn.x.data_ptr(), bn.mean.data_ptr(), bn.invstd.data_ptr(),
+                                  bn.w.data_ptr(), bn.b.data_ptr(), bn.slope, 0, 0, ctx.bn_sums.data_ptr(),
+                                  bdw.data_ptr(), bdb.data_ptr())
+                bn.dw, bn.db, bn.dw_sunk, bn.db_sunk, bn.applied = bdw, bdb, w_sunk, b_sunk, True
+                bn.part = bn.gy = None
+                _grad_done(bn.params[0] if w_sunk else None, bn.params[1] if b_sunk else None)
+            elif bn is not None and bn.acc is not None and bn.ready(dz) and (C // 8) <= 256 and 256 % (C // 8) == 0:
                 # dz is the gy of the BN+LeakyReLU that produced z: sum its backward
                 # statistics here, into the BN call's accumulator
                 _count('head_backward_bn')
@@ -1884,9 +1929,24 @@ def _head_function():
 
 
 _HEAD_FN = None
+# the fused head works out the BN's backward sums in its forward and applies that backward in
+# its own (BT_HEAD_BN_BWD=0: the head sums into the BN's accumulator and the BN applies)
+_HEAD_BN_BWD = os.environ.get('BT_HEAD_BN_BWD', '1') not in ('', '0')
 
 
 _HEAD_TICKETS = {}
+_HEAD_BN_SCRATCH = {}
+
+
+def _head_bn_scratch(dev, N, C):
+    """The zeroed [2][N][C] fp32 A / B scratch of the head forward's BN sums
+    (cleared again by the kernel's last block)."""
+    import torch
+    key = (dev, int(N), int(C))
+    t = _HEAD_BN_SCRATCH.get(key)
+    if t is None:
+        t = _HEAD_BN_SCRATCH[key] = torch.zeros(2 * N * C, dtype=torch.float32, device=dev)
+    return t
 
 
 def _head_ticket(dev):

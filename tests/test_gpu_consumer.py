@@ -572,3 +572,39 @@ def test_captured_step_never_replays_for_another_layout(dev):
             calls = ops.KERNEL_CALLS.get('conv_fwd', 0)
             assert bool(torch.isfinite(loss))
         assert torch.equal(buf, keep)                       # the caller's tensor was never written
+
+
+@pytest.mark.parametrize('N,H,W', [(4, 240, 320), (3, 96, 128)])
+def test_head_applies_bn_backward(dev, monkeypatch, N, H, W):
+    """The fused head works out the last BN's backward sums in its forward
+    (factored through dlogit) and applies that BN's backward itself, so the
+    BN's input gradient leaves the head backward and no BN apply launch runs
+    (BT_HEAD_BN_BWD): the same loss, and gradients equal to the accumulator
+    path's within the rounding of their differently ordered sums."""
+    from blendtorch.models import Discriminator
+    cl = torch.channels_last
+    g = torch.Generator(device=dev).manual_seed(12)
+    x = torch.rand(N, 3, H, W, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    runs = []
+    for on in (True, False):
+        monkeypatch.setattr(ops, '_HEAD_BN_BWD', on)
+        torch.manual_seed(4)
+        m = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
+        m.lazy_head_bn = True
+        before = (ops.KERNEL_CALLS.get('bn_backward_by_head', 0), ops.KERNEL_CALLS.get('bn_backward_acc', 0))
+        for _ in range(2):   # (the second step reuses the zeroed scratch and accumulators)
+            m.zero_grad(set_to_none=True)
+            loss = m.bce_loss_bf16(x, 1.0)
+            loss.backward()
+        torch.cuda.synchronize()
+        by_head = ops.KERNEL_CALLS.get('bn_backward_by_head', 0) - before[0]
+        assert by_head == (2 if on else 0)
+        runs.append((loss.detach().clone(), [p.grad.clone() for p in m.parameters()],
+                     [b.clone() for b in m.buffers()]))
+    (la, ga, ba), (lb, gb, bb) = runs
+    torch.testing.assert_close(la, lb, rtol=1e-5, atol=1e-6)
+    for x_, y_ in zip(ba, bb):
+        torch.testing.assert_close(x_, y_, rtol=1e-5, atol=1e-6)
+    for (n, _), x_, y_ in zip(Discriminator(nc=3, ndf=32, adaptive=True).named_parameters(), ga, gb):
+        torch.testing.assert_close(x_, y_, rtol=2e-2, atol=2e-2 * float(y_.abs().max()), msg=n)
+    assert int(torch.count_nonzero(ops._head_bn_scratch(dev, N, 256))) == 0   # cleared by the kernel
