@@ -1856,7 +1856,7 @@ def _head_function():
             # the backward then applies that BN's backward itself (no apply launch)
             bn_ab = bn_sums = None
             if (act is not None and _HEAD_BN_BWD and bn_link is not None and bn_link.acc is not None
-                    and bn_link.params is not None and act.args is not None
+                    and bn_link.params is not None and not bn_link.defer_fold and act.args is not None
                     and ext.head_bn_bwd_supported(N, H, W, C, oh, ow, int(act.args[1]))):
                 bn_ab = _head_bn_scratch(dev, N, C)
                 bn_sums = torch.empty(2 * C, dtype=torch.float32, device=dev)
