@@ -111,7 +111,19 @@ struct BnBwdCoef {
 // finalized outputs (mean / invstd and running statistics, or dw / db).
 //
 // Sums of column j of [R][J] (J = 2C) over the replicas into part[j] (every
-// thread of the block; part: >= max(nt, J) doubles of LDS).
+// thread of the block; part: >= max(nt, J) doubles of LDS).  COH: the replicas
+// were added into by other blocks of THIS launch (read behind a grid barrier):
+// loads at agent scope, past this XCD's caches.
+template <bool COH = false>
+__device__ inline double bn_acc_load(const double* p) {
+  if constexpr (COH) {
+    return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
+                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  } else {
+    return *p;
+  }
+}
+template <bool COH = false>
 __device__ inline void bn_acc_column_sums(const double* acc, int R, int J, double* part) {
   const int t = int(threadIdx.x), nt = int(blockDim.x);
   const int G = J >= nt ? 1 : nt / J;
@@ -121,12 +133,12 @@ __device__ inline void bn_acc_column_sums(const double* acc, int R, int J, doubl
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int r = g + G * i;
-      v[i] = acc[int64_t(r < R ? r : 0) * J + j];
+      v[i] = bn_acc_load<COH>(acc + int64_t(r < R ? r : 0) * J + j);
     }
     double s = 0.0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) s += g + G * i < R ? v[i] : 0.0;
-    for (int r = g + 8 * G; r < R; r += G) s += acc[int64_t(r) * J + j];
+    for (int r = g + 8 * G; r < R; r += G) s += bn_acc_load<COH>(acc + int64_t(r) * J + j);
     part[g * J + j] = s;
   }
   __syncthreads();
@@ -149,6 +161,11 @@ constexpr int kBnTicketShards = 8;
 constexpr int kBnTicketStride = 32;   // words: one 128-byte line per counter (atomics contend per line)
 __device__ inline unsigned* bn_acc_ticket(double* acc, int R, int C) {
   return reinterpret_cast<unsigned*>(acc + int64_t(R) * 2 * C);
+}
+// The word after the top counter (spare in bn_acc_elems): a grid barrier of
+// the producing launch (conv.hip grid_barrier), zero between uses.
+__device__ inline unsigned* bn_acc_barrier(double* acc, int R, int C) {
+  return bn_acc_ticket(acc, R, C) + kBnTicketShards * kBnTicketStride + 1;
 }
 
 // After every reader of this block has its values (call after the block's

@@ -1241,6 +1241,34 @@ __device__ __forceinline__ int c1_row_chan(int f, int rho) {
 // shared 4 and the reads ran 4-way conflicted (PMC: 60-124 % conflict cycles)
 __device__ __forceinline__ int bkey(int r) { return ((r >> 1) & 1) | (((r >> 3) & 3) << 1); }
 
+// Blocks of one launch wait here for each other (all of them resident: the
+// caller's duty).  bar: a zero word; the last arriver resets it, the others
+// spin on it with s_sleep.  A spin that outlasts ~1 s gives up and counts
+// itself in g_grid_barrier_timeouts (conv_grid_barrier_timeouts): a wrong
+// result instead of a hung GPU.
+__device__ unsigned g_grid_barrier_timeouts = 0;
+constexpr unsigned kBarrierSpins = 1u << 22;
+__device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned nblk) {
+  __threadfence();   // this thread's atomics and stores performed at agent scope
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == nblk - 1) {
+      __hip_atomic_store(bar, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      unsigned n = 0;
+      while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+        __builtin_amdgcn_s_sleep(4);
+        if (++n == kBarrierSpins) {
+          atomicAdd(&g_grid_barrier_timeouts, 1u);
+          break;
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
 struct TapGemm {
   const uint16_t* src = nullptr;
   const uint16_t* w = nullptr;     // [NOUT][16][C]
@@ -1258,6 +1286,10 @@ struct TapGemm {
   // staged; act_out (nullable) receives the activation itself (every input element once)
   BnActIn act;
   uint16_t* act_out = nullptr;
+  // forward (tap_gemm_body OBN): the BatchNorm+LeakyReLU that consumes dst, applied by this
+  // launch after a grid barrier on its statistics (acc = stats); oy receives leaky(bn(dst))
+  BnActIn oact;
+  uint16_t* oy = nullptr;
 };
 
 // BN = output channels per block (128 or 64, or 32 for 32-channel outputs
@@ -1291,9 +1323,15 @@ constexpr int tap_gemm_lds() {
 // bx, by, nwg: the block's place in the GEMM's own grid (blockIdx.x / .y and
 // gridDim.x, or its place in a launch shared with a weight gradient:
 // dgrad_wgrad_kernel); smem: tap_gemm_lds() bytes
-template <bool DGRAD, int BN, bool C4 = false, int BM = FBM, int NST = 0, int CLS = 1, int ACT = 0>
+// OBN (forward, accumulator statistics, every block of the launch resident):
+// the output's BatchNorm+LeakyReLU applied here too -- the block adds its
+// sums, waits at a grid barrier, folds the accumulator (bn_apply_kernel's
+// fold: the same mean / invstd) and writes leaky(bn(z)) of its accumulators
+// to p.oy next to z (Conv1Bn has the first layer's form of the same).
+template <bool DGRAD, int BN, bool C4 = false, int BM = FBM, int NST = 0, int CLS = 1, int ACT = 0, bool OBN = false>
 __device__ __forceinline__ void tap_gemm_body(const TapGemm& p, char* smem, int bx, int by, int nwg) {
   static_assert(ACT == 0 || (!DGRAD && !C4 && NST >= 2), "the BN apply rides on the forward's LDS-DMA staging");
+  static_assert(!OBN || (!DGRAD && !C4 && ACT == 0), "the output BN: plain forward only");
   constexpr int RJ = BM / 32;                  // staged A rows per thread (ar + 32 j)
   constexpr int A_TILE = BM * F_ROW;
   constexpr int WGM = BN >= 64 ? 2 : 4, WGN = 4 / WGM;
@@ -1844,6 +1882,71 @@ __device__ __forceinline__ void tap_gemm_body(const TapGemm& p, char* smem, int 
       }
       __syncthreads();
     }
+    if constexpr (OBN) {
+      // the block's sums (as at the end of the body otherwise), the barrier, the fold
+      double* acc64 = reinterpret_cast<double*>(p.stats);
+      if (t < 2 * BN) {
+        const int which = t / BN, c = t - which * BN;
+        float v = 0.f;
+#pragma unroll
+        for (int g2 = 0; g2 < WGM; ++g2) v += red[(g2 * 2 + which) * BN + c];
+        unsafeAtomicAdd(acc64 + ((mt % p.acc_r) * 2 + which) * p.NOUT + n0 + c, double(v));
+      }
+      grid_barrier(bn_acc_barrier(acc64, p.acc_r, p.NOUT), unsigned(nwg));
+      // (the staging LDS is free: the sums, then every channel's mean / invstd)
+      double* part = reinterpret_cast<double*>(smem);
+      float* coef = reinterpret_cast<float*>(smem + 8 * (2 * kBnFoldMaxC > kThreads ? 2 * kBnFoldMaxC : kThreads));
+      static_assert(NBUF * STG >= 8 * 2 * kBnFoldMaxC + 4 * 2 * kBnFoldMaxC, "fold scratch");
+      __shared__ int oflag;
+      bn_acc_column_sums<true>(acc64, p.acc_r, 2 * p.NOUT, part);
+      for (int c = t; c < p.NOUT; c += kThreads) {
+        BnFwdFinal fin;
+        fin.eps = p.oact.eps, fin.momentum = p.oact.momentum;
+        fin.mean = p.oact.mean, fin.invstd = p.oact.invstd;
+        fin.rm = p.oact.rm, fin.rv = p.oact.rv, fin.tracked = p.oact.tracked;
+        float mu, is1;
+        bn_fwd_finalize(fin, part, p.NOUT, p.oact.M, c, bx == 0 && by == 0, mu, is1);
+        coef[c] = mu;
+        coef[p.NOUT + c] = is1;
+      }
+      __syncthreads();
+      bn_acc_release(acc64, p.acc_r, p.NOUT, &oflag, unsigned(bx), unsigned(nwg));
+      float ois[NQ][8], onm[NQ][8], oww[NQ][8], obb[NQ][8];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int c = n0 + col0 + 32 * q + 8 * g + e;
+          ois[q][e] = coef[p.NOUT + c];
+          onm[q][e] = -coef[c] * ois[q][e];
+          oww[q][e] = p.oact.w[c];
+          obb[q][e] = p.oact.b[c];
+        }
+      const float slope = p.oact.slope;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          if (!pv[i]) continue;
+          uint32_t o[4];
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {   // the same bf16 z as stored above, then bn_apply_kernel's arithmetic
+            const f32x4& a = acc[i][2 * q + (h >> 1)];
+            const f32x2 pr = {a[2 * (h & 1)], a[2 * (h & 1) + 1]};
+            const uint32_t zz = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2));
+            f32x2 r;
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+              const int e = 2 * h + s2;
+              const float x = s2 ? __uint_as_float(zz & 0xFFFF0000u) : __uint_as_float(zz << 16);
+              const float z = fmaf(fmaf(x, ois[q][e], onm[q][e]), oww[q][e], obb[q][e]);
+              r[s2] = z > 0.f ? z : z * slope;
+            }
+            o[h] = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, bf16x2));
+          }
+          *reinterpret_cast<uint4*>(p.oy + ob[i] + 32 * q) = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+    }
   } else {
   // Epilogue stores (geometry above)
   int eob[NJ];
@@ -2044,7 +2147,7 @@ __device__ __forceinline__ void tap_gemm_body(const TapGemm& p, char* smem, int 
       }
     }
   }
-  if (!DGRAD && p.stats && t < 2 * BN) {
+  if (!OBN && !DGRAD && p.stats && t < 2 * BN) {
     const int which = t / BN, c = t - which * BN;   // 0: sum, 1: sum of squares
     float v = 0.f;
 #pragma unroll
@@ -2057,10 +2160,10 @@ __device__ __forceinline__ void tap_gemm_body(const TapGemm& p, char* smem, int 
   }
 }
 
-template <bool DGRAD, int BN, bool C4 = false, int BM = FBM, int NST = 0, int CLS = 1, int ACT = 0>
+template <bool DGRAD, int BN, bool C4 = false, int BM = FBM, int NST = 0, int CLS = 1, int ACT = 0, bool OBN = false>
 __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   __shared__ __attribute__((aligned(16))) char smem[tap_gemm_lds<DGRAD, BN, C4, BM, NST>()];
-  tap_gemm_body<DGRAD, BN, C4, BM, NST, CLS, ACT>(p, smem, int(blockIdx.x), int(blockIdx.y), int(gridDim.x));
+  tap_gemm_body<DGRAD, BN, C4, BM, NST, CLS, ACT, OBN>(p, smem, int(blockIdx.x), int(blockIdx.y), int(gridDim.x));
 }
 
 // ---------------------------------------------------------------------------
@@ -2087,9 +2190,22 @@ __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
 // stay in registers until the block's last tile.
 constexpr int kC1Cols = 64;   // output columns per tile
 
+// KEEP > 0: the BatchNorm+LeakyReLU that consumes this layer's output is
+// applied here too.  Every block keeps its KEEP tiles' bf16 outputs in
+// registers, adds its BN sums into the accumulator, and waits at a grid
+// barrier (every block resident: the host launches at most the occupancy
+// limit); then each block folds the accumulator (as bn_apply_kernel does: the
+// same mean / invstd, bit for bit), applies leaky(bn(z)) to its kept tiles and
+// writes them to y.  z still goes out as before (the BN's saved input).  One
+// launch and one read of z fewer than conv1 + the BN apply kernel.
+struct Conv1Bn {
+  BnActIn act;              // acc = p.stats (fp64 [R][2][BN]); mean / invstd / running statistics written by block 0
+  uint16_t* y = nullptr;    // leaky(bn(z)), [N][OH][OW][BN] bf16
+};
+constexpr int kConv1Keep = 10;   // tiles per block of the BN-applying launch (80 VGPRs of kept outputs)
 
-template <int BN, int TR, bool U8>
-__global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tiles_per_block) {
+template <int BN, int TR, bool U8, int KEEP = 0>
+__global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tiles_per_block, Conv1Bn ob) {
   constexpr int PR = 2 * TR + 2, PC = 2 * kC1Cols + 2, PX = PR * PC;
   constexpr int NL = (PX + kThreads - 1) / kThreads;   // patch pixels per thread
   constexpr int FC = BN / 16, CP = BN / 32;            // channel fragments, 32-channel groups
@@ -2101,6 +2217,7 @@ __global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tile
   const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
   const int tiles_r = (p.OH + TR - 1) / TR, tiles_c = (p.OW + kC1Cols - 1) / kC1Cols;
   const int ntiles = p.N * tiles_r * tiles_c;
+  if constexpr (KEEP > 0) tiles_per_block = KEEP;
   const int tile0 = int(blockIdx.x) * tiles_per_block;
   const int tile1 = tile0 + tiles_per_block < ntiles ? tile0 + tiles_per_block : ntiles;
   constexpr bool u8in = U8;   // raw u8 frames through the table (a template parameter: a runtime branch
@@ -2184,8 +2301,9 @@ __global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tile
 #pragma unroll
     for (int e = 0; e < 8; ++e) sum[q][e] = sq[q][e] = 0.f;
 
-  if (tile0 < tile1) load_patch(tile0);
-  for (int tile = tile0; tile < tile1; ++tile) {
+  // KEEP: the tiles' bf16 outputs, kept for the BN apply after the grid barrier
+  uint32_t keep[KEEP > 0 ? KEEP : 1][PF][CP][4];
+  auto tile_body = [&](int tile, int k) __attribute__((always_inline)) {
     __syncthreads();                 // the previous tile's fragment reads are done (and, first, the table)
     store_patch();                   // decode (the table lookups wait for this tile's loads)
     if (tile + 1 < tile1) load_patch(tile + 1);   // in flight while this tile computes and stores
@@ -2225,10 +2343,19 @@ __global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tile
           const float lo = __uint_as_float(pk[h] << 16), hi = __uint_as_float(pk[h] & 0xFFFF0000u);
           sum[q][2 * h] += lo, sq[q][2 * h] += lo * lo;
           sum[q][2 * h + 1] += hi, sq[q][2 * h + 1] += hi * hi;
+          if constexpr (KEEP > 0) keep[k][j][q][h] = pk[h];
         }
         *reinterpret_cast<uint4*>(out + 32 * q) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
       }
     }
+  };
+  if (tile0 < tile1) load_patch(tile0);
+  if constexpr (KEEP > 0) {
+#pragma unroll
+    for (int k = 0; k < KEEP; ++k)
+      if (tile0 + k < tile1) tile_body(tile0 + k, k);
+  } else {
+    for (int tile = tile0; tile < tile1; ++tile) tile_body(tile, 0);
   }
   if (!p.stats) return;
   // the block's BatchNorm sums: the 16 lanes of a group hold the same 8 channels
@@ -2259,6 +2386,73 @@ __global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tile
     for (int w = 0; w < 4; ++w) v += red[(w * 2 + which) * BN + c];
     unsafeAtomicAdd(reinterpret_cast<double*>(p.stats) + ((int(blockIdx.x) % p.acc_r) * 2 + which) * p.NOUT + c,
                     double(v));
+  }
+  if constexpr (KEEP > 0) {
+    double* acc = reinterpret_cast<double*>(p.stats);
+    grid_barrier(bn_acc_barrier(acc, p.acc_r, BN), gridDim.x);
+    // the fold, as bn_apply_kernel's (the patch area is free now: >= 2 KiB of sums, then the coefficients)
+    double* part = reinterpret_cast<double*>(smem);
+    float* coef = reinterpret_cast<float*>(smem + 2048);
+    static_assert(PX * 8 >= 2048 + 2 * BN * 4 && 2 * BN <= kThreads, "fold scratch");
+    __shared__ int flag;
+    bn_acc_column_sums<true>(acc, p.acc_r, 2 * BN, part);
+    if (t < BN) {
+      BnFwdFinal fin;
+      fin.eps = ob.act.eps, fin.momentum = ob.act.momentum;
+      fin.mean = ob.act.mean, fin.invstd = ob.act.invstd;
+      fin.rm = ob.act.rm, fin.rv = ob.act.rv, fin.tracked = ob.act.tracked;
+      float mu, is;
+      bn_fwd_finalize(fin, part, BN, ob.act.M, t, blockIdx.x == 0, mu, is);
+      coef[t] = mu;
+      coef[BN + t] = is;
+    }
+    __syncthreads();
+    bn_acc_release(acc, p.acc_r, BN, &flag, blockIdx.x, gridDim.x);
+    // this lane's channels 32 q + 8 g + e: xhat = v is + nm, z = xhat ww + bb (bn_apply_kernel's order)
+    float is[CP][8], nm[CP][8], ww[CP][8], bb[CP][8];
+#pragma unroll
+    for (int q = 0; q < CP; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = 32 * q + 8 * g + e;
+        is[q][e] = coef[BN + c];
+        nm[q][e] = -coef[c] * is[q][e];
+        ww[q][e] = ob.act.w[c];
+        bb[q][e] = ob.act.b[c];
+      }
+    const float slope = ob.act.slope;
+#pragma unroll
+    for (int k = 0; k < KEEP; ++k) {
+      const int tile = tile0 + k;
+      if (tile >= tile1) break;
+      const int n = tile / (tiles_r * tiles_c), rem = tile - n * (tiles_r * tiles_c);
+      const int orow0 = (rem / tiles_c) * TR, ocol0 = (rem % tiles_c) * kC1Cols;
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
+        const int fi = wave * PF + j;
+        const int orow = orow0 + (fi >> 2), ocol = ocol0 + 16 * (fi & 3) + (lane & 15);
+        if (orow >= p.OH || ocol >= p.OW) continue;
+        uint16_t* out = ob.y + (int64_t(n * p.OH + orow) * p.OW + ocol) * p.NOUT + 8 * g;
+#pragma unroll
+        for (int q = 0; q < CP; ++q) {
+          uint32_t o[4];
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            const uint32_t v = keep[k][j][q][h];
+            f32x2 r;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+              const int e = 2 * h + s;
+              const float x = s ? __uint_as_float(v & 0xFFFF0000u) : __uint_as_float(v << 16);
+              const float z = fmaf(fmaf(x, is[q][e], nm[q][e]), ww[q][e], bb[q][e]);
+              r[s] = z > 0.f ? z : z * slope;
+            }
+            o[h] = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, bf16x2));
+          }
+          *reinterpret_cast<uint4*>(out + 32 * q) = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+      }
+    }
   }
 }
 
@@ -2889,7 +3083,71 @@ int g_conv1_tiles = env_int("BT_CONV1_TILES");
 int g_conv1_rows = env_int("BT_CONV1_ROWS");
 int conv1_tiles() { return g_conv1_tiles > 0 ? g_conv1_tiles : g_conv1_tiles < 0 ? 0 : 4; }
 int conv1_rows() { return g_conv1_rows == 4 ? 4 : 2; }
+// BT_CONV1_BN=0: the first layer never applies its output's BN (the apply launch does)
+bool g_conv1_bn = !(std::getenv("BT_CONV1_BN") && std::getenv("BT_CONV1_BN")[0] == '0');
+// blocks of the BN-applying first-layer kernel that fit on the device at once (occupancy x CUs, cached)
+int conv1_bn_resident() {
+  static int cap = -1;
+  if (cap < 0) {
+    int nb = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, conv1_fwd_kernel<32, 2, true, kConv1Keep>, kThreads, 0) !=
+            hipSuccess ||
+        hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      nb = cus = 0;
+    cap = nb * cus;
+  }
+  return cap;
+}
+int64_t conv1_tiles_of(int N, int Ho, int Wo, int tr) {
+  return int64_t(N) * ((Ho + tr - 1) / tr) * ((Wo + kC1Cols - 1) / kC1Cols);
+}
+// BT_CONV_OUT_BN=0: the tap-GEMM forward never applies its output's BN
+bool g_out_bn = !(std::getenv("BT_CONV_OUT_BN") && std::getenv("BT_CONV_OUT_BN")[0] == '0');
+// blocks of the BN-applying tap-GEMM forward (64-channel tiles, 2 LDS-DMA stages) resident at once
+template <int BM>
+int tap_obn_resident() {
+  static int cap = -1;
+  if (cap < 0) {
+    int nb = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, tap_gemm_kernel<false, 64, false, BM, 2, 1, 0, true>,
+                                                     kThreads, 0) != hipSuccess ||
+        hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      nb = cus = 0;
+    cap = nb * cus;
+  }
+  return cap;
+}
 }  // namespace
+
+// the tap-GEMM forward's tile for an output BN it applies (0: it cannot: tile, staging or grid)
+int tap_obn_bm(int64_t M, int NOUT) {
+  if (!g_out_bn || M <= 0 || NOUT > kBnFoldMaxC || conv_tile_channels(NOUT, false) != 64 || staging() != 2) return 0;
+  const int bm = conv_tile_pixels(M, NOUT, 1);
+  if (bm != 64 && bm != FBM) return 0;
+  const int64_t blocks = (M + bm - 1) / bm * (NOUT / 64);
+  return blocks <= (bm == 64 ? tap_obn_resident<64>() : tap_obn_resident<FBM>()) ? bm : 0;
+}
+
+bool conv_out_bn_fits(int N, int Ho, int Wo, int Cin, int Cout) {
+  if (Cin == 4) return conv1_bn_apply_fits(N, Ho, Wo, Cout);
+  if (N <= 0 || Ho <= 0 || Wo <= 0 || Cout % 64) return false;
+  return tap_obn_bm(int64_t(N) * Ho * Wo, Cout) > 0;
+}
+
+bool conv1_bn_apply_fits(int N, int Ho, int Wo, int Cout) {
+  if (!g_conv1_bn || Cout != 32 || conv1_tiles() <= 0 || conv1_rows() != 2 || N <= 0 || Ho <= 0 || Wo <= 0)
+    return false;
+  const int64_t blocks = (conv1_tiles_of(N, Ho, Wo, 2) + kConv1Keep - 1) / kConv1Keep;
+  return blocks <= conv1_bn_resident();
+}
+
+unsigned conv_grid_barrier_timeouts() {
+  unsigned v = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_grid_barrier_timeouts), sizeof(v)) != hipSuccess) return ~0u;
+  return v;
+}
 
 void conv_set_conv1_tiles(int tiles, int rows) {   // tiles: > 0 patch kernel, -1 the tap-GEMM path, 0 default
   g_conv1_tiles = tiles;
@@ -2969,16 +3227,40 @@ hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream) {
   // the first layer from a decoded input patch (conv1_fwd_kernel): BN sums
   // into an accumulator (or none), Cout 32 / 64
   const int bn1 = conv_tile_channels(p.Cout, true);
+  if (p.out_act.on() && p.Cin != 4) {   // the tap GEMM applies the output's BN too (grid barrier)
+    const int bm = tap_obn_bm(p.M, p.Cout);
+    if (p.act.on() || !p.stats || g.acc_r <= 0 || !p.out_y || (reinterpret_cast<uintptr_t>(p.out_y) & 15) ||
+        p.out_act.acc != reinterpret_cast<double*>(p.stats) || p.out_act.R != g.acc_r || p.out_act.M != p.M ||
+        !p.out_act.b || !p.out_act.mean || !p.out_act.invstd || bm == 0 || p.M >= int64_t(kOOB))
+      return hipErrorInvalidValue;
+    g.oact = p.out_act, g.oy = p.out_y;
+    const dim3 grid(unsigned((p.M + bm - 1) / bm * (p.Cout / 64)));
+    if (bm == 64) tap_gemm_kernel<false, 64, false, 64, 2, 1, 0, true><<<grid, kThreads, 0, stream>>>(g);
+    else tap_gemm_kernel<false, 64, false, FBM, 2, 1, 0, true><<<grid, kThreads, 0, stream>>>(g);
+    return hipGetLastError();
+  }
+  if (p.out_act.on()) {   // the output's BN applied here too (grid barrier): checked again, as the caller asked
+    if (p.Cin != 4 || !p.lut || !p.stats || g.acc_r <= 0 || !p.out_y || p.Cout != 32 || bn1 != 32 ||
+        (reinterpret_cast<uintptr_t>(p.out_y) & 15) || p.out_act.acc != reinterpret_cast<double*>(p.stats) ||
+        p.out_act.R != g.acc_r || p.out_act.M != p.M || !p.out_act.b || !p.out_act.mean || !p.out_act.invstd ||
+        !conv1_bn_apply_fits(p.N, p.Ho, p.Wo, p.Cout))
+      return hipErrorInvalidValue;
+    Conv1Bn ob;
+    ob.act = p.out_act, ob.y = p.out_y;
+    const unsigned blocks = unsigned((conv1_tiles_of(p.N, p.Ho, p.Wo, 2) + kConv1Keep - 1) / kConv1Keep);
+    conv1_fwd_kernel<32, 2, true, kConv1Keep><<<blocks, kThreads, 0, stream>>>(g, kConv1Keep, ob);
+    return hipGetLastError();
+  }
   if (p.Cin == 4 && (!p.stats || g.acc_r > 0) && p.Cout == bn1 && conv1_tiles() > 0) {
     const int tr = conv1_rows(), tpb = conv1_tiles();
-    const int64_t ntiles = int64_t(p.N) * ((p.Ho + tr - 1) / tr) * ((p.Wo + kC1Cols - 1) / kC1Cols);
+    const int64_t ntiles = conv1_tiles_of(p.N, p.Ho, p.Wo, tr);
     const unsigned blocks = unsigned((ntiles + tpb - 1) / tpb);
     const dim3 grid(blocks);
     const bool u8 = g.lut != nullptr;
 #define BT_CONV1(BN_, TR_)                                                   \
     do {                                                                     \
-      if (u8) conv1_fwd_kernel<BN_, TR_, true><<<grid, kThreads, 0, stream>>>(g, tpb);  \
-      else conv1_fwd_kernel<BN_, TR_, false><<<grid, kThreads, 0, stream>>>(g, tpb);    \
+      if (u8) conv1_fwd_kernel<BN_, TR_, true><<<grid, kThreads, 0, stream>>>(g, tpb, Conv1Bn());  \
+      else conv1_fwd_kernel<BN_, TR_, false><<<grid, kThreads, 0, stream>>>(g, tpb, Conv1Bn());    \
     } while (0)
     if (bn1 == 64 && tr == 4) BT_CONV1(64, 4);
     else if (bn1 == 64) BT_CONV1(64, 2);

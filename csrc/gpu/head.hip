@@ -323,8 +323,10 @@ __global__ __launch_bounds__(kHeadThreads) void head_fwd_act_kernel(HeadParams p
       float s0 = 0.f, s1 = 0.f;
       for (int l = 0; l < PL; ++l) s0 += sa_l[l * 9 * G + (c >> 3) * 9 + (c & 7)], s1 += sb_l[l * 9 * G + (c >> 3) * 9 + (c & 7)];
       const float m = wc * inv;
-      __hip_atomic_fetch_add(p.bn_ab + int64_t(n) * p.C + c, s0 * m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(p.bn_ab + (int64_t(p.N) + n) * p.C + c, s1 * m, __ATOMIC_RELAXED,
+      // (fp64: the 16-odd window adds of an (n, c) give the same sum in any order)
+      __hip_atomic_fetch_add(p.bn_ab + int64_t(n) * p.C + c, double(s0 * m), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(p.bn_ab + (int64_t(p.N) + n) * p.C + c, double(s1 * m), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -366,21 +368,19 @@ __global__ __launch_bounds__(kHeadThreads) void head_fwd_act_kernel(HeadParams p
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const int NC = p.N * p.C;
-    const __amdgpu_buffer_rsrc_t rab = __builtin_amdgcn_make_buffer_rsrc(p.bn_ab, 0, 2 * NC * 4, 0x00020000);
     const __amdgpu_buffer_rsrc_t rdl = __builtin_amdgcn_make_buffer_rsrc(p.dlogit, 0, p.N * 4, 0x00020000);
     for (int c = t; c < p.C; c += kHeadThreads) {
       float s0 = 0.f, s1 = 0.f;
-      for (int n = 0; n < p.N; ++n) {   // (write-through reads: sc1 buffer loads)
+      for (int n = 0; n < p.N; ++n) {   // (write-through reads: sc1 buffer loads; the sums at agent scope)
         const float dl = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rdl, n * 4, 0, 16));
-        const float av = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rab, (n * p.C + c) * 4, 0, 16));
-        const float bv =
-            __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rab, (NC + n * p.C + c) * 4, 0, 16));
+        const float av = float(bn_acc_load<true>(p.bn_ab + n * p.C + c));
+        const float bv = float(bn_acc_load<true>(p.bn_ab + NC + n * p.C + c));
         s0 += dl * av;
         s1 += dl * bv;
       }
       p.bn_sums[c] = s0;
       p.bn_sums[p.C + c] = s1;
-      for (int n = 0; n < p.N; ++n) p.bn_ab[n * p.C + c] = 0.f, p.bn_ab[NC + n * p.C + c] = 0.f;   // for the next step
+      for (int n = 0; n < p.N; ++n) p.bn_ab[n * p.C + c] = 0.0, p.bn_ab[NC + n * p.C + c] = 0.0;   // for the next step
     }
   }
 }

@@ -444,7 +444,22 @@ struct ConvFwdParams {
   // apply pass (BnActIn)
   BnActIn act;
   uint16_t* act_out = nullptr;
+  // out_act.on() (first layer, u8 frames, accumulator statistics): the
+  // BatchNorm+LeakyReLU that consumes y is applied by this launch too (a grid
+  // barrier after its statistics); out_y receives leaky(bn(y)), y is still
+  // written.  Only where conv1_bn_apply_fits says so.
+  BnActIn out_act;
+  uint16_t* out_y = nullptr;
 };
+// True when conv_fwd can apply the output's BatchNorm+LeakyReLU itself on a
+// first layer of this shape (every block of the launch resident at once).
+// Needs the GPU (occupancy query); BT_CONV1_BN=0 turns it off.
+bool conv1_bn_apply_fits(int N, int Ho, int Wo, int Cout);
+// The same for any layer (Cin == 4: conv1_bn_apply_fits; else the tap-GEMM
+// forward: 64-channel tiles, its whole grid resident; BT_CONV_OUT_BN=0 off).
+bool conv_out_bn_fits(int N, int Ho, int Wo, int Cin, int Cout);
+// Grid-barrier waits that gave up (should stay 0; see conv.hip grid_barrier).
+unsigned conv_grid_barrier_timeouts();
 // Cin a power of two >= 8, or Cin == 4 (first layer, RGBA-decoded frames); Cout % 32 == 0.
 bool conv_fwd_supported(int Cin, int Cout);
 int64_t conv_fwd_tiles(int64_t M, int Cout);
@@ -558,10 +573,10 @@ struct HeadParams {
   // head_fwd_act_kernel): dz = g dlogit_n M[h][w][c] factors, so the BN
   // backward's sums are sum_n dlogit_n A[n][c] (db) and sum_n dlogit_n B[n][c]
   // (dw), A / B = sum over the pixels of M s (s = the LeakyReLU slope at the
-  // pixel) and M s xhat.  bn_ab: [2][N][C] fp32 scratch, zero before the launch
+  // pixel) and M s xhat.  bn_ab: [2][N][C] fp64 scratch (order-free sums), zero before the launch
   // and cleared again by it; bn_sums: [2][C] the two sums (db, dw) before the
   // backward's loss gradient g
-  float* bn_ab = nullptr;
+  double* bn_ab = nullptr;
   float* bn_sums = nullptr;
   // backward with bn_sums: write the BN's INPUT gradient gx (not dz) into dz,
   // and the BN's dw / db (g times the sums) into bn_dw_out / bn_db_out

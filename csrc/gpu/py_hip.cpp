@@ -401,10 +401,12 @@ PYBIND11_MODULE(_hip, m) {
   m.def("conv_fwd",
         [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, int N, int H, int W, int Cin, int Ho, int Wo,
            int Cout, uintptr_t stream, int w_channels, int acc_r, uintptr_t lut, py::object act,
-           uintptr_t act_out) {
+           uintptr_t act_out, py::object out_act, uintptr_t out_y) {
           ConvFwdParams p;
           p.act = act_from(act, "conv_fwd");
           p.act_out = ptr<uint16_t>(act_out);
+          p.out_act = act_from(out_act, "conv_fwd(out_act)");
+          p.out_y = ptr<uint16_t>(out_y);
           p.lut = ptr<const uint16_t>(lut);
           p.w_channels = w_channels;
           p.acc_r = acc_r;
@@ -418,7 +420,11 @@ PYBIND11_MODULE(_hip, m) {
         },
         py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"), py::arg("N"), py::arg("H"), py::arg("W"),
         py::arg("Cin"), py::arg("Ho"), py::arg("Wo"), py::arg("Cout"), py::arg("stream"), py::arg("w_channels") = 0,
-        py::arg("acc_r") = 0, py::arg("lut") = 0, py::arg("act") = py::none(), py::arg("act_out") = 0);
+        py::arg("acc_r") = 0, py::arg("lut") = 0, py::arg("act") = py::none(), py::arg("act_out") = 0,
+        py::arg("out_act") = py::none(), py::arg("out_y") = 0);
+  m.def("conv1_bn_apply_fits", &conv1_bn_apply_fits);
+  m.def("conv_out_bn_fits", &conv_out_bn_fits);
+  m.def("conv_grid_barrier_timeouts", &conv_grid_barrier_timeouts);
   // BatchNorm+LeakyReLU forward from conv_fwd's per-tile statistics: finalize + apply
   m.def("bn_forward_from_stats",
         [](uintptr_t x, uintptr_t y, int64_t M, int C, int dtype, uintptr_t stats, int nrows, float eps,
@@ -440,7 +446,7 @@ PYBIND11_MODULE(_hip, m) {
            uintptr_t bn_sums) {
           HeadParams p;
           p.act = act_from(act, "head_forward");
-          p.bn_ab = ptr<float>(bn_ab);
+          p.bn_ab = ptr<double>(bn_ab);
           p.bn_sums = ptr<float>(bn_sums);
           p.ticket = ptr<uint32_t>(ticket);
           p.z = ptr<const uint16_t>(z);

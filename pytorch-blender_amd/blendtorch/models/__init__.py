@@ -55,6 +55,12 @@ class Discriminator(nn.Module):
     # output): measured +9 us per step against the apply launches, so off by default (the first
     # layer, which has no data gradient, always takes its BN's backward: defer_first_bn)
     defer_bn_bwd = _env_flag('BT_DEFER_BN_BWD', False)
+    # the first BN's forward apply in the u8 first layer's own kernel, after a grid barrier on its
+    # statistics (ops.BnProduced): no apply launch, no second read of the layer's output
+    conv1_bn = _env_flag('BT_CONV1_BN', True)
+    # the same for the other layers whose forward grid fits on the chip at once (ops.conv_out_bn_fits),
+    # except the last BN, which the fused head applies (lazy_head_bn: no activation written at all)
+    conv_out_bn = _env_flag('BT_CONV_OUT_BN', True)
 
     def __init__(self, nc=3, ndf=32, adaptive=False, fused=True):
         super().__init__()
@@ -208,7 +214,7 @@ class Discriminator(nn.Module):
             if need:
                 wts = dict(zip(need, ops.conv_weights_t([w16s[k] for k in need])))
         ci = -1
-        stats = link = defer = lazy = act_next = None
+        stats = link = defer = lazy = act_next = early = None
         # the MFMA weight gradients of one backward hand their slice reduce to the
         # next one (ops.WgradChain): the first such layer's runs last and closes it
         wchain = ops.WgradChain() if (mfma and torch.is_grad_enabled() and x.is_cuda) else None
@@ -250,6 +256,15 @@ class Discriminator(nn.Module):
                         defer = wk['bn_out'] = ops.BnDeferred()
                     if closes:
                         first_mfma = False
+                    if fuse and ops.bn_acc_supported(m.out_channels) and not self.lazy_conv_bn:
+                        # the BN applied in this layer's kernel when its grid fits (ops.BnProduced) --
+                        # not the BN the caller's consumer applies (lazy_tail)
+                        j2 = i + 2
+                        while j2 < len(layers) and isinstance(layers[j2], nn.Identity):
+                            j2 += 1
+                        first = ci == 0 and lut is not None
+                        if (self.conv1_bn if first else self.conv_out_bn) and not (lazy_tail and j2 == len(layers)):
+                            early = wk['bn_early'] = nxt.produced_by_conv(x.device)
                     if fuse and ops.bn_acc_supported(m.out_channels):
                         # BN statistics come out of the conv kernel's epilogue, added into
                         # the BN call's zeroed accumulator (its apply kernel folds them)
@@ -276,10 +291,12 @@ class Discriminator(nn.Module):
                     lazy = ops.BnActLazy()   # the caller's consumer applies this BN
                 elif acc_bf16 and self.lazy_conv_bn and self._conv_applies_bn(x, layers, j, mfma):
                     lazy = act_next = ops.BnActLazy()   # the next convolution applies this BN
+                if early is not None and early.y is not None:
+                    lazy, act_next = early, None   # the first convolution applied this BN (ops.BnProduced)
                 x = m.forward_from_stats(x, stats, link, defer, lazy)
-                if lazy is act_next:
+                if lazy is act_next or lazy is early:
                     lazy = None
-                stats = defer = None
+                stats = defer = early = None
             else:
                 if not isinstance(m, nn.Identity):
                     link = None

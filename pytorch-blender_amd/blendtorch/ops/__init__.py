@@ -968,6 +968,33 @@ class BnActLazy:
         return a
 
 
+class BnProduced:
+    """Hand-off of a training BatchNorm+LeakyReLU's FORWARD apply to the
+    convolution that PRODUCES its input (the u8 first layer, :func:`conv_fwd`
+    ``out_bn=``): made by the BN module (:meth:`BatchNormLeakyReLU2d.produced_by_conv`)
+    before the convolution runs, so the kernel has the affine parameters and
+    the mean / invstd / running-statistics destinations; the kernel waits for
+    every block's statistics at a grid barrier, folds them and writes
+    ``y = leaky(bn(z))`` next to ``z``.  The BN call then launches nothing and
+    returns ``y`` (``z`` stays its saved input).  ``y`` / ``z``: set by the
+    convolution when it applied the BN (else None: the BN applies itself)."""
+    __slots__ = ('w', 'b', 'mean', 'invstd', 'eps', 'momentum', 'slope', 'rm', 'rv', 'tracked', 'y', 'z')
+
+    def __init__(self, w, b, mean, invstd, eps, momentum, slope, rm, rv, tracked):
+        self.w, self.b, self.mean, self.invstd = w, b, mean, invstd
+        self.eps, self.momentum, self.slope = float(eps), float(momentum), float(slope)
+        self.rm, self.rv, self.tracked = rm, rv, tracked
+        self.y = self.z = None
+
+    def args(self, acc, R, M):
+        """The kernel's BnActIn tuple for accumulator ``acc`` (fp64, ``R``
+        replicas) over ``M`` elements per channel."""
+        ptr = (lambda t: t.data_ptr() if t is not None else 0)
+        return (acc.data_ptr(), int(R), int(M), self.eps, self.momentum, self.w.data_ptr(), self.b.data_ptr(),
+                self.slope, self.mean.data_ptr(), self.invstd.data_ptr(), ptr(self.rm), ptr(self.rv),
+                ptr(self.tracked))
+
+
 def _bn_function():
     import torch
 
@@ -989,8 +1016,18 @@ def _bn_function():
             tr = tracked.data_ptr() if tracked is not None else 0
             if lazy is not None and not (isinstance(stats, BnAccumulator) and dt == OUT_DTYPES['bfloat16']):
                 raise ValueError('BatchNormLeakyReLU2d(lazy=): bf16 input with accumulated statistics only')
-            y = xs if lazy is not None else torch.empty_like(xs)
-            if lazy is not None:
+            produced = lazy if isinstance(lazy, BnProduced) else None
+            if produced is not None:
+                lazy = None
+                if produced.y is None or produced.z is None or produced.z.data_ptr() != xs.data_ptr():
+                    raise RuntimeError('BatchNormLeakyReLU2d: the producing convolution did not apply this BN')
+            y = xs if lazy is not None else (_as_nhwc(produced.y) if produced is not None else torch.empty_like(xs))
+            if produced is not None:
+                # the producing convolution applied this op after its statistics (BnProduced): no launch
+                _count('bn_forward_by_producer')
+                w, b, mean, invstd = produced.w, produced.b, produced.mean, produced.invstd
+                produced.y = produced.z = None
+            elif lazy is not None:
                 # the consumer applies this op while it reads x (BnActLazy): no launch here
                 _count('bn_forward_lazy')
                 lazy.args = (stats.fwd.data_ptr(), stats.R, M, float(eps), float(momentum), w.data_ptr(),
@@ -1225,6 +1262,16 @@ def _bn_module():
             ring[1] = (i + 1) % len(accs)
             return accs[i]
 
+        def produced_by_conv(self, device):
+            """A :class:`BnProduced` for the convolution that produces this
+            module's next training input: it may apply this op itself (pass
+            it to :meth:`forward_from_stats` as ``lazy`` afterwards)."""
+            import torch
+            mean = torch.empty(self.num_features, dtype=torch.float32, device=device)
+            return BnProduced(self.weight.detach().float().contiguous(), self.bias.detach().float().contiguous(),
+                              mean, torch.empty_like(mean), self.eps, self.momentum, self.slope, self.running_mean,
+                              self.running_var, self.num_batches_tracked)
+
         def forward_from_stats(self, x, stats, link=None, defer=None, lazy=None):
             """Training forward with the batch statistics already summed by
             the producing kernel (``conv_fwd``'s epilogue rows, see
@@ -1235,7 +1282,9 @@ def _bn_module():
             reduction).  ``defer``: a :class:`BnDeferred` armed by the first
             convolution that produced ``x`` (it then applies this op's
             backward itself).  ``lazy``: a :class:`BnActLazy` -- the
-            consumer applies this op itself; returns ``x`` (pre-BN)."""
+            consumer applies this op itself; returns ``x`` (pre-BN) -- or a
+            :class:`BnProduced` the producing convolution filled (returns its
+            ``y``; when the convolution did not apply it, pass None instead)."""
             global _BN_FN
             if _BN_FN is None:
                 _BN_FN = _bn_function()
@@ -1448,7 +1497,7 @@ def conv_wgrad(x, dy, out, target_blocks=None, chain=None, last=True, lut=None, 
     return out
 
 
-def conv_fwd(x, w16, stats=None, acc_r=0, lut=None, act=None, act_out=None):
+def conv_fwd(x, w16, stats=None, acc_r=0, lut=None, act=None, act_out=None, out_bn=None):
     """y = conv2d(x, w16, stride 2, pad 1) on the gfx950 MFMA kernel: ``x``
     [N, Cin, H, W] bf16 channels-last, ``w16`` [Cout, Cin, 4, 4] bf16
     channels-last; returns channels-last bf16 y.  ``stats`` (optional fp32
@@ -1463,7 +1512,11 @@ def conv_fwd(x, w16, stats=None, acc_r=0, lut=None, act=None, act_out=None):
     ``x``: also receives the decoded frames, for the weight gradient).  ``act``: the
     :class:`BnActLazy` of the BatchNorm+LeakyReLU whose INPUT ``x`` is -- the
     convolution applies it to its operand tiles; ``act_out`` (same shape as
-    ``x``, optional) receives that activation."""
+    ``x``, optional) receives that activation.  ``out_bn`` (first layer, u8
+    frames, accumulator): a :class:`BnProduced` of the BatchNorm+LeakyReLU
+    whose input y is -- when :func:`conv1_bn_apply_fits`, the kernel applies it
+    after a grid barrier and ``out_bn.y`` receives the activation (else
+    ``out_bn.y`` stays None and the BN applies itself)."""
     import torch
     ext = hip_ext()
     N, Cin, H, W = x.shape
@@ -1490,11 +1543,49 @@ def conv_fwd(x, w16, stats=None, acc_r=0, lut=None, act=None, act_out=None):
         raise ValueError('conv_fwd: acc_r needs an fp64 accumulator of 2 * Cout * acc_r elements')
     if act is not None:
         _count('conv_fwd_act')
+    oargs, oy = None, None
+    if out_bn is not None:
+        out_bn.y = out_bn.z = None
+        if acc_r and act is None and (lut is not None or Cin != 4) and conv_out_bn_fits(N, Ho, Wo, Cin, Cout,
+                                                                                      x.device):
+            oy = torch.empty_like(y)
+            oargs = out_bn.args(stats, acc_r, N * Ho * Wo)
+            _count('conv_fwd_bn_apply')
     ext.conv_fwd(x.data_ptr(), w16.data_ptr(), y.data_ptr(), stats.data_ptr() if stats is not None else 0,
                  N, H, W, Cin, Ho, Wo, Cout, _stream(x.device), wc if Cin == 4 else 0, int(acc_r),
                  lut.data_ptr() if lut is not None else 0, act.take() if act is not None else None,
-                 act_out.data_ptr() if act_out is not None else 0)
+                 act_out.data_ptr() if act_out is not None else 0, oargs, oy.data_ptr() if oy is not None else 0)
+    if oy is not None:
+        out_bn.y, out_bn.z = oy, y
     return y
+
+
+_CONV_OUT_BN_FITS = {}
+
+
+def conv_out_bn_fits(N, Ho, Wo, Cin, Cout, device):
+    """True when the forward kernel of a layer of this shape can also apply
+    the BatchNorm+LeakyReLU of its output (:class:`BnProduced`; every block
+    of the launch resident at once -- an occupancy query, cached per shape).
+    ``BT_CONV1_BN=0`` / ``BT_CONV_OUT_BN=0`` turn it off for the first layer /
+    the others."""
+    key = (int(N), int(Ho), int(Wo), int(Cin), int(Cout), str(device))
+    ok = _CONV_OUT_BN_FITS.get(key)
+    if ok is None:
+        ok = _CONV_OUT_BN_FITS[key] = bool(hip_ext().conv_out_bn_fits(int(N), int(Ho), int(Wo), int(Cin),
+                                                                      int(Cout)))
+    return ok
+
+
+def conv1_bn_apply_fits(N, Ho, Wo, Cout, device):
+    """:func:`conv_out_bn_fits` of the 4-channel (u8 frames) first layer."""
+    return conv_out_bn_fits(N, Ho, Wo, 4, Cout, device)
+
+
+def conv_grid_barrier_timeouts():
+    """Grid-barrier waits of the first-layer BN-applying kernel that gave up
+    (a wrong result instead of a hang); stays 0."""
+    return int(hip_ext().conv_grid_barrier_timeouts())
 
 
 def conv_weights_t(weights):
@@ -1606,7 +1697,7 @@ def _conv_function():
 
         @staticmethod
         def forward(ctx, x, w32, w16, with_stats=False, wt=None, bn_link=None, wchain=None, wlast=True, lut=None,
-                    bn_out=None, act=None):
+                    bn_out=None, act=None, bn_early=None):
             ctx.set_materialize_grads(False)   # no zero-filled gradient for the stats output
             if act is not None:
                 # x is the input of the BN that produced this layer's input (BnActLazy): the
@@ -1639,16 +1730,17 @@ def _conv_function():
                         # those (bf16) instead of decoding the u8 frames again
                         xd = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device,
                                          memory_format=torch.channels_last)
-                        y = conv_fwd(x, w16, with_stats.fwd, with_stats.R, lut=lut, act_out=xd)
+                        # (bn_early: the BN that consumes y is applied here too, BnProduced)
+                        y = conv_fwd(x, w16, with_stats.fwd, with_stats.R, lut=lut, act_out=xd, out_bn=bn_early)
                         ctx.save_for_backward(xd, w16)
                         ctx.lut = None
                         return y
-                    return conv_fwd(x, w16, with_stats.fwd, with_stats.R, lut=lut)
+                    return conv_fwd(x, w16, with_stats.fwd, with_stats.R, lut=lut, out_bn=bn_early)
                 if with_stats:
                     raise ValueError('conv4x4s2: u8 input takes accumulator statistics only')
                 return conv_fwd(x, w16, lut=lut)
             if isinstance(with_stats, BnAccumulator):
-                return conv_fwd(x, w16, with_stats.fwd, with_stats.R)
+                return conv_fwd(x, w16, with_stats.fwd, with_stats.R, out_bn=bn_early)
             if with_stats:
                 N, _, H, W = x.shape
                 M = N * ((H - 2) // 2 + 1) * ((W - 2) // 2 + 1)
@@ -1670,7 +1762,7 @@ def _conv_function():
             if gy is None:
                 if ctx.wchain is not None and ctx.wlast:
                     ctx.wchain.flush(x.device)
-                return None, None, None, None, None, None, None, None, None, None, None
+                return None, None, None, None, None, None, None, None, None, None, None, None
             fold_bn = isinstance(bn_dy, BnBwdFold)
             if bn_dy is not None and ctx.needs_input_grad[0] and not fold_bn:
                 raise RuntimeError('conv4x4s2: a deferred BN backward with folded sums needs a layer without a '
@@ -1752,7 +1844,7 @@ def _conv_function():
                 finally:
                     if held:
                         hip_ext().conv_dgrad_flush()   # (no-op once the weight gradient launched both)
-            return gx, gw, None, None, None, None, None, None, None, None, None
+            return gx, gw, None, None, None, None, None, None, None, None, None, None
 
         @staticmethod
         def _wgrad_side(ctx, x, gy, bn_dy, side):
@@ -1799,7 +1891,7 @@ _CONV_FN = None
 
 
 def conv4x4s2(x, w32, w16, with_stats=False, wt=None, bn_link=None, wchain=None, wlast=True, lut=None,
-              bn_out=None, act=None):
+              bn_out=None, act=None, bn_early=None):
     """4x4 / stride-2 / pad-1 convolution of bf16 channels-last ``x`` with the
     bf16 copy ``w16`` of fp32 weight ``w32``; the gradient goes to ``w32``
     (fp32, from the MFMA weight-gradient kernel).  See :func:`conv_wgrad_supported`.
@@ -1817,13 +1909,17 @@ def conv4x4s2(x, w32, w16, with_stats=False, wt=None, bn_link=None, wchain=None,
     runs inside this layer's weight-gradient kernel.  ``act``: the
     :class:`BnActLazy` of the BatchNorm+LeakyReLU whose input ``x`` is (it
     skipped its apply): the forward kernel applies it while staging its
-    operand tiles and writes the activation for the weight gradient."""
+    operand tiles and writes the activation for the weight gradient.
+    ``bn_early`` (with ``lut`` and a :class:`BnAccumulator`): a
+    :class:`BnProduced` of the BatchNorm+LeakyReLU that consumes the output
+    -- the forward kernel applies it too when :func:`conv1_bn_apply_fits`
+    (check ``bn_early.y`` afterwards)."""
     global _CONV_FN
     if _CONV_FN is None:
         _CONV_FN = _conv_function()
     if with_stats and not conv_fwd_supported(x, w16):
         raise ValueError('conv4x4s2(with_stats=True) needs the MFMA forward (see conv_fwd_supported)')
-    return _CONV_FN.apply(x, w32, w16.detach(), with_stats, wt, bn_link, wchain, wlast, lut, bn_out, act)
+    return _CONV_FN.apply(x, w32, w16.detach(), with_stats, wt, bn_link, wchain, wlast, lut, bn_out, act, bn_early)
 
 
 # ---------------------------------------------------------------------------
@@ -1939,13 +2035,14 @@ _HEAD_BN_SCRATCH = {}
 
 
 def _head_bn_scratch(dev, N, C):
-    """The zeroed [2][N][C] fp32 A / B scratch of the head forward's BN sums
-    (cleared again by the kernel's last block)."""
+    """The zeroed [2][N][C] fp64 A / B scratch of the head forward's BN sums
+    (cleared again by the kernel's last block; fp64 so the per-window adds
+    give the same sums in any order -- the step stays deterministic)."""
     import torch
     key = (dev, int(N), int(C))
     t = _HEAD_BN_SCRATCH.get(key)
     if t is None:
-        t = _HEAD_BN_SCRATCH[key] = torch.zeros(2 * N * C, dtype=torch.float32, device=dev)
+        t = _HEAD_BN_SCRATCH[key] = torch.zeros(2 * N * C, dtype=torch.float64, device=dev)
     return t
 
 
