@@ -1560,21 +1560,14 @@ def conv_fwd(x, w16, stats=None, acc_r=0, lut=None, act=None, act_out=None, out_
     return y
 
 
-_CONV_OUT_BN_FITS = {}
-
-
 def conv_out_bn_fits(N, Ho, Wo, Cin, Cout, device):
     """True when the forward kernel of a layer of this shape can also apply
     the BatchNorm+LeakyReLU of its output (:class:`BnProduced`; every block
-    of the launch resident at once -- an occupancy query, cached per shape).
-    ``BT_CONV1_BN=0`` / ``BT_CONV_OUT_BN=0`` turn it off for the first layer /
-    the others."""
-    key = (int(N), int(Ho), int(Wo), int(Cin), int(Cout), str(device))
-    ok = _CONV_OUT_BN_FITS.get(key)
-    if ok is None:
-        ok = _CONV_OUT_BN_FITS[key] = bool(hip_ext().conv_out_bn_fits(int(N), int(Ho), int(Wo), int(Cin),
-                                                                      int(Cout)))
-    return ok
+    of the launch resident at once -- the occupancy is queried once; asked on
+    every call, since the tile overrides (:func:`conv_set_tiles`) change the
+    answer).  ``BT_CONV1_BN=0`` / ``BT_CONV_OUT_BN=0`` turn it off for the
+    first layer / the others."""
+    return bool(hip_ext().conv_out_bn_fits(int(N), int(Ho), int(Wo), int(Cin), int(Cout)))
 
 
 def conv1_bn_apply_fits(N, Ho, Wo, Cout, device):
