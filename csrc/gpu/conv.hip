@@ -1243,21 +1243,25 @@ __device__ __forceinline__ int bkey(int r) { return ((r >> 1) & 1) | (((r >> 3) 
 
 // Blocks of one launch wait here for each other (all of them resident: the
 // caller's duty).  bar: a zero word; the last arriver resets it, the others
-// spin on it with s_sleep.  A spin that outlasts ~1 s gives up and counts
-// itself in g_grid_barrier_timeouts (conv_grid_barrier_timeouts): a wrong
-// result instead of a hung GPU.
+// spin on it with s_sleep.  No fences: what the blocks hand over is atomics
+// at agent scope (the BN sums, performed past the XCD caches once this wave's
+// vmcnt drains) read back with agent-scope loads -- a release / acquire per
+// wave wrote back and invalidated the XCD's L2 and made the launch 4-5x slower
+// (profiles/r5/b13).  A spin that outlasts ~1 s gives up and counts itself in
+// g_grid_barrier_timeouts (conv_grid_barrier_timeouts): a wrong result
+// instead of a hung GPU.
 __device__ unsigned g_grid_barrier_timeouts = 0;
 constexpr unsigned kBarrierSpins = 1u << 22;
 __device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned nblk) {
-  __threadfence();   // this thread's atomics and stores performed at agent scope
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's atomics have been performed
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned old = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned old = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (old == nblk - 1) {
-      __hip_atomic_store(bar, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
       unsigned n = 0;
-      while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+      while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
         __builtin_amdgcn_s_sleep(4);
         if (++n == kBarrierSpins) {
           atomicAdd(&g_grid_barrier_timeouts, 1u);
