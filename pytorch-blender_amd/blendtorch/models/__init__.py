@@ -56,11 +56,14 @@ class Discriminator(nn.Module):
     # layer, which has no data gradient, always takes its BN's backward: defer_first_bn)
     defer_bn_bwd = _env_flag('BT_DEFER_BN_BWD', False)
     # the first BN's forward apply in the u8 first layer's own kernel, after a grid barrier on its
-    # statistics (ops.BnProduced): no apply launch, no second read of the layer's output
-    conv1_bn = _env_flag('BT_CONV1_BN', True)
+    # statistics (ops.BnProduced): no apply launch, no second read of the layer's output.  Measured
+    # slower (conv1 24.7 + 11.6 us -> 60.3 us: the barrier's tail and the 2-waves-per-SIMD launch,
+    # profiles/r5/b14), so off by default
+    conv1_bn = _env_flag('BT_CONV1_BN', False)
     # the same for the other layers whose forward grid fits on the chip at once (ops.conv_out_bn_fits),
-    # except the last BN, which the fused head applies (lazy_head_bn: no activation written at all)
-    conv_out_bn = _env_flag('BT_CONV_OUT_BN', True)
+    # except the last BN, which the fused head applies (lazy_head_bn: no activation written at all);
+    # conv3 20.2 + 9.3 -> 46.0 us (profiles/r5/b14), off by default
+    conv_out_bn = _env_flag('BT_CONV_OUT_BN', False)
 
     def __init__(self, nc=3, ndf=32, adaptive=False, fused=True):
         super().__init__()
