@@ -157,6 +157,9 @@ def parse_args(argv=None):
     ap.add_argument('--backend', choices=['nccl', 'gloo'], default='nccl',
                     help='process-group backend (nccl = RCCL over xGMI; gloo only to rehearse several ranks on one GPU)')
     ap.add_argument('--start-port', type=int, default=0)
+    ap.add_argument('--sustain-s', type=float, default=2.0,
+                    help='after the timed steps, time about this many more seconds of steps and report them as '
+                         '"sustained" (a short timed window is served from the warm-up backlog); 0: off')
     ap.add_argument('--host-sync', choices=['auto', 'on', 'off'], default='auto',
                     help='loader/consumer ordering by host-side event checks (on) or cross-stream waits (off); '
                          'auto = on (a stream of cross-stream waits keeps a HIP runtime thread busy: 43 -> 20 '
@@ -414,7 +417,8 @@ def main(argv=None):
         crit = torch.nn.BCELoss()
 
     WARM_RESERVE = 2000   # extra warm-up batches allowed while producers come up
-    total_batches = args.warmup + args.steps + (WARM_RESERVE if args.dist != 'scatter' else 0)
+    SUSTAIN_RESERVE = 12000 if args.sustain_s > 0 else 0   # batches the sustained window may draw (bound only)
+    total_batches = args.warmup + args.steps + (WARM_RESERVE + SUSTAIN_RESERVE if args.dist != 'scatter' else 0)
     last = {'btid': None}
     from contextlib import ExitStack
     from blendtorch.parallel import ScatterLoader
@@ -558,6 +562,40 @@ def main(argv=None):
         snap1 = dl.snapshot() if dl is not None else {}
         ru1 = os.times()
         cg1 = cgroup_cpu_stat()
+        # Sustained rate, reported next to (never instead of) the timed K steps:
+        # a short driver window (e.g. 20 steps) is served from the frames the
+        # producers queued during warm-up (backlog_covers_window), so the same
+        # run also times ~--sustain-s more seconds of steps that the backlog
+        # cannot cover, with its own loader window.  Every rank runs the same
+        # number of steps (the data-parallel step all-reduces per step).
+        sustained = None
+        if args.sustain_s > 0 and args.dist != 'scatter':
+            te = torch.tensor([elapsed], dtype=torch.float64, device=pg_dev)
+            if world > 1:
+                dist.all_reduce(te, op=dist.ReduceOp.MAX)
+            per = float(te.item()) / max(1, args.steps)
+            left = total_batches - n_warm - args.steps - 2
+            n_sus = int(min(left, max(0, args.sustain_s / max(per, 1e-6))))
+            if n_sus * args.batch * (1 + world) > 16 * args.batch and n_sus >= 4 * args.steps:
+                sa = dl.snapshot() if dl is not None else {}
+                ts = time.perf_counter()
+                for _ in range(n_sus):
+                    step()
+                if stepper is not None:
+                    stepper.flush()
+                torch.cuda.synchronize()
+                if world > 1:
+                    dist.barrier()
+                tsx = torch.tensor([time.perf_counter() - ts], dtype=torch.float64, device=pg_dev)
+                if world > 1:
+                    dist.all_reduce(tsx, op=dist.ReduceOp.MAX)
+                sb = dl.snapshot() if dl is not None else {}
+                ws = DeviceLoader.window(sa, sb) if dl is not None else {}
+                sustained = {'steps': n_sus, 'seconds': round(float(tsx.item()), 4),
+                             'images_per_s': round(n_sus * args.batch * world / float(tsx.item()), 2),
+                             'ms_per_step': round(float(tsx.item()) / n_sus * 1e3, 4),
+                             'backlog_covers_window': ws.get('backlog_covers_window') if ws else None,
+                             'producer_share_max_over_min': ws.get('producer_share_max_over_min') if ws else None}
         cpu = {'consumer_cpu_s': round((ru1.user - ru0.user) + (ru1.system - ru0.system), 3)}
         for k in ('usage_usec', 'throttled_usec', 'nr_throttled'):
             if k in cg0 and k in cg1:
@@ -695,6 +733,8 @@ def main(argv=None):
             'ring_t0': win.get('ring_t0'),
             'ring_t1': win.get('ring_t1'),
             'consumer_wait_ms_per_batch': _r(win.get('consumer_wait_ms_per_batch'), 4),
+            # ~--sustain-s more steps right after the timed ones (not part of value)
+            'sustained': sustained,
             # whole run incl. start-up (for comparison with the window)
             'run_frames_per_producer': metrics.get('frames_per_producer'),
             'cpu': cpu,

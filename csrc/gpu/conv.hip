@@ -33,6 +33,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstdint>
+#include <cstring>
 #include <type_traits>
 
 #include "adam_sched.h"
@@ -175,7 +176,59 @@ __device__ __forceinline__ void zero_output(const ConvWgradParams& p) { zero_out
 constexpr int kSliceGroup = 8;   // (groups of 32 for the first layer's 512 slices -- 16 atomics per
                                  // element instead of 64 -- measured slower: 8.4 -> 11.0 us)
 
+// The ordered form (r.sub > 0, the default; BT_WGRAD_ORDERED=0: the atomic
+// groups above): bit-identical gradients run to run.  Lane groups of `sub`
+// (a power of two <= 64, <= S) share 4 elements; lane `part` of a group sums
+// slices part, part + sub, ... in that order, 8 loads in flight, then the
+// group adds its lanes with a fixed xor-shuffle tree (commutative adds: every
+// lane ends with the same bits) and lane 0 stores.  Same bytes read as the
+// atomic form, no zeroing of the output, no atomics.
+__device__ __forceinline__ void wgrad_reduce_ordered(const ConvWgradParams::Reduce& r, int bx) {
+  if (int(threadIdx.x) >= kThreads) return;   // (wave-uniform: a side job of a wider block)
+  const float* __restrict__ partial = r.partial;
+  const int S = r.S, sub = r.sub, Cin = r.Cin, cin_out = r.cin_out;
+  const int KC = 16 * Cin;
+  const int total = r.Cout * KC;
+  const int gl = bx * kThreads + int(threadIdx.x);
+  const int part = gl & (sub - 1);
+  const int e0 = (gl / sub) * 4;
+  const bool live = e0 < total;   // (group-uniform: all sub lanes of a group share e0)
+  const int64_t base = live ? e0 : 0;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int k0 = part; k0 < S; k0 += kSliceGroup * sub) {
+    float4 v[kSliceGroup];
+#pragma unroll
+    for (int j = 0; j < kSliceGroup; ++j) {   // past the last slice: re-read slice `part` (< S), not added
+      const int k = k0 + j * sub;
+      v[j] = *reinterpret_cast<const float4*>(partial + int64_t(k < S ? k : part) * total + base);
+    }
+#pragma unroll
+    for (int j = 0; j < kSliceGroup; ++j)
+      if (k0 + j * sub < S) acc.x += v[j].x, acc.y += v[j].y, acc.z += v[j].z, acc.w += v[j].w;
+  }
+  for (int o = sub >> 1; o > 0; o >>= 1) {
+    acc.x += __shfl_xor(acc.x, o);
+    acc.y += __shfl_xor(acc.y, o);
+    acc.z += __shfl_xor(acc.z, o);
+    acc.w += __shfl_xor(acc.w, o);
+  }
+  if (!live || part != 0) return;
+  const float vals[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int e = e0 + j;
+    const int co = e / KC, kc = e - co * KC;
+    const int tap = kc / Cin, ci = kc - tap * Cin;
+    if (ci >= cin_out) continue;
+    r.out[co * r.s_co + ci * r.s_ci + (tap >> 2) * r.s_kh + (tap & 3) * r.s_kw] = vals[j];
+  }
+}
+
 __device__ __forceinline__ void wgrad_reduce_block(const ConvWgradParams::Reduce& r, int bx, int by) {
+  if (r.sub > 0) {
+    wgrad_reduce_ordered(r, bx);
+    return;
+  }
   const float* __restrict__ partial = r.partial;
   const int S = r.S, Cin = r.Cin, cin_out = r.cin_out;
   float* __restrict__ out = r.out;
@@ -1247,10 +1300,13 @@ __device__ __forceinline__ int bkey(int r) { return ((r >> 1) & 1) | (((r >> 3) 
 // at agent scope (the BN sums, performed past the XCD caches once this wave's
 // vmcnt drains) read back with agent-scope loads -- a release / acquire per
 // wave wrote back and invalidated the XCD's L2 and made the launch 4-5x slower
-// (profiles/r5/b13).  A spin that outlasts ~1 s gives up and counts itself in
-// g_grid_barrier_timeouts (conv_grid_barrier_timeouts): a wrong result
-// instead of a hung GPU.
+// (profiles/r5/b13).  A spin that outlasts ~1 s gives up (never a hung GPU),
+// counts itself in g_grid_barrier_timeouts (conv_grid_barrier_timeouts) and
+// raises the host-mapped flag g_grid_barrier_flag: the host polls that word
+// without a HIP call (conv_grid_barrier_failed) and ops / CapturedStep raise
+// on it, so BN statistics folded past a failed barrier never train silently.
 __device__ unsigned g_grid_barrier_timeouts = 0;
+__device__ unsigned* g_grid_barrier_flag = nullptr;   // host-mapped (conv_grid_barrier_arm)
 constexpr unsigned kBarrierSpins = 1u << 22;
 __device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned nblk) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's atomics have been performed
@@ -1265,6 +1321,8 @@ __device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned nblk) {
         __builtin_amdgcn_s_sleep(4);
         if (++n == kBarrierSpins) {
           atomicAdd(&g_grid_barrier_timeouts, 1u);
+          if (unsigned* f = g_grid_barrier_flag)
+            __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           break;
         }
       }
@@ -2738,6 +2796,15 @@ int wgrad_pipe() {
   }
   return g_wgrad_pipe;
 }
+// the ordered (deterministic) slice reduce (wgrad_reduce_ordered); BT_WGRAD_ORDERED=0: atomic groups
+int g_wgrad_ordered = -1;
+bool wgrad_ordered() {
+  if (g_wgrad_ordered < 0) {
+    const char* v = std::getenv("BT_WGRAD_ORDERED");
+    g_wgrad_ordered = v && v[0] == '0' ? 0 : 1;
+  }
+  return g_wgrad_ordered == 1;
+}
 int g_wgrad_staging = -1;
 int wgrad_staging() {
   if (g_wgrad_staging < 0) {
@@ -2776,6 +2843,8 @@ void conv_set_c4w_waves(int nw) { g_c4w_waves = nw == 4 || nw == 8 ? nw : -1; }
 void conv_set_dgrad_patch(int on) { g_dgrad_patch = on < 0 ? -1 : (on ? 1 : 0); }
 void conv_set_wgrad_wide(int on) { g_wgrad_wide = on < 0 ? -1 : (on ? 1 : 0); }
 void conv_set_wgrad_pipe(int on) { g_wgrad_pipe = on < 0 ? -1 : (on ? 1 : 0); }
+void conv_set_wgrad_ordered(int on) { g_wgrad_ordered = on < 0 ? -1 : (on ? 1 : 0); }
+
 void conv_set_wgrad_staging(int staging) { g_wgrad_staging = staging == 0 || staging == 2 || staging == 3 ? staging : -1; }
 
 bool conv_wgrad_supported(int Cin, int Cout) {
@@ -2902,7 +2971,7 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
   const int64_t blocks = tiles * p.slices;
   if (blocks > (int64_t(1) << 31) - 1) return hipErrorInvalidValue;
   ConvWgradParams q = p;
-  if (p.slices > kSliceGroup) {   // groups add atomically: the main kernel zeroes out first (dense tensor)
+  if (p.slices > kSliceGroup && !wgrad_ordered()) {   // groups add atomically: the main kernel zeroes out first
     q.zero_out = out;
     q.zero_count = p.Cout * 16 * (p.cin_out > 0 ? p.cin_out : p.Cin);
   }
@@ -2975,8 +3044,16 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
   r.partial = p.partial, r.S = p.slices, r.Cout = p.Cout, r.Cin = p.Cin;
   r.cin_out = p.cin_out > 0 ? p.cin_out : p.Cin;
   r.out = out, r.s_co = s_co, r.s_ci = s_ci, r.s_kh = s_kh, r.s_kw = s_kw;
-  r.rx = int((total / 4 + kThreads - 1) / kThreads);
-  r.ry = (p.slices + kSliceGroup - 1) / kSliceGroup;
+  if (wgrad_ordered()) {
+    int sub = 1;   // lanes per 4 elements: each walks <= 16 slices (two rounds of 8 loads in flight)
+    while (sub < 64 && (p.slices + sub - 1) / sub > 2 * kSliceGroup) sub <<= 1;
+    r.sub = sub;
+    r.rx = int((total / 4 * sub + kThreads - 1) / kThreads);
+    r.ry = 1;
+  } else {
+    r.rx = int((total / 4 + kThreads - 1) / kThreads);
+    r.ry = (p.slices + kSliceGroup - 1) / kSliceGroup;
+  }
   if (defer) {
     *defer = r;
     return hipGetLastError();
@@ -3151,6 +3228,35 @@ unsigned conv_grid_barrier_timeouts() {
   unsigned v = 0;
   if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_grid_barrier_timeouts), sizeof(v)) != hipSuccess) return ~0u;
   return v;
+}
+
+namespace {
+volatile unsigned* g_barrier_host_flag = nullptr;   // host view of g_grid_barrier_flag
+}
+
+bool conv_grid_barrier_arm() {
+  // once per process, outside any graph capture (a symbol copy cannot be
+  // captured): the callers arm it when a grid-barrier path is first chosen
+  if (g_barrier_host_flag) return true;
+  void* host = nullptr;
+  if (hipHostMalloc(&host, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return false;
+  std::memset(host, 0, 64);
+  void* dev = nullptr;
+  if (hipHostGetDevicePointer(&dev, host, 0) != hipSuccess ||
+      hipMemcpyToSymbol(HIP_SYMBOL(g_grid_barrier_flag), &dev, sizeof(dev)) != hipSuccess) {
+    (void)hipHostFree(host);
+    return false;
+  }
+  g_barrier_host_flag = static_cast<volatile unsigned*>(host);
+  return true;
+}
+
+int conv_grid_barrier_failed() {   // no HIP call: a plain read of the host-mapped word
+  return g_barrier_host_flag ? int(*g_barrier_host_flag) : -1;
+}
+
+void conv_grid_barrier_clear(int value) {   // value != 0: simulate a failure (tests)
+  if (g_barrier_host_flag) *g_barrier_host_flag = unsigned(value);
 }
 
 void conv_set_conv1_tiles(int tiles, int rows) {   // tiles: > 0 patch kernel, -1 the tap-GEMM path, 0 default

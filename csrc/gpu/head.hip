@@ -323,7 +323,8 @@ __global__ __launch_bounds__(kHeadThreads) void head_fwd_act_kernel(HeadParams p
       float s0 = 0.f, s1 = 0.f;
       for (int l = 0; l < PL; ++l) s0 += sa_l[l * 9 * G + (c >> 3) * 9 + (c & 7)], s1 += sb_l[l * 9 * G + (c >> 3) * 9 + (c & 7)];
       const float m = wc * inv;
-      // (fp64: the 16-odd window adds of an (n, c) give the same sum in any order)
+      // (fp64 atomics: the ~16 window adds of an (n, c) arrive in any order; the sum is not order-exact in
+      // general, but its rounding error is ~1e-16 relative -- far below the fp32 the backward reads it as)
       __hip_atomic_fetch_add(p.bn_ab + int64_t(n) * p.C + c, double(s0 * m), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_fetch_add(p.bn_ab + (int64_t(p.N) + n) * p.C + c, double(s1 * m), __ATOMIC_RELAXED,

@@ -326,6 +326,10 @@ struct ConvWgradParams {
     float* out = nullptr;
     int64_t s_co = 0, s_ci = 0, s_kh = 0, s_kw = 0;
     int rx = 0, ry = 0;   // its grid: element blocks x slice groups
+    // sub > 0: the ordered (deterministic) reduce -- ry == 1, sub lanes per
+    // 4 elements each sum a fixed subset of the slices in a fixed order, then
+    // a fixed xor-shuffle tree; one plain store per element (no atomics)
+    int sub = 0;
   } side;
   // fold.acc != nullptr (not the 4-channel first layer): one more block folds
   // the BatchNorm backward accumulator the preceding data gradient's epilogue
@@ -373,6 +377,7 @@ bool conv_wgrad_supported(int Cin, int Cout);
 int conv_wgrad_slices(int64_t M, int Cin, int Cout, int target_blocks);
 // Weight-gradient staging (not the 4-channel layer): 0 = register ring,
 // 2 / 3 = LDS-DMA stages of 64 pixels (default 0; -1 = BT_WGRAD_STAGING or default).
+void conv_set_wgrad_ordered(int on);   // 1 ordered (deterministic) slice reduce, 0 atomic groups, -1 env
 void conv_set_wgrad_staging(int staging);
 // Register-staged weight gradient: 1 = read the next step's fragments while this step's MFMAs run
 // (two fragment sets), 0 = one set (default), -1 = BT_WGRAD_PIPE / default.
@@ -460,6 +465,10 @@ bool conv1_bn_apply_fits(int N, int Ho, int Wo, int Cout);
 bool conv_out_bn_fits(int N, int Ho, int Wo, int Cin, int Cout);
 // Grid-barrier waits that gave up (should stay 0; see conv.hip grid_barrier).
 unsigned conv_grid_barrier_timeouts();
+// host-mapped failure flag of the grid barrier: arm once (outside capture), poll without a HIP call
+bool conv_grid_barrier_arm();
+int conv_grid_barrier_failed();   // -1 not armed, 0 ok, 1 a barrier gave up
+void conv_grid_barrier_clear(int value);
 // Cin a power of two >= 8, or Cin == 4 (first layer, RGBA-decoded frames); Cout % 32 == 0.
 bool conv_fwd_supported(int Cin, int Cout);
 int64_t conv_fwd_tiles(int64_t M, int Cout);

@@ -144,20 +144,21 @@ void fill_cmap(int* dst, const std::vector<int>& cmap) {
 }  // namespace
 
 // a deferred weight-gradient slice reduce (ConvWgradParams::Reduce) as a
-// plain tuple: (partial, S, Cout, Cin, cin_out, out, s_co, s_ci, s_kh, s_kw, rx, ry)
+// plain tuple: (partial, S, Cout, Cin, cin_out, out, s_co, s_ci, s_kh, s_kw, rx, ry, sub)
 py::tuple reduce_to_tuple(const ConvWgradParams::Reduce& r) {
   return py::make_tuple(reinterpret_cast<uintptr_t>(r.partial), r.S, r.Cout, r.Cin, r.cin_out,
-                        reinterpret_cast<uintptr_t>(r.out), r.s_co, r.s_ci, r.s_kh, r.s_kw, r.rx, r.ry);
+                        reinterpret_cast<uintptr_t>(r.out), r.s_co, r.s_ci, r.s_kh, r.s_kw, r.rx, r.ry, r.sub);
 }
 
 ConvWgradParams::Reduce reduce_from_tuple(const py::tuple& t) {
-  if (t.size() != 12) throw std::invalid_argument("conv_wgrad: a deferred reduce is a 12-tuple");
+  if (t.size() != 13) throw std::invalid_argument("conv_wgrad: a deferred reduce is a 13-tuple");
   ConvWgradParams::Reduce r;
   r.partial = reinterpret_cast<const float*>(t[0].cast<uintptr_t>());
   r.S = t[1].cast<int>(), r.Cout = t[2].cast<int>(), r.Cin = t[3].cast<int>(), r.cin_out = t[4].cast<int>();
   r.out = reinterpret_cast<float*>(t[5].cast<uintptr_t>());
   r.s_co = t[6].cast<int64_t>(), r.s_ci = t[7].cast<int64_t>(), r.s_kh = t[8].cast<int64_t>();
   r.s_kw = t[9].cast<int64_t>(), r.rx = t[10].cast<int>(), r.ry = t[11].cast<int>();
+  r.sub = t[12].cast<int>();
   return r;
 }
 
@@ -333,6 +334,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("conv_set_tiles", &conv_set_tiles, py::arg("bm") = 0, py::arg("bn") = 0, py::arg("staging") = -1,
         py::arg("dgrad_cls") = 0);
   m.def("conv_dgrad_classes_per_block", &conv_dgrad_classes_per_block);
+  m.def("conv_set_wgrad_ordered", &conv_set_wgrad_ordered);
   m.def("conv_set_wgrad_staging", &conv_set_wgrad_staging);
   m.def("conv_set_wgrad_pipe", &conv_set_wgrad_pipe);
   m.def("conv_set_wgrad_wide", &conv_set_wgrad_wide);
@@ -425,6 +427,9 @@ PYBIND11_MODULE(_hip, m) {
   m.def("conv1_bn_apply_fits", &conv1_bn_apply_fits);
   m.def("conv_out_bn_fits", &conv_out_bn_fits);
   m.def("conv_grid_barrier_timeouts", &conv_grid_barrier_timeouts);
+  m.def("conv_grid_barrier_arm", &conv_grid_barrier_arm);
+  m.def("conv_grid_barrier_failed", &conv_grid_barrier_failed);
+  m.def("conv_grid_barrier_clear", &conv_grid_barrier_clear, pybind11::arg("value") = 0);
   // BatchNorm+LeakyReLU forward from conv_fwd's per-tile statistics: finalize + apply
   m.def("bn_forward_from_stats",
         [](uintptr_t x, uintptr_t y, int64_t M, int C, int dtype, uintptr_t stats, int nrows, float eps,

@@ -1351,7 +1351,7 @@ class WgradChain:
 
     def flush(self, device):
         if self.pending is not None:
-            side = _SIDE_STREAMS.get(device)
+            side = _SIDE_STREAMS.get(device) if device in _SIDE_PENDING else None
             if side is not None:   # the pending reduce's partials may have been written on the side stream
                 import torch
                 torch.cuda.current_stream(device).wait_stream(side)
@@ -1368,6 +1368,11 @@ _C4W_BLOCKS = int(os.environ.get('BT_C4W_BLOCKS', str(_WGRAD_BLOCKS)))
 _SIDE_WGRAD = os.environ.get('BT_WGRAD_SIDE', '0') not in ('', '0')
 _SIDE_STREAMS = {}
 _SIDE_KEEP = []   # main-stream tensors the side stream reads, until it joins the main stream
+# devices whose side stream holds weight-gradient work of this backward not yet joined to the
+# main stream: only then must a reduce or a gradient bucket's all-reduce wait for it (a stream
+# that exists from an earlier run is not waited on -- inside a later capture that wait would
+# reach work recorded outside the capture)
+_SIDE_PENDING = set()
 
 
 def _side_stream(device):
@@ -1551,6 +1556,7 @@ def conv_fwd(x, w16, stats=None, acc_r=0, lut=None, act=None, act_out=None, out_
             oy = torch.empty_like(y)
             oargs = out_bn.args(stats, acc_r, N * Ho * Wo)
             _count('conv_fwd_bn_apply')
+            _grid_barrier_armed()
     ext.conv_fwd(x.data_ptr(), w16.data_ptr(), y.data_ptr(), stats.data_ptr() if stats is not None else 0,
                  N, H, W, Cin, Ho, Wo, Cout, _stream(x.device), wc if Cin == 4 else 0, int(acc_r),
                  lut.data_ptr() if lut is not None else 0, act.take() if act is not None else None,
@@ -1576,9 +1582,50 @@ def conv1_bn_apply_fits(N, Ho, Wo, Cout, device):
 
 
 def conv_grid_barrier_timeouts():
-    """Grid-barrier waits of the first-layer BN-applying kernel that gave up
-    (a wrong result instead of a hang); stays 0."""
+    """Grid-barrier waits of the BN-applying forward kernels that gave up
+    (the block went on instead of hanging the GPU); stays 0."""
     return int(hip_ext().conv_grid_barrier_timeouts())
+
+
+# set once a grid-barrier (BN-applying forward) launch has been enqueued in this process
+GRID_BARRIER_USED = False
+
+
+class GridBarrierError(RuntimeError):
+    """A BN-applying forward kernel's grid barrier timed out: some of its
+    blocks were not co-resident (e.g. another stream or process held CUs), so
+    the launch folded incomplete BatchNorm statistics."""
+
+
+def _grid_barrier_armed():
+    global GRID_BARRIER_USED
+    if not GRID_BARRIER_USED:
+        # host-mapped failure word, armed outside any capture the first time the
+        # path is taken (the same launch's shape also ran eagerly before capture)
+        if not hip_ext().conv_grid_barrier_arm():
+            raise RuntimeError('conv_fwd: could not map the grid-barrier failure flag')
+        GRID_BARRIER_USED = True
+    check_grid_barrier()
+
+
+def check_grid_barrier():
+    """Raise :class:`GridBarrierError` if any grid barrier enqueued so far has
+    been seen to give up.  A plain read of a host-mapped word (no HIP call, no
+    synchronisation): a failure surfaces at the first check after the kernel
+    ran.  Called by :func:`conv_fwd` and after every :class:`CapturedStep`;
+    ``bench.py`` checks once more after its final synchronize.  The flag is
+    sticky: :func:`clear_grid_barrier` resets it (tests)."""
+    if GRID_BARRIER_USED and hip_ext().conv_grid_barrier_failed() > 0:
+        raise GridBarrierError(
+            f'a BN-applying convolution\'s grid barrier timed out ({conv_grid_barrier_timeouts()} waits gave up): '
+            'the launch was not co-resident and folded incomplete BatchNorm statistics.  Run without '
+            'BT_CONV1_BN / BT_CONV_OUT_BN, or keep other work off the GPU during the step')
+
+
+def clear_grid_barrier(_simulate_failure=False):
+    """Reset the sticky failure flag (``_simulate_failure``: set it, for tests)."""
+    if GRID_BARRIER_USED:
+        hip_ext().conv_grid_barrier_clear(1 if _simulate_failure else 0)
 
 
 def conv_weights_t(weights):
@@ -1819,7 +1866,7 @@ def _conv_function():
             elif gy_dgrad is gy and side is not None:   # (no data gradient: the chain's last, the first layer)
                 gw = _Conv4x4s2._wgrad_side(ctx, x, gy, bn_dy, side)
             elif gy_dgrad is gy:   # (not already run before the data gradient)
-                prior = _SIDE_STREAMS.get(x.device) if x.is_cuda else None
+                prior = _SIDE_STREAMS.get(x.device) if x.is_cuda and x.device in _SIDE_PENDING else None
                 if prior is not None and ctx.wchain is not None and ctx.wchain.pending is not None:
                     # the chain's pending reduce reads partials an earlier launch wrote on the side stream
                     torch.cuda.current_stream(x.device).wait_stream(prior)
@@ -1847,6 +1894,7 @@ def _conv_function():
             accumulates itself."""
             main = torch.cuda.current_stream(x.device)
             with torch.cuda.stream(side):
+                _SIDE_PENDING.add(x.device)
                 gw = _Conv4x4s2._wgrad(ctx, x, gy, None, ctx.bn_link, bn_dy)
             # x and gy live in main-stream memory the side stream still reads: they
             # stay referenced until the join (a block freed earlier could be handed
@@ -1856,6 +1904,7 @@ def _conv_function():
             if ctx.wlast or gw is not None:
                 main.wait_stream(side)
                 _SIDE_KEEP.clear()
+                _SIDE_PENDING.discard(x.device)
             return gw
 
         @staticmethod

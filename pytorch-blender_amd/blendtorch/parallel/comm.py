@@ -230,7 +230,10 @@ class DeviceComm:
         1. a point-to-point ring (send ``nbytes`` to rank+1, receive from
            rank-1) -- the xGMI P2P path scatter mode uses, which an all-reduce
            alone does not prove;
-        2. an all-reduce of device tensors (sum of rank+1 == w(w+1)/2).
+        2. an all-reduce of device tensors (sum of rank+1 == w(w+1)/2);
+        3. (native RCCL) the same all-reduce captured in a HIP graph between
+           two kernels and replayed twice -- the form the data-parallel
+           training step replays every step.
 
         Each stage is waited for with a host-side timeout; a hang or a wrong
         value raises ``RuntimeError`` naming this rank, the peer(s) and RCCL's
@@ -277,4 +280,40 @@ class DeviceComm:
             raise RuntimeError(f'rank {r}/{w}: RCCL all-reduce gave {float(t[0])}, expected {want}')
         out['all_reduce_ms'] = (time.perf_counter() - t0) * 1e3
         out['native'] = self.native
+        if self.native:
+            out['graph_all_reduce_ms'] = self._selfcheck_graph(wait)
         return out
+
+    def _selfcheck_graph(self, wait) -> float:
+        """Stage 3: the collective as :class:`~.step.CapturedStep` runs it at
+        world > 1 -- ``ncclAllReduce`` captured into a HIP graph with kernels
+        around it, replayed twice.  A capture that RCCL rejects, a replay that
+        hangs, or a wrong sum raises here, before any training step depends on it."""
+        import time
+        w, r = self.world, self.rank
+        t0 = time.perf_counter()
+        dev = self.device
+        t = torch.empty((1024,), device=dev)
+        acc = torch.zeros((1024,), device=dev)
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        g = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.stream(side):
+                with torch.cuda.graph(g, stream=side, capture_error_mode='thread_local'):
+                    t.fill_(float(r + 1))
+                    self.all_reduce_(t)
+                    acc.add_(t)
+        except RuntimeError as e:
+            raise RuntimeError(f'rank {r}/{w}: capturing ncclAllReduce into a HIP graph failed ({e}); async '
+                               f'error: {self.async_error() or "none"}') from e
+        torch.cuda.current_stream(dev).wait_stream(side)
+        for _ in range(2):
+            g.replay()
+        wait('graph all_reduce (captured, 2 replays)', 'all')
+        want = 2.0 * w * (w + 1) / 2
+        if not bool((acc == want).all()):
+            raise RuntimeError(f'rank {r}/{w}: graph-captured RCCL all-reduce gave {float(acc[0])} after 2 replays, '
+                               f'expected {want}')
+        del g
+        return (time.perf_counter() - t0) * 1e3

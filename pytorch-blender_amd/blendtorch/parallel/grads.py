@@ -166,7 +166,7 @@ class GradBuckets:
             # weight gradients run on a side stream (ops.set_side_wgrad): a bucket
             # completed from the main stream also waits for the side stream's
             # launches; one completed from the side stream reduces there, behind them
-            side = ops._SIDE_STREAMS.get(b.device)
+            side = ops._SIDE_STREAMS.get(b.device) if b.device in ops._SIDE_PENDING else None
             cur = torch.cuda.current_stream(b.device)
             if side is not None and cur != side:
                 cur.wait_stream(side)

@@ -34,7 +34,7 @@ from typing import Callable, List, Optional, Sequence
 import torch
 import torch.distributed as dist
 
-__all__ = ['allreduce_gradients', 'CapturedStep']
+__all__ = ['allreduce_gradients', 'CapturedStep', 'ReplayWatchdog']
 
 
 def _buckets(params: Sequence[torch.Tensor], bucket_bytes: int) -> List[List[torch.Tensor]]:
@@ -72,6 +72,60 @@ def allreduce_gradients(params: Sequence[torch.nn.Parameter], group=None, bucket
         torch._foreach_copy_(b, [v.view_as(g) for v, g in zip(torch.split(flat, [g.numel() for g in b]), b)])
         n += 1
     return n
+
+
+class ReplayWatchdog:
+    """Host-side bound on steps that never finish (a collective waiting on a
+    dead or diverged peer hangs the replay, and with it the whole job, with
+    no message).  After every step an event is recorded; once more than
+    ``depth`` steps are in flight the oldest one must complete within
+    ``timeout_s`` or :class:`RuntimeError` names this rank and RCCL's
+    asynchronous error state.  Costs one event record and one query per step
+    (the oldest event is normally long done: the host waits on nothing).
+
+    ``make_event`` / ``clock`` are injectable (CPU tests)."""
+
+    def __init__(self, timeout_s: float, depth: int = 8, describe: Optional[Callable[[], str]] = None,
+                 make_event: Optional[Callable[[], object]] = None, clock=None, sleep=None):
+        import collections
+        import time
+        self.timeout_s, self.depth = float(timeout_s), max(1, int(depth))
+        self.describe = describe or (lambda: '')
+        self._make = make_event or self._cuda_event
+        self._clock = clock or time.monotonic
+        self._sleep = sleep or time.sleep
+        self._q = collections.deque()
+        self.steps = 0
+        self.max_wait_s = 0.0
+
+    @staticmethod
+    def _cuda_event():
+        ev = torch.cuda.Event()
+        ev.record()
+        return ev
+
+    def record(self):
+        self._q.append((self.steps, self._make()))
+        self.steps += 1
+        while len(self._q) > self.depth:
+            self._wait(*self._q.popleft())
+
+    def drain(self):
+        while self._q:
+            self._wait(*self._q.popleft())
+
+    def _wait(self, step, ev):
+        if ev.query():
+            return
+        t0 = self._clock()
+        while not ev.query():
+            waited = self._clock() - t0
+            if waited > self.timeout_s:
+                raise RuntimeError(f'CapturedStep: step {step} did not complete within {self.timeout_s:.0f} s '
+                                   f'({self.steps - step - 1} later steps enqueued behind it); '
+                                   f'{self.describe()}')
+            self._sleep(1e-3)
+        self.max_wait_s = max(self.max_wait_s, self._clock() - t0)
 
 
 class CapturedStep:
@@ -124,6 +178,15 @@ class CapturedStep:
         it.  An input modified in place while held (``x.copy_(batch);
         step(x)``, seen through the tensor's version counter) raises instead
         of training twice on the last batch.
+    watchdog_s: a :class:`ReplayWatchdog` bound on each step's completion,
+        checked once ``watchdog_depth`` later steps are enqueued: a step
+        (collective) that hangs raises with the rank and RCCL's asynchronous
+        error instead of hanging the job.  Default: 300 s when the step
+        all-reduces over more than one rank, off otherwise (0 / None: off).
+    strict: a capture failure raises instead of falling back to eager
+        steps.  Default: on when the step all-reduces over more than one rank
+        (a rank silently stepping eagerly replays its collectives in another
+        form than its peers' graphs).
     split: capture forward+loss and backward+update as two graphs sharing one
         memory pool, so a caller can act between them: ``step(x, mid=fn)``
         runs ``fn()`` after enqueuing the forward (e.g. to gate the next
@@ -145,7 +208,8 @@ class CapturedStep:
                  loss_fn: Callable[[torch.nn.Module, torch.Tensor], torch.Tensor], allreduce=True,
                  warmup: int = 3, graph: bool = True, group=None, bucket_mb: float = 256.0, split: bool = False,
                  comm=None, buckets: bool = True, static_inputs: int = 0, overlap: bool = False,
-                 pair_steps: bool = False, group_steps: int = 1, reuse_distance: int = 2):
+                 pair_steps: bool = False, group_steps: int = 1, reuse_distance: int = 2,
+                 watchdog_s: Optional[float] = -1.0, watchdog_depth: int = 8, strict: Optional[bool] = None):
         self.model, self.opt, self.loss_fn = model, optimizer, loss_fn
         self.split = split
         self.static_inputs = 0 if split else max(0, int(static_inputs))
@@ -213,6 +277,25 @@ class CapturedStep:
                 optimizer.set_grad_scale(1.0 / self.comm.world)   # folded into the update kernel
             else:
                 self._op = 'avg'
+        multi = active and dist.get_world_size(group) > 1
+        self.strict = multi if strict is None else bool(strict)
+        if watchdog_s is not None and watchdog_s < 0:
+            watchdog_s = 300.0 if multi else None
+        self.watchdog = None
+        on_gpu = any(p.is_cuda for p in model.parameters())
+        if watchdog_s and on_gpu:
+            self.watchdog = ReplayWatchdog(watchdog_s, watchdog_depth, describe=self._describe)
+
+    def _describe(self) -> str:
+        rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+        world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        err = ''
+        if self.comm is not None:
+            try:
+                err = self.comm.async_error()
+            except Exception as e:     # (the report must not hide the hang)
+                err = f'<async_error failed: {e}>'
+        return f'rank {rank}/{world}, state {self.state!r}, RCCL async error: {err or "none"}'
 
     def _forward(self, x):
         if self.grads is not None:
@@ -300,6 +383,8 @@ class CapturedStep:
         except RuntimeError as e:          # keep the run alive; callers report which mode ran
             self.error = str(e)
             self.state = 'eager'
+            if self.strict:
+                raise RuntimeError(f'CapturedStep: capture failed ({self._describe()}): {e}') from e
 
     def _same_layout(self, x):
         return (x.shape == self.x.shape and x.stride() == self.x.stride() and x.dtype == self.x.dtype
@@ -438,6 +523,11 @@ class CapturedStep:
             loss = self._call(x, mid)
         finally:
             ran, self._ran = self._ran, None
+        if self.watchdog is not None and ran:
+            self.watchdog.record()
+        from .. import ops
+        if ops.GRID_BARRIER_USED:
+            ops.check_grid_barrier()   # a replayed BN-applying forward whose barrier gave up raises here
         if not ran and loss is not None:
             ran = [loss]
         if ran:

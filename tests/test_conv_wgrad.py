@@ -66,6 +66,30 @@ def test_wgrad_matches_fp32_reference(dev, N, Cin, H, W, Cout, layout, wgrad_sta
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('ordered', [1, 0], ids=['ordered', 'atomic'])
+@pytest.mark.parametrize('N,Cin,H,W,Cout', [(8, 4, 480, 640, 32), (8, 32, 240, 320, 64), (8, 64, 120, 160, 128),
+                                            (1, 128, 60, 64, 256), (3, 32, 10, 66, 64)])
+def test_wgrad_slice_reduce_modes(dev, N, Cin, H, W, Cout, ordered):
+    """Both slice reduces (ordered, the default: bit-identical run to run;
+    atomic groups: BT_WGRAD_ORDERED=0) against the fp32 reference, over the
+    disc step's slice counts (first layer: 512 slices, 32 lanes per element
+    group), and the ordered one twice for bit-identity."""
+    g = torch.Generator(device=dev).manual_seed(Cin + W)
+    cl = torch.channels_last
+    x = torch.randn(N, Cin, H, W, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    dy = torch.randn(N, Cout, H // 2, W // 2, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    ops.hip_ext().conv_set_wgrad_ordered(ordered)
+    try:
+        outs = [ops.conv_wgrad(x, dy, torch.full((Cout, Cin, 4, 4), float('nan'), device=dev)) for _ in range(2)]
+    finally:
+        ops.hip_ext().conv_set_wgrad_ordered(-1)
+    ref = _ref(x, dy, Cout)
+    torch.testing.assert_close(outs[0], ref, rtol=1e-3, atol=1e-4 * float(ref.abs().max()))
+    if ordered:
+        assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.gpu
 def test_wgrad_asymmetric_operands(dev, wgrad_staging, wgrad_pipe):
     """Structured (non-random) operands: a transposed or mis-swizzled tile
     cannot pass by symmetry."""
@@ -588,9 +612,16 @@ def test_conv_applies_its_output_bn(dev, shape):
         lb.backward()
         torch.cuda.synchronize()
         assert ops.conv_grid_barrier_timeouts() == t0
-        torch.testing.assert_close(la, lb, rtol=0, atol=0)
+        ops.check_grid_barrier()
+        # the BN sums are fp64 atomics whose arrival order differs between the two paths (and
+        # from run to run): equal up to 1 float ulp once rounded to the fp32 buffers / loss
+        ulp = dict(rtol=1.2e-7, atol=1e-30)
+        torch.testing.assert_close(la, lb, rtol=1e-6, atol=1e-30)   # (ulps of the stats, propagated)
         for (n, ba), bb in zip(a.named_buffers(), b.buffers()):
-            torch.testing.assert_close(ba, bb, rtol=0, atol=0, msg=n)
+            if ba.is_floating_point():
+                torch.testing.assert_close(ba, bb, **ulp, msg=n)
+            else:
+                torch.testing.assert_close(ba, bb, rtol=0, atol=0, msg=n)
         # the same backward inputs bit for bit: the gradients differ only by the float atomics'
         # order of the weight-gradient reduces (small layers: a few large cancelling partials)
         for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
@@ -965,3 +996,29 @@ def test_dgrad_wgrad_kernel_matches_separate_launches(dev, cin, cout, hw):
     torch.testing.assert_close(outs[1][1], outs[0][1], rtol=1e-5, atol=1e-5 * float(outs[0][1].abs().max()))
     ref = torch.nn.grad.conv2d_weight(x.float(), (cout, cin, 4, 4), dy.float(), stride=2, padding=1)
     torch.testing.assert_close(outs[1][1], ref, rtol=1e-3, atol=1e-3 * float(ref.abs().max()))
+
+
+@pytest.mark.gpu
+def test_grid_barrier_failure_raises(dev):
+    """a grid barrier that gives up must not train on
+    incomplete BN statistics silently.  The kernel raises a host-mapped flag;
+    ops.check_grid_barrier and every CapturedStep call raise on it."""
+    from blendtorch.parallel.step import CapturedStep
+    ops._grid_barrier_armed()                 # maps the flag (as the first BN-applying launch does)
+    assert ops.GRID_BARRIER_USED
+    assert ops.hip_ext().conv_grid_barrier_failed() == 0
+    ops.check_grid_barrier()
+    net = torch.nn.Linear(4, 1).to(dev)
+    opt = torch.optim.SGD(net.parameters(), lr=0.1)
+    step = CapturedStep(net, opt, lambda m, x: m(x).square().mean(), allreduce=False, graph=False)
+    step(torch.ones(2, 4, device=dev))
+    ops.clear_grid_barrier(_simulate_failure=True)
+    try:
+        with pytest.raises(ops.GridBarrierError, match='grid barrier timed out'):
+            step(torch.ones(2, 4, device=dev))
+        with pytest.raises(ops.GridBarrierError):
+            ops.check_grid_barrier()
+    finally:
+        ops.clear_grid_barrier()
+    ops.check_grid_barrier()
+    step(torch.ones(2, 4, device=dev))

@@ -296,3 +296,68 @@ def test_device_comm_refuses_a_destroyed_process_group(monkeypatch):
     assert commmod._nonblocking()
     monkeypatch.setenv('TORCH_NCCL_USE_COMM_NONBLOCKING', '0')
     assert not commmod._nonblocking()
+
+
+class _FakeEvent:
+    def __init__(self, done_after):
+        self.n = done_after
+
+    def query(self):
+        self.n -= 1
+        return self.n < 0
+
+
+def test_replay_watchdog_passes_finished_steps():
+    """Events that complete (at once or after a few polls) never raise; the
+    queue keeps at most ``depth`` steps in flight."""
+    from blendtorch.parallel.step import ReplayWatchdog
+    now = [0.0]
+    wd = ReplayWatchdog(5.0, depth=3, make_event=lambda: _FakeEvent(2), clock=lambda: now[0],
+                        sleep=lambda s: now.__setitem__(0, now[0] + s))
+    for _ in range(10):
+        wd.record()
+        assert len(wd._q) <= 3
+    wd.drain()
+    assert wd.steps == 10 and not wd._q and wd.max_wait_s < 5.0
+
+
+def test_replay_watchdog_names_the_rank_of_a_hung_step():
+    """a replay that hangs on a collective raises with the
+    rank and RCCL's asynchronous error instead of hanging the job."""
+    from blendtorch.parallel.step import ReplayWatchdog
+    now = [0.0]
+    wd = ReplayWatchdog(2.0, depth=2, describe=lambda: 'rank 3/8, RCCL async error: unhandled system error',
+                        make_event=lambda: _FakeEvent(10 ** 9), clock=lambda: now[0],
+                        sleep=lambda s: now.__setitem__(0, now[0] + 0.25))
+    wd.record()
+    wd.record()
+    with pytest.raises(RuntimeError, match=r'step 0 did not complete within 2 s .*rank 3/8.*unhandled system error'):
+        wd.record()
+
+
+def test_captured_step_strict_capture_and_watchdog_defaults(monkeypatch):
+    """world > 1 all-reducing steps: strict capture (no silent eager fallback)
+    and a watchdog by default; a 1-rank step keeps both off.  A strict step
+    whose capture fails raises with the rank in the message."""
+    import torch.distributed as dist
+    from blendtorch.parallel import step as stepmod
+    net = torch.nn.Linear(4, 1)
+    opt = torch.optim.SGD(net.parameters(), lr=0.1)
+    s1 = stepmod.CapturedStep(net, opt, lambda m, x: m(x).sum(), allreduce=False, graph=False)
+    assert not s1.strict and s1.watchdog is None
+    s2 = stepmod.CapturedStep(net, opt, lambda m, x: m(x).sum(), allreduce=False, graph=False, strict=True)
+    assert s2.strict
+    s2.state = 'pending'
+
+    def _graph(*a, **k):
+        raise RuntimeError('operation not permitted when stream is capturing')
+    fake_stream = type('S', (), {'wait_stream': lambda *a: None})
+    monkeypatch.setattr(torch.cuda, 'Stream', lambda *a, **k: fake_stream())
+    monkeypatch.setattr(torch.cuda, 'current_stream', lambda *a, **k: fake_stream())
+    monkeypatch.setattr(torch.cuda, 'stream', lambda s: __import__('contextlib').nullcontext())
+    monkeypatch.setattr(torch.cuda, 'CUDAGraph', lambda *a, **k: object())
+    monkeypatch.setattr(torch.cuda, 'graph', _graph)
+    with pytest.raises(RuntimeError, match=r'capture failed \(rank 0/1'):
+        s2._capture(torch.ones(2, 4))
+    assert s2.state == 'eager'
+    assert not dist.is_initialized()
