@@ -2720,6 +2720,226 @@ __global__ __launch_bounds__(kThreads) void dgrad_patch_kernel(TapGemm p) {
   dgrad_patch_body(p, smem, int(blockIdx.x));
 }
 
+// ---------------------------------------------------------------------------
+// The 32 -> 64 channel forward (the disc's conv2: 8 x 240 x 320 x 32 in,
+// 120 x 160 x 64 out) as a PERSISTENT PATCH GEMM.  The tap GEMM gathers an
+// im2col A tile per k-step through LDS-DMA (a stride-2 4x4 window stages every
+// input pixel 4x) and re-stages the weights in every block: 192 KB of LDS fills
+// per 128-pixel tile.  Those fills -- ~65 GB/s per CU from L2
+// (MI355X_MICROARCH.md, 'gather into LDS') -- set the tap GEMMs' time, not the
+// MFMAs (profiles/r6/disc_roofline.md).  Here one block per CU keeps all 64 KB
+// of weights in LDS for the whole launch and walks its share of 4 x 32-pixel
+// output tiles, staging each tile's (10 x 66)-pixel input patch ONCE (42 KB,
+// double-buffered: the next tile's patch lands while this one computes) --
+// 42 KB of fills per tile instead of 192, and no grid tail of a second wave of
+// blocks (1,200 tiles over 256 persistent blocks).
+//
+// Patch layout: the 66 columns split by parity into two 33-pixel lines per
+// row, pixel u = (row * 2 + parity) * 33 + col / 2, 64 bytes each with chunk q
+// at slot q ^ ((u >> 1) & 3): the 16 pixels of an MFMA B fragment (output
+// columns b..b+15 -> input columns 2b + kw, one parity) are 16 consecutive u
+// and, in ds_read_b128's lane groups, on distinct 16-byte bank slots
+// (/tmp-free model: scripts/lds_banks.py's groups).  Weights: row co (1 KB:
+// 16 taps x 32 ci), chunk kc at kc ^ key(co) (dpw_off's key).  MFMA A = the
+// weights (rows: channels in c1_row_chan order, so a lane's accumulators are 8
+// consecutive channels of one pixel: 16-byte stores), B = patch pixels, K =
+// one tap's 32 channels in tap order 0..15 -- the tap GEMM's accumulation
+// order, the same bf16 output bit for bit.  BN sums (accumulator, acc_r > 0)
+// stay in registers across the block's tiles: one fp64 add per channel per block.
+constexpr int FP_CIN = 32, FP_COUT = 64;
+constexpr int FP_TA = 4, FP_TB = 32;                  // output rows (one per wave) x columns per tile
+constexpr int FP_PR = 2 * FP_TA + 2;                  // 10 patch rows
+constexpr int FP_PL = FP_TB + 1;                      // 33 pixels per parity line
+constexpr int FP_NPIX = FP_PR * 2 * FP_PL;            // 660 patch pixels of 64 bytes
+constexpr int FP_PIECES = 44;                         // 1 KiB LDS-DMA pieces per patch: 11 per wave
+constexpr int FP_PPW = FP_PIECES / 4;
+constexpr int FP_PATCH = FP_PIECES * 1024;            // 45,056 bytes (41.25 KiB of pixels)
+constexpr int FP_W = FP_COUT * 16 * FP_CIN * 2;       // 65,536 bytes
+constexpr int kFwdPatchLds = FP_W + 2 * FP_PATCH + 4 * 2 * FP_COUT * 4;   // 157,696 bytes: one block per CU
+static_assert(FP_NPIX * 64 <= FP_PATCH && kFwdPatchLds <= 163840, "patch GEMM LDS");
+__device__ __forceinline__ int fp_off(int u, int q) { return u * 64 + ((q ^ ((u >> 1) & 3)) << 4); }
+__device__ __forceinline__ int fpw_key(int co) { return (co & 3) | (((co >> 3) & 3) << 2); }
+
+__global__ __launch_bounds__(kThreads) void conv_fwd_patch_kernel(TapGemm p, int ntiles) {
+  __shared__ __attribute__((aligned(16))) char smem[kFwdPatchLds];
+  char* const wl = smem;
+  char* const pb = smem + FP_W;
+  float* const red = reinterpret_cast<float*>(smem + FP_W + 2 * FP_PATCH);
+  const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6, g = lane >> 4, lb = lane & 15;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const int tb = (p.OW + FP_TB - 1) / FP_TB, ta = (p.OH + FP_TA - 1) / FP_TA;
+  const int G = int(gridDim.x), first = int(blockIdx.x);
+  const int mine = first < ntiles ? (ntiles - 1 - first) / G + 1 : 0;
+  const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(p.src, int64_t(p.N) * p.SH * p.SW * FP_CIN * 2);
+  const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(p.w, int64_t(FP_W));
+  const __amdgpu_buffer_rsrc_t rs_y = make_rsrc(p.dst, int64_t(p.N) * p.OH * p.OW * FP_COUT * 2);
+  typedef __attribute__((address_space(3))) void lds_void;
+
+  // the weights, once: wave piece co = wv + 4 m; lane l lands at physical chunk l = logical l ^ key(co)
+#pragma unroll
+  for (int m = 0; m < FP_COUT / 4; ++m) {
+    const int co = wv + 4 * m;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w, (lds_void*)(wl + co * 1024), 16,
+                                             co * 1024 + ((lane ^ fpw_key(co)) << 4), 0, 0, 0);
+  }
+  // this lane's patch pieces (tile-invariant): piece k = wv + 4 i, LDS byte 1024 k + 16 lane = pixel u,
+  // physical slot lane & 3 = logical chunk q; patch row pr, column pc, byte offset from the patch origin
+  int prow[FP_PPW], pcol[FP_PPW], prel[FP_PPW];
+#pragma unroll
+  for (int i = 0; i < FP_PPW; ++i) {
+    const int u = (wv + 4 * i) * 16 + (lane >> 2);
+    const int q = (lane & 3) ^ ((u >> 1) & 3);
+    const int r = u / (2 * FP_PL), rem = u - r * (2 * FP_PL);
+    const int pa = rem >= FP_PL ? 1 : 0, c = 2 * (rem - pa * FP_PL) + pa;
+    prow[i] = u < FP_NPIX ? r : -1000;   // past the patch: never in range (zeros into the padding)
+    pcol[i] = c;
+    prel[i] = (r * p.SW + c) * (FP_CIN * 2) + q * 16;
+  }
+  auto tile_of = [&](int i, int& n, int& a0, int& b0) {
+    const int T = first + i * G;
+    n = T / (ta * tb);
+    const int rem = T - n * (ta * tb);
+    a0 = (rem / tb) * FP_TA;
+    b0 = (rem - (rem / tb) * tb) * FP_TB;
+  };
+  auto issue = [&](int i) {
+    int n, a0, b0;
+    tile_of(i, n, a0, b0);
+    const int y0 = 2 * a0 - 1, x0 = 2 * b0 - 1;
+    const int base = ((n * p.SH + y0) * p.SW + x0) * (FP_CIN * 2);   // (negative at the top-left border)
+    char* const dst = pb + (i & 1) * FP_PATCH;
+#pragma unroll
+    for (int k = 0; k < FP_PPW; ++k) {
+      const bool ok = unsigned(y0 + prow[k]) < unsigned(p.SH) && unsigned(x0 + pcol[k]) < unsigned(p.SW);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_x, (lds_void*)(dst + (wv + 4 * k) * 1024), 16,
+                                               int(ok ? uint32_t(base + prel[k]) : kOOB), 0, 0, 0);
+    }
+  };
+  // MFMA operand offsets (tile-invariant).  Weights: fragment f's row co, chunk (4 kw + g) ^ key at
+  // tap (kh, kw) = chunk 16 kh + that: offset wo[f][kw] + 256 kh.  Patch: pixel u of tap (kh, kw),
+  // fragment j: row 2 wave + kh, parity kw & 1, column 16 j + lb + kw / 2.
+  int wo[4][4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    const int co = c1_row_chan(f, lb);
+#pragma unroll
+    for (int kw = 0; kw < 4; ++kw) wo[f][kw] = co * 1024 + (((4 * kw + g) ^ fpw_key(co)) << 4);
+  }
+  int po[16][2];
+#pragma unroll
+  for (int tap = 0; tap < 16; ++tap)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int kh = tap >> 2, kw = tap & 3;
+      po[tap][j] = fp_off(((2 * wave + kh) * 2 + (kw & 1)) * FP_PL + 16 * j + lb + (kw >> 1), g);
+    }
+  const bool stats = p.stats != nullptr;
+  float sm[2][8], sq[2][8];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sm[q][e] = sq[q][e] = 0.f;
+
+  constexpr uint32_t kWaitAll = (7u << 4) | (0xFu << 8);   // vmcnt(0), no lgkm / exp wait
+  constexpr uint32_t kWaitP = kWaitAll | uint32_t(FP_PPW);                 // the next patch's pieces out
+  constexpr uint32_t kWaitPS = kWaitAll | uint32_t((FP_PPW + 4) & 15) | (uint32_t((FP_PPW + 4) >> 4) << 14);
+  constexpr uint32_t kWaitS = kWaitAll | 4u;                                // the last tile's 4 stores out
+  if (mine > 0) issue(0);
+  for (int i = 0; i < mine; ++i) {
+    const bool next = i + 1 < mine;
+    if (next) issue(i + 1);
+    asm volatile("" ::: "memory");
+    // this tile's pieces are older than everything but the previous tile's 4 stores and the next pieces
+    if (i == 0) {
+      if (next) __builtin_amdgcn_s_waitcnt(kWaitP);
+      else __builtin_amdgcn_s_waitcnt(kWaitAll);
+    } else {
+      if (next) __builtin_amdgcn_s_waitcnt(kWaitPS);
+      else __builtin_amdgcn_s_waitcnt(kWaitS);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const char* const P = pb + (i & 1) * FP_PATCH;
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tap = 0; tap < 16; ++tap) {
+      bf16x8 wa[4], bm[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bm[j] = *reinterpret_cast<const bf16x8*>(P + po[tap][j]);
+#pragma unroll
+      for (int f = 0; f < 4; ++f) wa[f] = *reinterpret_cast<const bf16x8*>(wl + wo[f][tap & 3] + 256 * (tap >> 2));
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[f], bm[j], acc[f][j], 0, 0, 0);
+    }
+    // epilogue: pixel (a0 + wave, b0 + 16 j + lb), channels 32 q + 8 g .. + 7; 4 buffer stores per wave
+    // always (out-of-range lanes store nowhere), so the wait counts above hold
+    int n, a0, b0;
+    tile_of(i, n, a0, b0);
+    const int a = a0 + wave;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int b = b0 + 16 * j + lb;
+      const bool ok = a < p.OH && b < p.OW;
+      const uint32_t ob = uint32_t(((n * p.OH + a) * p.OW + b) * FP_COUT + 8 * g) * 2u;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        uint32_t pk[4];
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {   // channels 8 g + 2 h, + 1: fragment 2 q + (h >> 1), rows 2 (h & 1), + 1
+          const f32x4& av = acc[2 * q + (h >> 1)][j];
+          const f32x2 pr = {av[2 * (h & 1)], av[2 * (h & 1) + 1]};
+          pk[h] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2));   // RNE
+        }
+        const u32x4 v = {pk[0], pk[1], pk[2], pk[3]};
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs_y, int(ok ? ob + uint32_t(64 * q) : kOOB), 0, 0);
+        if (stats && ok) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float x = __uint_as_float(e & 1 ? pk[e >> 1] & 0xFFFF0000u : pk[e >> 1] << 16);
+            sm[q][e] += x;
+            sq[q][e] += x * x;
+          }
+        }
+      }
+    }
+    asm volatile("" ::: "memory");
+    __syncthreads();   // every wave is done with patch buffer i & 1 before tile i + 2 is issued into it
+  }
+  if (!stats) return;
+  // the 16 lanes of a group hold the same channels; then the 4 waves through LDS; one fp64 add per
+  // channel per block into replica blockIdx % acc_r of the accumulator [acc_r][2][64]
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) sm[q][e] += __shfl_xor(sm[q][e], o), sq[q][e] += __shfl_xor(sq[q][e], o);
+  if (lb == 0) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(wave * 2 + 0) * FP_COUT + 32 * q + 8 * g + e] = sm[q][e];
+        red[(wave * 2 + 1) * FP_COUT + 32 * q + 8 * g + e] = sq[q][e];
+      }
+  }
+  __syncthreads();
+  if (t < 2 * FP_COUT) {
+    const int which = t / FP_COUT, c = t - which * FP_COUT;
+    float v = 0.f;
+#pragma unroll
+    for (int w4 = 0; w4 < 4; ++w4) v += red[(w4 * 2 + which) * FP_COUT + c];
+    unsafeAtomicAdd(reinterpret_cast<double*>(p.stats) + ((first % p.acc_r) * 2 + which) * FP_COUT + c, double(v));
+  }
+}
+
 // several weights at once (blockIdx.y = tensor): the data gradients' operands for every layer in one launch
 __global__ __launch_bounds__(kThreads) void weight_t_multi_kernel(WeightTParams p) {
   const int k = int(blockIdx.y);
@@ -3183,6 +3403,25 @@ int conv1_bn_resident() {
 int64_t conv1_tiles_of(int N, int Ho, int Wo, int tr) {
   return int64_t(N) * ((Ho + tr - 1) / tr) * ((Wo + kC1Cols - 1) / kC1Cols);
 }
+// the 32 -> 64 forward as the persistent patch GEMM (conv_fwd_patch_kernel); BT_CONV_FWD_PATCH=0: the tap GEMM
+int g_fwd_patch = -1;
+bool fwd_patch() {
+  if (g_fwd_patch < 0) {
+    const char* v = std::getenv("BT_CONV_FWD_PATCH");
+    g_fwd_patch = v && v[0] == '0' ? 0 : 1;
+  }
+  return g_fwd_patch == 1;
+}
+int device_cus() {
+  static int cus = 0;
+  if (cus <= 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+        hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
 // BT_CONV_OUT_BN=0: the tap-GEMM forward never applies its output's BN
 bool g_out_bn = !(std::getenv("BT_CONV_OUT_BN") && std::getenv("BT_CONV_OUT_BN")[0] == '0');
 // blocks of the BN-applying tap-GEMM forward (64-channel tiles, 2 LDS-DMA stages) resident at once
@@ -3258,6 +3497,8 @@ int conv_grid_barrier_failed() {   // no HIP call: a plain read of the host-mapp
 void conv_grid_barrier_clear(int value) {   // value != 0: simulate a failure (tests)
   if (g_barrier_host_flag) *g_barrier_host_flag = unsigned(value);
 }
+
+void conv_set_fwd_patch(int on) { g_fwd_patch = on < 0 ? -1 : (on ? 1 : 0); }
 
 void conv_set_conv1_tiles(int tiles, int rows) {   // tiles: > 0 patch kernel, -1 the tap-GEMM path, 0 default
   g_conv1_tiles = tiles;
@@ -3378,6 +3619,16 @@ hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream) {
     else BT_CONV1(32, 2);
 #undef BT_CONV1
     return hipGetLastError();
+  }
+  if (p.Cin == FP_CIN && p.Cout == FP_COUT && fwd_patch() && !p.act.on() && !p.act_out && (!p.stats || g.acc_r > 0)) {
+    // the persistent patch GEMM: one block per CU (its LDS), each walking a share of the tiles
+    const int64_t ntiles = int64_t(p.N) * ((p.Ho + FP_TA - 1) / FP_TA) * ((p.Wo + FP_TB - 1) / FP_TB);
+    if (ntiles < (int64_t(1) << 30)) {
+      const int cus = device_cus();
+      const unsigned blocks = unsigned(ntiles < cus ? ntiles : cus);
+      conv_fwd_patch_kernel<<<blocks, kThreads, 0, stream>>>(g, int(ntiles));
+      return hipGetLastError();
+    }
   }
   launch_tap_gemm<false>(g, 1, stream);
   return hipGetLastError();

@@ -377,6 +377,7 @@ bool conv_wgrad_supported(int Cin, int Cout);
 int conv_wgrad_slices(int64_t M, int Cin, int Cout, int target_blocks);
 // Weight-gradient staging (not the 4-channel layer): 0 = register ring,
 // 2 / 3 = LDS-DMA stages of 64 pixels (default 0; -1 = BT_WGRAD_STAGING or default).
+void conv_set_fwd_patch(int on);       // 1 the 32->64 forward's persistent patch GEMM, 0 the tap GEMM, -1 env
 void conv_set_wgrad_ordered(int on);   // 1 ordered (deterministic) slice reduce, 0 atomic groups, -1 env
 void conv_set_wgrad_staging(int staging);
 // Register-staged weight gradient: 1 = read the next step's fragments while this step's MFMAs run

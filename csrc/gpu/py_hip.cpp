@@ -334,6 +334,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("conv_set_tiles", &conv_set_tiles, py::arg("bm") = 0, py::arg("bn") = 0, py::arg("staging") = -1,
         py::arg("dgrad_cls") = 0);
   m.def("conv_dgrad_classes_per_block", &conv_dgrad_classes_per_block);
+  m.def("conv_set_fwd_patch", &conv_set_fwd_patch);
   m.def("conv_set_wgrad_ordered", &conv_set_wgrad_ordered);
   m.def("conv_set_wgrad_staging", &conv_set_wgrad_staging);
   m.def("conv_set_wgrad_pipe", &conv_set_wgrad_pipe);

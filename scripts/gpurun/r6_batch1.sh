@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 6, GPU session 1: the whole GPU suite (ordered slice reduce, grid-barrier flag, graph
+# Round 6, GPU session 1: the whole GPU suite (persistent patch forward for conv2, ordered slice reduce, grid-barrier flag, graph
 # all-reduce self-check, determinism), smoke(), headline bench (2000 steps and a 20-step
 # driver-like run with the sustained window), disc ordered vs atomic reduce, the disc step
 # with a 1-rank RCCL group (self-check incl. the captured all-reduce stage), the 8-rank gloo
@@ -20,7 +20,7 @@ timeout -k 10 300 python bench.py > $O/bench_default.log 2>&1 || { tail -5 $O/be
 grep '^{' $O/bench_default.log | tee $O/bench_default.jsonl | cut -c1-300
 timeout -k 10 300 python bench.py --steps 20 --warmup 10 > $O/bench_20.log 2>&1 || { tail -5 $O/bench_20.log; exit 1; }
 grep '^{' $O/bench_20.log | tee $O/bench_20.jsonl | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'v20':d['value'],'backlog':d['backlog_covers_window'],'sustained':d['sustained']}))"
-for v in "ordered:" "atomic:BT_WGRAD_ORDERED=0" "ordered:" "atomic:BT_WGRAD_ORDERED=0"; do
+for v in "default:" "nopatch:BT_CONV_FWD_PATCH=0" "atomic:BT_WGRAD_ORDERED=0" "default:" "nopatch:BT_CONV_FWD_PATCH=0" "atomic:BT_WGRAD_ORDERED=0"; do
   name=${v%%:*}; e=${v#*:}
   timeout -k 10 200 env $e python bench.py --consumer disc --steps 2000 > $O/disc.log 2>&1 || { tail -5 $O/disc.log; exit 1; }
   grep '^{' $O/disc.log | tee -a $O/disc_$name.jsonl | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'v':'$name','disc':d['value'],'ms':d['ms_per_step']}))"

@@ -1022,3 +1022,38 @@ def test_grid_barrier_failure_raises(dev):
         ops.clear_grid_barrier()
     ops.check_grid_barrier()
     step(torch.ones(2, 4, device=dev))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('N,H,W', [(8, 240, 320), (2, 30, 40), (3, 10, 66), (1, 18, 130)])
+def test_fwd_patch_gemm_matches_tap_gemm(dev, N, H, W):
+    """The 32 -> 64 forward's persistent patch GEMM (conv_fwd_patch_kernel)
+    against the tap GEMM: the same tap order, so the bf16 output is bit for
+    bit the same; the accumulator's BN sums agree to fp32 rounding (summed in
+    another order), and both match an fp32 conv2d.  Shapes with partial
+    tiles (rows and columns) included."""
+    cl = torch.channels_last
+    g = torch.Generator(device=dev).manual_seed(H + W)
+    x = torch.randn(N, 32, H, W, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    w = (0.1 * torch.randn(64, 32, 4, 4, device=dev, generator=g)).to(torch.bfloat16).contiguous(memory_format=cl)
+    ext = ops.hip_ext()
+    out = {}
+    for on in (1, 0):
+        acc = ops.BnAccumulator(64, dev)
+        ext.conv_set_fwd_patch(on)
+        try:
+            y = ops.conv_fwd(x, w, acc.fwd, acc.R)
+            y2 = ops.conv_fwd(x, w)                     # no statistics
+        finally:
+            ext.conv_set_fwd_patch(-1)
+        torch.cuda.synchronize()
+        s = acc.fwd.view(acc.R, 2, 64).sum(0)
+        out[on] = (y, y2, s)
+    assert torch.equal(out[1][0], out[0][0])
+    assert torch.equal(out[1][1], out[0][0])
+    torch.testing.assert_close(out[1][2], out[0][2], rtol=1e-5, atol=1e-3)
+    ref = torch.nn.functional.conv2d(x.float(), w.float(), stride=2, padding=1)
+    torch.testing.assert_close(out[1][0].float(), ref, rtol=2e-2, atol=2e-2)
+    yf = out[1][0].float().permute(0, 2, 3, 1).reshape(-1, 64).double()
+    torch.testing.assert_close(out[1][2][0], yf.sum(0), rtol=1e-5, atol=1e-2)
+    torch.testing.assert_close(out[1][2][1], (yf * yf).sum(0), rtol=1e-5, atol=1e-2)
