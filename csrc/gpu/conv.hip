@@ -2760,7 +2760,8 @@ static_assert(FP_NPIX * 64 <= FP_PATCH && kFwdPatchLds <= 163840, "patch GEMM LD
 __device__ __forceinline__ int fp_off(int u, int q) { return u * 64 + ((q ^ ((u >> 1) & 3)) << 4); }
 __device__ __forceinline__ int fpw_key(int co) { return (co & 3) | (((co >> 3) & 3) << 2); }
 
-__global__ __launch_bounds__(kThreads) void conv_fwd_patch_kernel(TapGemm p, int ntiles) {
+// dbg (experiments only; 0 in production): bit 0 no patch fills, bit 1 no MFMAs, bit 2 no stores
+__global__ __launch_bounds__(kThreads) void conv_fwd_patch_kernel(TapGemm p, int ntiles, int dbg) {
   __shared__ __attribute__((aligned(16))) char smem[kFwdPatchLds];
   char* const wl = smem;
   char* const pb = smem + FP_W;
@@ -2805,6 +2806,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_patch_kernel(TapGemm p, int
   auto issue = [&](int i) {
     int n, a0, b0;
     tile_of(i, n, a0, b0);
+    if (dbg & 1) return;
     const int y0 = 2 * a0 - 1, x0 = 2 * b0 - 1;
     const int base = ((n * p.SH + y0) * p.SW + x0) * (FP_CIN * 2);   // (negative at the top-left border)
     char* const dst = pb + (i & 1) * FP_PATCH;
@@ -2868,6 +2870,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_patch_kernel(TapGemm p, int
       for (int j = 0; j < 2; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int tap = 0; tap < 16; ++tap) {
+      if (dbg & 2) break;
       bf16x8 wa[4], bm[2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) bm[j] = *reinterpret_cast<const bf16x8*>(P + po[tap][j]);
@@ -2898,7 +2901,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_patch_kernel(TapGemm p, int
           pk[h] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2));   // RNE
         }
         const u32x4 v = {pk[0], pk[1], pk[2], pk[3]};
-        __builtin_amdgcn_raw_buffer_store_b128(v, rs_y, int(ok ? ob + uint32_t(64 * q) : kOOB), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs_y, int(ok && !(dbg & 4) ? ob + uint32_t(64 * q) : kOOB), 0, 0);
         if (stats && ok) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
@@ -3405,6 +3408,7 @@ int64_t conv1_tiles_of(int N, int Ho, int Wo, int tr) {
 }
 // the 32 -> 64 forward as the persistent patch GEMM (conv_fwd_patch_kernel); BT_CONV_FWD_PATCH=0: the tap GEMM
 int g_fwd_patch = -1;
+int g_fwd_patch_dbg = 0, g_fwd_patch_blocks = 0;   // (experiments: conv_set_fwd_patch)
 bool fwd_patch() {
   if (g_fwd_patch < 0) {
     const char* v = std::getenv("BT_CONV_FWD_PATCH");
@@ -3498,7 +3502,11 @@ void conv_grid_barrier_clear(int value) {   // value != 0: simulate a failure (t
   if (g_barrier_host_flag) *g_barrier_host_flag = unsigned(value);
 }
 
-void conv_set_fwd_patch(int on) { g_fwd_patch = on < 0 ? -1 : (on ? 1 : 0); }
+void conv_set_fwd_patch(int on, int dbg, int blocks) {
+  g_fwd_patch = on < 0 ? -1 : (on ? 1 : 0);
+  g_fwd_patch_dbg = dbg;
+  g_fwd_patch_blocks = blocks;
+}
 
 void conv_set_conv1_tiles(int tiles, int rows) {   // tiles: > 0 patch kernel, -1 the tap-GEMM path, 0 default
   g_conv1_tiles = tiles;
@@ -3624,9 +3632,9 @@ hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream) {
     // the persistent patch GEMM: one block per CU (its LDS), each walking a share of the tiles
     const int64_t ntiles = int64_t(p.N) * ((p.Ho + FP_TA - 1) / FP_TA) * ((p.Wo + FP_TB - 1) / FP_TB);
     if (ntiles < (int64_t(1) << 30)) {
-      const int cus = device_cus();
+      const int cus = g_fwd_patch_blocks > 0 ? g_fwd_patch_blocks : device_cus();
       const unsigned blocks = unsigned(ntiles < cus ? ntiles : cus);
-      conv_fwd_patch_kernel<<<blocks, kThreads, 0, stream>>>(g, int(ntiles));
+      conv_fwd_patch_kernel<<<blocks, kThreads, 0, stream>>>(g, int(ntiles), g_fwd_patch_dbg);
       return hipGetLastError();
     }
   }

@@ -377,7 +377,7 @@ bool conv_wgrad_supported(int Cin, int Cout);
 int conv_wgrad_slices(int64_t M, int Cin, int Cout, int target_blocks);
 // Weight-gradient staging (not the 4-channel layer): 0 = register ring,
 // 2 / 3 = LDS-DMA stages of 64 pixels (default 0; -1 = BT_WGRAD_STAGING or default).
-void conv_set_fwd_patch(int on);       // 1 the 32->64 forward's persistent patch GEMM, 0 the tap GEMM, -1 env
+void conv_set_fwd_patch(int on, int dbg = 0, int blocks = 0);       // 1 the 32->64 forward's persistent patch GEMM, 0 the tap GEMM, -1 env
 void conv_set_wgrad_ordered(int on);   // 1 ordered (deterministic) slice reduce, 0 atomic groups, -1 env
 void conv_set_wgrad_staging(int staging);
 // Register-staged weight gradient: 1 = read the next step's fragments while this step's MFMAs run
@@ -620,5 +620,39 @@ void conv_attach_adam_schedule(const AdamSchedJob& j);
 bool conv_adam_schedule_taken();
 void conv_detach_adam_schedule();
 
+
+// densityopt's gate and S step (dopt.hip): per-iteration control math on the device
+struct DoptParams {
+  const float* logit_real = nullptr;   // [B] discriminator logits of the target batch
+  const float* logit_sim = nullptr;    // [B] ... of the simulated batch (before the D update)
+  const float* logit_s = nullptr;      // [B] ... of the simulated batch after the D update (S step)
+  float* stats = nullptr;              // [2] D_real, D_sim: mean sigmoid(logits)
+  float* gate_d = nullptr;             // [1] D_real - D_sim < threshold
+  float threshold = 0.7f;
+  const int64_t* sid = nullptr;        // [B] global sample ids of the simulated images (device or host-mapped)
+  float* samples = nullptr;            // [2][N] m1, m2 of every rank (read, then the next ones written)
+  float* mean = nullptr;               // [2] ProbModel.m1m2_mean (updated in place)
+  float* log_std = nullptr;            // [2] ProbModel.m1m2_log_std
+  float* exp_avg = nullptr;            // [4] Adam moments of (mean, log_std)
+  float* exp_avg_sq = nullptr;         // [4]
+  float* adam_step = nullptr;          // [1]
+  float lr = 5e-2f, b1 = 0.7f, b2 = 0.999f, eps = 1e-8f;
+  float* b = nullptr;                  // [1] baseline
+  float* first = nullptr;              // [1] 1 until the first S step
+  float* gate_s = nullptr;             // [1]
+  float alpha = 0.9f;
+  float* params_out = nullptr;         // [4] mu1, mu2, std1, std2 after the step
+  float* red = nullptr;                // [5] per-rank means (data parallel: averaged between phases 1 and 2)
+  float* host = nullptr;               // host-mapped [2B + 8]: this rank's samples, params, stats, gates (nullable)
+  uint32_t* counter = nullptr;         // [1] iteration counter of the sampler
+  uint64_t seed = 0;
+  int B = 0, N = 0, rank = 0, world = 1;
+};
+hipError_t dopt_gate(const DoptParams& p, int phase, hipStream_t stream);    // phase 0 all, 1 stats, 2 gate
+// phase 0 all, 1 partials, 2 update, 3 samples only
+hipError_t dopt_sstep(const DoptParams& p, int phase, hipStream_t stream);
+// host-mapped pinned memory (hipHostMalloc mapped + coherent): (host pointer, device pointer)
+void* host_mapped_alloc(size_t bytes, void** dev);
+void host_mapped_free(void* host);
 }  // namespace gpu
 }  // namespace btn

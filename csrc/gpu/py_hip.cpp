@@ -162,6 +162,40 @@ ConvWgradParams::Reduce reduce_from_tuple(const py::tuple& t) {
   return r;
 }
 
+
+// densityopt gate / S step: the parameters as a dict of device pointers (ints) and scalars
+DoptParams dopt_from_dict(const py::dict& d) {
+  DoptParams p;
+  auto ptr = [&](const char* k) -> uintptr_t { return d.contains(k) ? d[k].cast<uintptr_t>() : 0; };
+  auto f32 = [&](const char* k, float dflt) { return d.contains(k) ? d[k].cast<float>() : dflt; };
+  auto i32 = [&](const char* k, int dflt) { return d.contains(k) ? d[k].cast<int>() : dflt; };
+  p.logit_real = reinterpret_cast<const float*>(ptr("logit_real"));
+  p.logit_sim = reinterpret_cast<const float*>(ptr("logit_sim"));
+  p.logit_s = reinterpret_cast<const float*>(ptr("logit_s"));
+  p.stats = reinterpret_cast<float*>(ptr("stats"));
+  p.gate_d = reinterpret_cast<float*>(ptr("gate_d"));
+  p.threshold = f32("threshold", 0.7f);
+  p.sid = reinterpret_cast<const int64_t*>(ptr("sid"));
+  p.samples = reinterpret_cast<float*>(ptr("samples"));
+  p.mean = reinterpret_cast<float*>(ptr("mean"));
+  p.log_std = reinterpret_cast<float*>(ptr("log_std"));
+  p.exp_avg = reinterpret_cast<float*>(ptr("exp_avg"));
+  p.exp_avg_sq = reinterpret_cast<float*>(ptr("exp_avg_sq"));
+  p.adam_step = reinterpret_cast<float*>(ptr("adam_step"));
+  p.lr = f32("lr", 5e-2f), p.b1 = f32("b1", 0.7f), p.b2 = f32("b2", 0.999f), p.eps = f32("eps", 1e-8f);
+  p.b = reinterpret_cast<float*>(ptr("b"));
+  p.first = reinterpret_cast<float*>(ptr("first"));
+  p.gate_s = reinterpret_cast<float*>(ptr("gate_s"));
+  p.alpha = f32("alpha", 0.9f);
+  p.params_out = reinterpret_cast<float*>(ptr("params_out"));
+  p.red = reinterpret_cast<float*>(ptr("red"));
+  p.host = reinterpret_cast<float*>(ptr("host"));
+  p.counter = reinterpret_cast<uint32_t*>(ptr("counter"));
+  p.seed = d.contains("seed") ? d["seed"].cast<uint64_t>() : 0;
+  p.B = i32("B", 0), p.N = i32("N", 0), p.rank = i32("rank", 0), p.world = i32("world", 1);
+  return p;
+}
+
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "blendtorch gfx950 kernels + GPU stream loader";
 
@@ -334,7 +368,20 @@ PYBIND11_MODULE(_hip, m) {
   m.def("conv_set_tiles", &conv_set_tiles, py::arg("bm") = 0, py::arg("bn") = 0, py::arg("staging") = -1,
         py::arg("dgrad_cls") = 0);
   m.def("conv_dgrad_classes_per_block", &conv_dgrad_classes_per_block);
-  m.def("conv_set_fwd_patch", &conv_set_fwd_patch);
+  m.def("conv_set_fwd_patch", &conv_set_fwd_patch, py::arg("on"), py::arg("dbg") = 0, py::arg("blocks") = 0);
+  m.def("dopt_gate", [](const py::dict& d, int phase, uintptr_t stream) {
+    check(dopt_gate(dopt_from_dict(d), phase, reinterpret_cast<hipStream_t>(stream)), "dopt_gate");
+  });
+  m.def("dopt_sstep", [](const py::dict& d, int phase, uintptr_t stream) {
+    check(dopt_sstep(dopt_from_dict(d), phase, reinterpret_cast<hipStream_t>(stream)), "dopt_sstep");
+  });
+  m.def("host_mapped_alloc", [](size_t bytes) {
+    void* dev = nullptr;
+    void* host = host_mapped_alloc(bytes, &dev);
+    if (!host) throw std::runtime_error("host_mapped_alloc: hipHostMalloc(mapped) failed");
+    return py::make_tuple(reinterpret_cast<uintptr_t>(host), reinterpret_cast<uintptr_t>(dev));
+  });
+  m.def("host_mapped_free", [](uintptr_t host) { host_mapped_free(reinterpret_cast<void*>(host)); });
   m.def("conv_set_wgrad_ordered", &conv_set_wgrad_ordered);
   m.def("conv_set_wgrad_staging", &conv_set_wgrad_staging);
   m.def("conv_set_wgrad_pipe", &conv_set_wgrad_pipe);

@@ -118,8 +118,10 @@ def run(args):
             # first MFMA conv reads 8-byte pixels and its weight ignores channel 3
             dec = (DecodeConfig.densityopt(channels=(0, 1, 2, 2), dtype='bfloat16', layout='nhwc') if bf16
                    else DecodeConfig.densityopt(channels='rgb'))
+            # a fixed ring of output tensors: the fused step keeps a sim-half graph per
+            # ring tensor and reads each batch where the loader decoded it (no copy)
             sim = DeviceLoader(bl.launch_info.addresses['DATA'], batch_size=B, device=dev, prefetch=2,
-                               decode=dec, timeoutms=30000)
+                               decode=dec, timeoutms=30000, reuse_buffers=True)
             gen_sim = iter(sim)
         else:
             gen_sim = cpu_stream(bl.launch_info.addresses['DATA'], B)
@@ -154,7 +156,8 @@ def run(args):
                     comm.broadcast_(t, 0)
         if bf16:
             netD = netD.to(memory_format=torch.channels_last)
-        step = DensityOptStep(netD, pm, real, B, comm=comm, bf16=bf16, graph=not args.no_graph)
+        step = DensityOptStep(netD, pm, real, B, comm=comm, bf16=bf16, graph=not args.no_graph,
+                              fused=None if not args.unfused_sstep else False, seed=args.seed)
         pin = dev.type == 'cuda'
         host_samples = torch.empty((2, B), dtype=torch.float32, pin_memory=pin)
         host_params = torch.empty(4, dtype=torch.float32, pin_memory=pin)
@@ -162,7 +165,16 @@ def run(args):
         ids = np.arange(rank * B, (rank + 1) * B)
 
         def fetch():
-            """The one device->host copy per iteration: next samples (+ logging scalars)."""
+            """The one device->host hand-off per iteration: next samples (+ logging scalars).
+            Fused step: its kernel wrote them to host-mapped memory -- wait and read."""
+            if step.fused:
+                torch.cuda.current_stream(dev).synchronize()
+                hs = step.host_state()
+                host_params.copy_(hs['params'])
+                host_stats[:2].copy_(hs['stats'])
+                host_stats[2:3].copy_(hs['gate_d'])
+                host_stats[3:4].copy_(hs['gate_s'])
+                return hs['samples'].numpy().copy()
             mine, _ = step.my_samples()
             host_samples.copy_(mine, non_blocking=pin)
             host_params.copy_(step.params_out, non_blocking=pin)
@@ -271,7 +283,7 @@ def run(args):
         res = {'iterations': epoch, 'seconds': dt, 'iterations_per_s': epoch / dt, 'sim_wait_s': wait_s,
                'images_per_s': epoch * B * world / dt, 'world': world, 'batch_per_rank': B,
                'final_params': history[-1].tolist(), 'target': tgt.tolist(), 'abs_diff': diff.tolist(),
-               'd_steps': d_steps, 's_steps': s_steps, 'graph': step.graph is not None,
+               'd_steps': d_steps, 's_steps': s_steps, 'graph': step.graph is not None, 'fused_sstep': step.fused,
                'dtype': 'bf16' if bf16 else 'fp32', 'collectives': ('rccl-direct' if comm is not None and comm.native
                                                                    else ('gloo' if comm is not None else None))}
         if n_steady:
@@ -321,6 +333,8 @@ def main(argv=None):
     ap.add_argument('--json', default=None)
     ap.add_argument('--fp32', action='store_true', help='fp32 discriminator (PyTorch/MIOpen) instead of bf16 MFMA')
     ap.add_argument('--no-graph', action='store_true', help='eager iterations (no HIP graph)')
+    ap.add_argument('--unfused-sstep', action='store_true',
+                    help='the S step / gates in PyTorch ops (ProbModel + autograd) instead of the gfx950 kernels')
     ap.add_argument('--no-fused-bn', action='store_true',
                     help='discriminator with MIOpen BatchNorm + PyTorch LeakyReLU instead of the fused gfx950 op')
     ap.add_argument('--num-runs', default=1, type=int, help='independent runs (one history file each)')

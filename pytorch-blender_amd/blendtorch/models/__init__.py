@@ -138,7 +138,9 @@ class Discriminator(nn.Module):
     def bce_bf16(self, x, target=1.0, mfma=True, probs=True, decode=None):
         """``(mean BCE loss, per-sample probabilities)`` of the bf16 forward
         (``probs=False``: the fused head's logits are not turned into
-        probabilities -- one kernel fewer when only the loss is used).
+        probabilities -- one kernel fewer when only the loss is used;
+        ``probs='logits'``: the fused head's fp32 logits instead, for a
+        consumer that applies the sigmoid itself).
 
         The fused head applies to the adaptive stack (pool -> conv -> sigmoid)
         and to the plain DCGAN stack whose last conv consumes the whole
@@ -173,6 +175,8 @@ class Discriminator(nn.Module):
                         raise RuntimeError('bce_bf16: the lazily applied BN input is not channels-last')
                     z, link = z.contiguous(memory_format=torch.channels_last), None
                 loss, logits = ops.disc_head_bce(z, head.weight, target, pool, bn_link=link, act=lazy)
+                if probs == 'logits':
+                    return loss, logits
                 return loss, (torch.sigmoid(logits) if probs else None)
             out = self._run_bf16(z, layers[len(body):], mfma)
         else:

@@ -729,7 +729,11 @@ def test_forward_applies_input_bn(dev, cin, cout, hw):
     assert float(acc_in2.fwd.abs().sum()) == 0.0          # cleared by the last block
     assert torch.equal(xa, a)                               # the activation, every element
     assert torch.equal(y, y_ref)
-    torch.testing.assert_close(acc_out2.fwd, s_ref, rtol=1e-9, atol=1e-6)
+    # (the reference forward may be the patch GEMM, whose blocks add into other replicas: compare the
+    # per-channel sums over the replicas)
+    R2 = acc_out2.R
+    torch.testing.assert_close(acc_out2.fwd[:R2 * 2 * cout].view(R2, -1).sum(0),
+                               s_ref[:R2 * 2 * cout].view(R2, -1).sum(0), rtol=1e-6, atol=1e-3)
     for ba, bb in zip(bns[0].buffers(), bns[1].buffers()):
         assert torch.equal(ba, bb)
 
@@ -1047,7 +1051,7 @@ def test_fwd_patch_gemm_matches_tap_gemm(dev, N, H, W):
         finally:
             ext.conv_set_fwd_patch(-1)
         torch.cuda.synchronize()
-        s = acc.fwd.view(acc.R, 2, 64).sum(0)
+        s = acc.fwd[:acc.R * 128].view(acc.R, 2, 64).sum(0)
         out[on] = (y, y2, s)
     assert torch.equal(out[1][0], out[0][0])
     assert torch.equal(out[1][1], out[0][0])

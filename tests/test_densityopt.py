@@ -157,3 +157,35 @@ def test_densityopt_data_parallel_gloo_world2(tmp_path):
     assert res[0]['weights_sha'] == res[1]['weights_sha']
     assert res[0]['final_params'] == res[1]['final_params']
     assert res[0]['d_steps'] == res[1]['d_steps'] and res[0]['s_steps'] == res[1]['s_steps']
+
+
+def test_sstep_reference_matches_probmodel_autograd_cpu():
+    """The fused S step's closed-form gradient (models.densityopt.sstep_reference:
+    the arithmetic of csrc/gpu/dopt.hip's dopt_sstep_kernel) against autograd
+    through the PyTorch ProbModel on the reference's loss
+    ``(log_probs[shape_id] * (errS - b)).mean()`` (densityopt.py:290-300),
+    including out-of-order shape ids and saturated probabilities (the BCE's
+    -100 clamp)."""
+    from blendtorch.models import ProbModel
+    from blendtorch.models.densityopt import sstep_reference
+    g = torch.Generator().manual_seed(3)
+    B, N = 16, 48
+    pm = ProbModel([1.2, 3.0], [0.4, 0.3])
+    with torch.no_grad():
+        pm.m1m2_mean.add_(torch.randn(2, generator=g) * 0.1)
+    torch.manual_seed(5)
+    s = pm.sample(N)
+    samples = torch.stack([s['m1'], s['m2']])
+    sid = torch.randperm(N, generator=g)[:B]
+    logit = torch.randn(B, generator=g) * 3
+    logit[0] = -200.0                                  # log(sigmoid) below -100: clamped
+    b = 0.55
+    out = sstep_reference(logit, sid, samples, pm.m1m2_mean.detach(), pm.m1m2_log_std.detach(), b)
+    p = torch.sigmoid(logit)
+    err = torch.nn.functional.binary_cross_entropy(p, torch.ones_like(p), reduction='none')
+    log_probs = pm.log_prob({'m1': samples[0], 'm2': samples[1]})
+    loss = (log_probs[sid] * (err - b)).mean()
+    loss.backward()
+    torch.testing.assert_close(out[0], err.mean(), rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(out[1:3], pm.m1m2_mean.grad, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(out[3:5], pm.m1m2_log_std.grad, rtol=1e-5, atol=1e-6)

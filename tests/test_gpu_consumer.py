@@ -658,3 +658,136 @@ def test_head_applies_bn_backward(dev, monkeypatch, N, H, W):
     for (n, _), x_, y_ in zip(Discriminator(nc=3, ndf=32, adaptive=True).named_parameters(), ga, gb):
         torch.testing.assert_close(x_, y_, rtol=2e-2, atol=2e-2 * float(y_.abs().max()), msg=n)
     assert int(torch.count_nonzero(ops._head_bn_scratch(dev, N, 256))) == 0   # cleared by the kernel
+
+
+def _dopt_state(dev, B, N, seed=7):
+    from blendtorch.models import ProbModel
+    g = torch.Generator(device=dev).manual_seed(seed)
+    pm = ProbModel([1.2, 3.0], [0.4, 0.3]).to(dev)
+    st = {k: torch.zeros(n, device=dev) for k, n in
+          (('stats', 2), ('gate_d', 1), ('gate_s', 1), ('b', 1), ('first', 1), ('params_out', 4), ('red', 5),
+           ('adam', 9))}
+    st['samples'] = torch.exp(torch.randn(2, N, device=dev, generator=g) * 0.3 + 1.0)
+    st['counter'] = torch.zeros(1, dtype=torch.int32, device=dev)
+    st['logit_s'] = torch.randn(B, device=dev, generator=g) * 2
+    st['logit_real'] = torch.randn(B, device=dev, generator=g) + 1
+    st['logit_sim'] = torch.randn(B, device=dev, generator=g) - 1
+    st['sid'] = torch.randperm(N, device=dev, generator=g)[:B].to(torch.int64)
+    return pm, st
+
+
+def _dopt_kp(pm, st, B, N, rank=0, world=1, seed=11):
+    return dict(samples=st['samples'].data_ptr(), mean=pm.m1m2_mean.data_ptr(), log_std=pm.m1m2_log_std.data_ptr(),
+                exp_avg=st['adam'][0:4].data_ptr(), exp_avg_sq=st['adam'][4:8].data_ptr(),
+                adam_step=st['adam'][8:9].data_ptr(), lr=5e-2, b1=0.7, b2=0.999, eps=1e-8, b=st['b'].data_ptr(),
+                first=st['first'].data_ptr(), gate_s=st['gate_s'].data_ptr(), gate_d=st['gate_d'].data_ptr(),
+                stats=st['stats'].data_ptr(), alpha=0.9, threshold=0.7, params_out=st['params_out'].data_ptr(),
+                red=st['red'].data_ptr(), counter=st['counter'].data_ptr(), seed=seed, B=B, N=N, rank=rank,
+                world=world, logit_s=st['logit_s'].data_ptr(), sid=st['sid'].data_ptr(),
+                logit_real=st['logit_real'].data_ptr(), logit_sim=st['logit_sim'].data_ptr())
+
+
+def test_dopt_kernels_match_reference(dev):
+    """the densityopt gate and S step as gfx950 kernels
+    (csrc/gpu/dopt.hip) against PyTorch: the D statistics / gate, the
+    per-rank means of the fused S step (models.densityopt.sstep_reference,
+    itself pinned to ProbModel autograd on the CPU), the gated Adam update
+    (FusedAdam's reference arithmetic), baseline / first-step bookkeeping,
+    and the Philox resampling: LogNormal moments, bit-identical for the same
+    key and counter, a new draw per iteration."""
+    from blendtorch.models.densityopt import sstep_reference
+    ext = ops.hip_ext()
+    st_ = ops._stream(dev)
+    B, N = 64, 4096
+    pm, st = _dopt_state(dev, B, N)
+    st['b'].fill_(0.6)
+    st['first'].fill_(1.0)
+    kp = _dopt_kp(pm, st, B, N)
+    ext.dopt_gate(kp, 0, st_)
+    torch.cuda.synchronize()
+    dr, ds = torch.sigmoid(st['logit_real']).mean(), torch.sigmoid(st['logit_sim']).mean()
+    torch.testing.assert_close(st['stats'], torch.stack([dr, ds]), rtol=1e-5, atol=1e-6)
+    assert float(st['gate_d']) == float(dr - ds < 0.7)
+    st['gate_d'].fill_(0.0)                      # separated: the first S step runs (gate_s 1)
+    ref = sstep_reference(st['logit_s'], st['sid'], st['samples'], pm.m1m2_mean.detach().clone(),
+                          pm.m1m2_log_std.detach().clone(), 0.6)
+    ext.dopt_sstep(kp, 1, st_)                   # phase 1: the means only
+    torch.cuda.synchronize()
+    torch.testing.assert_close(st['red'], ref, rtol=2e-5, atol=2e-6)
+    p0 = torch.cat([pm.m1m2_mean.detach(), pm.m1m2_log_std.detach()]).clone()
+    old = st['samples'].clone()
+    ext.dopt_sstep(kp, 0, st_)                   # the whole step
+    torch.cuda.synchronize()
+    assert float(st['gate_s']) == 1.0 and float(st['first']) == 0.0 and float(st['adam'][8]) == 1.0
+    torch.testing.assert_close(st['b'], ref[0:1], rtol=2e-5, atol=2e-6)   # first step: b = err mean
+    # Adam, step 1: m = 0.3 g, v = 0.001 g^2 -> p -= lr / 0.3 * m / (sqrt(v) / sqrt(0.001) + eps)
+    g = ref[1:5]
+    m, v = 0.3 * g, 0.001 * g * g
+    want = p0 - (5e-2 / 0.3) * m / (v.sqrt() / (0.001 ** 0.5) + 1e-8)
+    got = torch.cat([pm.m1m2_mean.detach(), pm.m1m2_log_std.detach()])
+    torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(st['params_out'], torch.cat([got[:2], got[2:].exp()]), rtol=1e-6, atol=1e-6)
+    # the new samples: LogNormal(mu, s) moments over N draws, a fresh draw (counter advanced)
+    assert int(st['counter']) == 1 and not torch.equal(st['samples'], old)
+    ls = st['samples'].log()
+    torch.testing.assert_close(ls.mean(1), got[:2], rtol=0, atol=4 * float(got[2:].exp().max()) / N ** 0.5)
+    torch.testing.assert_close(ls.std(1), got[2:].exp(), rtol=0.05, atol=0)
+    # the same key and counter draw the same samples (every rank of a data-parallel run)
+    _, st2 = _dopt_state(dev, B, N)
+    st2['counter'].fill_(0)
+    kp2 = _dopt_kp(pm, st2, B, N)
+    ext.dopt_sstep(kp2, 3, st_)                  # phase 3: samples only, at the parameters now
+    ext.dopt_sstep(kp2, 3, st_)
+    st3 = dict(st2, counter=torch.ones(1, dtype=torch.int32, device=dev), samples=torch.empty_like(st2['samples']))
+    ext.dopt_sstep(_dopt_kp(pm, st3, B, N), 3, st_)
+    torch.cuda.synchronize()
+    assert torch.equal(st3['samples'], st2['samples'])    # counter 1 in both
+    # a skipped S step (not first, gate_s from gate_d = 1 and first = 1 -> 0): nothing moves but the samples
+    st['first'].fill_(1.0)
+    st['gate_d'].fill_(1.0)
+    before = (got.clone(), st['b'].clone(), st['adam'].clone())
+    ext.dopt_sstep(kp, 0, st_)
+    torch.cuda.synchronize()
+    assert float(st['gate_s']) == 0.0
+    assert torch.equal(torch.cat([pm.m1m2_mean.detach(), pm.m1m2_log_std.detach()]), before[0])
+    assert torch.equal(st['b'], before[1]) and torch.equal(st['adam'], before[2])
+
+
+def test_densityopt_fused_host_state_and_static_sims(dev):
+    """The fused DensityOptStep: sim batches read in place from a fixed ring of
+    buffers (one sim-half graph each, no copy), shape ids from host-mapped
+    memory, results in host-mapped memory (host_state) equal to the device
+    tensors, and the same run twice is bit-identical (fixed-order sums, Philox
+    sampler keyed by the seed)."""
+    from blendtorch.models import Discriminator, ProbModel
+    from blendtorch.models.densityopt import DensityOptStep
+    B = 64
+    runs = []
+    for _ in range(2):
+        torch.manual_seed(0)
+        netD = Discriminator().to(dev).to(memory_format=torch.channels_last)
+        pm = ProbModel([1.2, 3.0], [0.4, 0.4]).to(dev)
+        g = torch.Generator(device=dev).manual_seed(2)
+        ring = [(torch.rand(B, 64, 64, 4, device=dev, generator=g) * 2 - 1).to(torch.bfloat16) for _ in range(3)]
+        step = DensityOptStep(netD, pm, ring[0].permute(0, 3, 1, 2).clone(), B, graph=True, warmup=2, seed=5)
+        assert step.fused
+        step.start()
+        torch.cuda.synchronize()
+        assert torch.equal(step.host_state()['samples'], step.samples[:, :B].cpu())
+        sids = torch.Generator().manual_seed(4)
+        hist = []
+        for i in range(8):
+            step(ring[i % 3].permute(0, 3, 1, 2), torch.randperm(B, generator=sids))
+            torch.cuda.synchronize()
+            hs = step.host_state()
+            assert torch.equal(hs['samples'], step.samples[:, :B].cpu())
+            assert torch.equal(hs['params'], step.params_out.cpu())
+            assert torch.equal(hs['stats'], step.stats.cpu())
+            assert float(hs['gate_d']) == float(step.gate_d) and float(hs['gate_s']) == float(step.gate_s)
+            hist.append(hs['params'].clone())
+        assert step.graph is not None and 'copy' not in step._sims and len(step._sims) == 3
+        assert bool(torch.isfinite(step.samples).all()) and bool((step.samples > 0).all())
+        runs.append((torch.stack(hist), [p.detach().clone() for p in netD.parameters()]))
+    assert torch.equal(runs[0][0], runs[1][0])
+    for a, b in zip(runs[0][1], runs[1][1]):
+        assert torch.equal(a, b)
