@@ -134,6 +134,9 @@ def parse_args(argv=None):
     ap.add_argument('--shm', type=int, default=48,
                     help='>0 (default 48): producers render into an N-slot shared-memory ring (same host) and '
                          'send descriptors; 0: images inline in the ZMTP messages')
+    ap.add_argument('--inline-producers', type=int, default=0,
+                    help='with --shm: this many of each rank\'s producers send their images inline in the ZMTP '
+                         'messages instead (a mixed fleet: inline frames land in pinned slots, batches stay direct)')
     ap.add_argument('--codec', choices=['none', 'tile16'], default='none',
                     help='shm frames: none = raw HWC; tile16 = key-frame deltas (the background crosses PCIe once, '
                          'then only the 16x16 tiles that differ from it; csrc/codec/tiledelta.h)')
@@ -384,8 +387,10 @@ def main(argv=None):
                    and args.head == 'fused' and decode.channels == 'rgba' and decode.dtype == 'bfloat16')
     launch = dict(producer='cubesim', num_instances=nprod, named_sockets=['DATA'], start_port=start_port,
                   proto=args.proto, seed=1000 * rank, cpu_affinity=affinity,
-                  instance_args=[['--mode', args.mode, '--sndhwm', '10', '--resolution', f'{res_w}x{res_h}'] + (['--shm', str(shm_slots), '--codec', args.codec] if shm_slots else [])]
-                  * nprod)
+                  instance_args=[['--mode', args.mode, '--sndhwm', '10', '--resolution', f'{res_w}x{res_h}']
+                                 + (['--shm', str(shm_slots), '--codec', args.codec]
+                                    if shm_slots and i >= args.inline_producers else [])
+                                 for i in range(nprod)])
     model = opt = None
     copy_streams = args.copy_streams or (1 if args.consumer == 'disc' else 2)
     # the next frames' DMA starts between the step's forward and backward graphs
@@ -698,6 +703,7 @@ def main(argv=None):
                 'launch_depth': args.launch_depth, 'prefetch': args.prefetch,
                 'copy_streams': copy_streams if args.h2d == 'copy' else None,
                 'codec': args.codec if shm_slots else 'none',
+                'inline_producers': min(nprod, args.inline_producers) if shm_slots else nprod,
                 'consumer_step': stepper.state if stepper is not None else None,
                 'decode_in_step': step_decode,
                 'decode_fused_in_conv': fuse_decode,
@@ -717,7 +723,8 @@ def main(argv=None):
             'sec_per_image': round(tmax / images, 7),
             'sec_per_batch': round(tmax / args.steps, 6),
             'loader_stats': {k: stats.get(k) for k in ('frames', 'batches', 'bad', 'pool_fallbacks', 'direct_batches',
-                                                       'launches', 'shm_frames', 'shm_torn', 'tiled_frames')},
+                                                       'launches', 'shm_frames', 'shm_torn', 'tiled_frames',
+                                                       'staged_frames')},
             # rank 0's loader over the TIMED WINDOW only (snapshots at t0 / t1):
             # device time per image (H2D + decode, sampled launches after the cold
             # start), image bytes host -> device per second (tile16 moves only the

@@ -271,10 +271,15 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_reduce_kernel(ConvWgradPa
 
 namespace {
 AdamSchedJob g_sched_job;     // attached, not yet launched
+int g_sched_device = -1;      // the optimizer's device and stream: the only launches that take it
+hipStream_t g_sched_stream = nullptr;
 bool g_sched_taken = false;   // a launch ran the attached job
-AdamSchedJob take_sched_job() {
+AdamSchedJob take_sched_job(hipStream_t stream) {
+  if (!g_sched_job.step || stream != g_sched_stream) return AdamSchedJob();
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess || dev != g_sched_device) return AdamSchedJob();
   AdamSchedJob j = g_sched_job;
-  if (j.step) g_sched_taken = true;
+  g_sched_taken = true;
   g_sched_job = AdamSchedJob();
   return j;
 }
@@ -2966,8 +2971,9 @@ __global__ __launch_bounds__(kThreads) void weight_t_kernel(const uint16_t* __re
 
 }  // namespace
 
-void conv_attach_adam_schedule(const AdamSchedJob& j) {
+void conv_attach_adam_schedule(const AdamSchedJob& j, int device, hipStream_t stream) {
   g_sched_job = j;
+  g_sched_device = device, g_sched_stream = stream;
   g_sched_taken = false;
 }
 bool conv_adam_schedule_taken() {
@@ -3085,7 +3091,7 @@ int conv_wgrad_slices(int64_t M, int Cin, int Cout, int target_blocks) {
 
 hipError_t conv_wgrad_reduce(const ConvWgradParams::Reduce& r, hipStream_t stream) {
   if (!r.partial || !r.out || r.S <= 0 || r.rx <= 0 || r.ry <= 0) return hipErrorInvalidValue;
-  conv_wgrad_reduce_kernel<<<dim3(unsigned(r.rx), unsigned(r.ry)), kThreads, 0, stream>>>(r, take_sched_job());
+  conv_wgrad_reduce_kernel<<<dim3(unsigned(r.rx), unsigned(r.ry)), kThreads, 0, stream>>>(r, take_sched_job(stream));
   return hipGetLastError();
 }
 
@@ -3281,7 +3287,7 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
     *defer = r;
     return hipGetLastError();
   }
-  conv_wgrad_reduce_kernel<<<dim3(unsigned(r.rx), unsigned(r.ry)), kThreads, 0, stream>>>(r, take_sched_job());
+  conv_wgrad_reduce_kernel<<<dim3(unsigned(r.rx), unsigned(r.ry)), kThreads, 0, stream>>>(r, take_sched_job(stream));
   return hipGetLastError();
 }
 

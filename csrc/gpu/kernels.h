@@ -160,7 +160,22 @@ struct Color4x4Params {
   int B = 0, H = 0, W = 0, Cout = 4;
   int flip_all = 0;
   uint64_t flip_bits[4] = {0, 0, 0, 0};
+  // Per-image transforms (photometric augmentation), by mat_mode:
+  //   kColorOne     one matrix for every image (M, bias)
+  //   kColorPos     Ms + 20 * mat_pos[b]  (16 matrix + 4 bias floats; B <= kMaxSrcs)
+  //   kColorEach    Ms + 20 * b
+  //   kColorJitter  built in the kernel from jit[b] = (brightness, contrast,
+  //                 saturation, hue in turns) about `pivot` (B <= kMaxSrcs):
+  //                 rgb' = bc * (Hue(h) . Sat(s)) rgb + (1 - c) * pivot, alpha kept,
+  //                 Sat(s) = s I + (1 - s) 1 w^T and Hue the rotation about the grey
+  //                 axis with luminance w = (0.213, 0.715, 0.072) (ops.color_jitter_matrix)
+  int mat_mode = 0;
+  const float* Ms = nullptr;
+  uint8_t mat_pos[kMaxSrcs] = {};
+  float jit[kMaxSrcs][4] = {};
+  float pivot = 0.5f;
 };
+enum { kColorOne = 0, kColorPos = 1, kColorEach = 2, kColorJitter = 3 };
 hipError_t color4x4(const Color4x4Params& p, hipStream_t stream);
 
 // Batched pinhole projection (btb.Camera.world_to_ndc + ndc_to_pixel):
@@ -616,7 +631,9 @@ struct AdamSchedJob {
   float beta1 = 0.f, beta2 = 0.f;
   const float* gate = nullptr;  // optional: 0 closes the step
 };
-void conv_attach_adam_schedule(const AdamSchedJob& j);
+// keyed by the optimizer's device and stream: only a slice-reduce launch on that
+// stream of that device takes it (another device's or a side stream's reduce does not)
+void conv_attach_adam_schedule(const AdamSchedJob& j, int device, hipStream_t stream);
 bool conv_adam_schedule_taken();
 void conv_detach_adam_schedule();
 

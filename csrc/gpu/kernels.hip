@@ -918,6 +918,39 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // 64*r + 4*blk + s; over s that is 4 consecutive pixels -> one float4 per
 // reg, and for a fixed reg the 16 lanes of one channel cover 64 contiguous
 // pixels: every store instruction writes four 256-byte plane runs.
+// Row j (output channel) of image b's affine transform, by p.mat_mode.
+__device__ __forceinline__ void color_row(const Color4x4Params& p, int b, int j, float bm[4], float& bj) {
+  if (p.mat_mode == kColorJitter) {
+    const float br = p.jit[b][0], c = p.jit[b][1], s = p.jit[b][2];
+    float sn, cs;
+    __sincosf(6.283185307179586f * p.jit[b][3], &sn, &cs);
+    // row j of the hue rotation about the grey axis (rows sum to 1)
+    float h0, h1, h2;
+    if (j == 0) h0 = 0.213f + cs * 0.787f - sn * 0.213f, h1 = 0.715f - cs * 0.715f - sn * 0.715f,
+                h2 = 0.072f - cs * 0.072f + sn * 0.928f;
+    else if (j == 1) h0 = 0.213f - cs * 0.213f + sn * 0.143f, h1 = 0.715f + cs * 0.285f + sn * 0.140f,
+                     h2 = 0.072f - cs * 0.072f - sn * 0.283f;
+    else h0 = 0.213f - cs * 0.213f - sn * 0.787f, h1 = 0.715f - cs * 0.715f + sn * 0.715f,
+         h2 = 0.072f + cs * 0.928f + sn * 0.072f;
+    // (Hue . Sat)[j][k] = s * Hue[j][k] + (1 - s) * w[k]  (Hue's rows sum to 1)
+    const float bc = br * c, t = 1.f - s;
+    if (j < 3) {
+      bm[0] = bc * (s * h0 + t * 0.213f), bm[1] = bc * (s * h1 + t * 0.715f), bm[2] = bc * (s * h2 + t * 0.072f);
+      bm[3] = 0.f;
+      bj = (1.f - c) * p.pivot;
+    } else {
+      bm[0] = bm[1] = bm[2] = 0.f, bm[3] = 1.f, bj = 0.f;
+    }
+    return;
+  }
+  const float* M = p.mat_mode == kColorPos ? p.Ms + 20 * int(p.mat_pos[b])
+                   : p.mat_mode == kColorEach ? p.Ms + 20 * int64_t(b) : p.M;
+  const float* bias = p.mat_mode == kColorOne ? p.bias : M + 16;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) bm[k] = M[j * 4 + k];
+  bj = bias[j];
+}
+
 __global__ __launch_bounds__(kBlock) void color4x4_kernel(Color4x4Params p) {
   __shared__ uint32_t tab[kTabWords];
   const Xf xf = stage_xf(p.lut, tab, 4);   // indexed by INPUT channel here
@@ -926,9 +959,8 @@ __global__ __launch_bounds__(kBlock) void color4x4_kernel(Color4x4Params p) {
   const int wave = threadIdx.x >> 6;
   const int j = lane & 3;
   float bm[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) bm[k] = p.M[j * 4 + k];
-  const float bj = p.bias[j];
+  float bj = 0.f;
+  int mat_b = -1;   // the image whose matrix row bm / bj hold
   const int64_t HW = int64_t(p.H) * p.W;
   const int64_t segs_per_img = HW / 256;   // host guarantees HW % 256 == 0
   const int64_t total = segs_per_img * p.B;
@@ -936,6 +968,10 @@ __global__ __launch_bounds__(kBlock) void color4x4_kernel(Color4x4Params p) {
   for (int64_t g = int64_t(blockIdx.x) * (kBlock / 64) + wave; g < total; g += stride) {
     const int b = int(g / segs_per_img);
     const int64_t q0 = (g - int64_t(b) * segs_per_img) * 256;
+    if (b != mat_b) {   // wave-uniform: a new image's row j of its transform
+      mat_b = b;
+      color_row(p, b, j, bm, bj);
+    }
     // lane's 4 pixels share a row (W % 4 == 0); the segment may span rows
     const int blk = lane >> 2;
     const int64_t pl = q0 + 64 * j + 4 * blk;
@@ -992,6 +1028,8 @@ __global__ void project_kernel(const float* pts, int64_t N, const float* PV, con
 
 hipError_t color4x4(const Color4x4Params& p, hipStream_t stream) {
   if (p.B <= 0) return hipSuccess;
+  if ((p.mat_mode == kColorPos || p.mat_mode == kColorJitter) && p.B > kMaxSrcs) return hipErrorInvalidValue;
+  if ((p.mat_mode == kColorPos || p.mat_mode == kColorEach) && !p.Ms) return hipErrorInvalidValue;
   if ((int64_t(p.H) * p.W) % 256 != 0 || p.W % 4 != 0 || p.Cout < 1 || p.Cout > 4 ||
       (p.ndsts ? !dsts_ok(p.dsts, p.ndsts, p.B, 16) : (reinterpret_cast<uintptr_t>(p.dst) % 16) != 0) ||
       (p.nsrcs ? !srcs_ok(p.srcs, p.nsrcs, p.B, 16) : (reinterpret_cast<uintptr_t>(p.src) % 16) != 0))

@@ -100,6 +100,25 @@ BufPtr PinnedPool::alloc(size_t n) {
   return b;
 }
 
+BufPtr PinnedPool::try_alloc(size_t n) {
+  if (n > slot_bytes_) return nullptr;
+  int id;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (free_.empty()) return nullptr;
+    id = free_.back();
+    free_.pop_back();
+  }
+  auto b = std::make_shared<Buffer>();
+  b->data = base_ + size_t(id) * slot_bytes_;
+  b->capacity = slot_bytes_;
+  b->owner = this;
+  b->tag = id;
+  b->pinned = true;
+  b->release = &PinnedPool::release;
+  return b;
+}
+
 void PinnedPool::release(void* owner, Buffer* b) {
   auto* self = static_cast<PinnedPool*>(owner);
   {
@@ -121,8 +140,13 @@ StreamLoader::StreamLoader(const LoaderConfig& cfg) : cfg_(cfg) {
   if (cfg_.lut.size() != size_t(kTableFloats))
     throw std::invalid_argument("StreamLoader: lut must hold 4*256 or kTableFloats floats");
   if (cfg_.cout < 1 || cfg_.cout > 4) throw std::invalid_argument("StreamLoader: cout must be 1..4");
-  if (cfg_.color_matrix && (cfg_.matrix.size() != 16 || cfg_.bias.size() != 4))
+  if (cfg_.color_matrix && !cfg_.jitter && cfg_.matrices.empty() && (cfg_.matrix.size() != 16 || cfg_.bias.size() != 4))
     throw std::invalid_argument("StreamLoader: colour matrix needs 16 + 4 floats");
+  if (!cfg_.matrices.empty() && cfg_.matrices.size() != size_t(cfg_.batch_size) * 20)
+    throw std::invalid_argument("StreamLoader: per-position colour matrices need batch_size x (16 + 4) floats");
+  if ((cfg_.jitter || !cfg_.matrices.empty()) && cfg_.batch_size > kMaxSrcs)
+    throw std::invalid_argument("StreamLoader: per-image colour transforms need batch_size <= 64");
+  jit_state_ = cfg_.jitter_seed * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull;
   int k = std::max(1, std::min<int>(cfg_.io_threads, int(cfg_.addresses.size())));
   for (int i = 0; i < k; ++i) {
     ctxs_.emplace_back(new zmtp::Context());
@@ -628,7 +652,12 @@ bool StreamLoader::process(zmtp::Message&& msg) {
       passthrough_ = cfg_.cmap[k] == k;
       for (int v = 0; passthrough_ && v < 256; ++v) passthrough_ = cfg_.lut[size_t(k) * 256 + size_t(v)] == float(v);
     }
-    size_t slot = cfg_.max_frame_bytes ? cfg_.max_frame_bytes : size_t(double(n) * 1.05) + 4096;
+    // sized for an inline frame of this image even when the first message is a
+    // shared-memory descriptor (a few hundred bytes): in a mixed fleet the
+    // inline producers' frames must fit the slots, or they land on the heap
+    // and their batches fall off the direct path
+    const size_t inline_bytes = std::max(n, size_t(h) * w * c + n + 1024);
+    size_t slot = cfg_.max_frame_bytes ? cfg_.max_frame_bytes : size_t(double(inline_bytes) * 1.05) + 4096;
     slot = (slot + 4095) & ~size_t(4095);
     int nslots = cfg_.pool_slots;
     if (nslots <= 0) {
@@ -640,7 +669,10 @@ bool StreamLoader::process(zmtp::Message&& msg) {
       if (size_t(nslots) * slot > cap) nslots = int(std::max<size_t>(16, cap / slot));
     }
     pool_ = std::make_shared<PinnedPool>(slot, nslots);
-    for (auto& s : socks_) s->set_allocator(pool_, 64 * 1024);
+    // every image-bearing frame goes to a pinned slot (small images too: a
+    // frame below 64 KB used to be heap-received and took its batch to the
+    // copy path); descriptor-only messages stay on the heap
+    for (auto& s : socks_) s->set_allocator(pool_, std::min<size_t>(64 * 1024, size_t(h) * w * c));
     for (int k = 0; k < std::max(2, cfg_.staging_depth); ++k) {
       uint8_t* p = nullptr;
       check(hipMalloc(reinterpret_cast<void**>(&p), img_bytes_ * size_t(cfg_.batch_size)), "hipMalloc(staging)");
@@ -648,11 +680,14 @@ bool StreamLoader::process(zmtp::Message&& msg) {
     }
     check(hipMalloc(reinterpret_cast<void**>(&d_lut_), kTableFloats * sizeof(float)), "hipMalloc(lut)");
     check(hipMemcpy(d_lut_, cfg_.lut.data(), kTableFloats * sizeof(float), hipMemcpyHostToDevice), "upload lut");
-    if (cfg_.color_matrix) {
-      check(hipMalloc(reinterpret_cast<void**>(&d_mat_), 20 * sizeof(float)), "hipMalloc(matrix)");
-      std::vector<float> mb(cfg_.matrix);
-      mb.insert(mb.end(), cfg_.bias.begin(), cfg_.bias.end());
-      check(hipMemcpy(d_mat_, mb.data(), 20 * sizeof(float), hipMemcpyHostToDevice), "upload matrix");
+    if (cfg_.color_matrix && !cfg_.jitter) {
+      std::vector<float> mb(cfg_.matrices);
+      if (mb.empty()) {
+        mb = cfg_.matrix;
+        mb.insert(mb.end(), cfg_.bias.begin(), cfg_.bias.end());
+      }
+      check(hipMalloc(reinterpret_cast<void**>(&d_mat_), mb.size() * sizeof(float)), "hipMalloc(matrix)");
+      check(hipMemcpy(d_mat_, mb.data(), mb.size() * sizeof(float), hipMemcpyHostToDevice), "upload matrix");
     }
     {
       std::lock_guard<std::mutex> lk(mu_);
@@ -677,6 +712,19 @@ bool StreamLoader::process(zmtp::Message&& msg) {
   }
   it.meta.tree = root;
 
+  if (cfg_.jitter) {
+    // splitmix64: brightness, contrast, saturation in [max(0, 1 - r), 1 + r], hue in [-r, r] turns
+    for (int k = 0; k < 4; ++k) {
+      uint64_t z = (jit_state_ += 0x9E3779B97F4A7C15ull);
+      z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+      z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+      z ^= z >> 31;
+      const float u = float(z >> 40) * (1.f / 16777216.f);   // [0, 1)
+      const float r = cfg_.jitter_range[k];
+      const float lo = k < 3 ? std::max(0.f, 1.f - r) : -r, hi = k < 3 ? 1.f + r : r;
+      it.jit[k] = lo + (hi - lo) * u;
+    }
+  }
   if (cur_.empty()) batch_t0_ = now_ms();
   {
     std::lock_guard<std::mutex> lk(mu_);
@@ -866,17 +914,31 @@ void StreamLoader::launch() {
   pb.dst = p.dst;
   pb.ready = p.ready;
   pb.t0 = batch_t0_;
-  pb.direct = cfg_.direct && int(cur_.size()) <= kMaxSrcs;
-  for (auto& it : cur_)
-    pb.direct = pb.direct && it.dsrc && (reinterpret_cast<uintptr_t>(it.dsrc) % 16) == 0 &&
-                !(it.tiled && cfg_.color_matrix);
+  auto aligned = [](const Item& it) { return it.dsrc && (reinterpret_cast<uintptr_t>(it.dsrc) % 16) == 0; };
+  const bool direct = cfg_.direct && int(cur_.size()) <= kMaxSrcs;
   // a batch of key-frame deltas only decodes as such (fill + tile scatter);
   // in any other batch (copy path, MFMA colour kernel, mixed producers) they
   // are rebuilt on the host
-  pb.tiled = pb.direct && std::all_of(cur_.begin(), cur_.end(), [](const Item& it) { return it.tiled; });
+  pb.tiled = direct && !cfg_.color_matrix &&
+             std::all_of(cur_.begin(), cur_.end(), [&](const Item& it) { return it.tiled && aligned(it); });
   if (!pb.tiled)
     for (auto& it : cur_) materialize(it);
-  pb.direct = pb.direct && std::all_of(cur_.begin(), cur_.end(), [](const Item& it) { return it.dsrc != nullptr; });
+  // mixed batches stay on the direct path: a frame the kernel cannot read in
+  // place (heap-received: dry pool, rebuilt on the host, unaligned) is copied
+  // into a free pinned slot here, and the rest are still read where they lie
+  if (direct && !pb.tiled && pool_)
+    for (auto& it : cur_) {
+      if (aligned(it)) continue;
+      BufPtr b = pool_->try_alloc(img_bytes_);
+      if (!b) break;   // no slot free now: this batch takes the copy path
+      std::memcpy(b->data, it.src, img_bytes_);
+      it.src = b->data;
+      it.dsrc = pool_->device_ptr(b->data);
+      it.staged = std::move(b);
+      std::lock_guard<std::mutex> lk(mu_);
+      stats_.staged_frames++;
+    }
+  pb.direct = direct && std::all_of(cur_.begin(), cur_.end(), aligned);
   pb.items = std::move(cur_);
   cur_.clear();
   pending_images_ += int(pb.items.size());
@@ -932,7 +994,7 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
     total += int(b.items.size());
   }
   const size_t elem = cfg_.color_matrix ? 4 : (cfg_.out_dtype == OUT_F32 ? 4 : (cfg_.out_dtype == OUT_U8 ? 1 : 2));
-  const int cout = cfg_.color_matrix ? 4 : cfg_.cout;
+  const int cout = cfg_.cout;   // (colour kernel: 4, or 3 for RGB jitter)
   const size_t out_img_bytes = size_t(H_) * W_ * cout * elem;
   uint64_t flips[4] = {0, 0, 0, 0};
   std::vector<const Item*> all;
@@ -1052,8 +1114,20 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
           cp.dsts[i++] = reinterpret_cast<float*>(static_cast<uint8_t*>(b.dst) + k * out_img_bytes);
     }
     cp.lut = d_lut_;
-    cp.M = d_mat_;
-    cp.bias = d_mat_ + 16;
+    if (cfg_.jitter) {
+      cp.mat_mode = kColorJitter;
+      cp.pivot = cfg_.pivot;
+      for (int i = 0; i < total; ++i) std::memcpy(cp.jit[i], all[size_t(i)]->jit, sizeof(cp.jit[i]));
+    } else if (!cfg_.matrices.empty()) {
+      cp.mat_mode = kColorPos;
+      cp.Ms = d_mat_;
+      int i = 0;
+      for (auto& b : group)
+        for (size_t k = 0; k < b.items.size(); ++k) cp.mat_pos[i++] = uint8_t(k);
+    } else {
+      cp.M = d_mat_;
+      cp.bias = d_mat_ + 16;
+    }
     cp.B = total, cp.H = H_, cp.W = W_, cp.Cout = cfg_.cout;
     cp.flip_all = cfg_.flip_all;
     std::memcpy(cp.flip_bits, flips, sizeof(flips));
@@ -1126,6 +1200,8 @@ void StreamLoader::launch_group(std::vector<Pending>& group) {
         if (cfg_.host_sync) rb.slots.push_back({it.seg, it.slot, it.gen});
       }
       if (!it.expanded.empty()) fl.expanded.push_back(std::move(it.expanded));
+      if (cfg_.jitter) rb.jitter.insert(rb.jitter.end(), it.jit, it.jit + 4);
+      if (it.staged) fl.staged.push_back(std::move(it.staged));
       rb.items.push_back(std::move(it.meta));
     }
     if (host_passthrough) {

@@ -62,6 +62,9 @@ class PinnedPool : public Allocator, public std::enable_shared_from_this<PinnedP
   // Blocks up to `wait_ms` for a free slot (backpressure on the IO thread),
   // then returns nullptr (heap fallback) if the pool is still dry.
   BufPtr alloc(size_t n) override;
+  // A free slot now or nullptr: no wait, not counted as a fallback (the
+  // worker stages a heap-received frame into it, StreamLoader::launch)
+  BufPtr try_alloc(size_t n);
   void set_wait_ms(int ms) { wait_ms_ = ms; }
   size_t slot_bytes() const { return slot_bytes_; }
   int nslots() const { return nslots_; }
@@ -130,6 +133,16 @@ struct LoaderConfig {
   std::vector<float> lut;            // 4*256 floats (host)
   bool color_matrix = false;         // use the MFMA colour-transform kernel
   std::vector<float> matrix, bias;   // 16 + 4 floats
+  // per-image transforms on the same kernel (photometric augmentation):
+  // matrices: batch_size x (16 + 4) floats, the transform of each batch position;
+  // jitter: every image draws (brightness, contrast, saturation, hue) uniformly from
+  // [1 - r, 1 + r] (hue: [-r, r] turns) with a seeded splitmix64 stream in arrival
+  // order, and the batch reports the factors it was decoded with
+  std::vector<float> matrices;
+  bool jitter = false;
+  float jitter_range[4] = {0.f, 0.f, 0.f, 0.f};
+  float pivot = 0.5f;
+  uint64_t jitter_seed = 0;
 };
 
 // One delivered batch: metadata of each item (non-image bytes of the frame,
@@ -172,6 +185,7 @@ struct ReadyBatch {
   };
   std::vector<SlotRef> slots;        // host_sync: shm slots re-validated before hand-out
   int64_t launch_no = 0;             // host_sync: the launch that read them
+  std::vector<float> jitter;         // colour jitter: 4 factors per image (LoaderConfig::jitter)
 };
 
 struct LoaderStats {
@@ -192,6 +206,7 @@ struct LoaderStats {
   // yet claimed (waiting in queues), frames claimed by this loader
   uint64_t ring_slots = 0, ring_published = 0, ring_held = 0;
   uint64_t passthrough_batches = 0;        // copy path, identity decode: DMA only, no kernel
+  uint64_t staged_frames = 0;              // heap-received frames copied into a pinned slot (batch kept direct)
   std::map<int64_t, uint64_t> frames_per_btid;   // provenance: frames per producer id
   // worker-thread CPU (thread clock, ms) per stage of its loop -- where the
   // consumer process's CPU per delivered frame goes: socket poll, receive +
@@ -236,6 +251,8 @@ class StreamLoader {
     KeyFrame* key = nullptr;
     const uint8_t* key_host = nullptr;
     std::vector<uint8_t> expanded;     // copy path: the frame rebuilt on the host
+    BufPtr staged;                     // pinned slot a heap-received image was copied into (direct path)
+    float jit[4] = {1.f, 1.f, 1.f, 0.f};   // colour-jitter factors (LoaderConfig::jitter)
     BatchMeta meta;
   };
   void materialize(Item& it);
@@ -286,7 +303,8 @@ class StreamLoader {
   hipStream_t stream_ = nullptr;
   std::vector<uint8_t*> staging_;
   float* d_lut_ = nullptr;
-  float* d_mat_ = nullptr;   // 16 matrix + 4 bias
+  float* d_mat_ = nullptr;   // 16 matrix + 4 bias (or batch_size x 20: LoaderConfig::matrices)
+  uint64_t jit_state_ = 0;   // splitmix64 state of the colour-jitter draws
   std::vector<Item> cur_;
   std::deque<Pending> pending_;
   int pending_images_ = 0;
@@ -318,6 +336,7 @@ class StreamLoader {
     };
     std::vector<Slot> slots;
     std::vector<std::vector<uint8_t>> expanded;   // pageable copy sources, alive until `copied`
+    std::vector<BufPtr> staged;                   // pinned slots of staged heap frames, alive until `copied`
   };
   struct MappedSegment {
     std::unique_ptr<shm::Segment> seg;

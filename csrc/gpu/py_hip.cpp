@@ -615,12 +615,14 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("off") = 1.0f);
   // the Adam schedule attached to the next weight-gradient slice-reduce launch (adam_sched.h)
   m.def("adam_attach_schedule",
-        [](uintptr_t step, uintptr_t hp, uintptr_t sched, float beta1, float beta2) {
+        [](uintptr_t step, uintptr_t hp, uintptr_t sched, float beta1, float beta2, int device, uintptr_t stream) {
           AdamSchedJob j;
           j.step = ptr<float>(step), j.hp = ptr<const float>(hp), j.sched = ptr<float>(sched);
           j.beta1 = beta1, j.beta2 = beta2;
-          conv_attach_adam_schedule(j);
-        });
+          conv_attach_adam_schedule(j, device, stream_of(stream));
+        },
+        py::arg("step"), py::arg("hp"), py::arg("sched"), py::arg("beta1"), py::arg("beta2"), py::arg("device"),
+        py::arg("stream"));
   m.def("adam_schedule_taken", []() { return conv_adam_schedule_taken(); });
   m.def("adam_detach_schedule", []() { conv_detach_adam_schedule(); });
 
@@ -673,7 +675,8 @@ PYBIND11_MODULE(_hip, m) {
 
   m.def("color4x4",
         [](uintptr_t src, uintptr_t dst, uintptr_t lut, uintptr_t M, uintptr_t bias, uintptr_t flip, int B, int H,
-           int W, int Cout, int flip_all, uintptr_t stream) {
+           int W, int Cout, int flip_all, uintptr_t stream, int mat_mode, uintptr_t Ms, std::vector<float> jitter,
+           float pivot) {
           Color4x4Params p;
           p.src = ptr<const uint8_t>(src);
           p.dst = ptr<float>(dst);
@@ -683,10 +686,20 @@ PYBIND11_MODULE(_hip, m) {
           p.flip = ptr<const uint8_t>(flip);
           p.B = B, p.H = H, p.W = W, p.Cout = Cout;
           p.flip_all = flip_all;
+          p.mat_mode = mat_mode;
+          p.Ms = ptr<const float>(Ms);
+          p.pivot = pivot;
+          if (mat_mode == kColorJitter) {
+            if (B > kMaxSrcs || jitter.size() != size_t(4) * size_t(B))
+              throw std::invalid_argument("color4x4: jitter needs 4 factors per image, B <= 64");
+            for (int b = 0; b < B; ++b)
+              for (int k = 0; k < 4; ++k) p.jit[b][k] = jitter[size_t(b) * 4 + size_t(k)];
+          }
           check(color4x4(p, stream_of(stream)), "color4x4");
         },
         py::arg("src"), py::arg("dst"), py::arg("lut"), py::arg("M"), py::arg("bias"), py::arg("flip"), py::arg("B"),
-        py::arg("H"), py::arg("W"), py::arg("Cout"), py::arg("flip_all"), py::arg("stream"));
+        py::arg("H"), py::arg("W"), py::arg("Cout"), py::arg("flip_all"), py::arg("stream"), py::arg("mat_mode") = 0,
+        py::arg("Ms") = 0, py::arg("jitter") = std::vector<float>(), py::arg("pivot") = 0.5f);
 
   m.def("project",
         [](uintptr_t pts, int64_t N, uintptr_t PV, uintptr_t V, int W, int H, int upper_left, uintptr_t out_px,
@@ -1040,7 +1053,8 @@ PYBIND11_MODULE(_hip, m) {
                        int io_threads, int device, int64_t max_batches, size_t max_frame_bytes, int pool_slots,
                        int staging_depth, bool skip_bad, int cout, std::vector<int> cmap, int flip_all,
                        int out_dtype, int layout, std::vector<float> lut, std::vector<float> matrix,
-                       std::vector<float> bias, bool direct, int launch_depth, int copy_streams, bool host_sync) {
+                       std::vector<float> bias, bool direct, int launch_depth, int copy_streams, bool host_sync,
+                       std::vector<float> matrices, std::vector<float> jitter, uint64_t jitter_seed) {
              LoaderConfig c;
              c.direct = direct;
              c.host_sync = host_sync;
@@ -1066,6 +1080,17 @@ PYBIND11_MODULE(_hip, m) {
              c.color_matrix = !matrix.empty();
              c.matrix = std::move(matrix);
              c.bias = std::move(bias);
+             // per-batch-position matrices (B x (16 + 4)) or random colour jitter
+             // (4 ranges + pivot), both on the MFMA colour kernel
+             if (!matrices.empty() || !jitter.empty()) c.color_matrix = true;
+             c.matrices = std::move(matrices);
+             if (!jitter.empty()) {
+               if (jitter.size() != 5) throw std::invalid_argument("StreamLoader: jitter = 4 ranges + pivot");
+               c.jitter = true;
+               for (int k = 0; k < 4; ++k) c.jitter_range[k] = jitter[size_t(k)];
+               c.pivot = jitter[4];
+               c.jitter_seed = jitter_seed;
+             }
              return new StreamLoader(c);
            }),
            py::arg("addresses"), py::arg("batch_size"), py::arg("image_key"), py::arg("rcvhwm"),
@@ -1073,7 +1098,8 @@ PYBIND11_MODULE(_hip, m) {
            py::arg("pool_slots"), py::arg("staging_depth"), py::arg("skip_bad"), py::arg("cout"), py::arg("cmap"),
            py::arg("flip_all"), py::arg("out_dtype"), py::arg("layout"), py::arg("lut"), py::arg("matrix"),
            py::arg("bias"), py::arg("direct") = true, py::arg("launch_depth") = 2,
-           py::arg("copy_streams") = 2, py::arg("host_sync") = true)
+           py::arg("copy_streams") = 2, py::arg("host_sync") = true, py::arg("matrices") = std::vector<float>(),
+           py::arg("jitter") = std::vector<float>(), py::arg("jitter_seed") = 0)
       .def("start", &StreamLoader::start)
       .def("wait_shape",
            [](StreamLoader& l, long timeout_ms) -> py::object {
@@ -1119,7 +1145,13 @@ PYBIND11_MODULE(_hip, m) {
              }
              if (!ok) return py::none();
              if (rb.index < 0) return py::make_tuple(-1, py::dict(), 0.0);
-             return py::make_tuple(rb.index, collate_meta(rb.items), rb.recv_ms);
+             py::dict meta = collate_meta(rb.items);
+             if (!rb.jitter.empty()) {   // the colour-jitter factors each image was decoded with
+               py::array_t<float> f({py::ssize_t(rb.jitter.size() / 4), py::ssize_t(4)});
+               std::memcpy(f.mutable_data(), rb.jitter.data(), rb.jitter.size() * sizeof(float));
+               meta["color_jitter"] = f;
+             }
+             return py::make_tuple(rb.index, meta, rb.recv_ms);
            })
       .def("stop",
            [](StreamLoader& l) {
@@ -1147,6 +1179,7 @@ PYBIND11_MODULE(_hip, m) {
         d["timed_gpu_ms"] = s.timed_gpu_ms;
         d["keys_evicted"] = s.keys_evicted;
         d["passthrough_batches"] = s.passthrough_batches;
+        d["staged_frames"] = s.staged_frames;
         d["ring_slots"] = s.ring_slots;
         d["ring_published"] = s.ring_published;
         d["ring_held"] = s.ring_held;

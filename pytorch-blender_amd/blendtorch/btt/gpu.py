@@ -23,6 +23,7 @@ Semantics kept from the reference:
 from __future__ import annotations
 
 import logging
+import os
 import time
 from typing import Optional, Sequence
 
@@ -38,6 +39,17 @@ from .constants import DEFAULT_TIMEOUTMS
 logger = logging.getLogger('blendtorch')
 
 __all__ = ['DeviceLoader', 'DecodeConfig']
+
+
+def _default_io_threads(addresses) -> int:
+    n = len(addresses)
+    if not any(str(a).startswith('tcp://') for a in addresses):
+        return max(1, min(4, n))
+    try:
+        cpus = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        cpus = os.cpu_count() or 4
+    return max(1, min(n, max(4, cpus - 2)))
 
 
 class DeviceLoader:
@@ -62,7 +74,10 @@ class DeviceLoader:
     prefetch: int
         Output batches the native pipeline may run ahead of the consumer.
     io_threads: int, optional
-        Receive IO threads (default: one per address, at most 4).
+        Receive IO threads (default: one per address, at most 4 for ipc://
+        addresses -- shared-memory descriptors and local frames -- and up to
+        the process's usable CPUs minus two for tcp:// ones, whose inline
+        frames each thread copies out of its sockets).
     image_key: str
         Dict key holding the u8 HxWxC image.
     skip_bad: bool
@@ -136,8 +151,11 @@ class DeviceLoader:
         self.prefetch = max(1, int(prefetch))
         # one receive thread per producer up to 4: a thread copying inline
         # 1.2 MB frames out of sockets tops out near 7-9k frames/s
-        # (profiles/reference_harness.md), shm descriptors cost it little
-        self.io_threads = io_threads or max(1, min(4, len(self.addresses)))
+        # (profiles/reference_harness.md), shm descriptors cost it little;
+        # over TCP (remote producers, inline frames) every pipe gets its own
+        # thread, up to the CPUs this process may use minus the worker and
+        # the consumer
+        self.io_threads = io_threads or _default_io_threads(self.addresses)
         self.image_key = image_key
         self.skip_bad = skip_bad
         self.meta_to_device = meta_to_device
@@ -192,12 +210,25 @@ class DeviceLoader:
         lut = ops.build_table(cfg).tolist()
         matrix = [] if cfg.color_matrix is None else np.asarray(cfg.color_matrix, np.float32).reshape(-1).tolist()
         bias = [] if cfg.color_matrix is None else list(cfg.color_bias or (0.0, 0.0, 0.0, 0.0))
+        # per-image colour transforms on the same MFMA kernel: one per batch position,
+        # or random jitter drawn per image in the loader (factors in batch['color_jitter'])
+        matrices, jitter, seed = [], [], 0
+        if cfg.color_matrices is not None:
+            if len(cfg.color_matrices) != self.batch_size:
+                raise ValueError(f'DecodeConfig.color_matrices holds {len(cfg.color_matrices)} transforms for '
+                                 f'batch_size {self.batch_size}')
+            m = np.asarray(cfg.color_matrices, np.float32).reshape(self.batch_size, 16)
+            matrices = np.concatenate([m, np.asarray(cfg.color_biases, np.float32)], axis=1).reshape(-1).tolist()
+        if cfg.color_jitter is not None:
+            j = cfg.color_jitter
+            jitter = [j.brightness, j.contrast, j.saturation, j.hue, cfg.jitter_pivot]
+            seed = int(j.seed) & ((1 << 64) - 1)
         max_batches = -1 if self.max_items is None else self.max_items // self.batch_size
         return ext.StreamLoader(
             self.addresses, self.batch_size, self.image_key, self.rcvhwm, self.io_threads, self.device.index,
             max_batches, 0, 0, self.staging_depth, self.skip_bad, cfg.cout, list(cfg.cmap) + [0] * (4 - len(cfg.cmap)),
             int(cfg.flip), ops.OUT_DTYPES[cfg.dtype], ops.LAYOUTS[cfg.layout], lut, matrix, bias,
-            self.h2d == 'auto', self.launch_depth, self.copy_streams, self.host_sync)
+            self.h2d == 'auto', self.launch_depth, self.copy_streams, self.host_sync, matrices, jitter, seed)
 
     def _post(self, loader, stream):
         shape = self.decode.out_shape(self.batch_size, *self.shape[:2])
@@ -264,6 +295,7 @@ class DeviceLoader:
             'launches': s['launches'],
             'images_per_launch': s['frames'] / s['launches'] if s['launches'] else None,
             'direct_batches': s['direct_batches'],
+            'staged_frames': s.get('staged_frames', 0),
             'consumer_wait_s': self._wait_s,
             'bad': s['bad'], 'shm_stale': s['shm_stale'], 'shm_torn': s['shm_torn'],
             'pool_fallbacks': s['pool_fallbacks'],

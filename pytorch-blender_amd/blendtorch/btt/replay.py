@@ -233,10 +233,10 @@ class DeviceReplayBuffer:
 
     # -- sampling --------------------------------------------------------------
     def _fused(self, decode: DecodeConfig):
-        return self.device.type == 'cuda' and decode.color_matrix is None and self.store.is_contiguous()
+        return self.device.type == 'cuda' and not decode.colour_kernel and self.store.is_contiguous()
 
     def _decode(self, idx: torch.Tensor, decode: DecodeConfig):
-        if self.device.type == 'cuda' and decode.color_matrix is None:
+        if self.device.type == 'cuda' and not decode.colour_kernel:
             return ops.decode_gather(self.store, idx, decode)
         imgs = self.store.index_select(0, idx)
         if self.device.type == 'cuda':

@@ -29,7 +29,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 __all__ = [
-    'DecodeConfig', 'hip_ext', 'hip_available', 'gamma_lut', 'build_lut', 'build_table', 'decode', 'decode_gather',
+    'DecodeConfig', 'ColorJitter', 'color_jitter_matrix', 'jitter_factors', 'hip_ext', 'hip_available', 'gamma_lut', 'build_lut', 'build_table', 'decode', 'decode_gather',
     'color4x4',
     'project', 'adaptive_avg_pool_nhwc', 'AdaptiveAvgPool2d', 'batch_norm_leaky_relu', 'BatchNormLeakyReLU2d',
     'reference_decode', 'reference_color4x4', 'reference_project', 'reference_gamma',
@@ -89,6 +89,82 @@ def gamma_lut(gamma: Optional[float]) -> np.ndarray:
 
 
 @dataclasses.dataclass(frozen=True)
+class ColorJitter:
+    """Random photometric augmentation on the loader's MFMA colour kernel.
+
+    Every image draws brightness, contrast and saturation factors uniformly
+    from ``[max(0, 1 - r), 1 + r]`` and a hue shift from ``[-hue, hue]``
+    (turns), from a seeded stream in arrival order; each batch reports the
+    factors it was decoded with (``batch['color_jitter']``, [B, 4]).  The
+    transform of one image is the affine map of :func:`color_jitter_matrix`
+    applied to ``gamma(x) * scale``; ``pivot`` (default: mid-grey in output
+    units, 127.5 * scale) is the contrast pivot.  The reference has no such
+    stage: it generalises the per-image colour handling of
+    ``btb/offscreen.py:105-112`` to augmentation at PCIe rate.
+    """
+    brightness: float = 0.0
+    contrast: float = 0.0
+    saturation: float = 0.0
+    hue: float = 0.0
+    seed: int = 0
+    pivot: Optional[float] = None
+
+    def __post_init__(self):
+        for f in ('brightness', 'contrast', 'saturation'):
+            if getattr(self, f) < 0:
+                raise ValueError(f'ColorJitter.{f} must be >= 0')
+        if not 0.0 <= self.hue <= 0.5:
+            raise ValueError('ColorJitter.hue must be in [0, 0.5]')
+
+
+def jitter_factors(seed: int, ranges, n: int) -> np.ndarray:
+    """float32 [n, 4]: the colour-jitter factors the stream loader draws for
+    its first ``n`` images (csrc/gpu/loader.cpp, splitmix64 in arrival
+    order): brightness, contrast, saturation in ``[max(0, 1 - r), 1 + r]``,
+    hue in ``[-r, r]`` turns, for ``ranges`` = (r_b, r_c, r_s, r_h)."""
+    M64 = (1 << 64) - 1
+    state = (int(seed) * 0x9E3779B97F4A7C15 + 0x632BE59BD9B4E019) & M64
+    out = np.zeros((n, 4), np.float32)
+    for i in range(n):
+        for k in range(4):
+            state = (state + 0x9E3779B97F4A7C15) & M64
+            z = state
+            z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+            z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
+            z ^= z >> 31
+            u = np.float32(z >> 40) * np.float32(1.0 / 16777216.0)
+            r = np.float32(ranges[k])
+            lo = max(np.float32(0.0), np.float32(1.0) - r) if k < 3 else -r
+            hi = np.float32(1.0) + r if k < 3 else r
+            out[i, k] = np.float32(lo) + (np.float32(hi) - np.float32(lo)) * u
+    return out
+
+
+_LUMA = np.array([0.213, 0.715, 0.072])
+
+
+def color_jitter_matrix(factors, pivot=0.5):
+    """(M [4, 4], bias [4]) float32 of the colour jitter ``factors`` =
+    (brightness b, contrast c, saturation s, hue h in turns), as the loader's
+    kernel builds it (csrc/gpu/kernels.hip ``color_row``):
+    ``rgb' = b c (Hue(h) Sat(s)) rgb + (1 - c) pivot``, alpha unchanged, with
+    ``Sat(s) = s I + (1 - s) 1 w^T`` and ``Hue`` the rotation about the grey
+    axis (luminance ``w = (0.213, 0.715, 0.072)``).  Both keep grey grey."""
+    b, c, s, h = (float(v) for v in factors)
+    cs, sn = np.cos(2 * np.pi * h), np.sin(2 * np.pi * h)
+    hue = np.array([
+        [0.213 + cs * 0.787 - sn * 0.213, 0.715 - cs * 0.715 - sn * 0.715, 0.072 - cs * 0.072 + sn * 0.928],
+        [0.213 - cs * 0.213 + sn * 0.143, 0.715 + cs * 0.285 + sn * 0.140, 0.072 - cs * 0.072 - sn * 0.283],
+        [0.213 - cs * 0.213 - sn * 0.787, 0.715 - cs * 0.715 + sn * 0.715, 0.072 + cs * 0.928 + sn * 0.072]])
+    sat = s * np.eye(3) + (1 - s) * np.outer(np.ones(3), _LUMA)
+    M = np.eye(4)
+    M[:3, :3] = b * c * (hue @ sat)
+    bias = np.zeros(4)
+    bias[:3] = (1 - c) * pivot
+    return M.astype(np.float32), bias.astype(np.float32)
+
+
+@dataclasses.dataclass(frozen=True)
 class DecodeConfig:
     """What the fused decode kernel does to each u8 HWC image.
 
@@ -105,6 +181,11 @@ class DecodeConfig:
         flipped per image automatically by the stream loader.
     color_matrix / color_bias: optional 4x4 affine colour transform applied
         after gamma (RGBA input, fp32 NCHW output; runs on the MFMA units).
+    color_matrices / color_biases: one such transform per batch position
+        ([B, 4, 4] / [B, 4]; the loader's batch size must be B).
+    color_jitter: a :class:`ColorJitter` -- a random transform per image,
+        built inside the same kernel, applied to ``gamma(x) * scale``
+        (channels 'rgb' or 'rgba', no mean/std).
     """
     channels: object = 'rgb'
     gamma: Optional[float] = None
@@ -116,6 +197,9 @@ class DecodeConfig:
     flip: bool = False
     color_matrix: Optional[Sequence[Sequence[float]]] = None
     color_bias: Optional[Sequence[float]] = None
+    color_matrices: Optional[Sequence] = None
+    color_biases: Optional[Sequence] = None
+    color_jitter: Optional[ColorJitter] = None
 
     def __post_init__(self):
         # normalise sequences to tuples: configs are hashable cache keys
@@ -139,6 +223,26 @@ class DecodeConfig:
                 raise ValueError('color_matrix must be 4x4')
             if self.dtype != 'float32' or self.layout != 'nchw':
                 raise ValueError('color_matrix produces float32 NCHW output')
+        if self.color_matrices is not None:
+            m = np.asarray(self.color_matrices, dtype=np.float32)
+            if m.ndim != 3 or m.shape[1:] != (4, 4) or not 1 <= m.shape[0] <= 64:
+                raise ValueError('color_matrices must be [B, 4, 4] with B <= 64')
+            object.__setattr__(self, 'color_matrices', tuple(tuple(tuple(float(x) for x in r) for r in mm) for mm in m))
+            bb = np.zeros((m.shape[0], 4), np.float32) if self.color_biases is None else \
+                np.asarray(self.color_biases, np.float32)
+            if bb.shape != (m.shape[0], 4):
+                raise ValueError('color_biases must be [B, 4]')
+            object.__setattr__(self, 'color_biases', tuple(tuple(float(x) for x in r) for r in bb))
+        if self.color_jitter is not None:
+            if not isinstance(self.color_jitter, ColorJitter):
+                raise TypeError('color_jitter must be an ops.ColorJitter')
+            if self.channels not in ('rgb', 'rgba') or self.mean is not None or self.std is not None:
+                raise ValueError("color_jitter needs channels 'rgb' or 'rgba' and no mean/std")
+        if sum(x is not None for x in (self.color_matrix, self.color_matrices, self.color_jitter)) > 1:
+            raise ValueError('color_matrix, color_matrices and color_jitter are exclusive')
+        if (self.color_matrices is not None or self.color_jitter is not None) and \
+                (self.dtype != 'float32' or self.layout != 'nchw'):
+            raise ValueError('per-image colour transforms produce float32 NCHW output')
 
     # -- presets -----------------------------------------------------------
     @classmethod
@@ -165,8 +269,20 @@ class DecodeConfig:
         return list(self.channels)
 
     @property
+    def colour_kernel(self):
+        """Decoded by the MFMA colour kernel (RGBA input)."""
+        return self.color_matrix is not None or self.color_matrices is not None or self.color_jitter is not None
+
+    @property
     def cout(self):
-        return 4 if self.color_matrix is not None else len(self.cmap)
+        if self.color_jitter is not None:
+            return len(self.cmap)
+        return 4 if self.colour_kernel else len(self.cmap)
+
+    @property
+    def jitter_pivot(self):
+        j = self.color_jitter
+        return float(j.pivot) if j is not None and j.pivot is not None else 127.5 * float(self.scale)
 
     def out_shape(self, B, H, W):
         c = self.cout
@@ -187,9 +303,13 @@ def build_lut(cfg: DecodeConfig) -> np.ndarray:
     g = gamma_lut(cfg.gamma).astype(np.float32)
     ident = np.arange(256, dtype=np.float32)
     lut = np.zeros((4, 256), dtype=np.float32)
-    if cfg.color_matrix is not None:
+    if cfg.color_matrix is not None or cfg.color_matrices is not None:
         for k in range(4):
             lut[k] = g if k < 3 else ident
+        return lut
+    if cfg.color_jitter is not None:   # the jitter works on gamma(x) * scale (alpha: x * scale)
+        for k in range(4):
+            lut[k] = (g if k < 3 else ident) * np.float32(cfg.scale)
         return lut
     mean = np.asarray(cfg.mean if cfg.mean is not None else [0.0] * 4, dtype=np.float32)
     std = np.asarray(cfg.std if cfg.std is not None else [1.0] * 4, dtype=np.float32)
@@ -261,9 +381,9 @@ def build_table(cfg: DecodeConfig) -> np.ndarray:
     g = gamma_lut(cfg.gamma)
     gf = g.astype(np.float32)
     ident = np.arange(256, dtype=np.float32)
-    if cfg.color_matrix is not None:
+    if cfg.colour_kernel:
         chans = [(k, k) for k in range(4)]          # indexed by input channel, no normalisation
-        normalize = False
+        normalize = cfg.color_jitter is not None and cfg.scale != 1.0   # (jitter: gamma(x) * scale)
     else:
         chans = list(enumerate(cfg.cmap))
         normalize = not (cfg.mean is None and cfg.std is None and cfg.scale == 1.0)
@@ -311,12 +431,31 @@ def reference_gamma(images, gamma):
     return rgb
 
 
-def reference_decode(images, cfg: DecodeConfig, flip=None):
-    """fp32 PyTorch reference of :func:`decode` (images: u8 [B,H,W,C])."""
+def reference_decode(images, cfg: DecodeConfig, flip=None, jitter=None):
+    """fp32 PyTorch reference of :func:`decode` (images: u8 [B,H,W,C]); for a
+    ``color_jitter`` config, ``jitter`` holds the [B, 4] factors of the batch
+    (``batch['color_jitter']``)."""
     import torch
     x = images
     if x.dim() == 3:
         x = x.unsqueeze(-1)
+    if cfg.colour_kernel:
+        if flip is not None:
+            f = torch.as_tensor(flip, dtype=torch.bool, device=x.device)
+            x = torch.where(f.view(-1, 1, 1, 1), torch.flip(x, dims=[1]), x)
+        if cfg.color_matrix is not None:
+            M, b = np.asarray(cfg.color_matrix, np.float32), np.asarray(cfg.color_bias or [0.0] * 4, np.float32)
+        elif cfg.color_matrices is not None:
+            M, b = np.asarray(cfg.color_matrices, np.float32), np.asarray(cfg.color_biases, np.float32)
+        else:
+            if jitter is None:
+                raise ValueError('reference_decode: a color_jitter config needs the batch\'s jitter factors')
+            mb = [color_jitter_matrix(f, cfg.jitter_pivot) for f in np.asarray(jitter, np.float64)]
+            # the jitter works on gamma(x) * scale: fold the scale into the matrix columns
+            M = np.stack([m for m, _ in mb]) * np.float32(cfg.scale)
+            b = np.stack([bb for _, bb in mb])
+        out = reference_color4x4(x, M, b, gamma=cfg.gamma, flip=cfg.flip)
+        return out[:, :cfg.cout]
     if cfg.flip:
         x = torch.flip(x, dims=[1])
     if flip is not None:
@@ -339,6 +478,7 @@ def reference_decode(images, cfg: DecodeConfig, flip=None):
 
 
 def reference_color4x4(images, M, bias, gamma=None, flip=False):
+    """fp32 reference: ``M`` [4, 4] / ``bias`` [4], or one per image ([B, 4, 4] / [B, 4])."""
     import torch
     x = images
     if flip:
@@ -346,8 +486,13 @@ def reference_color4x4(images, M, bias, gamma=None, flip=False):
     if gamma:
         x = reference_gamma(x, gamma)
     x = x.to(torch.float32)
-    M = torch.as_tensor(M, dtype=torch.float32, device=x.device)
-    b = torch.as_tensor(bias, dtype=torch.float32, device=x.device)
+    M = torch.as_tensor(np.asarray(M, np.float32) if not isinstance(M, torch.Tensor) else M,
+                        dtype=torch.float32, device=x.device)
+    b = torch.as_tensor(np.asarray(bias, np.float32) if not isinstance(bias, torch.Tensor) else bias,
+                        dtype=torch.float32, device=x.device)
+    if M.dim() == 3:
+        out = torch.einsum('bhwk,bck->bchw', x, M)
+        return out + (b.view(-1, b.shape[-1], 1, 1) if b.dim() == 2 else b.view(1, -1, 1, 1))
     out = torch.einsum('bhwk,ck->bchw', x, M) + b.view(1, -1, 1, 1)
     return out
 
@@ -419,6 +564,13 @@ def decode(images, cfg: DecodeConfig = DecodeConfig(), flip=None, out=None):
         raise ValueError(f'channel map {cfg.cmap} needs more than {C} input channels')
     if cfg.color_matrix is not None:
         return color4x4(x, cfg.color_matrix, cfg.color_bias or [0.0] * 4, gamma=cfg.gamma, flip=cfg.flip)
+    if cfg.color_matrices is not None:
+        if B != len(cfg.color_matrices):
+            raise ValueError(f'decode: {len(cfg.color_matrices)} colour matrices for {B} images')
+        return color4x4(x, cfg.color_matrices, cfg.color_biases, gamma=cfg.gamma, flip=cfg.flip)
+    if cfg.color_jitter is not None:
+        raise ValueError('decode: colour jitter draws its factors in the stream loader; apply given factors with '
+                         'color4x4(images, jitter=factors)')
     if out is None:
         out = torch.empty(cfg.out_shape(B, H, W), dtype=cfg.torch_dtype(), device=x.device)
     lut = device_lut(cfg, x.device)
@@ -442,7 +594,7 @@ def decode_gather(store, index, cfg: DecodeConfig = DecodeConfig(), out=None):
     ext = hip_ext()
     if store.dtype != torch.uint8 or not store.is_cuda or not store.is_contiguous() or store.dim() != 4:
         raise TypeError('decode_gather expects a contiguous uint8 [N,H,W,C] CUDA/HIP tensor')
-    if cfg.color_matrix is not None:
+    if cfg.colour_kernel:
         raise ValueError('decode_gather: colour matrices are not supported; use color4x4 on store[index]')
     N, H, W, C = store.shape
     if max(cfg.cmap) >= C:
@@ -496,7 +648,7 @@ def replay_sample(store, count: int, batch: int, cfg: DecodeConfig = DecodeConfi
     ext = hip_ext()
     if store.dtype != torch.uint8 or not store.is_cuda or store.dim() != 4 or not store.is_contiguous():
         raise TypeError('replay_sample expects a contiguous uint8 [N,H,W,C] device tensor')
-    if cfg.color_matrix is not None:
+    if cfg.colour_kernel:
         raise ValueError('replay_sample does not apply colour matrices (use gather + color4x4)')
     N, H, W, C = store.shape
     if max(cfg.cmap) >= C:
@@ -537,8 +689,13 @@ def replay_sample(store, count: int, batch: int, cfg: DecodeConfig = DecodeConfi
     return out, idx_out, mout
 
 
-def color4x4(images, M, bias=(0.0, 0.0, 0.0, 0.0), gamma=None, flip=False, cout=4):
-    """out[b,c] = M[c,:] . g(in[b,:,y,x]) + bias[c] on the MFMA units (fp32)."""
+def color4x4(images, M=None, bias=(0.0, 0.0, 0.0, 0.0), gamma=None, flip=False, cout=4, jitter=None, pivot=127.5):
+    """out[b,c] = M[c,:] . g(in[b,:,y,x]) + bias[c] on the MFMA units (fp32).
+
+    ``M`` [4, 4] (one transform) or [B, 4, 4] with ``bias`` [4] / [B, 4] (one
+    per image); or ``jitter`` [B, 4] colour-jitter factors (B <= 64), whose
+    transforms the kernel builds itself (:func:`color_jitter_matrix` about
+    ``pivot``, in the units of ``g``: 0..255)."""
     import torch
     ext = hip_ext()
     x = images.contiguous()
@@ -547,7 +704,36 @@ def color4x4(images, M, bias=(0.0, 0.0, 0.0, 0.0), gamma=None, flip=False, cout=
         raise ValueError('color4x4 needs RGBA input')
     if (H * W) % 256 or W % 4:
         raise ValueError('color4x4 needs H*W % 256 == 0 and W % 4 == 0')
-    Mn = np.ascontiguousarray(M, np.float32)
+    if jitter is not None:
+        f = np.ascontiguousarray(jitter, np.float32)
+        if f.shape != (B, 4) or B > 64:
+            raise ValueError('color4x4: jitter must be [B, 4] with B <= 64')
+        lut = device_lut(DecodeConfig(channels='rgba', gamma=gamma, color_matrix=np.eye(4)), x.device)
+        out = torch.empty((B, cout, H, W), dtype=torch.float32, device=x.device)
+        ext.color4x4(x.data_ptr(), out.data_ptr(), lut.data_ptr(), 0, 0, 0, B, H, W, cout, int(flip),
+                     _stream(x.device), 3, 0, f.reshape(-1).tolist(), float(pivot))
+        return out
+    Mt_in = M.detach().to(torch.float32) if isinstance(M, torch.Tensor) else None
+    Mn = None if Mt_in is not None else np.ascontiguousarray(M, np.float32)
+    shape = tuple(Mt_in.shape) if Mt_in is not None else Mn.shape
+    if len(shape) == 3:
+        if shape != (B, 4, 4):
+            raise ValueError(f'color4x4: per-image M must be [{B}, 4, 4]')
+        # one transform per image: [B, 16 + 4] rows on the device
+        Mt = Mt_in.to(x.device).reshape(B, 16) if Mt_in is not None else torch.from_numpy(Mn.reshape(B, 16)).to(x.device)
+        bt = torch.as_tensor(np.asarray(bias, np.float32) if not isinstance(bias, torch.Tensor) else bias,
+                             dtype=torch.float32, device=x.device)
+        bt = bt.expand(B, 4) if bt.dim() == 1 else bt
+        rows = torch.cat([Mt, bt.reshape(B, 4)], dim=1).contiguous()
+        lut = device_lut(DecodeConfig(channels='rgba', gamma=gamma, color_matrix=np.eye(4)), x.device)
+        out = torch.empty((B, cout, H, W), dtype=torch.float32, device=x.device)
+        ext.color4x4(x.data_ptr(), out.data_ptr(), lut.data_ptr(), 0, 0, 0, B, H, W, cout, int(flip),
+                     _stream(x.device), 2, rows.data_ptr(), [], 0.0)
+        return out
+    if Mn is None:
+        Mn = Mt_in.cpu().numpy()
+    if Mn.shape != (4, 4):
+        raise ValueError(f'color4x4: M must be [4, 4] or [{B}, 4, 4]')
     bn = np.ascontiguousarray(bias, np.float32)
     key = ('color4x4', Mn.tobytes(), bn.tobytes(), gamma, str(x.device))
     cached = _lut_cache.get(key)
@@ -1326,7 +1512,7 @@ def decode_lut_bf16(cfg: DecodeConfig, device):
     through (``conv4x4s2(..., lut=)``) -- the same values the decode kernel
     writes for a bf16 NHWC RGBA output.  Cached per (config, device)."""
     import torch
-    if cfg.cmap != [0, 1, 2, 3] or cfg.flip or cfg.color_matrix is not None:
+    if cfg.cmap != [0, 1, 2, 3] or cfg.flip or cfg.colour_kernel:
         raise ValueError('decode_lut_bf16: RGBA identity channel map, no flip, no colour matrix')
     key = (cfg, str(device))
     t = _LUTS.get(key)

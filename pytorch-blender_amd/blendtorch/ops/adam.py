@@ -128,15 +128,24 @@ class FusedAdam(torch.optim.Optimizer):
             gs['hp'][0].fill_(float(group['lr']))
             gs['lr'] = float(group['lr'])
         b1, b2 = group['betas']
-        hip_ext().adam_attach_schedule(gs['step'].data_ptr(), gs['hp'].data_ptr(), gs['sched'].data_ptr(), b1, b2)
-        self._attached = (id(group), gs['lr'])
+        dev = gs['step'].device
+        hip_ext().adam_attach_schedule(gs['step'].data_ptr(), gs['hp'].data_ptr(), gs['sched'].data_ptr(), b1, b2,
+                                       dev.index if dev.index is not None else torch.cuda.current_device(),
+                                       _stream(dev))
+        self._attached = (id(group), gs['lr'], gs)
         return True
 
     def detach_schedule(self):
-        """Drop a schedule :meth:`attach_schedule` handed out and no launch ran
-        (e.g. the backward raised)."""
+        """Drop a schedule :meth:`attach_schedule` handed out (e.g. the
+        backward raised).  If a slice-reduce launch already ran it, the device
+        counter has advanced for an update that will not happen: step it back,
+        so the next update's bias correction is the right one."""
         if self._attached is not None:
-            hip_ext().adam_detach_schedule()
+            ext = hip_ext()
+            taken = bool(ext.adam_schedule_taken())
+            ext.adam_detach_schedule()
+            if taken:
+                self._attached[2]['step'].sub_(1.0)
             self._attached = None
 
     def load_state_dict(self, state_dict):

@@ -280,7 +280,7 @@ class DeviceComm:
             raise RuntimeError(f'rank {r}/{w}: RCCL all-reduce gave {float(t[0])}, expected {want}')
         out['all_reduce_ms'] = (time.perf_counter() - t0) * 1e3
         out['native'] = self.native
-        if self.native:
+        if self.native and os.environ.get('BT_SELFCHECK_GRAPH', '1') != '0':   # (0: diagnostics only)
             out['graph_all_reduce_ms'] = self._selfcheck_graph(wait)
         return out
 
@@ -295,19 +295,18 @@ class DeviceComm:
         dev = self.device
         t = torch.empty((1024,), device=dev)
         acc = torch.zeros((1024,), device=dev)
-        side = torch.cuda.Stream(dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
         g = torch.cuda.CUDAGraph()
         try:
-            with torch.cuda.stream(side):
-                with torch.cuda.graph(g, stream=side, capture_error_mode='thread_local'):
-                    t.fill_(float(r + 1))
-                    self.all_reduce_(t)
-                    acc.add_(t)
+            # torch's shared default capture stream (the one CapturedStep's graphs use
+            # too): a stream of its own here would be one more HIP stream for the
+            # runtime to spread over its few hardware queues for the rest of the run
+            with torch.cuda.device(dev), torch.cuda.graph(g, capture_error_mode='thread_local'):
+                t.fill_(float(r + 1))
+                self.all_reduce_(t)
+                acc.add_(t)
         except RuntimeError as e:
             raise RuntimeError(f'rank {r}/{w}: capturing ncclAllReduce into a HIP graph failed ({e}); async '
                                f'error: {self.async_error() or "none"}') from e
-        torch.cuda.current_stream(dev).wait_stream(side)
         for _ in range(2):
             g.replay()
         wait('graph all_reduce (captured, 2 replays)', 'all')

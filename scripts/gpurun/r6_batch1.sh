@@ -27,9 +27,3 @@ for v in "default:" "nopatch:BT_CONV_FWD_PATCH=0" "atomic:BT_WGRAD_ORDERED=0" "d
 done
 timeout -k 10 300 python bench.py --consumer disc --force-pg --steps 500 > $O/disc_pg1.log 2>&1 || { tail -20 $O/disc_pg1.log; exit 1; }
 grep '^{' $O/disc_pg1.log | tee $O/disc_pg1.jsonl | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'pg1':d['value'],'check':d['allreduce_check'],'coll':d['config']['collectives'],'step':d['config']['consumer_step']}))"
-timeout -k 10 400 python bench.py --gpus 8 --backend gloo --steps 300 --warmup 30 > $O/gloo8.log 2>&1 || { tail -30 $O/gloo8.log; exit 1; }
-grep '^{' $O/gloo8.log | tee $O/gloo8.jsonl | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'gloo8':d['value'],'seen':d['world_size_seen'],'rates':[r['images_per_s'] for r in d['per_rank']],'prod':[r['producers'] for r in d['per_rank']],'cpus':[r['cpus'] for r in d['per_rank']]}))"
-bash scripts/gpurun/disc_trace.sh r6b1 > /dev/null || exit 1
-cp gpurun_out/trace_r6b1/step_sequence.txt $O/disc_step_sequence.txt
-grep -A22 "mean over" $O/disc_step_sequence.txt
-grep "busy\|median step" $O/disc_step_sequence.txt

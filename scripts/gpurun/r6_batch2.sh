@@ -1,6 +1,7 @@
 #!/bin/bash
-# Round 6, GPU session 2: the patch forward's decomposition (which part sets its time), the tests of the
-# new kernels (patch forward, fused densityopt), densityopt 70 epochs x 4 seeds on the fused iteration,
+# Round 6, GPU session 2: the patch forward's decomposition, the tests of the new kernels (patch forward,
+# fused densityopt, per-image colour transforms, mixed-fleet loader), the 1-rank RCCL step with and without the
+# graph self-check stage, densityopt 70 epochs x 4 seeds on the fused iteration,
 # its graph-only steady-state trace (launches and device copies per iteration) and the steady run's phases.
 set -u
 cd "$(dirname "$0")/../.."
@@ -11,9 +12,15 @@ trap 'find gpurun_out -type f -size +4M -print -delete; du -sh gpurun_out' EXIT
 timeout -k 10 120 python scripts/fwd_patch_bench.py > $O/fwd_patch_bench.jsonl 2>&1 || { tail -20 $O/fwd_patch_bench.jsonl; exit 1; }
 cat $O/fwd_patch_bench.jsonl
 timeout -k 10 400 python -u -m pytest -q --timeout 150 --timeout-method thread -p no:cacheprovider -m gpu \
-  tests/test_conv_wgrad.py tests/test_gpu_consumer.py > $O/pytest.log 2>&1
+  tests/test_conv_wgrad.py tests/test_gpu_consumer.py tests/test_gpu_kernels.py tests/test_gpu_loader.py tests/test_adam.py \
+  > $O/pytest.log 2>&1
 rc=$?; tail -3 $O/pytest.log; grep -E "^(FAILED|ERROR)" $O/pytest.log | head -20
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+for v in "graphcheck:" "nographcheck:BT_SELFCHECK_GRAPH=0"; do
+  name=${v%%:*}; e=${v#*:}
+  timeout -k 10 300 env $e python bench.py --consumer disc --force-pg --steps 1000 > $O/disc_pg1.log 2>&1 || { tail -20 $O/disc_pg1.log; exit 1; }
+  grep '^{' $O/disc_pg1.log | tee -a $O/disc_pg1_$name.jsonl | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'v':'$name','pg1':d['value'],'sc':d['allreduce_check'].get('selfcheck')}))"
+done
 timeout -k 10 300 python examples/densityopt/densityopt.py --num-epochs 70 --num-runs 4 --image-every 0 \
   --out-dir $O/dopt_e70 --json $O/dopt_e70.json > $O/dopt_e70.log 2>&1 || { tail -5 $O/dopt_e70.log; exit 1; }
 python -c "

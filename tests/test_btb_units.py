@@ -97,7 +97,8 @@ def test_value_table_arithmetic_forms_reproduce_reference_tables():
             ops.DecodeConfig.densityopt(channels='rgb', gamma=2.2),
             ops.DecodeConfig.raw(), ops.DecodeConfig.raw(channels='rgb'),
             ops.DecodeConfig(channels='bgr', mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225), scale=1 / 255),
-            ops.DecodeConfig(channels='rgba', gamma=1.8, color_matrix=np.eye(4).tolist())]
+            ops.DecodeConfig(channels='rgba', gamma=1.8, color_matrix=np.eye(4).tolist()),
+            ops.DecodeConfig.unit(channels='rgb', gamma=2.2, color_jitter=ops.ColorJitter(0.4, 0.4, 0.4, 0.1))]
     import os
     os.environ['BLENDTORCH_DECODE_XFORM'] = '1'      # the forced arithmetic path (auto keeps the table for gamma)
     try:
@@ -114,7 +115,7 @@ def test_value_table_arithmetic_forms_reproduce_reference_tables():
         gw = t[ops.XF_GAMMA:ops.XF_GAMMA + 64].view(np.uint32)
         tab = np.repeat(gw, 32).view(np.uint8)                  # word i = gamma dword i >> 5 (32 copies)
         assert hdr[1] in (0.0, 32.0)
-        nch = 4 if cfg.color_matrix is not None else cfg.cout
+        nch = 4 if cfg.colour_kernel else cfg.cout
         v = np.arange(256)
         from blendtorch import _native
         for lane in (0, 7, 31):
@@ -127,3 +128,52 @@ def test_value_table_arithmetic_forms_reproduce_reference_tables():
                 z = np.array([_native.xform_apply(op, a, b, d, r, float(xi)) for xi in x], dtype=np.float32)
                 assert op in (0, 1, 3) or cfg.std is not None, (cfg, op)     # division only as the last resort
                 assert np.array_equal(z.view(np.uint32), lut[c].view(np.uint32)), (cfg, c, lane)
+
+
+def test_color_jitter_matrix_and_configs():
+    """ops.color_jitter_matrix: identity factors give the identity, every
+    transform keeps grey grey (rows sum to b*c, bias (1-c)*pivot), and hue /
+    saturation compose as documented; DecodeConfig validates the per-image
+    transforms; the jitter reference with identity factors is the plain decode."""
+    import numpy as np
+    import pytest
+    import torch
+    from blendtorch import ops
+    M, b = ops.color_jitter_matrix([1, 1, 1, 0])
+    np.testing.assert_allclose(M, np.eye(4), atol=1e-7)
+    assert not b.any()
+    rng = np.random.default_rng(0)
+    for _ in range(20):
+        f = [rng.uniform(0.5, 1.5), rng.uniform(0.5, 1.5), rng.uniform(0, 2), rng.uniform(-0.5, 0.5)]
+        M, b = ops.color_jitter_matrix(f, 0.5)
+        np.testing.assert_allclose(M[:3, :3].sum(1), f[0] * f[1], rtol=1e-5)
+        np.testing.assert_allclose(b[:3], (1 - f[1]) * 0.5, rtol=1e-6)
+        assert M[3].tolist() == [0, 0, 0, 1] and not M[:3, 3].any()
+    # saturation 0: every output channel is the luminance
+    M, _ = ops.color_jitter_matrix([1, 1, 0, 0.3])
+    np.testing.assert_allclose(M[:3, :3], np.tile([0.213, 0.715, 0.072], (3, 1)), atol=1e-6)
+    # a full turn of hue is the identity
+    M, _ = ops.color_jitter_matrix([1, 1, 1, 0.5])
+    M2, _ = ops.color_jitter_matrix([1, 1, 1, -0.5])
+    np.testing.assert_allclose(M, M2, atol=1e-6)
+    f = ops.jitter_factors(3, [0.4, 0.2, 0.0, 0.1], 50)
+    assert f.shape == (50, 4) and (f[:, 0] >= 0.6).all() and (f[:, 0] <= 1.4).all()
+    assert (f[:, 2] == 1).all() and (np.abs(f[:, 3]) <= 0.1).all()
+    np.testing.assert_array_equal(f, ops.jitter_factors(3, [0.4, 0.2, 0.0, 0.1], 50))
+    assert not np.array_equal(f, ops.jitter_factors(4, [0.4, 0.2, 0.0, 0.1], 50))
+    with pytest.raises(ValueError):
+        ops.DecodeConfig.unit(channels='bgr', color_jitter=ops.ColorJitter(0.1))
+    with pytest.raises(ValueError):
+        ops.DecodeConfig(color_jitter=ops.ColorJitter(0.1), color_matrix=np.eye(4))
+    with pytest.raises(ValueError):
+        ops.ColorJitter(hue=0.7)
+    with pytest.raises(ValueError):
+        ops.DecodeConfig(channels='rgba', color_matrices=np.zeros((2, 3, 4)))
+    cfg = ops.DecodeConfig(channels='rgba', color_matrices=np.stack([np.eye(4)] * 3))
+    assert cfg.cout == 4 and cfg.colour_kernel and len(cfg.color_biases) == 3
+    x = torch.randint(0, 256, (2, 8, 16, 4), dtype=torch.uint8)
+    jc = ops.DecodeConfig.unit(channels='rgb', gamma=2.2, color_jitter=ops.ColorJitter(0.3, 0.3, 0.3, 0.1))
+    assert jc.cout == 3 and jc.jitter_pivot == 0.5
+    got = ops.reference_decode(x, jc, jitter=[[1, 1, 1, 0]] * 2)
+    want = ops.reference_decode(x, ops.DecodeConfig.unit(channels='rgb', gamma=2.2))
+    torch.testing.assert_close(got, want, rtol=1e-6, atol=1e-6)

@@ -90,6 +90,36 @@ def test_color4x4_identity_layout_probe(dev):
         assert torch.equal(out[0, c].cpu(), xs[0, :, :, k]), (k, c)
 
 
+def test_color4x4_per_image_matrices(dev):
+    """One transform per image ([B, 4, 4] + [B, 4]): every image equals the
+    fp32 reference with its own matrix."""
+    x = _imgs(5, 32, 64, 4, dev, seed=8)
+    rng = np.random.default_rng(5)
+    M = rng.uniform(-1, 1, size=(5, 4, 4)).astype(np.float32)
+    b = rng.normal(size=(5, 4)).astype(np.float32)
+    out = ops.color4x4(x, M, b, gamma=2.2)
+    ref = ops.reference_color4x4(x.cpu(), M, b, gamma=2.2)
+    torch.testing.assert_close(out.cpu(), ref, rtol=1e-5, atol=1e-3)
+    for k in range(5):   # and each image alone through the one-matrix path
+        one = ops.color4x4(x[k:k + 1], M[k], b[k], gamma=2.2)
+        torch.testing.assert_close(out[k:k + 1], one, rtol=1e-5, atol=1e-3)
+
+
+def test_color4x4_jitter_built_in_kernel(dev):
+    """Colour jitter: the kernel builds each image's transform from its 4
+    factors; it must equal reference_color4x4 with ops.color_jitter_matrix
+    per image (atol 1e-3 on 0..255 values), identity factors included."""
+    x = _imgs(6, 48, 64, 4, dev, seed=9)
+    f = np.array([[1, 1, 1, 0], [1.3, 0.7, 1.4, 0.1], [0.6, 1.2, 0.5, -0.2], [1.0, 1.0, 0.0, 0.0],
+                  [0.9, 1.4, 1.2, 0.5], [1.1, 0.9, 0.8, -0.05]], np.float32)
+    out = ops.color4x4(x, jitter=f, gamma=2.2, pivot=127.5)
+    mb = [ops.color_jitter_matrix(r, 127.5) for r in f]
+    ref = ops.reference_color4x4(x.cpu(), np.stack([m for m, _ in mb]), np.stack([b for _, b in mb]), gamma=2.2)
+    torch.testing.assert_close(out.cpu(), ref, rtol=1e-4, atol=1e-3)
+    ident = ops.reference_color4x4(x[:1].cpu(), np.eye(4), [0] * 4, gamma=2.2)
+    torch.testing.assert_close(out[:1].cpu(), ident, rtol=0, atol=1e-3)
+
+
 @pytest.mark.parametrize('flip', [False, True])
 def test_color4x4_full_frame(dev, flip):
     x = _imgs(3, 480, 640, 4, dev, seed=6)

@@ -210,6 +210,75 @@ def test_device_loader_direct_color4x4(dev, free_port):
     torch.testing.assert_close(res['auto'], res['copy'], rtol=0, atol=0)
 
 
+def _known_frames_producer(addr, n, H=48, W=64, shm_slots=0):
+    """A Python producer of n RGBA frames whose pixels are a function of
+    their 'k' (so a test can rebuild what the loader decoded)."""
+    import threading
+    from blendtorch.btb.publisher import DataPublisher
+
+    def frame(k):
+        return np.random.default_rng(1000 + k).integers(0, 256, size=(H, W, 4), dtype=np.uint8)
+
+    pub = DataPublisher(addr, btid=1, lingerms=5000, **({'shm_slots': shm_slots} if shm_slots else {}))
+
+    def produce():
+        for k in range(n):
+            pub.publish(image=frame(k), k=k)
+
+    return threading.Thread(target=produce), pub, frame
+
+
+@pytest.mark.parametrize('shm', [0, 8])
+def test_device_loader_color_jitter_per_image(dev, free_port, shm):
+    """Photometric augmentation on the loader path: every image gets its own
+    random colour transform inside the MFMA decode (direct path), the batch
+    reports the factors, and each image equals the fp32 reference decode with
+    those factors (atol 1e-3); the same seed draws the same factors."""
+    addr = f'tcp://127.0.0.1:{free_port}'
+    jit = ops.ColorJitter(brightness=0.4, contrast=0.4, saturation=0.6, hue=0.2, seed=7)
+    cfg = ops.DecodeConfig.unit(channels='rgb', gamma=2.2, color_jitter=jit)
+    th, pub, frame = _known_frames_producer(addr, 32, shm_slots=shm)
+    dl = DeviceLoader([addr], batch_size=8, max_items=32, device=dev, decode=cfg)
+    th.start()
+    batches = [dict(image=b['image'].clone(), k=b['k'].clone(), f=b['color_jitter'].clone()) for b in dl]
+    th.join()
+    pub.close()
+    assert len(batches) == 4 and dl.stats['direct_batches'] == 4, dl.stats
+    fs = torch.cat([b['f'] for b in batches])
+    assert fs.shape == (32, 4) and len({tuple(r.tolist()) for r in fs}) == 32
+    assert float(fs[:, :3].min()) >= 0.4 - 1e-6 and float(fs[:, 2].max()) <= 1.6 + 1e-6
+    assert float(fs[:, 3].abs().max()) <= 0.2 + 1e-6
+    for b in batches:
+        x = torch.from_numpy(np.stack([frame(int(k)) for k in b['k']]))
+        ref = ops.reference_decode(x, cfg, jitter=b['f'].numpy())
+        assert b['image'].shape == (8, 3, 48, 64)
+        torch.testing.assert_close(b['image'].cpu(), ref, rtol=1e-4, atol=1e-3)
+    # the factors are a function of the seed and the arrival order
+    want = ops.jitter_factors(7, [0.4, 0.4, 0.6, 0.2], 32)
+    np.testing.assert_allclose(fs.numpy(), want, rtol=0, atol=1e-6)
+
+
+def test_device_loader_color_matrices_per_position(dev, free_port):
+    """DecodeConfig(color_matrices=[B,4,4]): batch position i is decoded
+    with transform i, on the direct path."""
+    addr = f'tcp://127.0.0.1:{free_port}'
+    rng = np.random.default_rng(11)
+    M = rng.uniform(-1, 1, size=(4, 4, 4)).astype(np.float32)
+    bb = rng.normal(size=(4, 4)).astype(np.float32)
+    cfg = ops.DecodeConfig(channels='rgba', gamma=2.2, color_matrices=M, color_biases=bb)
+    th, pub, frame = _known_frames_producer(addr, 8)
+    dl = DeviceLoader([addr], batch_size=4, max_items=8, device=dev, decode=cfg)
+    th.start()
+    got = [(b['image'].clone(), b['k'].clone()) for b in dl]
+    th.join()
+    pub.close()
+    assert dl.stats['direct_batches'] == 2
+    for img, ks in got:
+        x = torch.from_numpy(np.stack([frame(int(k)) for k in ks]))
+        ref = ops.reference_color4x4(x, M, bb, gamma=2.2)
+        torch.testing.assert_close(img.cpu(), ref, rtol=1e-5, atol=1e-3)
+
+
 def test_gpu_topology_resolves(dev):
     """hipDeviceGetPCIBusId -> sysfs local_cpulist gives the GPU's NUMA-local CPUs."""
     import os
@@ -355,10 +424,11 @@ def test_device_loader_end_to_end_integrity(dev, free_port, launch_depth):
     for btid, seqs in seen.items():
         assert len(seqs) == len(set(seqs))             # no duplicates
         assert sorted(seqs) == seqs                     # per-producer order preserved
-    # fair fan-in puts inline frames (heap-received: below the pinned pool's
-    # 64 KB threshold) into every batch, so batches take the copy path; the
-    # shm frames were read in place or DMA'd from the registered ring
+    # fair fan-in puts inline frames into every batch: they land in pinned pool
+    # slots (any image-sized frame does), so mixed batches stay on the direct
+    # path beside the shm frames read in place from the registered ring
     assert st['shm_frames'] > 0 and st['batches'] == 750
+    assert st['direct_batches'] > 0, st
 
 
 _MATRIX = [
