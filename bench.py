@@ -137,6 +137,9 @@ def parse_args(argv=None):
     ap.add_argument('--inline-producers', type=int, default=0,
                     help='with --shm: this many of each rank\'s producers send their images inline in the ZMTP '
                          'messages instead (a mixed fleet: inline frames land in pinned slots, batches stay direct)')
+    ap.add_argument('--color-jitter', action='store_true',
+                    help='photometric augmentation in the decode: a random colour transform per image '
+                         '(brightness/contrast/saturation 0.4, hue 0.1) on the MFMA colour kernel, fp32 RGB out')
     ap.add_argument('--codec', choices=['none', 'tile16'], default='none',
                     help='shm frames: none = raw HWC; tile16 = key-frame deltas (the background crosses PCIe once, '
                          'then only the 16x16 tiles that differ from it; csrc/codec/tiledelta.h)')
@@ -368,6 +371,12 @@ def main(argv=None):
     start_port = args.start_port or rp['start_port']
 
     decode = DecodeConfig.unit(channels='rgb', gamma=2.2)
+    if args.color_jitter:
+        if args.consumer != 'none' or args.mode != 'rgba':
+            raise SystemExit('--color-jitter: RGBA frames, no consumer (fp32 RGB output)')
+        from blendtorch.ops import ColorJitter
+        decode = DecodeConfig.unit(channels='rgb', gamma=2.2,
+                                   color_jitter=ColorJitter(0.4, 0.4, 0.4, 0.1, seed=rank))
     amp = args.consumer == 'disc' and args.consumer_dtype == 'bf16'
     # decode inside the consumer's captured step (frames arrive by DMA only)
     step_decode = (args.consumer == 'disc' and args.h2d == 'copy' and args.dist != 'scatter'
@@ -694,7 +703,8 @@ def main(argv=None):
                 'cpus_per_gpu': share,
                 'numa_local': plan['numa_local'],
                 'decode': ('rgba->rgb, gamma 2.2, /255, bf16 NHWC (gfx950 kernel)' if amp else
-                           'rgba->rgb, gamma 2.2, /255, HWC->CHW fp32 (gfx950 kernel)'),
+                           'rgba->rgb, gamma 2.2, /255, per-image colour jitter (MFMA), HWC->CHW fp32 (gfx950 kernel)'
+                           if args.color_jitter else 'rgba->rgb, gamma 2.2, /255, HWC->CHW fp32 (gfx950 kernel)'),
                 'out_shape': list(shape),
                 'proto': args.proto,
                 'pinned_producers': pin,

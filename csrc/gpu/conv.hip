@@ -576,6 +576,130 @@ __device__ __forceinline__ void conv_wgrad_body(const ConvWgradParams& p, char* 
       for (int r = 0; r < 4; ++r) out[(16 * i + r) * KC + 16 * j] = acc[i][j][r];
 }
 
+// 128-channel tiles (BT_WGRAD_CO128, layers with Cout % 128 == 0): a block's
+// tile is 128 output channels x 128 im2col columns, 4 waves of 64 x 64 (16
+// MFMAs per wave and 32-pixel step instead of 8).  Every staged X chunk then
+// feeds twice the channels: per FLOP the block stages 2/3 of the bytes of the
+// 64 x 128 tile (16 KiB per step for 2 MFLOP against 12 KiB for 1), and the
+// L2 -> LDS fills are what the tap-gather GEMMs of this file wait on (the
+// MFMAs of a step are 128 cycles per wave).  Plain variant only (no BN on dY).
+constexpr int BCO2 = 128;
+constexpr int DY2_ROW = BCO2 * 2;             // 256-byte LDS rows (x_off's swizzle)
+constexpr int DY2_TILE = BPX * DY2_ROW;       // 8 KiB
+constexpr int STAGE_CO2 = DY2_TILE + X_TILE;     // 16 KiB
+constexpr int kWgrad2Lds = 2 * STAGE_CO2;
+
+template <int kDepth = 2>
+__device__ __forceinline__ void conv_wgrad_co128_body(const ConvWgradParams& p, char* smem, int bid) {
+  if (run_side(p, smem, bid)) return;
+  const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
+  const int KC = 16 * p.Cin, KT = KC / BKC, T = (p.Cout / BCO2) * KT;
+  const int nwg = main_blocks(p), b = bid;
+  const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  const int slice = w / T, tile = w - slice * T;
+  const int co0 = (tile / KT) * BCO2, kt = tile - (tile / KT) * KT;
+  const int m_begin = slice * int(p.px_per_slice);
+  const int m_end = m_begin + int(p.px_per_slice) < int(p.M) ? m_begin + int(p.px_per_slice) : int(p.M);
+  const int nsteps = m_end > m_begin ? (m_end - m_begin + BPX - 1) / BPX : 0;
+  // staging: dY chunks of pixels dpx and dpx + 16 (16 chunks per 128-channel row), X as the 64-channel body
+  const int dpx = t >> 4, dch = t & 15;
+  const int xpx = t >> 3, xch = t & 7;
+  const int kc = kt * BKC + xch * 8, kc1 = kc + 64;
+  const int cs = __builtin_ctz(unsigned(p.Cin));   // (power-of-two channels: the host checks)
+  const int kh = kc >> (cs + 2), kw = (kc >> cs) & 3, ci = kc & (p.Cin - 1);
+  const int kh1 = kc1 >> (cs + 2), kw1 = (kc1 >> cs) & 3, ci1 = kc1 & (p.Cin - 1);
+  const int dkh = kh1 - kh, dkw = kw1 - kw;
+  const int de = (dkh * p.W + dkw) * p.Cin + (ci1 - ci);
+  XCursor c0;
+  c0.init(m_begin + xpx, p, kh, kw, ci);
+  const int j_col = 2 * BPX * p.Cin, j_row = 2 * (p.W - p.Wo) * p.Cin, j_img = (p.H - 2 * p.Ho) * p.W * p.Cin;
+  const bool single = p.Wo >= BPX;
+  const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(p.x, int64_t(p.N) * p.H * p.W * p.Cin * 2);
+  const __amdgpu_buffer_rsrc_t rs_dy = make_rsrc(p.dy, p.M * p.Cout * 2);
+  // (a 4-deep ring holds the fused launch at 2 waves per SIMD: 150 VGPRs + 88 AGPRs)
+  static_assert(kDepth % 2 == 0, "even ring depth: step parity picks the LDS buffer");
+  struct Stage {
+    uint4 dy0, dy1, x0, x1;
+  };
+  Stage ring[kDepth];
+  int md = m_begin + dpx;
+  uint32_t dy_byte = uint32_t(md) * uint32_t(p.Cout * 2) + uint32_t((co0 + dch * 8) * 2);
+  const uint32_t dy_step = uint32_t(BPX * p.Cout * 2), dy_half = uint32_t(16 * p.Cout * 2);
+  auto load = [&](Stage& r) {
+    r.dy0 = bload(rs_dy, md < m_end ? dy_byte : kOOB);
+    r.dy1 = bload(rs_dy, md + 16 < m_end ? dy_byte + dy_half : kOOB);
+    const int ih = 2 * c0.oh - 1 + kh, iw = 2 * c0.ow - 1 + kw;
+    const bool ok0 = unsigned(ih) < unsigned(p.H) && unsigned(iw) < unsigned(p.W);
+    const bool ok1 = unsigned(ih + dkh) < unsigned(p.H) && unsigned(iw + dkw) < unsigned(p.W);
+    r.x0 = bload(rs_x, ok0 ? uint32_t(c0.e) * 2u : kOOB);
+    r.x1 = bload(rs_x, ok1 ? uint32_t(c0.e + de) * 2u : kOOB);
+    md += BPX;
+    dy_byte += dy_step;
+    c0.advance(p.Ho, p.Wo, j_col, j_row, j_img, single);
+  };
+  const int st_dy0 = x_off(dpx, dch * 16), st_dy1 = x_off(dpx + 16, dch * 16);
+  const int st_x0 = DY2_TILE + x_off(xpx, xch * 16), st_x1 = DY2_TILE + x_off(xpx, (xch + 8) * 16);
+  auto store = [&](const Stage& r, int buf) {
+    char* base = smem + buf * STAGE_CO2;
+    *reinterpret_cast<uint4*>(base + st_dy0) = r.dy0;
+    *reinterpret_cast<uint4*>(base + st_dy1) = r.dy1;
+    *reinterpret_cast<uint4*>(base + st_x0) = r.x0;
+    *reinterpret_cast<uint4*>(base + st_x1) = r.x1;
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int wco = (wave >> 1) * 64, wkc = (wave & 1) * 64;
+  int ra[4], rb[4];
+  {
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ra[i] = x_off(8 * g + q, (wco + 16 * i + 4 * pp) * 2);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) rb[j] = DY2_TILE + x_off(8 * g + q, (wkc + 16 * j + 4 * pp) * 2);
+  }
+#pragma unroll
+  for (int u = 0; u < kDepth; ++u) load(ring[u]);
+  const int padded = (nsteps + kDepth - 1) / kDepth * kDepth;
+  for (int s0 = 0; s0 < padded; s0 += kDepth) {
+#pragma unroll
+    for (int u = 0; u < kDepth; ++u) {
+      const int buf = u & 1;
+      store(ring[u], buf);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      load(ring[u]);
+      const char* base = smem + buf * STAGE_CO2;
+      bf16x8 bm[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bm[j] = frag_at(base, rb[j], 4 * X_ROW);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bf16x8 a = frag_at(base, ra[i], 4 * X_ROW);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  zero_output(p, bid);
+  float* out = p.partial + int64_t(slice) * p.Cout * KC + (co0 + wco + 4 * (lane >> 4)) * KC +
+               (kt * BKC + wkc + (lane & 15));
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[(16 * i + r) * KC + 16 * j] = acc[i][j][r];
+}
+
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3))) void conv_wgrad_co128_kernel(ConvWgradParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[kWgrad2Lds];
+  conv_wgrad_co128_body<>(p, smem, int(blockIdx.x));
+}
+
 template <bool BND, bool PIPE = false>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradParams p) {
   __shared__ __attribute__((aligned(16))) char smem[kWgradLds];
@@ -1250,6 +1374,185 @@ __global__ __launch_bounds__(64 * NW) void conv_wgrad_c4w_kernel(ConvWgradParams
     out[e] = v;
   }
 }
+
+// ---------------------------------------------------------------------------
+// The first layer's weight gradient from a DECODED INPUT PATCH (c4p).  The
+// wave-private kernel above gathers every output pixel's 16 taps straight from
+// the u8 frames each step: a stride-2 4x4 window reads every input pixel 4x,
+// and each read is a dword load plus 4 table lookups and a 16-byte LDS store
+// of the im2col row -- 12 loads, 32 lookups and 6 stores per lane and step,
+// at 206 VGPRs (2 waves per SIMD; profiles/r5/disc_roofline.md: 34 us, 1.9
+// TB/s).  Here a block takes a BAND of R output rows of one image (a slice
+// of R x Wo pixels), decodes the band's 2R + 2 input rows ONCE into LDS
+// ([row][column + 1][4 ch] bf16, the padding columns and rows zero), and
+// reads the MFMA B fragments (32 pixels x 16 im2col columns = 4 taps x 4
+// channels) straight out of that image with the transposing LDS read: lane
+// (q, p) of a 16-lane group addresses output pixel 8g + q at tap (kh = j, kw
+// = p), i.e. input column 2 ow + p of patch row 2 orow + j -- 8 bytes, the
+// pixel's 4 channels.  The 32 such reads of a half-wave hit 20 distinct
+// 8-byte words of one patch row (2 q + p, overlapping lanes broadcast): no
+// bank conflict.  A step then costs a lane 4 dY loads (dY and the BN input
+// of 2 pixels x 8 channels), the BN backward of those 16 values, 2 LDS
+// stores and 8 MFMAs; the decode is one lookup set per input pixel per band.
+// Same slices-then-reduce contract as conv_wgrad_c4w_kernel (slice = band).
+constexpr int kC4pMaxW = 640;                    // input width the static LDS image is sized for
+constexpr int kC4pPW = kC4pMaxW + 2;             // + the two zero padding columns
+template <int R>
+constexpr int c4p_patch() { return (2 * R + 2) * kC4pPW * 8; }
+template <int R>
+constexpr int c4p_lds() {
+  // patch | 4 waves x 2 A tiles (2 KiB each) | decode table; the closing combine of the 4 waves'
+  // 32 x 64 fp32 tiles (32 KiB) and the BN fold's scratch alias the front
+  return c4p_patch<R>() + 4 * 2 * C4W_DY + kLutBytes > 4 * 32 * 64 * 4 ? c4p_patch<R>() + 4 * 2 * C4W_DY + kLutBytes
+                                                                       : 4 * 32 * 64 * 4;
+}
+
+template <int R>
+__global__ __launch_bounds__(kThreads) void conv_wgrad_c4p_kernel(ConvWgradParams p) {
+  constexpr int PR = 2 * R + 2;
+  constexpr int PATCH = c4p_patch<R>();
+  __shared__ __attribute__((aligned(16))) char smem[c4p_lds<R>()];
+  if (run_side(p, smem)) return;
+  char* const patch = smem;
+  char* const lutl = smem + PATCH + 4 * 2 * C4W_DY;
+  const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
+  const int nwg = main_blocks(p), b = int(blockIdx.x);
+  // neighbouring bands share their two halo input rows: keep them on one XCD (its L2)
+  const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int band = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  const int bpi = p.Ho / R;
+  const int n = band / bpi, oh0 = (band - n * bpi) * R;
+  const int m_begin = band * R * p.Wo;
+  const int spr = p.Wo / BPX, nsteps = R * spr;
+  const int PW = p.W + 2;
+  const int dc = lane & 3, dp = lane >> 2;
+  const bool bnd = p.bn_dy.y != nullptr;
+  BnBwdCoef bc[8];
+  if (bnd) {   // (LDS scratch: the front, free until the patch is written)
+    bn_dy_coefs(p.bn_dy, p.Cout, p.M, dc * 8, reinterpret_cast<double*>(smem), reinterpret_cast<int*>(smem + 4096),
+                unsigned(b), unsigned(nwg), bc);
+  }
+  stage_lut(p.lut, lutl);
+  __syncthreads();
+  // the band's input rows 2 oh0 - 1 .. 2 (oh0 + R) decoded once: 8 loads in flight per thread, then lookups
+  {
+    const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(p.x, int64_t(p.N) * p.H * p.W * 4);
+    const int npx = PR * PW, ih0 = 2 * oh0 - 1;
+    for (int i0 = 0; i0 < npx; i0 += 8 * kThreads) {
+      uint32_t wv[8];
+      bool ok[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int i = i0 + k * kThreads + t;
+        const int pr = i / PW, pc = i - pr * PW;
+        const int ih = ih0 + pr, iw = pc - 1;
+        ok[k] = i < npx && unsigned(ih) < unsigned(p.H) && unsigned(iw) < unsigned(p.W);
+        wv[k] = bload4(rs_x, ok[k] ? uint32_t(((n * p.H + ih) * p.W + iw) * 4) : kOOB);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int i = i0 + k * kThreads + t;
+        if (i < npx) *reinterpret_cast<uint2*>(patch + i * 8) = lut_px(lutl, wv[k], ok[k]);
+      }
+    }
+  }
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t rs_dy = make_rsrc(p.dy, p.M * p.Cout * 2);
+  const __amdgpu_buffer_rsrc_t rs_by = make_rsrc(bnd ? p.bn_dy.y : p.dy, p.M * p.Cout * 2);
+  const float slope = p.bn_dy.slope;
+  char* const ws = smem + PATCH + wave * 2 * C4W_DY;
+  int ra[2], rbl[4];
+  {
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) ra[i] = c4dy_off(8 * g + q, (16 * i + 4 * pp) * 2);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) rbl[j] = (j * PW + 2 * (8 * g + q) + pp) * 8;
+  }
+  // steps wave, wave + 4, ...; stage u of the ring holds the dY / BN-input chunks of pixels dp, dp + 16
+  struct Stage {
+    uint4 g[2], y[2];
+  };
+  Stage ring[2];
+  int s_load = wave;
+  auto load = [&](Stage& r) {
+    const bool live = s_load < nsteps;
+    const uint32_t base = uint32_t(m_begin + s_load * BPX + dp) * uint32_t(p.Cout * 2) + uint32_t(dc * 16);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t off = live ? base + uint32_t(h * 16 * p.Cout * 2) : kOOB;
+      r.g[h] = bload(rs_dy, off);
+      if (bnd) r.y[h] = bload(rs_by, off);
+    }
+    s_load += 4;
+  };
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  load(ring[0]);
+  load(ring[1]);
+  const int mysteps = nsteps > wave ? (nsteps - wave + 3) / 4 : 0;
+  const int padded = (mysteps + 1) / 2 * 2;
+  int s = wave;
+  for (int i0 = 0; i0 < padded; i0 += 2) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u, s += 4) {
+      const bool live = s < nsteps;   // (wave-uniform: false on the ring's padding step)
+      const Stage& r = ring[u];
+      char* const A = ws + u * C4W_DY;
+#pragma unroll
+      for (int h = 0; h < 2 && live; ++h) {
+        uint4 d = r.g[h];
+        if (bnd) {   // gx of BN1 from its input (y) and its output gradient (g), rounded to bf16
+          const uint32_t gw[4] = {r.g[h].x, r.g[h].y, r.g[h].z, r.g[h].w}, yw[4] = {r.y[h].x, r.y[h].y, r.y[h].z, r.y[h].w};
+          uint32_t o[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const f32x2 pr = {bc[2 * k].gx(__uint_as_float(yw[k] << 16), __uint_as_float(gw[k] << 16), slope),
+                              bc[2 * k + 1].gx(__uint_as_float(yw[k] & 0xFFFF0000u), __uint_as_float(gw[k] & 0xFFFF0000u),
+                                               slope)};
+            o[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2));
+          }
+          d = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+        *reinterpret_cast<uint4*>(A + c4dy_off(dp + 16 * h, dc * 16)) = d;
+      }
+      load(ring[u]);   // two steps ahead (past the end: out of range, zeros, never used)
+      if (!live) continue;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const int orow = s / spr, ow0 = (s - orow * spr) * BPX;
+      const int sb = (2 * orow * PW + 2 * ow0) * 8;
+      bf16x8 a[2], bm[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = frag_at(A, ra[i], 4 * C4_DY_ROW);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bm[j] = frag_at(patch, sb + rbl[j], 64);   // pixel + 4: column + 8
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bm[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  // combine the 4 waves' tiles: [wave][co 32][kc 64] fp32 over the patch
+  __syncthreads();
+  float* cmb = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        cmb[(wave * 32 + 16 * i + 4 * (lane >> 4) + r) * 64 + 16 * j + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+  zero_output(p);
+  float* out = p.partial + int64_t(band) * p.Cout * 64;
+  for (int e = t; e < 32 * 64; e += kThreads) out[e] = cmb[e] + cmb[2048 + e] + cmb[4096 + e] + cmb[6144 + e];
+}
+
+// rows per band of conv_wgrad_c4p_kernel for this first layer (0: the shape does not take it)
+int c4p_rows_for(int N, int H, int W, int Ho, int Wo, int Cout);
 
 // ---------------------------------------------------------------------------
 // Tap-gather GEMM: the forward convolution AND the data gradient.
@@ -3018,6 +3321,15 @@ int wgrad_wide() {
 // the wide kernel's layers: power-of-two Cin with whole 256-column tiles, plain dY
 bool wgrad_wide_ok(int Cin, int Cout) { return wgrad_wide() && Cin >= 16 && (Cin & (Cin - 1)) == 0 && Cout % BCO == 0; }
 int g_wgrad_pipe = -1;   // register-staged weight gradient: fragments read a step ahead (BT_WGRAD_PIPE)
+// BT_WGRAD_CO128 (default 0): 128-channel weight-gradient tiles (conv_wgrad_co128_body) where Cout % 128 == 0
+int g_wgrad_co128 = -1;
+bool wgrad_co128_ok(int Cin, int Cout) {
+  if (g_wgrad_co128 < 0) {
+    const char* v = std::getenv("BT_WGRAD_CO128");
+    g_wgrad_co128 = v ? (std::atoi(v) ? 1 : 0) : 0;
+  }
+  return g_wgrad_co128 == 1 && Cout % BCO2 == 0 && Cin >= 16 && (Cin & (Cin - 1)) == 0;
+}
 int wgrad_pipe() {
   if (g_wgrad_pipe < 0) {
     const char* v = std::getenv("BT_WGRAD_PIPE");
@@ -3057,6 +3369,26 @@ int c4w_waves() {
   return g_c4w_waves;
 }
 
+// BT_C4W_PATCH (default 1): the first layer's weight gradient from a decoded input patch
+// (conv_wgrad_c4p_kernel) when the shape takes it; BT_C4P_ROWS: output rows per band (1, 2, 4)
+int g_c4p_override = -1;   // conv_set_c4p_rows (tests / benches): -1 = the environment's choice
+int c4p_rows_for(int N, int H, int W, int Ho, int Wo, int Cout) {
+  static const int env_rows = [] {
+    const char* v = std::getenv("BT_C4W_PATCH");
+    if (v && v[0] == '0') return 0;
+    // 4 rows: 27.8 us with the BN backward against 31.3 at 2 rows, 40.8 at 1 and 31.0 for the
+    // wave-private kernel (profiles/r6/b2/c4w_bench.jsonl)
+    const char* r = std::getenv("BT_C4P_ROWS");
+    const int k = r ? std::atoi(r) : 4;
+    return k == 1 || k == 2 || k == 4 ? k : 4;
+  }();
+  const int rows = g_c4p_override >= 0 ? g_c4p_override : env_rows;
+  if (rows == 0 || Cout != 32 || W > kC4pMaxW || W != 2 * Wo || H != 2 * Ho || Wo % BPX != 0 || Ho % rows != 0 ||
+      N <= 0)
+    return 0;
+  return rows;
+}
+
 bool c4_wave_private() {
   if (g_c4w < 0) {
     const char* v = std::getenv("BT_C4_WAVE");
@@ -3080,9 +3412,22 @@ bool conv_wgrad_supported(int Cin, int Cout) {
   return (Cin >= 32 && Cin % 32 == 0 && Cout >= 64 && Cout % 64 == 0) || (Cin == 4 && Cout % 32 == 0 && Cout > 0);
 }
 
+int conv_c4p_rows(int N, int H, int W, int Ho, int Wo, int Cout) { return c4p_rows_for(N, H, W, Ho, Wo, Cout); }
+void conv_set_wgrad_co128(int on) { g_wgrad_co128 = on < 0 ? -1 : (on ? 1 : 0); }
+void conv_set_c4p_rows(int rows) { g_c4p_override = rows == 0 || rows == 1 || rows == 2 || rows == 4 ? rows : -1; }
+
 int conv_wgrad_slices(int64_t M, int Cin, int Cout, int target_blocks) {
   if (!conv_wgrad_supported(Cin, Cout) || M <= 0) return 0;
-  const int64_t tiles = Cin == 4 ? Cout / 32 : int64_t(Cout / BCO) * (16 * Cin / (wgrad_wide_ok(Cin, Cout) ? BKC2 : BKC));
+  const int64_t tiles = Cin == 4 ? Cout / 32 : wgrad_co128_ok(Cin, Cout) ? int64_t(Cout / BCO2) * (16 * Cin / BKC)
+                                          : int64_t(Cout / BCO) * (16 * Cin / (wgrad_wide_ok(Cin, Cout) ? BKC2 : BKC));
+  // 128-channel tiles: half the blocks by default (each stages twice the channels; the same
+  // partial volume, [slices][Cout][KC], as the 64-channel tiles at the full target)
+  static const int co128_div = [] {
+    const char* v = std::getenv("BT_WGRAD_CO128_DIV");
+    const int d = v ? std::atoi(v) : 2;
+    return d >= 1 ? d : 2;
+  }();
+  if (Cin != 4 && wgrad_co128_ok(Cin, Cout)) target_blocks = (target_blocks + co128_div - 1) / co128_div;
   int64_t s = (target_blocks + tiles - 1) / tiles;
   const int64_t max_s = (M + BPX - 1) / BPX;
   s = s < 1 ? 1 : (s > max_s ? max_s : s);
@@ -3109,10 +3454,11 @@ hipError_t conv_wgrad_reduce(const ConvWgradParams::Reduce& r, hipStream_t strea
 // it in its own apply).  conv_dgrad holds its tap-GEMM launch while
 // conv_dgrad_hold(1) is set; the next conv_wgrad on that stream launches
 // both, or conv_dgrad_flush launches the data gradient alone.
-template <int BM, bool PIPE>
-__global__ __launch_bounds__(kThreads) void dgrad_wgrad_kernel(TapGemm g, ConvWgradParams q, int gx, int nd, int nw) {
+template <int BM, bool PIPE, bool W2 = false>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(W2 ? 3 : 1))) void dgrad_wgrad_kernel(TapGemm g, ConvWgradParams q, int gx, int nd, int nw) {
   constexpr int TL = tap_gemm_lds<true, 64, false, BM, 2>();
-  __shared__ __attribute__((aligned(16))) char smem[TL > kWgradLds ? TL : kWgradLds];
+  constexpr int WL = W2 ? kWgrad2Lds : kWgradLds;
+  __shared__ __attribute__((aligned(16))) char smem[TL > WL ? TL : WL];
   const int b = int(blockIdx.x);
   const int nd8 = (nd + 7) & ~7, nw8 = (nw + 7) & ~7, m8 = nd8 < nw8 ? nd8 : nw8;
   int kind, idx;
@@ -3129,7 +3475,8 @@ __global__ __launch_bounds__(kThreads) void dgrad_wgrad_kernel(TapGemm g, ConvWg
     tap_gemm_body<true, 64, false, BM, 2, 1, 0>(g, smem, idx % gx, idx / gx, gx);
   } else {
     if (idx >= nw) return;
-    conv_wgrad_body<false, PIPE>(q, smem, idx);
+    if constexpr (W2) conv_wgrad_co128_body<>(q, smem, idx);
+    else conv_wgrad_body<false, PIPE>(q, smem, idx);
   }
 }
 
@@ -3195,8 +3542,11 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
     return hipErrorInvalidValue;   // 32-bit buffer offsets
   const bool c4 = p.Cin == 4;
   // 256-column tiles (BT_WGRAD_WIDE): the plain register-staged path only
-  const bool wide = !c4 && wgrad_wide_ok(p.Cin, p.Cout) && !p.bn_dy.y && wgrad_staging() == 0;
-  const int64_t tiles = c4 ? p.Cout / 32 : int64_t(p.Cout / BCO) * (16 * p.Cin / (wide ? BKC2 : BKC));
+  // 128-channel tiles: the plain path only (its slices were counted with them: conv_wgrad_slices)
+  const bool co128 = !c4 && wgrad_co128_ok(p.Cin, p.Cout) && !p.bn_dy.y;
+  const bool wide = !c4 && !co128 && wgrad_wide_ok(p.Cin, p.Cout) && !p.bn_dy.y && wgrad_staging() == 0;
+  const int64_t tiles = c4 ? p.Cout / 32 : co128 ? int64_t(p.Cout / BCO2) * (16 * p.Cin / BKC)
+                                               : int64_t(p.Cout / BCO) * (16 * p.Cin / (wide ? BKC2 : BKC));
   const int64_t blocks = tiles * p.slices;
   if (blocks > (int64_t(1) << 31) - 1) return hipErrorInvalidValue;
   ConvWgradParams q = p;
@@ -3223,7 +3573,7 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
   bool fused = false;
   if (g_held.on) {   // a held data gradient: one launch for both when this is the plain kernel's case
     const bool dma = (wgrad_staging() == 2 || wgrad_staging() == 3) && (p.Cin & (p.Cin - 1)) == 0 && p.Wo >= 32;
-    const bool plain = !c4 && !bn_folds && !p.bn_dy.y && !p.fold.acc && !dma && !wide;
+    const bool plain = !c4 && !bn_folds && !p.bn_dy.y && !p.fold.acc && !dma && !wide && (!co128 || !wgrad_pipe());
     const int64_t nd = int64_t(g_held.gx) * (g_held.patch ? 1 : 4);
     if (plain && stream == g_held.s && nd + grid + 16 < (int64_t(1) << 31)) {
       const unsigned total = unsigned(((nd + 7) & ~int64_t(7)) + ((grid + 7) & ~int64_t(7)));
@@ -3232,6 +3582,10 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
         dpatch_wgrad_kernel<true><<<total, kThreads, 0, stream>>>(g_held.g, q, ndi, nwi);
       else if (g_held.patch)
         dpatch_wgrad_kernel<false><<<total, kThreads, 0, stream>>>(g_held.g, q, ndi, nwi);
+      else if (co128 && g_held.bm == 64)
+        dgrad_wgrad_kernel<64, false, true><<<total, kThreads, 0, stream>>>(g_held.g, q, gx, ndi, nwi);
+      else if (co128)
+        dgrad_wgrad_kernel<FBM, false, true><<<total, kThreads, 0, stream>>>(g_held.g, q, gx, ndi, nwi);
       else if (g_held.bm == 64 && wgrad_pipe())
         dgrad_wgrad_kernel<64, true><<<total, kThreads, 0, stream>>>(g_held.g, q, gx, ndi, nwi);
       else if (g_held.bm == 64)
@@ -3247,7 +3601,12 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
       if (e != hipSuccess) return e;
     }
   }
+  const int c4p = c4 && p.lut ? c4p_rows_for(p.N, p.H, p.W, p.Ho, p.Wo, p.Cout) : 0;
   if (fused) {
+  } else if (c4p > 0 && p.px_per_slice == int64_t(c4p) * p.Wo && int64_t(p.slices) * p.px_per_slice == p.M) {
+    if (c4p == 1) conv_wgrad_c4p_kernel<1><<<unsigned(grid), kThreads, 0, stream>>>(q);
+    else if (c4p == 2) conv_wgrad_c4p_kernel<2><<<unsigned(grid), kThreads, 0, stream>>>(q);
+    else conv_wgrad_c4p_kernel<4><<<unsigned(grid), kThreads, 0, stream>>>(q);
   } else if (c4 && (c4_wave_private() || bn_folds)) {
     const bool u8 = p.lut != nullptr;
     static const bool ldsc = std::getenv("BT_C4W_LDS_COEF") && std::getenv("BT_C4W_LDS_COEF")[0] == '1';
@@ -3259,6 +3618,7 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
     else conv_wgrad_c4w_kernel<4, false><<<unsigned(grid), kThreads, 0, stream>>>(q);
   }
   else if (c4) conv_wgrad_c4_kernel<<<unsigned(grid), kThreads, 0, stream>>>(q);
+  else if (co128) conv_wgrad_co128_kernel<<<unsigned(grid), kThreads, 0, stream>>>(q);
   else if (bn_folds && wgrad_pipe()) conv_wgrad_kernel<true, true><<<unsigned(grid), kThreads, 0, stream>>>(q);
   else if (bn_folds) conv_wgrad_kernel<true><<<unsigned(grid), kThreads, 0, stream>>>(q);
   else if (wgrad_staging() == 2 && (p.Cin & (p.Cin - 1)) == 0 && p.Wo >= 32)
@@ -3412,13 +3772,35 @@ int conv1_bn_resident() {
 int64_t conv1_tiles_of(int N, int Ho, int Wo, int tr) {
   return int64_t(N) * ((Ho + tr - 1) / tr) * ((Wo + kC1Cols - 1) / kC1Cols);
 }
-// the 32 -> 64 forward as the persistent patch GEMM (conv_fwd_patch_kernel); BT_CONV_FWD_PATCH=0: the tap GEMM
+// A launch whose blocks meet at grid_barrier: outside a graph capture it goes
+// through hipLaunchCooperativeKernel, which checks that the whole grid is
+// co-resident with what else runs on the device (another stream's kernels, another
+// process) and fails instead of starting blocks that would spin into the barrier's
+// timeout -- the caller (ops.conv_fwd) then runs the plain forward and the separate
+// BN apply.  Inside a capture (cooperative launches are not captured) the plain
+// launch, sized by the occupancy query (conv_out_bn_fits); the barrier's timeout
+// flag still catches a grid that was not resident.
+template <typename... A>
+hipError_t launch_grid_barrier(void (*kernel)(A...), dim3 grid, hipStream_t stream, A... args) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &st) == hipSuccess && st == hipStreamCaptureStatusNone) {
+    void* argv[] = {static_cast<void*>(&args)...};
+    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(kernel), grid, dim3(kThreads), argv, 0, stream);
+  }
+  kernel<<<grid, kThreads, 0, stream>>>(args...);
+  return hipGetLastError();
+}
+
+// the 32 -> 64 forward as the persistent patch GEMM (conv_fwd_patch_kernel), BT_CONV_FWD_PATCH=1; default
+// the tap GEMM: alone the patch kernel is 22.5 us against 23.6, but 7.3 us of it is a fixed cost (the
+// weights' 64 KB per CU and one block per CU), and in the step the tap GEMM's launch ran faster
+// (20.95k vs 20.7k img/s, profiles/r6/b1/disc_*.jsonl, profiles/r6/b2/fwd_patch_bench.jsonl)
 int g_fwd_patch = -1;
 int g_fwd_patch_dbg = 0, g_fwd_patch_blocks = 0;   // (experiments: conv_set_fwd_patch)
 bool fwd_patch() {
   if (g_fwd_patch < 0) {
     const char* v = std::getenv("BT_CONV_FWD_PATCH");
-    g_fwd_patch = v && v[0] == '0' ? 0 : 1;
+    g_fwd_patch = v && v[0] == '1' ? 1 : 0;
   }
   return g_fwd_patch == 1;
 }
@@ -3600,9 +3982,8 @@ hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream) {
       return hipErrorInvalidValue;
     g.oact = p.out_act, g.oy = p.out_y;
     const dim3 grid(unsigned((p.M + bm - 1) / bm * (p.Cout / 64)));
-    if (bm == 64) tap_gemm_kernel<false, 64, false, 64, 2, 1, 0, true><<<grid, kThreads, 0, stream>>>(g);
-    else tap_gemm_kernel<false, 64, false, FBM, 2, 1, 0, true><<<grid, kThreads, 0, stream>>>(g);
-    return hipGetLastError();
+    if (bm == 64) return launch_grid_barrier(tap_gemm_kernel<false, 64, false, 64, 2, 1, 0, true>, grid, stream, g);
+    return launch_grid_barrier(tap_gemm_kernel<false, 64, false, FBM, 2, 1, 0, true>, grid, stream, g);
   }
   if (p.out_act.on()) {   // the output's BN applied here too (grid barrier): checked again, as the caller asked
     if (p.Cin != 4 || !p.lut || !p.stats || g.acc_r <= 0 || !p.out_y || p.Cout != 32 || bn1 != 32 ||
@@ -3613,8 +3994,7 @@ hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream) {
     Conv1Bn ob;
     ob.act = p.out_act, ob.y = p.out_y;
     const unsigned blocks = unsigned((conv1_tiles_of(p.N, p.Ho, p.Wo, 2) + kConv1Keep - 1) / kConv1Keep);
-    conv1_fwd_kernel<32, 2, true, kConv1Keep><<<blocks, kThreads, 0, stream>>>(g, kConv1Keep, ob);
-    return hipGetLastError();
+    return launch_grid_barrier(conv1_fwd_kernel<32, 2, true, kConv1Keep>, dim3(blocks), stream, g, kConv1Keep, ob);
   }
   if (p.Cin == 4 && (!p.stats || g.acc_r > 0) && p.Cout == bn1 && conv1_tiles() > 0) {
     const int tr = conv1_rows(), tpb = conv1_tiles();

@@ -298,6 +298,9 @@ PYBIND11_MODULE(_hip, m) {
         });
 
   m.def("conv_wgrad_slices", &conv_wgrad_slices);
+  m.def("conv_c4p_rows", &conv_c4p_rows);
+  m.def("conv_set_c4p_rows", &conv_set_c4p_rows);
+  m.def("conv_set_wgrad_co128", &conv_set_wgrad_co128);
   m.def("conv_dgrad_hold", [](int on) { conv_dgrad_hold(on); });
   m.def("conv_dgrad_flush", []() { check(conv_dgrad_flush(), "conv_dgrad_flush"); });
   m.def("conv_dgrad_held", []() { return conv_dgrad_held(); });

@@ -1630,6 +1630,11 @@ def conv_wgrad(x, dy, out, target_blocks=None, chain=None, last=True, lut=None, 
     px = -(-M // slices)
     px = -(-px // 32) * 32
     slices = -(-M // px)
+    # the u8 first layer from a decoded input patch: its slices are bands of whole output rows
+    rows = ext.conv_c4p_rows(N, H, W, Ho, Wo, Cout) if (lut is not None and Cin == 4) else 0
+    if rows > 0:
+        px = rows * Wo
+        slices = M // px
     partial = torch.empty(slices * Cout * 16 * Cin, dtype=torch.float32, device=x.device)
     _count('conv_wgrad')
     side = chain.pending if chain is not None else None
@@ -1743,10 +1748,25 @@ def conv_fwd(x, w16, stats=None, acc_r=0, lut=None, act=None, act_out=None, out_
             oargs = out_bn.args(stats, acc_r, N * Ho * Wo)
             _count('conv_fwd_bn_apply')
             _grid_barrier_armed()
-    ext.conv_fwd(x.data_ptr(), w16.data_ptr(), y.data_ptr(), stats.data_ptr() if stats is not None else 0,
-                 N, H, W, Cin, Ho, Wo, Cout, _stream(x.device), wc if Cin == 4 else 0, int(acc_r),
-                 lut.data_ptr() if lut is not None else 0, act.take() if act is not None else None,
-                 act_out.data_ptr() if act_out is not None else 0, oargs, oy.data_ptr() if oy is not None else 0)
+    actp = act.take() if act is not None else None
+
+    def launch(oargs, oy):
+        ext.conv_fwd(x.data_ptr(), w16.data_ptr(), y.data_ptr(), stats.data_ptr() if stats is not None else 0,
+                     N, H, W, Cin, Ho, Wo, Cout, _stream(x.device), wc if Cin == 4 else 0, int(acc_r),
+                     lut.data_ptr() if lut is not None else 0, actp,
+                     act_out.data_ptr() if act_out is not None else 0, oargs, oy.data_ptr() if oy is not None else 0)
+    if oargs is not None:
+        try:
+            launch(oargs, oy)
+        except RuntimeError:
+            # the cooperative launch of the grid-barrier kernel was refused (its grid is
+            # not co-resident with what else runs on the device): nothing ran -- the
+            # plain forward, and the BatchNorm applies itself
+            _count('conv_fwd_bn_apply_refused')
+            oargs, oy = None, None
+            launch(None, None)
+    else:
+        launch(None, None)
     if oy is not None:
         out_bn.y, out_bn.z = oy, y
     return y

@@ -280,8 +280,23 @@ class DeviceComm:
             raise RuntimeError(f'rank {r}/{w}: RCCL all-reduce gave {float(t[0])}, expected {want}')
         out['all_reduce_ms'] = (time.perf_counter() - t0) * 1e3
         out['native'] = self.native
-        if self.native and os.environ.get('BT_SELFCHECK_GRAPH', '1') != '0':   # (0: diagnostics only)
-            out['graph_all_reduce_ms'] = self._selfcheck_graph(wait)
+        mode = os.environ.get('BT_SELFCHECK_GRAPH', 'temp')   # temp (default) | same | 0 (diagnostics)
+        if self.native and mode != '0':
+            if mode == 'same':
+                out['graph_all_reduce_ms'] = self._selfcheck_graph(wait)
+            else:
+                # on a temporary communicator over the same ranks, destroyed afterwards: a
+                # graph-captured collective on the training step's own communicator left it
+                # ~25 % slower for the rest of the run (15.2k vs 20.9k img/s on the 1-rank
+                # disc step, profiles/r6/b2/disc_pg1_*.jsonl)
+                sub = dist.new_group(ranks=dist.get_process_group_ranks(self.group), backend='nccl')
+                tmp = DeviceComm(group=sub, device=self.device)
+                try:
+                    out['graph_all_reduce_ms'] = tmp._selfcheck_graph(wait)
+                finally:
+                    tmp.close()
+                    torch.cuda.synchronize(self.device)
+                    dist.destroy_process_group(sub)
         return out
 
     def _selfcheck_graph(self, wait) -> float:

@@ -25,6 +25,7 @@ from conv_bench import timed  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--iters', type=int, default=200)
+    ap.add_argument('--patch-only', action='store_true', help='the c4p kernel against the default c4w only')
     a = ap.parse_args()
     dev = torch.device('cuda', 0)
     cl = torch.channels_last
@@ -47,7 +48,32 @@ def main():
     out = torch.empty(C, 3, 4, 4, device=dev)
     ref = torch.nn.grad.conv2d_weight(x_bf.float()[:, :3], (C, 3, 4, 4), dy.float(), stride=2, padding=1)
     rows = []
+    ap_only = a.patch_only
     for bn in (False, True):
+        # the decoded-patch kernel (conv_wgrad_c4p_kernel, u8 only): bands of 1, 2, 4 output rows
+        for r in (1, 2, 4):
+            ext.conv_set_c4p_rows(r)
+            x = x_u8
+            bnd = (y, mean, invstd, bw, bb, dw, db, 0.2) if bn else None
+            fn = lambda: ops.conv_wgrad(x, dy, out, lut=lut, bn_dy=bnd)
+            us = timed(fn, a.iters)
+            row = {'kernel': 'c4p', 'bn_dy': bn, 'u8': True, 'rows': r, 'us': round(us, 2)}
+            if not bn:
+                fn()
+                row['rel_err'] = float(f'{float((out - ref).abs().max() / ref.abs().max()):.2e}')
+            print(json.dumps(row), flush=True)
+            rows.append(row)
+        ext.conv_set_c4p_rows(0)
+        if ap_only:
+            for tb in (512,):
+                x = x_u8
+                bnd = (y, mean, invstd, bw, bb, dw, db, 0.2) if bn else None
+                fn = lambda: ops.conv_wgrad(x, dy, out, target_blocks=tb, lut=lut, bn_dy=bnd)
+                row = {'kernel': 'c4w', 'bn_dy': bn, 'u8': True, 'waves': 4, 'target_blocks': tb,
+                       'us': round(timed(fn, a.iters), 2)}
+                print(json.dumps(row), flush=True)
+            ext.conv_set_c4p_rows(-1)
+            continue
         for u8 in (True, False):
             for nw in (4, 8):
                 for tb in (256, 512, 768, 1024):
@@ -63,6 +89,7 @@ def main():
                     print(json.dumps(row), flush=True)
                     rows.append(row)
     ext.conv_set_c4w_waves(-1)
+    ext.conv_set_c4p_rows(-1)
 
 
 if __name__ == '__main__':

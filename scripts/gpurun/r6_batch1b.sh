@@ -9,7 +9,7 @@ mkdir -p $O
 export TMPDIR=/tmp
 trap 'find gpurun_out -type f -size +4M -print -delete; du -sh gpurun_out' EXIT
 summ() { python -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'v':'$1','img_s':d['value'],'share':d.get('producer_share_max_over_min'),'direct':d['loader_stats'].get('direct_batches'),'batches':d['loader_stats'].get('batches'),'staged':d['loader_stats'].get('staged_frames'),'fallbacks':d['loader_stats'].get('pool_fallbacks'),'cpu':d.get('cpu',{}).get('us_per_frame')}))"; }
-for v in "shm6:--producers 6" "mixed3x3:--producers 6 --inline-producers 3" "tcp4:--proto tcp --shm 0 --producers 4" "tcp4_io4:--proto tcp --shm 0 --producers 4 --io-threads 4" "tcp8:--proto tcp --shm 0 --producers 8" "tcp8_io4:--proto tcp --shm 0 --producers 8 --io-threads 4" "ipc8_inline:--shm 0 --producers 8"; do
+for v in "jitter:--color-jitter" "shm6:--producers 6" "mixed3x3:--producers 6 --inline-producers 3" "tcp4:--proto tcp --shm 0 --producers 4" "tcp4_io4:--proto tcp --shm 0 --producers 4 --io-threads 4" "tcp8:--proto tcp --shm 0 --producers 8" "tcp8_io4:--proto tcp --shm 0 --producers 8 --io-threads 4" "ipc8_inline:--shm 0 --producers 8"; do
   name=${v%%:*}; a=${v#*:}
   timeout -k 10 240 python bench.py $a --steps 2000 > $O/fleet.log 2>&1 || { tail -5 $O/fleet.log; exit 1; }
   grep '^{' $O/fleet.log | tee -a $O/fleet_$name.jsonl | summ $name

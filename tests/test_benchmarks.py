@@ -49,3 +49,22 @@ def test_sweep_rows_carry_reference_and_producers(monkeypatch, capsys):
     assert r5['reference_row']['sec_per_image'] == 0.011 and r5['reference_row']['note'] == 'no UI refresh'
     assert r5['ratio_vs_reference_row'] == round(0.011 * 5000, 1)
     assert rows[2]['reference_row'] is None and rows[0]['cpus'] == 16 and 'stand-in' in rows[0]['producer']
+
+
+def test_bench_cli_fleet_and_jitter_flags():
+    """bench.py's mixed-fleet and colour-jitter switches parse (the GPU runs
+    are in profiles/r6/), and the loader gives every TCP pipe its own receive
+    thread while ipc:// loaders keep at most 4."""
+    import importlib.util
+    from helpers import ROOT
+    spec = importlib.util.spec_from_file_location('bench_cli', ROOT / 'bench.py')
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    a = mod.parse_args(['--producers', '6', '--inline-producers', '3', '--color-jitter'])
+    assert a.inline_producers == 3 and a.color_jitter and a.shm > 0
+    from blendtorch.btt.gpu import _default_io_threads
+    assert _default_io_threads(['ipc:///tmp/a'] * 8) == 4
+    assert _default_io_threads(['ipc:///tmp/a']) == 1
+    import os
+    cpus = len(os.sched_getaffinity(0))
+    assert _default_io_threads(['tcp://127.0.0.1:5000'] * 8) == min(8, max(4, cpus - 2))

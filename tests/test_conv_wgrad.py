@@ -24,15 +24,18 @@ def _ref(x, dy, cout):
     return torch.nn.grad.conv2d_weight(x.float(), (cout, x.shape[1], 4, 4), dy.float(), stride=2, padding=1)
 
 
-@pytest.fixture(params=['plain', 'pipe', 'wide'])
+@pytest.fixture(params=['plain', 'pipe', 'wide', 'co128'])
 def wgrad_pipe(request):
     """Register-staged weight gradient: plain, fragments read a step ahead of the MFMAs
-    (pipe), or 256-column tiles (wide; layers with Cin >= 16, plain dY)."""
+    (pipe), 256-column tiles (wide; layers with Cin >= 16, plain dY), or 128-channel
+    tiles (co128; layers with Cout % 128 == 0, plain dY)."""
     ops.hip_ext().conv_set_wgrad_pipe(1 if request.param == 'pipe' else 0)
     ops.hip_ext().conv_set_wgrad_wide(1 if request.param == 'wide' else 0)
+    ops.hip_ext().conv_set_wgrad_co128(1 if request.param == 'co128' else 0)
     yield request.param
     ops.hip_ext().conv_set_wgrad_pipe(-1)
     ops.hip_ext().conv_set_wgrad_wide(-1)
+    ops.hip_ext().conv_set_wgrad_co128(-1)
 
 
 @pytest.fixture(params=[0, 2, 3], ids=lambda s: f'staging{s}')
@@ -390,6 +393,60 @@ def test_wgrad_chain_defers_slice_reduces(dev):
     assert ops.KERNEL_CALLS.get('conv_wgrad_side_reduce', 0) == before + 3
     for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
         torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-4, atol=1e-6 + 1e-4 * float(pb.grad.abs().max()), msg=n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('rows', [1, 2, 4])
+@pytest.mark.parametrize('bn', [False, True])
+def test_first_layer_wgrad_from_decoded_patch(dev, rows, bn):
+    """conv_wgrad_c4p_kernel (bands of output rows, the input decoded once into
+    LDS, B fragments read from it): against fp32 PyTorch on the decoded frames
+    and against the wave-private kernel, with and without the BN1 backward
+    applied to dY while it is staged."""
+    cl = torch.channels_last
+    ext = ops.hip_ext()
+    cfg = ops.DecodeConfig.unit(channels='rgba', gamma=2.2, dtype='bfloat16', layout='nhwc')
+    g = torch.Generator(device=dev).manual_seed(11)
+    N, H, W, C = 3, 96, 128, 32
+    raw = torch.randint(0, 256, (N, H, W, 4), dtype=torch.uint8, device=dev, generator=g)
+    xu8 = raw.permute(0, 3, 1, 2)
+    xdec = ops.decode(raw, cfg).permute(0, 3, 1, 2)
+    lut = ops.decode_lut_bf16(cfg, dev)
+    dy = (torch.randn(N, C, H // 2, W // 2, device=dev, generator=g) * 0.1).to(torch.bfloat16).contiguous(memory_format=cl)
+    bnd = None
+    if bn:
+        y = torch.randn(N, H // 2, W // 2, C, device=dev, generator=g).to(torch.bfloat16)
+        mean = torch.randn(C, device=dev, generator=g) * 0.1
+        invstd = torch.rand(C, device=dev, generator=g) + 0.5
+        bw = torch.rand(C, device=dev, generator=g) + 0.5
+        bb = torch.randn(C, device=dev, generator=g) * 0.1
+        dws = torch.randn(C, device=dev, generator=g) * 10
+        dbs = torch.randn(C, device=dev, generator=g) * 10
+        bnd = (y, mean, invstd, bw, bb, dws, dbs, 0.2)
+    try:
+        ext.conv_set_c4p_rows(rows)
+        assert ext.conv_c4p_rows(N, H, W, H // 2, W // 2, C) == rows
+        got = ops.conv_wgrad(xu8, dy, torch.empty(C, 3, 4, 4, device=dev), lut=lut, bn_dy=bnd)
+        ext.conv_set_c4p_rows(0)
+        assert ext.conv_c4p_rows(N, H, W, H // 2, W // 2, C) == 0
+        wave = ops.conv_wgrad(xu8, dy, torch.empty(C, 3, 4, 4, device=dev), lut=lut, bn_dy=bnd)
+    finally:
+        ext.conv_set_c4p_rows(-1)
+    if bn:   # the BN backward's gx in fp32, rounded to bf16 as the kernels stage it
+        yf = y.float().permute(0, 3, 1, 2)
+        xh = (yf - mean.view(1, -1, 1, 1)) * invstd.view(1, -1, 1, 1)
+        z = xh * bw.view(1, -1, 1, 1) + bb.view(1, -1, 1, 1)
+        gz = torch.where(z > 0, dy.float(), dy.float() * 0.2)
+        M = N * (H // 2) * (W // 2)
+        gx = bw.view(1, -1, 1, 1) * invstd.view(1, -1, 1, 1) * (gz - dbs.view(1, -1, 1, 1) / M
+                                                             - xh * dws.view(1, -1, 1, 1) / M)
+        dyr = gx.to(torch.bfloat16).float()
+    else:
+        dyr = dy.float()
+    ref = torch.nn.grad.conv2d_weight(xdec.float()[:, :3], (C, 3, 4, 4), dyr, stride=2, padding=1)
+    torch.testing.assert_close(got, ref, rtol=1e-3, atol=2e-3 * float(ref.abs().max()))
+    # the same bf16 operands summed in another order: equal to fp32 rounding
+    torch.testing.assert_close(got, wave, rtol=1e-4, atol=1e-4 * float(wave.abs().max()))
 
 
 @pytest.mark.gpu
@@ -970,8 +1027,9 @@ def test_fused_data_and_weight_gradient_launch(dev):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('co128', [0, 1], ids=['co64', 'co128'])
 @pytest.mark.parametrize('cin,cout,hw', [(64, 128, (60, 80)), (128, 256, (30, 40)), (64, 128, (12, 18))])
-def test_dgrad_wgrad_kernel_matches_separate_launches(dev, cin, cout, hw):
+def test_dgrad_wgrad_kernel_matches_separate_launches(dev, cin, cout, hw, co128):
     """One layer, direct ops: conv_dgrad held + conv_wgrad (one launch) give
     the bit-identical data gradient and the same weight gradient as the two
     launches (odd shapes: partial tiles and runs of 8 padded with exiting
@@ -983,6 +1041,7 @@ def test_dgrad_wgrad_kernel_matches_separate_launches(dev, cin, cout, hw):
     dy = torch.randn(8, cout, H // 2, W // 2, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
     w = (0.05 * torch.randn(cout, cin, 4, 4, device=dev, generator=g)).to(torch.bfloat16).contiguous(memory_format=cl)
     ext = ops.hip_ext()
+    ext.conv_set_wgrad_co128(co128)
     outs = []
     for fuse in (False, True):
         if fuse:
@@ -996,6 +1055,7 @@ def test_dgrad_wgrad_kernel_matches_separate_launches(dev, cin, cout, hw):
         assert not ext.conv_dgrad_held()
         torch.cuda.synchronize()
         outs.append((dx, gw))
+    ext.conv_set_wgrad_co128(-1)
     assert torch.equal(outs[0][0], outs[1][0])
     torch.testing.assert_close(outs[1][1], outs[0][1], rtol=1e-5, atol=1e-5 * float(outs[0][1].abs().max()))
     ref = torch.nn.grad.conv2d_weight(x.float(), (cout, cin, 4, 4), dy.float(), stride=2, padding=1)
