@@ -726,12 +726,14 @@ __device__ __forceinline__ int x2_off(int r, int byte) {
   return r * X2_ROW + ((((byte >> 5) ^ f) << 5) | (byte & 31));
 }
 
-__global__ __launch_bounds__(kThreads) void conv_wgrad_wide_kernel(ConvWgradParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE2];
-  if (run_side(p, smem)) return;
+constexpr int kWgradWideLds = 2 * STAGE2;
+// bid: the block's index in the weight gradient's own grid (a launch shared with
+// the 32-channel patch data gradient: dpatch_wgrad_kernel<.., true>)
+__device__ __forceinline__ void conv_wgrad_wide_body(const ConvWgradParams& p, char* smem, int bid) {
+  if (run_side(p, smem, bid)) return;
   const int t = int(threadIdx.x), lane = t & 63, wave = t >> 6;
   const int KC = 16 * p.Cin, KT = KC / BKC2, T = (p.Cout / BCO) * KT;
-  const int nwg = main_blocks(p), b = int(blockIdx.x);
+  const int nwg = main_blocks(p), b = bid;
   const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
   const int slice = w / T, tile = w - slice * T;
@@ -828,7 +830,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_wide_kernel(ConvWgradPara
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bm[j], acc[i][j], 0, 0, 0);
     }
   }
-  zero_output(p);
+  zero_output(p, bid);
   float* out = p.partial + int64_t(slice) * p.Cout * KC + (co0 + wco + 4 * (lane >> 4)) * KC +
                (kt * BKC2 + wkc + (lane & 15));
 #pragma unroll
@@ -837,6 +839,11 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_wide_kernel(ConvWgradPara
     for (int j = 0; j < 8; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) out[(16 * i + r) * KC + 16 * j] = acc[i][j][r];
+}
+
+__global__ __launch_bounds__(kThreads) void conv_wgrad_wide_kernel(ConvWgradParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[kWgradWideLds];
+  conv_wgrad_wide_body(p, smem, int(blockIdx.x));
 }
 
 // ---------------------------------------------------------------------------
@@ -1407,7 +1414,10 @@ constexpr int c4p_lds() {
                                                                        : 4 * 32 * 64 * 4;
 }
 
-template <int R>
+// KD: dY ring depth (steps in flight per wave).  2 (136 VGPRs, 3 waves per SIMD):
+// 4 (173 VGPRs, 2 waves) measured 29.6 against 27.8 us with the BN backward
+// (profiles/r6/b4/c4w_bench.jsonl, profiles/r6/b2/c4w_bench.jsonl)
+template <int R, int KD = 2>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_c4p_kernel(ConvWgradParams p) {
   constexpr int PR = 2 * R + 2;
   constexpr int PATCH = c4p_patch<R>();
@@ -1438,11 +1448,12 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4p_kernel(ConvWgradParam
   {
     const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(p.x, int64_t(p.N) * p.H * p.W * 4);
     const int npx = PR * PW, ih0 = 2 * oh0 - 1;
-    for (int i0 = 0; i0 < npx; i0 += 8 * kThreads) {
-      uint32_t wv[8];
-      bool ok[8];
+    constexpr int DL = 8;    // loads in flight per thread and round
+    for (int i0 = 0; i0 < npx; i0 += DL * kThreads) {
+      uint32_t wv[DL];
+      bool ok[DL];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
+      for (int k = 0; k < DL; ++k) {
         const int i = i0 + k * kThreads + t;
         const int pr = i / PW, pc = i - pr * PW;
         const int ih = ih0 + pr, iw = pc - 1;
@@ -1450,7 +1461,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4p_kernel(ConvWgradParam
         wv[k] = bload4(rs_x, ok[k] ? uint32_t(((n * p.H + ih) * p.W + iw) * 4) : kOOB);
       }
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
+      for (int k = 0; k < DL; ++k) {
         const int i = i0 + k * kThreads + t;
         if (i < npx) *reinterpret_cast<uint2*>(patch + i * 8) = lut_px(lutl, wv[k], ok[k]);
       }
@@ -1473,7 +1484,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4p_kernel(ConvWgradParam
   struct Stage {
     uint4 g[2], y[2];
   };
-  Stage ring[2];
+  Stage ring[KD];
   int s_load = wave;
   auto load = [&](Stage& r) {
     const bool live = s_load < nsteps;
@@ -1491,17 +1502,17 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4p_kernel(ConvWgradParam
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  load(ring[0]);
-  load(ring[1]);
-  const int mysteps = nsteps > wave ? (nsteps - wave + 3) / 4 : 0;
-  const int padded = (mysteps + 1) / 2 * 2;
-  int s = wave;
-  for (int i0 = 0; i0 < padded; i0 += 2) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u, s += 4) {
-      const bool live = s < nsteps;   // (wave-uniform: false on the ring's padding step)
+  for (int u = 0; u < KD; ++u) load(ring[u]);
+  const int mysteps = nsteps > wave ? (nsteps - wave + 3) / 4 : 0;
+  const int padded = (mysteps + KD - 1) / KD * KD;
+  int s = wave;
+  for (int i0 = 0; i0 < padded; i0 += KD) {
+#pragma unroll
+    for (int u = 0; u < KD; ++u, s += 4) {
+      const bool live = s < nsteps;   // (wave-uniform: false on the ring's padding steps)
       const Stage& r = ring[u];
-      char* const A = ws + u * C4W_DY;
+      char* const A = ws + (u & 1) * C4W_DY;
 #pragma unroll
       for (int h = 0; h < 2 && live; ++h) {
         uint4 d = r.g[h];
@@ -1519,7 +1530,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4p_kernel(ConvWgradParam
         }
         *reinterpret_cast<uint4*>(A + c4dy_off(dp + 16 * h, dc * 16)) = d;
       }
-      load(ring[u]);   // two steps ahead (past the end: out of range, zeros, never used)
+      load(ring[u]);   // KD steps ahead (past the end: out of range, zeros, never used)
       if (!live) continue;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       const int orow = s / spr, ow0 = (s - orow * spr) * BPX;
@@ -3321,12 +3332,24 @@ int wgrad_wide() {
 // the wide kernel's layers: power-of-two Cin with whole 256-column tiles, plain dY
 bool wgrad_wide_ok(int Cin, int Cout) { return wgrad_wide() && Cin >= 16 && (Cin & (Cin - 1)) == 0 && Cout % BCO == 0; }
 int g_wgrad_pipe = -1;   // register-staged weight gradient: fragments read a step ahead (BT_WGRAD_PIPE)
-// BT_WGRAD_CO128 (default 0): 128-channel weight-gradient tiles (conv_wgrad_co128_body) where Cout % 128 == 0
+// BT_DGRAD_BN128 (default 0): the held data gradient of a layer with Cin % 128 == 0 takes 128-channel
+// tiles in the fused data + weight gradient launch (with the 128-channel weight-gradient tiles)
+int g_dgrad_bn128 = -1;
+bool dgrad_bn128() {
+  if (g_dgrad_bn128 < 0) {
+    const char* v = std::getenv("BT_DGRAD_BN128");
+    g_dgrad_bn128 = v ? (std::atoi(v) ? 1 : 0) : 0;
+  }
+  return g_dgrad_bn128 == 1;
+}
+// BT_WGRAD_CO128 (default 1): 128-channel weight-gradient tiles (conv_wgrad_co128_body) where Cout % 128 == 0
 int g_wgrad_co128 = -1;
 bool wgrad_co128_ok(int Cin, int Cout) {
   if (g_wgrad_co128 < 0) {
+    // default on: the step's 64->128 pair 49.5 -> 41.6 us, 21.1-21.4k -> 21.9-22.0k img/s
+    // (profiles/r6/b3/disc_co*.jsonl, disc_step_sequence*.txt)
     const char* v = std::getenv("BT_WGRAD_CO128");
-    g_wgrad_co128 = v ? (std::atoi(v) ? 1 : 0) : 0;
+    g_wgrad_co128 = v ? (std::atoi(v) ? 1 : 0) : 1;
   }
   return g_wgrad_co128 == 1 && Cout % BCO2 == 0 && Cin >= 16 && (Cin & (Cin - 1)) == 0;
 }
@@ -3413,6 +3436,7 @@ bool conv_wgrad_supported(int Cin, int Cout) {
 }
 
 int conv_c4p_rows(int N, int H, int W, int Ho, int Wo, int Cout) { return c4p_rows_for(N, H, W, Ho, Wo, Cout); }
+void conv_set_dgrad_bn128(int on) { g_dgrad_bn128 = on < 0 ? -1 : (on ? 1 : 0); }
 void conv_set_wgrad_co128(int on) { g_wgrad_co128 = on < 0 ? -1 : (on ? 1 : 0); }
 void conv_set_c4p_rows(int rows) { g_c4p_override = rows == 0 || rows == 1 || rows == 2 || rows == 4 ? rows : -1; }
 
@@ -3454,9 +3478,11 @@ hipError_t conv_wgrad_reduce(const ConvWgradParams::Reduce& r, hipStream_t strea
 // it in its own apply).  conv_dgrad holds its tap-GEMM launch while
 // conv_dgrad_hold(1) is set; the next conv_wgrad on that stream launches
 // both, or conv_dgrad_flush launches the data gradient alone.
-template <int BM, bool PIPE, bool W2 = false>
+// DBN: the data gradient's output-channel tile (64, or 128 with BT_DGRAD_BN128 where Cin % 128 == 0:
+// each tap-gathered dY tile then feeds twice the channels)
+template <int BM, bool PIPE, bool W2 = false, int DBN = 64>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(W2 ? 3 : 1))) void dgrad_wgrad_kernel(TapGemm g, ConvWgradParams q, int gx, int nd, int nw) {
-  constexpr int TL = tap_gemm_lds<true, 64, false, BM, 2>();
+  constexpr int TL = tap_gemm_lds<true, DBN, false, BM, 2>();
   constexpr int WL = W2 ? kWgrad2Lds : kWgradLds;
   __shared__ __attribute__((aligned(16))) char smem[TL > WL ? TL : WL];
   const int b = int(blockIdx.x);
@@ -3472,7 +3498,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(W2 ? 3
   }
   if (kind == 0) {
     if (idx >= nd) return;   // (padding of the run: block-uniform, before any barrier)
-    tap_gemm_body<true, 64, false, BM, 2, 1, 0>(g, smem, idx % gx, idx / gx, gx);
+    tap_gemm_body<true, DBN, false, BM, 2, 1, 0>(g, smem, idx % gx, idx / gx, gx);
   } else {
     if (idx >= nw) return;
     if constexpr (W2) conv_wgrad_co128_body<>(q, smem, idx);
@@ -3481,9 +3507,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(W2 ? 3
 }
 
 // the same for the 32-channel layer's patch data gradient (dgrad_patch_body)
-template <bool PIPE>
-__global__ __launch_bounds__(kThreads) void dpatch_wgrad_kernel(TapGemm g, ConvWgradParams q, int nd, int nw) {
-  __shared__ __attribute__((aligned(16))) char smem[kDpatchLds > kWgradLds ? kDpatchLds : kWgradLds];
+// WIDE: the weight gradient's 256-column tiles (conv_wgrad_wide_body; 32 x 128 per wave)
+template <bool PIPE, bool WIDE = false>
+__global__ __launch_bounds__(kThreads) void dpatch_wgrad_kernel(
+    TapGemm g, ConvWgradParams q, int nd, int nw) {
+  constexpr int WL = WIDE ? kWgradWideLds : kWgradLds;
+  __shared__ __attribute__((aligned(16))) char smem[kDpatchLds > WL ? kDpatchLds : WL];
   const int b = int(blockIdx.x);
   const int nd8 = (nd + 7) & ~7, nw8 = (nw + 7) & ~7, m8 = nd8 < nw8 ? nd8 : nw8;
   int kind, idx;
@@ -3500,7 +3529,8 @@ __global__ __launch_bounds__(kThreads) void dpatch_wgrad_kernel(TapGemm g, ConvW
     dgrad_patch_body(g, smem, idx);
   } else {
     if (idx >= nw) return;
-    conv_wgrad_body<false, PIPE>(q, smem, idx);
+    if constexpr (WIDE) conv_wgrad_wide_body(q, smem, idx);
+    else conv_wgrad_body<false, PIPE>(q, smem, idx);
   }
 }
 
@@ -3510,6 +3540,7 @@ struct HeldDgrad {
   bool patch = false;   // dgrad_patch_kernel's grid (gx blocks), else the tap GEMM's (gx x 4 classes)
   TapGemm g;
   int bm = 0;
+  int bn = 64;          // the data gradient's channel tile (128: BT_DGRAD_BN128)
   unsigned gx = 0;   // the data gradient's x grid (4 parity classes in y)
   hipStream_t s = nullptr;
 };
@@ -3573,15 +3604,24 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
   bool fused = false;
   if (g_held.on) {   // a held data gradient: one launch for both when this is the plain kernel's case
     const bool dma = (wgrad_staging() == 2 || wgrad_staging() == 3) && (p.Cin & (p.Cin - 1)) == 0 && p.Wo >= 32;
-    const bool plain = !c4 && !bn_folds && !p.bn_dy.y && !p.fold.acc && !dma && !wide && (!co128 || !wgrad_pipe());
+    // (256-column tiles fuse with the patch data gradient; the tap GEMM's launch takes 128-column
+    // or 128-channel tiles)
+    const bool plain = !c4 && !bn_folds && !p.bn_dy.y && !p.fold.acc && !dma && (!wide || g_held.patch) &&
+                       (!co128 || !wgrad_pipe()) && (g_held.bn == 64 || co128);
     const int64_t nd = int64_t(g_held.gx) * (g_held.patch ? 1 : 4);
     if (plain && stream == g_held.s && nd + grid + 16 < (int64_t(1) << 31)) {
       const unsigned total = unsigned(((nd + 7) & ~int64_t(7)) + ((grid + 7) & ~int64_t(7)));
       const int gx = int(g_held.gx), ndi = int(nd), nwi = int(grid);
-      if (g_held.patch && wgrad_pipe())
+      if (g_held.patch && wide)
+        dpatch_wgrad_kernel<false, true><<<total, kThreads, 0, stream>>>(g_held.g, q, ndi, nwi);
+      else if (g_held.patch && wgrad_pipe())
         dpatch_wgrad_kernel<true><<<total, kThreads, 0, stream>>>(g_held.g, q, ndi, nwi);
       else if (g_held.patch)
         dpatch_wgrad_kernel<false><<<total, kThreads, 0, stream>>>(g_held.g, q, ndi, nwi);
+      else if (co128 && g_held.bn == 128 && g_held.bm == 64)
+        dgrad_wgrad_kernel<64, false, true, 128><<<total, kThreads, 0, stream>>>(g_held.g, q, gx, ndi, nwi);
+      else if (co128 && g_held.bn == 128)
+        dgrad_wgrad_kernel<FBM, false, true, 128><<<total, kThreads, 0, stream>>>(g_held.g, q, gx, ndi, nwi);
       else if (co128 && g_held.bm == 64)
         dgrad_wgrad_kernel<64, false, true><<<total, kThreads, 0, stream>>>(g_held.g, q, gx, ndi, nwi);
       else if (co128)
@@ -4096,11 +4136,13 @@ hipError_t conv_dgrad(const uint16_t* dy, const uint16_t* wt, uint16_t* dx, int 
   if (g_hold) {   // held for the weight gradient that follows (dgrad_wgrad_kernel)
     const hipError_t e = conv_dgrad_flush();
     if (e != hipSuccess) return e;
-    const int bn = conv_tile_channels(g.NOUT, false), bm = conv_tile_pixels(g.M, g.NOUT, 4);
-    if (g.cls_per_block == 1 && bn == 64 && staging() == 2 && (bm == 64 || bm == FBM)) {
+    const int bn = dgrad_bn128() && g.NOUT % 128 == 0 ? 128 : conv_tile_channels(g.NOUT, false);
+    const int bm = conv_tile_pixels(g.M, g.NOUT, 4);
+    if (g.cls_per_block == 1 && (bn == 64 || bn == 128) && staging() == 2 && (bm == 64 || bm == FBM)) {
       g_held.g = g;
       g_held.patch = false;
       g_held.bm = bm;
+      g_held.bn = bn;
       g_held.gx = unsigned((g.M + bm - 1) / bm * (g.NOUT / bn));
       g_held.s = stream;
       g_held.on = true;

@@ -312,6 +312,10 @@ struct AdamParams {
   // channels-last [tcout][4][4][tcin] to [tcin][4][4][tcout] (a 4x4
   // convolution's data-gradient operand, conv_weight_t).
   uint16_t* shadow_t[kMaxAdam] = {};
+  // g2[k] (nullable, fp32 grads): a second gradient contribution of the same step
+  // (a second backward pass, GradBuckets(second_sinks=True)) added to g[k] here --
+  // what autograd's AccumulateGrad kernel would have done, without its launch
+  const float* g2[kMaxAdam] = {};
   int tcout[kMaxAdam] = {};
   int tcin[kMaxAdam] = {};
 };
@@ -394,7 +398,8 @@ int conv_wgrad_slices(int64_t M, int Cin, int Cout, int target_blocks);
 // per band -- its slices must then be bands, px_per_slice = rows * Wo -- or 0 when the shape does not take it
 int conv_c4p_rows(int N, int H, int W, int Ho, int Wo, int Cout);
 void conv_set_c4p_rows(int rows);
-void conv_set_wgrad_co128(int on);   // 128-channel weight-gradient tiles: 1 on, 0 off, -1 BT_WGRAD_CO128   // 0: off, 1 / 2 / 4 rows, else back to BT_C4W_PATCH / BT_C4P_ROWS
+void conv_set_wgrad_co128(int on);
+void conv_set_dgrad_bn128(int on);   // 128-channel tiles for the held (fused) data gradient: 1 / 0 / -1 env   // 128-channel weight-gradient tiles: 1 on, 0 off, -1 BT_WGRAD_CO128   // 0: off, 1 / 2 / 4 rows, else back to BT_C4W_PATCH / BT_C4P_ROWS
 // Weight-gradient staging (not the 4-channel layer): 0 = register ring,
 // 2 / 3 = LDS-DMA stages of 64 pixels (default 0; -1 = BT_WGRAD_STAGING or default).
 void conv_set_fwd_patch(int on, int dbg = 0, int blocks = 0);       // 1 the 32->64 forward's persistent patch GEMM, 0 the tap GEMM, -1 env

@@ -301,6 +301,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("conv_c4p_rows", &conv_c4p_rows);
   m.def("conv_set_c4p_rows", &conv_set_c4p_rows);
   m.def("conv_set_wgrad_co128", &conv_set_wgrad_co128);
+  m.def("conv_set_dgrad_bn128", &conv_set_dgrad_bn128);
   m.def("conv_dgrad_hold", [](int on) { conv_dgrad_hold(on); });
   m.def("conv_dgrad_flush", []() { check(conv_dgrad_flush(), "conv_dgrad_flush"); });
   m.def("conv_dgrad_held", []() { return conv_dgrad_held(); });
@@ -634,7 +635,8 @@ PYBIND11_MODULE(_hip, m) {
            std::vector<uintptr_t> exp_avg_sq, std::vector<uintptr_t> shadow, std::vector<int64_t> numel,
            uintptr_t sched, int grad_bf16, float beta1, float beta2, float eps, float weight_decay, int decoupled,
            int maximize, uintptr_t stream, uintptr_t step, uintptr_t hp, uintptr_t gate, uintptr_t ticket,
-           int zero_grad, std::vector<uintptr_t> shadow_t, std::vector<int> tcout, std::vector<int> tcin) {
+           int zero_grad, std::vector<uintptr_t> shadow_t, std::vector<int> tcout, std::vector<int> tcin,
+           std::vector<uintptr_t> grads2) {
           const size_t n = params.size();
           if (grads.size() != n || exp_avg.size() != n || exp_avg_sq.size() != n || shadow.size() != n ||
               numel.size() != n || n > size_t(kMaxAdam))
@@ -653,6 +655,10 @@ PYBIND11_MODULE(_hip, m) {
             // every tensor starts on a 256-group block boundary (transposed
             // shadows are walked a block per tile; the padding groups are no-ops)
             a.gstart[k + 1] = (a.gstart[k] + (numel[k] + 3) / 4 + 255) / 256 * 256;
+          }
+          if (!grads2.empty()) {
+            if (grads2.size() != n || grad_bf16) throw std::invalid_argument("adam_update: grads2 (fp32) must match params");
+            for (size_t k = 0; k < n; ++k) a.g2[k] = ptr<const float>(grads2[k]);
           }
           for (size_t k = 0; k < shadow_t.size(); ++k) {
             a.shadow_t[k] = ptr<uint16_t>(shadow_t[k]);
@@ -674,7 +680,7 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("weight_decay"), py::arg("decoupled"), py::arg("maximize"), py::arg("stream"), py::arg("step") = 0,
         py::arg("hp") = 0, py::arg("gate") = 0, py::arg("ticket") = 0, py::arg("zero_grad") = 0,
         py::arg("shadow_t") = std::vector<uintptr_t>(), py::arg("tcout") = std::vector<int>(),
-        py::arg("tcin") = std::vector<int>());
+        py::arg("tcin") = std::vector<int>(), py::arg("grads2") = std::vector<uintptr_t>());
 
   m.def("color4x4",
         [](uintptr_t src, uintptr_t dst, uintptr_t lut, uintptr_t M, uintptr_t bias, uintptr_t flip, int B, int H,

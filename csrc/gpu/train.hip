@@ -831,6 +831,7 @@ __global__ void adam_schedule_kernel(float* step, const float* hp, float* sched,
 struct AdamSlot {
   float* p;
   const void* g;
+  const float* g2;
   float* m;
   float* v;
   uint16_t* shadow;
@@ -847,7 +848,7 @@ __global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
     const int t = int(threadIdx.x);
     if (t < a.n) {
       AdamSlot sl;
-      sl.p = a.p[t], sl.g = a.g[t], sl.m = a.m[t], sl.v = a.v[t], sl.shadow = a.shadow[t];
+      sl.p = a.p[t], sl.g = a.g[t], sl.g2 = a.g2[t], sl.m = a.m[t], sl.v = a.v[t], sl.shadow = a.shadow[t];
       sl.shadow_t = a.shadow_t[t], sl.numel = a.numel[t], sl.tcin = a.tcin[t], sl.tcout = a.tcout[t];
       slot[t] = sl;
     }
@@ -882,6 +883,7 @@ __global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
   float* M = in ? slot[k].m : nullptr;
   float* V = in ? slot[k].v : nullptr;
   const void* GR = in ? slot[k].g : nullptr;
+  const float* G2 = in && !GBF16 ? slot[k].g2 : nullptr;
   float pv[4] = {0.f, 0.f, 0.f, 0.f}, gv[4] = {0.f, 0.f, 0.f, 0.f}, mv[4] = {0.f, 0.f, 0.f, 0.f},
         vv[4] = {0.f, 0.f, 0.f, 0.f};
   // every load is issued before the schedule below (its fp64 math and the
@@ -900,6 +902,10 @@ __global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
     } else {
       const float4 g4 = *reinterpret_cast<const float4*>(static_cast<const float*>(GR) + e0);
       gv[0] = g4.x, gv[1] = g4.y, gv[2] = g4.z, gv[3] = g4.w;
+      if (G2) {   // the second contribution: g1 + g2, autograd's accumulate order
+        const float4 h4 = *reinterpret_cast<const float4*>(G2 + e0);
+        gv[0] += h4.x, gv[1] += h4.y, gv[2] += h4.z, gv[3] += h4.w;
+      }
     }
   } else if (in) {
 #pragma unroll
@@ -911,7 +917,7 @@ __global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
       if constexpr (GBF16)
         gv[j] = ok ? __uint_as_float(uint32_t(static_cast<const uint16_t*>(GR)[e0 + j]) << 16) : 0.f;
       else
-        gv[j] = ok ? static_cast<const float*>(GR)[e0 + j] : 0.f;
+        gv[j] = ok ? static_cast<const float*>(GR)[e0 + j] + (G2 ? G2[e0 + j] : 0.f) : 0.f;
     }
   }
   float step_size, inv_bc2, lr, gscale;
@@ -931,8 +937,16 @@ __global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
   if (in) {
     if (!GBF16 && a.zero_grad) {   // consumed (also when a closed gate skips the update)
       float* G = static_cast<float*>(const_cast<void*>(GR));
-      if (full) *reinterpret_cast<float4*>(G + e0) = make_float4(0.f, 0.f, 0.f, 0.f);
-      else for (int j = 0; j < 4 && e0 + j < n; ++j) G[e0 + j] = 0.f;
+      float* H = const_cast<float*>(G2);
+      if (full) {
+        *reinterpret_cast<float4*>(G + e0) = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (H) *reinterpret_cast<float4*>(H + e0) = make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        for (int j = 0; j < 4 && e0 + j < n; ++j) {
+          G[e0 + j] = 0.f;
+          if (H) H[e0 + j] = 0.f;
+        }
+      }
     }
     if (active) {
       const float b1 = a.beta1, b2 = a.beta2, wd = a.weight_decay;

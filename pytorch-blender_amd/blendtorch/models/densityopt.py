@@ -111,7 +111,10 @@ class DensityOptStep:
         self.N = self.B * self.world
         self.bf16 = (dev.type == 'cuda') if bf16 is None else bool(bf16)
         self.threshold, self.alpha = float(threshold), float(alpha)
-        self.gd = GradBuckets(netD.parameters())
+        # the D step's real and sim halves are two backward passes before one update:
+        # the sim half's gradients go to second bucket views that optD (FusedAdam) adds
+        # in its update kernel -- no AccumulateGrad launch per parameter
+        self.gd = GradBuckets(netD.parameters(), second_sinks=True)
         self.gs = GradBuckets(pm.parameters())
         scale = 1.0 / self.world
         self.optD = ops.FusedAdam(netD.parameters(), lr=lr_d, betas=betas_d, grad_scale=scale)
@@ -192,6 +195,10 @@ class DensityOptStep:
         return ops.hip_ext(), ops._stream(self.device)
 
     def _real_half_fused(self):
+        # fresh bucket views for this iteration's two backward passes (host flags only: optD
+        # clears the gradients it reads): the real half writes the buckets, the sim half the
+        # second views optD adds -- no AccumulateGrad launches, in the eager and the captured form
+        self.gd.zero_(memset=False)
         loss_r, logits = self.netD.bce_bf16(self.real, 1.0, probs='logits')
         loss_r.backward()
         self._logit_real = logits       # read by the sim half's gate kernel

@@ -908,7 +908,8 @@ def _grad_sink_ready(param):
     (fp32, contiguous)?  Consumes nothing."""
     import torch
     sink = grad_sink(param) if param is not None else None
-    return (sink is not None and param.grad is sink and getattr(param, '_bt_grad_fresh', False)
+    return (sink is not None and param.grad is sink and (getattr(param, '_bt_grad_fresh', False)
+                                                          or getattr(param, '_bt_grad_fresh2', False))
             and sink.dtype == torch.float32 and sink.is_contiguous())
 
 
@@ -919,13 +920,21 @@ def _grad_dest(param, like=None):
     returns None for that input (no AccumulateGrad kernel); any further one
     in the same step (several backward passes before the optimizer step)
     goes to a fresh tensor that autograd adds into ``param.grad`` -- the
-    usual accumulate semantics either way.  A bucket view that is no longer
+    usual accumulate semantics either way -- or, with a second bucket view
+    (``GradBuckets(second_sinks=True)``), the second one into that view,
+    which :class:`FusedAdam` adds in its update kernel.  A bucket view that is no longer
     ``param.grad`` (e.g. after ``zero_grad(set_to_none=True)``) is ignored."""
     import torch
     sink = grad_sink(param) if param is not None else None
     if sink is not None and param.grad is sink and getattr(param, '_bt_grad_fresh', False):
         param._bt_grad_fresh = False
         return sink, True
+    if sink is not None and param.grad is sink and getattr(param, '_bt_grad_fresh2', False):
+        # the second contribution of the step (GradBuckets(second_sinks=True)): into the
+        # second bucket view, which the FusedAdam update adds -- no AccumulateGrad launch
+        param._bt_grad_fresh2 = False
+        param._bt_grad_second = True
+        return param._bt_grad_sink2, True
     if sink is not None and _GRAD_LATE is not None:
         _GRAD_LATE(param)
     return torch.empty_like(param if like is None else like), False

@@ -49,6 +49,15 @@ import torch
 
 from . import _count, _dense, _stream, hip_ext
 
+
+def _second_grad(p):
+    """The second gradient contribution of this step held in ``p``'s second
+    bucket view (:class:`~blendtorch.parallel.GradBuckets` ``second_sinks``),
+    or None."""
+    if getattr(p, '_bt_grad_second', False) and p.grad is getattr(p, '_bt_grad_sink', None):
+        return p._bt_grad_sink2
+    return None
+
 __all__ = ['FusedAdam']
 
 import os  # noqa: E402
@@ -269,6 +278,8 @@ class FusedAdam(torch.optim.Optimizer):
                 if self._zero_grads:
                     for p in params:
                         p.grad.zero_()
+                        if _second_grad(p) is not None:
+                            _second_grad(p).zero_()
         return loss
 
     def _step_gpu(self, group, gs, params, states, gate=None):
@@ -313,6 +324,12 @@ class FusedAdam(torch.optim.Optimizer):
                 grads.append(g)
             _count('adam_update')
             trans = any('shadow_t' in s for s in ss)
+            # a second contribution of this step (a second backward pass) sits in the
+            # parameter's second bucket view (GradBuckets(second_sinks=True)): the update
+            # kernel adds it, instead of an AccumulateGrad launch per parameter
+            g2 = [_second_grad(p) for p in ps]
+            if any(x is not None for x in g2) and grads[0].dtype != torch.float32:
+                raise ValueError('FusedAdam: second gradient contributions need fp32 gradients')
             ext.adam_update([p.data_ptr() for p in ps], [g.data_ptr() for g in grads],
                             [s['exp_avg'].data_ptr() for s in ss], [s['exp_avg_sq'].data_ptr() for s in ss],
                             [s['shadow'].data_ptr() if 'shadow' in s else 0 for s in ss],
@@ -324,7 +341,9 @@ class FusedAdam(torch.optim.Optimizer):
                             ticket=gs['ticket'].data_ptr() if one else 0, zero_grad=int(zero),
                             shadow_t=[s['shadow_t'].data_ptr() if 'shadow_t' in s else 0 for s in ss] if trans else [],
                             tcout=[int(p.shape[0]) if 'shadow_t' in s else 0 for p, s in zip(ps, ss)] if trans else [],
-                            tcin=[int(p.shape[1]) if 'shadow_t' in s else 0 for p, s in zip(ps, ss)] if trans else [])
+                            tcin=[int(p.shape[1]) if 'shadow_t' in s else 0 for p, s in zip(ps, ss)] if trans else [],
+                            grads2=[x.data_ptr() if x is not None else 0 for x in g2]
+                            if any(x is not None for x in g2) else [])
             if zero:
                 for p, g in zip(ps, grads):
                     if g is not p.grad:      # a re-strided copy was read and cleared: clear the real one
@@ -344,6 +363,9 @@ class FusedAdam(torch.optim.Optimizer):
         scale = float(gs['hp'][1])
         for p, st in zip(params, states):
             g = p.grad.float()
+            g2 = _second_grad(p)
+            if g2 is not None:
+                g = g + g2
             if scale != 1.0:
                 g = g * scale
             if group['maximize']:

@@ -59,7 +59,15 @@ class GradBuckets:
     """
 
     def __init__(self, params: Sequence[torch.nn.Parameter], bucket_mb: float = 256.0, n_buckets: int = 0,
-                 first_fraction: float = 0.7):
+                 first_fraction: float = 0.7, second_sinks: bool = False):
+        # second_sinks: a mirror of every bucket for a second gradient contribution per
+        # step (two backward passes before one update, as densityopt's real / sim
+        # halves): the backward kernels write it there and ops.FusedAdam adds it in
+        # its update kernel -- without it autograd adds each second gradient into
+        # .grad with one launch per parameter.  Only for optimizers that read it
+        # (FusedAdam); the all-reduce covers the mirrors that were written.
+        self.second_sinks = bool(second_sinks)
+        self.buckets2: List[torch.Tensor] = []
         ps = [p for p in params if p.requires_grad]
         seen = set()
         self.params: List[torch.nn.Parameter] = []
@@ -109,11 +117,16 @@ class GradBuckets:
 
     def _make(self, dev, dt, members, offs, size):
         flat = torch.zeros(size, dtype=dt, device=dev)
+        flat2 = torch.zeros(size, dtype=dt, device=dev) if self.second_sinks else None
         for p, off in zip(members, offs):
             view = flat.as_strided(p.shape, p.stride(), off)
             p.grad = view
             p._bt_grad_sink = view
+            if flat2 is not None:
+                p._bt_grad_sink2 = flat2.as_strided(p.shape, p.stride(), off)
         self.buckets.append(flat)
+        if flat2 is not None:
+            self.buckets2.append(flat2)
         self._members.append(list(members))
 
     @property
@@ -133,10 +146,13 @@ class GradBuckets:
             raise RuntimeError('GradBuckets: a parameter\'s .grad was replaced (zero_grad(set_to_none=True)?); '
                                'bucketed gradients must stay attached')
         if memset:
-            for b in self.buckets:
+            for b in self.buckets + self.buckets2:
                 b.zero_()
         for p in self.params:
             p._bt_grad_fresh = True
+            if self.second_sinks:
+                p._bt_grad_fresh2 = True
+                p._bt_grad_second = False
 
     # -- all-reduce as soon as a bucket is complete ---------------------------------
     def arm(self, comm, op: str = 'sum'):
@@ -207,9 +223,14 @@ class GradBuckets:
         communicator is native.  Returns the number of collectives issued."""
         if not self.attached():
             raise RuntimeError('GradBuckets: gradients were detached from their buckets')
-        for b in self.buckets:
+        n = 0
+        for i, b in enumerate(self.buckets):
             comm.all_reduce_(b, op)
-        return len(self.buckets)
+            n += 1
+            if self.buckets2 and any(getattr(p, '_bt_grad_second', False) for p in self._members[i]):
+                comm.all_reduce_(self.buckets2[i], op)
+                n += 1
+        return n
 
     def detach(self):
         """Remove the buckets: parameters get ordinary gradients again."""
@@ -218,9 +239,10 @@ class GradBuckets:
                 if p.grad is p._bt_grad_sink:
                     p.grad = p.grad.clone()
                 del p._bt_grad_sink
-            if hasattr(p, '_bt_grad_fresh'):
-                del p._bt_grad_fresh
-        self.buckets, self._members = [], []
+            for a in ('_bt_grad_fresh', '_bt_grad_fresh2', '_bt_grad_second', '_bt_grad_sink2'):
+                if hasattr(p, a):
+                    delattr(p, a)
+        self.buckets, self._members, self.buckets2 = [], [], []
 
     def __repr__(self):
         return (f'GradBuckets({len(self.params)} params, {len(self.buckets)} buckets, '

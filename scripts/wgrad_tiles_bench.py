@@ -20,7 +20,7 @@ import torch  # noqa: E402
 from blendtorch import ops  # noqa: E402
 from conv_bench import timed  # noqa: E402
 
-LAYERS = [(64, 120, 160, 128), (128, 60, 80, 256)]   # Cin, H, W, Cout (input side), batch 8
+LAYERS = [(32, 240, 320, 64), (64, 120, 160, 128), (128, 60, 80, 256)]   # Cin, H, W, Cout (input side), batch 8
 
 
 def main():
@@ -39,8 +39,17 @@ def main():
             memory_format=cl)
         out = torch.empty(cout, cin, 4, 4, device=dev)
         ref = torch.nn.grad.conv2d_weight(x.float(), (cout, cin, 4, 4), dy.float(), stride=2, padding=1)
-        for co128 in (0, 1):
-            ext.conv_set_wgrad_co128(co128)
+        # 32 -> 64 (Cout 64): 128-column tiles against 256-column ones (conv_wgrad_wide_body, fused
+        # with the patch data gradient); the deeper layers: 64- against 128-channel tiles
+        for co128 in ((0, 1) if cout % 128 else (0, 1, 2)):
+            if cout % 128:
+                ext.conv_set_wgrad_co128(0)
+                ext.conv_set_wgrad_wide(co128)
+            else:
+                ext.conv_set_wgrad_co128(1 if co128 else 0)
+                ext.conv_set_wgrad_wide(0)
+            # 2: the fused launch's data gradient in 128-channel tiles too (Cin % 128 == 0)
+            ext.conv_set_dgrad_bn128(1 if co128 == 2 else 0)
             alone = timed(lambda: ops.conv_wgrad(x, dy, out), a.iters)
             ops.conv_wgrad(x, dy, out)
             err = float((out - ref).abs().max() / ref.abs().max())
@@ -54,10 +63,12 @@ def main():
                 ops.conv_wgrad(x, dy, out)
             fused = timed(pair, a.iters)
             dgrad = timed(lambda: ops.conv_dgrad(dy, w, tuple(x.shape)), a.iters)
-            print(json.dumps({'layer': f'{cin}->{cout} @{H}x{W}', 'co128': co128, 'wgrad_us': round(alone, 2),
+            print(json.dumps({'layer': f'{cin}->{cout} @{H}x{W}', ('wide' if cout % 128 else 'co128'): co128, 'wgrad_us': round(alone, 2),
                               'fused_pair_us': round(fused, 2), 'dgrad_alone_us': round(dgrad, 2),
                               'rel_err': float(f'{err:.2e}')}), flush=True)
     ext.conv_set_wgrad_co128(-1)
+    ext.conv_set_wgrad_wide(-1)
+    ext.conv_set_dgrad_bn128(-1)
 
 
 if __name__ == '__main__':

@@ -1027,8 +1027,9 @@ def test_fused_data_and_weight_gradient_launch(dev):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('co128', [0, 1], ids=['co64', 'co128'])
-@pytest.mark.parametrize('cin,cout,hw', [(64, 128, (60, 80)), (128, 256, (30, 40)), (64, 128, (12, 18))])
+@pytest.mark.parametrize('co128', [0, 1, 2], ids=['co64', 'co128', 'co128_dbn128'])
+@pytest.mark.parametrize('cin,cout,hw', [(64, 128, (60, 80)), (128, 256, (30, 40)), (64, 128, (12, 18)),
+                                         (128, 256, (14, 22))])
 def test_dgrad_wgrad_kernel_matches_separate_launches(dev, cin, cout, hw, co128):
     """One layer, direct ops: conv_dgrad held + conv_wgrad (one launch) give
     the bit-identical data gradient and the same weight gradient as the two
@@ -1041,7 +1042,8 @@ def test_dgrad_wgrad_kernel_matches_separate_launches(dev, cin, cout, hw, co128)
     dy = torch.randn(8, cout, H // 2, W // 2, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
     w = (0.05 * torch.randn(cout, cin, 4, 4, device=dev, generator=g)).to(torch.bfloat16).contiguous(memory_format=cl)
     ext = ops.hip_ext()
-    ext.conv_set_wgrad_co128(co128)
+    ext.conv_set_wgrad_co128(1 if co128 else 0)
+    ext.conv_set_dgrad_bn128(1 if co128 == 2 else 0)
     outs = []
     for fuse in (False, True):
         if fuse:
@@ -1056,6 +1058,7 @@ def test_dgrad_wgrad_kernel_matches_separate_launches(dev, cin, cout, hw, co128)
         torch.cuda.synchronize()
         outs.append((dx, gw))
     ext.conv_set_wgrad_co128(-1)
+    ext.conv_set_dgrad_bn128(-1)
     assert torch.equal(outs[0][0], outs[1][0])
     torch.testing.assert_close(outs[1][1], outs[0][1], rtol=1e-5, atol=1e-5 * float(outs[0][1].abs().max()))
     ref = torch.nn.grad.conv2d_weight(x.float(), (cout, cin, 4, 4), dy.float(), stride=2, padding=1)
@@ -1121,3 +1124,38 @@ def test_fwd_patch_gemm_matches_tap_gemm(dev, N, H, W):
     yf = out[1][0].float().permute(0, 2, 3, 1).reshape(-1, 64).double()
     torch.testing.assert_close(out[1][2][0], yf.sum(0), rtol=1e-5, atol=1e-2)
     torch.testing.assert_close(out[1][2][1], (yf * yf).sum(0), rtol=1e-5, atol=1e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('wide', [0, 1], ids=['w128', 'w256'])
+@pytest.mark.parametrize('hw', [(240, 320), (30, 46)])
+def test_patch_dgrad_with_wide_wgrad_one_launch(dev, hw, wide):
+    """The 32-channel layer's patch data gradient held and launched together
+    with its weight gradient (dpatch_wgrad_kernel), with 128- or 256-column
+    weight-gradient tiles (conv_wgrad_wide_body): the data gradient is
+    bit-identical to its own launch, the weight gradient matches fp32 PyTorch."""
+    cl = torch.channels_last
+    g = torch.Generator(device=dev).manual_seed(hw[0] + wide)
+    H, W = hw
+    cin, cout = 32, 64
+    x = torch.randn(8, cin, H, W, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    dy = torch.randn(8, cout, H // 2, W // 2, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    w = (0.05 * torch.randn(cout, cin, 4, 4, device=dev, generator=g)).to(torch.bfloat16).contiguous(memory_format=cl)
+    ext = ops.hip_ext()
+    ext.conv_set_wgrad_wide(wide)
+    try:
+        alone = ops.conv_dgrad(dy, w, tuple(x.shape))
+        ext.conv_dgrad_hold(1)
+        try:
+            dx = ops.conv_dgrad(dy, w, tuple(x.shape))
+        finally:
+            ext.conv_dgrad_hold(0)
+        assert ext.conv_dgrad_held()
+        gw = ops.conv_wgrad(x, dy, torch.empty(cout, cin, 4, 4, device=dev))
+        assert not ext.conv_dgrad_held()
+        torch.cuda.synchronize()
+    finally:
+        ext.conv_set_wgrad_wide(-1)
+    assert torch.equal(dx, alone)
+    ref = torch.nn.grad.conv2d_weight(x.float(), (cout, cin, 4, 4), dy.float(), stride=2, padding=1)
+    torch.testing.assert_close(gw, ref, rtol=1e-3, atol=1e-3 * float(ref.abs().max()))

@@ -791,3 +791,38 @@ def test_densityopt_fused_host_state_and_static_sims(dev):
     assert torch.equal(runs[0][0], runs[1][0])
     for a, b in zip(runs[0][1], runs[1][1]):
         assert torch.equal(a, b)
+
+
+def test_second_gradient_sinks_match_autograd_accumulate(dev):
+    """GradBuckets(second_sinks=True): two backward passes before one
+    FusedAdam step (densityopt's real / sim halves).  The second pass writes
+    its gradients into the second bucket views and the update kernel adds
+    them -- no AccumulateGrad launches -- and the weights after the step are
+    bit-identical to autograd adding the second gradients into .grad."""
+    from blendtorch.models import Discriminator
+    from blendtorch.parallel import GradBuckets
+    torch.manual_seed(3)
+    g = torch.Generator(device=dev).manual_seed(4)
+    xa = (torch.rand(16, 64, 64, 4, device=dev, generator=g) * 2 - 1).to(torch.bfloat16).permute(0, 3, 1, 2)
+    xb = (torch.rand(16, 64, 64, 4, device=dev, generator=g) * 2 - 1).to(torch.bfloat16).permute(0, 3, 1, 2)
+    nets, adds = [], []
+    base = Discriminator().to(dev).to(memory_format=torch.channels_last)
+    for second in (False, True):
+        net = Discriminator().to(dev).to(memory_format=torch.channels_last)
+        net.load_state_dict(base.state_dict())
+        gb = GradBuckets(net.parameters(), second_sinks=second)
+        opt = ops.FusedAdam(net.parameters(), lr=1e-3, betas=(0.5, 0.999))
+        opt.set_zero_grads(True)
+        for _ in range(3):
+            gb.zero_()
+            la, _ = net.bce_bf16(xa, 1.0)
+            la.backward()
+            lb, _ = net.bce_bf16(xb, 0.0)
+            lb.backward()
+            opt.step()
+        torch.cuda.synchronize()
+        nets.append(net)
+        adds.append(sum(1 for p in net.parameters() if getattr(p, '_bt_grad_second', False)))
+    assert adds[0] == 0 and adds[1] == len(list(nets[1].parameters()))
+    for (n, pa), pb in zip(nets[0].named_parameters(), nets[1].parameters()):
+        assert torch.equal(pa, pb), n
