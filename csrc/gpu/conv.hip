@@ -1417,7 +1417,9 @@ constexpr int c4p_lds() {
 // KD: dY ring depth (steps in flight per wave).  2 (136 VGPRs, 3 waves per SIMD):
 // 4 (173 VGPRs, 2 waves) measured 29.6 against 27.8 us with the BN backward
 // (profiles/r6/b4/c4w_bench.jsonl, profiles/r6/b2/c4w_bench.jsonl)
-template <int R, int KD = 2>
+// PRE: the first decode round's loads issued before the BN fold (139 VGPRs: 2 waves per SIMD,
+// against 3 without; the launch holds ~1.9 waves per SIMD either way) -- BT_C4P_PRE
+template <int R, int KD = 2, bool PRE = false>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_c4p_kernel(ConvWgradParams p) {
   constexpr int PR = 2 * R + 2;
   constexpr int PATCH = c4p_patch<R>();
@@ -1437,6 +1439,32 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4p_kernel(ConvWgradParam
   const int PW = p.W + 2;
   const int dc = lane & 3, dp = lane >> 2;
   const bool bnd = p.bn_dy.y != nullptr;
+  // the band's input rows 2 oh0 - 1 .. 2 (oh0 + R) decoded once: DL loads in flight per thread and
+  // round, then their lookups; the first round's loads are issued before the BN fold, so their
+  // latency hides under the fold's own accumulator reads
+  const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(p.x, int64_t(p.N) * p.H * p.W * 4);
+  const int npx = PR * PW, ih0 = 2 * oh0 - 1;
+  constexpr int DL = 8;
+  auto issue = [&](int i0, uint32_t (&wv)[DL], bool (&ok)[DL]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < DL; ++k) {
+      const int i = i0 + k * kThreads + t;
+      const int pr = i / PW, pc = i - pr * PW;
+      const int ih = ih0 + pr, iw = pc - 1;
+      ok[k] = i < npx && unsigned(ih) < unsigned(p.H) && unsigned(iw) < unsigned(p.W);
+      wv[k] = bload4(rs_x, ok[k] ? uint32_t(((n * p.H + ih) * p.W + iw) * 4) : kOOB);
+    }
+  };
+  auto lookups = [&](int i0, const uint32_t (&wv)[DL], const bool (&ok)[DL]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < DL; ++k) {
+      const int i = i0 + k * kThreads + t;
+      if (i < npx) *reinterpret_cast<uint2*>(patch + i * 8) = lut_px(lutl, wv[k], ok[k]);
+    }
+  };
+  uint32_t wv0[DL];
+  bool ok0[DL];
+  if constexpr (PRE) issue(0, wv0, ok0);
   BnBwdCoef bc[8];
   if (bnd) {   // (LDS scratch: the front, free until the patch is written)
     bn_dy_coefs(p.bn_dy, p.Cout, p.M, dc * 8, reinterpret_cast<double*>(smem), reinterpret_cast<int*>(smem + 4096),
@@ -1444,28 +1472,12 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4p_kernel(ConvWgradParam
   }
   stage_lut(p.lut, lutl);
   __syncthreads();
-  // the band's input rows 2 oh0 - 1 .. 2 (oh0 + R) decoded once: 8 loads in flight per thread, then lookups
-  {
-    const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(p.x, int64_t(p.N) * p.H * p.W * 4);
-    const int npx = PR * PW, ih0 = 2 * oh0 - 1;
-    constexpr int DL = 8;    // loads in flight per thread and round
-    for (int i0 = 0; i0 < npx; i0 += DL * kThreads) {
-      uint32_t wv[DL];
-      bool ok[DL];
-#pragma unroll
-      for (int k = 0; k < DL; ++k) {
-        const int i = i0 + k * kThreads + t;
-        const int pr = i / PW, pc = i - pr * PW;
-        const int ih = ih0 + pr, iw = pc - 1;
-        ok[k] = i < npx && unsigned(ih) < unsigned(p.H) && unsigned(iw) < unsigned(p.W);
-        wv[k] = bload4(rs_x, ok[k] ? uint32_t(((n * p.H + ih) * p.W + iw) * 4) : kOOB);
-      }
-#pragma unroll
-      for (int k = 0; k < DL; ++k) {
-        const int i = i0 + k * kThreads + t;
-        if (i < npx) *reinterpret_cast<uint2*>(patch + i * 8) = lut_px(lutl, wv[k], ok[k]);
-      }
-    }
+  if constexpr (PRE) lookups(0, wv0, ok0);
+  for (int i0 = PRE ? DL * kThreads : 0; i0 < npx; i0 += DL * kThreads) {
+    uint32_t wv[DL];
+    bool ok[DL];
+    issue(i0, wv, ok);
+    lookups(i0, wv, ok);
   }
   __syncthreads();
   const __amdgpu_buffer_rsrc_t rs_dy = make_rsrc(p.dy, p.M * p.Cout * 2);
@@ -3394,6 +3406,10 @@ int c4w_waves() {
 
 // BT_C4W_PATCH (default 1): the first layer's weight gradient from a decoded input patch
 // (conv_wgrad_c4p_kernel) when the shape takes it; BT_C4P_ROWS: output rows per band (1, 2, 4)
+bool c4p_pre() {
+  static const bool on = std::getenv("BT_C4P_PRE") && std::getenv("BT_C4P_PRE")[0] == '1';
+  return on;
+}
 int g_c4p_override = -1;   // conv_set_c4p_rows (tests / benches): -1 = the environment's choice
 int c4p_rows_for(int N, int H, int W, int Ho, int Wo, int Cout) {
   static const int env_rows = [] {
@@ -3646,6 +3662,7 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
   } else if (c4p > 0 && p.px_per_slice == int64_t(c4p) * p.Wo && int64_t(p.slices) * p.px_per_slice == p.M) {
     if (c4p == 1) conv_wgrad_c4p_kernel<1><<<unsigned(grid), kThreads, 0, stream>>>(q);
     else if (c4p == 2) conv_wgrad_c4p_kernel<2><<<unsigned(grid), kThreads, 0, stream>>>(q);
+    else if (c4p_pre()) conv_wgrad_c4p_kernel<4, 2, true><<<unsigned(grid), kThreads, 0, stream>>>(q);
     else conv_wgrad_c4p_kernel<4><<<unsigned(grid), kThreads, 0, stream>>>(q);
   } else if (c4 && (c4_wave_private() || bn_folds)) {
     const bool u8 = p.lut != nullptr;
@@ -3674,8 +3691,15 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
   r.cin_out = p.cin_out > 0 ? p.cin_out : p.Cin;
   r.out = out, r.s_co = s_co, r.s_ci = s_ci, r.s_kh = s_kh, r.s_kw = s_kw;
   if (wgrad_ordered()) {
-    int sub = 1;   // lanes per 4 elements: each walks <= 16 slices (two rounds of 8 loads in flight)
-    while (sub < 64 && (p.slices + sub - 1) / sub > 2 * kSliceGroup) sub <<= 1;
+    // lanes per 4 elements: each walks <= rounds x 8 slices (rounds of 8 loads in flight);
+    // BT_REDUCE_ROUNDS (default 2; 1: twice the lanes, one round)
+    static const int rounds = [] {
+      const char* v = std::getenv("BT_REDUCE_ROUNDS");
+      const int k = v ? std::atoi(v) : 2;
+      return k >= 1 && k <= 8 ? k : 2;
+    }();
+    int sub = 1;
+    while (sub < 64 && (p.slices + sub - 1) / sub > rounds * kSliceGroup) sub <<= 1;
     r.sub = sub;
     r.rx = int((total / 4 * sub + kThreads - 1) / kThreads);
     r.ry = 1;

@@ -205,6 +205,7 @@ class DensityOptStep:
 
     def _sim_half_fused(self, sim):
         ext, st = self._ext()
+        self.gd.arm_second()   # (each sim-half capture records the second views, not autograd adds)
         loss_s, logit_sim = self.netD.bce_bf16(sim, 0.0, probs='logits')
         loss_s.backward()
         kp = dict(self._kp, logit_real=self._logit_real.data_ptr(), logit_sim=logit_sim.data_ptr())

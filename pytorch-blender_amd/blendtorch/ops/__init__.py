@@ -937,6 +937,8 @@ def _grad_dest(param, like=None):
         return param._bt_grad_sink2, True
     if sink is not None and _GRAD_LATE is not None:
         _GRAD_LATE(param)
+    if sink is not None:
+        _count('grad_dest_autograd_add')   # a bucketed gradient autograd will add (one launch)
     return torch.empty_like(param if like is None else like), False
 
 

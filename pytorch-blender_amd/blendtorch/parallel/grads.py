@@ -154,6 +154,16 @@ class GradBuckets:
                 p._bt_grad_fresh2 = True
                 p._bt_grad_second = False
 
+    def arm_second(self):
+        """Before a step's second backward pass (second_sinks): its gradients go to
+        the second views again.  Host flags only -- a pass captured into a graph
+        records where it writes, so call it before every capture of the second
+        pass (densityopt captures one sim-half graph per static input tensor)."""
+        if not self.second_sinks:
+            return
+        for p in self.params:
+            p._bt_grad_fresh2 = True
+
     # -- all-reduce as soon as a bucket is complete ---------------------------------
     def arm(self, comm, op: str = 'sum'):
         """Before ONE backward pass: enqueue each bucket's all-reduce the

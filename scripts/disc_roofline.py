@@ -75,6 +75,24 @@ MODEL_FUSED = MODEL[:10] + [
 MODEL_FUSED2 = MODEL_FUSED[:14] + [('conv2 dgrad (patch) + wgrad (one launch)', 2 * G, 2 * (A2 + A1))] + MODEL_FUSED[16:]
 
 
+# round 6's step (17 kernels): the head applies the last BN's backward (no BN4 apply), the Adam
+# schedule rides in a slice-reduce launch, every tap-GEMM layer's data and weight gradient is one
+# launch, the first layer's weight gradient reads a decoded input patch (conv_wgrad_c4p_kernel)
+MODEL_R6 = MODEL[:7] + [
+    ('head fwd (BN4 apply, pool, conv, BCE, BN4 bwd sums)', 0, A4),
+    ('head bwd (+ BN4 bwd apply)', 0, 3 * A4),
+    ('conv4 dgrad + wgrad (one launch)', 2 * G, 2 * (A4 + A3)),
+    ('BN3 apply bwd', 0, 3 * A3),
+    ('conv3 dgrad + wgrad (one launch)', 2 * G, 2 * (A3 + A2)),
+    ('BN2 apply bwd', 0, 3 * A2),
+    ('conv2 dgrad (patch) + wgrad (one launch)', 2 * G, 2 * (A2 + A1)),
+    ('conv1 wgrad (decoded patch, BN1 bwd fused)', G1, U8 + 2 * A1),
+    ('wgrad slice reduce (+ Adam schedule)', 0, 0),
+    ('adam update', 0, 4 * PARAMS),
+]
+CLOCK_HZ, CUS = 2.4e9, 256
+
+
 def short(name):
     n = name.replace('(anonymous namespace)::', '').replace('btn::gpu::', '').replace('void ', '')
     return re.sub(r'\(.*$', '', n).strip()
@@ -153,14 +171,16 @@ def main():
     model = MODEL_FUSED if any(base(n) == 'dgrad_wgrad_kernel' for n, _ in seq) else MODEL
     if any(base(n) == 'dpatch_wgrad_kernel' for n, _ in seq):
         model = MODEL_FUSED2
+    if len(seq) == len(MODEL_R6) and any(base(n) == 'conv_wgrad_c4p_kernel' for n, _ in seq):
+        model = MODEL_R6
     if len(seq) != len(model):
         print(f'warning: {len(seq)} kernels per step, the model has {len(model)}', file=sys.stderr)
     rows = []
     tot = collections.defaultdict(float)
     hdr = ('| # | kernel | what | us | GFLOP | TFLOP/s | % bf16 peak | min MB | fetch MB | write MB | TB/s (meas.) '
-           '| % HBM | VALU/MFMA | LDS/MFMA | bank conflict % |')
+           '| % HBM | VALU/MFMA | LDS/MFMA | bank conflict % | conflict cycles % of runtime |')
     rows.append(hdr)
-    rows.append('|' + '---|' * 15)
+    rows.append('|' + '---|' * 16)
     for i, (nm, us) in enumerate(seq):
         what, fl, mb = model[i] if i < len(model) else ('?', 0, 0)
         c = ctrs[i] if i < len(ctrs) else {}
@@ -178,14 +198,16 @@ def main():
                     f'| {mb / 1e6:.1f} | {fetch:.1f} | {write:.1f} | {tbs:.2f} | {100 * tbs / PEAK_TBS:.0f} '
                     f'| {c.get("SQ_INSTS_VALU", 0) / mf if mf else float("nan"):.2f} '
                     f'| {c.get("SQ_INSTS_LDS", 0) / mf if mf else float("nan"):.2f} '
-                    f'| {100 * c.get("SQ_LDS_BANK_CONFLICT", 0) / lds_act if lds_act else float("nan"):.1f} |')
+                    f'| {100 * c.get("SQ_LDS_BANK_CONFLICT", 0) / lds_act if lds_act else float("nan"):.1f} '
+                    # extra LDS cycles of all CUs over the kernel's CU-cycles (trace duration x clock x CUs)
+                    f'| {100 * c.get("SQ_LDS_BANK_CONFLICT", 0) / (us * 1e-6 * CLOCK_HZ * CUS) if (c and us) else float("nan"):.2f} |')
         tot['us'] += us
         tot['fl'] += fl
         tot['mb'] += mb / 1e6
         tot['moved'] += moved
     rows.append(f'| | **step** | | **{tot["us"]:.1f}** | {tot["fl"] / 1e9:.1f} | {tot["fl"] / (tot["us"] * 1e-6) / 1e12:.0f} '
                 f'| {100 * tot["fl"] / (tot["us"] * 1e-6) / 1e12 / PEAK_TFLOPS:.1f} | {tot["mb"]:.0f} | | '
-                f'| {tot["moved"] * 1e6 / (tot["us"] * 1e-6) / 1e12:.2f} | | | | |')
+                f'| {tot["moved"] * 1e6 / (tot["us"] * 1e-6) / 1e12:.2f} | | | | | |')
     txt = '\n'.join(rows)
     print(txt)
     if a.md:

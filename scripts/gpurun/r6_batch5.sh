@@ -17,7 +17,7 @@ timeout -k 10 200 python scripts/wgrad_tiles_bench.py > $O/wgrad_tiles.jsonl 2>&
 cat $O/wgrad_tiles.jsonl
 timeout -k 10 200 python scripts/c4w_bench.py --patch-only > $O/c4w_bench.jsonl 2>&1 || { tail -20 $O/c4w_bench.jsonl; exit 1; }
 cat $O/c4w_bench.jsonl
-for v in "default:" "dbn128:BT_DGRAD_BN128=1" "wide:BT_WGRAD_WIDE=1" "default:" "dbn128:BT_DGRAD_BN128=1" "wide:BT_WGRAD_WIDE=1"; do
+for v in "default:" "dbn128:BT_DGRAD_BN128=1" "wide:BT_WGRAD_WIDE=1" "red1:BT_REDUCE_ROUNDS=1" "bn128all:BT_CONV_BN=128" "default:" "dbn128:BT_DGRAD_BN128=1" "wide:BT_WGRAD_WIDE=1" "red1:BT_REDUCE_ROUNDS=1" "bn128all:BT_CONV_BN=128"; do
   name=${v%%:*}; e=${v#*:}
   timeout -k 10 200 env $e python bench.py --consumer disc --steps 2000 > $O/disc.log 2>&1 || { tail -5 $O/disc.log; exit 1; }
   grep '^{' $O/disc.log | tee -a $O/disc_$name.jsonl | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'v':'$name','disc':d['value'],'ms':d['ms_per_step']}))"

@@ -776,6 +776,7 @@ def test_densityopt_fused_host_state_and_static_sims(dev):
         assert torch.equal(step.host_state()['samples'], step.samples[:, :B].cpu())
         sids = torch.Generator().manual_seed(4)
         hist = []
+        adds0 = ops.KERNEL_CALLS.get('grad_dest_autograd_add', 0)
         for i in range(8):
             step(ring[i % 3].permute(0, 3, 1, 2), torch.randperm(B, generator=sids))
             torch.cuda.synchronize()
@@ -786,6 +787,9 @@ def test_densityopt_fused_host_state_and_static_sims(dev):
             assert float(hs['gate_d']) == float(step.gate_d) and float(hs['gate_s']) == float(step.gate_s)
             hist.append(hs['params'].clone())
         assert step.graph is not None and 'copy' not in step._sims and len(step._sims) == 3
+        # every capture (the real half, one sim half per ring buffer) writes the bucket views:
+        # no gradient of the D step goes through an autograd add
+        assert ops.KERNEL_CALLS.get('grad_dest_autograd_add', 0) == adds0
         assert bool(torch.isfinite(step.samples).all()) and bool((step.samples > 0).all())
         runs.append((torch.stack(hist), [p.detach().clone() for p in netD.parameters()]))
     assert torch.equal(runs[0][0], runs[1][0])
@@ -813,6 +817,7 @@ def test_second_gradient_sinks_match_autograd_accumulate(dev):
         gb = GradBuckets(net.parameters(), second_sinks=second)
         opt = ops.FusedAdam(net.parameters(), lr=1e-3, betas=(0.5, 0.999))
         opt.set_zero_grads(True)
+        adds0 = ops.KERNEL_CALLS.get('grad_dest_autograd_add', 0)
         for _ in range(3):
             gb.zero_()
             la, _ = net.bce_bf16(xa, 1.0)
@@ -822,7 +827,9 @@ def test_second_gradient_sinks_match_autograd_accumulate(dev):
             opt.step()
         torch.cuda.synchronize()
         nets.append(net)
-        adds.append(sum(1 for p in net.parameters() if getattr(p, '_bt_grad_second', False)))
-    assert adds[0] == 0 and adds[1] == len(list(nets[1].parameters()))
+        adds.append((sum(1 for p in net.parameters() if getattr(p, '_bt_grad_second', False)),
+                     ops.KERNEL_CALLS.get('grad_dest_autograd_add', 0) - adds0))
+    n = len(list(nets[1].parameters()))
+    assert adds[0] == (0, 3 * n) and adds[1] == (n, 0), adds
     for (n, pa), pb in zip(nets[0].named_parameters(), nets[1].parameters()):
         assert torch.equal(pa, pb), n
