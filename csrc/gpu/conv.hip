@@ -1417,8 +1417,9 @@ constexpr int c4p_lds() {
 // KD: dY ring depth (steps in flight per wave).  2 (136 VGPRs, 3 waves per SIMD):
 // 4 (173 VGPRs, 2 waves) measured 29.6 against 27.8 us with the BN backward
 // (profiles/r6/b4/c4w_bench.jsonl, profiles/r6/b2/c4w_bench.jsonl)
-// PRE: the first decode round's loads issued before the BN fold (139 VGPRs: 2 waves per SIMD,
-// against 3 without; the launch holds ~1.9 waves per SIMD either way) -- BT_C4P_PRE
+// PRE: the first decode round's loads issued before the BN fold, so their latency hides under
+// the fold's accumulator reads (BT_C4P_PRE, default on; 4-row bands are LDS-limited to 2 blocks
+// per CU either way)
 template <int R, int KD = 2, bool PRE = false>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_c4p_kernel(ConvWgradParams p) {
   constexpr int PR = 2 * R + 2;
@@ -3406,8 +3407,9 @@ int c4w_waves() {
 
 // BT_C4W_PATCH (default 1): the first layer's weight gradient from a decoded input patch
 // (conv_wgrad_c4p_kernel) when the shape takes it; BT_C4P_ROWS: output rows per band (1, 2, 4)
+// default on: 21.55k / 21.54k against 21.27k / 21.45k img/s (profiles/r6/b6/disc_*.jsonl); BT_C4P_PRE=0: off
 bool c4p_pre() {
-  static const bool on = std::getenv("BT_C4P_PRE") && std::getenv("BT_C4P_PRE")[0] == '1';
+  static const bool on = !(std::getenv("BT_C4P_PRE") && std::getenv("BT_C4P_PRE")[0] == '0');
   return on;
 }
 int g_c4p_override = -1;   // conv_set_c4p_rows (tests / benches): -1 = the environment's choice

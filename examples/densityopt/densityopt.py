@@ -212,10 +212,13 @@ def run(args):
         t0 = time.time()
         wait_s = 0.0
         epoch = 0
+        cpu0 = None
+        prod_pids = [p.pid for p in bl.launch_info.processes] if bl.launch_info is not None else []
         while True:
             steady = epoch >= steady_from
             if steady and t_steady is None:
                 t_steady = time.perf_counter()
+                cpu0 = _cpu_snapshot(prod_pids)
             ta = time.perf_counter()
             batch = next(gen_sim)
             tb = time.perf_counter()
@@ -271,6 +274,7 @@ def run(args):
             if epoch > args.num_epochs:
                 break
         t_end = time.perf_counter()
+        cpu1 = _cpu_snapshot(prod_pids) if cpu0 is not None else None
         dt = time.time() - t0
         for f in pending:
             f.result()
@@ -300,6 +304,8 @@ def run(args):
             if ev is None:
                 res['steady']['ms_per_iteration'].pop('gpu_iteration')
                 res['steady']['ms_per_iteration'].pop('gpu_real_half')
+            if cpu1 is not None:
+                res['steady']['cpu'] = _cpu_report(cpu0, cpu1, n_steady, st)
         # the reference's record of convergence: parameter history with the
         # target appended as the last row (densityopt.py:326-331, 350-354)
         hist = torch.stack(history + [tgt]).numpy()
@@ -317,6 +323,57 @@ def run(args):
             res['weights_checksum'] = float(w.double().sum())
             res['weights_sha'] = __import__('hashlib').sha1(w.cpu().numpy().tobytes()).hexdigest()[:16]
         return res
+
+
+def _cpu_snapshot(pids=()):
+    """(this process's threads {tid: (name, cpu seconds)}, the producer processes' cpu
+    seconds, the host's busy and total jiffies from /proc/stat): where the CPU of the steady
+    window goes -- this process's threads (main, loader IO / worker, HIP runtime), the
+    producers, and the whole machine (which on a shared host includes other tenants)."""
+    import os
+    tick = os.sysconf('SC_CLK_TCK')
+    prod = 0.0
+    for pid in pids:
+        try:
+            with open(f'/proc/{pid}/stat') as f:
+                parts = f.read().rsplit(')', 1)[1].split()
+            prod += sum(int(x) for x in parts[11:15]) / tick   # utime stime cutime cstime
+        except (OSError, ValueError, IndexError):
+            pass
+    th = {}
+    try:
+        for tid in os.listdir('/proc/self/task'):
+            try:
+                with open(f'/proc/self/task/{tid}/stat') as f:
+                    parts = f.read().rsplit(')', 1)[1].split()
+                with open(f'/proc/self/task/{tid}/comm') as f:
+                    name = f.read().strip()
+                th[int(tid)] = (name, (int(parts[11]) + int(parts[12])) / tick)
+            except (OSError, ValueError, IndexError):
+                pass
+        with open('/proc/stat') as f:
+            v = [int(x) for x in f.readline().split()[1:]]
+        busy, total = sum(v) - v[3] - (v[4] if len(v) > 4 else 0), sum(v)
+    except OSError:
+        busy = total = 0
+    return th, busy, total, prod
+
+
+def _cpu_report(a, b, iters, seconds):
+    """CPU-ms per iteration of this process (total and its 5 busiest threads) and the
+    host's busy CPUs over the window."""
+    import os
+    th = {}
+    for tid, (name, t1) in b[0].items():
+        t0 = a[0].get(tid, (name, 0.0))[1]
+        th[f'{name}:{tid}'] = t1 - t0
+    top = sorted(th.items(), key=lambda kv: -kv[1])[:5]
+    ncpu = os.cpu_count() or 1
+    frac = (b[1] - a[1]) / max(1, b[2] - a[2])
+    return {'process_ms_per_iteration': round(sum(th.values()) * 1e3 / iters, 4),
+            'threads_ms_per_iteration': {k: round(v * 1e3 / iters, 4) for k, v in top},
+            'producers_ms_per_iteration': round((b[3] - a[3]) * 1e3 / iters, 4),
+            'host_busy_cpus': round(frac * ncpu, 2), 'host_cpus': ncpu}
 
 
 def main(argv=None):

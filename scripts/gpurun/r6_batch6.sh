@@ -38,3 +38,9 @@ for r in d.get('runs',[d]): print(json.dumps({'it_s':round(r['iterations_per_s']
 bash scripts/gpurun/disc_roofline.sh r6b6 > $O/roofline.log 2>&1 || { tail -20 $O/roofline.log; exit 1; }
 cp gpurun_out/roof_r6b6/roofline.md gpurun_out/roof_r6b6/step_sequence.txt $O/
 cat $O/roofline.md
+for v in "inline:" "prefetch:--prefetch" "inline:" "prefetch:--prefetch"; do
+  name=${v%%:*}; a=${v#*:}
+  timeout -k 10 300 python examples/densityopt/densityopt.py --num-epochs 1000 --image-every 0 --out-dir '' $a \
+    --json $O/dopt_ab.json > $O/dopt_ab.log 2>&1 || { tail -5 $O/dopt_ab.log; exit 1; }
+  python -c "import json; d=json.load(open('$O/dopt_ab.json')); s=d['steady']; print(json.dumps({'v':'$name','it_s':round(s['iterations_per_s'],1),'ms':s['ms_per_iteration'],'cpu':s.get('cpu')}))" | tee -a $O/dopt_ab.jsonl
+done
