@@ -35,6 +35,7 @@
 #include <cstdint>
 #include <cstring>
 #include <type_traits>
+#include <vector>
 
 #include "adam_sched.h"
 #include "bn_fold.h"
@@ -1440,31 +1441,40 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4p_kernel(ConvWgradParam
   const int PW = p.W + 2;
   const int dc = lane & 3, dp = lane >> 2;
   const bool bnd = p.bn_dy.y != nullptr;
-  // the band's input rows 2 oh0 - 1 .. 2 (oh0 + R) decoded once: DL loads in flight per thread and
-  // round, then their lookups; the first round's loads are issued before the BN fold, so their
-  // latency hides under the fold's own accumulator reads
+  // the band's input rows 2 oh0 - 1 .. 2 (oh0 + R) decoded once: 16-byte loads of 4 input pixels
+  // (W % 64 == 0: c4p_rows_for), DQ in flight per thread and round -- a 4-row band of a 640-wide
+  // frame is one round (1600 quads; 4-byte loads took 4 rounds of 8, a memory latency each) --
+  // then their lookups; the first round's loads are issued before the BN fold, so their latency
+  // hides under the fold's own accumulator reads
   const __amdgpu_buffer_rsrc_t rs_x = make_rsrc(p.x, int64_t(p.N) * p.H * p.W * 4);
-  const int npx = PR * PW, ih0 = 2 * oh0 - 1;
-  constexpr int DL = 8;
-  auto issue = [&](int i0, uint32_t (&wv)[DL], bool (&ok)[DL]) __attribute__((always_inline)) {
+  const int QW = p.W >> 2, nq = PR * QW, ih0 = 2 * oh0 - 1;
+  constexpr int DQ = 8;
+  auto issue = [&](int i0, uint4 (&wv)[DQ], bool (&ok)[DQ]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int k = 0; k < DL; ++k) {
+    for (int k = 0; k < DQ; ++k) {
       const int i = i0 + k * kThreads + t;
-      const int pr = i / PW, pc = i - pr * PW;
-      const int ih = ih0 + pr, iw = pc - 1;
-      ok[k] = i < npx && unsigned(ih) < unsigned(p.H) && unsigned(iw) < unsigned(p.W);
-      wv[k] = bload4(rs_x, ok[k] ? uint32_t(((n * p.H + ih) * p.W + iw) * 4) : kOOB);
+      const int pr = i / QW, qc = i - pr * QW;
+      const int ih = ih0 + pr;
+      ok[k] = i < nq && unsigned(ih) < unsigned(p.H);
+      wv[k] = bload(rs_x, ok[k] ? uint32_t(((n * p.H + ih) * p.W + 4 * qc) * 4) : kOOB);
     }
   };
-  auto lookups = [&](int i0, const uint32_t (&wv)[DL], const bool (&ok)[DL]) __attribute__((always_inline)) {
+  auto lookups = [&](int i0, const uint4 (&wv)[DQ], const bool (&ok)[DQ]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int k = 0; k < DL; ++k) {
+    for (int k = 0; k < DQ; ++k) {
       const int i = i0 + k * kThreads + t;
-      if (i < npx) *reinterpret_cast<uint2*>(patch + i * 8) = lut_px(lutl, wv[k], ok[k]);
+      if (i < nq) {
+        const int pr = i / QW, qc = i - pr * QW;
+        uint2* d = reinterpret_cast<uint2*>(patch + (pr * PW + 4 * qc + 1) * 8);   // columns 4 qc + 1 ..
+        d[0] = lut_px(lutl, wv[k].x, ok[k]);
+        d[1] = lut_px(lutl, wv[k].y, ok[k]);
+        d[2] = lut_px(lutl, wv[k].z, ok[k]);
+        d[3] = lut_px(lutl, wv[k].w, ok[k]);
+      }
     }
   };
-  uint32_t wv0[DL];
-  bool ok0[DL];
+  uint4 wv0[DQ];
+  bool ok0[DQ];
   if constexpr (PRE) issue(0, wv0, ok0);
   BnBwdCoef bc[8];
   if (bnd) {   // (LDS scratch: the front, free until the patch is written)
@@ -1473,10 +1483,12 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4p_kernel(ConvWgradParam
   }
   stage_lut(p.lut, lutl);
   __syncthreads();
+  for (int i = t; i < 2 * PR; i += kThreads)   // the zero padding columns 0 and W + 1
+    *reinterpret_cast<uint2*>(patch + ((i >> 1) * PW + ((i & 1) ? PW - 1 : 0)) * 8) = make_uint2(0u, 0u);
   if constexpr (PRE) lookups(0, wv0, ok0);
-  for (int i0 = PRE ? DL * kThreads : 0; i0 < npx; i0 += DL * kThreads) {
-    uint32_t wv[DL];
-    bool ok[DL];
+  for (int i0 = PRE ? DQ * kThreads : 0; i0 < nq; i0 += DQ * kThreads) {
+    uint4 wv[DQ];
+    bool ok[DQ];
     issue(i0, wv, ok);
     lookups(i0, wv, ok);
   }
@@ -1684,6 +1696,12 @@ struct TapGemm {
   // launch after a grid barrier on its statistics (acc = stats); oy receives leaky(bn(dst))
   BnActIn oact;
   uint16_t* oy = nullptr;
+  // forward split-K (tap_gemm_body SPLIT = 2): the first block of a tile's pair to finish its
+  // K half parks its fp32 accumulators here ([tile][FM * FN][kThreads] float4) and raises
+  // split_ready[tile]; the second adds them to its own and runs the epilogue.  Both words zero
+  // between launches (the second block resets them).
+  float* split_part = nullptr;
+  unsigned* split_ticket = nullptr;   // [2 * tiles]: ticket, ready
 };
 
 // BN = output channels per block (128 or 64, or 32 for 32-channel outputs
@@ -1722,9 +1740,12 @@ constexpr int tap_gemm_lds() {
 // sums, waits at a grid barrier, folds the accumulator (bn_apply_kernel's
 // fold: the same mean / invstd) and writes leaky(bn(z)) of its accumulators
 // to p.oy next to z (Conv1Bn has the first layer's form of the same).
-template <bool DGRAD, int BN, bool C4 = false, int BM = FBM, int NST = 0, int CLS = 1, int ACT = 0, bool OBN = false>
+// SPLIT (plain forward, LDS-DMA staging): 2 blocks per tile, each half of K; see TapGemm::split_part
+template <bool DGRAD, int BN, bool C4 = false, int BM = FBM, int NST = 0, int CLS = 1, int ACT = 0, bool OBN = false,
+          int SPLIT = 1>
 __device__ __forceinline__ void tap_gemm_body(const TapGemm& p, char* smem, int bx, int by, int nwg) {
   static_assert(ACT == 0 || (!DGRAD && !C4 && NST >= 2), "the BN apply rides on the forward's LDS-DMA staging");
+  static_assert(SPLIT == 1 || (SPLIT == 2 && !DGRAD && !C4 && NST >= 2 && ACT == 0 && !OBN), "split-K: plain forward");
   static_assert(!OBN || (!DGRAD && !C4 && ACT == 0), "the output BN: plain forward only");
   constexpr int RJ = BM / 32;                  // staged A rows per thread (ar + 32 j)
   constexpr int A_TILE = BM * F_ROW;
@@ -1769,7 +1790,9 @@ __device__ __forceinline__ void tap_gemm_body(const TapGemm& p, char* smem, int 
 
   const int b = bx;
   const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  const int wr = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  // split-K: consecutive work ids (one XCD) are the two K halves of one tile
+  const int w = SPLIT > 1 ? wr / SPLIT : wr, khalf = SPLIT > 1 ? wr - w * SPLIT : 0;
   const int mt = w / NT, n0 = (w - mt * NT) * BN;
   const int m0 = mt * BM;
   // epilogue geometry: every thread takes whole 16-byte row chunks -- CPR
@@ -1940,7 +1963,8 @@ __device__ __forceinline__ void tap_gemm_body(const TapGemm& p, char* smem, int 
       }
     }
   };
-  const int nsteps = K / FBK;
+  const int nsteps = K / FBK / SPLIT;   // (split-K: this block's half; the host checks divisibility)
+  const int ks0 = khalf * nsteps;
   auto load = [&](int ks) {
     if constexpr (C4) {
       load_c4();
@@ -1991,6 +2015,7 @@ __device__ __forceinline__ void tap_gemm_body(const TapGemm& p, char* smem, int 
   const int wv = __builtin_amdgcn_readfirstlane(wave);
   const uint32_t wrow_b = uint32_t((n0 + ar) * 16 * p.C) * 2u;   // byte offset of B row ar
   auto issue = [&](int ks, int buf) {
+    ks += ks0;
     const int kc = ks * FBK + acs * 8;
     const int tap = kc >> p.cshift, ch = kc & (p.C - 1);
     int dr, dc;
@@ -2182,6 +2207,53 @@ __device__ __forceinline__ void tap_gemm_body(const TapGemm& p, char* smem, int 
       }
     }
     __syncthreads();   // the epilogue reuses the staging LDS
+  }
+
+  if constexpr (SPLIT > 1) {
+    // split-K: the first block of the tile's pair to get here parks its accumulators (device-scope
+    // stores, written through this XCD's L2) and leaves; the second waits for them (the first is
+    // running -- it took the ticket -- so the wait is bounded), adds them to its own (a + b == b + a:
+    // the same bits whichever half finishes first) and runs the epilogue
+    unsigned* role = reinterpret_cast<unsigned*>(smem);   // (the staging LDS is free: DIRECT epilogue)
+    unsigned* tk = p.split_ticket + 2 * w;
+    if (t == 0) *role = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const unsigned first = *role == 0u;
+    const __amdgpu_buffer_rsrc_t rs_part =
+        make_rsrc(p.split_part + int64_t(w) * (FM * FN) * kThreads * 4, int64_t(FM * FN) * kThreads * 16);
+    if (first) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs_part,
+                                                 ((i * FN + j) * kThreads + t) * 16, 0, 16 /* sc1 */);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t == 0) __hip_atomic_store(tk + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    if (t == 0) {
+      unsigned n = 0;
+      while (__hip_atomic_load(tk + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++n == kBarrierSpins) {   // (never expected: flag it like a failed grid barrier)
+          atomicAdd(&g_grid_barrier_timeouts, 1u);
+          if (unsigned* f = g_grid_barrier_flag) __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+      }
+      __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // both words zero for the next launch
+      __hip_atomic_store(tk + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs_part, ((i * FN + j) * kThreads + t) * 16, 0, 16);
+        acc[i][j] += __builtin_bit_cast(f32x4, v);
+      }
   }
 
   if constexpr (DIRECT) {
@@ -2554,10 +2626,12 @@ __device__ __forceinline__ void tap_gemm_body(const TapGemm& p, char* smem, int 
   }
 }
 
-template <bool DGRAD, int BN, bool C4 = false, int BM = FBM, int NST = 0, int CLS = 1, int ACT = 0, bool OBN = false>
+template <bool DGRAD, int BN, bool C4 = false, int BM = FBM, int NST = 0, int CLS = 1, int ACT = 0, bool OBN = false,
+          int SPLIT = 1>
 __global__ __launch_bounds__(kThreads) void tap_gemm_kernel(TapGemm p) {
   __shared__ __attribute__((aligned(16))) char smem[tap_gemm_lds<DGRAD, BN, C4, BM, NST>()];
-  tap_gemm_body<DGRAD, BN, C4, BM, NST, CLS, ACT, OBN>(p, smem, int(blockIdx.x), int(blockIdx.y), int(gridDim.x));
+  tap_gemm_body<DGRAD, BN, C4, BM, NST, CLS, ACT, OBN, SPLIT>(p, smem, int(blockIdx.x), int(blockIdx.y),
+                                                             int(gridDim.x));
 }
 
 // ---------------------------------------------------------------------------
@@ -3880,6 +3954,67 @@ int device_cus() {
   }
   return cus;
 }
+// Split-K forward (tap_gemm_body SPLIT = 2, BT_CONV_FWD_SPLIT=1): 128-channel tiles whose two K
+// halves run as two blocks, for the deep layers whose grids are short of tiles (conv3: 300 tiles of
+// 128 x 128, conv4: 150 of 64 x 128).  A 128 x 128 tile stages 64 FLOP per byte against 43 for the
+// 128 x 64 tiles it replaces; the cost is the parked accumulators (64 KiB per tile, written once
+// through to memory and read once by the partner block).  The scratch is per device, grown outside
+// a graph capture (a forward captured before an eager one of its size runs unsplit): split forwards
+// of one device run one at a time -- on one stream, as a training step's graph does (torch captures
+// on its own stream, warm-up runs on another: per-stream scratch would never be there to capture).
+int g_fwd_split = -1;
+int64_t g_fwd_split_launches = 0;   // (tests: the split path ran)
+bool fwd_split_on() {
+  if (g_fwd_split < 0) {
+    const char* v = std::getenv("BT_CONV_FWD_SPLIT");
+    g_fwd_split = v && v[0] == '1' ? 1 : 0;
+  }
+  return g_fwd_split == 1;
+}
+struct SplitScratch {
+  int device = -1;
+  float* part = nullptr;
+  unsigned* ticket = nullptr;
+  int64_t tiles = 0;
+};
+std::vector<SplitScratch> g_split_scratch;
+SplitScratch& split_scratch() {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  for (auto& s : g_split_scratch)
+    if (s.device == dev) return s;
+  g_split_scratch.push_back(SplitScratch{dev});
+  return g_split_scratch.back();
+}
+// the split forward's pixel tile (64 / 128) for this GEMM, or 0: run it unsplit
+int fwd_split_bm(const TapGemm& g, hipStream_t stream) {
+  if (!fwd_split_on() || g.C == 4 || g.act.on() || g.oact.on() || g.NOUT % 128 || staging() != 2 ||
+      (16 * g.C / FBK) % 2)
+    return 0;
+  const int bm = (int64_t(g.M) + FBM - 1) / FBM * (g.NOUT / 128) * 2 >= g_bm64_below ? FBM : 64;
+  const int64_t tiles = (int64_t(g.M) + bm - 1) / bm * (g.NOUT / 128);
+  SplitScratch& sc = split_scratch();
+  if (sc.tiles < tiles) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return 0;
+    if (hipDeviceSynchronize() != hipSuccess) return 0;   // (the old scratch may be in use)
+    if (sc.part) (void)hipFree(sc.part);
+    if (sc.ticket) (void)hipFree(sc.ticket);
+    sc.part = nullptr, sc.ticket = nullptr, sc.tiles = 0;
+    // (FM * FN float4 per thread: 64 KiB per 128 x 128 tile, half that for 64 x 128)
+    if (hipMalloc(&sc.part, size_t(tiles * (FBM / 32) * 4 * kThreads * 16)) != hipSuccess ||
+        hipMalloc(&sc.ticket, size_t(tiles) * 2 * sizeof(unsigned)) != hipSuccess ||
+        hipMemset(sc.ticket, 0, size_t(tiles) * 2 * sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+      if (sc.part) (void)hipFree(sc.part);
+      if (sc.ticket) (void)hipFree(sc.ticket);
+      sc.part = nullptr, sc.ticket = nullptr;
+      (void)hipGetLastError();
+      return 0;
+    }
+    sc.tiles = tiles;
+  }
+  return bm;
+}
 // BT_CONV_OUT_BN=0: the tap-GEMM forward never applies its output's BN
 bool g_out_bn = !(std::getenv("BT_CONV_OUT_BN") && std::getenv("BT_CONV_OUT_BN")[0] == '0');
 // blocks of the BN-applying tap-GEMM forward (64-channel tiles, 2 LDS-DMA stages) resident at once
@@ -4090,9 +4225,21 @@ hipError_t conv_fwd(const ConvFwdParams& p, hipStream_t stream) {
       return hipGetLastError();
     }
   }
+  if (const int sbm = fwd_split_bm(g, stream)) {
+    SplitScratch& sc = split_scratch();
+    g.split_part = sc.part, g.split_ticket = sc.ticket;
+    ++g_fwd_split_launches;
+    const dim3 grid(unsigned((g.M + sbm - 1) / sbm * (g.NOUT / 128) * 2));
+    if (sbm == 64) tap_gemm_kernel<false, 128, false, 64, 2, 1, 0, false, 2><<<grid, kThreads, 0, stream>>>(g);
+    else tap_gemm_kernel<false, 128, false, FBM, 2, 1, 0, false, 2><<<grid, kThreads, 0, stream>>>(g);
+    return hipGetLastError();
+  }
   launch_tap_gemm<false>(g, 1, stream);
   return hipGetLastError();
 }
+
+void conv_set_fwd_split(int on) { g_fwd_split = on < 0 ? -1 : (on ? 1 : 0); }
+int64_t conv_fwd_split_launches() { return g_fwd_split_launches; }
 
 hipError_t conv_weight_t(const uint16_t* w, uint16_t* wt, int Cout, int Cin, hipStream_t stream) {
   if (!w || !wt || Cout <= 0 || Cin <= 0) return hipErrorInvalidValue;

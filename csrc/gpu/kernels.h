@@ -397,9 +397,11 @@ int conv_wgrad_slices(int64_t M, int Cin, int Cout, int target_blocks);
 // the u8 first layer's weight gradient from a decoded input patch (conv_wgrad_c4p_kernel): output rows
 // per band -- its slices must then be bands, px_per_slice = rows * Wo -- or 0 when the shape does not take it
 int conv_c4p_rows(int N, int H, int W, int Ho, int Wo, int Cout);
-void conv_set_c4p_rows(int rows);
-void conv_set_wgrad_co128(int on);
-void conv_set_dgrad_bn128(int on);   // 128-channel tiles for the held (fused) data gradient: 1 / 0 / -1 env   // 128-channel weight-gradient tiles: 1 on, 0 off, -1 BT_WGRAD_CO128   // 0: off, 1 / 2 / 4 rows, else back to BT_C4W_PATCH / BT_C4P_ROWS
+void conv_set_c4p_rows(int rows);       // 0: off, 1 / 2 / 4 rows, else back to BT_C4W_PATCH / BT_C4P_ROWS
+void conv_set_wgrad_co128(int on);      // 128-channel weight-gradient tiles: 1 on, 0 off, -1 BT_WGRAD_CO128
+void conv_set_dgrad_bn128(int on);      // 128-channel tiles for the held (fused) data gradient: 1 / 0 / -1 env
+void conv_set_fwd_split(int on);        // split-K forward of the 128-channel layers: 1 / 0 / -1 BT_CONV_FWD_SPLIT
+int64_t conv_fwd_split_launches();      // forwards launched split so far (this process)
 // Weight-gradient staging (not the 4-channel layer): 0 = register ring,
 // 2 / 3 = LDS-DMA stages of 64 pixels (default 0; -1 = BT_WGRAD_STAGING or default).
 void conv_set_fwd_patch(int on, int dbg = 0, int blocks = 0);       // 1 the 32->64 forward's persistent patch GEMM, 0 the tap GEMM, -1 env

@@ -302,6 +302,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("conv_set_c4p_rows", &conv_set_c4p_rows);
   m.def("conv_set_wgrad_co128", &conv_set_wgrad_co128);
   m.def("conv_set_dgrad_bn128", &conv_set_dgrad_bn128);
+  m.def("conv_set_fwd_split", &conv_set_fwd_split);
+  m.def("conv_fwd_split_launches", &conv_fwd_split_launches);
   m.def("conv_dgrad_hold", [](int on) { conv_dgrad_hold(on); });
   m.def("conv_dgrad_flush", []() { check(conv_dgrad_flush(), "conv_dgrad_flush"); });
   m.def("conv_dgrad_held", []() { return conv_dgrad_held(); });

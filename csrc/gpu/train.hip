@@ -375,7 +375,7 @@ struct BnApplyFold {
   int release = 1;             // 0: no ticket / clear (BT_BN_RELEASE=0: timing diagnostics only)
 };
 
-template <int DT, bool BWD, bool FOLD = false>
+template <int DT, bool BWD, bool FOLD = false, int U = kBnUnroll>
 __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const void* __restrict__ x, const void* __restrict__ gy,
                                                           void* __restrict__ out, int64_t M, int C,
                                                           const float* __restrict__ mean,
@@ -383,7 +383,7 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const void* __restrict
                                                           const float* __restrict__ w, const float* __restrict__ b,
                                                           const float* __restrict__ dw, const float* __restrict__ db,
                                                           float slope, BnApplyFold fa = BnApplyFold()) {
-  constexpr int V = BnVec<DT>::V, U = kBnUnroll;
+  constexpr int V = BnVec<DT>::V;
   const int G = C / V;
   const int64_t total = M * G;
   const float invM = 1.f / float(M);
@@ -542,8 +542,8 @@ void bn_blocks(int64_t M, int C, int dtype, int& nblocks, int64_t& rows_per_bloc
   rows_per_block = (M + nblocks - 1) / nblocks;
 }
 
-int bn_grid(int64_t work) {   // work = 16-byte vectors; kBnUnroll per lane per pass
-  const int64_t blocks = (work + kBlock * kBnUnroll - 1) / (kBlock * kBnUnroll);
+int bn_grid(int64_t work, int unroll = kBnUnroll) {   // work = 16-byte vectors; `unroll` per lane per pass
+  const int64_t blocks = (work + kBlock * unroll - 1) / (kBlock * unroll);
   return int(blocks < 4096 ? (blocks < 1 ? 1 : blocks) : 4096);
 }
 
@@ -554,17 +554,34 @@ int bn_grid(int64_t work) {   // work = 16-byte vectors; kBnUnroll per lane per 
 // some blocks and 1 for the rest).  Disc step: 18.8k -> 19.1-19.3k img/s,
 // forward applies 42.2 -> 37.3 us (profiles/r4/b33/).  BT_BN_FOLD_GRID: the
 // cap; BT_BN_FOLD_BALANCE=0: plain capping.
-int bn_fold_grid(int64_t work) {
+int bn_fold_cap() {
   static const int cap = [] {
     const char* e = std::getenv("BT_BN_FOLD_GRID");
     const int v = e ? std::atoi(e) : 512;
     return v > 0 ? v : 512;
   }();
+  return cap;
+}
+// Vectors per lane and pass of the folding applies: 8 when 4 would take more than one pass of the
+// capped grid.  A memory-bound launch needs ~16 MB in flight (8 TB/s x ~2 us); the 128-channel
+// layer's forward apply ran 300 blocks x 4 waves x 64 B per lane (~5 MB): 2.1 TB/s.  BT_BN_UNROLL=4 / 8
+// forces one.
+int bn_fold_unroll(int64_t work) {
+  static const int force = [] {
+    const char* e = std::getenv("BT_BN_UNROLL");
+    const int v = e ? std::atoi(e) : 0;
+    return v == 4 || v == 8 ? v : 0;
+  }();
+  if (force) return force;
+  return bn_grid(work) > bn_fold_cap() ? 8 : 4;
+}
+int bn_fold_grid(int64_t work, int unroll = kBnUnroll) {
+  const int cap = bn_fold_cap();
   static const bool balance = [] {
     const char* e = std::getenv("BT_BN_FOLD_BALANCE");
     return !(e && e[0] == '0');
   }();
-  const int g = bn_grid(work);
+  const int g = bn_grid(work, unroll);
   if (g <= cap) return g;
   if (!balance) return cap;
   const int passes = (g + cap - 1) / cap;
@@ -696,13 +713,16 @@ hipError_t bn_apply_acc(const void* x, void* y, int64_t M, int C, int dtype, BnA
   fa.o0 = mean, fa.o1 = invstd, fa.rm = running_mean, fa.rv = running_var, fa.tracked = tracked;
   fa.release = bn_release_env();
   const int V = dtype == OUT_BF16 ? 8 : 4;
-  const int grid = bn_fold_grid(M * (C / V));
-  if (dtype == OUT_BF16)
-    bn_apply_kernel<OUT_BF16, false, true><<<grid, kBlock, 0, stream>>>(x, nullptr, y, M, C, nullptr, nullptr, w, b,
-                                                                        nullptr, nullptr, slope, fa);
-  else
-    bn_apply_kernel<OUT_F32, false, true><<<grid, kBlock, 0, stream>>>(x, nullptr, y, M, C, nullptr, nullptr, w, b,
-                                                                       nullptr, nullptr, slope, fa);
+  const int u = bn_fold_unroll(M * (C / V));
+  const int grid = bn_fold_grid(M * (C / V), u);
+#define BT_BN_FWD(DT_, U_) \
+  bn_apply_kernel<DT_, false, true, U_><<<grid, kBlock, 0, stream>>>(x, nullptr, y, M, C, nullptr, nullptr, w, b, \
+                                                                     nullptr, nullptr, slope, fa)
+  if (dtype == OUT_BF16 && u == 8) BT_BN_FWD(OUT_BF16, 8);
+  else if (dtype == OUT_BF16) BT_BN_FWD(OUT_BF16, 4);
+  else if (u == 8) BT_BN_FWD(OUT_F32, 8);
+  else BT_BN_FWD(OUT_F32, 4);
+#undef BT_BN_FWD
   return hipGetLastError();
 }
 
@@ -716,13 +736,16 @@ hipError_t bn_bwd_apply_acc(const void* x, const void* gy, void* gx, int64_t M, 
   fa.acc = acc.acc, fa.R = acc.R, fa.o0 = db, fa.o1 = dw;
   fa.release = bn_release_env();
   const int V = dtype == OUT_BF16 ? 8 : 4;
-  const int grid = bn_fold_grid(M * (C / V));
-  if (dtype == OUT_BF16)
-    bn_apply_kernel<OUT_BF16, true, true><<<grid, kBlock, 0, stream>>>(x, gy, gx, M, C, mean, invstd, w, b, nullptr,
-                                                                       nullptr, slope, fa);
-  else
-    bn_apply_kernel<OUT_F32, true, true><<<grid, kBlock, 0, stream>>>(x, gy, gx, M, C, mean, invstd, w, b, nullptr,
-                                                                      nullptr, slope, fa);
+  const int u = bn_fold_unroll(M * (C / V));
+  const int grid = bn_fold_grid(M * (C / V), u);
+#define BT_BN_BWD(DT_, U_) \
+  bn_apply_kernel<DT_, true, true, U_><<<grid, kBlock, 0, stream>>>(x, gy, gx, M, C, mean, invstd, w, b, nullptr, \
+                                                                    nullptr, slope, fa)
+  if (dtype == OUT_BF16 && u == 8) BT_BN_BWD(OUT_BF16, 8);
+  else if (dtype == OUT_BF16) BT_BN_BWD(OUT_BF16, 4);
+  else if (u == 8) BT_BN_BWD(OUT_F32, 8);
+  else BT_BN_BWD(OUT_F32, 4);
+#undef BT_BN_BWD
   return hipGetLastError();
 }
 

@@ -1161,3 +1161,55 @@ def test_patch_dgrad_with_wide_wgrad_one_launch(dev, hw, wide):
     assert torch.equal(dx, alone)
     ref = torch.nn.grad.conv2d_weight(x.float(), (cout, cin, 4, 4), dy.float(), stride=2, padding=1)
     torch.testing.assert_close(gw, ref, rtol=1e-3, atol=1e-3 * float(ref.abs().max()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('N,C,H,W,CO', [(8, 64, 120, 160, 128), (8, 128, 60, 80, 256), (2, 64, 30, 46, 128),
+                                        (1, 128, 18, 130, 256)])
+def test_fwd_split_k_matches_fp32(dev, N, C, H, W, CO):
+    """The split-K forward (tap_gemm_body SPLIT = 2: two blocks per 128-channel
+    tile, one K half each, the first to finish parks its accumulators for the
+    second): matches fp32 conv2d and the unsplit forward to bf16 rounding, its
+    BN sums match the output's, and repeated runs (eager and graph replays --
+    the tickets reset themselves) are bit-identical: a + b is the same bits
+    whichever half finishes first."""
+    cl = torch.channels_last
+    g = torch.Generator(device=dev).manual_seed(C + H)
+    x = torch.randn(N, C, H, W, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    w = (0.05 * torch.randn(CO, C, 4, 4, device=dev, generator=g)).to(torch.bfloat16).contiguous(memory_format=cl)
+    ext = ops.hip_ext()
+    ref = torch.nn.functional.conv2d(x.float(), w.float(), stride=2, padding=1)
+    y0 = ops.conv_fwd(x, w)
+    ext.conv_set_fwd_split(1)
+    try:
+        n0 = ext.conv_fwd_split_launches()
+        acc = ops.BnAccumulator(CO, dev)
+        y1 = ops.conv_fwd(x, w, acc.fwd, acc.R)
+        y2 = ops.conv_fwd(x, w)
+        assert ext.conv_fwd_split_launches() == n0 + 2
+        stream = torch.cuda.Stream(dev)
+        stream.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(stream):
+            ops.conv_fwd(x, w)             # (the capture stream's scratch, allocated eagerly)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=stream):
+                yg = ops.conv_fwd(x, w)
+        torch.cuda.current_stream(dev).wait_stream(stream)
+        outs = []
+        for _ in range(3):
+            graph.replay()
+            outs.append(yg.clone())
+    finally:
+        ext.conv_set_fwd_split(-1)
+    torch.cuda.synchronize()
+    assert ext.conv_fwd_split_launches() == n0 + 4
+    assert torch.equal(y1, y2)
+    for o in outs:
+        assert torch.equal(o, y1)
+    torch.testing.assert_close(y1.float(), ref, rtol=2e-2, atol=2e-2)
+    # against the unsplit forward: the same products, summed as two halves (bf16 rounding apart)
+    assert (y1.float() - y0.float()).abs().max() <= 2 ** -6 * y0.float().abs().max()
+    s = acc.fwd[:acc.R * 2 * CO].view(acc.R, 2, CO).sum(0)
+    yf = y1.float().permute(0, 2, 3, 1).reshape(-1, CO).double()
+    torch.testing.assert_close(s[0], yf.sum(0), rtol=1e-4, atol=5e-2)
+    torch.testing.assert_close(s[1], (yf * yf).sum(0), rtol=1e-4, atol=5e-2)
