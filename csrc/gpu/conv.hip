@@ -3954,11 +3954,13 @@ int device_cus() {
   }
   return cus;
 }
-// Split-K forward (tap_gemm_body SPLIT = 2, BT_CONV_FWD_SPLIT=1): 128-channel tiles whose two K
-// halves run as two blocks, for the deep layers whose grids are short of tiles (conv3: 300 tiles of
-// 128 x 128, conv4: 150 of 64 x 128).  A 128 x 128 tile stages 64 FLOP per byte against 43 for the
-// 128 x 64 tiles it replaces; the cost is the parked accumulators (64 KiB per tile, written once
-// through to memory and read once by the partner block).  The scratch is per device, grown outside
+// Split-K forward (tap_gemm_body SPLIT = 2, BT_CONV_FWD_SPLIT=1, opt-in): 128-channel tiles whose
+// two K halves run as two blocks, for the deep layers whose grids are short of tiles (conv3: 300
+// tiles of 128 x 128, conv4: 150 of 64 x 128).  A 128 x 128 tile stages 64 FLOP per byte against 43
+// for the 128 x 64 tiles it replaces; the cost is the parked accumulators (64 KiB per tile, written
+// through to memory and read back by the partner block).  Measured slower: conv3 28.7-29.9 vs
+// 16.5-18.3 us, conv4 25.3 vs 16.7-17.4 us, the disc step 20.4-20.6k vs 21.5-21.7k img/s
+// (profiles/r6/b7/): the parked accumulators are ~20 MB a layer, as many bytes as the GEMM's own.  The scratch is per device, grown outside
 // a graph capture (a forward captured before an eager one of its size runs unsplit): split forwards
 // of one device run one at a time -- on one stream, as a training step's graph does (torch captures
 // on its own stream, warm-up runs on another: per-stream scratch would never be there to capture).

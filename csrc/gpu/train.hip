@@ -562,18 +562,16 @@ int bn_fold_cap() {
   }();
   return cap;
 }
-// Vectors per lane and pass of the folding applies: 8 when 4 would take more than one pass of the
-// capped grid.  A memory-bound launch needs ~16 MB in flight (8 TB/s x ~2 us); the 128-channel
-// layer's forward apply ran 300 blocks x 4 waves x 64 B per lane (~5 MB): 2.1 TB/s.  BT_BN_UNROLL=4 / 8
-// forces one.
-int bn_fold_unroll(int64_t work) {
-  static const int force = [] {
+// Vectors per lane and pass of the folding applies (BT_BN_UNROLL=8: twice the bytes in flight per
+// lane).  4: 8 measured no faster alone (bn3 fwd 7.41 vs 7.47 us, bn2 fwd 10.51 vs 9.78, bn2 bwd
+// 14.88 vs 13.06) and slower in the step (21.5-21.7k vs 21.9k img/s, profiles/r6/b7/): the applies'
+// excess over the plain pass is the fold's latency (2.0-3.1 us a launch), not the bytes in flight.
+int bn_fold_unroll(int64_t) {
+  static const int u = [] {
     const char* e = std::getenv("BT_BN_UNROLL");
-    const int v = e ? std::atoi(e) : 0;
-    return v == 4 || v == 8 ? v : 0;
+    return e && std::atoi(e) == 8 ? 8 : 4;
   }();
-  if (force) return force;
-  return bn_grid(work) > bn_fold_cap() ? 8 : 4;
+  return u;
 }
 int bn_fold_grid(int64_t work, int unroll = kBnUnroll) {
   const int cap = bn_fold_cap();
