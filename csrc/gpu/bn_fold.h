@@ -197,6 +197,40 @@ __device__ inline void bn_acc_release(double* acc, int R, int C, int* flag) {   
   bn_acc_release(acc, R, C, flag, blockIdx.x, gridDim.x);
 }
 
+// bn_acc_release in two halves, for a block with more work after its reads (bn_apply_kernel): thread
+// 0 takes the shard ticket as soon as the block's reads are back (behind a barrier) and keeps the
+// answer in a register; the block's remaining loads and stores then overlap that atomic's round
+// trip, and at the end (every thread) the shard's last block takes the top ticket and the device's
+// last block clears.  Waiting for the shard ticket before the apply pass cost 0.9-1.4 us a launch
+// (profiles/r6/b8/bn_apply_norel.jsonl against bn_apply.jsonl).
+__device__ inline unsigned bn_acc_ticket_take(double* acc, int R, int C, unsigned blk) {   // thread 0
+  // (+ the lane id, 0 here: with an address the compiler sees as uniform, its atomic optimizer
+  // folds the wave's lanes through the returned value right away -- a wait for the round trip)
+  return atomicAdd(bn_acc_ticket(acc, R, C) + (blk % kBnTicketShards) * kBnTicketStride + __lane_id(), 1u);
+}
+__device__ inline void bn_acc_ticket_finish(double* acc, int R, int C, int* flag, unsigned tk, unsigned blk,
+                                            unsigned nblk) {
+  const int t = int(threadIdx.x), nt = int(blockDim.x);
+  unsigned* ticket = bn_acc_ticket(acc, R, C);
+  if (t == 0) {
+    const unsigned s = blk % kBnTicketShards;
+    const unsigned in_shard = (nblk - s + kBnTicketShards - 1) / kBnTicketShards;
+    const unsigned shards = nblk < unsigned(kBnTicketShards) ? nblk : unsigned(kBnTicketShards);
+    int last = 0;
+    if (tk == in_shard - 1) {
+      ticket[s * kBnTicketStride] = 0u;
+      last = atomicAdd(ticket + kBnTicketShards * kBnTicketStride, 1u) == shards - 1 ? 1 : 0;
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  if (*flag) {
+    const int n = R * 2 * C;
+    for (int i = t; i < n; i += nt) acc[i] = 0.0;
+    if (t == 0) ticket[kBnTicketShards * kBnTicketStride] = 0u;
+  }
+}
+
 // The forward finalize of a folded accumulator (part[c] = sum, part[C + c] =
 // sum of squares over M elements; bn_acc_column_sums), exactly as
 // bn_fold_block computes it: mean and invstd of channel c; the block that
@@ -233,9 +267,11 @@ __device__ inline void bn_fwd_finalize(const BnFwdFinal& f, const double* part, 
 // block; part: >= max(nt, 2 C) doubles of LDS, flag: one int; blk / nblk:
 // this block among the nblk that fold), block 0 writes db / dw, the last
 // block clears it; else dw / db are read as given.  M: elements per channel.
+// tk (nullable): take the release's ticket only (thread 0 writes it to *tk); the caller finishes
+// the release at its end (bn_acc_ticket_finish)
 template <class BnDy>
 __device__ inline void bn_dy_coefs(const BnDy& d, int C, int64_t M, int chan0, double* part, int* flag, unsigned blk,
-                                   unsigned nblk, BnBwdCoef (&bc)[8]) {
+                                   unsigned nblk, BnBwdCoef (&bc)[8], unsigned* tk = nullptr) {
   const float invM = 1.f / float(M);
   if (d.acc) {
     bn_acc_column_sums(d.acc, d.R, 2 * C, part);   // part[c] = db = sum gz, part[C + c] = dw = sum gz xhat
@@ -251,7 +287,11 @@ __device__ inline void bn_dy_coefs(const BnDy& d, int C, int64_t M, int chan0, d
       bc[i].init(d.mean[c], d.invstd[c], d.w[c], d.b[c], float(part[C + c]), float(part[c]), invM);
     }
     __syncthreads();
-    bn_acc_release(d.acc, d.R, C, flag, blk, nblk);
+    if (tk) {
+      if (threadIdx.x == 0) *tk = bn_acc_ticket_take(d.acc, d.R, C, blk);
+    } else {
+      bn_acc_release(d.acc, d.R, C, flag, blk, nblk);
+    }
   } else {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {

@@ -1477,9 +1477,10 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4p_kernel(ConvWgradParam
   bool ok0[DQ];
   if constexpr (PRE) issue(0, wv0, ok0);
   BnBwdCoef bc[8];
+  unsigned rel_tk = 0;   // the accumulator release's ticket (thread 0), answered at the end
   if (bnd) {   // (LDS scratch: the front, free until the patch is written)
     bn_dy_coefs(p.bn_dy, p.Cout, p.M, dc * 8, reinterpret_cast<double*>(smem), reinterpret_cast<int*>(smem + 4096),
-                unsigned(b), unsigned(nwg), bc);
+                unsigned(b), unsigned(nwg), bc, &rel_tk);
   }
   stage_lut(p.lut, lutl);
   __syncthreads();
@@ -1585,6 +1586,11 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4p_kernel(ConvWgradParam
   zero_output(p);
   float* out = p.partial + int64_t(band) * p.Cout * 64;
   for (int e = t; e < 32 * 64; e += kThreads) out[e] = cmb[e] + cmb[2048 + e] + cmb[4096 + e] + cmb[6144 + e];
+  if (bnd && p.bn_dy.acc) {
+    __syncthreads();   // (the flag word reuses the combine area)
+    bn_acc_ticket_finish(p.bn_dy.acc, p.bn_dy.R, p.Cout, reinterpret_cast<int*>(smem), rel_tk, unsigned(b),
+                         unsigned(nwg));
+  }
 }
 
 // rows per band of conv_wgrad_c4p_kernel for this first layer (0: the shape does not take it)

@@ -372,7 +372,8 @@ struct BnApplyFold {
   float* rm = nullptr;         // forward: running statistics, num_batches_tracked
   float* rv = nullptr;
   int64_t* tracked = nullptr;
-  int release = 1;             // 0: no ticket / clear (BT_BN_RELEASE=0: timing diagnostics only)
+  int release = 1;             // 1: ticket taken after the fold, answered at the end; 2: whole release
+                               // before the pass (BT_BN_RELEASE=2); 0: none (=0: timing diagnostics only)
 };
 
 template <int DT, bool BWD, bool FOLD = false, int U = kBnUnroll>
@@ -396,6 +397,7 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const void* __restrict
   const int64_t pass = int64_t(gridDim.x) * kBlock * U;
   int64_t idx = int64_t(blockIdx.x) * kBlock * U + threadIdx.x;
   uint4 rv[U], rg[U];
+  unsigned rel_tk = 0;   // FOLD: this block's release ticket (thread 0)
   auto load_pass = [&]() {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -417,7 +419,6 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const void* __restrict
     // one at a 32-byte stride ran 2-4 way conflicted: PMC 30-69 % for C >= 64)
     __shared__ double part[2 * kBnAccMaxC > kBlock ? 2 * kBnAccMaxC : kBlock];
     __shared__ __attribute__((aligned(16))) float coef[2 * kBnAccMaxC];
-    __shared__ int flag;
     auto pos = [&](int c) {
       if constexpr (V == 8) {
         const int gg = c >> 3, k = c & 7;
@@ -426,6 +427,13 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const void* __restrict
         return c;
       }
     };
+    // the lane's BN weights (and backward: the forward statistics) now, in flight with the fold's reads
+    float wl[V], bl[V], ml[BWD ? V : 1], il[BWD ? V : 1];
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      wl[i] = w[c0 + i], bl[i] = b[c0 + i];
+      if constexpr (BWD) ml[i] = mean[c0 + i], il[i] = invstd[c0 + i];
+    }
     bn_acc_column_sums(fa.acc, fa.R, 2 * C, part);
     const bool first = blockIdx.x == 0;
     for (int c = int(threadIdx.x); c < C; c += kBlock) {
@@ -455,9 +463,14 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const void* __restrict
       coef[C + pos(c)] = c1v;
     }
     __syncthreads();
-    // (the release at the kernel's end instead, after the stores: measured no
-    // faster -- profiles/r5/b7/bn_apply_bench.jsonl)
-    if (fa.release) bn_acc_release(fa.acc, fa.R, C, &flag);
+    // the release's shard ticket now (every read of the accumulator is back), its answer at the end;
+    // release 2: the whole release here (round 5's form, for A/Bs)
+    if (fa.release == 2) {
+      __shared__ int flag2;
+      bn_acc_release(fa.acc, fa.R, C, &flag2);
+    } else if (fa.release && threadIdx.x == 0) {
+      rel_tk = bn_acc_ticket_take(fa.acc, fa.R, C, blockIdx.x);
+    }
     const int gl = int(threadIdx.x) % G;   // this lane's channel group: channels V gl .. + V - 1
     float a0[V], a1[V];
 #pragma unroll
@@ -469,14 +482,13 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const void* __restrict
     }
 #pragma unroll
     for (int i = 0; i < V; ++i) {
-      const int c = c0 + i;
       if constexpr (BWD) {
-        bc[i].init(mean[c], invstd[c], w[c], b[c], a1[i], a0[i], invM);
+        bc[i].init(ml[i], il[i], wl[i], bl[i], a1[i], a0[i], invM);
       } else {
         is[i] = a1[i];
         nm[i] = -a0[i] * is[i];
-        ww[i] = w[c];
-        bb[i] = b[c];
+        ww[i] = wl[i];
+        bb[i] = bl[i];
       }
     }
   } else {
@@ -524,6 +536,10 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const void* __restrict
     if constexpr (BWD) bn_load<DT>(gy, idx * V, gv);
     apply(v, gv, o);
     bn_store<DT>(out, idx * V, o);
+  }
+  if constexpr (FOLD) {
+    __shared__ int flag;
+    if (fa.release == 1) bn_acc_ticket_finish(fa.acc, fa.R, C, &flag, rel_tk, blockIdx.x, gridDim.x);
   }
 }
 
@@ -695,7 +711,10 @@ namespace {
 // clear) -- wrong for a second use of the accumulator; for the per-phase timing
 // of scripts/bn_apply_bench.py only
 int bn_release_env() {
-  static const int v = std::getenv("BT_BN_RELEASE") && std::getenv("BT_BN_RELEASE")[0] == '0' ? 0 : 1;
+  static const int v = [] {
+    const char* e = std::getenv("BT_BN_RELEASE");
+    return e && e[0] == '0' ? 0 : e && e[0] == '2' ? 2 : 1;
+  }();
   return v;
 }
 }  // namespace
