@@ -267,11 +267,24 @@ __device__ inline void bn_fwd_finalize(const BnFwdFinal& f, const double* part, 
 // block; part: >= max(nt, 2 C) doubles of LDS, flag: one int; blk / nblk:
 // this block among the nblk that fold), block 0 writes db / dw, the last
 // block clears it; else dw / db are read as given.  M: elements per channel.
+// The forward statistics and affine parameters of channels chan0 .. chan0 + 7, loaded ahead (at a
+// kernel's start, in flight with its other first loads) for bn_dy_coefs: otherwise they are a
+// memory round trip of their own after the fold's
+struct BnDyPre {
+  float m[8], is[8], w[8], b[8];
+  template <class BnDy>
+  __device__ void load(const BnDy& d, int chan0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) m[i] = d.mean[chan0 + i], is[i] = d.invstd[chan0 + i], w[i] = d.w[chan0 + i], b[i] = d.b[chan0 + i];
+  }
+};
+
 // tk (nullable): take the release's ticket only (thread 0 writes it to *tk); the caller finishes
-// the release at its end (bn_acc_ticket_finish)
+// the release at its end (bn_acc_ticket_finish).  pre (nullable): BnDyPre of chan0, loaded ahead.
 template <class BnDy>
 __device__ inline void bn_dy_coefs(const BnDy& d, int C, int64_t M, int chan0, double* part, int* flag, unsigned blk,
-                                   unsigned nblk, BnBwdCoef (&bc)[8], unsigned* tk = nullptr) {
+                                   unsigned nblk, BnBwdCoef (&bc)[8], unsigned* tk = nullptr,
+                                   const BnDyPre* pre = nullptr) {
   const float invM = 1.f / float(M);
   if (d.acc) {
     bn_acc_column_sums(d.acc, d.R, 2 * C, part);   // part[c] = db = sum gz, part[C + c] = dw = sum gz xhat
@@ -284,7 +297,8 @@ __device__ inline void bn_dy_coefs(const BnDy& d, int C, int64_t M, int chan0, d
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int c = chan0 + i;
-      bc[i].init(d.mean[c], d.invstd[c], d.w[c], d.b[c], float(part[C + c]), float(part[c]), invM);
+      if (pre) bc[i].init(pre->m[i], pre->is[i], pre->w[i], pre->b[i], float(part[C + c]), float(part[c]), invM);
+      else bc[i].init(d.mean[c], d.invstd[c], d.w[c], d.b[c], float(part[C + c]), float(part[c]), invM);
     }
     __syncthreads();
     if (tk) {

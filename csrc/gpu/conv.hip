@@ -1476,13 +1476,18 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4p_kernel(ConvWgradParam
   uint4 wv0[DQ];
   bool ok0[DQ];
   if constexpr (PRE) issue(0, wv0, ok0);
+  // the decode table and the BN coefficients' inputs go out with the first decode round too: the
+  // fold's accumulator reads are then the prologue's only other round trip
+  const uint2 lut8 = *reinterpret_cast<const uint2*>(p.lut + 4 * t);   // (kThreads == 256: stage_lut's split)
+  BnDyPre pre;
+  if (bnd) pre.load(p.bn_dy, dc * 8);
   BnBwdCoef bc[8];
   unsigned rel_tk = 0;   // the accumulator release's ticket (thread 0), answered at the end
   if (bnd) {   // (LDS scratch: the front, free until the patch is written)
     bn_dy_coefs(p.bn_dy, p.Cout, p.M, dc * 8, reinterpret_cast<double*>(smem), reinterpret_cast<int*>(smem + 4096),
-                unsigned(b), unsigned(nwg), bc, &rel_tk);
+                unsigned(b), unsigned(nwg), bc, &rel_tk, &pre);
   }
-  stage_lut(p.lut, lutl);
+  *reinterpret_cast<uint2*>(lutl + 8 * t) = lut8;
   __syncthreads();
   for (int i = t; i < 2 * PR; i += kThreads)   // the zero padding columns 0 and W + 1
     *reinterpret_cast<uint2*>(patch + ((i >> 1) * PW + ((i & 1) ? PW - 1 : 0)) * 8) = make_uint2(0u, 0u);
@@ -1519,7 +1524,11 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4p_kernel(ConvWgradParam
     for (int h = 0; h < 2; ++h) {
       const uint32_t off = live ? base + uint32_t(h * 16 * p.Cout * 2) : kOOB;
       r.g[h] = bload(rs_dy, off);
-      if (bnd) r.y[h] = bload(rs_by, off);
+      // (unconditional, out of range without the BN: a load issued on only some paths made every
+      // wait in this loop count the smaller total -- each stage's wait then took the next stage's
+      // first load with it)
+      r.y[h] = bload(rs_by, bnd ? off : kOOB);
+      __builtin_amdgcn_sched_barrier(0);   // issue in consumption order: the waits count a FIFO
     }
     s_load += 4;
   };
@@ -2731,13 +2740,23 @@ __global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tile
   // pixels it owns (patch rows 1 .. 2 TR, columns 1 .. 128; even sides: every pixel once), the
   // weight gradient's operand without a decode of its own
   uint32_t eo[NL];
+  // Every load and store of the tile loop is issued unconditionally (buffer ops: out-of-range ones
+  // read zeros / are dropped), so the compiler's memory-counter waits count exactly: a store issued
+  // on only some paths made its wait for a tile's patch loads vmcnt(0) -- the previous tile's
+  // output stores too, a write round trip per tile in series with the read one.  tile < 0: a dead
+  // prefetch past the block's last tile.
+  const __amdgpu_buffer_rsrc_t rs_dst = make_rsrc(p.dst, int64_t(p.N) * p.OH * p.OW * p.NOUT * 2);
+  const __amdgpu_buffer_rsrc_t rs_act =
+      make_rsrc(p.act_out, p.act_out ? int64_t(p.N) * p.SH * p.SW * 8 : 0);   // (none: every store dropped)
   auto load_patch = [&](int tile) __attribute__((always_inline)) {
-    const int n = tile / (tiles_r * tiles_c), rem = tile - n * (tiles_r * tiles_c);
+    const bool live = tile >= 0;
+    const int tl = live ? tile : 0;
+    const int n = tl / (tiles_r * tiles_c), rem = tl - n * (tiles_r * tiles_c);
     const int r0 = 2 * (rem / tiles_c) * TR - 1, c0 = 2 * (rem % tiles_c) * kC1Cols - 1;
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const int ir = r0 + pr[i], ic = c0 + pc[i];
-      ok[i] = unsigned(ir) < unsigned(p.SH) && unsigned(ic) < unsigned(p.SW);
+      ok[i] = live && unsigned(ir) < unsigned(p.SH) && unsigned(ic) < unsigned(p.SW);
       const uint32_t e = uint32_t(((n * p.SH + ir) * p.SW + ic) * 4);
       eo[i] = ok[i] && unsigned(pr[i] - 1) < unsigned(2 * TR) && unsigned(pc[i] - 1) < unsigned(2 * kC1Cols) ? e : ~0u;
       if constexpr (u8in) {
@@ -2753,7 +2772,8 @@ __global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tile
     for (int i = 0; i < NL; ++i) {
       const uint2 v = u8in ? lut_px(smem + LUT_OFF, w0[i], ok[i]) : make_uint2(w0[i], w1[i]);
       if ((i + 1) * kThreads <= PX || t + kThreads * i < PX) *reinterpret_cast<uint2*>(smem + (t + kThreads * i) * 8) = v;
-      if (u8in && p.act_out && eo[i] != ~0u) *reinterpret_cast<uint2*>(reinterpret_cast<char*>(p.act_out) + eo[i] * 2u) = v;
+      if constexpr (u8in)
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{v.x, v.y}, rs_act, eo[i] != ~0u ? eo[i] * 2u : kOOB, 0, 0);
     }
   };
   // the B fragments' patch offsets (tile-invariant): pixel fragment j of this
@@ -2780,7 +2800,7 @@ __global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tile
   auto tile_body = [&](int tile, int k) __attribute__((always_inline)) {
     __syncthreads();                 // the previous tile's fragment reads are done (and, first, the table)
     store_patch();                   // decode (the table lookups wait for this tile's loads)
-    if (tile + 1 < tile1) load_patch(tile + 1);   // in flight while this tile computes and stores
+    load_patch(tile + 1 < tile1 ? tile + 1 : -1);   // in flight while this tile computes and stores
     __syncthreads();
     f32x4 acc[FC][PF];
 #pragma unroll
@@ -2804,8 +2824,8 @@ __global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tile
     for (int j = 0; j < PF; ++j) {
       const int fi = wave * PF + j;
       const int orow = orow0 + (fi >> 2), ocol = ocol0 + 16 * (fi & 3) + (lane & 15);
-      if (orow >= p.OH || ocol >= p.OW) continue;
-      uint16_t* out = p.dst + (int64_t(n * p.OH + orow) * p.OW + ocol) * p.NOUT + 8 * g;
+      const bool in = orow < p.OH && ocol < p.OW;
+      const uint32_t ob0 = in ? uint32_t(((n * p.OH + orow) * p.OW + ocol) * p.NOUT + 8 * g) * 2u : kOOB;
 #pragma unroll
       for (int q = 0; q < CP; ++q) {
         uint32_t pk[4];
@@ -2814,16 +2834,22 @@ __global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tile
           const f32x4& a = acc[2 * q + (h >> 1)][j];
           const f32x2 pr2 = {a[2 * (h & 1)], a[2 * (h & 1) + 1]};
           pk[h] = __builtin_bit_cast(uint32_t, __builtin_convertvector(pr2, bf16x2));
-          const float lo = __uint_as_float(pk[h] << 16), hi = __uint_as_float(pk[h] & 0xFFFF0000u);
+          const float lo = in ? __uint_as_float(pk[h] << 16) : 0.f, hi = in ? __uint_as_float(pk[h] & 0xFFFF0000u) : 0.f;
           sum[q][2 * h] += lo, sq[q][2 * h] += lo * lo;
           sum[q][2 * h + 1] += hi, sq[q][2 * h + 1] += hi * hi;
           if constexpr (KEEP > 0) keep[k][j][q][h] = pk[h];
         }
-        *reinterpret_cast<uint4*>(out + 32 * q) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{pk[0], pk[1], pk[2], pk[3]}, rs_dst,
+                                               ob0 == kOOB ? kOOB : ob0 + 64u * q, 0, 0);
       }
     }
   };
   if (tile0 < tile1) load_patch(tile0);
+  // every prologue load (weights, table, the first patch) complete here, as a real waitcnt the
+  // compiler's counter tracking sees: otherwise the weight fragments' loads stay "pending" through
+  // the tile loop's merge and every tile's MFMAs waited for vmcnt(0) -- the NEXT tile's patch loads
+  // too, which serialised the prefetch with the compute
+  __builtin_amdgcn_s_waitcnt(0xF70);   // vmcnt(0)
   if constexpr (KEEP > 0) {
 #pragma unroll
     for (int k = 0; k < KEEP; ++k)
@@ -2995,6 +3021,21 @@ __device__ __forceinline__ void dgrad_patch_body(const TapGemm& p, char* smem, i
   auto store_w = [&](int buf) __attribute__((always_inline)) {
     *wdst(buf, 0) = wv0, *wdst(buf, 1) = wv1, *wdst(buf, 2) = wv2, *wdst(buf, 3) = wv3;
   };
+  const bool bnf = p.bn.part != nullptr;
+  // the BN's per-channel inputs of this lane's channels 8 g .. + 7: 16-byte loads issued first, in
+  // flight with the patch (a scalar load per value, each consumed at once, made the compiler reuse
+  // one register for all of them -- 8 round trips in series after the patch's); without the BN: out
+  // of range, zeros
+  float4 cv[4][2];
+  {
+    const float* src[4] = {p.bn.invstd, p.bn.mean, p.bn.w, p.bn.b};
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const __amdgpu_buffer_rsrc_t rc = make_rsrc(bnf ? static_cast<const void*>(src[a]) : p.w, bnf ? DP_NOUT * 4 : 0);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) cv[a][h] = __builtin_bit_cast(float4, bload(rc, uint32_t(32 * g + 16 * h)));
+    }
+  }
   load_w(0);
   // the patch: chunk u = t + 256 i is chunk u & 7 of patch pixel u >> 3
   {
@@ -3017,18 +3058,19 @@ __device__ __forceinline__ void dgrad_patch_body(const TapGemm& p, char* smem, i
   store_w(0);
   // this wave: class-grid row a0 + wave, columns b0 + 16 j + (lane & 15), j = 0, 1
   const int ra = a0 + wave;
-  const bool bnf = p.bn.part != nullptr;
   float is[8], nm[8], ww[8], bb[8], bs[8], bq[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     bs[e] = bq[e] = 0.f;
-    if (bnf) {
-      const int c = 8 * g + e;
-      is[e] = p.bn.invstd[c];
-      nm[e] = -p.bn.mean[c] * is[e];
-      ww[e] = p.bn.w[c];
-      bb[e] = p.bn.b[c];
-    }
+    auto pick = [&](int a) {
+      const float4 f = cv[a][e >> 2];
+      const int k = e & 3;
+      return k == 0 ? f.x : k == 1 ? f.y : k == 2 ? f.z : f.w;
+    };
+    is[e] = pick(0);
+    nm[e] = -pick(1) * is[e];
+    ww[e] = pick(2);
+    bb[e] = pick(3);
   }
   // A fragment offsets (class-invariant): row c1_row_chan(f, lane & 15), chunk 4 s + g
   int aoff[2];
@@ -3578,6 +3620,8 @@ hipError_t conv_wgrad_reduce(const ConvWgradParams::Reduce& r, hipStream_t strea
 // both, or conv_dgrad_flush launches the data gradient alone.
 // DBN: the data gradient's output-channel tile (64, or 128 with BT_DGRAD_BN128 where Cin % 128 == 0:
 // each tap-gathered dY tile then feeds twice the channels)
+// (a 4-deep dY / X ring in the 128-channel weight-gradient blocks -- 184 VGPRs, 2 waves per SIMD --
+// ran the step at 20.2 / 20.6k against 21.4 / 21.5k img/s, profiles/r6/b10/)
 template <int BM, bool PIPE, bool W2 = false, int DBN = 64>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(W2 ? 3 : 1))) void dgrad_wgrad_kernel(TapGemm g, ConvWgradParams q, int gx, int nd, int nw) {
   constexpr int TL = tap_gemm_lds<true, DBN, false, BM, 2>();

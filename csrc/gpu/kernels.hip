@@ -51,9 +51,14 @@ __device__ __forceinline__ T* image_out(const P& p, int b, int64_t img_elems) {
   return p.ndsts ? reinterpret_cast<T*>(p.dsts[b]) : reinterpret_cast<T*>(p.dst) + int64_t(b) * img_elems;
 }
 
+// PPT pixels of CIN u8 channels as 32-bit words; byte j is read by shifts (j a compile-time index
+// in every use).  (A byte array written through 16-byte stores and read bytewise was kept on the
+// stack in the replay kernels: 64-272 bytes of scratch per lane.)
 template <int PPT, int CIN>
 struct Pixels {
-  uint8_t v[PPT * CIN];
+  static constexpr int NW = (PPT * CIN + 3) / 4;
+  uint32_t w[NW];
+  __device__ __forceinline__ uint32_t v(int j) const { return (w[j >> 2] >> (8 * (j & 3))) & 0xFFu; }
 };
 
 // Load PPT pixels (PPT*CIN bytes) with the widest aligned accesses.
@@ -62,13 +67,19 @@ __device__ __forceinline__ void load_pixels(const uint8_t* p, Pixels<PPT, CIN>& 
   constexpr int NB = PPT * CIN;
   if constexpr (NB % 16 == 0) {
 #pragma unroll
-    for (int i = 0; i < NB / 16; ++i) *reinterpret_cast<uint4*>(&px.v[16 * i]) = reinterpret_cast<const uint4*>(p)[i];
+    for (int i = 0; i < NB / 16; ++i) {
+      const uint4 q = reinterpret_cast<const uint4*>(p)[i];
+      px.w[4 * i] = q.x, px.w[4 * i + 1] = q.y, px.w[4 * i + 2] = q.z, px.w[4 * i + 3] = q.w;
+    }
   } else if constexpr (NB % 8 == 0) {
 #pragma unroll
-    for (int i = 0; i < NB / 8; ++i) *reinterpret_cast<uint2*>(&px.v[8 * i]) = reinterpret_cast<const uint2*>(p)[i];
+    for (int i = 0; i < NB / 8; ++i) {
+      const uint2 q = reinterpret_cast<const uint2*>(p)[i];
+      px.w[2 * i] = q.x, px.w[2 * i + 1] = q.y;
+    }
   } else {
 #pragma unroll
-    for (int i = 0; i < NB / 4; ++i) *reinterpret_cast<uint32_t*>(&px.v[4 * i]) = reinterpret_cast<const uint32_t*>(p)[i];
+    for (int i = 0; i < NB / 4; ++i) px.w[i] = reinterpret_cast<const uint32_t*>(p)[i];
   }
 }
 
@@ -175,25 +186,25 @@ template <int PPT, int CIN, int IC, int TBL = 0>
 __device__ __forceinline__ void lookup_static(const Pixels<PPT, CIN>& px, const Xf& xf, int c, float (&o)[PPT]) {
   if constexpr (TBL == 2) {   // one table for every output channel, 32 copies: xf.lut is this lane's copy
 #pragma unroll
-    for (int i = 0; i < PPT; ++i) o[i] = xf.lut[px.v[i * CIN + IC] * 32u];
+    for (int i = 0; i < PPT; ++i) o[i] = xf.lut[px.v(i * CIN + IC) * 32u];
     return;
   }
   if (TBL || !xf.arith) {   // TBL: the host promised a table-mode value table (no arithmetic code at all)
     const float* l = xf.lut + c * 256;
 #pragma unroll
-    for (int i = 0; i < PPT; ++i) o[i] = l[px.v[i * CIN + IC]];
+    for (int i = 0; i < PPT; ++i) o[i] = l[px.v(i * CIN + IC)];
     return;
   }
   float x[PPT];
   if (xf.gam[c]) {
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
-      const uint32_t v = px.v[i * CIN + IC];
+      const uint32_t v = px.v(i * CIN + IC);
       x[i] = float(xf.g[((v >> 2) << xf.gshift) + (v & 3)]);
     }
   } else {
 #pragma unroll
-    for (int i = 0; i < PPT; ++i) x[i] = float(px.v[i * CIN + IC]);
+    for (int i = 0; i < PPT; ++i) x[i] = float(px.v(i * CIN + IC));
   }
   const float a = xf.a[c], b = xf.b[c], d = xf.d[c], r = xf.r[c];
   if (xf.op[c] == 0) {

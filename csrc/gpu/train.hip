@@ -376,7 +376,11 @@ struct BnApplyFold {
                                // before the pass (BT_BN_RELEASE=2); 0: none (=0: timing diagnostics only)
 };
 
-template <int DT, bool BWD, bool FOLD = false, int U = kBnUnroll>
+// PF (FOLD launches, BT_BN_PREFETCH): the next pass's loads go out before this pass is applied (two
+// register sets), every load a buffer load issued unconditionally (past the end: out of range, no
+// traffic) so the memory-counter waits count exactly -- a pass then waits only for its own loads,
+// not for the previous pass's stores or a load issued behind them
+template <int DT, bool BWD, bool FOLD = false, int U = kBnUnroll, bool PF = false>
 __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const void* __restrict__ x, const void* __restrict__ gy,
                                                           void* __restrict__ out, int64_t M, int C,
                                                           const float* __restrict__ mean,
@@ -405,8 +409,22 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const void* __restrict
       if constexpr (BWD) rg[u] = bn_load_raw<DT>(gy, (idx + u * kBlock) * V);
     }
   };
+  // (PF) 16-byte vector e of x / gy at byte 16 e; a dead pass (i < 0) reads out of range: zeros
+  const __amdgpu_buffer_rsrc_t rs_xv = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(x), 0, int(PF ? total * 16 : 0),
+                                                                         0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_gv =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(BWD ? gy : x), 0, int(PF ? total * 16 : 0), 0x00020000);
+  auto load_pass_b = [&](int64_t i, uint4 (&a)[U], uint4 (&c)[U]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t off = i >= 0 ? uint32_t((i + u * kBlock) * 16) : 0x80000000u;
+      a[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs_xv, off, 0, 0));
+      if constexpr (BWD) c[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs_gv, off, 0, 0));
+    }
+  };
   bool have = idx + (U - 1) * kBlock < total;   // a whole pass: U vectors per lane
-  if (have) load_pass();
+  if constexpr (PF) load_pass_b(have ? idx : -1, rv, rg);
+  else if (have) load_pass();
   // xhat = v * is + nm;  z = xhat * ww + bb;  backward: gx = P * (gz - dbm) - pdw * xhat (BnBwdCoef)
   float is[V], nm[V], ww[V], bb[V];
   BnBwdCoef bc[BWD ? V : 1];
@@ -518,6 +536,28 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const void* __restrict
     }
   };
   while (have) {
+    if constexpr (PF) {
+      const int64_t nidx = idx + pass;
+      const bool nhave = nidx + (U - 1) * kBlock < total;
+      uint4 nv[U], ng[U];
+      load_pass_b(nhave ? nidx : -1, nv, ng);   // in flight while this pass is applied
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        float v[V], gv[V], o[V];
+        bn_unpack<DT>(rv[u], v);
+        if constexpr (BWD) bn_unpack<DT>(rg[u], gv);
+        apply(v, gv, o);
+        bn_store<DT>(out, (idx + u * kBlock) * V, o);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        rv[u] = nv[u];
+        if constexpr (BWD) rg[u] = ng[u];
+      }
+      idx = nidx;
+      have = nhave;
+      continue;
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       float v[V], gv[V], o[V];
@@ -588,6 +628,12 @@ int bn_fold_unroll(int64_t) {
     return e && std::atoi(e) == 8 ? 8 : 4;
   }();
   return u;
+}
+// the folding applies' next-pass prefetch (bn_apply_kernel PF): BT_BN_PREFETCH=0 turns it off; only
+// where the tensor's bytes fit a buffer resource's 32-bit range
+int bn_prefetch(int64_t work) {
+  static const bool on = !(std::getenv("BT_BN_PREFETCH") && std::getenv("BT_BN_PREFETCH")[0] == '0');
+  return on && work * 16 < (int64_t(1) << 31);
 }
 int bn_fold_grid(int64_t work, int unroll = kBnUnroll) {
   const int cap = bn_fold_cap();
@@ -732,13 +778,16 @@ hipError_t bn_apply_acc(const void* x, void* y, int64_t M, int C, int dtype, BnA
   const int V = dtype == OUT_BF16 ? 8 : 4;
   const int u = bn_fold_unroll(M * (C / V));
   const int grid = bn_fold_grid(M * (C / V), u);
-#define BT_BN_FWD(DT_, U_) \
-  bn_apply_kernel<DT_, false, true, U_><<<grid, kBlock, 0, stream>>>(x, nullptr, y, M, C, nullptr, nullptr, w, b, \
-                                                                     nullptr, nullptr, slope, fa)
-  if (dtype == OUT_BF16 && u == 8) BT_BN_FWD(OUT_BF16, 8);
-  else if (dtype == OUT_BF16) BT_BN_FWD(OUT_BF16, 4);
-  else if (u == 8) BT_BN_FWD(OUT_F32, 8);
-  else BT_BN_FWD(OUT_F32, 4);
+  const bool pf = bn_prefetch(M * (C / V));
+#define BT_BN_FWD(DT_, U_, PF_) \
+  bn_apply_kernel<DT_, false, true, U_, PF_><<<grid, kBlock, 0, stream>>>(x, nullptr, y, M, C, nullptr, nullptr, w, b, \
+                                                                          nullptr, nullptr, slope, fa)
+  if (dtype == OUT_BF16 && u == 8) BT_BN_FWD(OUT_BF16, 8, false);
+  else if (dtype == OUT_BF16 && pf) BT_BN_FWD(OUT_BF16, 4, true);
+  else if (dtype == OUT_BF16) BT_BN_FWD(OUT_BF16, 4, false);
+  else if (u == 8) BT_BN_FWD(OUT_F32, 8, false);
+  else if (pf) BT_BN_FWD(OUT_F32, 4, true);
+  else BT_BN_FWD(OUT_F32, 4, false);
 #undef BT_BN_FWD
   return hipGetLastError();
 }
@@ -755,13 +804,16 @@ hipError_t bn_bwd_apply_acc(const void* x, const void* gy, void* gx, int64_t M, 
   const int V = dtype == OUT_BF16 ? 8 : 4;
   const int u = bn_fold_unroll(M * (C / V));
   const int grid = bn_fold_grid(M * (C / V), u);
-#define BT_BN_BWD(DT_, U_) \
-  bn_apply_kernel<DT_, true, true, U_><<<grid, kBlock, 0, stream>>>(x, gy, gx, M, C, mean, invstd, w, b, nullptr, \
-                                                                    nullptr, slope, fa)
-  if (dtype == OUT_BF16 && u == 8) BT_BN_BWD(OUT_BF16, 8);
-  else if (dtype == OUT_BF16) BT_BN_BWD(OUT_BF16, 4);
-  else if (u == 8) BT_BN_BWD(OUT_F32, 8);
-  else BT_BN_BWD(OUT_F32, 4);
+  const bool pf = bn_prefetch(M * (C / V));
+#define BT_BN_BWD(DT_, U_, PF_) \
+  bn_apply_kernel<DT_, true, true, U_, PF_><<<grid, kBlock, 0, stream>>>(x, gy, gx, M, C, mean, invstd, w, b, nullptr, \
+                                                                         nullptr, slope, fa)
+  if (dtype == OUT_BF16 && u == 8) BT_BN_BWD(OUT_BF16, 8, false);
+  else if (dtype == OUT_BF16 && pf) BT_BN_BWD(OUT_BF16, 4, true);
+  else if (dtype == OUT_BF16) BT_BN_BWD(OUT_BF16, 4, false);
+  else if (u == 8) BT_BN_BWD(OUT_F32, 8, false);
+  else if (pf) BT_BN_BWD(OUT_F32, 4, true);
+  else BT_BN_BWD(OUT_F32, 4, false);
 #undef BT_BN_BWD
   return hipGetLastError();
 }
