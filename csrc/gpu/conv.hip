@@ -196,15 +196,17 @@ __device__ __forceinline__ void wgrad_reduce_ordered(const ConvWgradParams::Redu
   const bool live = e0 < total;   // (group-uniform: all sub lanes of a group share e0)
   const int64_t base = live ? e0 : 0;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int k0 = part; k0 < S; k0 += kSliceGroup * sub) {
-    float4 v[kSliceGroup];
+  // two rounds of kSliceGroup loads in flight at once (the default heuristic gives a lane <= 2
+  // rounds: one round trip instead of two); the sums stay in slice order
+  for (int k0 = part; k0 < S; k0 += 2 * kSliceGroup * sub) {
+    float4 v[2 * kSliceGroup];
 #pragma unroll
-    for (int j = 0; j < kSliceGroup; ++j) {   // past the last slice: re-read slice `part` (< S), not added
+    for (int j = 0; j < 2 * kSliceGroup; ++j) {   // past the last slice: re-read slice `part` (< S), not added
       const int k = k0 + j * sub;
       v[j] = *reinterpret_cast<const float4*>(partial + int64_t(k < S ? k : part) * total + base);
     }
 #pragma unroll
-    for (int j = 0; j < kSliceGroup; ++j)
+    for (int j = 0; j < 2 * kSliceGroup; ++j)
       if (k0 + j * sub < S) acc.x += v[j].x, acc.y += v[j].y, acc.z += v[j].z, acc.w += v[j].w;
   }
   for (int o = sub >> 1; o > 0; o >>= 1) {
@@ -2283,25 +2285,44 @@ __device__ __forceinline__ void tap_gemm_body(const TapGemm& p, char* smem, int 
       const int4 r = rtab[row0 + 16 * i + (lane & 15)];
       ob[i] = r.z + n0 + col0 + 8 * g, pv[i] = r.w != 0;
     }
-    uint4 xq[FM][NQ];   // BN-backward fusion: the BN input at the same offsets, loads issued first
-    if (bnf) {
+    // BN-backward fusion: the BN input at the same offsets and the lane's per-channel BN inputs, every
+    // load issued before any is used, unconditionally (buffer loads; out of range without the BN or
+    // past the tile: zeros).  The per-channel values as scalar loads, each consumed at once, made the
+    // compiler reuse one register for all of them: 8 memory round trips in series in every data-
+    // gradient block's epilogue.
+    uint4 xq[FM][NQ];
+    float is[NQ][8], nm[NQ][8], ww[NQ][8], bb[NQ][8];
+    if constexpr (DGRAD) {
+      const __amdgpu_buffer_rsrc_t rs_bx =
+          make_rsrc(bnf ? static_cast<const void*>(p.bn.x) : p.dst, bnf ? int64_t(p.N) * p.OH * p.OW * p.NOUT * 2 : 0);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
+        for (int q = 0; q < NQ; ++q) xq[i][q] = bload(rs_bx, pv[i] ? uint32_t(ob[i] + 32 * q) * 2u : kOOB);
+      const float* src[4] = {p.bn.invstd, p.bn.mean, p.bn.w, p.bn.b};
+      float4 cv[4][NQ][2];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const __amdgpu_buffer_rsrc_t rc = make_rsrc(bnf ? static_cast<const void*>(src[a]) : p.dst, bnf ? p.NOUT * 4 : 0);
+#pragma unroll
         for (int q = 0; q < NQ; ++q)
-          xq[i][q] = pv[i] ? *reinterpret_cast<const uint4*>(p.bn.x + ob[i] + 32 * q) : make_uint4(0, 0, 0, 0);
-    }
-    float is[NQ][8], nm[NQ][8], ww[NQ][8], bb[NQ][8];
-    if (bnf) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            cv[a][q][h] = __builtin_bit_cast(float4, bload(rc, uint32_t(n0 + col0 + 32 * q + 8 * g + 4 * h) * 4u));
+      }
 #pragma unroll
       for (int q = 0; q < NQ; ++q)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const int c = n0 + col0 + 32 * q + 8 * g + e;
-          is[q][e] = p.bn.invstd[c];
-          nm[q][e] = -p.bn.mean[c] * is[q][e];
-          ww[q][e] = p.bn.w[c];
-          bb[q][e] = p.bn.b[c];
+          auto pick = [&](int a) {
+            const float4 f = cv[a][q][e >> 2];
+            const int k = e & 3;
+            return k == 0 ? f.x : k == 1 ? f.y : k == 2 ? f.z : f.w;
+          };
+          is[q][e] = pick(0);
+          nm[q][e] = -pick(1) * is[q][e];
+          ww[q][e] = pick(2);
+          bb[q][e] = pick(3);
         }
     }
     float sum[NQ][8], sq[NQ][8];

@@ -460,6 +460,45 @@ __global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p, in
   const int c0 = (t % groups) * 8;
   const bool live = t < PXB * groups && w < p.W;
   const bool bnf = p.bn_acc != nullptr;
+  // Every per-channel input (the BN's statistics, affine and sums) as two 16-byte loads of the
+  // lane's 8 channels, and each pass's images' dlogit with their BN inputs, issued together before
+  // any is used and unconditionally (buffer loads; absent or past the end: zeros).  As scalar loads
+  // each consumed at once they were ~14 memory round trips in series (the compiler reused one
+  // register for all of them): most of this kernel's 10.6 us.
+  const bool bna = p.bn_sums != nullptr;
+  auto rsrc_of = [](const void* a, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a), 0, int(a ? bytes : 0), 0x00020000);
+  };
+  auto load8 = [&](const float* a, int n, int at, float (&o)[8]) __attribute__((always_inline)) {
+    const __amdgpu_buffer_rsrc_t r = rsrc_of(a, int64_t(n) * 4);
+    const float4 x = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, at * 4, 0, 0));
+    const float4 y = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, at * 4 + 16, 0, 0));
+    o[0] = x.x, o[1] = x.y, o[2] = x.z, o[3] = x.w, o[4] = y.x, o[5] = y.y, o[6] = y.z, o[7] = y.w;
+  };
+  const bool need = bnf || bna;
+  float cm_[8], ci_[8], cw_[8], cb_[8], sdb[8], sdw[8];
+  load8(need ? p.bn_mean : nullptr, p.C, c0, cm_);
+  load8(need ? p.bn_invstd : nullptr, p.C, c0, ci_);
+  load8(need ? p.bn_w : nullptr, p.C, c0, cw_);
+  load8(need ? p.bn_b : nullptr, p.C, c0, cb_);
+  load8(bna ? p.bn_sums : nullptr, 2 * p.C, c0, sdb);
+  load8(bna ? p.bn_sums : nullptr, 2 * p.C, p.C + c0, sdw);
+  const int64_t img = int64_t(p.H) * p.W * p.C;
+  const int64_t off = (int64_t(h) * p.W + w) * p.C + c0;
+  const __amdgpu_buffer_rsrc_t rs_x = rsrc_of(need ? p.bn_x : nullptr, int64_t(p.N) * img * 2);
+  const __amdgpu_buffer_rsrc_t rs_dl = rsrc_of(p.dlogit, int64_t(p.N) * 4);
+  uint4 xv[kHeadImgs];
+  float dl[kHeadImgs];
+  auto issue_pass = [&](int n0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < kHeadImgs; ++u) {
+      const bool in = live && n0 + u < p.N;
+      xv[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            rs_x, in ? uint32_t(((n0 + u) * img + off) * 2) : 0x80000000u, 0, 0));
+      dl[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_dl, in ? (n0 + u) * 4 : 0x80000000u, 0, 0));
+    }
+  };
+  issue_pass(0);
   float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (live) {
     const int i0 = (h * p.OH) / p.H, i1 = ((h + 1) * p.OH + p.H - 1) / p.H;
@@ -480,38 +519,27 @@ __global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p, in
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     bs[q] = bq[q] = 0.f;
-    if (bnf) {
-      is[q] = p.bn_invstd[c0 + q];
-      nm[q] = -p.bn_mean[c0 + q] * is[q];
-      bw[q] = p.bn_w[c0 + q];
-      bb[q] = p.bn_b[c0 + q];
-    }
+    is[q] = ci_[q];
+    nm[q] = -cm_[q] * is[q];
+    bw[q] = cw_[q];
+    bb[q] = cb_[q];
   }
   // the BN backward applied here (its sums worked out by the forward, HeadParams::bn_sums):
   // dz becomes the BN's input gradient gx, from the same bf16-rounded gy as the apply kernel reads
-  const bool bna = p.bn_sums != nullptr;
   BnBwdCoef bc[8];
   if (bna) {
     const float invM = 1.f / float(int64_t(p.N) * p.H * p.W);
 #pragma unroll
-    for (int q = 0; q < 8; ++q)
-      bc[q].init(p.bn_mean[c0 + q], p.bn_invstd[c0 + q], p.bn_w[c0 + q], p.bn_b[c0 + q], g * p.bn_sums[p.C + c0 + q],
-                 g * p.bn_sums[c0 + q], invM);
+    for (int q = 0; q < 8; ++q) bc[q].init(cm_[q], ci_[q], cw_[q], cb_[q], g * sdw[q], g * sdb[q], invM);
     if (blockIdx.x == 0)
       for (int c = t; c < p.C; c += kHeadThreads) p.bn_dw_out[c] = g * p.bn_sums[p.C + c], p.bn_db_out[c] = g * p.bn_sums[c];
   }
-  const int64_t img = int64_t(p.H) * p.W * p.C;
-  const int64_t off = (int64_t(h) * p.W + w) * p.C + c0;
   for (int n0 = 0; live && n0 < p.N; n0 += kHeadImgs) {
-    uint4 xv[kHeadImgs];
-#pragma unroll
-    for (int u = 0; u < kHeadImgs; ++u)
-      xv[u] = (bnf || bna) && n0 + u < p.N ? *reinterpret_cast<const uint4*>(p.bn_x + (n0 + u) * img + off)
-                                           : make_uint4(0, 0, 0, 0);
+    if (n0 > 0) issue_pass(n0);
 #pragma unroll
     for (int u = 0; u < kHeadImgs; ++u) {
       if (n0 + u >= p.N) break;
-      const float d = g * p.dlogit[n0 + u];
+      const float d = g * dl[u];
       uint32_t packed[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
