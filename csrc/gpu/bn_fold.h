@@ -279,8 +279,9 @@ struct BnDyPre {
   }
 };
 
-// tk (nullable): take the release's ticket only (thread 0 writes it to *tk); the caller finishes
-// the release at its end (bn_acc_ticket_finish).  pre (nullable): BnDyPre of chan0, loaded ahead.
+// tk (nullable): no release here -- the caller takes the release's ticket (bn_acc_ticket_take, any
+// time after this returns) and finishes it at its end (bn_acc_ticket_finish).  pre (nullable):
+// BnDyPre of chan0, loaded ahead.
 template <class BnDy>
 __device__ inline void bn_dy_coefs(const BnDy& d, int C, int64_t M, int chan0, double* part, int* flag, unsigned blk,
                                    unsigned nblk, BnBwdCoef (&bc)[8], unsigned* tk = nullptr,
@@ -301,11 +302,7 @@ __device__ inline void bn_dy_coefs(const BnDy& d, int C, int64_t M, int chan0, d
       else bc[i].init(d.mean[c], d.invstd[c], d.w[c], d.b[c], float(part[C + c]), float(part[c]), invM);
     }
     __syncthreads();
-    if (tk) {
-      if (threadIdx.x == 0) *tk = bn_acc_ticket_take(d.acc, d.R, C, blk);
-    } else {
-      bn_acc_release(d.acc, d.R, C, flag, blk, nblk);
-    }
+    if (!tk) bn_acc_release(d.acc, d.R, C, flag, blk, nblk);
   } else {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {

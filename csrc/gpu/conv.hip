@@ -1541,6 +1541,10 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_c4p_kernel(ConvWgradParam
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int u = 0; u < KD; ++u) load(ring[u]);
+  // the accumulator release's ticket behind the ring's first loads: its round trip overlaps the
+  // loop, and no wait before the loop counts it (taken before the table's LDS store it made that
+  // store -- a wait on a path without the BN -- wait for the atomic too)
+  if (bnd && p.bn_dy.acc && t == 0) rel_tk = bn_acc_ticket_take(p.bn_dy.acc, p.bn_dy.R, p.Cout, unsigned(b));
   const int mysteps = nsteps > wave ? (nsteps - wave + 3) / 4 : 0;
   const int padded = (mysteps + KD - 1) / KD * KD;
   int s = wave;

@@ -489,16 +489,18 @@ __global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p, in
   const __amdgpu_buffer_rsrc_t rs_dl = rsrc_of(p.dlogit, int64_t(p.N) * 4);
   uint4 xv[kHeadImgs];
   float dl[kHeadImgs];
-  auto issue_pass = [&](int n0) __attribute__((always_inline)) {
+  // (the next pass's loads go out before this pass is worked: with 64 images that is 16 passes,
+  // one round trip each when every pass waited for its own)
+  auto issue_pass = [&](int n0, uint4 (&xa)[kHeadImgs], float (&da)[kHeadImgs]) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < kHeadImgs; ++u) {
       const bool in = live && n0 + u < p.N;
-      xv[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+      xa[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
                                             rs_x, in ? uint32_t(((n0 + u) * img + off) * 2) : 0x80000000u, 0, 0));
-      dl[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_dl, in ? (n0 + u) * 4 : 0x80000000u, 0, 0));
+      da[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_dl, in ? (n0 + u) * 4 : 0x80000000u, 0, 0));
     }
   };
-  issue_pass(0);
+  issue_pass(0, xv, dl);
   float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (live) {
     const int i0 = (h * p.OH) / p.H, i1 = ((h + 1) * p.OH + p.H - 1) / p.H;
@@ -535,7 +537,9 @@ __global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p, in
       for (int c = t; c < p.C; c += kHeadThreads) p.bn_dw_out[c] = g * p.bn_sums[p.C + c], p.bn_db_out[c] = g * p.bn_sums[c];
   }
   for (int n0 = 0; live && n0 < p.N; n0 += kHeadImgs) {
-    if (n0 > 0) issue_pass(n0);
+    uint4 xn[kHeadImgs];
+    float dn[kHeadImgs];
+    issue_pass(n0 + kHeadImgs, xn, dn);   // (past the last image: out of range, no traffic)
 #pragma unroll
     for (int u = 0; u < kHeadImgs; ++u) {
       if (n0 + u >= p.N) break;
@@ -571,6 +575,8 @@ __global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p, in
         }
       }
     }
+#pragma unroll
+    for (int u = 0; u < kHeadImgs; ++u) xv[u] = xn[u], dl[u] = dn[u];
   }
   if (!bnf) return;
   // fold the PXB pixel lanes of each channel group in LDS ([PXB][C] per sum,
