@@ -448,7 +448,21 @@ __global__ __launch_bounds__(kHeadThreads) void head_bwd_kernel(HeadParams p, in
     for (int e = (int(blockIdx.x) - nbwd) * kHeadThreads + t; e < total; e += nw * kHeadThreads) {
       const int c = e % p.C, cell = e / p.C;
       float s = 0.f;
-      for (int n = 0; n < p.N; ++n) s += p.dlogit[n] * p.pooled[(int64_t(n) * cells + cell) * p.C + c];
+      // 8 images' loads in flight at a time (past the last image: image 0 re-read, multiplied by 0),
+      // summed in image order; one image per iteration waited out a round trip per image (64 with
+      // densityopt's batch)
+      for (int n0 = 0; n0 < p.N; n0 += 8) {
+        float dv[8], pv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int n = n0 + u < p.N ? n0 + u : 0;
+          dv[u] = p.dlogit[n];
+          pv[u] = p.pooled[(int64_t(n) * cells + cell) * p.C + c];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (n0 + u < p.N) s += dv[u] * pv[u];
+      }
       const int i = cell / p.OW, j = cell - i * p.OW;
       p.dw[c * p.ws_c + i * p.ws_i + j * p.ws_j] = g * s;
     }
