@@ -2759,16 +2759,12 @@ __global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tile
     pr[i] = u < PX ? u / PC : -8;   // past the patch: never in range
     pc[i] = u - (u / PC) * PC;
   }
-  // a tile's raw pixels in flight (u8: the RGBA word; bf16: two words), their range flags and act_out
-  // offsets.  act_out (u8 input): the decoded frame, bf16 NHWC RGBA -- each tile stores the 2 TR x 128
-  // input pixels it owns (patch rows 1 .. 2 TR, columns 1 .. 128; even sides: every pixel once), the
-  // weight gradient's operand without a decode of its own.  Two sets (KEEP == 0): a tile's loads go
-  // out two tiles ahead.
-  struct PatchRegs {
-    uint32_t w0[NL], w1[NL], eo[NL];
-    bool ok[NL];
-  };
-  PatchRegs ra, rb;
+  uint32_t w0[NL], w1[NL];   // raw pixels in flight (u8: the RGBA word; bf16: two words)
+  bool ok[NL];
+  // act_out (u8 input): the decoded frame, bf16 NHWC RGBA -- each tile stores the 2 TR x 128 input
+  // pixels it owns (patch rows 1 .. 2 TR, columns 1 .. 128; even sides: every pixel once), the
+  // weight gradient's operand without a decode of its own
+  uint32_t eo[NL];
   // Every load and store of the tile loop is issued unconditionally (buffer ops: out-of-range ones
   // read zeros / are dropped), so the compiler's memory-counter waits count exactly: a store issued
   // on only some paths made its wait for a tile's patch loads vmcnt(0) -- the previous tile's
@@ -2777,11 +2773,7 @@ __global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tile
   const __amdgpu_buffer_rsrc_t rs_dst = make_rsrc(p.dst, int64_t(p.N) * p.OH * p.OW * p.NOUT * 2);
   const __amdgpu_buffer_rsrc_t rs_act =
       make_rsrc(p.act_out, p.act_out ? int64_t(p.N) * p.SH * p.SW * 8 : 0);   // (none: every store dropped)
-  auto load_patch = [&](int tile, PatchRegs& R) __attribute__((always_inline)) {
-    uint32_t (&w0)[NL] = R.w0;
-    uint32_t (&w1)[NL] = R.w1;
-    uint32_t (&eo)[NL] = R.eo;
-    bool (&ok)[NL] = R.ok;
+  auto load_patch = [&](int tile) __attribute__((always_inline)) {
     const bool live = tile >= 0;
     const int tl = live ? tile : 0;
     const int n = tl / (tiles_r * tiles_c), rem = tl - n * (tiles_r * tiles_c);
@@ -2800,11 +2792,7 @@ __global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tile
       }
     }
   };
-  auto store_patch = [&](const PatchRegs& R) __attribute__((always_inline)) {
-    const uint32_t (&w0)[NL] = R.w0;
-    const uint32_t (&w1)[NL] = R.w1;
-    const uint32_t (&eo)[NL] = R.eo;
-    const bool (&ok)[NL] = R.ok;
+  auto store_patch = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const uint2 v = u8in ? lut_px(smem + LUT_OFF, w0[i], ok[i]) : make_uint2(w0[i], w1[i]);
@@ -2834,14 +2822,11 @@ __global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tile
 
   // KEEP: the tiles' bf16 outputs, kept for the BN apply after the grid barrier
   uint32_t keep[KEEP > 0 ? KEEP : 1][PF][CP][4];
-  // tile < 0 (KEEP == 0): a dead tile past the block's last (its stores out of range, no sums)
-  auto tile_body = [&](int tile, int k, PatchRegs& R, int next) __attribute__((always_inline)) {
+  auto tile_body = [&](int tile, int k) __attribute__((always_inline)) {
     __syncthreads();                 // the previous tile's fragment reads are done (and, first, the table)
-    store_patch(R);                  // decode (the table lookups wait for this tile's loads)
-    load_patch(next, R);             // in flight while this tile (and, KEEP == 0, the next) computes
+    store_patch();                   // decode (the table lookups wait for this tile's loads)
+    load_patch(tile + 1 < tile1 ? tile + 1 : -1);   // in flight while this tile computes and stores
     __syncthreads();
-    const bool tlive = tile >= 0;
-    if (!tlive) tile = 0;
     f32x4 acc[FC][PF];
 #pragma unroll
     for (int f = 0; f < FC; ++f)
@@ -2864,7 +2849,7 @@ __global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tile
     for (int j = 0; j < PF; ++j) {
       const int fi = wave * PF + j;
       const int orow = orow0 + (fi >> 2), ocol = ocol0 + 16 * (fi & 3) + (lane & 15);
-      const bool in = tlive && orow < p.OH && ocol < p.OW;
+      const bool in = orow < p.OH && ocol < p.OW;
       const uint32_t ob0 = in ? uint32_t(((n * p.OH + orow) * p.OW + ocol) * p.NOUT + 8 * g) * 2u : kOOB;
 #pragma unroll
       for (int q = 0; q < CP; ++q) {
@@ -2884,9 +2869,8 @@ __global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tile
       }
     }
   };
-  load_patch(tile0 < tile1 ? tile0 : -1, ra);
-  if constexpr (KEEP == 0) load_patch(tile0 + 1 < tile1 ? tile0 + 1 : -1, rb);
-  // every prologue load (weights, table, the first patches) complete here, as a real waitcnt the
+  if (tile0 < tile1) load_patch(tile0);
+  // every prologue load (weights, table, the first patch) complete here, as a real waitcnt the
   // compiler's counter tracking sees: otherwise the weight fragments' loads stay "pending" through
   // the tile loop's merge and every tile's MFMAs waited for vmcnt(0) -- the NEXT tile's patch loads
   // too, which serialised the prefetch with the compute
@@ -2894,14 +2878,9 @@ __global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(TapGemm p, int tile
   if constexpr (KEEP > 0) {
 #pragma unroll
     for (int k = 0; k < KEEP; ++k)
-      if (tile0 + k < tile1) tile_body(tile0 + k, k, ra, tile0 + k + 1 < tile1 ? tile0 + k + 1 : -1);
+      if (tile0 + k < tile1) tile_body(tile0 + k, k);
   } else {
-    // tiles in pairs, each register set reloaded two tiles ahead (every body runs: a dead one past
-    // the last tile keeps the memory-counter waits exact)
-    for (int tile = tile0; tile < tile1; tile += 2) {
-      tile_body(tile, 0, ra, tile + 2 < tile1 ? tile + 2 : -1);
-      tile_body(tile + 1 < tile1 ? tile + 1 : -1, 0, rb, tile + 3 < tile1 ? tile + 3 : -1);
-    }
+    for (int tile = tile0; tile < tile1; ++tile) tile_body(tile, 0);
   }
   if (!p.stats) return;
   // the block's BatchNorm sums: the 16 lanes of a group hold the same 8 channels
