@@ -34,7 +34,9 @@ __host__ __device__ __forceinline__ int wstart(int i, int in, int out) { return 
 __host__ __device__ __forceinline__ int wend(int i, int in, int out) { return ((i + 1) * in + out - 1) / out; }
 __device__ __forceinline__ float bf(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
 
-__device__ void head_loss_wave(const HeadParams& p, bool write_through);
+constexpr int kHeadParts = 4;   // per-wave partial logits per cell (head_fwd_act_kernel: 256 threads)
+static_assert(kHeadThreads / 64 == kHeadParts, "one partial per wave");
+__device__ void head_loss_wave(const HeadParams& p, bool write_through, int parts);
 
 // one block per (pooling cell, image): pooled values of the cell and the
 // cell's share of the image's logit.  Lanes own 8 channels (one 16-byte load)
@@ -168,7 +170,7 @@ __global__ __launch_bounds__(kHeadThreads) void head_fwd_kernel(HeadParams p) {
     if (last) __hip_atomic_store(p.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (!__shfl(last, 0)) return;
-  head_loss_wave(p, true);
+  head_loss_wave(p, true, 1);
 }
 
 // The same forward with the BatchNorm applied (act.on()) and the loss ticket,
@@ -192,7 +194,6 @@ constexpr int kHeadFlat = 8;   // accumulator doubles per thread: 2 C R = 2048 (
 // BNB: also the BN's backward sums, factored through dlogit (HeadParams::bn_ab)
 template <int KMAX, bool BNB = false>
 __global__ __launch_bounds__(kHeadThreads) void head_fwd_act_kernel(HeadParams p) {
-  __shared__ float red[kHeadThreads / 64];
   // (BNB) per lane group: sums of s and s * xhat over the lane's window pixels, [pl][g][9]
   __shared__ float sa_l[BNB ? kHeadThreads * 9 : 1], sb_l[BNB ? kHeadThreads * 9 : 1];
   // per-lane-group channel sums, [pl][g][9]: 9 words per channel group (8 +
@@ -332,16 +333,16 @@ __global__ __launch_bounds__(kHeadThreads) void head_fwd_act_kernel(HeadParams p
     }
   }
   for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
-  if ((t & 63) == 0) red[t >> 6] = part;
-  if constexpr (BNB) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the block's adds are done before its ticket
+  // 4. each wave's partial logit (write-through, slot 4 cell + wave: head_loss_wave adds a cell's 4
+  // in wave order, the block sum it had before), then one wait for it together with the block's
+  // BN adds (BNB) and the shard ticket -- one round trip where the block-summed partial's store
+  // took a second -- then the loss ticket and, for the shard's last block, the release's top counter
+  if ((t & 63) == 0)
+    __hip_atomic_store(p.partial + (n * p.OH * p.OW + cell) * kHeadParts + (t >> 6), part, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  // 4. partial logit (write-through), then the loss ticket and -- for the
-  // shard's last block -- the release's top counter, in one round trip
   if (t == 0) {
-    float s = 0.f;
-    for (int k = 0; k < kHeadThreads / 64; ++k) s += red[k];
-    __hip_atomic_store(p.partial + n * p.OH * p.OW + cell, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the partial is visible; the shard ticket is back
     const unsigned in_shard = (nblk - shard + kBnTicketShards - 1) / kBnTicketShards;
     const unsigned shards = nblk < unsigned(kBnTicketShards) ? nblk : unsigned(kBnTicketShards);
     const bool shard_last = shard_old == in_shard - 1;
@@ -361,7 +362,7 @@ __global__ __launch_bounds__(kHeadThreads) void head_fwd_act_kernel(HeadParams p
     for (int e = t; e < RJ; e += kHeadThreads) p.act.acc[e] = 0.0;
     if (t == 0) ticket[kBnTicketShards * kBnTicketStride] = 0u;
   }
-  if (flags[1] && t < 64) head_loss_wave(p, true);
+  if (flags[1] && t < 64) head_loss_wave(p, true, kHeadParts);
   if constexpr (BNB) {
     if (!flags[1]) return;
     // the last block: every block's A / B adds are done (they preceded its ticket),
@@ -370,14 +371,28 @@ __global__ __launch_bounds__(kHeadThreads) void head_fwd_act_kernel(HeadParams p
     __syncthreads();
     const int NC = p.N * p.C;
     const __amdgpu_buffer_rsrc_t rdl = __builtin_amdgcn_make_buffer_rsrc(p.dlogit, 0, p.N * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rab = __builtin_amdgcn_make_buffer_rsrc(p.bn_ab, 0, 2 * NC * 8, 0x00020000);
     for (int c = t; c < p.C; c += kHeadThreads) {
       float s0 = 0.f, s1 = 0.f;
-      for (int n = 0; n < p.N; ++n) {   // (write-through reads: sc1 buffer loads; the sums at agent scope)
-        const float dl = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rdl, n * 4, 0, 16));
-        const float av = float(bn_acc_load<true>(p.bn_ab + n * p.C + c));
-        const float bv = float(bn_acc_load<true>(p.bn_ab + NC + n * p.C + c));
-        s0 += dl * av;
-        s1 += dl * bv;
+      // 8 images' values in flight at a time (write-through reads: sc1 buffer loads, what an agent-
+      // scope relaxed atomic load compiles to -- as atomic loads the compiler waited out one image at
+      // a time: 8 round trips in series in the launch's last block), summed in image order
+      for (int n0 = 0; n0 < p.N; n0 += 8) {
+        float dl[8];
+        double av[8], bv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int n = n0 + u < p.N ? n0 + u : 0;
+          dl[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rdl, n * 4, 0, 16));
+          av[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rab, (n * p.C + c) * 8, 0, 16));
+          bv[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rab, (NC + n * p.C + c) * 8, 0, 16));
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (n0 + u < p.N) {
+            s0 += dl[u] * float(av[u]);
+            s1 += dl[u] * float(bv[u]);
+          }
       }
       p.bn_sums[c] = s0;
       p.bn_sums[p.C + c] = s1;
@@ -386,10 +401,39 @@ __global__ __launch_bounds__(kHeadThreads) void head_fwd_act_kernel(HeadParams p
   }
 }
 
-// one wave: logits, sigmoid, mean BCE, and dlogit/g for the backward
-__device__ void head_loss_wave(const HeadParams& p, bool wt) {
+// one wave: logits, sigmoid, mean BCE, and dlogit/g for the backward.  parts: partials per cell
+// (head_fwd_act_kernel: kHeadParts per-wave ones, added in wave order; else 1)
+__device__ void head_loss_wave(const HeadParams& p, bool wt, int parts) {
   const int cells = p.OH * p.OW;
   float total = 0.f;
+  if (parts == kHeadParts) {   // 16-byte loads of a cell's 4 partials, 16 cells at a time (write-through)
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(p.partial, 0, p.N * cells * kHeadParts * 4, 0x00020000);
+    for (int n = int(threadIdx.x); n < p.N; n += 64) {
+      float logit = 0.f;
+      const float y = p.target ? p.target[n] : p.target_value;   // (in flight with the partials)
+      for (int k0 = 0; k0 < cells; k0 += 16) {
+        float4 v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int k = k0 + u < cells ? k0 + u : k0;
+          v[u] = __builtin_bit_cast(float4, wt ? __builtin_amdgcn_raw_buffer_load_b128(rs, (n * cells + k) * 16, 0, 16)
+                                               : __builtin_amdgcn_raw_buffer_load_b128(rs, (n * cells + k) * 16, 0, 0));
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (k0 + u < cells) logit += ((v[u].x + v[u].y) + v[u].z) + v[u].w;
+      }
+      const float pr = 1.f / (1.f + expf(-logit));
+      const float lp = fmaxf(logf(pr), -100.f), lq = fmaxf(logf(1.f - pr), -100.f);
+      total += -(y * lp + (1.f - y) * lq);
+      p.dlogit[n] = (pr - y) / float(p.N);
+      if (p.logit) p.logit[n] = logit;
+    }
+    for (int o = 32; o > 0; o >>= 1) total += __shfl_xor(total, o);
+    if (threadIdx.x == 0) p.loss[0] = total / float(p.N);
+    return;
+  }
   for (int n = int(threadIdx.x); n < p.N; n += 64) {
     float logit = 0.f;
     // 16 partials at a time, every load issued before the adds (summed in cell
@@ -422,7 +466,7 @@ __device__ void head_loss_wave(const HeadParams& p, bool wt) {
   if (threadIdx.x == 0) p.loss[0] = total / float(p.N);
 }
 
-__global__ __launch_bounds__(64) void head_loss_kernel(HeadParams p) { head_loss_wave(p, false); }
+__global__ __launch_bounds__(64) void head_loss_kernel(HeadParams p) { head_loss_wave(p, false, 1); }
 
 // Backward in ONE launch: blocks [0, nbwd) write dz, blocks [nbwd, ...) the
 // weight gradient.  dz[n][h][w][c] = g dlogit_n * M[h][w][c], where M (the

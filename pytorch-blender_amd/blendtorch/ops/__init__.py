@@ -2196,7 +2196,8 @@ def _head_function():
             N, C, H, W = z.shape
             dev = z.device
             pooled = torch.empty(N * oh * ow * C, dtype=torch.float32, device=dev)
-            partial = torch.empty(N * oh * ow, dtype=torch.float32, device=dev)
+            # (4 per cell: the lean BN-applying forward writes one partial logit per wave, head.hip kHeadParts)
+            partial = torch.empty(N * oh * ow * 4, dtype=torch.float32, device=dev)
             loss = torch.empty((), dtype=torch.float32, device=dev)
             dlogit = torch.empty(N, dtype=torch.float32, device=dev)
             logit = torch.empty(N, dtype=torch.float32, device=dev)
