@@ -40,6 +40,7 @@
 #include "adam_sched.h"
 #include "bn_fold.h"
 #include "kernels.h"
+#include "wgrad_reduce.h"
 
 namespace btn {
 namespace gpu {
@@ -183,48 +184,20 @@ constexpr int kSliceGroup = 8;   // (groups of 32 for the first layer's 512 slic
 // slices part, part + sub, ... in that order, 8 loads in flight, then the
 // group adds its lanes with a fixed xor-shuffle tree (commutative adds: every
 // lane ends with the same bits) and lane 0 stores.  Same bytes read as the
-// atomic form, no zeroing of the output, no atomics.
+// atomic form, no zeroing of the output, no atomics (wgrad_reduce.h).
 __device__ __forceinline__ void wgrad_reduce_ordered(const ConvWgradParams::Reduce& r, int bx) {
-  if (int(threadIdx.x) >= kThreads) return;   // (wave-uniform: a side job of a wider block)
-  const float* __restrict__ partial = r.partial;
-  const int S = r.S, sub = r.sub, Cin = r.Cin, cin_out = r.cin_out;
-  const int KC = 16 * Cin;
-  const int total = r.Cout * KC;
-  const int gl = bx * kThreads + int(threadIdx.x);
-  const int part = gl & (sub - 1);
-  const int e0 = (gl / sub) * 4;
-  const bool live = e0 < total;   // (group-uniform: all sub lanes of a group share e0)
-  const int64_t base = live ? e0 : 0;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  // two rounds of kSliceGroup loads in flight at once (the default heuristic gives a lane <= 2
-  // rounds: one round trip instead of two); the sums stay in slice order
-  for (int k0 = part; k0 < S; k0 += 2 * kSliceGroup * sub) {
-    float4 v[2 * kSliceGroup];
+  wgrad_slice_sum<kThreads, kSliceGroup>(r, bx, [&](int e0, float4 acc) {
+    const int Cin = r.Cin, KC = 16 * Cin;
+    const float vals[4] = {acc.x, acc.y, acc.z, acc.w};
 #pragma unroll
-    for (int j = 0; j < 2 * kSliceGroup; ++j) {   // past the last slice: re-read slice `part` (< S), not added
-      const int k = k0 + j * sub;
-      v[j] = *reinterpret_cast<const float4*>(partial + int64_t(k < S ? k : part) * total + base);
+    for (int j = 0; j < 4; ++j) {
+      const int e = e0 + j;
+      const int co = e / KC, kc = e - co * KC;
+      const int tap = kc / Cin, ci = kc - tap * Cin;
+      if (ci >= r.cin_out) continue;
+      r.out[co * r.s_co + ci * r.s_ci + (tap >> 2) * r.s_kh + (tap & 3) * r.s_kw] = vals[j];
     }
-#pragma unroll
-    for (int j = 0; j < 2 * kSliceGroup; ++j)
-      if (k0 + j * sub < S) acc.x += v[j].x, acc.y += v[j].y, acc.z += v[j].z, acc.w += v[j].w;
-  }
-  for (int o = sub >> 1; o > 0; o >>= 1) {
-    acc.x += __shfl_xor(acc.x, o);
-    acc.y += __shfl_xor(acc.y, o);
-    acc.z += __shfl_xor(acc.z, o);
-    acc.w += __shfl_xor(acc.w, o);
-  }
-  if (!live || part != 0) return;
-  const float vals[4] = {acc.x, acc.y, acc.z, acc.w};
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int e = e0 + j;
-    const int co = e / KC, kc = e - co * KC;
-    const int tap = kc / Cin, ci = kc - tap * Cin;
-    if (ci >= cin_out) continue;
-    r.out[co * r.s_co + ci * r.s_ci + (tap >> 2) * r.s_kh + (tap & 3) * r.s_kw] = vals[j];
-  }
+  });
 }
 
 __device__ __forceinline__ void wgrad_reduce_block(const ConvWgradParams::Reduce& r, int bx, int by) {
@@ -277,6 +250,15 @@ AdamSchedJob g_sched_job;     // attached, not yet launched
 int g_sched_device = -1;      // the optimizer's device and stream: the only launches that take it
 hipStream_t g_sched_stream = nullptr;
 bool g_sched_taken = false;   // a launch ran the attached job
+// BT_SCHED_EARLY (default on): the first fused data + weight gradient launch takes the job
+// (dgrad_wgrad_kernel), 0: the slice reduce
+bool sched_early() {
+  static const bool on = [] {
+    const char* v = std::getenv("BT_SCHED_EARLY");
+    return !v || v[0] != '0';
+  }();
+  return on;
+}
 AdamSchedJob take_sched_job(hipStream_t stream) {
   if (!g_sched_job.step || stream != g_sched_stream) return AdamSchedJob();
   int dev = -1;
@@ -3666,6 +3648,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(W2 ? 3
   if (kind == 0) {
     if (idx >= nd) return;   // (padding of the run: block-uniform, before any barrier)
     tap_gemm_body<true, DBN, false, BM, 2, 1, 0>(g, smem, idx % gx, idx / gx, gx);
+    // the attached Adam schedule (block 0: the first tile; the update launch may take the
+    // backward's last slice reduce, so the schedule cannot wait for that launch)
+    if (b == 0 && q.job.step && threadIdx.x == 0) adam_schedule_run(q.job);
   } else {
     if (idx >= nw) return;
     if constexpr (W2) conv_wgrad_co128_body<>(q, smem, idx);
@@ -3694,6 +3679,7 @@ __global__ __launch_bounds__(kThreads) void dpatch_wgrad_kernel(
   if (kind == 0) {
     if (idx >= nd) return;
     dgrad_patch_body(g, smem, idx);
+    if (b == 0 && q.job.step && threadIdx.x == 0) adam_schedule_run(q.job);   // (dgrad_wgrad_kernel)
   } else {
     if (idx >= nw) return;
     if constexpr (WIDE) conv_wgrad_wide_body(q, smem, idx);
@@ -3748,6 +3734,7 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
   const int64_t blocks = tiles * p.slices;
   if (blocks > (int64_t(1) << 31) - 1) return hipErrorInvalidValue;
   ConvWgradParams q = p;
+  q.job = AdamSchedJob();
   if (p.slices > kSliceGroup && !wgrad_ordered()) {   // groups add atomically: the main kernel zeroes out first
     q.zero_out = out;
     q.zero_count = p.Cout * 16 * (p.cin_out > 0 ? p.cin_out : p.Cin);
@@ -3777,6 +3764,7 @@ hipError_t conv_wgrad(const ConvWgradParams& p, float* out, int64_t s_co, int64_
                        (!co128 || !wgrad_pipe()) && (g_held.bn == 64 || co128);
     const int64_t nd = int64_t(g_held.gx) * (g_held.patch ? 1 : 4);
     if (plain && stream == g_held.s && nd + grid + 16 < (int64_t(1) << 31)) {
+      if (sched_early()) q.job = take_sched_job(stream);
       const unsigned total = unsigned(((nd + 7) & ~int64_t(7)) + ((grid + 7) & ~int64_t(7)));
       const int gx = int(g_held.gx), ndi = int(nd), nwi = int(grid);
       if (g_held.patch && wide)

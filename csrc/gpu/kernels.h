@@ -265,6 +265,20 @@ struct CastParams {
 };
 hipError_t multi_cast(const CastParams& p, hipStream_t stream);
 
+// The Adam step schedule as a one-lane job (adam_sched.h): run by
+// adam_schedule, or attached ahead of the backward to the first fused data +
+// weight gradient launch (block 0's first lane, after its tile) or else the
+// next weight-gradient slice-reduce launch.  taken() reports -- and clears --
+// whether a launch ran the attached job; detach drops an unused one
+// (conv_attach_adam_schedule below).
+struct AdamSchedJob {
+  float* step = nullptr;        // null: no job
+  const float* hp = nullptr;    // lr, gradient scale
+  float* sched = nullptr;       // step size, 1 / sqrt(bc2), lr, gradient scale, active
+  float beta1 = 0.f, beta2 = 0.f;
+  const float* gate = nullptr;  // optional: 0 closes the step
+};
+
 // Adam / AdamW over a list of fp32 parameters in ONE launch, graph-capturable:
 // the step counter and the bias corrections live on the device.
 //   adam_schedule (one lane): step += 1; sched = {lr / (1 - b1^step),
@@ -318,6 +332,23 @@ struct AdamParams {
   const float* g2[kMaxAdam] = {};
   int tcout[kMaxAdam] = {};
   int tcin[kMaxAdam] = {};
+  // fr.partial != nullptr: one more convolution weight, NOT in the lists, whose
+  // gradient is not given but summed here from the backward's last weight-gradient
+  // slices (the deferred ordered slice reduce, ConvWgradParams::Reduce fields;
+  // ops.FusedAdam.attach_reduce): blocks [0, fr.rx) of the launch sum it
+  // (wgrad_reduce.h) and update p / m / v / shadow at the gradient's strides
+  // themselves, and write the gradient (0 with zero_grad) to g -- the reduce
+  // launch goes away.  fp32 gradients, not the one-launch form.
+  struct FusedReduce {
+    const float* partial = nullptr;
+    int S = 0, Cout = 0, Cin = 0, cin_out = 0, sub = 0, rx = 0;
+    int64_t s_co = 0, s_ci = 0, s_kh = 0, s_kw = 0;
+    float* g = nullptr;
+    float* p = nullptr;
+    float* m = nullptr;
+    float* v = nullptr;
+    uint16_t* shadow = nullptr;
+  } fr;
 };
 // Weight gradient of a 4x4 / stride-2 / pad-1 convolution over channels-last
 // bf16 activations on the MFMA units (conv.hip): x [N][H][W][Cin],
@@ -390,6 +421,9 @@ struct ConvWgradParams {
     float* db_out = nullptr;
     uint16_t* gx_out = nullptr;
   } bn_dy;
+  // set by conv_wgrad (null: none): the attached Adam schedule, run by block 0
+  // of a fused data + weight gradient launch (BT_SCHED_EARLY, default on)
+  AdamSchedJob job;
 };
 // Cin % 32 == 0 with Cout % 64 == 0, or Cin == 4 (the first layer) with Cout % 32 == 0.
 bool conv_wgrad_supported(int Cin, int Cout);
@@ -632,19 +666,8 @@ hipError_t adam_update(const AdamParams& p, hipStream_t stream);
 hipError_t adam_schedule_prime(const float* step, const float* hp, float* sched, float beta1, float beta2,
                                hipStream_t stream, float off = 1.f);
 
-// The Adam step schedule as a one-lane job (adam_sched.h): run by
-// adam_schedule, or attached ahead of the backward to the next weight-gradient
-// slice-reduce launch.  taken() reports -- and clears -- whether a launch ran
-// the attached job; detach drops an unused one.
-struct AdamSchedJob {
-  float* step = nullptr;        // null: no job
-  const float* hp = nullptr;    // lr, gradient scale
-  float* sched = nullptr;       // step size, 1 / sqrt(bc2), lr, gradient scale, active
-  float beta1 = 0.f, beta2 = 0.f;
-  const float* gate = nullptr;  // optional: 0 closes the step
-};
-// keyed by the optimizer's device and stream: only a slice-reduce launch on that
-// stream of that device takes it (another device's or a side stream's reduce does not)
+// keyed by the optimizer's device and stream: only a launch on that stream of that
+// device takes it (another device's or a side stream's launch does not)
 void conv_attach_adam_schedule(const AdamSchedJob& j, int device, hipStream_t stream);
 bool conv_adam_schedule_taken();
 void conv_detach_adam_schedule();

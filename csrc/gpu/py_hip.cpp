@@ -638,7 +638,7 @@ PYBIND11_MODULE(_hip, m) {
            uintptr_t sched, int grad_bf16, float beta1, float beta2, float eps, float weight_decay, int decoupled,
            int maximize, uintptr_t stream, uintptr_t step, uintptr_t hp, uintptr_t gate, uintptr_t ticket,
            int zero_grad, std::vector<uintptr_t> shadow_t, std::vector<int> tcout, std::vector<int> tcin,
-           std::vector<uintptr_t> grads2) {
+           std::vector<uintptr_t> grads2, py::object fused_reduce, std::vector<uintptr_t> fr_tensors) {
           const size_t n = params.size();
           if (grads.size() != n || exp_avg.size() != n || exp_avg_sq.size() != n || shadow.size() != n ||
               numel.size() != n || n > size_t(kMaxAdam))
@@ -675,6 +675,17 @@ PYBIND11_MODULE(_hip, m) {
           a.zero_grad = zero_grad;
           a.grad_bf16 = grad_bf16, a.decoupled = decoupled, a.maximize = maximize;
           a.beta1 = beta1, a.beta2 = beta2, a.eps = eps, a.weight_decay = weight_decay;
+          if (!fused_reduce.is_none()) {   // a deferred slice reduce (conv_wgrad defer=1) + (g, p, m, v, shadow)
+            const ConvWgradParams::Reduce r = reduce_from_tuple(fused_reduce.cast<py::tuple>());
+            if (fr_tensors.size() != 5 || r.ry != 1 || r.sub <= 0)
+              throw std::invalid_argument("adam_update: fused_reduce needs an ordered reduce and 5 tensors");
+            AdamParams::FusedReduce& f = a.fr;
+            f.partial = r.partial, f.S = r.S, f.Cout = r.Cout, f.Cin = r.Cin, f.cin_out = r.cin_out;
+            f.sub = r.sub, f.rx = r.rx;
+            f.s_co = r.s_co, f.s_ci = r.s_ci, f.s_kh = r.s_kh, f.s_kw = r.s_kw;
+            f.g = ptr<float>(fr_tensors[0]), f.p = ptr<float>(fr_tensors[1]), f.m = ptr<float>(fr_tensors[2]);
+            f.v = ptr<float>(fr_tensors[3]), f.shadow = ptr<uint16_t>(fr_tensors[4]);
+          }
           check(adam_update(a, stream_of(stream)), "adam_update");
         },
         py::arg("params"), py::arg("grads"), py::arg("exp_avg"), py::arg("exp_avg_sq"), py::arg("shadow"),
@@ -682,7 +693,8 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("weight_decay"), py::arg("decoupled"), py::arg("maximize"), py::arg("stream"), py::arg("step") = 0,
         py::arg("hp") = 0, py::arg("gate") = 0, py::arg("ticket") = 0, py::arg("zero_grad") = 0,
         py::arg("shadow_t") = std::vector<uintptr_t>(), py::arg("tcout") = std::vector<int>(),
-        py::arg("tcin") = std::vector<int>(), py::arg("grads2") = std::vector<uintptr_t>());
+        py::arg("tcin") = std::vector<int>(), py::arg("grads2") = std::vector<uintptr_t>(),
+        py::arg("fused_reduce") = py::none(), py::arg("fr_tensors") = std::vector<uintptr_t>());
 
   m.def("color4x4",
         [](uintptr_t src, uintptr_t dst, uintptr_t lut, uintptr_t M, uintptr_t bias, uintptr_t flip, int B, int H,

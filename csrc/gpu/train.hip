@@ -11,6 +11,7 @@
 #include "adam_sched.h"
 #include "bn_fold.h"
 #include "kernels.h"
+#include "wgrad_reduce.h"
 
 namespace btn {
 namespace gpu {
@@ -932,10 +933,70 @@ struct AdamSlot {
   int tcin, tcout;
 };
 
-template <bool GBF16>
+// one element's update (torch.optim.Adam, non-amsgrad): both paths below
+__device__ __forceinline__ void adam_elem(const AdamParams& a, float step_size, float inv_bc2, float lr, float gscale,
+                                          float gin, float& p, float& m, float& v) {
+  const float b1 = a.beta1, b2 = a.beta2, wd = a.weight_decay;
+  float g = (a.maximize ? -gin : gin) * gscale;
+  if (wd != 0.f) {
+    if (a.decoupled) p *= 1.f - lr * wd;
+    else g += wd * p;
+  }
+  m = b1 * m + (1.f - b1) * g;
+  v = b2 * v + (1.f - b2) * g * g;
+  p -= step_size * m / (sqrtf(v) * inv_bc2 + a.eps);
+}
+
+// AdamParams::fr: the block sums its share of the weight's slices (the ordered
+// reduce's lanes and order, wgrad_reduce.h) and the group's lane 0 updates the
+// weight's elements at the gradient's strides.  The lane's parameter, moment and
+// shadow accesses are scattered 4-byte ones: ~3 K elements, a few hundred lanes.
+__device__ __forceinline__ void adam_fused_reduce(const AdamParams& a, int bx) {
+  const AdamParams::FusedReduce& r = a.fr;
+  const float step_size = a.sched[0], inv_bc2 = a.sched[1], lr = a.sched[2], gscale = a.sched[3];
+  const bool active = a.sched[4] != 0.f;
+  wgrad_slice_sum<kBlock, 8>(r, bx, [&](int e0, float4 acc) {
+    const int Cin = r.Cin, KC = 16 * Cin;
+    const float vals[4] = {acc.x, acc.y, acc.z, acc.w};
+    int64_t off[4];
+    bool ok[4];
+    float pv[4], mv[4], vv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = e0 + j;
+      const int co = e / KC, kc = e - co * KC;
+      const int tap = kc / Cin, ci = kc - tap * Cin;
+      ok[j] = ci < r.cin_out;
+      off[j] = ok[j] ? co * r.s_co + ci * r.s_ci + (tap >> 2) * r.s_kh + (tap & 3) * r.s_kw : 0;
+      pv[j] = r.p[off[j]], mv[j] = r.m[off[j]], vv[j] = r.v[off[j]];   // (off 0: a valid element, unused)
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!ok[j]) continue;
+      r.g[off[j]] = a.zero_grad ? 0.f : vals[j];   // the gradient, as the reduce launch left it
+      if (!active) continue;
+      adam_elem(a, step_size, inv_bc2, lr, gscale, vals[j], pv[j], mv[j], vv[j]);
+      r.p[off[j]] = pv[j], r.m[off[j]] = mv[j], r.v[off[j]] = vv[j];
+      if (r.shadow) r.shadow[off[j]] = f2bf(pv[j]);
+    }
+  });
+}
+
+// FR: blocks [0, fr.rx) take the weight whose slice reduce this launch took (its
+// own instantiation: the slice loads' registers would cost the plain update
+// occupancy -- 92 VGPRs against 48)
+template <bool GBF16, bool FR = false>
 __global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
   __shared__ AdamSlot slot[kMaxAdam];
   __shared__ int64_t gst[kMaxAdam + 1];
+  const int nfr = FR ? a.fr.rx : 0;
+  if constexpr (FR) {
+    if (int(blockIdx.x) < nfr) {   // (block-uniform)
+      adam_fused_reduce(a, int(blockIdx.x));
+      return;
+    }
+  }
+  const int64_t bid = int64_t(blockIdx.x) - nfr;
   {
     const int t = int(threadIdx.x);
     if (t < a.n) {
@@ -947,7 +1008,7 @@ __global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
     if (t <= a.n) gst[t] = a.gstart[t];
     __syncthreads();
   }
-  const int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x;   // 4-element group
+  const int64_t q = bid * kBlock + threadIdx.x;   // 4-element group
   const bool in = q < gst[a.n];
   int k = 0;
   if (in)
@@ -1041,18 +1102,8 @@ __global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
       }
     }
     if (active) {
-      const float b1 = a.beta1, b2 = a.beta2, wd = a.weight_decay;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float g = (a.maximize ? -gv[j] : gv[j]) * gscale;
-        if (wd != 0.f) {
-          if (a.decoupled) pv[j] *= 1.f - lr * wd;
-          else g += wd * pv[j];
-        }
-        mv[j] = b1 * mv[j] + (1.f - b1) * g;
-        vv[j] = b2 * vv[j] + (1.f - b2) * g * g;
-        pv[j] -= step_size * mv[j] / (sqrtf(vv[j]) * inv_bc2 + a.eps);
-      }
+      for (int j = 0; j < 4; ++j) adam_elem(a, step_size, inv_bc2, lr, gscale, gv[j], pv[j], mv[j], vv[j]);
       uint16_t* S = slot[k].shadow;
       if (full) {
         *reinterpret_cast<float4*>(P + e0) = make_float4(pv[0], pv[1], pv[2], pv[3]);
@@ -1087,7 +1138,7 @@ __global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
   if (a.step && threadIdx.x == 0) {
     // every block has read this step's schedule (its update used it) before its ticket
     const uint32_t tk = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (tk == gridDim.x - 1) {
+    if (tk == gridDim.x - 1) {   // (no fused reduce blocks in the one-launch form: host-checked)
       if (active) {
         const float s = a.step[0] + 1.f;
         a.step[0] = s;
@@ -1115,7 +1166,7 @@ hipError_t adam_schedule(float* step, const float* hp, float* sched, float beta1
 }
 
 hipError_t adam_update(const AdamParams& p, hipStream_t stream) {
-  if (p.n <= 0) return hipSuccess;
+  if (p.n <= 0 && !p.fr.partial) return hipSuccess;
   if (p.n > kMaxAdam || (!p.sched && !p.step)) return hipErrorInvalidValue;
   if (p.step && (!p.hp || !p.ticket)) return hipErrorInvalidValue;
   if (p.zero_grad && p.grad_bf16) return hipErrorInvalidValue;
@@ -1136,11 +1187,22 @@ hipError_t adam_update(const AdamParams& p, hipStream_t stream) {
                           p.gstart[k + 1] - p.gstart[k] != p.numel[k] / 4))
       return hipErrorInvalidValue;
   }
+  int64_t nfr = 0;
+  if (p.fr.partial) {
+    const AdamParams::FusedReduce& r = p.fr;
+    const int64_t total = int64_t(r.Cout) * 16 * r.Cin;
+    if (p.step || p.grad_bf16 || r.S <= 0 || r.Cout <= 0 || r.Cin <= 0 || r.cin_out <= 0 || r.cin_out > r.Cin ||
+        r.sub <= 0 || r.sub > 64 || (r.sub & (r.sub - 1)) || total % 4 || total >= (int64_t(1) << 31) ||
+        int64_t(r.rx) * kBlock < total / 4 * r.sub || r.rx > 65536 || !r.g || !r.p || !r.m || !r.v)
+      return hipErrorInvalidValue;
+    nfr = r.rx;
+  }
   const int64_t groups = p.gstart[p.n];
-  if (groups == 0) return hipSuccess;
-  const int64_t blocks = (groups + kBlock - 1) / kBlock;
+  if (groups == 0 && nfr == 0) return hipSuccess;
+  const int64_t blocks = (groups + kBlock - 1) / kBlock + nfr;
   if (blocks > int64_t(1) << 30) return hipErrorInvalidValue;
   if (p.grad_bf16) adam_update_kernel<true><<<unsigned(blocks), kBlock, 0, stream>>>(p);
+  else if (nfr) adam_update_kernel<false, true><<<unsigned(blocks), kBlock, 0, stream>>>(p);
   else adam_update_kernel<false><<<unsigned(blocks), kBlock, 0, stream>>>(p);
   return hipGetLastError();
 }

@@ -1532,6 +1532,25 @@ def decode_lut_bf16(cfg: DecodeConfig, device):
     return t
 
 
+# ops.FusedAdam.attach_reduce: the backward's last weight-gradient slice reduce
+# handed to the optimizer's update launch (AdamParams::fr) instead of a launch
+# of its own.  {'params': ids of the parameters the update takes, 'got': the
+# deferred reduce (ext tuple, tensors to keep alive, param, device) or None}
+_REDUCE_CLAIM = None
+
+
+def _claim_flush():
+    """Run a claimed slice reduce now (another weight gradient follows it in
+    the backward, or no update takes it)."""
+    c = _REDUCE_CLAIM
+    if c is not None and c['got'] is not None:
+        res, _keep, param, device = c['got']
+        c['got'] = None
+        hip_ext().conv_wgrad_reduce(res, _stream(device))
+        _count('conv_wgrad_reduce_claim_flushed')
+        _grad_done(param)
+
+
 class WgradChain:
     """Weight-gradient launches of one backward pass that hand their slice
     reduce forward: each :func:`conv_wgrad` in the chain leaves its reduce to
@@ -1648,8 +1667,14 @@ def conv_wgrad(x, dy, out, target_blocks=None, chain=None, last=True, lut=None, 
         slices = M // px
     partial = torch.empty(slices * Cout * 16 * Cin, dtype=torch.float32, device=x.device)
     _count('conv_wgrad')
+    _claim_flush()   # a reduce handed to the optimizer is not the backward's last after all
     side = chain.pending if chain is not None else None
     defer = chain is not None and not last
+    # this layer's own reduce handed to the optimizer update (FusedAdam.attach_reduce): the first
+    # contribution of this step, written into the parameter's gradient bucket view
+    claim = _REDUCE_CLAIM
+    hand = (not defer and claim is not None and param is not None and id(param) in claim['params']
+            and _GRAD_DONE is None and not _SIDE_WGRAD and out is grad_sink(param))
     if (lut is not None) != (x.dtype == torch.uint8) or (lut is not None and Cin != 4):
         raise ValueError('conv_wgrad: u8 input (4 channels) needs its decode table lut, and only u8 takes one')
     bnt = None
@@ -1684,7 +1709,14 @@ def conv_wgrad(x, dy, out, target_blocks=None, chain=None, last=True, lut=None, 
                    bdb.data_ptr(), float(bslope))
     res = ext.conv_wgrad(x.data_ptr(), dy.data_ptr(), partial.data_ptr(), N, H, W, Cin, Ho, Wo, Cout, slices, px,
                          out.data_ptr(), out.stride(0), out.stride(1), out.stride(2), out.stride(3), _stream(x.device),
-                         cin_out, defer, side, lut.data_ptr() if lut is not None else 0, fold, bnt)
+                         cin_out, defer or hand, side, lut.data_ptr() if lut is not None else 0, fold, bnt)
+    if hand:
+        if int(res[12]) > 0:   # the ordered reduce: the update sums it (AdamParams::fr)
+            claim['got'] = (res, (partial, out), param, x.device)
+            _count('conv_wgrad_reduce_handed')
+        else:
+            ext.conv_wgrad_reduce(res, _stream(x.device))
+            hand = False
     if fold is not None:
         _count('conv_wgrad_bn_fold')
         _grad_done(*fold_params)
@@ -1699,7 +1731,7 @@ def conv_wgrad(x, dy, out, target_blocks=None, chain=None, last=True, lut=None, 
             _grad_done(chain.param)
         chain.pending, chain.keep = (res, (partial, out)) if defer else (None, None)
         chain.param = param if defer else None
-    if not defer:
+    if not defer and not hand:
         _grad_done(param)
     return out
 

@@ -67,6 +67,14 @@ _ONE_LAUNCH_DEFAULT = os.environ.get('BT_ADAM_ONE_LAUNCH', '0') == '1'
 _ATTACH = os.environ.get('BT_ADAM_ATTACH', '1') not in ('', '0')
 
 _MAX_PER_LAUNCH = 32   # kMaxAdam (csrc/gpu/kernels.h)
+# the backward's last weight-gradient slice reduce summed inside the update launch (attach_reduce;
+# BT_ADAM_FUSE_REDUCE=0: its own launch)
+_FUSE_REDUCE = os.environ.get('BT_ADAM_FUSE_REDUCE', '1') not in ('', '0')
+
+
+def _ops():
+    import sys
+    return sys.modules[__package__]
 
 
 class FusedAdam(torch.optim.Optimizer):
@@ -143,6 +151,33 @@ class FusedAdam(torch.optim.Optimizer):
                                        _stream(dev))
         self._attached = (id(group), gs['lr'], gs)
         return True
+
+    def attach_reduce(self):
+        """Let the update take the backward's last weight-gradient slice
+        reduce (the ordered one of a 4x4 convolution weight whose gradient is
+        written into its bucket view, ``parallel.GradBuckets``): the reduce is
+        not launched but summed by extra blocks of the update launch, which also
+        write the gradient (0 under :meth:`set_zero_grads`) -- one launch fewer
+        per step.  Call right before a backward that no collective follows,
+        then :meth:`step`; :meth:`detach_reduce` runs a reduce no update took.
+        One GPU parameter group outside the one-launch form; returns whether it
+        attached."""
+        if not _FUSE_REDUCE or self._one_launch:
+            return False
+        groups = [g for g in self.param_groups if g['params']]
+        if len(groups) != 1 or not groups[0]['params'][0].is_cuda:
+            return False
+        ops = _ops()
+        ops._claim_flush()
+        ops._REDUCE_CLAIM = {'params': {id(p) for p in groups[0]['params']}, 'got': None}
+        return True
+
+    def detach_reduce(self):
+        """Run a slice reduce :meth:`attach_reduce` let the backward hand over
+        that no update took (e.g. the backward raised), and stop taking them."""
+        ops = _ops()
+        ops._claim_flush()
+        ops._REDUCE_CLAIM = None
 
     def detach_schedule(self):
         """Drop a schedule :meth:`attach_schedule` handed out (e.g. the
@@ -312,7 +347,24 @@ class FusedAdam(torch.optim.Optimizer):
             ext.adam_schedule(gs['step'].data_ptr(), gs['hp'].data_ptr(), gs['sched'].data_ptr(), b1, b2, stream,
                               gate.data_ptr() if gate is not None else 0)
         zero = self._zero_grads and all(p.grad.dtype == torch.float32 for p in params)
-        for i in range(0, len(params), _MAX_PER_LAUNCH):
+        # a slice reduce the backward handed over (attach_reduce): its weight leaves the lists and
+        # extra blocks of the first launch sum its gradient and update it (AdamParams::fr)
+        ops = _ops()
+        claim, fr = ops._REDUCE_CLAIM, None
+        if claim is not None and claim['got'] is not None:
+            res, keep, fp, _dev = claim['got']
+            k = next((i for i, p in enumerate(params) if p is fp), -1)
+            st = states[k] if k >= 0 else None
+            if (k >= 0 and not one and fp.grad is keep[1] and fp.grad.dtype == torch.float32
+                    and fp.grad.stride() == fp.stride() and _second_grad(fp) is None and 'shadow_t' not in st):
+                claim['got'] = None
+                fr = (res, [fp.grad.data_ptr(), fp.data_ptr(), st['exp_avg'].data_ptr(), st['exp_avg_sq'].data_ptr(),
+                            st['shadow'].data_ptr() if 'shadow' in st else 0], keep)
+                params, states = params[:k] + params[k + 1:], states[:k] + states[k + 1:]
+                _count('adam_fused_reduce')
+            else:
+                ops._claim_flush()   # the gradient first, then the plain update reads it
+        for i in range(0, max(len(params), 1 if fr is not None else 0), _MAX_PER_LAUNCH):
             ps, ss = params[i:i + _MAX_PER_LAUNCH], states[i:i + _MAX_PER_LAUNCH]
             grads = []
             for p in ps:
@@ -328,12 +380,13 @@ class FusedAdam(torch.optim.Optimizer):
             # parameter's second bucket view (GradBuckets(second_sinks=True)): the update
             # kernel adds it, instead of an AccumulateGrad launch per parameter
             g2 = [_second_grad(p) for p in ps]
-            if any(x is not None for x in g2) and grads[0].dtype != torch.float32:
+            if any(x is not None for x in g2) and grads and grads[0].dtype != torch.float32:
                 raise ValueError('FusedAdam: second gradient contributions need fp32 gradients')
             ext.adam_update([p.data_ptr() for p in ps], [g.data_ptr() for g in grads],
                             [s['exp_avg'].data_ptr() for s in ss], [s['exp_avg_sq'].data_ptr() for s in ss],
                             [s['shadow'].data_ptr() if 'shadow' in s else 0 for s in ss],
-                            [p.numel() for p in ps], gs['sched'].data_ptr(), int(grads[0].dtype == torch.bfloat16),
+                            [p.numel() for p in ps], gs['sched'].data_ptr(),
+                            int(bool(grads) and grads[0].dtype == torch.bfloat16),
                             b1, b2, group['eps'], group['weight_decay'], int(group['decoupled']),
                             int(group['maximize']), stream,
                             step=gs['step'].data_ptr() if one else 0, hp=gs['hp'].data_ptr() if one else 0,
@@ -343,7 +396,9 @@ class FusedAdam(torch.optim.Optimizer):
                             tcout=[int(p.shape[0]) if 'shadow_t' in s else 0 for p, s in zip(ps, ss)] if trans else [],
                             tcin=[int(p.shape[1]) if 'shadow_t' in s else 0 for p, s in zip(ps, ss)] if trans else [],
                             grads2=[x.data_ptr() if x is not None else 0 for x in g2]
-                            if any(x is not None for x in g2) else [])
+                            if any(x is not None for x in g2) else [],
+                            fused_reduce=fr[0] if (fr is not None and i == 0) else None,
+                            fr_tensors=fr[1] if (fr is not None and i == 0) else [])
             if zero:
                 for p, g in zip(ps, grads):
                     if g is not p.grad:      # a re-strided copy was read and cleared: clear the real one

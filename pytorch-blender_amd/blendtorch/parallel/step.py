@@ -228,6 +228,7 @@ class CapturedStep:
         active = bool(allreduce) and dist.is_available() and dist.is_initialized() and (
             dist.get_world_size(group) > 1 or allreduce == 'always')
         self._legacy = active and not buckets
+        self._active = active
         self.overlap = bool(overlap) and active and buckets
         self._memset = True
         self._seed = None
@@ -310,18 +311,27 @@ class CapturedStep:
         if self._seed is None or self._seed.shape != loss.shape or self._seed.device != loss.device \
                 or self._seed.dtype != loss.dtype:
             self._seed = torch.ones_like(loss)
-        # ops.FusedAdam: the step's schedule rides in the backward's last weight-gradient
-        # slice-reduce launch (one launch fewer per step)
+        # ops.FusedAdam: the step's schedule rides in a launch of the backward (its first fused
+        # data + weight gradient, or its last slice reduce: one launch fewer per step)
         attach = getattr(self.opt, 'attach_schedule', None)
         if attach is not None:
             attach()
+        # ... and, with no collective reading the gradients before the update, the backward's last
+        # slice reduce rides in the update launch (FusedAdam.attach_reduce)
+        fuse = not self._active and getattr(self.opt, 'attach_reduce', None) is not None and self.opt.attach_reduce()
         try:
             self._backward_only(loss)
         except BaseException:
             if attach is not None:
                 self.opt.detach_schedule()
+            if fuse:
+                self.opt.detach_reduce()
             raise
-        self.opt.step()
+        try:
+            self.opt.step()
+        finally:
+            if fuse:
+                self.opt.detach_reduce()
         return loss.detach()
 
     def _backward_only(self, loss):

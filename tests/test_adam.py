@@ -455,3 +455,88 @@ def test_schedule_attached_to_backward_reduce(monkeypatch):
     torch.cuda.synchronize()
     assert ops.KERNEL_CALLS.get('adam_schedule', 0) > before
     assert not ops.hip_ext().adam_schedule_taken()
+
+
+@pytest.mark.gpu
+def test_update_takes_backward_reduce(monkeypatch):
+    """CapturedStep lets FusedAdam's update take the backward's last weight-
+    gradient slice reduce (FusedAdam.attach_reduce): extra blocks of the update
+    launch sum the deferred slices, update that weight and write its gradient.
+    Weights and moments agree with the plain path's (its own reduce launch),
+    and no claim outlives the step."""
+    from blendtorch import ops
+    from blendtorch.models import Discriminator
+    from blendtorch.parallel.step import CapturedStep
+    import blendtorch.ops.adam as adam_mod
+    dev = torch.device('cuda', 0)
+    cl = torch.channels_last
+    g = torch.Generator(device=dev).manual_seed(5)
+    xs = [torch.rand(4, 3, 96, 128, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+          for _ in range(4)]
+    outs = []
+    for fuse in (True, False):
+        monkeypatch.setattr(adam_mod, '_FUSE_REDUCE', fuse)
+        torch.manual_seed(8)
+        m = Discriminator(nc=3, ndf=32, adaptive=True).to(dev).to(memory_format=cl)
+        opt = ops.FusedAdam(m.parameters(), lr=2e-4)
+        st = CapturedStep(m, opt, lambda mm, x: mm.bce_loss_bf16(x, 1.0), allreduce=False, warmup=1)
+        before = ops.KERNEL_CALLS.get('adam_fused_reduce', 0)
+        for x in xs:
+            st(x)
+        torch.cuda.synchronize()
+        assert st.state == 'graph'
+        n = ops.KERNEL_CALLS.get('adam_fused_reduce', 0) - before
+        assert (n > 0) if fuse else (n == 0)
+        assert ops._REDUCE_CLAIM is None
+        ps = list(m.parameters())
+        outs.append(([p.detach().clone() for p in ps], [opt.state[p]['exp_avg'].clone() for p in ps]))
+    (pa, ma), (pb, mb) = outs
+    lr = 2e-4
+    for a, b in zip(pa, pb):   # (slice groups of some layers add with float atomics: rounding)
+        d = (a - b).abs()
+        assert float(d.mean()) < 0.1 * lr and float((d > 0.5 * lr).float().mean()) < 0.02
+    for a, b in zip(ma, mb):   # (the same rounding, through four steps)
+        assert float((a - b).abs().mean()) <= 0.05 * float(b.abs().mean()) + 1e-9
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('zero', [False, True])
+def test_fused_reduce_update_matches_plain(zero):
+    """One 4x4 weight gradient (32 -> 64 channels) whose ordered slice reduce
+    is handed to FusedAdam (AdamParams::fr) against the same reduce launched on
+    its own and the plain update: identical gradient bits (or zeros under
+    set_zero_grads) and the same weights and moments."""
+    from blendtorch import ops
+    dev = torch.device('cuda', 0)
+    cl = torch.channels_last
+    g = torch.Generator(device=dev).manual_seed(11)
+    x = torch.randn(2, 32, 64, 96, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    dy = torch.randn(2, 64, 32, 48, device=dev, generator=g).to(torch.bfloat16).contiguous(memory_format=cl)
+    w0 = (0.05 * torch.randn(64, 32, 4, 4, device=dev, generator=g)).contiguous(memory_format=cl)
+    res = []
+    for fuse in (True, False):
+        w = torch.nn.Parameter(w0.clone())
+        out = torch.zeros_like(w)
+        w.grad = out
+        w._bt_grad_sink = out
+        opt = ops.FusedAdam([w], lr=1e-3, weight_decay=0.01)
+        opt.set_zero_grads(zero)
+        before = ops.KERNEL_CALLS.get('adam_fused_reduce', 0)
+        for _ in range(2):
+            if fuse:
+                ops._REDUCE_CLAIM = {'params': {id(w)}, 'got': None}
+            ops.conv_wgrad(x, dy, out, param=w)
+            if fuse:
+                assert ops._REDUCE_CLAIM['got'] is not None
+            opt.step()
+            ops._REDUCE_CLAIM = None
+        torch.cuda.synchronize()
+        assert (ops.KERNEL_CALLS.get('adam_fused_reduce', 0) - before == 2) == fuse
+        st = opt.state[w]
+        res.append((w.detach().clone(), st['exp_avg'].clone(), st['exp_avg_sq'].clone(), out.clone()))
+    (wa, ma, va, ga), (wb, mb, vb, gb) = res
+    assert torch.equal(ga, gb)
+    if zero:
+        assert not ga.any()
+    for a, b in ((wa, wb), (ma, mb), (va, vb)):
+        assert torch.allclose(a, b, rtol=1e-6, atol=1e-9)
