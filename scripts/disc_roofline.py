@@ -90,6 +90,9 @@ MODEL_R6 = MODEL[:7] + [
     ('wgrad slice reduce (+ Adam schedule)', 0, 0),
     ('adam update', 0, 4 * PARAMS),
 ]
+# ... and its last form (16 kernels): the update launch sums the first layer's weight-gradient
+# slices itself (FusedAdam.attach_reduce), the schedule rides in the conv4 pair's launch
+MODEL_R6B = MODEL_R6[:15] + [('adam update (+ conv1 wgrad slice reduce)', 0, 4 * PARAMS)]
 CLOCK_HZ, CUS = 2.4e9, 256
 
 
@@ -173,6 +176,8 @@ def main():
         model = MODEL_FUSED2
     if len(seq) == len(MODEL_R6) and any(base(n) == 'conv_wgrad_c4p_kernel' for n, _ in seq):
         model = MODEL_R6
+    if len(seq) == len(MODEL_R6B) and any(base(n) == 'conv_wgrad_c4p_kernel' for n, _ in seq):
+        model = MODEL_R6B
     if len(seq) != len(model):
         print(f'warning: {len(seq)} kernels per step, the model has {len(model)}', file=sys.stderr)
     rows = []
