@@ -951,11 +951,12 @@ __device__ __forceinline__ void adam_elem(const AdamParams& a, float step_size, 
 // reduce's lanes and order, wgrad_reduce.h) and the group's lane 0 updates the
 // weight's elements at the gradient's strides.  The lane's parameter, moment and
 // shadow accesses are scattered 4-byte ones: ~3 K elements, a few hundred lanes.
+template <int SG>
 __device__ __forceinline__ void adam_fused_reduce(const AdamParams& a, int bx) {
   const AdamParams::FusedReduce& r = a.fr;
   const float step_size = a.sched[0], inv_bc2 = a.sched[1], lr = a.sched[2], gscale = a.sched[3];
   const bool active = a.sched[4] != 0.f;
-  wgrad_slice_sum<kBlock, 8>(r, bx, [&](int e0, float4 acc) {
+  wgrad_slice_sum<kBlock, SG>(r, bx, [&](int e0, float4 acc) {
     const int Cin = r.Cin, KC = 16 * Cin;
     const float vals[4] = {acc.x, acc.y, acc.z, acc.w};
     int64_t off[4];
@@ -985,14 +986,15 @@ __device__ __forceinline__ void adam_fused_reduce(const AdamParams& a, int bx) {
 // FR: blocks [0, fr.rx) take the weight whose slice reduce this launch took (its
 // own instantiation: the slice loads' registers would cost the plain update
 // occupancy -- 92 VGPRs against 48)
-template <bool GBF16, bool FR = false>
+// FSG: the fused slice sum's loads per round (8: the reduce launch's; 4: 58 VGPRs, two round trips)
+template <bool GBF16, bool FR = false, int FSG = 8>
 __global__ __launch_bounds__(kBlock) void adam_update_kernel(AdamParams a) {
   __shared__ AdamSlot slot[kMaxAdam];
   __shared__ int64_t gst[kMaxAdam + 1];
   const int nfr = FR ? a.fr.rx : 0;
   if constexpr (FR) {
     if (int(blockIdx.x) < nfr) {   // (block-uniform)
-      adam_fused_reduce(a, int(blockIdx.x));
+      adam_fused_reduce<FSG>(a, int(blockIdx.x));
       return;
     }
   }
@@ -1165,6 +1167,16 @@ hipError_t adam_schedule(float* step, const float* hp, float* sched, float beta1
   return hipGetLastError();
 }
 
+namespace {
+int adam_fr_sg() {   // BT_ADAM_FR_SG: 4 or 8 (default) slice loads per round in the fused reduce
+  static const int v = [] {
+    const char* e = std::getenv("BT_ADAM_FR_SG");
+    return e && std::atoi(e) == 4 ? 4 : 8;
+  }();
+  return v;
+}
+}  // namespace
+
 hipError_t adam_update(const AdamParams& p, hipStream_t stream) {
   if (p.n <= 0 && !p.fr.partial) return hipSuccess;
   if (p.n > kMaxAdam || (!p.sched && !p.step)) return hipErrorInvalidValue;
@@ -1202,6 +1214,7 @@ hipError_t adam_update(const AdamParams& p, hipStream_t stream) {
   const int64_t blocks = (groups + kBlock - 1) / kBlock + nfr;
   if (blocks > int64_t(1) << 30) return hipErrorInvalidValue;
   if (p.grad_bf16) adam_update_kernel<true><<<unsigned(blocks), kBlock, 0, stream>>>(p);
+  else if (nfr && adam_fr_sg() == 4) adam_update_kernel<false, true, 4><<<unsigned(blocks), kBlock, 0, stream>>>(p);
   else if (nfr) adam_update_kernel<false, true><<<unsigned(blocks), kBlock, 0, stream>>>(p);
   else adam_update_kernel<false><<<unsigned(blocks), kBlock, 0, stream>>>(p);
   return hipGetLastError();
