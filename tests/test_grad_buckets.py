@@ -155,3 +155,22 @@ def test_armed_buckets_reduce_as_soon_as_complete():
     ops._GRAD_LATE(m[0].weight)               # bucket 1 not reduced yet: fine
     assert gb.finish() == 2 and c.calls[1] == gb.buckets[1].data_ptr()
     assert ops._GRAD_DONE is None and ops._GRAD_LATE is None
+
+
+def test_reduce_claim_stays_off_the_cpu_path():
+    """FusedAdam.attach_reduce (the update summing the backward's last weight-
+    gradient slice reduce) is a GPU-only handshake: on CPU parameters it does
+    not attach, a CapturedStep leaves no claim behind, and flushing with no
+    claim is a no-op."""
+    m = _net()
+    opt = ops.FusedAdam(m.parameters(), lr=1e-3)
+    assert opt.attach_reduce() is False
+    assert ops._REDUCE_CLAIM is None
+    ops._claim_flush()
+    from blendtorch.parallel.step import CapturedStep
+    st = CapturedStep(m, opt, lambda mm, x: mm(x).pow(2).mean(), graph=False, allreduce=False)
+    for _ in range(2):
+        st(torch.randn(2, 3, 16, 16))
+    assert ops._REDUCE_CLAIM is None
+    opt.detach_reduce()
+    assert ops._REDUCE_CLAIM is None
