@@ -78,7 +78,8 @@ def test_dataset_shared_memory_producers(free_port):
     args = dict(producer='cubesim', num_instances=2, named_sockets=['DATA'], start_port=free_port, proto='ipc',
                 instance_args=[['--mode', 'rgb', '--shm', '4', '--rotation', '0.1', '0.2', '0.3']] * 2)
     with btt.BlenderLauncher(**args) as bl:
-        ds = btt.RemoteIterableDataset(bl.launch_info.addresses['DATA'], max_items=40)
+        # (a generous timeout: the producers start slowly on a loaded host, e.g. under pytest -n)
+        ds = btt.RemoteIterableDataset(bl.launch_info.addresses['DATA'], max_items=40, timeoutms=60000)
         items = list(tud.DataLoader(ds, batch_size=4, num_workers=2))
     assert len(items) == 10
     assert items[0]['image'].shape == (4, 480, 640, 3)
